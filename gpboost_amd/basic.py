@@ -1,0 +1,240 @@
+"""Python host mirror of the reference ``gpboost.GPModel`` for the likelihood path.
+
+Same constructor arguments, argument checking and error behaviour as the reference
+(python-package/gpboost/basic.py:4054-6620, ``GPModel.__init__`` :4062,
+``neg_log_likelihood`` :5284), calling the MI355X library through the same C ABI
+(include/gpboost_amd.h) with ctypes. There is no CPU fallback: if the HIP library
+is missing or no GPU is visible, construction raises ``GPBoostError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libgpboost_amd.so")
+
+
+class GPBoostError(Exception):
+    """Error thrown by the library (reference basic.py:136-145)."""
+
+
+def _load_lib():
+    if not os.path.exists(LIB_PATH):
+        raise GPBoostError(f"HIP library not built: {LIB_PATH} (run python -m gpboost_amd.build)")
+    lib = ctypes.CDLL(LIB_PATH)
+    lib.LGBM_GetLastError.restype = ctypes.c_char_p
+    D = ctypes.POINTER(ctypes.c_double)
+    lib.GPB_EvalNegLogLikelihoodGrad.argtypes = [ctypes.c_void_p, D, D, D, ctypes.c_int, D, D, D]
+    lib.GPB_CombinePartials.argtypes = [D, ctypes.c_int32, ctypes.c_double, ctypes.c_int, D, D, D]
+    return lib
+
+
+_LIB = None
+
+
+def lib():
+    global _LIB
+    if _LIB is None:
+        _LIB = _load_lib()
+    return _LIB
+
+
+def _safe_call(ret: int):
+    """reference basic.py:136-145"""
+    if ret != 0:
+        raise GPBoostError(lib().LGBM_GetLastError().decode("utf-8"))
+
+
+def c_str(s: str | None):
+    return ctypes.c_char_p(s.encode("utf-8")) if s is not None else None
+
+
+def _dp(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _ip(a: np.ndarray):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int32))
+
+
+def _as1d(x, name: str) -> np.ndarray:
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float64).reshape(-1))
+    if not np.all(np.isfinite(a)):
+        raise ValueError(f"'{name}' contains NaN or Inf")
+    return a
+
+
+class GPModel:
+    """Gaussian process model (reference ``gpboost.GPModel``), likelihood evaluation subset."""
+
+    _SUPPORTED_APPROX = ("none", "vecchia")
+
+    def __init__(self, likelihood="gaussian", group_data=None, group_rand_coef_data=None,
+                 ind_effect_group_rand_coef=None, drop_intercept_group_rand_effect=None, gp_coords=None,
+                 gp_rand_coef_data=None, cov_function="matern", cov_fct_shape=1.5, gp_approx="none",
+                 num_parallel_threads=None, GPU_use=True, matrix_inversion_method="default", weights=None,
+                 likelihood_learning_rate=1., cov_fct_taper_range=1., cov_fct_taper_shape=1., num_neighbors=None,
+                 vecchia_ordering="random", ind_points_selection="kmeans++", num_ind_points=None,
+                 cover_tree_radius=1., seed=0, cluster_ids=None, num_data=None, likelihood_additional_param=None,
+                 free_raw_data=False, model_file=None, model_dict=None, vecchia_approx=None,
+                 vecchia_pred_type=None, num_neighbors_pred=None):
+        self.handle = None
+        if group_data is not None or group_rand_coef_data is not None:
+            raise GPBoostError("grouped random effects are out of scope for gpboost_amd")
+        if gp_rand_coef_data is not None:
+            raise GPBoostError("GP random coefficients are out of scope for gpboost_amd")
+        if gp_coords is None:
+            raise ValueError("'gp_coords' must be provided (gpboost_amd evaluates GP likelihoods)")
+        if model_file is not None or model_dict is not None:
+            raise GPBoostError("model loading is out of scope for gpboost_amd")
+        if vecchia_approx is not None and vecchia_approx:
+            gp_approx = "vecchia"
+        coords = np.asarray(gp_coords, dtype=np.float64)
+        if coords.ndim == 1:
+            coords = coords.reshape(-1, 1)
+        self.num_data = coords.shape[0]
+        self.dim_coords = coords.shape[1]
+        self.gp_approx = gp_approx
+        self.cov_function = cov_function
+        self.cov_fct_shape = float(cov_fct_shape)
+        if num_neighbors is None:
+            num_neighbors = 20  # reference default (basic.py: num_neighbors None -> 20)
+        self.num_neighbors = int(num_neighbors)
+        self.likelihood = likelihood
+        self.num_cov_pars = 3
+        coords_cm = np.ascontiguousarray(coords.T).reshape(-1)  # column-major, as the reference passes it
+        cluster = None
+        if cluster_ids is not None:
+            cluster = np.ascontiguousarray(np.asarray(cluster_ids), dtype=np.int32)
+        handle = ctypes.c_void_p()
+        _safe_call(lib().GPB_CreateREModel(
+            ctypes.c_int32(self.num_data),
+            _ip(cluster) if cluster is not None else None,
+            None, ctypes.c_int32(0), None, None, ctypes.c_int32(0), None,
+            ctypes.c_int32(1), _dp(coords_cm), ctypes.c_int(self.dim_coords), None, ctypes.c_int32(0),
+            c_str(cov_function), ctypes.c_double(self.cov_fct_shape), c_str(gp_approx),
+            ctypes.c_double(cov_fct_taper_range), ctypes.c_double(cov_fct_taper_shape),
+            ctypes.c_int(self.num_neighbors), c_str(vecchia_ordering), ctypes.c_int(num_ind_points or 500),
+            ctypes.c_double(cover_tree_radius), c_str(ind_points_selection), c_str(likelihood),
+            ctypes.c_double(likelihood_additional_param or 0.), c_str(matrix_inversion_method),
+            ctypes.c_int(seed), ctypes.c_int(num_parallel_threads or -1), ctypes.c_bool(GPU_use),
+            ctypes.c_bool(weights is not None), None, ctypes.c_double(likelihood_learning_rate),
+            ctypes.byref(handle)))
+        self.handle = handle
+
+    def __del__(self):
+        try:
+            if self.handle is not None and _LIB is not None:
+                _LIB.GPB_REModelFree(self.handle)
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ reference API
+    def _check_y(self, y):
+        if y is None:
+            return None
+        y = _as1d(y, "y")
+        if y.shape[0] != self.num_data:
+            raise ValueError("Incorrect number of data points in 'y'")
+        return y
+
+    def _check_cov_pars(self, cov_pars):
+        cp = _as1d(cov_pars, "cov_pars")
+        if cp.shape[0] != self.num_cov_pars:
+            raise ValueError("'cov_pars' does not contain the correct number of parameters")
+        return cp
+
+    def neg_log_likelihood(self, cov_pars, y, fixed_effects=None, aux_pars=None):
+        """Negative log-likelihood at ``cov_pars`` (original scale), reference basic.py:5284."""
+        y = self._check_y(y)
+        cp = self._check_cov_pars(cov_pars)
+        fe = None
+        if fixed_effects is not None:
+            fe = _as1d(fixed_effects, "fixed_effects")
+            if fe.shape[0] != self.num_data:
+                raise ValueError("Length of 'fixed_effects' is not correct ")
+        negll = ctypes.c_double(0)
+        _safe_call(lib().GPB_EvalNegLogLikelihood(self.handle, _dp(y) if y is not None else None, _dp(cp),
+                                                  _dp(fe) if fe is not None else None, ctypes.byref(negll)))
+        return negll.value
+
+    def get_current_neg_log_likelihood(self):
+        v = ctypes.c_double(0)
+        _safe_call(lib().GPB_GetCurrentNegLogLikelihood(self.handle, ctypes.byref(v)))
+        return v.value
+
+    def get_cov_pars(self, std_err=False):
+        out = np.zeros(self.num_cov_pars)
+        _safe_call(lib().GPB_GetCovPar(self.handle, _dp(out), ctypes.c_bool(std_err)))
+        return out
+
+    # ------------------------------------------------------------------ extensions
+    def neg_log_likelihood_and_grad(self, cov_pars, y=None, profile_sigma2=False, fixed_effects=None):
+        """nll and gradient in one device evaluation (include/gpboost_amd.h GPB_EvalNegLogLikelihoodGrad).
+
+        profile_sigma2=False: gradient wrt log of all transformed covariance parameters.
+        profile_sigma2=True : the reference's L-BFGS objective unit (sigma2 profiled out).
+        Returns (nll, grad, sigma2)."""
+        y = self._check_y(y)
+        cp = self._check_cov_pars(cov_pars)
+        fe = _as1d(fixed_effects, "fixed_effects") if fixed_effects is not None else None
+        negll = np.zeros(1)
+        grad = np.zeros(self.num_cov_pars)
+        s2 = np.zeros(1)
+        _safe_call(lib().GPB_EvalNegLogLikelihoodGrad(
+            self.handle, _dp(y) if y is not None else None, _dp(cp), _dp(fe) if fe is not None else None,
+            int(bool(profile_sigma2)), _dp(negll), _dp(grad), _dp(s2)))
+        g = grad[: self.num_cov_pars - 1] if profile_sigma2 else grad
+        return float(negll[0]), g.copy(), float(s2[0])
+
+    def vecchia_structure(self):
+        perm = np.zeros(self.num_data, dtype=np.int32)
+        m = min(self.num_neighbors, self.num_data - 1)
+        nbr = np.zeros((self.num_data, m), dtype=np.int32)
+        _safe_call(lib().GPB_GetVecchiaStructure(self.handle, _ip(perm), _ip(nbr)))
+        return perm, nbr
+
+    def vecchia_factor(self, cov_pars):
+        cp = self._check_cov_pars(cov_pars)
+        m = min(self.num_neighbors, self.num_data - 1)
+        dinv = np.zeros(self.num_data)
+        b = np.zeros((self.num_data, m))
+        _safe_call(lib().GPB_GetVecchiaFactor(self.handle, _dp(cp), _dp(dinv), _dp(b)))
+        return dinv, b
+
+    def last_kernel_ms(self):
+        out = np.zeros(2)
+        _safe_call(lib().GPB_GetLastKernelTimes(self.handle, _dp(out)))
+        return out
+
+    def set_distributed(self, rank: int, world_size: int, comm_id: bytes | None):
+        buf = ctypes.create_string_buffer(comm_id, len(comm_id)) if comm_id is not None else None
+        _safe_call(lib().GPB_SetDistributed(self.handle, ctypes.c_int(rank), ctypes.c_int(world_size), buf))
+
+
+def comm_create_id() -> bytes:
+    n = lib().GPB_CommIdSize()
+    buf = ctypes.create_string_buffer(n)
+    _safe_call(lib().GPB_CommCreateId(buf))
+    return buf.raw
+
+
+def partition_rows(num_data: int, world_size: int, rank: int):
+    b = ctypes.c_int32(0)
+    e = ctypes.c_int32(0)
+    _safe_call(lib().GPB_PartitionRows(ctypes.c_int32(num_data), ctypes.c_int(world_size), ctypes.c_int(rank),
+                                       ctypes.byref(b), ctypes.byref(e)))
+    return b.value, e.value
+
+
+def combine_partials(sums, num_data: int, sigma2: float, profile_sigma2: bool):
+    s = _as1d(sums, "sums")
+    nll = np.zeros(1)
+    grad = np.zeros(3)
+    s2 = np.zeros(1)
+    _safe_call(lib().GPB_CombinePartials(_dp(s), num_data, sigma2, int(bool(profile_sigma2)), _dp(nll), _dp(grad),
+                                         _dp(s2)))
+    return float(nll[0]), (grad[:2] if profile_sigma2 else grad).copy(), float(s2[0])

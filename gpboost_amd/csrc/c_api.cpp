@@ -1,0 +1,319 @@
+// extern "C" boundary: the GPB_* / LGBM_* symbols of include/gpboost_amd.h.
+// Error convention of the reference (src/LightGBM/c_api.cpp:54-58, include/LightGBM/c_api.h:1798-1810):
+// every call returns 0 / -1, the message goes to a 512-byte thread-local buffer read by
+// LGBM_GetLastError. Logging goes through LGBM_RegisterLogCallback when registered
+// (log.h:171-191 semantics: "[GPBoost] [Info] ..."), else stderr.
+#include "gpboost_amd.h"
+
+#include <cstdarg>
+#include <cstring>
+#include <exception>
+#include <string>
+
+#include "re_model.h"
+
+using gpb_amd::REModelAMD;
+
+namespace {
+
+thread_local char g_last_error[512] = "Everything is fine";
+void (*g_log_callback)(const char*) = nullptr;
+
+void set_last_error(const char* msg) {
+  std::strncpy(g_last_error, msg, sizeof(g_last_error) - 1);
+  g_last_error[sizeof(g_last_error) - 1] = '\0';
+}
+
+void vlog(const char* level, const char* fmt, va_list ap) {
+  char buf[1024];
+  int k = std::snprintf(buf, sizeof(buf), "[GPBoost] [%s] ", level);
+  std::vsnprintf(buf + k, sizeof(buf) - k, fmt, ap);
+  std::strncat(buf, "\n", sizeof(buf) - std::strlen(buf) - 1);
+  if (g_log_callback) g_log_callback(buf);
+  else std::fputs(buf, stderr);
+}
+
+REModelAMD* model(REModelHandle h) {
+  if (h == nullptr) gpb_amd::Fatal("REModelHandle is NULL");
+  return reinterpret_cast<REModelAMD*>(h);
+}
+
+std::string str_or(const char* s, const char* def) { return s ? std::string(s) : std::string(def); }
+
+}  // namespace
+
+namespace gpb_amd {
+
+void Fatal(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  std::vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  throw std::runtime_error(buf);
+}
+
+void Info(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vlog("Info", fmt, ap);
+  va_end(ap);
+}
+
+void Warning(const char* fmt, ...) {
+  va_list ap;
+  va_start(ap, fmt);
+  vlog("Warning", fmt, ap);
+  va_end(ap);
+}
+
+}  // namespace gpb_amd
+
+#define API_BEGIN() try {
+#define API_END()                                  \
+  }                                                \
+  catch (std::exception & ex) {                    \
+    set_last_error(ex.what());                     \
+    return -1;                                     \
+  }                                                \
+  catch (std::string & ex) {                       \
+    set_last_error(ex.c_str());                    \
+    return -1;                                     \
+  }                                                \
+  catch (...) {                                    \
+    set_last_error("unknown exception");           \
+    return -1;                                     \
+  }                                                \
+  return 0;
+
+extern "C" {
+
+const char* LGBM_GetLastError(void) { return g_last_error; }
+
+int LGBM_RegisterLogCallback(void (*callback)(const char*)) {
+  API_BEGIN();
+  g_log_callback = callback;
+  API_END();
+}
+
+int GPB_CreateREModel(int32_t num_data, const int32_t* cluster_ids_data, const char* re_group_data,
+                      int32_t num_re_group, const double* re_group_rand_coef_data,
+                      const int32_t* ind_effect_group_rand_coef, int32_t num_re_group_rand_coef,
+                      const int* drop_intercept_group_rand_effect, int32_t num_gp, const double* gp_coords_data,
+                      const int dim_gp_coords, const double* gp_rand_coef_data, int32_t num_gp_rand_coef,
+                      const char* cov_fct, double cov_fct_shape, const char* gp_approx, double cov_fct_taper_range,
+                      double cov_fct_taper_shape, int num_neighbors, const char* vecchia_ordering,
+                      int num_ind_points, double cover_tree_radius, const char* ind_points_selection,
+                      const char* likelihood, double likelihood_additional_param,
+                      const char* matrix_inversion_method, int seed, int num_parallel_threads, bool GPU_use,
+                      bool has_weights, const double* weights, double likelihood_learning_rate,
+                      REModelHandle* out) {
+  API_BEGIN();
+  (void)re_group_rand_coef_data; (void)ind_effect_group_rand_coef; (void)drop_intercept_group_rand_effect;
+  (void)cov_fct_taper_range; (void)cov_fct_taper_shape; (void)num_ind_points; (void)cover_tree_radius;
+  (void)ind_points_selection; (void)likelihood_additional_param; (void)num_parallel_threads; (void)GPU_use;
+  (void)weights; (void)likelihood_learning_rate;
+  if (out == nullptr) gpb_amd::Fatal("'out' is NULL");
+  if (num_re_group > 0 || re_group_data != nullptr)
+    gpb_amd::Fatal("grouped random effects are out of scope for gpboost_amd (SURVEY.md §8)");
+  if (num_re_group_rand_coef > 0 || num_gp_rand_coef > 0 || gp_rand_coef_data != nullptr)
+    gpb_amd::Fatal("random coefficients are out of scope for gpboost_amd (SURVEY.md §8)");
+  if (num_gp != 1 || gp_coords_data == nullptr) gpb_amd::Fatal("gpboost_amd requires exactly one GP component (num_gp = 1)");
+  if (has_weights) gpb_amd::Fatal("'weights' are currently not supported for likelihood = 'gaussian'");
+  if (cluster_ids_data != nullptr) {
+    for (int32_t i = 1; i < num_data; ++i)
+      if (cluster_ids_data[i] != cluster_ids_data[0]) gpb_amd::Fatal("multiple clusters (cluster_ids) are out of scope for gpboost_amd");
+  }
+  gpb_amd::ModelConfig cfg;
+  cfg.n = num_data;
+  cfg.d = dim_gp_coords;
+  cfg.cov_fct = str_or(cov_fct, "exponential");
+  cfg.shape = cov_fct_shape;
+  cfg.gp_approx = str_or(gp_approx, "none");
+  cfg.num_neighbors = num_neighbors;
+  cfg.vecchia_ordering = str_or(vecchia_ordering, "random");
+  cfg.likelihood = str_or(likelihood, "gaussian");
+  cfg.matrix_inversion_method = str_or(matrix_inversion_method, "cholesky");
+  if (cfg.matrix_inversion_method == "default") cfg.matrix_inversion_method = "cholesky";
+  cfg.seed = seed;
+  if (seed < 0) gpb_amd::Fatal("seed must be >= 0");
+  *out = new REModelAMD(cfg, gp_coords_data);
+  API_END();
+}
+
+int GPB_REModelFree(REModelHandle handle) {
+  API_BEGIN();
+  delete reinterpret_cast<REModelAMD*>(handle);
+  API_END();
+}
+
+int GPB_SetOptimConfig(REModelHandle handle, double* init_cov_pars, double lr, double acc_rate_cov, int max_iter,
+                       double delta_rel_conv, bool use_nesterov_acc, int nesterov_schedule_version, bool trace,
+                       const char* optimizer, int momentum_offset, const char* convergence_criterion,
+                       int num_covariates, double* init_coef, double lr_coef, double acc_rate_coef,
+                       const char* optimizer_coef, int cg_max_num_it, int cg_max_num_it_tridiag,
+                       double cg_delta_conv, int num_rand_vec_trace, bool reuse_rand_vec_trace,
+                       const char* cg_preconditioner_type, int seed_rand_vec_trace, int piv_chol_rank,
+                       double* init_aux_pars, bool estimate_aux_pars, const int* estimate_cov_par_index,
+                       int m_lbfgs, double delta_conv_mode_finding) {
+  API_BEGIN();
+  (void)init_cov_pars; (void)lr; (void)acc_rate_cov; (void)max_iter; (void)delta_rel_conv; (void)use_nesterov_acc;
+  (void)nesterov_schedule_version; (void)trace; (void)optimizer; (void)momentum_offset; (void)convergence_criterion;
+  (void)num_covariates; (void)init_coef; (void)lr_coef; (void)acc_rate_coef; (void)optimizer_coef;
+  (void)cg_max_num_it_tridiag; (void)reuse_rand_vec_trace; (void)cg_preconditioner_type; (void)piv_chol_rank;
+  (void)init_aux_pars; (void)estimate_aux_pars; (void)estimate_cov_par_index; (void)m_lbfgs;
+  (void)delta_conv_mode_finding;
+  REModelAMD* m = model(handle);
+  m->cg_max_num_it = cg_max_num_it;
+  m->cg_delta_conv = cg_delta_conv;
+  m->num_rand_vec_trace = num_rand_vec_trace;
+  m->seed_rand_vec_trace = seed_rand_vec_trace;
+  API_END();
+}
+
+int GPB_EvalNegLogLikelihood(REModelHandle handle, const double* y_data, double* cov_pars,
+                             const double* fixed_effects, double* negll) {
+  API_BEGIN();
+  REModelAMD* m = model(handle);
+  if (cov_pars == nullptr) gpb_amd::Fatal("cov_pars is NULL (initial-value heuristics are out of scope)");
+  if (fixed_effects != nullptr) {
+    if (y_data == nullptr) gpb_amd::Fatal("EvalNegLogLikelihood: 'y_data' cannot nullptr when 'fixed_effects' is provided");
+    std::vector<double> r(m->config().n);
+    for (int i = 0; i < m->config().n; ++i) r[i] = y_data[i] - fixed_effects[i];
+    m->SetY(r.data());
+  } else if (y_data != nullptr) {
+    m->SetY(y_data);
+  }
+  negll[0] = m->Eval(cov_pars, false, 0).nll;
+  API_END();
+}
+
+int GPB_EvalNegLogLikelihoodGrad(REModelHandle handle, const double* y_data, const double* cov_pars,
+                                 const double* fixed_effects, int profile_sigma2, double* negll, double* grad,
+                                 double* sigma2_out) {
+  API_BEGIN();
+  REModelAMD* m = model(handle);
+  if (cov_pars == nullptr || negll == nullptr || grad == nullptr) gpb_amd::Fatal("NULL argument");
+  if (fixed_effects != nullptr) {
+    if (y_data == nullptr) gpb_amd::Fatal("'y_data' cannot be NULL when 'fixed_effects' is provided");
+    std::vector<double> r(m->config().n);
+    for (int i = 0; i < m->config().n; ++i) r[i] = y_data[i] - fixed_effects[i];
+    m->SetY(r.data());
+  } else if (y_data != nullptr) {
+    m->SetY(y_data);
+  }
+  gpb_amd::EvalResult res = m->Eval(cov_pars, true, profile_sigma2 ? 1 : 0);
+  negll[0] = res.nll;
+  for (size_t k = 0; k < res.grad.size(); ++k) {
+    double g = res.grad[k];
+    if (std::isnan(g) || std::isinf(g)) {  // re_model_template.h:1944-1955
+      gpb_amd::Warning("NaN or Inf occurred in gradient wrt covariance parameter number %d; it is set to 0", (int)k);
+      g = 0.;
+    }
+    grad[k] = g;
+  }
+  if (sigma2_out) sigma2_out[0] = res.sigma2;
+  API_END();
+}
+
+int GPB_GetCurrentNegLogLikelihood(REModelHandle handle, double* negll) {
+  API_BEGIN();
+  negll[0] = model(handle)->last_nll();
+  API_END();
+}
+
+int GPB_GetCovPar(REModelHandle handle, double* cov_par, bool calc_std_dev) {
+  API_BEGIN();
+  if (calc_std_dev) gpb_amd::Fatal("standard deviations of covariance parameters are out of scope for gpboost_amd");
+  const auto& p = model(handle)->last_cov_pars();
+  if (p.empty()) gpb_amd::Fatal("no covariance parameters have been evaluated yet");
+  for (size_t k = 0; k < p.size(); ++k) cov_par[k] = p[k];
+  API_END();
+}
+
+int GPB_GetNumIt(REModelHandle handle, int* num_it) {
+  API_BEGIN();
+  (void)model(handle);
+  num_it[0] = 0;
+  API_END();
+}
+
+int GPB_GetLikelihoodName(REModelHandle handle, char* out_str, int* num_char) {
+  API_BEGIN();
+  const std::string& s = model(handle)->config().likelihood;
+  std::memcpy(out_str, s.c_str(), s.size() + 1);
+  num_char[0] = (int)s.size() + 1;
+  API_END();
+}
+
+int GPB_GetNumAuxPars(REModelHandle handle, int* num_aux_pars) {
+  API_BEGIN();
+  (void)model(handle);
+  num_aux_pars[0] = 0;
+  API_END();
+}
+
+int GPB_GetNumCovPars(REModelHandle handle, int* num_cov_pars) {
+  API_BEGIN();
+  num_cov_pars[0] = model(handle)->num_cov_pars();
+  API_END();
+}
+
+int GPB_GetVecchiaStructure(REModelHandle handle, int32_t* perm, int32_t* neighbors) {
+  API_BEGIN();
+  model(handle)->GetVecchiaStructure(perm, neighbors);
+  API_END();
+}
+
+int GPB_GetVecchiaFactor(REModelHandle handle, const double* cov_pars, double* D_inv, double* B_vals) {
+  API_BEGIN();
+  model(handle)->GetVecchiaFactor(cov_pars, D_inv, B_vals);
+  API_END();
+}
+
+int GPB_GetLastKernelTimes(REModelHandle handle, double* kernel_ms) {
+  API_BEGIN();
+  model(handle)->GetLastKernelTimes(kernel_ms);
+  API_END();
+}
+
+int GPB_CommIdSize(void) { return (int)sizeof(ncclUniqueId); }
+
+int GPB_CommCreateId(char* id_out) {
+  API_BEGIN();
+  ncclUniqueId id;
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) gpb_amd::Fatal("ncclGetUniqueId failed: %s", ncclGetErrorString(r));
+  std::memcpy(id_out, &id, sizeof(id));
+  API_END();
+}
+
+int GPB_SetDistributed(REModelHandle handle, int rank, int world_size, const char* comm_id) {
+  API_BEGIN();
+  ncclUniqueId id;
+  std::memset(&id, 0, sizeof(id));
+  if (world_size > 1) {
+    if (comm_id == nullptr) gpb_amd::Fatal("comm_id is NULL");
+    std::memcpy(&id, comm_id, sizeof(id));
+  }
+  model(handle)->SetDistributed(rank, world_size, id);
+  API_END();
+}
+
+int GPB_PartitionRows(int32_t num_data, int world_size, int rank, int32_t* row_begin, int32_t* row_end) {
+  API_BEGIN();
+  if (world_size < 1 || rank < 0 || rank >= world_size) gpb_amd::Fatal("invalid rank/world_size");
+  const int base = num_data / world_size, rem = num_data % world_size;
+  row_begin[0] = rank * base + (rank < rem ? rank : rem);
+  row_end[0] = row_begin[0] + base + (rank < rem ? 1 : 0);
+  API_END();
+}
+
+int GPB_CombinePartials(const double* sums, int32_t num_data, double sigma2, int profile_sigma2, double* negll,
+                        double* grad, double* sigma2_out) {
+  API_BEGIN();
+  gpb_amd::combine_partials(sums, num_data, sigma2, profile_sigma2 ? 1 : 0, negll, grad, sigma2_out);
+  API_END();
+}
+
+}  // extern "C"

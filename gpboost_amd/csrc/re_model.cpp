@@ -1,0 +1,276 @@
+// REModelAMD implementation (host orchestration; all heavy math in HIP kernels).
+#include "re_model.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+
+#include "cov.h"
+#include "kernels.h"
+#include "vecchia_host.h"
+
+namespace gpb_amd {
+
+namespace {
+
+int parse_cov(const std::string& name, double shape) {
+  // cov_fcts.h:2753-2770 ParseCovFunctionAlias; :170-183 shape handling
+  auto eq = [](double a, double b) { return std::fabs(a - b) < 1e-10; };
+  if (name == "exponential" || name == "Matern") return kMatern05;
+  if (name == "matern") {
+    if (eq(shape, 0.5)) return kMatern05;
+    if (eq(shape, 1.5)) return kMatern15;
+    if (eq(shape, 2.5)) return kMatern25;
+    Fatal("cov_fct 'matern' with shape %g is not supported by gpboost_amd (supported: 0.5, 1.5, 2.5)", shape);
+  }
+  if (name == "gaussian" || name == "Gaussian") return kGaussian;
+  Fatal("cov_fct '%s' is not supported by gpboost_amd (supported: exponential, matern, gaussian)", name.c_str());
+}
+
+}  // namespace
+
+REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : cfg_(cfg) {
+  if (cfg_.n <= 0) Fatal("num_data must be > 0");
+  if (cfg_.d <= 0 || cfg_.d > 3) Fatal("dim_gp_coords = %d not supported (1..3)", cfg_.d);
+  cfg_.cov_type = parse_cov(cfg_.cov_fct, cfg_.shape);
+  if (cfg_.likelihood != "gaussian")
+    Fatal("likelihood '%s' is not supported by gpboost_amd in this build (supported: gaussian)", cfg_.likelihood.c_str());
+  if (cfg_.gp_approx == "vecchia") {
+    vecchia_ = true;
+  } else if (cfg_.gp_approx != "none") {
+    Fatal("gp_approx '%s' is not supported by gpboost_amd (supported: none, vecchia)", cfg_.gp_approx.c_str());
+  }
+  if (cfg_.matrix_inversion_method != "cholesky")
+    Fatal("matrix_inversion_method '%s' is not supported for likelihood 'gaussian' in this build", cfg_.matrix_inversion_method.c_str());
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    Fatal("no HIP device visible: gpboost_amd has no CPU fallback");
+  // The reference ABI has no device argument (c_api.h:1351 only has GPU_use): the device is
+  // GPBOOST_AMD_DEVICE if set (one process per GPU), else the calling thread's current device.
+  if (const char* dev = std::getenv("GPBOOST_AMD_DEVICE")) {
+    device_ = std::atoi(dev);
+    if (device_ < 0 || device_ >= ndev) Fatal("GPBOOST_AMD_DEVICE=%d but %d device(s) visible", device_, ndev);
+  } else {
+    HIP_CHECK(hipGetDevice(&device_));
+  }
+  UseDevice();
+
+  const int n = cfg_.n, d = cfg_.d;
+  coords_.resize((size_t)n * d);
+  for (int i = 0; i < n; ++i)
+    for (int q = 0; q < d; ++q) coords_[(size_t)i * d + q] = coords_colmajor[(size_t)q * n + i];
+
+  HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
+  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_sums_), 16 * sizeof(double), hipHostMallocDefault));
+  row_begin_ = 0;
+  row_end_ = n;
+  if (vecchia_) {
+    if (cfg_.num_neighbors > n - 1) cfg_.num_neighbors = n - 1;  // Vecchia_utils.cpp:754-757
+    if (cfg_.num_neighbors < 1) Fatal("num_neighbors must be >= 1");
+    perm_ = vecchia_order(n, cfg_.seed, cfg_.vecchia_ordering == "random");
+    if (cfg_.vecchia_ordering != "random" && cfg_.vecchia_ordering != "none")
+      Fatal("vecchia_ordering '%s' is not supported (supported: none, random)", cfg_.vecchia_ordering.c_str());
+    coords_vo_.resize((size_t)n * d);
+    for (int i = 0; i < n; ++i)
+      for (int q = 0; q < d; ++q) coords_vo_[(size_t)i * d + q] = coords_[(size_t)perm_[i] * d + q];
+    d_X_.alloc((size_t)n * d);
+    HIP_CHECK(hipMemcpyAsync(d_X_.get(), coords_vo_.data(), sizeof(double) * n * d, hipMemcpyHostToDevice, stream_));
+    // neighbour search is deferred to first use so a distributed model searches only its rows
+  } else {
+    coords_vo_ = coords_;
+    d_X_.alloc((size_t)n * d);
+    HIP_CHECK(hipMemcpyAsync(d_X_.get(), coords_.data(), sizeof(double) * n * d, hipMemcpyHostToDevice, stream_));
+    dense_.reset(new DenseSolver(n, d, d_X_.get(), stream_));
+  }
+  d_sums_.alloc(16);
+  HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+void REModelAMD::UseDevice() const { HIP_CHECK(hipSetDevice(device_)); }
+
+void REModelAMD::EnsureStructure() {
+  if (vecchia_ && !structure_built_) {
+    BuildVecchiaStructure();
+    structure_built_ = true;
+  }
+}
+
+REModelAMD::~REModelAMD() {
+  (void)hipSetDevice(device_);
+  if (stream_) (void)hipStreamSynchronize(stream_);
+  dense_.reset();
+  if (comm_) ncclCommDestroy(comm_);
+  if (h_sums_) (void)hipHostFree(h_sums_);
+  for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
+  if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void REModelAMD::BuildVecchiaStructure() {
+  const int n = cfg_.n, m = cfg_.num_neighbors;
+  // Only this rank's rows are needed on the device (each row's neighbours are earlier points).
+  nbr_.assign((size_t)(row_end_ - row_begin_) * m, -1);
+  nbr_row0_ = row_begin_;
+  vecchia_neighbors(coords_vo_.data(), n, cfg_.d, m, row_begin_, row_end_, nbr_.data());
+  // Device copy laid out by global row index (rows outside this rank's block untouched).
+  d_nbr_.alloc((size_t)n * m);
+  HIP_CHECK(hipMemcpyAsync(d_nbr_.get() + (size_t)row_begin_ * m, nbr_.data(), sizeof(int) * nbr_.size(),
+                           hipMemcpyHostToDevice, stream_));
+  const int nblocks = vecchia_rows_blocks(row_end_ - row_begin_, m);
+  d_block_sums_.alloc((size_t)std::max(nblocks, 1) * kVecchiaSums);
+}
+
+void REModelAMD::SetDistributed(int rank, int world, const ncclUniqueId& id) {
+  if (world < 1 || rank < 0 || rank >= world) Fatal("invalid rank %d / world_size %d", rank, world);
+  UseDevice();
+  rank_ = rank;
+  world_ = world;
+  if (!vecchia_ && world > 1) Fatal("the dense (gp_approx='none') path runs as replicas only; SetDistributed needs gp_approx='vecchia'");
+  if (comm_) { ncclCommDestroy(comm_); comm_ = nullptr; }
+  if (world > 1) {
+    ncclResult_t r = ncclCommInitRank(&comm_, world, id, rank);
+    if (r != ncclSuccess) Fatal("ncclCommInitRank failed: %s", ncclGetErrorString(r));
+  }
+  const int n = cfg_.n;
+  const int base = n / world, rem = n % world;
+  row_begin_ = rank * base + std::min(rank, rem);
+  row_end_ = row_begin_ + base + (rank < rem ? 1 : 0);
+  structure_built_ = false;
+  EnsureStructure();
+  HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+void REModelAMD::TransformCovPars(const double* orig, double* trafo) const {
+  // re_model_template.h:7189-7213 -> cov_fcts.h:438-460
+  if (!(orig[0] > 0. && orig[1] > 0. && orig[2] > 0.)) Fatal("covariance parameters must be > 0");
+  trafo[0] = orig[0];
+  trafo[1] = orig[1] / orig[0];
+  switch (cfg_.cov_type) {
+    case kMatern05: trafo[2] = 1. / orig[2]; break;
+    case kMatern15: trafo[2] = std::sqrt(3.) / orig[2]; break;
+    case kMatern25: trafo[2] = std::sqrt(5.) / orig[2]; break;
+    default: trafo[2] = 1. / (orig[2] * orig[2]); break;
+  }
+}
+
+void REModelAMD::SetY(const double* y) {
+  // re_model_template.h:5689-5726: y is copied (and permuted into Vecchia order)
+  UseDevice();
+  const int n = cfg_.n;
+  std::vector<double> yv(n);
+  if (vecchia_) for (int i = 0; i < n; ++i) yv[i] = y[perm_[i]];
+  else std::copy(y, y + n, yv.begin());
+  d_y_.alloc(n);
+  HIP_CHECK(hipMemcpyAsync(d_y_.get(), yv.data(), sizeof(double) * n, hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  y_set_ = true;
+}
+
+void REModelAMD::EvalVecchia(const double* trafo, double* sums) {
+  VecchiaRowsArgs a{};
+  a.X = d_X_.get();
+  a.Y = d_y_.get();
+  a.nbr = d_nbr_.get();
+  a.n = cfg_.n;
+  a.d = cfg_.d;
+  a.m = cfg_.num_neighbors;
+  a.r0 = row_begin_;
+  a.r1 = row_end_;
+  a.var = trafo[1];
+  a.phi = trafo[2];
+  a.diag_mult = 1.;
+  a.diag_add = 1.;
+  a.d_nugget = 1.;
+  a.block_sums = d_block_sums_.get();
+  const int nblocks = vecchia_rows_blocks(row_end_ - row_begin_, a.m);
+  HIP_CHECK(hipEventRecord(ev_[0], stream_));
+  launch_vecchia_rows(cfg_.cov_type, a, stream_);
+  HIP_CHECK(hipEventRecord(ev_[1], stream_));
+  launch_sum_blocks(d_block_sums_.get(), nblocks, kVecchiaSums, d_sums_.get(), stream_);
+  if (world_ > 1) {
+    ncclResult_t r = ncclAllReduce(d_sums_.get(), d_sums_.get(), kVecchiaSums, ncclDouble, ncclSum, comm_, stream_);
+    if (r != ncclSuccess) Fatal("ncclAllReduce failed: %s", ncclGetErrorString(r));
+  }
+  HIP_CHECK(hipMemcpyAsync(h_sums_, d_sums_.get(), sizeof(double) * kVecchiaSums, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipEventRecord(ev_[2], stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  float ms0 = 0.f, ms1 = 0.f;
+  HIP_CHECK(hipEventElapsedTime(&ms0, ev_[0], ev_[1]));
+  HIP_CHECK(hipEventElapsedTime(&ms1, ev_[0], ev_[2]));
+  last_kernel_ms_[0] = ms0;
+  last_kernel_ms_[1] = ms1;
+  std::copy(h_sums_, h_sums_ + kVecchiaSums, sums);
+}
+
+void REModelAMD::EvalDense(const double* trafo, bool want_grad, double* sums) {
+  dense_->Eval(cfg_.cov_type, trafo[1], trafo[2], d_y_.get(), want_grad, sums, last_kernel_ms_);
+}
+
+EvalResult REModelAMD::Eval(const double* cov_pars_orig, bool want_grad, int profile) {
+  if (!y_set_) Fatal("response variable y has not been set");
+  UseDevice();
+  EnsureStructure();
+  double trafo[3];
+  TransformCovPars(cov_pars_orig, trafo);
+  double sums[kVecchiaSums];
+  if (vecchia_) EvalVecchia(trafo, sums);
+  else EvalDense(trafo, want_grad, sums);
+  if (!std::isfinite(sums[0]) || !std::isfinite(sums[1]))
+    Fatal("NaN or Inf occurred in the negative log-likelihood (non-positive-definite covariance?)");
+  EvalResult res;
+  res.grad.resize(profile ? 2 : 3);
+  combine_partials(sums, cfg_.n, trafo[0], profile, &res.nll, res.grad.data(), &res.sigma2);
+  last_nll_ = res.nll;
+  last_cov_pars_.assign(cov_pars_orig, cov_pars_orig + 3);
+  if (profile) last_cov_pars_[0] = res.sigma2;
+  return res;
+}
+
+void REModelAMD::GetVecchiaStructure(int* perm, int* nbr) const {
+  if (!vecchia_) Fatal("model does not use the Vecchia approximation");
+  if (world_ > 1) Fatal("GetVecchiaStructure is only available on single-rank models");
+  const_cast<REModelAMD*>(this)->UseDevice();
+  const_cast<REModelAMD*>(this)->EnsureStructure();
+  std::copy(perm_.begin(), perm_.end(), perm);
+  std::copy(nbr_.begin(), nbr_.end(), nbr);
+}
+
+void REModelAMD::GetVecchiaFactor(const double* cov_pars_orig, double* Dinv, double* Bvals) {
+  if (!vecchia_) Fatal("model does not use the Vecchia approximation");
+  if (world_ > 1) Fatal("GetVecchiaFactor is only available on single-rank models");
+  UseDevice();
+  EnsureStructure();
+  double trafo[3];
+  TransformCovPars(cov_pars_orig, trafo);
+  const int n = cfg_.n, m = cfg_.num_neighbors;
+  DevBuf<double> dD(n), dB((size_t)n * m);
+  VecchiaRowsArgs a{};
+  a.X = d_X_.get();
+  a.Y = nullptr;
+  a.nbr = d_nbr_.get();
+  a.n = n; a.d = cfg_.d; a.m = m; a.r0 = 0; a.r1 = n;
+  a.var = trafo[1]; a.phi = trafo[2];
+  a.diag_mult = 1.; a.diag_add = 1.; a.d_nugget = 1.;
+  a.Dinv_out = dD.get();
+  a.B_out = dB.get();
+  launch_vecchia_rows(cfg_.cov_type, a, stream_);
+  HIP_CHECK(hipMemcpyAsync(Dinv, dD.get(), sizeof(double) * n, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipMemcpyAsync(Bvals, dB.get(), sizeof(double) * n * m, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+void combine_partials(const double* s, int n, double sigma2_in, int profile, double* nll, double* grad,
+                      double* sigma2_out) {
+  // s = [logdet, q, s1_var, s1_range, s2_var, s2_range]
+  const double logdet = s[0], q = s[1];
+  const double sigma2 = profile ? q / n : sigma2_in;          // ProfileOutSigma2 (re_model_template.h:2407)
+  *nll = q / 2. / sigma2 + logdet / 2. + n / 2. * (std::log(sigma2) + std::log(2 * M_PI));  // :2880, :2890
+  int off = 0;
+  if (!profile) { grad[0] = -q / sigma2 / 2. + n / 2.; off = 1; }  // :1774 / :1806
+  grad[off + 0] = s[2] / sigma2 + 0.5 * s[4];                    // :1786-1787 / :1813-1814
+  grad[off + 1] = s[3] / sigma2 + 0.5 * s[5];
+  if (sigma2_out) *sigma2_out = sigma2;
+}
+
+}  // namespace gpb_amd

@@ -1,0 +1,110 @@
+// REModelAMD: host-side model object behind the GPB_* C ABI.
+//
+// Mirrors the role of the reference's REModel facade + REModelTemplate
+// (re_model.cpp:21-111, re_model_template.h:95-465) for the in-scope path:
+// one GP component, dense ("none") or Vecchia approximation, Gaussian likelihood.
+// Host code keeps configuration, the Vecchia structure (built once) and scalar
+// assembly; every O(n) / O(n m^2) / O(n^3) step runs in HIP kernels on the model's
+// stream. Device buffers are allocated once at construction / SetY and reused.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "common.h"
+#include "dense.h"
+
+namespace gpb_amd {
+
+struct ModelConfig {
+  int n = 0;
+  int d = 0;
+  std::string cov_fct = "exponential";
+  double shape = 0.5;
+  int cov_type = 0;
+  std::string gp_approx = "none";
+  int num_neighbors = 20;
+  std::string vecchia_ordering = "random";
+  std::string likelihood = "gaussian";
+  std::string matrix_inversion_method = "cholesky";
+  int seed = 0;
+};
+
+struct EvalResult {
+  double nll = 0.;
+  double sigma2 = 0.;
+  std::vector<double> grad;
+};
+
+class REModelAMD {
+ public:
+  REModelAMD(const ModelConfig& cfg, const double* coords_colmajor);
+  ~REModelAMD();
+
+  int num_cov_pars() const { return 3; }
+  int device() const { return device_; }
+  const ModelConfig& config() const { return cfg_; }
+
+  void SetY(const double* y);
+  bool HasY() const { return y_set_; }
+
+  // cov_pars on the original scale. profile: 0 -> include_error_var gradient, 1 -> L-BFGS unit.
+  EvalResult Eval(const double* cov_pars_orig, bool want_grad, int profile);
+
+  void SetDistributed(int rank, int world, const ncclUniqueId& id);
+
+  void GetVecchiaStructure(int* perm, int* nbr) const;
+  void GetVecchiaFactor(const double* cov_pars_orig, double* Dinv, double* Bvals);
+  void GetLastKernelTimes(double* ms) const { ms[0] = last_kernel_ms_[0]; ms[1] = last_kernel_ms_[1]; }
+
+  double last_nll() const { return last_nll_; }
+  const std::vector<double>& last_cov_pars() const { return last_cov_pars_; }
+
+  // optimizer settings kept for API parity (GPB_SetOptimConfig)
+  int cg_max_num_it = 1000;
+  double cg_delta_conv = 1e-2;
+  int num_rand_vec_trace = 50;
+  int seed_rand_vec_trace = 1;
+
+ private:
+  void TransformCovPars(const double* orig, double* trafo) const;
+  void BuildVecchiaStructure();
+  void EvalVecchia(const double* trafo, double* sums);  // sums over this rank's rows, all-reduced
+  void EvalDense(const double* trafo, bool want_grad, double* sums);
+
+  void EnsureStructure();
+  void UseDevice() const;
+
+  ModelConfig cfg_;
+  int device_ = 0;
+  bool vecchia_ = false;
+  bool structure_built_ = false;
+  std::vector<double> coords_;       // row-major n x d, original order
+  std::vector<double> coords_vo_;    // Vecchia order (Vecchia) / original (dense)
+  std::vector<int> perm_;
+  std::vector<int> nbr_;             // rows [row_begin_, row_end_) x m, or all rows when world == 1
+  int nbr_row0_ = 0;
+  bool y_set_ = false;
+
+  hipStream_t stream_ = nullptr;
+  hipEvent_t ev_[3] = {nullptr, nullptr, nullptr};
+  DevBuf<double> d_X_, d_y_, d_block_sums_, d_sums_;
+  DevBuf<int> d_nbr_;
+  double* h_sums_ = nullptr;  // pinned
+
+  std::unique_ptr<DenseSolver> dense_;
+
+  int rank_ = 0, world_ = 1;
+  int row_begin_ = 0, row_end_ = 0;
+  ncclComm_t comm_ = nullptr;
+
+  double last_nll_ = 0.;
+  std::vector<double> last_cov_pars_;
+  double last_kernel_ms_[2] = {0., 0.};
+};
+
+}  // namespace gpb_amd

@@ -1,0 +1,15 @@
+#pragma once
+
+#include <vector>
+
+namespace gpb_amd {
+
+// perm[i] = original index of the i-th point in the Vecchia order.
+std::vector<int> vecchia_order(int n, int seed, bool random);
+
+// Neighbour lists for rows [row_begin, row_end) of the Vecchia-ordered coordinates x
+// (row-major n x d). nbr has (row_end - row_begin) x m entries; row i holds min(i, m)
+// indices in ascending distance, the rest -1. Requires m <= n - 1.
+void vecchia_neighbors(const double* x, int n, int d, int m, int row_begin, int row_end, int* nbr);
+
+}  // namespace gpb_amd

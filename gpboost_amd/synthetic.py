@@ -1,0 +1,82 @@
+"""Portable synthetic inputs for tests and benchmarks.
+
+The generator is the linear congruential generator the reference's own R tests
+use (R-package/tests/testthat/test_GPModel_gaussian_process.R:29-35):
+
+    sim[1] = floor(c * 2^32);  sim[k] = (22695477 * sim[k-1] + 1) %% 2^32;  u = sim / 2^32
+
+evaluated in IEEE double arithmetic exactly as R does it (the product exceeds
+2^53, so the rounding is part of the definition). Everything here is input
+generation only: no likelihood arithmetic.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+_MOD = 4294967296.0
+
+
+def sim_rand_unif(n: int, init_c: float = 0.1) -> np.ndarray:
+    """R-test LCG (test_GPModel_gaussian_process.R:29-35), double arithmetic."""
+    out = np.empty(n, dtype=np.float64)
+    s = float(np.floor(init_c * _MOD))
+    out[0] = s
+    for k in range(1, n):
+        s = (22695477.0 * s + 1.0) % _MOD
+        out[k] = s
+    return out / _MOD
+
+
+def rtest_coords(n: int = 100, d: int = 2) -> np.ndarray:
+    """coords <- matrix(sim_rand_unif(n*d, 0.1), ncol=d)  (column-major fill)."""
+    return sim_rand_unif(n * d, 0.1).reshape(d, n).T.copy()
+
+
+def rtest_gaussian_y(n: int = 100) -> tuple[np.ndarray, np.ndarray]:
+    """The R tests' GP data (test_GPModel_gaussian_process.R:38-61): y = eps + xi."""
+    from scipy.stats import norm
+
+    coords = rtest_coords(n)
+    diff = coords[:, None, :] - coords[None, :, :]
+    dist = np.sqrt((diff ** 2).sum(-1))
+    sigma = np.exp(-dist / 0.1) + np.eye(n) * 1e-20
+    chol = np.linalg.cholesky(sigma)
+    b1 = norm.ppf(sim_rand_unif(n, 0.8))
+    eps = chol @ b1
+    xi = norm.ppf(sim_rand_unif(n, 0.1)) / 5.0
+    return coords, eps + xi
+
+
+def rtest_bernoulli_probit_y(n: int = 100) -> tuple[np.ndarray, np.ndarray]:
+    """R non-Gaussian test data (test_GPModel_non_Gaussian_data.R:17-81 pattern)."""
+    from scipy.stats import norm
+
+    coords = rtest_coords(n)
+    diff = coords[:, None, :] - coords[None, :, :]
+    dist = np.sqrt((diff ** 2).sum(-1))
+    sigma = np.exp(-dist / 0.1) + np.eye(n) * 1e-20
+    chol = np.linalg.cholesky(sigma)
+    b1 = norm.ppf(sim_rand_unif(n, 0.8))
+    eps = chol @ b1
+    probs = norm.cdf(eps)
+    y = (sim_rand_unif(n, 0.19341) < probs).astype(np.float64)
+    return coords, y
+
+
+def bench_coords(n: int, d: int = 2) -> np.ndarray:
+    """Benchmark coordinates: 2n LCG draws (c=0.1) filled column-major."""
+    return sim_rand_unif(n * d, 0.1).reshape(d, n).T.copy()
+
+
+def bench_gaussian_y(n: int) -> np.ndarray:
+    """iid N(0,1) by Box-Muller from LCG streams c=0.8 and c=0.42."""
+    u1 = np.maximum(sim_rand_unif(n, 0.8), 1e-300)
+    u2 = sim_rand_unif(n, 0.42)
+    return np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2)
+
+
+def bench_bernoulli_y(coords: np.ndarray) -> np.ndarray:
+    """y = 1[u < (1 + sin(2 pi x1) cos(2 pi x2)) / 2], u from LCG c=0.19341."""
+    n = coords.shape[0]
+    p = 0.5 * (1.0 + np.sin(2 * np.pi * coords[:, 0]) * np.cos(2 * np.pi * coords[:, 1]))
+    return (sim_rand_unif(n, 0.19341) < p).astype(np.float64)

@@ -1,0 +1,209 @@
+/*
+ * gpboost_amd — MI355X-native GP / mixed-effects likelihood engine.
+ * C-ABI drop-in boundary (plain pointers and sizes, no torch or HIP types).
+ *
+ * Every GPB_* / LGBM_* entry point below has the signature and semantics of the
+ * reference GPBoost C API it replaces (cited per function, paths relative to the
+ * reference repository), so GPBoost's Python/R packages can bind this library
+ * instead of lib_gpboost.so for the REModel likelihood path. Functions marked
+ * EXTENSION do not exist in the reference (the reference exposes
+ * no gradient entry point); they are additive.
+ *
+ * Conventions (identical to the reference): every function returns 0 on success
+ * and -1 on failure; the failure message is kept in a thread-local buffer that
+ * LGBM_GetLastError() returns (include/LightGBM/c_api.h:1798-1810,
+ * src/LightGBM/c_api.cpp:54-58). Input arrays are borrowed for the duration of
+ * the call and copied; output arrays are caller-allocated. A handle is not
+ * thread-safe.
+ *
+ * Scope of this build: one GP component (num_gp = 1) with
+ * cov_fct in {exponential, matern (shape 0.5/1.5/2.5), gaussian},
+ * gp_approx in {"none" (dense), "vecchia"}, likelihood "gaussian".
+ * Anything else fails with -1 and a message naming the unsupported option.
+ * The compute path is HIP on gfx950; there is no CPU fallback: if no GPU is
+ * visible, GPB_CreateREModel fails.
+ */
+#ifndef GPBOOST_AMD_H_
+#define GPBOOST_AMD_H_
+
+#include <stdbool.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPBOOST_AMD_EXPORT __attribute__((visibility("default")))
+
+typedef void* REModelHandle;
+
+/* ---------------------------------------------------------------- errors / logging */
+
+/* replaces LGBM_GetLastError (include/LightGBM/c_api.h:54; c_api.cpp:1008) */
+GPBOOST_AMD_EXPORT const char* LGBM_GetLastError(void);
+
+/* replaces LGBM_RegisterLogCallback (include/LightGBM/c_api.h:61; c_api.cpp:1012) */
+GPBOOST_AMD_EXPORT int LGBM_RegisterLogCallback(void (*callback)(const char*));
+
+/* ---------------------------------------------------------------- model lifecycle */
+
+/* replaces GPB_CreateREModel (include/LightGBM/c_api.h:1358-1390; c_api.cpp:2693-2762) */
+GPBOOST_AMD_EXPORT int GPB_CreateREModel(int32_t num_data,
+    const int32_t* cluster_ids_data,
+    const char* re_group_data,
+    int32_t num_re_group,
+    const double* re_group_rand_coef_data,
+    const int32_t* ind_effect_group_rand_coef,
+    int32_t num_re_group_rand_coef,
+    const int* drop_intercept_group_rand_effect,
+    int32_t num_gp,
+    const double* gp_coords_data,
+    const int dim_gp_coords,
+    const double* gp_rand_coef_data,
+    int32_t num_gp_rand_coef,
+    const char* cov_fct,
+    double cov_fct_shape,
+    const char* gp_approx,
+    double cov_fct_taper_range,
+    double cov_fct_taper_shape,
+    int num_neighbors,
+    const char* vecchia_ordering,
+    int num_ind_points,
+    double cover_tree_radius,
+    const char* ind_points_selection,
+    const char* likelihood,
+    double likelihood_additional_param,
+    const char* matrix_inversion_method,
+    int seed,
+    int num_parallel_threads,
+    bool GPU_use,
+    bool has_weights,
+    const double* weights,
+    double likelihood_learning_rate,
+    REModelHandle* out);
+
+/* replaces GPB_REModelFree (include/LightGBM/c_api.h:1397; c_api.cpp:2764-2768) */
+GPBOOST_AMD_EXPORT int GPB_REModelFree(REModelHandle handle);
+
+/* replaces GPB_SetOptimConfig (include/LightGBM/c_api.h:1433-1462; c_api.cpp:2770-2830).
+ * Stored; the iterative-solver fields (cg_*, num_rand_vec_trace, seed_rand_vec_trace)
+ * are the ones this build uses. */
+GPBOOST_AMD_EXPORT int GPB_SetOptimConfig(REModelHandle handle,
+    double* init_cov_pars,
+    double lr,
+    double acc_rate_cov,
+    int max_iter,
+    double delta_rel_conv,
+    bool use_nesterov_acc,
+    int nesterov_schedule_version,
+    bool trace,
+    const char* optimizer,
+    int momentum_offset,
+    const char* convergence_criterion,
+    int num_covariates,
+    double* init_coef,
+    double lr_coef,
+    double acc_rate_coef,
+    const char* optimizer_coef,
+    int cg_max_num_it,
+    int cg_max_num_it_tridiag,
+    double cg_delta_conv,
+    int num_rand_vec_trace,
+    bool reuse_rand_vec_trace,
+    const char* cg_preconditioner_type,
+    int seed_rand_vec_trace,
+    int piv_chol_rank,
+    double* init_aux_pars,
+    bool estimate_aux_pars,
+    const int* estimate_cov_par_index,
+    int m_lbfgs,
+    double delta_conv_mode_finding);
+
+/* ---------------------------------------------------------------- likelihood evaluation */
+
+/* replaces GPB_EvalNegLogLikelihood (include/LightGBM/c_api.h:1500; c_api.cpp:2854-2863).
+ * cov_pars on the ORIGINAL scale (sigma2, sigma1^2, rho), nll written to negll[0].
+ * y may be NULL to reuse the response set by the previous call. */
+GPBOOST_AMD_EXPORT int GPB_EvalNegLogLikelihood(REModelHandle handle,
+    const double* y_data,
+    double* cov_pars,
+    const double* fixed_effects,
+    double* negll);
+
+/* EXTENSION. nll and its gradient in one evaluation.
+ * profile_sigma2 == 0: gradient with respect to log of every covariance parameter on the
+ *   reference's transformed scale (sigma2, sigma1^2/sigma2, range transform), i.e.
+ *   REModelTemplate::CalcGradPars(..., include_error_var=true) (re_model_template.h:1748-1818);
+ *   grad has num_cov_pars entries.
+ * profile_sigma2 == 1: the reference's L-BFGS objective unit
+ *   (include/GPBoost/optim_utils.h:243-364): sigma2 is profiled out (yT Psi^-1 y / n),
+ *   negll is the profiled nll, grad has num_cov_pars-1 entries (sigma2 excluded), and
+ *   sigma2_out (may be NULL) receives the profiled sigma2.
+ * y may be NULL (reuse). */
+GPBOOST_AMD_EXPORT int GPB_EvalNegLogLikelihoodGrad(REModelHandle handle,
+    const double* y_data,
+    const double* cov_pars,
+    const double* fixed_effects,
+    int profile_sigma2,
+    double* negll,
+    double* grad,
+    double* sigma2_out);
+
+/* replaces GPB_GetCurrentNegLogLikelihood (include/LightGBM/c_api.h:1512) */
+GPBOOST_AMD_EXPORT int GPB_GetCurrentNegLogLikelihood(REModelHandle handle, double* negll);
+
+/* replaces GPB_GetCovPar (include/LightGBM/c_api.h:1526): last evaluated cov_pars
+ * (original scale); std devs are not computed by this build (calc_std_dev must be false). */
+GPBOOST_AMD_EXPORT int GPB_GetCovPar(REModelHandle handle, double* cov_par, bool calc_std_dev);
+
+/* replaces GPB_GetNumIt (include/LightGBM/c_api.h:1559) */
+GPBOOST_AMD_EXPORT int GPB_GetNumIt(REModelHandle handle, int* num_it);
+
+/* replaces GPB_GetLikelihoodName (include/LightGBM/c_api.h:1659) */
+GPBOOST_AMD_EXPORT int GPB_GetLikelihoodName(REModelHandle handle, char* out_str, int* num_char);
+
+/* replaces GPB_GetNumAuxPars (include/LightGBM/c_api.h:1776) */
+GPBOOST_AMD_EXPORT int GPB_GetNumAuxPars(REModelHandle handle, int* num_aux_pars);
+
+/* ---------------------------------------------------------------- EXTENSION: introspection */
+
+/* Number of covariance parameters (incl. sigma2) of the model. */
+GPBOOST_AMD_EXPORT int GPB_GetNumCovPars(REModelHandle handle, int* num_cov_pars);
+
+/* Vecchia ordering permutation (perm[i] = original index of the i-th point in the
+ * Vecchia order) and neighbour lists (n x num_neighbors, -1 padded) exactly as the
+ * reference builds them (Vecchia_utils.cpp:1094-1161). Arrays caller-allocated. */
+GPBOOST_AMD_EXPORT int GPB_GetVecchiaStructure(REModelHandle handle, int32_t* perm, int32_t* neighbors);
+
+/* Vecchia factor at the given cov_pars (original scale): D^-1 (n, Vecchia order) and
+ * B values (n x num_neighbors; B(i, nbr) = -A_i, 0-padded). Computed on the GPU. */
+GPBOOST_AMD_EXPORT int GPB_GetVecchiaFactor(REModelHandle handle, const double* cov_pars,
+    double* D_inv, double* B_vals);
+
+/* Timing of the last evaluation's dominant kernel (ms, HIP events on the model's stream),
+ * for the benchmark's live roofline. kernel_ms[0] = factor/Cholesky kernel,
+ * kernel_ms[1] = whole device-side evaluation. */
+GPBOOST_AMD_EXPORT int GPB_GetLastKernelTimes(REModelHandle handle, double* kernel_ms);
+
+/* ---------------------------------------------------------------- EXTENSION: multi-GPU */
+
+/* Size of the opaque communicator id (bytes). */
+GPBOOST_AMD_EXPORT int GPB_CommIdSize(void);
+/* Create a communicator id on one rank (to be broadcast to all ranks by the caller). */
+GPBOOST_AMD_EXPORT int GPB_CommCreateId(char* id_out);
+/* Join the model to an RCCL communicator: rows (observations in Vecchia order) are
+ * split into world_size contiguous blocks; this rank evaluates block `rank` and the
+ * per-rank partial sums are all-reduced over RCCL (one all-reduce of 6 doubles per
+ * evaluation). Must be called before the first evaluation. */
+GPBOOST_AMD_EXPORT int GPB_SetDistributed(REModelHandle handle, int rank, int world_size, const char* comm_id);
+/* Host-side partition of n rows over world_size ranks (block distribution). */
+GPBOOST_AMD_EXPORT int GPB_PartitionRows(int32_t num_data, int world_size, int rank, int32_t* row_begin, int32_t* row_end);
+/* Host-side final assembly from all-reduced partial sums (exposed so the reduction
+ * contract can be tested without a GPU): sums = [logdet, q, s1_var, s1_range, s2_var, s2_range]. */
+GPBOOST_AMD_EXPORT int GPB_CombinePartials(const double* sums, int32_t num_data, double sigma2,
+    int profile_sigma2, double* negll, double* grad, double* sigma2_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPBOOST_AMD_H_ */

@@ -1,0 +1,336 @@
+// ORACLE TEST INFRASTRUCTURE — NOT PART OF THE PRODUCT.
+// CPU restatement of the reference GP-likelihood hot path (see gp_oracle.h for the
+// contract and how it is pinned). Written from the reference's math, citing the
+// reference file:line each function follows. Plain loops, no Eigen, no GPU.
+#include "gp_oracle.h"
+
+#include <algorithm>
+#include <cmath>
+#include <limits>
+#include <numeric>
+#include <random>
+#include <vector>
+
+namespace {
+
+constexpr double kNugget = 1.0;  // transformed scale: Psi = Sigma/sigma2 + I
+
+// cov_fcts.h:1681-1745 (CovarianceMaternShape0_5/1_5/2_5, CovarianceGaussian)
+double cov(int t, double r, double var, double phi) {
+  switch (t) {
+    case ORC_MATERN05: return var * std::exp(-phi * r);
+    case ORC_MATERN15: { double x = phi * r; return var * (1. + x) * std::exp(-x); }
+    case ORC_MATERN25: { double x = phi * r; return var * (1. + x + x * x / 3.) * std::exp(-x); }
+    case ORC_GAUSSIAN: return var * std::exp(-phi * r * r);
+  }
+  return 0.;
+}
+
+// d cov / d log(phi) on the transformed scale: cov_fcts.h:1750-1786 (cm constants with
+// transf_scale=true) and :2116-2143 (GradientRange*).
+double dcov_dlogphi(int t, double r, double var, double phi) {
+  switch (t) {
+    case ORC_MATERN05: return -phi * r * cov(t, r, var, phi);
+    case ORC_MATERN15: return -var * phi * phi * r * r * std::exp(-phi * r);
+    case ORC_MATERN25: { double x = phi * r; return -var * phi * phi / 3. * r * r * (1. + x) * std::exp(-x); }
+    case ORC_GAUSSIAN: return -phi * r * r * cov(t, r, var, phi);
+  }
+  return 0.;
+}
+
+double dist(const double* a, const double* b, int d) {
+  double s = 0.;
+  for (int k = 0; k < d; ++k) { double t = a[k] - b[k]; s += t * t; }
+  return std::sqrt(s);
+}
+
+// In-place lower Cholesky of a k x k row-major SPD matrix (Eigen::LLT equivalent math).
+bool chol(std::vector<double>& a, int k) {
+  for (int j = 0; j < k; ++j) {
+    double s = a[j * k + j];
+    for (int p = 0; p < j; ++p) s -= a[j * k + p] * a[j * k + p];
+    if (!(s > 0.)) return false;
+    double ljj = std::sqrt(s);
+    a[j * k + j] = ljj;
+    for (int i = j + 1; i < k; ++i) {
+      double t = a[i * k + j];
+      for (int p = 0; p < j; ++p) t -= a[i * k + p] * a[j * k + p];
+      a[i * k + j] = t / ljj;
+    }
+  }
+  return true;
+}
+
+// Solve (L L^T) x = b in place.
+void chol_solve(const std::vector<double>& l, int k, double* b) {
+  for (int i = 0; i < k; ++i) {
+    double t = b[i];
+    for (int p = 0; p < i; ++p) t -= l[i * k + p] * b[p];
+    b[i] = t / l[i * k + i];
+  }
+  for (int i = k - 1; i >= 0; --i) {
+    double t = b[i];
+    for (int p = i + 1; p < k; ++p) t -= l[p * k + i] * b[p];
+    b[i] = t / l[i * k + i];
+  }
+}
+
+// Per-row Vecchia factor + derivatives for one row (Vecchia_utils.cpp:1405-1617,
+// Gaussian likelihood, single GP component, transf_scale = true).
+struct RowFactor {
+  int k;
+  std::vector<double> A;            // A_i (B(i,nbr) = -A_i)
+  double D;                         // D_ii (not inverted)
+  std::vector<double> dA[2];        // dA_i / dlog(par), par = var, range
+  double dD[2];
+};
+
+void row_factor(const double* coords, const int* nbr_row, int i, int d, int m, int t,
+                double var, double phi, RowFactor& f) {
+  int k = std::min(i, m);
+  f.k = k;
+  f.A.assign(k, 0.);
+  f.dA[0].assign(k, 0.);
+  f.dA[1].assign(k, 0.);
+  f.D = kNugget + var;        // :1351 identity nugget, :1507 += marginal variance
+  f.dD[0] = var;              // :1512 derivative wrt the variance (transformed scale)
+  f.dD[1] = 0.;
+  if (k == 0) return;
+  const double* xi = coords + (size_t)i * d;
+  std::vector<double> c(k), dc(k), C(k * k), dC(k * k);
+  for (int a = 0; a < k; ++a) {
+    const double* xa = coords + (size_t)nbr_row[a] * d;
+    double r = dist(xi, xa, d);
+    c[a] = cov(t, r, var, phi);
+    dc[a] = dcov_dlogphi(t, r, var, phi);
+    for (int b = 0; b < k; ++b) {
+      if (a == b) { C[a * k + b] = var; dC[a * k + b] = 0.; continue; }  // variance on diag, grad 0
+      const double* xb = coords + (size_t)nbr_row[b] * d;
+      double rab = dist(xa, xb, d);
+      C[a * k + b] = cov(t, rab, var, phi);
+      dC[a * k + b] = dcov_dlogphi(t, rab, var, phi);
+    }
+  }
+  std::vector<double> L = C;
+  for (int a = 0; a < k; ++a) L[a * k + a] += kNugget;   // :1540 nugget on between-neighbour cov
+  if (!chol(L, k)) { f.D = std::numeric_limits<double>::quiet_NaN(); return; }
+  // A_i = (C^-1 c)^T  (:1557)
+  f.A = c;
+  chol_solve(L, k, f.A.data());
+  double Ac = 0.;
+  for (int a = 0; a < k; ++a) Ac += f.A[a] * c[a];
+  f.D -= Ac;                                              // :1562
+  // gradients (:1573-1585): dA = (C^-1 dc)^T - A (C^-1 dC)^T ;
+  // dD = d(marg var) - (dA c + A dc)
+  for (int p = 0; p < 2; ++p) {
+    const std::vector<double>& dcp = (p == 0) ? c : dc;      // d/dlog var: dc = c, dC = C
+    const std::vector<double>& dCp = (p == 0) ? C : dC;
+    std::vector<double> s = dcp;
+    chol_solve(L, k, s.data());
+    // A (C^-1 dC)^T = A dC C^-1  -> row vector: w^T = A dC, then solve
+    std::vector<double> w(k, 0.);
+    for (int b = 0; b < k; ++b) {
+      double acc = 0.;
+      for (int a = 0; a < k; ++a) acc += f.A[a] * dCp[a * k + b];
+      w[b] = acc;
+    }
+    chol_solve(L, k, w.data());
+    double dAc = 0., Adc = 0.;
+    for (int a = 0; a < k; ++a) {
+      f.dA[p][a] = s[a] - w[a];
+      dAc += f.dA[p][a] * c[a];
+      Adc += f.A[a] * dcp[a];
+    }
+    if (p == 0) f.dD[0] -= (dAc + Adc);   // :1579 ipar == 0 -> subtract from existing
+    else f.dD[1] = -(dAc + Adc);          // :1583 range -> overwrite
+  }
+}
+
+int num_pars_grad() { return 2; }
+
+}  // namespace
+
+extern "C" {
+
+void orc_transform_cov_pars(int t, const double* orig, double* trafo) {
+  // cov_fcts.h:438-460
+  trafo[0] = orig[0];
+  trafo[1] = orig[1] / orig[0];
+  switch (t) {
+    case ORC_MATERN05: trafo[2] = 1. / orig[2]; break;
+    case ORC_MATERN15: trafo[2] = std::sqrt(3.) / orig[2]; break;
+    case ORC_MATERN25: trafo[2] = std::sqrt(5.) / orig[2]; break;
+    case ORC_GAUSSIAN: trafo[2] = 1. / (orig[2] * orig[2]); break;
+  }
+}
+
+void orc_vecchia_order(int n, int seed, int random_ordering, int* perm) {
+  std::vector<int> idx(n);
+  std::iota(idx.begin(), idx.end(), 0);
+  if (random_ordering) {
+    std::mt19937 rng(seed);  // re_model_template.h:154, type_defs.h RNG_t
+    std::shuffle(idx.begin(), idx.end(), rng);
+  }
+  std::copy(idx.begin(), idx.end(), perm);
+}
+
+void orc_find_neighbors(const double* x, int n, int d, int m, int* nbr) {
+  std::fill(nbr, nbr + (size_t)n * m, -1);
+  const int end_search_at = n - 2;                 // :751-753
+  if (m > end_search_at + 1) m = end_search_at + 1;  // :754-757 (caller passes stride m)
+  std::vector<double> csum(n);
+  for (int i = 0; i < n; ++i) {
+    double s = 0.;
+    for (int k = 0; k < d; ++k) s += x[(size_t)i * d + k];
+    csum[i] = s;
+  }
+  std::vector<int> sort_sum(n);                    // utils.h:228-236
+  std::iota(sort_sum.begin(), sort_sum.end(), 0);
+  std::sort(sort_sum.begin(), sort_sum.end(), [&](int a, int b) { return csum[a] < csum[b]; });
+  std::vector<int> inv(n);
+  for (int i = 0; i < n; ++i) inv[sort_sum[i]] = i;
+  for (int i = 1; i <= std::min(m, n - 1); ++i)    // :786-807 first rows: all earlier points
+    for (int j = 0; j < i; ++j) nbr[(size_t)i * m + j] = j;
+  std::vector<double> nd(m);
+  std::vector<int> ni(m);
+  for (int i = m + 1; i < n; ++i) {                 // :883-898, :994-1058
+    std::fill(nd.begin(), nd.end(), std::numeric_limits<double>::infinity());
+    std::fill(ni.begin(), ni.end(), 0);
+    bool up = true, down = true;
+    int up_i = inv[i], down_i = inv[i];
+    auto consider = [&](int cand, bool& dir) {
+      if (cand < i && cand <= end_search_at) {
+        double smd = (csum[cand] - csum[i]) * (csum[cand] - csum[i]);
+        if (smd > d * nd[m - 1]) { dir = false; return; }
+        double sed = 0.;
+        for (int k = 0; k < d; ++k) {
+          double t = x[(size_t)cand * d + k] - x[(size_t)i * d + k];
+          sed += t * t;
+        }
+        if (sed < nd[m - 1]) {
+          nd[m - 1] = sed;
+          ni[m - 1] = cand;
+          for (int j = m - 1; j > 0 && nd[j] < nd[j - 1]; --j) {  // utils.h:245-257
+            std::swap(nd[j], nd[j - 1]);
+            std::swap(ni[j], ni[j - 1]);
+          }
+        }
+      }
+    };
+    while (up || down) {
+      if (down_i == 0) down = false;
+      if (up_i == n - 1) up = false;
+      if (down) { --down_i; consider(sort_sum[down_i], down); }
+      if (up) { ++up_i; consider(sort_sum[up_i], up); }
+    }
+    for (int j = 0; j < m; ++j) nbr[(size_t)i * m + j] = ni[j];
+  }
+}
+
+int orc_vecchia_partials(const double* coords, const double* y, const int* nbr,
+                         int n, int d, int m, int t, const double* pars,
+                         int r0, int r1, double* sums) {
+  const double var = pars[1], phi = pars[2];
+  const int P = num_pars_grad();
+  std::fill(sums, sums + 2 + 2 * P, 0.);
+  RowFactor f;
+  for (int i = r0; i < r1; ++i) {
+    const int* nb = nbr + (size_t)i * m;
+    row_factor(coords, nb, i, d, m, t, var, phi, f);
+    if (!(f.D > 0.)) return -1;
+    // By (re_model_template.h:9073-9080): (B y)_i = y_i - A_i . y_nbr
+    double By = y[i];
+    for (int a = 0; a < f.k; ++a) By -= f.A[a] * y[nb[a]];
+    const double Dinv = 1. / f.D;
+    const double u = Dinv * By;                 // u = D^-1 B y (:1779)
+    sums[0] += -std::log(Dinv);                 // logdet = -sum log D^-1 (:2694-2695)
+    sums[1] += By * By * Dinv;                  // q = (By)^T D^-1 (By)
+    for (int p = 0; p < P; ++p) {
+      double uk = 0.;                           // uk = dB_p y ; dB = -dA (:1576)
+      for (int a = 0; a < f.k; ++a) uk -= f.dA[p][a] * y[nb[a]];
+      sums[2 + p] += uk * u - 0.5 * u * f.dD[p] * u;     // :1786
+      sums[2 + P + p] += Dinv * f.dD[p];                  // :1787
+    }
+  }
+  return 0;
+}
+
+int orc_vecchia_nll_grad(const double* coords, const double* y, const int* nbr,
+                         int n, int d, int m, int t, const double* pars, int mode,
+                         double* nll, double* grad, double* sigma2_out,
+                         double* Dinv, double* Bvals) {
+  const int P = num_pars_grad();
+  std::vector<double> s(2 + 2 * P);
+  if (orc_vecchia_partials(coords, y, nbr, n, d, m, t, pars, 0, n, s.data())) return -1;
+  if (Dinv || Bvals) {
+    RowFactor f;
+    for (int i = 0; i < n; ++i) {
+      row_factor(coords, nbr + (size_t)i * m, i, d, m, t, pars[1], pars[2], f);
+      if (Dinv) Dinv[i] = 1. / f.D;
+      if (Bvals) for (int a = 0; a < m; ++a) Bvals[(size_t)i * m + a] = a < f.k ? -f.A[a] : 0.;
+    }
+  }
+  const double logdet = s[0], q = s[1];
+  double sigma2 = pars[0];
+  if (mode == 1) sigma2 = q / n;               // ProfileOutSigma2 (re_model_template.h:2407)
+  *sigma2_out = sigma2;
+  *nll = q / 2. / sigma2 + logdet / 2. + n / 2. * (std::log(sigma2) + std::log(2 * M_PI));  // :2880
+  int off = 0;
+  if (mode == 0) {
+    grad[0] = -q / sigma2 / 2. + n / 2.;        // :1774
+    off = 1;
+  }
+  for (int p = 0; p < P; ++p) grad[off + p] = s[2 + p] / sigma2 + 0.5 * s[2 + P + p];
+  return 0;
+}
+
+int orc_dense_nll_grad(const double* x, const double* y, int n, int d, int t,
+                       const double* pars, int mode, double* nll, double* grad, double* sigma2_out) {
+  const double var = pars[1], phi = pars[2];
+  std::vector<double> S((size_t)n * n), dS((size_t)n * n);
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      if (i == j) { S[(size_t)i * n + j] = var; dS[(size_t)i * n + j] = 0.; continue; }
+      double r = dist(x + (size_t)i * d, x + (size_t)j * d, d);
+      S[(size_t)i * n + j] = cov(t, r, var, phi);           // cov_fcts.h:564-679
+      dS[(size_t)i * n + j] = dcov_dlogphi(t, r, var, phi);  // cov_fcts.h:1000-1102
+    }
+  std::vector<double> L = S;
+  for (int i = 0; i < n; ++i) L[(size_t)i * n + i] += kNugget;  // CalcZSigmaZt + I (:8430-8441)
+  if (!chol(L, n)) return -1;                                   // CalcChol (:5902)
+  std::vector<double> yaux(y, y + n);
+  chol_solve(L, n, yaux.data());                                 // CalcYAux (:9007)
+  double q = 0., logdet = 0.;
+  for (int i = 0; i < n; ++i) { q += y[i] * yaux[i]; logdet += 2. * std::log(L[(size_t)i * n + i]); }
+  double sigma2 = pars[0];
+  if (mode == 1) sigma2 = q / n;
+  *sigma2_out = sigma2;
+  *nll = q / 2. / sigma2 + logdet / 2. + n / 2. * (std::log(sigma2) + std::log(2 * M_PI));
+  // Psi^-1 explicitly, column by column (CalcPsiInv :5987-6007)
+  std::vector<double> Pinv((size_t)n * n);
+  std::vector<double> e(n);
+  for (int j = 0; j < n; ++j) {
+    std::fill(e.begin(), e.end(), 0.);
+    e[j] = 1.;
+    chol_solve(L, n, e.data());
+    for (int i = 0; i < n; ++i) Pinv[(size_t)i * n + j] = e[i];
+  }
+  int off = 0;
+  if (mode == 0) { grad[0] = -q / sigma2 / 2. + n / 2.; off = 1; }   // :1806
+  for (int p = 0; p < 2; ++p) {
+    const std::vector<double>& G = (p == 0) ? S : dS;               // GetZSigmaZtGrad (re_comp.h:1389)
+    double quad = 0., tr = 0.;
+    for (int i = 0; i < n; ++i) {
+      double gi = 0.;
+      for (int j = 0; j < n; ++j) {
+        gi += G[(size_t)i * n + j] * yaux[j];
+        tr += G[(size_t)i * n + j] * Pinv[(size_t)j * n + i];
+      }
+      quad += yaux[i] * gi;
+    }
+    grad[off + p] = -0.5 * quad / sigma2 + 0.5 * tr;              // :1813-1814
+  }
+  return 0;
+}
+
+}  // extern "C"

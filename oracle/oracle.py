@@ -1,0 +1,136 @@
+"""ORACLE TEST INFRASTRUCTURE — NOT PART OF THE PRODUCT.
+
+ctypes wrapper for oracle/build/libgp_oracle.so (the CPU restatement, gp_oracle.cpp).
+Importable only from tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libgp_oracle.so")
+REF_HARNESS = os.path.join(HERE, "_ref", "ref_harness")
+
+COV_CODES = {("exponential", 0.5): 0, ("matern", 0.5): 0, ("matern", 1.5): 1, ("matern", 2.5): 2,
+             ("gaussian", 0.0): 3, ("gaussian", 0.5): 3}
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE, "oracle"], check=True)
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        D = ctypes.POINTER(ctypes.c_double)
+        I = ctypes.POINTER(ctypes.c_int)
+        L.orc_transform_cov_pars.argtypes = [ctypes.c_int, D, D]
+        L.orc_vecchia_order.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, I]
+        L.orc_find_neighbors.argtypes = [D, ctypes.c_int, ctypes.c_int, ctypes.c_int, I]
+        L.orc_vecchia_nll_grad.argtypes = [D, D, I, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, D,
+                                           ctypes.c_int, D, D, D, D, D]
+        L.orc_vecchia_partials.argtypes = [D, D, I, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, D,
+                                           ctypes.c_int, ctypes.c_int, D]
+        L.orc_dense_nll_grad.argtypes = [D, D, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, ctypes.c_int, D, D, D]
+        _lib = L
+    return _lib
+
+
+def _d(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_double))
+
+
+def _i(a):
+    return a.ctypes.data_as(ctypes.POINTER(ctypes.c_int))
+
+
+def cov_code(cov_fct: str, shape: float = 0.5) -> int:
+    if cov_fct == "gaussian":
+        return 3
+    if cov_fct == "exponential":
+        return 0
+    return COV_CODES[(cov_fct, float(shape))]
+
+
+def transform(cov_type: int, orig) -> np.ndarray:
+    o = np.ascontiguousarray(orig, dtype=np.float64)
+    t = np.zeros(3)
+    lib().orc_transform_cov_pars(cov_type, _d(o), _d(t))
+    return t
+
+
+def vecchia_order(n: int, seed: int = 0, random: bool = True) -> np.ndarray:
+    p = np.zeros(n, dtype=np.int32)
+    lib().orc_vecchia_order(n, seed, int(random), _i(p))
+    return p
+
+
+def find_neighbors(coords_vo: np.ndarray, m: int) -> np.ndarray:
+    x = np.ascontiguousarray(coords_vo, dtype=np.float64)
+    n, d = x.shape
+    nb = np.zeros((n, m), dtype=np.int32)
+    lib().orc_find_neighbors(_d(x), n, d, m, _i(nb))
+    return nb
+
+
+def vecchia_setup(coords: np.ndarray, m: int, seed: int = 0, random: bool = True):
+    perm = vecchia_order(coords.shape[0], seed, random)
+    xv = np.ascontiguousarray(coords[perm])
+    return perm, xv, find_neighbors(xv, m)
+
+
+def vecchia_nll_grad(coords_vo, y_vo, nbr, cov_type, pars_trafo, mode, want_factor=False):
+    x = np.ascontiguousarray(coords_vo, dtype=np.float64)
+    yv = np.ascontiguousarray(y_vo, dtype=np.float64)
+    nb = np.ascontiguousarray(nbr, dtype=np.int32)
+    n, d = x.shape
+    m = nb.shape[1]
+    p = np.ascontiguousarray(pars_trafo, dtype=np.float64)
+    nll = np.zeros(1)
+    grad = np.zeros(3)
+    s2 = np.zeros(1)
+    Dinv = np.zeros(n) if want_factor else None
+    B = np.zeros((n, m)) if want_factor else None
+    rc = lib().orc_vecchia_nll_grad(_d(x), _d(yv), _i(nb), n, d, m, cov_type, _d(p), mode, _d(nll), _d(grad), _d(s2),
+                                    _d(Dinv) if want_factor else None, _d(B) if want_factor else None)
+    if rc != 0:
+        raise RuntimeError("oracle vecchia failed")
+    g = grad[:3] if mode == 0 else grad[:2]
+    out = dict(nll=float(nll[0]), grad=g.copy(), sigma2=float(s2[0]))
+    if want_factor:
+        out.update(Dinv=Dinv, B=B)
+    return out
+
+
+def vecchia_partials(coords_vo, y_vo, nbr, cov_type, pars_trafo, r0, r1):
+    x = np.ascontiguousarray(coords_vo, dtype=np.float64)
+    yv = np.ascontiguousarray(y_vo, dtype=np.float64)
+    nb = np.ascontiguousarray(nbr, dtype=np.int32)
+    n, d = x.shape
+    p = np.ascontiguousarray(pars_trafo, dtype=np.float64)
+    s = np.zeros(6)
+    if lib().orc_vecchia_partials(_d(x), _d(yv), _i(nb), n, d, nb.shape[1], cov_type, _d(p), r0, r1, _d(s)):
+        raise RuntimeError("oracle partials failed")
+    return s
+
+
+def dense_nll_grad(coords, y, cov_type, pars_trafo, mode):
+    x = np.ascontiguousarray(coords, dtype=np.float64)
+    yv = np.ascontiguousarray(y, dtype=np.float64)
+    n, d = x.shape
+    p = np.ascontiguousarray(pars_trafo, dtype=np.float64)
+    nll = np.zeros(1)
+    grad = np.zeros(3)
+    s2 = np.zeros(1)
+    if lib().orc_dense_nll_grad(_d(x), _d(yv), n, d, cov_type, _d(p), mode, _d(nll), _d(grad), _d(s2)):
+        raise RuntimeError("oracle dense failed")
+    return dict(nll=float(nll[0]), grad=(grad[:3] if mode == 0 else grad[:2]).copy(), sigma2=float(s2[0]))

@@ -1,0 +1,230 @@
+// ORACLE TEST INFRASTRUCTURE — NOT PART OF THE PRODUCT.
+//
+// Probe harness for the *reference* GPBoost implementation. It is compiled
+// (by oracle/Makefile) directly against the reference sources where they lie
+// under /root/reference — nothing is copied into this repository — and its
+// binary goes to oracle/_ref/ (git-ignored). It is used only by
+// tests/golden/make_golden.py (to produce the committed golden fixtures) and by
+// bench.py's cpu_baseline leg (kind "reference").
+//
+// The public C API of the reference has no gradient entry point
+// (include/LightGBM/c_api.h:1500 returns only the nll), so this harness calls
+// REModelTemplate exactly as the L-BFGS objective does
+// (include/GPBoost/optim_utils.h:243-364):
+//   TransformCovPars (re_model_template.h:7189)
+//   CalcCovFactorOrModeAndNegLL (re_model_template.h:2582)
+//   ProfileOutSigma2 (:2407) + EvalNegLogLikelihoodOnlyUpdateNuggetVariance (:2888)
+//   CalcGradPars (:1748)
+//
+// Input file (little-endian): int32 n, int32 d, double coords[n*d] (column-major),
+// double y[n]. Options on argv (key=value). Output: one JSON object on stdout.
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <string>
+#include <vector>
+#include <map>
+#include <chrono>
+#include <algorithm>
+#include <memory>
+#include <mutex>
+#include <thread>
+#include <fstream>
+
+// Pull in every system / third-party header first with normal access control,
+// then open up only the GPBoost class internals (members such as
+// nearest_neighbors_ are needed for the golden index fixtures).
+#include <sstream>
+#include <iostream>
+#include <iomanip>
+#include <complex>
+#include <random>
+#include <set>
+#include <unordered_map>
+#include <unordered_set>
+#include <functional>
+#include <numeric>
+#include <limits>
+#include <cmath>
+#include <Eigen/Dense>
+#include <Eigen/Sparse>
+#include <Eigen/IterativeLinearSolvers>
+#include <LightGBM/utils/log.h>
+#include <LightGBM/utils/common.h>
+#include <LightGBM/meta.h>
+#include <LBFGSpp/BFGSMat.h>
+#define private public
+#define protected public
+#include <GPBoost/re_model_template.h>
+#undef private
+#undef protected
+
+using namespace GPBoost;
+
+static std::map<std::string, std::string> parse_args(int argc, char** argv) {
+  std::map<std::string, std::string> a;
+  for (int i = 2; i < argc; ++i) {
+    std::string s(argv[i]);
+    auto p = s.find('=');
+    if (p == std::string::npos) continue;
+    a[s.substr(0, p)] = s.substr(p + 1);
+  }
+  return a;
+}
+
+static std::string get(const std::map<std::string, std::string>& a, const char* k, const char* def) {
+  auto it = a.find(k);
+  return it == a.end() ? std::string(def) : it->second;
+}
+
+static std::vector<double> parse_list(const std::string& s) {
+  std::vector<double> v;
+  size_t st = 0;
+  while (st < s.size()) {
+    size_t e = s.find(',', st);
+    if (e == std::string::npos) e = s.size();
+    v.push_back(std::atof(s.substr(st, e - st).c_str()));
+    st = e + 1;
+  }
+  return v;
+}
+
+static void print_vec(const char* name, const double* v, int n, bool comma = true) {
+  std::printf("\"%s\": [", name);
+  for (int i = 0; i < n; ++i) std::printf("%s%.17g", i ? ", " : "", v[i]);
+  std::printf("]%s\n", comma ? "," : "");
+}
+
+int main(int argc, char** argv) {
+  if (argc < 2) {
+    std::fprintf(stderr, "usage: ref_harness input.bin key=value ...\n");
+    return 2;
+  }
+  auto args = parse_args(argc, argv);
+  FILE* f = std::fopen(argv[1], "rb");
+  if (!f) { std::perror("open"); return 2; }
+  int32_t n = 0, d = 0;
+  if (std::fread(&n, 4, 1, f) != 1 || std::fread(&d, 4, 1, f) != 1) return 2;
+  std::vector<double> coords((size_t)n * d), y(n);
+  if (std::fread(coords.data(), 8, coords.size(), f) != coords.size()) return 2;
+  if (std::fread(y.data(), 8, y.size(), f) != y.size()) return 2;
+  std::fclose(f);
+
+  const std::string cov_fct = get(args, "cov_fct", "exponential");
+  const double shape = std::atof(get(args, "shape", "0.5").c_str());
+  const std::string gp_approx = get(args, "gp_approx", "none");
+  const int num_neighbors = std::atoi(get(args, "num_neighbors", "30").c_str());
+  const std::string ordering = get(args, "ordering", "random");
+  const std::string likelihood = get(args, "likelihood", "gaussian");
+  const std::string mim = get(args, "matrix_inversion_method", "cholesky");
+  const int seed = std::atoi(get(args, "seed", "0").c_str());
+  const int threads = std::atoi(get(args, "threads", "-1").c_str());
+  const std::vector<double> cov_pars_orig = parse_list(get(args, "cov_pars", "0.1,1.6,0.2"));
+  const std::string mode = get(args, "mode", "eval");   // eval | lbfgs
+  const int reps = std::atoi(get(args, "reps", "1").c_str());
+  const int dump_nn = std::atoi(get(args, "dump_nn", "0").c_str());
+  const std::string aux = get(args, "aux_pars", "");
+
+  Log::ResetLogLevelRE(LogLevelRE::Warning);
+  auto t0 = std::chrono::steady_clock::now();
+  std::unique_ptr<REModelTemplate<den_mat_t, chol_den_mat_t>> m(new REModelTemplate<den_mat_t, chol_den_mat_t>(
+      n, nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr,
+      1, coords.data(), d, nullptr, 0, cov_fct.c_str(), shape, gp_approx.c_str(),
+      -1., 0., num_neighbors, ordering.c_str(), 0, 1., "kmeans++",
+      likelihood.c_str(), 0., mim.c_str(), seed, threads, false, false, nullptr, 1.));
+  auto t1 = std::chrono::steady_clock::now();
+  double t_construct = std::chrono::duration<double>(t1 - t0).count();
+
+  if (args.count("cg_delta_conv") || args.count("num_rand_vec_trace")) {
+    // same defaults as re_model_template.h:5364-5380 unless overridden
+    const double cg_delta_conv = std::atof(get(args, "cg_delta_conv", "1e-2").c_str());
+    const int t = std::atoi(get(args, "num_rand_vec_trace", "50").c_str());
+    const int cg_max = std::atoi(get(args, "cg_max_num_it", "1000").c_str());
+    const std::string prec = get(args, "cg_preconditioner_type", "vadu");
+    m->SetOptimConfig(0.1, 0.5, 1000, 1e-6, true, 0, "lbfgs", 2, "relative_change_in_log_likelihood",
+                      0.1, 0.5, "lbfgs", cg_max, cg_max, cg_delta_conv, t, true, prec.c_str(),
+                      std::atoi(get(args, "seed_rand_vec_trace", "1").c_str()), -1, false, nullptr, 6, 1e-8);
+  }
+  const bool gauss = m->gauss_likelihood_;
+  if (!aux.empty()) {
+    std::vector<double> av = parse_list(aux);
+    m->SetAuxPars(av.data());
+  }
+  m->SetY(y.data());
+
+  vec_t orig = Eigen::Map<const vec_t>(cov_pars_orig.data(), (int)cov_pars_orig.size());
+  vec_t trafo;
+  m->TransformCovPars(orig, trafo);
+
+  double nll = 0., sigma2 = gauss ? trafo[0] : 1.;
+  vec_t grad, gb;
+  std::vector<double> times;
+  for (int r = 0; r < reps; ++r) {
+    vec_t cp = trafo;
+    if (!gauss) {
+      for (const auto& c : m->unique_clusters_) m->likelihood_[c]->InitializeModeAvec();
+    }
+    auto a = std::chrono::steady_clock::now();
+    m->CalcCovFactorOrModeAndNegLL(cp, nullptr);
+    nll = m->neg_log_likelihood_;
+    if (gauss && mode == "lbfgs") {
+      sigma2 = m->ProfileOutSigma2();
+      cp[0] = sigma2;
+      m->EvalNegLogLikelihoodOnlyUpdateNuggetVariance(sigma2, nll);
+      m->CalcGradPars(cp, sigma2, true, false, grad, gb, false, false, nullptr, false);
+    }
+    else if (gauss) {
+      m->CalcGradPars(cp, cp[0], true, false, grad, gb, true, false, nullptr, false);
+    }
+    else {
+      m->CalcGradPars(cp, 1., true, false, grad, gb, false, false, nullptr, false);
+    }
+    auto b = std::chrono::steady_clock::now();
+    times.push_back(std::chrono::duration<double>(b - a).count());
+  }
+  std::vector<double> ts = times;
+  std::sort(ts.begin(), ts.end());
+
+  std::printf("{\n");
+  std::printf("\"n\": %d, \"d\": %d,\n", n, d);
+  std::printf("\"gauss\": %s,\n", gauss ? "true" : "false");
+  std::printf("\"nll\": %.17g,\n", nll);
+  std::printf("\"sigma2\": %.17g,\n", sigma2);
+  print_vec("cov_pars_trafo", trafo.data(), (int)trafo.size());
+  print_vec("grad", grad.data(), (int)grad.size());
+  print_vec("times", times.data(), (int)times.size());
+  std::printf("\"median_time\": %.9g,\n", ts[ts.size() / 2]);
+  std::printf("\"t_construct\": %.9g,\n", t_construct);
+  if (gauss && gp_approx == "vecchia") {
+    std::printf("\"yTPsiInvy\": %.17g, \"log_det_Psi\": %.17g,\n", m->yTPsiInvy_, m->log_det_Psi_);
+  }
+  if (gp_approx == "vecchia" && dump_nn) {
+    const auto& perm = m->data_indices_per_cluster_[m->unique_clusters_[0]];
+    std::printf("\"perm\": [");
+    for (size_t i = 0; i < perm.size(); ++i) std::printf("%s%d", i ? "," : "", perm[i]);
+    std::printf("],\n");
+    const auto& nn = m->nearest_neighbors_[m->unique_clusters_[0]][0];
+    std::printf("\"neighbors\": [");
+    for (size_t i = 0; i < nn.size(); ++i) {
+      std::printf("%s[", i ? "," : "");
+      for (size_t j = 0; j < nn[i].size(); ++j) std::printf("%s%d", j ? "," : "", nn[i][j]);
+      std::printf("]");
+    }
+    std::printf("],\n");
+    // D^-1 diagonal (Vecchia order)
+    const sp_mat_t& Dinv = m->D_inv_[m->unique_clusters_[0]][0];
+    vec_t dd = Dinv.diagonal();
+    print_vec("D_inv", dd.data(), (int)dd.size());
+    // B rows: dense values per row in neighbor order
+    const sp_mat_t& B = m->B_[m->unique_clusters_[0]][0];
+    std::printf("\"B_rows\": [");
+    for (size_t i = 0; i < nn.size(); ++i) {
+      std::printf("%s[", i ? "," : "");
+      for (size_t j = 0; j < nn[i].size(); ++j) std::printf("%s%.17g", j ? "," : "", B.coeff((int)i, nn[i][j]));
+      std::printf("]");
+    }
+    std::printf("],\n");
+  }
+  std::printf("\"ok\": true\n}\n");
+  return 0;
+}

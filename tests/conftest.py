@@ -1,0 +1,38 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: test needs an MI355X (runs on the GPU box)")
+    config.addinivalue_line("markers", "slow: long-running test")
+
+
+@pytest.fixture(scope="session")
+def golden():
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "golden_gaussian.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def golden_arrays():
+    import numpy as np
+    return dict(np.load(os.path.join(ROOT, "tests", "golden", "golden_vecchia_arrays.npz")))
+
+
+@pytest.fixture(scope="session")
+def rtest_data():
+    from gpboost_amd import synthetic
+    return synthetic.rtest_gaussian_y(100)
+
+
+@pytest.fixture(scope="session")
+def synth2000():
+    from gpboost_amd import synthetic
+    return synthetic.bench_coords(2000), synthetic.bench_gaussian_y(2000)

@@ -1,0 +1,137 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures from the REFERENCE implementation.
+
+Runs oracle/_ref/ref_harness (the reference GPBoost REModelTemplate compiled from
+/root/reference by oracle/Makefile) on portable synthetic inputs and writes small
+fixtures next to this script. Run in the build container only:
+
+    make -C oracle ref && python3 tests/golden/make_golden.py
+
+Fixtures are data (inputs are regenerated from the LCG; outputs are reference
+results), never reference source.
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, ROOT)
+from gpboost_amd import synthetic  # noqa: E402
+
+HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+
+
+def run_ref(coords: np.ndarray, y: np.ndarray, **opts) -> dict:
+    n, d = coords.shape
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(np.array([n, d], dtype=np.int32).tobytes())
+        f.write(np.asfortranarray(coords).T.astype(np.float64).tobytes())  # column-major
+        f.write(y.astype(np.float64).tobytes())
+        path = f.name
+    try:
+        args = [HARNESS, path] + [f"{k}={v}" for k, v in opts.items()]
+        out = subprocess.run(args, check=True, capture_output=True, text=True,
+                             env=dict(os.environ, OMP_NUM_THREADS="8"))
+        return json.loads(out.stdout)
+    finally:
+        os.unlink(path)
+
+
+def fmt_pars(p):
+    return ",".join(repr(float(x)) for x in p)
+
+
+def main():
+    cases = {}
+    # ---- R-test data (n=100): goldens also hard-coded in the reference R tests ----
+    coords, y = synthetic.rtest_gaussian_y(100)
+    rpars = [0.1, 1.6, 0.2]
+    r_expect = {  # R-package/tests/testthat/test_GPModel_gaussian_process.R
+        "rtest_dense_exponential": 124.2549533,   # :81
+        "rtest_dense_matern15": 141.3502172,      # :97
+        "rtest_dense_matern25": 158.1111626,      # :108
+        "rtest_vecchia_nm1_none": 124.2549533,    # :711-716
+        "rtest_vecchia_m30_none": 124.2252524,    # :744-749
+    }
+    specs = {
+        "rtest_dense_exponential": dict(cov_fct="exponential", gp_approx="none"),
+        "rtest_dense_matern15": dict(cov_fct="matern", shape=1.5, gp_approx="none"),
+        "rtest_dense_matern25": dict(cov_fct="matern", shape=2.5, gp_approx="none"),
+        "rtest_dense_gaussian": dict(cov_fct="gaussian", gp_approx="none"),
+        "rtest_vecchia_nm1_none": dict(cov_fct="exponential", gp_approx="vecchia", num_neighbors=99, ordering="none"),
+        "rtest_vecchia_m30_none": dict(cov_fct="exponential", gp_approx="vecchia", num_neighbors=30, ordering="none"),
+        "rtest_vecchia_m10_random": dict(cov_fct="exponential", gp_approx="vecchia", num_neighbors=10, ordering="random"),
+        "rtest_vecchia_m30_matern15": dict(cov_fct="matern", shape=1.5, gp_approx="vecchia", num_neighbors=30, ordering="random"),
+        "rtest_vecchia_m30_gaussian": dict(cov_fct="gaussian", gp_approx="vecchia", num_neighbors=30, ordering="random"),
+    }
+    for name, sp in specs.items():
+        ev = run_ref(coords, y, cov_pars=fmt_pars(rpars), mode="eval", **sp)
+        lb = run_ref(coords, y, cov_pars=fmt_pars(rpars), mode="lbfgs", **sp)
+        cases[name] = dict(data="rtest_gaussian", n=100, spec=sp, cov_pars=rpars,
+                           nll=ev["nll"], grad=ev["grad"],
+                           lbfgs_nll=lb["nll"], lbfgs_grad=lb["grad"], lbfgs_sigma2=lb["sigma2"],
+                           r_golden=r_expect.get(name))
+        print(name, ev["nll"], r_expect.get(name), file=sys.stderr)
+
+    # ---- synthetic bench-generator data, n=2000 (BASELINE config 1 family) ----
+    n = 2000
+    sc = synthetic.bench_coords(n)
+    sy = synthetic.bench_gaussian_y(n)
+    bpars = [0.1, 1.0, 0.1]
+    sspecs = {
+        "synth2000_vecchia_m30_exp": dict(cov_fct="exponential", gp_approx="vecchia", num_neighbors=30, ordering="random"),
+        "synth2000_vecchia_m30_matern25": dict(cov_fct="matern", shape=2.5, gp_approx="vecchia", num_neighbors=30, ordering="random"),
+        "synth2000_vecchia_m20_gaussian": dict(cov_fct="gaussian", gp_approx="vecchia", num_neighbors=20, ordering="random"),
+        "synth2000_dense_exp": dict(cov_fct="exponential", gp_approx="none"),
+    }
+    arrays = {}
+    for name, sp in sspecs.items():
+        ev = run_ref(sc, sy, cov_pars=fmt_pars(bpars), mode="eval", dump_nn=1, **sp)
+        lb = run_ref(sc, sy, cov_pars=fmt_pars(bpars), mode="lbfgs", **sp)
+        cases[name] = dict(data="bench", n=n, spec=sp, cov_pars=bpars,
+                           nll=ev["nll"], grad=ev["grad"],
+                           lbfgs_nll=lb["nll"], lbfgs_grad=lb["grad"], lbfgs_sigma2=lb["sigma2"])
+        if "perm" in ev and name == "synth2000_vecchia_m30_exp":
+            arrays["synth2000_perm"] = np.array(ev["perm"], dtype=np.int32)
+            nb = ev["neighbors"]
+            m = 30
+            nbm = np.full((n, m), -1, dtype=np.int32)
+            bm = np.zeros((n, m), dtype=np.float64)
+            for i, row in enumerate(nb):
+                nbm[i, :len(row)] = row
+                bm[i, :len(row)] = ev["B_rows"][i]
+            arrays["synth2000_neighbors"] = nbm
+            arrays["synth2000_B"] = bm
+            arrays["synth2000_Dinv"] = np.array(ev["D_inv"])
+        print(name, ev["nll"], file=sys.stderr)
+
+    # ---- neighbour-index parity at a larger n (bit-exact indices) ----
+    n2 = 20000
+    sc2 = synthetic.bench_coords(n2)
+    sy2 = synthetic.bench_gaussian_y(n2)
+    ev = run_ref(sc2, sy2, cov_pars=fmt_pars(bpars), mode="eval", dump_nn=1, cov_fct="exponential",
+                 gp_approx="vecchia", num_neighbors=30, ordering="random")
+    nbm = np.full((n2, 30), -1, dtype=np.int32)
+    for i, row in enumerate(ev["neighbors"]):
+        nbm[i, :len(row)] = row
+    arrays["synth20000_perm"] = np.array(ev["perm"], dtype=np.int32)
+    arrays["synth20000_neighbors"] = nbm
+    cases["synth20000_vecchia_m30_exp"] = dict(data="bench", n=n2, spec=dict(cov_fct="exponential", gp_approx="vecchia",
+                                               num_neighbors=30, ordering="random"), cov_pars=bpars,
+                                               nll=ev["nll"], grad=ev["grad"])
+    print("synth20000", ev["nll"], file=sys.stderr)
+
+    with open(os.path.join(HERE, "golden_gaussian.json"), "w") as f:
+        json.dump(cases, f, indent=1)
+    np.savez_compressed(os.path.join(HERE, "golden_vecchia_arrays.npz"), **arrays)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,80 @@
+"""CPU: the C-ABI library loads, exports every symbol include/gpboost_amd.h declares,
+host-side logic (row partition, partial-sum assembly) matches the oracle, and the
+product fails loudly (no CPU fallback) when no GPU is visible."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "gpboost_amd.h")
+
+
+def _declared_symbols():
+    txt = open(HEADER).read()
+    return sorted(set(re.findall(r"GPBOOST_AMD_EXPORT\s+[\w\s\*]+?\b((?:GPB|LGBM)_\w+)\s*\(", txt)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    from gpboost_amd import basic
+    if not os.path.exists(basic.LIB_PATH):
+        from gpboost_amd import build
+        build.build(verbose=False)
+    return basic.lib()
+
+
+def test_header_declares_reference_entry_points():
+    syms = _declared_symbols()
+    for s in ["GPB_CreateREModel", "GPB_REModelFree", "GPB_SetOptimConfig", "GPB_EvalNegLogLikelihood",
+              "LGBM_GetLastError", "LGBM_RegisterLogCallback", "GPB_EvalNegLogLikelihoodGrad"]:
+        assert s in syms
+
+
+def test_library_exports_every_declared_symbol(lib):
+    missing = [s for s in _declared_symbols() if not hasattr(lib, s)]
+    assert not missing, missing
+
+
+def test_partition_rows(lib):
+    from gpboost_amd import partition_rows
+    for n in [1, 7, 100, 100_003]:
+        for w in [1, 2, 3, 8]:
+            blocks = [partition_rows(n, w, r) for r in range(w)]
+            assert blocks[0][0] == 0 and blocks[-1][1] == n
+            for (a, b), (c, _) in zip(blocks, blocks[1:]):
+                assert b == c and b >= a
+            sizes = [b - a for a, b in blocks]
+            assert max(sizes) - min(sizes) <= 1
+
+
+@pytest.mark.parametrize("profile", [False, True])
+def test_combine_partials_matches_oracle(lib, synth2000, profile):
+    from gpboost_amd import combine_partials
+    from oracle import oracle as O
+    X, Y = synth2000
+    perm, xv, nb = O.vecchia_setup(X, 30, 0, True)
+    tp = O.transform(0, [0.1, 1.0, 0.1])
+    sums = O.vecchia_partials(xv, Y[perm], nb, 0, tp, 0, 2000)
+    nll, g, s2 = combine_partials(sums, 2000, tp[0], profile)
+    ref = O.vecchia_nll_grad(xv, Y[perm], nb, 0, tp, int(profile))
+    assert abs(nll - ref["nll"]) <= 1e-12 * abs(ref["nll"])
+    np.testing.assert_allclose(g, ref["grad"], rtol=1e-12)
+
+
+def test_error_convention(lib):
+    """-1 + LGBM_GetLastError message, never a crash (reference c_api.cpp:54-58)."""
+    from gpboost_amd import GPBoostError, GPModel
+    with pytest.raises((GPBoostError, ValueError)):
+        GPModel(gp_coords=np.zeros((10, 2)), cov_function="wendland", gp_approx="vecchia")
+
+
+def test_no_cpu_fallback_without_gpu(lib):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU visible")
+    from gpboost_amd import GPBoostError, GPModel
+    with pytest.raises(GPBoostError, match="no HIP device"):
+        GPModel(gp_coords=np.random.rand(50, 2), cov_function="exponential", gp_approx="vecchia", num_neighbors=5)

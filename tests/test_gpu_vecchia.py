@@ -1,0 +1,176 @@
+"""GPU parity: the HIP Vecchia path (through the C ABI) against the oracle and the
+reference fixtures. Tolerance (BASELINE.json north_star): nll and gradient within
+1e-6 relative in fp64 — the kernel computes the same quantities in a different
+(O(k^2)-per-parameter) arithmetic order, so observed differences are ~1e-12.
+Neighbour indices and the ordering must be bit-exact."""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+RTOL = 1e-6
+
+
+def _model(X, m, cov="exponential", shape=0.5, ordering="random", seed=0):
+    from gpboost_amd import GPModel
+    return GPModel(gp_coords=X, cov_function=cov, cov_fct_shape=shape, gp_approx="vecchia",
+                   num_neighbors=m, vecchia_ordering=ordering, seed=seed)
+
+
+def _close(a, b, rtol=RTOL, scale=None):
+    a, b = np.asarray(a, float), np.asarray(b, float)
+    s = np.maximum(np.abs(b), 1.0) if scale is None else scale
+    return np.all(np.abs(a - b) <= rtol * s)
+
+
+@pytest.mark.parametrize("name", ["rtest_vecchia_m30_none", "rtest_vecchia_m10_random",
+                                  "rtest_vecchia_m30_matern15", "rtest_vecchia_m30_gaussian",
+                                  "synth2000_vecchia_m30_exp", "synth2000_vecchia_m30_matern25",
+                                  "synth2000_vecchia_m20_gaussian"])
+def test_vecchia_matches_reference(golden, rtest_data, synth2000, name):
+    case = golden[name]
+    X, Y = rtest_data if case["data"] == "rtest_gaussian" else synth2000
+    sp = case["spec"]
+    gm = _model(X, sp["num_neighbors"], sp["cov_fct"], sp.get("shape", 0.5), sp["ordering"])
+    nll = gm.neg_log_likelihood(case["cov_pars"], Y)
+    assert abs(nll - case["nll"]) <= RTOL * abs(case["nll"])
+    if case.get("r_golden") is not None:
+        assert abs(nll - case["r_golden"]) < 1e-5
+    nll0, g0, _ = gm.neg_log_likelihood_and_grad(case["cov_pars"], Y, profile_sigma2=False)
+    assert abs(nll0 - case["nll"]) <= RTOL * abs(case["nll"])
+    assert _close(g0, case["grad"]), (g0, case["grad"])
+    nll1, g1, s2 = gm.neg_log_likelihood_and_grad(case["cov_pars"], None, profile_sigma2=True)
+    assert abs(nll1 - case["lbfgs_nll"]) <= RTOL * abs(case["lbfgs_nll"])
+    assert _close(g1, case["lbfgs_grad"]), (g1, case["lbfgs_grad"])
+    assert abs(s2 - case["lbfgs_sigma2"]) <= RTOL * case["lbfgs_sigma2"]
+
+
+def test_vecchia_structure_bit_exact(golden_arrays, synth2000):
+    X, _ = synth2000
+    gm = _model(X, 30)
+    perm, nbr = gm.vecchia_structure()
+    assert np.array_equal(perm, golden_arrays["synth2000_perm"])
+    assert np.array_equal(nbr, golden_arrays["synth2000_neighbors"])
+
+
+def test_vecchia_structure_bit_exact_20000(golden_arrays):
+    from gpboost_amd import synthetic
+    gm = _model(synthetic.bench_coords(20000), 30)
+    perm, nbr = gm.vecchia_structure()
+    assert np.array_equal(perm, golden_arrays["synth20000_perm"])
+    assert np.array_equal(nbr, golden_arrays["synth20000_neighbors"])
+
+
+def test_vecchia_factor_matches_reference(golden_arrays, synth2000):
+    X, _ = synth2000
+    gm = _model(X, 30)
+    dinv, b = gm.vecchia_factor([0.1, 1.0, 0.1])
+    np.testing.assert_allclose(dinv, golden_arrays["synth2000_Dinv"], rtol=1e-10)
+    np.testing.assert_allclose(b, golden_arrays["synth2000_B"], rtol=1e-8, atol=1e-11)
+
+
+@pytest.mark.parametrize("cov,shape,ct", [("exponential", 0.5, 0), ("matern", 1.5, 1), ("matern", 2.5, 2),
+                                          ("gaussian", 0.5, 3)])
+@pytest.mark.parametrize("m", [1, 5, 16, 31, 48, 64])
+def test_vecchia_vs_oracle_grid(cov, shape, ct, m):
+    """Neighbour counts across all three lane-group widths (16/32/64) and padding edges."""
+    from gpboost_amd import synthetic
+    n = 700
+    X = synthetic.bench_coords(n)
+    Y = synthetic.bench_gaussian_y(n)
+    pars = [0.3, 1.2, 0.15]
+    gm = _model(X, m, cov, shape)
+    perm, xv, nb = O.vecchia_setup(X, m, 0, True)
+    tp = O.transform(ct, pars)
+    for mode in (0, 1):
+        ref = O.vecchia_nll_grad(xv, Y[perm], nb, ct, tp, mode)
+        nll, g, s2 = gm.neg_log_likelihood_and_grad(pars, Y, profile_sigma2=bool(mode))
+        assert abs(nll - ref["nll"]) <= RTOL * abs(ref["nll"])
+        assert _close(g, ref["grad"]), (m, cov, mode, g, ref["grad"])
+
+
+@pytest.mark.parametrize("d", [1, 3])
+def test_vecchia_other_dims(d):
+    from gpboost_amd import synthetic
+    n = 500
+    X = synthetic.sim_rand_unif(n * d, 0.3).reshape(d, n).T.copy()
+    Y = synthetic.bench_gaussian_y(n)
+    pars = [0.2, 1.0, 0.2]
+    gm = _model(X, 12)
+    perm, xv, nb = O.vecchia_setup(X, 12, 0, True)
+    tp = O.transform(0, pars)
+    ref = O.vecchia_nll_grad(xv, Y[perm], nb, 0, tp, 0)
+    nll, g, _ = gm.neg_log_likelihood_and_grad(pars, Y)
+    assert abs(nll - ref["nll"]) <= RTOL * abs(ref["nll"])
+    assert _close(g, ref["grad"])
+
+
+def test_edge_tiny_n_and_clamped_m():
+    """n = 2 and num_neighbors >= n (clamped to n-1, Vecchia_utils.cpp:754-757); ordering 'none'."""
+    from gpboost_amd import synthetic
+    for n, m in [(2, 1), (3, 5), (33, 40)]:
+        X = synthetic.bench_coords(n)
+        Y = synthetic.bench_gaussian_y(n)
+        gm = _model(X, m, ordering="none")
+        mm = min(m, n - 1)
+        perm, xv, nb = O.vecchia_setup(X, mm, 0, False)
+        tp = O.transform(0, [0.1, 1.0, 0.3])
+        ref = O.vecchia_nll_grad(xv, Y[perm], nb, 0, tp, 0)
+        nll, g, _ = gm.neg_log_likelihood_and_grad([0.1, 1.0, 0.3], Y)
+        assert abs(nll - ref["nll"]) <= RTOL * abs(ref["nll"]), (n, m)
+        assert _close(g, ref["grad"]), (n, m)
+
+
+def test_gradient_matches_finite_differences():
+    """Size-independent property: analytic gradient vs central differences of the GPU nll."""
+    from gpboost_amd import synthetic
+    n = 3000
+    X = synthetic.bench_coords(n)
+    Y = synthetic.bench_gaussian_y(n)
+    gm = _model(X, 20)
+    orig = np.array([0.1, 1.0, 0.1])
+    # transformed-scale log parameters: (log s2, log s1^2/s2, log 1/rho)
+    _, g, _ = gm.neg_log_likelihood_and_grad(orig, Y)
+    h = 1e-5
+    def nll_at(lt):
+        s2 = np.exp(lt[0]); v = np.exp(lt[1]) * s2; rho = 1.0 / np.exp(lt[2])
+        return gm.neg_log_likelihood([s2, v, rho], None)
+    lt0 = np.array([np.log(0.1), np.log(10.0), np.log(10.0)])
+    fd = []
+    for k in range(3):
+        e = np.zeros(3); e[k] = h
+        fd.append((nll_at(lt0 + e) - nll_at(lt0 - e)) / (2 * h))
+    np.testing.assert_allclose(g, fd, rtol=1e-5, atol=1e-4)
+
+
+def test_large_n_determinism_and_finiteness():
+    """n = 100k (BASELINE config 3 size): two evaluations bit-identical (fixed-order reductions)."""
+    from gpboost_amd import synthetic
+    n = 100_000
+    X = synthetic.bench_coords(n)
+    Y = synthetic.bench_gaussian_y(n)
+    gm = _model(X, 30)
+    a = gm.neg_log_likelihood_and_grad([0.1, 1.0, 0.1], Y, profile_sigma2=True)
+    b = gm.neg_log_likelihood_and_grad([0.1, 1.0, 0.1], None, profile_sigma2=True)
+    assert a[0] == b[0] and np.array_equal(a[1], b[1])
+    assert np.isfinite(a[0]) and np.all(np.isfinite(a[1]))
+
+
+def test_large_n_partials_match_oracle_on_row_subset():
+    """n = 100k: oracle on a row window vs the GPU on the same window via a 2-rank-style split
+    would need RCCL; instead compare the full nll against the oracle computed with OpenMP-free
+    C code (takes a few seconds)."""
+    from gpboost_amd import synthetic
+    n = 100_000
+    X = synthetic.bench_coords(n)
+    Y = synthetic.bench_gaussian_y(n)
+    gm = _model(X, 30)
+    perm, nbr = gm.vecchia_structure()
+    xv = np.ascontiguousarray(X[perm])
+    tp = O.transform(0, [0.1, 1.0, 0.1])
+    ref = O.vecchia_nll_grad(xv, Y[perm], nbr, 0, tp, 1)
+    nll, g, _ = gm.neg_log_likelihood_and_grad([0.1, 1.0, 0.1], Y, profile_sigma2=True)
+    assert abs(nll - ref["nll"]) <= RTOL * abs(ref["nll"])
+    assert _close(g, ref["grad"])
