@@ -20,10 +20,14 @@ class DenseSolver {
   void Eval(int cov_type, double var, double phi, const double* d_y, bool want_grad, double* sums, double* kernel_ms);
 
  private:
+  void Potrf();
+  void Trtri(int a, int b);
+
   int n_, d_, ld_;
   const double* d_X_;
   hipStream_t stream_;
-  DevBuf<double> A_, W_, vec_, red_;
+  DevBuf<double> A_, W_, T_, vec_, red_;
+  DevBuf<int> info_;
   double* h_red_ = nullptr;
   hipEvent_t ev_[3] = {nullptr, nullptr, nullptr};
 };

@@ -1,14 +1,457 @@
-// Dense path kernels (placeholder until the blocked MFMA Cholesky lands).
+// Dense Gaussian-process likelihood + gradient on gfx950 (gp_approx = "none").
+//
+// Reference path replaced (re_model_template.h):
+//   CalcChol (:5902-5904, Eigen::LLT)              -> blocked right-looking POTRF, fp64 MFMA updates
+//   CalcYAux (:9007) / logdet (:2875)              -> W = L^-1 (TRTRI), z = W y, q = |z|^2, 2 sum log L_ii
+//   CalcPsiInv (:5987-6007, L^-1 then L^-T L^-1)   -> recursive TRTRI + out-of-place LAUUM (P = W^T W)
+//   dense gradient (:1798-1818)                    -> one fused pass over the lower triangle of P that
+//                                                     recomputes Sigma_ij and dSigma_ij from the coordinates
+// Matrices are column-major with leading dimension ld (a multiple of 64), lower triangles only.
+// Every GEMM-shaped step (TRSM-as-GEMM with the inverted diagonal block, panel and trailing
+// updates, the TRTRI products and LAUUM) goes through one MFMA kernel:
+//   C[M x N] = alpha * op(A) op(B) + beta * C,  64 x 64 output tile per 256-thread workgroup,
+//   4 waves x (32 x 32) = 2 x 2 v_mfma_f64_16x16x4 tiles per wave, K staged through LDS in steps of 16,
+// with per-tile K ranges that skip the structural zeros of triangular operands and optional
+// skipping of output tiles above the diagonal.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
+#include "cov.h"
 #include "dense.h"
 #include "kernels.h"
 
 namespace gpb_amd {
+namespace {
+
+typedef double double4_t __attribute__((ext_vector_type(4)));
+
+constexpr int TM = 64, TN = 64, TK = 16;
+
+struct GemmArgs {
+  int M, N, K;
+  double alpha, beta;
+  const double* A; int lda; int transA;
+  const double* B; int ldb; int transB;
+  double* C; int ldc;
+  int lower_out;     // skip output tiles entirely above the diagonal (local indices)
+  int a_lower;       // op(A)[i][k] == 0 for k > i   -> k_end = min(K, m0 + TM); mask
+  int a_upper;       // op(A)[i][k] == 0 for k < i   -> k_begin >= m0; mask
+  int b_lower;       // op(B)[k][j] == 0 for k < j   -> k_begin >= n0; mask
+};
+
+__global__ void __launch_bounds__(256) gemm_f64_kernel(GemmArgs g) {
+  __shared__ double As[TK][TM + 1];
+  __shared__ double Bs[TK][TN + 1];
+  const int m0 = blockIdx.y * TM, n0 = blockIdx.x * TN;
+  if (g.lower_out && n0 > m0 + TM - 1) return;
+  int k_begin = 0, k_end = g.K;
+  if (g.a_lower) k_end = min(k_end, m0 + TM);
+  if (g.a_upper) k_begin = max(k_begin, m0);
+  if (g.b_lower) k_begin = max(k_begin, n0);
+  k_begin = (k_begin / TK) * TK;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;   // wave's 32x32 sub-tile
+  double4_t acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = (double4_t){0., 0., 0., 0.};
+
+  for (int kk = k_begin; kk < k_end; kk += TK) {
+    // stage op(A)[m0:m0+64, kk:kk+16] and op(B)[kk:kk+16, n0:n0+64]; 4 elements per thread each
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int idx = tid + e * 256;
+      int i, k;
+      if (g.transA) { k = idx & 15; i = idx >> 4; } else { i = idx & 63; k = idx >> 6; }
+      const int gi = m0 + i, gk = kk + k;
+      double v = 0.;
+      if (gi < g.M && gk < k_end && gk >= k_begin && !(g.a_lower && gk > gi) && !(g.a_upper && gk < gi))
+        v = g.transA ? g.A[(size_t)gk + (size_t)gi * g.lda] : g.A[(size_t)gi + (size_t)gk * g.lda];
+      As[k][i] = v;
+      int j, kb;
+      if (g.transB) { j = idx & 63; kb = idx >> 6; } else { kb = idx & 15; j = idx >> 4; }
+      const int gj = n0 + j, gkb = kk + kb;
+      double w = 0.;
+      if (gj < g.N && gkb < k_end && gkb >= k_begin && !(g.b_lower && gkb < gj))
+        w = g.transB ? g.B[(size_t)gj + (size_t)gkb * g.ldb] : g.B[(size_t)gkb + (size_t)gj * g.ldb];
+      Bs[kb][j] = w;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k4 = 0; k4 < TK; k4 += 4) {
+      const int kl = k4 + (lane >> 4);
+      double a0 = As[kl][wm + (lane & 15)], a1 = As[kl][wm + 16 + (lane & 15)];
+      double b0 = Bs[kl][wn + (lane & 15)], b1 = Bs[kl][wn + 16 + (lane & 15)];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+  // epilogue: f64 MFMA C/D layout col = lane & 15, row = (lane >> 4) + 4 * reg
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int i = m0 + wm + a * 16 + (lane >> 4) + 4 * rg;
+        const int j = n0 + wn + b * 16 + (lane & 15);
+        if (i < g.M && j < g.N && !(g.lower_out && j > i)) {
+          double* c = g.C + (size_t)i + (size_t)j * g.ldc;
+          const double prev = (g.beta == 0.) ? 0. : g.beta * (*c);
+          *c = prev + g.alpha * acc[a][b][rg];
+        }
+      }
+}
+
+// Lower triangle (i >= j) of Psi = Sigma + I, tile-parallel, upper tiles skipped.
+template <int COV>
+__global__ void __launch_bounds__(256) build_psi_kernel(const double* __restrict__ X, int n, int d, int ld,
+                                                        double var, double phi, double* __restrict__ A) {
+  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+  if (j0 > i0 + 63) return;
+  const int ti = threadIdx.x & 63;
+  for (int jj = threadIdx.x >> 6; jj < 64; jj += 4) {
+    const int i = i0 + ti, j = j0 + jj;
+    if (i >= n || j >= n || j > i) continue;
+    double v;
+    if (i == j) {
+      v = var + 1.;
+    } else {
+      double s = 0.;
+      for (int q = 0; q < d; ++q) { const double t = X[(size_t)i * d + q] - X[(size_t)j * d + q]; s += t * t; }
+      double dc;
+      cov_dcov<COV>(sqrt(s), var, phi, v, dc);
+    }
+    A[(size_t)i + (size_t)j * ld] = v;
+  }
+}
+
+// Unblocked Cholesky of one (ib <= 64) diagonal block in LDS + its inverse.
+// L overwrites the lower triangle of A's block; L^-1 (upper part zero) is written to Winv's block.
+__global__ void __launch_bounds__(256) potrf_diag_kernel(double* A, int lda, int j0, int ib, double* Winv, int ldw,
+                                                       int* info) {
+  __shared__ double L[64][65];
+  __shared__ double I[64][65];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < 64 * 64; e += 256) {
+    const int i = e & 63, j = e >> 6;
+    L[i][j] = (i < ib && j < ib && j <= i) ? A[(size_t)(j0 + i) + (size_t)(j0 + j) * lda] : 0.;
+    I[i][j] = 0.;
+  }
+  __syncthreads();
+  for (int j = 0; j < ib; ++j) {
+    if (tid == 0) {
+      const double p = L[j][j];
+      if (!(p > 0.)) { atomicAdd(info, 1); L[j][j] = 1.; }   // not positive definite
+      else L[j][j] = sqrt(p);
+    }
+    __syncthreads();
+    const double ljj = L[j][j];
+    for (int i = j + 1 + tid; i < ib; i += 256) L[i][j] /= ljj;
+    __syncthreads();
+    const int w = ib - j - 1;
+    for (int e = tid; e < w * w; e += 256) {
+      const int i = j + 1 + e % w, c = j + 1 + e / w;
+      if (c <= i) L[i][c] -= L[i][j] * L[c][j];
+    }
+    __syncthreads();
+  }
+  // column c of L^-1 by thread c (forward substitution), in LDS
+  if (tid < ib) {
+    const int c = tid;
+    for (int i = c; i < ib; ++i) {
+      double s = (i == c) ? 1. : 0.;
+      for (int p = c; p < i; ++p) s -= L[i][p] * I[p][c];
+      I[i][c] = s / L[i][i];
+    }
+  }
+  __syncthreads();
+  for (int e = tid; e < ib * ib; e += 256) {
+    const int i = e % ib, j = e / ib;
+    if (j <= i) A[(size_t)(j0 + i) + (size_t)(j0 + j) * lda] = L[i][j];
+    Winv[(size_t)(j0 + i) + (size_t)(j0 + j) * ldw] = (j <= i) ? I[i][j] : 0.;
+  }
+}
+
+// 2 * sum log L_ii -> out (single block, fixed order)
+__global__ void __launch_bounds__(256) logdet_kernel(const double* A, int lda, int n, double* out) {
+  __shared__ double red[256];
+  double s = 0.;
+  for (int i = threadIdx.x; i < n; i += 256) s += log(A[(size_t)i + (size_t)i * lda]);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = 2. * red[0];
+}
+
+// z = W y for lower-triangular W: partial[cb][i] = sum_{j in column block cb, j <= i} W_ij y_j
+__global__ void __launch_bounds__(256) trmv_lower_partial_kernel(const double* W, int ld, int n, const double* y,
+                                                              double* partial) {
+  const int i = blockIdx.y * 256 + threadIdx.x;
+  const int cb = blockIdx.x;             // 256-column block
+  if (cb * 256 > blockIdx.y * 256 + 255) return;
+  __shared__ double ys[256];
+  const int jc = cb * 256 + threadIdx.x;
+  ys[threadIdx.x] = jc < n ? y[jc] : 0.;
+  __syncthreads();
+  if (i >= n) return;
+  double s = 0.;
+  const int jmax = min(min(cb * 256 + 256, n), i + 1);
+  for (int j = cb * 256; j < jmax; ++j) s += W[(size_t)i + (size_t)j * ld] * ys[j - cb * 256];
+  partial[(size_t)cb * n + i] = s;
+}
+
+__global__ void __launch_bounds__(256) trmv_lower_reduce_kernel(const double* partial, int n, double* z) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  double s = 0.;
+  for (int cb = 0; cb <= i / 256; ++cb) s += partial[(size_t)cb * n + i];
+  z[i] = s;
+}
+
+// out_j = sum_{i >= j} W_ij z_i (W^T z), one wave per column, coalesced down the column
+__global__ void __launch_bounds__(256) trmv_lower_t_kernel(const double* W, int ld, int n, const double* z, double* out) {
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (j >= n) return;
+  double s = 0.;
+  for (int i = j + lane; i < n; i += 64) s += W[(size_t)i + (size_t)j * ld] * z[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) out[j] = s;
+}
+
+// Fused gradient pass over the lower triangle of P = Psi^-1 (64 x 64 tiles):
+// per tile partial sums of [tr(dPsi_var P), tr(dPsi_rng P), yaux^T dPsi_var yaux, yaux^T dPsi_rng yaux]
+// with dPsi_var = Sigma (variance on the diagonal), dPsi_rng = dSigma/dlog(phi) (0 on the diagonal).
+template <int COV>
+__global__ void __launch_bounds__(256) dense_grad_kernel(const double* __restrict__ X, int n, int d, int ld,
+                                                         double var, double phi, const double* __restrict__ P,
+                                                         const double* __restrict__ yaux, double* __restrict__ part) {
+  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+  const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+  double s[4] = {0., 0., 0., 0.};
+  if (j0 <= i0 + 63) {
+    const int ti = threadIdx.x & 63;
+    const int i = i0 + ti;
+    double xi[3] = {0., 0., 0.};
+    if (i < n) for (int q = 0; q < d; ++q) xi[q] = X[(size_t)i * d + q];
+    const double yi = i < n ? yaux[i] : 0.;
+    for (int jj = threadIdx.x >> 6; jj < 64; jj += 4) {
+      const int j = j0 + jj;
+      if (i >= n || j >= n || j > i) continue;
+      const double pij = P[(size_t)i + (size_t)j * ld];
+      double c, dc;
+      if (i == j) {
+        c = var; dc = 0.;
+      } else {
+        double ss = 0.;
+        for (int q = 0; q < d; ++q) { const double t = xi[q] - X[(size_t)j * d + q]; ss += t * t; }
+        cov_dcov<COV>(sqrt(ss), var, phi, c, dc);
+      }
+      const double w = (i == j) ? 1. : 2.;
+      const double yy = w * yi * yaux[j];
+      s[0] += w * c * pij;
+      s[1] += w * dc * pij;
+      s[2] += yy * c;
+      s[3] += yy * dc;
+    }
+  }
+  __shared__ double red[4][256];
+  for (int q = 0; q < 4; ++q) red[q][threadIdx.x] = s[q];
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off)
+      for (int q = 0; q < 4; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) part[(size_t)tile * 4 + threadIdx.x] = red[threadIdx.x][0];
+}
+
+__global__ void dot_kernel(const double* a, const double* b, int n, double* out) {
+  __shared__ double red[256];
+  double s = 0.;
+  for (int i = threadIdx.x; i < n; i += 256) s += a[i] * b[i];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[0] = red[0];
+}
+
+void gemm(hipStream_t s, int M, int N, int K, double alpha, const double* A, int lda, int transA, const double* B,
+          int ldb, int transB, double beta, double* C, int ldc, int lower_out = 0, int a_lower = 0, int a_upper = 0,
+          int b_lower = 0) {
+  if (M <= 0 || N <= 0) return;
+  GemmArgs g{M, N, K, alpha, beta, A, lda, transA, B, ldb, transB, C, ldc, lower_out, a_lower, a_upper, b_lower};
+  dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM);
+  hipLaunchKernelGGL(gemm_f64_kernel, grid, dim3(256), 0, s, g);
+  HIP_CHECK(hipGetLastError());
+}
+
+template <typename F>
+void dispatch_cov(int cov, F&& f) {
+  switch (cov) {
+    case kMatern05: f(std::integral_constant<int, kMatern05>{}); break;
+    case kMatern15: f(std::integral_constant<int, kMatern15>{}); break;
+    case kMatern25: f(std::integral_constant<int, kMatern25>{}); break;
+    case kGaussian: f(std::integral_constant<int, kGaussian>{}); break;
+    default: Fatal("unsupported covariance type %d", cov);
+  }
+}
+
+}  // namespace
 
 DenseSolver::DenseSolver(int n, int d, const double* d_X, hipStream_t stream)
-    : n_(n), d_(d), ld_(n), d_X_(d_X), stream_(stream) {}
-DenseSolver::~DenseSolver() {}
-void DenseSolver::Eval(int, double, double, const double*, bool, double*, double*) {
-  Fatal("dense GPU path not available in this build yet");
+    : n_(n), d_(d), ld_(((n + 63) / 64) * 64), d_X_(d_X), stream_(stream) {
+  const size_t nn = (size_t)ld_ * (size_t)ld_;
+  A_.alloc(nn);
+  W_.alloc(nn);
+  T_.alloc((size_t)ld_ * (size_t)(ld_ / 2 + 64));
+  HIP_CHECK(hipMemsetAsync(A_.get(), 0, nn * sizeof(double), stream_));
+  HIP_CHECK(hipMemsetAsync(W_.get(), 0, nn * sizeof(double), stream_));
+  const int nb = (n + 255) / 256;
+  vec_.alloc((size_t)4 * ld_ + (size_t)nb * n);
+  const int tiles = ((n + 63) / 64) * ((n + 63) / 64);
+  red_.alloc((size_t)tiles * 4 + 16);
+  info_.alloc(1);
+  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_red_), 16 * sizeof(double), hipHostMallocDefault));
+  for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
+}
+
+DenseSolver::~DenseSolver() {
+  if (h_red_) (void)hipHostFree(h_red_);
+  for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
+}
+
+void DenseSolver::Potrf() {
+  // two-level right-looking Cholesky: 256-wide outer panels, 64-wide inner steps
+  const int n = n_, ld = ld_;
+  double* A = A_.get();
+  double* W = W_.get();
+  constexpr int NBO = 256, NBI = 64;
+  for (int J0 = 0; J0 < n; J0 += NBO) {
+    const int jb = std::min(NBO, n - J0);
+    for (int j0 = J0; j0 < J0 + jb; j0 += NBI) {
+      const int ib = std::min(NBI, J0 + jb - j0);
+      hipLaunchKernelGGL(potrf_diag_kernel, dim3(1), dim3(256), 0, stream_, A, ld, j0, ib, W, ld, info_.get());
+      HIP_CHECK(hipGetLastError());
+      const int r0 = j0 + ib;
+      if (r0 < n) {
+        // L21 = A21 * L11^-T  (in place: each 64-row tile reads its whole K = ib range first)
+        gemm(stream_, n - r0, ib, ib, 1., A + r0 + (size_t)j0 * ld, ld, 0, W + j0 + (size_t)j0 * ld, ld, 1, 0.,
+             A + r0 + (size_t)j0 * ld, ld, 0, 0, 0, 0);
+      }
+      if (r0 < J0 + jb) {
+        // remaining panel columns: A[r0:n, r0:J0+jb] -= L[r0:n, j0:r0] L[r0:J0+jb, j0:r0]^T
+        gemm(stream_, n - r0, J0 + jb - r0, ib, -1., A + r0 + (size_t)j0 * ld, ld, 0, A + r0 + (size_t)j0 * ld, ld, 1,
+             1., A + r0 + (size_t)r0 * ld, ld, 1, 0, 0, 0);
+      }
+    }
+    const int t0 = J0 + jb;
+    if (t0 < n) {
+      // trailing SYRK: A[t0:n, t0:n] -= L[t0:n, J0:t0] L[t0:n, J0:t0]^T  (lower tiles only)
+      gemm(stream_, n - t0, n - t0, jb, -1., A + t0 + (size_t)J0 * ld, ld, 0, A + t0 + (size_t)J0 * ld, ld, 1, 1.,
+           A + t0 + (size_t)t0 * ld, ld, 1, 0, 0, 0);
+    }
+  }
+}
+
+void DenseSolver::Trtri(int a, int b) {
+  // W[a:b, a:b] = L[a:b, a:b]^-1 (lower); diagonal 64-blocks were inverted by potrf_diag.
+  if (b - a <= 64) return;
+  const int half = ((b - a) / 2 + 63) / 64 * 64;
+  const int mid = a + half;
+  Trtri(a, mid);
+  Trtri(mid, b);
+  const int ld = ld_;
+  const double* L = A_.get();
+  double* W = W_.get();
+  double* X = T_.get();
+  const int m2 = b - mid, m1 = mid - a;
+  // X = L21 * W11   (W11 lower)
+  gemm(stream_, m2, m1, m1, 1., L + mid + (size_t)a * ld, ld, 0, W + a + (size_t)a * ld, ld, 0, 0., X, ld, 0, 0, 0, 1);
+  // W21 = -W22 * X  (W22 lower)
+  gemm(stream_, m2, m1, m2, -1., W + mid + (size_t)mid * ld, ld, 0, X, ld, 0, 0., W + mid + (size_t)a * ld, ld, 0, 1,
+       0, 0);
+}
+
+void DenseSolver::Eval(int cov_type, double var, double phi, const double* d_y, bool want_grad, double* sums,
+                       double* kernel_ms) {
+  const int n = n_, ld = ld_, d = d_;
+  double* A = A_.get();
+  double* W = W_.get();
+  double* z = vec_.get();
+  double* yaux = z + ld;
+  double* partial = z + 2 * (size_t)ld;
+  double* dred = red_.get();
+  HIP_CHECK(hipMemsetAsync(info_.get(), 0, sizeof(int), stream_));
+  HIP_CHECK(hipEventRecord(ev_[0], stream_));
+  const int nt = (n + 63) / 64;
+  dispatch_cov(cov_type, [&](auto c) {
+    hipLaunchKernelGGL((build_psi_kernel<decltype(c)::value>), dim3(nt, nt), dim3(256), 0, stream_, d_X_, n, d, ld, var,
+                       phi, A);
+  });
+  HIP_CHECK(hipGetLastError());
+  Potrf();
+  HIP_CHECK(hipEventRecord(ev_[1], stream_));
+  hipLaunchKernelGGL(logdet_kernel, dim3(1), dim3(256), 0, stream_, A, ld, n, dred + 0);
+  Trtri(0, n);
+  // z = W y, q = |z|^2
+  const int nb = (n + 255) / 256;
+  hipLaunchKernelGGL(trmv_lower_partial_kernel, dim3(nb, nb), dim3(256), 0, stream_, W, ld, n, d_y, partial);
+  hipLaunchKernelGGL(trmv_lower_reduce_kernel, dim3(nb), dim3(256), 0, stream_, partial, n, z);
+  hipLaunchKernelGGL(dot_kernel, dim3(1), dim3(256), 0, stream_, z, z, n, dred + 1);
+  HIP_CHECK(hipGetLastError());
+  int ngrad = 0;
+  if (want_grad) {
+    // y_aux = W^T z ; P = W^T W (lower) into A (L no longer needed)
+    hipLaunchKernelGGL(trmv_lower_t_kernel, dim3((n + 3) / 4), dim3(256), 0, stream_, W, ld, n, z, yaux);
+    gemm(stream_, n, n, n, 1., W, ld, 1, W, ld, 0, 0., A, ld, 1, 0, 1, 1);
+    dispatch_cov(cov_type, [&](auto c) {
+      hipLaunchKernelGGL((dense_grad_kernel<decltype(c)::value>), dim3(nt, nt), dim3(256), 0, stream_, d_X_, n, d, ld,
+                         var, phi, A, yaux, dred + 16);
+    });
+    HIP_CHECK(hipGetLastError());
+    ngrad = nt * nt;
+    launch_sum_blocks(dred + 16, ngrad, 4, dred + 2, stream_);
+  }
+  HIP_CHECK(hipMemcpyAsync(h_red_, dred, sizeof(double) * 6, hipMemcpyDeviceToHost, stream_));
+  int info = 0;
+  HIP_CHECK(hipMemcpyAsync(&info, info_.get(), sizeof(int), hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipEventRecord(ev_[2], stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  if (info != 0) Fatal("the covariance matrix is not positive definite (Cholesky failed)");
+  float ms0 = 0.f, ms1 = 0.f;
+  HIP_CHECK(hipEventElapsedTime(&ms0, ev_[0], ev_[1]));
+  HIP_CHECK(hipEventElapsedTime(&ms1, ev_[0], ev_[2]));
+  kernel_ms[0] = ms0;
+  kernel_ms[1] = ms1;
+  sums[0] = h_red_[0];
+  sums[1] = h_red_[1];
+  if (want_grad) {
+    // s1_k = -1/2 y_aux^T dPsi_k y_aux ; s2_k = tr(dPsi_k Psi^-1)   (re_model_template.h:1813-1814)
+    sums[2] = -0.5 * h_red_[4];
+    sums[3] = -0.5 * h_red_[5];
+    sums[4] = h_red_[2];
+    sums[5] = h_red_[3];
+  } else {
+    sums[2] = sums[3] = sums[4] = sums[5] = 0.;
+  }
 }
 
 }  // namespace gpb_amd
