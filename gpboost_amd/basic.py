@@ -190,6 +190,13 @@ class GPModel:
         g = grad[: self.num_cov_pars - 1] if profile_sigma2 else grad
         return float(negll[0]), g.copy(), float(s2[0])
 
+    def vecchia_partials(self, cov_pars, row_begin: int, row_end: int):
+        cp = self._check_cov_pars(cov_pars)
+        out = np.zeros(6)
+        _safe_call(lib().GPB_EvalVecchiaPartials(self.handle, _dp(cp), ctypes.c_int32(row_begin),
+                                                 ctypes.c_int32(row_end), _dp(out)))
+        return out
+
     def vecchia_structure(self):
         perm = np.zeros(self.num_data, dtype=np.int32)
         m = min(self.num_neighbors, self.num_data - 1)

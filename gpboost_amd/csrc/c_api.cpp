@@ -259,6 +259,13 @@ int GPB_GetNumCovPars(REModelHandle handle, int* num_cov_pars) {
   API_END();
 }
 
+int GPB_EvalVecchiaPartials(REModelHandle handle, const double* cov_pars, int32_t row_begin, int32_t row_end,
+                            double* sums) {
+  API_BEGIN();
+  model(handle)->EvalVecchiaPartials(cov_pars, row_begin, row_end, sums);
+  API_END();
+}
+
 int GPB_GetVecchiaStructure(REModelHandle handle, int32_t* perm, int32_t* neighbors) {
   API_BEGIN();
   model(handle)->GetVecchiaStructure(perm, neighbors);

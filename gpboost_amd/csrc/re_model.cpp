@@ -167,7 +167,7 @@ void REModelAMD::SetY(const double* y) {
   y_set_ = true;
 }
 
-void REModelAMD::EvalVecchia(const double* trafo, double* sums) {
+void REModelAMD::LaunchVecchiaRows(const double* trafo, int r0, int r1, double* sums, bool allreduce) {
   VecchiaRowsArgs a{};
   a.X = d_X_.get();
   a.Y = d_y_.get();
@@ -175,20 +175,20 @@ void REModelAMD::EvalVecchia(const double* trafo, double* sums) {
   a.n = cfg_.n;
   a.d = cfg_.d;
   a.m = cfg_.num_neighbors;
-  a.r0 = row_begin_;
-  a.r1 = row_end_;
+  a.r0 = r0;
+  a.r1 = r1;
   a.var = trafo[1];
   a.phi = trafo[2];
-  a.diag_mult = 1.;
+  a.diag_mult = 1.;   // Gaussian likelihood: nugget 1 on the transformed scale (Vecchia_utils.cpp:1540)
   a.diag_add = 1.;
   a.d_nugget = 1.;
   a.block_sums = d_block_sums_.get();
-  const int nblocks = vecchia_rows_blocks(row_end_ - row_begin_, a.m);
+  const int nblocks = vecchia_rows_blocks(r1 - r0, a.m);
   HIP_CHECK(hipEventRecord(ev_[0], stream_));
   launch_vecchia_rows(cfg_.cov_type, a, stream_);
   HIP_CHECK(hipEventRecord(ev_[1], stream_));
   launch_sum_blocks(d_block_sums_.get(), nblocks, kVecchiaSums, d_sums_.get(), stream_);
-  if (world_ > 1) {
+  if (allreduce && world_ > 1) {
     ncclResult_t r = ncclAllReduce(d_sums_.get(), d_sums_.get(), kVecchiaSums, ncclDouble, ncclSum, comm_, stream_);
     if (r != ncclSuccess) Fatal("ncclAllReduce failed: %s", ncclGetErrorString(r));
   }
@@ -201,6 +201,21 @@ void REModelAMD::EvalVecchia(const double* trafo, double* sums) {
   last_kernel_ms_[0] = ms0;
   last_kernel_ms_[1] = ms1;
   std::copy(h_sums_, h_sums_ + kVecchiaSums, sums);
+}
+
+void REModelAMD::EvalVecchia(const double* trafo, double* sums) {
+  LaunchVecchiaRows(trafo, row_begin_, row_end_, sums, true);
+}
+
+void REModelAMD::EvalVecchiaPartials(const double* cov_pars_orig, int r0, int r1, double* sums) {
+  if (!vecchia_) Fatal("model does not use the Vecchia approximation");
+  if (!y_set_) Fatal("response variable y has not been set");
+  if (r0 < row_begin_ || r1 > row_end_ || r0 > r1) Fatal("row range [%d, %d) outside this model's rows [%d, %d)", r0, r1, row_begin_, row_end_);
+  UseDevice();
+  EnsureStructure();
+  double trafo[3];
+  TransformCovPars(cov_pars_orig, trafo);
+  LaunchVecchiaRows(trafo, r0, r1, sums, false);
 }
 
 void REModelAMD::EvalDense(const double* trafo, bool want_grad, double* sums) {

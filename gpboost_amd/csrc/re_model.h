@@ -57,6 +57,9 @@ class REModelAMD {
 
   void SetDistributed(int rank, int world, const ncclUniqueId& id);
 
+  // Partial sums over rows [r0, r1) of this model's row block, no all-reduce (EXTENSION API).
+  void EvalVecchiaPartials(const double* cov_pars_orig, int r0, int r1, double* sums);
+
   void GetVecchiaStructure(int* perm, int* nbr) const;
   void GetVecchiaFactor(const double* cov_pars_orig, double* Dinv, double* Bvals);
   void GetLastKernelTimes(double* ms) const { ms[0] = last_kernel_ms_[0]; ms[1] = last_kernel_ms_[1]; }
@@ -74,6 +77,7 @@ class REModelAMD {
   void TransformCovPars(const double* orig, double* trafo) const;
   void BuildVecchiaStructure();
   void EvalVecchia(const double* trafo, double* sums);  // sums over this rank's rows, all-reduced
+  void LaunchVecchiaRows(const double* trafo, int r0, int r1, double* sums_host, bool allreduce);
   void EvalDense(const double* trafo, bool want_grad, double* sums);
 
   void EnsureStructure();

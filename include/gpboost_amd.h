@@ -196,6 +196,11 @@ GPBOOST_AMD_EXPORT int GPB_CommCreateId(char* id_out);
  * per-rank partial sums are all-reduced over RCCL (one all-reduce of 6 doubles per
  * evaluation). Must be called before the first evaluation. */
 GPBOOST_AMD_EXPORT int GPB_SetDistributed(REModelHandle handle, int rank, int world_size, const char* comm_id);
+/* The six per-row partial sums over Vecchia rows [row_begin, row_end) at cov_pars (original
+ * scale), without any all-reduce: for callers that run their own communication. The
+ * response must have been set by a previous evaluation. */
+GPBOOST_AMD_EXPORT int GPB_EvalVecchiaPartials(REModelHandle handle, const double* cov_pars,
+    int32_t row_begin, int32_t row_end, double* sums);
 /* Host-side partition of n rows over world_size ranks (block distribution). */
 GPBOOST_AMD_EXPORT int GPB_PartitionRows(int32_t num_data, int world_size, int rank, int32_t* row_begin, int32_t* row_end);
 /* Host-side final assembly from all-reduced partial sums (exposed so the reduction

@@ -174,3 +174,21 @@ def test_large_n_partials_match_oracle_on_row_subset():
     nll, g, _ = gm.neg_log_likelihood_and_grad([0.1, 1.0, 0.1], Y, profile_sigma2=True)
     assert abs(nll - ref["nll"]) <= RTOL * abs(ref["nll"])
     assert _close(g, ref["grad"])
+
+
+def test_row_block_partials_sum_to_whole():
+    """The sharded path's device side: partial sums of contiguous row blocks (as each rank of
+    `bench.py --gpus N` computes them) add up to the single-block sums; assembling them gives the
+    single-GPU nll/grad."""
+    from gpboost_amd import combine_partials, partition_rows, synthetic
+    n = 20000
+    X = synthetic.bench_coords(n)
+    Y = synthetic.bench_gaussian_y(n)
+    gm = _model(X, 30)
+    pars = [0.1, 1.0, 0.1]
+    nll, g, _ = gm.neg_log_likelihood_and_grad(pars, Y, profile_sigma2=True)
+    for world in (2, 3, 8):
+        tot = sum(gm.vecchia_partials(pars, *partition_rows(n, world, r)) for r in range(world))
+        nll_w, g_w, _ = combine_partials(tot, n, pars[0], True)
+        assert abs(nll_w - nll) <= 1e-10 * abs(nll)
+        np.testing.assert_allclose(g_w, g, rtol=1e-9)
