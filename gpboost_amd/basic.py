@@ -29,6 +29,12 @@ def _load_lib():
     D = ctypes.POINTER(ctypes.c_double)
     lib.GPB_EvalNegLogLikelihoodGrad.argtypes = [ctypes.c_void_p, D, D, D, ctypes.c_int, D, D, D]
     lib.GPB_CombinePartials.argtypes = [D, ctypes.c_int32, ctypes.c_double, ctypes.c_int, D, D, D]
+    I = ctypes.POINTER(ctypes.c_int)
+    c = ctypes
+    lib.GPB_SetOptimConfig.argtypes = [c.c_void_p, D, c.c_double, c.c_double, c.c_int, c.c_double, c.c_bool, c.c_int,
+                                       c.c_bool, c.c_char_p, c.c_int, c.c_char_p, c.c_int, D, c.c_double, c.c_double,
+                                       c.c_char_p, c.c_int, c.c_int, c.c_double, c.c_int, c.c_bool, c.c_char_p,
+                                       c.c_int, c.c_int, D, c.c_bool, I, c.c_int, c.c_double]
     return lib
 
 
@@ -70,7 +76,7 @@ def _as1d(x, name: str) -> np.ndarray:
 class GPModel:
     """Gaussian process model (reference ``gpboost.GPModel``), likelihood evaluation subset."""
 
-    _SUPPORTED_APPROX = ("none", "vecchia")
+    _SUPPORTED_APPROX = ("none", "vecchia", "vecchia_latent")
 
     def __init__(self, likelihood="gaussian", group_data=None, group_rand_coef_data=None,
                  ind_effect_group_rand_coef=None, drop_intercept_group_rand_effect=None, gp_coords=None,
@@ -104,7 +110,6 @@ class GPModel:
             num_neighbors = 20  # reference default (basic.py: num_neighbors None -> 20)
         self.num_neighbors = int(num_neighbors)
         self.likelihood = likelihood
-        self.num_cov_pars = 3
         coords_cm = np.ascontiguousarray(coords.T).reshape(-1)  # column-major, as the reference passes it
         cluster = None
         if cluster_ids is not None:
@@ -124,6 +129,16 @@ class GPModel:
             ctypes.c_bool(weights is not None), None, ctypes.c_double(likelihood_learning_rate),
             ctypes.byref(handle)))
         self.handle = handle
+        k = ctypes.c_int(0)
+        _safe_call(lib().GPB_GetNumCovPars(self.handle, ctypes.byref(k)))
+        self.num_cov_pars = k.value
+        _safe_call(lib().GPB_GetNumAuxPars(self.handle, ctypes.byref(k)))
+        self.num_aux_pars = k.value
+        # reference basic.py:4510-4533 (parameters of the likelihood path only)
+        self.params = {"cg_max_num_it": 1000, "cg_max_num_it_tridiag": 1000, "cg_delta_conv": 1e-2,
+                       "num_rand_vec_trace": 50, "reuse_rand_vec_trace": True, "seed_rand_vec_trace": 1,
+                       "cg_preconditioner_type": None, "init_aux_pars": None, "estimate_aux_pars": True,
+                       "delta_conv_mode_finding": -1.}
 
     def __del__(self):
         try:
@@ -147,10 +162,41 @@ class GPModel:
             raise ValueError("'cov_pars' does not contain the correct number of parameters")
         return cp
 
+    def set_optim_params(self, params=None):
+        """Store likelihood-path settings through GPB_SetOptimConfig (reference basic.py:5380-5540).
+        Optimizer-only keys are accepted and ignored (the optimizer is outside this library)."""
+        if params:
+            for key, val in params.items():
+                if key == "init_aux_pars" and val is not None:
+                    val = _as1d(val, "params['init_aux_pars']")
+                    if val.shape[0] != self.num_aux_pars:
+                        raise ValueError("params['init_aux_pars'] does not contain the correct number of parameters")
+                self.params[key] = val
+        p = self.params
+        aux = p["init_aux_pars"]
+        no_index = np.array([-1], dtype=np.int32)
+        _safe_call(lib().GPB_SetOptimConfig(
+            self.handle, None, -1., 0.5, 1000, -1., True, 0, False, None, 2,
+            b"relative_change_in_log_likelihood", 0, None, 0.1, 0.5, None,
+            int(p["cg_max_num_it"]), int(p["cg_max_num_it_tridiag"]), float(p["cg_delta_conv"]),
+            int(p["num_rand_vec_trace"]), bool(p["reuse_rand_vec_trace"]),
+            p["cg_preconditioner_type"].encode() if p["cg_preconditioner_type"] else None,
+            int(p["seed_rand_vec_trace"]), -1, _dp(aux) if aux is not None else None,
+            bool(p["estimate_aux_pars"]), no_index.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), -1,
+            float(p["delta_conv_mode_finding"])))
+
+    def get_aux_pars(self):
+        out = np.zeros(max(self.num_aux_pars, 1))
+        name = ctypes.create_string_buffer(128)
+        _safe_call(lib().GPB_GetAuxPars(self.handle, _dp(out), name))
+        return out[: self.num_aux_pars], name.value.decode()
+
     def neg_log_likelihood(self, cov_pars, y, fixed_effects=None, aux_pars=None):
         """Negative log-likelihood at ``cov_pars`` (original scale), reference basic.py:5284."""
         y = self._check_y(y)
         cp = self._check_cov_pars(cov_pars)
+        if aux_pars is not None:   # reference basic.py:5334-5335
+            self.set_optim_params({"init_aux_pars": aux_pars})
         fe = None
         if fixed_effects is not None:
             fe = _as1d(fixed_effects, "fixed_effects")
@@ -182,13 +228,32 @@ class GPModel:
         cp = self._check_cov_pars(cov_pars)
         fe = _as1d(fixed_effects, "fixed_effects") if fixed_effects is not None else None
         negll = np.zeros(1)
-        grad = np.zeros(self.num_cov_pars)
+        grad = np.full(self.num_cov_pars + self.num_aux_pars, np.nan)
         s2 = np.zeros(1)
         _safe_call(lib().GPB_EvalNegLogLikelihoodGrad(
             self.handle, _dp(y) if y is not None else None, _dp(cp), _dp(fe) if fe is not None else None,
             int(bool(profile_sigma2)), _dp(negll), _dp(grad), _dp(s2)))
-        g = grad[: self.num_cov_pars - 1] if profile_sigma2 else grad
+        if profile_sigma2:
+            g = grad[: self.num_cov_pars - 1]
+        elif self.num_aux_pars and self.params["estimate_aux_pars"]:
+            g = grad[: self.num_cov_pars + self.num_aux_pars]
+        else:
+            g = grad[: self.num_cov_pars]
         return float(negll[0]), g.copy(), float(s2[0])
+
+    def last_iteration_info(self):
+        """[newton iterations, CG iterations, Lanczos steps, log|Sigma W + I|] of the last latent evaluation."""
+        out = np.zeros(4)
+        _safe_call(lib().GPB_GetLastIterationInfo(self.handle, _dp(out)))
+        return out
+
+    def latent_vecchia_factor(self, cov_pars):
+        cp = self._check_cov_pars(cov_pars)
+        m = min(self.num_neighbors, self.num_data - 1)
+        dinv, dd = np.zeros(self.num_data), np.zeros(self.num_data)
+        b, db = np.zeros((self.num_data, m)), np.zeros((self.num_data, m))
+        _safe_call(lib().GPB_GetLatentVecchiaFactor(self.handle, _dp(cp), _dp(dinv), _dp(b), _dp(dd), _dp(db)))
+        return dict(Dinv=dinv, B=b, dD=dd, dB=db)
 
     def vecchia_partials(self, cov_pars, row_begin: int, row_end: int):
         cp = self._check_cov_pars(cov_pars)

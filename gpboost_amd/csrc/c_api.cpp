@@ -5,6 +5,7 @@
 // (log.h:171-191 semantics: "[GPBoost] [Info] ..."), else stderr.
 #include "gpboost_amd.h"
 
+#include <cmath>
 #include <cstdarg>
 #include <cstring>
 #include <exception>
@@ -119,7 +120,7 @@ int GPB_CreateREModel(int32_t num_data, const int32_t* cluster_ids_data, const c
   if (num_re_group_rand_coef > 0 || num_gp_rand_coef > 0 || gp_rand_coef_data != nullptr)
     gpb_amd::Fatal("random coefficients are out of scope for gpboost_amd (SURVEY.md §8)");
   if (num_gp != 1 || gp_coords_data == nullptr) gpb_amd::Fatal("gpboost_amd requires exactly one GP component (num_gp = 1)");
-  if (has_weights) gpb_amd::Fatal("'weights' are currently not supported for likelihood = 'gaussian'");
+  if (has_weights) gpb_amd::Fatal("'weights' are not supported by gpboost_amd");
   if (cluster_ids_data != nullptr) {
     for (int32_t i = 1; i < num_data; ++i)
       if (cluster_ids_data[i] != cluster_ids_data[0]) gpb_amd::Fatal("multiple clusters (cluster_ids) are out of scope for gpboost_amd");
@@ -133,8 +134,7 @@ int GPB_CreateREModel(int32_t num_data, const int32_t* cluster_ids_data, const c
   cfg.num_neighbors = num_neighbors;
   cfg.vecchia_ordering = str_or(vecchia_ordering, "random");
   cfg.likelihood = str_or(likelihood, "gaussian");
-  cfg.matrix_inversion_method = str_or(matrix_inversion_method, "cholesky");
-  if (cfg.matrix_inversion_method == "default") cfg.matrix_inversion_method = "cholesky";
+  cfg.matrix_inversion_method = str_or(matrix_inversion_method, "default");
   cfg.seed = seed;
   if (seed < 0) gpb_amd::Fatal("seed must be >= 0");
   *out = new REModelAMD(cfg, gp_coords_data);
@@ -156,18 +156,35 @@ int GPB_SetOptimConfig(REModelHandle handle, double* init_cov_pars, double lr, d
                        const char* cg_preconditioner_type, int seed_rand_vec_trace, int piv_chol_rank,
                        double* init_aux_pars, bool estimate_aux_pars, const int* estimate_cov_par_index,
                        int m_lbfgs, double delta_conv_mode_finding) {
+  // re_model_template.h:686-823: only the settings of the likelihood path are stored; the
+  // optimizer settings belong to GPB_OptimCovPar, which is outside this library's scope.
   API_BEGIN();
   (void)init_cov_pars; (void)lr; (void)acc_rate_cov; (void)max_iter; (void)delta_rel_conv; (void)use_nesterov_acc;
   (void)nesterov_schedule_version; (void)trace; (void)optimizer; (void)momentum_offset; (void)convergence_criterion;
   (void)num_covariates; (void)init_coef; (void)lr_coef; (void)acc_rate_coef; (void)optimizer_coef;
-  (void)cg_max_num_it_tridiag; (void)reuse_rand_vec_trace; (void)cg_preconditioner_type; (void)piv_chol_rank;
-  (void)init_aux_pars; (void)estimate_aux_pars; (void)estimate_cov_par_index; (void)m_lbfgs;
-  (void)delta_conv_mode_finding;
+  (void)piv_chol_rank; (void)m_lbfgs;
   REModelAMD* m = model(handle);
-  m->cg_max_num_it = cg_max_num_it;
-  m->cg_delta_conv = cg_delta_conv;
-  m->num_rand_vec_trace = num_rand_vec_trace;
-  m->seed_rand_vec_trace = seed_rand_vec_trace;
+  if (m->config().matrix_inversion_method == "iterative") {   // :775-801
+    m->iter.cg_max_num_it = cg_max_num_it;
+    m->iter.cg_max_num_it_tridiag = cg_max_num_it_tridiag;
+    m->iter.cg_delta_conv = cg_delta_conv;
+    if (cg_preconditioner_type != nullptr && std::string(cg_preconditioner_type) != "") {
+      const std::string p(cg_preconditioner_type);
+      if (p != "vadu" && p != "VADU" && p != "vecchia_approximation_with_diagonal_update" && p != "Sigma_inv_plus_BtWB")
+        gpb_amd::Fatal("cg_preconditioner_type '%s' is not supported by gpboost_amd (supported: vadu)", p.c_str());
+    }
+  }
+  if (num_rand_vec_trace <= 0) gpb_amd::Fatal("num_rand_vec_trace must be > 0");
+  m->iter.num_rand_vec_trace = num_rand_vec_trace;   // :771-773
+  m->iter.seed_rand_vec_trace = seed_rand_vec_trace;
+  m->iter.reuse_rand_vec_trace = reuse_rand_vec_trace;
+  if (delta_conv_mode_finding > 0.) m->iter.delta_conv_mode_finding = delta_conv_mode_finding;   // :820-822
+  if (init_aux_pars != nullptr) m->SetAuxPars(init_aux_pars);
+  m->estimate_aux_pars = estimate_aux_pars;   // :803
+  if (estimate_cov_par_index != nullptr && estimate_cov_par_index[0] >= 0) {
+    for (int k = 0; k < m->num_cov_pars(); ++k)
+      if (estimate_cov_par_index[k] <= 0) gpb_amd::Fatal("estimate_cov_par_index: fixing covariance parameters is not supported by gpboost_amd");
+  }
   API_END();
 }
 
@@ -178,6 +195,8 @@ int GPB_EvalNegLogLikelihood(REModelHandle handle, const double* y_data, double*
   if (cov_pars == nullptr) gpb_amd::Fatal("cov_pars is NULL (initial-value heuristics are out of scope)");
   if (fixed_effects != nullptr) {
     if (y_data == nullptr) gpb_amd::Fatal("EvalNegLogLikelihood: 'y_data' cannot nullptr when 'fixed_effects' is provided");
+    if (m->config().latent && m->config().lik != gpb_amd::kLikGaussian)
+      gpb_amd::Fatal("'fixed_effects' are not supported for likelihood '%s' by gpboost_amd", m->config().likelihood.c_str());
     std::vector<double> r(m->config().n);
     for (int i = 0; i < m->config().n; ++i) r[i] = y_data[i] - fixed_effects[i];
     m->SetY(r.data());
@@ -196,6 +215,8 @@ int GPB_EvalNegLogLikelihoodGrad(REModelHandle handle, const double* y_data, con
   if (cov_pars == nullptr || negll == nullptr || grad == nullptr) gpb_amd::Fatal("NULL argument");
   if (fixed_effects != nullptr) {
     if (y_data == nullptr) gpb_amd::Fatal("'y_data' cannot be NULL when 'fixed_effects' is provided");
+    if (m->config().latent && m->config().lik != gpb_amd::kLikGaussian)
+      gpb_amd::Fatal("'fixed_effects' are not supported for likelihood '%s' by gpboost_amd", m->config().likelihood.c_str());
     std::vector<double> r(m->config().n);
     for (int i = 0; i < m->config().n; ++i) r[i] = y_data[i] - fixed_effects[i];
     m->SetY(r.data());
@@ -248,8 +269,30 @@ int GPB_GetLikelihoodName(REModelHandle handle, char* out_str, int* num_char) {
 
 int GPB_GetNumAuxPars(REModelHandle handle, int* num_aux_pars) {
   API_BEGIN();
-  (void)model(handle);
-  num_aux_pars[0] = 0;
+  num_aux_pars[0] = model(handle)->num_aux_pars();
+  API_END();
+}
+
+int GPB_GetAuxPars(REModelHandle handle, double* aux_pars, char* out_str) {
+  API_BEGIN();
+  REModelAMD* m = model(handle);
+  const auto& a = m->aux_pars();
+  for (size_t k = 0; k < a.size(); ++k) aux_pars[k] = a[k];
+  const std::string name = m->aux_par_name();
+  if (out_str != nullptr) std::memcpy(out_str, name.c_str(), name.size() + 1);
+  API_END();
+}
+
+int GPB_GetLatentVecchiaFactor(REModelHandle handle, const double* cov_pars, double* D_inv, double* B_vals,
+                               double* dD_range, double* dB_range_vals) {
+  API_BEGIN();
+  model(handle)->GetLatentVecchiaFactor(cov_pars, D_inv, B_vals, dD_range, dB_range_vals);
+  API_END();
+}
+
+int GPB_GetLastIterationInfo(REModelHandle handle, double* info) {
+  API_BEGIN();
+  model(handle)->GetLastIterationInfo(info);
   API_END();
 }
 

@@ -1,0 +1,456 @@
+// LatentVecchia implementation: host orchestration of the iterative latent-Vecchia path.
+#include "latent.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "slq_host.h"
+
+namespace gpb_amd {
+
+namespace {
+constexpr double kJitterMultVecchia = 1. + 1e-10;   // JITTER_MULT_VECCHIA (utils.h)
+constexpr double kCArmijo = 1e-4;                   // c_armijo_ (likelihoods.h:12737)
+// ZERO_RHS_CG_THRESHOLD = 1e-100 on sum|rhs| (utils.h:45, CG_utils.cpp:42-45); tested here as
+// sum rhs^2 < 1e-200, which is implied by it and differs only below ~1e-100 magnitudes.
+constexpr double kZeroRhsSq = 1e-200;
+constexpr int kOutDoubles = 1024;
+}  // namespace
+
+LatentVecchia::LatentVecchia(int n, int d, int m, const double* d_X, const int* nbr, hipStream_t stream)
+    : n_(n), d_(d), m_(m), d_X_(d_X), s_(stream) {
+  HIP_CHECK(hipEventCreate(&ev0_));
+  HIP_CHECK(hipEventCreate(&ev1_));
+  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_out_), kOutDoubles * sizeof(double), hipHostMallocDefault));
+  BuildStructure(nbr);
+  for (auto* b : {&d_Bv_, &d_dBv_}) b->alloc((size_t)n * m);
+  for (auto* b : {&d_y_, &d_Dinv_, &d_dD_, &d_W_, &d_dw_, &d_sdw_, &d_d1_, &d_mode_, &d_mode_upd_, &d_mode_new_,
+                  &d_rhs_, &d_dir_, &d_Adir_, &d_vS_, &d_dmll_})
+    b->alloc(n);
+  d_out_.alloc(kOutDoubles);
+}
+
+LatentVecchia::~LatentVecchia() {
+  if (h_out_) (void)hipHostFree(h_out_);
+  if (ev0_) (void)hipEventDestroy(ev0_);
+  if (ev1_) (void)hipEventDestroy(ev1_);
+}
+
+// Host construction of the B^T lists and the level sets of both triangular solves.
+// Level of row i in the lower solve: 1 + max level of its neighbours (all earlier rows);
+// level of column j in the B^T (unit upper) solve: 1 + max level of the rows that have j
+// as a neighbour. Rows inside a level are independent.
+void LatentVecchia::BuildStructure(const int* nbr) {
+  const int n = n_, m = m_;
+  std::vector<int> cnt(n + 1, 0);
+  for (int i = 0; i < n; ++i) {
+    const int k = std::min(i, m);
+    for (int r = 0; r < k; ++r) ++cnt[nbr[(size_t)i * m + r] + 1];
+  }
+  std::vector<int> tptr(n + 1, 0);
+  for (int j = 0; j < n; ++j) tptr[j + 1] = tptr[j] + cnt[j + 1];
+  const int nnz = tptr[n];
+  std::vector<int> trow(std::max(nnz, 1)), tslot(std::max(nnz, 1)), fill(tptr.begin(), tptr.end() - 1);
+  for (int i = 0; i < n; ++i) {   // ascending i -> rows ascending within each column
+    const int k = std::min(i, m);
+    for (int r = 0; r < k; ++r) {
+      const int j = nbr[(size_t)i * m + r];
+      trow[fill[j]] = i;
+      tslot[fill[j]] = i * m + r;
+      ++fill[j];
+    }
+  }
+  std::vector<int> lf(n, 0), lb(n, 0);
+  int Lf = 0, Lb = 0;
+  for (int i = 0; i < n; ++i) {
+    const int k = std::min(i, m);
+    int l = 0;
+    for (int r = 0; r < k; ++r) l = std::max(l, lf[nbr[(size_t)i * m + r]] + 1);
+    lf[i] = l;
+    Lf = std::max(Lf, l + 1);
+  }
+  for (int i = n - 1; i >= 0; --i) {
+    const int k = std::min(i, m);
+    for (int r = 0; r < k; ++r) {
+      const int j = nbr[(size_t)i * m + r];
+      lb[j] = std::max(lb[j], lb[i] + 1);
+    }
+    Lb = std::max(Lb, lb[i] + 1);
+  }
+  auto bucket = [n](const std::vector<int>& lev, int L, std::vector<int>& ptr, std::vector<int>& rows) {
+    ptr.assign(L + 1, 0);
+    for (int i = 0; i < n; ++i) ++ptr[lev[i] + 1];
+    for (int l = 0; l < L; ++l) ptr[l + 1] += ptr[l];
+    std::vector<int> f(ptr.begin(), ptr.end() - 1);
+    rows.resize(n);
+    for (int i = 0; i < n; ++i) rows[f[lev[i]]++] = i;
+  };
+  std::vector<int> frows, brows;
+  bucket(lf, Lf, fptr_, frows);
+  bucket(lb, Lb, bptr_, brows);
+
+  d_nbr_.alloc((size_t)n * m);
+  d_tptr_.alloc(n + 1);
+  d_trow_.alloc(trow.size());
+  d_tslot_.alloc(tslot.size());
+  d_frows_.alloc(n);
+  d_brows_.alloc(n);
+  HIP_CHECK(hipMemcpyAsync(d_nbr_.get(), nbr, sizeof(int) * (size_t)n * m, hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipMemcpyAsync(d_tptr_.get(), tptr.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipMemcpyAsync(d_trow_.get(), trow.data(), sizeof(int) * trow.size(), hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipMemcpyAsync(d_tslot_.get(), tslot.data(), sizeof(int) * tslot.size(), hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipMemcpyAsync(d_frows_.get(), frows.data(), sizeof(int) * n, hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipMemcpyAsync(d_brows_.get(), brows.data(), sizeof(int) * n, hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  sp_.n = n;
+  sp_.m = m;
+  sp_.nbr = d_nbr_.get();
+  sp_.tptr = d_tptr_.get();
+  sp_.trow = d_trow_.get();
+  sp_.tslot = d_tslot_.get();
+}
+
+void LatentVecchia::SetY(const double* y_vo) {
+  HIP_CHECK(hipMemcpyAsync(d_y_.get(), y_vo, sizeof(double) * n_, hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  y_set_ = true;
+}
+
+LatentVecchia::Block& LatentVecchia::GetBlock(int which, int t, int pmax) {
+  std::unique_ptr<Block>& bp = which == 0 ? blk1_ : blkt_;
+  if (!bp) bp.reset(new Block());
+  Block& b = *bp;
+  if (b.t != t) {
+    const size_t nt = (size_t)n_ * t;
+    for (auto* buf : {&b.R, &b.Z, &b.H, &b.V, &b.G, &b.Xt}) buf->alloc(nt);
+    b.small.alloc((size_t)6 * t);
+    b.t = t;
+  }
+  if (b.a_hist.size() < (size_t)pmax * t) {
+    b.a_hist.alloc((size_t)pmax * t);
+    b.b_hist.alloc((size_t)pmax * t);
+  }
+  const size_t need = (size_t)kMaxRedBlocks * std::max(kGradCols * t, (int)kLatentScalars);
+  if (d_partials_.size() < need) d_partials_.alloc(need);
+  if (d_out_.size() < (size_t)kGradCols * t) d_out_.alloc((size_t)kGradCols * t);
+  return b;
+}
+
+void LatentVecchia::EnsureProbes(const IterativeConfig& cfg) {
+  const int t = cfg.num_rand_vec_trace;
+  if (probes_saved_ && probes_t_ == t) return;
+  // GenRandVecNormalParallel (CG_utils.cpp:930-947), drawn once when reuse_rand_vec_trace
+  std::vector<double> R((size_t)n_ * t);
+  gen_probes_normal(n_, t, cfg.seed_rand_vec_trace, probe_run_id_, R.data());
+  ++probe_run_id_;
+  d_probes_.alloc((size_t)n_ * t);
+  d_Zp_.alloc((size_t)n_ * t);
+  d_U_.alloc((size_t)n_ * t);
+  d_P_.alloc((size_t)n_ * t);
+  HIP_CHECK(hipMemcpyAsync(d_probes_.get(), R.data(), sizeof(double) * R.size(), hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  probes_t_ = t;
+  probes_saved_ = cfg.reuse_rand_vec_trace;
+}
+
+// V = (B^T D^-1 B + W) H   (CG_utils.cpp:75, 161-164)
+void LatentVecchia::ApplyA(const double* H, double* V, double* G, int t) {
+  launch_b_apply(sp_, d_Bv_.get(), true, H, t, d_Dinv_.get(), G, s_);
+  launch_bt_apply(sp_, d_Bv_.get(), true, G, t, nullptr, d_W_.get(), H, V, s_);
+}
+
+// Z = P^-1 R, P = B^T (D^-1 + W) B (VADU, CG_utils.cpp:56-60): B^T solve then (dw B) solve.
+void LatentVecchia::Precond(const double* R, double* Z, double* Xt, int t) {
+  for (size_t l = 0; l + 1 < bptr_.size(); ++l)
+    launch_trsv_bt_level(sp_, d_Bv_.get(), d_brows_.get() + bptr_[l], bptr_[l + 1] - bptr_[l], R, Xt, t, s_);
+  for (size_t l = 0; l + 1 < fptr_.size(); ++l)
+    launch_trsv_b_level(sp_, d_Bv_.get(), d_dw_.get(), d_frows_.get() + fptr_[l], fptr_[l + 1] - fptr_[l], Xt, Z, t,
+                        s_);
+}
+
+double LatentVecchia::Dot1(const double* x, const double* y) {
+  const double* A[1] = {x};
+  const double* Bm[1] = {y};
+  launch_coldots(n_, 1, 1, A, Bm, d_partials_.get(), d_out_.get(), s_);
+  HIP_CHECK(hipMemcpyAsync(h_out_, d_out_.get(), sizeof(double), hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  return h_out_[0];
+}
+
+void LatentVecchia::Scalars(const ScalarArgs& a, double* out) {
+  launch_latent_scalars(a, d_partials_.get(), d_out_.get(), s_);
+  HIP_CHECK(hipMemcpyAsync(h_out_, d_out_.get(), sizeof(double) * kLatentScalars, hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  std::copy(h_out_, h_out_ + kLatentScalars, out);
+}
+
+int LatentVecchia::Pcg(Block& b, const double* RHS, double* U, bool init_zero, bool u_is_zero, int pmax,
+                       double delta, bool tridiag, bool* nan, bool* zero_rhs) {
+  const int t = b.t;
+  const size_t nt = (size_t)n_ * t;
+  if (h_rr_.size() < (size_t)t) h_rr_.resize(t);
+  *nan = false;
+  *zero_rhs = false;
+  pmax = std::min(pmax, n_);
+  if (!tridiag) {
+    if (Dot1(RHS, RHS) < kZeroRhsSq) {   // CG_utils.cpp:42-45
+      HIP_CHECK(hipMemsetAsync(U, 0, sizeof(double) * nt, s_));
+      *zero_rhs = true;
+      return 0;
+    }
+  }
+  if (tridiag || init_zero || u_is_zero) {
+    HIP_CHECK(hipMemsetAsync(U, 0, sizeof(double) * nt, s_));
+    launch_copy(nt, RHS, b.R.get(), s_);
+  } else {   // r = rhs - A u (warm start, CG_utils.cpp:53-55)
+    ApplyA(U, b.V.get(), b.G.get(), t);
+    launch_axpby(nt, 1., RHS, -1., b.V.get(), b.R.get(), s_);
+  }
+  Precond(b.R.get(), b.Z.get(), b.Xt.get(), t);
+  launch_copy(nt, b.Z.get(), b.H.get(), s_);
+  {
+    const double* A[1] = {b.R.get()};
+    const double* Bm[1] = {b.Z.get()};
+    launch_coldots(n_, t, 1, A, Bm, d_partials_.get(), b.rz(), s_);
+  }
+  int j = 0;
+  for (; j < pmax; ++j) {
+    ApplyA(b.H.get(), b.V.get(), b.G.get(), t);
+    {
+      const double* A[1] = {b.H.get()};
+      const double* Bm[1] = {b.V.get()};
+      launch_coldots(n_, t, 1, A, Bm, d_partials_.get(), b.hv(), s_);
+    }
+    launch_cg_alpha(t, b.rz(), b.hv(), b.a(), tridiag ? b.a_hist.get() + (size_t)j * t : nullptr, s_);
+    launch_cg_update(n_, t, b.a(), b.H.get(), b.V.get(), U, b.R.get(), d_partials_.get(), b.rr(), s_);
+    HIP_CHECK(hipMemcpyAsync(h_rr_.data(), b.rr(), sizeof(double) * t, hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipStreamSynchronize(s_));
+    double norm = 0.;
+    for (int c = 0; c < t; ++c) norm += std::sqrt(h_rr_[c]);
+    norm /= t;   // t = 1: ||r||; block: mean column norm (CG_utils.cpp:172)
+    if (std::isnan(norm) || std::isinf(norm)) {
+      *nan = true;
+      return j + 1;
+    }
+    if (norm < delta) return j + 1;
+    Precond(b.R.get(), b.Z.get(), b.Xt.get(), t);
+    {
+      const double* A[1] = {b.R.get()};
+      const double* Bm[1] = {b.Z.get()};
+      launch_coldots(n_, t, 1, A, Bm, d_partials_.get(), b.rz_new(), s_);
+    }
+    launch_cg_beta(t, b.rz_new(), b.rz(), b.b(), tridiag ? b.b_hist.get() + (size_t)j * t : nullptr, s_);
+    launch_h_update(n_, t, b.b(), b.Z.get(), b.H.get(), s_);
+  }
+  return j;
+}
+
+LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, double aux, const IterativeConfig& cfg,
+                                 bool want_grad, bool want_aux_grad) {
+  if (!y_set_) Fatal("response variable y has not been set");
+  if (!(trafo[0] > 0. && trafo[1] > 0.)) Fatal("covariance parameters must be > 0");
+  if (lik == kLikGaussian && !(aux > 0.)) Fatal("the error variance (aux_pars) must be > 0");
+  const int n = n_;
+  const bool gauss = lik == kLikGaussian;
+  const int t = cfg.num_rand_vec_trace;
+  if (t < 1) Fatal("num_rand_vec_trace must be >= 1");
+  LatentResult res;
+  HIP_CHECK(hipEventRecord(ev0_, s_));
+
+  // ---- 1. latent Vecchia factor (+ range derivatives)
+  LatentFactorArgs fa{};
+  fa.X = d_X_;
+  fa.nbr = d_nbr_.get();
+  fa.n = n; fa.d = d_; fa.m = m_;
+  fa.var = trafo[0];
+  fa.phi = trafo[1];
+  fa.jitter = kJitterMultVecchia;
+  fa.Bv = d_Bv_.get();
+  fa.dBv = want_grad ? d_dBv_.get() : nullptr;
+  fa.Dinv = d_Dinv_.get();
+  fa.dD = want_grad ? d_dD_.get() : nullptr;
+  launch_latent_factor(cov_type, fa, s_);
+
+  Block& b1 = GetBlock(0, 1, std::max(cfg.cg_max_num_it, 1));
+  ScalarArgs sa{};
+  sa.n = n; sa.m = m_; sa.lik = lik; sa.aux = aux;
+  sa.nbr = d_nbr_.get(); sa.Bv = d_Bv_.get(); sa.Dinv = d_Dinv_.get(); sa.y = d_y_.get();
+
+  // ---- 2. mode finding (likelihoods.h:2780-3000); mode re-initialised to 0 (InitializeModeAvec)
+  HIP_CHECK(hipMemsetAsync(d_mode_.get(), 0, sizeof(double) * n, s_));
+  HIP_CHECK(hipMemsetAsync(d_mode_upd_.get(), 0, sizeof(double) * n, s_));
+  double sc[kLatentScalars];
+  sa.mode = d_mode_.get();
+  Scalars(sa, sc);
+  if (std::isnan(sc[kSqLogDinv]) || std::isinf(sc[kSqLogDinv]))   // Vecchia_utils.cpp:1619-1630
+    Fatal("The matrix D in the Vecchia approximation contains negative or zero values. "
+          "This likely results from numerical instabilities ");
+  double mll = sc[kSqLogLik] - 0.5 * sc[kSqQuad];
+  const bool info_changes = !gauss;              // information_changes_during/after_mode_finding_
+  const int maxit = gauss ? 1 : 1000;            // maxit_mode_newton_ (likelihoods.h:255, 12721)
+  const int max_shrink = gauss ? 1 : 20;         // max_number_lr_shrinkage_steps_newton_ (:256, 12725)
+  bool upd_zero = true;
+  for (int it = 0; it < maxit; ++it) {
+    NewtonPrepArgs np{};
+    np.n = n; np.lik = lik; np.aux = aux; np.y = d_y_.get(); np.loc = d_mode_.get(); np.mode = d_mode_.get();
+    np.Dinv = d_Dinv_.get(); np.d1 = d_d1_.get(); np.W = d_W_.get();
+    np.W_update = (it == 0 || info_changes) ? 1 : 0;
+    np.rhs = d_rhs_.get();
+    np.dw = (it == 0 || info_changes) ? d_dw_.get() : nullptr;
+    launch_newton_prep(np, s_);
+    bool nan = false, zr = false;
+    const int its = Pcg(b1, d_rhs_.get(), d_mode_upd_.get(), it == 0, upd_zero, cfg.cg_max_num_it, cfg.cg_delta_conv,
+                        false, &nan, &zr);
+    res.cg_its += its;
+    upd_zero = zr;
+    if (nan) Fatal("NaN or Inf occurred in the conjugate gradient algorithm during mode finding");
+    // Armijo (likelihoods.h:2957-2966): only consulted when more than one step size is tried
+    double gdd = 0.;
+    if (max_shrink > 1) {
+      launch_axpby(n, 1., d_mode_upd_.get(), -1., d_mode_.get(), d_dir_.get(), s_);
+      ApplyA(d_dir_.get(), d_Adir_.get(), b1.G.get(), 1);
+      gdd = Dot1(d_dir_.get(), d_Adir_.get());
+    }
+    double lr = 1., mll_new = mll;
+    for (int ih = 0; ih < max_shrink; ++ih) {
+      if (ih == 0) launch_copy(n, d_mode_upd_.get(), d_mode_new_.get(), s_);
+      else launch_axpby(n, 1. - lr, d_mode_.get(), lr, d_mode_upd_.get(), d_mode_new_.get(), s_);
+      sa.mode = d_mode_new_.get();
+      Scalars(sa, sc);
+      mll_new = sc[kSqLogLik] - 0.5 * sc[kSqQuad];
+      if (mll_new < mll + kCArmijo * lr * gdd || std::isnan(mll_new) || std::isinf(mll_new)) lr *= 0.5;
+      else break;
+    }
+    std::swap(d_mode_, d_mode_new_);
+    res.newton_its = it + 1;
+    // CheckConvergenceModeFinding (likelihoods.h:11820-11870)
+    if (std::isnan(mll_new) || std::isinf(mll_new))
+      Fatal("NaN or Inf occurred in the mode finding algorithm for the Laplace approximation");
+    const double dc = cfg.delta_conv_mode_finding;
+    const bool term = (it == 0) ? std::fabs(mll_new - mll) < dc * std::fabs(mll) : (mll_new - mll) < dc * std::fabs(mll);
+    mll = mll_new;
+    if (term) break;
+  }
+  {   // derivative / information at the mode, VADU diagonal and its square root (:3000-3005, 12163-12166)
+    NewtonPrepArgs np{};
+    np.n = n; np.lik = lik; np.aux = aux; np.y = d_y_.get(); np.loc = d_mode_.get(); np.mode = d_mode_.get();
+    np.Dinv = d_Dinv_.get(); np.d1 = d_d1_.get(); np.W = d_W_.get();
+    np.W_update = info_changes ? 1 : 0;
+    np.dw = d_dw_.get();
+    np.sdw = d_sdw_.get();
+    launch_newton_prep(np, s_);
+  }
+
+  // ---- 3. SLQ log-determinant (likelihoods.h:3018-3045, 12155-12212)
+  EnsureProbes(cfg);
+  const int pmax_tri = std::max(1, std::min(cfg.cg_max_num_it_tridiag, n));
+  Block& bt = GetBlock(1, t, pmax_tri);
+  // z_i = B^T (D^-1 + W)^(1/2) r_i
+  launch_bt_apply(sp_, d_Bv_.get(), true, d_probes_.get(), t, d_sdw_.get(), nullptr, nullptr, d_Zp_.get(), s_);
+  bool nan = false, zr = false;
+  const int L = Pcg(bt, d_Zp_.get(), d_U_.get(), true, true, pmax_tri, cfg.cg_delta_conv, true, &nan, &zr);
+  if (nan) Fatal("NaN or Inf occurred in the stochastic Lanczos quadrature (log-determinant)");
+  res.lanczos_steps = L;
+  std::vector<double> ah((size_t)L * t), bh((size_t)L * t);
+  HIP_CHECK(hipMemcpyAsync(ah.data(), bt.a_hist.get(), sizeof(double) * ah.size(), hipMemcpyDeviceToHost, s_));
+  if (L > 1)
+    HIP_CHECK(hipMemcpyAsync(bh.data(), bt.b_hist.get(), sizeof(double) * (size_t)(L - 1) * t, hipMemcpyDeviceToHost,
+                             s_));
+  sa.mode = d_mode_.get();
+  sa.dw = d_dw_.get();
+  Scalars(sa, sc);   // synchronises the stream
+  std::vector<std::vector<double>> Td(t), Ts(t);
+  for (int c = 0; c < t; ++c) {   // CG_utils.cpp:200-206 (a_old = 1, b_old = 0 before the first step)
+    Td[c].resize(L);
+    Ts[c].resize(L > 0 ? L - 1 : 0);
+    for (int j = 0; j < L; ++j) {
+      const double a = ah[(size_t)j * t + c];
+      const double a_old = j > 0 ? ah[(size_t)(j - 1) * t + c] : 1.;
+      const double b_old = j > 0 ? bh[(size_t)(j - 1) * t + c] : 0.;
+      Td[c][j] = 1. / a + b_old / a_old;
+      if (j > 0) Ts[c][j - 1] = std::sqrt(b_old) / a_old;
+    }
+  }
+  const double ldet_PI = slq_logdet(Td, Ts, n);
+  res.logdet = ldet_PI - sc[kSqLogDinv] + sc[kSqLogDw];
+  const double mll_final = mll - 0.5 * res.logdet;
+  res.nll = -mll_final;
+
+  if (want_grad) {
+    // ---- 4. gradient (likelihoods.h:4951-5206)
+    Precond(d_Zp_.get(), d_P_.get(), bt.Xt.get(), t);   // PI_Z = P^-1 Z (:12321-12327)
+    if (!gauss) {   // grad_information_wrt_mode_non_zero_: implicit derivative through the mode
+      ModeDerivArgs md{};
+      md.n = n; md.m = m_; md.t = t; md.lik = lik; md.nbr = d_nbr_.get(); md.Bv = d_Bv_.get(); md.dw = d_dw_.get();
+      md.loc = d_mode_.get(); md.U = d_U_.get(); md.P = d_P_.get(); md.dmll = d_dmll_.get();
+      launch_mode_deriv(md, s_);
+      bool nan2 = false, zr2 = false;
+      res.cg_its += Pcg(b1, d_dmll_.get(), d_vS_.get(), true, true, cfg.cg_max_num_it, cfg.cg_delta_conv, false, &nan2,
+                        &zr2);
+      if (nan2) Warning("NaN or Inf occurred in the conjugate gradient algorithm of the gradient calculation");
+    }
+    GradColsArgs ga{};
+    ga.n = n; ga.m = m_; ga.t = t; ga.nbr = d_nbr_.get(); ga.Bv = d_Bv_.get(); ga.dBv = d_dBv_.get();
+    ga.Dinv = d_Dinv_.get(); ga.dD = d_dD_.get(); ga.W = d_W_.get();
+    ga.daux = gauss ? -1. / aux : 0.;   // d information / dlog(aux) (likelihoods.h:10967-10976)
+    ga.U = d_U_.get(); ga.P = d_P_.get();
+    DevBuf<double>& cols = d_out_;
+    launch_grad_cols(ga, d_partials_.get(), cols.get(), s_);
+    std::vector<double> z((size_t)kGradCols * t);
+    HIP_CHECK(hipMemcpyAsync(z.data(), cols.get(), sizeof(double) * z.size(), hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipStreamSynchronize(s_));
+    ScalarArgs sg = sa;
+    sg.dBv = d_dBv_.get();
+    sg.dD = d_dD_.get();
+    sg.vS = gauss ? nullptr : d_vS_.get();
+    Scalars(sg, sc);
+    auto mean = [t](const double* v) {
+      double s = 0.;
+      for (int c = 0; c < t; ++c) s += v[c];
+      return s / t;
+    };
+    // marginal variance: SigmaI_deriv = -Sigma^-1 (:5036-5038, 12445-12458)
+    {
+      const double* z1 = z.data();
+      const double* zP = z.data() + t;
+      const double tr1 = mean(z1), trP = mean(zP);
+      const double trD = -sc[kSqTrVar];
+      const double c = optimal_c(z1, zP, t, tr1, trP);
+      const double dld = tr1 + n + c * trD - c * trP;
+      double g = 0.5 * (-sc[kSqQuad] + dld);
+      if (!gauss) g += sc[kSqImpVar];   // - vS^T (-Sigma^-1 m)
+      res.grad.push_back(g);
+    }
+    // range (:5040-5063, 12449-12465)
+    {
+      const double* z1 = z.data() + 2 * t;
+      const double* zP = z.data() + 3 * t;
+      const double tr1 = mean(z1), trP = mean(zP);
+      const double trD = -sc[kSqTrRng];
+      const double c = optimal_c(z1, zP, t, tr1, trP);
+      const double dld = tr1 + sc[kSqDinvDD] + c * trD - c * trP;
+      double g = 0.5 * (2. * sc[kSqDQuadRng] - sc[kSqDDQuad] + dld);
+      if (!gauss) g -= sc[kSqImpRng];
+      res.grad.push_back(g);
+    }
+    // gaussian error variance on the log scale (:5166-5200, 10586-10597, 12520-12546)
+    if (gauss && want_aux_grad) {
+      const double* z1 = z.data() + 4 * t;
+      const double* zP = z.data() + 5 * t;
+      const double tr1 = mean(z1), trP = mean(zP);
+      const double trD = sc[kSqTrDw] * (-1. / aux);
+      const double c = optimal_c(z1, zP, t, tr1, trP);
+      const double dd = tr1 + c * trD - c * trP;
+      res.grad.push_back(sc[kSqRss] * (-0.5 / aux) + 0.5 * n + 0.5 * dd);
+    }
+  }
+  HIP_CHECK(hipEventRecord(ev1_, s_));
+  HIP_CHECK(hipEventSynchronize(ev1_));
+  float ms = 0.f;
+  HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_));
+  res.ms_total = ms;
+  return res;
+}
+
+}  // namespace gpb_amd

@@ -1,0 +1,108 @@
+// LatentVecchia: the latent-GP Vecchia likelihood with iterative methods on one GPU.
+//
+// Replaces, for one GP component in Vecchia order, the reference's
+//   FindModePostRandEffCalcMLLVecchia      likelihoods.h:2765-3076   (Newton + PCG + Armijo)
+//   CalcLogDetStochVecchia (vadu)          likelihoods.h:12069-12212 (SLQ log-determinant)
+//   CalcGradNegMargLikelihoodLaplaceApproxVecchia (iterative, vadu)
+//                                          likelihoods.h:4951-5206, 12225-12546
+//   CGVecchiaLaplaceVec / CGTridiagVecchiaLaplace / GenRandVecNormalParallel
+//                                          CG_utils.cpp:21-217, 930-1041
+// for likelihood "gaussian" under gp_approx = "vecchia_latent" (aux par = error variance)
+// and "bernoulli_logit". Every O(n) / O(n m) / O(n m t) step is a HIP kernel on the
+// model's stream; the host runs the iteration logic (stopping tests, line search) and
+// the O(t k^2) tridiagonal eigenproblems, exactly where the reference branches.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <memory>
+#include <vector>
+
+#include "common.h"
+#include "latent_kernels.h"
+
+namespace gpb_amd {
+
+struct IterativeConfig {
+  int cg_max_num_it = 1000;                // re_model_template.h:5364
+  int cg_max_num_it_tridiag = 1000;        // :5366
+  double cg_delta_conv = 1e-2;             // :5368
+  int num_rand_vec_trace = 50;             // :5376
+  int seed_rand_vec_trace = 1;             // :5380
+  bool reuse_rand_vec_trace = true;
+  double delta_conv_mode_finding = 1e-8;   // likelihoods.h:12723
+};
+
+struct LatentResult {
+  double nll = 0.;
+  std::vector<double> grad;   // [d/dlog sigma1^2, d/dlog phi, (gaussian, if requested) d/dlog aux]
+  int newton_its = 0, cg_its = 0, lanczos_steps = 0;
+  double logdet = 0.;         // log|Sigma W + I|
+  double ms_total = 0.;       // device time of the whole evaluation (HIP events)
+};
+
+class LatentVecchia {
+ public:
+  // d_X: coordinates (Vecchia order, row-major n x d) on the device, owned by the caller.
+  // nbr: host n x m neighbour table (row i holds min(i, m) entries).
+  LatentVecchia(int n, int d, int m, const double* d_X, const int* nbr, hipStream_t stream);
+  ~LatentVecchia();
+
+  void SetY(const double* y_vo);   // host, Vecchia order
+
+  // trafo = (sigma1^2, phi). aux = gaussian error variance (ignored for bernoulli_logit).
+  LatentResult Eval(int cov_type, int lik, const double* trafo, double aux, const IterativeConfig& cfg,
+                    bool want_grad, bool want_aux_grad);
+
+  int num_levels_fwd() const { return (int)fptr_.size() - 1; }
+  int num_levels_bwd() const { return (int)bptr_.size() - 1; }
+
+ private:
+  // Device work space of a t-column PCG (t = 1 for the Newton solves, t probes for SLQ).
+  struct Block {
+    int t = 0;
+    DevBuf<double> R, Z, H, V, G, Xt;     // n x t
+    DevBuf<double> small;                 // rz, rz_new, hv, rr, a, b: 6 x t
+    DevBuf<double> a_hist, b_hist;        // pmax x t (Lanczos coefficients)
+    double* rz() const { return small.get(); }
+    double* rz_new() const { return small.get() + t; }
+    double* hv() const { return small.get() + 2 * t; }
+    double* rr() const { return small.get() + 3 * t; }
+    double* a() const { return small.get() + 4 * t; }
+    double* b() const { return small.get() + 5 * t; }
+  };
+
+  void BuildStructure(const int* nbr);
+  Block& GetBlock(int which, int t, int pmax);
+  void EnsureProbes(const IterativeConfig& cfg);
+  void ApplyA(const double* H, double* V, double* G, int t);
+  void Precond(const double* R, double* Z, double* Xt, int t);
+  // PCG on t columns (CG_utils.cpp:21-108 for t = 1, :110-217 with tridiag). Returns the
+  // number of iterations; *nan on NaN/Inf residual; *zero_rhs for the zero-RHS shortcut.
+  int Pcg(Block& b, const double* RHS, double* U, bool init_zero, bool u_is_zero, int pmax, double delta,
+          bool tridiag, bool* nan, bool* zero_rhs);
+  void Scalars(const ScalarArgs& a, double* out);
+  double Dot1(const double* x, const double* y);   // single-vector dot, synchronous
+
+  int n_, d_, m_;
+  const double* d_X_;
+  hipStream_t s_;
+  SparseB sp_{};
+  DevBuf<int> d_nbr_, d_tptr_, d_trow_, d_tslot_, d_frows_, d_brows_;
+  std::vector<int> fptr_, bptr_;
+  DevBuf<double> d_y_, d_Bv_, d_dBv_, d_Dinv_, d_dD_, d_W_, d_dw_, d_sdw_, d_d1_;
+  DevBuf<double> d_mode_, d_mode_upd_, d_mode_new_, d_rhs_, d_dir_, d_Adir_, d_vS_, d_dmll_;
+  DevBuf<double> d_probes_, d_Zp_, d_U_, d_P_;   // n x t
+  int probes_t_ = 0;
+  uint64_t probe_run_id_ = 0;                    // cg_generator_counter_ (likelihoods.h:12800)
+  bool probes_saved_ = false;
+  DevBuf<double> d_partials_, d_out_;
+  double* h_out_ = nullptr;                      // pinned
+  std::vector<double> h_rr_;
+  std::unique_ptr<Block> blk1_, blkt_;
+  hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+  bool y_set_ = false;
+};
+
+}  // namespace gpb_amd

@@ -1,0 +1,220 @@
+// Latent Vecchia factor kernel for gfx950: B = I - A, D^-1 and their range derivatives
+// for the latent GP of non-Gaussian likelihoods / gp_approx = "vecchia_latent".
+//
+// Reference replaced: CalcCovFactorGradientVecchia (Vecchia_utils.cpp:1307-1632) with
+// gauss_likelihood = false: no nugget, D_ii starts at 0 (:1354-1356) and receives the
+// marginal variance (:1507), the between-neighbour diagonal is multiplied by
+// JITTER_MULT_VECCHIA (:1547), the marginal-variance derivative is not formed
+// (exclude_marg_var_grad: its SigmaI derivative is -Sigma^-1, likelihoods.h:5036-5038).
+//
+// Same lane-group mapping as the exact-Gaussian row kernel (vecchia_kernels.hip): K lanes
+// own one row, the k x k between-neighbour covariance C and dC/dlog(phi) live in packed
+// LDS triangles, and the solves are symmetric Gauss-Jordan eliminations with one LDS
+// broadcast per step. The factor needs two right-hand sides that are not known together
+// (dA = C^-1 (dc - dC a) needs a = C^-1 c first), so the elimination runs twice over the
+// unchanged packed C; this kernel runs once per likelihood evaluation.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "cov.h"
+#include "latent_kernels.h"
+
+namespace gpb_amd {
+namespace {
+
+constexpr int kDMax = 3;
+constexpr int kMaxBlocks = 4096;
+
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
+
+template <int K>
+__device__ __forceinline__ double group_sum(double v) {
+#pragma unroll
+  for (int off = K / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+template <int K>
+constexpr int block_threads() { return K == 64 ? 64 : 128; }
+
+template <int K>
+constexpr int group_lds_doubles() { return K * (K + 1) + kDMax * K + 2 * K; }
+
+__device__ __forceinline__ int packed(int r, int c) { return r * (r + 1) / 2 + c; }
+
+// Symmetric Gauss-Jordan on [C | rhs] with lane r holding row r of C (from the packed
+// triangle) and rhs_r; returns (C^-1 rhs)_r. Rows >= k are identity padding.
+template <int K>
+__device__ __forceinline__ double gj_solve(const double* Cp, int r, double* slot_c, double* slot_a, double rhs) {
+  double row[K];
+#pragma unroll
+  for (int c = 0; c < K; ++c) row[c] = (c <= r) ? Cp[packed(r, c)] : Cp[packed(c, r)];
+  double aug = rhs;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    compiler_fence();
+    slot_c[r] = row[j];
+    slot_a[r] = aug;
+    wave_lds_sync();
+    const double piv = slot_c[j];
+    double rinv = __builtin_amdgcn_rcp(piv);
+    rinv = fma(rinv, fma(-piv, rinv, 1.), rinv);
+    rinv = fma(rinv, fma(-piv, rinv, 1.), rinv);
+    const double f = (r == j) ? 0. : row[j] * rinv;
+    aug = fma(-f, slot_a[j], aug);
+#pragma unroll
+    for (int c = j + 1; c < K; ++c) row[c] = fma(-f, slot_c[c], row[c]);
+#pragma unroll
+    for (int c = j + 1; c < K; ++c) asm volatile("" : "+v"(row[c]));
+    asm volatile("" : "+v"(aug));
+  }
+  double mydiag = row[0];
+#pragma unroll
+  for (int c = 1; c < K; ++c) mydiag = (c == r) ? row[c] : mydiag;
+  compiler_fence();
+  return aug / mydiag;
+}
+
+template <int K, int COV>
+__global__ void __launch_bounds__(block_threads<K>()) latent_factor_kernel(LatentFactorArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  constexpr int BT = block_threads<K>();
+  constexpr int G = 64 / K;
+  constexpr int rows_per_block = (BT / 64) * G;
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int g = lane / K;
+  const int r = lane - g * K;
+  const int group_id = wave * G + g;
+  const int d = a.d;
+  const double var = a.var, phi = a.phi;
+  const double cdiag = var * a.jitter;
+  const bool want_grad = a.dBv != nullptr;
+
+  double* Cp = smem + group_id * group_lds_doubles<K>();
+  double* dCp = Cp + K * (K + 1) / 2;
+  double* nbx = dCp + K * (K + 1) / 2;
+  double* slot_c = nbx + K * kDMax;
+  double* slot_a = slot_c + K;
+
+  for (int base = blockIdx.x * rows_per_block; base < a.n; base += gridDim.x * rows_per_block) {
+    const int i = base + group_id;
+    const bool active = i < a.n;
+    const int k = active ? min(i, a.m) : 0;
+    const bool rv = r < k;
+    const int irow = active ? i : 0;
+
+    const int nb = rv ? a.nbr[(size_t)i * a.m + r] : 0;
+    double xi[kDMax], xr[kDMax];
+#pragma unroll
+    for (int q = 0; q < kDMax; ++q) {
+      xi[q] = (q < d) ? a.X[(size_t)irow * d + q] : 0.;
+      xr[q] = (q < d && rv) ? a.X[(size_t)nb * d + q] : 0.;
+    }
+    compiler_fence();
+#pragma unroll
+    for (int q = 0; q < kDMax; ++q) nbx[r * kDMax + q] = xr[q];
+
+    double cvec = 0., dcvec = 0.;
+    {
+      double s = 0.;
+#pragma unroll
+      for (int q = 0; q < kDMax; ++q) { const double t = xi[q] - xr[q]; s += t * t; }
+      double cv, dcv;
+      cov_dcov<COV>(sqrt(s), var, phi, cv, dcv);
+      cvec = rv ? cv : 0.;
+      dcvec = rv ? dcv : 0.;
+    }
+    Cp[packed(r, r)] = rv ? cdiag : 1.;
+    dCp[packed(r, r)] = 0.;
+    wave_lds_sync();
+    {
+      const int h = r & (K / 2 - 1);
+      const int qlo = (r >= K / 2) ? K / 2 : 0;
+      for (int q = qlo; q < qlo + K / 2 && q < K - 1; ++q) {
+        int rr, cc;
+        if (q < h) { rr = h; cc = q; } else { rr = K - 1 - h; cc = q - h; }
+        double cv = 0., dcv = 0.;
+        if (rr < k) {
+          double s = 0.;
+#pragma unroll
+          for (int qq = 0; qq < kDMax; ++qq) {
+            const double t = nbx[rr * kDMax + qq] - nbx[cc * kDMax + qq];
+            s += t * t;
+          }
+          cov_dcov<COV>(sqrt(s), var, phi, cv, dcv);
+        }
+        Cp[packed(rr, cc)] = cv;
+        dCp[packed(rr, cc)] = dcv;
+      }
+    }
+    wave_lds_sync();
+
+    const double av_r = gj_solve<K>(Cp, r, slot_c, slot_a, cvec);   // a = C^-1 c
+    const double ac = group_sum<K>(av_r * cvec);
+    if (active && r < a.m) a.Bv[(size_t)i * a.m + r] = rv ? -av_r : 0.;
+    if (active && r == 0) a.Dinv[i] = 1. / (var - ac);             // Vecchia_utils.cpp:1507, 1562, 1615
+
+    if (want_grad) {
+      // t = dC a (dC diagonal is 0), then w = C^-1 (dc - t) = dA^T (:1573-1574)
+      slot_c[r] = av_r;
+      wave_lds_sync();
+      double t = 0.;
+      for (int c = 0; c < k; ++c) {
+        const double dcrc = (c < r) ? dCp[packed(r, c)] : dCp[packed(c, r)];
+        t = fma(dcrc, slot_c[c], t);
+      }
+      t = rv ? t : 0.;
+      const double dca = group_sum<K>(dcvec * av_r);
+      const double ta = group_sum<K>(t * av_r);
+      const double w_r = gj_solve<K>(Cp, r, slot_c, slot_a, dcvec - t);
+      if (active && r < a.m) a.dBv[(size_t)i * a.m + r] = rv ? -w_r : 0.;
+      if (active && r == 0) a.dD[i] = -(2. * dca - ta);               // :1583 (range: overwrite)
+    }
+    compiler_fence();
+  }
+}
+
+int lanes_for_m(int m) {
+  if (m <= 16) return 16;
+  if (m <= 32) return 32;
+  if (m <= 64) return 64;
+  return 0;
+}
+
+template <int K, int COV>
+void launch_k(const LatentFactorArgs& a, hipStream_t s) {
+  constexpr int rpb = (block_threads<K>() / 64) * (64 / K);
+  int blocks = (a.n + rpb - 1) / rpb;
+  if (blocks > kMaxBlocks) blocks = kMaxBlocks;
+  const size_t lds = (size_t)rpb * group_lds_doubles<K>() * sizeof(double);
+  hipLaunchKernelGGL((latent_factor_kernel<K, COV>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
+  HIP_CHECK(hipGetLastError());
+}
+
+template <int K>
+void launch_cov(int cov, const LatentFactorArgs& a, hipStream_t s) {
+  switch (cov) {
+    case kMatern05: launch_k<K, kMatern05>(a, s); break;
+    case kMatern15: launch_k<K, kMatern15>(a, s); break;
+    case kMatern25: launch_k<K, kMatern25>(a, s); break;
+    case kGaussian: launch_k<K, kGaussian>(a, s); break;
+    default: Fatal("unsupported covariance type %d", cov);
+  }
+}
+
+}  // namespace
+
+void launch_latent_factor(int cov_type, const LatentFactorArgs& a, hipStream_t s) {
+  if (a.d < 1 || a.d > kDMax) Fatal("GPU Vecchia kernel supports 1 <= dim_gp_coords <= %d, got %d", kDMax, a.d);
+  if (a.n <= 0) return;
+  switch (lanes_for_m(a.m)) {
+    case 16: launch_cov<16>(cov_type, a, s); break;
+    case 32: launch_cov<32>(cov_type, a, s); break;
+    case 64: launch_cov<64>(cov_type, a, s); break;
+    default: Fatal("num_neighbors = %d > 64 is not supported by the GPU Vecchia kernel", a.m);
+  }
+}
+
+}  // namespace gpb_amd

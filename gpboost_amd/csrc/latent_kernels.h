@@ -1,0 +1,156 @@
+// Launchers for the latent-Vecchia iterative path (latent_factor.hip, sparse_kernels.hip).
+//
+// Data layout in HBM (all in Vecchia order):
+//   nbr    int32 n x m        neighbour j of row i at nbr[i*m + r], r < k_i = min(i, m)
+//   Bv     fp64  n x m        B(i, nbr[i*m+r]) = -A_i[r]; B has a unit diagonal (implicit)
+//   dBv    fp64  n x m        dB / dlog(phi), same sparsity (zero diagonal)
+//   Dinv, dD fp64 n           D^-1 and dD / dlog(phi)
+//   tptr/trow/tslot           transposed lists for B^T: column j -> entries e in
+//                             [tptr[j], tptr[j+1]) with row trow[e] and value slot tslot[e]
+//                             (= trow*m + r), rows ascending (deterministic sums)
+//   blocks of t vectors       row-major n x t ("probe-interleaved"): X[i*t + c], so one
+//                             neighbour gather reads t contiguous doubles
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+namespace gpb_amd {
+
+struct LatentFactorArgs {
+  const double* X;   // coords row-major n x d (Vecchia order)
+  const int* nbr;
+  int n, d, m;
+  double var, phi;   // sigma1^2, range transform
+  double jitter;     // between-neighbour diagonal multiplier (JITTER_MULT_VECCHIA)
+  double* Bv;
+  double* dBv;       // nullable (no gradient)
+  double* Dinv;
+  double* dD;        // nullable
+};
+void launch_latent_factor(int cov_type, const LatentFactorArgs& a, hipStream_t s);
+
+struct SparseB {
+  int n, m;
+  const int* nbr;
+  const int* tptr;
+  const int* trow;
+  const int* tslot;
+};
+
+// Y = diag(scale) (unit*X + V X)   with V = vals on the B pattern (rows list optional)
+void launch_b_apply(const SparseB& B, const double* vals, bool unit, const double* X, int t, const double* scale,
+                    double* Y, hipStream_t s);
+// Y = unit*pre.*X + V^T (pre.*X) + W.*H  (pre, W/H nullable)
+void launch_bt_apply(const SparseB& B, const double* vals, bool unit, const double* X, int t, const double* pre,
+                     const double* W, const double* H, double* Y, hipStream_t s);
+// One level of the unit-upper solve B^T Y = R (rows of the level listed in rows[0..cnt)).
+void launch_trsv_bt_level(const SparseB& B, const double* Bv, const int* rows, int cnt, const double* R, double* Y,
+                          int t, hipStream_t s);
+// One level of the lower solve (diag(dw) B) Z = X.
+void launch_trsv_b_level(const SparseB& B, const double* Bv, const double* dw, const int* rows, int cnt,
+                         const double* X, double* Z, int t, hipStream_t s);
+
+// Per-column dot products: out[q*t + c] = sum_i A_q[i,c] * B_q[i,c], q < np (np <= 3).
+// Deterministic two-pass reduction through `partials` (>= kMaxRedBlocks * np * t doubles).
+constexpr int kMaxRedBlocks = 512;
+void launch_coldots(int n, int t, int np, const double* const* A, const double* const* Bm, double* partials,
+                    double* out, hipStream_t s);
+// U += a .* H ; R -= a .* V ; rr[c] = sum_i R[i,c]^2 (per-column a from device memory)
+void launch_cg_update(int n, int t, const double* a, const double* H, const double* V, double* U, double* R,
+                      double* partials, double* rr, hipStream_t s);
+// H = Z + b .* H
+void launch_h_update(int n, int t, const double* b, const double* Z, double* H, hipStream_t s);
+// a = rz / hv (hist[it*t + c] = a)  |  b = rz_new / rz, rz = rz_new (hist[it*t + c] = b)
+void launch_cg_alpha(int t, const double* rz, const double* hv, double* a, double* hist, hipStream_t s);
+void launch_cg_beta(int t, const double* rz_new, double* rz, double* b, double* hist, hipStream_t s);
+// Y = X (n x t copy)
+void launch_copy(size_t count, const double* X, double* Y, hipStream_t s);
+// Z = alpha X + beta Y (elementwise, count entries; Z may alias X or Y)
+void launch_axpby(size_t count, double alpha, const double* X, double beta, const double* Y, double* Z,
+                  hipStream_t s);
+
+// ---- likelihood-specific elementwise and reductions
+enum LatentLik : int { kLikGaussian = 0, kLikBernoulliLogit = 1 };
+
+struct NewtonPrepArgs {
+  int n, lik;
+  double aux;           // gaussian error variance
+  const double* y;
+  const double* loc;    // mode (+ offset)
+  const double* mode;
+  const double* Dinv;
+  double* d1;           // first derivative of the log-likelihood
+  double* W;            // information (read; rewritten when W_update)
+  int W_update;
+  double* rhs;          // W*mode + d1 (nullable)
+  double* dw;           // D^-1 + W (nullable)
+  double* sdw;          // sqrt(dw) (nullable)
+};
+void launch_newton_prep(const NewtonPrepArgs& a, hipStream_t s);
+
+// Scalar row sums (one thread per row), fixed order -> out[kLatentScalars].
+enum LatentScalar : int {
+  kSqQuad = 0,     // (Bm)^T D^-1 (Bm)
+  kSqLogLik,       // sum log p(y | loc)
+  kSqLogDinv,      // sum log D^-1
+  kSqLogDw,        // sum log(D^-1 + W)
+  kSqRss,          // sum (y - loc)^2 (gaussian)
+  kSqDQuadRng,     // (dB m)^T D^-1 (Bm)
+  kSqDDQuad,       // (Bm)^T D^-1 dD D^-1 (Bm)
+  kSqTrVar,        // sum dw^-1 D^-1
+  kSqTrRng,        // sum dw^-1 D^-2 dD
+  kSqDinvDD,       // sum D^-1 dD
+  kSqTrDw,         // sum dw^-1  (aux trace, times dW/dlog aux)
+  kSqImpVar,       // (B vS)^T D^-1 (Bm)
+  kSqImpRng,       // (dB vS)^T D^-1 Bm + (B vS)^T D^-1 dB m - (B vS)^T D^-1 dD D^-1 Bm
+  kLatentScalars
+};
+struct ScalarArgs {
+  int n, m, lik;
+  double aux;
+  const int* nbr;
+  const double* Bv;
+  const double* dBv;    // nullable -> gradient terms skipped
+  const double* Dinv;
+  const double* dD;
+  const double* dw;     // nullable -> log/trace terms skipped
+  const double* y;
+  const double* mode;
+  const double* vS;     // nullable -> implicit terms skipped
+};
+void launch_latent_scalars(const ScalarArgs& a, double* partials, double* out, hipStream_t s);
+
+// Per-column stochastic-trace sums for the gradient (U = (Sigma^-1+W)^-1 Z, P = P^-1 Z):
+// out[q*t + c], q = 0 zt1_var, 1 ztP_var, 2 zt1_rng, 3 ztP_rng, 4 zt1_aux, 5 ztP_aux
+// (aux terms use the constant dW/dlog aux = daux).
+constexpr int kGradCols = 6;
+struct GradColsArgs {
+  int n, m, t;
+  const int* nbr;
+  const double* Bv;
+  const double* dBv;
+  const double* Dinv;
+  const double* dD;
+  const double* W;
+  double daux;
+  const double* U;
+  const double* P;
+};
+void launch_grad_cols(const GradColsArgs& a, double* partials, double* out, hipStream_t s);
+
+// Row-wise (per-observation) stochastic estimate of d log|Sigma W + I| / d mode with
+// per-row control variates (likelihoods.h:12320-12341, CG_utils.cpp:1026-1041):
+// dmll[i] = 0.5 * ( tr1_i + c_i * dW_i / dw_i - c_i * trP_i ).
+struct ModeDerivArgs {
+  int n, m, t, lik;
+  const int* nbr;
+  const double* Bv;
+  const double* dw;
+  const double* loc;
+  const double* U;
+  const double* P;
+  double* dmll;
+};
+void launch_mode_deriv(const ModeDerivArgs& a, hipStream_t s);
+
+}  // namespace gpb_amd

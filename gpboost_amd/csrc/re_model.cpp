@@ -8,6 +8,7 @@
 
 #include "cov.h"
 #include "kernels.h"
+#include "latent_kernels.h"
 #include "vecchia_host.h"
 
 namespace gpb_amd {
@@ -28,21 +29,45 @@ int parse_cov(const std::string& name, double shape) {
   Fatal("cov_fct '%s' is not supported by gpboost_amd (supported: exponential, matern, gaussian)", name.c_str());
 }
 
+// cov_fcts.h:438-460: range rho -> phi on the transformed scale
+double range_trafo(int cov_type, double rho) {
+  switch (cov_type) {
+    case kMatern05: return 1. / rho;
+    case kMatern15: return std::sqrt(3.) / rho;
+    case kMatern25: return std::sqrt(5.) / rho;
+    default: return 1. / (rho * rho);
+  }
+}
+
 }  // namespace
 
 REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : cfg_(cfg) {
   if (cfg_.n <= 0) Fatal("num_data must be > 0");
   if (cfg_.d <= 0 || cfg_.d > 3) Fatal("dim_gp_coords = %d not supported (1..3)", cfg_.d);
   cfg_.cov_type = parse_cov(cfg_.cov_fct, cfg_.shape);
-  if (cfg_.likelihood != "gaussian")
-    Fatal("likelihood '%s' is not supported by gpboost_amd in this build (supported: gaussian)", cfg_.likelihood.c_str());
-  if (cfg_.gp_approx == "vecchia") {
+  // likelihood and approximation (re_model_template.h:207-211, 563; likelihoods.h:240-257)
+  if (cfg_.likelihood == "gaussian") cfg_.lik = kLikGaussian;
+  else if (cfg_.likelihood == "bernoulli_logit") cfg_.lik = kLikBernoulliLogit;
+  else Fatal("likelihood '%s' is not supported by gpboost_amd (supported: gaussian, bernoulli_logit)", cfg_.likelihood.c_str());
+  if (cfg_.gp_approx == "vecchia_latent") {
     vecchia_ = true;
-  } else if (cfg_.gp_approx != "none") {
-    Fatal("gp_approx '%s' is not supported by gpboost_amd (supported: none, vecchia)", cfg_.gp_approx.c_str());
+    cfg_.latent = true;
+  } else if (cfg_.gp_approx == "vecchia") {
+    vecchia_ = true;
+    cfg_.latent = cfg_.lik != kLikGaussian;
+  } else if (cfg_.gp_approx == "none") {
+    if (cfg_.lik != kLikGaussian)
+      Fatal("likelihood '%s' requires gp_approx = 'vecchia' in gpboost_amd (dense Laplace is out of scope)", cfg_.likelihood.c_str());
+  } else {
+    Fatal("gp_approx '%s' is not supported by gpboost_amd (supported: none, vecchia, vecchia_latent)", cfg_.gp_approx.c_str());
   }
-  if (cfg_.matrix_inversion_method != "cholesky")
-    Fatal("matrix_inversion_method '%s' is not supported for likelihood 'gaussian' in this build", cfg_.matrix_inversion_method.c_str());
+  std::string& mim = cfg_.matrix_inversion_method;
+  if (mim == "default") mim = cfg_.latent ? "iterative" : "cholesky";
+  if (cfg_.latent && mim != "iterative")
+    Fatal("matrix_inversion_method '%s' is not supported for latent Vecchia models in gpboost_amd (supported: iterative)", mim.c_str());
+  if (!cfg_.latent && mim != "cholesky")
+    Fatal("matrix_inversion_method '%s' is not supported for likelihood 'gaussian' in gpboost_amd (supported: cholesky)", mim.c_str());
+  if (cfg_.latent && cfg_.lik == kLikGaussian) aux_pars_ = {1.};   // likelihoods.h:241 (error_variance)
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
     Fatal("no HIP device visible: gpboost_amd has no CPU fallback");
@@ -93,7 +118,18 @@ void REModelAMD::UseDevice() const { HIP_CHECK(hipSetDevice(device_)); }
 void REModelAMD::EnsureStructure() {
   if (vecchia_ && !structure_built_) {
     BuildVecchiaStructure();
+    if (cfg_.latent) {
+      latent_.reset(new LatentVecchia(cfg_.n, cfg_.d, cfg_.num_neighbors, d_X_.get(), nbr_.data(), stream_));
+      if (y_set_) latent_->SetY(y_vo_.data());
+    }
     structure_built_ = true;
+  }
+}
+
+void REModelAMD::SetAuxPars(const double* aux) {
+  for (size_t k = 0; k < aux_pars_.size(); ++k) {
+    if (!(aux[k] > 0.)) Fatal("aux_pars must be > 0");
+    aux_pars_[k] = aux[k];
   }
 }
 
@@ -101,6 +137,7 @@ REModelAMD::~REModelAMD() {
   (void)hipSetDevice(device_);
   if (stream_) (void)hipStreamSynchronize(stream_);
   dense_.reset();
+  latent_.reset();
   if (comm_) ncclCommDestroy(comm_);
   if (h_sums_) (void)hipHostFree(h_sums_);
   for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
@@ -127,6 +164,7 @@ void REModelAMD::SetDistributed(int rank, int world, const ncclUniqueId& id) {
   rank_ = rank;
   world_ = world;
   if (!vecchia_ && world > 1) Fatal("the dense (gp_approx='none') path runs as replicas only; SetDistributed needs gp_approx='vecchia'");
+  if (cfg_.latent && world > 1) Fatal("the latent Vecchia (iterative) path runs as replicas only in this build");
   if (comm_) { ncclCommDestroy(comm_); comm_ = nullptr; }
   if (world > 1) {
     ncclResult_t r = ncclCommInitRank(&comm_, world, id, rank);
@@ -146,12 +184,7 @@ void REModelAMD::TransformCovPars(const double* orig, double* trafo) const {
   if (!(orig[0] > 0. && orig[1] > 0. && orig[2] > 0.)) Fatal("covariance parameters must be > 0");
   trafo[0] = orig[0];
   trafo[1] = orig[1] / orig[0];
-  switch (cfg_.cov_type) {
-    case kMatern05: trafo[2] = 1. / orig[2]; break;
-    case kMatern15: trafo[2] = std::sqrt(3.) / orig[2]; break;
-    case kMatern25: trafo[2] = std::sqrt(5.) / orig[2]; break;
-    default: trafo[2] = 1. / (orig[2] * orig[2]); break;
-  }
+  trafo[2] = range_trafo(cfg_.cov_type, orig[2]);
 }
 
 void REModelAMD::SetY(const double* y) {
@@ -161,6 +194,14 @@ void REModelAMD::SetY(const double* y) {
   std::vector<double> yv(n);
   if (vecchia_) for (int i = 0; i < n; ++i) yv[i] = y[perm_[i]];
   else std::copy(y, y + n, yv.begin());
+  if (cfg_.latent) {
+    if (cfg_.lik == kLikBernoulliLogit) {   // likelihoods.h CheckY: binary labels
+      for (int i = 0; i < n; ++i)
+        if (yv[i] != 0. && yv[i] != 1.) Fatal("Response variable (label) data needs to be 0 or 1 for likelihood = 'bernoulli_logit' ");
+    }
+    y_vo_ = yv;
+    if (latent_) latent_->SetY(y_vo_.data());
+  }
   d_y_.alloc(n);
   HIP_CHECK(hipMemcpyAsync(d_y_.get(), yv.data(), sizeof(double) * n, hipMemcpyHostToDevice, stream_));
   HIP_CHECK(hipStreamSynchronize(stream_));
@@ -209,6 +250,7 @@ void REModelAMD::EvalVecchia(const double* trafo, double* sums) {
 
 void REModelAMD::EvalVecchiaPartials(const double* cov_pars_orig, int r0, int r1, double* sums) {
   if (!vecchia_) Fatal("model does not use the Vecchia approximation");
+  if (cfg_.latent) Fatal("row-range partial sums exist only for the exact Gaussian Vecchia likelihood");
   if (!y_set_) Fatal("response variable y has not been set");
   if (r0 < row_begin_ || r1 > row_end_ || r0 > r1) Fatal("row range [%d, %d) outside this model's rows [%d, %d)", r0, r1, row_begin_, row_end_);
   UseDevice();
@@ -222,10 +264,36 @@ void REModelAMD::EvalDense(const double* trafo, bool want_grad, double* sums) {
   dense_->Eval(cfg_.cov_type, trafo[1], trafo[2], d_y_.get(), want_grad, sums, last_kernel_ms_);
 }
 
+EvalResult REModelAMD::EvalLatent(const double* cov_pars_orig, bool want_grad) {
+  if (!(cov_pars_orig[0] > 0. && cov_pars_orig[1] > 0.)) Fatal("covariance parameters must be > 0");
+  // TransformCovPars for non-Gaussian likelihoods: no division by a nugget (cov_fcts.h:438-460)
+  const double trafo[2] = {cov_pars_orig[0], range_trafo(cfg_.cov_type, cov_pars_orig[1])};
+  const double aux = aux_pars_.empty() ? 1. : aux_pars_[0];
+  LatentResult r = latent_->Eval(cfg_.cov_type, cfg_.lik, trafo, aux, iter, want_grad,
+                                 estimate_aux_pars && !aux_pars_.empty());
+  if (!std::isfinite(r.nll)) Fatal("NaN or Inf occurred in the approximate negative marginal log-likelihood");
+  EvalResult res;
+  res.nll = r.nll;
+  res.grad = r.grad;
+  res.sigma2 = aux;
+  last_iter_info_[0] = r.newton_its;
+  last_iter_info_[1] = r.cg_its;
+  last_iter_info_[2] = r.lanczos_steps;
+  last_iter_info_[3] = r.logdet;
+  last_kernel_ms_[0] = last_kernel_ms_[1] = r.ms_total;
+  last_nll_ = res.nll;
+  last_cov_pars_.assign(cov_pars_orig, cov_pars_orig + 2);
+  return res;
+}
+
 EvalResult REModelAMD::Eval(const double* cov_pars_orig, bool want_grad, int profile) {
   if (!y_set_) Fatal("response variable y has not been set");
   UseDevice();
   EnsureStructure();
+  if (cfg_.latent) {
+    if (profile) Fatal("profile_sigma2 is only defined for the Gaussian likelihood without 'vecchia_latent'");
+    return EvalLatent(cov_pars_orig, want_grad);
+  }
   double trafo[3];
   TransformCovPars(cov_pars_orig, trafo);
   double sums[kVecchiaSums];
@@ -251,8 +319,32 @@ void REModelAMD::GetVecchiaStructure(int* perm, int* nbr) const {
   std::copy(nbr_.begin(), nbr_.end(), nbr);
 }
 
+void REModelAMD::GetLatentVecchiaFactor(const double* cov_pars_orig, double* Dinv, double* Bvals, double* dD,
+                                        double* dBvals) {
+  if (!cfg_.latent) Fatal("model does not use a latent Vecchia approximation");
+  if (world_ > 1) Fatal("GetLatentVecchiaFactor is only available on single-rank models");
+  if (!(cov_pars_orig[0] > 0. && cov_pars_orig[1] > 0.)) Fatal("covariance parameters must be > 0");
+  UseDevice();
+  EnsureStructure();
+  const int n = cfg_.n, m = cfg_.num_neighbors;
+  DevBuf<double> a(n), b((size_t)n * m), c(n), e((size_t)n * m);
+  LatentFactorArgs fa{};
+  fa.X = d_X_.get(); fa.nbr = d_nbr_.get(); fa.n = n; fa.d = cfg_.d; fa.m = m;
+  fa.var = cov_pars_orig[0];
+  fa.phi = range_trafo(cfg_.cov_type, cov_pars_orig[1]);
+  fa.jitter = 1. + 1e-10;
+  fa.Bv = b.get(); fa.dBv = e.get(); fa.Dinv = a.get(); fa.dD = c.get();
+  launch_latent_factor(cfg_.cov_type, fa, stream_);
+  HIP_CHECK(hipMemcpyAsync(Dinv, a.get(), sizeof(double) * n, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipMemcpyAsync(Bvals, b.get(), sizeof(double) * n * m, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipMemcpyAsync(dD, c.get(), sizeof(double) * n, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipMemcpyAsync(dBvals, e.get(), sizeof(double) * n * m, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
 void REModelAMD::GetVecchiaFactor(const double* cov_pars_orig, double* Dinv, double* Bvals) {
   if (!vecchia_) Fatal("model does not use the Vecchia approximation");
+  if (cfg_.latent) Fatal("latent Vecchia model: use GPB_GetLatentVecchiaFactor");
   if (world_ > 1) Fatal("GetVecchiaFactor is only available on single-rank models");
   UseDevice();
   EnsureStructure();

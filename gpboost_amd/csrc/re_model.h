@@ -17,6 +17,7 @@
 
 #include "common.h"
 #include "dense.h"
+#include "latent.h"
 
 namespace gpb_amd {
 
@@ -32,6 +33,9 @@ struct ModelConfig {
   std::string likelihood = "gaussian";
   std::string matrix_inversion_method = "cholesky";
   int seed = 0;
+  // derived
+  bool latent = false;     // latent GP + Laplace approximation (non-Gaussian or "vecchia_latent")
+  int lik = 0;             // LatentLik code when latent
 };
 
 struct EvalResult {
@@ -45,7 +49,11 @@ class REModelAMD {
   REModelAMD(const ModelConfig& cfg, const double* coords_colmajor);
   ~REModelAMD();
 
-  int num_cov_pars() const { return 3; }
+  int num_cov_pars() const { return cfg_.latent ? 2 : 3; }
+  int num_aux_pars() const { return (int)aux_pars_.size(); }
+  const std::vector<double>& aux_pars() const { return aux_pars_; }
+  std::string aux_par_name() const { return cfg_.latent && cfg_.lik == kLikGaussian ? "error_variance" : ""; }
+  void SetAuxPars(const double* aux);
   int device() const { return device_; }
   const ModelConfig& config() const { return cfg_; }
 
@@ -53,6 +61,7 @@ class REModelAMD {
   bool HasY() const { return y_set_; }
 
   // cov_pars on the original scale. profile: 0 -> include_error_var gradient, 1 -> L-BFGS unit.
+  // Latent models: gradient wrt log(cov_pars) (+ log(aux_pars) when estimate_aux_pars).
   EvalResult Eval(const double* cov_pars_orig, bool want_grad, int profile);
 
   void SetDistributed(int rank, int world, const ncclUniqueId& id);
@@ -62,16 +71,18 @@ class REModelAMD {
 
   void GetVecchiaStructure(int* perm, int* nbr) const;
   void GetVecchiaFactor(const double* cov_pars_orig, double* Dinv, double* Bvals);
+  // Latent factor with range derivatives (EXTENSION, latent models only).
+  void GetLatentVecchiaFactor(const double* cov_pars_orig, double* Dinv, double* Bvals, double* dD, double* dBvals);
+  // [newton iterations, mode-finding CG iterations, Lanczos steps, log|Sigma W + I|] of the last latent eval
+  void GetLastIterationInfo(double* out) const { for (int k = 0; k < 4; ++k) out[k] = last_iter_info_[k]; }
   void GetLastKernelTimes(double* ms) const { ms[0] = last_kernel_ms_[0]; ms[1] = last_kernel_ms_[1]; }
 
   double last_nll() const { return last_nll_; }
   const std::vector<double>& last_cov_pars() const { return last_cov_pars_; }
 
-  // optimizer settings kept for API parity (GPB_SetOptimConfig)
-  int cg_max_num_it = 1000;
-  double cg_delta_conv = 1e-2;
-  int num_rand_vec_trace = 50;
-  int seed_rand_vec_trace = 1;
+  // iterative-method settings (GPB_SetOptimConfig, re_model_template.h:686-823)
+  IterativeConfig iter;
+  bool estimate_aux_pars = true;   // InitializeDefaultSettings (re_model_template.h:6492-6499) for latent models
 
  private:
   void TransformCovPars(const double* orig, double* trafo) const;
@@ -82,6 +93,7 @@ class REModelAMD {
 
   void EnsureStructure();
   void UseDevice() const;
+  EvalResult EvalLatent(const double* cov_pars_orig, bool want_grad);
 
   ModelConfig cfg_;
   int device_ = 0;
@@ -101,6 +113,10 @@ class REModelAMD {
   double* h_sums_ = nullptr;  // pinned
 
   std::unique_ptr<DenseSolver> dense_;
+  std::unique_ptr<LatentVecchia> latent_;
+  std::vector<double> y_vo_;          // host copy (Vecchia order) for the latent solver
+  std::vector<double> aux_pars_;
+  double last_iter_info_[4] = {0., 0., 0., 0.};
 
   int rank_ = 0, world_ = 1;
   int row_begin_ = 0, row_end_ = 0;

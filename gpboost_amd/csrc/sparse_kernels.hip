@@ -1,0 +1,588 @@
+// Sparse Vecchia operators and block-CG vector kernels for the iterative path (gfx950).
+//
+// Reference replaced (CG_utils.cpp:21-217, likelihoods.h:2765-3076, 4951-5206,
+// 12069-12546): the row-major Eigen SpMVs B*h, B^T*(D^-1 B h), the two triangular solves
+// of the VADU preconditioner, the block-CG column updates and the column / row
+// reductions of the stochastic traces.
+//
+// Thread mapping for blocks of t vectors stored row-major n x t: a group of T lanes
+// (T = next power of two >= t, at most 64) owns one row; lane c owns column
+// c + 64*blockIdx.y. A neighbour gather is therefore one contiguous t*8-byte read, and
+// the per-row sparse pattern (nbr / values) is a same-address broadcast across the group.
+// All reductions are two-pass with fixed orders, so results are bitwise reproducible.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+
+#include "common.h"
+#include "latent_kernels.h"
+
+namespace gpb_amd {
+namespace {
+
+constexpr int kBT = 256;          // threads per block
+constexpr int kMaxGridX = 4096;
+
+struct Lanes {
+  int shift;  // log2(T)
+  int T;
+  int rpb;    // rows per block
+  int gy;     // grid.y (column chunks of 64)
+};
+
+Lanes lanes_for(int t) {
+  Lanes L;
+  int T = 1, sh = 0;
+  const int tc = t < 64 ? t : 64;
+  while (T < tc) { T <<= 1; ++sh; }
+  L.shift = sh;
+  L.T = T;
+  L.rpb = kBT >> sh;
+  L.gy = (t + 63) / 64;
+  return L;
+}
+
+int grid_x(int rows, int rpb, int cap = kMaxGridX) {
+  int g = (rows + rpb - 1) / rpb;
+  if (g > cap) g = cap;
+  return g < 1 ? 1 : g;
+}
+
+// ------------------------------------------------------------------ SpMV
+__global__ void __launch_bounds__(kBT) b_apply_kernel(int n, int m, const int* __restrict__ nbr,
+                                                      const double* __restrict__ vals, int unit,
+                                                      const double* __restrict__ X, int t, int shift,
+                                                      const double* __restrict__ scale, double* __restrict__ Y) {
+  const int T = 1 << shift;
+  const int c = (threadIdx.x & (T - 1)) + blockIdx.y * 64;
+  const int rpb = kBT >> shift;
+  if (c >= t) return;
+  for (int i = blockIdx.x * rpb + (threadIdx.x >> shift); i < n; i += gridDim.x * rpb) {
+    const int k = i < m ? i : m;
+    const int* nb = nbr + (size_t)i * m;
+    const double* v = vals + (size_t)i * m;
+    double s = unit ? X[(size_t)i * t + c] : 0.;
+#pragma unroll 4
+    for (int r = 0; r < k; ++r) s = fma(v[r], X[(size_t)nb[r] * t + c], s);
+    if (scale) s *= scale[i];
+    Y[(size_t)i * t + c] = s;
+  }
+}
+
+__global__ void __launch_bounds__(kBT) bt_apply_kernel(int n, const int* __restrict__ tptr,
+                                                       const int* __restrict__ trow, const int* __restrict__ tslot,
+                                                       const double* __restrict__ vals, int unit,
+                                                       const double* __restrict__ X, int t, int shift,
+                                                       const double* __restrict__ pre, const double* __restrict__ W,
+                                                       const double* __restrict__ H, double* __restrict__ Y) {
+  const int T = 1 << shift;
+  const int c = (threadIdx.x & (T - 1)) + blockIdx.y * 64;
+  const int rpb = kBT >> shift;
+  if (c >= t) return;
+  for (int j = blockIdx.x * rpb + (threadIdx.x >> shift); j < n; j += gridDim.x * rpb) {
+    double s = 0.;
+    if (unit) s = pre ? pre[j] * X[(size_t)j * t + c] : X[(size_t)j * t + c];
+    const int e1 = tptr[j + 1];
+#pragma unroll 4
+    for (int e = tptr[j]; e < e1; ++e) {
+      const int i = trow[e];
+      const double w = pre ? vals[tslot[e]] * pre[i] : vals[tslot[e]];
+      s = fma(w, X[(size_t)i * t + c], s);
+    }
+    if (W) s = fma(W[j], H[(size_t)j * t + c], s);
+    Y[(size_t)j * t + c] = s;
+  }
+}
+
+// ------------------------------------------------------------------ level-scheduled solves
+// B^T Y = R (unit upper): y_j = r_j - sum_{i: j in nbr(i)} B(i,j) y_i, rows of one level.
+__global__ void __launch_bounds__(kBT) trsv_bt_level_kernel(const int* __restrict__ rows, int cnt,
+                                                            const int* __restrict__ tptr,
+                                                            const int* __restrict__ trow,
+                                                            const int* __restrict__ tslot,
+                                                            const double* __restrict__ Bv,
+                                                            const double* __restrict__ R, double* __restrict__ Y,
+                                                            int t, int shift) {
+  const int T = 1 << shift;
+  const int c = (threadIdx.x & (T - 1)) + blockIdx.y * 64;
+  const int rpb = kBT >> shift;
+  const int task = blockIdx.x * rpb + (threadIdx.x >> shift);
+  if (c >= t || task >= cnt) return;
+  const int j = rows[task];
+  double s = R[(size_t)j * t + c];
+  const int e1 = tptr[j + 1];
+#pragma unroll 4
+  for (int e = tptr[j]; e < e1; ++e) s = fma(-Bv[tslot[e]], Y[(size_t)trow[e] * t + c], s);
+  Y[(size_t)j * t + c] = s;
+}
+
+// (diag(dw) B) Z = X (lower): z_i = x_i / dw_i - sum_r B(i, nbr_r) z_nbr_r.
+__global__ void __launch_bounds__(kBT) trsv_b_level_kernel(const int* __restrict__ rows, int cnt, int m,
+                                                           const int* __restrict__ nbr,
+                                                           const double* __restrict__ Bv,
+                                                           const double* __restrict__ dw,
+                                                           const double* __restrict__ X, double* __restrict__ Z,
+                                                           int t, int shift) {
+  const int T = 1 << shift;
+  const int c = (threadIdx.x & (T - 1)) + blockIdx.y * 64;
+  const int rpb = kBT >> shift;
+  const int task = blockIdx.x * rpb + (threadIdx.x >> shift);
+  if (c >= t || task >= cnt) return;
+  const int i = rows[task];
+  const int k = i < m ? i : m;
+  const int* nb = nbr + (size_t)i * m;
+  const double* v = Bv + (size_t)i * m;
+  double s = X[(size_t)i * t + c] / dw[i];
+#pragma unroll 4
+  for (int r = 0; r < k; ++r) s = fma(-v[r], Z[(size_t)nb[r] * t + c], s);
+  Z[(size_t)i * t + c] = s;
+}
+
+// ------------------------------------------------------------------ column reductions
+// Block-level fixed-order tree over the row slots of one block; writes partials[blk][q*t+c].
+template <int NP>
+__device__ __forceinline__ void block_col_reduce(double (&acc)[NP], int shift, int c, int t, double* partials) {
+  __shared__ double red[NP][kBT];
+  const int rpb = kBT >> shift;
+  const int slot = threadIdx.x >> shift;
+#pragma unroll
+  for (int q = 0; q < NP; ++q) red[q][threadIdx.x] = acc[q];
+  __syncthreads();
+  for (int off = rpb >> 1; off > 0; off >>= 1) {
+    if (slot < off) {
+#pragma unroll
+      for (int q = 0; q < NP; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + (off << shift)];
+    }
+    __syncthreads();
+  }
+  if (slot == 0 && c < t) {
+#pragma unroll
+    for (int q = 0; q < NP; ++q) partials[(size_t)blockIdx.x * NP * t + (size_t)q * t + c] = red[q][threadIdx.x];
+  }
+}
+
+template <int NP>
+__global__ void __launch_bounds__(kBT) coldots_kernel(int n, int t, int shift, const double* A0, const double* B0,
+                                                      const double* A1, const double* B1, const double* A2,
+                                                      const double* B2, double* partials) {
+  const int T = 1 << shift;
+  const int c = (threadIdx.x & (T - 1)) + blockIdx.y * 64;
+  const int rpb = kBT >> shift;
+  double acc[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) acc[q] = 0.;
+  if (c < t) {
+    for (int i = blockIdx.x * rpb + (threadIdx.x >> shift); i < n; i += gridDim.x * rpb) {
+      const size_t o = (size_t)i * t + c;
+      acc[0] = fma(A0[o], B0[o], acc[0]);
+      if constexpr (NP > 1) acc[1] = fma(A1[o], B1[o], acc[1]);
+      if constexpr (NP > 2) acc[2] = fma(A2[o], B2[o], acc[2]);
+    }
+  }
+  block_col_reduce<NP>(acc, shift, c, t, partials);
+}
+
+// out[w] = sum over blocks of partials[b*width + w]; one block per output, fixed order.
+__global__ void __launch_bounds__(kBT) reduce_blocks_kernel(const double* __restrict__ partials, int nblocks,
+                                                            int width, double* __restrict__ out) {
+  __shared__ double red[kBT];
+  const int w = blockIdx.x;
+  double s = 0.;
+  for (int b = threadIdx.x; b < nblocks; b += kBT) s += partials[(size_t)b * width + w];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = kBT / 2; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[w] = red[0];
+}
+
+__global__ void __launch_bounds__(kBT) cg_update_kernel(int n, int t, int shift, const double* __restrict__ a,
+                                                        const double* __restrict__ H, const double* __restrict__ V,
+                                                        double* __restrict__ U, double* __restrict__ R,
+                                                        double* partials) {
+  const int T = 1 << shift;
+  const int c = (threadIdx.x & (T - 1)) + blockIdx.y * 64;
+  const int rpb = kBT >> shift;
+  double acc[1] = {0.};
+  if (c < t) {
+    const double ac = a[c];
+    for (int i = blockIdx.x * rpb + (threadIdx.x >> shift); i < n; i += gridDim.x * rpb) {
+      const size_t o = (size_t)i * t + c;
+      U[o] = fma(ac, H[o], U[o]);
+      const double r = fma(-ac, V[o], R[o]);
+      R[o] = r;
+      acc[0] = fma(r, r, acc[0]);
+    }
+  }
+  block_col_reduce<1>(acc, shift, c, t, partials);
+}
+
+__global__ void __launch_bounds__(kBT) h_update_kernel(size_t total, int t, const double* __restrict__ b,
+                                                       const double* __restrict__ Z, double* __restrict__ H) {
+  for (size_t o = (size_t)blockIdx.x * kBT + threadIdx.x; o < total; o += (size_t)gridDim.x * kBT) {
+    const int c = (int)(o % t);
+    H[o] = fma(b[c], H[o], Z[o]);
+  }
+}
+
+__global__ void copy_kernel(size_t total, const double* __restrict__ X, double* __restrict__ Y) {
+  for (size_t o = (size_t)blockIdx.x * kBT + threadIdx.x; o < total; o += (size_t)gridDim.x * kBT) Y[o] = X[o];
+}
+
+__global__ void axpby_kernel(size_t total, double alpha, const double* X, double beta, const double* Y, double* Z) {
+  for (size_t o = (size_t)blockIdx.x * kBT + threadIdx.x; o < total; o += (size_t)gridDim.x * kBT)
+    Z[o] = alpha * X[o] + beta * Y[o];
+}
+
+__global__ void cg_alpha_kernel(int t, const double* rz, const double* hv, double* a, double* hist) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= t) return;
+  const double v = rz[c] / hv[c];
+  a[c] = v;
+  if (hist) hist[c] = v;
+}
+
+__global__ void cg_beta_kernel(int t, const double* rz_new, double* rz, double* b, double* hist) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= t) return;
+  const double v = rz_new[c] / rz[c];
+  rz[c] = rz_new[c];
+  b[c] = v;
+  if (hist) hist[c] = v;
+}
+
+// ------------------------------------------------------------------ likelihoods
+// likelihoods.h: gaussian :8795, 9263, 9937; bernoulli_logit :8724, 9226, 9896, 10187;
+// sigmoid_stable / softplus DF_utils.h:37-60
+__device__ __forceinline__ double sigmoid_stable(double x) {
+  if (x >= 0.) {
+    const double e = exp(-x);
+    return 1. / (1. + e);
+  }
+  const double e = exp(x);
+  return e / (1. + e);
+}
+__device__ __forceinline__ double softplus(double x) { return log1p(exp(-fabs(x))) + fmax(x, 0.); }
+
+__device__ __forceinline__ double lik_loglik(int lik, double aux, double y, double l) {
+  if (lik == kLikGaussian) {
+    const double r = y - l;
+    return -r * r / 2. / aux - 0.91893853320467274178 - 0.5 * log(aux);   // M_LOGSQRT2PI
+  }
+  return y * l - softplus(l);
+}
+__device__ __forceinline__ double lik_d1(int lik, double aux, double y, double l) {
+  return lik == kLikGaussian ? (y - l) / aux : y - sigmoid_stable(l);
+}
+__device__ __forceinline__ double lik_info(int lik, double aux, double l) {
+  if (lik == kLikGaussian) return 1. / aux;
+  const double p = sigmoid_stable(l);
+  return p * (1. - p);
+}
+__device__ __forceinline__ double lik_dinfo(int lik, double l) {
+  if (lik == kLikGaussian) return 0.;
+  const double p = sigmoid_stable(l);
+  return -p * (1. - p) * (2. * p - 1.);
+}
+
+__global__ void __launch_bounds__(kBT) newton_prep_kernel(NewtonPrepArgs a) {
+  for (int i = blockIdx.x * kBT + threadIdx.x; i < a.n; i += gridDim.x * kBT) {
+    const double l = a.loc[i];
+    const double d1 = lik_d1(a.lik, a.aux, a.y[i], l);
+    a.d1[i] = d1;
+    // W is only refreshed when requested (information_changes_*); otherwise the stored W is used
+    const double w = a.W_update ? lik_info(a.lik, a.aux, l) : a.W[i];
+    if (a.W_update) a.W[i] = w;
+    if (a.rhs) a.rhs[i] = fma(w, a.mode[i], d1);
+    if (a.dw) {
+      const double dw = a.Dinv[i] + w;
+      a.dw[i] = dw;
+      if (a.sdw) a.sdw[i] = sqrt(dw);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kBT) latent_scalars_kernel(ScalarArgs a, double* partials) {
+  double acc[kLatentScalars];
+#pragma unroll
+  for (int q = 0; q < kLatentScalars; ++q) acc[q] = 0.;
+  for (int i = blockIdx.x * kBT + threadIdx.x; i < a.n; i += gridDim.x * kBT) {
+    const int k = i < a.m ? i : a.m;
+    const int* nb = a.nbr + (size_t)i * a.m;
+    const double* v = a.Bv + (size_t)i * a.m;
+    const double mi = a.mode[i];
+    double bm = mi, dbm = 0., bv = 0., dbv = 0.;
+    if (a.vS) bv = a.vS[i];
+    for (int r = 0; r < k; ++r) {
+      const int j = nb[r];
+      const double mj = a.mode[j];
+      bm = fma(v[r], mj, bm);
+      if (a.dBv) dbm = fma(a.dBv[(size_t)i * a.m + r], mj, dbm);
+      if (a.vS) {
+        const double sj = a.vS[j];
+        bv = fma(v[r], sj, bv);
+        if (a.dBv) dbv = fma(a.dBv[(size_t)i * a.m + r], sj, dbv);
+      }
+    }
+    const double Di = a.Dinv[i];
+    acc[kSqQuad] += bm * Di * bm;
+    acc[kSqLogLik] += lik_loglik(a.lik, a.aux, a.y[i], mi);
+    acc[kSqLogDinv] += log(Di);
+    const double r = a.y[i] - mi;
+    acc[kSqRss] += r * r;
+    if (a.dw) {
+      const double dwi = a.dw[i];
+      acc[kSqLogDw] += log(dwi);
+      acc[kSqTrVar] += Di / dwi;
+      acc[kSqTrDw] += 1. / dwi;
+      if (a.dD) acc[kSqTrRng] += Di * a.dD[i] * Di / dwi;
+    }
+    if (a.dBv) {
+      const double dDi = a.dD[i];
+      acc[kSqDQuadRng] += dbm * Di * bm;
+      acc[kSqDDQuad] += bm * Di * dDi * Di * bm;
+      acc[kSqDinvDD] += Di * dDi;
+      if (a.vS) {
+        acc[kSqImpVar] += bv * Di * bm;
+        acc[kSqImpRng] += dbv * Di * bm + bv * Di * dbm - bv * Di * dDi * Di * bm;
+      }
+    }
+  }
+  __shared__ double red[kLatentScalars][kBT];
+#pragma unroll
+  for (int q = 0; q < kLatentScalars; ++q) red[q][threadIdx.x] = acc[q];
+  __syncthreads();
+  for (int off = kBT / 2; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) {
+#pragma unroll
+      for (int q = 0; q < kLatentScalars; ++q) red[q][threadIdx.x] += red[q][threadIdx.x + off];
+    }
+    __syncthreads();
+  }
+  if ((int)threadIdx.x < kLatentScalars)
+    partials[(size_t)blockIdx.x * kLatentScalars + threadIdx.x] = red[threadIdx.x][0];
+}
+
+// Per-column trace sums for the gradient (likelihoods.h:12440-12465, 12520-12546).
+__global__ void __launch_bounds__(kBT) grad_cols_kernel(GradColsArgs a, int shift, double* partials) {
+  const int T = 1 << shift;
+  const int c = (threadIdx.x & (T - 1)) + blockIdx.y * 64;
+  const int rpb = kBT >> shift;
+  const int t = a.t;
+  double acc[kGradCols];
+#pragma unroll
+  for (int q = 0; q < kGradCols; ++q) acc[q] = 0.;
+  if (c < t) {
+    for (int i = blockIdx.x * rpb + (threadIdx.x >> shift); i < a.n; i += gridDim.x * rpb) {
+      const int k = i < a.m ? i : a.m;
+      const int* nb = a.nbr + (size_t)i * a.m;
+      const double* bv = a.Bv + (size_t)i * a.m;
+      const double* dbv = a.dBv + (size_t)i * a.m;
+      const size_t o = (size_t)i * t + c;
+      const double ui = a.U[o], pi = a.P[o];
+      double bu = ui, dbu = 0., bp = pi, dbp = 0.;
+#pragma unroll 2
+      for (int r = 0; r < k; ++r) {
+        const size_t oj = (size_t)nb[r] * t + c;
+        const double uj = a.U[oj], pj = a.P[oj];
+        bu = fma(bv[r], uj, bu);
+        bp = fma(bv[r], pj, bp);
+        dbu = fma(dbv[r], uj, dbu);
+        dbp = fma(dbv[r], pj, dbp);
+      }
+      const double Di = a.Dinv[i], dDi = a.dD[i], wi = a.W[i];
+      acc[0] -= Di * bu * bp;
+      acc[1] -= Di * bp * bp;
+      acc[2] += Di * (dbu * bp + bu * dbp - Di * dDi * bu * bp);
+      acc[3] += Di * (2. * dbp * bp - Di * dDi * bp * bp) + 2. * wi * bp * dbp;
+      acc[4] += ui * a.daux * pi;
+      acc[5] += bp * a.daux * bp;
+    }
+  }
+  block_col_reduce<kGradCols>(acc, shift, c, t, partials);
+}
+
+// Row-wise stochastic d log|Sigma W + I| / d mode (vadu branch, likelihoods.h:12320-12341).
+__global__ void __launch_bounds__(kBT) mode_deriv_kernel(ModeDerivArgs a, int shift) {
+  const int T = 1 << shift;
+  const int lane = threadIdx.x & (T - 1);
+  const int rpb = kBT >> shift;
+  const int t = a.t;
+  for (int i = blockIdx.x * rpb + (threadIdx.x >> shift); i < a.n; i += gridDim.x * rpb) {
+    const int k = i < a.m ? i : a.m;
+    const int* nb = a.nbr + (size_t)i * a.m;
+    const double* bv = a.Bv + (size_t)i * a.m;
+    const double dWi = lik_dinfo(a.lik, a.loc[i]);
+    // pass 1: row means of z1 = U dW P and zP = (BP)^2 dW over the t probes
+    double s1 = 0., sP = 0.;
+    for (int c = lane; c < t; c += T) {
+      const size_t o = (size_t)i * t + c;
+      double bp = a.P[o];
+      for (int r = 0; r < k; ++r) bp = fma(bv[r], a.P[(size_t)nb[r] * t + c], bp);
+      s1 += a.U[o] * dWi * a.P[o];
+      sP += bp * dWi * bp;
+    }
+    for (int off = T >> 1; off > 0; off >>= 1) {
+      s1 += __shfl_xor(s1, off, 64);
+      sP += __shfl_xor(sP, off, 64);
+    }
+    const double tr1 = s1 / t, trP = sP / t;
+    // pass 2: centred covariance / variance -> optimal c (CalcOptimalCVectorized)
+    double cv = 0., vv = 0.;
+    for (int c = lane; c < t; c += T) {
+      const size_t o = (size_t)i * t + c;
+      double bp = a.P[o];
+      for (int r = 0; r < k; ++r) bp = fma(bv[r], a.P[(size_t)nb[r] * t + c], bp);
+      const double z1 = a.U[o] * dWi * a.P[o] - tr1;
+      const double zP = bp * dWi * bp - trP;
+      cv += z1 * zP;
+      vv += zP * zP;
+    }
+    for (int off = T >> 1; off > 0; off >>= 1) {
+      cv += __shfl_xor(cv, off, 64);
+      vv += __shfl_xor(vv, off, 64);
+    }
+    cv /= t;
+    vv /= t;
+    const double copt = (vv == 0.) ? 1. : cv / vv;
+    if (lane == 0) a.dmll[i] = 0.5 * (tr1 + copt * (dWi / a.dw[i]) - copt * trP);
+  }
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------ launchers
+void launch_b_apply(const SparseB& B, const double* vals, bool unit, const double* X, int t, const double* scale,
+                    double* Y, hipStream_t s) {
+  const Lanes L = lanes_for(t);
+  hipLaunchKernelGGL(b_apply_kernel, dim3(grid_x(B.n, L.rpb), L.gy), dim3(kBT), 0, s, B.n, B.m, B.nbr, vals,
+                     unit ? 1 : 0, X, t, L.shift, scale, Y);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_bt_apply(const SparseB& B, const double* vals, bool unit, const double* X, int t, const double* pre,
+                     const double* W, const double* H, double* Y, hipStream_t s) {
+  const Lanes L = lanes_for(t);
+  hipLaunchKernelGGL(bt_apply_kernel, dim3(grid_x(B.n, L.rpb), L.gy), dim3(kBT), 0, s, B.n, B.tptr, B.trow,
+                     B.tslot, vals, unit ? 1 : 0, X, t, L.shift, pre, W, H, Y);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_trsv_bt_level(const SparseB& B, const double* Bv, const int* rows, int cnt, const double* R, double* Y,
+                          int t, hipStream_t s) {
+  const Lanes L = lanes_for(t);
+  hipLaunchKernelGGL(trsv_bt_level_kernel, dim3((cnt + L.rpb - 1) / L.rpb, L.gy), dim3(kBT), 0, s, rows, cnt,
+                     B.tptr, B.trow, B.tslot, Bv, R, Y, t, L.shift);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_trsv_b_level(const SparseB& B, const double* Bv, const double* dw, const int* rows, int cnt,
+                         const double* X, double* Z, int t, hipStream_t s) {
+  const Lanes L = lanes_for(t);
+  hipLaunchKernelGGL(trsv_b_level_kernel, dim3((cnt + L.rpb - 1) / L.rpb, L.gy), dim3(kBT), 0, s, rows, cnt, B.m,
+                     B.nbr, Bv, dw, X, Z, t, L.shift);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_coldots(int n, int t, int np, const double* const* A, const double* const* Bm, double* partials,
+                    double* out, hipStream_t s) {
+  const Lanes L = lanes_for(t);
+  const int gx = grid_x(n, L.rpb, kMaxRedBlocks);
+  const dim3 grid(gx, L.gy);
+  switch (np) {
+    case 1:
+      hipLaunchKernelGGL(coldots_kernel<1>, grid, dim3(kBT), 0, s, n, t, L.shift, A[0], Bm[0], nullptr, nullptr,
+                         nullptr, nullptr, partials);
+      break;
+    case 2:
+      hipLaunchKernelGGL(coldots_kernel<2>, grid, dim3(kBT), 0, s, n, t, L.shift, A[0], Bm[0], A[1], Bm[1], nullptr,
+                         nullptr, partials);
+      break;
+    case 3:
+      hipLaunchKernelGGL(coldots_kernel<3>, grid, dim3(kBT), 0, s, n, t, L.shift, A[0], Bm[0], A[1], Bm[1], A[2],
+                         Bm[2], partials);
+      break;
+    default: Fatal("coldots: np = %d", np);
+  }
+  HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(reduce_blocks_kernel, dim3(np * t), dim3(kBT), 0, s, partials, gx, np * t, out);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_cg_update(int n, int t, const double* a, const double* H, const double* V, double* U, double* R,
+                      double* partials, double* rr, hipStream_t s) {
+  const Lanes L = lanes_for(t);
+  const int gx = grid_x(n, L.rpb, kMaxRedBlocks);
+  hipLaunchKernelGGL(cg_update_kernel, dim3(gx, L.gy), dim3(kBT), 0, s, n, t, L.shift, a, H, V, U, R, partials);
+  HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(reduce_blocks_kernel, dim3(t), dim3(kBT), 0, s, partials, gx, t, rr);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_h_update(int n, int t, const double* b, const double* Z, double* H, hipStream_t s) {
+  const size_t total = (size_t)n * t;
+  int g = (int)((total + kBT - 1) / kBT);
+  if (g > kMaxGridX) g = kMaxGridX;
+  hipLaunchKernelGGL(h_update_kernel, dim3(g), dim3(kBT), 0, s, total, t, b, Z, H);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_copy(size_t count, const double* X, double* Y, hipStream_t s) {
+  int g = (int)((count + kBT - 1) / kBT);
+  if (g > kMaxGridX) g = kMaxGridX;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(copy_kernel, dim3(g), dim3(kBT), 0, s, count, X, Y);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_axpby(size_t count, double alpha, const double* X, double beta, const double* Y, double* Z,
+                  hipStream_t s) {
+  int g = (int)((count + kBT - 1) / kBT);
+  if (g > kMaxGridX) g = kMaxGridX;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(axpby_kernel, dim3(g), dim3(kBT), 0, s, count, alpha, X, beta, Y, Z);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_cg_alpha(int t, const double* rz, const double* hv, double* a, double* hist, hipStream_t s) {
+  hipLaunchKernelGGL(cg_alpha_kernel, dim3((t + 63) / 64), dim3(64), 0, s, t, rz, hv, a, hist);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_cg_beta(int t, const double* rz_new, double* rz, double* b, double* hist, hipStream_t s) {
+  hipLaunchKernelGGL(cg_beta_kernel, dim3((t + 63) / 64), dim3(64), 0, s, t, rz_new, rz, b, hist);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_newton_prep(const NewtonPrepArgs& a, hipStream_t s) {
+  hipLaunchKernelGGL(newton_prep_kernel, dim3(grid_x(a.n, kBT, 1024)), dim3(kBT), 0, s, a);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_latent_scalars(const ScalarArgs& a, double* partials, double* out, hipStream_t s) {
+  const int gx = grid_x(a.n, kBT, kMaxRedBlocks);
+  hipLaunchKernelGGL(latent_scalars_kernel, dim3(gx), dim3(kBT), 0, s, a, partials);
+  HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(reduce_blocks_kernel, dim3(kLatentScalars), dim3(kBT), 0, s, partials, gx, kLatentScalars, out);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_grad_cols(const GradColsArgs& a, double* partials, double* out, hipStream_t s) {
+  const Lanes L = lanes_for(a.t);
+  const int gx = grid_x(a.n, L.rpb, kMaxRedBlocks);
+  hipLaunchKernelGGL(grad_cols_kernel, dim3(gx, L.gy), dim3(kBT), 0, s, a, L.shift, partials);
+  HIP_CHECK(hipGetLastError());
+  hipLaunchKernelGGL(reduce_blocks_kernel, dim3(kGradCols * a.t), dim3(kBT), 0, s, partials, gx, kGradCols * a.t,
+                     out);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_mode_deriv(const ModeDerivArgs& a, hipStream_t s) {
+  const Lanes L = lanes_for(a.t);
+  hipLaunchKernelGGL(mode_deriv_kernel, dim3(grid_x(a.n, L.rpb)), dim3(kBT), 0, s, a, L.shift);
+  HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace gpb_amd

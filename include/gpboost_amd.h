@@ -122,8 +122,12 @@ GPBOOST_AMD_EXPORT int GPB_SetOptimConfig(REModelHandle handle,
 /* ---------------------------------------------------------------- likelihood evaluation */
 
 /* replaces GPB_EvalNegLogLikelihood (include/LightGBM/c_api.h:1500; c_api.cpp:2854-2863).
- * cov_pars on the ORIGINAL scale (sigma2, sigma1^2, rho), nll written to negll[0].
- * y may be NULL to reuse the response set by the previous call. */
+ * cov_pars on the ORIGINAL scale: (sigma2, sigma1^2, rho) for the Gaussian likelihood,
+ * (sigma1^2, rho) for latent models (likelihood "bernoulli_logit", or gp_approx
+ * "vecchia_latent" whose error variance is the aux par set by GPB_SetOptimConfig's
+ * init_aux_pars); for latent models negll is the Laplace-approximated value computed with
+ * iterative methods (PCG + stochastic Lanczos quadrature, likelihoods.h:2765-3076).
+ * nll written to negll[0]. y may be NULL to reuse the response set by the previous call. */
 GPBOOST_AMD_EXPORT int GPB_EvalNegLogLikelihood(REModelHandle handle,
     const double* y_data,
     double* cov_pars,
@@ -139,6 +143,11 @@ GPBOOST_AMD_EXPORT int GPB_EvalNegLogLikelihood(REModelHandle handle,
  *   (include/GPBoost/optim_utils.h:243-364): sigma2 is profiled out (yT Psi^-1 y / n),
  *   negll is the profiled nll, grad has num_cov_pars-1 entries (sigma2 excluded), and
  *   sigma2_out (may be NULL) receives the profiled sigma2.
+ * Latent models (profile_sigma2 must be 0): gradient of the approximate negative marginal
+ *   log-likelihood with respect to log(sigma1^2), log(range transform) and, for
+ *   "vecchia_latent" with estimate_aux_pars, log(error variance) — what
+ *   CalcGradPars -> CalcGradNegMargLikelihoodLaplaceApproxVecchia returns
+ *   (likelihoods.h:4951-5206); grad needs num_cov_pars + num_aux_pars entries.
  * y may be NULL (reuse). */
 GPBOOST_AMD_EXPORT int GPB_EvalNegLogLikelihoodGrad(REModelHandle handle,
     const double* y_data,
@@ -165,6 +174,10 @@ GPBOOST_AMD_EXPORT int GPB_GetLikelihoodName(REModelHandle handle, char* out_str
 /* replaces GPB_GetNumAuxPars (include/LightGBM/c_api.h:1776) */
 GPBOOST_AMD_EXPORT int GPB_GetNumAuxPars(REModelHandle handle, int* num_aux_pars);
 
+/* replaces GPB_GetAuxPars (include/LightGBM/c_api.h:1766; c_api.cpp:3098-3107): aux_pars
+ * caller-allocated (num_aux_pars), out_str receives the name of the first parameter. */
+GPBOOST_AMD_EXPORT int GPB_GetAuxPars(REModelHandle handle, double* aux_pars, char* out_str);
+
 /* ---------------------------------------------------------------- EXTENSION: introspection */
 
 /* Number of covariance parameters (incl. sigma2) of the model. */
@@ -179,6 +192,17 @@ GPBOOST_AMD_EXPORT int GPB_GetVecchiaStructure(REModelHandle handle, int32_t* pe
  * B values (n x num_neighbors; B(i, nbr) = -A_i, 0-padded). Computed on the GPU. */
 GPBOOST_AMD_EXPORT int GPB_GetVecchiaFactor(REModelHandle handle, const double* cov_pars,
     double* D_inv, double* B_vals);
+
+/* Latent Vecchia factor at cov_pars = (sigma1^2, rho) (latent models): D^-1 (n), B values
+ * (n x num_neighbors) and their derivatives with respect to log(range transform)
+ * (Vecchia_utils.cpp:1307-1632 with gauss_likelihood = false). Computed on the GPU. */
+GPBOOST_AMD_EXPORT int GPB_GetLatentVecchiaFactor(REModelHandle handle, const double* cov_pars,
+    double* D_inv, double* B_vals, double* dD_range, double* dB_range_vals);
+
+/* Iterative-method statistics of the last latent evaluation: info[0] Newton iterations,
+ * info[1] mode-finding (and gradient) CG iterations, info[2] Lanczos steps of the SLQ
+ * block CG, info[3] the estimate of log|Sigma W + I|. */
+GPBOOST_AMD_EXPORT int GPB_GetLastIterationInfo(REModelHandle handle, double* info);
 
 /* Timing of the last evaluation's dominant kernel (ms, HIP events on the model's stream),
  * for the benchmark's live roofline. kernel_ms[0] = factor/Cholesky kernel,

@@ -62,6 +62,29 @@ int orc_dense_nll_grad(const double* coords, const double* y, int n, int d,
                        int cov_type, const double* pars, int mode,
                        double* nll, double* grad, double* sigma2_out);
 
+/* ---- latent Vecchia + iterative methods (gp_oracle_iter.cpp) ---- */
+enum { ORC_LIK_GAUSSIAN = 0, ORC_LIK_BERNOULLI_LOGIT = 1 };
+
+/* Latent Vecchia factor (Vecchia_utils.cpp:1307-1632, gauss_likelihood = false):
+ * trafo = (sigma1^2, phi). Bv/dBv: n x m row-major, B(i, nbr[i][r]) and its derivative wrt
+ * log(phi) (0-padded); Dinv, dD (= dD/dlog phi): n. Returns 0 or -1 (not SPD). */
+int orc_latent_vecchia_factor(const double* coords_vo, const int* nbr, int n, int d, int m, int cov_type,
+                              const double* trafo, double* Bv, double* dBv, double* Dinv, double* dD);
+
+/* GenRandVecNormalParallel (CG_utils.cpp:930-947): R column-major n x t. */
+void orc_gen_probes(int n, int t, int seed, unsigned long long run_id, double* R);
+
+/* Laplace-approximated nll and gradient for the latent Vecchia model with iterative
+ * methods and the VADU preconditioner (likelihoods.h:2765-3076, 4951-5206, 12069-12546;
+ * CG_utils.cpp:21-217, 930-1041). Mode starts at 0; probes use run_id 0 (first draw,
+ * reuse_rand_vec_trace). trafo = (sigma1^2, phi); aux = gaussian error variance.
+ * grad = [d/dlog sigma1^2, d/dlog phi, (gaussian) d/dlog aux]. info (optional, 4):
+ * newton iterations, total mode-finding CG iterations, Lanczos steps, log|Sigma W + I|. */
+int orc_latent_vecchia_iterative(const double* coords_vo, const double* y_vo, const int* nbr, int n, int d, int m,
+                                 int cov_type, const double* trafo, int likelihood, double aux, int t, int seed,
+                                 double cg_delta_conv, int cg_max_num_it, int cg_max_num_it_tridiag, int want_grad,
+                                 double* nll, double* grad, double* info);
+
 #ifdef __cplusplus
 }
 #endif

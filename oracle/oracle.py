@@ -28,8 +28,7 @@ def build():
 def lib():
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB_PATH):
-            build()
+        build()  # incremental: rebuilds only when a restatement source changed
         L = ctypes.CDLL(LIB_PATH)
         D = ctypes.POINTER(ctypes.c_double)
         I = ctypes.POINTER(ctypes.c_int)
@@ -41,6 +40,12 @@ def lib():
         L.orc_vecchia_partials.argtypes = [D, D, I, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, D,
                                            ctypes.c_int, ctypes.c_int, D]
         L.orc_dense_nll_grad.argtypes = [D, D, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, ctypes.c_int, D, D, D]
+        L.orc_latent_vecchia_factor.argtypes = [D, I, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, D,
+                                                D, D, D, D]
+        L.orc_gen_probes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_ulonglong, D]
+        L.orc_latent_vecchia_iterative.argtypes = [D, D, I, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, D,
+                                                   ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
+                                                   ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, D, D]
         _lib = L
     return _lib
 
@@ -134,3 +139,52 @@ def dense_nll_grad(coords, y, cov_type, pars_trafo, mode):
     if lib().orc_dense_nll_grad(_d(x), _d(yv), n, d, cov_type, _d(p), mode, _d(nll), _d(grad), _d(s2)):
         raise RuntimeError("oracle dense failed")
     return dict(nll=float(nll[0]), grad=(grad[:3] if mode == 0 else grad[:2]).copy(), sigma2=float(s2[0]))
+
+
+LIKELIHOODS = {"gaussian": 0, "bernoulli_logit": 1}
+
+
+def transform_latent(cov_type: int, orig) -> np.ndarray:
+    """(sigma1^2, rho) -> (sigma1^2, phi): TransformCovPars without a nugget (non-Gaussian / latent)."""
+    t = transform(cov_type, [1.0, orig[0], orig[1]])
+    return t[1:].copy()
+
+
+def latent_factor(coords_vo, nbr, cov_type, trafo2):
+    x = np.ascontiguousarray(coords_vo, dtype=np.float64)
+    nb = np.ascontiguousarray(nbr, dtype=np.int32)
+    n, d = x.shape
+    m = nb.shape[1]
+    p = np.ascontiguousarray(trafo2, dtype=np.float64)
+    B, dB = np.zeros((n, m)), np.zeros((n, m))
+    Dinv, dD = np.zeros(n), np.zeros(n)
+    if lib().orc_latent_vecchia_factor(_d(x), _i(nb), n, d, m, cov_type, _d(p), _d(B), _d(dB), _d(Dinv), _d(dD)):
+        raise RuntimeError("oracle latent factor failed")
+    return dict(B=B, dB=dB, Dinv=Dinv, dD=dD)
+
+
+def gen_probes(n: int, t: int, seed: int = 1, run_id: int = 0) -> np.ndarray:
+    R = np.zeros((t, n))   # column-major n x t == row-major t x n
+    lib().orc_gen_probes(n, t, seed, run_id, _d(R))
+    return R.T
+
+
+def latent_iterative(coords_vo, y_vo, nbr, cov_type, trafo2, likelihood="gaussian", aux=1.0, t=50, seed=1,
+                     cg_delta_conv=1e-2, cg_max_num_it=1000, cg_max_num_it_tridiag=1000, want_grad=True):
+    x = np.ascontiguousarray(coords_vo, dtype=np.float64)
+    yv = np.ascontiguousarray(y_vo, dtype=np.float64)
+    nb = np.ascontiguousarray(nbr, dtype=np.int32)
+    n, d = x.shape
+    p = np.ascontiguousarray(trafo2, dtype=np.float64)
+    nll = np.zeros(1)
+    grad = np.zeros(3)
+    info = np.zeros(4)
+    lk = LIKELIHOODS[likelihood]
+    rc = lib().orc_latent_vecchia_iterative(_d(x), _d(yv), _i(nb), n, d, nb.shape[1], cov_type, _d(p), lk,
+                                            float(aux), t, seed, cg_delta_conv, cg_max_num_it, cg_max_num_it_tridiag,
+                                            int(want_grad), _d(nll), _d(grad), _d(info))
+    if rc != 0:
+        raise RuntimeError(f"oracle latent iterative failed ({rc})")
+    ng = 3 if lk == 0 else 2
+    return dict(nll=float(nll[0]), grad=grad[:ng].copy(), newton_its=int(info[0]), cg_its=int(info[1]),
+                lanczos_steps=int(info[2]), logdet=float(info[3]))

@@ -141,9 +141,11 @@ int main(int argc, char** argv) {
     const int t = std::atoi(get(args, "num_rand_vec_trace", "50").c_str());
     const int cg_max = std::atoi(get(args, "cg_max_num_it", "1000").c_str());
     const std::string prec = get(args, "cg_preconditioner_type", "vadu");
+    const int no_index[1] = {-1};   // SetOptimConfig reads estimate_cov_par_index[0] (re_model_template.h:810)
     m->SetOptimConfig(0.1, 0.5, 1000, 1e-6, true, 0, "lbfgs", 2, "relative_change_in_log_likelihood",
                       0.1, 0.5, "lbfgs", cg_max, cg_max, cg_delta_conv, t, true, prec.c_str(),
-                      std::atoi(get(args, "seed_rand_vec_trace", "1").c_str()), -1, false, nullptr, 6, 1e-8);
+                      std::atoi(get(args, "seed_rand_vec_trace", "1").c_str()), -1,
+                      std::atoi(get(args, "estimate_aux", "1").c_str()) != 0, no_index, 6, 1e-8);
   }
   const bool gauss = m->gauss_likelihood_;
   if (!aux.empty()) {

@@ -36,3 +36,21 @@ def rtest_data():
 def synth2000():
     from gpboost_amd import synthetic
     return synthetic.bench_coords(2000), synthetic.bench_gaussian_y(2000)
+
+
+@pytest.fixture(scope="session")
+def golden_latent():
+    import json
+    with open(os.path.join(ROOT, "tests", "golden", "golden_latent.json")) as f:
+        return json.load(f)
+
+
+def latent_case_data(case):
+    """Inputs of a golden_latent.json case (regenerated from the portable LCG generators)."""
+    from gpboost_amd import synthetic
+    if case["data"] == "rtest_bern":
+        return synthetic.rtest_bernoulli_probit_y(100)
+    X = synthetic.bench_coords(case["n"])
+    if case["data"] == "bench":
+        return X, synthetic.bench_gaussian_y(case["n"])
+    return X, synthetic.bench_bernoulli_y(X)

@@ -1,0 +1,61 @@
+"""CPU: pin the latent-Vecchia iterative oracle (oracle/gp_oracle_iter.cpp) to the reference.
+
+Fixtures: tests/golden/golden_latent.json, produced by the reference itself
+(tests/golden/make_golden_latent.py -> oracle/_ref/ref_harness): Laplace-approximated nll
+and gradient with PCG + SLQ (VADU preconditioner, identical probe vectors) for the
+gaussian ("vecchia_latent") and bernoulli_logit likelihoods. Tolerance 1e-6 relative
+(BASELINE.json north_star); with tight CG tolerance the match is ~1e-13.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+from conftest import latent_case_data
+
+RTOL = 1e-6
+
+
+def _run_oracle(case):
+    X, y = latent_case_data(case)
+    ct = O.cov_code(case["cov_fct"], case["shape"])
+    perm, xv, nb = O.vecchia_setup(X, case["num_neighbors"], 0, True)
+    tp = O.transform_latent(ct, case["cov_pars"])
+    return O.latent_iterative(xv, y[perm], nb, ct, tp, case["likelihood"], case["aux"] or 1.0,
+                              t=case["num_rand_vec_trace"], seed=case["seed_rand_vec_trace"],
+                              cg_delta_conv=case["cg_delta_conv"])
+
+
+@pytest.mark.parametrize("name", ["gauss_m30_exp_tight", "gauss_m30_exp_default", "gauss_m20_matern15_t20",
+                                  "bern_m30_exp_tight", "bern_m30_exp_default", "bern_m10_gaussian_t30",
+                                  "bern_m16_matern25", "rtest_bern_m30_exp"])
+def test_oracle_latent_matches_reference(golden_latent, name):
+    case = golden_latent[name]
+    r = _run_oracle(case)
+    assert abs(r["nll"] - case["nll"]) <= RTOL * abs(case["nll"]), (r["nll"], case["nll"])
+    g_ref = np.array(case["grad"])
+    assert r["grad"].shape == g_ref.shape
+    np.testing.assert_allclose(r["grad"], g_ref, rtol=RTOL, atol=RTOL * np.abs(g_ref).max())
+
+
+def test_probe_generator_is_standard_normal():
+    R = O.gen_probes(20000, 4, seed=1)
+    assert R.shape == (20000, 4)
+    assert abs(R.mean()) < 0.02 and abs(R.std() - 1) < 0.02
+    # columns are independent streams seeded by the column index (CG_utils.cpp:938-941)
+    assert not np.allclose(R[:, 0], R[:, 1])
+    np.testing.assert_array_equal(O.gen_probes(100, 2, seed=1)[:, 1], O.gen_probes(100, 3, seed=1)[:, 1])
+
+
+def test_latent_factor_range_derivative_fd():
+    """Size-independent property: dB/dlog(phi), dD/dlog(phi) vs central differences."""
+    from gpboost_amd import synthetic
+    X = synthetic.bench_coords(300)
+    perm, xv, nb = O.vecchia_setup(X, 12, 0, True)
+    tp = np.array([1.3, 7.0])
+    f0 = O.latent_factor(xv, nb, 0, tp)
+    h = 1e-6
+    fp = O.latent_factor(xv, nb, 0, tp * np.array([1, np.exp(h)]))
+    fm = O.latent_factor(xv, nb, 0, tp * np.array([1, np.exp(-h)]))
+    np.testing.assert_allclose((fp["B"] - fm["B"]) / (2 * h), f0["dB"], atol=1e-6)
+    Dp, Dm = 1 / fp["Dinv"], 1 / fm["Dinv"]
+    np.testing.assert_allclose((Dp - Dm) / (2 * h), f0["dD"], atol=1e-6)
