@@ -3,6 +3,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
+#include <cstdio>
 #include <cstring>
 
 #include "slq_host.h"
@@ -16,6 +18,32 @@ constexpr double kCArmijo = 1e-4;                   // c_armijo_ (likelihoods.h:
 // sum rhs^2 < 1e-200, which is implied by it and differs only below ~1e-100 magnitudes.
 constexpr double kZeroRhsSq = 1e-200;
 constexpr int kOutDoubles = 1024;
+}  // namespace
+
+namespace {
+// Optional phase timing (GPBOOST_AMD_TIMING=1): device time of preconditioner applications,
+// operator applications and the rest, printed once per evaluation.
+struct PhaseTimer {
+  bool on = std::getenv("GPBOOST_AMD_TIMING") != nullptr;
+  hipEvent_t a = nullptr, b = nullptr;
+  double ms[4] = {0, 0, 0, 0};
+  int cnt[4] = {0, 0, 0, 0};
+  void begin(hipStream_t s) {
+    if (!on) return;
+    if (!a) { (void)hipEventCreate(&a); (void)hipEventCreate(&b); }
+    (void)hipEventRecord(a, s);
+  }
+  void end(hipStream_t s, int k) {
+    if (!on) return;
+    (void)hipEventRecord(b, s);
+    (void)hipEventSynchronize(b);
+    float x = 0.f;
+    (void)hipEventElapsedTime(&x, a, b);
+    ms[k] += x;
+    ++cnt[k];
+  }
+};
+PhaseTimer g_timer;
 }  // namespace
 
 LatentVecchia::LatentVecchia(int n, int d, int m, const double* d_X, const int* nbr, hipStream_t stream)
@@ -32,6 +60,7 @@ LatentVecchia::LatentVecchia(int n, int d, int m, const double* d_X, const int* 
 }
 
 LatentVecchia::~LatentVecchia() {
+  for (GraphEntry& g : graphs_) (void)hipGraphExecDestroy(g.exec);
   if (h_out_) (void)hipHostFree(h_out_);
   if (ev0_) (void)hipEventDestroy(ev0_);
   if (ev1_) (void)hipEventDestroy(ev1_);
@@ -89,19 +118,16 @@ void LatentVecchia::BuildStructure(const int* nbr) {
   std::vector<int> frows, brows;
   bucket(lf, Lf, fptr_, frows);
   bucket(lb, Lb, bptr_, brows);
+  BuildSweepPlan(nbr, tptr, trow, tslot, lf, lb);
 
   d_nbr_.alloc((size_t)n * m);
   d_tptr_.alloc(n + 1);
   d_trow_.alloc(trow.size());
   d_tslot_.alloc(tslot.size());
-  d_frows_.alloc(n);
-  d_brows_.alloc(n);
   HIP_CHECK(hipMemcpyAsync(d_nbr_.get(), nbr, sizeof(int) * (size_t)n * m, hipMemcpyHostToDevice, s_));
   HIP_CHECK(hipMemcpyAsync(d_tptr_.get(), tptr.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice, s_));
   HIP_CHECK(hipMemcpyAsync(d_trow_.get(), trow.data(), sizeof(int) * trow.size(), hipMemcpyHostToDevice, s_));
   HIP_CHECK(hipMemcpyAsync(d_tslot_.get(), tslot.data(), sizeof(int) * tslot.size(), hipMemcpyHostToDevice, s_));
-  HIP_CHECK(hipMemcpyAsync(d_frows_.get(), frows.data(), sizeof(int) * n, hipMemcpyHostToDevice, s_));
-  HIP_CHECK(hipMemcpyAsync(d_brows_.get(), brows.data(), sizeof(int) * n, hipMemcpyHostToDevice, s_));
   HIP_CHECK(hipStreamSynchronize(s_));
   sp_.n = n;
   sp_.m = m;
@@ -156,17 +182,182 @@ void LatentVecchia::EnsureProbes(const IterativeConfig& cfg) {
 
 // V = (B^T D^-1 B + W) H   (CG_utils.cpp:75, 161-164)
 void LatentVecchia::ApplyA(const double* H, double* V, double* G, int t) {
+  g_timer.begin(s_);
   launch_b_apply(sp_, d_Bv_.get(), true, H, t, d_Dinv_.get(), G, s_);
   launch_bt_apply(sp_, d_Bv_.get(), true, G, t, nullptr, d_W_.get(), H, V, s_);
+  g_timer.end(s_, t == 1 ? 2 : 3);
+}
+
+// Step plan for the VADU sweep kernel: rows in level order, each level cut into steps of at
+// most kSweepRows rows / kSweepEnts entries, each step one contiguous blob (SweepPlan).
+void LatentVecchia::BuildSweepPlan(const int* nbr, const std::vector<int>& tptr, const std::vector<int>& trow,
+                                   const std::vector<int>& tslot, const std::vector<int>& lf,
+                                   const std::vector<int>& lb) {
+  const int n = n_, m = m_;
+  std::vector<int> blob, step_off, vpos, eslot;
+  int max_words = 4;
+  auto entries_of = [&](bool lower, int row, std::vector<int>& idx, std::vector<int>& slot) {
+    idx.clear();
+    slot.clear();
+    if (lower) {
+      const int k = std::min(row, m);
+      for (int r = 0; r < k; ++r) { idx.push_back(nbr[(size_t)row * m + r]); slot.push_back(row * m + r); }
+    } else {
+      for (int e = tptr[row]; e < tptr[row + 1]; ++e) { idx.push_back(trow[e]); slot.push_back(tslot[e]); }
+    }
+  };
+  std::vector<int> idx, slot;
+  std::vector<int> lrows, beoff(1, 0), beidx, beslot, fidx, fslot;
+  lplan_.lptr.assign(1, 0);
+  for (int phase = 0; phase < 2; ++phase) {
+    const bool lower = phase == 1;
+    const std::vector<int>& lev = lower ? lf : lb;
+    // rows by level (stable by index)
+    int L = 0;
+    for (int i = 0; i < n; ++i) L = std::max(L, lev[i] + 1);
+    std::vector<std::vector<int>> by_level(L);
+    for (int i = 0; i < n; ++i) by_level[lev[i]].push_back(i);
+    for (int l = 0; l < L; ++l) {
+      const std::vector<int>& rows = by_level[l];
+      for (int r : rows) {
+        entries_of(lower, r, idx, slot);
+        lrows.push_back(r);
+        if (lower) {   // fixed stride m, zero-value padding (slot -1)
+          for (int q = 0; q < m; ++q) {
+            fidx.push_back(q < (int)idx.size() ? idx[q] : 0);
+            fslot.push_back(q < (int)idx.size() ? slot[q] : -1);
+          }
+        } else {
+          beidx.insert(beidx.end(), idx.begin(), idx.end());
+          beslot.insert(beslot.end(), slot.begin(), slot.end());
+          beoff.push_back((int)beidx.size());
+        }
+      }
+      lplan_.lptr.push_back((int)lrows.size());
+      size_t q = 0;
+      while (q < rows.size()) {
+        // greedily take rows while both limits hold
+        std::vector<int> srows;
+        std::vector<int> sidx, sslot, soff(1, 0);
+        while (q < rows.size() && (int)srows.size() < kSweepRows) {
+          entries_of(lower, rows[q], idx, slot);
+          if ((int)idx.size() > kSweepEnts) Fatal("Vecchia row with %d dependents exceeds the sweep step capacity", (int)idx.size());
+          if (!srows.empty() && (int)(sidx.size() + idx.size()) > kSweepEnts) break;
+          srows.push_back(rows[q]);
+          sidx.insert(sidx.end(), idx.begin(), idx.end());
+          sslot.insert(sslot.end(), slot.begin(), slot.end());
+          soff.push_back((int)sidx.size());
+          ++q;
+        }
+        const int R = (int)srows.size(), E = (int)sidx.size();
+        const int base = (int)blob.size();
+        int v0 = kSweepHdr + 2 * R + 1;
+        v0 += v0 & 1;                                  // fp64 values 8-byte aligned
+        int words = v0 + 3 * E;
+        words = (words + 3) & ~3;                      // next blob 16-byte aligned
+        blob.resize(base + words, 0);
+        blob[base + 0] = R;
+        blob[base + 1] = E;
+        blob[base + 2] = v0;
+        blob[base + 3] = words;
+        blob[base + 5] = lower ? 1 : 0;
+        if (!step_off.empty()) blob[step_off.back() + 4] = words;   // previous blob: size of this one
+        std::copy(srows.begin(), srows.end(), blob.begin() + base + kSweepHdr);
+        std::copy(soff.begin(), soff.end(), blob.begin() + base + kSweepHdr + R);
+        std::copy(sidx.begin(), sidx.end(), blob.begin() + base + v0 + 2 * E);
+        for (int e = 0; e < E; ++e) {
+          vpos.push_back((base + v0) / 2 + e);         // index in the blob viewed as fp64
+          eslot.push_back(sslot[e]);
+        }
+        step_off.push_back(base);
+        max_words = std::max(max_words, words);
+      }
+    }
+  }
+  lplan_.nlev = (int)lplan_.lptr.size() - 1;
+  lplan_.n = n;
+  lplan_.m = m;
+  lplan_.nlev_b = 0;
+  for (int i = 0; i < n; ++i) lplan_.nlev_b = std::max(lplan_.nlev_b, lb[i] + 1);
+  // value slots of both phases in one refresh gather: [beslot | fslot]
+  std::vector<int> lslot(beslot);
+  lslot.insert(lslot.end(), fslot.begin(), fslot.end());
+  lplan_entries_ = (int)lslot.size();
+  d_lrows_.alloc(lrows.size());
+  d_beoff_.alloc(beoff.size());
+  d_beidx_.alloc(std::max<size_t>(beidx.size(), 1));
+  d_fidx_.alloc(std::max<size_t>(fidx.size(), 1));
+  d_lslot_.alloc(std::max<size_t>(lslot.size(), 1));
+  d_lval_.alloc(std::max<size_t>(lslot.size(), 1));
+  HIP_CHECK(hipMemcpyAsync(d_lrows_.get(), lrows.data(), sizeof(int) * lrows.size(), hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipMemcpyAsync(d_beoff_.get(), beoff.data(), sizeof(int) * beoff.size(), hipMemcpyHostToDevice, s_));
+  if (!beidx.empty())
+    HIP_CHECK(hipMemcpyAsync(d_beidx_.get(), beidx.data(), sizeof(int) * beidx.size(), hipMemcpyHostToDevice, s_));
+  if (!fidx.empty())
+    HIP_CHECK(hipMemcpyAsync(d_fidx_.get(), fidx.data(), sizeof(int) * fidx.size(), hipMemcpyHostToDevice, s_));
+  if (!lslot.empty())
+    HIP_CHECK(hipMemcpyAsync(d_lslot_.get(), lslot.data(), sizeof(int) * lslot.size(), hipMemcpyHostToDevice, s_));
+  lplan_.lrows = d_lrows_.get();
+  lplan_.beoff = d_beoff_.get();
+  lplan_.beidx = d_beidx_.get();
+  lplan_.beval = d_lval_.get();
+  lplan_.fidx = d_fidx_.get();
+  lplan_.fval = d_lval_.get() + beslot.size();
+  use_graph_ = std::getenv("GPBOOST_AMD_SWEEP_KERNEL") == nullptr;
+  plan_.nsteps = (int)step_off.size();
+  plan_.first_words = step_off.empty() ? 0 : blob[3];
+  // each LDS buffer is a whole number of 64-word wave slices (staging writes full slices)
+  plan_.max_words = (max_words + 63) & ~63;
+  plan_entries_ = (int)vpos.size();
+  if ((size_t)2 * plan_.max_words * sizeof(int) > 160 * 1024) Fatal("sweep plan exceeds the LDS capacity");
+  blob.resize(blob.size() + 64, 0);                  // staging of the (empty) step after the last
+  d_blob_.alloc(blob.size());
+  d_vpos_.alloc(std::max<size_t>(vpos.size(), 1));
+  d_eslot_.alloc(std::max<size_t>(eslot.size(), 1));
+  HIP_CHECK(hipMemcpyAsync(d_blob_.get(), blob.data(), sizeof(int) * blob.size(), hipMemcpyHostToDevice, s_));
+  if (!vpos.empty()) {
+    HIP_CHECK(hipMemcpyAsync(d_vpos_.get(), vpos.data(), sizeof(int) * vpos.size(), hipMemcpyHostToDevice, s_));
+    HIP_CHECK(hipMemcpyAsync(d_eslot_.get(), eslot.data(), sizeof(int) * eslot.size(), hipMemcpyHostToDevice, s_));
+  }
+  HIP_CHECK(hipStreamSynchronize(s_));
+  plan_.blob = d_blob_.get();
 }
 
 // Z = P^-1 R, P = B^T (D^-1 + W) B (VADU, CG_utils.cpp:56-60): B^T solve then (dw B) solve.
+// Default: one kernel per level replayed from a hipGraph captured once per buffer set
+// (a graph boundary costs ~1.5 us, far below a host launch); alternative: the one-launch
+// per-column sweep (GPBOOST_AMD_SWEEP_KERNEL).
 void LatentVecchia::Precond(const double* R, double* Z, double* Xt, int t) {
-  for (size_t l = 0; l + 1 < bptr_.size(); ++l)
-    launch_trsv_bt_level(sp_, d_Bv_.get(), d_brows_.get() + bptr_[l], bptr_[l + 1] - bptr_[l], R, Xt, t, s_);
-  for (size_t l = 0; l + 1 < fptr_.size(); ++l)
-    launch_trsv_b_level(sp_, d_Bv_.get(), d_dw_.get(), d_frows_.get() + fptr_[l], fptr_[l + 1] - fptr_[l], Xt, Z, t,
-                        s_);
+  g_timer.begin(s_);
+  PrecondImpl(R, Z, Xt, t);
+  g_timer.end(s_, t == 1 ? 0 : 1);
+}
+
+void LatentVecchia::PrecondImpl(const double* R, double* Z, double* Xt, int t) {
+  if (!use_graph_) {
+    launch_vadu_sweep(plan_, d_dw_.get(), R, Xt, Z, t, s_);
+    return;
+  }
+  static const bool eager = std::getenv("GPBOOST_AMD_NO_GRAPH") != nullptr;   // diagnostics (profilers)
+  if (eager) {
+    for (int l = 0; l < lplan_.nlev; ++l) launch_vadu_level(lplan_, l, d_dw_.get(), R, Xt, Z, t, s_);
+    return;
+  }
+  for (const GraphEntry& g : graphs_) {
+    if (g.key[0] == R && g.key[1] == Xt && g.key[2] == Z && g.t == t) {
+      HIP_CHECK(hipGraphLaunch(g.exec, s_));
+      return;
+    }
+  }
+  hipGraph_t graph;
+  HIP_CHECK(hipStreamBeginCapture(s_, hipStreamCaptureModeThreadLocal));
+  for (int l = 0; l < lplan_.nlev; ++l) launch_vadu_level(lplan_, l, d_dw_.get(), R, Xt, Z, t, s_);
+  HIP_CHECK(hipStreamEndCapture(s_, &graph));
+  GraphEntry e{{R, Xt, Z}, t, nullptr};
+  HIP_CHECK(hipGraphInstantiate(&e.exec, graph, nullptr, nullptr, 0));
+  HIP_CHECK(hipGraphDestroy(graph));
+  graphs_.push_back(e);
+  HIP_CHECK(hipGraphLaunch(e.exec, s_));
 }
 
 double LatentVecchia::Dot1(const double* x, const double* y) {
@@ -271,8 +462,32 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
   fa.Dinv = d_Dinv_.get();
   fa.dD = want_grad ? d_dD_.get() : nullptr;
   launch_latent_factor(cov_type, fa, s_);
+  launch_sweep_values(plan_entries_, d_vpos_.get(), d_eslot_.get(), d_Bv_.get(), d_blob_.get(), s_);
+  launch_gather(lplan_entries_, d_lslot_.get(), d_Bv_.get(), d_lval_.get(), s_);
 
   Block& b1 = GetBlock(0, 1, std::max(cfg.cg_max_num_it, 1));
+  if (std::getenv("GPBOOST_AMD_BENCH_PRECOND")) {   // diagnostics: preconditioner cost alone
+    NewtonPrepArgs np{};
+    np.n = n; np.lik = lik; np.aux = aux; np.y = d_y_.get(); np.loc = d_mode_.get(); np.mode = d_mode_.get();
+    np.Dinv = d_Dinv_.get(); np.d1 = d_d1_.get(); np.W = d_W_.get(); np.W_update = 1; np.dw = d_dw_.get();
+    HIP_CHECK(hipMemsetAsync(d_mode_.get(), 0, sizeof(double) * n, s_));
+    launch_newton_prep(np, s_);
+    HIP_CHECK(hipMemsetAsync(b1.R.get(), 0, sizeof(double) * n, s_));
+    for (int tt : {1, t}) {
+      Block& bb = GetBlock(tt == 1 ? 0 : 1, tt, std::max(cfg.cg_max_num_it, 1));
+      HIP_CHECK(hipMemsetAsync(bb.R.get(), 0, sizeof(double) * n * tt, s_));
+      Precond(bb.R.get(), bb.Z.get(), bb.Xt.get(), tt);
+      HIP_CHECK(hipStreamSynchronize(s_));
+      HIP_CHECK(hipEventRecord(ev0_, s_));
+      for (int r = 0; r < 20; ++r) Precond(bb.R.get(), bb.Z.get(), bb.Xt.get(), tt);
+      HIP_CHECK(hipEventRecord(ev1_, s_));
+      HIP_CHECK(hipEventSynchronize(ev1_));
+      float pm = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&pm, ev0_, ev1_));
+      std::fprintf(stderr, "[precond bench] t=%d: %.3f ms per application (%d levels)\n", tt, pm / 20,
+                   lplan_.nlev);
+    }
+  }
   ScalarArgs sa{};
   sa.n = n; sa.m = m_; sa.lik = lik; sa.aux = aux;
   sa.nbr = d_nbr_.get(); sa.Bv = d_Bv_.get(); sa.Dinv = d_Dinv_.get(); sa.y = d_y_.get();
@@ -450,6 +665,15 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
   float ms = 0.f;
   HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_));
   res.ms_total = ms;
+  if (g_timer.on) {
+    std::fprintf(stderr, "[latent timing] total %.1f ms | precond t=1: %d x %.3f ms, t=%d: %d x %.3f ms | "
+                 "A t=1: %d x %.3f ms, t=%d: %d x %.3f ms\n", ms, g_timer.cnt[0],
+                 g_timer.cnt[0] ? g_timer.ms[0] / g_timer.cnt[0] : 0., t, g_timer.cnt[1],
+                 g_timer.cnt[1] ? g_timer.ms[1] / g_timer.cnt[1] : 0., g_timer.cnt[2],
+                 g_timer.cnt[2] ? g_timer.ms[2] / g_timer.cnt[2] : 0., t, g_timer.cnt[3],
+                 g_timer.cnt[3] ? g_timer.ms[3] / g_timer.cnt[3] : 0.);
+    g_timer = PhaseTimer();
+  }
   return res;
 }
 

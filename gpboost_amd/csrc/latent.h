@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <map>
 #include <memory>
 #include <vector>
 
@@ -78,6 +79,7 @@ class LatentVecchia {
   void EnsureProbes(const IterativeConfig& cfg);
   void ApplyA(const double* H, double* V, double* G, int t);
   void Precond(const double* R, double* Z, double* Xt, int t);
+  void PrecondImpl(const double* R, double* Z, double* Xt, int t);
   // PCG on t columns (CG_utils.cpp:21-108 for t = 1, :110-217 with tridiag). Returns the
   // number of iterations; *nan on NaN/Inf residual; *zero_rhs for the zero-RHS shortcut.
   int Pcg(Block& b, const double* RHS, double* U, bool init_zero, bool u_is_zero, int pmax, double delta,
@@ -89,8 +91,22 @@ class LatentVecchia {
   const double* d_X_;
   hipStream_t s_;
   SparseB sp_{};
-  DevBuf<int> d_nbr_, d_tptr_, d_trow_, d_tslot_, d_frows_, d_brows_;
-  std::vector<int> fptr_, bptr_;
+  DevBuf<int> d_nbr_, d_tptr_, d_trow_, d_tslot_;
+  // step plan of the two VADU triangular solves (see SweepPlan)
+  std::vector<int> fptr_, bptr_;           // level pointers (host, diagnostics)
+  SweepPlan plan_{};
+  DevBuf<int> d_blob_, d_vpos_, d_eslot_;
+  int plan_entries_ = 0;
+  // level-by-level form replayed as hipGraphs (one per (R, Y, Z, t) buffer set)
+  LevelPlan lplan_{};
+  DevBuf<int> d_lrows_, d_beoff_, d_beidx_, d_fidx_, d_lslot_;
+  DevBuf<double> d_lval_;
+  int lplan_entries_ = 0;
+  struct GraphEntry { const void* key[3]; int t; hipGraphExec_t exec; };
+  std::vector<GraphEntry> graphs_;
+  bool use_graph_ = true;
+  void BuildSweepPlan(const int* nbr, const std::vector<int>& tptr, const std::vector<int>& trow,
+                      const std::vector<int>& tslot, const std::vector<int>& lf, const std::vector<int>& lb);
   DevBuf<double> d_y_, d_Bv_, d_dBv_, d_Dinv_, d_dD_, d_W_, d_dw_, d_sdw_, d_d1_;
   DevBuf<double> d_mode_, d_mode_upd_, d_mode_new_, d_rhs_, d_dir_, d_Adir_, d_vS_, d_dmll_;
   DevBuf<double> d_probes_, d_Zp_, d_U_, d_P_;   // n x t

@@ -9,10 +9,12 @@
 //
 // Same lane-group mapping as the exact-Gaussian row kernel (vecchia_kernels.hip): K lanes
 // own one row, the k x k between-neighbour covariance C and dC/dlog(phi) live in packed
-// LDS triangles, and the solves are symmetric Gauss-Jordan eliminations with one LDS
-// broadcast per step. The factor needs two right-hand sides that are not known together
-// (dA = C^-1 (dc - dC a) needs a = C^-1 c first), so the elimination runs twice over the
-// unchanged packed C; this kernel runs once per likelihood evaluation.
+// LDS triangles, one LDS broadcast per elimination step. The solves use a Cholesky factor
+// (not the Gauss-Jordan sweep of the nugget-regularised exact-Gaussian kernel): without a
+// nugget, C has only a 1e-10 jitter and can be very ill-conditioned (e.g. Gaussian kernel),
+// where only triangular solves stay as accurate as the reference's LLT. L overwrites the
+// packed C in LDS; the second right-hand side (dA = C^-1 (dc - dC a) needs a first)
+// reuses it. The kernel runs once per likelihood evaluation.
 #include <hip/hip_runtime.h>
 
 #include "common.h"
@@ -43,14 +45,25 @@ constexpr int group_lds_doubles() { return K * (K + 1) + kDMax * K + 2 * K; }
 
 __device__ __forceinline__ int packed(int r, int c) { return r * (r + 1) / 2 + c; }
 
-// Symmetric Gauss-Jordan on [C | rhs] with lane r holding row r of C (from the packed
-// triangle) and rhs_r; returns (C^-1 rhs)_r. Rows >= k are identity padding.
+__device__ __forceinline__ double rcp_nr(double x) {   // 1/x: hardware reciprocal + 2 Newton steps
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(r, fma(-x, r, 1.), r);
+  return fma(r, fma(-x, r, 1.), r);
+}
+
+// Right-looking Cholesky C = L L^T of the packed lower triangle, lane r owning row r,
+// with the forward solve L y = rhs fused in (one LDS broadcast of column j per step).
+// On return row[p] = L(r, p) for p <= r, *inv_diag = 1 / L(r, r), result = y_r.
+// Rows >= k are identity padding. (Cholesky rather than Gauss-Jordan: without a nugget the
+// between-neighbour covariance can be very ill-conditioned, and only the triangular
+// solves keep the error at the level of the reference's LLT, Vecchia_utils.cpp:1556.)
 template <int K>
-__device__ __forceinline__ double gj_solve(const double* Cp, int r, double* slot_c, double* slot_a, double rhs) {
-  double row[K];
+__device__ __forceinline__ double chol_fwd(const double* Cp, int r, double* slot_c, double* slot_a, double rhs,
+                                           double (&row)[K], double* inv_diag) {
 #pragma unroll
-  for (int c = 0; c < K; ++c) row[c] = (c <= r) ? Cp[packed(r, c)] : Cp[packed(c, r)];
+  for (int c = 0; c < K; ++c) row[c] = (c <= r) ? Cp[packed(r, c)] : 0.;
   double aug = rhs;
+  double invd = 1.;
 #pragma unroll
   for (int j = 0; j < K; ++j) {
     compiler_fence();
@@ -58,22 +71,57 @@ __device__ __forceinline__ double gj_solve(const double* Cp, int r, double* slot
     slot_a[r] = aug;
     wave_lds_sync();
     const double piv = slot_c[j];
-    double rinv = __builtin_amdgcn_rcp(piv);
-    rinv = fma(rinv, fma(-piv, rinv, 1.), rinv);
-    rinv = fma(rinv, fma(-piv, rinv, 1.), rinv);
-    const double f = (r == j) ? 0. : row[j] * rinv;
-    aug = fma(-f, slot_a[j], aug);
+    const double ljj = sqrt(piv);
+    const double inv = rcp_nr(ljj);
+    const double yj = slot_a[j] * inv;
+    const double lr = row[j] * inv;            // L(r, j) for r > j
+    const double f = (r > j) ? lr * inv : 0.;  // L(r, j) / L(j, j)
 #pragma unroll
     for (int c = j + 1; c < K; ++c) row[c] = fma(-f, slot_c[c], row[c]);
+    if (r == j) { row[j] = ljj; aug = yj; invd = inv; }
+    if (r > j) { row[j] = lr; aug = fma(-lr, yj, aug); }
 #pragma unroll
-    for (int c = j + 1; c < K; ++c) asm volatile("" : "+v"(row[c]));
+    for (int c = j; c < K; ++c) asm volatile("" : "+v"(row[c]));
     asm volatile("" : "+v"(aug));
   }
-  double mydiag = row[0];
-#pragma unroll
-  for (int c = 1; c < K; ++c) mydiag = (c == r) ? row[c] : mydiag;
+  *inv_diag = invd;
   compiler_fence();
-  return aug / mydiag;
+  return aug;
+}
+
+// Forward solve L y = rhs with L in registers (row[p] = L(r, p)).
+template <int K>
+__device__ __forceinline__ double fwd_solve(const double (&row)[K], double inv_diag, int r, double* slot_a,
+                                            double rhs) {
+  double v = rhs;
+#pragma unroll
+  for (int j = 0; j < K; ++j) {
+    compiler_fence();
+    if (r == j) slot_a[j] = v * inv_diag;
+    wave_lds_sync();
+    const double yj = slot_a[j];
+    if (r > j) v = fma(-row[j], yj, v);
+    if (r == j) v = yj;
+  }
+  compiler_fence();
+  return v;
+}
+
+// Back solve L^T x = y with L packed in LDS (Lp); lane r owns y_r / x_r.
+template <int K>
+__device__ __forceinline__ double back_solve(const double* Lp, double inv_diag, int r, double* slot_a, double y) {
+  double v = y;
+#pragma unroll
+  for (int j = K - 1; j >= 0; --j) {
+    compiler_fence();
+    if (r == j) slot_a[j] = v * inv_diag;
+    wave_lds_sync();
+    const double xj = slot_a[j];
+    if (r < j) v = fma(-Lp[packed(j, r)], xj, v);
+    if (r == j) v = xj;
+  }
+  compiler_fence();
+  return v;
 }
 
 template <int K, int COV>
@@ -151,13 +199,22 @@ __global__ void __launch_bounds__(block_threads<K>()) latent_factor_kernel(Laten
     }
     wave_lds_sync();
 
-    const double av_r = gj_solve<K>(Cp, r, slot_c, slot_a, cvec);   // a = C^-1 c
+    // a = C^-1 c: Cholesky with fused forward solve, L to LDS (over C), back solve
+    double row[K];
+    double invd;
+    const double y1 = chol_fwd<K>(Cp, r, slot_c, slot_a, cvec, row, &invd);
+#pragma unroll
+    for (int c = 0; c < K; ++c)
+      if (c <= r) Cp[packed(r, c)] = row[c];
+    wave_lds_sync();
+    const double av_r = back_solve<K>(Cp, invd, r, slot_a, y1);
     const double ac = group_sum<K>(av_r * cvec);
     if (active && r < a.m) a.Bv[(size_t)i * a.m + r] = rv ? -av_r : 0.;
     if (active && r == 0) a.Dinv[i] = 1. / (var - ac);             // Vecchia_utils.cpp:1507, 1562, 1615
 
     if (want_grad) {
       // t = dC a (dC diagonal is 0), then w = C^-1 (dc - t) = dA^T (:1573-1574)
+      compiler_fence();
       slot_c[r] = av_r;
       wave_lds_sync();
       double t = 0.;
@@ -168,7 +225,8 @@ __global__ void __launch_bounds__(block_threads<K>()) latent_factor_kernel(Laten
       t = rv ? t : 0.;
       const double dca = group_sum<K>(dcvec * av_r);
       const double ta = group_sum<K>(t * av_r);
-      const double w_r = gj_solve<K>(Cp, r, slot_c, slot_a, dcvec - t);
+      const double y2 = fwd_solve<K>(row, invd, r, slot_a, dcvec - t);
+      const double w_r = back_solve<K>(Cp, invd, r, slot_a, y2);
       if (active && r < a.m) a.dBv[(size_t)i * a.m + r] = rv ? -w_r : 0.;
       if (active && r == 0) a.dD[i] = -(2. * dca - ta);               // :1583 (range: overwrite)
     }

@@ -14,6 +14,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <vector>
+
 namespace gpb_amd {
 
 struct LatentFactorArgs {
@@ -43,12 +45,53 @@ void launch_b_apply(const SparseB& B, const double* vals, bool unit, const doubl
 // Y = unit*pre.*X + V^T (pre.*X) + W.*H  (pre, W/H nullable)
 void launch_bt_apply(const SparseB& B, const double* vals, bool unit, const double* X, int t, const double* pre,
                      const double* W, const double* H, double* Y, hipStream_t s);
-// One level of the unit-upper solve B^T Y = R (rows of the level listed in rows[0..cnt)).
-void launch_trsv_bt_level(const SparseB& B, const double* Bv, const int* rows, int cnt, const double* R, double* Y,
-                          int t, hipStream_t s);
-// One level of the lower solve (diag(dw) B) Z = X.
-void launch_trsv_b_level(const SparseB& B, const double* Bv, const double* dw, const int* rows, int cnt,
-                         const double* X, double* Z, int t, hipStream_t s);
+// VADU preconditioner Z = P^-1 R = (diag(dw) B)^-1 B^-T R for t columns in one launch
+// (vadu_sweep.hip): one workgroup per column walks the level sets of both triangular
+// solves with a workgroup barrier between "steps" (a level, or a slice of a large one),
+// while the next step's structure is copied into LDS asynchronously.
+// Step s is a contiguous blob of 32-bit words (blobs back to back, 16-byte aligned):
+//   [0, kSweepHdr)        header: R rows, E entries, v0, own size, next blob's size, phase
+//   [H, H + R)            row indices (original Vecchia index) of the step    (H = kSweepHdr)
+//   [H + R, H + 2R + 1)   entry offsets (relative, eoff[0] = 0)
+//   [v0, v0 + 2E)         entry values (fp64, 8-byte aligned)
+//   [v0 + 2E, +E)         entry column indices
+// B^T solve entries of row j: (child i, B(i, j)); lower solve entries of row i:
+// (nbr[i][r], B(i, nbr[i][r])); phase 0 = B^T solve, 1 = lower solve.
+constexpr int kSweepRows = 512;      // rows per step (= threads per workgroup)
+constexpr int kSweepEnts = 6144;     // entries per step (two staged blobs fill ~156 KB of LDS)
+constexpr int kSweepHdr = 8;
+struct SweepPlan {
+  int nsteps;
+  int max_words;                     // largest blob (LDS buffer size, words)
+  int first_words;                   // size of the first blob
+  int* blob;                         // values refreshed per evaluation (launch_sweep_values)
+};
+void launch_vadu_sweep(const SweepPlan& plan, const double* dw, const double* R, double* Y, double* Z, int t,
+                       hipStream_t s);
+// Level-by-level form of the same preconditioner (one kernel per level, replayed as a
+// hipGraph; rows of a level spread over all CUs, T lanes per row = the t columns).
+// Rows in level order p: B^T solve rows p in [0, n) (levels [0, nlev_b)), lower solve rows
+// p in [n, 2n). B^T solve: entries [beoff[p], beoff[p+1]) of (beidx, beval) = (child, B(child, row)).
+// Lower solve: fixed stride m, entries (fidx, fval)[(p - n) * m + r] = (nbr, B(row, nbr)),
+// zero-value padding, so a row's structure is one dependency-free load.
+struct LevelPlan {
+  int n, m;
+  int nlev_b, nlev;
+  std::vector<int> lptr;             // host, nlev + 1 (row positions p)
+  const int* lrows;                  // 2n
+  const int* beoff;                  // n + 1
+  const int* beidx;
+  const double* beval;
+  const int* fidx;                   // n x m
+  const double* fval;                // n x m
+};
+void launch_vadu_level(const LevelPlan& lp, int l, const double* dw, const double* R, double* Y, double* Z, int t,
+                       hipStream_t s);
+// blob_f64[vpos[e]] = Bv[eslot[e]] for all count entries (per-evaluation value refresh)
+void launch_sweep_values(int count, const int* vpos, const int* eslot, const double* Bv, int* blob, hipStream_t s);
+// dst[p*m + r] = src[rows[p]*m + r]  (n x m, level order)  |  dst[e] = idx[e] >= 0 ? src[idx[e]] : 0
+void launch_gather_rows(int n, int m, const int* rows, const double* src, double* dst, hipStream_t s);
+void launch_gather(int count, const int* idx, const double* src, double* dst, hipStream_t s);
 
 // Per-column dot products: out[q*t + c] = sum_i A_q[i,c] * B_q[i,c], q < np (np <= 3).
 // Deterministic two-pass reduction through `partials` (>= kMaxRedBlocks * np * t doubles).

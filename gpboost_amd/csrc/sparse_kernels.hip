@@ -94,48 +94,21 @@ __global__ void __launch_bounds__(kBT) bt_apply_kernel(int n, const int* __restr
   }
 }
 
-// ------------------------------------------------------------------ level-scheduled solves
-// B^T Y = R (unit upper): y_j = r_j - sum_{i: j in nbr(i)} B(i,j) y_i, rows of one level.
-__global__ void __launch_bounds__(kBT) trsv_bt_level_kernel(const int* __restrict__ rows, int cnt,
-                                                            const int* __restrict__ tptr,
-                                                            const int* __restrict__ trow,
-                                                            const int* __restrict__ tslot,
-                                                            const double* __restrict__ Bv,
-                                                            const double* __restrict__ R, double* __restrict__ Y,
-                                                            int t, int shift) {
-  const int T = 1 << shift;
-  const int c = (threadIdx.x & (T - 1)) + blockIdx.y * 64;
-  const int rpb = kBT >> shift;
-  const int task = blockIdx.x * rpb + (threadIdx.x >> shift);
-  if (c >= t || task >= cnt) return;
-  const int j = rows[task];
-  double s = R[(size_t)j * t + c];
-  const int e1 = tptr[j + 1];
-#pragma unroll 4
-  for (int e = tptr[j]; e < e1; ++e) s = fma(-Bv[tslot[e]], Y[(size_t)trow[e] * t + c], s);
-  Y[(size_t)j * t + c] = s;
+__global__ void __launch_bounds__(kBT) gather_rows_kernel(int n, int m, const int* __restrict__ rows,
+                                                          const double* __restrict__ src, double* __restrict__ dst) {
+  const size_t total = (size_t)n * m;
+  for (size_t o = (size_t)blockIdx.x * kBT + threadIdx.x; o < total; o += (size_t)gridDim.x * kBT) {
+    const size_t p = o / m, r = o - p * m;
+    dst[o] = src[(size_t)rows[p] * m + r];
+  }
 }
 
-// (diag(dw) B) Z = X (lower): z_i = x_i / dw_i - sum_r B(i, nbr_r) z_nbr_r.
-__global__ void __launch_bounds__(kBT) trsv_b_level_kernel(const int* __restrict__ rows, int cnt, int m,
-                                                           const int* __restrict__ nbr,
-                                                           const double* __restrict__ Bv,
-                                                           const double* __restrict__ dw,
-                                                           const double* __restrict__ X, double* __restrict__ Z,
-                                                           int t, int shift) {
-  const int T = 1 << shift;
-  const int c = (threadIdx.x & (T - 1)) + blockIdx.y * 64;
-  const int rpb = kBT >> shift;
-  const int task = blockIdx.x * rpb + (threadIdx.x >> shift);
-  if (c >= t || task >= cnt) return;
-  const int i = rows[task];
-  const int k = i < m ? i : m;
-  const int* nb = nbr + (size_t)i * m;
-  const double* v = Bv + (size_t)i * m;
-  double s = X[(size_t)i * t + c] / dw[i];
-#pragma unroll 4
-  for (int r = 0; r < k; ++r) s = fma(-v[r], Z[(size_t)nb[r] * t + c], s);
-  Z[(size_t)i * t + c] = s;
+__global__ void __launch_bounds__(kBT) gather_kernel(int count, const int* __restrict__ idx,
+                                                     const double* __restrict__ src, double* __restrict__ dst) {
+  for (int e = blockIdx.x * kBT + threadIdx.x; e < count; e += gridDim.x * kBT) {
+    const int k = idx[e];
+    dst[e] = k >= 0 ? src[k] : 0.;
+  }
 }
 
 // ------------------------------------------------------------------ column reductions
@@ -406,6 +379,9 @@ __global__ void __launch_bounds__(kBT) grad_cols_kernel(GradColsArgs a, int shif
 
 // Row-wise stochastic d log|Sigma W + I| / d mode (vadu branch, likelihoods.h:12320-12341).
 __global__ void __launch_bounds__(kBT) mode_deriv_kernel(ModeDerivArgs a, int shift) {
+  // No FMA contraction in this kernel: pass 2 must recompute the products of pass 1
+  // bit-identically (for t = 1 the centred values are then exactly 0 -> c = 1).
+#pragma clang fp contract(off)
   const int T = 1 << shift;
   const int lane = threadIdx.x & (T - 1);
   const int rpb = kBT >> shift;
@@ -416,6 +392,7 @@ __global__ void __launch_bounds__(kBT) mode_deriv_kernel(ModeDerivArgs a, int sh
     const double* bv = a.Bv + (size_t)i * a.m;
     const double dWi = lik_dinfo(a.lik, a.loc[i]);
     // pass 1: row means of z1 = U dW P and zP = (BP)^2 dW over the t probes
+    // (c_var == 0 -> c = 1, CG_utils.cpp:1036-1039).
     double s1 = 0., sP = 0.;
     for (int c = lane; c < t; c += T) {
       const size_t o = (size_t)i * t + c;
@@ -470,19 +447,18 @@ void launch_bt_apply(const SparseB& B, const double* vals, bool unit, const doub
   HIP_CHECK(hipGetLastError());
 }
 
-void launch_trsv_bt_level(const SparseB& B, const double* Bv, const int* rows, int cnt, const double* R, double* Y,
-                          int t, hipStream_t s) {
-  const Lanes L = lanes_for(t);
-  hipLaunchKernelGGL(trsv_bt_level_kernel, dim3((cnt + L.rpb - 1) / L.rpb, L.gy), dim3(kBT), 0, s, rows, cnt,
-                     B.tptr, B.trow, B.tslot, Bv, R, Y, t, L.shift);
+void launch_gather_rows(int n, int m, const int* rows, const double* src, double* dst, hipStream_t s) {
+  const size_t total = (size_t)n * m;
+  int g = (int)((total + kBT - 1) / kBT);
+  if (g > kMaxGridX) g = kMaxGridX;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(gather_rows_kernel, dim3(g), dim3(kBT), 0, s, n, m, rows, src, dst);
   HIP_CHECK(hipGetLastError());
 }
 
-void launch_trsv_b_level(const SparseB& B, const double* Bv, const double* dw, const int* rows, int cnt,
-                         const double* X, double* Z, int t, hipStream_t s) {
-  const Lanes L = lanes_for(t);
-  hipLaunchKernelGGL(trsv_b_level_kernel, dim3((cnt + L.rpb - 1) / L.rpb, L.gy), dim3(kBT), 0, s, rows, cnt, B.m,
-                     B.nbr, Bv, dw, X, Z, t, L.shift);
+void launch_gather(int count, const int* idx, const double* src, double* dst, hipStream_t s) {
+  if (count <= 0) return;
+  hipLaunchKernelGGL(gather_kernel, dim3(grid_x(count, kBT)), dim3(kBT), 0, s, count, idx, src, dst);
   HIP_CHECK(hipGetLastError());
 }
 
