@@ -151,6 +151,7 @@ LatentVecchia::Block& LatentVecchia::GetBlock(int which, int t, int pmax) {
     const size_t nt = (size_t)n_ * t;
     for (auto* buf : {&b.R, &b.Z, &b.H, &b.V, &b.G, &b.Xt}) buf->alloc(nt);
     b.small.alloc((size_t)6 * t);
+    b.act.alloc(t);
     b.t = t;
   }
   if (b.a_hist.size() < (size_t)pmax * t) {
@@ -376,28 +377,31 @@ void LatentVecchia::Scalars(const ScalarArgs& a, double* out) {
   std::copy(h_out_, h_out_ + kLatentScalars, out);
 }
 
-int LatentVecchia::Pcg(Block& b, const double* RHS, double* U, bool init_zero, bool u_is_zero, int pmax,
-                       double delta, bool tridiag, bool* nan, bool* zero_rhs) {
+LatentVecchia::PcgResult LatentVecchia::Pcg(Block& b, const double* RHS, double* U, int n_single, bool init_zero,
+                                             bool u_is_zero, int pmax_single, int pmax_block, double delta) {
   const int t = b.t;
   const size_t nt = (size_t)n_ * t;
+  PcgResult res;
   if (h_rr_.size() < (size_t)t) h_rr_.resize(t);
-  *nan = false;
-  *zero_rhs = false;
-  pmax = std::min(pmax, n_);
-  if (!tridiag) {
+  pmax_single = std::min(pmax_single, n_);
+  pmax_block = std::min(pmax_block, n_);
+  if (t == 1 && n_single == 1) {
     if (Dot1(RHS, RHS) < kZeroRhsSq) {   // CG_utils.cpp:42-45
       HIP_CHECK(hipMemsetAsync(U, 0, sizeof(double) * nt, s_));
-      *zero_rhs = true;
-      return 0;
+      res.zero_rhs = true;
+      return res;
     }
   }
-  if (tridiag || init_zero || u_is_zero) {
-    HIP_CHECK(hipMemsetAsync(U, 0, sizeof(double) * nt, s_));
-    launch_copy(nt, RHS, b.R.get(), s_);
-  } else {   // r = rhs - A u (warm start, CG_utils.cpp:53-55)
+  if (t == 1 && n_single == 1 && !init_zero && !u_is_zero) {   // r = rhs - A u (warm start, CG_utils.cpp:53-55)
     ApplyA(U, b.V.get(), b.G.get(), t);
     launch_axpby(nt, 1., RHS, -1., b.V.get(), b.R.get(), s_);
+  } else {
+    HIP_CHECK(hipMemsetAsync(U, 0, sizeof(double) * nt, s_));
+    launch_copy(nt, RHS, b.R.get(), s_);
   }
+  std::vector<int> act(t, 1);
+  HIP_CHECK(hipMemcpyAsync(b.act.get(), act.data(), sizeof(int) * t, hipMemcpyHostToDevice, s_));
+  bool act_s = n_single > 0 && pmax_single > 0, act_b = n_single < t && pmax_block > 0;
   Precond(b.R.get(), b.Z.get(), b.Xt.get(), t);
   launch_copy(nt, b.Z.get(), b.H.get(), s_);
   {
@@ -405,36 +409,54 @@ int LatentVecchia::Pcg(Block& b, const double* RHS, double* U, bool init_zero, b
     const double* Bm[1] = {b.Z.get()};
     launch_coldots(n_, t, 1, A, Bm, d_partials_.get(), b.rz(), s_);
   }
-  int j = 0;
-  for (; j < pmax; ++j) {
+  for (int j = 0; act_s || act_b; ++j) {
     ApplyA(b.H.get(), b.V.get(), b.G.get(), t);
     {
       const double* A[1] = {b.H.get()};
       const double* Bm[1] = {b.V.get()};
       launch_coldots(n_, t, 1, A, Bm, d_partials_.get(), b.hv(), s_);
     }
-    launch_cg_alpha(t, b.rz(), b.hv(), b.a(), tridiag ? b.a_hist.get() + (size_t)j * t : nullptr, s_);
+    launch_cg_alpha(t, b.rz(), b.hv(), b.act.get(), b.a(), b.a_hist.get() + (size_t)j * t, s_);
     launch_cg_update(n_, t, b.a(), b.H.get(), b.V.get(), U, b.R.get(), d_partials_.get(), b.rr(), s_);
     HIP_CHECK(hipMemcpyAsync(h_rr_.data(), b.rr(), sizeof(double) * t, hipMemcpyDeviceToHost, s_));
     HIP_CHECK(hipStreamSynchronize(s_));
-    double norm = 0.;
-    for (int c = 0; c < t; ++c) norm += std::sqrt(h_rr_[c]);
-    norm /= t;   // t = 1: ||r||; block: mean column norm (CG_utils.cpp:172)
-    if (std::isnan(norm) || std::isinf(norm)) {
-      *nan = true;
-      return j + 1;
+    bool changed = false;
+    if (act_s) {   // single-vector CGs: own ||r|| (CG_utils.cpp:80-90)
+      res.its_single = j + 1;
+      bool all_done = true;
+      for (int c = 0; c < n_single; ++c) {
+        if (!act[c]) continue;
+        const double norm = std::sqrt(h_rr_[c]);
+        if (std::isnan(norm) || std::isinf(norm)) { res.nan = true; return res; }
+        if (norm < delta || j + 1 >= pmax_single) { act[c] = 0; changed = true; }
+        else all_done = false;
+      }
+      act_s = !all_done;
     }
-    if (norm < delta) return j + 1;
+    if (act_b) {   // block: mean column ||r|| (CG_utils.cpp:172-178)
+      res.its_block = j + 1;
+      double norm = 0.;
+      for (int c = n_single; c < t; ++c) norm += std::sqrt(h_rr_[c]);
+      norm /= (t - n_single);
+      if (std::isnan(norm) || std::isinf(norm)) { res.nan = true; return res; }
+      if (norm < delta || j + 1 >= pmax_block) {
+        for (int c = n_single; c < t; ++c) act[c] = 0;
+        act_b = false;
+        changed = true;
+      }
+    }
+    if (!act_s && !act_b) break;
+    if (changed) HIP_CHECK(hipMemcpyAsync(b.act.get(), act.data(), sizeof(int) * t, hipMemcpyHostToDevice, s_));
     Precond(b.R.get(), b.Z.get(), b.Xt.get(), t);
     {
       const double* A[1] = {b.R.get()};
       const double* Bm[1] = {b.Z.get()};
       launch_coldots(n_, t, 1, A, Bm, d_partials_.get(), b.rz_new(), s_);
     }
-    launch_cg_beta(t, b.rz_new(), b.rz(), b.b(), tridiag ? b.b_hist.get() + (size_t)j * t : nullptr, s_);
+    launch_cg_beta(t, b.rz_new(), b.rz(), b.act.get(), b.b(), b.b_hist.get() + (size_t)j * t, s_);
     launch_h_update(n_, t, b.b(), b.Z.get(), b.H.get(), s_);
   }
-  return j;
+  return res;
 }
 
 LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, double aux, const IterativeConfig& cfg,
@@ -505,28 +527,12 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
   const bool info_changes = !gauss;              // information_changes_during/after_mode_finding_
   const int maxit = gauss ? 1 : 1000;            // maxit_mode_newton_ (likelihoods.h:255, 12721)
   const int max_shrink = gauss ? 1 : 20;         // max_number_lr_shrinkage_steps_newton_ (:256, 12725)
-  bool upd_zero = true;
-  for (int it = 0; it < maxit; ++it) {
-    NewtonPrepArgs np{};
-    np.n = n; np.lik = lik; np.aux = aux; np.y = d_y_.get(); np.loc = d_mode_.get(); np.mode = d_mode_.get();
-    np.Dinv = d_Dinv_.get(); np.d1 = d_d1_.get(); np.W = d_W_.get();
-    np.W_update = (it == 0 || info_changes) ? 1 : 0;
-    np.rhs = d_rhs_.get();
-    np.dw = (it == 0 || info_changes) ? d_dw_.get() : nullptr;
-    launch_newton_prep(np, s_);
-    bool nan = false, zr = false;
-    const int its = Pcg(b1, d_rhs_.get(), d_mode_upd_.get(), it == 0, upd_zero, cfg.cg_max_num_it, cfg.cg_delta_conv,
-                        false, &nan, &zr);
-    res.cg_its += its;
-    upd_zero = zr;
-    if (nan) Fatal("NaN or Inf occurred in the conjugate gradient algorithm during mode finding");
-    // Armijo (likelihoods.h:2957-2966): only consulted when more than one step size is tried
-    double gdd = 0.;
-    if (max_shrink > 1) {
-      launch_axpby(n, 1., d_mode_upd_.get(), -1., d_mode_.get(), d_dir_.get(), s_);
-      ApplyA(d_dir_.get(), d_Adir_.get(), b1.G.get(), 1);
-      gdd = Dot1(d_dir_.get(), d_Adir_.get());
-    }
+  const int pmax_tri = std::max(1, std::min(cfg.cg_max_num_it_tridiag, n));
+  const int cg_max = std::max(0, cfg.cg_max_num_it);
+  Block* bslq = nullptr;
+  int n_lead = 0;   // leading non-probe columns of the SLQ block
+  PcgResult slq;
+  auto line_search_and_check = [&](int it, double gdd) -> bool {   // likelihoods.h:2967-2995, 11820-11870
     double lr = 1., mll_new = mll;
     for (int ih = 0; ih < max_shrink; ++ih) {
       if (ih == 0) launch_copy(n, d_mode_upd_.get(), d_mode_new_.get(), s_);
@@ -539,50 +545,96 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
     }
     std::swap(d_mode_, d_mode_new_);
     res.newton_its = it + 1;
-    // CheckConvergenceModeFinding (likelihoods.h:11820-11870)
     if (std::isnan(mll_new) || std::isinf(mll_new))
       Fatal("NaN or Inf occurred in the mode finding algorithm for the Laplace approximation");
     const double dc = cfg.delta_conv_mode_finding;
     const bool term = (it == 0) ? std::fabs(mll_new - mll) < dc * std::fabs(mll) : (mll_new - mll) < dc * std::fabs(mll);
     mll = mll_new;
-    if (term) break;
-  }
-  {   // derivative / information at the mode, VADU diagonal and its square root (:3000-3005, 12163-12166)
+    return term;
+  };
+  EnsureProbes(cfg);
+  if (gauss) {
+    // Gaussian: W = 1/aux does not depend on the mode, so the single Newton step's solve
+    // (Sigma^-1 + W)^-1 (y / aux) and the SLQ block solve the same system. Both run as one
+    // PCG over 1 + t columns: column 0 keeps the single-vector stopping rule, columns 1..t
+    // the block rule (each column's iterates are exactly those of a separate run).
     NewtonPrepArgs np{};
     np.n = n; np.lik = lik; np.aux = aux; np.y = d_y_.get(); np.loc = d_mode_.get(); np.mode = d_mode_.get();
-    np.Dinv = d_Dinv_.get(); np.d1 = d_d1_.get(); np.W = d_W_.get();
-    np.W_update = info_changes ? 1 : 0;
-    np.dw = d_dw_.get();
-    np.sdw = d_sdw_.get();
+    np.Dinv = d_Dinv_.get(); np.d1 = d_d1_.get(); np.W = d_W_.get(); np.W_update = 1;
+    np.rhs = d_rhs_.get(); np.dw = d_dw_.get(); np.sdw = d_sdw_.get();
     launch_newton_prep(np, s_);
+    n_lead = 1;
+    const int tf = t + 1;
+    bslq = &GetBlock(1, tf, std::max(pmax_tri, cg_max));
+    d_rhsf_.alloc((size_t)n * tf);
+    d_Uf_.alloc((size_t)n * tf);
+    // z_i = B^T (D^-1 + W)^(1/2) r_i into columns 1..t, y / aux into column 0
+    launch_bt_apply(sp_, d_Bv_.get(), true, d_probes_.get(), t, d_sdw_.get(), nullptr, nullptr, d_Zp_.get(), s_);
+    launch_pack_columns(n, t, d_Zp_.get(), t, 0, d_rhsf_.get(), tf, 1, s_);
+    launch_pack_columns(n, 1, d_rhs_.get(), 1, 0, d_rhsf_.get(), tf, 0, s_);
+    slq = Pcg(*bslq, d_rhsf_.get(), d_Uf_.get(), 1, true, true, cg_max, pmax_tri, cfg.cg_delta_conv);
+    if (slq.nan) Fatal("NaN or Inf occurred in the conjugate gradient algorithm (mode finding / log-determinant)");
+    res.cg_its = slq.its_single;
+    launch_pack_columns(n, 1, d_Uf_.get(), tf, 0, d_mode_upd_.get(), 1, 0, s_);
+    launch_pack_columns(n, t, d_Uf_.get(), tf, 1, d_U_.get(), t, 0, s_);
+    line_search_and_check(0, 0.);
+  } else {
+    // ---- 2. mode finding (likelihoods.h:2780-3000)
+    bool upd_zero = true;
+    for (int it = 0; it < maxit; ++it) {
+      NewtonPrepArgs np{};
+      np.n = n; np.lik = lik; np.aux = aux; np.y = d_y_.get(); np.loc = d_mode_.get(); np.mode = d_mode_.get();
+      np.Dinv = d_Dinv_.get(); np.d1 = d_d1_.get(); np.W = d_W_.get();
+      np.W_update = 1;
+      np.rhs = d_rhs_.get();
+      np.dw = d_dw_.get();
+      launch_newton_prep(np, s_);
+      const PcgResult pr = Pcg(b1, d_rhs_.get(), d_mode_upd_.get(), 1, it == 0, upd_zero, cg_max, 0, cfg.cg_delta_conv);
+      res.cg_its += pr.its_single;
+      upd_zero = pr.zero_rhs;
+      if (pr.nan) Fatal("NaN or Inf occurred in the conjugate gradient algorithm during mode finding");
+      // Armijo (likelihoods.h:2957-2966)
+      launch_axpby(n, 1., d_mode_upd_.get(), -1., d_mode_.get(), d_dir_.get(), s_);
+      ApplyA(d_dir_.get(), d_Adir_.get(), b1.G.get(), 1);
+      const double gdd = Dot1(d_dir_.get(), d_Adir_.get());
+      if (line_search_and_check(it, gdd)) break;
+    }
+    {   // derivative / information at the mode, VADU diagonal and its square root (:3000-3005, 12163-12166)
+      NewtonPrepArgs np{};
+      np.n = n; np.lik = lik; np.aux = aux; np.y = d_y_.get(); np.loc = d_mode_.get(); np.mode = d_mode_.get();
+      np.Dinv = d_Dinv_.get(); np.d1 = d_d1_.get(); np.W = d_W_.get();
+      np.W_update = info_changes ? 1 : 0;
+      np.dw = d_dw_.get();
+      np.sdw = d_sdw_.get();
+      launch_newton_prep(np, s_);
+    }
+    // ---- 3. SLQ block (likelihoods.h:3018-3045, 12155-12212): z_i = B^T (D^-1 + W)^(1/2) r_i
+    bslq = &GetBlock(1, t, pmax_tri);
+    launch_bt_apply(sp_, d_Bv_.get(), true, d_probes_.get(), t, d_sdw_.get(), nullptr, nullptr, d_Zp_.get(), s_);
+    slq = Pcg(*bslq, d_Zp_.get(), d_U_.get(), 0, true, true, 0, pmax_tri, cfg.cg_delta_conv);
+    if (slq.nan) Fatal("NaN or Inf occurred in the stochastic Lanczos quadrature (log-determinant)");
   }
-
-  // ---- 3. SLQ log-determinant (likelihoods.h:3018-3045, 12155-12212)
-  EnsureProbes(cfg);
-  const int pmax_tri = std::max(1, std::min(cfg.cg_max_num_it_tridiag, n));
-  Block& bt = GetBlock(1, t, pmax_tri);
-  // z_i = B^T (D^-1 + W)^(1/2) r_i
-  launch_bt_apply(sp_, d_Bv_.get(), true, d_probes_.get(), t, d_sdw_.get(), nullptr, nullptr, d_Zp_.get(), s_);
-  bool nan = false, zr = false;
-  const int L = Pcg(bt, d_Zp_.get(), d_U_.get(), true, true, pmax_tri, cfg.cg_delta_conv, true, &nan, &zr);
-  if (nan) Fatal("NaN or Inf occurred in the stochastic Lanczos quadrature (log-determinant)");
+  Block& bt = *bslq;
+  const int L = slq.its_block;
   res.lanczos_steps = L;
-  std::vector<double> ah((size_t)L * t), bh((size_t)L * t);
+  const int tb = bt.t;
+  std::vector<double> ah((size_t)L * tb), bh((size_t)L * tb);
   HIP_CHECK(hipMemcpyAsync(ah.data(), bt.a_hist.get(), sizeof(double) * ah.size(), hipMemcpyDeviceToHost, s_));
   if (L > 1)
-    HIP_CHECK(hipMemcpyAsync(bh.data(), bt.b_hist.get(), sizeof(double) * (size_t)(L - 1) * t, hipMemcpyDeviceToHost,
+    HIP_CHECK(hipMemcpyAsync(bh.data(), bt.b_hist.get(), sizeof(double) * (size_t)(L - 1) * tb, hipMemcpyDeviceToHost,
                              s_));
   sa.mode = d_mode_.get();
   sa.dw = d_dw_.get();
   Scalars(sa, sc);   // synchronises the stream
   std::vector<std::vector<double>> Td(t), Ts(t);
   for (int c = 0; c < t; ++c) {   // CG_utils.cpp:200-206 (a_old = 1, b_old = 0 before the first step)
+    const int cc = c + n_lead;
     Td[c].resize(L);
     Ts[c].resize(L > 0 ? L - 1 : 0);
     for (int j = 0; j < L; ++j) {
-      const double a = ah[(size_t)j * t + c];
-      const double a_old = j > 0 ? ah[(size_t)(j - 1) * t + c] : 1.;
-      const double b_old = j > 0 ? bh[(size_t)(j - 1) * t + c] : 0.;
+      const double a = ah[(size_t)j * tb + cc];
+      const double a_old = j > 0 ? ah[(size_t)(j - 1) * tb + cc] : 1.;
+      const double b_old = j > 0 ? bh[(size_t)(j - 1) * tb + cc] : 0.;
       Td[c][j] = 1. / a + b_old / a_old;
       if (j > 0) Ts[c][j - 1] = std::sqrt(b_old) / a_old;
     }
@@ -600,10 +652,9 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
       md.n = n; md.m = m_; md.t = t; md.lik = lik; md.nbr = d_nbr_.get(); md.Bv = d_Bv_.get(); md.dw = d_dw_.get();
       md.loc = d_mode_.get(); md.U = d_U_.get(); md.P = d_P_.get(); md.dmll = d_dmll_.get();
       launch_mode_deriv(md, s_);
-      bool nan2 = false, zr2 = false;
-      res.cg_its += Pcg(b1, d_dmll_.get(), d_vS_.get(), true, true, cfg.cg_max_num_it, cfg.cg_delta_conv, false, &nan2,
-                        &zr2);
-      if (nan2) Warning("NaN or Inf occurred in the conjugate gradient algorithm of the gradient calculation");
+      const PcgResult pv = Pcg(b1, d_dmll_.get(), d_vS_.get(), 1, true, true, cg_max, 0, cfg.cg_delta_conv);
+      res.cg_its += pv.its_single;
+      if (pv.nan) Warning("NaN or Inf occurred in the conjugate gradient algorithm of the gradient calculation");
     }
     GradColsArgs ga{};
     ga.n = n; ga.m = m_; ga.t = t; ga.nbr = d_nbr_.get(); ga.Bv = d_Bv_.get(); ga.dBv = d_dBv_.get();

@@ -65,7 +65,8 @@ class LatentVecchia {
     int t = 0;
     DevBuf<double> R, Z, H, V, G, Xt;     // n x t
     DevBuf<double> small;                 // rz, rz_new, hv, rr, a, b: 6 x t
-    DevBuf<double> a_hist, b_hist;        // pmax x t (Lanczos coefficients)
+    DevBuf<double> a_hist, b_hist;        // pmax x t (CG coefficients per iteration)
+    DevBuf<int> act;                      // per-column activity mask
     double* rz() const { return small.get(); }
     double* rz_new() const { return small.get() + t; }
     double* hv() const { return small.get() + 2 * t; }
@@ -80,10 +81,17 @@ class LatentVecchia {
   void ApplyA(const double* H, double* V, double* G, int t);
   void Precond(const double* R, double* Z, double* Xt, int t);
   void PrecondImpl(const double* R, double* Z, double* Xt, int t);
-  // PCG on t columns (CG_utils.cpp:21-108 for t = 1, :110-217 with tridiag). Returns the
-  // number of iterations; *nan on NaN/Inf residual; *zero_rhs for the zero-RHS shortcut.
-  int Pcg(Block& b, const double* RHS, double* U, bool init_zero, bool u_is_zero, int pmax, double delta,
-          bool tridiag, bool* nan, bool* zero_rhs);
+  // PCG on the b.t columns of RHS sharing every operator application. Columns [0, n_single)
+  // are independent single-vector CGs (CG_utils.cpp:21-108: own ||r|| < delta, warm start
+  // allowed when t == 1); columns [n_single, t) are the block of CGTridiagVecchiaLaplace
+  // (:110-217: mean ||r|| < delta). Stopped columns are frozen (a = b = 0). The per-
+  // iteration coefficients land in b.a_hist / b.b_hist (Lanczos tridiagonals).
+  struct PcgResult {
+    int its_single = 0, its_block = 0;
+    bool nan = false, zero_rhs = false;
+  };
+  PcgResult Pcg(Block& b, const double* RHS, double* U, int n_single, bool init_zero, bool u_is_zero,
+                int pmax_single, int pmax_block, double delta);
   void Scalars(const ScalarArgs& a, double* out);
   double Dot1(const double* x, const double* y);   // single-vector dot, synchronous
 
@@ -110,6 +118,7 @@ class LatentVecchia {
   DevBuf<double> d_y_, d_Bv_, d_dBv_, d_Dinv_, d_dD_, d_W_, d_dw_, d_sdw_, d_d1_;
   DevBuf<double> d_mode_, d_mode_upd_, d_mode_new_, d_rhs_, d_dir_, d_Adir_, d_vS_, d_dmll_;
   DevBuf<double> d_probes_, d_Zp_, d_U_, d_P_;   // n x t
+  DevBuf<double> d_rhsf_, d_Uf_;                 // n x (1 + t): mode column fused with the probes (gaussian)
   int probes_t_ = 0;
   uint64_t probe_run_id_ = 0;                    // cg_generator_counter_ (likelihoods.h:12800)
   bool probes_saved_ = false;

@@ -103,9 +103,15 @@ void launch_cg_update(int n, int t, const double* a, const double* H, const doub
                       double* partials, double* rr, hipStream_t s);
 // H = Z + b .* H
 void launch_h_update(int n, int t, const double* b, const double* Z, double* H, hipStream_t s);
-// a = rz / hv (hist[it*t + c] = a)  |  b = rz_new / rz, rz = rz_new (hist[it*t + c] = b)
-void launch_cg_alpha(int t, const double* rz, const double* hv, double* a, double* hist, hipStream_t s);
-void launch_cg_beta(int t, const double* rz_new, double* rz, double* b, double* hist, hipStream_t s);
+// a = rz / hv (hist[it*t + c] = a)  |  b = rz_new / rz, rz = rz_new (hist[it*t + c] = b);
+// act (nullable): per-column activity mask, inactive columns get a = b = 0 (frozen)
+void launch_cg_alpha(int t, const double* rz, const double* hv, const int* act, double* a, double* hist,
+                     hipStream_t s);
+void launch_cg_beta(int t, const double* rz_new, double* rz, const int* act, double* b, double* hist,
+                    hipStream_t s);
+// dst[i*ld_dst + c_dst + c] = src[i*ld_src + c_src + c], c < ncols (row-major column blocks)
+void launch_pack_columns(int n, int ncols, const double* src, int ld_src, int c_src, double* dst, int ld_dst,
+                         int c_dst, hipStream_t s);
 // Y = X (n x t copy)
 void launch_copy(size_t count, const double* X, double* Y, hipStream_t s);
 // Z = alpha X + beta Y (elementwise, count entries; Z may alias X or Y)

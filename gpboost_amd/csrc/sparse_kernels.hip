@@ -209,21 +209,35 @@ __global__ void axpby_kernel(size_t total, double alpha, const double* X, double
     Z[o] = alpha * X[o] + beta * Y[o];
 }
 
-__global__ void cg_alpha_kernel(int t, const double* rz, const double* hv, double* a, double* hist) {
+// Columns whose CG has stopped (act[c] == 0) get a = b = 0: their U and R stay frozen.
+__global__ void cg_alpha_kernel(int t, const double* rz, const double* hv, const int* act, double* a, double* hist) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= t) return;
-  const double v = rz[c] / hv[c];
+  const double v = (act == nullptr || act[c]) ? rz[c] / hv[c] : 0.;
   a[c] = v;
   if (hist) hist[c] = v;
 }
 
-__global__ void cg_beta_kernel(int t, const double* rz_new, double* rz, double* b, double* hist) {
+__global__ void cg_beta_kernel(int t, const double* rz_new, double* rz, const int* act, double* b, double* hist) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= t) return;
+  if (act != nullptr && !act[c]) {
+    b[c] = 0.;
+    return;
+  }
   const double v = rz_new[c] / rz[c];
   rz[c] = rz_new[c];
   b[c] = v;
   if (hist) hist[c] = v;
+}
+
+__global__ void pack_columns_kernel(size_t rows, int ncols, const double* __restrict__ src, int ld_src, int c_src,
+                                   double* __restrict__ dst, int ld_dst, int c_dst) {
+  const size_t total = rows * ncols;
+  for (size_t o = (size_t)blockIdx.x * kBT + threadIdx.x; o < total; o += (size_t)gridDim.x * kBT) {
+    const size_t i = o / ncols, c = o - i * ncols;
+    dst[i * ld_dst + c_dst + c] = src[i * ld_src + c_src + c];
+  }
 }
 
 // ------------------------------------------------------------------ likelihoods
@@ -505,6 +519,17 @@ void launch_h_update(int n, int t, const double* b, const double* Z, double* H, 
   HIP_CHECK(hipGetLastError());
 }
 
+void launch_pack_columns(int n, int ncols, const double* src, int ld_src, int c_src, double* dst, int ld_dst,
+                         int c_dst, hipStream_t s) {
+  const size_t total = (size_t)n * ncols;
+  int g = (int)((total + kBT - 1) / kBT);
+  if (g > kMaxGridX) g = kMaxGridX;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(pack_columns_kernel, dim3(g), dim3(kBT), 0, s, (size_t)n, ncols, src, ld_src, c_src, dst, ld_dst,
+                     c_dst);
+  HIP_CHECK(hipGetLastError());
+}
+
 void launch_copy(size_t count, const double* X, double* Y, hipStream_t s) {
   int g = (int)((count + kBT - 1) / kBT);
   if (g > kMaxGridX) g = kMaxGridX;
@@ -522,13 +547,15 @@ void launch_axpby(size_t count, double alpha, const double* X, double beta, cons
   HIP_CHECK(hipGetLastError());
 }
 
-void launch_cg_alpha(int t, const double* rz, const double* hv, double* a, double* hist, hipStream_t s) {
-  hipLaunchKernelGGL(cg_alpha_kernel, dim3((t + 63) / 64), dim3(64), 0, s, t, rz, hv, a, hist);
+void launch_cg_alpha(int t, const double* rz, const double* hv, const int* act, double* a, double* hist,
+                     hipStream_t s) {
+  hipLaunchKernelGGL(cg_alpha_kernel, dim3((t + 63) / 64), dim3(64), 0, s, t, rz, hv, act, a, hist);
   HIP_CHECK(hipGetLastError());
 }
 
-void launch_cg_beta(int t, const double* rz_new, double* rz, double* b, double* hist, hipStream_t s) {
-  hipLaunchKernelGGL(cg_beta_kernel, dim3((t + 63) / 64), dim3(64), 0, s, t, rz_new, rz, b, hist);
+void launch_cg_beta(int t, const double* rz_new, double* rz, const int* act, double* b, double* hist,
+                    hipStream_t s) {
+  hipLaunchKernelGGL(cg_beta_kernel, dim3((t + 63) / 64), dim3(64), 0, s, t, rz_new, rz, act, b, hist);
   HIP_CHECK(hipGetLastError());
 }
 

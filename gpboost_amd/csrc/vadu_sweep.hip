@@ -261,6 +261,12 @@ __global__ void __launch_bounds__(NW * 64) vadu_levelT_kernel(LevelPlan lp, int 
     e1 = lp.beoff[p + 1];
   }
   const int cc = c < t ? c : t - 1;   // lanes beyond t gather a valid column, result unused
+  // the row's own input is loaded up front, next to the structure loads (no extra round trip)
+  double x = 0.;
+  if (wave == 0) {
+    x = in[(size_t)i * t + cc];
+    if (LOWER) x /= dw[i];
+  }
   constexpr int B = 16;
   double acc = 0.;
   for (int e = e0 + wave; e < e1; e += NW * B) {
@@ -283,8 +289,6 @@ __global__ void __launch_bounds__(NW * 64) vadu_levelT_kernel(LevelPlan lp, int 
     double sum = red[0][lane];
 #pragma unroll
     for (int w = 1; w < NW; ++w) sum += red[w][lane];
-    double x = in[(size_t)i * t + c];
-    if (LOWER) x /= dw[i];
     X[(size_t)i * t + c] = x - sum;
   }
 }
