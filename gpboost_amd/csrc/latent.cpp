@@ -208,7 +208,7 @@ void LatentVecchia::BuildSweepPlan(const int* nbr, const std::vector<int>& tptr,
     }
   };
   std::vector<int> idx, slot;
-  std::vector<int> lrows, beoff(1, 0), beidx, beslot, fidx, fslot;
+  std::vector<int> lrows, beoff(1, 0), beidx, beslot, fidx, fslot, crit;
   lplan_.lptr.assign(1, 0);
   for (int phase = 0; phase < 2; ++phase) {
     const bool lower = phase == 1;
@@ -223,6 +223,14 @@ void LatentVecchia::BuildSweepPlan(const int* nbr, const std::vector<int>& tptr,
       for (int r : rows) {
         entries_of(lower, r, idx, slot);
         lrows.push_back(r);
+        {   // the dependency finished last in level order: the sync-free solve polls it first
+          int best = -1, bl = -1;
+          for (int d : idx) {
+            const int dl = lev[d];
+            if (dl > bl) { bl = dl; best = d; }
+          }
+          crit.push_back(best);
+        }
         if (lower) {   // fixed stride m, zero-value padding (slot -1)
           for (int q = 0; q < m; ++q) {
             fidx.push_back(q < (int)idx.size() ? idx[q] : 0);
@@ -285,6 +293,9 @@ void LatentVecchia::BuildSweepPlan(const int* nbr, const std::vector<int>& tptr,
   lslot.insert(lslot.end(), fslot.begin(), fslot.end());
   lplan_entries_ = (int)lslot.size();
   d_lrows_.alloc(lrows.size());
+  h_crit_ = crit;
+  d_crit_.alloc(crit.size());
+  HIP_CHECK(hipMemcpyAsync(d_crit_.get(), crit.data(), sizeof(int) * crit.size(), hipMemcpyHostToDevice, s_));
   d_beoff_.alloc(beoff.size());
   d_beidx_.alloc(std::max<size_t>(beidx.size(), 1));
   d_fidx_.alloc(std::max<size_t>(fidx.size(), 1));
@@ -305,6 +316,16 @@ void LatentVecchia::BuildSweepPlan(const int* nbr, const std::vector<int>& tptr,
   lplan_.fidx = d_fidx_.get();
   lplan_.fval = d_lval_.get() + beslot.size();
   use_graph_ = std::getenv("GPBOOST_AMD_SWEEP_KERNEL") == nullptr;
+  if (const char* pm = std::getenv("GPBOOST_AMD_PRECOND")) precond_mode_ = std::atoi(pm);
+  if (!use_graph_) precond_mode_ = 2;
+  {
+    int dev = 0, cus = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    max_flow_blocks_ = 2 * std::max(cus, 1);   // 2 x 256-thread blocks per CU: all resident
+  }
+  d_err_.alloc(4);
+  HIP_CHECK(hipMemsetAsync(d_err_.get(), 0, sizeof(int) * 4, s_));
   plan_.nsteps = (int)step_off.size();
   plan_.first_words = step_off.empty() ? 0 : blob[3];
   // each LDS buffer is a whole number of 64-word wave slices (staging writes full slices)
@@ -335,7 +356,34 @@ void LatentVecchia::Precond(const double* R, double* Z, double* Xt, int t) {
 }
 
 void LatentVecchia::PrecondImpl(const double* R, double* Z, double* Xt, int t) {
-  if (!use_graph_) {
+  if (precond_mode_ == 0) {
+    FlowArgs fa{};
+    fa.n = n_;
+    fa.m = m_;
+    fa.t = t;
+    fa.err = d_err_.get();
+    fa.prof = prof_;
+    fa.lrows = lplan_.lrows;              // B^T solve: Xt = B^-T R
+    fa.crit = d_crit_.get();
+    fa.eoff = lplan_.beoff;
+    fa.eidx = lplan_.beidx;
+    fa.eval = lplan_.beval;
+    fa.in = R;
+    fa.X = Xt;
+    launch_vadu_flow(fa, false, max_flow_blocks_, s_);
+    fa.lrows = lplan_.lrows + n_;         // lower solve: Z = ((D^-1 + W) B)^-1 Xt
+    fa.crit = d_crit_.get() + n_;
+    fa.eoff = nullptr;
+    fa.eidx = lplan_.fidx;
+    fa.eval = lplan_.fval;
+    fa.dw = d_dw_.get();
+    fa.in = Xt;
+    fa.X = Z;
+    if (prof_) fa.prof = prof_ + (size_t)n_ * 4;
+    launch_vadu_flow(fa, true, max_flow_blocks_, s_);
+    return;
+  }
+  if (precond_mode_ == 2) {
     launch_vadu_sweep(plan_, d_dw_.get(), R, Xt, Z, t, s_);
     return;
   }
@@ -359,6 +407,16 @@ void LatentVecchia::PrecondImpl(const double* R, double* Z, double* Xt, int t) {
   HIP_CHECK(hipGraphDestroy(graph));
   graphs_.push_back(e);
   HIP_CHECK(hipGraphLaunch(e.exec, s_));
+}
+
+// A bounded spin of the sync-free solves gave up (a dependency never arrived): fail loudly.
+void LatentVecchia::CheckSolveError() {
+  int err = 0;
+  HIP_CHECK(hipMemcpy(&err, d_err_.get(), sizeof(int), hipMemcpyDeviceToHost));
+  if (err) {
+    HIP_CHECK(hipMemset(d_err_.get(), 0, sizeof(int)));
+    Fatal("VADU triangular solve did not complete (dependency wait timed out)");
+  }
 }
 
 double LatentVecchia::Dot1(const double* x, const double* y) {
@@ -427,7 +485,7 @@ LatentVecchia::PcgResult LatentVecchia::Pcg(Block& b, const double* RHS, double*
       for (int c = 0; c < n_single; ++c) {
         if (!act[c]) continue;
         const double norm = std::sqrt(h_rr_[c]);
-        if (std::isnan(norm) || std::isinf(norm)) { res.nan = true; return res; }
+        if (std::isnan(norm) || std::isinf(norm)) { CheckSolveError(); res.nan = true; return res; }
         if (norm < delta || j + 1 >= pmax_single) { act[c] = 0; changed = true; }
         else all_done = false;
       }
@@ -438,7 +496,7 @@ LatentVecchia::PcgResult LatentVecchia::Pcg(Block& b, const double* RHS, double*
       double norm = 0.;
       for (int c = n_single; c < t; ++c) norm += std::sqrt(h_rr_[c]);
       norm /= (t - n_single);
-      if (std::isnan(norm) || std::isinf(norm)) { res.nan = true; return res; }
+      if (std::isnan(norm) || std::isinf(norm)) { CheckSolveError(); res.nan = true; return res; }
       if (norm < delta || j + 1 >= pmax_block) {
         for (int c = n_single; c < t; ++c) act[c] = 0;
         act_b = false;
@@ -508,6 +566,27 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
       HIP_CHECK(hipEventElapsedTime(&pm, ev0_, ev1_));
       std::fprintf(stderr, "[precond bench] t=%d: %.3f ms per application (%d levels)\n", tt, pm / 20,
                    lplan_.nlev);
+      if (const char* path = std::getenv("GPBOOST_AMD_FLOW_PROF")) {   // per-row timestamps of one application
+        DevBuf<unsigned long long> prof((size_t)2 * n * 4);
+        HIP_CHECK(hipMemsetAsync(prof.get(), 0, sizeof(unsigned long long) * 2 * n * 4, s_));
+        prof_ = prof.get();
+        Precond(bb.R.get(), bb.Z.get(), bb.Xt.get(), tt);
+        prof_ = nullptr;
+        std::vector<unsigned long long> h((size_t)2 * n * 4);
+        HIP_CHECK(hipMemcpy(h.data(), prof.get(), sizeof(unsigned long long) * h.size(), hipMemcpyDeviceToHost));
+        std::string fn = std::string(path) + "_t" + std::to_string(tt) + ".bin";
+        if (FILE* f = std::fopen(fn.c_str(), "wb")) {
+          int hdr[4] = {n, lplan_.nlev_b, lplan_.nlev, tt};
+          std::fwrite(hdr, sizeof(int), 4, f);
+          std::fwrite(lplan_.lptr.data(), sizeof(int), lplan_.lptr.size(), f);
+          std::fwrite(h_crit_.data(), sizeof(int), h_crit_.size(), f);
+          std::vector<int> lr((size_t)2 * n);
+          HIP_CHECK(hipMemcpy(lr.data(), lplan_.lrows, sizeof(int) * lr.size(), hipMemcpyDeviceToHost));
+          std::fwrite(lr.data(), sizeof(int), lr.size(), f);
+          std::fwrite(h.data(), sizeof(unsigned long long), h.size(), f);
+          std::fclose(f);
+        }
+      }
     }
   }
   ScalarArgs sa{};
@@ -713,6 +792,7 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
   }
   HIP_CHECK(hipEventRecord(ev1_, s_));
   HIP_CHECK(hipEventSynchronize(ev1_));
+  CheckSolveError();
   float ms = 0.f;
   HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_));
   res.ms_total = ms;

@@ -93,7 +93,8 @@ class LatentVecchia {
   PcgResult Pcg(Block& b, const double* RHS, double* U, int n_single, bool init_zero, bool u_is_zero,
                 int pmax_single, int pmax_block, double delta);
   void Scalars(const ScalarArgs& a, double* out);
-  double Dot1(const double* x, const double* y);   // single-vector dot, synchronous
+  double Dot1(const double* x, const double* y);
+  void CheckSolveError();   // single-vector dot, synchronous
 
   int n_, d_, m_;
   const double* d_X_;
@@ -107,12 +108,18 @@ class LatentVecchia {
   int plan_entries_ = 0;
   // level-by-level form replayed as hipGraphs (one per (R, Y, Z, t) buffer set)
   LevelPlan lplan_{};
+  DevBuf<int> d_crit_;
+  std::vector<int> h_crit_;
+  unsigned long long* prof_ = nullptr;   // diagnostics: flow-kernel timestamps
   DevBuf<int> d_lrows_, d_beoff_, d_beidx_, d_fidx_, d_lslot_;
   DevBuf<double> d_lval_;
   int lplan_entries_ = 0;
   struct GraphEntry { const void* key[3]; int t; hipGraphExec_t exec; };
   std::vector<GraphEntry> graphs_;
   bool use_graph_ = true;
+  int precond_mode_ = 1;                         // 0 = sync-free flow kernels, 1 = level graphs, 2 = sweep
+  int max_flow_blocks_ = 512;
+  DevBuf<int> d_err_;
   void BuildSweepPlan(const int* nbr, const std::vector<int>& tptr, const std::vector<int>& trow,
                       const std::vector<int>& tslot, const std::vector<int>& lf, const std::vector<int>& lb);
   DevBuf<double> d_y_, d_Bv_, d_dBv_, d_Dinv_, d_dD_, d_W_, d_dw_, d_sdw_, d_d1_;

@@ -37,6 +37,10 @@ struct SparseB {
   const int* tptr;
   const int* trow;
   const int* tslot;
+  // nullable: tval[e] = tval_of[tslot[e]], the values array in transposed-list order
+  // (refreshed per evaluation); launch_bt_apply reads it when vals == tval_of
+  const double* tval;
+  const double* tval_of;
 };
 
 // Y = diag(scale) (unit*X + V X)   with V = vals on the B pattern (rows list optional)
@@ -87,6 +91,25 @@ struct LevelPlan {
 };
 void launch_vadu_level(const LevelPlan& lp, int l, const double* dw, const double* R, double* Y, double* Z, int t,
                        hipStream_t s);
+// Sync-free form of one of the two solves (vadu_flow.hip): one launch runs the whole DAG,
+// each solved value doubling as its readiness flag. Positions q in [0, n) follow the solve's
+// level order (row lrows[q]); B^T solve: entries [eoff[q], eoff[q+1]) of (eidx, eval);
+// lower solve (eoff null): entries q*m + r, r < min(row, m), and the input is divided by dw.
+// X (n x t) is filled with the sentinel by the launcher; err is set if a spin gives up.
+struct FlowArgs {
+  const int* lrows;
+  const int* crit;     // per position: the dependency of highest level (-1: none), polled first
+  const int* eoff;
+  const int* eidx;
+  const double* eval;
+  const double* dw;
+  const double* in;
+  double* X;
+  int* err;
+  unsigned long long* prof;   // diagnostics (nullable): per position {setup, crit seen, published} timestamps
+  int n, m, t, shift;
+};
+void launch_vadu_flow(const FlowArgs& a, bool lower, int max_blocks, hipStream_t s);
 // blob_f64[vpos[e]] = Bv[eslot[e]] for all count entries (per-evaluation value refresh)
 void launch_sweep_values(int count, const int* vpos, const int* eslot, const double* Bv, int* blob, hipStream_t s);
 // dst[p*m + r] = src[rows[p]*m + r]  (n x m, level order)  |  dst[e] = idx[e] >= 0 ? src[idx[e]] : 0

@@ -71,7 +71,8 @@ __global__ void __launch_bounds__(kBT) b_apply_kernel(int n, int m, const int* _
 
 __global__ void __launch_bounds__(kBT) bt_apply_kernel(int n, const int* __restrict__ tptr,
                                                        const int* __restrict__ trow, const int* __restrict__ tslot,
-                                                       const double* __restrict__ vals, int unit,
+                                                       const double* __restrict__ vals,
+                                                       const double* __restrict__ tval, int unit,
                                                        const double* __restrict__ X, int t, int shift,
                                                        const double* __restrict__ pre, const double* __restrict__ W,
                                                        const double* __restrict__ H, double* __restrict__ Y) {
@@ -86,11 +87,64 @@ __global__ void __launch_bounds__(kBT) bt_apply_kernel(int n, const int* __restr
 #pragma unroll 4
     for (int e = tptr[j]; e < e1; ++e) {
       const int i = trow[e];
-      const double w = pre ? vals[tslot[e]] * pre[i] : vals[tslot[e]];
+      const double v = tval ? tval[e] : vals[tslot[e]];
+      const double w = pre ? v * pre[i] : v;
       s = fma(w, X[(size_t)i * t + c], s);
     }
     if (W) s = fma(W[j], H[(size_t)j * t + c], s);
     Y[(size_t)j * t + c] = s;
+  }
+}
+
+// t = 1: G lanes per row, entry r on lane r mod G (structure loads coalesced, one gather
+// instruction per row instead of a serial chain per lane); fixed shuffle tree -> deterministic.
+template <int G>
+__global__ void __launch_bounds__(kBT) b_apply1_kernel(int n, int m, const int* __restrict__ nbr,
+                                                       const double* __restrict__ vals, int unit,
+                                                       const double* __restrict__ X,
+                                                       const double* __restrict__ scale, double* __restrict__ Y) {
+  const int lane = threadIdx.x & (G - 1);
+  constexpr int rpb = kBT / G;
+  for (int i = blockIdx.x * rpb + threadIdx.x / G; i < n; i += gridDim.x * rpb) {
+    const int k = i < m ? i : m;
+    const size_t o = (size_t)i * m;
+    double acc = 0.;
+    for (int r = lane; r < k; r += G) acc = fma(vals[o + r], X[nbr[o + r]], acc);
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) {
+      double s = unit ? X[i] + acc : acc;
+      if (scale) s *= scale[i];
+      Y[i] = s;
+    }
+  }
+}
+
+template <int G>
+__global__ void __launch_bounds__(kBT) bt_apply1_kernel(int n, const int* __restrict__ tptr,
+                                                        const int* __restrict__ trow,
+                                                        const double* __restrict__ tval, int unit,
+                                                        const double* __restrict__ X,
+                                                        const double* __restrict__ pre,
+                                                        const double* __restrict__ W,
+                                                        const double* __restrict__ H, double* __restrict__ Y) {
+  const int lane = threadIdx.x & (G - 1);
+  constexpr int rpb = kBT / G;
+  for (int j = blockIdx.x * rpb + threadIdx.x / G; j < n; j += gridDim.x * rpb) {
+    const int e1 = tptr[j + 1];
+    double acc = 0.;
+    for (int e = tptr[j] + lane; e < e1; e += G) {
+      const int i = trow[e];
+      acc = fma(pre ? tval[e] * pre[i] : tval[e], X[i], acc);
+    }
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    if (lane == 0) {
+      double s = unit ? (pre ? pre[j] * X[j] : X[j]) : 0.;
+      s += acc;
+      if (W) s = fma(W[j], H[j], s);
+      Y[j] = s;
+    }
   }
 }
 
@@ -447,6 +501,13 @@ __global__ void __launch_bounds__(kBT) mode_deriv_kernel(ModeDerivArgs a, int sh
 // ------------------------------------------------------------------ launchers
 void launch_b_apply(const SparseB& B, const double* vals, bool unit, const double* X, int t, const double* scale,
                     double* Y, hipStream_t s) {
+  if (t == 1) {
+    constexpr int G = 32;
+    hipLaunchKernelGGL(b_apply1_kernel<G>, dim3(grid_x(B.n, kBT / G, 8192)), dim3(kBT), 0, s, B.n, B.m, B.nbr, vals,
+                       unit ? 1 : 0, X, scale, Y);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   const Lanes L = lanes_for(t);
   hipLaunchKernelGGL(b_apply_kernel, dim3(grid_x(B.n, L.rpb), L.gy), dim3(kBT), 0, s, B.n, B.m, B.nbr, vals,
                      unit ? 1 : 0, X, t, L.shift, scale, Y);
@@ -455,9 +516,17 @@ void launch_b_apply(const SparseB& B, const double* vals, bool unit, const doubl
 
 void launch_bt_apply(const SparseB& B, const double* vals, bool unit, const double* X, int t, const double* pre,
                      const double* W, const double* H, double* Y, hipStream_t s) {
+  const double* tval = (B.tval != nullptr && vals == B.tval_of) ? B.tval : nullptr;
+  if (t == 1 && tval != nullptr) {
+    constexpr int G = 32;
+    hipLaunchKernelGGL(bt_apply1_kernel<G>, dim3(grid_x(B.n, kBT / G, 8192)), dim3(kBT), 0, s, B.n, B.tptr, B.trow,
+                       tval, unit ? 1 : 0, X, pre, W, H, Y);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   const Lanes L = lanes_for(t);
   hipLaunchKernelGGL(bt_apply_kernel, dim3(grid_x(B.n, L.rpb), L.gy), dim3(kBT), 0, s, B.n, B.tptr, B.trow,
-                     B.tslot, vals, unit ? 1 : 0, X, t, L.shift, pre, W, H, Y);
+                     B.tslot, vals, tval, unit ? 1 : 0, X, t, L.shift, pre, W, H, Y);
   HIP_CHECK(hipGetLastError());
 }
 

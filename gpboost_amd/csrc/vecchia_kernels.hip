@@ -26,6 +26,8 @@
 // Optional outputs D^-1 and B(i, nbr) = -a are written for the factor API.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "common.h"
 #include "cov.h"
 #include "kernels.h"
@@ -239,6 +241,233 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
   }
 }
 
+// ---------------------------------------------------------------- v4: two matrix rows per lane
+// For K = 16 / 32 (m <= 32) a row problem is owned by H = K/2 lanes; lane h owns matrix rows
+// h and h + H. v3 is bound by LDS traffic (one ds_read broadcast per FMA in the Gauss-Jordan
+// steps plus three slot writes per step, on an LDS shared by the CU's four SIMDs). Here every
+// broadcast feeds two FMAs, the pivot row's augmented entries come from the pivot lane by a
+// lane shuffle instead of LDS slots, and the packed triangle holds C until the rows are in
+// registers and dC/dlog(phi) afterwards (the pair phase keeps dC in registers meanwhile), so
+// a problem needs one triangle instead of two. The per-row arithmetic is v3's.
+constexpr int kV4Threads = 64;   // one wave per block: 64 / H problems
+
+template <int K>
+constexpr int v4_lds_doubles() {
+  return K * (K + 1) / 2 + kDMax * K + K;   // packed C (then dC) | neighbour coords | pivot slot
+}
+
+template <int K, int COV>
+__global__ void __launch_bounds__(kV4Threads, 1) vecchia_rows2_kernel(VecchiaRowsArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  constexpr int H = K / 2;   // lanes per problem
+  constexpr int P = 64 / H;  // problems per wave (= per block)
+  const int lane = threadIdx.x & 63;
+  const int g = lane / H;
+  const int h = lane - g * H;
+  const int gbase = g * H;
+  const int r0 = h, r1 = h + H;
+  const int d = a.d;
+  const double var = a.var, phi = a.phi;
+  const double cdiag = var * a.diag_mult + a.diag_add;
+  const double delta = cdiag - var;
+  const bool want_like = a.Y != nullptr;
+
+  double* Cp = smem + g * v4_lds_doubles<K>();
+  double* nbx = Cp + K * (K + 1) / 2;
+  double* slot = nbx + K * kDMax;
+
+  double acc[kVecchiaSums] = {0., 0., 0., 0., 0., 0.};
+  const int total = a.r1 - a.r0;
+  for (int base = blockIdx.x * P; base < total; base += gridDim.x * P) {
+    const int i = a.r0 + base + g;
+    const bool active = i < a.r1;
+    const int k = active ? min(i, a.m) : 0;
+    const bool v0 = r0 < k, v1 = r1 < k;
+    const int irow = active ? i : a.r0;
+
+    // ---- gather: neighbour indices, coordinates, responses (Vecchia order)
+    const int nb0 = v0 ? a.nbr[(size_t)i * a.m + r0] : 0;
+    const int nb1 = v1 ? a.nbr[(size_t)i * a.m + r1] : 0;
+    double xi[kDMax], x0[kDMax], x1[kDMax];
+#pragma unroll
+    for (int q = 0; q < kDMax; ++q) {
+      xi[q] = (q < d) ? a.X[(size_t)irow * d + q] : 0.;
+      x0[q] = (q < d && v0) ? a.X[(size_t)nb0 * d + q] : 0.;
+      x1[q] = (q < d && v1) ? a.X[(size_t)nb1 * d + q] : 0.;
+    }
+    const double yi = want_like ? a.Y[irow] : 0.;
+    const double y0 = (want_like && v0) ? a.Y[nb0] : 0.;
+    const double y1 = (want_like && v1) ? a.Y[nb1] : 0.;
+    compiler_fence();   // previous iteration's LDS reads are issued before these writes
+#pragma unroll
+    for (int q = 0; q < kDMax; ++q) {
+      nbx[r0 * kDMax + q] = x0[q];
+      nbx[r1 * kDMax + q] = x1[q];
+    }
+    // observation-neighbour covariances c and their range derivatives
+    double c0, dc0, c1, dc1;
+    {
+      double s0 = 0., s1 = 0.;
+#pragma unroll
+      for (int q = 0; q < kDMax; ++q) {
+        const double t0 = xi[q] - x0[q], t1 = xi[q] - x1[q];
+        s0 += t0 * t0;
+        s1 += t1 * t1;
+      }
+      cov_dcov<COV>(sqrt(s0), var, phi, c0, dc0);
+      cov_dcov<COV>(sqrt(s1), var, phi, c1, dc1);
+      c0 = v0 ? c0 : 0.;
+      dc0 = v0 ? dc0 : 0.;
+      c1 = v1 ? c1 : 0.;
+      dc1 = v1 ? dc1 : 0.;
+    }
+    Cp[packed(r0, r0)] = v0 ? cdiag : 1.;
+    Cp[packed(r1, r1)] = v1 ? cdiag : 1.;
+    wave_lds_sync();
+
+    // ---- 1. pairs: lane h takes row h (columns < h) and row K-1-h (columns < K-1-h)
+    double dstash[K - 1];
+#pragma unroll
+    for (int q = 0; q < K - 1; ++q) {
+      const bool lo = q < h;
+      const int rr = lo ? h : K - 1 - h;
+      const int cc = lo ? q : q - h;
+      double s = 0.;
+#pragma unroll
+      for (int qq = 0; qq < kDMax; ++qq) {
+        const double t = nbx[rr * kDMax + qq] - nbx[cc * kDMax + qq];
+        s += t * t;
+      }
+      double cv, dcv;
+      cov_dcov<COV>(sqrt(s), var, phi, cv, dcv);
+      Cp[packed(rr, cc)] = rr < k ? cv : 0.;
+      dstash[q] = rr < k ? dcv : 0.;
+    }
+    wave_lds_sync();
+
+    // ---- 2. rows r0, r1 of C into registers; then the triangle becomes dC
+    double row0[K], row1[K];
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
+      row0[c] = (c <= r0) ? Cp[packed(r0, c)] : Cp[packed(c, r0)];
+      row1[c] = (c <= r1) ? Cp[packed(r1, c)] : Cp[packed(c, r1)];
+    }
+    wave_lds_sync();   // every lane's reads of C have returned before dC overwrites it
+#pragma unroll
+    for (int q = 0; q < K - 1; ++q) {
+      const bool lo = q < h;
+      const int rr = lo ? h : K - 1 - h;
+      const int cc = lo ? q : q - h;
+      Cp[packed(rr, cc)] = dstash[q];
+    }
+    Cp[packed(r0, r0)] = 0.;
+    Cp[packed(r1, r1)] = 0.;
+
+    // ---- 3. symmetric Gauss-Jordan on [C | c | y_nbr], rows r0 and r1 in registers
+    double p0a = c0, p0b = y0, p1a = c1, p1b = y1;
+#pragma unroll
+    for (int j = 0; j < K; ++j) {
+      compiler_fence();
+      slot[r0] = row0[j];
+      slot[r1] = row1[j];
+      // augmented entries of pivot row j, from its owner (row j < H: lane j's r0, else r1)
+      const int src = gbase + (j < H ? j : j - H);
+      const double sa1 = __shfl(j < H ? p0a : p1a, src, 64);
+      const double sa2 = __shfl(j < H ? p0b : p1b, src, 64);
+      wave_lds_sync();
+      const double piv = slot[j];
+      double rinv = __builtin_amdgcn_rcp(piv);
+      rinv = fma(rinv, fma(-piv, rinv, 1.), rinv);
+      rinv = fma(rinv, fma(-piv, rinv, 1.), rinv);
+      // the pivot row itself is left unchanged
+      const double f0 = (j < H && r0 == j) ? 0. : row0[j] * rinv;
+      const double f1 = (j >= H && r1 == j) ? 0. : row1[j] * rinv;
+      p0a = fma(-f0, sa1, p0a);
+      p0b = fma(-f0, sa2, p0b);
+      p1a = fma(-f1, sa1, p1a);
+      p1b = fma(-f1, sa2, p1b);
+#pragma unroll
+      for (int c = j + 1; c < K; ++c) {
+        const double s = slot[c];
+        row0[c] = fma(-f0, s, row0[c]);
+        row1[c] = fma(-f1, s, row1[c]);
+      }
+      // pin this step's updates here (see v3: otherwise every broadcast value stays live)
+#pragma unroll
+      for (int c = j + 1; c < K; ++c) asm volatile("" : "+v"(row0[c]), "+v"(row1[c]));
+      asm volatile("" : "+v"(p0a), "+v"(p0b), "+v"(p1a), "+v"(p1b));
+    }
+    double dg0 = row0[0], dg1 = row1[H];
+#pragma unroll
+    for (int c = 1; c < H; ++c) dg0 = (c == r0) ? row0[c] : dg0;
+#pragma unroll
+    for (int c = H + 1; c < K; ++c) dg1 = (c == r1) ? row1[c] : dg1;
+    const double a0 = p0a / dg0, w0 = p0b / dg0;   // a = C^-1 c, v = C^-1 y_nbr
+    const double a1 = p1a / dg1, w1 = p1b / dg1;
+
+    if (active && a.B_out != nullptr) {
+      if (r0 < a.m) a.B_out[(size_t)i * a.m + r0] = v0 ? -a0 : 0.;
+      if (r1 < a.m) a.B_out[(size_t)i * a.m + r1] = v1 ? -a1 : 0.;
+    }
+
+    // ---- 4. t = dC a (dC from the packed triangle; its diagonal is 0)
+    compiler_fence();
+    slot[r0] = a0;
+    slot[r1] = a1;
+    wave_lds_sync();
+    double t0 = 0., t1 = 0.;
+    for (int c = 0; c < k; ++c) {
+      const double s = slot[c];
+      t0 = fma((c < r0) ? Cp[packed(r0, c)] : Cp[packed(c, r0)], s, t0);
+      t1 = fma((c < r1) ? Cp[packed(r1, c)] : Cp[packed(c, r1)], s, t1);
+    }
+    t0 = v0 ? t0 : 0.;
+    t1 = v1 ? t1 : 0.;
+
+    // ---- group reductions
+    const double ac = group_sum<H>(a0 * c0 + a1 * c1);
+    const double ay = group_sum<H>(a0 * y0 + a1 * y1);
+    const double aa = group_sum<H>(a0 * a0 + a1 * a1);
+    const double avv = group_sum<H>(a0 * w0 + a1 * w1);
+    const double dca = group_sum<H>(dc0 * a0 + dc1 * a1);
+    const double dcv = group_sum<H>(dc0 * w0 + dc1 * w1);
+    const double ta = group_sum<H>(t0 * a0 + t1 * a1);
+    const double tv = group_sum<H>(t0 * w0 + t1 * w1);
+
+    const double D = var + a.d_nugget - ac;          // Vecchia_utils.cpp:1351, 1507, 1562
+    const double Dinv = 1. / D;
+    if (active && h == 0 && a.Dinv_out != nullptr) a.Dinv_out[i] = Dinv;
+    if (want_like && active && h == 0) {
+      const double By = yi - ay;
+      const double u = By * Dinv;
+      const double dD_var = var - delta * aa - ac;
+      const double uk_var = -delta * avv;
+      const double dD_rng = -(2. * dca - ta);
+      const double uk_rng = -(dcv - tv);
+      acc[0] += log(D);
+      acc[1] += By * u;
+      acc[2] += uk_var * u - 0.5 * u * u * dD_var;
+      acc[3] += uk_rng * u - 0.5 * u * u * dD_rng;
+      acc[4] += Dinv * dD_var;
+      acc[5] += Dinv * dD_rng;
+    }
+  }
+  if (!want_like) return;
+  // ---- block (= wave) reduction of the per-problem sums, fixed order
+  __syncthreads();
+  double* red = smem;   // P x kVecchiaSums
+  if (h == 0) {
+#pragma unroll
+    for (int s = 0; s < kVecchiaSums; ++s) red[g * kVecchiaSums + s] = acc[s];
+  }
+  __syncthreads();
+  if (threadIdx.x < kVecchiaSums) {
+    double v = 0.;
+    for (int gi = 0; gi < P; ++gi) v += red[gi * kVecchiaSums + threadIdx.x];
+    a.block_sums[(size_t)blockIdx.x * kVecchiaSums + threadIdx.x] = v;
+  }
+}
+
 __global__ void __launch_bounds__(1024) sum_blocks_kernel(const double* __restrict__ in, int nblocks, int width,
                                                        double* __restrict__ out) {
   // width <= 8: thread t sums column (t & 7) over blocks (t >> 3) + 128 u, four loads in flight
@@ -271,8 +500,16 @@ int lanes_for_m(int m) {
   return 0;
 }
 
+// v3 is the default: measured on MI355X at n = 100k, m = 30 v4 took 0.578 ms per launch against
+// v3's 0.474 ms (gpurun_out r01b). v4 (two rows per lane) stays selectable for K <= 32 with
+// GPBOOST_AMD_ROWS_V4 for A/B measurements.
+bool use_v4(int K) {
+  static const bool v4 = std::getenv("GPBOOST_AMD_ROWS_V4") != nullptr;
+  return K <= 32 && v4;
+}
+
 template <int K>
-int rows_per_block() { return (block_threads<K>() / 64) * (64 / K); }
+int rows_per_block() { return use_v4(K) ? 64 / (K / 2) : (block_threads<K>() / 64) * (64 / K); }
 
 template <int K>
 int blocks_for(int rows) {
@@ -285,8 +522,17 @@ template <int K, int COV>
 void launch_k(const VecchiaRowsArgs& a, hipStream_t s) {
   const int rpb = rows_per_block<K>();
   const int blocks = blocks_for<K>(a.r1 - a.r0);
-  size_t lds = (size_t)rpb * group_lds_doubles<K>() * sizeof(double);
   const size_t red = (size_t)rpb * kVecchiaSums * sizeof(double);
+  if constexpr (K <= 32) {
+    if (use_v4(K)) {
+      size_t lds = (size_t)rpb * v4_lds_doubles<K>() * sizeof(double);
+      if (lds < red) lds = red;
+      hipLaunchKernelGGL((vecchia_rows2_kernel<K, COV>), dim3(blocks), dim3(kV4Threads), lds, s, a);
+      HIP_CHECK(hipGetLastError());
+      return;
+    }
+  }
+  size_t lds = (size_t)rpb * group_lds_doubles<K>() * sizeof(double);
   if (lds < red) lds = red;
   hipLaunchKernelGGL((vecchia_rows_kernel<K, COV>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
   HIP_CHECK(hipGetLastError());
