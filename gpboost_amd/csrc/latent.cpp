@@ -51,7 +51,9 @@ LatentVecchia::LatentVecchia(int n, int d, int m, const double* d_X, const int* 
   HIP_CHECK(hipEventCreate(&ev0_));
   HIP_CHECK(hipEventCreate(&ev1_));
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_out_), kOutDoubles * sizeof(double), hipHostMallocDefault));
-  BuildStructure(nbr);
+  std::vector<int> nbr_p;
+  Relabel(nbr, nbr_p);
+  BuildStructure(nbr_p.data());
   for (auto* b : {&d_Bv_, &d_dBv_}) b->alloc((size_t)n * m);
   for (auto* b : {&d_y_, &d_Dinv_, &d_dD_, &d_W_, &d_dw_, &d_sdw_, &d_d1_, &d_mode_, &d_mode_upd_, &d_mode_new_,
                   &d_rhs_, &d_dir_, &d_Adir_, &d_vS_, &d_dmll_})
@@ -66,10 +68,74 @@ LatentVecchia::~LatentVecchia() {
   if (ev1_) (void)hipEventDestroy(ev1_);
 }
 
-// Host construction of the B^T lists and the level sets of both triangular solves.
-// Level of row i in the lower solve: 1 + max level of its neighbours (all earlier rows);
-// level of column j in the B^T (unit upper) solve: 1 + max level of the rows that have j
-// as a neighbour. Rows inside a level are independent.
+namespace {
+// 2-D / 3-D Morton key of a point in the unit-scaled bounding box (21 bits per axis).
+uint64_t spread_bits(uint64_t v, int dims) {
+  uint64_t r = 0;
+  for (int b = 0; b < 21; ++b) r |= ((v >> b) & 1ull) << (b * dims);
+  return r;
+}
+}  // namespace
+
+// Storage relabelling for locality. The latent problem is solved in a symmetric permutation
+// of the Vecchia order: storage row p holds Vecchia row vo_[p]. Rows 0..m-1 keep their
+// labels (so k_p = min(p, m) still gives each row's neighbour count), rows >= m follow the
+// Morton (Z-order) curve of their coordinates, so a row's neighbours — spatially close
+// points — sit close in storage and the neighbour gathers of the operator, the solves and
+// the trace kernels hit L2 instead of streaming from HBM / MALL. Every quantity the path
+// returns (nll, gradient, log-determinants, CG coefficients) is invariant under the
+// relabelling up to summation order. GPBOOST_AMD_NO_RELABEL keeps the Vecchia order (A/B).
+void LatentVecchia::Relabel(const int* nbr, std::vector<int>& nbr_p) {
+  const int n = n_, m = m_, d = d_;
+  vo_.resize(n);
+  lab_.resize(n);
+  for (int i = 0; i < n; ++i) vo_[i] = i;
+  const int m0 = std::min(m, n);
+  std::vector<double> X((size_t)n * d);   // the caller's upload runs on our (non-blocking) stream
+  HIP_CHECK(hipMemcpyAsync(X.data(), d_X_, sizeof(double) * X.size(), hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  if (std::getenv("GPBOOST_AMD_NO_RELABEL") == nullptr && n > m0 && d >= 1 && d <= 3) {
+    std::vector<double> lo(d, 0.), hi(d, 0.);
+    for (int q = 0; q < d; ++q) {
+      lo[q] = hi[q] = X[q];
+      for (int i = 1; i < n; ++i) {
+        lo[q] = std::min(lo[q], X[(size_t)i * d + q]);
+        hi[q] = std::max(hi[q], X[(size_t)i * d + q]);
+      }
+    }
+    std::vector<uint64_t> key(n, 0);
+    for (int i = m0; i < n; ++i) {
+      uint64_t k = 0;
+      for (int q = 0; q < d; ++q) {
+        const double w = hi[q] > lo[q] ? (X[(size_t)i * d + q] - lo[q]) / (hi[q] - lo[q]) : 0.;
+        const uint64_t c = (uint64_t)(std::min(std::max(w, 0.), 1.) * 2097151.);
+        k |= spread_bits(c, d) << q;
+      }
+      key[i] = k;
+    }
+    std::stable_sort(vo_.begin() + m0, vo_.end(), [&](int a, int b) { return key[a] < key[b]; });
+  }
+  for (int p = 0; p < n; ++p) lab_[vo_[p]] = p;
+  nbr_p.assign((size_t)n * m, 0);
+  for (int p = 0; p < n; ++p) {
+    const int i = vo_[p];
+    const int k = std::min(i, m);
+    for (int r = 0; r < k; ++r) nbr_p[(size_t)p * m + r] = lab_[nbr[(size_t)i * m + r]];
+  }
+  d_Xp_.alloc((size_t)n * d);
+  std::vector<double> Xp((size_t)n * d);
+  for (int p = 0; p < n; ++p)
+    for (int q = 0; q < d; ++q) Xp[(size_t)p * d + q] = X[(size_t)vo_[p] * d + q];
+  HIP_CHECK(hipMemcpyAsync(d_Xp_.get(), Xp.data(), sizeof(double) * Xp.size(), hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+}
+
+// Host construction of the B^T lists and the level sets of both triangular solves (in the
+// storage labels of Relabel). Level of a row in the lower solve: 1 + max level of its
+// neighbours (all earlier Vecchia rows); level of column j in the B^T (unit upper) solve:
+// 1 + max level of the rows that have j as a neighbour. Rows inside a level are
+// independent. Level recursions walk the rows in Vecchia order (lab_ = storage label of
+// each Vecchia row).
 void LatentVecchia::BuildStructure(const int* nbr) {
   const int n = n_, m = m_;
   std::vector<int> cnt(n + 1, 0);
@@ -92,14 +158,16 @@ void LatentVecchia::BuildStructure(const int* nbr) {
   }
   std::vector<int> lf(n, 0), lb(n, 0);
   int Lf = 0, Lb = 0;
-  for (int i = 0; i < n; ++i) {
+  for (int ii = 0; ii < n; ++ii) {
+    const int i = lab_[ii];   // storage label of Vecchia row ii
     const int k = std::min(i, m);
     int l = 0;
     for (int r = 0; r < k; ++r) l = std::max(l, lf[nbr[(size_t)i * m + r]] + 1);
     lf[i] = l;
     Lf = std::max(Lf, l + 1);
   }
-  for (int i = n - 1; i >= 0; --i) {
+  for (int ii = n - 1; ii >= 0; --ii) {
+    const int i = lab_[ii];   // storage label of Vecchia row ii
     const int k = std::min(i, m);
     for (int r = 0; r < k; ++r) {
       const int j = nbr[(size_t)i * m + r];
@@ -135,10 +203,16 @@ void LatentVecchia::BuildStructure(const int* nbr) {
   sp_.tptr = d_tptr_.get();
   sp_.trow = d_trow_.get();
   sp_.tslot = d_tslot_.get();
+  tnnz_ = nnz;
+  d_tval_.alloc(trow.size());
+  sp_.tval = d_tval_.get();
+  sp_.tval_of = nullptr;   // set once the values of an evaluation are gathered
 }
 
 void LatentVecchia::SetY(const double* y_vo) {
-  HIP_CHECK(hipMemcpyAsync(d_y_.get(), y_vo, sizeof(double) * n_, hipMemcpyHostToDevice, s_));
+  std::vector<double> yp(n_);
+  for (int p = 0; p < n_; ++p) yp[p] = y_vo[vo_[p]];
+  HIP_CHECK(hipMemcpyAsync(d_y_.get(), yp.data(), sizeof(double) * n_, hipMemcpyHostToDevice, s_));
   HIP_CHECK(hipStreamSynchronize(s_));
   y_set_ = true;
 }
@@ -169,7 +243,12 @@ void LatentVecchia::EnsureProbes(const IterativeConfig& cfg) {
   if (probes_saved_ && probes_t_ == t) return;
   // GenRandVecNormalParallel (CG_utils.cpp:930-947), drawn once when reuse_rand_vec_trace
   std::vector<double> R((size_t)n_ * t);
-  gen_probes_normal(n_, t, cfg.seed_rand_vec_trace, probe_run_id_, R.data());
+  {   // drawn in Vecchia order (the reference's), stored in the relabelled rows
+    std::vector<double> Rv((size_t)n_ * t);
+    gen_probes_normal(n_, t, cfg.seed_rand_vec_trace, probe_run_id_, Rv.data());
+    for (int p = 0; p < n_; ++p)
+      std::copy(Rv.begin() + (size_t)vo_[p] * t, Rv.begin() + (size_t)(vo_[p] + 1) * t, R.begin() + (size_t)p * t);
+  }
   ++probe_run_id_;
   d_probes_.alloc((size_t)n_ * t);
   d_Zp_.alloc((size_t)n_ * t);
@@ -531,7 +610,7 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
 
   // ---- 1. latent Vecchia factor (+ range derivatives)
   LatentFactorArgs fa{};
-  fa.X = d_X_;
+  fa.X = d_Xp_.get();
   fa.nbr = d_nbr_.get();
   fa.n = n; fa.d = d_; fa.m = m_;
   fa.var = trafo[0];
@@ -544,6 +623,8 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
   launch_latent_factor(cov_type, fa, s_);
   launch_sweep_values(plan_entries_, d_vpos_.get(), d_eslot_.get(), d_Bv_.get(), d_blob_.get(), s_);
   launch_gather(lplan_entries_, d_lslot_.get(), d_Bv_.get(), d_lval_.get(), s_);
+  launch_gather(tnnz_, d_tslot_.get(), d_Bv_.get(), d_tval_.get(), s_);   // B^T operator values, list order
+  sp_.tval_of = d_Bv_.get();
 
   Block& b1 = GetBlock(0, 1, std::max(cfg.cg_max_num_it, 1));
   if (std::getenv("GPBOOST_AMD_BENCH_PRECOND")) {   // diagnostics: preconditioner cost alone

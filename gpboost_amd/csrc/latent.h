@@ -75,6 +75,7 @@ class LatentVecchia {
     double* b() const { return small.get() + 5 * t; }
   };
 
+  void Relabel(const int* nbr, std::vector<int>& nbr_p);   // storage order for locality
   void BuildStructure(const int* nbr);
   Block& GetBlock(int which, int t, int pmax);
   void EnsureProbes(const IterativeConfig& cfg);
@@ -93,12 +94,16 @@ class LatentVecchia {
   PcgResult Pcg(Block& b, const double* RHS, double* U, int n_single, bool init_zero, bool u_is_zero,
                 int pmax_single, int pmax_block, double delta);
   void Scalars(const ScalarArgs& a, double* out);
-  double Dot1(const double* x, const double* y);
-  void CheckSolveError();   // single-vector dot, synchronous
+  double Dot1(const double* x, const double* y);   // single-vector dot, synchronous
+  void CheckSolveError();
 
   int n_, d_, m_;
   const double* d_X_;
   hipStream_t s_;
+  std::vector<int> vo_, lab_;   // storage row p holds Vecchia row vo_[p]; lab_ = inverse
+  DevBuf<double> d_Xp_;         // coordinates in storage order
+  DevBuf<double> d_tval_;       // B values in transposed-list order (refreshed per evaluation)
+  int tnnz_ = 0;
   SparseB sp_{};
   DevBuf<int> d_nbr_, d_tptr_, d_trow_, d_tslot_;
   // step plan of the two VADU triangular solves (see SweepPlan)

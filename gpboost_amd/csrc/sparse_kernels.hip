@@ -13,9 +13,12 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 
 #include "common.h"
 #include "latent_kernels.h"
+#include "wave_ops.h"
 
 namespace gpb_amd {
 namespace {
@@ -49,6 +52,63 @@ int grid_x(int rows, int rpb, int cap = kMaxGridX) {
 }
 
 // ------------------------------------------------------------------ SpMV
+// Workgroups are dispatched round-robin over the 8 XCDs (block b on XCD b % 8). Rows are
+// stored in a locality order (LatentVecchia::Relabel), so consecutive rows share most of
+// their neighbours: give every XCD one contiguous range of row blocks so those shared
+// neighbour rows are served from that XCD's L2.
+
+// Row r of a t >= 2 operator runs on the lane group of (block, slot): with PERS the grid is
+// capped and block b walks the row groups [L*span, (L+1)*span) of its logical index
+// L = xcd_block(b) (one contiguous, spatially coherent range per XCD); otherwise one row
+// group per block. CH = 0: the row's entries one after another (unroll 4); CH > 0: CH
+// structure loads, then CH gathers in flight. Summation order is the same in every form:
+// unit term, then entries ascending.
+template <int CH>
+__device__ __forceinline__ double row_dot(const int* __restrict__ idx, const double* __restrict__ val, int k,
+                                          const double* __restrict__ pre, const double* __restrict__ X, int t, int c,
+                                          int self, double s) {
+  if constexpr (CH == 0) {
+#pragma unroll 4
+    for (int r = 0; r < k; ++r) {
+      const int j = idx[r];
+      const double w = pre ? val[r] * pre[j] : val[r];
+      s = fma(w, X[(size_t)j * t + c], s);
+    }
+  } else {
+    for (int r0 = 0; r0 < k; r0 += CH) {
+      int id[CH];
+      double w[CH], g[CH];
+#pragma unroll
+      for (int q = 0; q < CH; ++q) {
+        const bool ok = r0 + q < k;
+        id[q] = ok ? idx[r0 + q] : self;
+        const double v = ok ? val[r0 + q] : 0.;
+        w[q] = pre ? v * pre[id[q]] : v;
+      }
+#pragma unroll
+      for (int q = 0; q < CH; ++q) g[q] = X[(size_t)id[q] * t + c];
+#pragma unroll
+      for (int q = 0; q < CH; ++q) s = fma(w[q], g[q], s);
+    }
+  }
+  return s;
+}
+
+struct RowWalk {
+  int g0, g1;   // row groups of this block
+};
+template <bool PERS>
+__device__ __forceinline__ RowWalk row_walk(int ngroups) {
+  if (!PERS) return {(int)blockIdx.x, (int)blockIdx.x + 1};
+  const int G = gridDim.x;
+  const int span = (ngroups + G - 1) / G;
+  const int L = xcd_block(blockIdx.x, G);
+  const int g0 = L * span;
+  return {g0, min(g0 + span, ngroups)};
+}
+
+// Y = diag(scale) (unit*X + V X)
+template <int CH, bool PERS>
 __global__ void __launch_bounds__(kBT) b_apply_kernel(int n, int m, const int* __restrict__ nbr,
                                                       const double* __restrict__ vals, int unit,
                                                       const double* __restrict__ X, int t, int shift,
@@ -57,18 +117,21 @@ __global__ void __launch_bounds__(kBT) b_apply_kernel(int n, int m, const int* _
   const int c = (threadIdx.x & (T - 1)) + blockIdx.y * 64;
   const int rpb = kBT >> shift;
   if (c >= t) return;
-  for (int i = blockIdx.x * rpb + (threadIdx.x >> shift); i < n; i += gridDim.x * rpb) {
+  const RowWalk w = row_walk<PERS>((n + rpb - 1) / rpb);
+  for (int g = w.g0; g < w.g1; ++g) {
+    const int i = g * rpb + (threadIdx.x >> shift);
+    if (i >= n) break;
     const int k = i < m ? i : m;
-    const int* nb = nbr + (size_t)i * m;
-    const double* v = vals + (size_t)i * m;
     double s = unit ? X[(size_t)i * t + c] : 0.;
-#pragma unroll 4
-    for (int r = 0; r < k; ++r) s = fma(v[r], X[(size_t)nb[r] * t + c], s);
+    s = row_dot<CH>(nbr + (size_t)i * m, vals + (size_t)i * m, k, nullptr, X, t, c, i, s);
     if (scale) s *= scale[i];
     Y[(size_t)i * t + c] = s;
   }
 }
 
+// Y = unit*pre.*X + V^T (pre.*X) + W.*H over the transposed lists; values from tval (list
+// order, contiguous) when given, else gathered through tslot (CH = 0 form only).
+template <int CH, bool PERS>
 __global__ void __launch_bounds__(kBT) bt_apply_kernel(int n, const int* __restrict__ tptr,
                                                        const int* __restrict__ trow, const int* __restrict__ tslot,
                                                        const double* __restrict__ vals,
@@ -80,20 +143,85 @@ __global__ void __launch_bounds__(kBT) bt_apply_kernel(int n, const int* __restr
   const int c = (threadIdx.x & (T - 1)) + blockIdx.y * 64;
   const int rpb = kBT >> shift;
   if (c >= t) return;
-  for (int j = blockIdx.x * rpb + (threadIdx.x >> shift); j < n; j += gridDim.x * rpb) {
+  const RowWalk w = row_walk<PERS>((n + rpb - 1) / rpb);
+  for (int g = w.g0; g < w.g1; ++g) {
+    const int j = g * rpb + (threadIdx.x >> shift);
+    if (j >= n) break;
     double s = 0.;
     if (unit) s = pre ? pre[j] * X[(size_t)j * t + c] : X[(size_t)j * t + c];
-    const int e1 = tptr[j + 1];
-#pragma unroll 4
-    for (int e = tptr[j]; e < e1; ++e) {
-      const int i = trow[e];
-      const double v = tval ? tval[e] : vals[tslot[e]];
-      const double w = pre ? v * pre[i] : v;
-      s = fma(w, X[(size_t)i * t + c], s);
+    const int e0 = tptr[j], e1 = tptr[j + 1];
+    if (tval) {
+      s = row_dot<CH>(trow + e0, tval + e0, e1 - e0, pre, X, t, c, j, s);
+    } else {
+      for (int e = e0; e < e1; ++e) {
+        const int i = trow[e];
+        const double v = vals[tslot[e]];
+        s = fma(pre ? v * pre[i] : v, X[(size_t)i * t + c], s);
+      }
     }
     if (W) s = fma(W[j], H[(size_t)j * t + c], s);
     Y[(size_t)j * t + c] = s;
   }
+}
+
+// ---- wave-per-row forms (t >= 2): the TA issue rate, not bandwidth, bounds the per-entry
+// forms above (every entry costs a structure load AND a gather, 64 lanes each). Here lane r
+// loads entry r of the row's structure (ONE coalesced load for up to 64 entries), and the
+// gathers take each entry's index and value from that lane with v_readlane (scalar
+// registers), so a row costs one vector-memory instruction per entry. Same summation order
+// as the other forms (unit term, entries ascending).
+constexpr int kWaveChunk = 16;   // gathers in flight per lane (A/B: GPBOOST_AMD_SPMV ch = -2 -> 32)
+
+// Y = diag(scale) (unit*X + V X); 4 waves per block, one row per wave, lane = column.
+template <int CH>
+__global__ void __launch_bounds__(kBT) b_apply_wave_kernel(int n, int m, const int* __restrict__ nbr,
+                                                           const double* __restrict__ vals, int unit,
+                                                           const double* __restrict__ X, int t,
+                                                           const double* __restrict__ scale, double* __restrict__ Y) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int i = xcd_block(blockIdx.x, gridDim.x) * (kBT / 64) + wave;
+  if (i >= n) return;
+  const int c = lane + blockIdx.y * 64;
+  const int cc = c < t ? c : t - 1;   // lanes beyond t gather a valid column, result unused
+  const int k = i < m ? i : m;
+  const int my_id = lane < k ? nbr[(size_t)i * m + lane] : i;
+  const double my_w = lane < k ? vals[(size_t)i * m + lane] : 0.;
+  double s = unit ? X[(size_t)i * t + cc] : 0.;
+  s = wave_dot<CH>(my_id, my_w, k, X, t, cc, i, s);
+  if (scale) s *= scale[i];
+  if (c < t) Y[(size_t)i * t + c] = s;
+}
+
+// Y = unit*pre.*X + V^T (pre.*X) + W.*H over the transposed lists (values in list order).
+template <int CH>
+__global__ void __launch_bounds__(kBT) bt_apply_wave_kernel(int n, const int* __restrict__ tptr,
+                                                            const int* __restrict__ trow,
+                                                            const double* __restrict__ tval, int unit,
+                                                            const double* __restrict__ X, int t,
+                                                            const double* __restrict__ pre,
+                                                            const double* __restrict__ W,
+                                                            const double* __restrict__ H, double* __restrict__ Y) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = xcd_block(blockIdx.x, gridDim.x) * (kBT / 64) + wave;
+  if (j >= n) return;
+  const int c = lane + blockIdx.y * 64;
+  const int cc = c < t ? c : t - 1;
+  double s = 0.;
+  if (unit) s = pre ? pre[j] * X[(size_t)j * t + cc] : X[(size_t)j * t + cc];
+  const int e0 = tptr[j], e1 = tptr[j + 1];
+  for (int b0 = e0; b0 < e1; b0 += 64) {
+    const int e = b0 + lane;
+    const bool ok = e < e1;
+    const int my_id = ok ? trow[e] : j;
+    double my_w = ok ? tval[e] : 0.;
+    if (pre && ok) my_w *= pre[my_id];
+    const int cnt = e1 - b0 < 64 ? e1 - b0 : 64;
+    s = wave_dot<CH>(my_id, my_w, cnt, X, t, cc, j, s);
+  }
+  if (W) s = fma(W[j], H[(size_t)j * t + cc], s);
+  if (c < t) Y[(size_t)j * t + c] = s;
 }
 
 // t = 1: G lanes per row, entry r on lane r mod G (structure loads coalesced, one gather
@@ -105,7 +233,9 @@ __global__ void __launch_bounds__(kBT) b_apply1_kernel(int n, int m, const int* 
                                                        const double* __restrict__ scale, double* __restrict__ Y) {
   const int lane = threadIdx.x & (G - 1);
   constexpr int rpb = kBT / G;
-  for (int i = blockIdx.x * rpb + threadIdx.x / G; i < n; i += gridDim.x * rpb) {
+  {
+    const int i = xcd_block(blockIdx.x, gridDim.x) * rpb + threadIdx.x / G;
+    if (i >= n) return;   // whole lane groups exit together
     const int k = i < m ? i : m;
     const size_t o = (size_t)i * m;
     double acc = 0.;
@@ -130,7 +260,9 @@ __global__ void __launch_bounds__(kBT) bt_apply1_kernel(int n, const int* __rest
                                                         const double* __restrict__ H, double* __restrict__ Y) {
   const int lane = threadIdx.x & (G - 1);
   constexpr int rpb = kBT / G;
-  for (int j = blockIdx.x * rpb + threadIdx.x / G; j < n; j += gridDim.x * rpb) {
+  {
+    const int j = xcd_block(blockIdx.x, gridDim.x) * rpb + threadIdx.x / G;
+    if (j >= n) return;   // whole lane groups exit together
     const int e1 = tptr[j + 1];
     double acc = 0.;
     for (int e = tptr[j] + lane; e < e1; e += G) {
@@ -499,34 +631,86 @@ __global__ void __launch_bounds__(kBT) mode_deriv_kernel(ModeDerivArgs a, int sh
 }  // namespace
 
 // ------------------------------------------------------------------ launchers
+// Form of the t >= 2 operator kernels (A/B switch GPBOOST_AMD_SPMV="ch,pers,cap"; ch = -1,
+// the default, selects the wave-per-row kernels).
+struct SpmvForm {
+  int ch, pers, cap;
+};
+SpmvForm spmv_form() {
+  static const SpmvForm f = [] {
+    SpmvForm r{-1, 0, 2048};
+    if (const char* e = std::getenv("GPBOOST_AMD_SPMV")) std::sscanf(e, "%d,%d,%d", &r.ch, &r.pers, &r.cap);
+    if (r.cap < 8) r.cap = 8;
+    return r;
+  }();
+  return f;
+}
+
+// The SpMV grids cover every row with one pass (no grid-stride loop): the XCD block mapping
+// needs the whole grid, and at n <= 2^31 / rpb the x dimension never overflows.
 void launch_b_apply(const SparseB& B, const double* vals, bool unit, const double* X, int t, const double* scale,
                     double* Y, hipStream_t s) {
+  if (B.n <= 0) return;
   if (t == 1) {
     constexpr int G = 32;
-    hipLaunchKernelGGL(b_apply1_kernel<G>, dim3(grid_x(B.n, kBT / G, 8192)), dim3(kBT), 0, s, B.n, B.m, B.nbr, vals,
-                       unit ? 1 : 0, X, scale, Y);
+    hipLaunchKernelGGL(b_apply1_kernel<G>, dim3(grid_x(B.n, kBT / G, 1 << 30)), dim3(kBT), 0, s, B.n, B.m, B.nbr,
+                       vals, unit ? 1 : 0, X, scale, Y);
     HIP_CHECK(hipGetLastError());
     return;
   }
   const Lanes L = lanes_for(t);
-  hipLaunchKernelGGL(b_apply_kernel, dim3(grid_x(B.n, L.rpb), L.gy), dim3(kBT), 0, s, B.n, B.m, B.nbr, vals,
-                     unit ? 1 : 0, X, t, L.shift, scale, Y);
+  const SpmvForm f = spmv_form();
+  if (f.ch < 0 && B.m <= 64) {   // default: wave-per-row form
+    const dim3 g(grid_x(B.n, kBT / 64, 1 << 30), L.gy);
+    if (f.ch == -2)
+      hipLaunchKernelGGL(b_apply_wave_kernel<32>, g, dim3(kBT), 0, s, B.n, B.m, B.nbr, vals, unit ? 1 : 0, X, t, scale, Y);
+    else
+      hipLaunchKernelGGL(b_apply_wave_kernel<kWaveChunk>, g, dim3(kBT), 0, s, B.n, B.m, B.nbr, vals, unit ? 1 : 0, X, t,
+                         scale, Y);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
+  const dim3 grid(grid_x(B.n, L.rpb, f.pers ? f.cap : (1 << 30)), L.gy);
+#define GPB_B_APPLY(CH, P)                                                                                     \
+  hipLaunchKernelGGL((b_apply_kernel<CH, P>), grid, dim3(kBT), 0, s, B.n, B.m, B.nbr, vals, unit ? 1 : 0, X, t, \
+                     L.shift, scale, Y)
+  if (f.ch == 0) { if (f.pers) GPB_B_APPLY(0, true); else GPB_B_APPLY(0, false); }
+  else { if (f.pers) GPB_B_APPLY(16, true); else GPB_B_APPLY(16, false); }
+#undef GPB_B_APPLY
   HIP_CHECK(hipGetLastError());
 }
 
 void launch_bt_apply(const SparseB& B, const double* vals, bool unit, const double* X, int t, const double* pre,
                      const double* W, const double* H, double* Y, hipStream_t s) {
+  if (B.n <= 0) return;
   const double* tval = (B.tval != nullptr && vals == B.tval_of) ? B.tval : nullptr;
   if (t == 1 && tval != nullptr) {
     constexpr int G = 32;
-    hipLaunchKernelGGL(bt_apply1_kernel<G>, dim3(grid_x(B.n, kBT / G, 8192)), dim3(kBT), 0, s, B.n, B.tptr, B.trow,
-                       tval, unit ? 1 : 0, X, pre, W, H, Y);
+    hipLaunchKernelGGL(bt_apply1_kernel<G>, dim3(grid_x(B.n, kBT / G, 1 << 30)), dim3(kBT), 0, s, B.n, B.tptr,
+                       B.trow, tval, unit ? 1 : 0, X, pre, W, H, Y);
     HIP_CHECK(hipGetLastError());
     return;
   }
   const Lanes L = lanes_for(t);
-  hipLaunchKernelGGL(bt_apply_kernel, dim3(grid_x(B.n, L.rpb), L.gy), dim3(kBT), 0, s, B.n, B.tptr, B.trow,
-                     B.tslot, vals, tval, unit ? 1 : 0, X, t, L.shift, pre, W, H, Y);
+  const SpmvForm f = spmv_form();
+  if (f.ch < 0 && tval != nullptr) {   // default: wave-per-row form
+    const dim3 g(grid_x(B.n, kBT / 64, 1 << 30), L.gy);
+    if (f.ch == -2)
+      hipLaunchKernelGGL(bt_apply_wave_kernel<32>, g, dim3(kBT), 0, s, B.n, B.tptr, B.trow, tval, unit ? 1 : 0, X, t,
+                         pre, W, H, Y);
+    else
+      hipLaunchKernelGGL(bt_apply_wave_kernel<kWaveChunk>, g, dim3(kBT), 0, s, B.n, B.tptr, B.trow, tval, unit ? 1 : 0,
+                         X, t, pre, W, H, Y);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
+  const dim3 grid(grid_x(B.n, L.rpb, f.pers ? f.cap : (1 << 30)), L.gy);
+#define GPB_BT_APPLY(CH, P)                                                                                     \
+  hipLaunchKernelGGL((bt_apply_kernel<CH, P>), grid, dim3(kBT), 0, s, B.n, B.tptr, B.trow, B.tslot, vals, tval, \
+                     unit ? 1 : 0, X, t, L.shift, pre, W, H, Y)
+  if (f.ch == 0) { if (f.pers) GPB_BT_APPLY(0, true); else GPB_BT_APPLY(0, false); }
+  else { if (f.pers) GPB_BT_APPLY(16, true); else GPB_BT_APPLY(16, false); }
+#undef GPB_BT_APPLY
   HIP_CHECK(hipGetLastError());
 }
 

@@ -17,6 +17,7 @@
 
 #include "common.h"
 #include "latent_kernels.h"
+#include "wave_ops.h"
 
 namespace gpb_amd {
 namespace {
@@ -135,6 +136,7 @@ __device__ __forceinline__ double level_dot(const int* __restrict__ idx, const d
   return acc;
 }
 
+
 template <bool LOWER, bool EMPTY>
 __global__ void __launch_bounds__(256) vadu_level_kernel(LevelPlan lp, int p0, int cnt, const double* __restrict__ dw,
                                                          const double* in, double* X, int t, int shift) {
@@ -213,7 +215,7 @@ __global__ void __launch_bounds__(256) vadu_level1_kernel(LevelPlan lp, int p0, 
                                                           const double* __restrict__ dw, const double* in,
                                                           double* X) {
   const int lane = threadIdx.x & (G - 1);
-  const int task = blockIdx.x * (256 / G) + threadIdx.x / G;
+  const int task = xcd_block(blockIdx.x, gridDim.x) * (256 / G) + threadIdx.x / G;
   if (task >= cnt) return;   // whole groups exit together (cnt is per group)
   const int p = p0 + task;
   const int i = lp.lrows[p];
@@ -243,7 +245,7 @@ __global__ void __launch_bounds__(NW * 64) vadu_levelT_kernel(LevelPlan lp, int 
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int c = lane + blockIdx.y * 64;
-  const int p = p0 + blockIdx.x;
+  const int p = p0 + xcd_block(blockIdx.x, gridDim.x);
   const int i = lp.lrows[p];
   int e0, e1;
   const int* idx;
@@ -293,6 +295,44 @@ __global__ void __launch_bounds__(NW * 64) vadu_levelT_kernel(LevelPlan lp, int 
   }
 }
 
+// t >= 2, wave-per-row: one 64-lane workgroup per row (lane = column), the row's structure
+// loaded by one coalesced load (lane r = entry r) and broadcast to the gathers by v_readlane,
+// all of a typical row's gathers in flight at once (CH = 32). Summation: entries ascending.
+template <bool LOWER, int CH>
+__global__ void __launch_bounds__(64) vadu_levelW_kernel(LevelPlan lp, int p0, const double* __restrict__ dw,
+                                                        const double* in, double* X, int t) {
+  const int lane = threadIdx.x;
+  const int p = p0 + xcd_block(blockIdx.x, gridDim.x);
+  const int i = lp.lrows[p];
+  const int c = lane + blockIdx.y * 64;
+  const int cc = c < t ? c : t - 1;   // lanes beyond t gather a valid column, result unused
+  const int* idx;
+  const double* val;
+  int cnt;
+  if (LOWER) {
+    const size_t q = (size_t)(p - lp.n) * lp.m;
+    idx = lp.fidx + q;
+    val = lp.fval + q;
+    cnt = i < lp.m ? i : lp.m;
+  } else {
+    const int e0 = lp.beoff[p];
+    idx = lp.beidx + e0;
+    val = lp.beval + e0;
+    cnt = lp.beoff[p + 1] - e0;
+  }
+  double x = in[(size_t)i * t + cc];
+  if (LOWER) x /= dw[i];
+  double acc = 0.;
+  for (int b0 = 0; b0 < cnt; b0 += 64) {
+    const int nb = cnt - b0 < 64 ? cnt - b0 : 64;
+    const bool ok = lane < nb;
+    const int my_id = ok ? idx[b0 + lane] : 0;
+    const double my_w = ok ? val[b0 + lane] : 0.;
+    acc = wave_dot<CH>(my_id, my_w, nb, X, t, cc, __builtin_amdgcn_readlane(my_id, 0), acc);
+  }
+  if (c < t) X[(size_t)i * t + c] = x - acc;
+}
+
 void launch_vadu_level(const LevelPlan& lp, int l, const double* dw, const double* R, double* Y, double* Z, int t,
                        hipStream_t s) {
   int T = 1, shift = 0;
@@ -309,6 +349,21 @@ void launch_vadu_level(const LevelPlan& lp, int l, const double* dw, const doubl
       constexpr int G = 32;
       hipLaunchKernelGGL((vadu_level1_kernel<true, G>), dim3((cnt + 256 / G - 1) / (256 / G)), dim3(256), 0, s, lp,
                          p0, cnt, dw, Y, Z);
+    }
+    return;
+  }
+  // Level form for t >= 2 (GPBOOST_AMD_LEVEL_FORM): 1 (default) = vadu_levelT_kernel (4 waves
+  // share a row's entries); 0 / 2 = wave-per-row with 32 / 16 gathers in flight, measured
+  // slower on MI355X at n = 100k, t = 51 (7.2 / 7.4 ms against 4.66 ms per application).
+  static const int lform = std::getenv("GPBOOST_AMD_LEVEL_FORM") ? std::atoi(std::getenv("GPBOOST_AMD_LEVEL_FORM")) : 1;
+  if (lform == 0 || lform == 2) {
+    const dim3 g(cnt, (t + 63) / 64);
+    if (lform == 0) {
+      if (l < lp.nlev_b) hipLaunchKernelGGL((vadu_levelW_kernel<false, 32>), g, dim3(64), 0, s, lp, p0, dw, R, Y, t);
+      else hipLaunchKernelGGL((vadu_levelW_kernel<true, 32>), g, dim3(64), 0, s, lp, p0, dw, Y, Z, t);
+    } else {
+      if (l < lp.nlev_b) hipLaunchKernelGGL((vadu_levelW_kernel<false, 16>), g, dim3(64), 0, s, lp, p0, dw, R, Y, t);
+      else hipLaunchKernelGGL((vadu_levelW_kernel<true, 16>), g, dim3(64), 0, s, lp, p0, dw, Y, Z, t);
     }
     return;
   }

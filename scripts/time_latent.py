@@ -33,5 +33,5 @@ def run(lik, n, reps=3, t=50):
 
 if __name__ == "__main__":
     for lik in sys.argv[1:] or ["gaussian", "bernoulli_logit"]:
-        for n in (20000, 100000):
+        for n in [int(v) for v in os.environ.get("SIZES", "20000 100000").split()]:
             run(lik, n)
