@@ -48,6 +48,19 @@ def vecchia_exps(n: int, m: int) -> float:
     return sum(min(i, m) * (min(i, m) + 1) / 2 for i in range(min(n, m))) + (n - m) * m * (m + 1) / 2
 
 
+def pmc_traffic(scale: float) -> dict | None:
+    """HBM bytes per launch of the row kernel from the committed rocprofv3 PMC passes of this
+    same command (profiles/<round>/pmc_rows.json: FETCH_SIZE + WRITE_SIZE, KB per dispatch;
+    PMC counters cannot be read from inside the process)."""
+    path = os.path.join(ROOT, "profiles", "r01", "pmc_rows.json")
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        p = json.load(f)
+    return {"bytes": (p["FETCH_SIZE_KB"] + p["WRITE_SIZE_KB"]) * 1024.0 * scale,
+            "source": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), " + os.path.relpath(path, ROOT)}
+
+
 def cpu_baseline(X, Y, reps: int = 3) -> dict:
     """Reference CPU path on this host (oracle/_ref/ref_harness, the reference GPBoost REModelTemplate
     compiled from its own sources), bounded sample: `reps` evaluations of the same n=100k unit."""
@@ -87,12 +100,99 @@ def cpu_baseline(X, Y, reps: int = 3) -> dict:
             "sample": f"1 eval at n={X.shape[0]} (oracle restatement, 1 thread)"}
 
 
+LATENT_T = 50                     # num_rand_vec_trace (reference default, re_model_template.h:5376)
+LATENT_PARS = [1.0, 0.1]          # sigma1^2, rho (original scale); Gaussian error variance (aux) 0.1
+
+
+def latent_matvec_bytes(n: int, nnz: int, r: int) -> float:
+    """one application of A = B^T D^-1 B + W to an n x r block."""
+    return 2 * nnz * (8 + 4) + 2 * (n + 1) * 4 + 2 * n * 8 + 2 * r * n * 8
+
+
+def latent_cpu_baseline(X, Y, reps: int = 1) -> dict | None:
+    """The reference's latent-Vecchia iterative evaluation (oracle/_ref/ref_harness) on this host."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(harness):
+        return None
+    import numpy as np
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", str(os.cpu_count() or 1))), 16))
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(np.array([X.shape[0], X.shape[1]], dtype=np.int32).tobytes())
+        f.write(np.ascontiguousarray(X.T).tobytes())
+        f.write(np.ascontiguousarray(Y).tobytes())
+        path = f.name
+    try:
+        out = subprocess.run([harness, path, "cov_fct=exponential", "gp_approx=vecchia_latent", "likelihood=gaussian",
+                              "matrix_inversion_method=iterative", f"num_neighbors={M_NEIGHBORS}", "ordering=random",
+                              "cov_pars=" + ",".join(map(str, LATENT_PARS)), "aux_pars=0.1", "cg_delta_conv=1e-2",
+                              f"num_rand_vec_trace={LATENT_T}", "seed_rand_vec_trace=1", f"reps={reps}"],
+                             capture_output=True, text=True, timeout=600,
+                             env=dict(os.environ, OMP_NUM_THREADS=str(threads)), check=True)
+        r = json.loads(out.stdout)
+        t = r["median_time"]
+        return {"value": 1.0 / t, "unit": "evals/s", "cores": threads, "kind": "reference",
+                "sample": f"{reps} latent-Vecchia iterative eval(s) at n={X.shape[0]} (nll+grad, {t:.2f} s/eval)",
+                "nll": r["nll"], "grad": r["grad"]}
+    except Exception as e:  # noqa: BLE001
+        sys.stderr.write(f"reference latent CPU baseline failed: {e}\n")
+        return None
+    finally:
+        os.unlink(path)
+
+
+def latent_leg(X, Y, steps: int, cpu: bool) -> dict:
+    """Secondary measurement: BASELINE config 3 in its PCG + stochastic-trace realisation
+    (gp_approx='vecchia_latent', matrix_inversion_method='iterative': Newton solve, block PCG
+    with the VADU preconditioner, SLQ log-determinant, stochastic-trace gradient), plus the
+    operator roofline of the CG matvec (SURVEY.md §8d bytes / HIP-event time)."""
+    import numpy as np
+
+    from gpboost_amd import GPModel
+    gm = GPModel(gp_coords=X, likelihood="gaussian", cov_function="exponential", gp_approx="vecchia_latent",
+                 num_neighbors=M_NEIGHBORS, vecchia_ordering="random", seed=0, matrix_inversion_method="iterative")
+    gm.set_optim_params(dict(num_rand_vec_trace=LATENT_T, init_aux_pars=[0.1]))
+    nll, g, _ = gm.neg_log_likelihood_and_grad(LATENT_PARS, Y)          # construction + first eval (warm-up)
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        nll, g, _ = gm.neg_log_likelihood_and_grad(LATENT_PARS, None)
+        ts.append(time.perf_counter() - t0)
+    info = gm.last_iteration_info()
+    r = LATENT_T + 1     # the Gaussian Newton column rides along the probe block (latent.cpp)
+    ms_a, ms_p, nnz, nlev = gm.bench_latent_operators(r, 20)
+    n = X.shape[0]
+    byts = latent_matvec_bytes(n, int(nnz), r)
+    ach = byts / (ms_a * 1e-3) / 1e9
+    t_med = float(np.median(ts))
+    leg = {
+        "metric": "latent Vecchia iterative neg-log-lik + grad evals/sec, n=100k m=30",
+        "value": 1.0 / t_med, "unit": "evals/s", "steps": steps, "ms_per_step": t_med * 1e3,
+        "config": {"workload": "vecchia_latent_gaussian_iterative_vadu", "n": n, "num_neighbors": M_NEIGHBORS,
+                   "cov_pars": LATENT_PARS, "aux": 0.1, "num_rand_vec_trace": LATENT_T, "cg_delta_conv": 1e-2,
+                   "preconditioner": "vadu", "nll": nll, "grad": [float(x) for x in g],
+                   "newton_its": int(info[0]), "cg_its_block": int(info[2])},
+        "cg_matvec_roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                               "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel": "b_apply_wave + bt_apply_wave",
+                               "kernel_ms": ms_a, "columns": r, "algorithmic_bytes_per_launch": byts},
+        "preconditioner": {"kernel": "vadu_levelT (level sets replayed from a hipGraph)", "ms": ms_p,
+                           "levels": int(nlev), "us_per_level": ms_p * 1e3 / max(nlev, 1),
+                           "share_of_eval": None},
+    }
+    its = int(info[2])
+    leg["preconditioner"]["share_of_eval"] = min(1.0, its * ms_p / (t_med * 1e3)) if its > 0 else None
+    if cpu:
+        leg["cpu_baseline"] = latent_cpu_baseline(X, Y)
+    return leg
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-latent", action="store_true", help="skip the secondary latent/iterative leg")
+    ap.add_argument("--latent-steps", type=int, default=3)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -175,10 +275,17 @@ def main():
                      "exp_per_launch": vecchia_exps(N_DATA, M_NEIGHBORS) * rows_local / N_DATA,
                      "note": "fp64 VALU-bound (per-row k<=30 Cholesky + solves); FP64 vector peak = FP64 matrix peak"},
     }
+    traffic = pmc_traffic(rows_local / N_DATA)
+    if traffic is not None:
+        line["roofline"]["traffic"] = traffic["bytes"]
+        line["roofline"]["traffic_source"] = traffic["source"]
     if world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(X, Y)
     else:
         line["cpu_baseline"] = None
+    if world == 1 and not args.no_latent:
+        del gm
+        line["latent_iterative"] = latent_leg(X, Y, args.latent_steps, not args.no_cpu_baseline)
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()

@@ -282,6 +282,12 @@ class GPModel:
         _safe_call(lib().GPB_GetLastKernelTimes(self.handle, _dp(out)))
         return out
 
+    def bench_latent_operators(self, t: int, reps: int = 20):
+        """(ms per A application, ms per preconditioner application, nnz(B), level sets)."""
+        out = np.zeros(4)
+        _safe_call(lib().GPB_BenchLatentOperators(self.handle, ctypes.c_int(t), ctypes.c_int(reps), _dp(out)))
+        return out
+
     def set_distributed(self, rank: int, world_size: int, comm_id: bytes | None):
         buf = ctypes.create_string_buffer(comm_id, len(comm_id)) if comm_id is not None else None
         _safe_call(lib().GPB_SetDistributed(self.handle, ctypes.c_int(rank), ctypes.c_int(world_size), buf))

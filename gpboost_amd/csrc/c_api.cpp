@@ -327,6 +327,12 @@ int GPB_GetLastKernelTimes(REModelHandle handle, double* kernel_ms) {
   API_END();
 }
 
+int GPB_BenchLatentOperators(REModelHandle handle, int t, int reps, double* out) {
+  API_BEGIN();
+  model(handle)->BenchLatentOperators(t, reps, out);
+  API_END();
+}
+
 int GPB_CommIdSize(void) { return (int)sizeof(ncclUniqueId); }
 
 int GPB_CommCreateId(char* id_out) {

@@ -218,7 +218,7 @@ void LatentVecchia::SetY(const double* y_vo) {
 }
 
 LatentVecchia::Block& LatentVecchia::GetBlock(int which, int t, int pmax) {
-  std::unique_ptr<Block>& bp = which == 0 ? blk1_ : blkt_;
+  std::unique_ptr<Block>& bp = which == 0 ? blk1_ : (which == 1 ? blkt_ : blkb_);
   if (!bp) bp.reset(new Block());
   Block& b = *bp;
   if (b.t != t) {
@@ -258,6 +258,32 @@ void LatentVecchia::EnsureProbes(const IterativeConfig& cfg) {
   HIP_CHECK(hipStreamSynchronize(s_));
   probes_t_ = t;
   probes_saved_ = cfg.reuse_rand_vec_trace;
+}
+
+void LatentVecchia::BenchOperators(int t, int reps, double* out) {
+  if (!factor_ready_) Fatal("BenchOperators needs a previous evaluation (the factor of its parameters)");
+  if (t < 1 || reps < 1) Fatal("BenchOperators: t and reps must be >= 1");
+  Block& b = GetBlock(2, t, 1);
+  const size_t nt = (size_t)n_ * t;
+  HIP_CHECK(hipMemsetAsync(b.R.get(), 0, sizeof(double) * nt, s_));   // finite inputs (timing only)
+  HIP_CHECK(hipMemsetAsync(b.H.get(), 0, sizeof(double) * nt, s_));
+  ApplyA(b.H.get(), b.V.get(), b.G.get(), t);              // warm (and graph capture below)
+  PrecondImpl(b.R.get(), b.Z.get(), b.Xt.get(), t);
+  float ms = 0.f;
+  HIP_CHECK(hipEventRecord(ev0_, s_));
+  for (int r = 0; r < reps; ++r) ApplyA(b.H.get(), b.V.get(), b.G.get(), t);
+  HIP_CHECK(hipEventRecord(ev1_, s_));
+  HIP_CHECK(hipEventSynchronize(ev1_));
+  HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_));
+  out[0] = ms / reps;
+  HIP_CHECK(hipEventRecord(ev0_, s_));
+  for (int r = 0; r < reps; ++r) PrecondImpl(b.R.get(), b.Z.get(), b.Xt.get(), t);
+  HIP_CHECK(hipEventRecord(ev1_, s_));
+  HIP_CHECK(hipEventSynchronize(ev1_));
+  HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_));
+  out[1] = ms / reps;
+  out[2] = (double)tnnz_ + n_;
+  out[3] = lplan_.nlev;
 }
 
 // V = (B^T D^-1 B + W) H   (CG_utils.cpp:75, 161-164)
@@ -402,6 +428,8 @@ void LatentVecchia::BuildSweepPlan(const int* nbr, const std::vector<int>& tptr,
     HIP_CHECK(hipGetDevice(&dev));
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     max_flow_blocks_ = 2 * std::max(cus, 1);   // 2 x 256-thread blocks per CU: all resident
+    sf_grid_ = std::max(cus, 1);                  // one single-wave workgroup per CU
+    if (const char* g = std::getenv("GPBOOST_AMD_SF_GRID")) sf_grid_ = std::max(1, std::atoi(g));
   }
   d_err_.alloc(4);
   HIP_CHECK(hipMemsetAsync(d_err_.get(), 0, sizeof(int) * 4, s_));
@@ -464,6 +492,31 @@ void LatentVecchia::PrecondImpl(const double* R, double* Z, double* Xt, int t) {
   }
   if (precond_mode_ == 2) {
     launch_vadu_sweep(plan_, d_dw_.get(), R, Xt, Z, t, s_);
+    return;
+  }
+  if (precond_mode_ == 3) {
+    SfArgs sa{};
+    sa.n = n_;
+    sa.m = m_;
+    sa.t = t;
+    sa.err = d_err_.get();
+    sa.lrows = lplan_.lrows;              // B^T solve: Xt = B^-T R
+    sa.crit = d_crit_.get();
+    sa.eoff = lplan_.beoff;
+    sa.eidx = lplan_.beidx;
+    sa.eval = lplan_.beval;
+    sa.in = R;
+    sa.X = Xt;
+    launch_vadu_sf(sa, false, sf_grid_, s_);
+    sa.lrows = lplan_.lrows + n_;         // lower solve: Z = ((D^-1 + W) B)^-1 Xt
+    sa.crit = d_crit_.get() + n_;
+    sa.eoff = nullptr;
+    sa.eidx = lplan_.fidx;
+    sa.eval = lplan_.fval;
+    sa.dw = d_dw_.get();
+    sa.in = Xt;
+    sa.X = Z;
+    launch_vadu_sf(sa, true, sf_grid_, s_);
     return;
   }
   static const bool eager = std::getenv("GPBOOST_AMD_NO_GRAPH") != nullptr;   // diagnostics (profilers)
@@ -625,6 +678,7 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
   launch_gather(lplan_entries_, d_lslot_.get(), d_Bv_.get(), d_lval_.get(), s_);
   launch_gather(tnnz_, d_tslot_.get(), d_Bv_.get(), d_tval_.get(), s_);   // B^T operator values, list order
   sp_.tval_of = d_Bv_.get();
+  factor_ready_ = true;
 
   Block& b1 = GetBlock(0, 1, std::max(cfg.cg_max_num_it, 1));
   if (std::getenv("GPBOOST_AMD_BENCH_PRECOND")) {   // diagnostics: preconditioner cost alone

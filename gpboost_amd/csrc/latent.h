@@ -56,6 +56,11 @@ class LatentVecchia {
   LatentResult Eval(int cov_type, int lik, const double* trafo, double aux, const IterativeConfig& cfg,
                     bool want_grad, bool want_aux_grad);
 
+  // Operator costs on the factor of the last evaluation (benchmark roofline): out[0] = ms per
+  // A = B^T D^-1 B + W application, out[1] = ms per VADU preconditioner application (both on
+  // t columns, averaged over reps, HIP events on the model's stream), out[2] = nnz(B) incl.
+  // the unit diagonal, out[3] = level sets of the two triangular solves.
+  void BenchOperators(int t, int reps, double* out);
   int num_levels_fwd() const { return (int)fptr_.size() - 1; }
   int num_levels_bwd() const { return (int)bptr_.size() - 1; }
 
@@ -122,8 +127,9 @@ class LatentVecchia {
   struct GraphEntry { const void* key[3]; int t; hipGraphExec_t exec; };
   std::vector<GraphEntry> graphs_;
   bool use_graph_ = true;
-  int precond_mode_ = 1;                         // 0 = sync-free flow kernels, 1 = level graphs, 2 = sweep
+  int precond_mode_ = 1;   // 0 = sync-free flow kernels, 1 = level graphs, 2 = sweep, 3 = sync-free resident waves
   int max_flow_blocks_ = 512;
+  int sf_grid_ = 256;                            // precond_mode_ 3: resident single-wave workgroups
   DevBuf<int> d_err_;
   void BuildSweepPlan(const int* nbr, const std::vector<int>& tptr, const std::vector<int>& trow,
                       const std::vector<int>& tslot, const std::vector<int>& lf, const std::vector<int>& lb);
@@ -137,9 +143,10 @@ class LatentVecchia {
   DevBuf<double> d_partials_, d_out_;
   double* h_out_ = nullptr;                      // pinned
   std::vector<double> h_rr_;
-  std::unique_ptr<Block> blk1_, blkt_;
+  std::unique_ptr<Block> blk1_, blkt_, blkb_;   // blkb_: BenchOperators
   hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
   bool y_set_ = false;
+  bool factor_ready_ = false;
 };
 
 }  // namespace gpb_amd

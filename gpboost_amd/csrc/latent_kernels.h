@@ -110,6 +110,22 @@ struct FlowArgs {
   int n, m, t, shift;
 };
 void launch_vadu_flow(const FlowArgs& a, bool lower, int max_blocks, hipStream_t s);
+// Sync-free form with a fixed grid of resident single-wave workgroups (vadu_sf.hip): position
+// q in [0, n) of the solve's level order is owned by workgroup q mod grid. Same structure
+// arrays as FlowArgs; X is filled with the sentinel by the launcher.
+struct SfArgs {
+  const int* lrows;
+  const int* crit;     // per position: the dependency of highest level (-1: none)
+  const int* eoff;     // B^T solve: entry offsets per position (null for the lower solve)
+  const int* eidx;
+  const double* eval;
+  const double* dw;    // lower solve: input divided by dw
+  const double* in;
+  double* X;
+  int* err;
+  int n, m, t;
+};
+void launch_vadu_sf(const SfArgs& a, bool lower, int grid, hipStream_t s);
 // blob_f64[vpos[e]] = Bv[eslot[e]] for all count entries (per-evaluation value refresh)
 void launch_sweep_values(int count, const int* vpos, const int* eslot, const double* Bv, int* blob, hipStream_t s);
 // dst[p*m + r] = src[rows[p]*m + r]  (n x m, level order)  |  dst[e] = idx[e] >= 0 ? src[idx[e]] : 0

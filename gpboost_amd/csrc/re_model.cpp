@@ -286,6 +286,12 @@ EvalResult REModelAMD::EvalLatent(const double* cov_pars_orig, bool want_grad) {
   return res;
 }
 
+void REModelAMD::BenchLatentOperators(int t, int reps, double* out) {
+  if (!cfg_.latent || !latent_) Fatal("BenchLatentOperators needs an evaluated latent Vecchia (iterative) model");
+  UseDevice();
+  latent_->BenchOperators(t, reps, out);
+}
+
 EvalResult REModelAMD::Eval(const double* cov_pars_orig, bool want_grad, int profile) {
   if (!y_set_) Fatal("response variable y has not been set");
   UseDevice();

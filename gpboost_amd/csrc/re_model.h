@@ -75,6 +75,7 @@ class REModelAMD {
   void GetLatentVecchiaFactor(const double* cov_pars_orig, double* Dinv, double* Bvals, double* dD, double* dBvals);
   // [newton iterations, mode-finding CG iterations, Lanczos steps, log|Sigma W + I|] of the last latent eval
   void GetLastIterationInfo(double* out) const { for (int k = 0; k < 4; ++k) out[k] = last_iter_info_[k]; }
+  void BenchLatentOperators(int t, int reps, double* out);
   void GetLastKernelTimes(double* ms) const { ms[0] = last_kernel_ms_[0]; ms[1] = last_kernel_ms_[1]; }
 
   double last_nll() const { return last_nll_; }
