@@ -283,7 +283,7 @@ class GPModel:
         return out
 
     def bench_latent_operators(self, t: int, reps: int = 20):
-        """(ms per A application, ms per preconditioner application, nnz(B), level sets)."""
+        """(ms per A application, ms per preconditioner application, nnz(B), launches per preconditioner application)."""
         out = np.zeros(4)
         _safe_call(lib().GPB_BenchLatentOperators(self.handle, ctypes.c_int(t), ctypes.c_int(reps), _dp(out)))
         return out

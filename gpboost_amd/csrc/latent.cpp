@@ -63,6 +63,7 @@ LatentVecchia::LatentVecchia(int n, int d, int m, const double* d_X, const int* 
 
 LatentVecchia::~LatentVecchia() {
   for (GraphEntry& g : graphs_) (void)hipGraphExecDestroy(g.exec);
+  for (GraphEntry& g : hgraphs_) (void)hipGraphExecDestroy(g.exec);
   if (h_out_) (void)hipHostFree(h_out_);
   if (ev0_) (void)hipEventDestroy(ev0_);
   if (ev1_) (void)hipEventDestroy(ev1_);
@@ -187,6 +188,7 @@ void LatentVecchia::BuildStructure(const int* nbr) {
   bucket(lf, Lf, fptr_, frows);
   bucket(lb, Lb, bptr_, brows);
   BuildSweepPlan(nbr, tptr, trow, tslot, lf, lb);
+  BuildHeadPlan(nbr, tptr, trow, tslot, lb);
 
   d_nbr_.alloc((size_t)n * m);
   d_tptr_.alloc(n + 1);
@@ -282,8 +284,30 @@ void LatentVecchia::BenchOperators(int t, int reps, double* out) {
   HIP_CHECK(hipEventSynchronize(ev1_));
   HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_));
   out[1] = ms / reps;
+  if (precond_mode_ == 4 && std::getenv("GPBOOST_AMD_PRECOND_SPLIT")) {   // diagnostics: per-part cost
+    const double* dw = d_dw_.get();
+    double* R = b.R.get();
+    double* Xt = b.Xt.get();
+    double* Z = b.Z.get();
+    auto part = [&](const char* name, auto fn) {
+      float pm = 0.f;
+      HIP_CHECK(hipEventRecord(ev0_, s_));
+      for (int r = 0; r < reps; ++r) fn();
+      HIP_CHECK(hipEventRecord(ev1_, s_));
+      HIP_CHECK(hipEventSynchronize(ev1_));
+      HIP_CHECK(hipEventElapsedTime(&pm, ev0_, ev1_));
+      std::fprintf(stderr, "[precond split t=%d] %-12s %.4f ms\n", t, name, pm / reps);
+    };
+    part("tail_bt", [&] { for (int l = 0; l < tplan_.nlev_b; ++l) launch_vadu_level(tplan_, l, dw, R, Xt, Z, t, s_); });
+    part("head_part", [&] { launch_vadu_head_partial(hpart_, R, Xt, t, s_); });
+    part("head_bt", [&] { launch_vadu_head(hbt_, false, dw, nullptr, Xt, t, s_); });
+    part("head_lower", [&] { launch_vadu_head(hlow_, true, dw, Xt, Z, t, s_); });
+    part("tail_lower", [&] { for (int l = tplan_.nlev_b; l < tplan_.nlev; ++l) launch_vadu_level(tplan_, l, dw, R, Xt, Z, t, s_); });
+    std::fprintf(stderr, "[precond split t=%d] K=%d passes lower=%d bt=%d tail levels bt=%d lower=%d\n", t, head_K_,
+                 hlow_.npass, hbt_.npass, tplan_.nlev_b, tplan_.nlev - tplan_.nlev_b);
+  }
   out[2] = (double)tnnz_ + n_;
-  out[3] = lplan_.nlev;
+  out[3] = precond_mode_ == 4 ? tplan_.nlev + 3 : lplan_.nlev;   // dependent launches per application
 }
 
 // V = (B^T D^-1 B + W) H   (CG_utils.cpp:75, 161-164)
@@ -452,6 +476,200 @@ void LatentVecchia::BuildSweepPlan(const int* nbr, const std::vector<int>& tptr,
   plan_.blob = d_blob_.get();
 }
 
+// Head/tail plan of the two solves (precond mode 4; vadu_head.hip explains the split).
+// Head = storage rows whose Vecchia index is < K. In the lower solve a head row depends only
+// on head rows (its neighbours are earlier); in the B^T solve a tail row depends only on tail
+// rows (the rows that have it as a neighbour are later). So: lower = head kernel, then the
+// tail levels (levels over tail dependencies only; head values are final by then); B^T = the
+// tail levels (the full-DAG levels lb, exact for tail rows), then the tail contributions to
+// the head rows (one launch), then the head kernel over head-only dependencies.
+void LatentVecchia::BuildHeadPlan(const int* nbr, const std::vector<int>& tptr, const std::vector<int>& trow,
+                                  const std::vector<int>& tslot, const std::vector<int>& lb) {
+  const int n = n_, m = m_;
+  int K = 12288;   // 96 KB of LDS per column workgroup
+  if (const char* e = std::getenv("GPBOOST_AMD_HEAD_ROWS")) K = std::atoi(e);
+  K = std::max(0, std::min(std::min(K, kHeadMaxRows), n));
+  head_K_ = K;
+  const int nt = n - K;
+  auto head = [&](int p) { return vo_[p] < K; };
+  std::vector<int> ints;       // every index array of the plan, one upload
+  std::vector<int> vslot;      // value slots into Bv (-1: zero padding), one gather per evaluation
+  auto put = [&](const std::vector<int>& v) { const size_t at = ints.size(); ints.insert(ints.end(), v.begin(), v.end()); return at; };
+  // ---- tail level plan
+  std::vector<int> lt(n, 0);
+  int Lb = 0, Lt = 0;
+  for (int ii = K; ii < n; ++ii) {
+    const int i = lab_[ii];
+    const int k = std::min(i, m);
+    int l = 0;
+    for (int r = 0; r < k; ++r) {
+      const int j = nbr[(size_t)i * m + r];
+      if (!head(j)) l = std::max(l, lt[j] + 1);
+    }
+    lt[i] = l;
+    Lt = std::max(Lt, l + 1);
+    Lb = std::max(Lb, lb[i] + 1);
+  }
+  auto by_level = [&](const std::vector<int>& lev, int L) {
+    std::vector<std::vector<int>> b(L);
+    for (int p = 0; p < n; ++p)
+      if (!head(p)) b[lev[p]].push_back(p);
+    return b;
+  };
+  std::vector<int> lrows, beoff(1, 0), beidx, fidx, beslot, fslot;
+  tplan_.lptr.assign(1, 0);
+  for (const auto& rows : by_level(lb, Lb)) {
+    for (int j : rows) {
+      lrows.push_back(j);
+      for (int e = tptr[j]; e < tptr[j + 1]; ++e) { beidx.push_back(trow[e]); beslot.push_back(tslot[e]); }
+      beoff.push_back((int)beidx.size());
+    }
+    tplan_.lptr.push_back((int)lrows.size());
+  }
+  for (const auto& rows : by_level(lt, Lt)) {
+    for (int i : rows) {
+      lrows.push_back(i);
+      const int k = std::min(i, m);
+      for (int r = 0; r < m; ++r) {
+        fidx.push_back(r < k ? nbr[(size_t)i * m + r] : 0);
+        fslot.push_back(r < k ? i * m + r : -1);
+      }
+    }
+    tplan_.lptr.push_back((int)lrows.size());
+  }
+  tplan_.n = nt;
+  tplan_.m = m;
+  tplan_.nlev_b = nt > 0 ? Lb : 0;
+  tplan_.nlev = (int)tplan_.lptr.size() - 1;
+  if (nt == 0) { tplan_.lptr.assign(1, 0); tplan_.nlev = 0; }
+  const size_t o_lrows = put(lrows), o_beoff = put(beoff), o_beidx = put(beidx), o_fidx = put(fidx);
+  const size_t v_be = vslot.size();
+  vslot.insert(vslot.end(), beslot.begin(), beslot.end());
+  const size_t v_f = vslot.size();
+  vslot.insert(vslot.end(), fslot.begin(), fslot.end());
+  // ---- head solves: positions by level (head-only dependencies), passes of <= kHeadRowsPerPass
+  struct HeadArrays { std::vector<int> rec, eidx, slot, ooff{0}, oidx, oslot; };
+  auto build_head = [&](bool lower) {
+    HeadArrays h;
+    const int epl = lower ? kHeadEplLower : kHeadEplUpper, fix = epl * kHeadG;
+    std::vector<int> lev(K, 0);
+    std::vector<std::vector<int>> deps(K), dslot(K);
+    for (int ii = 0; ii < K; ++ii) {
+      const int p = lab_[ii];
+      if (lower) {
+        const int k = std::min(p, m);
+        for (int r = 0; r < k; ++r) { deps[ii].push_back(vo_[nbr[(size_t)p * m + r]]); dslot[ii].push_back(p * m + r); }
+      } else {
+        for (int e = tptr[p]; e < tptr[p + 1]; ++e)
+          if (head(trow[e])) { deps[ii].push_back(vo_[trow[e]]); dslot[ii].push_back(tslot[e]); }
+      }
+    }
+    int L = 0;
+    for (int s = 0; s < K; ++s) {   // lower: ascending Vecchia index; B^T: descending
+      const int ii = lower ? s : K - 1 - s;
+      int l = 0;
+      for (int d : deps[ii]) l = std::max(l, lev[d] + 1);
+      lev[ii] = l;
+      L = std::max(L, l + 1);
+    }
+    std::vector<std::vector<int>> byl(L);
+    for (int s = 0; s < K; ++s) {
+      const int ii = lower ? s : K - 1 - s;
+      byl[lev[ii]].push_back(ii);
+    }
+    for (const auto& rows : byl) {
+      for (size_t q0 = 0; q0 < rows.size(); q0 += kHeadRowsPerPass) {
+        for (int q = 0; q < kHeadRowsPerPass; ++q) {
+          const size_t base = h.eidx.size();
+          h.eidx.resize(base + fix, 0);
+          h.slot.resize(base + fix, -1);
+          if (q0 + q >= rows.size()) {
+            h.rec.push_back(K);
+            h.ooff.push_back((int)h.oidx.size());
+            continue;
+          }
+          const int ii = rows[q0 + q];
+          const int cnt = (int)deps[ii].size();
+          for (int e = 0; e < std::min(cnt, fix); ++e) {   // entry e -> lane e % G, k = e / G
+            const size_t at = base + (size_t)(e / kHeadG) * kHeadG + e % kHeadG;
+            h.eidx[at] = deps[ii][e];
+            h.slot[at] = dslot[ii][e];
+          }
+          for (int e = fix; e < cnt; ++e) { h.oidx.push_back(deps[ii][e]); h.oslot.push_back(dslot[ii][e]); }
+          h.rec.push_back(cnt > fix ? (int)(0x80000000u | (unsigned)ii) : ii);
+          h.ooff.push_back((int)h.oidx.size());
+        }
+      }
+    }
+    return h;
+  };
+  HeadArrays hl = build_head(true), hb = build_head(false);
+  // B^T tail contributions to every head row (rows without any still copy R)
+  std::vector<int> prow, poff(1, 0), pidx, pslot;
+  for (int ii = 0; ii < K; ++ii) {
+    const int j = lab_[ii];
+    prow.push_back(j);
+    for (int e = tptr[j]; e < tptr[j + 1]; ++e)
+      if (!head(trow[e])) { pidx.push_back(trow[e]); pslot.push_back(tslot[e]); }
+    poff.push_back((int)pidx.size());
+  }
+  std::vector<int> hrow(K);
+  for (int v = 0; v < K; ++v) hrow[v] = lab_[v];
+  const size_t o_hrow = put(hrow);
+  size_t o_h[2][4], v_h[2][2];
+  for (int w = 0; w < 2; ++w) {
+    HeadArrays& h = w == 0 ? hl : hb;
+    o_h[w][0] = put(h.rec);
+    o_h[w][1] = put(h.eidx);
+    o_h[w][2] = put(h.oidx);
+    o_h[w][3] = put(h.ooff);
+    v_h[w][0] = vslot.size();
+    vslot.insert(vslot.end(), h.slot.begin(), h.slot.end());
+    v_h[w][1] = vslot.size();
+    vslot.insert(vslot.end(), h.oslot.begin(), h.oslot.end());
+  }
+  const size_t o_prow = put(prow), o_poff = put(poff), o_pidx = put(pidx);
+  const size_t v_p = vslot.size();
+  vslot.insert(vslot.end(), pslot.begin(), pslot.end());
+  d_hint_.alloc(std::max<size_t>(ints.size(), 1));
+  d_hslot_.alloc(std::max<size_t>(vslot.size(), 1));
+  d_hval_.alloc(std::max<size_t>(vslot.size(), 1));
+  if (!ints.empty())
+    HIP_CHECK(hipMemcpyAsync(d_hint_.get(), ints.data(), sizeof(int) * ints.size(), hipMemcpyHostToDevice, s_));
+  if (!vslot.empty())
+    HIP_CHECK(hipMemcpyAsync(d_hslot_.get(), vslot.data(), sizeof(int) * vslot.size(), hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  hslot_count_ = (int)vslot.size();
+  const int* I = d_hint_.get();
+  const double* V = d_hval_.get();
+  tplan_.lrows = I + o_lrows;
+  tplan_.beoff = I + o_beoff;
+  tplan_.beidx = I + o_beidx;
+  tplan_.fidx = I + o_fidx;
+  tplan_.beval = V + v_be;
+  tplan_.fval = V + v_f;
+  for (int w = 0; w < 2; ++w) {
+    HeadSolve& h = w == 0 ? hlow_ : hbt_;
+    const HeadArrays& a = w == 0 ? hl : hb;
+    h.K = K;
+    h.npass = (int)(a.rec.size() / kHeadRowsPerPass);
+    h.hrow = I + o_hrow;
+    h.rec = I + o_h[w][0];
+    h.eidx = I + o_h[w][1];
+    h.oidx = I + o_h[w][2];
+    h.ooff = I + o_h[w][3];
+    h.eval = V + v_h[w][0];
+    h.oval = V + v_h[w][1];
+  }
+  hpart_.rows = K;
+  hpart_.row = I + o_prow;
+  hpart_.eoff = I + o_poff;
+  hpart_.eidx = I + o_pidx;
+  hpart_.eval = V + v_p;
+  head_passes_ = hlow_.npass + hbt_.npass;
+  if (K > 0) set_vadu_head_lds_limit(K);
+}
+
 // Z = P^-1 R, P = B^T (D^-1 + W) B (VADU, CG_utils.cpp:56-60): B^T solve then (dw B) solve.
 // Default: one kernel per level replayed from a hipGraph captured once per buffer set
 // (a graph boundary costs ~1.5 us, far below a host launch); alternative: the one-launch
@@ -520,6 +738,32 @@ void LatentVecchia::PrecondImpl(const double* R, double* Z, double* Xt, int t) {
     return;
   }
   static const bool eager = std::getenv("GPBOOST_AMD_NO_GRAPH") != nullptr;   // diagnostics (profilers)
+  if (precond_mode_ == 4) {
+    auto record = [&]() {
+      for (int l = 0; l < tplan_.nlev_b; ++l) launch_vadu_level(tplan_, l, d_dw_.get(), R, Xt, Z, t, s_);
+      launch_vadu_head_partial(hpart_, R, Xt, t, s_);
+      launch_vadu_head(hbt_, false, d_dw_.get(), nullptr, Xt, t, s_);
+      launch_vadu_head(hlow_, true, d_dw_.get(), Xt, Z, t, s_);
+      for (int l = tplan_.nlev_b; l < tplan_.nlev; ++l) launch_vadu_level(tplan_, l, d_dw_.get(), R, Xt, Z, t, s_);
+    };
+    if (eager) { record(); return; }
+    for (const GraphEntry& g : hgraphs_) {
+      if (g.key[0] == R && g.key[1] == Xt && g.key[2] == Z && g.t == t) {
+        HIP_CHECK(hipGraphLaunch(g.exec, s_));
+        return;
+      }
+    }
+    hipGraph_t graph;
+    HIP_CHECK(hipStreamBeginCapture(s_, hipStreamCaptureModeThreadLocal));
+    record();
+    HIP_CHECK(hipStreamEndCapture(s_, &graph));
+    GraphEntry e{{R, Xt, Z}, t, nullptr};
+    HIP_CHECK(hipGraphInstantiate(&e.exec, graph, nullptr, nullptr, 0));
+    HIP_CHECK(hipGraphDestroy(graph));
+    hgraphs_.push_back(e);
+    HIP_CHECK(hipGraphLaunch(e.exec, s_));
+    return;
+  }
   if (eager) {
     for (int l = 0; l < lplan_.nlev; ++l) launch_vadu_level(lplan_, l, d_dw_.get(), R, Xt, Z, t, s_);
     return;
@@ -676,6 +920,7 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
   launch_latent_factor(cov_type, fa, s_);
   launch_sweep_values(plan_entries_, d_vpos_.get(), d_eslot_.get(), d_Bv_.get(), d_blob_.get(), s_);
   launch_gather(lplan_entries_, d_lslot_.get(), d_Bv_.get(), d_lval_.get(), s_);
+  launch_gather(hslot_count_, d_hslot_.get(), d_Bv_.get(), d_hval_.get(), s_);
   launch_gather(tnnz_, d_tslot_.get(), d_Bv_.get(), d_tval_.get(), s_);   // B^T operator values, list order
   sp_.tval_of = d_Bv_.get();
   factor_ready_ = true;

@@ -127,7 +127,19 @@ class LatentVecchia {
   struct GraphEntry { const void* key[3]; int t; hipGraphExec_t exec; };
   std::vector<GraphEntry> graphs_;
   bool use_graph_ = true;
-  int precond_mode_ = 1;   // 0 = sync-free flow kernels, 1 = level graphs, 2 = sweep, 3 = sync-free resident waves
+  // 0 = sync-free flow kernels, 1 = level graphs, 2 = sweep, 3 = sync-free resident waves,
+  // 4 = head/tail split (head kernels + tail level graphs)
+  int precond_mode_ = 4;
+  // head/tail plan (BuildHeadPlan): tail level plan, the two head solves, the B^T partial
+  LevelPlan tplan_{};
+  HeadSolve hlow_{}, hbt_{};
+  HeadPartial hpart_{};
+  DevBuf<int> d_hint_, d_hslot_;
+  DevBuf<double> d_hval_;
+  int hslot_count_ = 0, head_K_ = 0, head_passes_ = 0;
+  std::vector<GraphEntry> hgraphs_;
+  void BuildHeadPlan(const int* nbr, const std::vector<int>& tptr, const std::vector<int>& trow,
+                     const std::vector<int>& tslot, const std::vector<int>& lb);
   int max_flow_blocks_ = 512;
   int sf_grid_ = 256;                            // precond_mode_ 3: resident single-wave workgroups
   DevBuf<int> d_err_;

@@ -126,6 +126,45 @@ struct SfArgs {
   int n, m, t;
 };
 void launch_vadu_sf(const SfArgs& a, bool lower, int grid, hipStream_t s);
+// Head/tail split of the two solves (precond mode 4, vadu_head.hip). Head = the first K rows
+// in Vecchia order (a thin, deep part of the DAG), solved by ONE workgroup per column with the
+// column's head values in LDS (slot = Vecchia index < K); tail = the other rows, by the level
+// kernels on a LevelPlan of the tail rows only. Lower solve: head, then tail levels. B^T
+// solve: tail levels, then launch_vadu_head_partial (tail contributions to head rows), then
+// the head.
+// One solve's head rows in level order are cut into passes of at most kHeadRowsPerPass rows
+// of ONE level. Record r = q * kHeadRowsPerPass + slot of pass q: the row's LDS slot (K =
+// padding), bit 31 set when the row has overflow entries [ooff[r], ooff[r+1]). Entries (head
+// dependencies only) in a fixed lane-major layout: entry k < EPL of lane l of record r at
+// ((r * EPL + k) * kHeadG + l) (zero value = padding); a row's entries beyond kHeadG * EPL
+// go to the overflow lists.
+constexpr int kHeadRowsPerPass = 64;
+constexpr int kHeadMaxRows = 16384;  // K limit: 128 KB of LDS per column workgroup
+constexpr int kHeadG = 16;            // lanes per row
+constexpr int kHeadEplLower = 2;      // lower solve: k_i <= m <= 32 entries per row
+constexpr int kHeadEplUpper = 4;      // B^T solve: early rows have many dependents
+struct HeadSolve {
+  int K;              // head rows = LDS slots (+ 1 scratch slot)
+  int npass;
+  const int* hrow;    // K: storage row of head slot v (Vecchia index v)
+  const int* rec;     // npass * kHeadRowsPerPass records
+  const int* eidx;    // fixed layout: LDS slot of the dependency
+  const double* eval; // fixed layout: B value (refreshed per evaluation)
+  const int* ooff;    // npass * kHeadRowsPerPass + 1
+  const int* oidx;    // overflow entries
+  const double* oval;
+};
+struct HeadPartial {  // B^T solve: tail rows' contributions to the head rows
+  int rows;
+  const int* row;     // storage row of head row w
+  const int* eoff;    // entries [eoff[w], eoff[w+1])
+  const int* eidx;    // storage row of the (tail) dependency
+  const double* eval;
+};
+void launch_vadu_head(const HeadSolve& h, bool lower, const double* dw, const double* in, double* X, int t,
+                      hipStream_t s);
+void launch_vadu_head_partial(const HeadPartial& h, const double* R, double* X, int t, hipStream_t s);
+void set_vadu_head_lds_limit(int K);
 // blob_f64[vpos[e]] = Bv[eslot[e]] for all count entries (per-evaluation value refresh)
 void launch_sweep_values(int count, const int* vpos, const int* eslot, const double* Bv, int* blob, hipStream_t s);
 // dst[p*m + r] = src[rows[p]*m + r]  (n x m, level order)  |  dst[e] = idx[e] >= 0 ? src[idx[e]] : 0

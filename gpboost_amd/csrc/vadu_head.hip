@@ -1,0 +1,187 @@
+// Head/tail split of the VADU triangular solves (precond mode 4, the default).
+//
+// Reference replaced: the two sparse triangular solves of the VADU preconditioner
+// P^-1 = B^-1 (D^-1 + W)^-1 B^-T (CG_utils.cpp:56-60, likelihoods.h:11963-12041 and the
+// Lanczos variant CG_utils.cpp:110-217).
+//
+// Why: in a random Vecchia ordering the dependency DAG is thin at its early end — row i
+// depends on its m nearest EARLIER points, which for small i are spread over the whole
+// domain. At n = 100k, m = 30 the first 12288 Vecchia rows already span ~280 of the 388
+// dependency levels, with ~44 rows per level; the remaining 88% of the rows fit in ~110
+// wide levels. One launch per level (launch_vadu_level, ~4.9 us each at t = 51) is pure
+// latency on the thin part. Here ONE workgroup per column solves the whole head with that
+// column's head values resident in LDS: a level costs an LDS gather + a workgroup barrier,
+// and the next pass's structure (global) is loaded while the current one computes.
+//
+// Row arithmetic is the reference's: x_i = in_i (/ dw_i) - sum_e v_e x_{idx_e}; the entries
+// are split over G = 16 lanes (lane l: entries l, l+16, ...) and combined by a fixed xor
+// tree, so repeated runs are bitwise identical.
+#include <hip/hip_runtime.h>
+
+#include "common.h"
+#include "latent_kernels.h"
+#include "wave_ops.h"
+
+namespace gpb_amd {
+namespace {
+
+constexpr int kHeadThreads = kHeadRowsPerPass * kHeadG;
+
+// LDS writes of this wave done, then the workgroup barrier. Global accesses are left in
+// flight on purpose (prefetched structure; result stores nobody reads inside the launch),
+// which a __syncthreads() (workgroup release: vmcnt(0)) would drain.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
+// Stage of one pass on this thread: its row's record and this lane's EPL fixed-layout
+// entries. Every address is a function of the pass index alone (no dependent loads), so the
+// next pass's stage is in flight while this one gathers from LDS; the loop is unrolled by
+// two so the stages alternate between two register sets (a copy would force a wait).
+template <int EPL>
+struct Stage {
+  int loc;             // LDS slot of the row (K = padding); bit 31 set: the row has overflow entries
+  int id[EPL];
+  double v[EPL];
+};
+
+template <int EPL>
+__device__ __forceinline__ void load_stage(const HeadSolve& h, int q, int slot, int lane, Stage<EPL>& st) {
+  const int r = q * kHeadRowsPerPass + slot;
+  st.loc = h.rec[r];
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) {
+    const size_t e = ((size_t)r * EPL + k) * kHeadG + lane;
+    st.id[k] = h.eidx[e];
+    st.v[k] = h.eval[e];
+  }
+}
+
+template <bool LOWER, int EPL>
+__device__ __forceinline__ void solve_row(const HeadSolve& h, const Stage<EPL>& st, int q, int slot, int lane,
+                                          double* xs) {
+  double acc = 0.;
+#pragma unroll
+  for (int k = 0; k < EPL; ++k) acc = fma(st.v[k], xs[st.id[k]], acc);
+  if (st.loc < 0) {   // long row (B^T solve: early rows have many dependents)
+    const int r = q * kHeadRowsPerPass + slot;
+    for (int e = h.ooff[r] + lane; e < h.ooff[r + 1]; e += kHeadG) acc = fma(h.oval[e], xs[h.oidx[e]], acc);
+  }
+#pragma unroll
+  for (int off = kHeadG / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if (lane == 0) xs[st.loc & 0x7fffffff] -= acc;
+}
+
+template <bool LOWER, int EPL>
+__global__ void __launch_bounds__(kHeadThreads) vadu_head_kernel(HeadSolve h, int t, const double* __restrict__ dw,
+                                                                 const double* in, double* X) {
+  extern __shared__ double xs[];   // this column's head values, slot = Vecchia index; slot K = scratch
+  const int c = blockIdx.x;
+  const int lane = threadIdx.x & (kHeadG - 1);
+  const int slot = threadIdx.x / kHeadG;
+  // inputs of all head rows first (independent loads): in / dw (lower), or the B^T input
+  // minus the tail contributions (head_partial wrote it into X)
+  constexpr int kPer = (kHeadMaxRows + kHeadThreads - 1) / kHeadThreads;
+  {   // all loads of the phase in flight at once (no loop-carried wait)
+    int r[kPer];
+    double x[kPer], w[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int v = threadIdx.x + k * kHeadThreads;
+      r[k] = h.hrow[v < h.K ? v : 0];
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      x[k] = LOWER ? in[(size_t)r[k] * t + c] : X[(size_t)r[k] * t + c];
+      w[k] = LOWER ? dw[r[k]] : 1.;
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int v = threadIdx.x + k * kHeadThreads;
+      if (v < h.K) xs[v] = LOWER ? x[k] / w[k] : x[k];
+    }
+  }
+  if (threadIdx.x == 0) xs[h.K] = 0.;
+  __syncthreads();
+  const int last = h.npass - 1;
+  Stage<EPL> A, B;
+  load_stage<EPL>(h, 0, slot, lane, A);
+  for (int q = 0; q < h.npass; q += 2) {
+    load_stage<EPL>(h, min(q + 1, last), slot, lane, B);
+    solve_row<LOWER, EPL>(h, A, q, slot, lane, xs);
+    lds_barrier();
+    if (q + 1 > last) break;
+    load_stage<EPL>(h, min(q + 2, last), slot, lane, A);
+    solve_row<LOWER, EPL>(h, B, min(q + 1, last), slot, lane, xs);
+    lds_barrier();
+  }
+  // results out after the loop: a global store inside it would make the compiler drain the
+  // prefetch (its registers are reused by the next stage's loads)
+  __syncthreads();
+  int r[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int v = threadIdx.x + k * kHeadThreads;
+    r[k] = h.hrow[v < h.K ? v : 0];
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int v = threadIdx.x + k * kHeadThreads;
+    if (v < h.K) X[(size_t)r[k] * t + c] = xs[v];
+  }
+}
+
+// B^T solve, before the head: X[j] = R[j] - sum over the TAIL rows i that have head row j as
+// a neighbour of B(i, j) X[i] (all those X[i] are final: the tail is solved first). One wave
+// per head row, lane = column, entries ascending through v_readlane.
+__global__ void __launch_bounds__(256) vadu_head_partial_kernel(HeadPartial h, const double* __restrict__ R,
+                                                                double* X, int t) {
+  const int lane = threadIdx.x & 63;
+  const int w = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  if (w >= h.rows) return;
+  const int j = h.row[w];
+  const int c = lane + blockIdx.y * 64;
+  const int cc = c < t ? c : t - 1;
+  const int e0 = h.eoff[w], e1 = h.eoff[w + 1];
+  double acc = 0.;
+  for (int b0 = e0; b0 < e1; b0 += 64) {
+    const int e = b0 + lane;
+    const bool ok = e < e1;
+    const int my_id = ok ? h.eidx[e] : j;
+    const double my_w = ok ? h.eval[e] : 0.;
+    const int cnt = e1 - b0 < 64 ? e1 - b0 : 64;
+    acc = wave_dot<16>(my_id, my_w, cnt, X, t, cc, j, acc);
+  }
+  if (c < t) X[(size_t)j * t + c] = R[(size_t)j * t + c] - acc;
+}
+
+}  // namespace
+
+void launch_vadu_head(const HeadSolve& h, bool lower, const double* dw, const double* in, double* X, int t,
+                      hipStream_t s) {
+  if (h.npass <= 0 || t <= 0) return;
+  const size_t lds = sizeof(double) * ((size_t)h.K + 1);
+  if (lower)
+    hipLaunchKernelGGL((vadu_head_kernel<true, kHeadEplLower>), dim3(t), dim3(kHeadThreads), lds, s, h, t, dw, in, X);
+  else
+    hipLaunchKernelGGL((vadu_head_kernel<false, kHeadEplUpper>), dim3(t), dim3(kHeadThreads), lds, s, h, t, dw, in,
+                       X);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_vadu_head_partial(const HeadPartial& h, const double* R, double* X, int t, hipStream_t s) {
+  if (h.rows <= 0 || t <= 0) return;
+  hipLaunchKernelGGL(vadu_head_partial_kernel, dim3((h.rows + 3) / 4, (t + 63) / 64), dim3(256), 0, s, h, R, X,
+                     t);
+  HIP_CHECK(hipGetLastError());
+}
+
+void set_vadu_head_lds_limit(int K) {
+  const int bytes = (int)(sizeof(double) * ((size_t)K + 1));
+  HIP_CHECK(hipFuncSetAttribute((const void*)vadu_head_kernel<true, kHeadEplLower>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIP_CHECK(hipFuncSetAttribute((const void*)vadu_head_kernel<false, kHeadEplUpper>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+}
+
+}  // namespace gpb_amd

@@ -212,8 +212,9 @@ GPBOOST_AMD_EXPORT int GPB_GetLastKernelTimes(REModelHandle handle, double* kern
 /* Benchmark support (latent Vecchia, iterative): device time of the operator
  * A = B^T D^-1 B + W and of the VADU preconditioner on t columns, on the factor of the last
  * evaluation (HIP events, averaged over reps). out[0] = ms per A application, out[1] = ms
- * per preconditioner application, out[2] = nnz(B) incl. the unit diagonal, out[3] = level
- * sets of the two triangular solves. No reference counterpart (measurement only). */
+ * per preconditioner application, out[2] = nnz(B) incl. the unit diagonal, out[3] = dependent
+ * kernel launches per preconditioner application (level sets of the tail + the head
+ * kernels). No reference counterpart (measurement only). */
 GPBOOST_AMD_EXPORT int GPB_BenchLatentOperators(REModelHandle handle, int t, int reps, double* out);
 
 /* ---------------------------------------------------------------- EXTENSION: multi-GPU */
