@@ -209,6 +209,14 @@ void LatentVecchia::BuildStructure(const int* nbr) {
   d_tval_.alloc(trow.size());
   sp_.tval = d_tval_.get();
   sp_.tval_of = nullptr;   // set once the values of an evaluation are gathered
+  std::vector<int> longr;
+  for (int j = 0; j < n; ++j)
+    if (tptr[j + 1] - tptr[j] > kLongRow) longr.push_back(j);
+  d_longr_.alloc(std::max<size_t>(longr.size(), 1));
+  if (!longr.empty())
+    HIP_CHECK(hipMemcpy(d_longr_.get(), longr.data(), sizeof(int) * longr.size(), hipMemcpyHostToDevice));
+  sp_.longr = d_longr_.get();
+  sp_.nlong = (int)longr.size();
 }
 
 void LatentVecchia::SetY(const double* y_vo) {
@@ -551,7 +559,6 @@ void LatentVecchia::BuildHeadPlan(const int* nbr, const std::vector<int>& tptr, 
   struct HeadArrays { std::vector<int> rec, eidx, slot, ooff{0}, oidx, oslot; };
   auto build_head = [&](bool lower) {
     HeadArrays h;
-    const int epl = lower ? kHeadEplLower : kHeadEplUpper, fix = epl * kHeadG;
     std::vector<int> lev(K, 0);
     std::vector<std::vector<int>> deps(K), dslot(K);
     for (int ii = 0; ii < K; ++ii) {
@@ -577,28 +584,44 @@ void LatentVecchia::BuildHeadPlan(const int* nbr, const std::vector<int>& tptr, 
       const int ii = lower ? s : K - 1 - s;
       byl[lev[ii]].push_back(ii);
     }
-    for (const auto& rows : byl) {
-      for (size_t q0 = 0; q0 < rows.size(); q0 += kHeadRowsPerPass) {
-        for (int q = 0; q < kHeadRowsPerPass; ++q) {
-          const size_t base = h.eidx.size();
-          h.eidx.resize(base + fix, 0);
-          h.slot.resize(base + fix, -1);
-          if (q0 + q >= rows.size()) {
-            h.rec.push_back(K);
-            h.ooff.push_back((int)h.oidx.size());
-            continue;
-          }
-          const int ii = rows[q0 + q];
+    const int E = kHeadEpl;
+    auto nslots = [&](int ii) {   // 1, 2 or 4 slots of kHeadG lanes (rows beyond 4 slots overflow)
+      const int c = (int)deps[ii].size();
+      return c <= kHeadG * E ? 1 : c <= 2 * kHeadG * E ? 2 : 4;
+    };
+    for (auto rows : byl) {
+      // widest rows first: power-of-two sizes in descending order stay aligned in a pass
+      std::stable_sort(rows.begin(), rows.end(), [&](int x, int y) { return nslots(x) > nslots(y); });
+      size_t q = 0;
+      while (q < rows.size()) {   // one pass
+        const size_t r_pass = h.rec.size();
+        h.rec.resize(r_pass + kHeadRowsPerPass, K);
+        h.ooff.resize(r_pass + kHeadRowsPerPass + 1, (int)h.oidx.size());
+        h.eidx.resize((r_pass + kHeadRowsPerPass) * E * kHeadG, 0);
+        h.slot.resize((r_pass + kHeadRowsPerPass) * E * kHeadG, -1);
+        int used = 0;
+        while (q < rows.size() && used + nslots(rows[q]) <= kHeadRowsPerPass) {
+          const int ii = rows[q], ns = nslots(ii), GL = ns * kHeadG;
+          const int lg = ns == 1 ? 0 : ns == 2 ? 1 : 2;
+          const size_t r0 = r_pass + used;
           const int cnt = (int)deps[ii].size();
-          for (int e = 0; e < std::min(cnt, fix); ++e) {   // entry e -> lane e % G, k = e / G
-            const size_t at = base + (size_t)(e / kHeadG) * kHeadG + e % kHeadG;
+          const bool over = cnt > GL * E;
+          for (int sub = 0; sub < ns; ++sub)
+            h.rec[r0 + sub] = (int)((over ? 0x80000000u : 0u) | ((unsigned)sub << 18) | ((unsigned)lg << 16) |
+                                    (unsigned)(sub == 0 ? ii : K));
+          for (int e = 0; e < std::min(cnt, GL * E); ++e) {   // entry e -> group lane e % GL, k = e / GL
+            const int gl = e % GL, k = e / GL;
+            const size_t at = ((r0 + gl / kHeadG) * E + k) * kHeadG + gl % kHeadG;
             h.eidx[at] = deps[ii][e];
             h.slot[at] = dslot[ii][e];
           }
-          for (int e = fix; e < cnt; ++e) { h.oidx.push_back(deps[ii][e]); h.oslot.push_back(dslot[ii][e]); }
-          h.rec.push_back(cnt > fix ? (int)(0x80000000u | (unsigned)ii) : ii);
-          h.ooff.push_back((int)h.oidx.size());
+          h.ooff[r0] = (int)h.oidx.size();
+          for (int e = GL * E; e < cnt; ++e) { h.oidx.push_back(deps[ii][e]); h.oslot.push_back(dslot[ii][e]); }
+          for (int sub = 1; sub <= ns; ++sub) h.ooff[r0 + sub] = (int)h.oidx.size();
+          used += ns;
+          ++q;
         }
+        for (size_t r = r_pass + used; r <= r_pass + kHeadRowsPerPass; ++r) h.ooff[r] = (int)h.oidx.size();
       }
     }
     return h;

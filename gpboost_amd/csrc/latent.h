@@ -110,7 +110,7 @@ class LatentVecchia {
   DevBuf<double> d_tval_;       // B values in transposed-list order (refreshed per evaluation)
   int tnnz_ = 0;
   SparseB sp_{};
-  DevBuf<int> d_nbr_, d_tptr_, d_trow_, d_tslot_;
+  DevBuf<int> d_nbr_, d_tptr_, d_trow_, d_tslot_, d_longr_;
   // step plan of the two VADU triangular solves (see SweepPlan)
   std::vector<int> fptr_, bptr_;           // level pointers (host, diagnostics)
   SweepPlan plan_{};

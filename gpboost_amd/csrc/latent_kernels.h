@@ -41,7 +41,12 @@ struct SparseB {
   // (refreshed per evaluation); launch_bt_apply reads it when vals == tval_of
   const double* tval;
   const double* tval_of;
+  // rows j whose transposed list is longer than kLongRow (early Vecchia rows are the
+  // neighbours of hundreds of later rows): the t = 1 operator gives each a whole wave
+  const int* longr;
+  int nlong;
 };
+constexpr int kLongRow = 64;
 
 // Y = diag(scale) (unit*X + V X)   with V = vals on the B pattern (rows list optional)
 void launch_b_apply(const SparseB& B, const double* vals, bool unit, const double* X, int t, const double* scale,
@@ -133,16 +138,18 @@ void launch_vadu_sf(const SfArgs& a, bool lower, int grid, hipStream_t s);
 // solve: tail levels, then launch_vadu_head_partial (tail contributions to head rows), then
 // the head.
 // One solve's head rows in level order are cut into passes of at most kHeadRowsPerPass rows
-// of ONE level. Record r = q * kHeadRowsPerPass + slot of pass q: the row's LDS slot (K =
-// padding), bit 31 set when the row has overflow entries [ooff[r], ooff[r+1]). Entries (head
-// dependencies only) in a fixed lane-major layout: entry k < EPL of lane l of record r at
-// ((r * EPL + k) * kHeadG + l) (zero value = padding); a row's entries beyond kHeadG * EPL
-// go to the overflow lists.
+// of ONE level. A pass has kHeadRowsPerPass slots of kHeadG lanes; a row takes 1, 2 or 4
+// consecutive slots (aligned; by its entry count), so its group has GL = kHeadG << lg lanes.
+// Record r = q * kHeadRowsPerPass + slot: bits 0-15 the row's LDS slot (K = padding), bits
+// 16-17 lg, bits 18-19 the slot's index within the row, bit 31 set when the row has overflow
+// entries [ooff[r0], ooff[r0 + 1]) (r0 = the row's first slot). Entries (head dependencies
+// only) in a fixed lane-major layout: entry e < GL * EPL of the row sits at group lane
+// gl = e % GL, k = e / GL, i.e. slot r0 + gl / kHeadG, position ((r * EPL + k) * kHeadG + gl %
+// kHeadG) (zero value = padding); entries beyond GL * EPL go to the overflow lists.
 constexpr int kHeadRowsPerPass = 64;
 constexpr int kHeadMaxRows = 16384;  // K limit: 128 KB of LDS per column workgroup
-constexpr int kHeadG = 16;            // lanes per row
-constexpr int kHeadEplLower = 2;      // lower solve: k_i <= m <= 32 entries per row
-constexpr int kHeadEplUpper = 4;      // B^T solve: early rows have many dependents
+constexpr int kHeadG = 16;            // lanes per slot
+constexpr int kHeadEpl = 2;           // fixed-layout entries per lane
 struct HeadSolve {
   int K;              // head rows = LDS slots (+ 1 scratch slot)
   int npass;

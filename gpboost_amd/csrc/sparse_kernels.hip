@@ -280,6 +280,156 @@ __global__ void __launch_bounds__(kBT) bt_apply1_kernel(int n, const int* __rest
   }
 }
 
+// t = 1, several rows per lane group in flight: a group of G lanes owns R rows (rows
+// base + q * (kBT / G)) and issues every structure load of all R rows, then every gather, then
+// reduces. The one-row forms above are latency-bound (structure load -> gather -> store per
+// row, ~50 blocks per CU in turn); here each wave keeps R times as many loads in flight.
+// Lane l holds entries l and l + G of a row (m <= 2G); the B^T form loops over the rest.
+constexpr int k1G = 16, k1R = 4;
+
+template <int G, int R>
+__global__ void __launch_bounds__(kBT) b_apply1m_kernel(int n, int m, const int* __restrict__ nbr,
+                                                        const double* __restrict__ vals, int unit,
+                                                        const double* __restrict__ X,
+                                                        const double* __restrict__ scale, double* __restrict__ Y) {
+  constexpr int NG = kBT / G;
+  const int lane = threadIdx.x & (G - 1);
+  const int base = xcd_block(blockIdx.x, gridDim.x) * (NG * R) + (int)threadIdx.x / G;
+  int id[R][2];
+  double w[R][2], g[R][2], xs[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    const int i = base + q * NG;
+    const int k = i < n ? min(i, m) : 0;
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int r = lane + e * G;
+      const bool ok = r < k;
+      const size_t o = (size_t)i * m + r;
+      id[q][e] = ok ? nbr[o] : 0;
+      w[q][e] = ok ? vals[o] : 0.;
+    }
+    xs[q] = (unit && lane == 0 && i < n) ? X[i] : 0.;
+  }
+#pragma unroll
+  for (int q = 0; q < R; ++q)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) g[q][e] = X[id[q][e]];
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    double acc = fma(w[q][1], g[q][1], w[q][0] * g[q][0]);
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    const int i = base + q * NG;
+    if (lane == 0 && i < n) {
+      double s = xs[q] + acc;
+      if (scale) s *= scale[i];
+      Y[i] = s;
+    }
+  }
+}
+
+// Rows longer than kLongRow: one wave each, lanes stride the list, 4 chunks of loads in
+// flight (a 16-lane group walking a 300-entry list was the launch's critical path).
+__device__ __forceinline__ void bt_long_row(int j, const int* __restrict__ tptr, const int* __restrict__ trow,
+                                            const double* __restrict__ tval, int unit, const double* __restrict__ X,
+                                            const double* __restrict__ pre, const double* __restrict__ W,
+                                            const double* __restrict__ H, double* __restrict__ Y) {
+  const int lane = threadIdx.x & 63;
+  const int e0 = tptr[j], e1 = tptr[j + 1];
+  double acc = 0.;
+  for (int b = e0 + lane; b < e1; b += 4 * 64) {
+    int id[4];
+    double w[4], g[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int e = b + k * 64;
+      const bool ok = e < e1;
+      id[k] = ok ? trow[e] : 0;
+      w[k] = ok ? tval[e] : 0.;
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      g[k] = X[id[k]];
+      if (pre) w[k] *= pre[id[k]];
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc = fma(w[k], g[k], acc);
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  if (lane == 0) {
+    double s = unit ? (pre ? pre[j] * X[j] : X[j]) : 0.;
+    s += acc;
+    if (W) s = fma(W[j], H[j], s);
+    Y[j] = s;
+  }
+}
+
+template <int G, int R>
+__global__ void __launch_bounds__(kBT) bt_apply1m_kernel(int n, const int* __restrict__ tptr,
+                                                         const int* __restrict__ trow,
+                                                         const double* __restrict__ tval, int unit,
+                                                         const double* __restrict__ X,
+                                                         const double* __restrict__ pre,
+                                                         const double* __restrict__ W,
+                                                         const double* __restrict__ H, double* __restrict__ Y,
+                                                         int nmain, const int* __restrict__ longr, int nlong) {
+  if ((int)blockIdx.x >= nmain) {   // trailing blocks: the long rows, one wave each
+    const int w = ((int)blockIdx.x - nmain) * (kBT / 64) + (int)(threadIdx.x >> 6);
+    if (w < nlong) bt_long_row(longr[w], tptr, trow, tval, unit, X, pre, W, H, Y);
+    return;
+  }
+  constexpr int NG = kBT / G;
+  const int lane = threadIdx.x & (G - 1);
+  const int base = xcd_block(blockIdx.x, nmain) * (NG * R) + (int)threadIdx.x / G;
+  int e0[R], e1[R], id[R][2];
+  double w[R][2], g[R][2], xs[R], wv[R], hv[R];
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    const int j = base + q * NG;
+    e0[q] = j < n ? tptr[j] : 0;
+    e1[q] = j < n ? tptr[j + 1] : 0;
+    if (e1[q] - e0[q] > kLongRow) e1[q] = e0[q];   // a long-row wave writes this row
+    const bool own = lane == 0 && j < n;
+    xs[q] = (unit && own) ? (pre ? pre[j] * X[j] : X[j]) : 0.;
+    wv[q] = (W && own) ? W[j] : 0.;
+    hv[q] = (W && own) ? H[j] : 0.;
+  }
+#pragma unroll
+  for (int q = 0; q < R; ++q)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int ee = e0[q] + lane + e * G;
+      const bool ok = ee < e1[q];
+      id[q][e] = ok ? trow[ee] : 0;
+      w[q][e] = ok ? tval[ee] : 0.;
+    }
+#pragma unroll
+  for (int q = 0; q < R; ++q)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      g[q][e] = X[id[q][e]];
+      if (pre) w[q][e] *= pre[id[q][e]];
+    }
+#pragma unroll
+  for (int q = 0; q < R; ++q) {
+    double acc = fma(w[q][1], g[q][1], w[q][0] * g[q][0]);
+    for (int ee = e0[q] + lane + 2 * G; ee < e1[q]; ee += G) {   // rows with > 2G entries
+      const int i = trow[ee];
+      acc = fma(pre ? tval[ee] * pre[i] : tval[ee], X[i], acc);
+    }
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    const int j = base + q * NG;
+    if (lane == 0 && j < n && tptr[j + 1] - tptr[j] <= kLongRow) {
+      double s = xs[q] + acc;
+      if (W) s = fma(wv[q], hv[q], s);
+      Y[j] = s;
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kBT) gather_rows_kernel(int n, int m, const int* __restrict__ rows,
                                                           const double* __restrict__ src, double* __restrict__ dst) {
   const size_t total = (size_t)n * m;
@@ -651,6 +801,13 @@ SpmvForm spmv_form() {
 void launch_b_apply(const SparseB& B, const double* vals, bool unit, const double* X, int t, const double* scale,
                     double* Y, hipStream_t s) {
   if (B.n <= 0) return;
+  static const bool old1 = std::getenv("GPBOOST_AMD_SPMV1_OLD") != nullptr;   // A/B: one row per group
+  if (t == 1 && B.m <= 2 * k1G && !old1) {
+    hipLaunchKernelGGL((b_apply1m_kernel<k1G, k1R>), dim3(grid_x(B.n, kBT / k1G * k1R, 1 << 30)), dim3(kBT), 0, s,
+                       B.n, B.m, B.nbr, vals, unit ? 1 : 0, X, scale, Y);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (t == 1) {
     constexpr int G = 32;
     hipLaunchKernelGGL(b_apply1_kernel<G>, dim3(grid_x(B.n, kBT / G, 1 << 30)), dim3(kBT), 0, s, B.n, B.m, B.nbr,
@@ -684,6 +841,15 @@ void launch_bt_apply(const SparseB& B, const double* vals, bool unit, const doub
                      const double* W, const double* H, double* Y, hipStream_t s) {
   if (B.n <= 0) return;
   const double* tval = (B.tval != nullptr && vals == B.tval_of) ? B.tval : nullptr;
+  static const bool old1 = std::getenv("GPBOOST_AMD_SPMV1_OLD") != nullptr;
+  if (t == 1 && tval != nullptr && !old1) {
+    const int nmain = grid_x(B.n, kBT / k1G * k1R, 1 << 30);
+    const int nlb = (B.nlong + kBT / 64 - 1) / (kBT / 64);
+    hipLaunchKernelGGL((bt_apply1m_kernel<k1G, k1R>), dim3(nmain + nlb), dim3(kBT), 0, s, B.n, B.tptr, B.trow, tval,
+                       unit ? 1 : 0, X, pre, W, H, Y, nmain, B.longr, B.nlong);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (t == 1 && tval != nullptr) {
     constexpr int G = 32;
     hipLaunchKernelGGL(bt_apply1_kernel<G>, dim3(grid_x(B.n, kBT / G, 1 << 30)), dim3(kBT), 0, s, B.n, B.tptr,

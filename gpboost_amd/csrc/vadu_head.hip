@@ -34,13 +34,13 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// Stage of one pass on this thread: its row's record and this lane's EPL fixed-layout
-// entries. Every address is a function of the pass index alone (no dependent loads), so the
-// next pass's stage is in flight while this one gathers from LDS; the loop is unrolled by
-// two so the stages alternate between two register sets (a copy would force a wait).
+// Stage of one pass on this thread: its record and this lane's EPL fixed-layout entries.
+// Every address is a function of the pass index alone (no dependent loads), so the next
+// pass's stage is in flight while this one gathers from LDS; the loop is unrolled by two so
+// the stages alternate between two register sets (a copy would force a wait).
 template <int EPL>
 struct Stage {
-  int loc;             // LDS slot of the row (K = padding); bit 31 set: the row has overflow entries
+  int rec;             // see HeadSolve (latent_kernels.h)
   int id[EPL];
   double v[EPL];
 };
@@ -48,7 +48,7 @@ struct Stage {
 template <int EPL>
 __device__ __forceinline__ void load_stage(const HeadSolve& h, int q, int slot, int lane, Stage<EPL>& st) {
   const int r = q * kHeadRowsPerPass + slot;
-  st.loc = h.rec[r];
+  st.rec = h.rec[r];
 #pragma unroll
   for (int k = 0; k < EPL; ++k) {
     const size_t e = ((size_t)r * EPL + k) * kHeadG + lane;
@@ -57,19 +57,31 @@ __device__ __forceinline__ void load_stage(const HeadSolve& h, int q, int slot, 
   }
 }
 
-template <bool LOWER, int EPL>
+// A row spans 1, 2 or 4 slots (16 << lg lanes); group lane gl = sub * 16 + lane holds its
+// entries gl + k * GL (k < EPL), then overflow entries [ooff[r0], ooff[r0 + 1]) in steps of GL.
+template <int EPL>
 __device__ __forceinline__ void solve_row(const HeadSolve& h, const Stage<EPL>& st, int q, int slot, int lane,
                                           double* xs) {
+  const int lg = (st.rec >> 16) & 3, sub = (st.rec >> 18) & 3;
   double acc = 0.;
 #pragma unroll
   for (int k = 0; k < EPL; ++k) acc = fma(st.v[k], xs[st.id[k]], acc);
-  if (st.loc < 0) {   // long row (B^T solve: early rows have many dependents)
-    const int r = q * kHeadRowsPerPass + slot;
-    for (int e = h.ooff[r] + lane; e < h.ooff[r + 1]; e += kHeadG) acc = fma(h.oval[e], xs[h.oidx[e]], acc);
+  if (st.rec < 0) {   // long row: overflow entries
+    const int r0 = q * kHeadRowsPerPass + slot - sub;
+    const int GL = kHeadG << lg;
+    for (int e = h.ooff[r0] + sub * kHeadG + lane; e < h.ooff[r0 + 1]; e += GL) acc = fma(h.oval[e], xs[h.oidx[e]], acc);
   }
 #pragma unroll
   for (int off = kHeadG / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
-  if (lane == 0) xs[st.loc & 0x7fffffff] -= acc;
+  if (__ballot(lg >= 1)) {   // wave-uniform: only waves holding a multi-slot row pay the cross-slot steps
+    const double o16 = __shfl_xor(acc, 16, 64);
+    if (lg >= 1) acc += o16;
+    if (__ballot(lg >= 2)) {
+      const double o32 = __shfl_xor(acc, 32, 64);
+      if (lg >= 2) acc += o32;
+    }
+  }
+  if (lane == 0 && sub == 0) xs[st.rec & 0xffff] -= acc;
 }
 
 template <bool LOWER, int EPL>
@@ -108,11 +120,11 @@ __global__ void __launch_bounds__(kHeadThreads) vadu_head_kernel(HeadSolve h, in
   load_stage<EPL>(h, 0, slot, lane, A);
   for (int q = 0; q < h.npass; q += 2) {
     load_stage<EPL>(h, min(q + 1, last), slot, lane, B);
-    solve_row<LOWER, EPL>(h, A, q, slot, lane, xs);
+    solve_row<EPL>(h, A, q, slot, lane, xs);
     lds_barrier();
     if (q + 1 > last) break;
     load_stage<EPL>(h, min(q + 2, last), slot, lane, A);
-    solve_row<LOWER, EPL>(h, B, min(q + 1, last), slot, lane, xs);
+    solve_row<EPL>(h, B, min(q + 1, last), slot, lane, xs);
     lds_barrier();
   }
   // results out after the loop: a global store inside it would make the compiler drain the
@@ -162,9 +174,9 @@ void launch_vadu_head(const HeadSolve& h, bool lower, const double* dw, const do
   if (h.npass <= 0 || t <= 0) return;
   const size_t lds = sizeof(double) * ((size_t)h.K + 1);
   if (lower)
-    hipLaunchKernelGGL((vadu_head_kernel<true, kHeadEplLower>), dim3(t), dim3(kHeadThreads), lds, s, h, t, dw, in, X);
+    hipLaunchKernelGGL((vadu_head_kernel<true, kHeadEpl>), dim3(t), dim3(kHeadThreads), lds, s, h, t, dw, in, X);
   else
-    hipLaunchKernelGGL((vadu_head_kernel<false, kHeadEplUpper>), dim3(t), dim3(kHeadThreads), lds, s, h, t, dw, in,
+    hipLaunchKernelGGL((vadu_head_kernel<false, kHeadEpl>), dim3(t), dim3(kHeadThreads), lds, s, h, t, dw, in,
                        X);
   HIP_CHECK(hipGetLastError());
 }
@@ -178,9 +190,9 @@ void launch_vadu_head_partial(const HeadPartial& h, const double* R, double* X, 
 
 void set_vadu_head_lds_limit(int K) {
   const int bytes = (int)(sizeof(double) * ((size_t)K + 1));
-  HIP_CHECK(hipFuncSetAttribute((const void*)vadu_head_kernel<true, kHeadEplLower>,
+  HIP_CHECK(hipFuncSetAttribute((const void*)vadu_head_kernel<true, kHeadEpl>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  HIP_CHECK(hipFuncSetAttribute((const void*)vadu_head_kernel<false, kHeadEplUpper>,
+  HIP_CHECK(hipFuncSetAttribute((const void*)vadu_head_kernel<false, kHeadEpl>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
 }
 
