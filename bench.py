@@ -179,6 +179,14 @@ def latent_leg(X, Y, steps: int, cpu: bool) -> dict:
                            "launches": int(nlev), "us_per_launch": ms_p * 1e3 / max(nlev, 1),
                            "share_of_eval": None},
     }
+    # the single-vector CG of the Newton / mode-finding solves (CGVecchiaLaplaceVec, CG_utils.cpp:21-108)
+    ms_a1, ms_p1, _, _ = gm.bench_latent_operators(1, 50)
+    byts1 = latent_matvec_bytes(n, int(nnz), 1)
+    ach1 = byts1 / (ms_a1 * 1e-3) / 1e9
+    leg["cg_matvec_roofline_single"] = {"bound": "hbm", "achieved": ach1, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                        "frac": ach1 / HBM_PEAK_GBS, "traffic": None,
+                                        "kernel": "b_apply1m + bt_apply1m", "kernel_ms": ms_a1, "columns": 1,
+                                        "algorithmic_bytes_per_launch": byts1, "preconditioner_ms": ms_p1}
     its = int(info[2])
     leg["preconditioner"]["share_of_eval"] = min(1.0, its * ms_p / (t_med * 1e3)) if its > 0 else None
     if cpu:

@@ -225,14 +225,26 @@ class GPModel:
         profile_sigma2=True : the reference's L-BFGS objective unit (sigma2 profiled out).
         Returns (nll, grad, sigma2)."""
         y = self._check_y(y)
-        cp = self._check_cov_pars(cov_pars)
         fe = _as1d(fixed_effects, "fixed_effects") if fixed_effects is not None else None
-        negll = np.zeros(1)
-        grad = np.full(self.num_cov_pars + self.num_aux_pars, np.nan)
-        s2 = np.zeros(1)
+        # per-model argument buffers and their ctypes pointers, made once: an L-BFGS loop calls
+        # this every iteration and the device evaluation itself takes well under a millisecond
+        if getattr(self, "_eval_bufs", None) is None:
+            bufs = dict(cp=np.zeros(self.num_cov_pars), negll=np.zeros(1),
+                        grad=np.zeros(self.num_cov_pars + self.num_aux_pars), s2=np.zeros(1))
+            self._eval_bufs = (bufs, {k: _dp(v) for k, v in bufs.items()})
+        bufs, ptrs = self._eval_bufs
+        cp = bufs["cp"]
+        v = np.asarray(cov_pars, dtype=np.float64).reshape(-1)
+        if v.shape[0] != self.num_cov_pars:
+            raise ValueError("'cov_pars' does not contain the correct number of parameters")
+        cp[:] = v
+        if not np.isfinite(cp).all():
+            raise ValueError("'cov_pars' contains NaN or Inf")
+        negll, grad, s2 = bufs["negll"], bufs["grad"], bufs["s2"]
+        grad.fill(np.nan)
         _safe_call(lib().GPB_EvalNegLogLikelihoodGrad(
-            self.handle, _dp(y) if y is not None else None, _dp(cp), _dp(fe) if fe is not None else None,
-            int(bool(profile_sigma2)), _dp(negll), _dp(grad), _dp(s2)))
+            self.handle, _dp(y) if y is not None else None, ptrs["cp"], _dp(fe) if fe is not None else None,
+            int(bool(profile_sigma2)), ptrs["negll"], ptrs["grad"], ptrs["s2"]))
         if profile_sigma2:
             g = grad[: self.num_cov_pars - 1]
         elif self.num_aux_pars and self.params["estimate_aux_pars"]:

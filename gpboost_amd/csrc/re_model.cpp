@@ -89,6 +89,7 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
   HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_sums_), 16 * sizeof(double), hipHostMallocDefault));
+  HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_sums_dev_), h_sums_, 0));
   row_begin_ = 0;
   row_end_ = n;
   if (vecchia_) {
@@ -228,20 +229,32 @@ void REModelAMD::LaunchVecchiaRows(const double* trafo, int r0, int r1, double* 
   HIP_CHECK(hipEventRecord(ev_[0], stream_));
   launch_vecchia_rows(cfg_.cov_type, a, stream_);
   HIP_CHECK(hipEventRecord(ev_[1], stream_));
-  launch_sum_blocks(d_block_sums_.get(), nblocks, kVecchiaSums, d_sums_.get(), stream_);
   if (allreduce && world_ > 1) {
+    launch_sum_blocks(d_block_sums_.get(), nblocks, kVecchiaSums, d_sums_.get(), stream_);
     ncclResult_t r = ncclAllReduce(d_sums_.get(), d_sums_.get(), kVecchiaSums, ncclDouble, ncclSum, comm_, stream_);
     if (r != ncclSuccess) Fatal("ncclAllReduce failed: %s", ncclGetErrorString(r));
+    HIP_CHECK(hipMemcpyAsync(h_sums_, d_sums_.get(), sizeof(double) * kVecchiaSums, hipMemcpyDeviceToHost, stream_));
+  } else {   // one rank: the fixed-order block sum writes the pinned host buffer directly (no copy launch)
+    launch_sum_blocks(d_block_sums_.get(), nblocks, kVecchiaSums, h_sums_dev_, stream_);
   }
-  HIP_CHECK(hipMemcpyAsync(h_sums_, d_sums_.get(), sizeof(double) * kVecchiaSums, hipMemcpyDeviceToHost, stream_));
   HIP_CHECK(hipEventRecord(ev_[2], stream_));
   HIP_CHECK(hipStreamSynchronize(stream_));
-  float ms0 = 0.f, ms1 = 0.f;
-  HIP_CHECK(hipEventElapsedTime(&ms0, ev_[0], ev_[1]));
-  HIP_CHECK(hipEventElapsedTime(&ms1, ev_[0], ev_[2]));
-  last_kernel_ms_[0] = ms0;
-  last_kernel_ms_[1] = ms1;
+  events_pending_ = true;   // kernel times are read from the events only when asked for
   std::copy(h_sums_, h_sums_ + kVecchiaSums, sums);
+}
+
+void REModelAMD::GetLastKernelTimes(double* ms) {
+  if (events_pending_) {
+    UseDevice();
+    float ms0 = 0.f, ms1 = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms0, ev_[0], ev_[1]));
+    HIP_CHECK(hipEventElapsedTime(&ms1, ev_[0], ev_[2]));
+    last_kernel_ms_[0] = ms0;
+    last_kernel_ms_[1] = ms1;
+    events_pending_ = false;
+  }
+  ms[0] = last_kernel_ms_[0];
+  ms[1] = last_kernel_ms_[1];
 }
 
 void REModelAMD::EvalVecchia(const double* trafo, double* sums) {
@@ -261,6 +274,7 @@ void REModelAMD::EvalVecchiaPartials(const double* cov_pars_orig, int r0, int r1
 }
 
 void REModelAMD::EvalDense(const double* trafo, bool want_grad, double* sums) {
+  events_pending_ = false;
   dense_->Eval(cfg_.cov_type, trafo[1], trafo[2], d_y_.get(), want_grad, sums, last_kernel_ms_);
 }
 
@@ -280,6 +294,7 @@ EvalResult REModelAMD::EvalLatent(const double* cov_pars_orig, bool want_grad) {
   last_iter_info_[1] = r.cg_its;
   last_iter_info_[2] = r.lanczos_steps;
   last_iter_info_[3] = r.logdet;
+  events_pending_ = false;
   last_kernel_ms_[0] = last_kernel_ms_[1] = r.ms_total;
   last_nll_ = res.nll;
   last_cov_pars_.assign(cov_pars_orig, cov_pars_orig + 2);

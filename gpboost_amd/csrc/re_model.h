@@ -76,7 +76,7 @@ class REModelAMD {
   // [newton iterations, mode-finding CG iterations, Lanczos steps, log|Sigma W + I|] of the last latent eval
   void GetLastIterationInfo(double* out) const { for (int k = 0; k < 4; ++k) out[k] = last_iter_info_[k]; }
   void BenchLatentOperators(int t, int reps, double* out);
-  void GetLastKernelTimes(double* ms) const { ms[0] = last_kernel_ms_[0]; ms[1] = last_kernel_ms_[1]; }
+  void GetLastKernelTimes(double* ms);
 
   double last_nll() const { return last_nll_; }
   const std::vector<double>& last_cov_pars() const { return last_cov_pars_; }
@@ -112,6 +112,8 @@ class REModelAMD {
   DevBuf<double> d_X_, d_y_, d_block_sums_, d_sums_;
   DevBuf<int> d_nbr_;
   double* h_sums_ = nullptr;  // pinned
+  double* h_sums_dev_ = nullptr;  // device address of h_sums_ (the single-rank sum kernel writes it directly)
+  bool events_pending_ = false;   // last_kernel_ms_ of the last row launch not read from its events yet
 
   std::unique_ptr<DenseSolver> dense_;
   std::unique_ptr<LatentVecchia> latent_;
