@@ -150,7 +150,11 @@ void REModelAMD::BuildVecchiaStructure() {
   // Only this rank's rows are needed on the device (each row's neighbours are earlier points).
   nbr_.assign((size_t)(row_end_ - row_begin_) * m, -1);
   nbr_row0_ = row_begin_;
-  vecchia_neighbors(coords_vo_.data(), n, cfg_.d, m, row_begin_, row_end_, nbr_.data());
+  static const bool host_knn = std::getenv("GPBOOST_AMD_HOST_KNN") != nullptr;   // A/B: host OpenMP search
+  if (host_knn || m > 64 || cfg_.d > 3)
+    vecchia_neighbors(coords_vo_.data(), n, cfg_.d, m, row_begin_, row_end_, nbr_.data());
+  else
+    vecchia_neighbors_gpu(coords_vo_.data(), n, cfg_.d, m, row_begin_, row_end_, nbr_.data(), stream_);
   // Device copy laid out by global row index (rows outside this rank's block untouched).
   d_nbr_.alloc((size_t)n * m);
   HIP_CHECK(hipMemcpyAsync(d_nbr_.get() + (size_t)row_begin_ * m, nbr_.data(), sizeof(int) * nbr_.size(),

@@ -1,5 +1,7 @@
 #pragma once
 
+#include <hip/hip_runtime.h>
+
 #include <vector>
 
 namespace gpb_amd {
@@ -11,5 +13,9 @@ std::vector<int> vecchia_order(int n, int seed, bool random);
 // (row-major n x d). nbr has (row_end - row_begin) x m entries; row i holds min(i, m)
 // indices in ascending distance, the rest -1. Requires m <= n - 1.
 void vecchia_neighbors(const double* x, int n, int d, int m, int row_begin, int row_end, int* nbr);
+// Same lists, searched on the GPU (vecchia_knn.hip): one thread per row runs the identical
+// sweep; bit-identical output. Synchronous on stream s.
+void vecchia_neighbors_gpu(const double* x, int n, int d, int m, int row_begin, int row_end, int* nbr,
+                           hipStream_t s);
 
 }  // namespace gpb_amd

@@ -192,3 +192,17 @@ def test_row_block_partials_sum_to_whole():
         nll_w, g_w, _ = combine_partials(tot, n, pars[0], True)
         assert abs(nll_w - nll) <= 1e-10 * abs(nll)
         np.testing.assert_allclose(g_w, g, rtol=1e-9)
+
+
+@pytest.mark.parametrize("m", [4, 10, 30])
+def test_gpu_neighbor_search_ties_bit_exact(m):
+    """GPU neighbour search (vecchia_knn.hip) on integer-grid coordinates, where squared distances
+    and coordinate sums tie massively: the lists must equal the oracle's restatement of the
+    reference sweep (Vecchia_utils.cpp:732-1058), i.e. ties resolve in the same candidate order."""
+    g = np.arange(30, dtype=np.float64)
+    X = np.array([(a, b) for a in g for b in g])[:700] / 7.0
+    gm = _model(X, m)
+    perm, nbr = gm.vecchia_structure()
+    ref_perm, _, ref_nbr = O.vecchia_setup(X, m, 0, True)
+    assert np.array_equal(perm, ref_perm)
+    assert np.array_equal(nbr, ref_nbr)
