@@ -10,13 +10,15 @@
 // Every GEMM-shaped step (TRSM-as-GEMM with the inverted diagonal block, panel and trailing
 // updates, the TRTRI products and LAUUM) goes through one MFMA kernel:
 //   C[M x N] = alpha * op(A) op(B) + beta * C,  64 x 64 output tile per 256-thread workgroup,
-//   4 waves x (32 x 32) = 2 x 2 v_mfma_f64_16x16x4 tiles per wave, K staged through LDS in steps of 16,
+//   4 waves x (32 x 32) = 2 x 2 v_mfma_f64_16x16x4 tiles per wave, K staged through LDS in steps of 16
+//   (large problems: 128 x 128 tiles, 4 x 4 MFMA tiles per wave, double-buffered K staging),
 // with per-tile K ranges that skip the structural zeros of triangular operands and optional
 // skipping of output tiles above the diagonal.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 #include "cov.h"
@@ -100,6 +102,110 @@ __global__ void __launch_bounds__(256) gemm_f64_kernel(GemmArgs g) {
   for (int a = 0; a < 2; ++a)
 #pragma unroll
     for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int i = m0 + wm + a * 16 + (lane >> 4) + 4 * rg;
+        const int j = n0 + wn + b * 16 + (lane & 15);
+        if (i < g.M && j < g.N && !(g.lower_out && j > i)) {
+          double* c = g.C + (size_t)i + (size_t)j * g.ldc;
+          const double prev = (g.beta == 0.) ? 0. : g.beta * (*c);
+          *c = prev + g.alpha * acc[a][b][rg];
+        }
+      }
+}
+
+// Large-tile form for the big updates (trailing SYRK, TRTRI/LAUUM products): 128 x 128 output
+// tile per 256-thread workgroup, each wave 64 x 64 = 4 x 4 MFMA tiles (16 MFMAs per 8 LDS
+// reads instead of 4 per 4), K staged in steps of 16 through two LDS buffers: the next step's
+// operands are loaded into registers while the current step's MFMAs run, one barrier per step.
+// Same masks, K ranges and summation order per output element as gemm_f64_kernel (k ascending
+// in steps of 4 through the MFMA).
+constexpr int TB = 128;
+
+__global__ void __launch_bounds__(256) gemm_f64_big_kernel(GemmArgs g) {
+  __shared__ double As[2][TK][TB + 1];
+  __shared__ double Bs[2][TK][TB + 1];
+  const int m0 = blockIdx.y * TB, n0 = blockIdx.x * TB;
+  if (g.lower_out && n0 > m0 + TB - 1) return;
+  int k_begin = 0, k_end = g.K;
+  if (g.a_lower) k_end = min(k_end, m0 + TB);
+  if (g.a_upper) k_begin = max(k_begin, m0);
+  if (g.b_lower) k_begin = max(k_begin, n0);
+  k_begin = (k_begin / TK) * TK;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;   // wave's 64 x 64 sub-tile
+  double4_t acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b) acc[a][b] = (double4_t){0., 0., 0., 0.};
+
+  double ra[8], rb[8];
+  auto load = [&](int kk) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int idx = tid + e * 256;
+      int i, k;
+      if (g.transA) { k = idx & 15; i = idx >> 4; } else { i = idx & 127; k = idx >> 7; }
+      const int gi = m0 + i, gk = kk + k;
+      double v = 0.;
+      if (gi < g.M && gk < k_end && gk >= k_begin && !(g.a_lower && gk > gi) && !(g.a_upper && gk < gi))
+        v = g.transA ? g.A[(size_t)gk + (size_t)gi * g.lda] : g.A[(size_t)gi + (size_t)gk * g.lda];
+      ra[e] = v;
+      int j, kb;
+      if (g.transB) { j = idx & 127; kb = idx >> 7; } else { kb = idx & 15; j = idx >> 4; }
+      const int gj = n0 + j, gkb = kk + kb;
+      double w = 0.;
+      if (gj < g.N && gkb < k_end && gkb >= k_begin && !(g.b_lower && gkb < gj))
+        w = g.transB ? g.B[(size_t)gj + (size_t)gkb * g.ldb] : g.B[(size_t)gkb + (size_t)gj * g.ldb];
+      rb[e] = w;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int idx = tid + e * 256;
+      int i, k;
+      if (g.transA) { k = idx & 15; i = idx >> 4; } else { i = idx & 127; k = idx >> 7; }
+      As[buf][k][i] = ra[e];
+      int j, kb;
+      if (g.transB) { j = idx & 127; kb = idx >> 7; } else { kb = idx & 15; j = idx >> 4; }
+      Bs[buf][kb][j] = rb[e];
+    }
+  };
+  if (k_begin < k_end) {
+    load(k_begin);
+    store(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int kk = k_begin; kk < k_end; kk += TK) {
+    const bool more = kk + TK < k_end;
+    if (more) load(kk + TK);   // in flight during this step's MFMAs
+#pragma unroll
+    for (int k4 = 0; k4 < TK; k4 += 4) {
+      const int kl = k4 + (lane >> 4);
+      double a[4], b[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        a[q] = As[buf][kl][wm + 16 * q + (lane & 15)];
+        b[q] = Bs[buf][kl][wn + 16 * q + (lane & 15)];
+      }
+#pragma unroll
+      for (int p = 0; p < 4; ++p)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc[p][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[p], b[q], acc[p][q], 0, 0, 0);
+    }
+    if (more) store(buf ^ 1);   // the other buffer: last read before the previous barrier
+    __syncthreads();
+    buf ^= 1;
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int b = 0; b < 4; ++b)
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {
         const int i = m0 + wm + a * 16 + (lane >> 4) + 4 * rg;
@@ -298,6 +404,15 @@ void gemm(hipStream_t s, int M, int N, int K, double alpha, const double* A, int
           int b_lower = 0) {
   if (M <= 0 || N <= 0) return;
   GemmArgs g{M, N, K, alpha, beta, A, lda, transA, B, ldb, transB, C, ldc, lower_out, a_lower, a_upper, b_lower};
+  static const bool small_only = std::getenv("GPBOOST_AMD_GEMM64") != nullptr;   // A/B: 64 x 64 tiles only
+  // large tiles only where they still give every CU two tiles (small problems keep the 64 x 64
+  // form's parallelism: n = 2000 measured 7.6 ms vs 8.6 ms per evaluation with 128 x 128 tiles)
+  if ((long)((M + TB - 1) / TB) * ((N + TB - 1) / TB) >= 512 && !small_only) {
+    dim3 grid((N + TB - 1) / TB, (M + TB - 1) / TB);
+    hipLaunchKernelGGL(gemm_f64_big_kernel, grid, dim3(256), 0, s, g);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM);
   hipLaunchKernelGGL(gemm_f64_kernel, grid, dim3(256), 0, s, g);
   HIP_CHECK(hipGetLastError());
