@@ -116,22 +116,22 @@ __global__ void __launch_bounds__(256) gemm_f64_kernel(GemmArgs g) {
 
 // Large-tile form for the big updates (trailing SYRK, TRTRI/LAUUM products): 128 x 128 output
 // tile per 256-thread workgroup, each wave 64 x 64 = 4 x 4 MFMA tiles (16 MFMAs per 8 LDS
-// reads instead of 4 per 4), K staged in steps of 16 through two LDS buffers: the next step's
+// reads instead of 4 per 4), K staged in steps of 32 through two LDS buffers: the next step's
 // operands are loaded into registers while the current step's MFMAs run, one barrier per step.
 // Same masks, K ranges and summation order per output element as gemm_f64_kernel (k ascending
 // in steps of 4 through the MFMA).
-constexpr int TB = 128;
+constexpr int TB = 128, TKB = 32;   // K step 32: 128 MFMAs per wave between barriers
 
 __global__ void __launch_bounds__(256) gemm_f64_big_kernel(GemmArgs g) {
-  __shared__ double As[2][TK][TB + 1];
-  __shared__ double Bs[2][TK][TB + 1];
+  __shared__ double As[2][TKB][TB + 1];
+  __shared__ double Bs[2][TKB][TB + 1];
   const int m0 = blockIdx.y * TB, n0 = blockIdx.x * TB;
   if (g.lower_out && n0 > m0 + TB - 1) return;
   int k_begin = 0, k_end = g.K;
   if (g.a_lower) k_end = min(k_end, m0 + TB);
   if (g.a_upper) k_begin = max(k_begin, m0);
   if (g.b_lower) k_begin = max(k_begin, n0);
-  k_begin = (k_begin / TK) * TK;
+  k_begin = (k_begin / TKB) * TKB;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -142,20 +142,21 @@ __global__ void __launch_bounds__(256) gemm_f64_big_kernel(GemmArgs g) {
 #pragma unroll
     for (int b = 0; b < 4; ++b) acc[a][b] = (double4_t){0., 0., 0., 0.};
 
-  double ra[8], rb[8];
+  constexpr int EPT = TKB * TB / 256;   // staged elements per thread and operand
+  double ra[EPT], rb[EPT];
   auto load = [&](int kk) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
+    for (int e = 0; e < EPT; ++e) {
       const int idx = tid + e * 256;
       int i, k;
-      if (g.transA) { k = idx & 15; i = idx >> 4; } else { i = idx & 127; k = idx >> 7; }
+      if (g.transA) { k = idx & (TKB - 1); i = idx / TKB; } else { i = idx & 127; k = idx >> 7; }
       const int gi = m0 + i, gk = kk + k;
       double v = 0.;
       if (gi < g.M && gk < k_end && gk >= k_begin && !(g.a_lower && gk > gi) && !(g.a_upper && gk < gi))
         v = g.transA ? g.A[(size_t)gk + (size_t)gi * g.lda] : g.A[(size_t)gi + (size_t)gk * g.lda];
       ra[e] = v;
       int j, kb;
-      if (g.transB) { j = idx & 127; kb = idx >> 7; } else { kb = idx & 15; j = idx >> 4; }
+      if (g.transB) { j = idx & 127; kb = idx >> 7; } else { kb = idx & (TKB - 1); j = idx / TKB; }
       const int gj = n0 + j, gkb = kk + kb;
       double w = 0.;
       if (gj < g.N && gkb < k_end && gkb >= k_begin && !(g.b_lower && gkb < gj))
@@ -165,13 +166,13 @@ __global__ void __launch_bounds__(256) gemm_f64_big_kernel(GemmArgs g) {
   };
   auto store = [&](int buf) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
+    for (int e = 0; e < EPT; ++e) {
       const int idx = tid + e * 256;
       int i, k;
-      if (g.transA) { k = idx & 15; i = idx >> 4; } else { i = idx & 127; k = idx >> 7; }
+      if (g.transA) { k = idx & (TKB - 1); i = idx / TKB; } else { i = idx & 127; k = idx >> 7; }
       As[buf][k][i] = ra[e];
       int j, kb;
-      if (g.transB) { j = idx & 127; kb = idx >> 7; } else { kb = idx & 15; j = idx >> 4; }
+      if (g.transB) { j = idx & 127; kb = idx >> 7; } else { kb = idx & (TKB - 1); j = idx / TKB; }
       Bs[buf][kb][j] = rb[e];
     }
   };
@@ -181,11 +182,11 @@ __global__ void __launch_bounds__(256) gemm_f64_big_kernel(GemmArgs g) {
   }
   __syncthreads();
   int buf = 0;
-  for (int kk = k_begin; kk < k_end; kk += TK) {
-    const bool more = kk + TK < k_end;
-    if (more) load(kk + TK);   // in flight during this step's MFMAs
+  for (int kk = k_begin; kk < k_end; kk += TKB) {
+    const bool more = kk + TKB < k_end;
+    if (more) load(kk + TKB);   // in flight during this step's MFMAs
 #pragma unroll
-    for (int k4 = 0; k4 < TK; k4 += 4) {
+    for (int k4 = 0; k4 < TKB; k4 += 4) {
       const int kl = k4 + (lane >> 4);
       double a[4], b[4];
 #pragma unroll
