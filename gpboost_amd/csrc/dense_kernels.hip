@@ -289,6 +289,63 @@ __global__ void __launch_bounds__(256) potrf_diag_kernel(double* A, int lda, int
   }
 }
 
+// Same factorization and inverse by ONE wave (lane r owns row r in registers): the 256-thread
+// form above pays three workgroup barriers and an integer-division loop per column, ~123 us
+// per 64-block (313 blocks per n = 20000 evaluation). Here column j is broadcast through LDS
+// inside the wave (no barrier needed beyond the wave's own LDS wait), every update is the same
+// fma (c - l_rj * l_cj) in the same order, and column c of L^-1 is lane c's forward
+// substitution over the LDS copy of L (terms p < c are exact zeros, so the sums equal the
+// p = c.. form).
+__global__ void __launch_bounds__(64) potrf_diag_wave_kernel(double* A, int lda, int j0, int ib, double* Winv,
+                                                             int ldw, int* info) {
+  __shared__ double colb[2][64];
+  __shared__ double Ls[64][65];
+  const int r = threadIdx.x;
+  double row[64];
+#pragma unroll
+  for (int c = 0; c < 64; ++c)
+    row[c] = (r < ib && c < ib && c <= r) ? A[(size_t)(j0 + r) + (size_t)(j0 + c) * lda] : 0.;
+#pragma unroll
+  for (int j = 0; j < 64; ++j) {
+    if (j < ib) {
+      const double p = __shfl(row[j], j, 64);
+      double d;
+      if (!(p > 0.)) {   // not positive definite
+        if (r == 0) atomicAdd(info, 1);
+        d = 1.;
+      } else {
+        d = sqrt(p);
+      }
+      const double l = (r > j) ? row[j] / d : (r == j ? d : 0.);
+      if (r >= j) row[j] = l;
+      colb[j & 1][r] = l;
+      __syncthreads();   // one wave: orders the LDS write before the reads
+#pragma unroll
+      for (int c = j + 1; c < 64; ++c)
+        if (c <= r) row[c] = fma(-l, colb[j & 1][c], row[c]);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 64; ++c) {
+    Ls[r][c] = row[c];
+    if (r < ib && c < ib && c <= r) A[(size_t)(j0 + r) + (size_t)(j0 + c) * lda] = row[c];
+  }
+  __syncthreads();
+  // column c = r of L^-1 by forward substitution
+  double x[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    double s = (i == r) ? 1. : 0.;
+#pragma unroll
+    for (int p = 0; p < i; ++p) s -= Ls[i][p] * x[p];
+    x[i] = (i >= r && i < ib) ? s / Ls[i][i] : 0.;
+  }
+  // Winv[i][c] = x_c[i]: lane c holds column c
+#pragma unroll
+  for (int i = 0; i < 64; ++i)
+    if (i < ib && r < ib) Winv[(size_t)(j0 + i) + (size_t)(j0 + r) * ldw] = (r <= i) ? x[i] : 0.;
+}
+
 // 2 * sum log L_ii -> out (single block, fixed order)
 __global__ void __launch_bounds__(256) logdet_kernel(const double* A, int lda, int n, double* out) {
   __shared__ double red[256];
@@ -464,7 +521,11 @@ void DenseSolver::Potrf() {
     const int jb = std::min(NBO, n - J0);
     for (int j0 = J0; j0 < J0 + jb; j0 += NBI) {
       const int ib = std::min(NBI, J0 + jb - j0);
-      hipLaunchKernelGGL(potrf_diag_kernel, dim3(1), dim3(256), 0, stream_, A, ld, j0, ib, W, ld, info_.get());
+      static const bool diag_old = std::getenv("GPBOOST_AMD_DIAG_OLD") != nullptr;   // A/B: 256-thread form
+      if (diag_old)
+        hipLaunchKernelGGL(potrf_diag_kernel, dim3(1), dim3(256), 0, stream_, A, ld, j0, ib, W, ld, info_.get());
+      else
+        hipLaunchKernelGGL(potrf_diag_wave_kernel, dim3(1), dim3(64), 0, stream_, A, ld, j0, ib, W, ld, info_.get());
       HIP_CHECK(hipGetLastError());
       const int r0 = j0 + ib;
       if (r0 < n) {

@@ -6,4 +6,4 @@ timeout -k 10 600 python -u -m pytest tests/test_gpu_dense.py -x -q --timeout 30
 rc=$?; echo "tests rc=$rc" >> gpurun_out/dense_tests.log
 case $rc in 0|1) ;; *) exit $rc ;; esac
 timeout -k 10 300 python -u scripts/time_dense.py > gpurun_out/dense_ab.log 2>&1 || exit $?
-GPBOOST_AMD_GEMM64=1 timeout -k 10 300 python -u scripts/time_dense.py >> gpurun_out/dense_ab.log 2>&1
+GPBOOST_AMD_DIAG_OLD=1 timeout -k 10 300 python -u scripts/time_dense.py >> gpurun_out/dense_ab.log 2>&1
