@@ -179,6 +179,13 @@ def latent_leg(X, Y, steps: int, cpu: bool) -> dict:
                            "launches": int(nlev), "us_per_launch": ms_p * 1e3 / max(nlev, 1),
                            "share_of_eval": None},
     }
+    pmc = os.path.join(ROOT, "profiles", "r01", "pmc_latent_apply.json")
+    if os.path.exists(pmc) and r == 51:   # HBM bytes per application from the committed PMC passes
+        with open(pmc) as f:
+            p = json.load(f)
+        leg["cg_matvec_roofline"]["traffic"] = p["bytes_per_application"]
+        leg["cg_matvec_roofline"]["traffic_source"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
+                                                       + os.path.relpath(pmc, ROOT))
     # the single-vector CG of the Newton / mode-finding solves (CGVecchiaLaplaceVec, CG_utils.cpp:21-108)
     ms_a1, ms_p1, _, _ = gm.bench_latent_operators(1, 50)
     byts1 = latent_matvec_bytes(n, int(nnz), 1)
