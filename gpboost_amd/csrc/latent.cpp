@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
+#include <map>
 #include <cstring>
 
 #include "slq_host.h"
@@ -306,16 +307,17 @@ void LatentVecchia::BenchOperators(int t, int reps, double* out) {
       HIP_CHECK(hipEventElapsedTime(&pm, ev0_, ev1_));
       std::fprintf(stderr, "[precond split t=%d] %-12s %.4f ms\n", t, name, pm / reps);
     };
-    part("tail_bt", [&] { for (int l = 0; l < tplan_.nlev_b; ++l) launch_vadu_level(tplan_, l, dw, R, Xt, Z, t, s_); });
+    part("tail_bt", [&] { TailSolve(false, R, Xt, Z, t); });
     part("head_part", [&] { launch_vadu_head_partial(hpart_, R, Xt, t, s_); });
     part("head_bt", [&] { launch_vadu_head(hbt_, false, dw, nullptr, Xt, t, s_); });
     part("head_lower", [&] { launch_vadu_head(hlow_, true, dw, Xt, Z, t, s_); });
-    part("tail_lower", [&] { for (int l = tplan_.nlev_b; l < tplan_.nlev; ++l) launch_vadu_level(tplan_, l, dw, R, Xt, Z, t, s_); });
+    part("tail_lower", [&] { TailSolve(true, R, Xt, Z, t); });
     std::fprintf(stderr, "[precond split t=%d] K=%d passes lower=%d bt=%d tail levels bt=%d lower=%d\n", t, head_K_,
                  hlow_.npass, hbt_.npass, tplan_.nlev_b, tplan_.nlev - tplan_.nlev_b);
   }
   out[2] = (double)tnnz_ + n_;
-  out[3] = precond_mode_ == 4 ? tplan_.nlev + 3 : lplan_.nlev;   // dependent launches per application
+  out[3] = precond_mode_ != 4 ? lplan_.nlev
+           : (tail_tiles_ ? (int)(sup_b_.size() + sup_f_.size()) - 2 : tplan_.nlev) + 3;   // dependent launches per application
 }
 
 // V = (B^T D^-1 B + W) H   (CG_utils.cpp:75, 161-164)
@@ -524,9 +526,66 @@ void LatentVecchia::BuildHeadPlan(const int* nbr, const std::vector<int>& tptr, 
       if (!head(p)) b[lev[p]].push_back(p);
     return b;
   };
+  std::vector<std::vector<int>> groups_b = by_level(lb, Lb), groups_f = by_level(lt, Lt);
+  std::vector<int> item_off;
+  // tile-blocked schedule of the tail (launch_vadu_tile): rows regrouped by (superstep, tile,
+  // local level); each group then is one (superstep, tile) item's local level
+  // opt-in (measured slower: the earliest-placement schedule puts the wide early levels of a
+  // tile into ONE workgroup per superstep, 5.2 vs 1.9 ms per application at t = 51)
+  tail_tiles_ = false;
+  if (const char* e = std::getenv("GPBOOST_AMD_TAIL_TILES")) tail_tiles_ = nt > 0 && std::atoi(e) != 0;
+  int TS = 512;
+  if (const char* e = std::getenv("GPBOOST_AMD_TAIL_TILE")) TS = std::max(16, std::atoi(e));
+  const int LT = kTailLocalLevels;
+  std::vector<long long> keys_b, keys_f;   // (s, tile) item key of every group (tiles only)
+  if (tail_tiles_) {
+    const int ntiles = (n + TS - 1) / TS;
+    auto schedule = [&](bool lower, std::vector<std::vector<int>>& groups, std::vector<long long>& keys,
+                        std::vector<int>& sup_ptr) {
+      std::vector<int> ss(n, 0), lam(n, 0);
+      int S = 0;
+      for (int q = 0; q < nt; ++q) {   // processing order: lower ascending Vecchia index, B^T descending
+        const int r = lower ? lab_[K + q] : lab_[n - 1 - q];
+        const int tr = r / TS;
+        int bs = 0, bl = 0;
+        auto dep = [&](int d) {
+          int cs, cl;
+          if (d / TS == tr) { cs = ss[d]; cl = lam[d] + 1; if (cl >= LT) { ++cs; cl = 0; } }
+          else { cs = ss[d] + 1; cl = 0; }
+          if (cs > bs || (cs == bs && cl > bl)) { bs = cs; bl = cl; }
+        };
+        if (lower) {
+          const int k = std::min(r, m);
+          for (int e = 0; e < k; ++e) { const int d = nbr[(size_t)r * m + e]; if (!head(d)) dep(d); }
+        } else {
+          for (int e = tptr[r]; e < tptr[r + 1]; ++e) dep(trow[e]);
+        }
+        ss[r] = bs;
+        lam[r] = bl;
+        S = std::max(S, bs + 1);
+      }
+      std::map<long long, std::vector<int>> g;   // (s, tile, lam) -> rows in processing order
+      for (int q = 0; q < nt; ++q) {
+        const int r = lower ? lab_[K + q] : lab_[n - 1 - q];
+        g[((long long)ss[r] * ntiles + r / TS) * LT + lam[r]].push_back(r);
+      }
+      groups.clear();
+      keys.clear();
+      sup_ptr.assign(S + 1, 0);
+      for (auto& kv : g) {
+        const long long item = kv.first / LT;
+        if (keys.empty() || keys.back() != item) ++sup_ptr[(int)(item / ntiles) + 1];
+        keys.push_back(item);
+        groups.push_back(std::move(kv.second));
+      }
+      for (int q = 0; q < S; ++q) sup_ptr[q + 1] += sup_ptr[q];
+    };
+    schedule(false, groups_b, keys_b, sup_b_);
+    schedule(true, groups_f, keys_f, sup_f_);
+  }
   std::vector<int> lrows, beoff(1, 0), beidx, fidx, beslot, fslot;
   tplan_.lptr.assign(1, 0);
-  for (const auto& rows : by_level(lb, Lb)) {
+  for (const auto& rows : groups_b) {
     for (int j : rows) {
       lrows.push_back(j);
       for (int e = tptr[j]; e < tptr[j + 1]; ++e) { beidx.push_back(trow[e]); beslot.push_back(tslot[e]); }
@@ -534,7 +593,7 @@ void LatentVecchia::BuildHeadPlan(const int* nbr, const std::vector<int>& tptr, 
     }
     tplan_.lptr.push_back((int)lrows.size());
   }
-  for (const auto& rows : by_level(lt, Lt)) {
+  for (const auto& rows : groups_f) {
     for (int i : rows) {
       lrows.push_back(i);
       const int k = std::min(i, m);
@@ -545,12 +604,31 @@ void LatentVecchia::BuildHeadPlan(const int* nbr, const std::vector<int>& tptr, 
     }
     tplan_.lptr.push_back((int)lrows.size());
   }
+  if (tail_tiles_) {   // item offsets from the group boundaries: each item's local levels, padded to LT + 1
+    const int nb = (int)groups_b.size();
+    auto make_items = [&](int g0, const std::vector<long long>& keys) {
+      for (size_t gi = 0; gi < keys.size();) {
+        std::vector<int> offs{tplan_.lptr[g0 + gi]};
+        size_t gj = gi;
+        while (gj < keys.size() && keys[gj] == keys[gi]) { offs.push_back(tplan_.lptr[g0 + gj + 1]); ++gj; }
+        if ((int)offs.size() > LT + 1) Fatal("tail tile schedule: more than %d local levels in one item", LT);
+        while ((int)offs.size() < LT + 1) offs.push_back(offs.back());
+        item_off.insert(item_off.end(), offs.begin(), offs.end());
+        gi = gj;
+      }
+    };
+    make_items(0, keys_b);
+    const int items_b = (int)(item_off.size() / (LT + 1));
+    make_items(nb, keys_f);
+    for (int& v : sup_f_) v += items_b;
+  }
   tplan_.n = nt;
   tplan_.m = m;
   tplan_.nlev_b = nt > 0 ? Lb : 0;
   tplan_.nlev = (int)tplan_.lptr.size() - 1;
   if (nt == 0) { tplan_.lptr.assign(1, 0); tplan_.nlev = 0; }
   const size_t o_lrows = put(lrows), o_beoff = put(beoff), o_beidx = put(beidx), o_fidx = put(fidx);
+  const size_t o_items = put(item_off);
   const size_t v_be = vslot.size();
   vslot.insert(vslot.end(), beslot.begin(), beslot.end());
   const size_t v_f = vslot.size();
@@ -671,6 +749,7 @@ void LatentVecchia::BuildHeadPlan(const int* nbr, const std::vector<int>& tptr, 
   tplan_.fidx = I + o_fidx;
   tplan_.beval = V + v_be;
   tplan_.fval = V + v_f;
+  d_items_ = I + o_items;
   for (int w = 0; w < 2; ++w) {
     HeadSolve& h = w == 0 ? hlow_ : hbt_;
     const HeadArrays& a = w == 0 ? hl : hb;
@@ -691,6 +770,19 @@ void LatentVecchia::BuildHeadPlan(const int* nbr, const std::vector<int>& tptr, 
   hpart_.eval = V + v_p;
   head_passes_ = hlow_.npass + hbt_.npass;
   if (K > 0) set_vadu_head_lds_limit(K);
+}
+
+// Tail part of one solve (mode 4): level kernels, or the tile-blocked supersteps.
+void LatentVecchia::TailSolve(bool lower, const double* R, double* Xt, double* Z, int t) {
+  if (!tail_tiles_) {
+    const int l0 = lower ? tplan_.nlev_b : 0, l1 = lower ? tplan_.nlev : tplan_.nlev_b;
+    for (int l = l0; l < l1; ++l) launch_vadu_level(tplan_, l, d_dw_.get(), R, Xt, Z, t, s_);
+    return;
+  }
+  const std::vector<int>& sp = lower ? sup_f_ : sup_b_;
+  for (size_t q = 0; q + 1 < sp.size(); ++q)
+    launch_vadu_tile(tplan_, lower, d_items_, kTailLocalLevels, sp[q], sp[q + 1] - sp[q], d_dw_.get(),
+                     lower ? Xt : R, lower ? Z : Xt, t, s_);
 }
 
 // Z = P^-1 R, P = B^T (D^-1 + W) B (VADU, CG_utils.cpp:56-60): B^T solve then (dw B) solve.
@@ -763,11 +855,11 @@ void LatentVecchia::PrecondImpl(const double* R, double* Z, double* Xt, int t) {
   static const bool eager = std::getenv("GPBOOST_AMD_NO_GRAPH") != nullptr;   // diagnostics (profilers)
   if (precond_mode_ == 4) {
     auto record = [&]() {
-      for (int l = 0; l < tplan_.nlev_b; ++l) launch_vadu_level(tplan_, l, d_dw_.get(), R, Xt, Z, t, s_);
+      TailSolve(false, R, Xt, Z, t);
       launch_vadu_head_partial(hpart_, R, Xt, t, s_);
       launch_vadu_head(hbt_, false, d_dw_.get(), nullptr, Xt, t, s_);
       launch_vadu_head(hlow_, true, d_dw_.get(), Xt, Z, t, s_);
-      for (int l = tplan_.nlev_b; l < tplan_.nlev; ++l) launch_vadu_level(tplan_, l, d_dw_.get(), R, Xt, Z, t, s_);
+      TailSolve(true, R, Xt, Z, t);
     };
     if (eager) { record(); return; }
     for (const GraphEntry& g : hgraphs_) {

@@ -138,6 +138,11 @@ class LatentVecchia {
   DevBuf<double> d_hval_;
   int hslot_count_ = 0, head_K_ = 0, head_passes_ = 0;
   std::vector<GraphEntry> hgraphs_;
+  // tile-blocked tail (launch_vadu_tile): superstep -> item ranges of the two solves
+  bool tail_tiles_ = false;
+  std::vector<int> sup_b_, sup_f_;
+  const int* d_items_ = nullptr;   // inside d_hint_
+  void TailSolve(bool lower, const double* R, double* Xt, double* Z, int t);
   void BuildHeadPlan(const int* nbr, const std::vector<int>& tptr, const std::vector<int>& trow,
                      const std::vector<int>& tslot, const std::vector<int>& lb);
   int max_flow_blocks_ = 512;

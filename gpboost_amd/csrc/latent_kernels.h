@@ -172,6 +172,17 @@ void launch_vadu_head(const HeadSolve& h, bool lower, const double* dw, const do
                       hipStream_t s);
 void launch_vadu_head_partial(const HeadPartial& h, const double* R, double* X, int t, hipStream_t s);
 void set_vadu_head_lds_limit(int K);
+// Tile-blocked schedule of the tail solves (precond mode 4, GPBOOST_AMD_TAIL_TILES): tail rows
+// are grouped into spatial tiles (blocks of TS consecutive storage rows, Morton order) and each
+// row gets (superstep s, local level lam): the lexicographic max over its tail dependencies of
+// (s_d, lam_d + 1) for a dependency in the same tile (wrapping to (s_d + 1, 0) at lam = L) and
+// (s_d + 1, 0) for one in another tile. One launch per superstep, one workgroup per (s, tile)
+// item, which runs its local levels with a workgroup barrier between them (a dependency on
+// another workgroup's row was finished by an earlier launch). Positions of `lp` follow
+// (s, tile, lam); item i covers local level l at positions [item_off[i*(L+1)+l], ...[l+1]).
+constexpr int kTailLocalLevels = 8;
+void launch_vadu_tile(const LevelPlan& lp, bool lower, const int* item_off, int L, int item0, int nitems,
+                      const double* dw, const double* in, double* X, int t, hipStream_t s);
 // blob_f64[vpos[e]] = Bv[eslot[e]] for all count entries (per-evaluation value refresh)
 void launch_sweep_values(int count, const int* vpos, const int* eslot, const double* Bv, int* blob, hipStream_t s);
 // dst[p*m + r] = src[rows[p]*m + r]  (n x m, level order)  |  dst[e] = idx[e] >= 0 ? src[idx[e]] : 0

@@ -167,7 +167,91 @@ __global__ void __launch_bounds__(256) vadu_head_partial_kernel(HeadPartial h, c
   if (c < t) X[(size_t)j * t + c] = R[(size_t)j * t + c] - acc;
 }
 
+// One superstep of the tile-blocked tail solve: workgroup = (superstep, tile) item; its local
+// levels one after another, a workgroup barrier between them (the rows of a level read only
+// values finished by an earlier launch or by this workgroup at an earlier local level; the
+// barrier is the workgroup-scope release/acquire that makes those global stores visible).
+// t >= 2: one wave per row, lane = column, the row's structure by one coalesced load and
+// v_readlane broadcasts (as vadu_levelW / the operator kernels); t = 1: 16 lanes per row.
+// Row arithmetic: x_i = in_i (/ dw_i) - sum_e v_e x_{idx_e} (same as vadu_level*_kernel).
+template <bool LOWER, bool T1>
+__global__ void __launch_bounds__(256) vadu_tile_kernel(LevelPlan lp, const int* __restrict__ item_off, int L,
+                                                        int item0, const double* __restrict__ dw, const double* in,
+                                                        double* X, int t) {
+  const int* off = item_off + (size_t)(item0 + blockIdx.x) * (L + 1);
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  for (int l = 0; l < L; ++l) {
+    const int p0 = off[l], p1 = off[l + 1];
+    if (p0 == p1) break;   // local levels are contiguous from 0
+    if (T1) {
+      const int g = threadIdx.x >> 4, gl = threadIdx.x & 15;
+      for (int p = p0 + g; p < p1; p += 16) {
+        const int i = lp.lrows[p];
+        int e0, e1;
+        const int* idx;
+        const double* val;
+        if (LOWER) { const size_t q = (size_t)(p - lp.n) * lp.m; idx = lp.fidx + q; val = lp.fval + q; e0 = 0; e1 = lp.m; }
+        else { idx = lp.beidx; val = lp.beval; e0 = lp.beoff[p]; e1 = lp.beoff[p + 1]; }
+        double acc = 0.;
+        for (int e = e0 + gl; e < e1; e += 16) acc = fma(val[e], X[idx[e]], acc);
+#pragma unroll
+        for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+        if (gl == 0) {
+          double x = in[i];
+          if (LOWER) x /= dw[i];
+          X[i] = x - acc;
+        }
+      }
+    } else {
+      const int c = lane + blockIdx.y * 64;
+      const int cc = c < t ? c : t - 1;
+      for (int p = p0 + wave; p < p1; p += 4) {
+        const int i = lp.lrows[p];
+        double x = in[(size_t)i * t + cc];
+        if (LOWER) x /= dw[i];
+        double acc = 0.;
+        if (LOWER) {
+          const size_t q = (size_t)(p - lp.n) * lp.m;
+          for (int b0 = 0; b0 < lp.m; b0 += 64) {
+            const int e = b0 + lane;
+            const bool ok = e < lp.m;
+            const int my_id = ok ? lp.fidx[q + e] : i;
+            const double my_w = ok ? lp.fval[q + e] : 0.;
+            acc = wave_dot<16>(my_id, my_w, min(64, lp.m - b0), X, t, cc, i, acc);
+          }
+        } else {
+          const int e0 = lp.beoff[p], e1 = lp.beoff[p + 1];
+          for (int b0 = e0; b0 < e1; b0 += 64) {
+            const int e = b0 + lane;
+            const bool ok = e < e1;
+            const int my_id = ok ? lp.beidx[e] : i;
+            const double my_w = ok ? lp.beval[e] : 0.;
+            acc = wave_dot<16>(my_id, my_w, min(64, e1 - b0), X, t, cc, i, acc);
+          }
+        }
+        if (c < t) X[(size_t)i * t + c] = x - acc;
+      }
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
+
+void launch_vadu_tile(const LevelPlan& lp, bool lower, const int* item_off, int L, int item0, int nitems,
+                      const double* dw, const double* in, double* X, int t, hipStream_t s) {
+  if (nitems <= 0 || t <= 0) return;
+  if (t == 1) {
+    if (lower) hipLaunchKernelGGL((vadu_tile_kernel<true, true>), dim3(nitems), dim3(256), 0, s, lp, item_off, L, item0, dw, in, X, t);
+    else hipLaunchKernelGGL((vadu_tile_kernel<false, true>), dim3(nitems), dim3(256), 0, s, lp, item_off, L, item0, dw, in, X, t);
+  } else {
+    const dim3 g(nitems, (t + 63) / 64);
+    if (lower) hipLaunchKernelGGL((vadu_tile_kernel<true, false>), g, dim3(256), 0, s, lp, item_off, L, item0, dw, in, X, t);
+    else hipLaunchKernelGGL((vadu_tile_kernel<false, false>), g, dim3(256), 0, s, lp, item_off, L, item0, dw, in, X, t);
+  }
+  HIP_CHECK(hipGetLastError());
+}
 
 void launch_vadu_head(const HeadSolve& h, bool lower, const double* dw, const double* in, double* X, int t,
                       hipStream_t s) {
