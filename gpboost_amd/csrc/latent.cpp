@@ -634,7 +634,7 @@ void LatentVecchia::BuildHeadPlan(const int* nbr, const std::vector<int>& tptr, 
   const size_t v_f = vslot.size();
   vslot.insert(vslot.end(), fslot.begin(), fslot.end());
   // ---- head solves: positions by level (head-only dependencies), passes of <= kHeadRowsPerPass
-  struct HeadArrays { std::vector<int> rec, eidx, slot, ooff{0}, oidx, oslot; };
+  struct HeadArrays { std::vector<int> rec, eidx, slot, ooff{0}, oidx, oslot, pend; };
   auto build_head = [&](bool lower) {
     HeadArrays h;
     std::vector<int> lev(K, 0);
@@ -700,6 +700,7 @@ void LatentVecchia::BuildHeadPlan(const int* nbr, const std::vector<int>& tptr, 
           ++q;
         }
         for (size_t r = r_pass + used; r <= r_pass + kHeadRowsPerPass; ++r) h.ooff[r] = (int)h.oidx.size();
+        h.pend.push_back(q >= rows.size() ? 1 : 0);   // last pass of its level: barrier after it
       }
     }
     return h;
@@ -717,13 +718,14 @@ void LatentVecchia::BuildHeadPlan(const int* nbr, const std::vector<int>& tptr, 
   std::vector<int> hrow(K);
   for (int v = 0; v < K; ++v) hrow[v] = lab_[v];
   const size_t o_hrow = put(hrow);
-  size_t o_h[2][4], v_h[2][2];
+  size_t o_h[2][5], v_h[2][2];
   for (int w = 0; w < 2; ++w) {
     HeadArrays& h = w == 0 ? hl : hb;
     o_h[w][0] = put(h.rec);
     o_h[w][1] = put(h.eidx);
     o_h[w][2] = put(h.oidx);
     o_h[w][3] = put(h.ooff);
+    o_h[w][4] = put(h.pend);
     v_h[w][0] = vslot.size();
     vslot.insert(vslot.end(), h.slot.begin(), h.slot.end());
     v_h[w][1] = vslot.size();
@@ -760,6 +762,7 @@ void LatentVecchia::BuildHeadPlan(const int* nbr, const std::vector<int>& tptr, 
     h.eidx = I + o_h[w][1];
     h.oidx = I + o_h[w][2];
     h.ooff = I + o_h[w][3];
+    h.pend = I + o_h[w][4];
     h.eval = V + v_h[w][0];
     h.oval = V + v_h[w][1];
   }

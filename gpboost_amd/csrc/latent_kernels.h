@@ -158,6 +158,7 @@ struct HeadSolve {
   const int* eidx;    // fixed layout: LDS slot of the dependency
   const double* eval; // fixed layout: B value (refreshed per evaluation)
   const int* ooff;    // npass * kHeadRowsPerPass + 1
+  const int* pend;    // npass: 1 = the pass ends its level (the next pass reads its results)
   const int* oidx;    // overflow entries
   const double* oval;
 };

@@ -40,6 +40,7 @@ __device__ __forceinline__ void lds_barrier() {
 // the stages alternate between two register sets (a copy would force a wait).
 template <int EPL>
 struct Stage {
+  int pend;            // the pass ends its level: workgroup barrier after it
   int rec;             // see HeadSolve (latent_kernels.h)
   int id[EPL];
   double v[EPL];
@@ -48,6 +49,7 @@ struct Stage {
 template <int EPL>
 __device__ __forceinline__ void load_stage(const HeadSolve& h, int q, int slot, int lane, Stage<EPL>& st) {
   const int r = q * kHeadRowsPerPass + slot;
+  st.pend = h.pend[q];
   st.rec = h.rec[r];
 #pragma unroll
   for (int k = 0; k < EPL; ++k) {
@@ -121,11 +123,13 @@ __global__ void __launch_bounds__(kHeadThreads) vadu_head_kernel(HeadSolve h, in
   for (int q = 0; q < h.npass; q += 2) {
     load_stage<EPL>(h, min(q + 1, last), slot, lane, B);
     solve_row<EPL>(h, A, q, slot, lane, xs);
-    lds_barrier();
+    // rows of one level are independent: only a level's last pass needs the barrier (a
+    // workgroup-uniform flag, so every wave takes the same barriers)
+    if (__builtin_amdgcn_readfirstlane(A.pend)) lds_barrier();
     if (q + 1 > last) break;
     load_stage<EPL>(h, min(q + 2, last), slot, lane, A);
     solve_row<EPL>(h, B, min(q + 1, last), slot, lane, xs);
-    lds_barrier();
+    if (__builtin_amdgcn_readfirstlane(B.pend)) lds_barrier();
   }
   // results out after the loop: a global store inside it would make the compiler drain the
   // prefetch (its registers are reused by the next stage's loads)
