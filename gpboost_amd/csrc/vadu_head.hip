@@ -34,6 +34,23 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
+// Sum over each 16-lane DPP row, result in every lane of the row: quad swaps, then the half-row
+// and row mirrors (VALU data movement instead of four LDS-crossbar shuffles on the pass's
+// critical chain). Fixed order -> bitwise repeatable.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double row16_sum(double v) {
+  v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);   // row_half_mirror
+  v += dpp_f64<0x140>(v);   // row_mirror
+  return v;
+}
+
 // Stage of one pass on this thread: its record and this lane's EPL fixed-layout entries.
 // Every address is a function of the pass index alone (no dependent loads), so the next
 // pass's stage is in flight while this one gathers from LDS; the loop is unrolled by two so
@@ -73,8 +90,8 @@ __device__ __forceinline__ void solve_row(const HeadSolve& h, const Stage<EPL>& 
     const int GL = kHeadG << lg;
     for (int e = h.ooff[r0] + sub * kHeadG + lane; e < h.ooff[r0 + 1]; e += GL) acc = fma(h.oval[e], xs[h.oidx[e]], acc);
   }
-#pragma unroll
-  for (int off = kHeadG / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  static_assert(kHeadG == 16, "row16_sum reduces one 16-lane DPP row");
+  acc = row16_sum(acc);
   if (__ballot(lg >= 1)) {   // wave-uniform: only waves holding a multi-slot row pay the cross-slot steps
     const double o16 = __shfl_xor(acc, 16, 64);
     if (lg >= 1) acc += o16;
