@@ -43,10 +43,28 @@ __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcn
 // Compiler-only ordering (write-after-read on LDS within one wave is ordered by hardware).
 __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory"); }
 
+// Sum over a K-lane group (K = 16, 32, 64; smaller K by shuffles), result in every lane: the 16-lane DPP-row part by
+// VALU data movement (quad swaps, half-row and row mirrors), only the cross-row steps through
+// the LDS crossbar. Fixed order -> bitwise repeatable.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
 template <int K>
 __device__ __forceinline__ double group_sum(double v) {
+  if constexpr (K < 16) {   // sub-row groups (the two-rows-per-lane variant): plain shuffles
 #pragma unroll
-  for (int off = K / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    for (int off = K / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+  }
+  v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp_f64<0x141>(v);   // row_half_mirror
+  v += dpp_f64<0x140>(v);   // row_mirror
+  if (K >= 32) v += __shfl_xor(v, 16, 64);
+  if (K >= 64) v += __shfl_xor(v, 32, 64);
   return v;
 }
 
