@@ -318,8 +318,7 @@ __global__ void __launch_bounds__(kBT) b_apply1m_kernel(int n, int m, const int*
 #pragma unroll
   for (int q = 0; q < R; ++q) {
     double acc = fma(w[q][1], g[q][1], w[q][0] * g[q][0]);
-#pragma unroll
-    for (int off = G / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    acc = lane_group_sum<G>(acc);
     const int i = base + q * NG;
     if (lane == 0 && i < n) {
       double s = xs[q] + acc;
@@ -419,8 +418,7 @@ __global__ void __launch_bounds__(kBT) bt_apply1m_kernel(int n, const int* __res
       const int i = trow[ee];
       acc = fma(pre ? tval[ee] * pre[i] : tval[ee], X[i], acc);
     }
-#pragma unroll
-    for (int off = G / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+    acc = lane_group_sum<G>(acc);
     const int j = base + q * NG;
     if (lane == 0 && j < n && tptr[j + 1] - tptr[j] <= kLongRow) {
       double s = xs[q] + acc;

@@ -227,8 +227,7 @@ __global__ void __launch_bounds__(256) vadu_level1_kernel(LevelPlan lp, int p0, 
     const int e0 = lp.beoff[p], e1 = lp.beoff[p + 1];
     for (int e = e0 + lane; e < e1; e += G) acc = fma(lp.beval[e], X[lp.beidx[e]], acc);
   }
-#pragma unroll
-  for (int off = G / 2; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+  acc = lane_group_sum<G>(acc);
   if (lane == 0) {
     double x = in[i];
     if (LOWER) x /= dw[i];

@@ -47,4 +47,30 @@ __device__ __forceinline__ double wave_dot(int my_id, double my_w, int cnt, cons
   return s;
 }
 
+// Sum over groups of G consecutive lanes (G a power of two <= 64), result in every lane of the
+// group: inside 16-lane DPP rows by VALU data movement (quad swaps, half-row and row mirrors),
+// across rows through the LDS crossbar. Fixed order -> bitwise repeatable.
+template <int CTRL>
+__device__ __forceinline__ double dpp_move_f64(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+template <int G>
+__device__ __forceinline__ double lane_group_sum(double v) {
+  if constexpr (G < 16) {
+#pragma unroll
+    for (int off = G / 2; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+  } else {
+    v += dpp_move_f64<0xB1>(v);    // quad_perm [1,0,3,2]
+    v += dpp_move_f64<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += dpp_move_f64<0x141>(v);   // row_half_mirror
+    v += dpp_move_f64<0x140>(v);   // row_mirror
+    if constexpr (G >= 32) v += __shfl_xor(v, 16, 64);
+    if constexpr (G >= 64) v += __shfl_xor(v, 32, 64);
+    return v;
+  }
+}
+
 }  // namespace gpb_amd
