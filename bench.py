@@ -174,7 +174,7 @@ def latent_leg(X, Y, steps: int, cpu: bool) -> dict:
         "cg_matvec_roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel": "b_apply_wave + bt_apply_wave",
                                "kernel_ms": ms_a, "columns": r, "algorithmic_bytes_per_launch": byts},
-        "preconditioner": {"kernel": "vadu_head (first 12288 Vecchia rows, one workgroup per column, LDS) + "
+        "preconditioner": {"kernel": "vadu_head (first 14336 Vecchia rows, one workgroup per column, LDS) + "
                                      "vadu_levelT (tail level sets), replayed from a hipGraph", "ms": ms_p,
                            "launches": int(nlev), "us_per_launch": ms_p * 1e3 / max(nlev, 1),
                            "share_of_eval": None},
