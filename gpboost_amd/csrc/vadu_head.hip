@@ -293,8 +293,11 @@ void launch_vadu_head_partial(const HeadPartial& h, const double* R, double* X, 
   HIP_CHECK(hipGetLastError());
 }
 
+// The limit is per kernel function, not per model: always the largest head any model may use,
+// so a later model with a smaller K cannot lower it under an earlier model's launches.
 void set_vadu_head_lds_limit(int K) {
-  const int bytes = (int)(sizeof(double) * ((size_t)K + 1));
+  if (K > kHeadMaxRows) Fatal("head of %d rows exceeds the LDS capacity (%d)", K, kHeadMaxRows);
+  const int bytes = (int)(sizeof(double) * ((size_t)kHeadMaxRows + 1));
   HIP_CHECK(hipFuncSetAttribute((const void*)vadu_head_kernel<true, kHeadEpl>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
   HIP_CHECK(hipFuncSetAttribute((const void*)vadu_head_kernel<false, kHeadEpl>,

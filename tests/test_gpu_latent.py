@@ -192,3 +192,21 @@ def test_latent_many_neighbours_vs_oracle():
     ref = O.latent_iterative(xv, y[perm], nb, 0, O.transform_latent(0, [1.0, 0.1]), "bernoulli_logit", 0.1, t=10,
                              cg_delta_conv=1e-8)
     _check(nll, g, ref["nll"], ref["grad"])
+
+
+def test_two_live_models_different_head_sizes(monkeypatch):
+    """Two models alive in one process with different head sizes (the kernel's dynamic-LDS limit
+    is per function, so the second model must not lower it under the first)."""
+    from gpboost_amd import synthetic
+    case = dict(likelihood="gaussian", cov_fct="exponential", shape=0.5, num_neighbors=20, aux=0.1)
+    X = synthetic.bench_coords(9000)
+    y = synthetic.bench_gaussian_y(9000)
+    monkeypatch.setenv("GPBOOST_AMD_HEAD_ROWS", "8000")
+    a = _model(X, case, t=8, dc=1e-8)
+    ra = a.neg_log_likelihood_and_grad([1.0, 0.1], y)
+    monkeypatch.setenv("GPBOOST_AMD_HEAD_ROWS", "50")
+    b = _model(X, case, t=8, dc=1e-8)
+    rb = b.neg_log_likelihood_and_grad([1.0, 0.1], y)
+    ra2 = a.neg_log_likelihood_and_grad([1.0, 0.1], None)   # the large-head model again
+    assert ra2[0] == ra[0] and np.array_equal(ra2[1], ra[1])
+    assert abs(rb[0] - ra[0]) <= 1e-8 * abs(ra[0])
