@@ -368,7 +368,20 @@ void launch_vadu_level(const LevelPlan& lp, int l, const double* dw, const doubl
   }
   if (std::getenv("GPBOOST_AMD_LEVEL_T_OLD") == nullptr) {
     const dim3 g(cnt, (t + 63) / 64);
-    if (l < lp.nlev_b)
+    // waves sharing a row's entries: lower rows (m fixed entries) 2 waves — measured at
+    // n = 100k, t = 51: lower tail 0.506 -> 0.428 ms vs 4 waves; B^T rows (variable, some
+    // long) 4 waves (2 waves: 0.518 vs 0.510 ms). GPBOOST_AMD_LEVELT_NW forces one value.
+    static const int nw_env = std::getenv("GPBOOST_AMD_LEVELT_NW") ? std::atoi(std::getenv("GPBOOST_AMD_LEVELT_NW")) : 0;
+    const bool lower = l >= lp.nlev_b;
+    const int nw = nw_env ? nw_env : (lower ? 2 : 4);
+    if (nw == 2) {
+      if (!lower)
+        hipLaunchKernelGGL((vadu_levelT_kernel<false, 2>), g, dim3(128), 0, s, lp, p0, dw, R, Y, t);
+      else
+        hipLaunchKernelGGL((vadu_levelT_kernel<true, 2>), g, dim3(128), 0, s, lp, p0, dw, Y, Z, t);
+      return;
+    }
+    if (!lower)
       hipLaunchKernelGGL((vadu_levelT_kernel<false, 4>), g, dim3(256), 0, s, lp, p0, dw, R, Y, t);
     else
       hipLaunchKernelGGL((vadu_levelT_kernel<true, 4>), g, dim3(256), 0, s, lp, p0, dw, Y, Z, t);
