@@ -340,14 +340,27 @@ void launch_vadu_level(const LevelPlan& lp, int l, const double* dw, const doubl
   const int p0 = lp.lptr[l], cnt = lp.lptr[l + 1] - p0;
   if (cnt <= 0) return;
   if (t == 1 && std::getenv("GPBOOST_AMD_LEVEL_T1_OLD") == nullptr) {
+    static const int g_env = std::getenv("GPBOOST_AMD_LEVEL1_G") ? std::atoi(std::getenv("GPBOOST_AMD_LEVEL1_G")) : 0;
     if (l < lp.nlev_b) {
-      constexpr int G = 64;
-      hipLaunchKernelGGL((vadu_level1_kernel<false, G>), dim3((cnt + 256 / G - 1) / (256 / G)), dim3(256), 0, s, lp,
-                         p0, cnt, dw, R, Y);
+      if (g_env == 32) {
+        constexpr int G = 32;
+        hipLaunchKernelGGL((vadu_level1_kernel<false, G>), dim3((cnt + 256 / G - 1) / (256 / G)), dim3(256), 0, s,
+                           lp, p0, cnt, dw, R, Y);
+      } else {
+        constexpr int G = 64;
+        hipLaunchKernelGGL((vadu_level1_kernel<false, G>), dim3((cnt + 256 / G - 1) / (256 / G)), dim3(256), 0, s,
+                           lp, p0, cnt, dw, R, Y);
+      }
     } else {
-      constexpr int G = 32;
-      hipLaunchKernelGGL((vadu_level1_kernel<true, G>), dim3((cnt + 256 / G - 1) / (256 / G)), dim3(256), 0, s, lp,
-                         p0, cnt, dw, Y, Z);
+      if (g_env == 16) {
+        constexpr int G = 16;
+        hipLaunchKernelGGL((vadu_level1_kernel<true, G>), dim3((cnt + 256 / G - 1) / (256 / G)), dim3(256), 0, s,
+                           lp, p0, cnt, dw, Y, Z);
+      } else {
+        constexpr int G = 32;
+        hipLaunchKernelGGL((vadu_level1_kernel<true, G>), dim3((cnt + 256 / G - 1) / (256 / G)), dim3(256), 0, s,
+                           lp, p0, cnt, dw, Y, Z);
+      }
     }
     return;
   }
@@ -374,6 +387,13 @@ void launch_vadu_level(const LevelPlan& lp, int l, const double* dw, const doubl
     static const int nw_env = std::getenv("GPBOOST_AMD_LEVELT_NW") ? std::atoi(std::getenv("GPBOOST_AMD_LEVELT_NW")) : 0;
     const bool lower = l >= lp.nlev_b;
     const int nw = nw_env ? nw_env : (lower ? 2 : 4);
+    if (nw == 1) {
+      if (!lower)
+        hipLaunchKernelGGL((vadu_levelT_kernel<false, 1>), g, dim3(64), 0, s, lp, p0, dw, R, Y, t);
+      else
+        hipLaunchKernelGGL((vadu_levelT_kernel<true, 1>), g, dim3(64), 0, s, lp, p0, dw, Y, Z, t);
+      return;
+    }
     if (nw == 2) {
       if (!lower)
         hipLaunchKernelGGL((vadu_levelT_kernel<false, 2>), g, dim3(128), 0, s, lp, p0, dw, R, Y, t);
