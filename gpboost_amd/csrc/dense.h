@@ -32,6 +32,13 @@ class DenseSolver {
   hipEvent_t ev_[3] = {nullptr, nullptr, nullptr};
 };
 
+// C[M x N] = alpha op(A) op(B) + beta C, column-major fp64, MFMA tiles (dense_kernels.hip).
+// Masks: lower_out skips output tiles above the diagonal; a_lower / a_upper: op(A)[i][k] == 0
+// for k > i / k < i; b_lower: op(B)[k][j] == 0 for k < j (structural zeros are skipped).
+void gemm_f64(hipStream_t s, int M, int N, int K, double alpha, const double* A, int lda, int transA, const double* B,
+              int ldb, int transB, double beta, double* C, int ldc, int lower_out = 0, int a_lower = 0,
+              int a_upper = 0, int b_lower = 0);
+
 // host helper shared by all paths (re_model.cpp)
 void combine_partials(const double* s, int n, double sigma2_in, int profile, double* nll, double* grad,
                       double* sigma2_out);

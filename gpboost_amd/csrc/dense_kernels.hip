@@ -489,6 +489,12 @@ void dispatch_cov(int cov, F&& f) {
 
 }  // namespace
 
+void gemm_f64(hipStream_t s, int M, int N, int K, double alpha, const double* A, int lda, int transA, const double* B,
+              int ldb, int transB, double beta, double* C, int ldc, int lower_out, int a_lower, int a_upper,
+              int b_lower) {
+  gemm(s, M, N, K, alpha, A, lda, transA, B, ldb, transB, beta, C, ldc, lower_out, a_lower, a_upper, b_lower);
+}
+
 DenseSolver::DenseSolver(int n, int d, const double* d_X, hipStream_t stream)
     : n_(n), d_(d), ld_(((n + 63) / 64) * 64), d_X_(d_X), stream_(stream) {
   const size_t nn = (size_t)ld_ * (size_t)ld_;

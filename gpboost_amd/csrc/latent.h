@@ -22,6 +22,7 @@
 
 #include "common.h"
 #include "latent_kernels.h"
+#include "vadu_precond.h"
 
 namespace gpb_amd {
 
@@ -59,10 +60,8 @@ class LatentVecchia {
   // Operator costs on the factor of the last evaluation (benchmark roofline): out[0] = ms per
   // A = B^T D^-1 B + W application, out[1] = ms per VADU preconditioner application (both on
   // t columns, averaged over reps, HIP events on the model's stream), out[2] = nnz(B) incl.
-  // the unit diagonal, out[3] = level sets of the two triangular solves.
+  // the unit diagonal, out[3] = dependent launches per preconditioner application.
   void BenchOperators(int t, int reps, double* out);
-  int num_levels_fwd() const { return (int)fptr_.size() - 1; }
-  int num_levels_bwd() const { return (int)bptr_.size() - 1; }
 
  private:
   // Device work space of a t-column PCG (t = 1 for the Newton solves, t probes for SLQ).
@@ -72,6 +71,7 @@ class LatentVecchia {
     DevBuf<double> small;                 // rz, rz_new, hv, rr, a, b: 6 x t
     DevBuf<double> a_hist, b_hist;        // pmax x t (CG coefficients per iteration)
     DevBuf<int> act;                      // per-column activity mask
+    DevBuf<int> ctl;                      // PcgCtl (device side of the stopping rule)
     double* rz() const { return small.get(); }
     double* rz_new() const { return small.get() + t; }
     double* hv() const { return small.get() + 2 * t; }
@@ -86,12 +86,14 @@ class LatentVecchia {
   void EnsureProbes(const IterativeConfig& cfg);
   void ApplyA(const double* H, double* V, double* G, int t);
   void Precond(const double* R, double* Z, double* Xt, int t);
-  void PrecondImpl(const double* R, double* Z, double* Xt, int t);
+  void SetDiag();   // the preconditioner's D^-1 + W changed (after every newton_prep writing dw)
   // PCG on the b.t columns of RHS sharing every operator application. Columns [0, n_single)
   // are independent single-vector CGs (CG_utils.cpp:21-108: own ||r|| < delta, warm start
   // allowed when t == 1); columns [n_single, t) are the block of CGTridiagVecchiaLaplace
   // (:110-217: mean ||r|| < delta). Stopped columns are frozen (a = b = 0). The per-
-  // iteration coefficients land in b.a_hist / b.b_hist (Lanczos tridiagonals).
+  // iteration coefficients land in b.a_hist / b.b_hist (Lanczos tridiagonals). The stopping
+  // rule runs on the device (pcg_check); the host reads its verdict one preconditioner
+  // application behind, so the queue never drains between iterations.
   struct PcgResult {
     int its_single = 0, its_block = 0;
     bool nan = false, zero_rhs = false;
@@ -100,7 +102,7 @@ class LatentVecchia {
                 int pmax_single, int pmax_block, double delta);
   void Scalars(const ScalarArgs& a, double* out);
   double Dot1(const double* x, const double* y);   // single-vector dot, synchronous
-  void CheckSolveError();
+  void WaitCtl(int seq, int* out);
 
   int n_, d_, m_;
   const double* d_X_;
@@ -111,45 +113,8 @@ class LatentVecchia {
   int tnnz_ = 0;
   SparseB sp_{};
   DevBuf<int> d_nbr_, d_tptr_, d_trow_, d_tslot_, d_longr_;
-  // step plan of the two VADU triangular solves (see SweepPlan)
-  std::vector<int> fptr_, bptr_;           // level pointers (host, diagnostics)
-  SweepPlan plan_{};
-  DevBuf<int> d_blob_, d_vpos_, d_eslot_;
-  int plan_entries_ = 0;
-  // level-by-level form replayed as hipGraphs (one per (R, Y, Z, t) buffer set)
-  LevelPlan lplan_{};
-  DevBuf<int> d_crit_;
-  std::vector<int> h_crit_;
-  unsigned long long* prof_ = nullptr;   // diagnostics: flow-kernel timestamps
-  DevBuf<int> d_lrows_, d_beoff_, d_beidx_, d_fidx_, d_lslot_;
-  DevBuf<double> d_lval_;
-  int lplan_entries_ = 0;
-  struct GraphEntry { const void* key[3]; int t; hipGraphExec_t exec; };
-  std::vector<GraphEntry> graphs_;
-  bool use_graph_ = true;
-  // 0 = sync-free flow kernels, 1 = level graphs, 2 = sweep, 3 = sync-free resident waves,
-  // 4 = head/tail split (head kernels + tail level graphs)
-  int precond_mode_ = 4;
-  // head/tail plan (BuildHeadPlan): tail level plan, the two head solves, the B^T partial
-  LevelPlan tplan_{};
-  HeadSolve hlow_{}, hbt_{};
-  HeadPartial hpart_{};
-  DevBuf<int> d_hint_, d_hslot_;
-  DevBuf<double> d_hval_;
-  int hslot_count_ = 0, head_K_ = 0, head_passes_ = 0;
-  std::vector<GraphEntry> hgraphs_;
-  // tile-blocked tail (launch_vadu_tile): superstep -> item ranges of the two solves
-  bool tail_tiles_ = false;
-  std::vector<int> sup_b_, sup_f_;
-  const int* d_items_ = nullptr;   // inside d_hint_
-  void TailSolve(bool lower, const double* R, double* Xt, double* Z, int t);
-  void BuildHeadPlan(const int* nbr, const std::vector<int>& tptr, const std::vector<int>& trow,
-                     const std::vector<int>& tslot, const std::vector<int>& lb);
-  int max_flow_blocks_ = 512;
-  int sf_grid_ = 256;                            // precond_mode_ 3: resident single-wave workgroups
-  DevBuf<int> d_err_;
-  void BuildSweepPlan(const int* nbr, const std::vector<int>& tptr, const std::vector<int>& trow,
-                      const std::vector<int>& tslot, const std::vector<int>& lf, const std::vector<int>& lb);
+  int dense_rows_ = 0, head_rows_ = 0;   // VADU plan split (VaduPrecond)
+  std::unique_ptr<VaduPrecond> pre_;
   DevBuf<double> d_y_, d_Bv_, d_dBv_, d_Dinv_, d_dD_, d_W_, d_dw_, d_sdw_, d_d1_;
   DevBuf<double> d_mode_, d_mode_upd_, d_mode_new_, d_rhs_, d_dir_, d_Adir_, d_vS_, d_dmll_;
   DevBuf<double> d_probes_, d_Zp_, d_U_, d_P_;   // n x t
@@ -159,8 +124,10 @@ class LatentVecchia {
   bool probes_saved_ = false;
   DevBuf<double> d_partials_, d_out_;
   double* h_out_ = nullptr;                      // pinned
-  std::vector<double> h_rr_;
   std::unique_ptr<Block> blk1_, blkt_, blkb_;   // blkb_: BenchOperators
+  int* h_ctl_ = nullptr;                         // host-coherent PcgCtl words written by pcg_check
+  int* d_hctl_ = nullptr;                        // their device address
+  int pcg_seq_ = 0;
   hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
   bool y_set_ = false;
   bool factor_ready_ = false;

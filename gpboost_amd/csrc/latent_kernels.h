@@ -54,106 +54,64 @@ void launch_b_apply(const SparseB& B, const double* vals, bool unit, const doubl
 // Y = unit*pre.*X + V^T (pre.*X) + W.*H  (pre, W/H nullable)
 void launch_bt_apply(const SparseB& B, const double* vals, bool unit, const double* X, int t, const double* pre,
                      const double* W, const double* H, double* Y, hipStream_t s);
-// VADU preconditioner Z = P^-1 R = (diag(dw) B)^-1 B^-T R for t columns in one launch
-// (vadu_sweep.hip): one workgroup per column walks the level sets of both triangular
-// solves with a workgroup barrier between "steps" (a level, or a slice of a large one),
-// while the next step's structure is copied into LDS asynchronously.
-// Step s is a contiguous blob of 32-bit words (blobs back to back, 16-byte aligned):
-//   [0, kSweepHdr)        header: R rows, E entries, v0, own size, next blob's size, phase
-//   [H, H + R)            row indices (original Vecchia index) of the step    (H = kSweepHdr)
-//   [H + R, H + 2R + 1)   entry offsets (relative, eoff[0] = 0)
-//   [v0, v0 + 2E)         entry values (fp64, 8-byte aligned)
-//   [v0 + 2E, +E)         entry column indices
-// B^T solve entries of row j: (child i, B(i, j)); lower solve entries of row i:
-// (nbr[i][r], B(i, nbr[i][r])); phase 0 = B^T solve, 1 = lower solve.
-constexpr int kSweepRows = 512;      // rows per step (= threads per workgroup)
-constexpr int kSweepEnts = 6144;     // entries per step (two staged blobs fill ~156 KB of LDS)
-constexpr int kSweepHdr = 8;
-struct SweepPlan {
-  int nsteps;
-  int max_words;                     // largest blob (LDS buffer size, words)
-  int first_words;                   // size of the first blob
-  int* blob;                         // values refreshed per evaluation (launch_sweep_values)
+// ---- VADU preconditioner Z = P^-1 R = B^-1 diag(1/dw) B^-T R (CG_utils.cpp:56-60); the plan that
+// strings these kernels together is VaduPrecond (vadu_precond.h).
+//
+// Tail solves (vadu_level.hip): the wide part of the DAG, one launch per MERGED level. Rows of
+// g consecutive dependency levels are solved in one launch: a row's dependencies inside its own
+// merged level are substituted recursively by their own expressions, so every row reads only
+// values of earlier merged levels (X entries) and inputs (IN entries):
+//   x_i = sum_{IN e} c_e in[idx_e] (/ dw[idx_e], lower solve) + sum_{X e} c_e X[idx_e].
+// In a random Vecchia ordering a row depends on ~1 row of the level just before it and the
+// substituted rows' neighbourhoods overlap, so the fill is small (n = 100k, m = 30: g = 4 turns
+// 103 launches per solve into 26 for +53% entries). g = 1 is the plain level schedule
+// (x_i = in_i (/ dw_i) - sum_j b_ij x_j). The coefficients c are products of B values, computed
+// per factor by launch_merged_numeric (one launch per level offset inside a merged level).
+struct MergedSolve {
+  int npos;                          // tail rows (positions in level order)
+  std::vector<int> lptr;             // host: merged level boundaries (positions)
+  const int* rows;                   // npos: storage row of position p
+  const int* eoff;                   // npos + 1: entries [eoff[p], eoff[p+1])
+  const int* xoff;                   // npos: [eoff[p], xoff[p]) IN entries, [xoff[p], eoff[p+1]) X entries
+  const int* eidx;                   // storage row of the entry
+  double* eval;                      // coefficients (launch_merged_numeric)
+  // numeric plan: per position ops [opoff[p], opoff[p+1]): w = -Bv[op_slot]; op_map < 0: c[op_a] += w
+  // (op_a a position in p's list); else c[map[op_map + q]] += w * c_{op_a}[q] for every entry q of
+  // position op_a's list (a substituted dependency). c[0] = 1 is the row's own input.
+  const int* opoff;
+  const int* op_a;
+  const int* op_slot;
+  const int* op_map;
+  const int* map;
+  const int* offpos;                 // positions grouped by level offset inside their merged level
+  std::vector<int> offptr;           // host: offset o -> offpos[offptr[o], offptr[o+1])
 };
-void launch_vadu_sweep(const SweepPlan& plan, const double* dw, const double* R, double* Y, double* Z, int t,
-                       hipStream_t s);
-// Level-by-level form of the same preconditioner (one kernel per level, replayed as a
-// hipGraph; rows of a level spread over all CUs, T lanes per row = the t columns).
-// Rows in level order p: B^T solve rows p in [0, n) (levels [0, nlev_b)), lower solve rows
-// p in [n, 2n). B^T solve: entries [beoff[p], beoff[p+1]) of (beidx, beval) = (child, B(child, row)).
-// Lower solve: fixed stride m, entries (fidx, fval)[(p - n) * m + r] = (nbr, B(row, nbr)),
-// zero-value padding, so a row's structure is one dependency-free load.
-struct LevelPlan {
-  int n, m;
-  int nlev_b, nlev;
-  std::vector<int> lptr;             // host, nlev + 1 (row positions p)
-  const int* lrows;                  // 2n
-  const int* beoff;                  // n + 1
-  const int* beidx;
-  const double* beval;
-  const int* fidx;                   // n x m
-  const double* fval;                // n x m
-};
-void launch_vadu_level(const LevelPlan& lp, int l, const double* dw, const double* R, double* Y, double* Z, int t,
-                       hipStream_t s);
-// Sync-free form of one of the two solves (vadu_flow.hip): one launch runs the whole DAG,
-// each solved value doubling as its readiness flag. Positions q in [0, n) follow the solve's
-// level order (row lrows[q]); B^T solve: entries [eoff[q], eoff[q+1]) of (eidx, eval);
-// lower solve (eoff null): entries q*m + r, r < min(row, m), and the input is divided by dw.
-// X (n x t) is filled with the sentinel by the launcher; err is set if a spin gives up.
-struct FlowArgs {
-  const int* lrows;
-  const int* crit;     // per position: the dependency of highest level (-1: none), polled first
-  const int* eoff;
-  const int* eidx;
-  const double* eval;
-  const double* dw;
-  const double* in;
-  double* X;
-  int* err;
-  unsigned long long* prof;   // diagnostics (nullable): per position {setup, crit seen, published} timestamps
-  int n, m, t, shift;
-};
-void launch_vadu_flow(const FlowArgs& a, bool lower, int max_blocks, hipStream_t s);
-// Sync-free form with a fixed grid of resident single-wave workgroups (vadu_sf.hip): position
-// q in [0, n) of the solve's level order is owned by workgroup q mod grid. Same structure
-// arrays as FlowArgs; X is filled with the sentinel by the launcher.
-struct SfArgs {
-  const int* lrows;
-  const int* crit;     // per position: the dependency of highest level (-1: none)
-  const int* eoff;     // B^T solve: entry offsets per position (null for the lower solve)
-  const int* eidx;
-  const double* eval;
-  const double* dw;    // lower solve: input divided by dw
-  const double* in;
-  double* X;
-  int* err;
-  int n, m, t;
-};
-void launch_vadu_sf(const SfArgs& a, bool lower, int grid, hipStream_t s);
-// Head/tail split of the two solves (precond mode 4, vadu_head.hip). Head = the first K rows
-// in Vecchia order (a thin, deep part of the DAG), solved by ONE workgroup per column with the
-// column's head values in LDS (slot = Vecchia index < K); tail = the other rows, by the level
-// kernels on a LevelPlan of the tail rows only. Lower solve: head, then tail levels. B^T
-// solve: tail levels, then launch_vadu_head_partial (tail contributions to head rows), then
-// the head.
-// One solve's head rows in level order are cut into passes of at most kHeadRowsPerPass rows
-// of ONE level. A pass has kHeadRowsPerPass slots of kHeadG lanes; a row takes 1, 2 or 4
-// consecutive slots (aligned; by its entry count), so its group has GL = kHeadG << lg lanes.
+void launch_merged_numeric(const MergedSolve& ms, const double* Bv, hipStream_t s);
+// merged level L of one solve: X[rows] from in (and dw when lower) and earlier X
+void launch_merged_level(const MergedSolve& ms, int L, bool lower, const double* dw, const double* in, double* X,
+                         int t, hipStream_t s);
+// LDS segment kernel (vadu_head.hip): ONE workgroup per column solves a segment of K rows with
+// the column's segment values resident in LDS (slot = position in the segment); a level costs an
+// LDS gather + a workgroup barrier instead of a launch. Dependencies outside the segment were
+// folded into `in` by launch_vadu_partial, so the kernel serves both solves:
+//   x_v = in[hrow[v]] (/ dw) - sum_{e} val_e x_{slot_e}   in pass order.
+// The segment's rows in level order are cut into passes of at most kHeadRowsPerPass rows of ONE
+// level. A pass has kHeadRowsPerPass slots of kHeadG lanes; a row takes 1, 2 or 4 consecutive
+// slots (aligned; by its entry count), so its group has GL = kHeadG << lg lanes.
 // Record r = q * kHeadRowsPerPass + slot: bits 0-15 the row's LDS slot (K = padding), bits
 // 16-17 lg, bits 18-19 the slot's index within the row, bit 31 set when the row has overflow
-// entries [ooff[r0], ooff[r0 + 1]) (r0 = the row's first slot). Entries (head dependencies
+// entries [ooff[r0], ooff[r0 + 1]) (r0 = the row's first slot). Entries (segment dependencies
 // only) in a fixed lane-major layout: entry e < GL * EPL of the row sits at group lane
 // gl = e % GL, k = e / GL, i.e. slot r0 + gl / kHeadG, position ((r * EPL + k) * kHeadG + gl %
 // kHeadG) (zero value = padding); entries beyond GL * EPL go to the overflow lists.
 constexpr int kHeadRowsPerPass = 64;
-constexpr int kHeadMaxRows = 16384;  // K limit: 128 KB of LDS per column workgroup
+constexpr int kHeadMaxRows = 16384;  // segment limit: 128 KB of LDS per column workgroup
 constexpr int kHeadG = 16;            // lanes per slot
 constexpr int kHeadEpl = 2;           // fixed-layout entries per lane
 struct HeadSolve {
-  int K;              // head rows = LDS slots (+ 1 scratch slot)
+  int K;              // segment rows = LDS slots (+ 1 scratch slot)
   int npass;
-  const int* hrow;    // K: storage row of head slot v (Vecchia index v)
+  const int* hrow;    // K: storage row of slot v
   const int* rec;     // npass * kHeadRowsPerPass records
   const int* eidx;    // fixed layout: LDS slot of the dependency
   const double* eval; // fixed layout: B value (refreshed per evaluation)
@@ -162,32 +120,33 @@ struct HeadSolve {
   const int* oidx;    // overflow entries
   const double* oval;
 };
-struct HeadPartial {  // B^T solve: tail rows' contributions to the head rows
+void launch_vadu_head(const HeadSolve& h, const double* in, const double* dw, double* X, int t, hipStream_t s);
+void set_vadu_head_lds_limit(int K);
+// Partial sums of dependencies outside a step, for each listed row r (storage rows):
+//   out[r] = (in ? in[r] / (dw ? dw[r] : 1) : out[r]) - sum_{e in [eoff[w], eoff[w+1])} eval[e] src[eidx[e]]
+struct PartialList {
   int rows;
-  const int* row;     // storage row of head row w
-  const int* eoff;    // entries [eoff[w], eoff[w+1])
-  const int* eidx;    // storage row of the (tail) dependency
+  const int* row;     // storage row of list row w
+  const int* eoff;
+  const int* eidx;    // storage row of the dependency
   const double* eval;
 };
-void launch_vadu_head(const HeadSolve& h, bool lower, const double* dw, const double* in, double* X, int t,
-                      hipStream_t s);
-void launch_vadu_head_partial(const HeadPartial& h, const double* R, double* X, int t, hipStream_t s);
-void set_vadu_head_lds_limit(int K);
-// Tile-blocked schedule of the tail solves (precond mode 4, GPBOOST_AMD_TAIL_TILES): tail rows
-// are grouped into spatial tiles (blocks of TS consecutive storage rows, Morton order) and each
-// row gets (superstep s, local level lam): the lexicographic max over its tail dependencies of
-// (s_d, lam_d + 1) for a dependency in the same tile (wrapping to (s_d + 1, 0) at lam = L) and
-// (s_d + 1, 0) for one in another tile. One launch per superstep, one workgroup per (s, tile)
-// item, which runs its local levels with a workgroup barrier between them (a dependency on
-// another workgroup's row was finished by an earlier launch). Positions of `lp` follow
-// (s, tile, lam); item i covers local level l at positions [item_off[i*(L+1)+l], ...[l+1]).
-constexpr int kTailLocalLevels = 8;
-void launch_vadu_tile(const LevelPlan& lp, bool lower, const int* item_off, int L, int item0, int nitems,
-                      const double* dw, const double* in, double* X, int t, hipStream_t s);
-// blob_f64[vpos[e]] = Bv[eslot[e]] for all count entries (per-evaluation value refresh)
-void launch_sweep_values(int count, const int* vpos, const int* eslot, const double* Bv, int* blob, hipStream_t s);
-// dst[p*m + r] = src[rows[p]*m + r]  (n x m, level order)  |  dst[e] = idx[e] >= 0 ? src[idx[e]] : 0
-void launch_gather_rows(int n, int m, const int* rows, const double* src, double* dst, hipStream_t s);
+void launch_vadu_partial(const PartialList& p, const double* in, const double* dw, const double* src, double* out,
+                         int t, hipStream_t s);
+// Dense head block (vadu_dense.hip), K0 x K0 column-major with leading dimension ld (K0 rounded
+// up to 64, identity padding): per factor Bd = B_00, G = Bd^-1 and GT = G^T (T: ld x (ld/2 + 64)
+// scratch); per application S = diag(1/dw_0) G^T X[rows] (S: compact ld x t scratch), then
+// Y[rows] = G S (row-major t-column blocks, head-0 rows reached through DenseHead::row).
+struct DenseHead {
+  int K0, ld, m;
+  const int* row;      // K0: storage row of Vecchia row v < K0
+  const int* col;      // K0 x m: Vecchia index of entry (v, r) (-1: padding)
+  const double* val;   // K0 x m: B value of entry (v, r) (refreshed per factor)
+};
+void dense_head_factor(const DenseHead& d, double* Bd, double* G, double* GT, double* T, hipStream_t s);
+void launch_dense_head_apply(const DenseHead& d, const double* G, const double* GT, const double* dw, const double* X,
+                             double* S, double* Y, int t, hipStream_t s);
+// dst[e] = idx[e] >= 0 ? src[idx[e]] : 0
 void launch_gather(int count, const int* idx, const double* src, double* dst, hipStream_t s);
 
 // Per-column dot products: out[q*t + c] = sum_i A_q[i,c] * B_q[i,c], q < np (np <= 3).
@@ -198,6 +157,21 @@ void launch_coldots(int n, int t, int np, const double* const* A, const double* 
 // U += a .* H ; R -= a .* V ; rr[c] = sum_i R[i,c]^2 (per-column a from device memory)
 void launch_cg_update(int n, int t, const double* a, const double* H, const double* V, double* U, double* R,
                       double* partials, double* rr, hipStream_t s);
+// Device side of the PCG stopping rules (LatentVecchia::Pcg). ctl[kCtlActS]: single-vector
+// columns [0, n_single) still running; ctl[kCtlActB]: block columns [n_single, t) running;
+// ctl[kCtlItsS] / [kCtlItsB]: iterations done; ctl[kCtlNan]: NaN/Inf met in a residual norm.
+// ctl[kCtlSeq] (host copy only): sequence number of the check that wrote it.
+enum PcgCtlField : int { kCtlActS = 0, kCtlActB, kCtlItsS, kCtlItsB, kCtlNan, kCtlSeq, kPcgCtl = 8 };
+// act[c] = 1, except single columns whose right-hand side is zero (rr0[c] < zero_sq: the
+// reference returns u = 0 without iterating, CG_utils.cpp:42-45).
+void launch_pcg_init(int t, int n_single, int pmax_single, int pmax_block, double zero_sq, const double* rr0,
+                     int* act, int* ctl, hipStream_t s);
+// After iteration j's update (rr[c] = ||r_c||^2): single columns stop on their own norm
+// (CG_utils.cpp:80-90), the block on the mean column norm (:172-178), both at their pmax.
+// host_ctl (nullable, host-coherent memory mapped for the device): the fields are copied there,
+// then host_ctl[kCtlSeq] = seq after a system-scope fence.
+void launch_pcg_check(int j, int t, int n_single, int pmax_single, int pmax_block, double delta, const double* rr,
+                      int* act, int* ctl, int* host_ctl, int seq, hipStream_t s);
 // H = Z + b .* H
 void launch_h_update(int n, int t, const double* b, const double* Z, double* H, hipStream_t s);
 // a = rz / hv (hist[it*t + c] = a)  |  b = rz_new / rz, rz = rz_new (hist[it*t + c] = b);

@@ -428,15 +428,6 @@ __global__ void __launch_bounds__(kBT) bt_apply1m_kernel(int n, const int* __res
   }
 }
 
-__global__ void __launch_bounds__(kBT) gather_rows_kernel(int n, int m, const int* __restrict__ rows,
-                                                          const double* __restrict__ src, double* __restrict__ dst) {
-  const size_t total = (size_t)n * m;
-  for (size_t o = (size_t)blockIdx.x * kBT + threadIdx.x; o < total; o += (size_t)gridDim.x * kBT) {
-    const size_t p = o / m, r = o - p * m;
-    dst[o] = src[(size_t)rows[p] * m + r];
-  }
-}
-
 __global__ void __launch_bounds__(kBT) gather_kernel(int count, const int* __restrict__ idx,
                                                      const double* __restrict__ src, double* __restrict__ dst) {
   for (int e = blockIdx.x * kBT + threadIdx.x; e < count; e += gridDim.x * kBT) {
@@ -563,6 +554,56 @@ __global__ void cg_beta_kernel(int t, const double* rz_new, double* rz, const in
   rz[c] = rz_new[c];
   b[c] = v;
   if (hist) hist[c] = v;
+}
+
+__global__ void pcg_init_kernel(int t, int n_single, int pmax_single, int pmax_block, double zero_sq,
+                                const double* rr0, int* act, int* ctl) {
+  if (threadIdx.x != 0) return;
+  int any = 0;
+  for (int c = 0; c < t; ++c) {
+    const int a = (c < n_single && rr0 && rr0[c] < zero_sq) ? 0 : 1;
+    act[c] = a;
+    if (c < n_single) any |= a;
+  }
+  ctl[kCtlActS] = (any && pmax_single > 0) ? 1 : 0;
+  ctl[kCtlActB] = (n_single < t && pmax_block > 0) ? 1 : 0;
+  ctl[kCtlItsS] = 0;
+  ctl[kCtlItsB] = 0;
+  ctl[kCtlNan] = 0;
+}
+
+// One thread, columns in a fixed order (the block mean is bitwise repeatable).
+__global__ void pcg_check_kernel(int j, int t, int n_single, int pmax_single, int pmax_block, double delta,
+                                 const double* rr, int* act, int* ctl, int* host_ctl, int seq) {
+  if (threadIdx.x != 0) return;
+  if (ctl[kCtlActS]) {
+    ctl[kCtlItsS] = j + 1;
+    bool all_done = true;
+    for (int c = 0; c < n_single; ++c) {
+      if (!act[c]) continue;
+      const double norm = sqrt(rr[c]);
+      if (isnan(norm) || isinf(norm)) ctl[kCtlNan] = 1;
+      if (norm < delta || j + 1 >= pmax_single) act[c] = 0;
+      else all_done = false;
+    }
+    if (all_done) ctl[kCtlActS] = 0;
+  }
+  if (ctl[kCtlActB]) {
+    ctl[kCtlItsB] = j + 1;
+    double norm = 0.;
+    for (int c = n_single; c < t; ++c) norm += sqrt(rr[c]);
+    norm /= (t - n_single);
+    if (isnan(norm) || isinf(norm)) ctl[kCtlNan] = 1;
+    if (norm < delta || j + 1 >= pmax_block) {
+      for (int c = n_single; c < t; ++c) act[c] = 0;
+      ctl[kCtlActB] = 0;
+    }
+  }
+  if (host_ctl) {   // verdict straight into host-coherent memory, the sequence word last
+    for (int q = 0; q < kCtlSeq; ++q) host_ctl[q] = ctl[q];
+    __threadfence_system();
+    host_ctl[kCtlSeq] = seq;
+  }
 }
 
 __global__ void pack_columns_kernel(size_t rows, int ncols, const double* __restrict__ src, int ld_src, int c_src,
@@ -878,15 +919,6 @@ void launch_bt_apply(const SparseB& B, const double* vals, bool unit, const doub
   HIP_CHECK(hipGetLastError());
 }
 
-void launch_gather_rows(int n, int m, const int* rows, const double* src, double* dst, hipStream_t s) {
-  const size_t total = (size_t)n * m;
-  int g = (int)((total + kBT - 1) / kBT);
-  if (g > kMaxGridX) g = kMaxGridX;
-  if (g < 1) g = 1;
-  hipLaunchKernelGGL(gather_rows_kernel, dim3(g), dim3(kBT), 0, s, n, m, rows, src, dst);
-  HIP_CHECK(hipGetLastError());
-}
-
 void launch_gather(int count, const int* idx, const double* src, double* dst, hipStream_t s) {
   if (count <= 0) return;
   hipLaunchKernelGGL(gather_kernel, dim3(grid_x(count, kBT)), dim3(kBT), 0, s, count, idx, src, dst);
@@ -933,6 +965,20 @@ void launch_h_update(int n, int t, const double* b, const double* Z, double* H, 
   int g = (int)((total + kBT - 1) / kBT);
   if (g > kMaxGridX) g = kMaxGridX;
   hipLaunchKernelGGL(h_update_kernel, dim3(g), dim3(kBT), 0, s, total, t, b, Z, H);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_pcg_init(int t, int n_single, int pmax_single, int pmax_block, double zero_sq, const double* rr0,
+                     int* act, int* ctl, hipStream_t s) {
+  hipLaunchKernelGGL(pcg_init_kernel, dim3(1), dim3(64), 0, s, t, n_single, pmax_single, pmax_block, zero_sq, rr0, act,
+                     ctl);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_pcg_check(int j, int t, int n_single, int pmax_single, int pmax_block, double delta, const double* rr,
+                      int* act, int* ctl, int* host_ctl, int seq, hipStream_t s) {
+  hipLaunchKernelGGL(pcg_check_kernel, dim3(1), dim3(64), 0, s, j, t, n_single, pmax_single, pmax_block, delta, rr, act,
+                     ctl, host_ctl, seq);
   HIP_CHECK(hipGetLastError());
 }
 

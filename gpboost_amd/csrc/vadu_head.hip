@@ -1,4 +1,4 @@
-// Head/tail split of the VADU triangular solves (precond mode 4, the default).
+// LDS segment kernel and partial-sum kernels of the VADU triangular solves (vadu_precond.cpp).
 //
 // Reference replaced: the two sparse triangular solves of the VADU preconditioner
 // P^-1 = B^-1 (D^-1 + W)^-1 B^-T (CG_utils.cpp:56-60, likelihoods.h:11963-12041 and the
@@ -12,6 +12,10 @@
 // latency on the thin part. Here ONE workgroup per column solves the whole head with that
 // column's head values resident in LDS: a level costs an LDS gather + a workgroup barrier,
 // and the next pass's structure (global) is loaded while the current one computes.
+//
+// The rows handled here are Vecchia rows [K0, K) ("head 1"); the first K0 rows are solved by the
+// dense block of vadu_dense.hip, and every dependency outside the segment is folded into the
+// segment's input beforehand by vadu_partial_kernel, so the kernel itself is direction-agnostic.
 //
 // Row arithmetic is the reference's: x_i = in_i (/ dw_i) - sum_e v_e x_{idx_e}; the entries
 // are split over G = 16 lanes (lane l: entries l, l+16, ...) and combined by a fixed xor
@@ -103,15 +107,14 @@ __device__ __forceinline__ void solve_row(const HeadSolve& h, const Stage<EPL>& 
   if (lane == 0 && sub == 0) xs[st.rec & 0xffff] -= acc;
 }
 
-template <bool LOWER, int EPL>
-__global__ void __launch_bounds__(kHeadThreads) vadu_head_kernel(HeadSolve h, int t, const double* __restrict__ dw,
-                                                                 const double* in, double* X) {
-  extern __shared__ double xs[];   // this column's head values, slot = Vecchia index; slot K = scratch
+template <int EPL>
+__global__ void __launch_bounds__(kHeadThreads) vadu_head_kernel(HeadSolve h, int t, const double* in,
+                                                                 const double* __restrict__ dw, double* X) {
+  extern __shared__ double xs[];   // this column's segment values by slot; slot K = scratch
   const int c = blockIdx.x;
   const int lane = threadIdx.x & (kHeadG - 1);
   const int slot = threadIdx.x / kHeadG;
-  // inputs of all head rows first (independent loads): in / dw (lower), or the B^T input
-  // minus the tail contributions (head_partial wrote it into X)
+  // inputs of all segment rows first (independent loads): in (/ dw when given)
   constexpr int kPer = (kHeadMaxRows + kHeadThreads - 1) / kHeadThreads;
   {   // all loads of the phase in flight at once (no loop-carried wait)
     int r[kPer];
@@ -123,13 +126,13 @@ __global__ void __launch_bounds__(kHeadThreads) vadu_head_kernel(HeadSolve h, in
     }
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
-      x[k] = LOWER ? in[(size_t)r[k] * t + c] : X[(size_t)r[k] * t + c];
-      w[k] = LOWER ? dw[r[k]] : 1.;
+      x[k] = in[(size_t)r[k] * t + c];
+      w[k] = dw ? dw[r[k]] : 1.;
     }
 #pragma unroll
     for (int k = 0; k < kPer; ++k) {
       const int v = threadIdx.x + k * kHeadThreads;
-      if (v < h.K) xs[v] = LOWER ? x[k] / w[k] : x[k];
+      if (v < h.K) xs[v] = dw ? x[k] / w[k] : x[k];
     }
   }
   if (threadIdx.x == 0) xs[h.K] = 0.;
@@ -164,144 +167,77 @@ __global__ void __launch_bounds__(kHeadThreads) vadu_head_kernel(HeadSolve h, in
   }
 }
 
-// B^T solve, before the head: X[j] = R[j] - sum over the TAIL rows i that have head row j as
-// a neighbour of B(i, j) X[i] (all those X[i] are final: the tail is solved first). One wave
-// per head row, lane = column, entries ascending through v_readlane.
-__global__ void __launch_bounds__(256) vadu_head_partial_kernel(HeadPartial h, const double* __restrict__ R,
-                                                                double* X, int t) {
+// Partial sums of the dependencies outside a solve step, for every listed row r:
+//   out[r] = (in ? in[r] / (dw ? dw[r] : 1) : out[r]) - sum_e eval[e] src[eidx[e]]
+// (entries in list order). t >= 2: one wave per row, lane = column, the row's structure by one
+// coalesced load and v_readlane broadcasts; t = 1: 16 lanes per row over its entries.
+__global__ void __launch_bounds__(256) vadu_partial_kernel(PartialList p, const double* in,
+                                                           const double* __restrict__ dw, const double* src,
+                                                           double* out, int t) {
   const int lane = threadIdx.x & 63;
   const int w = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  if (w >= h.rows) return;
-  const int j = h.row[w];
+  if (w >= p.rows) return;
+  const int j = p.row[w];
   const int c = lane + blockIdx.y * 64;
   const int cc = c < t ? c : t - 1;
-  const int e0 = h.eoff[w], e1 = h.eoff[w + 1];
+  const int e0 = p.eoff[w], e1 = p.eoff[w + 1];
+  double x = in ? in[(size_t)j * t + cc] : out[(size_t)j * t + cc];
+  if (dw) x /= dw[j];
   double acc = 0.;
   for (int b0 = e0; b0 < e1; b0 += 64) {
     const int e = b0 + lane;
     const bool ok = e < e1;
-    const int my_id = ok ? h.eidx[e] : j;
-    const double my_w = ok ? h.eval[e] : 0.;
+    const int my_id = ok ? p.eidx[e] : j;
+    const double my_w = ok ? p.eval[e] : 0.;
     const int cnt = e1 - b0 < 64 ? e1 - b0 : 64;
-    acc = wave_dot<16>(my_id, my_w, cnt, X, t, cc, j, acc);
+    acc = wave_dot<16>(my_id, my_w, cnt, src, t, cc, j, acc);
   }
-  if (c < t) X[(size_t)j * t + c] = R[(size_t)j * t + c] - acc;
+  if (c < t) out[(size_t)j * t + c] = x - acc;
 }
 
-// One superstep of the tile-blocked tail solve: workgroup = (superstep, tile) item; its local
-// levels one after another, a workgroup barrier between them (the rows of a level read only
-// values finished by an earlier launch or by this workgroup at an earlier local level; the
-// barrier is the workgroup-scope release/acquire that makes those global stores visible).
-// t >= 2: one wave per row, lane = column, the row's structure by one coalesced load and
-// v_readlane broadcasts (as vadu_levelW / the operator kernels); t = 1: 16 lanes per row.
-// Row arithmetic: x_i = in_i (/ dw_i) - sum_e v_e x_{idx_e} (same as vadu_level*_kernel).
-template <bool LOWER, bool T1>
-__global__ void __launch_bounds__(256) vadu_tile_kernel(LevelPlan lp, const int* __restrict__ item_off, int L,
-                                                        int item0, const double* __restrict__ dw, const double* in,
-                                                        double* X, int t) {
-  const int* off = item_off + (size_t)(item0 + blockIdx.x) * (L + 1);
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  for (int l = 0; l < L; ++l) {
-    const int p0 = off[l], p1 = off[l + 1];
-    if (p0 == p1) break;   // local levels are contiguous from 0
-    if (T1) {
-      const int g = threadIdx.x >> 4, gl = threadIdx.x & 15;
-      for (int p = p0 + g; p < p1; p += 16) {
-        const int i = lp.lrows[p];
-        int e0, e1;
-        const int* idx;
-        const double* val;
-        if (LOWER) { const size_t q = (size_t)(p - lp.n) * lp.m; idx = lp.fidx + q; val = lp.fval + q; e0 = 0; e1 = lp.m; }
-        else { idx = lp.beidx; val = lp.beval; e0 = lp.beoff[p]; e1 = lp.beoff[p + 1]; }
-        double acc = 0.;
-        for (int e = e0 + gl; e < e1; e += 16) acc = fma(val[e], X[idx[e]], acc);
-#pragma unroll
-        for (int o = 8; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
-        if (gl == 0) {
-          double x = in[i];
-          if (LOWER) x /= dw[i];
-          X[i] = x - acc;
-        }
-      }
-    } else {
-      const int c = lane + blockIdx.y * 64;
-      const int cc = c < t ? c : t - 1;
-      for (int p = p0 + wave; p < p1; p += 4) {
-        const int i = lp.lrows[p];
-        double x = in[(size_t)i * t + cc];
-        if (LOWER) x /= dw[i];
-        double acc = 0.;
-        if (LOWER) {
-          const size_t q = (size_t)(p - lp.n) * lp.m;
-          for (int b0 = 0; b0 < lp.m; b0 += 64) {
-            const int e = b0 + lane;
-            const bool ok = e < lp.m;
-            const int my_id = ok ? lp.fidx[q + e] : i;
-            const double my_w = ok ? lp.fval[q + e] : 0.;
-            acc = wave_dot<16>(my_id, my_w, min(64, lp.m - b0), X, t, cc, i, acc);
-          }
-        } else {
-          const int e0 = lp.beoff[p], e1 = lp.beoff[p + 1];
-          for (int b0 = e0; b0 < e1; b0 += 64) {
-            const int e = b0 + lane;
-            const bool ok = e < e1;
-            const int my_id = ok ? lp.beidx[e] : i;
-            const double my_w = ok ? lp.beval[e] : 0.;
-            acc = wave_dot<16>(my_id, my_w, min(64, e1 - b0), X, t, cc, i, acc);
-          }
-        }
-        if (c < t) X[(size_t)i * t + c] = x - acc;
-      }
-    }
-    __syncthreads();
+__global__ void __launch_bounds__(256) vadu_partial1_kernel(PartialList p, const double* in,
+                                                            const double* __restrict__ dw, const double* src,
+                                                            double* out) {
+  const int g = blockIdx.x * 16 + (threadIdx.x >> 4), gl = threadIdx.x & 15;
+  if (g >= p.rows) return;   // whole 16-lane groups exit together
+  const int j = p.row[g];
+  double acc = 0.;
+  for (int e = p.eoff[g] + gl; e < p.eoff[g + 1]; e += 16) acc = fma(p.eval[e], src[p.eidx[e]], acc);
+  acc = lane_group_sum<16>(acc);
+  if (gl == 0) {
+    double x = in ? in[j] : out[j];
+    if (dw) x /= dw[j];
+    out[j] = x - acc;
   }
 }
 
 }  // namespace
 
-void launch_vadu_tile(const LevelPlan& lp, bool lower, const int* item_off, int L, int item0, int nitems,
-                      const double* dw, const double* in, double* X, int t, hipStream_t s) {
-  if (nitems <= 0 || t <= 0) return;
-  if (t == 1) {
-    if (lower) hipLaunchKernelGGL((vadu_tile_kernel<true, true>), dim3(nitems), dim3(256), 0, s, lp, item_off, L, item0, dw, in, X, t);
-    else hipLaunchKernelGGL((vadu_tile_kernel<false, true>), dim3(nitems), dim3(256), 0, s, lp, item_off, L, item0, dw, in, X, t);
-  } else {
-    const dim3 g(nitems, (t + 63) / 64);
-    if (lower) hipLaunchKernelGGL((vadu_tile_kernel<true, false>), g, dim3(256), 0, s, lp, item_off, L, item0, dw, in, X, t);
-    else hipLaunchKernelGGL((vadu_tile_kernel<false, false>), g, dim3(256), 0, s, lp, item_off, L, item0, dw, in, X, t);
-  }
-  HIP_CHECK(hipGetLastError());
-}
-
-void launch_vadu_head(const HeadSolve& h, bool lower, const double* dw, const double* in, double* X, int t,
-                      hipStream_t s) {
+void launch_vadu_head(const HeadSolve& h, const double* in, const double* dw, double* X, int t, hipStream_t s) {
   if (h.npass <= 0 || t <= 0) return;
   const size_t lds = sizeof(double) * ((size_t)h.K + 1);
-  if (lower)
-    hipLaunchKernelGGL((vadu_head_kernel<true, kHeadEpl>), dim3(t), dim3(kHeadThreads), lds, s, h, t, dw, in, X);
-  else
-    hipLaunchKernelGGL((vadu_head_kernel<false, kHeadEpl>), dim3(t), dim3(kHeadThreads), lds, s, h, t, dw, in,
-                       X);
+  hipLaunchKernelGGL((vadu_head_kernel<kHeadEpl>), dim3(t), dim3(kHeadThreads), lds, s, h, t, in, dw, X);
   HIP_CHECK(hipGetLastError());
 }
 
-void launch_vadu_head_partial(const HeadPartial& h, const double* R, double* X, int t, hipStream_t s) {
-  if (h.rows <= 0 || t <= 0) return;
-  hipLaunchKernelGGL(vadu_head_partial_kernel, dim3((h.rows + 3) / 4, (t + 63) / 64), dim3(256), 0, s, h, R, X,
-                     t);
+void launch_vadu_partial(const PartialList& p, const double* in, const double* dw, const double* src, double* out,
+                         int t, hipStream_t s) {
+  if (p.rows <= 0 || t <= 0) return;
+  if (t == 1)
+    hipLaunchKernelGGL(vadu_partial1_kernel, dim3((p.rows + 15) / 16), dim3(256), 0, s, p, in, dw, src, out);
+  else
+    hipLaunchKernelGGL(vadu_partial_kernel, dim3((p.rows + 3) / 4, (t + 63) / 64), dim3(256), 0, s, p, in, dw, src,
+                       out, t);
   HIP_CHECK(hipGetLastError());
 }
 
 // The limit is per kernel function, not per model: always the largest head any model may use,
 // so a later model with a smaller K cannot lower it under an earlier model's launches.
 void set_vadu_head_lds_limit(int K) {
-  if (K > kHeadMaxRows) Fatal("head of %d rows exceeds the LDS capacity (%d)", K, kHeadMaxRows);
+  if (K > kHeadMaxRows) Fatal("LDS segment of %d rows exceeds the LDS capacity (%d)", K, kHeadMaxRows);
   const int bytes = (int)(sizeof(double) * ((size_t)kHeadMaxRows + 1));
-  HIP_CHECK(hipFuncSetAttribute((const void*)vadu_head_kernel<true, kHeadEpl>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
-  HIP_CHECK(hipFuncSetAttribute((const void*)vadu_head_kernel<false, kHeadEpl>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  HIP_CHECK(hipFuncSetAttribute((const void*)vadu_head_kernel<kHeadEpl>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                bytes));
 }
 
 }  // namespace gpb_amd

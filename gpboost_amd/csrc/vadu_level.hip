@@ -1,0 +1,223 @@
+// Tail solves of the VADU preconditioner: one launch per merged dependency level.
+//
+// Reference replaced: the sparse triangular solves of P^-1 = B^-1 (D^-1 + W)^-1 B^-T
+// (CG_utils.cpp:56-60, 131-136: B^T unit-upper solve, then the (D^-1 + W) B lower solve) on the
+// tail rows (Vecchia index >= K, the wide part of the dependency DAG).
+//   B^T solve:   X_j = R_j - sum_{i : j in nbr(i)} B(i, j) X_i
+//   lower solve: X_i = Y_i / dw_i - sum_{r < k_i} B(i, nbr_r) X_{nbr_r}
+// Rows of g consecutive levels form one merged level: a dependency inside the merged level is
+// replaced by its own expression (recursively), so the launch reads only values of earlier merged
+// levels and inputs, with coefficients c that are products of B values (latent_kernels.h,
+// MergedSolve). The coefficients are refreshed once per factor by merge_numeric_kernel; each
+// application then costs one launch per merged level instead of one per level — the launches,
+// not the arithmetic, are what a level costs (a copy-only level kernel measured 2.8-4 us of the
+// 4.1-4.9 us of a real one at n = 100k, t = 51). Fixed summation orders throughout (bitwise
+// repeatable).
+#include <hip/hip_runtime.h>
+
+#include <cstdlib>
+
+#include "common.h"
+#include "latent_kernels.h"
+#include "wave_ops.h"
+
+namespace gpb_amd {
+namespace {
+
+// Coefficients of the positions at one level offset (their substituted dependencies sit at lower
+// offsets of the same merged level, done by earlier launches). One thread per position.
+__global__ void __launch_bounds__(256) merge_numeric_kernel(MergedSolve ms, const int* __restrict__ plist, int cnt,
+                                                            const double* __restrict__ Bv) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= cnt) return;
+  const int p = plist[k];
+  const int base = ms.eoff[p], len = ms.eoff[p + 1] - base;
+  double* c = ms.eval + base;
+  c[0] = 1.;   // the row's own input
+  for (int q = 1; q < len; ++q) c[q] = 0.;
+  for (int o = ms.opoff[p]; o < ms.opoff[p + 1]; ++o) {
+    const double w = -Bv[ms.op_slot[o]];
+    const int mo = ms.op_map[o];
+    if (mo < 0) {
+      c[ms.op_a[o]] += w;
+    } else {
+      const int pj = ms.op_a[o];
+      const double* cj = ms.eval + ms.eoff[pj];
+      const int lj = ms.eoff[pj + 1] - ms.eoff[pj];
+      for (int q = 0; q < lj; ++q) c[ms.map[mo + q]] = fma(w, cj[q], c[ms.map[mo + q]]);
+    }
+  }
+}
+
+// t >= 2: one workgroup per row; lane = column (coalesced t-wide gathers of a dependency's row),
+// wave w takes entries w, w + NW, ...; the NW partial sums meet in LDS in a fixed order.
+template <bool LOWER, int NW>
+__global__ void __launch_bounds__(NW * 64) merged_levelT_kernel(MergedSolve ms, int p0, const double* __restrict__ dw,
+                                                                const double* in, double* X, int t) {
+  __shared__ double red[NW][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane + blockIdx.y * 64;
+  const int cc = c < t ? c : t - 1;   // lanes beyond t gather a valid column, result unused
+  const int p = p0 + xcd_block(blockIdx.x, gridDim.x);
+  const int i = ms.rows[p];
+  const int e0 = ms.eoff[p], ex = ms.xoff[p], e1 = ms.eoff[p + 1];
+  constexpr int B = 16;
+  double acc = 0.;
+  for (int e = e0 + wave; e < e1; e += NW * B) {
+    int id[B];
+    double v[B], g[B];
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      const int ee = min(e + q * NW, e1 - 1);
+      id[q] = ms.eidx[ee];
+      v[q] = (e + q * NW < e1) ? ms.eval[ee] : 0.;
+    }
+#pragma unroll
+    for (int q = 0; q < B; ++q) {
+      const int ee = min(e + q * NW, e1 - 1);
+      if (ee < ex) g[q] = LOWER ? in[(size_t)id[q] * t + cc] / dw[id[q]] : in[(size_t)id[q] * t + cc];
+      else g[q] = X[(size_t)id[q] * t + cc];
+    }
+#pragma unroll
+    for (int q = 0; q < B; ++q) acc = fma(v[q], g[q], acc);
+  }
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && c < t) {
+    double sum = red[0][lane];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) sum += red[w][lane];
+    X[(size_t)i * t + c] = sum;
+  }
+}
+
+// t >= 2, wave per row (default): 4 rows per 256-thread workgroup, lane = column; a chunk of up
+// to 64 entries is ONE coalesced structure load (lane r = entry r) and each gather takes its
+// entry's index and coefficient by v_readlane, CH gathers in flight (the operator kernels' form,
+// sparse_kernels.hip). IN entries first (the lower solve folds 1/dw into their coefficients),
+// then X entries, each ascending.
+template <bool LOWER, int CH>
+__global__ void __launch_bounds__(256) merged_levelW_kernel(MergedSolve ms, int p0, int cnt,
+                                                            const double* __restrict__ dw, const double* in,
+                                                            double* X, int t) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int r = xcd_block(blockIdx.x, gridDim.x) * 4 + wave;
+  if (r >= cnt) return;
+  const int p = p0 + r;
+  const int i = ms.rows[p];
+  const int e0 = ms.eoff[p], ex = ms.xoff[p], e1 = ms.eoff[p + 1];
+  const int c = lane + blockIdx.y * 64;
+  const int cc = c < t ? c : t - 1;   // lanes beyond t gather a valid column, result unused
+  double s = 0.;
+  for (int b0 = e0; b0 < ex; b0 += 64) {
+    const int e = b0 + lane;
+    const bool ok = e < ex;
+    const int my_id = ok ? ms.eidx[e] : i;
+    double my_w = ok ? ms.eval[e] : 0.;
+    if (LOWER && ok) my_w /= dw[my_id];
+    s = wave_dot<CH>(my_id, my_w, ex - b0 < 64 ? ex - b0 : 64, in, t, cc, i, s);
+  }
+  for (int b0 = ex; b0 < e1; b0 += 64) {
+    const int e = b0 + lane;
+    const bool ok = e < e1;
+    const int my_id = ok ? ms.eidx[e] : i;
+    const double my_w = ok ? ms.eval[e] : 0.;
+    s = wave_dot<CH>(my_id, my_w, e1 - b0 < 64 ? e1 - b0 : 64, X, t, cc, i, s);
+  }
+  if (c < t) X[(size_t)i * t + c] = s;
+}
+
+// t = 1: a row's entries are spread over a lane group (G lanes, entry e on lane e mod G), the
+// group sums its lanes with a fixed tree.
+template <bool LOWER, int G>
+__global__ void __launch_bounds__(256) merged_level1_kernel(MergedSolve ms, int p0, int cnt,
+                                                            const double* __restrict__ dw, const double* in,
+                                                            double* X) {
+  const int lane = threadIdx.x & (G - 1);
+  const int task = xcd_block(blockIdx.x, gridDim.x) * (256 / G) + threadIdx.x / G;
+  if (task >= cnt) return;   // whole groups exit together (cnt is per group)
+  const int p = p0 + task;
+  const int i = ms.rows[p];
+  const int e0 = ms.eoff[p], ex = ms.xoff[p], e1 = ms.eoff[p + 1];
+  double acc = 0.;
+  for (int e = e0 + lane; e < e1; e += G) {
+    const int id = ms.eidx[e];
+    const double g = e < ex ? (LOWER ? in[id] / dw[id] : in[id]) : X[id];
+    acc = fma(ms.eval[e], g, acc);
+  }
+  acc = lane_group_sum<G>(acc);
+  if (lane == 0) X[i] = acc;
+}
+
+// Shape knobs (A/B only): GPBOOST_AMD_LEVELT_NW = 0 (default): wave per row; 1, 2 or 4: one
+// workgroup per row with that many waves sharing its entries; GPBOOST_AMD_LEVEL1_G = lanes per
+// row at t = 1 (16, 32 or 64; default 64). Other values: error.
+struct LevelShape {
+  int nw = 0, g = 64;
+};
+const LevelShape& level_shape() {
+  static const LevelShape v = [] {
+    LevelShape k;
+    if (const char* e = std::getenv("GPBOOST_AMD_LEVELT_NW")) {
+      k.nw = std::atoi(e);
+      if (k.nw != 0 && k.nw != 1 && k.nw != 2 && k.nw != 4)
+        Fatal("GPBOOST_AMD_LEVELT_NW must be 0, 1, 2 or 4 (got '%s')", e);
+      Info("tail level kernels: %d wave(s) per row at t >= 2", k.nw);
+    }
+    if (const char* e = std::getenv("GPBOOST_AMD_LEVEL1_G")) {
+      k.g = std::atoi(e);
+      if (k.g != 16 && k.g != 32 && k.g != 64) Fatal("GPBOOST_AMD_LEVEL1_G must be 16, 32 or 64 (got '%s')", e);
+      Info("tail level kernels: %d lanes per row at t = 1", k.g);
+    }
+    return k;
+  }();
+  return v;
+}
+
+template <bool LOWER>
+void launch_level(const MergedSolve& ms, int p0, int cnt, const double* dw, const double* in, double* X, int t,
+                  hipStream_t s) {
+  const LevelShape& ks = level_shape();
+  if (t == 1) {
+    const int G = ks.g;
+    const dim3 grid((cnt + 256 / G - 1) / (256 / G));
+    if (G == 16) hipLaunchKernelGGL((merged_level1_kernel<LOWER, 16>), grid, dim3(256), 0, s, ms, p0, cnt, dw, in, X);
+    else if (G == 32) hipLaunchKernelGGL((merged_level1_kernel<LOWER, 32>), grid, dim3(256), 0, s, ms, p0, cnt, dw, in, X);
+    else hipLaunchKernelGGL((merged_level1_kernel<LOWER, 64>), grid, dim3(256), 0, s, ms, p0, cnt, dw, in, X);
+    return;
+  }
+  if (ks.nw == 0) {
+    hipLaunchKernelGGL((merged_levelW_kernel<LOWER, 16>), dim3((cnt + 3) / 4, (t + 63) / 64), dim3(256), 0, s, ms, p0,
+                       cnt, dw, in, X, t);
+    return;
+  }
+  const dim3 g(cnt, (t + 63) / 64);
+  if (ks.nw == 1) hipLaunchKernelGGL((merged_levelT_kernel<LOWER, 1>), g, dim3(64), 0, s, ms, p0, dw, in, X, t);
+  else if (ks.nw == 2) hipLaunchKernelGGL((merged_levelT_kernel<LOWER, 2>), g, dim3(128), 0, s, ms, p0, dw, in, X, t);
+  else hipLaunchKernelGGL((merged_levelT_kernel<LOWER, 4>), g, dim3(256), 0, s, ms, p0, dw, in, X, t);
+}
+
+}  // namespace
+
+void launch_merged_numeric(const MergedSolve& ms, const double* Bv, hipStream_t s) {
+  for (size_t o = 0; o + 1 < ms.offptr.size(); ++o) {
+    const int cnt = ms.offptr[o + 1] - ms.offptr[o];
+    if (cnt <= 0) continue;
+    hipLaunchKernelGGL(merge_numeric_kernel, dim3((cnt + 255) / 256), dim3(256), 0, s, ms, ms.offpos + ms.offptr[o],
+                       cnt, Bv);
+  }
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_merged_level(const MergedSolve& ms, int L, bool lower, const double* dw, const double* in, double* X,
+                         int t, hipStream_t s) {
+  const int p0 = ms.lptr[L], cnt = ms.lptr[L + 1] - p0;
+  if (cnt <= 0 || t <= 0) return;
+  if (lower) launch_level<true>(ms, p0, cnt, dw, in, X, t, s);
+  else launch_level<false>(ms, p0, cnt, dw, in, X, t, s);
+  HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace gpb_amd

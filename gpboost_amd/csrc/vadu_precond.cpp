@@ -1,0 +1,525 @@
+// VaduPrecond implementation: host planning of the three-part VADU solves and their launch
+// sequence (vadu_precond.h explains the split).
+#include "vadu_precond.h"
+
+#include <algorithm>
+#include <cstdio>
+#include <cstdlib>
+
+namespace gpb_amd {
+
+VaduPrecond::~VaduPrecond() { DropGraphs(); }
+
+void VaduPrecond::DropGraphs() {
+  for (GraphEntry& g : graphs_) (void)hipGraphExecDestroy(g.exec);
+  graphs_.clear();
+}
+
+int VaduPrecond::launches() const {
+  int c = tail_levels_bt() + tail_levels_lower();
+  if (K_ > 0) ++c;                          // tail -> head partial
+  if (K_ > K0_) c += 2;                     // the two segment solves
+  if (K0_ > 0) c += 2 + (K_ > K0_ ? 2 : 0); // two dense products (+ the two head-1 <-> head-0 partials)
+  return c;
+}
+
+namespace {
+// Host side of one solve's merged tail (latent_kernels.h, MergedSolve): rows in level order,
+// g levels per merged level; deps(i, f) calls f(dependency row, value slot) for row i's entries
+// in order; in_tail(j) says whether row j is solved in this tail.
+struct MergeHost {
+  std::vector<int> rows, eoff{0}, xoff, eidx;
+  std::vector<int> opoff{0}, op_a, op_slot, op_map, map;
+  std::vector<int> lptr{0};
+  std::vector<int> offpos, offptr;
+};
+
+template <class Deps, class InTail>
+void build_merged(int n, int g, const std::vector<std::vector<int>>& levels, Deps deps, InTail in_tail,
+                  MergeHost& h) {
+  const int L = (int)levels.size();
+  std::vector<int> pos_of(n, -1), grp(n, -1);
+  int P = 0;
+  for (int l = 0; l < L; ++l)
+    for (int r : levels[l]) { pos_of[r] = P++; grp[r] = l / g; }
+  std::vector<std::vector<int>> by_off(std::max(1, std::min(g, L)));
+  std::vector<int> keypos(2 * (size_t)n, -1);   // list position of a key (X entry: j; IN entry: n + j)
+  std::vector<int> keys, lmap, perm;
+  struct Op { int a, slot, map; };
+  std::vector<Op> ops;
+  for (int l = 0; l < L; ++l) {
+    if (l > 0 && l % g == 0) h.lptr.push_back((int)h.rows.size());
+    for (int i : levels[l]) {
+      keys.clear();
+      lmap.clear();
+      ops.clear();
+      auto add = [&](int key) {
+        if (keypos[key] < 0) { keypos[key] = (int)keys.size(); keys.push_back(key); }
+        return keypos[key];
+      };
+      add(n + i);   // the row's own input: list position 0 after the IN-first reorder below
+      deps(i, [&](int j, int slot) {
+        if (in_tail(j) && grp[j] == grp[i]) {   // substitute j's expression
+          const int pj = pos_of[j];
+          ops.push_back(Op{pj, slot, (int)lmap.size()});
+          for (int e = h.eoff[pj]; e < h.eoff[pj + 1]; ++e)
+            lmap.push_back(add(e < h.xoff[pj] ? n + h.eidx[e] : h.eidx[e]));
+        } else {
+          ops.push_back(Op{add(j), slot, -1});
+        }
+      });
+      // final layout: IN entries first, then X entries (insertion order within each)
+      int nin = 0;
+      for (int k : keys) nin += k >= n;
+      perm.resize(keys.size());
+      int a = 0, b = nin;
+      for (size_t q = 0; q < keys.size(); ++q) perm[q] = keys[q] >= n ? a++ : b++;
+      const int base = (int)h.eidx.size();
+      h.rows.push_back(i);
+      h.eidx.resize(base + keys.size());
+      for (size_t q = 0; q < keys.size(); ++q) h.eidx[base + perm[q]] = keys[q] >= n ? keys[q] - n : keys[q];
+      h.xoff.push_back(base + nin);
+      h.eoff.push_back(base + (int)keys.size());
+      for (const Op& o : ops) {
+        h.op_slot.push_back(o.slot);
+        if (o.map < 0) {
+          h.op_a.push_back(perm[o.a]);
+          h.op_map.push_back(-1);
+        } else {
+          h.op_a.push_back(o.a);
+          h.op_map.push_back((int)h.map.size());
+          const int lj = h.eoff[o.a + 1] - h.eoff[o.a];
+          for (int q = 0; q < lj; ++q) h.map.push_back(perm[lmap[o.map + q]]);
+        }
+      }
+      h.opoff.push_back((int)h.op_a.size());
+      by_off[l % g].push_back(pos_of[i]);
+      for (int k : keys) keypos[k] = -1;
+    }
+  }
+  h.lptr.push_back((int)h.rows.size());
+  if (L == 0) h.lptr.assign(1, 0);
+  h.offptr.assign(1, 0);
+  for (const auto& v : by_off) {
+    h.offpos.insert(h.offpos.end(), v.begin(), v.end());
+    h.offptr.push_back((int)h.offpos.size());
+  }
+}
+}  // namespace
+
+void VaduPrecond::Build(const int* nbr, const std::vector<int>& vo, const std::vector<int>& lab,
+                        const std::vector<int>& tptr, const std::vector<int>& trow, const std::vector<int>& tslot,
+                        int K0, int K) {
+  const int n = n_, m = m_;
+  K = std::max(0, std::min(K, n));
+  K0 = std::max(0, std::min(K0, K));
+  K = std::min(K, K0 + kHeadMaxRows);
+  K0_ = K0;
+  K_ = K;
+  DropGraphs();
+  use_graph_ = std::getenv("GPBOOST_AMD_NO_GRAPH") == nullptr;   // diagnostics: eager launches (profilers)
+  auto kk = [&](int p) { return std::min(vo[p], m); };             // entries of storage row p
+  auto part = [&](int p) { return vo[p] < K0 ? 0 : (vo[p] < K ? 1 : 2); };
+  std::vector<int> ints;    // every index array of the plan, one upload
+  std::vector<int> vslot;   // value slots into Bv (-1: zero padding), one gather per factor
+  auto put = [&](const std::vector<int>& v) {
+    const size_t at = ints.size();
+    ints.insert(ints.end(), v.begin(), v.end());
+    return at;
+  };
+
+  // ---- tail level plan. Lower solve: levels over tail dependencies only (head values are final
+  // by then); B^T solve: a tail row's dependents are later Vecchia rows, all in the tail.
+  const int nt = n - K;
+  std::vector<int> lt(n, 0), lb(n, 0);
+  int Lt = 0, Lb = 0;
+  for (int ii = K; ii < n; ++ii) {
+    const int i = lab[ii];
+    int l = 0;
+    for (int r = 0; r < kk(i); ++r) {
+      const int j = nbr[(size_t)i * m + r];
+      if (part(j) == 2) l = std::max(l, lt[j] + 1);
+    }
+    lt[i] = l;
+    Lt = std::max(Lt, l + 1);
+  }
+  for (int ii = n - 1; ii >= K; --ii) {
+    const int i = lab[ii];
+    for (int r = 0; r < kk(i); ++r) {
+      const int j = nbr[(size_t)i * m + r];
+      if (part(j) == 2) lb[j] = std::max(lb[j], lb[i] + 1);
+    }
+    Lb = std::max(Lb, lb[i] + 1);
+  }
+  std::vector<std::vector<int>> groups_b(nt > 0 ? Lb : 0), groups_f(nt > 0 ? Lt : 0);
+  for (int p = 0; p < n; ++p)
+    if (part(p) == 2) {
+      groups_b[lb[p]].push_back(p);
+      groups_f[lt[p]].push_back(p);
+    }
+  // merged tail levels (g levels per launch; GPBOOST_AMD_TAIL_MERGE, 1 = the plain level schedule)
+  int g = 4;
+  if (const char* e = std::getenv("GPBOOST_AMD_TAIL_MERGE")) {
+    g = std::atoi(e);
+    if (g < 1 || g > 64) Fatal("GPBOOST_AMD_TAIL_MERGE must be 1..64 (got '%s')", e);
+  }
+  merge_g_ = g;
+  {
+    MergeHost mb, ml;
+    auto tail = [&](int j) { return part(j) == 2; };
+    build_merged(
+        n, g, groups_b, [&](int j, auto f) { for (int e = tptr[j]; e < tptr[j + 1]; ++e) f(trow[e], tslot[e]); }, tail,
+        mb);
+    build_merged(
+        n, g, groups_f, [&](int i, auto f) { for (int r = 0; r < kk(i); ++r) f(nbr[(size_t)i * m + r], i * m + r); },
+        tail, ml);
+    std::vector<int> mint;
+    MergeHost* hs[2] = {&mb, &ml};
+    size_t o[2][10];
+    size_t nval = 0, v0[2];
+    for (int w = 0; w < 2; ++w) {
+      const MergeHost& h = *hs[w];
+      const std::vector<int>* arrs[10] = {&h.rows, &h.eoff, &h.xoff, &h.eidx, &h.opoff, &h.op_a, &h.op_slot,
+                                          &h.op_map, &h.map, &h.offpos};
+      for (int a = 0; a < 10; ++a) {
+        o[w][a] = mint.size();
+        mint.insert(mint.end(), arrs[a]->begin(), arrs[a]->end());
+      }
+      v0[w] = nval;
+      nval += h.eidx.size();
+    }
+    d_mint_.alloc(std::max<size_t>(mint.size(), 1));
+    d_mval_.alloc(std::max<size_t>(nval, 1));
+    if (!mint.empty())
+      HIP_CHECK(hipMemcpyAsync(d_mint_.get(), mint.data(), sizeof(int) * mint.size(), hipMemcpyHostToDevice, s_));
+    HIP_CHECK(hipStreamSynchronize(s_));
+    for (int w = 0; w < 2; ++w) {
+      MergedSolve& ms = w == 0 ? mt_bt_ : mt_low_;
+      const MergeHost& h = *hs[w];
+      const int* I = d_mint_.get();
+      ms.npos = (int)h.rows.size();
+      ms.lptr = h.lptr;
+      ms.offptr = h.offptr;
+      ms.rows = I + o[w][0];
+      ms.eoff = I + o[w][1];
+      ms.xoff = I + o[w][2];
+      ms.eidx = I + o[w][3];
+      ms.opoff = I + o[w][4];
+      ms.op_a = I + o[w][5];
+      ms.op_slot = I + o[w][6];
+      ms.op_map = I + o[w][7];
+      ms.map = I + o[w][8];
+      ms.offpos = I + o[w][9];
+      ms.eval = d_mval_.get() + v0[w];
+    }
+    tail_entries_ = (long)nval;
+  }
+
+  // ---- head 1 segment [K0, K): slots = Vecchia index - K0, dependencies inside the segment
+  const int KS = K - K0;
+  struct SegArrays { std::vector<int> rec, eidx, slot, ooff{0}, oidx, oslot, pend; };
+  auto build_seg = [&](bool lower) {
+    SegArrays h;
+    std::vector<int> lev(KS, 0);
+    std::vector<std::vector<int>> deps(KS), dslot(KS);
+    for (int v = 0; v < KS; ++v) {
+      const int p = lab[K0 + v];
+      if (lower) {
+        for (int r = 0; r < kk(p); ++r) {
+          const int j = nbr[(size_t)p * m + r];
+          if (part(j) == 1) { deps[v].push_back(vo[j] - K0); dslot[v].push_back(p * m + r); }
+        }
+      } else {
+        for (int e = tptr[p]; e < tptr[p + 1]; ++e)
+          if (part(trow[e]) == 1) { deps[v].push_back(vo[trow[e]] - K0); dslot[v].push_back(tslot[e]); }
+      }
+    }
+    int L = 0;
+    for (int s = 0; s < KS; ++s) {   // lower: ascending Vecchia index; B^T: descending
+      const int v = lower ? s : KS - 1 - s;
+      int l = 0;
+      for (int d : deps[v]) l = std::max(l, lev[d] + 1);
+      lev[v] = l;
+      L = std::max(L, l + 1);
+    }
+    std::vector<std::vector<int>> byl(L);
+    for (int s = 0; s < KS; ++s) {
+      const int v = lower ? s : KS - 1 - s;
+      byl[lev[v]].push_back(v);
+    }
+    const int E = kHeadEpl;
+    auto nslots = [&](int v) {   // 1, 2 or 4 slots of kHeadG lanes (rows beyond 4 slots overflow)
+      const int c = (int)deps[v].size();
+      return c <= kHeadG * E ? 1 : c <= 2 * kHeadG * E ? 2 : 4;
+    };
+    for (auto rows : byl) {
+      // widest rows first: power-of-two sizes in descending order stay aligned in a pass
+      std::stable_sort(rows.begin(), rows.end(), [&](int x, int y) { return nslots(x) > nslots(y); });
+      size_t q = 0;
+      while (q < rows.size()) {   // one pass
+        const size_t r_pass = h.rec.size();
+        h.rec.resize(r_pass + kHeadRowsPerPass, KS);
+        h.ooff.resize(r_pass + kHeadRowsPerPass + 1, (int)h.oidx.size());
+        h.eidx.resize((r_pass + kHeadRowsPerPass) * E * kHeadG, 0);
+        h.slot.resize((r_pass + kHeadRowsPerPass) * E * kHeadG, -1);
+        int used = 0;
+        while (q < rows.size() && used + nslots(rows[q]) <= kHeadRowsPerPass) {
+          const int v = rows[q], ns = nslots(v), GL = ns * kHeadG;
+          const int lg = ns == 1 ? 0 : ns == 2 ? 1 : 2;
+          const size_t r0 = r_pass + used;
+          const int cnt = (int)deps[v].size();
+          const bool over = cnt > GL * E;
+          for (int sub = 0; sub < ns; ++sub)
+            h.rec[r0 + sub] = (int)((over ? 0x80000000u : 0u) | ((unsigned)sub << 18) | ((unsigned)lg << 16) |
+                                    (unsigned)(sub == 0 ? v : KS));
+          for (int e = 0; e < std::min(cnt, GL * E); ++e) {   // entry e -> group lane e % GL, k = e / GL
+            const int gl = e % GL, k = e / GL;
+            const size_t at = ((r0 + gl / kHeadG) * E + k) * kHeadG + gl % kHeadG;
+            h.eidx[at] = deps[v][e];
+            h.slot[at] = dslot[v][e];
+          }
+          h.ooff[r0] = (int)h.oidx.size();
+          for (int e = GL * E; e < cnt; ++e) { h.oidx.push_back(deps[v][e]); h.oslot.push_back(dslot[v][e]); }
+          for (int sub = 1; sub <= ns; ++sub) h.ooff[r0 + sub] = (int)h.oidx.size();
+          used += ns;
+          ++q;
+        }
+        for (size_t r = r_pass + used; r <= r_pass + kHeadRowsPerPass; ++r) h.ooff[r] = (int)h.oidx.size();
+        h.pend.push_back(q >= rows.size() ? 1 : 0);   // last pass of its level: barrier after it
+      }
+    }
+    return h;
+  };
+  SegArrays sl = build_seg(true), sb = build_seg(false);
+  std::vector<int> hrow(KS);
+  for (int v = 0; v < KS; ++v) hrow[v] = lab[K0 + v];
+  const size_t o_hrow = put(hrow);
+  size_t o_s[2][5], v_s[2][2];
+  for (int w = 0; w < 2; ++w) {
+    SegArrays& h = w == 0 ? sl : sb;
+    o_s[w][0] = put(h.rec);
+    o_s[w][1] = put(h.eidx);
+    o_s[w][2] = put(h.oidx);
+    o_s[w][3] = put(h.ooff);
+    o_s[w][4] = put(h.pend);
+    v_s[w][0] = vslot.size();
+    vslot.insert(vslot.end(), h.slot.begin(), h.slot.end());
+    v_s[w][1] = vslot.size();
+    vslot.insert(vslot.end(), h.oslot.begin(), h.oslot.end());
+  }
+
+  // ---- partial sums across parts
+  struct PartArrays { std::vector<int> row, off{0}, idx, slot; };
+  PartArrays th, p10, p01;
+  for (int v = 0; v < K; ++v) {   // B^T: tail dependents of every head row
+    const int j = lab[v];
+    th.row.push_back(j);
+    for (int e = tptr[j]; e < tptr[j + 1]; ++e)
+      if (part(trow[e]) == 2) { th.idx.push_back(trow[e]); th.slot.push_back(tslot[e]); }
+    th.off.push_back((int)th.idx.size());
+  }
+  if (KS > 0) {
+    for (int v = 0; v < K0; ++v) {   // B^T: head-1 dependents of every head-0 row
+      const int j = lab[v];
+      p10.row.push_back(j);
+      for (int e = tptr[j]; e < tptr[j + 1]; ++e)
+        if (part(trow[e]) == 1) { p10.idx.push_back(trow[e]); p10.slot.push_back(tslot[e]); }
+      p10.off.push_back((int)p10.idx.size());
+    }
+    if (K0 > 0) {
+      for (int v = 0; v < KS; ++v) {   // lower: head-0 neighbours of every head-1 row
+        const int p = lab[K0 + v];
+        p01.row.push_back(p);
+        for (int r = 0; r < kk(p); ++r) {
+          const int j = nbr[(size_t)p * m + r];
+          if (part(j) == 0) { p01.idx.push_back(j); p01.slot.push_back(p * m + r); }
+        }
+        p01.off.push_back((int)p01.idx.size());
+      }
+    }
+  }
+  size_t o_p[3][3], v_p[3];
+  PartArrays* pa[3] = {&th, &p10, &p01};
+  for (int w = 0; w < 3; ++w) {
+    o_p[w][0] = put(pa[w]->row);
+    o_p[w][1] = put(pa[w]->off);
+    o_p[w][2] = put(pa[w]->idx);
+    v_p[w] = vslot.size();
+    vslot.insert(vslot.end(), pa[w]->slot.begin(), pa[w]->slot.end());
+  }
+
+  // ---- dense head: storage rows of head-0 slots, and per entry (i, r) of its rows the Vecchia
+  // column of B_00 (-1: padding) next to the value slot
+  std::vector<int> h0row(K0), dcol((size_t)K0 * m, -1), dslot0((size_t)K0 * m, -1);
+  for (int v = 0; v < K0; ++v) {
+    const int p = lab[v];
+    h0row[v] = p;
+    for (int r = 0; r < kk(p); ++r) {
+      dcol[(size_t)v * m + r] = vo[nbr[(size_t)p * m + r]];
+      dslot0[(size_t)v * m + r] = p * m + r;
+    }
+  }
+  const size_t o_h0row = put(h0row), o_dcol = put(dcol);
+  const size_t v_d0 = vslot.size();
+  vslot.insert(vslot.end(), dslot0.begin(), dslot0.end());
+
+  // ---- upload, then point the plan structs into the two arrays
+  d_int_.alloc(std::max<size_t>(ints.size(), 1));
+  d_slot_.alloc(std::max<size_t>(vslot.size(), 1));
+  d_val_.alloc(std::max<size_t>(vslot.size(), 1));
+  if (!ints.empty())
+    HIP_CHECK(hipMemcpyAsync(d_int_.get(), ints.data(), sizeof(int) * ints.size(), hipMemcpyHostToDevice, s_));
+  if (!vslot.empty())
+    HIP_CHECK(hipMemcpyAsync(d_slot_.get(), vslot.data(), sizeof(int) * vslot.size(), hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  nslot_ = (int)vslot.size();
+  const int* I = d_int_.get();
+  const double* V = d_val_.get();
+  for (int w = 0; w < 2; ++w) {
+    HeadSolve& h = w == 0 ? seg_low_ : seg_bt_;
+    const SegArrays& a = w == 0 ? sl : sb;
+    h.K = KS;
+    h.npass = (int)(a.rec.size() / kHeadRowsPerPass);
+    h.hrow = I + o_hrow;
+    h.rec = I + o_s[w][0];
+    h.eidx = I + o_s[w][1];
+    h.oidx = I + o_s[w][2];
+    h.ooff = I + o_s[w][3];
+    h.pend = I + o_s[w][4];
+    h.eval = V + v_s[w][0];
+    h.oval = V + v_s[w][1];
+  }
+  PartialList* pl[3] = {&p_th_, &p_10_, &p_01_};
+  for (int w = 0; w < 3; ++w) {
+    pl[w]->rows = (int)pa[w]->row.size();
+    pl[w]->row = I + o_p[w][0];
+    pl[w]->eoff = I + o_p[w][1];
+    pl[w]->eidx = I + o_p[w][2];
+    pl[w]->eval = V + v_p[w];
+  }
+  dh_.K0 = K0;
+  dh_.m = m;
+  dh_.row = I + o_h0row;
+  dh_.col = I + o_dcol;
+  dh_.val = V + v_d0;
+  if (KS > 0) set_vadu_head_lds_limit(KS);
+  // ---- dense head buffers (G's strict upper triangle stays zero: TRTRI writes lower blocks only)
+  ld0_ = ((K0 + 63) / 64) * 64;
+  dh_.ld = ld0_;
+  if (K0 > 0) {
+    const size_t nn = (size_t)ld0_ * ld0_;
+    Bd_.alloc(nn);
+    G_.alloc(nn);
+    GT_.alloc(nn);
+    T_.alloc((size_t)ld0_ * (ld0_ / 2 + 64));
+    HIP_CHECK(hipMemsetAsync(G_.get(), 0, nn * sizeof(double), s_));
+    HIP_CHECK(hipStreamSynchronize(s_));
+  }
+}
+
+void VaduPrecond::Refresh(const double* Bv) {
+  launch_gather(nslot_, d_slot_.get(), Bv, d_val_.get(), s_);
+  launch_merged_numeric(mt_bt_, Bv, s_);
+  launch_merged_numeric(mt_low_, Bv, s_);
+  if (K0_ > 0) dense_head_factor(dh_, Bd_.get(), G_.get(), GT_.get(), T_.get(), s_);
+}
+
+void VaduPrecond::SetDiag(const double* dw) {
+  if (dw != dw_) DropGraphs();   // the captured launches hold the pointer
+  dw_ = dw;
+}
+
+void VaduPrecond::DenseApply(const double* Xt, double* Z, int t) {
+  // S_ holds >= ld0_ * t doubles: sized by Apply / TimeParts before any capture
+  launch_dense_head_apply(dh_, G_.get(), GT_.get(), dw_, Xt, S_.get(), Z, t, s_);
+}
+
+void VaduPrecond::TailSolve(bool lower, const double* R, double* Xt, double* Z, int t) {
+  const MergedSolve& ms = lower ? mt_low_ : mt_bt_;
+  for (int L = 0; L + 1 < (int)ms.lptr.size(); ++L)
+    launch_merged_level(ms, L, lower, dw_, lower ? Xt : R, lower ? Z : Xt, t, s_);
+}
+
+void VaduPrecond::Record(const double* R, double* Z, double* Xt, int t) {
+  const bool seg = K_ > K0_;
+  TailSolve(false, R, Xt, Z, t);
+  if (K_ > 0) launch_vadu_partial(p_th_, R, nullptr, Xt, Xt, t, s_);
+  if (seg) launch_vadu_head(seg_bt_, Xt, nullptr, Xt, t, s_);
+  if (K0_ > 0) {
+    if (seg) launch_vadu_partial(p_10_, nullptr, nullptr, Xt, Xt, t, s_);
+    DenseApply(Xt, Z, t);
+  }
+  if (seg) {
+    if (K0_ > 0) {
+      launch_vadu_partial(p_01_, Xt, dw_, Z, Z, t, s_);
+      launch_vadu_head(seg_low_, Z, nullptr, Z, t, s_);
+    } else {
+      launch_vadu_head(seg_low_, Xt, dw_, Z, t, s_);
+    }
+  }
+  TailSolve(true, R, Xt, Z, t);
+}
+
+void VaduPrecond::Apply(const double* R, double* Z, double* Xt, int t) {
+  if (!dw_) Fatal("VADU preconditioner applied before SetDiag");
+  if (K0_ > 0 && S_.size() < (size_t)ld0_ * t) {   // dense-head scratch sized before any capture
+    DropGraphs();
+    S_.alloc((size_t)ld0_ * t);
+  }
+  if (!use_graph_) {
+    Record(R, Z, Xt, t);
+    return;
+  }
+  for (const GraphEntry& g : graphs_) {
+    if (g.key[0] == R && g.key[1] == Z && g.key[2] == Xt && g.t == t) {
+      HIP_CHECK(hipGraphLaunch(g.exec, s_));
+      return;
+    }
+  }
+  hipGraph_t graph;
+  HIP_CHECK(hipStreamBeginCapture(s_, hipStreamCaptureModeThreadLocal));
+  Record(R, Z, Xt, t);
+  HIP_CHECK(hipStreamEndCapture(s_, &graph));
+  GraphEntry e{{R, Z, Xt}, t, nullptr};
+  HIP_CHECK(hipGraphInstantiate(&e.exec, graph, nullptr, nullptr, 0));
+  HIP_CHECK(hipGraphDestroy(graph));
+  graphs_.push_back(e);
+  HIP_CHECK(hipGraphLaunch(e.exec, s_));
+}
+
+void VaduPrecond::TimeParts(const double* R, double* Z, double* Xt, int t, int reps) {
+  if (K0_ > 0 && S_.size() < (size_t)ld0_ * t) {
+    DropGraphs();
+    S_.alloc((size_t)ld0_ * t);
+  }
+  hipEvent_t a, b;
+  HIP_CHECK(hipEventCreate(&a));
+  HIP_CHECK(hipEventCreate(&b));
+  const bool seg = K_ > K0_;
+  auto part = [&](const char* name, auto fn) {
+    float ms = 0.f;
+    HIP_CHECK(hipEventRecord(a, s_));
+    for (int r = 0; r < reps; ++r) fn();
+    HIP_CHECK(hipEventRecord(b, s_));
+    HIP_CHECK(hipEventSynchronize(b));
+    HIP_CHECK(hipEventElapsedTime(&ms, a, b));
+    std::fprintf(stderr, "[precond parts t=%d] %-11s %.4f ms\n", t, name, ms / reps);
+  };
+  part("tail_bt", [&] { TailSolve(false, R, Xt, Z, t); });
+  part("part_th", [&] { launch_vadu_partial(p_th_, R, nullptr, Xt, Xt, t, s_); });
+  if (seg) part("seg_bt", [&] { launch_vadu_head(seg_bt_, Xt, nullptr, Xt, t, s_); });
+  if (K0_ > 0 && seg) part("part_10", [&] { launch_vadu_partial(p_10_, nullptr, nullptr, Xt, Xt, t, s_); });
+  if (K0_ > 0) part("dense", [&] { DenseApply(Xt, Z, t); });
+  if (K0_ > 0 && seg) part("part_01", [&] { launch_vadu_partial(p_01_, Xt, dw_, Z, Z, t, s_); });
+  if (seg) part("seg_low", [&] { launch_vadu_head(seg_low_, Z, nullptr, Z, t, s_); });
+  part("tail_low", [&] { TailSolve(true, R, Xt, Z, t); });
+  std::fprintf(stderr,
+               "[precond parts t=%d] K0=%d K=%d passes bt=%d low=%d tail merged levels bt=%d low=%d (g=%d, %ld entries) "
+               "launches=%d\n",
+               t, K0_, K_, seg_bt_.npass, seg_low_.npass, tail_levels_bt(), tail_levels_lower(), merge_g_, tail_entries_,
+               launches());
+  HIP_CHECK(hipEventDestroy(a));
+  HIP_CHECK(hipEventDestroy(b));
+}
+
+}  // namespace gpb_amd

@@ -1,6 +1,8 @@
-"""A/B of the VADU preconditioner forms (GPBOOST_AMD_PRECOND) on the latent Vecchia path:
-one nll+grad evaluation per mode at n=100k (gaussian vecchia_latent and bernoulli_logit), the
-preconditioner's per-application time from GPB_BenchLatentOperators, and the results."""
+"""A/B of the VADU preconditioner plan split (vadu_precond.h) on the latent Vecchia path at
+n = 100k: per plan "K0:K[:g]" (dense head rows : head rows incl. the dense ones : tail levels merged per launch) one warm-up and
+two timed nll+grad evaluations, the preconditioner's per-application time (t = 51 and t = 1,
+GPB_BenchLatentOperators, with the per-step split when GPBOOST_AMD_PRECOND_SPLIT is set), and
+the results (they must agree across plans to rounding)."""
 import os
 import sys
 import time
@@ -11,13 +13,16 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from gpboost_amd import GPModel, synthetic  # noqa: E402
 
 n = int(os.environ.get("N", "100000"))
-modes = [int(v) for v in os.environ.get("MODES", "1 4").split()]
+plans = os.environ.get("PLANS", "0:14336 2048:14336").split()
 liks = os.environ.get("LIKS", "gaussian").split()
 X = synthetic.bench_coords(n)
 for lik in liks:
     y = synthetic.bench_gaussian_y(n) if lik == "gaussian" else synthetic.bench_bernoulli_y(X)
-    for mode in modes:
-        os.environ["GPBOOST_AMD_PRECOND"] = str(mode)
+    for plan in plans:
+        k0, k, g = (plan.split(":") + ["4"])[:3]
+        os.environ["GPBOOST_AMD_DENSE_ROWS"] = k0
+        os.environ["GPBOOST_AMD_HEAD_ROWS"] = k
+        os.environ["GPBOOST_AMD_TAIL_MERGE"] = g
         gm = GPModel(gp_coords=X, likelihood=lik, cov_function="exponential",
                      gp_approx="vecchia_latent" if lik == "gaussian" else "vecchia", num_neighbors=30,
                      vecchia_ordering="random", seed=0, matrix_inversion_method="iterative")
@@ -37,7 +42,7 @@ for lik in liks:
         t = 51 if lik == "gaussian" else 50
         ops = gm.bench_latent_operators(t, 10)
         ops1 = gm.bench_latent_operators(1, 10)
-        print(f"{lik} mode={mode} first={t1 - t0:.3f}s eval={np.median(ts):.4f}s nll={r[0]:.12g} grad={r[1]} "
+        print(f"{lik} plan={plan} first={t1 - t0:.3f}s eval={np.median(ts):.4f}s nll={r[0]:.12g} grad={r[1]} "
               f"info={info} A_ms(t={t})={ops[0]:.4f} P_ms(t={t})={ops[1]:.4f} launches={ops[3]:.0f} "
               f"A_ms(1)={ops1[0]:.4f} P_ms(1)={ops1[1]:.4f}", flush=True)
         del gm

@@ -154,28 +154,53 @@ def test_latent_errors():
         gm.neg_log_likelihood_and_grad([1.0, 0.1], synthetic.bench_bernoulli_y(X), profile_sigma2=True)
 
 
-@pytest.mark.parametrize("head_rows", ["0", "100", "12288", "20000"])
-def test_preconditioner_forms_agree(monkeypatch, head_rows):
-    """The head/tail split of the VADU solves (precond mode 4; head = the first K Vecchia rows
-    solved per column in LDS, tail by level kernels) against the one-launch-per-level form
-    (mode 1) on the same model: the row arithmetic is the same, only the summation split of a
-    row's entries differs, so the evaluations agree to rounding. K = 0 (tail only), a small
-    head, the default and K >= n (head only) cover every plan shape."""
+@pytest.mark.parametrize("dense_rows,head_rows,merge", [("0", "100", "1"), ("0", "6000", "4"), ("2048", "2048", "4"),
+                                                         ("512", "5000", "2"), ("2048", "8000", "4"),
+                                                         ("8000", "8000", "4"), ("0", "0", "4"), ("1024", "3000", "9")])
+def test_preconditioner_plans_agree(monkeypatch, dense_rows, head_rows, merge):
+    """The three-part VADU plan (vadu_precond.h: dense head [0, K0), LDS segment [K0, K), merged
+    level kernels for the tail, g levels per launch) against the plain level schedule (K0 = K = 0,
+    g = 1) on the same model. The solves are the same algebra; the dense block (an explicit
+    inverse), the substituted coefficients of merged levels and the entry splits change only the
+    rounding, so at a tight CG tolerance the evaluations agree to ~1e-10. Covers a tiny segment,
+    segment only, dense + tail, all three parts, dense + segment (no tail), dense only, and merged
+    tails without a head."""
     from gpboost_amd import synthetic
     n = 8000
     X = synthetic.bench_coords(n)
-    out = {}
     for lik in ("gaussian", "bernoulli_logit"):
         y = synthetic.bench_gaussian_y(n) if lik == "gaussian" else synthetic.bench_bernoulli_y(X)
         case = dict(likelihood=lik, cov_fct="exponential", shape=0.5, num_neighbors=30, aux=0.1)
-        for mode in ("1", "4"):
-            monkeypatch.setenv("GPBOOST_AMD_PRECOND", mode)
-            monkeypatch.setenv("GPBOOST_AMD_HEAD_ROWS", head_rows)
+        out = {}
+        for key, (k0, k, g) in {"levels": ("0", "0", "1"), "plan": (dense_rows, head_rows, merge)}.items():
+            monkeypatch.setenv("GPBOOST_AMD_DENSE_ROWS", k0)
+            monkeypatch.setenv("GPBOOST_AMD_HEAD_ROWS", k)
+            monkeypatch.setenv("GPBOOST_AMD_TAIL_MERGE", g)
             gm = _model(X, case, t=12, dc=1e-9)
-            out[(lik, mode)] = gm.neg_log_likelihood_and_grad([1.0, 0.1], y)
-        a, b = out[(lik, "1")], out[(lik, "4")]
+            out[key] = gm.neg_log_likelihood_and_grad([1.0, 0.1], y)
+        a, b = out["levels"], out["plan"]
         assert abs(a[0] - b[0]) <= 1e-9 * abs(a[0]), (lik, a[0], b[0])
         np.testing.assert_allclose(b[1], a[1], rtol=1e-7, atol=1e-7 * np.abs(a[1]).max())
+
+
+def test_latent_zero_response(monkeypatch):
+    """y == 0 under the Gaussian latent model: the Newton right-hand side y / aux is zero, so its
+    CG column (fused with the probes) must stop at u = 0 without iterating (CG_utils.cpp:42-45)
+    instead of dividing 0 by 0; checked against the oracle."""
+    from gpboost_amd import synthetic
+    n = 3000
+    X = synthetic.bench_coords(n)
+    y = np.zeros(n)
+    case = dict(likelihood="gaussian", cov_fct="exponential", shape=0.5, num_neighbors=20, aux=0.3)
+    for k0 in ("0", "2048"):
+        monkeypatch.setenv("GPBOOST_AMD_DENSE_ROWS", k0)
+        gm = _model(X, case, t=10, dc=1e-8)
+        nll, g, _ = gm.neg_log_likelihood_and_grad([0.8, 0.15], y)
+        perm, xv, nb = O.vecchia_setup(X, 20, 0, True)
+        ref = O.latent_iterative(xv, y[perm], nb, 0, O.transform_latent(0, [0.8, 0.15]), "gaussian", 0.3, t=10,
+                                 cg_delta_conv=1e-8)
+        assert np.isfinite(nll) and np.all(np.isfinite(g))
+        _check(nll, g, ref["nll"], ref["grad"])
 
 
 def test_latent_many_neighbours_vs_oracle():
@@ -201,6 +226,7 @@ def test_two_live_models_different_head_sizes(monkeypatch):
     case = dict(likelihood="gaussian", cov_fct="exponential", shape=0.5, num_neighbors=20, aux=0.1)
     X = synthetic.bench_coords(9000)
     y = synthetic.bench_gaussian_y(9000)
+    monkeypatch.setenv("GPBOOST_AMD_DENSE_ROWS", "0")
     monkeypatch.setenv("GPBOOST_AMD_HEAD_ROWS", "8000")
     a = _model(X, case, t=8, dc=1e-8)
     ra = a.neg_log_likelihood_and_grad([1.0, 0.1], y)
