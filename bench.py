@@ -174,8 +174,9 @@ def latent_leg(X, Y, steps: int, cpu: bool) -> dict:
         "cg_matvec_roofline": {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                "frac": ach / HBM_PEAK_GBS, "traffic": None, "kernel": "b_apply_wave + bt_apply_wave",
                                "kernel_ms": ms_a, "columns": r, "algorithmic_bytes_per_launch": byts},
-        "preconditioner": {"kernel": "vadu_head (first 14336 Vecchia rows, one workgroup per column, LDS) + "
-                                     "vadu_levelT (tail level sets), replayed from a hipGraph", "ms": ms_p,
+        "preconditioner": {"kernel": "VaduPrecond: dense MFMA head block (first 2048 Vecchia rows) + LDS segment "
+                                     "(rows 2048-14335, one workgroup per column) + merged tail levels (up to 16 "
+                                     "dependency levels per launch), replayed from a hipGraph", "ms": ms_p,
                            "launches": int(nlev), "us_per_launch": ms_p * 1e3 / max(nlev, 1),
                            "share_of_eval": None},
     }

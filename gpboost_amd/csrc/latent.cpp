@@ -2,7 +2,6 @@
 #include "latent.h"
 
 #include <algorithm>
-#include <atomic>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -66,10 +65,9 @@ LatentVecchia::LatentVecchia(int n, int d, int m, const double* d_X, const int* 
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_out_), kOutDoubles * sizeof(double), hipHostMallocDefault));
   // PCG verdicts: written by the device straight into host-coherent memory (no copy command on
   // the stream between iterations), polled by the host
-  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_ctl_), 2 * kPcgCtl * sizeof(int),
-                          hipHostMallocMapped | hipHostMallocCoherent));
+  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_ctl_), 4 * sizeof(int), hipHostMallocMapped | hipHostMallocCoherent));
   HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&d_hctl_), h_ctl_, 0));
-  std::fill(h_ctl_, h_ctl_ + 2 * kPcgCtl, 0);
+  std::fill(h_ctl_, h_ctl_ + 4, -1);   // two 64-bit verdict slots, no sequence number matches
   // VADU plan split (vadu_precond.h): dense head [0, K0), LDS segment [K0, K), level-scheduled
   // tail. K0 = 2048: the first 2048 rows span 201 of the 388 levels of each solve at n = 100k.
   // K = 14336: 112 KB of segment values per column workgroup (K sweep 12288 / 14336 / 16384:
@@ -327,17 +325,20 @@ void LatentVecchia::Scalars(const ScalarArgs& a, double* out) {
 // Spin until the device's stopping check `seq` has landed in the host-coherent words (it is
 // written last, after a system-scope fence). A stream that drained without it is an error.
 void LatentVecchia::WaitCtl(int seq, int* out) {
-  volatile int* hc = h_ctl_ + (seq & 1) * kPcgCtl;   // two slots: checks j and j + 1 may both be in flight
-  for (long spins = 1; hc[kCtlSeq] != seq; ++spins) {
+  // two slots: checks j and j + 1 may both be in flight
+  volatile unsigned long long* hc = reinterpret_cast<volatile unsigned long long*>(h_ctl_) + (seq & 1);
+  unsigned long long v = *hc;
+  for (long spins = 1; (int)(v & 0xFFFF) != (seq & 0xFFFF); ++spins) {
     if ((spins & ((1 << 16) - 1)) == 0) {
       const hipError_t e = hipStreamQuery(s_);
       if (e != hipSuccess && e != hipErrorNotReady) HIP_CHECK(e);
-      if (e == hipSuccess && hc[kCtlSeq] != seq) Fatal("PCG stopping check %d did not report", seq);
+      v = *hc;
+      if (e == hipSuccess && (int)(v & 0xFFFF) != (seq & 0xFFFF)) Fatal("PCG stopping check %d did not report", seq);
     }
     __builtin_ia32_pause();
+    v = *hc;
   }
-  std::atomic_thread_fence(std::memory_order_acquire);
-  for (int q = 0; q < kPcgCtl; ++q) out[q] = hc[q];
+  pcg_unpack(v, out);
 }
 
 LatentVecchia::PcgResult LatentVecchia::Pcg(Block& b, const double* RHS, double* U, int n_single, bool init_zero,
@@ -402,7 +403,7 @@ LatentVecchia::PcgResult LatentVecchia::Pcg(Block& b, const double* RHS, double*
     launch_cg_update(n_, t, b.a(), b.H.get(), b.V.get(), U, b.R.get(), d_partials_.get(), b.rr(), s_);
     const int seq = ++pcg_seq_;
     launch_pcg_check(j, t, n_single, pmax_single, pmax_block, delta, b.rr(), b.act.get(), b.ctl.get(),
-                     d_hctl_ + (seq & 1) * kPcgCtl, seq, s_);
+                     d_hctl_ + (seq & 1) * 2, seq, s_);
     Precond(b.R.get(), b.Z.get(), b.Xt.get(), t);
     {
       const double* A[1] = {b.R.get()};

@@ -125,7 +125,7 @@ class LatentVecchia {
   DevBuf<double> d_partials_, d_out_;
   double* h_out_ = nullptr;                      // pinned
   std::unique_ptr<Block> blk1_, blkt_, blkb_;   // blkb_: BenchOperators
-  int* h_ctl_ = nullptr;                         // host-coherent PcgCtl words written by pcg_check
+  int* h_ctl_ = nullptr;                         // host-coherent verdict words written by pcg_check (2 x 64 bit)
   int* d_hctl_ = nullptr;                        // their device address
   int pcg_seq_ = 0;
   hipEvent_t ev0_ = nullptr, ev1_ = nullptr;

@@ -104,6 +104,8 @@ void launch_merged_level(const MergedSolve& ms, int L, bool lower, const double*
 // only) in a fixed lane-major layout: entry e < GL * EPL of the row sits at group lane
 // gl = e % GL, k = e / GL, i.e. slot r0 + gl / kHeadG, position ((r * EPL + k) * kHeadG + gl %
 // kHeadG) (zero value = padding); entries beyond GL * EPL go to the overflow lists.
+// 64 slots of 16 lanes (2 entries each). (128 slots of 8 lanes x 4 entries: 40% fewer passes at
+// n = 100k but each pass slower, 0.318 vs 0.297 ms for the two segment solves at t = 51.)
 constexpr int kHeadRowsPerPass = 64;
 constexpr int kHeadMaxRows = 16384;  // segment limit: 128 KB of LDS per column workgroup
 constexpr int kHeadG = 16;            // lanes per slot
@@ -160,16 +162,29 @@ void launch_cg_update(int n, int t, const double* a, const double* H, const doub
 // Device side of the PCG stopping rules (LatentVecchia::Pcg). ctl[kCtlActS]: single-vector
 // columns [0, n_single) still running; ctl[kCtlActB]: block columns [n_single, t) running;
 // ctl[kCtlItsS] / [kCtlItsB]: iterations done; ctl[kCtlNan]: NaN/Inf met in a residual norm.
-// ctl[kCtlSeq] (host copy only): sequence number of the check that wrote it.
-enum PcgCtlField : int { kCtlActS = 0, kCtlActB, kCtlItsS, kCtlItsB, kCtlNan, kCtlSeq, kPcgCtl = 8 };
+enum PcgCtlField : int { kCtlActS = 0, kCtlActB, kCtlItsS, kCtlItsB, kCtlNan, kPcgCtl = 8 };
+// Host copy of a verdict: one 64-bit word, bits 0-15 the check's sequence number, 16 / 17 / 18
+// the single / block / NaN flags, 19-39 its_single, 40-60 its_block.
+__host__ __device__ inline unsigned long long pcg_pack(int seq, int act_s, int act_b, int nan, int its_s, int its_b) {
+  return (unsigned long long)(seq & 0xFFFF) | (unsigned long long)(act_s & 1) << 16 |
+         (unsigned long long)(act_b & 1) << 17 | (unsigned long long)(nan & 1) << 18 |
+         (unsigned long long)(its_s & 0x1FFFFF) << 19 | (unsigned long long)(its_b & 0x1FFFFF) << 40;
+}
+__host__ __device__ inline void pcg_unpack(unsigned long long v, int* ctl) {
+  ctl[kCtlActS] = (int)(v >> 16) & 1;
+  ctl[kCtlActB] = (int)(v >> 17) & 1;
+  ctl[kCtlNan] = (int)(v >> 18) & 1;
+  ctl[kCtlItsS] = (int)(v >> 19) & 0x1FFFFF;
+  ctl[kCtlItsB] = (int)(v >> 40) & 0x1FFFFF;
+}
 // act[c] = 1, except single columns whose right-hand side is zero (rr0[c] < zero_sq: the
 // reference returns u = 0 without iterating, CG_utils.cpp:42-45).
 void launch_pcg_init(int t, int n_single, int pmax_single, int pmax_block, double zero_sq, const double* rr0,
                      int* act, int* ctl, hipStream_t s);
 // After iteration j's update (rr[c] = ||r_c||^2): single columns stop on their own norm
 // (CG_utils.cpp:80-90), the block on the mean column norm (:172-178), both at their pmax.
-// host_ctl (nullable, host-coherent memory mapped for the device): the fields are copied there,
-// then host_ctl[kCtlSeq] = seq after a system-scope fence.
+// host_ctl (nullable, 8-byte aligned host-coherent memory mapped for the device): receives
+// pcg_pack(seq, ...) by one store.
 void launch_pcg_check(int j, int t, int n_single, int pmax_single, int pmax_block, double delta, const double* rr,
                       int* act, int* ctl, int* host_ctl, int seq, hipStream_t s);
 // H = Z + b .* H

@@ -599,10 +599,12 @@ __global__ void pcg_check_kernel(int j, int t, int n_single, int pmax_single, in
       ctl[kCtlActB] = 0;
     }
   }
-  if (host_ctl) {   // verdict straight into host-coherent memory, the sequence word last
-    for (int q = 0; q < kCtlSeq; ++q) host_ctl[q] = ctl[q];
-    __threadfence_system();
-    host_ctl[kCtlSeq] = seq;
+  if (host_ctl) {
+    // the verdict as ONE 64-bit word (pcg_pack) in host-coherent memory: a single untorn store,
+    // so no system-scope fence (which would write back the whole L2 and stall the stream)
+    const unsigned long long v = pcg_pack(seq, ctl[kCtlActS], ctl[kCtlActB], ctl[kCtlNan], ctl[kCtlItsS], ctl[kCtlItsB]);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(host_ctl), v, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 

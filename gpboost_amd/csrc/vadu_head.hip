@@ -38,8 +38,8 @@ __device__ __forceinline__ void lds_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
 }
 
-// Sum over each 16-lane DPP row, result in every lane of the row: quad swaps, then the half-row
-// and row mirrors (VALU data movement instead of four LDS-crossbar shuffles on the pass's
+// Sum over each slot of kHeadG lanes, result in every lane of the slot: quad swaps, then the
+// half-row (and row) mirrors (VALU data movement instead of LDS-crossbar shuffles on the pass's
 // critical chain). Fixed order -> bitwise repeatable.
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
@@ -47,11 +47,12 @@ __device__ __forceinline__ double dpp_f64(double v) {
   const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
   return __hiloint2double(hi, lo);
 }
-__device__ __forceinline__ double row16_sum(double v) {
+__device__ __forceinline__ double slot_sum(double v) {
+  static_assert(kHeadG == 8 || kHeadG == 16, "a slot is one half or one whole 16-lane DPP row");
   v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
   v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]
-  v += dpp_f64<0x141>(v);   // row_half_mirror
-  v += dpp_f64<0x140>(v);   // row_mirror
+  v += dpp_f64<0x141>(v);   // row_half_mirror: 8-lane sums
+  if constexpr (kHeadG == 16) v += dpp_f64<0x140>(v);   // row_mirror
   return v;
 }
 
@@ -80,7 +81,7 @@ __device__ __forceinline__ void load_stage(const HeadSolve& h, int q, int slot, 
   }
 }
 
-// A row spans 1, 2 or 4 slots (16 << lg lanes); group lane gl = sub * 16 + lane holds its
+// A row spans 1, 2 or 4 slots (kHeadG << lg lanes); group lane gl = sub * kHeadG + lane holds its
 // entries gl + k * GL (k < EPL), then overflow entries [ooff[r0], ooff[r0 + 1]) in steps of GL.
 template <int EPL>
 __device__ __forceinline__ void solve_row(const HeadSolve& h, const Stage<EPL>& st, int q, int slot, int lane,
@@ -94,14 +95,14 @@ __device__ __forceinline__ void solve_row(const HeadSolve& h, const Stage<EPL>& 
     const int GL = kHeadG << lg;
     for (int e = h.ooff[r0] + sub * kHeadG + lane; e < h.ooff[r0 + 1]; e += GL) acc = fma(h.oval[e], xs[h.oidx[e]], acc);
   }
-  static_assert(kHeadG == 16, "row16_sum reduces one 16-lane DPP row");
-  acc = row16_sum(acc);
+  acc = slot_sum(acc);
   if (__ballot(lg >= 1)) {   // wave-uniform: only waves holding a multi-slot row pay the cross-slot steps
-    const double o16 = __shfl_xor(acc, 16, 64);
-    if (lg >= 1) acc += o16;
+    // partner slot: the other half of the 16-lane DPP row (row_mirror) for 8-lane slots
+    const double o1 = kHeadG == 8 ? dpp_f64<0x140>(acc) : __shfl_xor(acc, kHeadG, 64);
+    if (lg >= 1) acc += o1;
     if (__ballot(lg >= 2)) {
-      const double o32 = __shfl_xor(acc, 32, 64);
-      if (lg >= 2) acc += o32;
+      const double o2 = __shfl_xor(acc, 2 * kHeadG, 64);
+      if (lg >= 2) acc += o2;
     }
   }
   if (lane == 0 && sub == 0) xs[st.rec & 0xffff] -= acc;

@@ -25,28 +25,58 @@ namespace gpb_amd {
 namespace {
 
 // Coefficients of the positions at one level offset (their substituted dependencies sit at lower
-// offsets of the same merged level, done by earlier launches). One thread per position.
+// offsets of the same merged level, done by earlier launches). One wave per position: the ops run
+// in order, the entries of one substitution in parallel over the lanes (they map to distinct
+// positions of the row's list), accumulated in LDS; lists longer than kNumericLds run on one lane
+// in global memory. Same order of accumulation either way.
+constexpr int kNumericLds = 512;
 __global__ void __launch_bounds__(256) merge_numeric_kernel(MergedSolve ms, const int* __restrict__ plist, int cnt,
                                                             const double* __restrict__ Bv) {
-  const int k = blockIdx.x * 256 + threadIdx.x;
+  __shared__ double cbuf[4][kNumericLds];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int k = blockIdx.x * 4 + w;
   if (k >= cnt) return;
   const int p = plist[k];
   const int base = ms.eoff[p], len = ms.eoff[p + 1] - base;
-  double* c = ms.eval + base;
-  c[0] = 1.;   // the row's own input
-  for (int q = 1; q < len; ++q) c[q] = 0.;
-  for (int o = ms.opoff[p]; o < ms.opoff[p + 1]; ++o) {
-    const double w = -Bv[ms.op_slot[o]];
+  const int o0 = ms.opoff[p], o1 = ms.opoff[p + 1];
+  if (len > kNumericLds) {   // rare: serial in global memory
+    if (lane != 0) return;
+    double* c = ms.eval + base;
+    c[0] = 1.;
+    for (int q = 1; q < len; ++q) c[q] = 0.;
+    for (int o = o0; o < o1; ++o) {
+      const double wt = -Bv[ms.op_slot[o]];
+      const int mo = ms.op_map[o];
+      if (mo < 0) {
+        c[ms.op_a[o]] += wt;
+      } else {
+        const double* cj = ms.eval + ms.eoff[ms.op_a[o]];
+        const int lj = ms.eoff[ms.op_a[o] + 1] - ms.eoff[ms.op_a[o]];
+        for (int q = 0; q < lj; ++q) c[ms.map[mo + q]] = fma(wt, cj[q], c[ms.map[mo + q]]);
+      }
+    }
+    return;
+  }
+  double* c = cbuf[w];
+  for (int q = lane; q < len; q += 64) c[q] = q == 0 ? 1. : 0.;   // c[0]: the row's own input
+  for (int o = o0; o < o1; ++o) {
+    const double wt = -Bv[ms.op_slot[o]];
     const int mo = ms.op_map[o];
     if (mo < 0) {
-      c[ms.op_a[o]] += w;
+      if (lane == 0) c[ms.op_a[o]] += wt;
     } else {
       const int pj = ms.op_a[o];
       const double* cj = ms.eval + ms.eoff[pj];
       const int lj = ms.eoff[pj + 1] - ms.eoff[pj];
-      for (int q = 0; q < lj; ++q) c[ms.map[mo + q]] = fma(w, cj[q], c[ms.map[mo + q]]);
+      for (int q = lane; q < lj; q += 64) {
+        const int at = ms.map[mo + q];
+        c[at] = fma(wt, cj[q], c[at]);
+      }
     }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");   // this op's LDS updates before the next op's reads
   }
+  for (int q = lane; q < len; q += 64) ms.eval[base + q] = c[q];
 }
 
 // t >= 2: one workgroup per row; lane = column (coalesced t-wide gathers of a dependency's row),
@@ -151,11 +181,12 @@ __global__ void __launch_bounds__(256) merged_level1_kernel(MergedSolve ms, int 
   if (lane == 0) X[i] = acc;
 }
 
-// Shape knobs (A/B only): GPBOOST_AMD_LEVELT_NW = 0 (default): wave per row; 1, 2 or 4: one
-// workgroup per row with that many waves sharing its entries; GPBOOST_AMD_LEVEL1_G = lanes per
-// row at t = 1 (16, 32 or 64; default 64). Other values: error.
+// Shape knobs (A/B only): GPBOOST_AMD_LEVELT_NW = 1, 2 or 4 (default): one workgroup per row with
+// that many waves sharing its entries; 0: wave per row (merged_levelW; measured slower at n = 100k,
+// t = 51: 1.03 vs 0.82 ms per application for g = 4); GPBOOST_AMD_LEVEL1_G = lanes per row at
+// t = 1 (16, 32 or 64; default 64). Other values: error.
 struct LevelShape {
-  int nw = 0, g = 64;
+  int nw = 4, g = 64;
 };
 const LevelShape& level_shape() {
   static const LevelShape v = [] {
@@ -205,8 +236,8 @@ void launch_merged_numeric(const MergedSolve& ms, const double* Bv, hipStream_t 
   for (size_t o = 0; o + 1 < ms.offptr.size(); ++o) {
     const int cnt = ms.offptr[o + 1] - ms.offptr[o];
     if (cnt <= 0) continue;
-    hipLaunchKernelGGL(merge_numeric_kernel, dim3((cnt + 255) / 256), dim3(256), 0, s, ms, ms.offpos + ms.offptr[o],
-                       cnt, Bv);
+    hipLaunchKernelGGL(merge_numeric_kernel, dim3((cnt + 3) / 4), dim3(256), 0, s, ms, ms.offpos + ms.offptr[o], cnt,
+                       Bv);
   }
   HIP_CHECK(hipGetLastError());
 }

@@ -34,67 +34,95 @@ struct MergeHost {
   std::vector<int> offpos, offptr;
 };
 
+// Levels are merged greedily in order: a merged level takes the next level while its entries
+// (fill included) stay within `budget` and it spans at most gmax levels. Fat levels (throughput-
+// bound already) stay alone; runs of thin ones (launch-bound) are merged deeply.
 template <class Deps, class InTail>
-void build_merged(int n, int g, const std::vector<std::vector<int>>& levels, Deps deps, InTail in_tail,
-                  MergeHost& h) {
+void build_merged(int n, long budget, int gmax, const std::vector<std::vector<int>>& levels, Deps deps,
+                  InTail in_tail, MergeHost& h) {
   const int L = (int)levels.size();
   std::vector<int> pos_of(n, -1), grp(n, -1);
   int P = 0;
   for (int l = 0; l < L; ++l)
-    for (int r : levels[l]) { pos_of[r] = P++; grp[r] = l / g; }
-  std::vector<std::vector<int>> by_off(std::max(1, std::min(g, L)));
+    for (int r : levels[l]) pos_of[r] = P++;
+  std::vector<std::vector<int>> by_off(std::max(1, gmax));
   std::vector<int> keypos(2 * (size_t)n, -1);   // list position of a key (X entry: j; IN entry: n + j)
   std::vector<int> keys, lmap, perm;
   struct Op { int a, slot, map; };
   std::vector<Op> ops;
+  int G = 0, l0 = 0;   // current merged level and its first level
+  long gent = 0;       // entries of the current merged level
   for (int l = 0; l < L; ++l) {
-    if (l > 0 && l % g == 0) h.lptr.push_back((int)h.rows.size());
-    for (int i : levels[l]) {
-      keys.clear();
-      lmap.clear();
-      ops.clear();
-      auto add = [&](int key) {
-        if (keypos[key] < 0) { keypos[key] = (int)keys.size(); keys.push_back(key); }
-        return keypos[key];
-      };
-      add(n + i);   // the row's own input: list position 0 after the IN-first reorder below
-      deps(i, [&](int j, int slot) {
-        if (in_tail(j) && grp[j] == grp[i]) {   // substitute j's expression
-          const int pj = pos_of[j];
-          ops.push_back(Op{pj, slot, (int)lmap.size()});
-          for (int e = h.eoff[pj]; e < h.eoff[pj + 1]; ++e)
-            lmap.push_back(add(e < h.xoff[pj] ? n + h.eidx[e] : h.eidx[e]));
-        } else {
-          ops.push_back(Op{add(j), slot, -1});
+    for (int attempt = 0; attempt < 2; ++attempt) {
+      const size_t c_rows = h.rows.size(), c_eidx = h.eidx.size(), c_ops = h.op_a.size(), c_map = h.map.size();
+      for (int r : levels[l]) grp[r] = G;
+      for (int i : levels[l]) {
+        keys.clear();
+        lmap.clear();
+        ops.clear();
+        auto add = [&](int key) {
+          if (keypos[key] < 0) { keypos[key] = (int)keys.size(); keys.push_back(key); }
+          return keypos[key];
+        };
+        add(n + i);   // the row's own input: list position 0 after the IN-first reorder below
+        deps(i, [&](int j, int slot) {
+          if (in_tail(j) && grp[j] == G) {   // substitute j's expression
+            const int pj = pos_of[j];
+            ops.push_back(Op{pj, slot, (int)lmap.size()});
+            for (int e = h.eoff[pj]; e < h.eoff[pj + 1]; ++e)
+              lmap.push_back(add(e < h.xoff[pj] ? n + h.eidx[e] : h.eidx[e]));
+          } else {
+            ops.push_back(Op{add(j), slot, -1});
+          }
+        });
+        // final layout: IN entries first, then X entries (insertion order within each)
+        int nin = 0;
+        for (int k : keys) nin += k >= n;
+        perm.resize(keys.size());
+        int a = 0, b = nin;
+        for (size_t q = 0; q < keys.size(); ++q) perm[q] = keys[q] >= n ? a++ : b++;
+        const int base = (int)h.eidx.size();
+        h.rows.push_back(i);
+        h.eidx.resize(base + keys.size());
+        for (size_t q = 0; q < keys.size(); ++q) h.eidx[base + perm[q]] = keys[q] >= n ? keys[q] - n : keys[q];
+        h.xoff.push_back(base + nin);
+        h.eoff.push_back(base + (int)keys.size());
+        for (const Op& o : ops) {
+          h.op_slot.push_back(o.slot);
+          if (o.map < 0) {
+            h.op_a.push_back(perm[o.a]);
+            h.op_map.push_back(-1);
+          } else {
+            h.op_a.push_back(o.a);
+            h.op_map.push_back((int)h.map.size());
+            const int lj = h.eoff[o.a + 1] - h.eoff[o.a];
+            for (int q = 0; q < lj; ++q) h.map.push_back(perm[lmap[o.map + q]]);
+          }
         }
-      });
-      // final layout: IN entries first, then X entries (insertion order within each)
-      int nin = 0;
-      for (int k : keys) nin += k >= n;
-      perm.resize(keys.size());
-      int a = 0, b = nin;
-      for (size_t q = 0; q < keys.size(); ++q) perm[q] = keys[q] >= n ? a++ : b++;
-      const int base = (int)h.eidx.size();
-      h.rows.push_back(i);
-      h.eidx.resize(base + keys.size());
-      for (size_t q = 0; q < keys.size(); ++q) h.eidx[base + perm[q]] = keys[q] >= n ? keys[q] - n : keys[q];
-      h.xoff.push_back(base + nin);
-      h.eoff.push_back(base + (int)keys.size());
-      for (const Op& o : ops) {
-        h.op_slot.push_back(o.slot);
-        if (o.map < 0) {
-          h.op_a.push_back(perm[o.a]);
-          h.op_map.push_back(-1);
-        } else {
-          h.op_a.push_back(o.a);
-          h.op_map.push_back((int)h.map.size());
-          const int lj = h.eoff[o.a + 1] - h.eoff[o.a];
-          for (int q = 0; q < lj; ++q) h.map.push_back(perm[lmap[o.map + q]]);
-        }
+        h.opoff.push_back((int)h.op_a.size());
+        for (int k : keys) keypos[k] = -1;
       }
-      h.opoff.push_back((int)h.op_a.size());
-      by_off[l % g].push_back(pos_of[i]);
-      for (int k : keys) keypos[k] = -1;
+      const long lent = (long)(h.eidx.size() - c_eidx);
+      if (l > l0 && (gent + lent > budget || l - l0 >= gmax) && attempt == 0) {
+        // over budget: undo this level and start a new merged level with it
+        h.rows.resize(c_rows);
+        h.eoff.resize(c_rows + 1);
+        h.xoff.resize(c_rows);
+        h.eidx.resize(c_eidx);
+        h.opoff.resize(c_rows + 1);
+        h.op_a.resize(c_ops);
+        h.op_slot.resize(c_ops);
+        h.op_map.resize(c_ops);
+        h.map.resize(c_map);
+        h.lptr.push_back((int)h.rows.size());
+        ++G;
+        l0 = l;
+        gent = 0;
+        continue;
+      }
+      gent += lent;
+      for (int r : levels[l]) by_off[l - l0].push_back(pos_of[r]);
+      break;
     }
   }
   h.lptr.push_back((int)h.rows.size());
@@ -157,21 +185,30 @@ void VaduPrecond::Build(const int* nbr, const std::vector<int>& vo, const std::v
       groups_b[lb[p]].push_back(p);
       groups_f[lt[p]].push_back(p);
     }
-  // merged tail levels (g levels per launch; GPBOOST_AMD_TAIL_MERGE, 1 = the plain level schedule)
-  int g = 4;
+  // merged tail levels: at most g levels per launch (GPBOOST_AMD_TAIL_MERGE, 1 = the plain level
+  // schedule) and at most `budget` entries per launch (GPBOOST_AMD_TAIL_BUDGET)
+  // (n = 100k, m = 30, t = 51, per application: g = 1 1.10 ms, g = 2 0.83, g = 3 0.79, g = 4 0.82,
+  // g = 8 1.05; g <= 16 with 150k entries 0.78 — beyond ~3 levels the fill's gather bytes, not the
+  // launches, set the time)
+  int g = 16;
   if (const char* e = std::getenv("GPBOOST_AMD_TAIL_MERGE")) {
     g = std::atoi(e);
     if (g < 1 || g > 64) Fatal("GPBOOST_AMD_TAIL_MERGE must be 1..64 (got '%s')", e);
+  }
+  long budget = 150000;
+  if (const char* e = std::getenv("GPBOOST_AMD_TAIL_BUDGET")) {
+    budget = std::atol(e);
+    if (budget < 1) Fatal("GPBOOST_AMD_TAIL_BUDGET must be >= 1 (got '%s')", e);
   }
   merge_g_ = g;
   {
     MergeHost mb, ml;
     auto tail = [&](int j) { return part(j) == 2; };
     build_merged(
-        n, g, groups_b, [&](int j, auto f) { for (int e = tptr[j]; e < tptr[j + 1]; ++e) f(trow[e], tslot[e]); }, tail,
+        n, budget, g, groups_b, [&](int j, auto f) { for (int e = tptr[j]; e < tptr[j + 1]; ++e) f(trow[e], tslot[e]); }, tail,
         mb);
     build_merged(
-        n, g, groups_f, [&](int i, auto f) { for (int r = 0; r < kk(i); ++r) f(nbr[(size_t)i * m + r], i * m + r); },
+        n, budget, g, groups_f, [&](int i, auto f) { for (int r = 0; r < kk(i); ++r) f(nbr[(size_t)i * m + r], i * m + r); },
         tail, ml);
     std::vector<int> mint;
     MergeHost* hs[2] = {&mb, &ml};

@@ -7,7 +7,7 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"
 O=gpurun_out
 mkdir -p $O/prof
-TAG="${TAG:-r01}"
+TAG="${TAG:-r02}"
 step() { echo "== $* $(date +%T)" >> $O/round.log; }
 : > $O/round.log
 step smoke
@@ -23,8 +23,10 @@ timeout -k 10 600 python -u bench.py ${BENCH_ARGS} > $O/bench_${TAG}.json 2> $O/
 step latent
 GPBOOST_AMD_TIMING=1 timeout -k 10 600 python -u scripts/time_latent.py > $O/latent_time.log 2>&1 || { echo "latent rc=$?" >> $O/round.log; exit 1; }
 step rocprof
-( cd /tmp && export TMPDIR=/tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
+# eager launches under the profiler: its tracer does not survive hipGraph replay on this image
+( cd /tmp && export TMPDIR=/tmp && GPBOOST_AMD_NO_GRAPH=1 timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv \
     -d "$R/$O/prof/${TAG}" -o run -- python3 "$R/bench.py" --steps 20 --warmup 3 --no-cpu-baseline ${BENCH_ARGS} \
     > "$R/$O/prof_${TAG}.log" 2>&1 ) || { echo "rocprof rc=$?" >> $O/round.log; exit 1; }
+find "$O/prof/${TAG}" -name "*kernel_trace.csv" -size +32M -delete
 step done
 exit $rc

@@ -1,5 +1,6 @@
 """A/B of the VADU preconditioner plan split (vadu_precond.h) on the latent Vecchia path at
-n = 100k: per plan "K0:K[:g]" (dense head rows : head rows incl. the dense ones : tail levels merged per launch) one warm-up and
+n = 100k: per plan "K0:K[:g[:budget]]" (dense head rows : head rows incl. the dense ones : at most g tail levels and
+`budget` entries per launch; empty = default) one warm-up and
 two timed nll+grad evaluations, the preconditioner's per-application time (t = 51 and t = 1,
 GPB_BenchLatentOperators, with the per-step split when GPBOOST_AMD_PRECOND_SPLIT is set), and
 the results (they must agree across plans to rounding)."""
@@ -19,10 +20,12 @@ X = synthetic.bench_coords(n)
 for lik in liks:
     y = synthetic.bench_gaussian_y(n) if lik == "gaussian" else synthetic.bench_bernoulli_y(X)
     for plan in plans:
-        k0, k, g = (plan.split(":") + ["4"])[:3]
-        os.environ["GPBOOST_AMD_DENSE_ROWS"] = k0
-        os.environ["GPBOOST_AMD_HEAD_ROWS"] = k
-        os.environ["GPBOOST_AMD_TAIL_MERGE"] = g
+        k0, k, g, budget = (plan.split(":") + ["", "", "", ""])[:4]
+        for name, v in (("DENSE_ROWS", k0), ("HEAD_ROWS", k), ("TAIL_MERGE", g), ("TAIL_BUDGET", budget)):
+            if v:
+                os.environ["GPBOOST_AMD_" + name] = v
+            else:
+                os.environ.pop("GPBOOST_AMD_" + name, None)
         gm = GPModel(gp_coords=X, likelihood=lik, cov_function="exponential",
                      gp_approx="vecchia_latent" if lik == "gaussian" else "vecchia", num_neighbors=30,
                      vecchia_ordering="random", seed=0, matrix_inversion_method="iterative")

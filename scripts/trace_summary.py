@@ -25,13 +25,13 @@ gap_after = defaultdict(lambda: [0, 0])
 for s, e, k in ev:
     busy += e - max(s, last_end) if e > last_end else 0
     last_end = max(last_end, e)
-    name = k.split("(")[0].replace("void ", "")[:80]
+    name = k.replace("gpb_amd::", "").replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:80]
     tot[name][0] += 1
     tot[name][1] += e - s
 for i in range(len(ev) - 1):
     g = ev[i + 1][0] - ev[i][1]
     if g > 0:
-        n2 = ev[i + 1][2].split("(")[0].replace("void ", "")[:60]
+        n2 = ev[i + 1][2].replace("gpb_amd::", "").replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0][:60]
         gap_after[n2][0] += 1
         gap_after[n2][1] += g
 with open(out, "w") as f:
