@@ -348,11 +348,11 @@ int GPB_SetDistributed(REModelHandle handle, int rank, int world_size, const cha
   API_BEGIN();
   ncclUniqueId id;
   std::memset(&id, 0, sizeof(id));
-  if (world_size > 1) {
-    if (comm_id == nullptr) gpb_amd::Fatal("comm_id is NULL");
-    std::memcpy(&id, comm_id, sizeof(id));
-  }
-  model(handle)->SetDistributed(rank, world_size, id);
+  if (world_size > 1 && comm_id == nullptr) gpb_amd::Fatal("comm_id is NULL");
+  if (comm_id != nullptr) std::memcpy(&id, comm_id, sizeof(id));
+  // a given id joins an RCCL communicator even at world_size 1 (one-rank communicator: the same
+  // in-library all-reduce path, which the single-GPU tests exercise)
+  model(handle)->SetDistributed(rank, world_size, id, comm_id != nullptr);
   API_END();
 }
 

@@ -133,12 +133,15 @@ struct PartialList {
   const int* eidx;    // storage row of the dependency
   const double* eval;
 };
+// compact (nullable): list rows w < ncompact are also stored at compact[w * t + c].
 void launch_vadu_partial(const PartialList& p, const double* in, const double* dw, const double* src, double* out,
-                         int t, hipStream_t s);
+                         int t, hipStream_t s, double* compact = nullptr, int ncompact = 0);
 // Dense head block (vadu_dense.hip), K0 x K0 column-major with leading dimension ld (K0 rounded
 // up to 64, identity padding): per factor Bd = B_00, G = Bd^-1 and GT = G^T (T: ld x (ld/2 + 64)
-// scratch); per application S = diag(1/dw_0) G^T X[rows] (S: compact ld x t scratch), then
-// Y[rows] = G S (row-major t-column blocks, head-0 rows reached through DenseHead::row).
+// scratch); per application, with X the head-0 rows of the B^T solve's result in Vecchia order
+// (compact row-major K0 x t, written by the last partial sum that touches them), S = diag(1/dw_0)
+// G^T X (S: 2 ld x t scratch, X may be its first half), then Y[rows] = G S (Y: the storage-order
+// t-column block, head-0 rows reached through DenseHead::row).
 struct DenseHead {
   int K0, ld, m;
   const int* row;      // K0: storage row of Vecchia row v < K0

@@ -163,7 +163,7 @@ void REModelAMD::BuildVecchiaStructure() {
   d_block_sums_.alloc((size_t)std::max(nblocks, 1) * kVecchiaSums);
 }
 
-void REModelAMD::SetDistributed(int rank, int world, const ncclUniqueId& id) {
+void REModelAMD::SetDistributed(int rank, int world, const ncclUniqueId& id, bool use_comm) {
   if (world < 1 || rank < 0 || rank >= world) Fatal("invalid rank %d / world_size %d", rank, world);
   UseDevice();
   rank_ = rank;
@@ -171,7 +171,7 @@ void REModelAMD::SetDistributed(int rank, int world, const ncclUniqueId& id) {
   if (!vecchia_ && world > 1) Fatal("the dense (gp_approx='none') path runs as replicas only; SetDistributed needs gp_approx='vecchia'");
   if (cfg_.latent && world > 1) Fatal("the latent Vecchia (iterative) path runs as replicas only in this build");
   if (comm_) { ncclCommDestroy(comm_); comm_ = nullptr; }
-  if (world > 1) {
+  if (world > 1 || use_comm) {
     ncclResult_t r = ncclCommInitRank(&comm_, world, id, rank);
     if (r != ncclSuccess) Fatal("ncclCommInitRank failed: %s", ncclGetErrorString(r));
   }
@@ -233,7 +233,7 @@ void REModelAMD::LaunchVecchiaRows(const double* trafo, int r0, int r1, double* 
   HIP_CHECK(hipEventRecord(ev_[0], stream_));
   launch_vecchia_rows(cfg_.cov_type, a, stream_);
   HIP_CHECK(hipEventRecord(ev_[1], stream_));
-  if (allreduce && world_ > 1) {
+  if (allreduce && comm_ != nullptr) {
     launch_sum_blocks(d_block_sums_.get(), nblocks, kVecchiaSums, d_sums_.get(), stream_);
     ncclResult_t r = ncclAllReduce(d_sums_.get(), d_sums_.get(), kVecchiaSums, ncclDouble, ncclSum, comm_, stream_);
     if (r != ncclSuccess) Fatal("ncclAllReduce failed: %s", ncclGetErrorString(r));

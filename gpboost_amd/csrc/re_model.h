@@ -64,7 +64,7 @@ class REModelAMD {
   // Latent models: gradient wrt log(cov_pars) (+ log(aux_pars) when estimate_aux_pars).
   EvalResult Eval(const double* cov_pars_orig, bool want_grad, int profile);
 
-  void SetDistributed(int rank, int world, const ncclUniqueId& id);
+  void SetDistributed(int rank, int world, const ncclUniqueId& id, bool use_comm);
 
   // Partial sums over rows [r0, r1) of this model's row block, no all-reduce (EXTENSION API).
   void EvalVecchiaPartials(const double* cov_pars_orig, int r0, int r1, double* sums);

@@ -88,13 +88,29 @@ __global__ void __launch_bounds__(256) transpose_kernel(int ld, const double* __
   }
 }
 
-// One triangular block product over the head-0 rows, t columns:
-//   UPPER (A = G^T, upper): Y[i] = (sum_{k >= i} A(i, k) X[row[k]]) / dw[row[i]],  Y compact (row i)
-//   !UPPER (A = G, lower):  Z[row[i]] = sum_{k <= i} A(i, k) X[k],                X compact
+// One triangular block product over the head-0 rows, t columns, compact row-major operands:
+//   UPPER (A = G^T, upper): Y[i] = (sum_{k >= i} A(i, k) X[k]) / dw[row[i]]
+//   !UPPER (A = G, lower):  Y[row[i]] = sum_{k <= i} A(i, k) X[k]   (scattered to the storage rows)
 // Workgroup = 16 output rows x 32 columns (two 16 x 16 f64 MFMA tiles); the tile's k range (the
-// structural zeros skipped) is split over 8 waves in whole trips of 8, ascending k, and the
-// partial tiles are combined through LDS in a fixed wave order (bitwise repeatable).
+// structural zeros skipped) is split over 8 waves in whole trips of 8, ascending k, loads of the
+// next trip issued before the current trip's MFMAs; the partial tiles are combined through LDS
+// in a fixed wave order (bitwise repeatable).
 constexpr int kApplyWaves = 8;
+struct ApplyTrip {
+  double a[2], b0[2], b1[2];
+};
+__device__ __forceinline__ void apply_load(const double* __restrict__ A, const double* __restrict__ X, int ld, int t,
+                                           int ai, int kl, int cA, int cB, bool okA, bool okB, int k, int ke,
+                                           ApplyTrip& tr) {
+#pragma unroll
+  for (int u = 0; u < 2; ++u) {
+    const int kk = k + 4 * u + kl;
+    const bool ok = kk < ke;
+    tr.a[u] = ok ? A[(size_t)ai + (size_t)kk * ld] : 0.;
+    tr.b0[u] = (ok && okA) ? X[(size_t)kk * t + cA] : 0.;
+    tr.b1[u] = (ok && okB) ? X[(size_t)kk * t + cB] : 0.;
+  }
+}
 template <bool UPPER>
 __global__ void __launch_bounds__(kApplyWaves * 64) dense_head_apply_kernel(DenseHead d, const double* __restrict__ A,
                                                                             const double* __restrict__ dw,
@@ -114,26 +130,16 @@ __global__ void __launch_bounds__(kApplyWaves * 64) dense_head_apply_kernel(Dens
   const int cA = c0 + (lane & 15), cB = cA + 16;
   const bool okA = cA < t, okB = cB < t;
   double4_t acc0 = {0., 0., 0., 0.}, acc1 = {0., 0., 0., 0.};
-  for (int k = kb; k < ke; k += 8) {   // two k-steps per trip: all loads issued first
-    int xr[2];
+  ApplyTrip cur, nxt;
+  if (kb < ke) apply_load(A, X, ld, t, ai, kl, cA, cB, okA, okB, kb, ke, cur);
+  for (int k = kb; k < ke; k += 8) {
+    if (k + 8 < ke) apply_load(A, X, ld, t, ai, kl, cA, cB, okA, okB, k + 8, ke, nxt);
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
-      const int kk = k + 4 * u + kl;
-      xr[u] = kk < ke ? (UPPER ? d.row[kk] : kk) : -1;
+      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(cur.a[u], cur.b0[u], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(cur.a[u], cur.b1[u], acc1, 0, 0, 0);
     }
-    double a[2], b0[2], b1[2];
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      const int kk = k + 4 * u + kl;
-      a[u] = xr[u] >= 0 ? A[(size_t)ai + (size_t)kk * ld] : 0.;
-      b0[u] = (xr[u] >= 0 && okA) ? X[(size_t)xr[u] * t + cA] : 0.;
-      b1[u] = (xr[u] >= 0 && okB) ? X[(size_t)xr[u] * t + cB] : 0.;
-    }
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b0[u], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u], b1[u], acc1, 0, 0, 0);
-    }
+    cur = nxt;
   }
 #pragma unroll
   for (int rg = 0; rg < 4; ++rg) {
@@ -191,8 +197,10 @@ void launch_dense_head_apply(const DenseHead& d, const double* G, const double* 
                              double* S, double* Y, int t, hipStream_t s) {
   if (d.K0 <= 0 || t <= 0) return;
   const dim3 grid(d.ld / 16, (t + 31) / 32);
-  hipLaunchKernelGGL((dense_head_apply_kernel<true>), grid, dim3(kApplyWaves * 64), 0, s, d, GT, dw, X, S, t);
-  hipLaunchKernelGGL((dense_head_apply_kernel<false>), grid, dim3(kApplyWaves * 64), 0, s, d, G, dw, S, Y, t);
+  hipLaunchKernelGGL((dense_head_apply_kernel<true>), grid, dim3(kApplyWaves * 64), 0, s, d, GT, dw, X, S + (size_t)d.ld * t,
+                     t);
+  hipLaunchKernelGGL((dense_head_apply_kernel<false>), grid, dim3(kApplyWaves * 64), 0, s, d, G, dw,
+                     S + (size_t)d.ld * t, Y, t);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -174,7 +174,7 @@ __global__ void __launch_bounds__(kHeadThreads) vadu_head_kernel(HeadSolve h, in
 // coalesced load and v_readlane broadcasts; t = 1: 16 lanes per row over its entries.
 __global__ void __launch_bounds__(256) vadu_partial_kernel(PartialList p, const double* in,
                                                            const double* __restrict__ dw, const double* src,
-                                                           double* out, int t) {
+                                                           double* out, int t, double* compact, int ncompact) {
   const int lane = threadIdx.x & 63;
   const int w = blockIdx.x * 4 + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (w >= p.rows) return;
@@ -193,12 +193,15 @@ __global__ void __launch_bounds__(256) vadu_partial_kernel(PartialList p, const 
     const int cnt = e1 - b0 < 64 ? e1 - b0 : 64;
     acc = wave_dot<16>(my_id, my_w, cnt, src, t, cc, j, acc);
   }
-  if (c < t) out[(size_t)j * t + c] = x - acc;
+  if (c < t) {
+    out[(size_t)j * t + c] = x - acc;
+    if (w < ncompact) compact[(size_t)w * t + c] = x - acc;
+  }
 }
 
 __global__ void __launch_bounds__(256) vadu_partial1_kernel(PartialList p, const double* in,
                                                             const double* __restrict__ dw, const double* src,
-                                                            double* out) {
+                                                            double* out, double* compact, int ncompact) {
   const int g = blockIdx.x * 16 + (threadIdx.x >> 4), gl = threadIdx.x & 15;
   if (g >= p.rows) return;   // whole 16-lane groups exit together
   const int j = p.row[g];
@@ -209,6 +212,7 @@ __global__ void __launch_bounds__(256) vadu_partial1_kernel(PartialList p, const
     double x = in ? in[j] : out[j];
     if (dw) x /= dw[j];
     out[j] = x - acc;
+    if (g < ncompact) compact[g] = x - acc;
   }
 }
 
@@ -222,13 +226,15 @@ void launch_vadu_head(const HeadSolve& h, const double* in, const double* dw, do
 }
 
 void launch_vadu_partial(const PartialList& p, const double* in, const double* dw, const double* src, double* out,
-                         int t, hipStream_t s) {
+                         int t, hipStream_t s, double* compact, int ncompact) {
   if (p.rows <= 0 || t <= 0) return;
+  if (!compact) ncompact = 0;
   if (t == 1)
-    hipLaunchKernelGGL(vadu_partial1_kernel, dim3((p.rows + 15) / 16), dim3(256), 0, s, p, in, dw, src, out);
+    hipLaunchKernelGGL(vadu_partial1_kernel, dim3((p.rows + 15) / 16), dim3(256), 0, s, p, in, dw, src, out, compact,
+                       ncompact);
   else
     hipLaunchKernelGGL(vadu_partial_kernel, dim3((p.rows + 3) / 4, (t + 63) / 64), dim3(256), 0, s, p, in, dw, src,
-                       out, t);
+                       out, t, compact, ncompact);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -466,9 +466,10 @@ void VaduPrecond::SetDiag(const double* dw) {
   dw_ = dw;
 }
 
-void VaduPrecond::DenseApply(const double* Xt, double* Z, int t) {
-  // S_ holds >= ld0_ * t doubles: sized by Apply / TimeParts before any capture
-  launch_dense_head_apply(dh_, G_.get(), GT_.get(), dw_, Xt, S_.get(), Z, t, s_);
+void VaduPrecond::DenseApply(const double* X0, double* Z, int t) {
+  // S_ holds >= 2 ld0_ t doubles (the compact head-0 block, then the scaled G^T product): sized by
+  // Apply / TimeParts before any capture
+  launch_dense_head_apply(dh_, G_.get(), GT_.get(), dw_, X0, S_.get(), Z, t, s_);
 }
 
 void VaduPrecond::TailSolve(bool lower, const double* R, double* Xt, double* Z, int t) {
@@ -480,11 +481,13 @@ void VaduPrecond::TailSolve(bool lower, const double* R, double* Xt, double* Z, 
 void VaduPrecond::Record(const double* R, double* Z, double* Xt, int t) {
   const bool seg = K_ > K0_;
   TailSolve(false, R, Xt, Z, t);
-  if (K_ > 0) launch_vadu_partial(p_th_, R, nullptr, Xt, Xt, t, s_);
+  // the last partial sum over the head-0 rows also stores them compactly for the dense products
+  double* x0 = K0_ > 0 ? S_.get() : nullptr;
+  if (K_ > 0) launch_vadu_partial(p_th_, R, nullptr, Xt, Xt, t, s_, seg ? nullptr : x0, K0_);
   if (seg) launch_vadu_head(seg_bt_, Xt, nullptr, Xt, t, s_);
   if (K0_ > 0) {
-    if (seg) launch_vadu_partial(p_10_, nullptr, nullptr, Xt, Xt, t, s_);
-    DenseApply(Xt, Z, t);
+    if (seg) launch_vadu_partial(p_10_, nullptr, nullptr, Xt, Xt, t, s_, x0, K0_);
+    DenseApply(x0, Z, t);
   }
   if (seg) {
     if (K0_ > 0) {
@@ -499,9 +502,9 @@ void VaduPrecond::Record(const double* R, double* Z, double* Xt, int t) {
 
 void VaduPrecond::Apply(const double* R, double* Z, double* Xt, int t) {
   if (!dw_) Fatal("VADU preconditioner applied before SetDiag");
-  if (K0_ > 0 && S_.size() < (size_t)ld0_ * t) {   // dense-head scratch sized before any capture
+  if (K0_ > 0 && S_.size() < (size_t)2 * ld0_ * t) {   // dense-head scratch sized before any capture
     DropGraphs();
-    S_.alloc((size_t)ld0_ * t);
+    S_.alloc((size_t)2 * ld0_ * t);
   }
   if (!use_graph_) {
     Record(R, Z, Xt, t);
@@ -525,9 +528,9 @@ void VaduPrecond::Apply(const double* R, double* Z, double* Xt, int t) {
 }
 
 void VaduPrecond::TimeParts(const double* R, double* Z, double* Xt, int t, int reps) {
-  if (K0_ > 0 && S_.size() < (size_t)ld0_ * t) {
+  if (K0_ > 0 && S_.size() < (size_t)2 * ld0_ * t) {
     DropGraphs();
-    S_.alloc((size_t)ld0_ * t);
+    S_.alloc((size_t)2 * ld0_ * t);
   }
   hipEvent_t a, b;
   HIP_CHECK(hipEventCreate(&a));
@@ -543,10 +546,10 @@ void VaduPrecond::TimeParts(const double* R, double* Z, double* Xt, int t, int r
     std::fprintf(stderr, "[precond parts t=%d] %-11s %.4f ms\n", t, name, ms / reps);
   };
   part("tail_bt", [&] { TailSolve(false, R, Xt, Z, t); });
-  part("part_th", [&] { launch_vadu_partial(p_th_, R, nullptr, Xt, Xt, t, s_); });
+  part("part_th", [&] { launch_vadu_partial(p_th_, R, nullptr, Xt, Xt, t, s_, seg ? nullptr : S_.get(), K0_); });
   if (seg) part("seg_bt", [&] { launch_vadu_head(seg_bt_, Xt, nullptr, Xt, t, s_); });
-  if (K0_ > 0 && seg) part("part_10", [&] { launch_vadu_partial(p_10_, nullptr, nullptr, Xt, Xt, t, s_); });
-  if (K0_ > 0) part("dense", [&] { DenseApply(Xt, Z, t); });
+  if (K0_ > 0 && seg) part("part_10", [&] { launch_vadu_partial(p_10_, nullptr, nullptr, Xt, Xt, t, s_, S_.get(), K0_); });
+  if (K0_ > 0) part("dense", [&] { DenseApply(S_.get(), Z, t); });
   if (K0_ > 0 && seg) part("part_01", [&] { launch_vadu_partial(p_01_, Xt, dw_, Z, Z, t, s_); });
   if (seg) part("seg_low", [&] { launch_vadu_head(seg_low_, Z, nullptr, Z, t, s_); });
   part("tail_low", [&] { TailSolve(true, R, Xt, Z, t); });

@@ -70,7 +70,7 @@ class VaduPrecond {
  private:
   void Record(const double* R, double* Z, double* Xt, int t);
   void TailSolve(bool lower, const double* R, double* Xt, double* Z, int t);
-  void DenseApply(const double* Xt, double* Z, int t);
+  void DenseApply(const double* X0, double* Z, int t);
 
   int n_, m_;
   hipStream_t s_;

@@ -226,7 +226,9 @@ GPBOOST_AMD_EXPORT int GPB_CommCreateId(char* id_out);
 /* Join the model to an RCCL communicator: rows (observations in Vecchia order) are
  * split into world_size contiguous blocks; this rank evaluates block `rank` and the
  * per-rank partial sums are all-reduced over RCCL (one all-reduce of 6 doubles per
- * evaluation). Must be called before the first evaluation. */
+ * evaluation). Must be called before the first evaluation. comm_id may be NULL only at
+ * world_size 1 (no communicator); a non-NULL id at world_size 1 creates a one-rank
+ * communicator (same data path). */
 GPBOOST_AMD_EXPORT int GPB_SetDistributed(REModelHandle handle, int rank, int world_size, const char* comm_id);
 /* The six per-row partial sums over Vecchia rows [row_begin, row_end) at cov_pars (original
  * scale), without any all-reduce: for callers that run their own communication. The

@@ -194,6 +194,26 @@ def test_row_block_partials_sum_to_whole():
         np.testing.assert_allclose(g_w, g, rtol=1e-9)
 
 
+def test_rccl_one_rank_communicator_matches():
+    """The in-library RCCL data path of `bench.py --gpus N` (ncclCommInitRank + one ncclAllReduce of
+    the six partial sums per evaluation on the model's stream), run as a one-rank communicator on the
+    single test GPU: identical nll and gradient to the plain single-GPU evaluation (a one-rank sum is
+    a copy)."""
+    from gpboost_amd import comm_create_id, synthetic
+    n = 20000
+    X = synthetic.bench_coords(n)
+    Y = synthetic.bench_gaussian_y(n)
+    pars = [0.1, 1.0, 0.1]
+    plain = _model(X, 30)
+    a = plain.neg_log_likelihood_and_grad(pars, Y, profile_sigma2=True)
+    comm = _model(X, 30)
+    comm.set_distributed(0, 1, comm_create_id())
+    b = comm.neg_log_likelihood_and_grad(pars, Y, profile_sigma2=True)
+    c = comm.neg_log_likelihood_and_grad(pars, None, profile_sigma2=True)
+    assert a[0] == b[0] == c[0]
+    assert np.array_equal(a[1], b[1]) and np.array_equal(b[1], c[1])
+
+
 @pytest.mark.parametrize("m", [4, 10, 30])
 def test_gpu_neighbor_search_ties_bit_exact(m):
     """GPU neighbour search (vecchia_knn.hip) on integer-grid coordinates, where squared distances
