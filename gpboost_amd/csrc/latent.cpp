@@ -284,6 +284,40 @@ void LatentVecchia::BenchOperators(int t, int reps, double* out) {
   HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_));
   out[1] = ms / reps;
   if (std::getenv("GPBOOST_AMD_PRECOND_SPLIT")) pre_->TimeParts(b.R.get(), b.Z.get(), b.Xt.get(), t, reps);
+  if (std::getenv("GPBOOST_AMD_BENCH_2STREAM") && t >= 2) {   // diagnostics: two column groups, two streams
+    const int t0 = (t + 1) / 2, t1 = t - t0;
+    DevBuf<double> R0((size_t)n_ * t0), Z0((size_t)n_ * t0), X0((size_t)n_ * t0);
+    DevBuf<double> R1((size_t)n_ * t1), Z1((size_t)n_ * t1), X1((size_t)n_ * t1);
+    for (auto* buf : {&R0, &R1}) HIP_CHECK(hipMemsetAsync(buf->get(), 0, sizeof(double) * buf->size(), s_));
+    hipStream_t s2;
+    HIP_CHECK(hipStreamCreateWithFlags(&s2, hipStreamNonBlocking));
+    hipEvent_t e_fork, e_join;
+    HIP_CHECK(hipEventCreateWithFlags(&e_fork, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&e_join, hipEventDisableTiming));
+    pre_->Apply(R0.get(), Z0.get(), X0.get(), t0, s_, 0);
+    pre_->Apply(R1.get(), Z1.get(), X1.get(), t1, s2, 1);
+    HIP_CHECK(hipStreamSynchronize(s2));
+    for (int mode = 0; mode < 2; ++mode) {
+      HIP_CHECK(hipEventRecord(ev0_, s_));
+      HIP_CHECK(hipEventRecord(e_fork, s_));
+      HIP_CHECK(hipStreamWaitEvent(s2, e_fork, 0));
+      for (int r = 0; r < reps; ++r) {
+        pre_->Apply(R0.get(), Z0.get(), X0.get(), t0, s_, 0);
+        pre_->Apply(R1.get(), Z1.get(), X1.get(), t1, mode ? s2 : s_, 1);
+      }
+      HIP_CHECK(hipEventRecord(e_join, s2));
+      HIP_CHECK(hipStreamWaitEvent(s_, e_join, 0));
+      HIP_CHECK(hipEventRecord(ev1_, s_));
+      HIP_CHECK(hipEventSynchronize(ev1_));
+      HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_));
+      std::fprintf(stderr, "[precond 2-group t=%d+%d] %s: %.4f ms per pair of applications\n", t0, t1,
+                   mode ? "two streams" : "one stream", ms / reps);
+    }
+    HIP_CHECK(hipEventDestroy(e_fork));
+    HIP_CHECK(hipEventDestroy(e_join));
+    HIP_CHECK(hipStreamDestroy(s2));
+    pre_->DropGraphs();
+  }
   out[2] = (double)tnnz_ + n_;
   out[3] = pre_->launches();
 }

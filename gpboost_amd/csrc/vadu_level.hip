@@ -81,7 +81,7 @@ __global__ void __launch_bounds__(256) merge_numeric_kernel(MergedSolve ms, cons
 
 // t >= 2: one workgroup per row; lane = column (coalesced t-wide gathers of a dependency's row),
 // wave w takes entries w, w + NW, ...; the NW partial sums meet in LDS in a fixed order.
-template <bool LOWER, int NW>
+template <bool LOWER, int NW, int B>
 __global__ void __launch_bounds__(NW * 64) merged_levelT_kernel(MergedSolve ms, int p0, const double* __restrict__ dw,
                                                                 const double* in, double* X, int t) {
   __shared__ double red[NW][64];
@@ -92,7 +92,6 @@ __global__ void __launch_bounds__(NW * 64) merged_levelT_kernel(MergedSolve ms, 
   const int p = p0 + xcd_block(blockIdx.x, gridDim.x);
   const int i = ms.rows[p];
   const int e0 = ms.eoff[p], ex = ms.xoff[p], e1 = ms.eoff[p + 1];
-  constexpr int B = 16;
   double acc = 0.;
   for (int e = e0 + wave; e < e1; e += NW * B) {
     int id[B];
@@ -193,8 +192,8 @@ const LevelShape& level_shape() {
     LevelShape k;
     if (const char* e = std::getenv("GPBOOST_AMD_LEVELT_NW")) {
       k.nw = std::atoi(e);
-      if (k.nw != 0 && k.nw != 1 && k.nw != 2 && k.nw != 4)
-        Fatal("GPBOOST_AMD_LEVELT_NW must be 0, 1, 2 or 4 (got '%s')", e);
+      if (k.nw != 0 && k.nw != 1 && k.nw != 2 && k.nw != 4 && k.nw != 8)
+        Fatal("GPBOOST_AMD_LEVELT_NW must be 0, 1, 2, 4 or 8 (got '%s')", e);
       Info("tail level kernels: %d wave(s) per row at t >= 2", k.nw);
     }
     if (const char* e = std::getenv("GPBOOST_AMD_LEVEL1_G")) {
@@ -225,9 +224,11 @@ void launch_level(const MergedSolve& ms, int p0, int cnt, const double* dw, cons
     return;
   }
   const dim3 g(cnt, (t + 63) / 64);
-  if (ks.nw == 1) hipLaunchKernelGGL((merged_levelT_kernel<LOWER, 1>), g, dim3(64), 0, s, ms, p0, dw, in, X, t);
-  else if (ks.nw == 2) hipLaunchKernelGGL((merged_levelT_kernel<LOWER, 2>), g, dim3(128), 0, s, ms, p0, dw, in, X, t);
-  else hipLaunchKernelGGL((merged_levelT_kernel<LOWER, 4>), g, dim3(256), 0, s, ms, p0, dw, in, X, t);
+  // entries in flight per row: NW waves x B gathers (64 for every shape)
+  if (ks.nw == 1) hipLaunchKernelGGL((merged_levelT_kernel<LOWER, 1, 64>), g, dim3(64), 0, s, ms, p0, dw, in, X, t);
+  else if (ks.nw == 2) hipLaunchKernelGGL((merged_levelT_kernel<LOWER, 2, 32>), g, dim3(128), 0, s, ms, p0, dw, in, X, t);
+  else if (ks.nw == 8) hipLaunchKernelGGL((merged_levelT_kernel<LOWER, 8, 8>), g, dim3(512), 0, s, ms, p0, dw, in, X, t);
+  else hipLaunchKernelGGL((merged_levelT_kernel<LOWER, 4, 16>), g, dim3(256), 0, s, ms, p0, dw, in, X, t);
 }
 
 }  // namespace

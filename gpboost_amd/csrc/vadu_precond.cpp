@@ -466,72 +466,75 @@ void VaduPrecond::SetDiag(const double* dw) {
   dw_ = dw;
 }
 
-void VaduPrecond::DenseApply(const double* X0, double* Z, int t) {
-  // S_ holds >= 2 ld0_ t doubles (the compact head-0 block, then the scaled G^T product): sized by
-  // Apply / TimeParts before any capture
-  launch_dense_head_apply(dh_, G_.get(), GT_.get(), dw_, X0, S_.get(), Z, t, s_);
+void VaduPrecond::DenseApply(const double* X0, double* Z, int t, hipStream_t st, double* S) {
+  // S holds >= 2 ld0_ t doubles (the compact head-0 block, then the scaled G^T product)
+  launch_dense_head_apply(dh_, G_.get(), GT_.get(), dw_, X0, S, Z, t, st);
 }
 
-void VaduPrecond::TailSolve(bool lower, const double* R, double* Xt, double* Z, int t) {
+void VaduPrecond::TailSolve(bool lower, const double* R, double* Xt, double* Z, int t, hipStream_t st) {
   const MergedSolve& ms = lower ? mt_low_ : mt_bt_;
   for (int L = 0; L + 1 < (int)ms.lptr.size(); ++L)
-    launch_merged_level(ms, L, lower, dw_, lower ? Xt : R, lower ? Z : Xt, t, s_);
+    launch_merged_level(ms, L, lower, dw_, lower ? Xt : R, lower ? Z : Xt, t, st);
 }
 
-void VaduPrecond::Record(const double* R, double* Z, double* Xt, int t) {
+void VaduPrecond::Record(const double* R, double* Z, double* Xt, int t, hipStream_t st, double* S) {
   const bool seg = K_ > K0_;
-  TailSolve(false, R, Xt, Z, t);
+  TailSolve(false, R, Xt, Z, t, st);
   // the last partial sum over the head-0 rows also stores them compactly for the dense products
-  double* x0 = K0_ > 0 ? S_.get() : nullptr;
-  if (K_ > 0) launch_vadu_partial(p_th_, R, nullptr, Xt, Xt, t, s_, seg ? nullptr : x0, K0_);
-  if (seg) launch_vadu_head(seg_bt_, Xt, nullptr, Xt, t, s_);
+  double* x0 = K0_ > 0 ? S : nullptr;
+  if (K_ > 0) launch_vadu_partial(p_th_, R, nullptr, Xt, Xt, t, st, seg ? nullptr : x0, K0_);
+  if (seg) launch_vadu_head(seg_bt_, Xt, nullptr, Xt, t, st);
   if (K0_ > 0) {
-    if (seg) launch_vadu_partial(p_10_, nullptr, nullptr, Xt, Xt, t, s_, x0, K0_);
-    DenseApply(x0, Z, t);
+    if (seg) launch_vadu_partial(p_10_, nullptr, nullptr, Xt, Xt, t, st, x0, K0_);
+    DenseApply(x0, Z, t, st, S);
   }
   if (seg) {
     if (K0_ > 0) {
-      launch_vadu_partial(p_01_, Xt, dw_, Z, Z, t, s_);
-      launch_vadu_head(seg_low_, Z, nullptr, Z, t, s_);
+      launch_vadu_partial(p_01_, Xt, dw_, Z, Z, t, st);
+      launch_vadu_head(seg_low_, Z, nullptr, Z, t, st);
     } else {
-      launch_vadu_head(seg_low_, Xt, dw_, Z, t, s_);
+      launch_vadu_head(seg_low_, Xt, dw_, Z, t, st);
     }
   }
-  TailSolve(true, R, Xt, Z, t);
+  TailSolve(true, R, Xt, Z, t, st);
 }
 
-void VaduPrecond::Apply(const double* R, double* Z, double* Xt, int t) {
-  if (!dw_) Fatal("VADU preconditioner applied before SetDiag");
-  if (K0_ > 0 && S_.size() < (size_t)2 * ld0_ * t) {   // dense-head scratch sized before any capture
+double* VaduPrecond::Scratch(int slot, int t) {
+  if (slot < 0 || slot >= kSlots) Fatal("VADU preconditioner scratch slot %d out of range", slot);
+  if (K0_ > 0 && S_[slot].size() < (size_t)2 * ld0_ * t) {   // sized before any capture that uses it
     DropGraphs();
-    S_.alloc((size_t)2 * ld0_ * t);
+    S_[slot].alloc((size_t)2 * ld0_ * t);
   }
+  return S_[slot].get();
+}
+
+void VaduPrecond::Apply(const double* R, double* Z, double* Xt, int t, hipStream_t st, int slot) {
+  if (!dw_) Fatal("VADU preconditioner applied before SetDiag");
+  if (!st) st = s_;
+  double* S = Scratch(slot, t);
   if (!use_graph_) {
-    Record(R, Z, Xt, t);
+    Record(R, Z, Xt, t, st, S);
     return;
   }
   for (const GraphEntry& g : graphs_) {
-    if (g.key[0] == R && g.key[1] == Z && g.key[2] == Xt && g.t == t) {
-      HIP_CHECK(hipGraphLaunch(g.exec, s_));
+    if (g.key[0] == R && g.key[1] == Z && g.key[2] == Xt && g.t == t && g.slot == slot) {
+      HIP_CHECK(hipGraphLaunch(g.exec, st));
       return;
     }
   }
   hipGraph_t graph;
-  HIP_CHECK(hipStreamBeginCapture(s_, hipStreamCaptureModeThreadLocal));
-  Record(R, Z, Xt, t);
-  HIP_CHECK(hipStreamEndCapture(s_, &graph));
-  GraphEntry e{{R, Z, Xt}, t, nullptr};
+  HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+  Record(R, Z, Xt, t, st, S);
+  HIP_CHECK(hipStreamEndCapture(st, &graph));
+  GraphEntry e{{R, Z, Xt}, t, slot, nullptr};
   HIP_CHECK(hipGraphInstantiate(&e.exec, graph, nullptr, nullptr, 0));
   HIP_CHECK(hipGraphDestroy(graph));
   graphs_.push_back(e);
-  HIP_CHECK(hipGraphLaunch(e.exec, s_));
+  HIP_CHECK(hipGraphLaunch(e.exec, st));
 }
 
 void VaduPrecond::TimeParts(const double* R, double* Z, double* Xt, int t, int reps) {
-  if (K0_ > 0 && S_.size() < (size_t)2 * ld0_ * t) {
-    DropGraphs();
-    S_.alloc((size_t)2 * ld0_ * t);
-  }
+  double* S = Scratch(0, t);
   hipEvent_t a, b;
   HIP_CHECK(hipEventCreate(&a));
   HIP_CHECK(hipEventCreate(&b));
@@ -545,14 +548,14 @@ void VaduPrecond::TimeParts(const double* R, double* Z, double* Xt, int t, int r
     HIP_CHECK(hipEventElapsedTime(&ms, a, b));
     std::fprintf(stderr, "[precond parts t=%d] %-11s %.4f ms\n", t, name, ms / reps);
   };
-  part("tail_bt", [&] { TailSolve(false, R, Xt, Z, t); });
-  part("part_th", [&] { launch_vadu_partial(p_th_, R, nullptr, Xt, Xt, t, s_, seg ? nullptr : S_.get(), K0_); });
+  part("tail_bt", [&] { TailSolve(false, R, Xt, Z, t, s_); });
+  part("part_th", [&] { launch_vadu_partial(p_th_, R, nullptr, Xt, Xt, t, s_, seg ? nullptr : S, K0_); });
   if (seg) part("seg_bt", [&] { launch_vadu_head(seg_bt_, Xt, nullptr, Xt, t, s_); });
-  if (K0_ > 0 && seg) part("part_10", [&] { launch_vadu_partial(p_10_, nullptr, nullptr, Xt, Xt, t, s_, S_.get(), K0_); });
-  if (K0_ > 0) part("dense", [&] { DenseApply(S_.get(), Z, t); });
+  if (K0_ > 0 && seg) part("part_10", [&] { launch_vadu_partial(p_10_, nullptr, nullptr, Xt, Xt, t, s_, S, K0_); });
+  if (K0_ > 0) part("dense", [&] { DenseApply(S, Z, t, s_, S); });
   if (K0_ > 0 && seg) part("part_01", [&] { launch_vadu_partial(p_01_, Xt, dw_, Z, Z, t, s_); });
   if (seg) part("seg_low", [&] { launch_vadu_head(seg_low_, Z, nullptr, Z, t, s_); });
-  part("tail_low", [&] { TailSolve(true, R, Xt, Z, t); });
+  part("tail_low", [&] { TailSolve(true, R, Xt, Z, t, s_); });
   std::fprintf(stderr,
                "[precond parts t=%d] K0=%d K=%d passes bt=%d low=%d tail merged levels bt=%d low=%d (g=%d, %ld entries) "
                "launches=%d\n",

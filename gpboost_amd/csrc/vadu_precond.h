@@ -55,7 +55,10 @@ class VaduPrecond {
   // Per system: dw = D^-1 + W (device, n). Must precede Apply; the pointer is captured.
   void SetDiag(const double* dw);
   // Z = P^-1 R for t columns (row-major n x t); Xt: n x t scratch (holds B^-T R afterwards).
-  void Apply(const double* R, double* Z, double* Xt, int t);
+  // stream: null = the model's; applications that may run concurrently (on different streams)
+  // use different scratch slots (< kSlots).
+  static constexpr int kSlots = 2;
+  void Apply(const double* R, double* Z, double* Xt, int t, hipStream_t stream = nullptr, int slot = 0);
   // Diagnostics: device time of each step (reps repetitions), printed to stderr.
   void TimeParts(const double* R, double* Z, double* Xt, int t, int reps);
   void DropGraphs();
@@ -68,9 +71,10 @@ class VaduPrecond {
   int launches() const;   // dependent launches per application
 
  private:
-  void Record(const double* R, double* Z, double* Xt, int t);
-  void TailSolve(bool lower, const double* R, double* Xt, double* Z, int t);
-  void DenseApply(const double* X0, double* Z, int t);
+  void Record(const double* R, double* Z, double* Xt, int t, hipStream_t st, double* S);
+  void TailSolve(bool lower, const double* R, double* Xt, double* Z, int t, hipStream_t st);
+  void DenseApply(const double* X0, double* Z, int t, hipStream_t st, double* S);
+  double* Scratch(int slot, int t);
 
   int n_, m_;
   hipStream_t s_;
@@ -87,10 +91,11 @@ class VaduPrecond {
   DevBuf<int> d_int_, d_slot_;
   DevBuf<double> d_val_;
   int nslot_ = 0;
-  DevBuf<double> Bd_, G_, GT_, T_, S_;
+  DevBuf<double> Bd_, G_, GT_, T_;
+  DevBuf<double> S_[kSlots];   // dense-head scratch per concurrent application
   struct GraphEntry {
     const void* key[3];
-    int t;
+    int t, slot;
     hipGraphExec_t exec;
   };
   std::vector<GraphEntry> graphs_;

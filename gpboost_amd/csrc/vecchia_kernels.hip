@@ -26,6 +26,7 @@
 // Optional outputs D^-1 and B(i, nbr) = -a are written for the factor API.
 #include <hip/hip_runtime.h>
 
+#include <cstdio>
 #include <cstdlib>
 
 #include "common.h"
@@ -80,7 +81,11 @@ __device__ __forceinline__ int packed(int r, int c) {  // r >= c
   return r * (r + 1) / 2 + c;
 }
 
-template <int K, int COV>
+// Diagnostics (GPBOOST_AMD_ROWS_PROF): per-phase s_memtime cycles of wave 0 of block 0, summed
+// over its row groups: [gather, pairs, gj, dca, reduce, iterations].
+__device__ unsigned long long g_rows_prof[8];
+
+template <int K, int COV, bool PROF = false>
 __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(VecchiaRowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int BT = block_threads<K>();
@@ -105,9 +110,20 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
   double* slot_a2 = slot_a1 + K;
 
   double acc[kVecchiaSums] = {0., 0., 0., 0., 0., 0.};
+  unsigned long long tp[6] = {0, 0, 0, 0, 0, 0}, t0 = 0;
+  const bool prof = PROF && blockIdx.x == 0 && threadIdx.x < 64;
+  auto mark = [&](int q) {
+    if (prof) {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+      tp[q] += t1 - t0;
+      t0 = t1;
+    }
+  };
 
   const int total_groups = a.r1 - a.r0;
   for (int gbase_row = blockIdx.x * rows_per_block; gbase_row < total_groups; gbase_row += gridDim.x * rows_per_block) {
+    if (prof) { t0 = __builtin_amdgcn_s_memtime(); ++tp[5]; }
     const int i = a.r0 + gbase_row + group_id;
     const bool active = i < a.r1;
     const int k = active ? min(i, a.m) : 0;
@@ -142,6 +158,7 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
     Cp[packed(r, r)] = rv ? cdiag : 1.;
     dCp[packed(r, r)] = 0.;
     wave_lds_sync();
+    mark(0);
 
     // ---- 1. pairs (rr > cc): lanes l and l + K/2 share the rows {l mod K/2, K-1-l mod K/2}
     {
@@ -165,6 +182,7 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
       }
     }
     wave_lds_sync();
+    mark(1);
 
     // ---- 2. symmetric Gauss-Jordan on [C | c | y_nbr], row r in registers
     double row[K];
@@ -202,6 +220,7 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
     const double vv_r = aug2 / mydiag;   // v = C^-1 y_nbr
 
     if (active && a.B_out != nullptr && r < a.m) a.B_out[(size_t)i * a.m + r] = rv ? -av_r : 0.;
+    mark(2);
 
     // ---- 3. t = dC a (dC from the packed image; its diagonal is 0)
     compiler_fence();
@@ -213,6 +232,7 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
       t = fma(dcrc, slot_c[c], t);
     }
     t = rv ? t : 0.;
+    mark(3);
 
     // ---- group reductions
     const double ac = group_sum<K>(av_r * cvec);
@@ -241,7 +261,10 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
       acc[4] += Dinv * dD_var;
       acc[5] += Dinv * dD_rng;
     }
+    mark(4);
   }
+  if (prof && threadIdx.x == 0)
+    for (int q = 0; q < 6; ++q) g_rows_prof[q] = tp[q];
   if (!want_like) return;
 
   // ---- block reduction of the per-group sums (fixed order -> deterministic)
@@ -552,7 +575,17 @@ void launch_k(const VecchiaRowsArgs& a, hipStream_t s) {
   }
   size_t lds = (size_t)rpb * group_lds_doubles<K>() * sizeof(double);
   if (lds < red) lds = red;
-  hipLaunchKernelGGL((vecchia_rows_kernel<K, COV>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
+  static const bool prof = std::getenv("GPBOOST_AMD_ROWS_PROF") != nullptr;
+  if (prof) {
+    hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, true>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
+    unsigned long long h[8];
+    HIP_CHECK(hipStreamSynchronize(s));
+    HIP_CHECK(hipMemcpyFromSymbol(h, HIP_SYMBOL(g_rows_prof), sizeof(h)));
+    std::fprintf(stderr, "[rows prof] K=%d blocks=%d iterations=%llu cycles: gather %llu pairs %llu gj %llu dca %llu reduce %llu\n",
+                 K, blocks, h[5], h[0], h[1], h[2], h[3], h[4]);
+  } else {
+    hipLaunchKernelGGL((vecchia_rows_kernel<K, COV>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
+  }
   HIP_CHECK(hipGetLastError());
 }
 
