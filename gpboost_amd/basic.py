@@ -14,7 +14,11 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libgpboost_amd.so")
+# GPBOOST_AMD_VARIANT=<name> selects an in-tree A/B build of the same sources
+# (gpboost_amd/lib/ab/libgpboost_amd_<name>.so, see build.py) for kernel experiments.
+_VARIANT = os.environ.get("GPBOOST_AMD_VARIANT", "")
+LIB_PATH = (os.path.join(_HERE, "lib", "ab", f"libgpboost_amd_{_VARIANT}.so") if _VARIANT
+            else os.path.join(_HERE, "lib", "libgpboost_amd.so"))
 
 
 class GPBoostError(Exception):

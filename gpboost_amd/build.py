@@ -3,6 +3,9 @@
     python -m gpboost_amd.build        # or gpboost_amd.build.build()
 
 Objects go to gpboost_amd/build/, the shared library to gpboost_amd/lib/.
+A/B variants: GPBOOST_AMD_VARIANT=<name> GPBOOST_AMD_DEFS="-DFOO=1 ..." builds the same sources
+with extra defines into gpboost_amd/build/ab_<name>/ and gpboost_amd/lib/ab/libgpboost_amd_<name>.so,
+which gpboost_amd.basic loads when GPBOOST_AMD_VARIANT is set at run time.
 The library links only the HIP runtime, RCCL and the LLVM OpenMP runtime.
 """
 from __future__ import annotations
@@ -16,9 +19,11 @@ import sys
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 CSRC = os.path.join(HERE, "csrc")
-OBJ = os.path.join(HERE, "build")
-LIBDIR = os.path.join(HERE, "lib")
-LIB = os.path.join(LIBDIR, "libgpboost_amd.so")
+VARIANT = os.environ.get("GPBOOST_AMD_VARIANT", "")
+DEFS = os.environ.get("GPBOOST_AMD_DEFS", "").split() if VARIANT else []
+OBJ = os.path.join(HERE, "build", f"ab_{VARIANT}") if VARIANT else os.path.join(HERE, "build")
+LIBDIR = os.path.join(HERE, "lib", "ab") if VARIANT else os.path.join(HERE, "lib")
+LIB = os.path.join(LIBDIR, f"libgpboost_amd_{VARIANT}.so" if VARIANT else "libgpboost_amd.so")
 ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
 ARCH = os.environ.get("GPBOOST_AMD_ARCH", "gfx950")
 
@@ -41,7 +46,7 @@ def _compile(src: str) -> str:
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(p) for p in deps):
         return obj
     lang = ["-x", "hip"] if src.endswith(".hip") else []
-    cmd = [os.path.join(ROCM, "bin", "hipcc")] + CXXFLAGS + lang + ["-c", path, "-o", obj]
+    cmd = [os.path.join(ROCM, "bin", "hipcc")] + CXXFLAGS + DEFS + lang + ["-c", path, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"compile failed: {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")

@@ -20,6 +20,10 @@
 //     no separate forward/backward substitution chains;
 //  3. t = dC_range a, with dC_rc = h(phi r_rc) C_rc recomputed from the packed C and the
 //     neighbour coordinates (no second exp, no second matrix image).
+// Measured (MI355X, n=100k, m=30, 2 waves/SIMD): pair phase unrolled by 8 and branch-free plus
+// the dC a sum unrolled with four partials: 0.455 -> 0.41 ms per launch; publishing the next
+// pivot's reciprocal with the column (reciprocal chain off the step chain) needs ~290 registers
+// (occupancy 1): 0.63 ms, rejected.
 // The row then emits six partial sums (logD, (By)^2/D, and per parameter
 // s1 = uk u - u^2 dD/2, s2 = dD/D; DESIGN.md "reduction contract"). Blocks stride over
 // row groups and keep per-lane accumulators, so one launch writes few block partials.
@@ -38,6 +42,10 @@ namespace {
 
 constexpr int kDMax = 3;
 constexpr int kMaxBlocks = 4096;
+#ifndef GPB_PAIR_UNROLL
+#define GPB_PAIR_UNROLL 8
+#endif
+constexpr int kPairUnroll = GPB_PAIR_UNROLL;   // pair-phase unroll (A/B builds override)
 
 // Orders a wave's own LDS writes before its subsequent LDS reads.
 __device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
@@ -53,6 +61,25 @@ __device__ __forceinline__ double dpp_f64(double v) {
   const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
   return __hiloint2double(hi, lo);
 }
+#ifndef GPB_PERMLANE_SWAP
+#define GPB_PERMLANE_SWAP 1
+#endif
+#if GPB_PERMLANE_SWAP
+template <bool ROW32>
+__device__ __forceinline__ double swap_sum(double v) {
+  const unsigned lo = __double2loint(v), hi = __double2hiint(v);
+  if constexpr (ROW32) {
+    const auto pl = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto ph = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    return __hiloint2double(ph[0], pl[0]) + __hiloint2double(ph[1], pl[1]);
+  } else {
+    const auto pl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto ph = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    return __hiloint2double(ph[0], pl[0]) + __hiloint2double(ph[1], pl[1]);
+  }
+}
+#endif
+
 template <int K>
 __device__ __forceinline__ double group_sum(double v) {
   if constexpr (K < 16) {   // sub-row groups (the two-rows-per-lane variant): plain shuffles
@@ -64,8 +91,15 @@ __device__ __forceinline__ double group_sum(double v) {
   v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]
   v += dpp_f64<0x141>(v);   // row_half_mirror
   v += dpp_f64<0x140>(v);   // row_mirror
+#if GPB_PERMLANE_SWAP
+  // cross-row steps by the gfx950 row-swap permutes (VALU, no LDS): the two outputs of a swap
+  // of v with itself are {own, partner} in some order, and own + partner is order-independent
+  if (K >= 32) v = swap_sum<false>(v);
+  if (K >= 64) v = swap_sum<true>(v);
+#else
   if (K >= 32) v += __shfl_xor(v, 16, 64);
   if (K >= 64) v += __shfl_xor(v, 32, 64);
+#endif
   return v;
 }
 
@@ -162,23 +196,28 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
 
     // ---- 1. pairs (rr > cc): lanes l and l + K/2 share the rows {l mod K/2, K-1-l mod K/2}
     {
+      // Branch-free (padding rows have zero coordinates and are masked by a select) and unrolled
+      // by 4 so independent sqrt/exp chains overlap (full unrolling exceeds 256 VGPRs).
       const int h = r & (K / 2 - 1);
       const int qlo = (r >= K / 2) ? K / 2 : 0;
-      for (int q = qlo; q < qlo + K / 2 && q < K - 1; ++q) {
-        int rr, cc;
-        if (q < h) { rr = h; cc = q; } else { rr = K - 1 - h; cc = q - h; }
-        double cv = 0., dcv = 0.;
-        if (rr < k) {
-          double s = 0.;
+#pragma unroll kPairUnroll
+      for (int qi = 0; qi < K / 2; ++qi) {
+        const int q = qlo + qi;
+        const bool lo = q < h;
+        const int rr = lo ? h : K - 1 - h;
+        const int cc = lo ? q : q - h;
+        double s = 0.;
 #pragma unroll
-          for (int qq = 0; qq < kDMax; ++qq) {
-            const double t = nbx[rr * kDMax + qq] - nbx[cc * kDMax + qq];
-            s += t * t;
-          }
-          cov_dcov<COV>(sqrt(s), var, phi, cv, dcv);
+        for (int qq = 0; qq < kDMax; ++qq) {
+          const double t = nbx[rr * kDMax + qq] - nbx[cc * kDMax + qq];
+          s += t * t;
         }
-        Cp[packed(rr, cc)] = cv;
-        dCp[packed(rr, cc)] = dcv;
+        double cv, dcv;
+        cov_dcov<COV>(sqrt(s), var, phi, cv, dcv);
+        if (q < K - 1) {
+          Cp[packed(rr, cc)] = rr < k ? cv : 0.;
+          dCp[packed(rr, cc)] = rr < k ? dcv : 0.;
+        }
       }
     }
     wave_lds_sync();
@@ -226,11 +265,15 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
     compiler_fence();
     slot_c[r] = av_r;
     wave_lds_sync();
-    double t = 0.;
-    for (int c = 0; c < k; ++c) {
+    // entries with c >= k are exact zeros (padding rows of dC and of a), so the sum runs over
+    // all K columns, unrolled with four partial sums
+    double tq[4] = {0., 0., 0., 0.};
+#pragma unroll
+    for (int c = 0; c < K; ++c) {
       const double dcrc = (c < r) ? dCp[packed(r, c)] : dCp[packed(c, r)];
-      t = fma(dcrc, slot_c[c], t);
+      tq[c & 3] = fma(dcrc, slot_c[c], tq[c & 3]);
     }
+    double t = (tq[0] + tq[1]) + (tq[2] + tq[3]);
     t = rv ? t : 0.;
     mark(3);
 
