@@ -87,9 +87,12 @@ struct MergedSolve {
   std::vector<int> offptr;           // host: offset o -> offpos[offptr[o], offptr[o+1])
 };
 void launch_merged_numeric(const MergedSolve& ms, const double* Bv, hipStream_t s);
-// merged level L of one solve: X[rows] from in (and dw when lower) and earlier X
-void launch_merged_level(const MergedSolve& ms, int L, bool lower, const double* dw, const double* in, double* X,
-                         int t, hipStream_t s);
+// coef = eval with 1/dw of the IN entry's row folded in (the lower solve's coefficients, per system)
+void launch_merged_scale(const MergedSolve& ms, const double* dw, double* coef, hipStream_t s);
+// merged level L of one solve: X[rows] = sum coef * (in for IN entries, earlier X for X entries);
+// coef = ms.eval for the B^T solve, the launch_merged_scale output for the lower solve
+void launch_merged_level(const MergedSolve& ms, int L, const double* coef, const double* in, double* X, int t,
+                         hipStream_t s);
 // LDS segment kernel (vadu_head.hip): ONE workgroup per column solves a segment of K rows with
 // the column's segment values resident in LDS (slot = position in the segment); a level costs an
 // LDS gather + a workgroup barrier instead of a launch. Dependencies outside the segment were

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdlib>
+#include <string>
 
 #include "common.h"
 #include "latent_kernels.h"
@@ -81,8 +82,8 @@ __global__ void __launch_bounds__(256) merge_numeric_kernel(MergedSolve ms, cons
 
 // t >= 2: one workgroup per row; lane = column (coalesced t-wide gathers of a dependency's row),
 // wave w takes entries w, w + NW, ...; the NW partial sums meet in LDS in a fixed order.
-template <bool LOWER, int NW, int B>
-__global__ void __launch_bounds__(NW * 64) merged_levelT_kernel(MergedSolve ms, int p0, const double* __restrict__ dw,
+template <int NW, int B>
+__global__ void __launch_bounds__(NW * 64) merged_levelT_kernel(MergedSolve ms, const double* __restrict__ coef, int p0,
                                                                 const double* in, double* X, int t) {
   __shared__ double red[NW][64];
   const int lane = threadIdx.x & 63;
@@ -100,13 +101,12 @@ __global__ void __launch_bounds__(NW * 64) merged_levelT_kernel(MergedSolve ms, 
     for (int q = 0; q < B; ++q) {
       const int ee = min(e + q * NW, e1 - 1);
       id[q] = ms.eidx[ee];
-      v[q] = (e + q * NW < e1) ? ms.eval[ee] : 0.;
+      v[q] = (e + q * NW < e1) ? coef[ee] : 0.;
     }
 #pragma unroll
     for (int q = 0; q < B; ++q) {
       const int ee = min(e + q * NW, e1 - 1);
-      if (ee < ex) g[q] = LOWER ? in[(size_t)id[q] * t + cc] / dw[id[q]] : in[(size_t)id[q] * t + cc];
-      else g[q] = X[(size_t)id[q] * t + cc];
+      g[q] = (ee < ex ? in : X)[(size_t)id[q] * t + cc];
     }
 #pragma unroll
     for (int q = 0; q < B; ++q) acc = fma(v[q], g[q], acc);
@@ -121,15 +121,69 @@ __global__ void __launch_bounds__(NW * 64) merged_levelT_kernel(MergedSolve ms, 
   }
 }
 
-// t >= 2, wave per row (default): 4 rows per 256-thread workgroup, lane = column; a chunk of up
+// t >= 2 (default form): one workgroup per row, wave w takes the chunks w, w + NW, ... of CH
+// consecutive entries; a chunk's structure is ONE coalesced load per array (lane q = entry q) and
+// each gather takes its entry's row and coefficient by v_readlane, so an entry costs one vector
+// memory instruction (the gather, from a scalar base) instead of three. CH gathers in flight.
+template <int NW, int CH>
+__global__ void __launch_bounds__(NW * 64) merged_levelR_kernel(MergedSolve ms, const double* __restrict__ coef, int p0,
+                                                                const double* in, double* X, int t) {
+  __shared__ double red[NW][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int c = lane + blockIdx.y * 64;
+  const int cc = c < t ? c : t - 1;   // lanes beyond t gather a valid column, result unused
+  const int p = p0 + xcd_block(blockIdx.x, gridDim.x);
+  const int i = ms.rows[p];
+  const int e0 = ms.eoff[p], ex = ms.xoff[p], e1 = ms.eoff[p + 1];
+  const int safe = ms.eidx[e0];       // padding gathers re-read the first entry's row
+  double acc = 0.;
+  for (int b = e0 + wave * CH; b < e1; b += NW * CH) {
+    const int e = b + lane;
+    const bool ok = lane < CH && e < e1;
+    const int my_id = ok ? ms.eidx[e] : safe;
+    const double my_w = ok ? coef[e] : 0.;
+    int id[CH];
+    double w[CH], g[CH];
+#pragma unroll
+    for (int q = 0; q < CH; ++q) {
+      id[q] = __builtin_amdgcn_readlane(my_id, q);
+      w[q] = readlane_f64(my_w, q);
+    }
+#pragma unroll
+    for (int q = 0; q < CH; ++q) g[q] = (b + q < ex ? in : X)[(size_t)id[q] * t + cc];
+#pragma unroll
+    for (int q = 0; q < CH; ++q) acc = fma(w[q], g[q], acc);
+  }
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (wave == 0 && c < t) {
+    double sum = red[0][lane];
+#pragma unroll
+    for (int w = 1; w < NW; ++w) sum += red[w][lane];
+    X[(size_t)i * t + c] = sum;
+  }
+}
+
+// IN-entry coefficients of the lower solve with 1/dw folded in (per system, after SetDiag):
+// coef[e] = eval[e] / dw[eidx[e]] for IN entries, eval[e] for X entries. One thread per position.
+__global__ void __launch_bounds__(256) merged_scale_kernel(MergedSolve ms, const double* __restrict__ dw,
+                                                           double* __restrict__ coef) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= ms.npos) return;
+  const int e0 = ms.eoff[p], ex = ms.xoff[p], e1 = ms.eoff[p + 1];
+  for (int e = e0; e < ex; ++e) coef[e] = ms.eval[e] / dw[ms.eidx[e]];
+  for (int e = ex; e < e1; ++e) coef[e] = ms.eval[e];
+}
+
+// t >= 2, wave per row (A/B): 4 rows per 256-thread workgroup, lane = column; a chunk of up
 // to 64 entries is ONE coalesced structure load (lane r = entry r) and each gather takes its
 // entry's index and coefficient by v_readlane, CH gathers in flight (the operator kernels' form,
 // sparse_kernels.hip). IN entries first (the lower solve folds 1/dw into their coefficients),
 // then X entries, each ascending.
-template <bool LOWER, int CH>
-__global__ void __launch_bounds__(256) merged_levelW_kernel(MergedSolve ms, int p0, int cnt,
-                                                            const double* __restrict__ dw, const double* in,
-                                                            double* X, int t) {
+template <int CH>
+__global__ void __launch_bounds__(256) merged_levelW_kernel(MergedSolve ms, const double* __restrict__ coef, int p0,
+                                                            int cnt, const double* in, double* X, int t) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int r = xcd_block(blockIdx.x, gridDim.x) * 4 + wave;
@@ -144,15 +198,14 @@ __global__ void __launch_bounds__(256) merged_levelW_kernel(MergedSolve ms, int 
     const int e = b0 + lane;
     const bool ok = e < ex;
     const int my_id = ok ? ms.eidx[e] : i;
-    double my_w = ok ? ms.eval[e] : 0.;
-    if (LOWER && ok) my_w /= dw[my_id];
+    const double my_w = ok ? coef[e] : 0.;
     s = wave_dot<CH>(my_id, my_w, ex - b0 < 64 ? ex - b0 : 64, in, t, cc, i, s);
   }
   for (int b0 = ex; b0 < e1; b0 += 64) {
     const int e = b0 + lane;
     const bool ok = e < e1;
     const int my_id = ok ? ms.eidx[e] : i;
-    const double my_w = ok ? ms.eval[e] : 0.;
+    const double my_w = ok ? coef[e] : 0.;
     s = wave_dot<CH>(my_id, my_w, e1 - b0 < 64 ? e1 - b0 : 64, X, t, cc, i, s);
   }
   if (c < t) X[(size_t)i * t + c] = s;
@@ -160,10 +213,9 @@ __global__ void __launch_bounds__(256) merged_levelW_kernel(MergedSolve ms, int 
 
 // t = 1: a row's entries are spread over a lane group (G lanes, entry e on lane e mod G), the
 // group sums its lanes with a fixed tree.
-template <bool LOWER, int G>
-__global__ void __launch_bounds__(256) merged_level1_kernel(MergedSolve ms, int p0, int cnt,
-                                                            const double* __restrict__ dw, const double* in,
-                                                            double* X) {
+template <int G>
+__global__ void __launch_bounds__(256) merged_level1_kernel(MergedSolve ms, const double* __restrict__ coef, int p0,
+                                                            int cnt, const double* in, double* X) {
   const int lane = threadIdx.x & (G - 1);
   const int task = xcd_block(blockIdx.x, gridDim.x) * (256 / G) + threadIdx.x / G;
   if (task >= cnt) return;   // whole groups exit together (cnt is per group)
@@ -173,27 +225,36 @@ __global__ void __launch_bounds__(256) merged_level1_kernel(MergedSolve ms, int 
   double acc = 0.;
   for (int e = e0 + lane; e < e1; e += G) {
     const int id = ms.eidx[e];
-    const double g = e < ex ? (LOWER ? in[id] / dw[id] : in[id]) : X[id];
-    acc = fma(ms.eval[e], g, acc);
+    const double g = e < ex ? in[id] : X[id];
+    acc = fma(coef[e], g, acc);
   }
   acc = lane_group_sum<G>(acc);
   if (lane == 0) X[i] = acc;
 }
 
-// Shape knobs (A/B only): GPBOOST_AMD_LEVELT_NW = 1, 2 or 4 (default): one workgroup per row with
-// that many waves sharing its entries; 0: wave per row (merged_levelW; measured slower at n = 100k,
-// t = 51: 1.03 vs 0.82 ms per application for g = 4); GPBOOST_AMD_LEVEL1_G = lanes per row at
-// t = 1 (16, 32 or 64; default 64). Other values: error.
+// Shape knobs (A/B only): GPBOOST_AMD_LEVELT_FORM = chunk (default: merged_levelR, coalesced
+// structure + readlane), gather (merged_levelT: per-entry structure loads) or wave (merged_levelW,
+// one wave per row); GPBOOST_AMD_LEVELT_NW = waves per row of the workgroup forms (1, 2, 4 default,
+// 8); GPBOOST_AMD_LEVEL1_G = lanes per row at t = 1 (16, 32 or 64; default 64). Other values:
+// error.
 struct LevelShape {
-  int nw = 4, g = 64;
+  int form = 0, nw = 4, g = 64;   // form 0 chunk, 1 gather, 2 wave
 };
 const LevelShape& level_shape() {
   static const LevelShape v = [] {
     LevelShape k;
+    if (const char* e = std::getenv("GPBOOST_AMD_LEVELT_FORM")) {
+      const std::string f(e);
+      if (f == "chunk") k.form = 0;
+      else if (f == "gather") k.form = 1;
+      else if (f == "wave") k.form = 2;
+      else Fatal("GPBOOST_AMD_LEVELT_FORM must be chunk, gather or wave (got '%s')", e);
+      Info("tail level kernels: form %s", e);
+    }
     if (const char* e = std::getenv("GPBOOST_AMD_LEVELT_NW")) {
       k.nw = std::atoi(e);
-      if (k.nw != 0 && k.nw != 1 && k.nw != 2 && k.nw != 4 && k.nw != 8)
-        Fatal("GPBOOST_AMD_LEVELT_NW must be 0, 1, 2, 4 or 8 (got '%s')", e);
+      if (k.nw != 1 && k.nw != 2 && k.nw != 4 && k.nw != 8)
+        Fatal("GPBOOST_AMD_LEVELT_NW must be 1, 2, 4 or 8 (got '%s')", e);
       Info("tail level kernels: %d wave(s) per row at t >= 2", k.nw);
     }
     if (const char* e = std::getenv("GPBOOST_AMD_LEVEL1_G")) {
@@ -206,29 +267,35 @@ const LevelShape& level_shape() {
   return v;
 }
 
-template <bool LOWER>
-void launch_level(const MergedSolve& ms, int p0, int cnt, const double* dw, const double* in, double* X, int t,
+void launch_level(const MergedSolve& ms, const double* coef, int p0, int cnt, const double* in, double* X, int t,
                   hipStream_t s) {
   const LevelShape& ks = level_shape();
   if (t == 1) {
     const int G = ks.g;
     const dim3 grid((cnt + 256 / G - 1) / (256 / G));
-    if (G == 16) hipLaunchKernelGGL((merged_level1_kernel<LOWER, 16>), grid, dim3(256), 0, s, ms, p0, cnt, dw, in, X);
-    else if (G == 32) hipLaunchKernelGGL((merged_level1_kernel<LOWER, 32>), grid, dim3(256), 0, s, ms, p0, cnt, dw, in, X);
-    else hipLaunchKernelGGL((merged_level1_kernel<LOWER, 64>), grid, dim3(256), 0, s, ms, p0, cnt, dw, in, X);
+    if (G == 16) hipLaunchKernelGGL((merged_level1_kernel<16>), grid, dim3(256), 0, s, ms, coef, p0, cnt, in, X);
+    else if (G == 32) hipLaunchKernelGGL((merged_level1_kernel<32>), grid, dim3(256), 0, s, ms, coef, p0, cnt, in, X);
+    else hipLaunchKernelGGL((merged_level1_kernel<64>), grid, dim3(256), 0, s, ms, coef, p0, cnt, in, X);
     return;
   }
-  if (ks.nw == 0) {
-    hipLaunchKernelGGL((merged_levelW_kernel<LOWER, 16>), dim3((cnt + 3) / 4, (t + 63) / 64), dim3(256), 0, s, ms, p0,
-                       cnt, dw, in, X, t);
+  if (ks.form == 2) {
+    hipLaunchKernelGGL((merged_levelW_kernel<16>), dim3((cnt + 3) / 4, (t + 63) / 64), dim3(256), 0, s, ms, coef, p0,
+                       cnt, in, X, t);
     return;
   }
   const dim3 g(cnt, (t + 63) / 64);
-  // entries in flight per row: NW waves x B gathers (64 for every shape)
-  if (ks.nw == 1) hipLaunchKernelGGL((merged_levelT_kernel<LOWER, 1, 64>), g, dim3(64), 0, s, ms, p0, dw, in, X, t);
-  else if (ks.nw == 2) hipLaunchKernelGGL((merged_levelT_kernel<LOWER, 2, 32>), g, dim3(128), 0, s, ms, p0, dw, in, X, t);
-  else if (ks.nw == 8) hipLaunchKernelGGL((merged_levelT_kernel<LOWER, 8, 8>), g, dim3(512), 0, s, ms, p0, dw, in, X, t);
-  else hipLaunchKernelGGL((merged_levelT_kernel<LOWER, 4, 16>), g, dim3(256), 0, s, ms, p0, dw, in, X, t);
+  const dim3 b(ks.nw * 64);
+  if (ks.form == 1) {   // entries in flight per row: NW waves x B gathers (64 for every shape)
+    if (ks.nw == 1) hipLaunchKernelGGL((merged_levelT_kernel<1, 64>), g, b, 0, s, ms, coef, p0, in, X, t);
+    else if (ks.nw == 2) hipLaunchKernelGGL((merged_levelT_kernel<2, 32>), g, b, 0, s, ms, coef, p0, in, X, t);
+    else if (ks.nw == 8) hipLaunchKernelGGL((merged_levelT_kernel<8, 8>), g, b, 0, s, ms, coef, p0, in, X, t);
+    else hipLaunchKernelGGL((merged_levelT_kernel<4, 16>), g, b, 0, s, ms, coef, p0, in, X, t);
+    return;
+  }
+  if (ks.nw == 1) hipLaunchKernelGGL((merged_levelR_kernel<1, 32>), g, b, 0, s, ms, coef, p0, in, X, t);
+  else if (ks.nw == 2) hipLaunchKernelGGL((merged_levelR_kernel<2, 16>), g, b, 0, s, ms, coef, p0, in, X, t);
+  else if (ks.nw == 8) hipLaunchKernelGGL((merged_levelR_kernel<8, 8>), g, b, 0, s, ms, coef, p0, in, X, t);
+  else hipLaunchKernelGGL((merged_levelR_kernel<4, 16>), g, b, 0, s, ms, coef, p0, in, X, t);
 }
 
 }  // namespace
@@ -243,12 +310,17 @@ void launch_merged_numeric(const MergedSolve& ms, const double* Bv, hipStream_t 
   HIP_CHECK(hipGetLastError());
 }
 
-void launch_merged_level(const MergedSolve& ms, int L, bool lower, const double* dw, const double* in, double* X,
-                         int t, hipStream_t s) {
+void launch_merged_scale(const MergedSolve& ms, const double* dw, double* coef, hipStream_t s) {
+  if (ms.npos <= 0) return;
+  hipLaunchKernelGGL(merged_scale_kernel, dim3((ms.npos + 255) / 256), dim3(256), 0, s, ms, dw, coef);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_merged_level(const MergedSolve& ms, int L, const double* coef, const double* in, double* X, int t,
+                         hipStream_t s) {
   const int p0 = ms.lptr[L], cnt = ms.lptr[L + 1] - p0;
   if (cnt <= 0 || t <= 0) return;
-  if (lower) launch_level<true>(ms, p0, cnt, dw, in, X, t, s);
-  else launch_level<false>(ms, p0, cnt, dw, in, X, t, s);
+  launch_level(ms, coef, p0, cnt, in, X, t, s);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -250,6 +250,7 @@ void VaduPrecond::Build(const int* nbr, const std::vector<int>& vo, const std::v
       ms.eval = d_mval_.get() + v0[w];
     }
     tail_entries_ = (long)nval;
+    d_mcoef_.alloc(std::max<size_t>(hs[1]->eidx.size(), 1));
   }
 
   // ---- head 1 segment [K0, K): slots = Vecchia index - K0, dependencies inside the segment
@@ -458,12 +459,14 @@ void VaduPrecond::Refresh(const double* Bv) {
   launch_gather(nslot_, d_slot_.get(), Bv, d_val_.get(), s_);
   launch_merged_numeric(mt_bt_, Bv, s_);
   launch_merged_numeric(mt_low_, Bv, s_);
+  if (dw_) launch_merged_scale(mt_low_, dw_, d_mcoef_.get(), s_);
   if (K0_ > 0) dense_head_factor(dh_, Bd_.get(), G_.get(), GT_.get(), T_.get(), s_);
 }
 
 void VaduPrecond::SetDiag(const double* dw) {
   if (dw != dw_) DropGraphs();   // the captured launches hold the pointer
   dw_ = dw;
+  launch_merged_scale(mt_low_, dw_, d_mcoef_.get(), s_);   // dw's values change with every Newton step
 }
 
 void VaduPrecond::DenseApply(const double* X0, double* Z, int t, hipStream_t st, double* S) {
@@ -474,7 +477,7 @@ void VaduPrecond::DenseApply(const double* X0, double* Z, int t, hipStream_t st,
 void VaduPrecond::TailSolve(bool lower, const double* R, double* Xt, double* Z, int t, hipStream_t st) {
   const MergedSolve& ms = lower ? mt_low_ : mt_bt_;
   for (int L = 0; L + 1 < (int)ms.lptr.size(); ++L)
-    launch_merged_level(ms, L, lower, dw_, lower ? Xt : R, lower ? Z : Xt, t, st);
+    launch_merged_level(ms, L, lower ? d_mcoef_.get() : ms.eval, lower ? Xt : R, lower ? Z : Xt, t, st);
 }
 
 void VaduPrecond::Record(const double* R, double* Z, double* Xt, int t, hipStream_t st, double* S) {

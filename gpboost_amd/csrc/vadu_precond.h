@@ -52,7 +52,8 @@ class VaduPrecond {
              const std::vector<int>& trow, const std::vector<int>& tslot, int K0, int K);
   // Per factor (B values in the n x m slot layout of `nbr`).
   void Refresh(const double* Bv);
-  // Per system: dw = D^-1 + W (device, n). Must precede Apply; the pointer is captured.
+  // Per system: dw = D^-1 + W (device, n), after its values are written (stream order). Must
+  // precede Apply; the pointer is captured and the lower solve's coefficients are rescaled.
   void SetDiag(const double* dw);
   // Z = P^-1 R for t columns (row-major n x t); Xt: n x t scratch (holds B^-T R afterwards).
   // stream: null = the model's; applications that may run concurrently (on different streams)
@@ -84,6 +85,7 @@ class VaduPrecond {
   MergedSolve mt_bt_{}, mt_low_{};   // merged tail levels of the two solves
   DevBuf<int> d_mint_;
   DevBuf<double> d_mval_;
+  DevBuf<double> d_mcoef_;   // lower-solve coefficients with 1/dw folded in (SetDiag)
   int merge_g_ = 1;
   long tail_entries_ = 0;
   HeadSolve seg_bt_{}, seg_low_{};
