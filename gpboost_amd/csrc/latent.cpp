@@ -283,7 +283,20 @@ void LatentVecchia::BenchOperators(int t, int reps, double* out) {
   HIP_CHECK(hipEventSynchronize(ev1_));
   HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_));
   out[1] = ms / reps;
-  if (std::getenv("GPBOOST_AMD_PRECOND_SPLIT")) pre_->TimeParts(b.R.get(), b.Z.get(), b.Xt.get(), t, reps);
+  if (std::getenv("GPBOOST_AMD_PRECOND_SPLIT")) {
+    pre_->TimeParts(b.R.get(), b.Z.get(), b.Xt.get(), t, reps);
+    for (int part = 0; part < 2; ++part) {   // the operator's two launches
+      HIP_CHECK(hipEventRecord(ev0_, s_));
+      for (int r = 0; r < reps; ++r) {
+        if (part == 0) launch_b_apply(sp_, d_Bv_.get(), true, b.H.get(), t, d_Dinv_.get(), b.G.get(), s_);
+        else launch_bt_apply(sp_, d_Bv_.get(), true, b.G.get(), t, nullptr, d_W_.get(), b.H.get(), b.V.get(), s_);
+      }
+      HIP_CHECK(hipEventRecord(ev1_, s_));
+      HIP_CHECK(hipEventSynchronize(ev1_));
+      HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_));
+      std::fprintf(stderr, "[operator parts t=%d] %s %.4f ms\n", t, part ? "bt_apply" : "b_apply ", ms / reps);
+    }
+  }
   if (std::getenv("GPBOOST_AMD_BENCH_2STREAM") && t >= 2) {   // diagnostics: two column groups, two streams
     const int t0 = (t + 1) / 2, t1 = t - t0;
     DevBuf<double> R0((size_t)n_ * t0), Z0((size_t)n_ * t0), X0((size_t)n_ * t0);
