@@ -21,6 +21,9 @@ LIB_PATH = (os.path.join(_HERE, "lib", "ab", f"libgpboost_amd_{_VARIANT}.so") if
             else os.path.join(_HERE, "lib", "libgpboost_amd.so"))
 
 
+_HostReduceFn = ctypes.CFUNCTYPE(None, ctypes.POINTER(ctypes.c_double), ctypes.c_int, ctypes.c_void_p)
+
+
 class GPBoostError(Exception):
     """Error thrown by the library (reference basic.py:136-145)."""
 
@@ -39,6 +42,7 @@ def _load_lib():
                                        c.c_bool, c.c_char_p, c.c_int, c.c_char_p, c.c_int, D, c.c_double, c.c_double,
                                        c.c_char_p, c.c_int, c.c_int, c.c_double, c.c_int, c.c_bool, c.c_char_p,
                                        c.c_int, c.c_int, D, c.c_bool, I, c.c_int, c.c_double]
+    lib.GPB_SetDistributedHostReduce.argtypes = [c.c_void_p, c.c_int, c.c_int, _HostReduceFn, c.c_void_p]
     return lib
 
 
@@ -305,8 +309,21 @@ class GPModel:
         return out
 
     def set_distributed(self, rank: int, world_size: int, comm_id: bytes | None):
+        """Join an RCCL communicator (GPB_SetDistributed): exact Vecchia shards rows, latent
+        Vecchia (iterative) shards the probe columns."""
         buf = ctypes.create_string_buffer(comm_id, len(comm_id)) if comm_id is not None else None
         _safe_call(lib().GPB_SetDistributed(self.handle, ctypes.c_int(rank), ctypes.c_int(world_size), buf))
+
+    def set_distributed_host(self, rank: int, world_size: int, allreduce):
+        """Same partition as set_distributed, with the cross-rank sums done by
+        ``allreduce(x: np.ndarray)`` (in place, e.g. a gloo all-reduce) instead of RCCL
+        (GPB_SetDistributedHostReduce): a test transport for several ranks on one GPU."""
+        def _cb(buf, count, _user):
+            arr = np.ctypeslib.as_array(buf, shape=(count,))
+            allreduce(arr)
+        self._host_reduce = _HostReduceFn(_cb)   # keep the trampoline alive with the model
+        _safe_call(lib().GPB_SetDistributedHostReduce(self.handle, ctypes.c_int(rank), ctypes.c_int(world_size),
+                                                      self._host_reduce, None))
 
 
 def comm_create_id() -> bytes:

@@ -356,6 +356,13 @@ int GPB_SetDistributed(REModelHandle handle, int rank, int world_size, const cha
   API_END();
 }
 
+int GPB_SetDistributedHostReduce(REModelHandle handle, int rank, int world_size,
+                                 void (*allreduce)(double* buf, int count, void* user), void* user) {
+  API_BEGIN();
+  model(handle)->SetDistributedHost(rank, world_size, allreduce, user);
+  API_END();
+}
+
 int GPB_PartitionRows(int32_t num_data, int world_size, int rank, int32_t* row_begin, int32_t* row_end) {
   API_BEGIN();
   if (world_size < 1 || rank < 0 || rank >= world_size) gpb_amd::Fatal("invalid rank/world_size");

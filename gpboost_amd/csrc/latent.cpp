@@ -239,22 +239,47 @@ LatentVecchia::Block& LatentVecchia::GetBlock(int which, int t, int pmax) {
   return b;
 }
 
+void LatentVecchia::SetShard(int rank, int world, Collective* coll) {
+  if (world < 1 || rank < 0 || rank >= world) Fatal("invalid rank %d / world_size %d", rank, world);
+  if (world > 1 && coll == nullptr) Fatal("the probe-sharded latent path needs a collective");
+  rank_ = rank;
+  world_ = world;
+  coll_ = coll;
+  probes_saved_ = false;   // this rank's share is drawn at the next evaluation
+  d_gsum_.alloc(1);
+}
+
+void LatentVecchia::AllReduceHost(double* v, int count) {
+  if (coll_ == nullptr || count <= 0) return;
+  if (d_red_.size() < (size_t)count) d_red_.alloc(count);
+  HIP_CHECK(hipMemcpyAsync(d_red_.get(), v, sizeof(double) * count, hipMemcpyHostToDevice, s_));
+  coll_->AllReduceSum(d_red_.get(), count, s_);
+  HIP_CHECK(hipMemcpyAsync(v, d_red_.get(), sizeof(double) * count, hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+}
+
 void LatentVecchia::EnsureProbes(const IterativeConfig& cfg) {
   const int t = cfg.num_rand_vec_trace;
   if (probes_saved_ && probes_t_ == t) return;
-  // GenRandVecNormalParallel (CG_utils.cpp:930-947), drawn once when reuse_rand_vec_trace
-  std::vector<double> R((size_t)n_ * t);
+  if (t < world_) Fatal("num_rand_vec_trace = %d < %d ranks: every rank needs at least one probe column", t, world_);
+  t_all_ = t;
+  c0_ = (int)((long)t * rank_ / world_);
+  c1_ = (int)((long)t * (rank_ + 1) / world_);
+  const int tw = probe_cols();   // this rank's block width (padding columns stay 0)
+  // GenRandVecNormalParallel (CG_utils.cpp:930-947), drawn once when reuse_rand_vec_trace;
+  // column c is seeded by its global index, so a rank draws exactly its share
+  std::vector<double> R((size_t)n_ * tw, 0.);
   {   // drawn in Vecchia order (the reference's), stored in the relabelled rows
-    std::vector<double> Rv((size_t)n_ * t);
-    gen_probes_normal(n_, t, cfg.seed_rand_vec_trace, probe_run_id_, Rv.data());
+    std::vector<double> Rv((size_t)n_ * tw, 0.);
+    gen_probes_normal_cols(n_, c0_, c1_, tw, cfg.seed_rand_vec_trace, probe_run_id_, Rv.data());
     for (int p = 0; p < n_; ++p)
-      std::copy(Rv.begin() + (size_t)vo_[p] * t, Rv.begin() + (size_t)(vo_[p] + 1) * t, R.begin() + (size_t)p * t);
+      std::copy(Rv.begin() + (size_t)vo_[p] * tw, Rv.begin() + (size_t)(vo_[p] + 1) * tw, R.begin() + (size_t)p * tw);
   }
   ++probe_run_id_;
-  d_probes_.alloc((size_t)n_ * t);
-  d_Zp_.alloc((size_t)n_ * t);
-  d_U_.alloc((size_t)n_ * t);
-  d_P_.alloc((size_t)n_ * t);
+  d_probes_.alloc((size_t)n_ * tw);
+  d_Zp_.alloc((size_t)n_ * tw);
+  d_U_.alloc((size_t)n_ * tw);
+  d_P_.alloc((size_t)n_ * tw);
   HIP_CHECK(hipMemcpyAsync(d_probes_.get(), R.data(), sizeof(double) * R.size(), hipMemcpyHostToDevice, s_));
   HIP_CHECK(hipStreamSynchronize(s_));
   probes_t_ = t;
@@ -389,8 +414,11 @@ void LatentVecchia::WaitCtl(int seq, int* out) {
 }
 
 LatentVecchia::PcgResult LatentVecchia::Pcg(Block& b, const double* RHS, double* U, int n_single, bool init_zero,
-                                             bool u_is_zero, int pmax_single, int pmax_block, double delta) {
+                                             bool u_is_zero, int pmax_single, int pmax_block, double delta,
+                                             int n_valid, int nblock_all) {
   const int t = b.t;
+  if (n_valid < 0) n_valid = t;
+  const bool gblock = coll_ != nullptr && nblock_all > 0;   // block rule on the all-rank norm sum
   const size_t nt = (size_t)n_ * t;
   PcgResult res;
   pmax_single = std::min(pmax_single, n_);
@@ -418,7 +446,7 @@ LatentVecchia::PcgResult LatentVecchia::Pcg(Block& b, const double* RHS, double*
     launch_coldots(n_, t, 1, A, Bm, d_partials_.get(), b.rr(), s_);
     rr0 = b.rr();
   }
-  launch_pcg_init(t, n_single, pmax_single, pmax_block, kZeroRhsSq, rr0, b.act.get(), b.ctl.get(), s_);
+  launch_pcg_init(t, n_valid, n_single, pmax_single, pmax_block, kZeroRhsSq, rr0, b.act.get(), b.ctl.get(), s_);
   Precond(b.R.get(), b.Z.get(), b.Xt.get(), t);
   launch_copy(nt, b.Z.get(), b.H.get(), s_);
   {
@@ -448,9 +476,13 @@ LatentVecchia::PcgResult LatentVecchia::Pcg(Block& b, const double* RHS, double*
     }
     launch_cg_alpha(t, b.rz(), b.hv(), b.act.get(), b.a(), b.a_hist.get() + (size_t)j * t, s_);
     launch_cg_update(n_, t, b.a(), b.H.get(), b.V.get(), U, b.R.get(), d_partials_.get(), b.rr(), s_);
+    if (gblock) {   // every rank runs the same iterations, so the collectives pair up
+      launch_pcg_block_sum(n_valid, n_single, b.rr(), d_gsum_.get(), s_);
+      coll_->AllReduceSum(d_gsum_.get(), 1, s_);
+    }
     const int seq = ++pcg_seq_;
-    launch_pcg_check(j, t, n_single, pmax_single, pmax_block, delta, b.rr(), b.act.get(), b.ctl.get(),
-                     d_hctl_ + (seq & 1) * 2, seq, s_);
+    launch_pcg_check(j, t, n_single, pmax_single, pmax_block, delta, b.rr(), gblock ? d_gsum_.get() : nullptr,
+                     nblock_all, b.act.get(), b.ctl.get(), d_hctl_ + (seq & 1) * 2, seq, s_);
     Precond(b.R.get(), b.Z.get(), b.Xt.get(), t);
     {
       const double* A[1] = {b.R.get()};
@@ -569,6 +601,9 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
     return term;
   };
   EnsureProbes(cfg);
+  const int tw = probe_cols();          // this rank's probe block width (t at world 1)
+  const int tl = c1_ - c0_;             // its real probe columns (the rest is padding)
+  const int nb_all = coll_ ? t : 0;     // block column count over all ranks (collective stop rule)
   if (gauss) {
     // Gaussian: W = 1/aux does not depend on the mode, so the single Newton step's solve
     // (Sigma^-1 + W)^-1 (y / aux) and the SLQ block solve the same system. Both run as one
@@ -581,19 +616,19 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
     launch_newton_prep(np, s_);
     SetDiag();
     n_lead = 1;
-    const int tf = t + 1;
+    const int tf = tw + 1;
     bslq = &GetBlock(1, tf, std::max(pmax_tri, cg_max));
     d_rhsf_.alloc((size_t)n * tf);
     d_Uf_.alloc((size_t)n * tf);
-    // z_i = B^T (D^-1 + W)^(1/2) r_i into columns 1..t, y / aux into column 0
-    launch_bt_apply(sp_, d_Bv_.get(), true, d_probes_.get(), t, d_sdw_.get(), nullptr, nullptr, d_Zp_.get(), s_);
-    launch_pack_columns(n, t, d_Zp_.get(), t, 0, d_rhsf_.get(), tf, 1, s_);
+    // z_i = B^T (D^-1 + W)^(1/2) r_i into columns 1..tw, y / aux into column 0
+    launch_bt_apply(sp_, d_Bv_.get(), true, d_probes_.get(), tw, d_sdw_.get(), nullptr, nullptr, d_Zp_.get(), s_);
+    launch_pack_columns(n, tw, d_Zp_.get(), tw, 0, d_rhsf_.get(), tf, 1, s_);
     launch_pack_columns(n, 1, d_rhs_.get(), 1, 0, d_rhsf_.get(), tf, 0, s_);
-    slq = Pcg(*bslq, d_rhsf_.get(), d_Uf_.get(), 1, true, true, cg_max, pmax_tri, cfg.cg_delta_conv);
+    slq = Pcg(*bslq, d_rhsf_.get(), d_Uf_.get(), 1, true, true, cg_max, pmax_tri, cfg.cg_delta_conv, 1 + tl, nb_all);
     if (slq.nan) Fatal("NaN or Inf occurred in the conjugate gradient algorithm (mode finding / log-determinant)");
     res.cg_its = slq.its_single;
     launch_pack_columns(n, 1, d_Uf_.get(), tf, 0, d_mode_upd_.get(), 1, 0, s_);
-    launch_pack_columns(n, t, d_Uf_.get(), tf, 1, d_U_.get(), t, 0, s_);
+    launch_pack_columns(n, tw, d_Uf_.get(), tf, 1, d_U_.get(), tw, 0, s_);
     line_search_and_check(0, 0.);
   } else {
     // ---- 2. mode finding (likelihoods.h:2780-3000)
@@ -628,9 +663,9 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
       SetDiag();
     }
     // ---- 3. SLQ block (likelihoods.h:3018-3045, 12155-12212): z_i = B^T (D^-1 + W)^(1/2) r_i
-    bslq = &GetBlock(1, t, pmax_tri);
-    launch_bt_apply(sp_, d_Bv_.get(), true, d_probes_.get(), t, d_sdw_.get(), nullptr, nullptr, d_Zp_.get(), s_);
-    slq = Pcg(*bslq, d_Zp_.get(), d_U_.get(), 0, true, true, 0, pmax_tri, cfg.cg_delta_conv);
+    bslq = &GetBlock(1, tw, pmax_tri);
+    launch_bt_apply(sp_, d_Bv_.get(), true, d_probes_.get(), tw, d_sdw_.get(), nullptr, nullptr, d_Zp_.get(), s_);
+    slq = Pcg(*bslq, d_Zp_.get(), d_U_.get(), 0, true, true, 0, pmax_tri, cfg.cg_delta_conv, tl, nb_all);
     if (slq.nan) Fatal("NaN or Inf occurred in the stochastic Lanczos quadrature (log-determinant)");
   }
   Block& bt = *bslq;
@@ -645,8 +680,8 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
   sa.mode = d_mode_.get();
   sa.dw = d_dw_.get();
   Scalars(sa, sc);   // synchronises the stream
-  std::vector<std::vector<double>> Td(t), Ts(t);
-  for (int c = 0; c < t; ++c) {   // CG_utils.cpp:200-206 (a_old = 1, b_old = 0 before the first step)
+  std::vector<std::vector<double>> Td(tl), Ts(tl);
+  for (int c = 0; c < tl; ++c) {   // CG_utils.cpp:200-206 (a_old = 1, b_old = 0 before the first step)
     const int cc = c + n_lead;
     Td[c].resize(L);
     Ts[c].resize(L > 0 ? L - 1 : 0);
@@ -658,33 +693,64 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
       if (j > 0) Ts[c][j - 1] = std::sqrt(b_old) / a_old;
     }
   }
-  const double ldet_PI = slq_logdet(Td, Ts, n);
+  double ldet_PI;
+  if (coll_ == nullptr) {
+    ldet_PI = slq_logdet(Td, Ts, n);
+  } else {   // every rank's per-probe terms at their global columns, summed in column order
+    const std::vector<double> mine = slq_terms(Td, Ts);
+    std::vector<double> all(t, 0.);
+    std::copy(mine.begin(), mine.end(), all.begin() + c0_);
+    AllReduceHost(all.data(), t);
+    double ld = 0.;
+    for (int c = 0; c < t; ++c) ld += all[c];
+    ldet_PI = ld * n / t;
+  }
   res.logdet = ldet_PI - sc[kSqLogDinv] + sc[kSqLogDw];
   const double mll_final = mll - 0.5 * res.logdet;
   res.nll = -mll_final;
 
   if (want_grad) {
     // ---- 4. gradient (likelihoods.h:4951-5206)
-    Precond(d_Zp_.get(), d_P_.get(), bt.Xt.get(), t);   // PI_Z = P^-1 Z (:12321-12327)
+    Precond(d_Zp_.get(), d_P_.get(), bt.Xt.get(), tw);   // PI_Z = P^-1 Z (:12321-12327)
     if (!gauss) {   // grad_information_wrt_mode_non_zero_: implicit derivative through the mode
       ModeDerivArgs md{};
-      md.n = n; md.m = m_; md.t = t; md.lik = lik; md.nbr = d_nbr_.get(); md.Bv = d_Bv_.get(); md.dw = d_dw_.get();
+      md.n = n; md.m = m_; md.t = tw; md.lik = lik; md.nbr = d_nbr_.get(); md.Bv = d_Bv_.get(); md.dw = d_dw_.get();
       md.loc = d_mode_.get(); md.U = d_U_.get(); md.P = d_P_.get(); md.dmll = d_dmll_.get();
-      launch_mode_deriv(md, s_);
+      md.t_valid = tl; md.t_all = t;
+      if (coll_ == nullptr) {
+        md.stage = 0;
+        launch_mode_deriv(md, s_);
+      } else {   // row moments over all ranks' probes: two all-reduces of n x 2
+        d_mom_.alloc((size_t)2 * n);
+        d_mom2_.alloc((size_t)2 * n);
+        md.mom = d_mom_.get();
+        md.mom2 = d_mom2_.get();
+        for (int st = 1; st <= 3; ++st) {
+          md.stage = st;
+          launch_mode_deriv(md, s_);
+          if (st < 3) coll_->AllReduceSum(st == 1 ? d_mom_.get() : d_mom2_.get(), 2 * n, s_);
+        }
+      }
       const PcgResult pv = Pcg(b1, d_dmll_.get(), d_vS_.get(), 1, true, true, cg_max, 0, cfg.cg_delta_conv);
       res.cg_its += pv.its_single;
       if (pv.nan) Warning("NaN or Inf occurred in the conjugate gradient algorithm of the gradient calculation");
     }
     GradColsArgs ga{};
-    ga.n = n; ga.m = m_; ga.t = t; ga.nbr = d_nbr_.get(); ga.Bv = d_Bv_.get(); ga.dBv = d_dBv_.get();
+    ga.n = n; ga.m = m_; ga.t = tw; ga.nbr = d_nbr_.get(); ga.Bv = d_Bv_.get(); ga.dBv = d_dBv_.get();
     ga.Dinv = d_Dinv_.get(); ga.dD = d_dD_.get(); ga.W = d_W_.get();
     ga.daux = gauss ? -1. / aux : 0.;   // d information / dlog(aux) (likelihoods.h:10967-10976)
     ga.U = d_U_.get(); ga.P = d_P_.get();
     DevBuf<double>& cols = d_out_;
     launch_grad_cols(ga, d_partials_.get(), cols.get(), s_);
-    std::vector<double> z((size_t)kGradCols * t);
-    HIP_CHECK(hipMemcpyAsync(z.data(), cols.get(), sizeof(double) * z.size(), hipMemcpyDeviceToHost, s_));
-    HIP_CHECK(hipStreamSynchronize(s_));
+    std::vector<double> z((size_t)kGradCols * t, 0.);
+    {   // per-column sums [q][c]; probe-sharded: this rank's columns at their global index, summed over ranks
+      std::vector<double> zl((size_t)kGradCols * tw);
+      HIP_CHECK(hipMemcpyAsync(zl.data(), cols.get(), sizeof(double) * zl.size(), hipMemcpyDeviceToHost, s_));
+      HIP_CHECK(hipStreamSynchronize(s_));
+      for (int q = 0; q < kGradCols; ++q)
+        for (int c = 0; c < tl; ++c) z[(size_t)q * t + c0_ + c] = zl[(size_t)q * tw + c];
+      AllReduceHost(z.data(), (int)z.size());
+    }
     ScalarArgs sg = sa;
     sg.dBv = d_dBv_.get();
     sg.dD = d_dD_.get();

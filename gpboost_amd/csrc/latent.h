@@ -21,6 +21,7 @@
 #include <vector>
 
 #include "common.h"
+#include "collective.h"
 #include "latent_kernels.h"
 #include "vadu_precond.h"
 
@@ -63,6 +64,15 @@ class LatentVecchia {
   // the unit diagonal, out[3] = dependent launches per preconditioner application.
   void BenchOperators(int t, int reps, double* out);
 
+  // Probe-column sharding (SURVEY.md §8e Option A): rank r of `world` runs the probe columns
+  // [t r / world, t (r+1) / world) of every SLQ block — padded to ceil(t / world) columns, so
+  // every rank's blocks have the same width and the replicated Newton / mode columns are
+  // computed bitwise alike on every rank — with one all-reduce per PCG iteration (the block
+  // stopping rule's norm sum) and the per-column log-determinant / trace terms and the
+  // mode-derivative row moments all-reduced at the end. coll: owned by the caller; null at
+  // world 1.
+  void SetShard(int rank, int world, Collective* coll);
+
  private:
   // Device work space of a t-column PCG (t = 1 for the Newton solves, t probes for SLQ).
   struct Block {
@@ -98,8 +108,13 @@ class LatentVecchia {
     int its_single = 0, its_block = 0;
     bool nan = false, zero_rhs = false;
   };
+  // n_valid: columns >= n_valid are padding (never active); nblock_all: the block's column count
+  // over all ranks (> 0 with a collective: the block rule uses the all-reduced norm sum).
   PcgResult Pcg(Block& b, const double* RHS, double* U, int n_single, bool init_zero, bool u_is_zero,
-                int pmax_single, int pmax_block, double delta);
+                int pmax_single, int pmax_block, double delta, int n_valid = -1, int nblock_all = 0);
+  // Sum of a host vector over ranks (identity at world 1).
+  void AllReduceHost(double* v, int count);
+  int probe_cols() const { return world_ > 1 ? (t_all_ + world_ - 1) / world_ : t_all_; }
   void Scalars(const ScalarArgs& a, double* out);
   double Dot1(const double* x, const double* y);   // single-vector dot, synchronous
   void WaitCtl(int seq, int* out);
@@ -129,6 +144,10 @@ class LatentVecchia {
   int* d_hctl_ = nullptr;                        // their device address
   int pcg_seq_ = 0;
   hipEvent_t ev0_ = nullptr, ev1_ = nullptr;
+  int rank_ = 0, world_ = 1;
+  Collective* coll_ = nullptr;
+  int t_all_ = 0, c0_ = 0, c1_ = 0;              // probes of all ranks; this rank's [c0_, c1_)
+  DevBuf<double> d_gsum_, d_red_, d_mom_, d_mom2_;
   bool y_set_ = false;
   bool factor_ready_ = false;
 };

@@ -185,14 +185,17 @@ __host__ __device__ inline void pcg_unpack(unsigned long long v, int* ctl) {
 }
 // act[c] = 1, except single columns whose right-hand side is zero (rr0[c] < zero_sq: the
 // reference returns u = 0 without iterating, CG_utils.cpp:42-45).
-void launch_pcg_init(int t, int n_single, int pmax_single, int pmax_block, double zero_sq, const double* rr0,
-                     int* act, int* ctl, hipStream_t s);
+void launch_pcg_init(int t, int n_valid, int n_single, int pmax_single, int pmax_block, double zero_sq,
+                     const double* rr0, int* act, int* ctl, hipStream_t s);
+// out[0] = sum of the block columns' norms [n_single, n_valid) of this rank
+void launch_pcg_block_sum(int n_valid, int n_single, const double* rr, double* out, hipStream_t s);
 // After iteration j's update (rr[c] = ||r_c||^2): single columns stop on their own norm
 // (CG_utils.cpp:80-90), the block on the mean column norm (:172-178), both at their pmax.
 // host_ctl (nullable, 8-byte aligned host-coherent memory mapped for the device): receives
 // pcg_pack(seq, ...) by one store.
+// gsum != null: the block norm sum over all ranks, nblock its column count (probe-sharded blocks)
 void launch_pcg_check(int j, int t, int n_single, int pmax_single, int pmax_block, double delta, const double* rr,
-                      int* act, int* ctl, int* host_ctl, int seq, hipStream_t s);
+                      const double* gsum, int nblock, int* act, int* ctl, int* host_ctl, int seq, hipStream_t s);
 // H = Z + b .* H
 void launch_h_update(int n, int t, const double* b, const double* Z, double* H, hipStream_t s);
 // a = rz / hv (hist[it*t + c] = a)  |  b = rz_new / rz, rz = rz_new (hist[it*t + c] = b);
@@ -284,6 +287,9 @@ void launch_grad_cols(const GradColsArgs& a, double* partials, double* out, hipS
 // dmll[i] = 0.5 * ( tr1_i + c_i * dW_i / dw_i - c_i * trP_i ).
 struct ModeDerivArgs {
   int n, m, t, lik;
+  int t_valid, t_all, stage;   // see mode_deriv_kernel; single rank: t_valid = t_all = t, stage 0
+  double* mom;                 // stages 1-3: n x 2 row sums (all-reduced between stages)
+  double* mom2;
   const int* nbr;
   const double* Bv;
   const double* dw;

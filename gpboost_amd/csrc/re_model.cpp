@@ -121,6 +121,7 @@ void REModelAMD::EnsureStructure() {
     BuildVecchiaStructure();
     if (cfg_.latent) {
       latent_.reset(new LatentVecchia(cfg_.n, cfg_.d, cfg_.num_neighbors, d_X_.get(), nbr_.data(), stream_));
+      latent_->SetShard(rank_, world_, coll_.get());   // probe columns over the ranks (§8e Option A)
       if (y_set_) latent_->SetY(y_vo_.data());
     }
     structure_built_ = true;
@@ -139,6 +140,7 @@ REModelAMD::~REModelAMD() {
   if (stream_) (void)hipStreamSynchronize(stream_);
   dense_.reset();
   latent_.reset();
+  coll_.reset();
   if (comm_) ncclCommDestroy(comm_);
   if (h_sums_) (void)hipHostFree(h_sums_);
   for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
@@ -163,25 +165,50 @@ void REModelAMD::BuildVecchiaStructure() {
   d_block_sums_.alloc((size_t)std::max(nblocks, 1) * kVecchiaSums);
 }
 
+// Exact Vecchia: rows (Vecchia order) split into `world` contiguous blocks, one all-reduce of the
+// six partial sums per evaluation. Latent Vecchia: every rank holds the whole factor and runs
+// its share of the probe columns (LatentVecchia::SetShard). Dense: replicas only.
+void REModelAMD::ApplyPartition(int rank, int world) {
+  if (world < 1 || rank < 0 || rank >= world) Fatal("invalid rank %d / world_size %d", rank, world);
+  if (!vecchia_ && world > 1) Fatal("the dense (gp_approx='none') path runs as replicas only; SetDistributed needs gp_approx='vecchia'");
+  rank_ = rank;
+  world_ = world;
+  const int n = cfg_.n;
+  if (cfg_.latent) {
+    row_begin_ = 0;
+    row_end_ = n;
+  } else {
+    const int base = n / world, rem = n % world;
+    row_begin_ = rank * base + std::min(rank, rem);
+    row_end_ = row_begin_ + base + (rank < rem ? 1 : 0);
+  }
+  structure_built_ = false;
+  EnsureStructure();
+  HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
 void REModelAMD::SetDistributed(int rank, int world, const ncclUniqueId& id, bool use_comm) {
   if (world < 1 || rank < 0 || rank >= world) Fatal("invalid rank %d / world_size %d", rank, world);
   UseDevice();
-  rank_ = rank;
-  world_ = world;
-  if (!vecchia_ && world > 1) Fatal("the dense (gp_approx='none') path runs as replicas only; SetDistributed needs gp_approx='vecchia'");
-  if (cfg_.latent && world > 1) Fatal("the latent Vecchia (iterative) path runs as replicas only in this build");
+  latent_.reset();   // holds a pointer to the collective
+  coll_.reset();
   if (comm_) { ncclCommDestroy(comm_); comm_ = nullptr; }
   if (world > 1 || use_comm) {
     ncclResult_t r = ncclCommInitRank(&comm_, world, id, rank);
     if (r != ncclSuccess) Fatal("ncclCommInitRank failed: %s", ncclGetErrorString(r));
+    coll_.reset(new RcclCollective(comm_));
   }
-  const int n = cfg_.n;
-  const int base = n / world, rem = n % world;
-  row_begin_ = rank * base + std::min(rank, rem);
-  row_end_ = row_begin_ + base + (rank < rem ? 1 : 0);
-  structure_built_ = false;
-  EnsureStructure();
-  HIP_CHECK(hipStreamSynchronize(stream_));
+  ApplyPartition(rank, world);
+}
+
+void REModelAMD::SetDistributedHost(int rank, int world, HostAllReduceFn fn, void* user) {
+  if (fn == nullptr) Fatal("SetDistributedHost: the all-reduce function is NULL");
+  UseDevice();
+  latent_.reset();
+  coll_.reset();
+  if (comm_) { ncclCommDestroy(comm_); comm_ = nullptr; }
+  coll_.reset(new HostCallbackCollective(fn, user));
+  ApplyPartition(rank, world);
 }
 
 void REModelAMD::TransformCovPars(const double* orig, double* trafo) const {
@@ -233,10 +260,9 @@ void REModelAMD::LaunchVecchiaRows(const double* trafo, int r0, int r1, double* 
   HIP_CHECK(hipEventRecord(ev_[0], stream_));
   launch_vecchia_rows(cfg_.cov_type, a, stream_);
   HIP_CHECK(hipEventRecord(ev_[1], stream_));
-  if (allreduce && comm_ != nullptr) {
+  if (allreduce && coll_ != nullptr) {
     launch_sum_blocks(d_block_sums_.get(), nblocks, kVecchiaSums, d_sums_.get(), stream_);
-    ncclResult_t r = ncclAllReduce(d_sums_.get(), d_sums_.get(), kVecchiaSums, ncclDouble, ncclSum, comm_, stream_);
-    if (r != ncclSuccess) Fatal("ncclAllReduce failed: %s", ncclGetErrorString(r));
+    coll_->AllReduceSum(d_sums_.get(), kVecchiaSums, stream_);
     HIP_CHECK(hipMemcpyAsync(h_sums_, d_sums_.get(), sizeof(double) * kVecchiaSums, hipMemcpyDeviceToHost, stream_));
   } else {   // one rank: the fixed-order block sum writes the pinned host buffer directly (no copy launch)
     launch_sum_blocks(d_block_sums_.get(), nblocks, kVecchiaSums, h_sums_dev_, stream_);

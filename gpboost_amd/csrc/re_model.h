@@ -15,6 +15,7 @@
 #include <string>
 #include <vector>
 
+#include "collective.h"
 #include "common.h"
 #include "dense.h"
 #include "latent.h"
@@ -65,6 +66,8 @@ class REModelAMD {
   EvalResult Eval(const double* cov_pars_orig, bool want_grad, int profile);
 
   void SetDistributed(int rank, int world, const ncclUniqueId& id, bool use_comm);
+  // Same partition, cross-rank sums through a host function instead of RCCL (test transport).
+  void SetDistributedHost(int rank, int world, HostAllReduceFn fn, void* user);
 
   // Partial sums over rows [r0, r1) of this model's row block, no all-reduce (EXTENSION API).
   void EvalVecchiaPartials(const double* cov_pars_orig, int r0, int r1, double* sums);
@@ -124,6 +127,8 @@ class REModelAMD {
   int rank_ = 0, world_ = 1;
   int row_begin_ = 0, row_end_ = 0;
   ncclComm_t comm_ = nullptr;
+  std::unique_ptr<Collective> coll_;   // RCCL (comm_) or host-callback sums; null = single rank
+  void ApplyPartition(int rank, int world);
 
   double last_nll_ = 0.;
   std::vector<double> last_cov_pars_;

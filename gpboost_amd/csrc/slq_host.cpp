@@ -6,15 +6,19 @@
 
 namespace gpb_amd {
 
-void gen_probes_normal(int n, int t, int seed, uint64_t run_id, double* R) {
+void gen_probes_normal_cols(int n, int c0, int c1, int ld, int seed, uint64_t run_id, double* R) {
   const uint32_t s32 = static_cast<uint32_t>(seed);
 #pragma omp parallel for schedule(dynamic, 1)
-  for (int c = 0; c < t; ++c) {
+  for (int c = c0; c < c1; ++c) {
     std::seed_seq seq{s32, static_cast<uint32_t>(run_id), static_cast<uint32_t>(run_id >> 32), static_cast<uint32_t>(c)};
     std::mt19937 gen(seq);
     std::normal_distribution<double> nd(0., 1.);
-    for (int i = 0; i < n; ++i) R[(size_t)i * t + c] = nd(gen);
+    for (int i = 0; i < n; ++i) R[(size_t)i * ld + (c - c0)] = nd(gen);
   }
+}
+
+void gen_probes_normal(int n, int t, int seed, uint64_t run_id, double* R) {
+  gen_probes_normal_cols(n, 0, t, t, seed, run_id, R);
 }
 
 namespace {
@@ -73,12 +77,19 @@ double e1_log_e1(std::vector<double> d, std::vector<double> e) {
 
 }  // namespace
 
-double slq_logdet(const std::vector<std::vector<double>>& diag, const std::vector<std::vector<double>>& offdiag,
-                  int n) {
+std::vector<double> slq_terms(const std::vector<std::vector<double>>& diag,
+                              const std::vector<std::vector<double>>& offdiag) {
   const int t = (int)diag.size();
   std::vector<double> per(t);
 #pragma omp parallel for schedule(dynamic, 1)
   for (int c = 0; c < t; ++c) per[c] = e1_log_e1(diag[c], offdiag[c]);
+  return per;
+}
+
+double slq_logdet(const std::vector<std::vector<double>>& diag, const std::vector<std::vector<double>>& offdiag,
+                  int n) {
+  const int t = (int)diag.size();
+  const std::vector<double> per = slq_terms(diag, offdiag);
   double ld = 0.;
   for (int c = 0; c < t; ++c) ld += per[c];
   return ld * n / t;

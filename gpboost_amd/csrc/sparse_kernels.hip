@@ -556,12 +556,13 @@ __global__ void cg_beta_kernel(int t, const double* rz_new, double* rz, const in
   if (hist) hist[c] = v;
 }
 
-__global__ void pcg_init_kernel(int t, int n_single, int pmax_single, int pmax_block, double zero_sq,
+// Columns >= n_valid are padding of a probe-sharded block: never active.
+__global__ void pcg_init_kernel(int t, int n_valid, int n_single, int pmax_single, int pmax_block, double zero_sq,
                                 const double* rr0, int* act, int* ctl) {
   if (threadIdx.x != 0) return;
   int any = 0;
   for (int c = 0; c < t; ++c) {
-    const int a = (c < n_single && rr0 && rr0[c] < zero_sq) ? 0 : 1;
+    const int a = (c >= n_valid || (c < n_single && rr0 && rr0[c] < zero_sq)) ? 0 : 1;
     act[c] = a;
     if (c < n_single) any |= a;
   }
@@ -572,9 +573,19 @@ __global__ void pcg_init_kernel(int t, int n_single, int pmax_single, int pmax_b
   ctl[kCtlNan] = 0;
 }
 
-// One thread, columns in a fixed order (the block mean is bitwise repeatable).
+// Sum of the block columns' norms of this rank (probe-sharded blocks: all-reduced before the check).
+__global__ void pcg_block_sum_kernel(int n_valid, int n_single, const double* rr, double* out) {
+  if (threadIdx.x != 0) return;
+  double norm = 0.;
+  for (int c = n_single; c < n_valid; ++c) norm += sqrt(rr[c]);
+  out[0] = norm;
+}
+
+// One thread, columns in a fixed order (the block mean is bitwise repeatable). gsum != null: the
+// block's norm sum over all ranks (pcg_block_sum_kernel + all-reduce) and its column count nblock.
 __global__ void pcg_check_kernel(int j, int t, int n_single, int pmax_single, int pmax_block, double delta,
-                                 const double* rr, int* act, int* ctl, int* host_ctl, int seq) {
+                                 const double* rr, const double* gsum, int nblock, int* act, int* ctl, int* host_ctl,
+                                 int seq) {
   if (threadIdx.x != 0) return;
   if (ctl[kCtlActS]) {
     ctl[kCtlItsS] = j + 1;
@@ -591,8 +602,12 @@ __global__ void pcg_check_kernel(int j, int t, int n_single, int pmax_single, in
   if (ctl[kCtlActB]) {
     ctl[kCtlItsB] = j + 1;
     double norm = 0.;
-    for (int c = n_single; c < t; ++c) norm += sqrt(rr[c]);
-    norm /= (t - n_single);
+    if (gsum) {
+      norm = gsum[0] / nblock;
+    } else {
+      for (int c = n_single; c < t; ++c) norm += sqrt(rr[c]);
+      norm /= (t - n_single);
+    }
     if (isnan(norm) || isinf(norm)) ctl[kCtlNan] = 1;
     if (norm < delta || j + 1 >= pmax_block) {
       for (int c = n_single; c < t; ++c) act[c] = 0;
@@ -785,35 +800,53 @@ __global__ void __launch_bounds__(kBT) mode_deriv_kernel(ModeDerivArgs a, int sh
     // pass 1: row means of z1 = U dW P and zP = (BP)^2 dW over the t probes
     // (c_var == 0 -> c = 1, CG_utils.cpp:1036-1039).
     double s1 = 0., sP = 0.;
-    for (int c = lane; c < t; c += T) {
-      const size_t o = (size_t)i * t + c;
-      double bp = a.P[o];
-      for (int r = 0; r < k; ++r) bp = fma(bv[r], a.P[(size_t)nb[r] * t + c], bp);
-      s1 += a.U[o] * dWi * a.P[o];
-      sP += bp * dWi * bp;
+    if (a.stage < 2) {
+      for (int c = lane; c < a.t_valid; c += T) {
+        const size_t o = (size_t)i * t + c;
+        double bp = a.P[o];
+        for (int r = 0; r < k; ++r) bp = fma(bv[r], a.P[(size_t)nb[r] * t + c], bp);
+        s1 += a.U[o] * dWi * a.P[o];
+        sP += bp * dWi * bp;
+      }
+      for (int off = T >> 1; off > 0; off >>= 1) {
+        s1 += __shfl_xor(s1, off, 64);
+        sP += __shfl_xor(sP, off, 64);
+      }
+      if (a.stage == 1) {   // sharded: this rank's column sums, all-reduced by the caller
+        if (lane == 0) { a.mom[2 * (size_t)i] = s1; a.mom[2 * (size_t)i + 1] = sP; }
+        continue;
+      }
+    } else {
+      s1 = a.mom[2 * (size_t)i];
+      sP = a.mom[2 * (size_t)i + 1];
     }
-    for (int off = T >> 1; off > 0; off >>= 1) {
-      s1 += __shfl_xor(s1, off, 64);
-      sP += __shfl_xor(sP, off, 64);
-    }
-    const double tr1 = s1 / t, trP = sP / t;
+    const double tr1 = s1 / a.t_all, trP = sP / a.t_all;
     // pass 2: centred covariance / variance -> optimal c (CalcOptimalCVectorized)
     double cv = 0., vv = 0.;
-    for (int c = lane; c < t; c += T) {
-      const size_t o = (size_t)i * t + c;
-      double bp = a.P[o];
-      for (int r = 0; r < k; ++r) bp = fma(bv[r], a.P[(size_t)nb[r] * t + c], bp);
-      const double z1 = a.U[o] * dWi * a.P[o] - tr1;
-      const double zP = bp * dWi * bp - trP;
-      cv += z1 * zP;
-      vv += zP * zP;
+    if (a.stage < 3) {
+      for (int c = lane; c < a.t_valid; c += T) {
+        const size_t o = (size_t)i * t + c;
+        double bp = a.P[o];
+        for (int r = 0; r < k; ++r) bp = fma(bv[r], a.P[(size_t)nb[r] * t + c], bp);
+        const double z1 = a.U[o] * dWi * a.P[o] - tr1;
+        const double zP = bp * dWi * bp - trP;
+        cv += z1 * zP;
+        vv += zP * zP;
+      }
+      for (int off = T >> 1; off > 0; off >>= 1) {
+        cv += __shfl_xor(cv, off, 64);
+        vv += __shfl_xor(vv, off, 64);
+      }
+      if (a.stage == 2) {   // sharded: centred sums of this rank
+        if (lane == 0) { a.mom2[2 * (size_t)i] = cv; a.mom2[2 * (size_t)i + 1] = vv; }
+        continue;
+      }
+    } else {
+      cv = a.mom2[2 * (size_t)i];
+      vv = a.mom2[2 * (size_t)i + 1];
     }
-    for (int off = T >> 1; off > 0; off >>= 1) {
-      cv += __shfl_xor(cv, off, 64);
-      vv += __shfl_xor(vv, off, 64);
-    }
-    cv /= t;
-    vv /= t;
+    cv /= a.t_all;
+    vv /= a.t_all;
     const double copt = (vv == 0.) ? 1. : cv / vv;
     if (lane == 0) a.dmll[i] = 0.5 * (tr1 + copt * (dWi / a.dw[i]) - copt * trP);
   }
@@ -970,17 +1003,22 @@ void launch_h_update(int n, int t, const double* b, const double* Z, double* H, 
   HIP_CHECK(hipGetLastError());
 }
 
-void launch_pcg_init(int t, int n_single, int pmax_single, int pmax_block, double zero_sq, const double* rr0,
-                     int* act, int* ctl, hipStream_t s) {
-  hipLaunchKernelGGL(pcg_init_kernel, dim3(1), dim3(64), 0, s, t, n_single, pmax_single, pmax_block, zero_sq, rr0, act,
-                     ctl);
+void launch_pcg_init(int t, int n_valid, int n_single, int pmax_single, int pmax_block, double zero_sq,
+                     const double* rr0, int* act, int* ctl, hipStream_t s) {
+  hipLaunchKernelGGL(pcg_init_kernel, dim3(1), dim3(64), 0, s, t, n_valid, n_single, pmax_single, pmax_block, zero_sq,
+                     rr0, act, ctl);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_pcg_block_sum(int n_valid, int n_single, const double* rr, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(pcg_block_sum_kernel, dim3(1), dim3(64), 0, s, n_valid, n_single, rr, out);
   HIP_CHECK(hipGetLastError());
 }
 
 void launch_pcg_check(int j, int t, int n_single, int pmax_single, int pmax_block, double delta, const double* rr,
-                      int* act, int* ctl, int* host_ctl, int seq, hipStream_t s) {
-  hipLaunchKernelGGL(pcg_check_kernel, dim3(1), dim3(64), 0, s, j, t, n_single, pmax_single, pmax_block, delta, rr, act,
-                     ctl, host_ctl, seq);
+                      const double* gsum, int nblock, int* act, int* ctl, int* host_ctl, int seq, hipStream_t s) {
+  hipLaunchKernelGGL(pcg_check_kernel, dim3(1), dim3(64), 0, s, j, t, n_single, pmax_single, pmax_block, delta, rr,
+                     gsum, nblock, act, ctl, host_ctl, seq);
   HIP_CHECK(hipGetLastError());
 }
 

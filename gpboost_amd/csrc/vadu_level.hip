@@ -235,10 +235,10 @@ __global__ void __launch_bounds__(256) merged_level1_kernel(MergedSolve ms, cons
 // Shape knobs (A/B only): GPBOOST_AMD_LEVELT_FORM = chunk (default: merged_levelR, coalesced
 // structure + readlane), gather (merged_levelT: per-entry structure loads) or wave (merged_levelW,
 // one wave per row); GPBOOST_AMD_LEVELT_NW = waves per row of the workgroup forms (1, 2, 4 default,
-// 8); GPBOOST_AMD_LEVEL1_G = lanes per row at t = 1 (16, 32 or 64; default 64). Other values:
+// 8); GPBOOST_AMD_LEVELT_CH = entries per chunk of the chunk form (8, 16 default, 32); GPBOOST_AMD_LEVEL1_G = lanes per row at t = 1 (16, 32 or 64; default 64). Other values:
 // error.
 struct LevelShape {
-  int form = 0, nw = 4, g = 64;   // form 0 chunk, 1 gather, 2 wave
+  int form = 0, nw = 4, ch = 16, g = 64;   // form 0 chunk, 1 gather, 2 wave
 };
 const LevelShape& level_shape() {
   static const LevelShape v = [] {
@@ -257,6 +257,11 @@ const LevelShape& level_shape() {
         Fatal("GPBOOST_AMD_LEVELT_NW must be 1, 2, 4 or 8 (got '%s')", e);
       Info("tail level kernels: %d wave(s) per row at t >= 2", k.nw);
     }
+    if (const char* e = std::getenv("GPBOOST_AMD_LEVELT_CH")) {
+      k.ch = std::atoi(e);
+      if (k.ch != 8 && k.ch != 16 && k.ch != 32) Fatal("GPBOOST_AMD_LEVELT_CH must be 8, 16 or 32 (got '%s')", e);
+      Info("tail level kernels: chunks of %d entries", k.ch);
+    }
     if (const char* e = std::getenv("GPBOOST_AMD_LEVEL1_G")) {
       k.g = std::atoi(e);
       if (k.g != 16 && k.g != 32 && k.g != 64) Fatal("GPBOOST_AMD_LEVEL1_G must be 16, 32 or 64 (got '%s')", e);
@@ -265,6 +270,21 @@ const LevelShape& level_shape() {
     return k;
   }();
   return v;
+}
+
+template <int NW>
+void launch_chunk_nw(int ch, dim3 g, dim3 b, hipStream_t s, const MergedSolve& ms, const double* coef, int p0,
+                     const double* in, double* X, int t) {
+  if (ch == 8) hipLaunchKernelGGL((merged_levelR_kernel<NW, 8>), g, b, 0, s, ms, coef, p0, in, X, t);
+  else if (ch == 32) hipLaunchKernelGGL((merged_levelR_kernel<NW, 32>), g, b, 0, s, ms, coef, p0, in, X, t);
+  else hipLaunchKernelGGL((merged_levelR_kernel<NW, 16>), g, b, 0, s, ms, coef, p0, in, X, t);
+}
+void launch_chunk(int nw, int ch, dim3 g, dim3 b, hipStream_t s, const MergedSolve& ms, const double* coef, int p0,
+                  const double* in, double* X, int t) {
+  if (nw == 1) launch_chunk_nw<1>(ch, g, b, s, ms, coef, p0, in, X, t);
+  else if (nw == 2) launch_chunk_nw<2>(ch, g, b, s, ms, coef, p0, in, X, t);
+  else if (nw == 8) launch_chunk_nw<8>(ch, g, b, s, ms, coef, p0, in, X, t);
+  else launch_chunk_nw<4>(ch, g, b, s, ms, coef, p0, in, X, t);
 }
 
 void launch_level(const MergedSolve& ms, const double* coef, int p0, int cnt, const double* in, double* X, int t,
@@ -292,10 +312,7 @@ void launch_level(const MergedSolve& ms, const double* coef, int p0, int cnt, co
     else hipLaunchKernelGGL((merged_levelT_kernel<4, 16>), g, b, 0, s, ms, coef, p0, in, X, t);
     return;
   }
-  if (ks.nw == 1) hipLaunchKernelGGL((merged_levelR_kernel<1, 32>), g, b, 0, s, ms, coef, p0, in, X, t);
-  else if (ks.nw == 2) hipLaunchKernelGGL((merged_levelR_kernel<2, 16>), g, b, 0, s, ms, coef, p0, in, X, t);
-  else if (ks.nw == 8) hipLaunchKernelGGL((merged_levelR_kernel<8, 8>), g, b, 0, s, ms, coef, p0, in, X, t);
-  else hipLaunchKernelGGL((merged_levelR_kernel<4, 16>), g, b, 0, s, ms, coef, p0, in, X, t);
+  launch_chunk(ks.nw, ks.ch, g, b, s, ms, coef, p0, in, X, t);
 }
 
 }  // namespace

@@ -223,13 +223,21 @@ GPBOOST_AMD_EXPORT int GPB_BenchLatentOperators(REModelHandle handle, int t, int
 GPBOOST_AMD_EXPORT int GPB_CommIdSize(void);
 /* Create a communicator id on one rank (to be broadcast to all ranks by the caller). */
 GPBOOST_AMD_EXPORT int GPB_CommCreateId(char* id_out);
-/* Join the model to an RCCL communicator: rows (observations in Vecchia order) are
- * split into world_size contiguous blocks; this rank evaluates block `rank` and the
+/* Join the model to an RCCL communicator. Exact Vecchia: rows (observations in Vecchia order)
+ * are split into world_size contiguous blocks; this rank evaluates block `rank` and the
  * per-rank partial sums are all-reduced over RCCL (one all-reduce of 6 doubles per
- * evaluation). Must be called before the first evaluation. comm_id may be NULL only at
- * world_size 1 (no communicator); a non-NULL id at world_size 1 creates a one-rank
- * communicator (same data path). */
+ * evaluation). Latent Vecchia (iterative): every rank holds the whole factor and runs its
+ * share of the num_rand_vec_trace probe columns; one all-reduce of 1 double per PCG iteration
+ * (block stopping rule) and of the per-probe terms at the end (SURVEY.md §8e Option A).
+ * Must be called before the first evaluation. comm_id may be NULL only at world_size 1 (no
+ * communicator); a non-NULL id at world_size 1 creates a one-rank communicator (same data
+ * path). */
 GPBOOST_AMD_EXPORT int GPB_SetDistributed(REModelHandle handle, int rank, int world_size, const char* comm_id);
+/* As GPB_SetDistributed, with the cross-rank sums done by `allreduce` on host buffers (it must
+ * replace buf[0..count) by the element-wise sum over all ranks, e.g. a gloo all-reduce) instead
+ * of RCCL: a transport for tests with several ranks on one GPU, where RCCL refuses to run. */
+GPBOOST_AMD_EXPORT int GPB_SetDistributedHostReduce(REModelHandle handle, int rank, int world_size,
+    void (*allreduce)(double* buf, int count, void* user), void* user);
 /* The six per-row partial sums over Vecchia rows [row_begin, row_end) at cov_pars (original
  * scale), without any all-reduce: for callers that run their own communication. The
  * response must have been set by a previous evaluation. */
