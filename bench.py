@@ -12,7 +12,8 @@ portable LCG (gpboost_amd/synthetic.py).
 N > 1 is launched by torch.distributed.run (one process per GPU): observations (rows in
 Vecchia order) are split into N contiguous blocks, every rank evaluates its rows, and the
 six partial sums are all-reduced over RCCL inside the library (strong scaling: the total
-problem is fixed). Rank 0 prints ONE JSON line.
+problem is fixed). The secondary latent/iterative leg runs at N > 1 with its probe columns
+sharded over the ranks (SURVEY.md §8e Option A). Rank 0 prints ONE JSON line.
 """
 from __future__ import annotations
 
@@ -202,6 +203,63 @@ def latent_leg(X, Y, steps: int, cpu: bool) -> dict:
     return leg
 
 
+def host_transport() -> bool:
+    """GPBOOST_AMD_BENCH_TRANSPORT=host (rehearsal of the N > 1 flow on a one-GPU box): every
+    rank on device 0, cross-rank sums through a gloo all-reduce instead of RCCL."""
+    return os.environ.get("GPBOOST_AMD_BENCH_TRANSPORT", "rccl") == "host"
+
+
+def join_ranks(gm, rank: int, world: int, dist) -> None:
+    if host_transport():
+        import torch
+
+        def allreduce(a):
+            dist.all_reduce(torch.from_numpy(a), op=dist.ReduceOp.SUM)
+        gm.set_distributed_host(rank, world, allreduce)
+        return
+    from gpboost_amd import comm_create_id
+    obj = [comm_create_id() if rank == 0 else None]
+    dist.broadcast_object_list(obj, src=0)
+    gm.set_distributed(rank, world, obj[0])
+
+
+def latent_leg_sharded(X, Y, steps: int, rank: int, world: int, dist) -> dict | None:
+    """The latent leg at N > 1: probe columns sharded over the ranks (SURVEY.md §8e Option A,
+    RCCL inside the library: one all-reduce of 1 double per PCG iteration + the per-probe terms
+    at the end); every rank times its evaluations, the max over ranks is reported."""
+    import numpy as np
+    import torch
+
+    from gpboost_amd import GPModel
+    gm = GPModel(gp_coords=X, likelihood="gaussian", cov_function="exponential", gp_approx="vecchia_latent",
+                 num_neighbors=M_NEIGHBORS, vecchia_ordering="random", seed=0, matrix_inversion_method="iterative")
+    gm.set_optim_params(dict(num_rand_vec_trace=LATENT_T, init_aux_pars=[0.1]))
+    join_ranks(gm, rank, world, dist)
+    nll, g, _ = gm.neg_log_likelihood_and_grad(LATENT_PARS, Y)          # construction + first eval (warm-up)
+    dist.barrier()
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        nll, g, _ = gm.neg_log_likelihood_and_grad(LATENT_PARS, None)
+        ts.append(time.perf_counter() - t0)
+    t = torch.tensor([float(np.median(ts))], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    info = gm.last_iteration_info()
+    t_med = float(t.item())
+    if rank != 0:
+        return None
+    return {
+        "metric": "latent Vecchia iterative neg-log-lik + grad evals/sec, n=100k m=30",
+        "value": 1.0 / t_med, "unit": "evals/s", "n_gpus": world, "steps": steps, "ms_per_step": t_med * 1e3,
+        "scaling": "strong",
+        "config": {"workload": "vecchia_latent_gaussian_iterative_vadu", "n": X.shape[0],
+                   "num_neighbors": M_NEIGHBORS, "cov_pars": LATENT_PARS, "aux": 0.1,
+                   "num_rand_vec_trace": LATENT_T, "cg_delta_conv": 1e-2, "preconditioner": "vadu",
+                   "parallelism": f"probes{world}", "nll": nll, "grad": [float(x) for x in g],
+                   "newton_its": int(info[0]), "cg_its_block": int(info[2])},
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -215,7 +273,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    os.environ["GPBOOST_AMD_DEVICE"] = str(local_rank)
+    os.environ["GPBOOST_AMD_DEVICE"] = "0" if host_transport() else str(local_rank)
 
     dist = None
     if world > 1:
@@ -224,7 +282,7 @@ def main():
 
     import numpy as np
 
-    from gpboost_amd import GPModel, comm_create_id, synthetic
+    from gpboost_amd import GPModel, synthetic
 
     X = synthetic.bench_coords(N_DATA)
     Y = synthetic.bench_gaussian_y(N_DATA)
@@ -232,11 +290,7 @@ def main():
     gm = GPModel(gp_coords=X, cov_function="exponential", gp_approx="vecchia", num_neighbors=M_NEIGHBORS,
                  vecchia_ordering="random", seed=0)
     if world > 1:
-        import torch
-        cid = comm_create_id() if rank == 0 else None
-        obj = [cid]
-        dist.broadcast_object_list(obj, src=0)
-        gm.set_distributed(rank, world, obj[0])
+        join_ranks(gm, rank, world, dist)
     gm.neg_log_likelihood_and_grad(THETA, Y, profile_sigma2=True)   # SetY + neighbour search + first eval
     t_construct = time.perf_counter() - t0
 
@@ -253,12 +307,16 @@ def main():
     for _ in range(min(args.steps, 20)):
         gm.neg_log_likelihood_and_grad(THETA, None, profile_sigma2=True)
         kms.append(gm.last_kernel_ms())
+    latent_sharded = None
     if dist is not None:
         import torch
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
         dist.barrier()
+        if not args.no_latent:   # every rank takes part (probe-sharded latent leg)
+            latent_sharded = latent_leg_sharded(X, Y, args.latent_steps, rank, world, dist)
+            dist.barrier()
     if rank != 0:
         dist.destroy_process_group()
         return
@@ -305,6 +363,8 @@ def main():
     if world == 1 and not args.no_latent:
         del gm
         line["latent_iterative"] = latent_leg(X, Y, args.latent_steps, not args.no_cpu_baseline)
+    elif latent_sharded is not None:
+        line["latent_iterative"] = latent_sharded
     print(json.dumps(line))
     if dist is not None:
         dist.destroy_process_group()
