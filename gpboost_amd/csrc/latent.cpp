@@ -206,6 +206,23 @@ void LatentVecchia::BuildStructure(const int* nbr) {
     HIP_CHECK(hipMemcpy(d_longr_.get(), longr.data(), sizeof(int) * longr.size(), hipMemcpyHostToDevice));
   sp_.longr = d_longr_.get();
   sp_.nlong = (int)longr.size();
+  {   // length buckets of the transposed lists (bt_apply1b_kernel)
+    std::vector<int> order;
+    order.reserve(n);
+    const int lim[4] = {kLongRow, 32, 16, -1};   // bucket b: length in (lim[b], lim[b-1]]
+    for (int b = 0; b < 4; ++b) {
+      const size_t before = order.size();
+      for (int j = 0; j < n; ++j) {
+        const int len = tptr[j + 1] - tptr[j];
+        const int hi = b == 0 ? INT32_MAX : lim[b - 1];
+        if (len > lim[b] && len <= hi) order.push_back(j);
+      }
+      sp_.nbkt[b] = (int)(order.size() - before);
+    }
+    d_border_.alloc(std::max<size_t>(order.size(), 1));
+    HIP_CHECK(hipMemcpy(d_border_.get(), order.data(), sizeof(int) * order.size(), hipMemcpyHostToDevice));
+    sp_.border = d_border_.get();
+  }
 }
 
 void LatentVecchia::SetY(const double* y_vo) {

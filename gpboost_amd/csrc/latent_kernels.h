@@ -45,6 +45,10 @@ struct SparseB {
   // neighbours of hundreds of later rows): the t = 1 operator gives each a whole wave
   const int* longr;
   int nlong;
+  // every row j in bucket order: lists longer than kLongRow, then (32, 64], (16, 32], [0, 16]
+  // entries (ascending row within a bucket); nbkt = the four bucket sizes (t = 1 operator)
+  const int* border;
+  int nbkt[4];
 };
 constexpr int kLongRow = 64;
 

@@ -92,18 +92,25 @@ __global__ void __launch_bounds__(256) transpose_kernel(int ld, const double* __
 //   UPPER (A = G^T, upper): Y[i] = (sum_{k >= i} A(i, k) X[k]) / dw[row[i]]
 //   !UPPER (A = G, lower):  Y[row[i]] = sum_{k <= i} A(i, k) X[k]   (scattered to the storage rows)
 // Workgroup = 16 output rows x 32 columns (two 16 x 16 f64 MFMA tiles); the tile's k range (the
-// structural zeros skipped) is split over 8 waves in whole trips of 8, ascending k, loads of the
+// structural zeros skipped) is split over 8 waves in whole trips, ascending k, loads of the
 // next trip issued before the current trip's MFMAs; the partial tiles are combined through LDS
 // in a fixed wave order (bitwise repeatable).
 constexpr int kApplyWaves = 8;
+#ifndef GPB_APPLY_U
+#define GPB_APPLY_U 8
+#endif
+// k steps of 4 per trip: a trip is 4 kApplyU k values, 2 kApplyU MFMAs; the loads of the next
+// trip are in flight during the current trip's MFMAs. Trips of 8 k (kApplyU = 2) left the
+// products bound by one load round trip per 4 MFMAs (25 us per product at K0 = 2048).
+constexpr int kApplyU = GPB_APPLY_U;
 struct ApplyTrip {
-  double a[2], b0[2], b1[2];
+  double a[kApplyU], b0[kApplyU], b1[kApplyU];
 };
 __device__ __forceinline__ void apply_load(const double* __restrict__ A, const double* __restrict__ X, int ld, int t,
                                            int ai, int kl, int cA, int cB, bool okA, bool okB, int k, int ke,
                                            ApplyTrip& tr) {
 #pragma unroll
-  for (int u = 0; u < 2; ++u) {
+  for (int u = 0; u < kApplyU; ++u) {
     const int kk = k + 4 * u + kl;
     const bool ok = kk < ke;
     tr.a[u] = ok ? A[(size_t)ai + (size_t)kk * ld] : 0.;
@@ -123,7 +130,8 @@ __global__ void __launch_bounds__(kApplyWaves * 64) dense_head_apply_kernel(Dens
   const int i0 = blockIdx.x * 16;
   const int c0 = blockIdx.y * 32;
   const int kt0 = UPPER ? i0 : 0, kt1 = UPPER ? K0 : min(i0 + 16, K0);
-  const int per = ((kt1 - kt0 + kApplyWaves * 8 - 1) / (kApplyWaves * 8)) * 8;
+  constexpr int trip = 4 * kApplyU;
+  const int per = ((kt1 - kt0 + kApplyWaves * trip - 1) / (kApplyWaves * trip)) * trip;
   const int kb = kt0 + wave * per, ke = min(kb + per, kt1);
   const int ai = i0 + (lane & 15);
   const int kl = lane >> 4;
@@ -132,10 +140,10 @@ __global__ void __launch_bounds__(kApplyWaves * 64) dense_head_apply_kernel(Dens
   double4_t acc0 = {0., 0., 0., 0.}, acc1 = {0., 0., 0., 0.};
   ApplyTrip cur, nxt;
   if (kb < ke) apply_load(A, X, ld, t, ai, kl, cA, cB, okA, okB, kb, ke, cur);
-  for (int k = kb; k < ke; k += 8) {
-    if (k + 8 < ke) apply_load(A, X, ld, t, ai, kl, cA, cB, okA, okB, k + 8, ke, nxt);
+  for (int k = kb; k < ke; k += trip) {
+    if (k + trip < ke) apply_load(A, X, ld, t, ai, kl, cA, cB, okA, okB, k + trip, ke, nxt);
 #pragma unroll
-    for (int u = 0; u < 2; ++u) {
+    for (int u = 0; u < kApplyU; ++u) {
       acc0 = __builtin_amdgcn_mfma_f64_16x16x4f64(cur.a[u], cur.b0[u], acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f64_16x16x4f64(cur.a[u], cur.b1[u], acc1, 0, 0, 0);
     }

@@ -119,7 +119,9 @@ __device__ __forceinline__ int packed(int r, int c) {  // r >= c
 // over its row groups: [gather, pairs, gj, dca, reduce, iterations].
 __device__ unsigned long long g_rows_prof[8];
 
-template <int K, int COV, bool PROF = false>
+// MK <= K: matrix rows (= elimination steps); lanes r >= MK of a group only take part in the
+// wave-level operations (m <= 30 with K = 32: the two identity-padding steps are not run).
+template <int K, int COV, bool PROF = false, int MK = K>
 __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(VecchiaRowsArgs a) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int BT = block_threads<K>();
@@ -224,12 +226,12 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
     mark(1);
 
     // ---- 2. symmetric Gauss-Jordan on [C | c | y_nbr], row r in registers
-    double row[K];
+    double row[MK];
 #pragma unroll
-    for (int c = 0; c < K; ++c) row[c] = (c <= r) ? Cp[packed(r, c)] : Cp[packed(c, r)];
+    for (int c = 0; c < MK; ++c) row[c] = (c <= r) ? Cp[packed(r, c)] : Cp[packed(c, r)];
     double aug1 = cvec, aug2 = ynb;
 #pragma unroll
-    for (int j = 0; j < K; ++j) {
+    for (int j = 0; j < MK; ++j) {
       compiler_fence();
       slot_c[r] = row[j];
       slot_a1[r] = aug1;
@@ -245,18 +247,18 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
       aug1 = fma(-f, slot_a1[j], aug1);
       aug2 = fma(-f, slot_a2[j], aug2);
 #pragma unroll
-      for (int c = j + 1; c < K; ++c) row[c] = fma(-f, slot_c[c], row[c]);
+      for (int c = j + 1; c < MK; ++c) row[c] = fma(-f, slot_c[c], row[c]);
       // Pin this step's updates here: without it the scheduler defers each column's FMAs to
       // the step that consumes it and keeps every broadcast value live (register blow-up).
 #pragma unroll
-      for (int c = j + 1; c < K; ++c) asm volatile("" : "+v"(row[c]));
+      for (int c = j + 1; c < MK; ++c) asm volatile("" : "+v"(row[c]));
       asm volatile("" : "+v"(aug1), "+v"(aug2));
     }
     double mydiag = row[0];
 #pragma unroll
-    for (int c = 1; c < K; ++c) mydiag = (c == r) ? row[c] : mydiag;
-    const double av_r = aug1 / mydiag;   // a = C^-1 c
-    const double vv_r = aug2 / mydiag;   // v = C^-1 y_nbr
+    for (int c = 1; c < MK; ++c) mydiag = (c == r) ? row[c] : mydiag;
+    const double av_r = rv ? aug1 / mydiag : 0.;   // a = C^-1 c (lanes r >= MK hold no row)
+    const double vv_r = rv ? aug2 / mydiag : 0.;   // v = C^-1 y_nbr
 
     if (active && a.B_out != nullptr && r < a.m) a.B_out[(size_t)i * a.m + r] = rv ? -av_r : 0.;
     mark(2);
@@ -269,7 +271,7 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
     // all K columns, unrolled with four partial sums
     double tq[4] = {0., 0., 0., 0.};
 #pragma unroll
-    for (int c = 0; c < K; ++c) {
+    for (int c = 0; c < MK; ++c) {
       const double dcrc = (c < r) ? dCp[packed(r, c)] : dCp[packed(c, r)];
       tq[c & 3] = fma(dcrc, slot_c[c], tq[c & 3]);
     }
@@ -619,6 +621,13 @@ void launch_k(const VecchiaRowsArgs& a, hipStream_t s) {
   size_t lds = (size_t)rpb * group_lds_doubles<K>() * sizeof(double);
   if (lds < red) lds = red;
   static const bool prof = std::getenv("GPBOOST_AMD_ROWS_PROF") != nullptr;
+  if constexpr (K == 32) {
+    if (!prof && a.m <= 30) {   // the headline configuration (m = 30): 30 elimination steps
+      hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, 30>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
+      HIP_CHECK(hipGetLastError());
+      return;
+    }
+  }
   if (prof) {
     hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, true>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
     unsigned long long h[8];
