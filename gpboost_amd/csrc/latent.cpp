@@ -206,22 +206,23 @@ void LatentVecchia::BuildStructure(const int* nbr) {
     HIP_CHECK(hipMemcpy(d_longr_.get(), longr.data(), sizeof(int) * longr.size(), hipMemcpyHostToDevice));
   sp_.longr = d_longr_.get();
   sp_.nlong = (int)longr.size();
-  {   // length buckets of the transposed lists (bt_apply1b_kernel)
-    std::vector<int> order;
-    order.reserve(n);
-    const int lim[4] = {kLongRow, 32, 16, -1};   // bucket b: length in (lim[b], lim[b-1]]
-    for (int b = 0; b < 4; ++b) {
-      const size_t before = order.size();
-      for (int j = 0; j < n; ++j) {
-        const int len = tptr[j + 1] - tptr[j];
-        const int hi = b == 0 ? INT32_MAX : lim[b - 1];
-        if (len > lim[b] && len <= hi) order.push_back(j);
+  {   // t = 1 form of B: ELL, column-major (SparseB)
+    std::vector<int> eidx((size_t)m * n), eslot((size_t)m * n);
+    for (int i = 0; i < n; ++i) {
+      const int k = std::min(i, m);
+      for (int r = 0; r < m; ++r) {
+        eidx[(size_t)r * n + i] = r < k ? nbr[(size_t)i * m + r] : i;
+        eslot[(size_t)r * n + i] = r < k ? i * m + r : -1;
       }
-      sp_.nbkt[b] = (int)(order.size() - before);
     }
-    d_border_.alloc(std::max<size_t>(order.size(), 1));
-    HIP_CHECK(hipMemcpy(d_border_.get(), order.data(), sizeof(int) * order.size(), hipMemcpyHostToDevice));
-    sp_.border = d_border_.get();
+    d_ell_idx_.alloc(eidx.size());
+    d_ell_slot_.alloc(eslot.size());
+    d_ell_val_.alloc(eidx.size());
+    HIP_CHECK(hipMemcpy(d_ell_idx_.get(), eidx.data(), sizeof(int) * eidx.size(), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_ell_slot_.get(), eslot.data(), sizeof(int) * eslot.size(), hipMemcpyHostToDevice));
+    sp_.ell_idx = d_ell_idx_.get();
+    sp_.ell_val = d_ell_val_.get();
+    sp_.vals_of = nullptr;
   }
 }
 
@@ -550,6 +551,8 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
   pre_->Refresh(d_Bv_.get());   // preconditioner plan values, dense head inverse
   launch_gather(tnnz_, d_tslot_.get(), d_Bv_.get(), d_tval_.get(), s_);   // B^T operator values, list order
   sp_.tval_of = d_Bv_.get();
+  launch_gather(n * m_, d_ell_slot_.get(), d_Bv_.get(), d_ell_val_.get(), s_);   // t = 1 form of B
+  sp_.vals_of = d_Bv_.get();
   factor_ready_ = true;
 
   Block& b1 = GetBlock(0, 1, std::max(cfg.cg_max_num_it, 1));

@@ -127,7 +127,9 @@ class LatentVecchia {
   DevBuf<double> d_tval_;       // B values in transposed-list order (refreshed per evaluation)
   int tnnz_ = 0;
   SparseB sp_{};
-  DevBuf<int> d_nbr_, d_tptr_, d_trow_, d_tslot_, d_longr_, d_border_;
+  DevBuf<int> d_nbr_, d_tptr_, d_trow_, d_tslot_, d_longr_;
+  DevBuf<int> d_ell_idx_, d_ell_slot_;
+  DevBuf<double> d_ell_val_;
   int dense_rows_ = 0, head_rows_ = 0;   // VADU plan split (VaduPrecond)
   std::unique_ptr<VaduPrecond> pre_;
   DevBuf<double> d_y_, d_Bv_, d_dBv_, d_Dinv_, d_dD_, d_W_, d_dw_, d_sdw_, d_d1_;

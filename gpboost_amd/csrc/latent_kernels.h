@@ -45,10 +45,12 @@ struct SparseB {
   // neighbours of hundreds of later rows): the t = 1 operator gives each a whole wave
   const int* longr;
   int nlong;
-  // every row j in bucket order: lists longer than kLongRow, then (32, 64], (16, 32], [0, 16]
-  // entries (ascending row within a bucket); nbkt = the four bucket sizes (t = 1 operator)
-  const int* border;
-  int nbkt[4];
+  // t = 1 default form of B: ELL stored column-major (entry r of row i at r n + i), so a wave's
+  // loads of entry r of 64 rows are coalesced and its gathers are the r-th neighbours of 64
+  // spatially close rows (Morton storage). Values refreshed per factor (vals_of = their source).
+  const int* ell_idx;
+  const double* ell_val;
+  const double* vals_of;
 };
 constexpr int kLongRow = 64;
 

@@ -365,7 +365,7 @@ __device__ __forceinline__ void bt_long_row(int j, const int* __restrict__ tptr,
   }
 }
 
-template <int G, int R>
+template <int G, int R, int E>
 __global__ void __launch_bounds__(kBT) bt_apply1m_kernel(int n, const int* __restrict__ tptr,
                                                          const int* __restrict__ trow,
                                                          const double* __restrict__ tval, int unit,
@@ -382,8 +382,8 @@ __global__ void __launch_bounds__(kBT) bt_apply1m_kernel(int n, const int* __res
   constexpr int NG = kBT / G;
   const int lane = threadIdx.x & (G - 1);
   const int base = xcd_block(blockIdx.x, nmain) * (NG * R) + (int)threadIdx.x / G;
-  int e0[R], e1[R], id[R][2];
-  double w[R][2], g[R][2], xs[R], wv[R], hv[R];
+  int e0[R], e1[R], id[R][E];
+  double w[R][E], g[R][E], xs[R], wv[R], hv[R];
 #pragma unroll
   for (int q = 0; q < R; ++q) {
     const int j = base + q * NG;
@@ -398,7 +398,7 @@ __global__ void __launch_bounds__(kBT) bt_apply1m_kernel(int n, const int* __res
 #pragma unroll
   for (int q = 0; q < R; ++q)
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
+    for (int e = 0; e < E; ++e) {
       const int ee = e0[q] + lane + e * G;
       const bool ok = ee < e1[q];
       id[q][e] = ok ? trow[ee] : 0;
@@ -407,14 +407,16 @@ __global__ void __launch_bounds__(kBT) bt_apply1m_kernel(int n, const int* __res
 #pragma unroll
   for (int q = 0; q < R; ++q)
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
+    for (int e = 0; e < E; ++e) {
       g[q][e] = X[id[q][e]];
       if (pre) w[q][e] *= pre[id[q][e]];
     }
 #pragma unroll
   for (int q = 0; q < R; ++q) {
-    double acc = fma(w[q][1], g[q][1], w[q][0] * g[q][0]);
-    for (int ee = e0[q] + lane + 2 * G; ee < e1[q]; ee += G) {   // rows with > 2G entries
+    double acc = w[q][0] * g[q][0];
+#pragma unroll
+    for (int e = 1; e < E; ++e) acc = fma(w[q][e], g[q][e], acc);
+    for (int ee = e0[q] + lane + E * G; ee < e1[q]; ee += G) {   // rows with > E G entries
       const int i = trow[ee];
       acc = fma(pre ? tval[ee] * pre[i] : tval[ee], X[i], acc);
     }
@@ -428,87 +430,37 @@ __global__ void __launch_bounds__(kBT) bt_apply1m_kernel(int n, const int* __res
   }
 }
 
-// t = 1, transposed lists bucketed by length (SparseB::border; a B^T row's length is ~30 ln(n/j)
-// for Vecchia index j: median 20, 12 % of the rows > 64 entries holding 38 % of the entries at
-// n = 100k, m = 30). Each wave takes R slots of 64 / G rows of one bucket, G = the bucket's lanes
-// per row (16 / 32 / 64: one entry per lane, every load issued before any reduction); rows longer
-// than kLongRow get a whole wave with chunked loads (bt_long_row). Waves: [0, wl) long rows,
-// then the G = 64, 32 and 16 buckets.
-template <int G, int R>
-__device__ __forceinline__ void bt1_bucket(int base, int cnt, const int* __restrict__ rows,
-                                           const int* __restrict__ tptr, const int* __restrict__ trow,
-                                           const double* __restrict__ tval, int unit, const double* __restrict__ X,
-                                           const double* __restrict__ pre, const double* __restrict__ W,
-                                           const double* __restrict__ H, double* __restrict__ Y) {
-  constexpr int S = 64 / G;   // rows per slot
-  const int lane = threadIdx.x & 63;
-  const int li = lane & (G - 1);
-  const int g = lane / G;
-  int j[R], id[R];
-  double w[R], gx[R];
+// t = 1 default form of B (SparseB::ell_*): one row per lane, entries in a fixed ascending order,
+// kU1 loads in flight per lane. (The same form for B^T — sliced ELL, rows sorted by length in
+// windows — measured 37-48 us against the lane groups' 20 us: rows-as-lanes only pays where every
+// row has the same length.)
+constexpr int kU1 = 10;
+__global__ void __launch_bounds__(kBT) b_apply1e_kernel(int n, int m, const int* __restrict__ idx,
+                                                        const double* __restrict__ val, int unit,
+                                                        const double* __restrict__ X,
+                                                        const double* __restrict__ scale, double* __restrict__ Y) {
+  const int i = xcd_block(blockIdx.x, gridDim.x) * kBT + (int)threadIdx.x;
+  if (i >= n) return;
+  const int k = i < m ? i : m;
+  double acc = 0.;
+  for (int r0 = 0; r0 < k; r0 += kU1) {
+    int id[kU1];
+    double w[kU1], g[kU1];
 #pragma unroll
-  for (int q = 0; q < R; ++q) {
-    const int idx = base + q * S + g;
-    j[q] = idx < cnt ? rows[idx] : -1;
-    const int e0 = j[q] >= 0 ? tptr[j[q]] : 0;
-    const int e1 = j[q] >= 0 ? tptr[j[q] + 1] : 0;
-    const int e = e0 + li;
-    const bool ok = e < e1;
-    id[q] = ok ? trow[e] : 0;
-    w[q] = ok ? tval[e] : 0.;
-  }
-#pragma unroll
-  for (int q = 0; q < R; ++q) {
-    gx[q] = X[id[q]];
-    if (pre) w[q] *= pre[id[q]];
-  }
-#pragma unroll
-  for (int q = 0; q < R; ++q) {
-    const double acc = lane_group_sum<G>(w[q] * gx[q]);
-    if (li == 0 && j[q] >= 0) {
-      const int jj = j[q];
-      double s = unit ? (pre ? pre[jj] * X[jj] : X[jj]) : 0.;
-      s += acc;
-      if (W) s = fma(W[jj], H[jj], s);
-      Y[jj] = s;
+    for (int u = 0; u < kU1; ++u) {
+      const int r = r0 + u;
+      const bool ok = r < k;
+      id[u] = ok ? idx[(size_t)r * n + i] : i;
+      w[u] = ok ? val[(size_t)r * n + i] : 0.;
     }
+#pragma unroll
+    for (int u = 0; u < kU1; ++u) g[u] = X[id[u]];
+#pragma unroll
+    for (int u = 0; u < kU1; ++u) acc = fma(w[u], g[u], acc);
   }
-}
-
-#ifndef GPB_BT1_R
-#define GPB_BT1_R 2
-#endif
-constexpr int kBt1R = GPB_BT1_R;   // slots per wave (A/B builds override)
-
-__global__ void __launch_bounds__(kBT) bt_apply1b_kernel(SparseB B, const double* __restrict__ tval, int unit,
-                                                         const double* __restrict__ X,
-                                                         const double* __restrict__ pre,
-                                                         const double* __restrict__ W,
-                                                         const double* __restrict__ H, double* __restrict__ Y) {
-  const int wv = blockIdx.x * (kBT / 64) + (int)(threadIdx.x >> 6);
-  const int* rows = B.border;
-  const int nl = B.nbkt[0], n64 = B.nbkt[1], n32 = B.nbkt[2], n16 = B.nbkt[3];
-  const int w64 = (n64 + kBt1R - 1) / kBt1R;
-  const int w32 = (n32 + 2 * kBt1R - 1) / (2 * kBt1R);
-  const int w16 = (n16 + 4 * kBt1R - 1) / (4 * kBt1R);
-  int w = wv;
-  if (w < nl) {
-    bt_long_row(rows[w], B.tptr, B.trow, tval, unit, X, pre, W, H, Y);
-    return;
-  }
-  w -= nl;
-  if (w < w64) {
-    bt1_bucket<64, kBt1R>(w * kBt1R, n64, rows + nl, B.tptr, B.trow, tval, unit, X, pre, W, H, Y);
-    return;
-  }
-  w -= w64;
-  if (w < w32) {
-    bt1_bucket<32, kBt1R>(w * 2 * kBt1R, n32, rows + nl + n64, B.tptr, B.trow, tval, unit, X, pre, W, H, Y);
-    return;
-  }
-  w -= w32;
-  if (w < w16)
-    bt1_bucket<16, kBt1R>(w * 4 * kBt1R, n16, rows + nl + n64 + n32, B.tptr, B.trow, tval, unit, X, pre, W, H, Y);
+  double s = unit ? X[i] + acc : acc;
+  if (scale) s *= scale[i];
+  Y[i] = s;
 }
 
 __global__ void __launch_bounds__(kBT) gather_kernel(int count, const int* __restrict__ idx,
@@ -959,6 +911,13 @@ void launch_b_apply(const SparseB& B, const double* vals, bool unit, const doubl
                     double* Y, hipStream_t s) {
   if (B.n <= 0) return;
   static const bool old1 = std::getenv("GPBOOST_AMD_SPMV1_OLD") != nullptr;   // A/B: one row per group
+  static const bool groups1 = std::getenv("GPBOOST_AMD_SPMV1_GROUPS") != nullptr;   // A/B: lane-group forms
+  if (t == 1 && !old1 && !groups1 && B.ell_idx != nullptr && vals == B.vals_of) {
+    hipLaunchKernelGGL(b_apply1e_kernel, dim3(grid_x(B.n, kBT, 1 << 30)), dim3(kBT), 0, s, B.n, B.m, B.ell_idx,
+                       B.ell_val, unit ? 1 : 0, X, scale, Y);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (t == 1 && B.m <= 2 * k1G && !old1) {
     hipLaunchKernelGGL((b_apply1m_kernel<k1G, k1R>), dim3(grid_x(B.n, kBT / k1G * k1R, 1 << 30)), dim3(kBT), 0, s,
                        B.n, B.m, B.nbr, vals, unit ? 1 : 0, X, scale, Y);
@@ -999,21 +958,25 @@ void launch_bt_apply(const SparseB& B, const double* vals, bool unit, const doub
   if (B.n <= 0) return;
   const double* tval = (B.tval != nullptr && vals == B.tval_of) ? B.tval : nullptr;
   static const bool old1 = std::getenv("GPBOOST_AMD_SPMV1_OLD") != nullptr;
-  // A/B: length-bucketed lists (measured 21.4 vs 20.0 us for the 16-lane groups at n = 100k)
-  static const bool bt1b = std::getenv("GPBOOST_AMD_SPMV1_BT_BUCKETS") != nullptr;
-  if (t == 1 && tval != nullptr && !old1 && bt1b && B.border != nullptr) {
-    const int waves = B.nbkt[0] + (B.nbkt[1] + kBt1R - 1) / kBt1R + (B.nbkt[2] + 2 * kBt1R - 1) / (2 * kBt1R) +
-                      (B.nbkt[3] + 4 * kBt1R - 1) / (4 * kBt1R);
-    const int blocks = (waves + kBT / 64 - 1) / (kBT / 64);
-    if (blocks > 0)
-      hipLaunchKernelGGL(bt_apply1b_kernel, dim3(blocks), dim3(kBT), 0, s, B, tval, unit ? 1 : 0, X, pre, W, H, Y);
-    HIP_CHECK(hipGetLastError());
-    return;
-  }
   if (t == 1 && tval != nullptr && !old1) {
-    const int nmain = grid_x(B.n, kBT / k1G * k1R, 1 << 30);
     const int nlb = (B.nlong + kBT / 64 - 1) / (kBT / 64);
-    hipLaunchKernelGGL((bt_apply1m_kernel<k1G, k1R>), dim3(nmain + nlb), dim3(kBT), 0, s, B.n, B.tptr, B.trow, tval,
+    // lane-group shape (A/B builds: GPB_BT1_SHAPE): 1 = 16 lanes x 4 entries, 2 rows per group (the
+    // whole <= kLongRow list in one shot; 18.1 us at n = 100k), 0 = 16 x 2, 4 rows (20.3 us),
+    // 2 = 32 x 2, 2 rows (22.1 us), 3 = 16 x 4, 4 rows (23.9 us)
+#ifndef GPB_BT1_SHAPE
+#define GPB_BT1_SHAPE 1
+#endif
+#if GPB_BT1_SHAPE == 1
+    constexpr int G1 = 16, R1 = 2, E1 = 4;
+#elif GPB_BT1_SHAPE == 2
+    constexpr int G1 = 32, R1 = 2, E1 = 2;
+#elif GPB_BT1_SHAPE == 3
+    constexpr int G1 = 16, R1 = 4, E1 = 4;
+#else
+    constexpr int G1 = k1G, R1 = k1R, E1 = 2;
+#endif
+    const int nmain = grid_x(B.n, kBT / G1 * R1, 1 << 30);
+    hipLaunchKernelGGL((bt_apply1m_kernel<G1, R1, E1>), dim3(nmain + nlb), dim3(kBT), 0, s, B.n, B.tptr, B.trow, tval,
                        unit ? 1 : 0, X, pre, W, H, Y, nmain, B.longr, B.nlong);
     HIP_CHECK(hipGetLastError());
     return;
