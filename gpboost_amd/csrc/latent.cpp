@@ -206,6 +206,75 @@ void LatentVecchia::BuildStructure(const int* nbr) {
     HIP_CHECK(hipMemcpy(d_longr_.get(), longr.data(), sizeof(int) * longr.size(), hipMemcpyHostToDevice));
   sp_.longr = d_longr_.get();
   sp_.nlong = (int)longr.size();
+  {   // LDS tiles of the t >= 2 operator (TileOp): greedy runs of consecutive storage rows
+    auto build = [&](bool trans, TileDev& td) {
+      std::vector<int> r0{0}, uoff{0}, urow, fb;
+      std::vector<uint16_t> lidx(trans ? std::max(nnz, 1) : (size_t)n * m, 0);
+      std::vector<unsigned char> isfb(n, 0);
+      std::vector<int> stamp(n, -1), loc(n, 0);
+      int tile = 0, umax = 0, i = 0;
+      auto range = [&](int r, int& e0, int& e1) {
+        e0 = trans ? tptr[r] : r * m;
+        e1 = trans ? tptr[r + 1] : r * m + std::min(r, m);
+      };
+      auto id_of = [&](int e) { return trans ? trow[e] : nbr[e]; };
+      while (i < n) {
+        int rows = 0, nu = 0;
+        const int start = i;
+        while (i < n && i - start < kTileRows) {   // the kernel covers kTileRows rows of range per tile
+          int e0, e1;
+          range(i, e0, e1);
+          if (e1 - e0 > kTileUnion) {   // a list that alone overflows the LDS union
+            isfb[i] = 1;
+            fb.push_back(i);
+            ++i;
+            continue;
+          }
+          int add = 0;
+          for (int e = e0; e < e1; ++e) add += stamp[id_of(e)] != tile;
+          if (rows > 0 && nu + add > kTileUnion) break;
+          for (int e = e0; e < e1; ++e) {
+            const int id = id_of(e);
+            if (stamp[id] != tile) {
+              stamp[id] = tile;
+              loc[id] = nu++;
+              urow.push_back(id);
+            }
+            lidx[e] = (uint16_t)loc[id];
+          }
+          ++rows;
+          ++i;
+        }
+        r0.push_back(i);
+        uoff.push_back((int)urow.size());
+        umax = std::max(umax, nu);
+        ++tile;
+      }
+      td.r0.alloc(r0.size());
+      td.uoff.alloc(uoff.size());
+      td.urow.alloc(std::max<size_t>(urow.size(), 1));
+      td.lidx.alloc(lidx.size());
+      td.fb.alloc(std::max<size_t>(fb.size(), 1));
+      td.isfb.alloc(n);
+      HIP_CHECK(hipMemcpy(td.r0.get(), r0.data(), sizeof(int) * r0.size(), hipMemcpyHostToDevice));
+      HIP_CHECK(hipMemcpy(td.uoff.get(), uoff.data(), sizeof(int) * uoff.size(), hipMemcpyHostToDevice));
+      if (!urow.empty()) HIP_CHECK(hipMemcpy(td.urow.get(), urow.data(), sizeof(int) * urow.size(), hipMemcpyHostToDevice));
+      HIP_CHECK(hipMemcpy(td.lidx.get(), lidx.data(), sizeof(uint16_t) * lidx.size(), hipMemcpyHostToDevice));
+      if (!fb.empty()) HIP_CHECK(hipMemcpy(td.fb.get(), fb.data(), sizeof(int) * fb.size(), hipMemcpyHostToDevice));
+      HIP_CHECK(hipMemcpy(td.isfb.get(), isfb.data(), n, hipMemcpyHostToDevice));
+      td.op.ntile = tile;
+      td.op.nfb = (int)fb.size();
+      td.op.r0 = td.r0.get();
+      td.op.uoff = td.uoff.get();
+      td.op.urow = td.urow.get();
+      td.op.lidx = td.lidx.get();
+      td.op.fb = td.fb.get();
+      td.op.isfb = td.isfb.get();
+      td.op.umax = umax;
+    };
+    build(false, tile_b_);
+    build(true, tile_bt_);
+  }
   {   // t = 1 form of B: ELL, column-major (SparseB)
     std::vector<int> eidx((size_t)m * n), eslot((size_t)m * n);
     for (int i = 0; i < n; ++i) {
@@ -331,8 +400,16 @@ void LatentVecchia::BenchOperators(int t, int reps, double* out) {
     for (int part = 0; part < 2; ++part) {   // the operator's two launches
       HIP_CHECK(hipEventRecord(ev0_, s_));
       for (int r = 0; r < reps; ++r) {
-        if (part == 0) launch_b_apply(sp_, d_Bv_.get(), true, b.H.get(), t, d_Dinv_.get(), b.G.get(), s_);
-        else launch_bt_apply(sp_, d_Bv_.get(), true, b.G.get(), t, nullptr, d_W_.get(), b.H.get(), b.V.get(), s_);
+        const bool tiled = t >= 2 && std::getenv("GPBOOST_AMD_SPMV_TILED") != nullptr;
+        if (part == 0) {
+          if (tiled) launch_b_apply_tiled(sp_, tile_b_.op, d_Bv_.get(), b.H.get(), t, d_Dinv_.get(), b.G.get(), s_);
+          else launch_b_apply(sp_, d_Bv_.get(), true, b.H.get(), t, d_Dinv_.get(), b.G.get(), s_);
+        } else {
+          if (tiled)
+            launch_bt_apply_tiled(sp_, tile_bt_.op, d_tval_.get(), b.G.get(), t, d_W_.get(), b.H.get(), b.V.get(), s_);
+          else
+            launch_bt_apply(sp_, d_Bv_.get(), true, b.G.get(), t, nullptr, d_W_.get(), b.H.get(), b.V.get(), s_);
+        }
       }
       HIP_CHECK(hipEventRecord(ev1_, s_));
       HIP_CHECK(hipEventSynchronize(ev1_));
@@ -381,6 +458,13 @@ void LatentVecchia::BenchOperators(int t, int reps, double* out) {
 // V = (B^T D^-1 B + W) H   (CG_utils.cpp:75, 161-164)
 void LatentVecchia::ApplyA(const double* H, double* V, double* G, int t) {
   g_timer.begin(s_);
+  static const bool tiled = std::getenv("GPBOOST_AMD_SPMV_TILED") != nullptr;   // A/B: LDS-tiled operator
+  if (t >= 2 && tiled && sp_.tval_of == d_Bv_.get()) {
+    launch_b_apply_tiled(sp_, tile_b_.op, d_Bv_.get(), H, t, d_Dinv_.get(), G, s_);
+    launch_bt_apply_tiled(sp_, tile_bt_.op, d_tval_.get(), G, t, d_W_.get(), H, V, s_);
+    g_timer.end(s_, 3);
+    return;
+  }
   launch_b_apply(sp_, d_Bv_.get(), true, H, t, d_Dinv_.get(), G, s_);
   launch_bt_apply(sp_, d_Bv_.get(), true, G, t, nullptr, d_W_.get(), H, V, s_);
   g_timer.end(s_, t == 1 ? 2 : 3);

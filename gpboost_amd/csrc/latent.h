@@ -129,6 +129,13 @@ class LatentVecchia {
   SparseB sp_{};
   DevBuf<int> d_nbr_, d_tptr_, d_trow_, d_tslot_, d_longr_;
   DevBuf<int> d_ell_idx_, d_ell_slot_;
+  struct TileDev {   // device arrays of a TileOp
+    DevBuf<int> r0, uoff, urow, fb;
+    DevBuf<uint16_t> lidx;
+    DevBuf<unsigned char> isfb;
+    TileOp op{};
+  };
+  TileDev tile_b_, tile_bt_;
   DevBuf<double> d_ell_val_;
   int dense_rows_ = 0, head_rows_ = 0;   // VADU plan split (VaduPrecond)
   std::unique_ptr<VaduPrecond> pre_;

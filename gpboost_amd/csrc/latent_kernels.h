@@ -14,6 +14,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
 #include <vector>
 
 namespace gpb_amd {
@@ -54,6 +55,33 @@ struct SparseB {
 };
 constexpr int kLongRow = 64;
 
+// LDS-tiled form of the t >= 2 operator (opt-in, GPBOOST_AMD_SPMV_TILED=1; slower than the
+// global-gather wave kernels, see sparse_kernels.hip) (one workgroup per tile of consecutive storage rows): the
+// union of the tile's dependency rows is staged once into LDS (a Morton tile of 64 rows has ~270
+// distinct neighbours for its ~1900 entries at m = 30), then every entry reads its row from LDS.
+// Entry e of the op's lists (B: row i's r-th neighbour at i m + r; B^T: the tptr/trow order)
+// carries its union-local index lidx[e]. Rows whose own list exceeds kTileUnion (early Vecchia
+// rows of B^T) are not in any tile: rows fb[...] take the global-gather wave path.
+struct TileOp {
+  int ntile, nfb;
+  const int* r0;        // ntile + 1: tile k = storage rows [r0[k], r0[k+1]) minus fallback rows
+  const int* uoff;      // ntile + 1
+  const int* urow;      // union rows (storage)
+  const uint16_t* lidx; // per entry
+  const int* fb;        // fallback rows
+  const unsigned char* isfb;   // n: row is a fallback row
+  int umax;             // largest union of a tile
+};
+#ifndef GPB_TILE_UNION
+#define GPB_TILE_UNION 176
+#endif
+constexpr int kTileRows = 64, kTileUnion = GPB_TILE_UNION;
+
+// tiled forms (t >= 2, vals = B's values in the op's entry order: B n x m / B^T tval)
+void launch_b_apply_tiled(const SparseB& B, const TileOp& op, const double* vals, const double* X, int t,
+                          const double* scale, double* Y, hipStream_t s);
+void launch_bt_apply_tiled(const SparseB& B, const TileOp& op, const double* tval, const double* X, int t,
+                           const double* W, const double* H, double* Y, hipStream_t s);
 // Y = diag(scale) (unit*X + V X)   with V = vals on the B pattern (rows list optional)
 void launch_b_apply(const SparseB& B, const double* vals, bool unit, const double* X, int t, const double* scale,
                     double* Y, hipStream_t s);
