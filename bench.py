@@ -53,8 +53,13 @@ def pmc_traffic(scale: float) -> dict | None:
     """HBM bytes per launch of the row kernel from the committed rocprofv3 PMC passes of this
     same command (profiles/<round>/pmc_rows.json: FETCH_SIZE + WRITE_SIZE, KB per dispatch;
     PMC counters cannot be read from inside the process)."""
-    path = os.path.join(ROOT, "profiles", "r01", "pmc_rows.json")
-    if not os.path.exists(path):
+    path = None
+    for rnd in ("r02", "r01"):   # the latest round's passes
+        cand = os.path.join(ROOT, "profiles", rnd, "pmc_rows.json")
+        if os.path.exists(cand):
+            path = cand
+            break
+    if path is None:
         return None
     with open(path) as f:
         p = json.load(f)
@@ -194,7 +199,7 @@ def latent_leg(X, Y, steps: int, cpu: bool) -> dict:
     ach1 = byts1 / (ms_a1 * 1e-3) / 1e9
     leg["cg_matvec_roofline_single"] = {"bound": "hbm", "achieved": ach1, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                         "frac": ach1 / HBM_PEAK_GBS, "traffic": None,
-                                        "kernel": "b_apply1m + bt_apply1m", "kernel_ms": ms_a1, "columns": 1,
+                                        "kernel": "b_apply1e (ELL) + bt_apply1m<16,2,4>", "kernel_ms": ms_a1, "columns": 1,
                                         "algorithmic_bytes_per_launch": byts1, "preconditioner_ms": ms_p1}
     its = int(info[2])
     leg["preconditioner"]["share_of_eval"] = min(1.0, its * ms_p / (t_med * 1e3)) if its > 0 else None
