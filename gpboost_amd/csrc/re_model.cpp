@@ -257,9 +257,12 @@ void REModelAMD::LaunchVecchiaRows(const double* trafo, int r0, int r1, double* 
   a.d_nugget = 1.;
   a.block_sums = d_block_sums_.get();
   const int nblocks = vecchia_rows_blocks(r1 - r0, a.m);
-  HIP_CHECK(hipEventRecord(ev_[0], stream_));
+  // HIP events cost ~10 us of host time per evaluation (a quarter of the host overhead): recorded
+  // only once GetLastKernelTimes has been called
+  const bool timing = timing_;
+  if (timing) HIP_CHECK(hipEventRecord(ev_[0], stream_));
   launch_vecchia_rows(cfg_.cov_type, a, stream_);
-  HIP_CHECK(hipEventRecord(ev_[1], stream_));
+  if (timing) HIP_CHECK(hipEventRecord(ev_[1], stream_));
   if (allreduce && coll_ != nullptr) {
     launch_sum_blocks(d_block_sums_.get(), nblocks, kVecchiaSums, d_sums_.get(), stream_);
     coll_->AllReduceSum(d_sums_.get(), kVecchiaSums, stream_);
@@ -267,13 +270,14 @@ void REModelAMD::LaunchVecchiaRows(const double* trafo, int r0, int r1, double* 
   } else {   // one rank: the fixed-order block sum writes the pinned host buffer directly (no copy launch)
     launch_sum_blocks(d_block_sums_.get(), nblocks, kVecchiaSums, h_sums_dev_, stream_);
   }
-  HIP_CHECK(hipEventRecord(ev_[2], stream_));
+  if (timing) HIP_CHECK(hipEventRecord(ev_[2], stream_));
   HIP_CHECK(hipStreamSynchronize(stream_));
-  events_pending_ = true;   // kernel times are read from the events only when asked for
+  events_pending_ = timing;   // kernel times are read from the events only when asked for
   std::copy(h_sums_, h_sums_ + kVecchiaSums, sums);
 }
 
 void REModelAMD::GetLastKernelTimes(double* ms) {
+  timing_ = true;   // evaluations from now on record their kernel events
   if (events_pending_) {
     UseDevice();
     float ms0 = 0.f, ms1 = 0.f;

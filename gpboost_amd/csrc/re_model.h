@@ -117,6 +117,7 @@ class REModelAMD {
   double* h_sums_ = nullptr;  // pinned
   double* h_sums_dev_ = nullptr;  // device address of h_sums_ (the single-rank sum kernel writes it directly)
   bool events_pending_ = false;   // last_kernel_ms_ of the last row launch not read from its events yet
+  bool timing_ = false;           // record kernel events (set by the first GetLastKernelTimes)
 
   std::unique_ptr<DenseSolver> dense_;
   std::unique_ptr<LatentVecchia> latent_;

@@ -206,7 +206,9 @@ GPBOOST_AMD_EXPORT int GPB_GetLastIterationInfo(REModelHandle handle, double* in
 
 /* Timing of the last evaluation's dominant kernel (ms, HIP events on the model's stream),
  * for the benchmark's live roofline. kernel_ms[0] = factor/Cholesky kernel,
- * kernel_ms[1] = whole device-side evaluation. */
+ * kernel_ms[1] = whole device-side evaluation. Exact Vecchia models record the events only for
+ * evaluations after the first call of this function (they cost ~10 us of host time each);
+ * before that it returns zeros. */
 GPBOOST_AMD_EXPORT int GPB_GetLastKernelTimes(REModelHandle handle, double* kernel_ms);
 
 /* Benchmark support (latent Vecchia, iterative): device time of the operator
