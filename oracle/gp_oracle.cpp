@@ -168,6 +168,83 @@ void orc_find_neighbors(const double* x, int n, int d, int m, int* nbr) {
   }
 }
 
+// Prediction neighbours, vecchia_pred_type = "order_obs_first_cond_obs_only"
+// (Vecchia_utils.cpp:1672-1674, 1715-1718 -> :732-1058 with start_at = n_obs,
+// end_search_at = n_obs - 1): x_all = observed points (model order) then prediction points; row
+// i >= n_obs takes its m nearest among the observed points by the same coordinate-sum sweep.
+// nbr: n_pred x m; m must be <= n_obs (the reference caps it at end_search_at + 1, :754-757).
+void orc_find_neighbors_pred(const double* x, int n_obs, int n_all, int d, int m, int* nbr) {
+  const int end_search_at = n_obs - 1;
+  std::vector<double> csum(n_all);
+  for (int i = 0; i < n_all; ++i) {
+    double s = 0.;
+    for (int k = 0; k < d; ++k) s += x[(size_t)i * d + k];
+    csum[i] = s;
+  }
+  std::vector<int> sort_sum(n_all);
+  std::iota(sort_sum.begin(), sort_sum.end(), 0);
+  std::sort(sort_sum.begin(), sort_sum.end(), [&](int a, int b) { return csum[a] < csum[b]; });
+  std::vector<int> inv(n_all);
+  for (int i = 0; i < n_all; ++i) inv[sort_sum[i]] = i;
+  std::vector<double> nd(m);
+  std::vector<int> ni(m);
+  for (int i = n_obs; i < n_all; ++i) {
+    std::fill(nd.begin(), nd.end(), std::numeric_limits<double>::infinity());
+    std::fill(ni.begin(), ni.end(), 0);
+    bool up = true, down = true;
+    int up_i = inv[i], down_i = inv[i];
+    auto consider = [&](int cand, bool& dir) {
+      if (cand < i && cand <= end_search_at) {
+        double smd = (csum[cand] - csum[i]) * (csum[cand] - csum[i]);
+        if (smd > d * nd[m - 1]) { dir = false; return; }
+        double sed = 0.;
+        for (int k = 0; k < d; ++k) {
+          double t = x[(size_t)cand * d + k] - x[(size_t)i * d + k];
+          sed += t * t;
+        }
+        if (sed < nd[m - 1]) {
+          nd[m - 1] = sed;
+          ni[m - 1] = cand;
+          for (int j = m - 1; j > 0 && nd[j] < nd[j - 1]; --j) {
+            std::swap(nd[j], nd[j - 1]);
+            std::swap(ni[j], ni[j - 1]);
+          }
+        }
+      }
+    };
+    while (up || down) {
+      if (down_i == 0) down = false;
+      if (up_i == n_all - 1) up = false;
+      if (down) { --down_i; consider(sort_sum[down_i], down); }
+      if (up) { ++up_i; consider(sort_sum[up_i], up); }
+    }
+    for (int j = 0; j < m; ++j) nbr[(size_t)(i - n_obs) * m + j] = ni[j];
+  }
+}
+
+// Predictive mean and variance, exact Gaussian Vecchia, "order_obs_first_cond_obs_only"
+// (Vecchia_utils.cpp:1779-1895, 1900-1931; re_model_template.h:3787-3803, :4066-4071): per
+// prediction point the row of (Bpo, Dp) from its observed neighbours — A = (C + I)^-1 c,
+// Dp = 1 + marginal variance - A c on the transformed scale — then mean = -Bpo y = A . y_nbr,
+// var = (Dp - [latent: 1]) * sigma2. pars = transformed (sigma2, sigma1^2 / sigma2, phi).
+int orc_vecchia_predict(const double* x_all, const double* y_obs, const int* nbr, int n_obs, int n_pred, int d,
+                        int m, int t, const double* pars, int predict_response, double* mean, double* var) {
+  RowFactor f;
+  std::vector<int> row(m);
+  for (int p = 0; p < n_pred; ++p) {
+    const int i = n_obs + p;
+    for (int r = 0; r < m; ++r) row[r] = nbr[(size_t)p * m + r];
+    // row_factor with k = min(i, m) = m: the same per-row algebra as the likelihood rows
+    row_factor(x_all, row.data(), i, d, m, t, pars[1], pars[2], f);
+    if (!(f.D > 0.)) return -1;
+    double mu = 0.;
+    for (int r = 0; r < f.k; ++r) mu += f.A[r] * y_obs[row[r]];
+    mean[p] = mu;
+    if (var) var[p] = (f.D - (predict_response ? 0. : kNugget)) * pars[0];
+  }
+  return 0;
+}
+
 int orc_vecchia_partials(const double* coords, const double* y, const int* nbr,
                          int n, int d, int m, int t, const double* pars,
                          int r0, int r1, double* sums) {

@@ -35,6 +35,11 @@ void orc_vecchia_order(int n, int seed, int random_ordering, int* perm);
  * coords_vo row-major n x d in Vecchia order. nbr: n x m, row i holds
  * k_i = min(i, m) indices (ascending distance), rest -1. */
 void orc_find_neighbors(const double* coords_vo, int n, int d, int m, int* nbr);
+// Prediction ("order_obs_first_cond_obs_only"): neighbours of rows [n_obs, n_all) among the
+// observed rows, and the predictive mean / variance (gp_oracle.cpp cites the reference lines).
+void orc_find_neighbors_pred(const double* x_all, int n_obs, int n_all, int d, int m, int* nbr);
+int orc_vecchia_predict(const double* x_all, const double* y_obs, const int* nbr, int n_obs, int n_pred, int d,
+                        int m, int t, const double* pars, int predict_response, double* mean, double* var);
 
 /* Exact Gaussian Vecchia nll + gradient (Vecchia_utils.cpp:1307-1632,
  * re_model_template.h:1748-1791, 2646-2881, 8885-9120).

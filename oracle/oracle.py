@@ -35,6 +35,9 @@ def lib():
         L.orc_transform_cov_pars.argtypes = [ctypes.c_int, D, D]
         L.orc_vecchia_order.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, I]
         L.orc_find_neighbors.argtypes = [D, ctypes.c_int, ctypes.c_int, ctypes.c_int, I]
+        L.orc_find_neighbors_pred.argtypes = [D, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, I]
+        L.orc_vecchia_predict.argtypes = [D, D, I, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, D, ctypes.c_int, D, D]
         L.orc_vecchia_nll_grad.argtypes = [D, D, I, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, D,
                                            ctypes.c_int, D, D, D, D, D]
         L.orc_vecchia_partials.argtypes = [D, D, I, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, D,
@@ -85,6 +88,34 @@ def find_neighbors(coords_vo: np.ndarray, m: int) -> np.ndarray:
     nb = np.zeros((n, m), dtype=np.int32)
     lib().orc_find_neighbors(_d(x), n, d, m, _i(nb))
     return nb
+
+
+def find_neighbors_pred(coords_vo: np.ndarray, coords_pred: np.ndarray, m: int) -> np.ndarray:
+    """Prediction neighbours among the observed points (order_obs_first_cond_obs_only)."""
+    x = np.ascontiguousarray(np.vstack([coords_vo, coords_pred]), dtype=np.float64)
+    n_obs = coords_vo.shape[0]
+    n_all, d = x.shape
+    nb = np.zeros((n_all - n_obs, m), dtype=np.int32)
+    lib().orc_find_neighbors_pred(_d(x), n_obs, n_all, d, m, _i(nb))
+    return nb
+
+
+def vecchia_predict(coords_vo, y_vo, coords_pred, m_pred, cov_type, pars_trafo, predict_response=True):
+    """(mean, var, nbr) of the exact Gaussian Vecchia prediction (order_obs_first_cond_obs_only)."""
+    xo = np.ascontiguousarray(coords_vo, dtype=np.float64)
+    xp = np.ascontiguousarray(coords_pred, dtype=np.float64)
+    m = min(m_pred, xo.shape[0])
+    nb = find_neighbors_pred(xo, xp, m)
+    x = np.ascontiguousarray(np.vstack([xo, xp]))
+    yv = np.ascontiguousarray(y_vo, dtype=np.float64)
+    p = np.ascontiguousarray(pars_trafo, dtype=np.float64)
+    n_pred = xp.shape[0]
+    mean = np.zeros(n_pred)
+    var = np.zeros(n_pred)
+    if lib().orc_vecchia_predict(_d(x), _d(yv), _i(nb), xo.shape[0], n_pred, x.shape[1], m, cov_type, _d(p),
+                                 int(predict_response), _d(mean), _d(var)):
+        raise RuntimeError("oracle prediction failed")
+    return mean, var, nb
 
 
 def vecchia_setup(coords: np.ndarray, m: int, seed: int = 0, random: bool = True):

@@ -93,3 +93,22 @@ def test_partials_sum_to_whole(synth2000):
     full = O.vecchia_partials(xv, Y[perm], nb, 0, tp, 0, 2000)
     parts = sum(O.vecchia_partials(xv, Y[perm], nb, 0, tp, a, b) for a, b in [(0, 7), (7, 999), (999, 2000)])
     np.testing.assert_allclose(parts, full, rtol=1e-12)
+
+
+def test_oracle_vecchia_prediction_matches_r_golden():
+    """Exact Gaussian Vecchia prediction, vecchia_pred_type = "order_obs_first_cond_obs_only",
+    30 neighbours, vecchia_ordering = "none", at the fitted parameters the R test prints
+    (test_GPModel_gaussian_process.R:912-931: cov_pars_vecchia (0.03297349, 1.07691542,
+    0.11378505) -> expected_mu_vecchia, expected_cov_vecchia diagonal; predict_response = TRUE).
+    The parameters are printed to 8 digits, so the golden pins the oracle to ~1e-7."""
+    from gpboost_amd import synthetic
+    coords, y = synthetic.rtest_gaussian_y(100)
+    xp = np.array([[0.1, 0.9], [0.10001, 0.90001], [0.7, 0.55]])
+    tp = O.transform(0, [0.03297349, 1.07691542, 0.11378505])
+    mu, var, nb = O.vecchia_predict(coords, y, xp, 30, 0, tp, predict_response=True)
+    assert np.abs(mu - np.array([0.06968068, 0.06967750, 0.44208925])).sum() < 2e-6
+    assert np.abs(var - np.array([0.6214955, 0.6215069, 0.4199531])).sum() < 2e-6
+    # latent process: the nugget variance (sigma2) removed
+    mu0, var0, _ = O.vecchia_predict(coords, y, xp, 30, 0, tp, predict_response=False)
+    np.testing.assert_array_equal(mu0, mu)
+    np.testing.assert_allclose(var0, var - 0.03297349, rtol=0, atol=1e-12)
