@@ -308,6 +308,72 @@ class GPModel:
         _safe_call(lib().GPB_BenchLatentOperators(self.handle, ctypes.c_int(t), ctypes.c_int(reps), _dp(out)))
         return out
 
+    def set_prediction_data(self, vecchia_pred_type=None, num_neighbors_pred=None, cg_delta_conv_pred=None,
+                            nsim_var_pred=None, rank_pred_approx_matrix_lanczos=None, group_data_pred=None,
+                            group_rand_coef_data_pred=None, gp_coords_pred=None, gp_rand_coef_data_pred=None,
+                            cluster_ids_pred=None, X_pred=None):
+        """Prediction settings (reference basic.py:6095, GPB_SetPredictionData). Only
+        vecchia_pred_type / num_neighbors_pred are supported; prediction data is passed to predict()."""
+        if any(v is not None for v in (group_data_pred, group_rand_coef_data_pred, gp_coords_pred,
+                                       gp_rand_coef_data_pred, cluster_ids_pred, X_pred)):
+            raise GPBoostError("set_prediction_data: saving prediction data is not supported by gpboost_amd; "
+                               "pass gp_coords_pred to predict()")
+        _safe_call(lib().GPB_SetPredictionData(
+            self.handle, ctypes.c_int32(0), None, None, None, None, None, None, c_str(vecchia_pred_type),
+            ctypes.c_int(int(num_neighbors_pred) if num_neighbors_pred is not None else -1),
+            ctypes.c_double(float(cg_delta_conv_pred) if cg_delta_conv_pred is not None else -1.),
+            ctypes.c_int(int(nsim_var_pred) if nsim_var_pred is not None else -1),
+            ctypes.c_int(int(rank_pred_approx_matrix_lanczos) if rank_pred_approx_matrix_lanczos is not None else -1)))
+
+    def predict(self, predict_response=True, predict_var=False, predict_cov_mat=False, y=None, cov_pars=None,
+                group_data_pred=None, group_rand_coef_data_pred=None, gp_coords_pred=None,
+                gp_rand_coef_data_pred=None, cluster_ids_pred=None, X_pred=None, use_saved_data=False, offset=None,
+                offset_pred=None, fixed_effects=None, fixed_effects_pred=None, vecchia_pred_type=None,
+                num_neighbors_pred=None):
+        """Predictions at new coordinates (reference basic.py:5778-6093, GPB_PredictREModel): returns
+        {"mu": mean, "cov": covariance or None, "var": variances or None}. Exact Gaussian Vecchia
+        models, vecchia_pred_type "order_obs_first_cond_obs_only"."""
+        if vecchia_pred_type is not None or num_neighbors_pred is not None:
+            self.set_prediction_data(vecchia_pred_type=vecchia_pred_type, num_neighbors_pred=num_neighbors_pred)
+        if any(v is not None for v in (group_data_pred, group_rand_coef_data_pred, gp_rand_coef_data_pred,
+                                       cluster_ids_pred, X_pred)):
+            raise GPBoostError("predictions with grouped random effects, random coefficients, clusters or "
+                               "covariates are not supported by gpboost_amd")
+        if gp_coords_pred is None:
+            raise ValueError("'gp_coords_pred' is missing")
+        xp = np.asarray(gp_coords_pred, dtype=np.float64)
+        if xp.ndim == 1:
+            xp = xp.reshape(-1, 1)
+        if xp.shape[1] != self.dim_coords:
+            raise ValueError("Incorrect number of covariates (columns) in 'gp_coords_pred'")
+        if not np.all(np.isfinite(xp)):
+            raise ValueError("'gp_coords_pred' contains NaN or Inf")
+        n_pred = xp.shape[0]
+        xcol = np.ascontiguousarray(xp.T.reshape(-1))   # column-major, as the reference passes it
+        yv = self._check_y(y)
+        if offset is not None:
+            fixed_effects = offset if fixed_effects is None else np.asarray(fixed_effects) + np.asarray(offset)
+        if offset_pred is not None:
+            fixed_effects_pred = offset_pred if fixed_effects_pred is None else (
+                np.asarray(fixed_effects_pred) + np.asarray(offset_pred))
+        fe = _as1d(fixed_effects, "fixed_effects") if fixed_effects is not None else None
+        fep = _as1d(fixed_effects_pred, "fixed_effects_pred") if fixed_effects_pred is not None else None
+        cp = self._check_cov_pars(cov_pars) if cov_pars is not None else None
+        size = n_pred + (n_pred * n_pred if predict_cov_mat else (n_pred if predict_var else 0))
+        out = np.zeros(size)
+        _safe_call(lib().GPB_PredictREModel(
+            self.handle, _dp(yv) if yv is not None else None, ctypes.c_int32(n_pred), _dp(out),
+            ctypes.c_bool(bool(predict_cov_mat)), ctypes.c_bool(bool(predict_var)),
+            ctypes.c_bool(bool(predict_response)), None, None, None, _dp(xcol), None,
+            _dp(cp) if cp is not None else None, None, ctypes.c_bool(bool(use_saved_data)),
+            _dp(fe) if fe is not None else None, _dp(fep) if fep is not None else None))
+        mu = out[:n_pred].copy()
+        cov = out[n_pred:].reshape(n_pred, n_pred).T.copy() if predict_cov_mat else None
+        var = out[n_pred:].copy() if (predict_var and not predict_cov_mat) else None
+        if predict_cov_mat and predict_var:
+            var = np.diag(cov).copy()
+        return {"mu": mu, "cov": cov, "var": var}
+
     def set_distributed(self, rank: int, world_size: int, comm_id: bytes | None):
         """Join an RCCL communicator (GPB_SetDistributed): exact Vecchia shards rows, latent
         Vecchia (iterative) shards the probe columns."""

@@ -207,6 +207,54 @@ int GPB_EvalNegLogLikelihood(REModelHandle handle, const double* y_data, double*
   API_END();
 }
 
+int GPB_SetPredictionData(REModelHandle handle, int32_t num_data_pred, const int32_t* cluster_ids_data_pred,
+                          const char* re_group_data_pred, const double* re_group_rand_coef_data_pred,
+                          double* gp_coords_data_pred, const double* gp_rand_coef_data_pred,
+                          const double* covariate_data_pred, const char* vecchia_pred_type, int num_neighbors_pred,
+                          double cg_delta_conv_pred, int nsim_var_pred, int rank_pred_approx_matrix_lanczos) {
+  API_BEGIN();
+  (void)cg_delta_conv_pred;
+  (void)nsim_var_pred;
+  (void)rank_pred_approx_matrix_lanczos;
+  if (num_data_pred > 0 || cluster_ids_data_pred != nullptr || re_group_data_pred != nullptr ||
+      re_group_rand_coef_data_pred != nullptr || gp_coords_data_pred != nullptr || gp_rand_coef_data_pred != nullptr ||
+      covariate_data_pred != nullptr)
+    gpb_amd::Fatal("GPB_SetPredictionData: saving prediction data is not supported by gpboost_amd; pass the "
+                   "prediction coordinates to GPB_PredictREModel");
+  model(handle)->SetPredictionData(vecchia_pred_type, num_neighbors_pred);
+  API_END();
+}
+
+int GPB_PredictREModel(REModelHandle handle, const double* y_data, int32_t num_data_pred, double* out_predict,
+                       bool predict_cov_mat, bool predict_var, bool predict_response,
+                       const int32_t* cluster_ids_data_pred, const char* re_group_data_pred,
+                       const double* re_group_rand_coef_data_pred, double* gp_coords_data_pred,
+                       const double* gp_rand_coef_data_pred, const double* cov_pars,
+                       const double* covariate_data_pred, bool use_saved_data, const double* fixed_effects,
+                       const double* fixed_effects_pred) {
+  API_BEGIN();
+  if (out_predict == nullptr) gpb_amd::Fatal("out_predict is NULL");
+  if (use_saved_data) gpb_amd::Fatal("use_saved_data: saved prediction data is not supported by gpboost_amd");
+  if (cluster_ids_data_pred != nullptr || re_group_data_pred != nullptr || re_group_rand_coef_data_pred != nullptr ||
+      gp_rand_coef_data_pred != nullptr || covariate_data_pred != nullptr)
+    gpb_amd::Fatal("predictions with clusters, grouped random effects, random coefficients or covariates are not "
+                   "supported by gpboost_amd");
+  REModelAMD* m = model(handle);
+  std::vector<double> r;
+  const double* y = y_data;
+  if (fixed_effects != nullptr) {   // the GP part of the response (re_model_template.h:3386-3393)
+    if (y_data == nullptr) gpb_amd::Fatal("'y_data' cannot be NULL when 'fixed_effects' is provided");
+    r.resize(m->config().n);
+    for (int i = 0; i < m->config().n; ++i) r[i] = y_data[i] - fixed_effects[i];
+    y = r.data();
+  }
+  m->Predict(y, num_data_pred, gp_coords_data_pred, cov_pars, predict_cov_mat, predict_var, predict_response,
+             out_predict);
+  if (fixed_effects_pred != nullptr)
+    for (int i = 0; i < num_data_pred; ++i) out_predict[i] += fixed_effects_pred[i];
+  API_END();
+}
+
 int GPB_EvalNegLogLikelihoodGrad(REModelHandle handle, const double* y_data, const double* cov_pars,
                                  const double* fixed_effects, int profile_sigma2, double* negll, double* grad,
                                  double* sigma2_out) {

@@ -23,11 +23,17 @@ struct VecchiaRowsArgs {
   double* block_sums;    // [num_blocks x kVecchiaSums] (nullable if Y is null)
   double* Dinv_out;      // optional [n]  (indexed by global row)
   double* B_out;         // optional [n x m], B(i, nbr) = -A_i, 0-padded
+  int row_base;          // nbr, B_out and Dinv_out hold rows from row_base on (0: all rows;
+                         // predictions: the rows after the observed ones)
 };
 
 // Returns the number of blocks used (needed to size/finish block_sums).
 int vecchia_rows_blocks(int rows, int m);
 void launch_vecchia_rows(int cov_type, const VecchiaRowsArgs& a, hipStream_t s);
+// Predictions from the prediction rows' factor: out[p] = -sum_r B[p, r] y[nbr[p, r]] (mean),
+// out[n_pred + p] = (1 / Dinv[p] - nugget_sub) * sigma2 (variance). B, nbr: n_pred x m.
+void launch_predict_mean_var(int n_pred, int m, const int* nbr, const double* B, const double* Dinv, const double* y,
+                             double sigma2, double nugget_sub, double* out, hipStream_t s);
 // Deterministic fixed-order sum of block partials -> out[kVecchiaSums].
 void launch_sum_blocks(const double* block_sums, int nblocks, int width, double* out, hipStream_t s);
 

@@ -92,6 +92,7 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
   HIP_CHECK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h_sums_dev_), h_sums_, 0));
   row_begin_ = 0;
   row_end_ = n;
+  num_neighbors_pred_ = 2 * cfg_.num_neighbors;   // re_model_template.h:299
   if (vecchia_) {
     if (cfg_.num_neighbors > n - 1) cfg_.num_neighbors = n - 1;  // Vecchia_utils.cpp:754-757
     if (cfg_.num_neighbors < 1) Fatal("num_neighbors must be >= 1");
@@ -209,6 +210,90 @@ void REModelAMD::SetDistributedHost(int rank, int world, HostAllReduceFn fn, voi
   if (comm_) { ncclCommDestroy(comm_); comm_ = nullptr; }
   coll_.reset(new HostCallbackCollective(fn, user));
   ApplyPartition(rank, world);
+}
+
+void REModelAMD::SetPredictionData(const char* vecchia_pred_type, int num_neighbors_pred) {
+  if (vecchia_pred_type != nullptr) {
+    const std::string t(vecchia_pred_type);
+    static const char* known[] = {"order_obs_first_cond_obs_only", "order_obs_first_cond_all", "order_pred_first",
+                                  "latent_order_obs_first_cond_obs_only", "latent_order_obs_first_cond_all"};
+    bool ok = false;
+    for (const char* k : known) ok |= t == k;
+    if (!ok) Fatal("Prediction type '%s' is not supported for the Veccia approximation ", t.c_str());
+    if (t != "order_obs_first_cond_obs_only")
+      Fatal("vecchia_pred_type '%s' is not supported by gpboost_amd (supported: order_obs_first_cond_obs_only)",
+            t.c_str());
+    vecchia_pred_type_ = t;
+  }
+  if (num_neighbors_pred > 0) num_neighbors_pred_ = num_neighbors_pred;
+}
+
+// Vecchia_utils.cpp:1634-1931 (CondObsOnly = true, Gaussian, no full-scale part) and
+// re_model_template.h:3787-3803, 3960-4071: neighbours of the prediction points among the
+// observed points (GPU sweep, end_search_at = n - 1), the per-point rows (A, Dp) by the
+// likelihood's row kernel (rows n .. n + n_pred - 1 of [observed; prediction] coordinates), then
+// mean = A . y_nbr and var = (Dp - [latent: 1]) sigma2 (predict_mean_var_kernel).
+void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,
+                         bool predict_cov_mat, bool predict_var, bool predict_response, double* out) {
+  if (!vecchia_ || cfg_.latent)
+    Fatal("predictions are implemented for the exact Gaussian Vecchia approximation (gp_approx = 'vecchia') only");
+  if (world_ > 1) Fatal("predictions are only available on single-rank models");
+  if (n_pred <= 0) Fatal("num_data_pred must be > 0");
+  if (coords_pred == nullptr) Fatal("gp_coords_data_pred must be provided");
+  UseDevice();
+  if (y != nullptr) SetY(y);
+  if (!y_set_) Fatal("response variable y has not been set (pass y or evaluate the likelihood first)");
+  double cp[3];
+  if (cov_pars != nullptr) std::copy(cov_pars, cov_pars + 3, cp);
+  else if (last_cov_pars_.size() == 3) std::copy(last_cov_pars_.begin(), last_cov_pars_.end(), cp);
+  else Fatal("cov_pars must be provided (no previous evaluation)");
+  double trafo[3];
+  TransformCovPars(cp, trafo);
+  const int n = cfg_.n, d = cfg_.d, na = n + n_pred;
+  const int mp = std::min(num_neighbors_pred_, n);   // end_search_at + 1 (Vecchia_utils.cpp:754-757)
+  if (mp > 64) Fatal("num_neighbors_pred = %d > 64 is not supported by the GPU prediction kernel", mp);
+  std::vector<double> xa((size_t)na * d);
+  std::copy(coords_vo_.begin(), coords_vo_.end(), xa.begin());
+  for (int p = 0; p < n_pred; ++p)
+    for (int q = 0; q < d; ++q) xa[(size_t)(n + p) * d + q] = coords_pred[(size_t)q * n_pred + p];
+  std::vector<int> nb((size_t)n_pred * mp);
+  if (d <= 3) vecchia_neighbors_gpu(xa.data(), na, d, mp, n, na, nb.data(), stream_, n - 1);
+  else vecchia_neighbors(xa.data(), na, d, mp, n, na, nb.data(), n - 1);
+  DevBuf<double> dxa((size_t)na * d), dB((size_t)n_pred * mp), dD(n_pred), dout((size_t)2 * n_pred);
+  DevBuf<int> dnb((size_t)n_pred * mp);
+  HIP_CHECK(hipMemcpyAsync(dxa.get(), xa.data(), sizeof(double) * xa.size(), hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(dnb.get(), nb.data(), sizeof(int) * nb.size(), hipMemcpyHostToDevice, stream_));
+  VecchiaRowsArgs a{};
+  a.X = dxa.get();
+  a.Y = nullptr;              // factor rows only
+  a.nbr = dnb.get();
+  a.n = na;
+  a.d = d;
+  a.m = mp;
+  a.r0 = n;
+  a.r1 = na;
+  a.var = trafo[1];
+  a.phi = trafo[2];
+  a.diag_mult = 1.;
+  a.diag_add = 1.;            // nugget on the between-neighbour covariance (Vecchia_utils.cpp:1877)
+  a.d_nugget = 1.;            // Dp starts at 1 (:1797-1798)
+  a.B_out = dB.get();
+  a.Dinv_out = dD.get();
+  a.row_base = n;
+  launch_vecchia_rows(cfg_.cov_type, a, stream_);
+  launch_predict_mean_var(n_pred, mp, dnb.get(), dB.get(), dD.get(), d_y_.get(), trafo[0],
+                          predict_response ? 0. : 1., dout.get(), stream_);
+  std::vector<double> h((size_t)2 * n_pred);
+  HIP_CHECK(hipMemcpyAsync(h.data(), dout.get(), sizeof(double) * h.size(), hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  std::copy(h.begin(), h.begin() + n_pred, out);
+  if (predict_cov_mat) {   // conditioning on observed points only: the predictive covariance is diagonal
+    double* c = out + n_pred;
+    std::fill(c, c + (size_t)n_pred * n_pred, 0.);
+    for (int p = 0; p < n_pred; ++p) c[(size_t)p * n_pred + p] = h[n_pred + p];
+  } else if (predict_var) {
+    std::copy(h.begin() + n_pred, h.end(), out + n_pred);
+  }
 }
 
 void REModelAMD::TransformCovPars(const double* orig, double* trafo) const {

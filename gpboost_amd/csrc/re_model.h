@@ -65,6 +65,15 @@ class REModelAMD {
   // Latent models: gradient wrt log(cov_pars) (+ log(aux_pars) when estimate_aux_pars).
   EvalResult Eval(const double* cov_pars_orig, bool want_grad, int profile);
 
+  // Prediction settings (GPB_SetPredictionData; vecchia_pred_type null / num_neighbors_pred <= 0:
+  // unchanged) and predictions at new coordinates (GPB_PredictREModel): exact Gaussian Vecchia,
+  // "order_obs_first_cond_obs_only". coords_pred column-major n_pred x d; cov_pars on the original
+  // scale (null: those of the last evaluation); y null: the response already set. out: means, then
+  // variances (predict_var) or the n_pred x n_pred covariance (predict_cov_mat; diagonal here).
+  void SetPredictionData(const char* vecchia_pred_type, int num_neighbors_pred);
+  void Predict(const double* y, int n_pred, const double* coords_pred, const double* cov_pars, bool predict_cov_mat,
+               bool predict_var, bool predict_response, double* out);
+
   void SetDistributed(int rank, int world, const ncclUniqueId& id, bool use_comm);
   // Same partition, cross-rank sums through a host function instead of RCCL (test transport).
   void SetDistributedHost(int rank, int world, HostAllReduceFn fn, void* user);
@@ -124,6 +133,9 @@ class REModelAMD {
   std::vector<double> y_vo_;          // host copy (Vecchia order) for the latent solver
   std::vector<double> aux_pars_;
   double last_iter_info_[4] = {0., 0., 0., 0.};
+
+  std::string vecchia_pred_type_ = "order_obs_first_cond_obs_only";   // re_model_template.h:6485-6490
+  int num_neighbors_pred_ = 0;                                         // 2 num_neighbors (:299)
 
   int rank_ = 0, world_ = 1;
   int row_begin_ = 0, row_end_ = 0;

@@ -27,8 +27,9 @@ std::vector<int> vecchia_order(int n, int seed, bool random) {
   return idx;
 }
 
-void vecchia_neighbors(const double* x, int n, int d, int m, int row_begin, int row_end, int* nbr) {
-  const int last_cand = n - 2;
+void vecchia_neighbors(const double* x, int n, int d, int m, int row_begin, int row_end, int* nbr,
+                       int end_search_at) {
+  const int last_cand = end_search_at < 0 ? n - 2 : end_search_at;
   // coordinate sums and the sweep order (utils.h:228-236 SortIndeces = std::sort on iota)
   std::vector<double> csum(n);
   for (int i = 0; i < n; ++i) {

@@ -173,7 +173,7 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
     const int irow = active ? i : a.r0;
 
     // ---- gather: neighbour index, coordinates, response (Vecchia order)
-    const int nb = rv ? a.nbr[(size_t)i * a.m + r] : 0;
+    const int nb = rv ? a.nbr[(size_t)(i - a.row_base) * a.m + r] : 0;
     double xi[kDMax], xr[kDMax];
 #pragma unroll
     for (int q = 0; q < kDMax; ++q) {
@@ -266,7 +266,7 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
     const double av_r = rv ? aug1 / mydiag : 0.;   // a = C^-1 c (lanes r >= MK hold no row)
     const double vv_r = rv ? aug2 / mydiag : 0.;   // v = C^-1 y_nbr
 
-    if (active && a.B_out != nullptr && r < a.m) a.B_out[(size_t)i * a.m + r] = rv ? -av_r : 0.;
+    if (active && a.B_out != nullptr && r < a.m) a.B_out[(size_t)(i - a.row_base) * a.m + r] = rv ? -av_r : 0.;
     mark(2);
 
     // ---- 3. t = dC a (dC from the packed image; its diagonal is 0)
@@ -297,7 +297,7 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
 
     const double D = var + a.d_nugget - ac;          // Vecchia_utils.cpp:1351, 1507, 1562
     const double Dinv = 1. / D;
-    if (active && r == 0 && a.Dinv_out != nullptr) a.Dinv_out[i] = Dinv;
+    if (active && r == 0 && a.Dinv_out != nullptr) a.Dinv_out[i - a.row_base] = Dinv;
     if (want_like && active && r == 0) {
       const double By = yi - ay;                         // (B y)_i
       const double u = By * Dinv;                        // (D^-1 B y)_i
@@ -378,8 +378,8 @@ __global__ void __launch_bounds__(kV4Threads, 1) vecchia_rows2_kernel(VecchiaRow
     const int irow = active ? i : a.r0;
 
     // ---- gather: neighbour indices, coordinates, responses (Vecchia order)
-    const int nb0 = v0 ? a.nbr[(size_t)i * a.m + r0] : 0;
-    const int nb1 = v1 ? a.nbr[(size_t)i * a.m + r1] : 0;
+    const int nb0 = v0 ? a.nbr[(size_t)(i - a.row_base) * a.m + r0] : 0;
+    const int nb1 = v1 ? a.nbr[(size_t)(i - a.row_base) * a.m + r1] : 0;
     double xi[kDMax], x0[kDMax], x1[kDMax];
 #pragma unroll
     for (int q = 0; q < kDMax; ++q) {
@@ -498,8 +498,8 @@ __global__ void __launch_bounds__(kV4Threads, 1) vecchia_rows2_kernel(VecchiaRow
     const double a1 = p1a / dg1, w1 = p1b / dg1;
 
     if (active && a.B_out != nullptr) {
-      if (r0 < a.m) a.B_out[(size_t)i * a.m + r0] = v0 ? -a0 : 0.;
-      if (r1 < a.m) a.B_out[(size_t)i * a.m + r1] = v1 ? -a1 : 0.;
+      if (r0 < a.m) a.B_out[(size_t)(i - a.row_base) * a.m + r0] = v0 ? -a0 : 0.;
+      if (r1 < a.m) a.B_out[(size_t)(i - a.row_base) * a.m + r1] = v1 ? -a1 : 0.;
     }
 
     // ---- 4. t = dC a (dC from the packed triangle; its diagonal is 0)
@@ -528,7 +528,7 @@ __global__ void __launch_bounds__(kV4Threads, 1) vecchia_rows2_kernel(VecchiaRow
 
     const double D = var + a.d_nugget - ac;          // Vecchia_utils.cpp:1351, 1507, 1562
     const double Dinv = 1. / D;
-    if (active && h == 0 && a.Dinv_out != nullptr) a.Dinv_out[i] = Dinv;
+    if (active && h == 0 && a.Dinv_out != nullptr) a.Dinv_out[i - a.row_base] = Dinv;
     if (want_like && active && h == 0) {
       const double By = yi - ay;
       const double u = By * Dinv;
@@ -583,6 +583,20 @@ __global__ void __launch_bounds__(1024) sum_blocks_kernel(const double* __restri
     __syncthreads();
   }
   if ((int)threadIdx.x < width) out[threadIdx.x] = red[threadIdx.x];
+}
+
+// One thread per prediction point; entries in neighbour order.
+__global__ void __launch_bounds__(256) predict_mean_var_kernel(int n_pred, int m, const int* __restrict__ nbr,
+                                                               const double* __restrict__ B,
+                                                               const double* __restrict__ Dinv,
+                                                               const double* __restrict__ y, double sigma2,
+                                                               double nugget_sub, double* __restrict__ out) {
+  const int p = blockIdx.x * 256 + threadIdx.x;
+  if (p >= n_pred) return;
+  double mu = 0.;
+  for (int r = 0; r < m; ++r) mu = fma(-B[(size_t)p * m + r], y[nbr[(size_t)p * m + r]], mu);
+  out[p] = mu;
+  out[n_pred + p] = (1. / Dinv[p] - nugget_sub) * sigma2;
 }
 
 int lanes_for_m(int m) {
@@ -678,6 +692,14 @@ void launch_vecchia_rows(int cov_type, const VecchiaRowsArgs& a, hipStream_t s) 
     case 64: launch_cov<64>(cov_type, a, s); break;
     default: Fatal("num_neighbors = %d > 64 is not supported by the GPU Vecchia kernel", a.m);
   }
+}
+
+void launch_predict_mean_var(int n_pred, int m, const int* nbr, const double* B, const double* Dinv, const double* y,
+                             double sigma2, double nugget_sub, double* out, hipStream_t s) {
+  if (n_pred <= 0) return;
+  hipLaunchKernelGGL(predict_mean_var_kernel, dim3((n_pred + 255) / 256), dim3(256), 0, s, n_pred, m, nbr, B, Dinv, y,
+                     sigma2, nugget_sub, out);
+  HIP_CHECK(hipGetLastError());
 }
 
 void launch_sum_blocks(const double* block_sums, int nblocks, int width, double* out, hipStream_t s) {

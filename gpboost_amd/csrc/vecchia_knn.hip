@@ -37,7 +37,7 @@ __global__ void __launch_bounds__(kKnnThreads) knn_kernel(const double* __restri
                                                          const double* __restrict__ csum,
                                                          const int* __restrict__ order,
                                                          const int* __restrict__ pos, int n, int d, int m,
-                                                         int r0, int r1, int* __restrict__ out) {
+                                                         int r0, int r1, int last_cand, int* __restrict__ out) {
   __shared__ double bd_s[kKnnMaxM * kKnnThreads];
   __shared__ int bi_s[kKnnMaxM * kKnnThreads];
   const int tid = threadIdx.x;
@@ -45,7 +45,6 @@ __global__ void __launch_bounds__(kKnnThreads) knn_kernel(const double* __restri
   int* bi = bi_s + tid;
   const int i = r0 + blockIdx.x * kKnnThreads + tid;
   if (i >= r1 || i <= m) return;   // rows i <= m: all earlier points (host)
-  const int last_cand = n - 2;
   for (int k = 0; k < m; ++k) {
     bd[k * kKnnThreads] = INFINITY;
     bi[k * kKnnThreads] = 0;
@@ -92,7 +91,8 @@ __global__ void __launch_bounds__(kKnnThreads) knn_kernel(const double* __restri
 }  // namespace
 
 void vecchia_neighbors_gpu(const double* x, int n, int d, int m, int row_begin, int row_end, int* nbr,
-                           hipStream_t s) {
+                           hipStream_t s, int end_search_at) {
+  const int last_cand = end_search_at < 0 ? n - 2 : end_search_at;
   if (m > kKnnMaxM) Fatal("GPU neighbour search supports num_neighbors <= %d", kKnnMaxM);
   if (d < 1 || d > 3) Fatal("GPU neighbour search supports 1 <= dim_gp_coords <= 3");
   const int rows = row_end - row_begin;
@@ -132,7 +132,7 @@ void vecchia_neighbors_gpu(const double* x, int n, int d, int m, int row_begin, 
   HIP_CHECK(hipMemcpyAsync(dpos.get(), pos.data(), sizeof(int) * n, hipMemcpyHostToDevice, s));
   const int blocks = (row_end - g0 + kKnnThreads - 1) / kKnnThreads;
   hipLaunchKernelGGL(knn_kernel, dim3(blocks), dim3(kKnnThreads), 0, s, dx.get(), dcs.get(), dord.get(), dpos.get(),
-                     n, d, m, g0, row_end, dout.get());
+                     n, d, m, g0, row_end, last_cand, dout.get());
   HIP_CHECK(hipGetLastError());
   HIP_CHECK(hipMemcpyAsync(nbr + (size_t)(g0 - row_begin) * m, dout.get(), sizeof(int) * (size_t)(row_end - g0) * m,
                            hipMemcpyDeviceToHost, s));

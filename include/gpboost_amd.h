@@ -219,6 +219,56 @@ GPBOOST_AMD_EXPORT int GPB_GetLastKernelTimes(REModelHandle handle, double* kern
  * kernels). No reference counterpart (measurement only). */
 GPBOOST_AMD_EXPORT int GPB_BenchLatentOperators(REModelHandle handle, int t, int reps, double* out);
 
+/* ---------------------------------------------------------------- prediction */
+
+/* replaces GPB_SetPredictionData (include/LightGBM/c_api.h:1578; c_api.cpp). Only the settings
+ * are supported: vecchia_pred_type (NULL: unchanged; supported: "order_obs_first_cond_obs_only",
+ * the reference's default for Gaussian likelihoods, re_model_template.h:6485-6487) and
+ * num_neighbors_pred (<= 0: unchanged; default 2 * num_neighbors, :299). Prediction data must be
+ * NULL / 0 (pass it to GPB_PredictREModel); cg_delta_conv_pred, nsim_var_pred and
+ * rank_pred_approx_matrix_lanczos are accepted and ignored (iterative prediction is out of scope). */
+GPBOOST_AMD_EXPORT int GPB_SetPredictionData(REModelHandle handle,
+    int32_t num_data_pred,
+    const int32_t* cluster_ids_data_pred,
+    const char* re_group_data_pred,
+    const double* re_group_rand_coef_data_pred,
+    double* gp_coords_data_pred,
+    const double* gp_rand_coef_data_pred,
+    const double* covariate_data_pred,
+    const char* vecchia_pred_type,
+    int num_neighbors_pred,
+    double cg_delta_conv_pred,
+    int nsim_var_pred,
+    int rank_pred_approx_matrix_lanczos);
+
+/* replaces GPB_PredictREModel (include/LightGBM/c_api.h:1617; Vecchia_utils.cpp:1634-1931,
+ * re_model_template.h:3700-4071) for the exact Gaussian Vecchia approximation: predictive mean
+ * (out_predict[0 .. num_data_pred)) and, if predict_var, variances (out_predict[num_data_pred ..
+ * 2 num_data_pred)), or, if predict_cov_mat, the num_data_pred^2 covariance (diagonal: each
+ * prediction point conditions on observed points only). gp_coords_data_pred column-major
+ * num_data_pred x dim_gp_coords. cov_pars on the original scale (NULL: those of the last
+ * evaluation); y_data NULL: the response set before. predict_response = false removes the
+ * nugget variance (latent process). Neighbours are searched among the observed points by the
+ * reference's sweep (bit-identical lists). Unsupported inputs (clusters, grouped effects,
+ * random coefficients, covariates, saved prediction data, latent / dense models) return -1. */
+GPBOOST_AMD_EXPORT int GPB_PredictREModel(REModelHandle handle,
+    const double* y_data,
+    int32_t num_data_pred,
+    double* out_predict,
+    bool predict_cov_mat,
+    bool predict_var,
+    bool predict_response,
+    const int32_t* cluster_ids_data_pred,
+    const char* re_group_data_pred,
+    const double* re_group_rand_coef_data_pred,
+    double* gp_coords_data_pred,
+    const double* gp_rand_coef_data_pred,
+    const double* cov_pars,
+    const double* covariate_data_pred,
+    bool use_saved_data,
+    const double* fixed_effects,
+    const double* fixed_effects_pred);
+
 /* ---------------------------------------------------------------- EXTENSION: multi-GPU */
 
 /* Size of the opaque communicator id (bytes). */

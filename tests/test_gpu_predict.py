@@ -1,0 +1,91 @@
+"""GPU parity of Vecchia predictions through the C ABI
+(GPB_SetPredictionData / GPB_PredictREModel): exact Gaussian Vecchia, vecchia_pred_type
+"order_obs_first_cond_obs_only" (the reference default for Gaussian likelihoods).
+
+Pinned to the reference R-test golden (test_GPModel_gaussian_process.R:912-931) and, at larger
+n, to the oracle restatement (oracle/gp_oracle.cpp orc_find_neighbors_pred /
+orc_vecchia_predict; its neighbour search is the reference's sweep, so the lists, and hence the
+predictions, match to rounding). Tolerance: 1e-10 relative against the oracle.
+"""
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _model(X, m=30, ordering="random"):
+    from gpboost_amd import GPModel
+    return GPModel(gp_coords=X, cov_function="exponential", gp_approx="vecchia", num_neighbors=m,
+                   vecchia_ordering=ordering, seed=0)
+
+
+def test_predict_r_golden():
+    from gpboost_amd import synthetic
+    coords, y = synthetic.rtest_gaussian_y(100)
+    gm = _model(coords, 30, "none")
+    gm.set_prediction_data(vecchia_pred_type="order_obs_first_cond_obs_only", num_neighbors_pred=30)
+    xp = np.array([[0.1, 0.9], [0.10001, 0.90001], [0.7, 0.55]])
+    cp = [0.03297349, 1.07691542, 0.11378505]
+    pred = gm.predict(y=y, gp_coords_pred=xp, cov_pars=cp, predict_cov_mat=True)
+    assert np.abs(pred["mu"] - np.array([0.06968068, 0.06967750, 0.44208925])).sum() < 2e-6
+    exp_cov = np.array([0.6214955, 0, 0, 0, 0.6215069, 0, 0, 0, 0.4199531])
+    assert np.abs(pred["cov"].reshape(-1) - exp_cov).sum() < 2e-6
+    pv = gm.predict(gp_coords_pred=xp, cov_pars=cp, predict_var=True, predict_response=False)
+    np.testing.assert_allclose(pv["var"], np.diag(pred["cov"]) - cp[0], rtol=0, atol=1e-12)
+    np.testing.assert_array_equal(pv["mu"], pred["mu"])
+
+
+@pytest.mark.parametrize("n,n_pred,m,m_pred,d", [(2000, 500, 30, None, 2), (20000, 3000, 30, 30, 2),
+                                                 (5000, 700, 10, 25, 3), (3000, 400, 16, 64, 1)])
+def test_predict_vs_oracle(n, n_pred, m, m_pred, d):
+    from gpboost_amd import synthetic
+    X = synthetic.bench_coords(n + n_pred, d)
+    Xo, Xp = X[:n], X[n:]
+    y = synthetic.bench_gaussian_y(n)
+    gm = _model(Xo, m)
+    if m_pred is not None:
+        gm.set_prediction_data(num_neighbors_pred=m_pred)
+    cp = [0.2, 1.3, 0.15]
+    pred = gm.predict(y=y, gp_coords_pred=Xp, cov_pars=cp, predict_var=True)
+    perm, xv, _ = O.vecchia_setup(Xo, m, 0, True)
+    mp = m_pred if m_pred is not None else 2 * m
+    mu, var, _ = O.vecchia_predict(xv, y[perm], Xp, mp, 0, O.transform(0, cp), predict_response=True)
+    np.testing.assert_allclose(pred["mu"], mu, rtol=1e-10, atol=1e-12 * np.abs(mu).max())
+    np.testing.assert_allclose(pred["var"], var, rtol=1e-10)
+
+
+def test_predict_defaults_and_fixed_effects():
+    from gpboost_amd import synthetic
+    X = synthetic.bench_coords(1200)
+    Xo, Xp = X[:1000], X[1000:]
+    y = synthetic.bench_gaussian_y(1000)
+    gm = _model(Xo)
+    cp = [0.1, 1.0, 0.1]
+    gm.neg_log_likelihood(cp, y)          # sets y and the last cov_pars
+    a = gm.predict(gp_coords_pred=Xp)     # both taken from the evaluation
+    b = gm.predict(y=y, gp_coords_pred=Xp, cov_pars=cp)
+    np.testing.assert_array_equal(a["mu"], b["mu"])
+    assert a["var"] is None and a["cov"] is None
+    fe = np.full(1000, 0.5)
+    fep = np.full(200, 0.25)
+    c = gm.predict(y=y + fe, gp_coords_pred=Xp, cov_pars=cp, fixed_effects=fe, fixed_effects_pred=fep)
+    np.testing.assert_allclose(c["mu"], b["mu"] + 0.25, rtol=1e-13, atol=1e-13)
+
+
+def test_predict_errors():
+    from gpboost_amd import GPBoostError, GPModel, synthetic
+    X = synthetic.bench_coords(600)
+    y = synthetic.bench_gaussian_y(500)
+    gm = _model(X[:500])
+    with pytest.raises(GPBoostError, match="not supported"):
+        gm.set_prediction_data(vecchia_pred_type="order_pred_first")
+    with pytest.raises(GPBoostError, match="not supported"):
+        gm.set_prediction_data(vecchia_pred_type="no_such_type")
+    with pytest.raises(ValueError):
+        gm.predict(y=y, gp_coords_pred=X[500:, :1], cov_pars=[0.1, 1.0, 0.1])
+    lat = GPModel(gp_coords=X[:500], likelihood="bernoulli_logit", cov_function="exponential", gp_approx="vecchia",
+                  num_neighbors=20, matrix_inversion_method="iterative")
+    with pytest.raises(GPBoostError, match="exact Gaussian Vecchia"):
+        lat.predict(y=(y > 0).astype(float), gp_coords_pred=X[500:], cov_pars=[1.0, 0.1])
