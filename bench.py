@@ -29,6 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 N_DATA = 100_000
+PRED_N = 100_000                 # prediction points of the secondary prediction leg
 M_NEIGHBORS = 30
 THETA = [0.1, 1.0, 0.1]          # sigma2, sigma1^2, rho (original scale), exponential kernel
 FP64_PEAK_TFLOPS = 78.6          # MI355X FP64 vector = FP64 matrix peak (spec)
@@ -366,6 +367,21 @@ def main():
         line["cpu_baseline"] = cpu_baseline(X, Y)
     else:
         line["cpu_baseline"] = None
+    if world == 1:   # §8f row f2: predictions at new points from the same model (end-to-end, incl. the search)
+        import numpy as np
+        Xp = synthetic.bench_coords(N_DATA + PRED_N)[N_DATA:]
+        gm.predict(gp_coords_pred=Xp, cov_pars=THETA, predict_var=True)   # warm-up
+        ts = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            pr = gm.predict(gp_coords_pred=Xp, cov_pars=THETA, predict_var=True)
+            ts.append(time.perf_counter() - t0)
+        tp = float(np.median(ts))
+        line["prediction"] = {"n_pred": PRED_N, "num_neighbors_pred": 2 * M_NEIGHBORS,
+                              "vecchia_pred_type": "order_obs_first_cond_obs_only", "ms": tp * 1e3,
+                              "predictions_per_s": PRED_N / tp, "mean_of_mu": float(np.mean(pr["mu"])),
+                              "note": "end to end: neighbour search among the 100k observed points (GPU), "
+                                      "prediction rows (row kernel, 64-lane groups), mean/variance"}
     if world == 1 and not args.no_latent:
         del gm
         line["latent_iterative"] = latent_leg(X, Y, args.latent_steps, not args.no_cpu_baseline)
