@@ -120,11 +120,35 @@ __global__ void __launch_bounds__(256) gemm_f64_kernel(GemmArgs g) {
 // operands are loaded into registers while the current step's MFMAs run, one barrier per step.
 // Same masks, K ranges and summation order per output element as gemm_f64_kernel (k ascending
 // in steps of 4 through the MFMA).
-constexpr int TB = 128, TKB = 32;   // K step 32: 128 MFMAs per wave between barriers
+#ifndef GPB_TKB
+#define GPB_TKB 32
+#endif
+#ifndef GPB_BIG_WPE
+#define GPB_BIG_WPE 0
+#endif
+#ifndef GPB_BIG_SWZ
+#define GPB_BIG_SWZ 0
+#endif
+constexpr int TB = 128, TKB = GPB_TKB;   // K step 32: 128 MFMAs per wave between barriers
 
-__global__ void __launch_bounds__(256) gemm_f64_big_kernel(GemmArgs g) {
+#if GPB_BIG_WPE
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPB_BIG_WPE, GPB_BIG_WPE)))
+#else
+__global__ void __launch_bounds__(256)
+#endif
+gemm_f64_big_kernel(GemmArgs g) {
+#if GPB_BIG_SWZ
+  // unpadded rows, column XOR-swizzled by the row: (k & 15) spreads a transposed store's 16 k rows
+  // over distinct banks, bit 4 = k & 1 puts the two rows of a 32-lane ds_read_b64 group in
+  // disjoint bank halves
+  __shared__ double As[2][TKB][TB];
+  __shared__ double Bs[2][TKB][TB];
+#define SWZ(k, c) ((c) ^ (((k) & 15) | (((k) & 1) << 4)))
+#else
   __shared__ double As[2][TKB][TB + 1];
   __shared__ double Bs[2][TKB][TB + 1];
+#define SWZ(k, c) (c)
+#endif
   const int m0 = blockIdx.y * TB, n0 = blockIdx.x * TB;
   if (g.lower_out && n0 > m0 + TB - 1) return;
   int k_begin = 0, k_end = g.K;
@@ -170,10 +194,10 @@ __global__ void __launch_bounds__(256) gemm_f64_big_kernel(GemmArgs g) {
       const int idx = tid + e * 256;
       int i, k;
       if (g.transA) { k = idx & (TKB - 1); i = idx / TKB; } else { i = idx & 127; k = idx >> 7; }
-      As[buf][k][i] = ra[e];
+      As[buf][k][SWZ(k, i)] = ra[e];
       int j, kb;
       if (g.transB) { j = idx & 127; kb = idx >> 7; } else { kb = idx & (TKB - 1); j = idx / TKB; }
-      Bs[buf][kb][j] = rb[e];
+      Bs[buf][kb][SWZ(kb, j)] = rb[e];
     }
   };
   if (k_begin < k_end) {
@@ -191,8 +215,8 @@ __global__ void __launch_bounds__(256) gemm_f64_big_kernel(GemmArgs g) {
       double a[4], b[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
-        a[q] = As[buf][kl][wm + 16 * q + (lane & 15)];
-        b[q] = Bs[buf][kl][wn + 16 * q + (lane & 15)];
+        a[q] = As[buf][kl][SWZ(kl, wm + 16 * q + (lane & 15))];
+        b[q] = Bs[buf][kl][SWZ(kl, wn + 16 * q + (lane & 15))];
       }
 #pragma unroll
       for (int p = 0; p < 4; ++p)
@@ -218,6 +242,7 @@ __global__ void __launch_bounds__(256) gemm_f64_big_kernel(GemmArgs g) {
         }
       }
 }
+#undef SWZ
 
 // Lower triangle (i >= j) of Psi = Sigma + I, tile-parallel, upper tiles skipped.
 template <int COV>

@@ -1,9 +1,13 @@
 #!/bin/bash
-# dense-path GPU tests with the 128x128 GEMM, then timing new vs 64x64-only
-cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+# GPU box: dense-path timing A/B over in-tree variant builds (gpboost_amd/lib/ab).
+set -o pipefail
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$R"
+TAG="${TAG:-r02}"
 mkdir -p gpurun_out
-timeout -k 10 600 python -u -m pytest tests/test_gpu_dense.py -x -q --timeout 300 --timeout-method thread > gpurun_out/dense_tests.log 2>&1
-rc=$?; echo "tests rc=$rc" >> gpurun_out/dense_tests.log
-case $rc in 0|1) ;; *) exit $rc ;; esac
-timeout -k 10 300 python -u scripts/time_dense.py > gpurun_out/dense_ab.log 2>&1 || exit $?
-GPBOOST_AMD_DIAG_OLD=1 timeout -k 10 300 python -u scripts/time_dense.py >> gpurun_out/dense_ab.log 2>&1
+OUT=gpurun_out/dense_ab_${TAG}.log
+: > $OUT
+for v in "" ${VARIANTS}; do
+  echo "== variant '${v}'" >> $OUT
+  GPBOOST_AMD_VARIANT=$v timeout -k 10 240 python scripts/time_dense.py 20000 >> $OUT 2>&1 || exit 1
+done
