@@ -209,6 +209,82 @@ def latent_leg(X, Y, steps: int, cpu: bool) -> dict:
     return leg
 
 
+DENSE_N = 20_000                  # BASELINE config 2: dense Cholesky fp64 on one GPU
+DENSE_CPU_N = 4_000               # bounded CPU sample of the same unit (the n=20000 unit is ~800 s)
+
+
+def dense_flops(n: int) -> float:
+    """Algorithmic FLOPs of one dense nll+grad: POTRF n^3/3 + TRTRI n^3/3 + LAUUM n^3/3 (Psi^-1
+    for the gradient traces, re_model_template.h:5987-6007); the O(n^2) covariance build, trace
+    and triangular-solve terms are left out."""
+    return float(n) ** 3
+
+
+def dense_leg(steps: int, cpu: bool) -> dict:
+    """BASELINE config 2: n=20000 2-D spatial GP, dense Cholesky fp64 (gp_approx='none'), the same
+    L-BFGS unit (nll + gradient, sigma2 profiled), inputs resident on the GPU."""
+    import numpy as np
+
+    from gpboost_amd import GPModel, synthetic
+    X = synthetic.bench_coords(DENSE_N)
+    Y = synthetic.bench_gaussian_y(DENSE_N)
+    gm = GPModel(gp_coords=X, cov_function="exponential", gp_approx="none")
+    gm.neg_log_likelihood_and_grad(THETA, Y, profile_sigma2=True)   # warm-up (allocation, first eval)
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        nll, g, _ = gm.neg_log_likelihood_and_grad(THETA, None, profile_sigma2=True)
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    fl = dense_flops(DENSE_N)
+    leg = {"metric": "dense nll + grad evals/sec, n=20000", "value": 1.0 / t, "unit": "evals/s", "steps": steps,
+           "ms_per_step": t * 1e3,
+           "config": {"workload": "dense_gaussian_lbfgs_unit", "n": DENSE_N, "cov_function": "exponential",
+                      "theta": THETA, "nll": nll, "grad": [float(x) for x in g]},
+           "roofline": {"bound": "mfma", "achieved": fl / t / 1e12, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": fl / t / 1e12 / FP64_PEAK_TFLOPS, "traffic": None,
+                        "kernel": "whole evaluation (POTRF + TRTRI + LAUUM through gemm_f64_big_kernel / "
+                                  "gemm_f64_kernel, v_mfma_f64_16x16x4f64)",
+                        "algorithmic_flops_per_eval": fl}}
+    del gm
+    if cpu:
+        leg["cpu_baseline"] = dense_cpu_baseline()
+    return leg
+
+
+def dense_cpu_baseline() -> dict | None:
+    """The reference's dense path (oracle/_ref/ref_harness) on this host, bounded sample at
+    n=4000; `value_scaled_n20000` scales it by (4000/20000)^3 (the unit is n^3-bound)."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(harness):
+        return None
+    import numpy as np
+
+    from gpboost_amd import synthetic
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", str(os.cpu_count() or 1))), 16))
+    X = synthetic.bench_coords(DENSE_CPU_N)
+    Y = synthetic.bench_gaussian_y(DENSE_CPU_N)
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(np.array([X.shape[0], X.shape[1]], dtype=np.int32).tobytes())
+        f.write(np.ascontiguousarray(X.T).tobytes())
+        f.write(np.ascontiguousarray(Y).tobytes())
+        path = f.name
+    try:
+        out = subprocess.run([harness, path, "cov_fct=exponential", "gp_approx=none", "mode=lbfgs", "reps=1",
+                              "cov_pars=" + ",".join(map(str, THETA))], capture_output=True, text=True, timeout=600,
+                             env=dict(os.environ, OMP_NUM_THREADS=str(threads)), check=True)
+        r = json.loads(out.stdout)
+        t = r["median_time"]
+        return {"value": 1.0 / t, "unit": "evals/s", "cores": threads, "kind": "reference",
+                "sample": f"1 dense L-BFGS-unit eval at n={DENSE_CPU_N} ({t:.2f} s)",
+                "value_scaled_n20000": (1.0 / t) * (DENSE_CPU_N / DENSE_N) ** 3}
+    except Exception as e:  # noqa: BLE001
+        sys.stderr.write(f"reference dense CPU baseline failed: {e}\n")
+        return None
+    finally:
+        os.unlink(path)
+
+
 def host_transport() -> bool:
     """GPBOOST_AMD_BENCH_TRANSPORT=host (rehearsal of the N > 1 flow on a one-GPU box): every
     rank on device 0, cross-rank sums through a gloo all-reduce instead of RCCL."""
@@ -274,6 +350,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-latent", action="store_true", help="skip the secondary latent/iterative leg")
     ap.add_argument("--latent-steps", type=int, default=3)
+    ap.add_argument("--no-dense", action="store_true", help="skip the secondary dense (config 2) leg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -382,6 +459,8 @@ def main():
                               "predictions_per_s": PRED_N / tp, "mean_of_mu": float(np.mean(pr["mu"])),
                               "note": "end to end: neighbour search among the 100k observed points (GPU), "
                                       "prediction rows (row kernel, 64-lane groups), mean/variance"}
+    if world == 1 and not args.no_dense:
+        line["dense"] = dense_leg(3, not args.no_cpu_baseline)
     if world == 1 and not args.no_latent:
         del gm
         line["latent_iterative"] = latent_leg(X, Y, args.latent_steps, not args.no_cpu_baseline)

@@ -21,6 +21,7 @@ class DenseSolver {
 
  private:
   void Potrf();
+  void PotrfLookahead();
   void Trtri(int a, int b);
 
   int n_, d_, ld_;
@@ -30,6 +31,10 @@ class DenseSolver {
   DevBuf<int> info_;
   double* h_red_ = nullptr;
   hipEvent_t ev_[3] = {nullptr, nullptr, nullptr};
+  // lookahead POTRF: panel chain on a high-priority stream, the rest of each trailing update on a
+  // second stream (created on first use)
+  hipStream_t s_chain_ = nullptr, s_rest_ = nullptr;
+  hipEvent_t ev_la_[3] = {nullptr, nullptr, nullptr};
 };
 
 // C[M x N] = alpha op(A) op(B) + beta C, column-major fp64, MFMA tiles (dense_kernels.hip).

@@ -114,73 +114,61 @@ __global__ void __launch_bounds__(256) gemm_f64_kernel(GemmArgs g) {
       }
 }
 
-// Large-tile form for the big updates (trailing SYRK, TRTRI/LAUUM products): 128 x 128 output
-// tile per 256-thread workgroup, each wave 64 x 64 = 4 x 4 MFMA tiles (16 MFMAs per 8 LDS
-// reads instead of 4 per 4), K staged in steps of 32 through two LDS buffers: the next step's
-// operands are loaded into registers while the current step's MFMAs run, one barrier per step.
-// Same masks, K ranges and summation order per output element as gemm_f64_kernel (k ascending
-// in steps of 4 through the MFMA).
+// Pipelined tile GEMM: TBt x TBt output tile per 256-thread workgroup, each wave (TBt/2)^2 =
+// WT x WT MFMA tiles, K staged in steps of TKB through two LDS buffers: the next step's operands
+// are loaded into registers while the current step's MFMAs run, one barrier per step.
+//   TBt = 128 (large updates: trailing SYRK, TRTRI / LAUUM products): 4 x 4 MFMA tiles per wave
+//     (16 MFMAs per 8 LDS reads); K step 16 and two waves per SIMD: 64 KB of LDS and <= 256
+//     registers let two workgroups share a CU, so one's barrier / store phase overlaps the
+//     other's MFMAs (n = 20000: 0.339 -> 0.260 s per evaluation vs K step 32 at one workgroup per
+//     CU; an XOR-swizzled unpadded LDS layout measured 6 % slower, profiles/r02/dense_ab_r02.log);
+//   TBt = 64 (panel / TRSM steps and small products): 2 x 2 MFMA tiles per wave; the pipelined
+//     staging replaces the load -> barrier -> MFMA -> barrier sequence whose global-load latency
+//     was exposed every K step (~30 us per call at K = 64).
+// Same masks, K ranges and summation order per output element for every TBt (k ascending in
+// steps of 4 through the MFMA), so the tile size never changes a result bit.
 #ifndef GPB_TKB
-#define GPB_TKB 32
+#define GPB_TKB 16
 #endif
-#ifndef GPB_BIG_WPE
-#define GPB_BIG_WPE 0
-#endif
-#ifndef GPB_BIG_SWZ
-#define GPB_BIG_SWZ 0
-#endif
-constexpr int TB = 128, TKB = GPB_TKB;   // K step 32: 128 MFMAs per wave between barriers
+constexpr int TB = 128, TKB = GPB_TKB;
 
-#if GPB_BIG_WPE
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPB_BIG_WPE, GPB_BIG_WPE)))
-#else
-__global__ void __launch_bounds__(256)
-#endif
-gemm_f64_big_kernel(GemmArgs g) {
-#if GPB_BIG_SWZ
-  // unpadded rows, column XOR-swizzled by the row: (k & 15) spreads a transposed store's 16 k rows
-  // over distinct banks, bit 4 = k & 1 puts the two rows of a 32-lane ds_read_b64 group in
-  // disjoint bank halves
-  __shared__ double As[2][TKB][TB];
-  __shared__ double Bs[2][TKB][TB];
-#define SWZ(k, c) ((c) ^ (((k) & 15) | (((k) & 1) << 4)))
-#else
-  __shared__ double As[2][TKB][TB + 1];
-  __shared__ double Bs[2][TKB][TB + 1];
-#define SWZ(k, c) (c)
-#endif
-  const int m0 = blockIdx.y * TB, n0 = blockIdx.x * TB;
-  if (g.lower_out && n0 > m0 + TB - 1) return;
+template <int TBt>
+__device__ __forceinline__ void gemm_tile_body(const GemmArgs& g) {
+  constexpr int WT = TBt / 32;   // MFMA tiles per wave and dimension
+  __shared__ double As[2][TKB][TBt + 1];
+  __shared__ double Bs[2][TKB][TBt + 1];
+  const int m0 = blockIdx.y * TBt, n0 = blockIdx.x * TBt;
+  if (g.lower_out && n0 > m0 + TBt - 1) return;
   int k_begin = 0, k_end = g.K;
-  if (g.a_lower) k_end = min(k_end, m0 + TB);
+  if (g.a_lower) k_end = min(k_end, m0 + TBt);
   if (g.a_upper) k_begin = max(k_begin, m0);
   if (g.b_lower) k_begin = max(k_begin, n0);
   k_begin = (k_begin / TKB) * TKB;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
-  const int wm = (wave >> 1) * 64, wn = (wave & 1) * 64;   // wave's 64 x 64 sub-tile
-  double4_t acc[4][4];
+  const int wm = (wave >> 1) * (TBt / 2), wn = (wave & 1) * (TBt / 2);   // wave's sub-tile
+  double4_t acc[WT][WT];
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < WT; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b) acc[a][b] = (double4_t){0., 0., 0., 0.};
+    for (int b = 0; b < WT; ++b) acc[a][b] = (double4_t){0., 0., 0., 0.};
 
-  constexpr int EPT = TKB * TB / 256;   // staged elements per thread and operand
+  constexpr int EPT = TKB * TBt / 256;   // staged elements per thread and operand
   double ra[EPT], rb[EPT];
   auto load = [&](int kk) {
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {
       const int idx = tid + e * 256;
       int i, k;
-      if (g.transA) { k = idx & (TKB - 1); i = idx / TKB; } else { i = idx & 127; k = idx >> 7; }
+      if (g.transA) { k = idx & (TKB - 1); i = idx / TKB; } else { i = idx & (TBt - 1); k = idx / TBt; }
       const int gi = m0 + i, gk = kk + k;
       double v = 0.;
       if (gi < g.M && gk < k_end && gk >= k_begin && !(g.a_lower && gk > gi) && !(g.a_upper && gk < gi))
         v = g.transA ? g.A[(size_t)gk + (size_t)gi * g.lda] : g.A[(size_t)gi + (size_t)gk * g.lda];
       ra[e] = v;
       int j, kb;
-      if (g.transB) { j = idx & 127; kb = idx >> 7; } else { kb = idx & (TKB - 1); j = idx / TKB; }
+      if (g.transB) { j = idx & (TBt - 1); kb = idx / TBt; } else { kb = idx & (TKB - 1); j = idx / TKB; }
       const int gj = n0 + j, gkb = kk + kb;
       double w = 0.;
       if (gj < g.N && gkb < k_end && gkb >= k_begin && !(g.b_lower && gkb < gj))
@@ -193,11 +181,11 @@ gemm_f64_big_kernel(GemmArgs g) {
     for (int e = 0; e < EPT; ++e) {
       const int idx = tid + e * 256;
       int i, k;
-      if (g.transA) { k = idx & (TKB - 1); i = idx / TKB; } else { i = idx & 127; k = idx >> 7; }
-      As[buf][k][SWZ(k, i)] = ra[e];
+      if (g.transA) { k = idx & (TKB - 1); i = idx / TKB; } else { i = idx & (TBt - 1); k = idx / TBt; }
+      As[buf][k][i] = ra[e];
       int j, kb;
-      if (g.transB) { j = idx & 127; kb = idx >> 7; } else { kb = idx & (TKB - 1); j = idx / TKB; }
-      Bs[buf][kb][SWZ(kb, j)] = rb[e];
+      if (g.transB) { j = idx & (TBt - 1); kb = idx / TBt; } else { kb = idx & (TKB - 1); j = idx / TKB; }
+      Bs[buf][kb][j] = rb[e];
     }
   };
   if (k_begin < k_end) {
@@ -212,25 +200,25 @@ gemm_f64_big_kernel(GemmArgs g) {
 #pragma unroll
     for (int k4 = 0; k4 < TKB; k4 += 4) {
       const int kl = k4 + (lane >> 4);
-      double a[4], b[4];
+      double a[WT], b[WT];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        a[q] = As[buf][kl][SWZ(kl, wm + 16 * q + (lane & 15))];
-        b[q] = Bs[buf][kl][SWZ(kl, wn + 16 * q + (lane & 15))];
+      for (int q = 0; q < WT; ++q) {
+        a[q] = As[buf][kl][wm + 16 * q + (lane & 15)];
+        b[q] = Bs[buf][kl][wn + 16 * q + (lane & 15)];
       }
 #pragma unroll
-      for (int p = 0; p < 4; ++p)
+      for (int p = 0; p < WT; ++p)
 #pragma unroll
-        for (int q = 0; q < 4; ++q) acc[p][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[p], b[q], acc[p][q], 0, 0, 0);
+        for (int q = 0; q < WT; ++q) acc[p][q] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[p], b[q], acc[p][q], 0, 0, 0);
     }
     if (more) store(buf ^ 1);   // the other buffer: last read before the previous barrier
     __syncthreads();
     buf ^= 1;
   }
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+  for (int a = 0; a < WT; ++a)
 #pragma unroll
-    for (int b = 0; b < 4; ++b)
+    for (int b = 0; b < WT; ++b)
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {
         const int i = m0 + wm + a * 16 + (lane >> 4) + 4 * rg;
@@ -242,7 +230,12 @@ gemm_f64_big_kernel(GemmArgs g) {
         }
       }
 }
-#undef SWZ
+
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) gemm_f64_big_kernel(GemmArgs g) {
+  gemm_tile_body<128>(g);
+}
+
+__global__ void __launch_bounds__(256) gemm_f64_pipe_kernel(GemmArgs g) { gemm_tile_body<64>(g); }
 
 // Lower triangle (i >= j) of Psi = Sigma + I, tile-parallel, upper tiles skipped.
 template <int COV>
@@ -321,6 +314,9 @@ __global__ void __launch_bounds__(256) potrf_diag_kernel(double* A, int lda, int
 // fma (c - l_rj * l_cj) in the same order, and column c of L^-1 is lane c's forward
 // substitution over the LDS copy of L (terms p < c are exact zeros, so the sums equal the
 // p = c.. form).
+#ifndef GPB_DIAG_NOMASK
+#define GPB_DIAG_NOMASK 1
+#endif
 __global__ void __launch_bounds__(64) potrf_diag_wave_kernel(double* A, int lda, int j0, int ib, double* Winv,
                                                              int ldw, int* info) {
   __shared__ double colb[2][64];
@@ -345,9 +341,16 @@ __global__ void __launch_bounds__(64) potrf_diag_wave_kernel(double* A, int lda,
       if (r >= j) row[j] = l;
       colb[j & 1][r] = l;
       __syncthreads();   // one wave: orders the LDS write before the reads
+#if GPB_DIAG_NOMASK
+      // no c <= r mask: lanes r < j have l = 0 here, and the entries c > r this updates (upper
+      // part) are never read as L (the inverse reads p < i and the diagonal; stores mask c <= r)
+#pragma unroll
+      for (int c = j + 1; c < 64; ++c) row[c] = fma(-l, colb[j & 1][c], row[c]);
+#else
 #pragma unroll
       for (int c = j + 1; c < 64; ++c)
         if (c <= r) row[c] = fma(-l, colb[j & 1][c], row[c]);
+#endif
     }
   }
 #pragma unroll
@@ -497,7 +500,11 @@ void gemm(hipStream_t s, int M, int N, int K, double alpha, const double* A, int
     return;
   }
   dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM);
-  hipLaunchKernelGGL(gemm_f64_kernel, grid, dim3(256), 0, s, g);
+  static const bool unpiped = std::getenv("GPBOOST_AMD_GEMM_UNPIPED") != nullptr;   // A/B: round-1 64-tile form
+  if (unpiped)
+    hipLaunchKernelGGL(gemm_f64_kernel, grid, dim3(256), 0, s, g);
+  else
+    hipLaunchKernelGGL(gemm_f64_pipe_kernel, grid, dim3(256), 0, s, g);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -540,6 +547,9 @@ DenseSolver::DenseSolver(int n, int d, const double* d_X, hipStream_t stream)
 DenseSolver::~DenseSolver() {
   if (h_red_) (void)hipHostFree(h_red_);
   for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
+  for (auto& e : ev_la_) if (e) (void)hipEventDestroy(e);
+  if (s_chain_) (void)hipStreamDestroy(s_chain_);
+  if (s_rest_) (void)hipStreamDestroy(s_rest_);
 }
 
 void DenseSolver::Potrf() {
@@ -579,6 +589,66 @@ void DenseSolver::Potrf() {
   }
 }
 
+// The same factorization with one panel of lookahead: after panel J's inner steps, the trailing
+// update is split into the next panel's columns (on the chain stream, immediately) and the rest
+// (on a second stream), so panel J+1's diagonal factorizations, TRSMs and panel updates run
+// while the bulk of panel J's SYRK is still in flight. Every output element receives the same
+// products in the same order as Potrf() (per-element K order is tile-size independent), so the
+// factor is bitwise identical.
+void DenseSolver::PotrfLookahead() {
+  const int n = n_, ld = ld_;
+  double* A = A_.get();
+  double* W = W_.get();
+  constexpr int NBO = 256, NBI = 64;
+  if (!s_chain_) {
+    int lo = 0, hi = 0;
+    HIP_CHECK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIP_CHECK(hipStreamCreateWithPriority(&s_chain_, hipStreamNonBlocking, hi));
+    HIP_CHECK(hipStreamCreateWithPriority(&s_rest_, hipStreamNonBlocking, lo));
+    for (auto& e : ev_la_) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  hipEvent_t ev_in = ev_la_[0], ev_panel = ev_la_[1], ev_rest = ev_la_[2];
+  HIP_CHECK(hipEventRecord(ev_in, stream_));
+  HIP_CHECK(hipStreamWaitEvent(s_chain_, ev_in, 0));
+  HIP_CHECK(hipStreamWaitEvent(s_rest_, ev_in, 0));
+  bool rest_pending = false;
+  for (int J0 = 0; J0 < n; J0 += NBO) {
+    const int jb = std::min(NBO, n - J0);
+    for (int j0 = J0; j0 < J0 + jb; j0 += NBI) {
+      const int ib = std::min(NBI, J0 + jb - j0);
+      hipLaunchKernelGGL(potrf_diag_wave_kernel, dim3(1), dim3(64), 0, s_chain_, A, ld, j0, ib, W, ld, info_.get());
+      HIP_CHECK(hipGetLastError());
+      const int r0 = j0 + ib;
+      if (r0 < n)
+        gemm(s_chain_, n - r0, ib, ib, 1., A + r0 + (size_t)j0 * ld, ld, 0, W + j0 + (size_t)j0 * ld, ld, 1, 0.,
+             A + r0 + (size_t)j0 * ld, ld, 0, 0, 0, 0);
+      if (r0 < J0 + jb)
+        gemm(s_chain_, n - r0, J0 + jb - r0, ib, -1., A + r0 + (size_t)j0 * ld, ld, 0, A + r0 + (size_t)j0 * ld, ld, 1,
+             1., A + r0 + (size_t)r0 * ld, ld, 1, 0, 0, 0);
+    }
+    const int t0 = J0 + jb;
+    if (t0 >= n) break;
+    const int nb = std::min(NBO, n - t0);   // the next panel's columns
+    // the previous rest update wrote these columns: wait for it before touching them
+    if (rest_pending) HIP_CHECK(hipStreamWaitEvent(s_chain_, ev_rest, 0));
+    HIP_CHECK(hipEventRecord(ev_panel, s_chain_));   // panel J final
+    gemm(s_chain_, n - t0, nb, jb, -1., A + t0 + (size_t)J0 * ld, ld, 0, A + t0 + (size_t)J0 * ld, ld, 1, 1.,
+         A + t0 + (size_t)t0 * ld, ld, 1, 0, 0, 0);
+    const int t1 = t0 + nb;
+    if (t1 < n) {
+      HIP_CHECK(hipStreamWaitEvent(s_rest_, ev_panel, 0));
+      gemm(s_rest_, n - t1, n - t1, jb, -1., A + t1 + (size_t)J0 * ld, ld, 0, A + t1 + (size_t)J0 * ld, ld, 1, 1.,
+           A + t1 + (size_t)t1 * ld, ld, 1, 0, 0, 0);
+      HIP_CHECK(hipEventRecord(ev_rest, s_rest_));
+      rest_pending = true;
+    }
+  }
+  HIP_CHECK(hipEventRecord(ev_panel, s_chain_));
+  HIP_CHECK(hipStreamWaitEvent(stream_, ev_panel, 0));
+  HIP_CHECK(hipEventRecord(ev_rest, s_rest_));
+  HIP_CHECK(hipStreamWaitEvent(stream_, ev_rest, 0));
+}
+
 void DenseSolver::Trtri(int a, int b) {
   // W[a:b, a:b] = L[a:b, a:b]^-1 (lower); diagonal 64-blocks were inverted by potrf_diag.
   if (b - a <= 64) return;
@@ -615,7 +685,11 @@ void DenseSolver::Eval(int cov_type, double var, double phi, const double* d_y, 
                        phi, A);
   });
   HIP_CHECK(hipGetLastError());
-  Potrf();
+  static const bool no_lookahead = std::getenv("GPBOOST_AMD_DENSE_NO_LOOKAHEAD") != nullptr;   // A/B
+  if (!no_lookahead)
+    PotrfLookahead();
+  else
+    Potrf();
   HIP_CHECK(hipEventRecord(ev_[1], stream_));
   hipLaunchKernelGGL(logdet_kernel, dim3(1), dim3(256), 0, stream_, A, ld, n, dred + 0);
   Trtri(0, n);
