@@ -146,7 +146,11 @@ class GPModel:
         self.params = {"cg_max_num_it": 1000, "cg_max_num_it_tridiag": 1000, "cg_delta_conv": 1e-2,
                        "num_rand_vec_trace": 50, "reuse_rand_vec_trace": True, "seed_rand_vec_trace": 1,
                        "cg_preconditioner_type": None, "init_aux_pars": None, "estimate_aux_pars": True,
-                       "delta_conv_mode_finding": -1.}
+                       "delta_conv_mode_finding": -1.,
+                       # covariance-parameter optimizer (reference basic.py:4510-4533 defaults)
+                       "optimizer_cov": None, "init_cov_pars": None, "maxit": 1000, "delta_rel_conv": -1.,
+                       "lr_cov": -1., "m_lbfgs": -1, "trace": False,
+                       "convergence_criterion": "relative_change_in_log_likelihood"}
 
     def __del__(self):
         try:
@@ -171,27 +175,59 @@ class GPModel:
         return cp
 
     def set_optim_params(self, params=None):
-        """Store likelihood-path settings through GPB_SetOptimConfig (reference basic.py:5380-5540).
-        Optimizer-only keys are accepted and ignored (the optimizer is outside this library)."""
+        """Store likelihood-path and optimizer settings through GPB_SetOptimConfig (reference
+        basic.py:5380-5540). Covariance-parameter optimizer: "lbfgs" (the reference default) only;
+        keys of the other optimizers (gradient descent, Nesterov, coefficients) are accepted and have
+        no effect."""
         if params:
             for key, val in params.items():
                 if key == "init_aux_pars" and val is not None:
                     val = _as1d(val, "params['init_aux_pars']")
                     if val.shape[0] != self.num_aux_pars:
                         raise ValueError("params['init_aux_pars'] does not contain the correct number of parameters")
+                if key == "init_cov_pars" and val is not None:
+                    val = _as1d(val, "params['init_cov_pars']")
+                    if val.shape[0] != self.num_cov_pars:
+                        raise ValueError("params['init_cov_pars'] does not contain the correct number of parameters")
                 self.params[key] = val
         p = self.params
         aux = p["init_aux_pars"]
+        init = p["init_cov_pars"]
         no_index = np.array([-1], dtype=np.int32)
         _safe_call(lib().GPB_SetOptimConfig(
-            self.handle, None, -1., 0.5, 1000, -1., True, 0, False, None, 2,
-            b"relative_change_in_log_likelihood", 0, None, 0.1, 0.5, None,
+            self.handle, _dp(init) if init is not None else None, float(p["lr_cov"]), 0.5, int(p["maxit"]),
+            float(p["delta_rel_conv"]), True, 0, bool(p["trace"]), c_str(p["optimizer_cov"]), 2,
+            c_str(p["convergence_criterion"]), 0, None, 0.1, 0.5, None,
             int(p["cg_max_num_it"]), int(p["cg_max_num_it_tridiag"]), float(p["cg_delta_conv"]),
             int(p["num_rand_vec_trace"]), bool(p["reuse_rand_vec_trace"]),
             p["cg_preconditioner_type"].encode() if p["cg_preconditioner_type"] else None,
             int(p["seed_rand_vec_trace"]), -1, _dp(aux) if aux is not None else None,
-            bool(p["estimate_aux_pars"]), no_index.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), -1,
+            bool(p["estimate_aux_pars"]), no_index.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), int(p["m_lbfgs"]),
             float(p["delta_conv_mode_finding"])))
+
+    def fit(self, y, X=None, params=None, offset=None, fixed_effects=None):
+        """Estimate the covariance parameters by maximising the (approximate marginal) likelihood
+        (reference basic.py:5067-5275 -> GPB_OptimCovPar). Covariates X are out of scope."""
+        if fixed_effects is not None:
+            raise GPBoostError("The argument 'fixed_effects' is discontinued. Use the renamed equivalent argument 'offset' instead")
+        if X is not None:
+            raise GPBoostError("linear regression covariates (X) are out of scope for gpboost_amd")
+        y = self._check_y(y)
+        off = None
+        if offset is not None:
+            off = _as1d(offset, "offset")
+            if off.shape[0] != self.num_data:
+                raise ValueError("Incorrect number of data points in 'offset'")
+        self.set_optim_params(params)
+        _safe_call(lib().GPB_OptimCovPar(self.handle, _dp(y), _dp(off) if off is not None else None))
+        self.model_fitted = True
+        return self
+
+    def get_num_optim_iter(self):
+        """Number of optimizer iterations of the last fit (GPB_GetNumIt)."""
+        k = ctypes.c_int(0)
+        _safe_call(lib().GPB_GetNumIt(self.handle, ctypes.byref(k)))
+        return k.value
 
     def get_aux_pars(self):
         out = np.zeros(max(self.num_aux_pars, 1))

@@ -156,14 +156,17 @@ int GPB_SetOptimConfig(REModelHandle handle, double* init_cov_pars, double lr, d
                        const char* cg_preconditioner_type, int seed_rand_vec_trace, int piv_chol_rank,
                        double* init_aux_pars, bool estimate_aux_pars, const int* estimate_cov_par_index,
                        int m_lbfgs, double delta_conv_mode_finding) {
-  // re_model_template.h:686-823: only the settings of the likelihood path are stored; the
-  // optimizer settings belong to GPB_OptimCovPar, which is outside this library's scope.
+  // re_model.cpp:234-332 / re_model_template.h:686-823: the settings of the likelihood path and
+  // of the covariance-parameter optimizer (GPB_OptimCovPar; "lbfgs" only). Settings of the
+  // gradient-descent / Nesterov / coefficient optimizers have no effect here (no covariates).
   API_BEGIN();
-  (void)init_cov_pars; (void)lr; (void)acc_rate_cov; (void)max_iter; (void)delta_rel_conv; (void)use_nesterov_acc;
-  (void)nesterov_schedule_version; (void)trace; (void)optimizer; (void)momentum_offset; (void)convergence_criterion;
-  (void)num_covariates; (void)init_coef; (void)lr_coef; (void)acc_rate_coef; (void)optimizer_coef;
-  (void)piv_chol_rank; (void)m_lbfgs;
+  (void)acc_rate_cov; (void)use_nesterov_acc; (void)nesterov_schedule_version; (void)trace; (void)momentum_offset;
+  (void)convergence_criterion;   // L-BFGS always tests the relative change of the objective (optim_utils.h:656-657)
+  (void)lr_coef; (void)acc_rate_coef; (void)optimizer_coef; (void)piv_chol_rank;
   REModelAMD* m = model(handle);
+  if (num_covariates > 0 || init_coef != nullptr)
+    gpb_amd::Fatal("linear regression coefficients (covariates) are not supported by gpboost_amd");
+  m->SetOptimSettings(init_cov_pars, lr, max_iter, delta_rel_conv, optimizer, m_lbfgs);
   if (m->config().matrix_inversion_method == "iterative") {   // :775-801
     m->iter.cg_max_num_it = cg_max_num_it;
     m->iter.cg_max_num_it_tridiag = cg_max_num_it_tridiag;
@@ -179,7 +182,10 @@ int GPB_SetOptimConfig(REModelHandle handle, double* init_cov_pars, double lr, d
   m->iter.seed_rand_vec_trace = seed_rand_vec_trace;
   m->iter.reuse_rand_vec_trace = reuse_rand_vec_trace;
   if (delta_conv_mode_finding > 0.) m->iter.delta_conv_mode_finding = delta_conv_mode_finding;   // :820-822
-  if (init_aux_pars != nullptr) m->SetAuxPars(init_aux_pars);
+  if (init_aux_pars != nullptr) {
+    m->SetAuxPars(init_aux_pars);
+    m->aux_pars_set_ = true;
+  }
   m->estimate_aux_pars = estimate_aux_pars;   // :803
   if (estimate_cov_par_index != nullptr && estimate_cov_par_index[0] >= 0) {
     for (int k = 0; k < m->num_cov_pars(); ++k)
@@ -302,8 +308,14 @@ int GPB_GetCovPar(REModelHandle handle, double* cov_par, bool calc_std_dev) {
 
 int GPB_GetNumIt(REModelHandle handle, int* num_it) {
   API_BEGIN();
-  (void)model(handle);
-  num_it[0] = 0;
+  num_it[0] = model(handle)->num_it();
+  API_END();
+}
+
+int GPB_OptimCovPar(REModelHandle handle, const double* y_data, const double* fixed_effects) {
+  // c_api.cpp GPB_OptimCovPar -> REModel::OptimCovPar(y, fixed_effects, false, false)
+  API_BEGIN();
+  model(handle)->OptimCovPar(y_data, fixed_effects);
   API_END();
 }
 

@@ -1,0 +1,397 @@
+// GPB_OptimCovPar: L-BFGS covariance-parameter estimation over the device likelihood.
+// See optim.h for the reference functions this restates.
+#include "optim.h"
+
+#include <algorithm>
+#include <cmath>
+#include <limits>
+#include <numeric>
+#include <random>
+
+#include "cov.h"
+#include "re_model.h"
+
+namespace gpb_amd {
+
+namespace {
+
+double dot(const std::vector<double>& a, const std::vector<double>& b) {
+  double s = 0.;
+  for (size_t i = 0; i < a.size(); ++i) s += a[i] * b[i];
+  return s;
+}
+
+double norm2(const std::vector<double>& a) { return std::sqrt(dot(a, a)); }
+
+// Limited-memory inverse-Hessian approximation: a ring of the last m (s, y) pairs and the
+// two-loop recursion (Nocedal & Wright Alg. 7.4), as BFGSMat.h:89-105 / 160-186 keeps it.
+class InverseHessian {
+ public:
+  InverseHessian(int dim, int m) : m_(m), s_(m, std::vector<double>(dim)), y_(m, std::vector<double>(dim)),
+                                   ys_(m), alpha_(m) {}
+  void Add(const std::vector<double>& s, const std::vector<double>& y) {
+    const int loc = ptr_ % m_;
+    s_[loc] = s;
+    y_[loc] = y;
+    ys_[loc] = dot(s, y);
+    theta_ = dot(y, y) / ys_[loc];
+    if (count_ < m_) ++count_;
+    ptr_ = loc + 1;
+  }
+  // out = a * H * v
+  void Apply(const std::vector<double>& v, double a, std::vector<double>& out) {
+    out.resize(v.size());
+    for (size_t i = 0; i < v.size(); ++i) out[i] = a * v[i];
+    int j = ptr_ % m_;
+    for (int k = 0; k < count_; ++k) {   // newest to oldest
+      j = (j + m_ - 1) % m_;
+      alpha_[j] = dot(s_[j], out) / ys_[j];
+      for (size_t i = 0; i < out.size(); ++i) out[i] -= alpha_[j] * y_[j][i];
+    }
+    for (double& o : out) o /= theta_;
+    for (int k = 0; k < count_; ++k) {   // oldest to newest
+      const double beta = dot(y_[j], out) / ys_[j];
+      for (size_t i = 0; i < out.size(); ++i) out[i] += (alpha_[j] - beta) * s_[j][i];
+      j = (j + 1) % m_;
+    }
+  }
+
+ private:
+  int m_;
+  std::vector<std::vector<double>> s_, y_;
+  std::vector<double> ys_, alpha_;
+  double theta_ = 1.;
+  int count_ = 0;
+  int ptr_ = 0;   // ptr_ % m_ is the next slot (BFGSMat reset sets m_ptr = m, i.e. slot 0)
+};
+
+// LineSearchBacktracking::LineSearch with the Armijo rule and GPBoost's changes
+// (LineSearchBacktracking.h:45-143): shrink by 1/2, or by 1/32 after a large increase;
+// after max_linesearch trials fall back to xp (step 0).
+void backtracking(LbfgsObjective& f, const LbfgsSettings& s, const std::vector<double>& xp,
+                  const std::vector<double>& drt, double& step, double& fx, std::vector<double>& grad,
+                  std::vector<double>& x) {
+  if (step <= 0.) Fatal("GPModel lbfgs: 'step' must be positive");
+  const double fx_init = fx;
+  const double dg_init = dot(grad, drt);
+  if (dg_init > 0) Fatal("GPModel lbfgs: the moving direction increases the objective function value");
+  const double test_decr = s.ftol * dg_init;
+  int iter = 0;
+  for (; iter < s.max_linesearch; ++iter) {
+    for (size_t i = 0; i < x.size(); ++i) x[i] = xp[i] + step * drt[i];
+    fx = f.Eval(x, grad, true, false, iter == 0);
+    if (fx > fx_init + step * test_decr || fx != fx) {
+      const double width = (fx - fx_init) > 2. * std::max(std::fabs(fx_init), 1.) ? 0.5 / 16. : 0.5;
+      step *= width;
+    } else {
+      break;   // Armijo condition met
+    }
+  }
+  if (iter >= s.max_linesearch) {
+    x = xp;
+    f.ResetProfiledOutVariablesToLag1();
+    fx = fx_init;
+    step = 0.;
+  }
+}
+
+}  // namespace
+
+int lbfgs_minimize(LbfgsObjective& f, std::vector<double>& x, double& fx, const LbfgsSettings& s) {
+  // LBFGS.h:86-301 (past = 1, epsilon = epsilon_rel = 1e-20, no neighbour re-determination)
+  const int n = (int)x.size();
+  InverseHessian H(n, s.m);
+  std::vector<double> grad(n), xp(n), gradp(n), drt(n), vs(n), vy(n);
+  fx = f.Eval(x, grad, true, true, true);
+  if (std::isnan(fx) || std::isinf(fx))
+    Fatal("%s occurred in initial negative log-likelihood. Possible solutions: try other initial values ('init_cov_pars')",
+          std::isnan(fx) ? "NaN" : "Inf");
+  const double eps_grad = 1e-20;
+  double gnorm = norm2(grad);
+  double fx_lag = fx;
+  if (gnorm <= eps_grad || gnorm <= eps_grad * norm2(x)) return 1;
+  for (int i = 0; i < n; ++i) drt[i] = -grad[i];
+  double step = s.initial_step_factor / norm2(drt);
+  const double eps = std::numeric_limits<double>::epsilon();
+  for (int k = 1;; ++k) {
+    xp = x;
+    gradp = grad;
+    // GetMaximalLearningRate (optim_utils.h:497-534 -> MaximalLearningRateCovAuxPars,
+    // re_model_template.h:4937-4945): no parameter changes by more than a factor of 100 per step
+    double max_abs = 0.;
+    for (int i = 0; i < n; ++i) max_abs = std::max(max_abs, std::fabs(drt[i]));
+    const double max_lr = s.max_log_change / max_abs;
+    if (max_lr < step) step = max_lr;
+    backtracking(f, s, xp, drt, step, fx, grad, x);
+    f.Eval(x, grad, false, true, false);   // gradient at the accepted point
+    gnorm = norm2(grad);
+    bool converged = gnorm <= eps_grad || gnorm <= eps_grad * norm2(x);
+    if ((fx_lag - fx) <= s.delta * std::max(std::fabs(fx_lag), 1.)) converged = true;
+    if (s.max_iterations != 0 && k >= s.max_iterations) converged = true;
+    f.SetLag1ProfiledOutVariables();
+    if (converged) return k;
+    for (int i = 0; i < n; ++i) {
+      vs[i] = x[i] - xp[i];
+      vy[i] = grad[i] - gradp[i];
+    }
+    if (dot(vs, vy) > eps * dot(vy, vy)) H.Add(vs, vy);
+    step = 1.;
+    H.Apply(grad, -1., drt);
+    fx_lag = fx;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// REModelAMD: initial values and the optimization driver
+
+namespace {
+
+// cov_fcts.h (TransformBackCovPars): phi -> range
+double range_back(int cov_type, double phi) {
+  switch (cov_type) {
+    case kMatern05: return 1. / phi;
+    case kMatern15: return std::sqrt(3.) / phi;
+    case kMatern25: return std::sqrt(5.) / phi;
+    default: return 1. / std::sqrt(phi);
+  }
+}
+
+// utils.h:189-202 CalculateMedianPartiallySortInput
+double median_partial_sort(std::vector<double>& v) {
+  const int num = (int)v.size();
+  const int pos = num / 2;
+  std::nth_element(v.begin(), v.begin() + pos, v.end());
+  double med = v[pos];
+  if (num % 2 == 0) {
+    std::nth_element(v.begin(), v.begin() + pos - 1, v.end());
+    med = (med + v[pos - 1]) / 2.;
+  }
+  return med;
+}
+
+constexpr double kEpsilonNumbers = 1e-10;   // EPSILON_NUMBERS (utils.h)
+
+}  // namespace
+
+double REModelAMD::InitialRangeTrafo() const {
+  // cov_fcts.h:1275-1450 FindInitCovPar: median distance among (at most 1000 sampled) points;
+  // correlation 0.05 at half the median distance. The sample draws continue the model's
+  // mt19937(seed) after the Vecchia ordering shuffle (re_model_template.h:154,
+  // Vecchia_utils.cpp:1094-1095).
+  const int n = cfg_.n, d = cfg_.d;
+  const int kMaxPoints = 1000;
+  const int nf = std::min(n, kMaxPoints);
+  std::vector<int> idx(nf);
+  if (nf < n) {
+    std::mt19937 rng(cfg_.seed);
+    if (vecchia_ && cfg_.vecchia_ordering == "random") {
+      std::vector<int> dummy(n);
+      std::iota(dummy.begin(), dummy.end(), 0);
+      std::shuffle(dummy.begin(), dummy.end(), rng);
+    }
+    std::uniform_int_distribution<> dis(0, n - 1);
+    for (int i = 0; i < nf; ++i) idx[i] = dis(rng);
+  } else {
+    std::iota(idx.begin(), idx.end(), 0);
+  }
+  const std::vector<double>& X = coords_vo_;   // the GP component's coordinates (Vecchia order)
+  std::vector<double> dist((size_t)nf * (nf - 1) / 2);
+  size_t p = 0;
+  for (int i = 0; i < nf - 1; ++i)
+    for (int j = i + 1; j < nf; ++j) {
+      double s = 0.;
+      for (int q = 0; q < d; ++q) {
+        const double t = X[(size_t)idx[i] * d + q] - X[(size_t)idx[j] * d + q];
+        s += t * t;
+      }
+      dist[p++] = std::sqrt(s);
+    }
+  if (dist.empty()) Fatal("Cannot find an initial value for the range parameter with a single data point");
+  double med = median_partial_sort(dist);
+  if (med < kEpsilonNumbers) med = std::accumulate(dist.begin(), dist.end(), 0.) / (double)dist.size();
+  if (med < kEpsilonNumbers)
+    Fatal("Cannot find an initial value for the range parameter since both the median and the average distances among coordinates are zero %s",
+          nf < n ? "on a random sub-sample of size 1000 " : "");
+  switch (cfg_.cov_type) {
+    case kMatern05: return 2. * 3. / med;
+    case kMatern15: return 2. * 4.7 / med;
+    case kMatern25: return 2. * 5.9 / med;
+    default: return 3. / std::pow(med / 2., 2.);
+  }
+}
+
+void REModelAMD::FindInitCovPar(const double* y, double* trafo) const {
+  // re_model_template.h:4388-4504 for one GP component
+  const int n = cfg_.n;
+  double var = 0.;
+  const bool gauss_data = !cfg_.latent || cfg_.lik == kLikGaussian;
+  if (gauss_data) {
+    double mean = 0.;
+    for (int i = 0; i < n; ++i) mean += y[i];
+    mean /= n;
+    for (int i = 0; i < n; ++i) var += (y[i] - mean) * (y[i] - mean);
+    var /= (n - 1);
+  }
+  if (!cfg_.latent) {
+    trafo[0] = var / 2.;   // nugget
+    trafo[1] = 1.;         // marginal variance / nugget
+    trafo[2] = InitialRangeTrafo();
+  } else {
+    trafo[0] = cfg_.lik == kLikGaussian ? var / 2. : 1.;
+    trafo[1] = InitialRangeTrafo();
+  }
+}
+
+void REModelAMD::SetOptimSettings(const double* init_cov_pars, double lr, int max_iter, double delta_rel_conv,
+                                  const char* optimizer, int m_lbfgs) {
+  // re_model.cpp:264-279 and re_model_template.h:710-823
+  if (optimizer != nullptr && optimizer[0] != '\0') {
+    const std::string o(optimizer);
+    if (o != "lbfgs")
+      Fatal("Optimizer option '%s' is not supported for covariance parameters by gpboost_amd (supported: lbfgs)", o.c_str());
+  }
+  if (init_cov_pars != nullptr) {
+    init_cov_pars_.assign(init_cov_pars, init_cov_pars + num_cov_pars());
+    for (double v : init_cov_pars_)
+      if (!(v > 0.)) Fatal("init_cov_pars must be > 0");
+    cov_pars_orig_ = init_cov_pars_;
+    cov_pars_initialized_ = true;
+  }
+  optim_.initial_step_factor = lr < 0. ? 1. : lr;               // SetInitialValueLRCov :7505-7521
+  optim_.max_iterations = max_iter;
+  optim_.delta = delta_rel_conv < 0. ? 1e-6 : delta_rel_conv;   // SetInitialValueDeltaRelConv :7524-7533
+  if (m_lbfgs > 0) optim_.m = m_lbfgs;
+}
+
+namespace {
+
+// EvalLLforLBFGSpp for the Gaussian likelihood with the nugget profiled out
+// (optim_utils.h:269-313, 333-348): x = log(sigma1^2 / sigma^2, phi).
+class GaussianProfiledObjective : public LbfgsObjective {
+ public:
+  GaussianProfiledObjective(REModelAMD* m) : m_(m) {}
+  double Eval(const std::vector<double>& x, std::vector<double>& grad, bool eval_ll, bool calc_grad,
+              bool hint_grad) override {
+    if (eval_ll || !(has_grad_ && x == x_)) {
+      const double trafo[3] = {1., std::exp(x[0]), std::exp(x[1])};
+      EvalResult r = m_->EvalTrafo(trafo, calc_grad || hint_grad, 1);
+      x_ = x;
+      nll_ = r.nll;
+      sigma2_ = r.sigma2;
+      has_grad_ = calc_grad || hint_grad;
+      if (has_grad_) grad_ = r.grad;
+    }
+    if (calc_grad) grad = grad_;
+    return nll_;
+  }
+  void SetLag1ProfiledOutVariables() override { sigma2_lag1_ = sigma2_; }
+  void ResetProfiledOutVariablesToLag1() override { sigma2_ = sigma2_lag1_; }
+  double sigma2() const { return sigma2_; }
+
+ private:
+  REModelAMD* m_;
+  std::vector<double> x_, grad_;
+  double nll_ = 0., sigma2_ = 1., sigma2_lag1_ = 1.;
+  bool has_grad_ = false;
+};
+
+// EvalLLforLBFGSpp for the latent (Laplace) models: x = log(sigma1^2, phi[, aux]).
+class LatentObjective : public LbfgsObjective {
+ public:
+  LatentObjective(REModelAMD* m, bool with_aux) : m_(m), with_aux_(with_aux) {}
+  double Eval(const std::vector<double>& x, std::vector<double>& grad, bool eval_ll, bool calc_grad,
+              bool hint_grad) override {
+    if (eval_ll || !(has_grad_ && x == x_)) {
+      const double trafo[2] = {std::exp(x[0]), std::exp(x[1])};
+      if (with_aux_) {
+        const double aux = std::exp(x[2]);
+        m_->SetAuxPars(&aux);
+      }
+      EvalResult r = m_->EvalLatentTrafo(trafo, calc_grad || hint_grad, /*fatal_on_nan=*/false);
+      x_ = x;
+      nll_ = r.nll;
+      has_grad_ = calc_grad || hint_grad;
+      if (has_grad_) grad_ = r.grad;
+    }
+    if (calc_grad) grad = grad_;
+    return nll_;
+  }
+
+ private:
+  REModelAMD* m_;
+  bool with_aux_;
+  std::vector<double> x_, grad_;
+  double nll_ = 0.;
+  bool has_grad_ = false;
+};
+
+}  // namespace
+
+void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects) {
+  // REModel::OptimCovPar (re_model.cpp:339-401) -> OptimLinRegrCoefCovPar without covariates
+  // (re_model_template.h:846-1700) -> OptimExternal "lbfgs" (optim_utils.h:561-706)
+  UseDevice();
+  const int n = cfg_.n;
+  std::vector<double> yv;
+  if (y != nullptr) {
+    yv.assign(y, y + n);
+    if (fixed_effects != nullptr) {
+      if (cfg_.latent && cfg_.lik != kLikGaussian)
+        Fatal("'fixed_effects' are not supported for likelihood '%s' by gpboost_amd", cfg_.likelihood.c_str());
+      for (int i = 0; i < n; ++i) yv[i] -= fixed_effects[i];
+    }
+    for (double v : yv)
+      if (std::isnan(v) || std::isinf(v)) Fatal("NaN or Inf in response variable / label ");
+    SetY(yv.data());
+  } else if (!y_set_) {
+    Fatal("response variable y has not been set");
+  }
+  EnsureStructure();
+  if (optim_.max_iterations <= 0) {   // max_iter_ = 0: nothing is estimated
+    num_it_ = 0;
+    return;
+  }
+  const bool with_aux = cfg_.latent && estimate_aux_pars && !aux_pars_.empty();
+  // initial values on the transformed scale (InitializeCovParsIfNotDefined re_model.cpp:1142-1164)
+  double trafo[3];
+  if (cov_pars_initialized_) {
+    if (cfg_.latent) { trafo[0] = cov_pars_orig_[0]; trafo[1] = range_trafo_of(cov_pars_orig_[1]); }
+    else TransformCovPars(cov_pars_orig_.data(), trafo);
+  } else {
+    if (yv.empty()) Fatal("initial covariance parameters need the response variable y");
+    FindInitCovPar(yv.data(), trafo);
+  }
+  if (with_aux && !aux_pars_set_) {
+    // likelihoods.h:1087-1116, 1223-1225 (FindInitialAuxPars, gaussian): sample variance / 2
+    if (yv.empty()) Fatal("initial auxiliary parameters need the response variable y");
+    double avg = 0., sum_sq = 0.;
+    for (int i = 0; i < n; ++i) { avg += yv[i]; sum_sq += yv[i] * yv[i]; }
+    avg /= n;
+    const double sample_var = std::max((sum_sq - n * avg * avg) / (n - 1), 1e-6);
+    aux_pars_[0] = sample_var / 2.;
+  }
+  std::vector<double> x;
+  double fx = 0.;
+  if (!cfg_.latent) {
+    x = {std::log(trafo[1]), std::log(trafo[2])};
+    GaussianProfiledObjective obj(this);
+    num_it_ = lbfgs_minimize(obj, x, fx, optim_);
+    const double s2 = obj.sigma2();
+    cov_pars_orig_ = {s2, std::exp(x[0]) * s2, range_back(cfg_.cov_type, std::exp(x[1]))};
+  } else {
+    x = {std::log(trafo[0]), std::log(trafo[1])};
+    if (with_aux) x.push_back(std::log(aux_pars_[0]));
+    LatentObjective obj(this, with_aux);
+    num_it_ = lbfgs_minimize(obj, x, fx, optim_);
+    cov_pars_orig_ = {std::exp(x[0]), range_back(cfg_.cov_type, std::exp(x[1]))};
+    if (with_aux) aux_pars_[0] = std::exp(x[2]);
+  }
+  for (double v : x)
+    if (std::isnan(v) || std::isinf(v))
+      Fatal("NaN or Inf occurred in covariance parameter optimization using 'lbfgs' (the reference's nelder_mead restart is not supported by gpboost_amd)");
+  cov_pars_initialized_ = true;
+  last_nll_ = fx;
+  last_cov_pars_ = cov_pars_orig_;
+}
+
+}  // namespace gpb_amd

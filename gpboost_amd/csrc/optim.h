@@ -1,0 +1,45 @@
+// Covariance-parameter estimation (GPB_OptimCovPar) on top of the device likelihood.
+//
+// The reference's default optimizer for covariance parameters is "lbfgs"
+// (re_model_template.h:7463-7466): L-BFGS on the log of the transformed parameters with an
+// Armijo backtracking line search, run by its vendored and modified LBFGSpp
+// (external_libs/LBFGSpp/include/LBFGS.h:86-301, LineSearchBacktracking.h:45-143,
+// BFGSMat.h:89-186) through the objective EvalLLforLBFGSpp (optim_utils.h:243-364) and the
+// driver OptimExternal (optim_utils.h:561-706). This is a restatement of that algorithm in plain
+// C++ (host side, O(P) work per iteration for P <= 3 parameters); every objective value and
+// gradient comes from the device evaluation of REModelAMD.
+#pragma once
+
+#include <vector>
+
+namespace gpb_amd {
+
+// LBFGSParam values set by OptimExternal (optim_utils.h:654-662) and the LBFGSpp defaults it
+// keeps (Param.h:182-190: ftol = 1e-4).
+struct LbfgsSettings {
+  int m = 6;                       // m_lbfgs_ (re_model_template.h:5355)
+  int max_iterations = 1000;       // max_iter_ (:5200)
+  double delta = 1e-6;             // delta_rel_conv_ (SetInitialValueDeltaRelConv :7524-7533), past = 1
+  double initial_step_factor = 1.; // lr_cov_init_ (SetInitialValueLRCov :7505-7521)
+  int max_linesearch = 20;
+  double ftol = 1e-4;
+  double max_log_change = 4.605170185988092;   // log(MAX_REL_CHANGE_GRADIENT_UPDATE_ = 100) (:5287-5289)
+};
+
+// Objective in the optimizer's coordinates x (log of the transformed parameters).
+class LbfgsObjective {
+ public:
+  virtual ~LbfgsObjective() = default;
+  // EvalLLforLBFGSpp::operator()(pars, gradient, eval_likelihood, calc_gradient). hint_grad: the
+  // caller expects to ask for the gradient at this x next (lets a device evaluation compute both).
+  virtual double Eval(const std::vector<double>& x, std::vector<double>& grad, bool eval_ll, bool calc_grad,
+                      bool hint_grad) = 0;
+  virtual void SetLag1ProfiledOutVariables() {}     // optim_utils.h (EvalLLforLBFGSpp) / LBFGS.h:232
+  virtual void ResetProfiledOutVariablesToLag1() {} // LineSearchBacktracking.h:133
+};
+
+// LBFGSSolver::minimize with LineSearchBacktracking (Armijo) as GPBoost runs it: returns the
+// number of iterations; x is overwritten with the minimiser and fx with its objective value.
+int lbfgs_minimize(LbfgsObjective& f, std::vector<double>& x, double& fx, const LbfgsSettings& s);
+
+}  // namespace gpb_amd

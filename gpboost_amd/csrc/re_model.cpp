@@ -5,6 +5,7 @@
 #include <cmath>
 #include <cstdlib>
 #include <cstring>
+#include <limits>
 
 #include "cov.h"
 #include "kernels.h"
@@ -29,7 +30,8 @@ int parse_cov(const std::string& name, double shape) {
   Fatal("cov_fct '%s' is not supported by gpboost_amd (supported: exponential, matern, gaussian)", name.c_str());
 }
 
-// cov_fcts.h:438-460: range rho -> phi on the transformed scale
+}  // namespace
+
 double range_trafo(int cov_type, double rho) {
   switch (cov_type) {
     case kMatern05: return 1. / rho;
@@ -38,8 +40,6 @@ double range_trafo(int cov_type, double rho) {
     default: return 1. / (rho * rho);
   }
 }
-
-}  // namespace
 
 REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : cfg_(cfg) {
   if (cfg_.n <= 0) Fatal("num_data must be > 0");
@@ -401,10 +401,19 @@ EvalResult REModelAMD::EvalLatent(const double* cov_pars_orig, bool want_grad) {
   if (!(cov_pars_orig[0] > 0. && cov_pars_orig[1] > 0.)) Fatal("covariance parameters must be > 0");
   // TransformCovPars for non-Gaussian likelihoods: no division by a nugget (cov_fcts.h:438-460)
   const double trafo[2] = {cov_pars_orig[0], range_trafo(cfg_.cov_type, cov_pars_orig[1])};
+  EvalResult res = EvalLatentTrafo(trafo, want_grad);
+  last_cov_pars_.assign(cov_pars_orig, cov_pars_orig + 2);
+  return res;
+}
+
+EvalResult REModelAMD::EvalLatentTrafo(const double* trafo, bool want_grad, bool fatal_on_nan) {
+  if (!y_set_) Fatal("response variable y has not been set");
+  UseDevice();
+  EnsureStructure();
   const double aux = aux_pars_.empty() ? 1. : aux_pars_[0];
   LatentResult r = latent_->Eval(cfg_.cov_type, cfg_.lik, trafo, aux, iter, want_grad,
                                  estimate_aux_pars && !aux_pars_.empty());
-  if (!std::isfinite(r.nll)) Fatal("NaN or Inf occurred in the approximate negative marginal log-likelihood");
+  if (fatal_on_nan && !std::isfinite(r.nll)) Fatal("NaN or Inf occurred in the approximate negative marginal log-likelihood");
   EvalResult res;
   res.nll = r.nll;
   res.grad = r.grad;
@@ -416,7 +425,6 @@ EvalResult REModelAMD::EvalLatent(const double* cov_pars_orig, bool want_grad) {
   events_pending_ = false;
   last_kernel_ms_[0] = last_kernel_ms_[1] = r.ms_total;
   last_nll_ = res.nll;
-  last_cov_pars_.assign(cov_pars_orig, cov_pars_orig + 2);
   return res;
 }
 
@@ -428,25 +436,32 @@ void REModelAMD::BenchLatentOperators(int t, int reps, double* out) {
 
 EvalResult REModelAMD::Eval(const double* cov_pars_orig, bool want_grad, int profile) {
   if (!y_set_) Fatal("response variable y has not been set");
-  UseDevice();
-  EnsureStructure();
   if (cfg_.latent) {
     if (profile) Fatal("profile_sigma2 is only defined for the Gaussian likelihood without 'vecchia_latent'");
     return EvalLatent(cov_pars_orig, want_grad);
   }
   double trafo[3];
   TransformCovPars(cov_pars_orig, trafo);
+  EvalResult res = EvalTrafo(trafo, want_grad, profile);
+  last_cov_pars_.assign(cov_pars_orig, cov_pars_orig + 3);
+  if (profile) last_cov_pars_[0] = res.sigma2;
+  return res;
+}
+
+EvalResult REModelAMD::EvalTrafo(const double* trafo, bool want_grad, int profile, bool fatal_on_nan) {
+  if (!y_set_) Fatal("response variable y has not been set");
+  UseDevice();
+  EnsureStructure();
   double sums[kVecchiaSums];
   if (vecchia_) EvalVecchia(trafo, sums);
   else EvalDense(trafo, want_grad, sums);
-  if (!std::isfinite(sums[0]) || !std::isfinite(sums[1]))
+  if (fatal_on_nan && (!std::isfinite(sums[0]) || !std::isfinite(sums[1])))
     Fatal("NaN or Inf occurred in the negative log-likelihood (non-positive-definite covariance?)");
   EvalResult res;
   res.grad.resize(profile ? 2 : 3);
   combine_partials(sums, cfg_.n, trafo[0], profile, &res.nll, res.grad.data(), &res.sigma2);
+  if (!std::isfinite(sums[0]) || !std::isfinite(sums[1])) res.nll = std::numeric_limits<double>::quiet_NaN();
   last_nll_ = res.nll;
-  last_cov_pars_.assign(cov_pars_orig, cov_pars_orig + 3);
-  if (profile) last_cov_pars_[0] = res.sigma2;
   return res;
 }
 

@@ -19,6 +19,7 @@
 #include "common.h"
 #include "dense.h"
 #include "latent.h"
+#include "optim.h"
 
 namespace gpb_amd {
 
@@ -38,6 +39,9 @@ struct ModelConfig {
   bool latent = false;     // latent GP + Laplace approximation (non-Gaussian or "vecchia_latent")
   int lik = 0;             // LatentLik code when latent
 };
+
+// cov_fcts.h:438-460: range rho -> phi on the transformed scale
+double range_trafo(int cov_type, double rho);
 
 struct EvalResult {
   double nll = 0.;
@@ -93,12 +97,29 @@ class REModelAMD {
   double last_nll() const { return last_nll_; }
   const std::vector<double>& last_cov_pars() const { return last_cov_pars_; }
 
+  // Covariance-parameter estimation (GPB_SetOptimConfig / GPB_OptimCovPar / GPB_GetNumIt;
+  // re_model.cpp:234-401, optim.cpp). Only the reference's default optimizer "lbfgs".
+  void SetOptimSettings(const double* init_cov_pars, double lr, int max_iter, double delta_rel_conv,
+                        const char* optimizer, int m_lbfgs);
+  void OptimCovPar(const double* y, const double* fixed_effects);
+  int num_it() const { return num_it_; }
+
+  // Evaluations on the transformed scale (used by the optimizer): Gaussian trafo =
+  // (sigma^2, sigma1^2 / sigma^2, phi); latent trafo = (sigma1^2, phi). fatal_on_nan = false
+  // returns a NaN / Inf objective instead of failing (the line search shrinks the step).
+  EvalResult EvalTrafo(const double* trafo, bool want_grad, int profile, bool fatal_on_nan = true);
+  EvalResult EvalLatentTrafo(const double* trafo, bool want_grad, bool fatal_on_nan = true);
+
   // iterative-method settings (GPB_SetOptimConfig, re_model_template.h:686-823)
   IterativeConfig iter;
   bool estimate_aux_pars = true;   // InitializeDefaultSettings (re_model_template.h:6492-6499) for latent models
+  bool aux_pars_set_ = false;      // aux_pars given by the caller (SetOptimConfig init_aux_pars / SetAuxPars)
 
  private:
   void TransformCovPars(const double* orig, double* trafo) const;
+  double range_trafo_of(double rho) const { return range_trafo(cfg_.cov_type, rho); }
+  void FindInitCovPar(const double* y, double* trafo) const;
+  double InitialRangeTrafo() const;
   void BuildVecchiaStructure();
   void EvalVecchia(const double* trafo, double* sums);  // sums over this rank's rows, all-reduced
   void LaunchVecchiaRows(const double* trafo, int r0, int r1, double* sums_host, bool allreduce);
@@ -146,6 +167,11 @@ class REModelAMD {
   double last_nll_ = 0.;
   std::vector<double> last_cov_pars_;
   double last_kernel_ms_[2] = {0., 0.};
+
+  LbfgsSettings optim_;
+  std::vector<double> init_cov_pars_, cov_pars_orig_;   // original scale
+  bool cov_pars_initialized_ = false;
+  int num_it_ = 0;
 };
 
 }  // namespace gpb_amd

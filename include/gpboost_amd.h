@@ -86,8 +86,11 @@ GPBOOST_AMD_EXPORT int GPB_CreateREModel(int32_t num_data,
 GPBOOST_AMD_EXPORT int GPB_REModelFree(REModelHandle handle);
 
 /* replaces GPB_SetOptimConfig (include/LightGBM/c_api.h:1433-1462; c_api.cpp:2770-2830).
- * Stored; the iterative-solver fields (cg_*, num_rand_vec_trace, seed_rand_vec_trace)
- * are the ones this build uses. */
+ * Stored: the iterative-solver fields (cg_*, num_rand_vec_trace, seed_rand_vec_trace,
+ * delta_conv_mode_finding), init_aux_pars / estimate_aux_pars, and the covariance-parameter
+ * optimizer fields GPB_OptimCovPar uses: init_cov_pars (original scale), lr (L-BFGS initial
+ * step factor, < 0: 1), max_iter, delta_rel_conv (< 0: 1e-6), optimizer (NULL / "" / "lbfgs";
+ * others fail), m_lbfgs (<= 0: 6). Covariates (num_covariates > 0, init_coef) fail. */
 GPBOOST_AMD_EXPORT int GPB_SetOptimConfig(REModelHandle handle,
     double* init_cov_pars,
     double lr,
@@ -165,8 +168,19 @@ GPBOOST_AMD_EXPORT int GPB_GetCurrentNegLogLikelihood(REModelHandle handle, doub
  * (original scale); std devs are not computed by this build (calc_std_dev must be false). */
 GPBOOST_AMD_EXPORT int GPB_GetCovPar(REModelHandle handle, double* cov_par, bool calc_std_dev);
 
-/* replaces GPB_GetNumIt (include/LightGBM/c_api.h:1559) */
+/* replaces GPB_GetNumIt (include/LightGBM/c_api.h:1559): iterations of the last GPB_OptimCovPar */
 GPBOOST_AMD_EXPORT int GPB_GetNumIt(REModelHandle handle, int* num_it);
+
+/* replaces GPB_OptimCovPar (include/LightGBM/c_api.h:1471; c_api.cpp GPB_OptimCovPar ->
+ * re_model.cpp:339-401): estimates the covariance parameters (and, for "vecchia_latent", the
+ * error variance aux par) with the reference's default optimizer "lbfgs" (optim_utils.h:561-706:
+ * L-BFGS on the log of the transformed parameters, Armijo backtracking, nugget profiled out for
+ * the Gaussian likelihood). Initial values: init_cov_pars of GPB_SetOptimConfig, the previous
+ * estimate, or the reference's FindInitCovPar heuristic (re_model_template.h:4388-4504). y may be
+ * NULL to reuse the response already set; fixed_effects (length n) is an offset (Gaussian:
+ * subtracted from y). Results: GPB_GetCovPar, GPB_GetAuxPars, GPB_GetNumIt,
+ * GPB_GetCurrentNegLogLikelihood. */
+GPBOOST_AMD_EXPORT int GPB_OptimCovPar(REModelHandle handle, const double* y_data, const double* fixed_effects);
 
 /* replaces GPB_GetLikelihoodName (include/LightGBM/c_api.h:1659) */
 GPBOOST_AMD_EXPORT int GPB_GetLikelihoodName(REModelHandle handle, char* out_str, int* num_char);

@@ -154,6 +154,57 @@ int main(int argc, char** argv) {
   }
   m->SetY(y.data());
 
+  if (mode == "fit") {
+    // GPB_OptimCovPar as the REModel facade runs it (re_model.cpp:339-401): initial values from
+    // init_cov_pars (original scale, SetOptimConfig re_model.cpp:264-279) or FindInitCovPar
+    // (InitializeCovParsIfNotDefined re_model.cpp:1142-1164), then OptimLinRegrCoefCovPar with the
+    // Python package's default optimizer settings (basic.py:4510-4533: lr_cov = -1,
+    // delta_rel_conv = -1, maxit = 1000, m_lbfgs = -1 -> C++ defaults; optimizer "lbfgs").
+    const int no_index[1] = {-1};
+    m->SetOptimConfig(std::atof(get(args, "lr_cov", "-1").c_str()), 0.5,
+                      std::atoi(get(args, "maxit", "1000").c_str()),
+                      std::atof(get(args, "delta_rel_conv", "-1").c_str()), true, 0, "lbfgs", 2,
+                      "relative_change_in_log_likelihood", 0.1, 0.5, "",
+                      std::atoi(get(args, "cg_max_num_it", "1000").c_str()),
+                      std::atoi(get(args, "cg_max_num_it", "1000").c_str()),
+                      std::atof(get(args, "cg_delta_conv", "1e-2").c_str()),
+                      std::atoi(get(args, "num_rand_vec_trace", "50").c_str()), true, "vadu",
+                      std::atoi(get(args, "seed_rand_vec_trace", "1").c_str()), -1,
+                      std::atoi(get(args, "estimate_aux", "1").c_str()) != 0, no_index,
+                      std::atoi(get(args, "m_lbfgs", "-1").c_str()), -1.);
+    if (!aux.empty()) {
+      std::vector<double> av = parse_list(aux);
+      m->SetAuxPars(av.data());
+    }
+    m->SetY(y.data());
+    vec_t cp(m->num_cov_par_);
+    const std::string init = get(args, "init_cov_pars", "");
+    if (!init.empty()) {
+      std::vector<double> iv = parse_list(init);
+      vec_t io = Eigen::Map<const vec_t>(iv.data(), (int)iv.size());
+      m->TransformCovPars(io, cp);
+    } else {
+      m->FindInitCovPar(y.data(), nullptr, cp.data());
+    }
+    vec_t init_orig;
+    m->TransformBackCovPars(cp, init_orig);
+    int num_it = 0;
+    auto a = std::chrono::steady_clock::now();
+    m->OptimLinRegrCoefCovPar(y.data(), nullptr, 0, cp.data(), nullptr, num_it, cp.data(), nullptr, nullptr,
+                              true, false, false, false, false);
+    auto b = std::chrono::steady_clock::now();
+    vec_t fit_orig;
+    m->TransformBackCovPars(cp, fit_orig);
+    std::printf("{\n\"n\": %d, \"d\": %d,\n", n, d);
+    print_vec("init_cov_pars", init_orig.data(), (int)init_orig.size());
+    print_vec("cov_pars", fit_orig.data(), (int)fit_orig.size());
+    if (m->NumAuxPars() > 0) print_vec("aux_pars", m->GetAuxPars(), m->NumAuxPars());
+    std::printf("\"nll\": %.17g,\n", m->neg_log_likelihood_);
+    std::printf("\"num_it\": %d, \"num_ll_evaluations\": %d,\n", num_it, m->num_ll_evaluations_);
+    std::printf("\"fit_time\": %.9g,\n\"ok\": true\n}\n", std::chrono::duration<double>(b - a).count());
+    return 0;
+  }
+
   vec_t orig = Eigen::Map<const vec_t>(cov_pars_orig.data(), (int)cov_pars_orig.size());
   vec_t trafo;
   m->TransformCovPars(orig, trafo);
