@@ -213,6 +213,46 @@ DENSE_N = 20_000                  # BASELINE config 2: dense Cholesky fp64 on on
 DENSE_CPU_N = 4_000               # bounded CPU sample of the same unit (the n=20000 unit is ~800 s)
 
 
+def fit_leg(X, Y, cpu: bool) -> dict:
+    """GPB_OptimCovPar end to end on the headline data (reference default optimizer "lbfgs",
+    initial values from the reference's FindInitCovPar heuristic), from model construction; the
+    reference's own fit of the same data on the host cores beside it (bounded: one fit)."""
+    from gpboost_amd import GPModel
+    t0 = time.perf_counter()
+    gm = GPModel(gp_coords=X, cov_function="exponential", gp_approx="vecchia", num_neighbors=M_NEIGHBORS,
+                 vecchia_ordering="random", seed=0)
+    gm.fit(Y)
+    t = time.perf_counter() - t0
+    out = {"workload": f"GPB_OptimCovPar (lbfgs, default settings), n={X.shape[0]} Vecchia m={M_NEIGHBORS}, "
+                       "from GPB_CreateREModel (ordering + neighbour search included)",
+           "s": t, "num_it": gm.get_num_optim_iter(), "nll": gm.get_current_neg_log_likelihood(),
+           "cov_pars": [float(v) for v in gm.get_cov_pars()], "cpu_baseline": None}
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if cpu and os.path.exists(harness):
+        import numpy as np
+        threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", str(os.cpu_count() or 1))), 16))
+        with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+            f.write(np.array([X.shape[0], X.shape[1]], dtype=np.int32).tobytes())
+            f.write(np.ascontiguousarray(X.T).tobytes())
+            f.write(np.ascontiguousarray(Y).tobytes())
+            path = f.name
+        try:
+            r = json.loads(subprocess.run([harness, path, "cov_fct=exponential", "gp_approx=vecchia",
+                                           f"num_neighbors={M_NEIGHBORS}", "ordering=random", "mode=fit"],
+                                          capture_output=True, text=True, timeout=900, check=True,
+                                          env=dict(os.environ, OMP_NUM_THREADS=str(threads))).stdout)
+            out["cpu_baseline"] = {"s": r["fit_time"] + r["t_construct"], "fit_s": r["fit_time"],
+                                   "construction_s": r["t_construct"], "num_it": r["num_it"],
+                                   "num_ll_evaluations": r["num_ll_evaluations"], "nll": r["nll"],
+                                   "cov_pars": r["cov_pars"], "cores": threads, "kind": "reference",
+                                   "sample": "one reference fit of the same data (construction + OptimLinRegrCoefCovPar)"}
+        except Exception as e:  # noqa: BLE001
+            sys.stderr.write(f"reference fit baseline failed: {e}\n")
+        finally:
+            os.unlink(path)
+    return out
+
+
 def dense_flops(n: int) -> float:
     """Algorithmic FLOPs of one dense nll+grad: POTRF n^3/3 + TRTRI n^3/3 + LAUUM n^3/3 (Psi^-1
     for the gradient traces, re_model_template.h:5987-6007); the O(n^2) covariance build, trace
@@ -351,6 +391,7 @@ def main():
     ap.add_argument("--no-latent", action="store_true", help="skip the secondary latent/iterative leg")
     ap.add_argument("--latent-steps", type=int, default=3)
     ap.add_argument("--no-dense", action="store_true", help="skip the secondary dense (config 2) leg")
+    ap.add_argument("--no-fit", action="store_true", help="skip the secondary GPB_OptimCovPar (fit) leg")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -459,6 +500,8 @@ def main():
                               "predictions_per_s": PRED_N / tp, "mean_of_mu": float(np.mean(pr["mu"])),
                               "note": "end to end: neighbour search among the 100k observed points (GPU), "
                                       "prediction rows (row kernel, 64-lane groups), mean/variance"}
+    if world == 1 and not args.no_fit:
+        line["fit"] = fit_leg(X, Y, not args.no_cpu_baseline)
     if world == 1 and not args.no_dense:
         line["dense"] = dense_leg(3, not args.no_cpu_baseline)
     if world == 1 and not args.no_latent:

@@ -120,7 +120,7 @@ int main(int argc, char** argv) {
   const int seed = std::atoi(get(args, "seed", "0").c_str());
   const int threads = std::atoi(get(args, "threads", "-1").c_str());
   const std::vector<double> cov_pars_orig = parse_list(get(args, "cov_pars", "0.1,1.6,0.2"));
-  const std::string mode = get(args, "mode", "eval");   // eval | lbfgs
+  const std::string mode = get(args, "mode", "eval");   // eval | lbfgs | fit
   const int reps = std::atoi(get(args, "reps", "1").c_str());
   const int dump_nn = std::atoi(get(args, "dump_nn", "0").c_str());
   const std::string aux = get(args, "aux_pars", "");
@@ -201,7 +201,8 @@ int main(int argc, char** argv) {
     if (m->NumAuxPars() > 0) print_vec("aux_pars", m->GetAuxPars(), m->NumAuxPars());
     std::printf("\"nll\": %.17g,\n", m->neg_log_likelihood_);
     std::printf("\"num_it\": %d, \"num_ll_evaluations\": %d,\n", num_it, m->num_ll_evaluations_);
-    std::printf("\"fit_time\": %.9g,\n\"ok\": true\n}\n", std::chrono::duration<double>(b - a).count());
+    std::printf("\"fit_time\": %.9g, \"t_construct\": %.9g,\n\"ok\": true\n}\n",
+                std::chrono::duration<double>(b - a).count(), t_construct);
     return 0;
   }
 
