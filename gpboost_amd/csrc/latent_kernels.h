@@ -52,8 +52,15 @@ struct SparseB {
   const int* ell_idx;
   const double* ell_val;
   const double* vals_of;
+  // t = 1 default form of B^T: nseg runs of consecutive storage rows [seg_rb[w], seg_rb[w + 1])
+  // with <= kSegEntries entries each (or one longer row); seg_rid[e] = entry e's row index within
+  // its run. One wave per run sums its entries 64 at a time with a segmented wave scan.
+  const int* seg_rb;
+  const unsigned char* seg_rid;
+  int nseg;
 };
 constexpr int kLongRow = 64;
+constexpr int kSegEntries = 512;
 
 // LDS-tiled form of the t >= 2 operator (opt-in, GPBOOST_AMD_SPMV_TILED=1; slower than the
 // global-gather wave kernels, see sparse_kernels.hip) (one workgroup per tile of consecutive storage rows): the

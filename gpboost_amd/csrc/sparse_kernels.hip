@@ -431,6 +431,102 @@ __global__ void __launch_bounds__(kBT) bt_apply1m_kernel(int n, const int* __res
   }
 }
 
+// t = 1 default form of B^T (SparseB::seg_*): one wave per run of consecutive storage rows
+// (<= kSegEntries entries, or one longer row). The run's entries are consumed 64 at a time, lane =
+// entry, kSegU chunks of coalesced (row, value, run-row) loads and gathers in flight; per chunk a
+// segmented inclusive scan over the wave (rows are contiguous in the list, so "same run-row as the
+// lane off below" is the segment test) leaves each row's chunk sum in its last lane, which adds it
+// to the row's LDS accumulator (one lane per row per chunk: no conflicts, chunk order fixed ->
+// bitwise repeatable). Every wave reads the same number of bytes whatever its rows' lengths,
+// where the lane-group form (bt_apply1m) idles lanes on short lists and serialises long ones.
+constexpr int kSegWaves = 4;
+constexpr int kSegU = 4;
+__device__ __forceinline__ double shfl_up_f64(double v, int off) {
+  const int lo = __shfl_up(__double2loint(v), off, 64);
+  const int hi = __shfl_up(__double2hiint(v), off, 64);
+  return __hiloint2double(hi, lo);
+}
+// Segmented inclusive scan step: p += p[src lane] where the source lane has the same key.
+// DPP form (no LDS crossbar): row_shr 1/2/4/8 inside 16-lane rows, then row_bcast 15 (rows 1, 3)
+// and 31 (rows 2, 3) across rows; lanes without a source see key -1 / value 0.
+template <int CTRL, int ROWMASK>
+__device__ __forceinline__ void seg_step_dpp(double& p, int k) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(p), CTRL, ROWMASK, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(p), CTRL, ROWMASK, 0xF, false);
+  const int kq = __builtin_amdgcn_update_dpp(-1, k, CTRL, ROWMASK, 0xF, false);
+  if (kq == k) p += __hiloint2double(hi, lo);
+}
+template <bool DPP>
+__device__ __forceinline__ double seg_scan(double p, int k, int lane) {
+  if constexpr (DPP) {
+    seg_step_dpp<0x111, 0xF>(p, k);   // row_shr:1
+    seg_step_dpp<0x112, 0xF>(p, k);   // row_shr:2
+    seg_step_dpp<0x114, 0xF>(p, k);   // row_shr:4
+    seg_step_dpp<0x118, 0xF>(p, k);   // row_shr:8
+    seg_step_dpp<0x142, 0xA>(p, k);   // row_bcast:15 -> rows 1, 3
+    seg_step_dpp<0x143, 0xC>(p, k);   // row_bcast:31 -> rows 2, 3
+  } else {
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const double q = shfl_up_f64(p, off);
+      const int kq = __shfl_up(k, off, 64);
+      if (lane >= off && kq == k) p += q;
+    }
+  }
+  return p;
+}
+
+template <bool DPP>
+__global__ void __launch_bounds__(64 * kSegWaves) bt_apply1s_kernel(
+    int nseg, const int* __restrict__ seg_rb, const unsigned char* __restrict__ rid, const int* __restrict__ tptr,
+    const int* __restrict__ trow, const double* __restrict__ tval, int unit, const double* __restrict__ X,
+    const double* __restrict__ pre, const double* __restrict__ W, const double* __restrict__ H,
+    double* __restrict__ Y) {
+  __shared__ double acc_s[kSegWaves][256];
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int w = xcd_block(blockIdx.x, gridDim.x) * kSegWaves + wv;
+  if (w >= nseg) return;   // whole waves only; no block-level synchronisation below
+  const int rb = seg_rb[w], re = seg_rb[w + 1];
+  const int nr = re - rb;
+  double* acc = acc_s[wv];
+  for (int q = lane; q < nr; q += 64) acc[q] = 0.;
+  const int e0 = tptr[rb], e1 = tptr[re];
+  for (int c = e0; c < e1; c += 64 * kSegU) {
+    int id[kSegU], key[kSegU];
+    double v[kSegU];
+#pragma unroll
+    for (int u = 0; u < kSegU; ++u) {
+      const int e = c + u * 64 + lane;
+      const bool ok = e < e1;
+      id[u] = ok ? trow[e] : 0;
+      v[u] = ok ? tval[e] : 0.;
+      key[u] = ok ? (int)rid[e] : 255;
+    }
+#pragma unroll
+    for (int u = 0; u < kSegU; ++u) {
+      double g = X[id[u]];
+      if (pre) g *= pre[id[u]];
+      v[u] *= g;
+    }
+#pragma unroll
+    for (int u = 0; u < kSegU; ++u) {
+      const int k = key[u];
+      const double p = seg_scan<DPP>(v[u], k, lane);
+      const int kn = __shfl_down(k, 1, 64);
+      if (k != 255 && (lane == 63 || kn != k)) acc[k] += p;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's accumulator writes before its reads
+  for (int q = lane; q < nr; q += 64) {
+    const int j = rb + q;
+    double s = unit ? (pre ? pre[j] * X[j] : X[j]) : 0.;
+    s += acc[q];
+    if (W) s = fma(W[j], H[j], s);
+    Y[j] = s;
+  }
+}
+
 // t = 1 default form of B (SparseB::ell_*): one row per lane, entries in a fixed ascending order,
 // kU1 loads in flight per lane. (The same form for B^T — sliced ELL, rows sorted by length in
 // windows — measured 37-48 us against the lane groups' 20 us: rows-as-lanes only pays where every
@@ -1093,6 +1189,19 @@ void launch_bt_apply(const SparseB& B, const double* vals, bool unit, const doub
   if (B.n <= 0) return;
   const double* tval = (B.tval != nullptr && vals == B.tval_of) ? B.tval : nullptr;
   static const bool old1 = std::getenv("GPBOOST_AMD_SPMV1_OLD") != nullptr;
+  static const bool groups1 = std::getenv("GPBOOST_AMD_BT1_GROUPS") != nullptr;   // A/B: lane-group form
+  if (t == 1 && tval != nullptr && !old1 && !groups1 && B.seg_rb != nullptr) {
+    static const bool shfl = std::getenv("GPBOOST_AMD_BT1_SCAN_SHFL") != nullptr;   // A/B: ds_bpermute scan
+    const dim3 g((B.nseg + kSegWaves - 1) / kSegWaves), b(64 * kSegWaves);
+    if (shfl)
+      hipLaunchKernelGGL(bt_apply1s_kernel<false>, g, b, 0, s, B.nseg, B.seg_rb, B.seg_rid, B.tptr, B.trow, tval,
+                         unit ? 1 : 0, X, pre, W, H, Y);
+    else
+      hipLaunchKernelGGL(bt_apply1s_kernel<true>, g, b, 0, s, B.nseg, B.seg_rb, B.seg_rid, B.tptr, B.trow, tval,
+                         unit ? 1 : 0, X, pre, W, H, Y);
+    HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (t == 1 && tval != nullptr && !old1) {
     const int nlb = (B.nlong + kBT / 64 - 1) / (kBT / 64);
     // lane-group shape (A/B builds: GPB_BT1_SHAPE): 1 = 16 lanes x 4 entries, 2 rows per group (the
