@@ -200,7 +200,7 @@ def latent_leg(X, Y, steps: int, cpu: bool) -> dict:
     ach1 = byts1 / (ms_a1 * 1e-3) / 1e9
     leg["cg_matvec_roofline_single"] = {"bound": "hbm", "achieved": ach1, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                         "frac": ach1 / HBM_PEAK_GBS, "traffic": None,
-                                        "kernel": "b_apply1e (ELL) + bt_apply1m<16,2,4>", "kernel_ms": ms_a1, "columns": 1,
+                                        "kernel": "b_apply1e (ELL) + bt_apply1s (segmented runs)", "kernel_ms": ms_a1, "columns": 1,
                                         "algorithmic_bytes_per_launch": byts1, "preconditioner_ms": ms_p1}
     its = int(info[2])
     leg["preconditioner"]["share_of_eval"] = min(1.0, its * ms_p / (t_med * 1e3)) if its > 0 else None

@@ -293,30 +293,32 @@ void LatentVecchia::BuildStructure(const int* nbr) {
     sp_.ell_val = d_ell_val_.get();
     sp_.vals_of = nullptr;
   }
-  {   // t = 1 default form of B^T (SparseB::seg_*): runs of consecutive storage rows holding
-      // <= kSegEntries entries (a longer row is a run of its own) and <= 255 rows, one wave each;
-      // per entry its row's index within the run (uint8) for the wave's segmented sums
+  if (n < (1 << 24)) {   // t = 1 default form of B^T (SparseB::seg_*): runs of consecutive storage
+      // rows holding <= kSegEntries entries (a longer row is a run of its own) and <= kSegRows rows,
+      // one wave each; per entry one packed word: source row (bits 0-23), the row's index within
+      // the run (bits 24-30) and "last entry of its row" (bit 31) for the wave's segmented sums
     std::vector<int> seg{0};
-    std::vector<unsigned char> rid(std::max(nnz, 1), 0);
+    std::vector<uint32_t> pk(std::max(nnz, 1), 0);
     int ce = 0, cr = 0;
     for (int j = 0; j < n; ++j) {
       const int len = tptr[j + 1] - tptr[j];
-      if (cr > 0 && (ce + len > kSegEntries || cr >= 255)) {
+      if (cr > 0 && (ce + len > kSegEntries || cr >= kSegRows)) {
         seg.push_back(j);
         ce = 0;
         cr = 0;
       }
-      for (int e = tptr[j]; e < tptr[j + 1]; ++e) rid[e] = (unsigned char)cr;
+      for (int e = tptr[j]; e < tptr[j + 1]; ++e)
+        pk[e] = (uint32_t)trow[e] | ((uint32_t)cr << 24) | (e + 1 == tptr[j + 1] ? 0x80000000u : 0u);
       ce += len;
       ++cr;
     }
     seg.push_back(n);
     d_seg_rb_.alloc(seg.size());
-    d_seg_rid_.alloc(rid.size());
+    d_seg_pk_.alloc(pk.size());
     HIP_CHECK(hipMemcpy(d_seg_rb_.get(), seg.data(), sizeof(int) * seg.size(), hipMemcpyHostToDevice));
-    HIP_CHECK(hipMemcpy(d_seg_rid_.get(), rid.data(), rid.size(), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMemcpy(d_seg_pk_.get(), pk.data(), sizeof(uint32_t) * pk.size(), hipMemcpyHostToDevice));
     sp_.seg_rb = d_seg_rb_.get();
-    sp_.seg_rid = d_seg_rid_.get();
+    sp_.seg_pk = d_seg_pk_.get();
     sp_.nseg = (int)seg.size() - 1;
   }
 }

@@ -129,7 +129,7 @@ class LatentVecchia {
   SparseB sp_{};
   DevBuf<int> d_nbr_, d_tptr_, d_trow_, d_tslot_, d_longr_;
   DevBuf<int> d_ell_idx_, d_ell_slot_, d_seg_rb_;
-  DevBuf<unsigned char> d_seg_rid_;
+  DevBuf<uint32_t> d_seg_pk_;
   struct TileDev {   // device arrays of a TileOp
     DevBuf<int> r0, uoff, urow, fb;
     DevBuf<uint16_t> lidx;

@@ -52,15 +52,20 @@ struct SparseB {
   const int* ell_idx;
   const double* ell_val;
   const double* vals_of;
-  // t = 1 default form of B^T: nseg runs of consecutive storage rows [seg_rb[w], seg_rb[w + 1])
-  // with <= kSegEntries entries each (or one longer row); seg_rid[e] = entry e's row index within
-  // its run. One wave per run sums its entries 64 at a time with a segmented wave scan.
+  // t = 1 default form of B^T (n < 2^24; else null): nseg runs of consecutive storage rows
+  // [seg_rb[w], seg_rb[w + 1]) with <= kSegEntries entries (or one longer row) and <= kSegRows rows;
+  // seg_pk[e] = trow[e] | run-row index << 24 | (last entry of its row) << 31. One wave per run
+  // sums its entries 64 at a time with a segmented wave scan.
   const int* seg_rb;
-  const unsigned char* seg_rid;
+  const uint32_t* seg_pk;
   int nseg;
 };
 constexpr int kLongRow = 64;
-constexpr int kSegEntries = 512;
+#ifndef GPB_SEG_ENTRIES
+#define GPB_SEG_ENTRIES 512
+#endif
+constexpr int kSegEntries = GPB_SEG_ENTRIES;   // (A/B builds override)
+constexpr int kSegRows = 127;                  // run-row index in 7 bits (127 = padding lanes)
 
 // LDS-tiled form of the t >= 2 operator (opt-in, GPBOOST_AMD_SPMV_TILED=1; slower than the
 // global-gather wave kernels, see sparse_kernels.hip) (one workgroup per tile of consecutive storage rows): the

@@ -440,7 +440,10 @@ __global__ void __launch_bounds__(kBT) bt_apply1m_kernel(int n, const int* __res
 // bitwise repeatable). Every wave reads the same number of bytes whatever its rows' lengths,
 // where the lane-group form (bt_apply1m) idles lanes on short lists and serialises long ones.
 constexpr int kSegWaves = 4;
-constexpr int kSegU = 4;
+#ifndef GPB_SEG_U
+#define GPB_SEG_U 4
+#endif
+constexpr int kSegU = GPB_SEG_U;   // 64-entry chunks per iteration (A/B builds override)
 __device__ __forceinline__ double shfl_up_f64(double v, int off) {
   const int lo = __shfl_up(__double2loint(v), off, 64);
   const int hi = __shfl_up(__double2hiint(v), off, 64);
@@ -478,11 +481,10 @@ __device__ __forceinline__ double seg_scan(double p, int k, int lane) {
 
 template <bool DPP>
 __global__ void __launch_bounds__(64 * kSegWaves) bt_apply1s_kernel(
-    int nseg, const int* __restrict__ seg_rb, const unsigned char* __restrict__ rid, const int* __restrict__ tptr,
-    const int* __restrict__ trow, const double* __restrict__ tval, int unit, const double* __restrict__ X,
-    const double* __restrict__ pre, const double* __restrict__ W, const double* __restrict__ H,
-    double* __restrict__ Y) {
-  __shared__ double acc_s[kSegWaves][256];
+    int nseg, const int* __restrict__ seg_rb, const uint32_t* __restrict__ seg_pk, const int* __restrict__ tptr,
+    const double* __restrict__ tval, int unit, const double* __restrict__ X, const double* __restrict__ pre,
+    const double* __restrict__ W, const double* __restrict__ H, double* __restrict__ Y) {
+  __shared__ double acc_s[kSegWaves][kSegRows + 1];
   const int lane = threadIdx.x & 63;
   const int wv = threadIdx.x >> 6;
   const int w = xcd_block(blockIdx.x, gridDim.x) * kSegWaves + wv;
@@ -493,28 +495,28 @@ __global__ void __launch_bounds__(64 * kSegWaves) bt_apply1s_kernel(
   for (int q = lane; q < nr; q += 64) acc[q] = 0.;
   const int e0 = tptr[rb], e1 = tptr[re];
   for (int c = e0; c < e1; c += 64 * kSegU) {
-    int id[kSegU], key[kSegU];
+    uint32_t pk[kSegU];
     double v[kSegU];
 #pragma unroll
     for (int u = 0; u < kSegU; ++u) {
       const int e = c + u * 64 + lane;
       const bool ok = e < e1;
-      id[u] = ok ? trow[e] : 0;
+      pk[u] = ok ? seg_pk[e] : ((uint32_t)kSegRows << 24);   // padding: key 127, never a row end
       v[u] = ok ? tval[e] : 0.;
-      key[u] = ok ? (int)rid[e] : 255;
     }
 #pragma unroll
     for (int u = 0; u < kSegU; ++u) {
-      double g = X[id[u]];
-      if (pre) g *= pre[id[u]];
+      const int id = (int)(pk[u] & 0xFFFFFFu);
+      double g = X[id];
+      if (pre) g *= pre[id];
       v[u] *= g;
     }
 #pragma unroll
     for (int u = 0; u < kSegU; ++u) {
-      const int k = key[u];
+      const int k = (int)((pk[u] >> 24) & 0x7Fu);
       const double p = seg_scan<DPP>(v[u], k, lane);
-      const int kn = __shfl_down(k, 1, 64);
-      if (k != 255 && (lane == 63 || kn != k)) acc[k] += p;
+      // a row's sum leaves the chunk at its last entry, or at lane 63 when it continues
+      if (k != kSegRows && ((pk[u] >> 31) != 0u || lane == 63)) acc[k] += p;
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's accumulator writes before its reads
@@ -531,7 +533,10 @@ __global__ void __launch_bounds__(64 * kSegWaves) bt_apply1s_kernel(
 // kU1 loads in flight per lane. (The same form for B^T — sliced ELL, rows sorted by length in
 // windows — measured 37-48 us against the lane groups' 20 us: rows-as-lanes only pays where every
 // row has the same length.)
-constexpr int kU1 = 10;
+#ifndef GPB_U1
+#define GPB_U1 10
+#endif
+constexpr int kU1 = GPB_U1;   // loads in flight per lane (A/B builds override)
 __global__ void __launch_bounds__(kBT) b_apply1e_kernel(int n, int m, const int* __restrict__ idx,
                                                         const double* __restrict__ val, int unit,
                                                         const double* __restrict__ X,
@@ -1194,10 +1199,10 @@ void launch_bt_apply(const SparseB& B, const double* vals, bool unit, const doub
     static const bool shfl = std::getenv("GPBOOST_AMD_BT1_SCAN_SHFL") != nullptr;   // A/B: ds_bpermute scan
     const dim3 g((B.nseg + kSegWaves - 1) / kSegWaves), b(64 * kSegWaves);
     if (shfl)
-      hipLaunchKernelGGL(bt_apply1s_kernel<false>, g, b, 0, s, B.nseg, B.seg_rb, B.seg_rid, B.tptr, B.trow, tval,
+      hipLaunchKernelGGL(bt_apply1s_kernel<false>, g, b, 0, s, B.nseg, B.seg_rb, B.seg_pk, B.tptr, tval,
                          unit ? 1 : 0, X, pre, W, H, Y);
     else
-      hipLaunchKernelGGL(bt_apply1s_kernel<true>, g, b, 0, s, B.nseg, B.seg_rb, B.seg_rid, B.tptr, B.trow, tval,
+      hipLaunchKernelGGL(bt_apply1s_kernel<true>, g, b, 0, s, B.nseg, B.seg_rb, B.seg_pk, B.tptr, tval,
                          unit ? 1 : 0, X, pre, W, H, Y);
     HIP_CHECK(hipGetLastError());
     return;

@@ -4,8 +4,7 @@ CPU restatement of GPB_OptimCovPar for the Gaussian likelihood (profiled nugget)
 oracle's exact nll / gradient (oracle.py -> gp_oracle.cpp):
 
   initial values  re_model_template.h:4388-4504 (FindInitCovPar), cov_fcts.h:1275-1450
-                  (median distance; only the n <= 1000 all-pairs case — the sampled case needs
-                  the model's mt19937 stream and is pinned by the GPU tests against the reference)
+                  (median distance of <= 1000 points; gp_oracle.cpp orc_init_range_trafo)
   objective       optim_utils.h:243-364 (EvalLLforLBFGSpp, profile_out_error_variance)
   L-BFGS          external_libs/LBFGSpp/include/LBFGS.h:86-301 (past = 1, epsilon = 1e-20),
                   LineSearchBacktracking.h:45-143 (Armijo, GPBoost's 1/32 shrink), BFGSMat.h:89-186
@@ -22,19 +21,14 @@ import numpy as np
 from oracle import oracle as O
 
 
-def init_trafo(coords: np.ndarray, y: np.ndarray, cov_type: int) -> np.ndarray:
+def init_trafo(coords: np.ndarray, y: np.ndarray, cov_type: int, seed: int = 0, shuffled: bool = False) -> np.ndarray:
+    """coords in the component's order (Vecchia order for the Vecchia approximation); the range
+    comes from gp_oracle.cpp (orc_init_range_trafo: the sampled case needs libstdc++'s mt19937,
+    shuffle and uniform_int_distribution)."""
     n = coords.shape[0]
-    if n > 1000:
-        raise ValueError("sampled initial range (n > 1000) is not restated here")
     mean = float(np.sum(y)) / n
     var = float(np.sum((y - mean) ** 2)) / (n - 1)
-    i, j = np.triu_indices(n, 1)
-    dist = np.sqrt(np.sum((coords[i] - coords[j]) ** 2, axis=1))
-    med = float(np.median(dist))
-    if med < 1e-10:
-        med = float(np.mean(dist))
-    phi = {0: 2. * 3. / med, 1: 2. * 4.7 / med, 2: 2. * 5.9 / med}.get(cov_type, 3. / (med / 2.) ** 2)
-    return np.array([var / 2., 1., phi])
+    return np.array([var / 2., 1., O.init_range_trafo(coords, cov_type, seed, shuffled)])
 
 
 def range_back(cov_type: int, phi: float) -> float:
@@ -102,7 +96,8 @@ def fit_gaussian(coords, y, cov_type, gp_approx="none", m=30, seed=0, random=Tru
         def ev(trafo):
             return O.dense_nll_grad(coords, y, cov_type, trafo, 1)
         cx = coords
-    t0 = O.transform(cov_type, init_orig) if init_orig is not None else init_trafo(cx, y, cov_type)
+    t0 = (O.transform(cov_type, init_orig) if init_orig is not None
+          else init_trafo(cx, y, cov_type, seed, gp_approx == "vecchia" and random))
     state = {}
 
     def f(x):

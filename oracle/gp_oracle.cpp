@@ -115,6 +115,53 @@ void orc_vecchia_order(int n, int seed, int random_ordering, int* perm) {
   std::copy(idx.begin(), idx.end(), perm);
 }
 
+// FindInitCovPar's range (re_model_template.h:4452-4458 -> cov_fcts.h:1275-1450): median of the
+// pairwise distances of at most 1000 points, for n > 1000 drawn by std::uniform_int_distribution
+// from the model's mt19937(seed) after the Vecchia ordering shuffle (Vecchia_utils.cpp:1094-1095);
+// phi such that the correlation is 0.05 at half the median. x: the component's coordinates
+// (Vecchia order for the Vecchia approximation), row-major n x d.
+double orc_init_range_trafo(const double* x, int n, int d, int seed, int shuffled, int t) {
+  const int nf = std::min(n, 1000);
+  std::vector<int> idx(nf);
+  if (nf < n) {
+    std::mt19937 rng(seed);
+    if (shuffled) {
+      std::vector<int> dummy(n);
+      std::iota(dummy.begin(), dummy.end(), 0);
+      std::shuffle(dummy.begin(), dummy.end(), rng);
+    }
+    std::uniform_int_distribution<> dis(0, n - 1);
+    for (int i = 0; i < nf; ++i) idx[i] = dis(rng);
+  } else {
+    std::iota(idx.begin(), idx.end(), 0);
+  }
+  std::vector<double> dist;
+  dist.reserve((size_t)nf * (nf - 1) / 2);
+  for (int i = 0; i < nf - 1; ++i)
+    for (int j = i + 1; j < nf; ++j) {
+      double s = 0.;
+      for (int q = 0; q < d; ++q) {
+        const double u = x[(size_t)idx[i] * d + q] - x[(size_t)idx[j] * d + q];
+        s += u * u;
+      }
+      dist.push_back(std::sqrt(s));
+    }
+  const size_t pos = dist.size() / 2;   // utils.h:189-202
+  std::nth_element(dist.begin(), dist.begin() + pos, dist.end());
+  double med = dist[pos];
+  if (dist.size() % 2 == 0) {
+    std::nth_element(dist.begin(), dist.begin() + pos - 1, dist.end());
+    med = (med + dist[pos - 1]) / 2.;
+  }
+  if (med < 1e-10) med = std::accumulate(dist.begin(), dist.end(), 0.) / (double)dist.size();
+  switch (t) {
+    case 0: return 2. * 3. / med;
+    case 1: return 2. * 4.7 / med;
+    case 2: return 2. * 5.9 / med;
+    default: return 3. / std::pow(med / 2., 2.);
+  }
+}
+
 void orc_find_neighbors(const double* x, int n, int d, int m, int* nbr) {
   std::fill(nbr, nbr + (size_t)n * m, -1);
   const int end_search_at = n - 2;                 // :751-753

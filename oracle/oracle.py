@@ -45,6 +45,8 @@ def lib():
         L.orc_dense_nll_grad.argtypes = [D, D, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, ctypes.c_int, D, D, D]
         L.orc_latent_vecchia_factor.argtypes = [D, I, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, D,
                                                 D, D, D, D]
+        L.orc_init_range_trafo.argtypes = [D, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.orc_init_range_trafo.restype = ctypes.c_double
         L.orc_gen_probes.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_ulonglong, D]
         L.orc_latent_vecchia_iterative.argtypes = [D, D, I, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, D,
                                                    ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
@@ -116,6 +118,12 @@ def vecchia_predict(coords_vo, y_vo, coords_pred, m_pred, cov_type, pars_trafo, 
                                  int(predict_response), _d(mean), _d(var)):
         raise RuntimeError("oracle prediction failed")
     return mean, var, nb
+
+
+def init_range_trafo(coords_vo: np.ndarray, cov_type: int, seed: int = 0, shuffled: bool = True) -> float:
+    """FindInitCovPar's initial phi (transformed range); coords in the component's order."""
+    x = np.ascontiguousarray(coords_vo, dtype=np.float64)
+    return float(lib().orc_init_range_trafo(_d(x), x.shape[0], x.shape[1], seed, int(shuffled), cov_type))
 
 
 def vecchia_setup(coords: np.ndarray, m: int, seed: int = 0, random: bool = True):
