@@ -8,7 +8,7 @@ O=gpurun_out/seg_ab
 mkdir -p $O
 for v in ${VARIANTS:-base u8 e256 u2e128}; do
   if [ "$v" = base ]; then export GPBOOST_AMD_VARIANT=; else export GPBOOST_AMD_VARIANT=$v; fi
-  for rep in 1 2; do
+  for rep in 1 2 3; do
     GPBOOST_AMD_PRECOND_SPLIT=1 timeout -k 10 200 python -u scripts/prof_op1.py > $O/op_${v}_$rep.log 2>&1 || exit $?
     echo "$v $rep $(grep 'operator parts' $O/op_${v}_$rep.log | tr '\n' ' ')" >> $O/summary.log
   done
