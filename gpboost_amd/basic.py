@@ -257,9 +257,11 @@ class GPModel:
         return v.value
 
     def get_cov_pars(self, std_err=False):
-        out = np.zeros(self.num_cov_pars)
+        """Covariance parameters (original scale); std_err=True: 2 x P array [parameters; standard
+        deviations] (reference basic.py get_cov_pars: a two-row table; dense Gaussian models only)."""
+        out = np.zeros(2 * self.num_cov_pars if std_err else self.num_cov_pars)
         _safe_call(lib().GPB_GetCovPar(self.handle, _dp(out), ctypes.c_bool(std_err)))
-        return out
+        return out.reshape(2, -1) if std_err else out
 
     # ------------------------------------------------------------------ extensions
     def neg_log_likelihood_and_grad(self, cov_pars, y=None, profile_sigma2=False, fixed_effects=None):

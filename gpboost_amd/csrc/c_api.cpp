@@ -299,10 +299,12 @@ int GPB_GetCurrentNegLogLikelihood(REModelHandle handle, double* negll) {
 
 int GPB_GetCovPar(REModelHandle handle, double* cov_par, bool calc_std_dev) {
   API_BEGIN();
-  if (calc_std_dev) gpb_amd::Fatal("standard deviations of covariance parameters are out of scope for gpboost_amd");
-  const auto& p = model(handle)->last_cov_pars();
-  if (p.empty()) gpb_amd::Fatal("no covariance parameters have been evaluated yet");
+  // re_model.cpp:767-811: cov_par[0, P) = parameters, cov_par[P, 2P) = std devs if calc_std_dev
+  REModelAMD* m = model(handle);
+  const auto p = m->last_cov_pars();
+  if (p.empty()) gpb_amd::Fatal("Covariance parameters have not been estimated or correctly set ");
   for (size_t k = 0; k < p.size(); ++k) cov_par[k] = p[k];
+  if (calc_std_dev) m->StdDevCovPars(p.data(), cov_par + p.size());
   API_END();
 }
 

@@ -18,6 +18,10 @@ class DenseSolver {
   // s1_k = -1/2 y_aux^T dPsi_k y_aux, s2_k = tr(dPsi_k Psi^-1).
   // kernel_ms[0] = Cholesky time, kernel_ms[1] = whole device evaluation.
   void Eval(int cov_type, double var, double phi, const double* d_y, bool want_grad, double* sums, double* kernel_ms);
+  // Traces of the Fisher information on the original scale (standard errors): with P = Psi^-1,
+  // D1 = correlation matrix, D2 = dscale * dcorr/dlog(phi) and G_k = P D_k, sums6 =
+  // [sum P^2, sum P o G1, sum P o G2, tr(G1 G1), tr(G1 G2), tr(G2 G2)].
+  void Fisher(int cov_type, double var, double phi, double dscale, double* sums6);
 
  private:
   void Potrf();

@@ -472,6 +472,99 @@ __global__ void __launch_bounds__(256) dense_grad_kernel(const double* __restric
   if (threadIdx.x < 4) part[(size_t)tile * 4 + threadIdx.x] = red[threadIdx.x][0];
 }
 
+// Fisher information (GPB_GetCovPar calc_std_dev, re_model_template.h:9144-9236 dense branch):
+// full derivative matrices of Sigma on the ORIGINAL scale (GetZSigmaZtGrad transf_scale = false,
+// re_comp.h:1389-1438): D1 = dSigma/dsigma1^2 = correlation (1 on the diagonal), D2 = dSigma/drho
+// = dscale * dcorr/dlog(phi) (0 on the diagonal; dscale = sigma1^2 dlog(phi)/drho).
+template <int COV>
+__global__ void __launch_bounds__(256) build_dsigma_kernel(const double* __restrict__ X, int n, int d, int ld,
+                                                           double phi, double dscale, double* __restrict__ D1,
+                                                           double* __restrict__ D2) {
+  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+  const int ti = threadIdx.x & 63;
+  for (int jj = threadIdx.x >> 6; jj < 64; jj += 4) {
+    const int i = i0 + ti, j = j0 + jj;
+    if (i >= n || j >= n) continue;
+    double c = 1., dc = 0.;
+    if (i != j) {
+      double s = 0.;
+      for (int q = 0; q < d; ++q) { const double t = X[(size_t)i * d + q] - X[(size_t)j * d + q]; s += t * t; }
+      cov_dcov<COV>(sqrt(s), 1., phi, c, dc);
+    }
+    D1[(size_t)i + (size_t)j * ld] = c;
+    D2[(size_t)i + (size_t)j * ld] = dscale * dc;
+  }
+}
+
+// Upper triangle of a symmetric matrix from its lower triangle (64 x 64 tiles above the diagonal).
+__global__ void __launch_bounds__(256) mirror_lower_kernel(double* A, int n, int ld) {
+  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+  if (j0 < i0) return;
+  const int ti = threadIdx.x & 63;
+  for (int jj = threadIdx.x >> 6; jj < 64; jj += 4) {
+    const int i = i0 + ti, j = j0 + jj;
+    if (i < n && j < n && i < j) A[(size_t)i + (size_t)j * ld] = A[(size_t)j + (size_t)i * ld];
+  }
+}
+
+// Per lower tile pair {T = (bi, bj), T' = (bj, bi)} of P (= Psi^-1, symmetric) and G_k = P D_k:
+// partial sums of [sum P^2, sum P o G1, sum P o G2, sum G1 o G1^T, sum G1 o G2^T, sum G2 o G2^T] over
+// both tiles (fixed order; the transposed tiles of G staged in LDS so every global read coalesces).
+__global__ void __launch_bounds__(256) fisher_trace_kernel(const double* __restrict__ P, const double* __restrict__ G1,
+                                                           const double* __restrict__ G2, int n, int ld,
+                                                           double* __restrict__ part) {
+  __shared__ double t1[64][65], t2[64][65];
+  const int bi = blockIdx.y, bj = blockIdx.x;
+  const int tile = bi * gridDim.x + bj;
+  const int ti = threadIdx.x & 63;
+  double s[6] = {0., 0., 0., 0., 0., 0.};
+  if (bj <= bi) {
+    const int i0 = bi * 64, j0 = bj * 64;
+    // stage T' = rows j0.., cols i0.. of G1, G2 transposed: t[a][b] = G(j0 + b, i0 + a)
+    for (int aa = threadIdx.x >> 6; aa < 64; aa += 4) {
+      const int r = j0 + ti, c = i0 + aa;
+      const bool ok = r < n && c < n;
+      t1[aa][ti] = ok ? G1[(size_t)r + (size_t)c * ld] : 0.;
+      t2[aa][ti] = ok ? G2[(size_t)r + (size_t)c * ld] : 0.;
+    }
+    __syncthreads();
+    const bool diag = bi == bj;
+    for (int jj = threadIdx.x >> 6; jj < 64; jj += 4) {
+      const int i = i0 + ti, j = j0 + jj;
+      if (i >= n || j >= n) continue;
+      const double p = P[(size_t)i + (size_t)j * ld];   // lower tile (i >= j on diagonal tiles below)
+      const double g1 = G1[(size_t)i + (size_t)j * ld], g2 = G2[(size_t)i + (size_t)j * ld];
+      const double h1 = t1[ti][jj], h2 = t2[ti][jj];   // G(j, i)
+      if (diag) {   // the tile is its own transpose: every (i, j) once
+        const double pp = (i >= j) ? p : P[(size_t)j + (size_t)i * ld];
+        s[0] += pp * pp;
+        s[1] += pp * g1;
+        s[2] += pp * g2;
+        s[3] += g1 * h1;
+        s[4] += g1 * h2;
+        s[5] += g2 * h2;
+      } else {      // (i, j) and (j, i)
+        s[0] += 2. * p * p;
+        s[1] += p * (g1 + h1);
+        s[2] += p * (g2 + h2);
+        s[3] += 2. * g1 * h1;
+        s[4] += g1 * h2 + h1 * g2;
+        s[5] += 2. * g2 * h2;
+      }
+    }
+  }
+  __syncthreads();
+  double* red = &t1[0][0];   // reuse: 6 x 256
+  for (int q = 0; q < 6; ++q) red[q * 256 + threadIdx.x] = s[q];
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off)
+      for (int q = 0; q < 6; ++q) red[q * 256 + threadIdx.x] += red[q * 256 + threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x < 6) part[(size_t)tile * 6 + threadIdx.x] = red[threadIdx.x * 256];
+}
+
 __global__ void dot_kernel(const double* a, const double* b, int n, double* out) {
   __shared__ double red[256];
   double s = 0.;
@@ -734,6 +827,42 @@ void DenseSolver::Eval(int cov_type, double var, double phi, const double* d_y, 
   } else {
     sums[2] = sums[3] = sums[4] = sums[5] = 0.;
   }
+}
+
+void DenseSolver::Fisher(int cov_type, double var, double phi, double dscale, double* sums6) {
+  // P = Psi^-1 as in Eval's gradient branch, then G_k = P D_k (two MFMA GEMMs) and the traces
+  const int n = n_, ld = ld_, d = d_;
+  double* A = A_.get();
+  double* W = W_.get();
+  HIP_CHECK(hipMemsetAsync(info_.get(), 0, sizeof(int), stream_));
+  const int nt = (n + 63) / 64;
+  dispatch_cov(cov_type, [&](auto c) {
+    hipLaunchKernelGGL((build_psi_kernel<decltype(c)::value>), dim3(nt, nt), dim3(256), 0, stream_, d_X_, n, d, ld, var,
+                       phi, A);
+  });
+  HIP_CHECK(hipGetLastError());
+  PotrfLookahead();
+  Trtri(0, n);
+  gemm(stream_, n, n, n, 1., W, ld, 1, W, ld, 0, 0., A, ld, 1, 0, 1, 1);   // P = W^T W (lower)
+  hipLaunchKernelGGL(mirror_lower_kernel, dim3(nt, nt), dim3(256), 0, stream_, A, n, ld);
+  DevBuf<double> D2((size_t)ld * ld), G1((size_t)ld * ld), G2((size_t)ld * ld), part((size_t)nt * nt * 6);
+  dispatch_cov(cov_type, [&](auto c) {
+    hipLaunchKernelGGL((build_dsigma_kernel<decltype(c)::value>), dim3(nt, nt), dim3(256), 0, stream_, d_X_, n, d, ld,
+                       phi, dscale, W, D2.get());   // D1 into W (L^-1 is no longer needed)
+  });
+  HIP_CHECK(hipGetLastError());
+  gemm(stream_, n, n, n, 1., A, ld, 0, W, ld, 0, 0., G1.get(), ld);
+  gemm(stream_, n, n, n, 1., A, ld, 0, D2.get(), ld, 0, 0., G2.get(), ld);
+  hipLaunchKernelGGL(fisher_trace_kernel, dim3(nt, nt), dim3(256), 0, stream_, A, G1.get(), G2.get(), n, ld, part.get());
+  HIP_CHECK(hipGetLastError());
+  double* dred = red_.get();
+  launch_sum_blocks(part.get(), nt * nt, 6, dred + 8, stream_);
+  HIP_CHECK(hipMemcpyAsync(h_red_, dred + 8, sizeof(double) * 6, hipMemcpyDeviceToHost, stream_));
+  int info = 0;
+  HIP_CHECK(hipMemcpyAsync(&info, info_.get(), sizeof(int), hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  if (info != 0) Fatal("the covariance matrix is not positive definite (Cholesky failed)");
+  for (int q = 0; q < 6; ++q) sums6[q] = h_red_[q];
 }
 
 }  // namespace gpb_amd

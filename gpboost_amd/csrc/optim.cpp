@@ -394,4 +394,34 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects) {
   last_cov_pars_ = cov_pars_orig_;
 }
 
+void REModelAMD::StdDevCovPars(const double* orig, double* sd) {
+  // CalcFisherInformation, dense branch (re_model_template.h:9179-9230), transf_scale = false,
+  // include_error_var = true: with Sigma^-1 = Psi^-1 / sigma^2 and dSigma_k on the original scale
+  // (sigma^2: I; sigma1^2: the correlation matrix; rho: sigma1^2 dcorr/drho)
+  //   FI_00 = tr(Sigma^-2) / 2, FI_0k = tr(Sigma^-2 dSigma_k) / 2, FI_kl = tr(Sigma^-1 dSigma_k Sigma^-1 dSigma_l) / 2
+  if (cfg_.latent || vecchia_)
+    Fatal("standard deviations of covariance parameters are supported by gpboost_amd only for gp_approx = 'none' "
+          "with the Gaussian likelihood");
+  UseDevice();
+  EnsureStructure();
+  double trafo[3];
+  TransformCovPars(orig, trafo);
+  const double s2 = orig[0], rho = orig[2];
+  const double dlogphi_drho = (cfg_.cov_type == kGaussian ? -2. : -1.) / rho;
+  double t[6];
+  dense_->Fisher(cfg_.cov_type, trafo[1], trafo[2], orig[1] * dlogphi_drho, t);
+  const double c = 0.5 / (s2 * s2);
+  const double F[3][3] = {{c * t[0], c * t[1], c * t[2]}, {c * t[1], c * t[3], c * t[4]}, {c * t[2], c * t[4], c * t[5]}};
+  // inverse of the symmetric 3 x 3 matrix by cofactors (FI.inverse(), :9788)
+  const double c00 = F[1][1] * F[2][2] - F[1][2] * F[2][1];
+  const double c11 = F[0][0] * F[2][2] - F[0][2] * F[2][0];
+  const double c22 = F[0][0] * F[1][1] - F[0][1] * F[1][0];
+  const double det = F[0][0] * c00 - F[0][1] * (F[1][0] * F[2][2] - F[1][2] * F[2][0]) +
+                     F[0][2] * (F[1][0] * F[2][1] - F[1][1] * F[2][0]);
+  if (!(det != 0.) || !std::isfinite(det)) Fatal("the Fisher information is singular");
+  sd[0] = std::sqrt(c00 / det);
+  sd[1] = std::sqrt(c11 / det);
+  sd[2] = std::sqrt(c22 / det);
+}
+
 }  // namespace gpb_amd

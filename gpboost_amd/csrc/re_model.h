@@ -102,6 +102,10 @@ class REModelAMD {
   void SetOptimSettings(const double* init_cov_pars, double lr, int max_iter, double delta_rel_conv,
                         const char* optimizer, int m_lbfgs);
   void OptimCovPar(const double* y, const double* fixed_effects);
+  // Standard deviations of the covariance parameters (original scale) at cov_pars_orig: square
+  // roots of the diagonal of the inverse Fisher information (CalcStdDevCovPar,
+  // re_model_template.h:9775-9789; dense Gaussian models only).
+  void StdDevCovPars(const double* cov_pars_orig, double* sd);
   int num_it() const { return num_it_; }
 
   // Evaluations on the transformed scale (used by the optimizer): Gaussian trafo =

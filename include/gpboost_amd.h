@@ -164,8 +164,11 @@ GPBOOST_AMD_EXPORT int GPB_EvalNegLogLikelihoodGrad(REModelHandle handle,
 /* replaces GPB_GetCurrentNegLogLikelihood (include/LightGBM/c_api.h:1512) */
 GPBOOST_AMD_EXPORT int GPB_GetCurrentNegLogLikelihood(REModelHandle handle, double* negll);
 
-/* replaces GPB_GetCovPar (include/LightGBM/c_api.h:1526): last evaluated cov_pars
- * (original scale); std devs are not computed by this build (calc_std_dev must be false). */
+/* replaces GPB_GetCovPar (include/LightGBM/c_api.h:1526; re_model.cpp:767-811): the estimated (or
+ * last evaluated) cov_pars on the original scale in cov_par[0, P); calc_std_dev = true also writes
+ * their standard deviations to cov_par[P, 2P) — square roots of the diagonal of the inverse Fisher
+ * information (CalcStdDevCovPar re_model_template.h:9775-9789), computed on the device for dense
+ * Gaussian models (gp_approx "none"); other models fail with a message. */
 GPBOOST_AMD_EXPORT int GPB_GetCovPar(REModelHandle handle, double* cov_par, bool calc_std_dev);
 
 /* replaces GPB_GetNumIt (include/LightGBM/c_api.h:1559): iterations of the last GPB_OptimCovPar */

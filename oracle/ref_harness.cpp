@@ -120,7 +120,7 @@ int main(int argc, char** argv) {
   const int seed = std::atoi(get(args, "seed", "0").c_str());
   const int threads = std::atoi(get(args, "threads", "-1").c_str());
   const std::vector<double> cov_pars_orig = parse_list(get(args, "cov_pars", "0.1,1.6,0.2"));
-  const std::string mode = get(args, "mode", "eval");   // eval | lbfgs | fit
+  const std::string mode = get(args, "mode", "eval");   // eval | lbfgs | fit | stddev
   const int reps = std::atoi(get(args, "reps", "1").c_str());
   const int dump_nn = std::atoi(get(args, "dump_nn", "0").c_str());
   const std::string aux = get(args, "aux_pars", "");
@@ -209,6 +209,18 @@ int main(int argc, char** argv) {
   vec_t orig = Eigen::Map<const vec_t>(cov_pars_orig.data(), (int)cov_pars_orig.size());
   vec_t trafo;
   m->TransformCovPars(orig, trafo);
+
+  if (mode == "stddev") {
+    // GPB_GetCovPar(calc_std_dev = true) at cov_pars: CalculateStandardErrorsCovPars
+    // (re_model_template.h:1634-1660 -> CalcStdDevCovPar :9775-9789), transformed-scale input
+    vec_t sd(m->num_cov_par_);
+    m->CalculateStandardErrorsCovPars(trafo.data(), sd.data());
+    std::printf("{\n\"n\": %d, \"d\": %d,\n", n, d);
+    print_vec("cov_pars", orig.data(), (int)orig.size());
+    print_vec("std_dev", sd.data(), (int)sd.size());
+    std::printf("\"ok\": true\n}\n");
+    return 0;
+  }
 
   double nll = 0., sigma2 = gauss ? trafo[0] : 1.;
   vec_t grad, gb;

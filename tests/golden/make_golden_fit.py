@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Golden fixtures for GPB_OptimCovPar from the REFERENCE implementation.
+"""Golden fixtures for GPB_OptimCovPar and GPB_GetCovPar(calc_std_dev) from the REFERENCE implementation.
 
 Runs oracle/_ref/ref_harness in mode=fit (REModelTemplate::FindInitCovPar +
 OptimLinRegrCoefCovPar with the Python package's default optimizer settings: "lbfgs",
@@ -75,6 +75,21 @@ def main():
         r = run_ref(lc, yy, mode="fit", **sp)
         cases[name] = dict(data="bench_latent", n=nl, spec=sp, **{k: r[k] for k in r if k not in ("ok", "n", "d")})
         print(name, r["cov_pars"], r.get("aux_pars"), r["nll"], r["num_it"], file=sys.stderr)
+
+    # standard deviations (GPB_GetCovPar calc_std_dev = true; dense Gaussian), at fixed parameters.
+    # rtest: R-package test_GPModel_gaussian_process.R cov_pars (estimate, std dev) pairs
+    sd_cases = {
+        "sd_rtest_exponential": (coords, y, dict(cov_fct="exponential", gp_approx="none"), "0.03784221,1.07390943,0.11451432"),
+        "sd_rtest_matern15": (coords, y, dict(cov_fct="matern", shape=1.5, gp_approx="none"), "0.1,1.6,0.2"),
+        "sd_rtest_matern25": (coords, y, dict(cov_fct="matern", shape=2.5, gp_approx="none"), "0.2,0.9,0.05"),
+        "sd_rtest_gaussian": (coords, y, dict(cov_fct="gaussian", gp_approx="none"), "0.1,1.2,0.15"),
+        "sd_synth2000_exponential": (sc, sy, dict(cov_fct="exponential", gp_approx="none"), "0.1,1.0,0.1"),
+    }
+    for name, (cx, yy, sp, pars) in sd_cases.items():
+        r = run_ref(cx, yy, mode="stddev", cov_pars=pars, **sp)
+        cases[name] = dict(data="rtest_gaussian" if cx is coords else "bench", n=cx.shape[0], spec=sp,
+                           cov_pars=r["cov_pars"], std_dev=r["std_dev"])
+        print(name, r["std_dev"], file=sys.stderr)
 
     with open(os.path.join(HERE, "golden_fit.json"), "w") as f:
         json.dump(cases, f, indent=1)

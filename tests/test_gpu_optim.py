@@ -128,3 +128,32 @@ def test_fit_errors():
         gm.fit(np.where(np.arange(100) == 3, np.nan, Y))
     with pytest.raises(GPBoostError, match="out of scope"):
         gm.fit(Y, X=np.ones((100, 1)))
+
+
+@pytest.mark.parametrize("name", ["sd_rtest_exponential", "sd_rtest_matern15", "sd_rtest_matern25", "sd_rtest_gaussian",
+                                  "sd_synth2000_exponential"])
+def test_std_dev_matches_reference(golden_fit, name):
+    # GPB_GetCovPar(calc_std_dev = true): CalcStdDevCovPar (re_model_template.h:9775-9789), dense
+    case = golden_fit[name]
+    X, Y = _data(case)
+    gm = _model(case, X)
+    gm.neg_log_likelihood(case["cov_pars"], Y)   # sets the parameters GPB_GetCovPar reports
+    out = gm.get_cov_pars(std_err=True)
+    np.testing.assert_allclose(out[0], case["cov_pars"], rtol=1e-15)
+    np.testing.assert_allclose(out[1], case["std_dev"], rtol=1e-8)
+    if name == "sd_rtest_exponential":   # test_GPModel_gaussian_process.R:122-124 (TOLERANCE_STRICT)
+        assert np.sum(np.abs(out[1] - [0.07943467, 0.25351519, 0.03840236])) < 1e-5
+
+
+def test_std_dev_after_fit_and_errors(golden_fit):
+    case = golden_fit["rtest_dense_exponential"]
+    X, Y = _data(case)
+    gm = _model(case, X)
+    gm.fit(Y)
+    out = gm.get_cov_pars(std_err=True)
+    np.testing.assert_allclose(out[0], case["cov_pars"], rtol=1e-6)
+    assert np.all(np.isfinite(out[1])) and np.all(out[1] > 0)
+    gv = GPModel(gp_coords=X, cov_function="exponential", gp_approx="vecchia", num_neighbors=10)
+    gv.neg_log_likelihood([0.1, 1.0, 0.1], Y)
+    with pytest.raises(GPBoostError, match="standard deviations"):
+        gv.get_cov_pars(std_err=True)
