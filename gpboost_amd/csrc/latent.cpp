@@ -275,13 +275,20 @@ void LatentVecchia::BuildStructure(const int* nbr) {
     build(false, tile_b_);
     build(true, tile_bt_);
   }
-  {   // t = 1 form of B: ELL, column-major (SparseB)
+  {   // t = 1 form of B: ELL, column-major (SparseB). A row's entries in ascending storage index:
+      // lane l's r-th gather is then the r-th smallest neighbour of row base + l, so the 64 gathers
+      // of one load instruction fall on fewer cache lines than in neighbour (distance) order
+      // (GPBOOST_AMD_ELL_UNSORTED: distance order, A/B)
+    static const bool unsorted = std::getenv("GPBOOST_AMD_ELL_UNSORTED") != nullptr;
     std::vector<int> eidx((size_t)m * n), eslot((size_t)m * n);
+    std::vector<std::pair<int, int>> row(m);
     for (int i = 0; i < n; ++i) {
       const int k = std::min(i, m);
+      for (int r = 0; r < k; ++r) row[r] = {nbr[(size_t)i * m + r], i * m + r};
+      if (!unsorted) std::sort(row.begin(), row.begin() + k);
       for (int r = 0; r < m; ++r) {
-        eidx[(size_t)r * n + i] = r < k ? nbr[(size_t)i * m + r] : i;
-        eslot[(size_t)r * n + i] = r < k ? i * m + r : -1;
+        eidx[(size_t)r * n + i] = r < k ? row[r].first : i;
+        eslot[(size_t)r * n + i] = r < k ? row[r].second : -1;
       }
     }
     d_ell_idx_.alloc(eidx.size());
@@ -317,8 +324,34 @@ void LatentVecchia::BuildStructure(const int* nbr) {
     d_seg_pk_.alloc(pk.size());
     HIP_CHECK(hipMemcpy(d_seg_rb_.get(), seg.data(), sizeof(int) * seg.size(), hipMemcpyHostToDevice));
     HIP_CHECK(hipMemcpy(d_seg_pk_.get(), pk.data(), sizeof(uint32_t) * pk.size(), hipMemcpyHostToDevice));
+    // entry-pair layout of the runs: each run's entries start at an even position of a padded copy
+    // (pad entries: key 127, value 0), so a lane's two entries are one 8-byte and one 16-byte load
+    std::vector<int4> info(seg.size() - 1);
+    std::vector<uint32_t> pk2;
+    std::vector<int> slot2;
+    for (size_t w = 0; w + 1 < seg.size(); ++w) {
+      const int a = tptr[seg[w]], b = tptr[seg[w + 1]];
+      const int p0 = (int)pk2.size();
+      for (int e = a; e < b; ++e) { pk2.push_back(pk[e]); slot2.push_back(tslot[e]); }
+      if ((b - a) & 1) { pk2.push_back((uint32_t)kSegRows << 24); slot2.push_back(-1); }
+      info[w] = make_int4(seg[w], seg[w + 1], p0, p0 + (b - a));
+    }
+    seg2_n_ = (int)pk2.size();
+    d_seg_info_.alloc(std::max<size_t>(info.size(), 1));
+    d_seg_pk2_.alloc(std::max<size_t>(pk2.size(), 2));
+    d_seg_slot2_.alloc(std::max<size_t>(slot2.size(), 2));
+    d_seg_val2_.alloc(std::max<size_t>(slot2.size(), 2));
+    if (!info.empty())
+      HIP_CHECK(hipMemcpy(d_seg_info_.get(), info.data(), sizeof(int4) * info.size(), hipMemcpyHostToDevice));
+    if (!pk2.empty()) {
+      HIP_CHECK(hipMemcpy(d_seg_pk2_.get(), pk2.data(), sizeof(uint32_t) * pk2.size(), hipMemcpyHostToDevice));
+      HIP_CHECK(hipMemcpy(d_seg_slot2_.get(), slot2.data(), sizeof(int) * slot2.size(), hipMemcpyHostToDevice));
+    }
+    sp_.seg_pk2 = d_seg_pk2_.get();
+    sp_.seg_val2 = d_seg_val2_.get();
     sp_.seg_rb = d_seg_rb_.get();
     sp_.seg_pk = d_seg_pk_.get();
+    sp_.seg_info = d_seg_info_.get();
     sp_.nseg = (int)seg.size() - 1;
   }
 }
@@ -662,6 +695,7 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
   launch_latent_factor(cov_type, fa, s_);
   pre_->Refresh(d_Bv_.get());   // preconditioner plan values, dense head inverse
   launch_gather(tnnz_, d_tslot_.get(), d_Bv_.get(), d_tval_.get(), s_);   // B^T operator values, list order
+  if (seg2_n_ > 0) launch_gather(seg2_n_, d_seg_slot2_.get(), d_Bv_.get(), d_seg_val2_.get(), s_);   // paired runs
   sp_.tval_of = d_Bv_.get();
   launch_gather(n * m_, d_ell_slot_.get(), d_Bv_.get(), d_ell_val_.get(), s_);   // t = 1 form of B
   sp_.vals_of = d_Bv_.get();

@@ -130,6 +130,11 @@ class LatentVecchia {
   DevBuf<int> d_nbr_, d_tptr_, d_trow_, d_tslot_, d_longr_;
   DevBuf<int> d_ell_idx_, d_ell_slot_, d_seg_rb_;
   DevBuf<uint32_t> d_seg_pk_;
+  DevBuf<int4> d_seg_info_;
+  DevBuf<uint32_t> d_seg_pk2_;
+  DevBuf<int> d_seg_slot2_;
+  DevBuf<double> d_seg_val2_;
+  int seg2_n_ = 0;
   struct TileDev {   // device arrays of a TileOp
     DevBuf<int> r0, uoff, urow, fb;
     DevBuf<uint16_t> lidx;

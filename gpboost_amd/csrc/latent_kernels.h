@@ -58,6 +58,9 @@ struct SparseB {
   // sums its entries 64 at a time with a segmented wave scan.
   const int* seg_rb;
   const uint32_t* seg_pk;
+  const int4* seg_info;   // per run {row begin, row end, entry begin, entry end} in the paired layout
+  const uint32_t* seg_pk2; // paired layout: seg_pk with every run starting at an even position
+  const double* seg_val2;  // values in the paired layout (refreshed with tval)
   int nseg;
 };
 constexpr int kLongRow = 64;

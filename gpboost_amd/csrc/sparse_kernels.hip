@@ -529,6 +529,200 @@ __global__ void __launch_bounds__(64 * kSegWaves) bt_apply1s_kernel(
   }
 }
 
+// Two entries per lane (entries c + 2 lane, c + 2 lane + 1 of a 128-entry chunk): one segmented
+// scan per 128 entries instead of per 64. A lane's element is the running sum of its LAST entry's row
+// (both entries when they share a row); when its first entry closes an earlier row, that row's
+// chunk sum is the first entry plus the previous lane's scanned value (wave_shr:1). Runs hold whole
+// rows, so the last valid entry of a run carries the row-end flag and padding never needs a flush.
+template <bool DPP>
+__global__ void __launch_bounds__(64 * kSegWaves) bt_apply1s2_kernel(
+    int nseg, const int* __restrict__ seg_rb, const uint32_t* __restrict__ seg_pk, const int* __restrict__ tptr,
+    const double* __restrict__ tval, int unit, const double* __restrict__ X, const double* __restrict__ pre,
+    const double* __restrict__ W, const double* __restrict__ H, double* __restrict__ Y) {
+  __shared__ double acc_s[kSegWaves][kSegRows + 1];
+  constexpr uint32_t kPad = (uint32_t)kSegRows << 24;
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int w = xcd_block(blockIdx.x, gridDim.x) * kSegWaves + wv;
+  if (w >= nseg) return;   // whole waves only; no block-level synchronisation below
+  const int rb = seg_rb[w], re = seg_rb[w + 1];
+  const int nr = re - rb;
+  double* acc = acc_s[wv];
+  for (int q = lane; q < nr; q += 64) acc[q] = 0.;
+  const int e0 = tptr[rb], e1 = tptr[re];
+  for (int c = e0; c < e1; c += 128 * kSegU) {
+    uint32_t pa[kSegU], pb[kSegU];
+    double va[kSegU], vb[kSegU];
+#pragma unroll
+    for (int u = 0; u < kSegU; ++u) {
+      const int e = c + u * 128 + 2 * lane;
+      pa[u] = e < e1 ? seg_pk[e] : kPad;
+      pb[u] = e + 1 < e1 ? seg_pk[e + 1] : kPad;
+      va[u] = e < e1 ? tval[e] : 0.;
+      vb[u] = e + 1 < e1 ? tval[e + 1] : 0.;
+    }
+#pragma unroll
+    for (int u = 0; u < kSegU; ++u) {
+      const int ia = (int)(pa[u] & 0xFFFFFFu), ib = (int)(pb[u] & 0xFFFFFFu);
+      double ga = X[ia], gb = X[ib];
+      if (pre) { ga *= pre[ia]; gb *= pre[ib]; }
+      va[u] *= ga;
+      vb[u] *= gb;
+    }
+#pragma unroll
+    for (int u = 0; u < kSegU; ++u) {
+      const int ka = (int)((pa[u] >> 24) & 0x7Fu), kb = (int)((pb[u] >> 24) & 0x7Fu);
+      const bool same = ka == kb;
+      const double p = seg_scan<DPP>(same ? va[u] + vb[u] : vb[u], kb, lane);
+      // previous lane's scanned value and key (lane 0: none)
+      const int plo = __builtin_amdgcn_update_dpp(0, __double2loint(p), 0x138, 0xF, 0xF, false);
+      const int phi = __builtin_amdgcn_update_dpp(0, __double2hiint(p), 0x138, 0xF, 0xF, false);
+      const int pk = __builtin_amdgcn_update_dpp(-1, kb, 0x138, 0xF, 0xF, false);
+      if (!same && ka != kSegRows) acc[ka] += va[u] + (pk == ka ? __hiloint2double(phi, plo) : 0.);
+      if (kb != kSegRows && ((pb[u] >> 31) != 0u || lane == 63)) acc[kb] += p;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's accumulator writes before its reads
+  for (int q = lane; q < nr; q += 64) {
+    const int j = rb + q;
+    double s = unit ? (pre ? pre[j] * X[j] : X[j]) : 0.;
+    s += acc[q];
+    if (W) s = fma(W[j], H[j], s);
+    Y[j] = s;
+  }
+}
+
+// E entries per lane (entries c + E lane + q of a 64 E-entry chunk), U chunks in flight, run bounds
+// and entry range from one 16-byte load: a lane walks its E entries (sorted by row), closes the rows
+// that end inside it (the first one takes the previous lane's scanned value as carry), and the
+// running sum of its last row enters ONE segmented scan per 64 E entries.
+template <int E, int U>
+__global__ void __launch_bounds__(64 * kSegWaves) bt_apply1sE_kernel(
+    int nseg, const int4* __restrict__ seg_info, const uint32_t* __restrict__ seg_pk, const double* __restrict__ tval,
+    int unit, const double* __restrict__ X, const double* __restrict__ pre, const double* __restrict__ W,
+    const double* __restrict__ H, double* __restrict__ Y) {
+  __shared__ double acc_s[kSegWaves][kSegRows + 1];
+  constexpr uint32_t kPad = (uint32_t)kSegRows << 24;
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int w = xcd_block(blockIdx.x, gridDim.x) * kSegWaves + wv;
+  if (w >= nseg) return;   // whole waves only; no block-level synchronisation below
+  const int4 inf = seg_info[w];   // rows [x, y), entries [z, w)
+  const int rb = inf.x, nr = inf.y - inf.x, e1 = inf.w;
+  double* acc = acc_s[wv];
+  for (int q = lane; q < nr; q += 64) acc[q] = 0.;
+  for (int c = inf.z; c < e1; c += 64 * E * U) {
+    uint32_t pk[U][E];
+    double v[U][E];
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int q = 0; q < E; ++q) {
+        const int e = c + u * 64 * E + E * lane + q;
+        pk[u][q] = e < e1 ? seg_pk[e] : kPad;
+        v[u][q] = e < e1 ? tval[e] : 0.;
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int q = 0; q < E; ++q) {
+        const int id = (int)(pk[u][q] & 0xFFFFFFu);
+        double g = X[id];
+        if (pre) g *= pre[id];
+        v[u][q] *= g;
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kf = (int)((pk[u][0] >> 24) & 0x7Fu);
+      int kc = kf;
+      double sc = v[u][0], sf = 0.;
+      bool open = true;   // the lane's first row has not closed inside the lane
+#pragma unroll
+      for (int q = 1; q < E; ++q) {
+        const int kq = (int)((pk[u][q] >> 24) & 0x7Fu);
+        if (kq == kc) {
+          sc += v[u][q];
+        } else {
+          if (open) { sf = sc; open = false; }
+          else if (kc != kSegRows) acc[kc] += sc;   // a row wholly inside this lane
+          kc = kq;
+          sc = v[u][q];
+        }
+      }
+      const double p = seg_scan<true>(sc, kc, lane);
+      const int plo = __builtin_amdgcn_update_dpp(0, __double2loint(p), 0x138, 0xF, 0xF, false);   // wave_shr:1
+      const int phi = __builtin_amdgcn_update_dpp(0, __double2hiint(p), 0x138, 0xF, 0xF, false);
+      const int pkey = __builtin_amdgcn_update_dpp(-1, kc, 0x138, 0xF, 0xF, false);
+      if (!open && kf != kSegRows) acc[kf] += sf + (pkey == kf ? __hiloint2double(phi, plo) : 0.);
+      if (kc != kSegRows && ((pk[u][E - 1] >> 31) != 0u || lane == 63)) acc[kc] += p;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's accumulator writes before its reads
+  for (int q = lane; q < nr; q += 64) {
+    const int j = rb + q;
+    double s = unit ? (pre ? pre[j] * X[j] : X[j]) : 0.;
+    s += acc[q];
+    if (W) s = fma(W[j], H[j], s);
+    Y[j] = s;
+  }
+}
+
+// Paired layout (SparseB::seg_pk2 / seg_val2: runs start at even positions): the E = 2 form with a
+// lane's two entries as one 8-byte structure load and one 16-byte value load.
+template <int U>
+__global__ void __launch_bounds__(64 * kSegWaves) bt_apply1p_kernel(
+    int nseg, const int4* __restrict__ seg_info, const uint2* __restrict__ pk2, const double2* __restrict__ val2,
+    int unit, const double* __restrict__ X, const double* __restrict__ pre, const double* __restrict__ W,
+    const double* __restrict__ H, double* __restrict__ Y) {
+  __shared__ double acc_s[kSegWaves][kSegRows + 1];
+  constexpr uint32_t kPad = (uint32_t)kSegRows << 24;
+  const int lane = threadIdx.x & 63;
+  const int wv = threadIdx.x >> 6;
+  const int w = xcd_block(blockIdx.x, gridDim.x) * kSegWaves + wv;
+  if (w >= nseg) return;   // whole waves only; no block-level synchronisation below
+  const int4 inf = seg_info[w];   // rows [x, y), entries [z, w) (z even)
+  const int rb = inf.x, nr = inf.y - inf.x, e1 = inf.w;
+  double* acc = acc_s[wv];
+  for (int q = lane; q < nr; q += 64) acc[q] = 0.;
+  for (int c = inf.z; c < e1; c += 128 * U) {
+    uint2 pk[U];
+    double2 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = c + u * 128 + 2 * lane;   // even; e + 1 is a real or pad slot of this run when e < e1
+      if (e < e1) { pk[u] = pk2[e >> 1]; v[u] = val2[e >> 1]; }
+      else { pk[u] = make_uint2(kPad, kPad); v[u] = make_double2(0., 0.); }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int ia = (int)(pk[u].x & 0xFFFFFFu), ib = (int)(pk[u].y & 0xFFFFFFu);
+      double ga = X[ia], gb = X[ib];
+      if (pre) { ga *= pre[ia]; gb *= pre[ib]; }
+      v[u].x *= ga;
+      v[u].y *= gb;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int ka = (int)((pk[u].x >> 24) & 0x7Fu), kb = (int)((pk[u].y >> 24) & 0x7Fu);
+      const bool same = ka == kb;
+      const double p = seg_scan<true>(same ? v[u].x + v[u].y : v[u].y, kb, lane);
+      const int plo = __builtin_amdgcn_update_dpp(0, __double2loint(p), 0x138, 0xF, 0xF, false);   // wave_shr:1
+      const int phi = __builtin_amdgcn_update_dpp(0, __double2hiint(p), 0x138, 0xF, 0xF, false);
+      const int pkey = __builtin_amdgcn_update_dpp(-1, kb, 0x138, 0xF, 0xF, false);
+      if (!same && ka != kSegRows) acc[ka] += v[u].x + (pkey == ka ? __hiloint2double(phi, plo) : 0.);
+      if (kb != kSegRows && ((pk[u].y >> 31) != 0u || lane == 63)) acc[kb] += p;
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this wave's accumulator writes before its reads
+  for (int q = lane; q < nr; q += 64) {
+    const int j = rb + q;
+    double s = unit ? (pre ? pre[j] * X[j] : X[j]) : 0.;
+    s += acc[q];
+    if (W) s = fma(W[j], H[j], s);
+    Y[j] = s;
+  }
+}
+
 // t = 1 default form of B (SparseB::ell_*): one row per lane, entries in a fixed ascending order,
 // kU1 loads in flight per lane. (The same form for B^T — sliced ELL, rows sorted by length in
 // windows — measured 37-48 us against the lane groups' 20 us: rows-as-lanes only pays where every
@@ -1197,8 +1391,30 @@ void launch_bt_apply(const SparseB& B, const double* vals, bool unit, const doub
   static const bool groups1 = std::getenv("GPBOOST_AMD_BT1_GROUPS") != nullptr;   // A/B: lane-group form
   if (t == 1 && tval != nullptr && !old1 && !groups1 && B.seg_rb != nullptr) {
     static const bool shfl = std::getenv("GPBOOST_AMD_BT1_SCAN_SHFL") != nullptr;   // A/B: ds_bpermute scan
+    static const bool one = std::getenv("GPBOOST_AMD_BT1_E1") != nullptr;   // A/B: one entry per lane
+    static const int epl = [] {   // A/B: GPBOOST_AMD_BT1_E = 2 / 4 (unpaired layout, E entries per lane)
+      const char* e = std::getenv("GPBOOST_AMD_BT1_E");
+      return e ? std::atoi(e) : 0;
+    }();
     const dim3 g((B.nseg + kSegWaves - 1) / kSegWaves), b(64 * kSegWaves);
-    if (shfl)
+    if (!one && !shfl && epl == 0 && B.seg_info != nullptr) {   // default: paired layout
+#ifndef GPB_PAIR_U
+#define GPB_PAIR_U 4
+#endif
+      hipLaunchKernelGGL((bt_apply1p_kernel<GPB_PAIR_U>), g, b, 0, s, B.nseg, B.seg_info,
+                         reinterpret_cast<const uint2*>(B.seg_pk2), reinterpret_cast<const double2*>(B.seg_val2),
+                         unit ? 1 : 0, X, pre, W, H, Y);
+    } else if (!one && !shfl && B.seg_info != nullptr && (epl == 2 || epl == 4)) {
+      if (epl == 4)
+        hipLaunchKernelGGL((bt_apply1sE_kernel<4, 2>), g, b, 0, s, B.nseg, B.seg_info, B.seg_pk2, B.seg_val2,
+                           unit ? 1 : 0, X, pre, W, H, Y);
+      else
+        hipLaunchKernelGGL((bt_apply1sE_kernel<2, 4>), g, b, 0, s, B.nseg, B.seg_info, B.seg_pk2, B.seg_val2,
+                           unit ? 1 : 0, X, pre, W, H, Y);
+    } else if (!one && !shfl)
+      hipLaunchKernelGGL(bt_apply1s2_kernel<true>, g, b, 0, s, B.nseg, B.seg_rb, B.seg_pk, B.tptr, tval,
+                         unit ? 1 : 0, X, pre, W, H, Y);
+    else if (shfl)
       hipLaunchKernelGGL(bt_apply1s_kernel<false>, g, b, 0, s, B.nseg, B.seg_rb, B.seg_pk, B.tptr, tval,
                          unit ? 1 : 0, X, pre, W, H, Y);
     else
