@@ -223,6 +223,45 @@ class GPModel:
         self.model_fitted = True
         return self
 
+    def get_init_cov_pars(self):
+        """Initial covariance parameters of the last fit (original scale; GPB_GetInitCovPar), or
+        None when none were given or determined (reference basic.py:5564-5570)."""
+        out = np.zeros(self.num_cov_pars)
+        _safe_call(lib().GPB_GetInitCovPar(self.handle, _dp(out)))
+        return None if np.all(out == -1.) else out
+
+    def cov_par_names(self):
+        """Parameter names as the reference labels them (error term only for the Gaussian likelihood)."""
+        return (["Error_term"] if self.num_cov_pars == 3 else []) + ["GP_var", "GP_range"]
+
+    def summary(self, std_err=False):
+        """Print a summary of the fitted parameters (reference basic.py:5709-5770, GP models):
+        log-likelihood, AIC and BIC after a fit, covariance parameters (with standard deviations
+        when std_err, dense Gaussian models only) and auxiliary parameters."""
+        import pandas as pd
+        cp = self.get_cov_pars(std_err=std_err)
+        rows = cp if std_err else cp.reshape(1, -1)
+        print("=====================================================")
+        print("Model summary:")
+        print("Nb. observations: " + str(self.num_data))
+        if getattr(self, "model_fitted", False):
+            ll = -self.get_current_neg_log_likelihood()
+            npar = self.num_cov_pars
+            aic = 2 * npar - 2 * ll
+            bic = npar * np.log(self.num_data) - 2 * ll
+            out = pd.DataFrame([[round(ll, 2), round(aic, 2), round(bic, 2)]], columns=["Log-lik", "AIC", "BIC"])
+            print(out.to_string(index=False))
+            print("-----------------------------------------------------")
+        print("Covariance parameters (random effects):")
+        print(pd.DataFrame(rows.T, index=self.cov_par_names(),
+                           columns=["Param.", "Std. dev."] if std_err else ["Param."]).round(4).to_string())
+        if self.num_aux_pars:
+            aux, name = self.get_aux_pars()
+            print("-----------------------------------------------------")
+            print("Additional parameters:")
+            print(pd.DataFrame(aux.reshape(-1, 1), index=[name or "aux"], columns=["Param."]).round(4).to_string())
+        print("=====================================================")
+
     def get_num_optim_iter(self):
         """Number of optimizer iterations of the last fit (GPB_GetNumIt)."""
         k = ctypes.c_int(0)

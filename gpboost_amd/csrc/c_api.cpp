@@ -314,6 +314,12 @@ int GPB_GetNumIt(REModelHandle handle, int* num_it) {
   API_END();
 }
 
+int GPB_GetInitCovPar(REModelHandle handle, double* init_cov_pars) {
+  API_BEGIN();
+  model(handle)->GetInitCovPar(init_cov_pars);
+  API_END();
+}
+
 int GPB_OptimCovPar(REModelHandle handle, const double* y_data, const double* fixed_effects) {
   // c_api.cpp GPB_OptimCovPar -> REModel::OptimCovPar(y, fixed_effects, false, false)
   API_BEGIN();

@@ -370,6 +370,9 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects) {
     const double sample_var = std::max((sum_sq - n * avg * avg) / (n - 1), 1e-6);
     aux_pars_[0] = sample_var / 2.;
   }
+  if (cfg_.latent) init_used_ = {trafo[0], range_back(cfg_.cov_type, trafo[1])};
+  else init_used_ = {trafo[0], trafo[1] * trafo[0], range_back(cfg_.cov_type, trafo[2])};
+  if (!init_cov_pars_.empty()) init_used_ = init_cov_pars_;
   std::vector<double> x;
   double fx = 0.;
   if (!cfg_.latent) {
@@ -392,6 +395,11 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects) {
   cov_pars_initialized_ = true;
   last_nll_ = fx;
   last_cov_pars_ = cov_pars_orig_;
+}
+
+void REModelAMD::GetInitCovPar(double* out) const {
+  const std::vector<double>& v = !init_cov_pars_.empty() ? init_cov_pars_ : init_used_;
+  for (int k = 0; k < num_cov_pars(); ++k) out[k] = v.empty() ? -1. : v[k];
 }
 
 void REModelAMD::StdDevCovPars(const double* orig, double* sd) {

@@ -107,6 +107,9 @@ class REModelAMD {
   // re_model_template.h:9775-9789; dense Gaussian models only).
   void StdDevCovPars(const double* cov_pars_orig, double* sd);
   int num_it() const { return num_it_; }
+  // GPB_GetInitCovPar (re_model.cpp:813-834): initial values on the original scale, or -1 each
+  // when none were given or determined yet
+  void GetInitCovPar(double* out) const;
 
   // Evaluations on the transformed scale (used by the optimizer): Gaussian trafo =
   // (sigma^2, sigma1^2 / sigma^2, phi); latent trafo = (sigma1^2, phi). fatal_on_nan = false
@@ -173,7 +176,7 @@ class REModelAMD {
   double last_kernel_ms_[2] = {0., 0.};
 
   LbfgsSettings optim_;
-  std::vector<double> init_cov_pars_, cov_pars_orig_;   // original scale
+  std::vector<double> init_cov_pars_, cov_pars_orig_, init_used_;   // original scale
   bool cov_pars_initialized_ = false;
   int num_it_ = 0;
 };

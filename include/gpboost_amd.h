@@ -174,6 +174,11 @@ GPBOOST_AMD_EXPORT int GPB_GetCovPar(REModelHandle handle, double* cov_par, bool
 /* replaces GPB_GetNumIt (include/LightGBM/c_api.h:1559): iterations of the last GPB_OptimCovPar */
 GPBOOST_AMD_EXPORT int GPB_GetNumIt(REModelHandle handle, int* num_it);
 
+/* replaces GPB_GetInitCovPar (include/LightGBM/c_api.h:1537; re_model.cpp:813-834): the initial
+ * covariance parameters on the original scale (given by GPB_SetOptimConfig or determined by the
+ * last GPB_OptimCovPar), -1 each when there are none yet */
+GPBOOST_AMD_EXPORT int GPB_GetInitCovPar(REModelHandle handle, double* init_cov_pars);
+
 /* replaces GPB_OptimCovPar (include/LightGBM/c_api.h:1471; c_api.cpp GPB_OptimCovPar ->
  * re_model.cpp:339-401): estimates the covariance parameters (and, for "vecchia_latent", the
  * error variance aux par) with the reference's default optimizer "lbfgs" (optim_utils.h:561-706:

@@ -88,6 +88,12 @@ def test_fit_r_golden():
     est = gm.get_cov_pars()
     assert np.sum(np.abs(est - np.array([0.03784221, 1.07390943, 0.11451432]))) < 1e-2
     assert abs(gm.get_current_neg_log_likelihood() - 122.7771373) < 1e-2
+    # FindInitCovPar values (reference fit fixture) and the summary printout
+    import json as _json
+    with open(os.path.join(HERE, "golden", "golden_fit.json")) as f:
+        ref = _json.load(f)["rtest_dense_exponential"]
+    np.testing.assert_allclose(gm.get_init_cov_pars(), ref["init_cov_pars"], rtol=1e-12)
+    gm.summary(std_err=True)
 
 
 @pytest.mark.parametrize("name", ["latent500_bernoulli_m20", "latent500_gaussian_m20"])
