@@ -347,10 +347,6 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects) {
     Fatal("response variable y has not been set");
   }
   EnsureStructure();
-  if (optim_.max_iterations <= 0) {   // max_iter_ = 0: nothing is estimated
-    num_it_ = 0;
-    return;
-  }
   const bool with_aux = cfg_.latent && estimate_aux_pars && !aux_pars_.empty();
   // initial values on the transformed scale (InitializeCovParsIfNotDefined re_model.cpp:1142-1164)
   double trafo[3];
@@ -373,6 +369,13 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects) {
   if (cfg_.latent) init_used_ = {trafo[0], range_back(cfg_.cov_type, trafo[1])};
   else init_used_ = {trafo[0], trafo[1] * trafo[0], range_back(cfg_.cov_type, trafo[2])};
   if (!init_cov_pars_.empty()) init_used_ = init_cov_pars_;
+  if (optim_.max_iterations <= 0) {   // max_iter_ = 0 (re_model_template.h:1223): the parameters stay at their initial values
+    num_it_ = 0;
+    cov_pars_orig_ = init_used_;
+    cov_pars_initialized_ = true;
+    last_cov_pars_ = cov_pars_orig_;
+    return;
+  }
   std::vector<double> x;
   double fx = 0.;
   if (!cfg_.latent) {

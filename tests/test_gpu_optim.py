@@ -163,3 +163,12 @@ def test_std_dev_after_fit_and_errors(golden_fit):
     gv.neg_log_likelihood([0.1, 1.0, 0.1], Y)
     with pytest.raises(GPBoostError, match="standard deviations"):
         gv.get_cov_pars(std_err=True)
+
+
+def test_fit_maxit_zero_keeps_initial_values(golden_fit):
+    case = golden_fit["rtest_dense_exponential"]
+    X, Y = _data(case)
+    gm = _model(case, X)
+    gm.fit(Y, params={"maxit": 0})
+    assert gm.get_num_optim_iter() == 0
+    np.testing.assert_allclose(gm.get_cov_pars(), case["init_cov_pars"], rtol=1e-12)
