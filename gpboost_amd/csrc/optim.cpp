@@ -366,12 +366,13 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects) {
     const double sample_var = std::max((sum_sq - n * avg * avg) / (n - 1), 1e-6);
     aux_pars_[0] = sample_var / 2.;
   }
-  if (cfg_.latent) init_used_ = {trafo[0], range_back(cfg_.cov_type, trafo[1])};
-  else init_used_ = {trafo[0], trafo[1] * trafo[0], range_back(cfg_.cov_type, trafo[2])};
-  if (!init_cov_pars_.empty()) init_used_ = init_cov_pars_;
+  std::vector<double> start_orig;
+  if (cfg_.latent) start_orig = {trafo[0], range_back(cfg_.cov_type, trafo[1])};
+  else start_orig = {trafo[0], trafo[1] * trafo[0], range_back(cfg_.cov_type, trafo[2])};
+  if (!cov_pars_initialized_) init_used_ = start_orig;   // FindInitCovPar's values (re_model.cpp:1159-1160)
   if (optim_.max_iterations <= 0) {   // max_iter_ = 0 (re_model_template.h:1223): the parameters stay at their initial values
     num_it_ = 0;
-    cov_pars_orig_ = init_used_;
+    cov_pars_orig_ = start_orig;
     cov_pars_initialized_ = true;
     last_cov_pars_ = cov_pars_orig_;
     return;
