@@ -86,6 +86,24 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
   for (int i = 0; i < n; ++i)
     for (int q = 0; q < d; ++q) coords_[(size_t)i * d + q] = coords_colmajor[(size_t)q * n + i];
 
+  if (cfg_.latent) {
+    // The reference runs latent GPs on the UNIQUE locations (RECompGP on unique REs with an
+    // incidence matrix, Vecchia_utils.cpp:1121-1139; only_one_GP_calculations_on_RE_scale): with
+    // repeated coordinates its latent dimension is the number of distinct points. This build keeps
+    // one latent variable per observation, so repeated coordinates would silently define a
+    // different model: refuse them.
+    std::vector<int> ord(n);
+    for (int i = 0; i < n; ++i) ord[i] = i;
+    auto row = [&](int i) { return coords_.data() + (size_t)i * d; };
+    std::sort(ord.begin(), ord.end(), [&](int a, int b) {
+      return std::lexicographical_compare(row(a), row(a) + d, row(b), row(b) + d);
+    });
+    for (int k = 1; k < n; ++k)
+      if (std::equal(row(ord[k - 1]), row(ord[k - 1]) + d, row(ord[k])))
+        Fatal("duplicate coordinates (observations %d and %d): latent Vecchia models with repeated locations "
+              "are not supported by gpboost_amd (the reference collapses them to unique locations)",
+              std::min(ord[k - 1], ord[k]), std::max(ord[k - 1], ord[k]));
+  }
   HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_sums_), 16 * sizeof(double), hipHostMallocDefault));

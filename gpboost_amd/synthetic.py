@@ -63,20 +63,33 @@ def rtest_bernoulli_probit_y(n: int = 100) -> tuple[np.ndarray, np.ndarray]:
     return coords, y
 
 
+def lcg_unif(n: int, init_c: float = 0.1) -> np.ndarray:
+    """The same LCG in exact integer arithmetic, u_{k+1} = (22695477 u_k + 1) mod 2^32.
+    The R tests' double-arithmetic version (sim_rand_unif) rounds 22695477 u_k once it exceeds 2^53
+    and falls into a cycle of ~40.6k draws: 2n draws for n = 100k coordinates give only 20318
+    distinct points. The benchmark generators use this exact form (period 2^32)."""
+    out = np.empty(n, dtype=np.float64)
+    s = int(np.floor(init_c * _MOD))
+    for k in range(n):
+        out[k] = s
+        s = (22695477 * s + 1) & 0xFFFFFFFF
+    return out / _MOD
+
+
 def bench_coords(n: int, d: int = 2) -> np.ndarray:
-    """Benchmark coordinates: 2n LCG draws (c=0.1) filled column-major."""
-    return sim_rand_unif(n * d, 0.1).reshape(d, n).T.copy()
+    """Benchmark coordinates: 2n LCG draws (c=0.1, exact arithmetic) filled column-major."""
+    return lcg_unif(n * d, 0.1).reshape(d, n).T.copy()
 
 
 def bench_gaussian_y(n: int) -> np.ndarray:
-    """iid N(0,1) by Box-Muller from LCG streams c=0.8 and c=0.42."""
-    u1 = np.maximum(sim_rand_unif(n, 0.8), 1e-300)
-    u2 = sim_rand_unif(n, 0.42)
+    """iid N(0,1) by Box-Muller from LCG streams c=0.8 and c=0.42 (exact arithmetic)."""
+    u1 = np.maximum(lcg_unif(n, 0.8), 1e-300)
+    u2 = lcg_unif(n, 0.42)
     return np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * u2)
 
 
 def bench_bernoulli_y(coords: np.ndarray) -> np.ndarray:
-    """y = 1[u < (1 + sin(2 pi x1) cos(2 pi x2)) / 2], u from LCG c=0.19341."""
+    """y = 1[u < (1 + sin(2 pi x1) cos(2 pi x2)) / 2], u from LCG c=0.19341 (exact arithmetic)."""
     n = coords.shape[0]
     p = 0.5 * (1.0 + np.sin(2 * np.pi * coords[:, 0]) * np.cos(2 * np.pi * coords[:, 1]))
-    return (sim_rand_unif(n, 0.19341) < p).astype(np.float64)
+    return (lcg_unif(n, 0.19341) < p).astype(np.float64)

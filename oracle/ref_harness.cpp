@@ -264,7 +264,7 @@ int main(int argc, char** argv) {
   if (gauss && gp_approx == "vecchia") {
     std::printf("\"yTPsiInvy\": %.17g, \"log_det_Psi\": %.17g,\n", m->yTPsiInvy_, m->log_det_Psi_);
   }
-  if (gp_approx == "vecchia" && dump_nn) {
+  if ((gp_approx == "vecchia" || gp_approx == "vecchia_latent") && dump_nn) {
     const auto& perm = m->data_indices_per_cluster_[m->unique_clusters_[0]];
     std::printf("\"perm\": [");
     for (size_t i = 0; i < perm.size(); ++i) std::printf("%s%d", i ? "," : "", perm[i]);
