@@ -465,7 +465,7 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (reference R-test LCG: uniform 2-D coords, Box-Muller N(0,1) y)",
+        "data": "synthetic (the R-test LCG in exact integer arithmetic: 100k distinct uniform 2-D coords, Box-Muller N(0,1) y)",
         "config": {"workload": "vecchia_gaussian_exact_lbfgs_unit", "n": N_DATA, "num_neighbors": M_NEIGHBORS,
                    "cov_function": "exponential", "theta": THETA, "ordering": "random",
                    "parallelism": f"rows{world}", "construction_s": round(t_construct, 3),
