@@ -236,3 +236,23 @@ def test_two_live_models_different_head_sizes(monkeypatch):
     ra2 = a.neg_log_likelihood_and_grad([1.0, 0.1], None)   # the large-head model again
     assert ra2[0] == ra[0] and np.array_equal(ra2[1], ra[1])
     assert abs(rb[0] - ra[0]) <= 1e-8 * abs(ra[0])
+
+
+def test_baseline_size_matches_reference():
+    """BASELINE config 3 at its full size (n = 100k, m = 30, t = 50, cg_delta_conv = 1e-2, VADU) against
+    the reference run here (tests/golden/make_golden_100k.py): the stochastic estimates use the
+    same probe streams and stopping rules, so they agree to the 1e-6 north-star tolerance (observed
+    ~1e-15 nll, ~1e-9 gradient)."""
+    import json
+    import os
+
+    from gpboost_amd import synthetic
+    with open(os.path.join(os.path.dirname(__file__), "golden", "golden_100k.json")) as f:
+        case = json.load(f)["latent"]
+    n = case["n"]
+    X = synthetic.bench_coords(n)
+    y = synthetic.bench_gaussian_y(n)
+    gm = _model(X, dict(likelihood="gaussian", cov_fct="exponential", shape=0.5, num_neighbors=30, aux=case["aux"]),
+                t=case["num_rand_vec_trace"], seed=1, dc=case["cg_delta_conv"])
+    nll, g, _ = gm.neg_log_likelihood_and_grad(case["cov_pars"], y)
+    _check(nll, g, case["nll"], case["grad"])

@@ -226,3 +226,21 @@ def test_gpu_neighbor_search_ties_bit_exact(m):
     ref_perm, _, ref_nbr = O.vecchia_setup(X, m, 0, True)
     assert np.array_equal(perm, ref_perm)
     assert np.array_equal(nbr, ref_nbr)
+
+
+def test_baseline_size_matches_reference():
+    """The headline unit (exact Gaussian Vecchia, L-BFGS objective, n = 100k, m = 30) against the
+    reference run here (tests/golden/make_golden_100k.py)."""
+    import json
+    import os
+
+    from gpboost_amd import synthetic
+    with open(os.path.join(os.path.dirname(__file__), "golden", "golden_100k.json")) as f:
+        case = json.load(f)["exact"]
+    X = synthetic.bench_coords(case["n"])
+    y = synthetic.bench_gaussian_y(case["n"])
+    gm = _model(X, 30)
+    nll, g, s2 = gm.neg_log_likelihood_and_grad(case["cov_pars"], y, profile_sigma2=True)
+    assert abs(nll - case["nll"]) <= 1e-10 * abs(case["nll"])
+    assert _close(g, case["grad"], rtol=1e-8)
+    assert abs(s2 - case["sigma2"]) <= 1e-10 * case["sigma2"]
