@@ -256,3 +256,29 @@ def test_baseline_size_matches_reference():
                 t=case["num_rand_vec_trace"], seed=1, dc=case["cg_delta_conv"])
     nll, g, _ = gm.neg_log_likelihood_and_grad(case["cov_pars"], y)
     _check(nll, g, case["nll"], case["grad"])
+
+
+def test_baseline_size_bernoulli_matches_reference():
+    """BASELINE config 5 (bernoulli_logit, Laplace + PCG / SLQ, n = 100k, m = 30, default tolerance)
+    against the reference run here (tests/golden/make_golden_100k.py)."""
+    import json
+    import os
+
+    from gpboost_amd import synthetic
+    with open(os.path.join(os.path.dirname(__file__), "golden", "golden_100k.json")) as f:
+        case = json.load(f)["bernoulli"]
+    X = synthetic.bench_coords(case["n"])
+    y = synthetic.bench_bernoulli_y(X)
+    gm = _model(X, dict(likelihood="bernoulli_logit", cov_fct="exponential", shape=0.5, num_neighbors=30),
+                t=case["num_rand_vec_trace"], seed=1, dc=case["cg_delta_conv"])
+    nll, g, _ = gm.neg_log_likelihood_and_grad(case["cov_pars"], y)
+    _check(nll, g, case["nll"], case["grad"])
+
+
+def test_latent_refuses_repeated_coordinates():
+    from gpboost_amd import GPModel, GPBoostError, synthetic
+    X = synthetic.bench_coords(500)
+    X[7] = X[3]
+    with pytest.raises(GPBoostError, match="duplicate coordinates"):
+        GPModel(gp_coords=X, likelihood="bernoulli_logit", gp_approx="vecchia", num_neighbors=10,
+                matrix_inversion_method="iterative")
