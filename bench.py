@@ -498,6 +498,7 @@ def main():
         "config": {"workload": "vecchia_gaussian_exact_lbfgs_unit", "n": N_DATA, "num_neighbors": M_NEIGHBORS,
                    "cov_function": "exponential", "theta": THETA, "ordering": "random",
                    "parallelism": f"rows{world}", "construction_s": round(t_construct, 3),
+                   **({"note": "RCCL row sharding at world_size > 1: first hardware run is this one"} if world > 1 else {}),
                    "nll": nll, "grad": [float(x) for x in g]},
         "roofline": {"bound": "mfma", "achieved": achieved_tf, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved_tf / FP64_PEAK_TFLOPS, "traffic": None,
