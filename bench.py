@@ -198,8 +198,13 @@ def latent_leg(X, Y, steps: int, cpu: bool) -> dict:
     ms_a1, ms_p1, _, _ = gm.bench_latent_operators(1, 50)
     byts1 = latent_matvec_bytes(n, int(nnz), 1)
     ach1 = byts1 / (ms_a1 * 1e-3) / 1e9
+    tr1 = None   # HBM-side bytes per application from the committed PMC passes (profiles/r02/pmc_op1_traffic.json)
+    pth = os.path.join(ROOT, "profiles", "r02", "pmc_op1_traffic.json")
+    if os.path.exists(pth):
+        with open(pth) as f:
+            tr1 = json.load(f).get("bytes_per_application")
     leg["cg_matvec_roofline_single"] = {"bound": "hbm", "achieved": ach1, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                        "frac": ach1 / HBM_PEAK_GBS, "traffic": None,
+                                        "frac": ach1 / HBM_PEAK_GBS, "traffic": tr1,
                                         "kernel": "b_apply1e (ELL) + bt_apply1s (segmented runs)", "kernel_ms": ms_a1, "columns": 1,
                                         "algorithmic_bytes_per_launch": byts1, "preconditioner_ms": ms_p1}
     its = int(info[2])
