@@ -137,6 +137,8 @@ class GPModel:
             ctypes.c_bool(weights is not None), None, ctypes.c_double(likelihood_learning_rate),
             ctypes.byref(handle)))
         self.handle = handle
+        self.has_covariates = False
+        self.num_covariates = 0
         k = ctypes.c_int(0)
         _safe_call(lib().GPB_GetNumCovPars(self.handle, ctypes.byref(k)))
         self.num_cov_pars = k.value
@@ -160,6 +162,15 @@ class GPModel:
             pass
 
     # ------------------------------------------------------------------ reference API
+    def _call(self, ret: int):
+        """_safe_call, then re-raise an exception of a host all-reduce callback (set_distributed_host):
+        the callback fills the buffer with NaN on failure, so the library stops with an error."""
+        err = getattr(self, "_host_reduce_error", None)
+        if err is not None:
+            self._host_reduce_error = None
+            raise GPBoostError(f"the host all-reduce callback failed: {err!r}") from err
+        _safe_call(ret)
+
     def _check_y(self, y):
         if y is None:
             return None
@@ -206,12 +217,11 @@ class GPModel:
             float(p["delta_conv_mode_finding"])))
 
     def fit(self, y, X=None, params=None, offset=None, fixed_effects=None):
-        """Estimate the covariance parameters by maximising the (approximate marginal) likelihood
-        (reference basic.py:5067-5275 -> GPB_OptimCovPar). Covariates X are out of scope."""
+        """Estimate the covariance parameters (and, with X, the linear regression coefficients) by
+        maximising the (approximate marginal) likelihood (reference basic.py:5067-5275 ->
+        GPB_OptimCovPar, or GPB_OptimLinRegrCoefCovPar when X is given: GLS coefficients)."""
         if fixed_effects is not None:
             raise GPBoostError("The argument 'fixed_effects' is discontinued. Use the renamed equivalent argument 'offset' instead")
-        if X is not None:
-            raise GPBoostError("linear regression covariates (X) are out of scope for gpboost_amd")
         y = self._check_y(y)
         off = None
         if offset is not None:
@@ -219,9 +229,81 @@ class GPModel:
             if off.shape[0] != self.num_data:
                 raise ValueError("Incorrect number of data points in 'offset'")
         self.set_optim_params(params)
-        _safe_call(lib().GPB_OptimCovPar(self.handle, _dp(y), _dp(off) if off is not None else None))
+        if X is None:
+            self.has_covariates = False
+            self._call(lib().GPB_OptimCovPar(self.handle, _dp(y), _dp(off) if off is not None else None))
+        else:
+            Xa = np.asarray(X, dtype=np.float64)
+            if Xa.ndim == 1:
+                Xa = Xa.reshape(-1, 1)
+            if Xa.shape[0] != self.num_data:
+                raise ValueError("Incorrect number of data points in 'X'")
+            if not np.all(np.isfinite(Xa)):
+                raise ValueError("'X' contains NaN or Inf")
+            self.num_covariates = Xa.shape[1]
+            self.has_covariates = True
+            xcol = np.ascontiguousarray(Xa.T).reshape(-1)   # column-major, as the reference passes it
+            self._call(lib().GPB_OptimLinRegrCoefCovPar(self.handle, _dp(y), _dp(xcol), ctypes.c_int(self.num_covariates),
+                                                        _dp(off) if off is not None else None))
         self.model_fitted = True
         return self
+
+    def get_coef(self, std_err=False):
+        """Linear regression coefficients (GPB_GetCoef); std_err=True: 2 x p [coefficients; std. devs.]
+        (reference basic.py:5630-5660)."""
+        if not getattr(self, "has_covariates", False):
+            raise GPBoostError("Model does not have covariates for a linear predictor")
+        p = self.num_covariates
+        out = np.zeros(2 * p if std_err else p)
+        _safe_call(lib().GPB_GetCoef(self.handle, _dp(out), ctypes.c_bool(std_err)))
+        return out.reshape(2, -1) if std_err else out
+
+    def predict_training_data_random_effects(self, predict_var=False):
+        """Predicted training-data random effects (GPB_PredictREModelTrainingDataRandomEffects,
+        reference basic.py:6316-6367): (n,) means, or (n, 2) [mean, variance] with predict_var."""
+        out = np.zeros(2 * self.num_data if predict_var else self.num_data)
+        _safe_call(lib().GPB_PredictREModelTrainingDataRandomEffects(self.handle, None, None, _dp(out), None,
+                                                                     ctypes.c_bool(bool(predict_var))))
+        return out.reshape(2, -1).T.copy() if predict_var else out
+
+    def _get_string(self, fn):
+        buf = ctypes.create_string_buffer(256)
+        k = ctypes.c_int(0)
+        _safe_call(fn(self.handle, buf, ctypes.byref(k)))
+        return buf.value.decode()
+
+    def get_optim_params(self):
+        """Optimizer settings incl. the names the library reports (reference basic.py:5544-5581:
+        GPB_GetOptimizerCovPars / GetOptimizerCoef / GetCGPreconditionerType / GetInitCovPar /
+        GetInitAuxPars)."""
+        params = dict(self.params)
+        params["optimizer_cov"] = self._get_string(lib().GPB_GetOptimizerCovPars)
+        params["optimizer_coef"] = self._get_string(lib().GPB_GetOptimizerCoef)
+        params["cg_preconditioner_type"] = self._get_string(lib().GPB_GetCGPreconditionerType)
+        init = self.get_init_cov_pars()
+        if init is not None:
+            params["init_cov_pars"] = init
+        if self.num_aux_pars > 0:
+            a = np.zeros(self.num_aux_pars)
+            _safe_call(lib().GPB_GetInitAuxPars(self.handle, _dp(a)))
+            if np.any(a != -1.):
+                params["init_aux_pars"] = a
+        return params
+
+    def get_response_data(self):
+        out = np.zeros(self.num_data)
+        _safe_call(lib().GPB_GetResponseData(self.handle, _dp(out)))
+        return out
+
+    def get_covariate_data(self):
+        out = np.zeros(self.num_data * self.num_covariates)
+        _safe_call(lib().GPB_GetCovariateData(self.handle, _dp(out)))
+        return out.reshape(self.num_covariates, self.num_data).T.copy()
+
+    def can_calculate_standard_errors_cov_pars(self):
+        out = ctypes.c_int(0)
+        _safe_call(lib().GPB_CanCalculateStandardErrorsCovPars(self.handle, ctypes.byref(out)))
+        return bool(out.value)
 
     def get_init_cov_pars(self):
         """Initial covariance parameters of the last fit (original scale; GPB_GetInitCovPar), or
@@ -286,7 +368,7 @@ class GPModel:
             if fe.shape[0] != self.num_data:
                 raise ValueError("Length of 'fixed_effects' is not correct ")
         negll = ctypes.c_double(0)
-        _safe_call(lib().GPB_EvalNegLogLikelihood(self.handle, _dp(y) if y is not None else None, _dp(cp),
+        self._call(lib().GPB_EvalNegLogLikelihood(self.handle, _dp(y) if y is not None else None, _dp(cp),
                                                   _dp(fe) if fe is not None else None, ctypes.byref(negll)))
         return negll.value
 
@@ -327,7 +409,7 @@ class GPModel:
             raise ValueError("'cov_pars' contains NaN or Inf")
         negll, grad, s2 = bufs["negll"], bufs["grad"], bufs["s2"]
         grad.fill(np.nan)
-        _safe_call(lib().GPB_EvalNegLogLikelihoodGrad(
+        self._call(lib().GPB_EvalNegLogLikelihoodGrad(
             self.handle, _dp(y) if y is not None else None, ptrs["cp"], _dp(fe) if fe is not None else None,
             int(bool(profile_sigma2)), ptrs["negll"], ptrs["grad"], ptrs["s2"]))
         if profile_sigma2:
@@ -337,6 +419,20 @@ class GPModel:
         else:
             g = grad[: self.num_cov_pars]
         return float(negll[0]), g.copy(), float(s2[0])
+
+    def calc_gradient_f(self, y=None, fixed_effects=None):
+        """Gradient of the (approximate marginal) negative log-likelihood wrt the fixed effects F at the
+        current covariance parameters (GPB_CalcGradientF = the reference's REModel::CalcGradient, the
+        GPBoost algorithm's boosting gradient). Gaussian likelihood: y = F - label, returns
+        Psi^-1 y / sigma^2; latent models: F = fixed_effects, returns -dlog p/dF + implicit terms."""
+        if y is not None:
+            out = _as1d(y, "y").copy()
+        else:
+            out = np.zeros(self.num_data)
+        fe = _as1d(fixed_effects, "fixed_effects") if fixed_effects is not None else None
+        self._call(lib().GPB_CalcGradientF(self.handle, _dp(out), _dp(fe) if fe is not None else None,
+                                           ctypes.c_bool(True)))
+        return out
 
     def last_iteration_info(self):
         """[newton iterations, CG iterations, Lanczos steps, log|Sigma W + I|] of the last latent evaluation."""
@@ -413,9 +509,15 @@ class GPModel:
         if vecchia_pred_type is not None or num_neighbors_pred is not None:
             self.set_prediction_data(vecchia_pred_type=vecchia_pred_type, num_neighbors_pred=num_neighbors_pred)
         if any(v is not None for v in (group_data_pred, group_rand_coef_data_pred, gp_rand_coef_data_pred,
-                                       cluster_ids_pred, X_pred)):
-            raise GPBoostError("predictions with grouped random effects, random coefficients, clusters or "
-                               "covariates are not supported by gpboost_amd")
+                                       cluster_ids_pred)):
+            raise GPBoostError("predictions with grouped random effects, random coefficients or clusters are not "
+                               "supported by gpboost_amd")
+        xpc = None
+        if X_pred is not None:
+            Xp = np.asarray(X_pred, dtype=np.float64)
+            if Xp.ndim == 1:
+                Xp = Xp.reshape(-1, 1)
+            xpc = np.ascontiguousarray(Xp.T).reshape(-1)
         if gp_coords_pred is None:
             raise ValueError("'gp_coords_pred' is missing")
         xp = np.asarray(gp_coords_pred, dtype=np.float64)
@@ -442,7 +544,7 @@ class GPModel:
             self.handle, _dp(yv) if yv is not None else None, ctypes.c_int32(n_pred), _dp(out),
             ctypes.c_bool(bool(predict_cov_mat)), ctypes.c_bool(bool(predict_var)),
             ctypes.c_bool(bool(predict_response)), None, None, None, _dp(xcol), None,
-            _dp(cp) if cp is not None else None, None, ctypes.c_bool(bool(use_saved_data)),
+            _dp(cp) if cp is not None else None, _dp(xpc) if xpc is not None else None, ctypes.c_bool(bool(use_saved_data)),
             _dp(fe) if fe is not None else None, _dp(fep) if fep is not None else None))
         mu = out[:n_pred].copy()
         cov = out[n_pred:].reshape(n_pred, n_pred).T.copy() if predict_cov_mat else None
@@ -461,9 +563,16 @@ class GPModel:
         """Same partition as set_distributed, with the cross-rank sums done by
         ``allreduce(x: np.ndarray)`` (in place, e.g. a gloo all-reduce) instead of RCCL
         (GPB_SetDistributedHostReduce): a test transport for several ranks on one GPU."""
+        self._host_reduce_error = None
+
         def _cb(buf, count, _user):
             arr = np.ctypeslib.as_array(buf, shape=(count,))
-            allreduce(arr)
+            try:
+                allreduce(arr)
+            except BaseException as e:   # ctypes would print and drop it: record it and poison the sums
+                if self._host_reduce_error is None:
+                    self._host_reduce_error = e
+                arr[:] = np.nan
         self._host_reduce = _HostReduceFn(_cb)   # keep the trampoline alive with the model
         _safe_call(lib().GPB_SetDistributedHostReduce(self.handle, ctypes.c_int(rank), ctypes.c_int(world_size),
                                                       self._host_reduce, None))

@@ -41,6 +41,11 @@ REModelAMD* model(REModelHandle h) {
 
 std::string str_or(const char* s, const char* def) { return s ? std::string(s) : std::string(def); }
 
+void copy_name(const std::string& name, char* out_str, int* num_char) {
+  if (num_char) *num_char = (int)name.size() + 1;
+  if (out_str) std::memcpy(out_str, name.c_str(), name.size() + 1);
+}
+
 }  // namespace
 
 namespace gpb_amd {
@@ -162,11 +167,11 @@ int GPB_SetOptimConfig(REModelHandle handle, double* init_cov_pars, double lr, d
   API_BEGIN();
   (void)acc_rate_cov; (void)use_nesterov_acc; (void)nesterov_schedule_version; (void)trace; (void)momentum_offset;
   (void)convergence_criterion;   // L-BFGS always tests the relative change of the objective (optim_utils.h:656-657)
-  (void)lr_coef; (void)acc_rate_coef; (void)optimizer_coef; (void)piv_chol_rank;
+  (void)lr_coef; (void)acc_rate_coef; (void)piv_chol_rank;
   REModelAMD* m = model(handle);
-  if (num_covariates > 0 || init_coef != nullptr)
-    gpb_amd::Fatal("linear regression coefficients (covariates) are not supported by gpboost_amd");
+  (void)num_covariates; (void)init_coef;   // the "wls" coefficient update profiles beta out at every evaluation
   m->SetOptimSettings(init_cov_pars, lr, max_iter, delta_rel_conv, optimizer, m_lbfgs);
+  m->SetOptimizerNames(optimizer, optimizer_coef, cg_preconditioner_type);
   if (m->config().matrix_inversion_method == "iterative") {   // :775-801
     m->iter.cg_max_num_it = cg_max_num_it;
     m->iter.cg_max_num_it_tridiag = cg_max_num_it_tridiag;
@@ -182,10 +187,7 @@ int GPB_SetOptimConfig(REModelHandle handle, double* init_cov_pars, double lr, d
   m->iter.seed_rand_vec_trace = seed_rand_vec_trace;
   m->iter.reuse_rand_vec_trace = reuse_rand_vec_trace;
   if (delta_conv_mode_finding > 0.) m->iter.delta_conv_mode_finding = delta_conv_mode_finding;   // :820-822
-  if (init_aux_pars != nullptr) {
-    m->SetAuxPars(init_aux_pars);
-    m->aux_pars_set_ = true;
-  }
+  if (init_aux_pars != nullptr) m->SetInitAuxPars(init_aux_pars);
   m->estimate_aux_pars = estimate_aux_pars;   // :803
   if (estimate_cov_par_index != nullptr && estimate_cov_par_index[0] >= 0) {
     for (int k = 0; k < m->num_cov_pars(); ++k)
@@ -199,16 +201,9 @@ int GPB_EvalNegLogLikelihood(REModelHandle handle, const double* y_data, double*
   API_BEGIN();
   REModelAMD* m = model(handle);
   if (cov_pars == nullptr) gpb_amd::Fatal("cov_pars is NULL (initial-value heuristics are out of scope)");
-  if (fixed_effects != nullptr) {
-    if (y_data == nullptr) gpb_amd::Fatal("EvalNegLogLikelihood: 'y_data' cannot nullptr when 'fixed_effects' is provided");
-    if (m->config().latent && m->config().lik != gpb_amd::kLikGaussian)
-      gpb_amd::Fatal("'fixed_effects' are not supported for likelihood '%s' by gpboost_amd", m->config().likelihood.c_str());
-    std::vector<double> r(m->config().n);
-    for (int i = 0; i < m->config().n; ++i) r[i] = y_data[i] - fixed_effects[i];
-    m->SetY(r.data());
-  } else if (y_data != nullptr) {
-    m->SetY(y_data);
-  }
+  if (fixed_effects != nullptr && y_data == nullptr && !m->config().latent)
+    gpb_amd::Fatal("EvalNegLogLikelihood: 'y_data' cannot nullptr when 'fixed_effects' is provided");
+  m->SetResponseAndOffset(y_data, fixed_effects);
   negll[0] = m->Eval(cov_pars, false, 0).nll;
   API_END();
 }
@@ -242,13 +237,20 @@ int GPB_PredictREModel(REModelHandle handle, const double* y_data, int32_t num_d
   if (out_predict == nullptr) gpb_amd::Fatal("out_predict is NULL");
   if (use_saved_data) gpb_amd::Fatal("use_saved_data: saved prediction data is not supported by gpboost_amd");
   if (cluster_ids_data_pred != nullptr || re_group_data_pred != nullptr || re_group_rand_coef_data_pred != nullptr ||
-      gp_rand_coef_data_pred != nullptr || covariate_data_pred != nullptr)
-    gpb_amd::Fatal("predictions with clusters, grouped random effects, random coefficients or covariates are not "
+      gp_rand_coef_data_pred != nullptr)
+    gpb_amd::Fatal("predictions with clusters, grouped random effects or random coefficients are not "
                    "supported by gpboost_amd");
   REModelAMD* m = model(handle);
   std::vector<double> r;
   const double* y = y_data;
-  if (fixed_effects != nullptr) {   // the GP part of the response (re_model_template.h:3386-3393)
+  if (m->has_covariates()) {   // y - X beta - offset (SetYCalcCovCalcYAuxForPred, re_model_template.h:3386-3410)
+    if (covariate_data_pred == nullptr)
+      gpb_amd::Fatal("Covariate data 'X_pred' is not provided but the model has covariates");
+    r = m->ResidualResponse(y_data, fixed_effects);
+    y = r.data();
+  } else if (covariate_data_pred != nullptr) {
+    gpb_amd::Fatal("Covariate data 'X_pred' is provided but the model has no covariates");
+  } else if (fixed_effects != nullptr) {   // the GP part of the response (re_model_template.h:3386-3393)
     if (y_data == nullptr) gpb_amd::Fatal("'y_data' cannot be NULL when 'fixed_effects' is provided");
     r.resize(m->config().n);
     for (int i = 0; i < m->config().n; ++i) r[i] = y_data[i] - fixed_effects[i];
@@ -256,6 +258,7 @@ int GPB_PredictREModel(REModelHandle handle, const double* y_data, int32_t num_d
   }
   m->Predict(y, num_data_pred, gp_coords_data_pred, cov_pars, predict_cov_mat, predict_var, predict_response,
              out_predict);
+  if (m->has_covariates()) m->AddLinearPredictor(covariate_data_pred, num_data_pred, out_predict);
   if (fixed_effects_pred != nullptr)
     for (int i = 0; i < num_data_pred; ++i) out_predict[i] += fixed_effects_pred[i];
   API_END();
@@ -267,16 +270,7 @@ int GPB_EvalNegLogLikelihoodGrad(REModelHandle handle, const double* y_data, con
   API_BEGIN();
   REModelAMD* m = model(handle);
   if (cov_pars == nullptr || negll == nullptr || grad == nullptr) gpb_amd::Fatal("NULL argument");
-  if (fixed_effects != nullptr) {
-    if (y_data == nullptr) gpb_amd::Fatal("'y_data' cannot be NULL when 'fixed_effects' is provided");
-    if (m->config().latent && m->config().lik != gpb_amd::kLikGaussian)
-      gpb_amd::Fatal("'fixed_effects' are not supported for likelihood '%s' by gpboost_amd", m->config().likelihood.c_str());
-    std::vector<double> r(m->config().n);
-    for (int i = 0; i < m->config().n; ++i) r[i] = y_data[i] - fixed_effects[i];
-    m->SetY(r.data());
-  } else if (y_data != nullptr) {
-    m->SetY(y_data);
-  }
+  m->SetResponseAndOffset(y_data, fixed_effects);
   gpb_amd::EvalResult res = m->Eval(cov_pars, true, profile_sigma2 ? 1 : 0);
   negll[0] = res.nll;
   for (size_t k = 0; k < res.grad.size(); ++k) {
@@ -324,6 +318,116 @@ int GPB_OptimCovPar(REModelHandle handle, const double* y_data, const double* fi
   // c_api.cpp GPB_OptimCovPar -> REModel::OptimCovPar(y, fixed_effects, false, false)
   API_BEGIN();
   model(handle)->OptimCovPar(y_data, fixed_effects);
+  API_END();
+}
+
+int GPB_OptimLinRegrCoefCovPar(REModelHandle handle, const double* y_data, const double* covariate_data,
+                               int num_covariates, const double* fixed_effects) {
+  // c_api.cpp:2843-2852 -> REModel::OptimLinRegrCoefCovPar (re_model.cpp:403-469)
+  API_BEGIN();
+  model(handle)->OptimLinRegrCoefCovPar(y_data, covariate_data, num_covariates, fixed_effects);
+  API_END();
+}
+
+int GPB_CalcGradientF(REModelHandle handle, double* y, const double* fixed_effects, bool calc_cov_factor) {
+  // REModel::CalcGradient (re_model.cpp:667-680), the call the boosting objective makes
+  // (regression_objective.hpp:164-179)
+  API_BEGIN();
+  model(handle)->CalcGradientF(y, fixed_effects, calc_cov_factor);
+  API_END();
+}
+
+int GPB_CanCalculateStandardErrorsCovPars(REModelHandle handle, int* out) {
+  API_BEGIN();
+  out[0] = (int)model(handle)->CanCalculateStandardErrorsCovPars();
+  API_END();
+}
+
+int GPB_GetCoef(REModelHandle handle, double* optim_coef, bool calc_std_dev) {
+  API_BEGIN();
+  model(handle)->GetCoef(optim_coef, calc_std_dev);
+  API_END();
+}
+
+int GPB_PredictREModelTrainingDataRandomEffects(REModelHandle handle, const double* cov_pars_pred, const double* y_obs,
+                                                double* out_predict, const double* fixed_effects, bool calc_var) {
+  API_BEGIN();
+  if (out_predict == nullptr) gpb_amd::Fatal("out_predict is NULL");
+  model(handle)->PredictTrainingDataRandomEffects(cov_pars_pred, y_obs, out_predict, fixed_effects, calc_var);
+  API_END();
+}
+
+int GPB_GetOptimizerCovPars(REModelHandle handle, char* out_str, int* num_char) {
+  API_BEGIN();
+  copy_name(model(handle)->optimizer_cov(), out_str, num_char);
+  API_END();
+}
+
+int GPB_GetOptimizerCoef(REModelHandle handle, char* out_str, int* num_char) {
+  API_BEGIN();
+  copy_name(model(handle)->optimizer_coef(), out_str, num_char);
+  API_END();
+}
+
+int GPB_GetCGPreconditionerType(REModelHandle handle, char* out_str, int* num_char) {
+  API_BEGIN();
+  copy_name(model(handle)->cg_preconditioner_type(), out_str, num_char);
+  API_END();
+}
+
+int GPB_GetNumCGSteps(REModelHandle handle, int* num_cg_steps) {
+  // re_model_template.h:527-537: defined for models of several grouped random effects only
+  API_BEGIN();
+  (void)model(handle);
+  (void)num_cg_steps;
+  gpb_amd::Fatal("GetNumCGStepLast: this function is currently only implemented when having multiple grouped random "
+                 "effects and iterative methods are used ");
+  API_END();
+}
+
+int GPB_GetNumCGStepsTridiag(REModelHandle handle, int* num_cg_steps) {
+  API_BEGIN();   // re_model_template.h:542-552
+  (void)model(handle);
+  (void)num_cg_steps;
+  gpb_amd::Fatal("GetNumCGStepLast: this function is currently only implemented when having multiple grouped random "
+                 "effects and iterative methods are used ");
+  API_END();
+}
+
+int GPB_SetLikelihood(REModelHandle handle, const char* likelihood) {
+  API_BEGIN();
+  if (likelihood == nullptr) gpb_amd::Fatal("likelihood is NULL");
+  model(handle)->SetLikelihood(std::string(likelihood));
+  API_END();
+}
+
+int GPB_GetResponseData(REModelHandle handle, double* response_data) {
+  API_BEGIN();
+  model(handle)->GetResponseData(response_data);
+  API_END();
+}
+
+int GPB_GetCovariateData(REModelHandle handle, double* covariate_data) {
+  API_BEGIN();
+  model(handle)->GetCovariateData(covariate_data);
+  API_END();
+}
+
+int GPB_GetOffsetData(REModelHandle handle, double* fixed_effects) {
+  API_BEGIN();
+  model(handle)->GetOffsetData(fixed_effects);
+  API_END();
+}
+
+int GPB_SetOffsetData(REModelHandle handle, const double* fixed_effects) {
+  API_BEGIN();
+  model(handle)->SetOffsetData(fixed_effects);
+  API_END();
+}
+
+int GPB_GetInitAuxPars(REModelHandle handle, double* aux_pars) {
+  API_BEGIN();
+  model(handle)->GetInitAuxPars(aux_pars);
   API_END();
 }
 

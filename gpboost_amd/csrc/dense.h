@@ -22,11 +22,18 @@ class DenseSolver {
   // D1 = correlation matrix, D2 = dscale * dcorr/dlog(phi) and G_k = P D_k, sums6 =
   // [sum P^2, sum P o G1, sum P o G2, tr(G1 G1), tr(G1 G2), tr(G2 G2)].
   void Fisher(int cov_type, double var, double phi, double dscale, double* sums6);
+  // Gram matrix of the covariates: G (host, c x c) = Z^T Psi^-1 Z for the host column-major n x c
+  // matrix Z = [X | y] (CalcXTPsiInvX, re_model_template.h:9125-9132).
+  void Gram(int cov_type, double var, double phi, const double* Z, int c, double* G);
+  // Psi^-1 y and diag(Psi^-1) (host, n each) for the training-data random-effect predictions.
+  void PsiInvDiag(int cov_type, double var, double phi, const double* d_y, double* yaux, double* diag);
 
  private:
   void Potrf();
   void PotrfLookahead();
   void Trtri(int a, int b);
+  void Factor(int cov_type, double var, double phi);   // Psi, L (POTRF) and W = L^-1 (TRTRI)
+  void CheckInfo();                                    // synchronises; fails if POTRF failed
 
   int n_, d_, ld_;
   const double* d_X_;

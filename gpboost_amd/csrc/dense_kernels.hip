@@ -565,6 +565,21 @@ __global__ void __launch_bounds__(256) fisher_trace_kernel(const double* __restr
   if (threadIdx.x < 6) part[(size_t)tile * 6 + threadIdx.x] = red[threadIdx.x * 256];
 }
 
+// diag_j = sum_{i >= j} W_ij^2 (diag(W^T W) = diag(Psi^-1) for W = L^-1), one wave per column
+__global__ void __launch_bounds__(256) colnorm2_lower_kernel(const double* W, int ld, int n, double* diag) {
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (j >= n) return;
+  double s = 0.;
+  for (int i = j + lane; i < n; i += 64) {
+    const double w = W[(size_t)i + (size_t)j * ld];
+    s += w * w;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) diag[j] = s;
+}
+
 __global__ void dot_kernel(const double* a, const double* b, int n, double* out) {
   __shared__ double red[256];
   double s = 0.;
@@ -863,6 +878,59 @@ void DenseSolver::Fisher(int cov_type, double var, double phi, double dscale, do
   HIP_CHECK(hipStreamSynchronize(stream_));
   if (info != 0) Fatal("the covariance matrix is not positive definite (Cholesky failed)");
   for (int q = 0; q < 6; ++q) sums6[q] = h_red_[q];
+}
+
+void DenseSolver::Factor(int cov_type, double var, double phi) {
+  const int n = n_, ld = ld_, d = d_;
+  HIP_CHECK(hipMemsetAsync(info_.get(), 0, sizeof(int), stream_));
+  const int nt = (n + 63) / 64;
+  dispatch_cov(cov_type, [&](auto c) {
+    hipLaunchKernelGGL((build_psi_kernel<decltype(c)::value>), dim3(nt, nt), dim3(256), 0, stream_, d_X_, n, d, ld, var,
+                       phi, A_.get());
+  });
+  HIP_CHECK(hipGetLastError());
+  PotrfLookahead();
+  Trtri(0, n);
+}
+
+void DenseSolver::CheckInfo() {
+  int info = 0;
+  HIP_CHECK(hipMemcpyAsync(&info, info_.get(), sizeof(int), hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  if (info != 0) Fatal("the covariance matrix is not positive definite (Cholesky failed)");
+}
+
+void DenseSolver::Gram(int cov_type, double var, double phi, const double* Z, int c, double* G) {
+  // [X | y]^T Psi^-1 [X | y] = (W Z)^T (W Z), W = L^-1 (CalcXTPsiInvX, re_model_template.h:9125-9132)
+  const int n = n_, ld = ld_;
+  Factor(cov_type, var, phi);
+  DevBuf<double> dZ((size_t)ld * c), WZ((size_t)ld * c), dG((size_t)c * c);
+  HIP_CHECK(hipMemsetAsync(dZ.get(), 0, sizeof(double) * dZ.size(), stream_));
+  HIP_CHECK(hipMemcpy2DAsync(dZ.get(), sizeof(double) * ld, Z, sizeof(double) * n, sizeof(double) * n, c,
+                             hipMemcpyHostToDevice, stream_));
+  gemm(stream_, n, c, n, 1., W_.get(), ld, 0, dZ.get(), ld, 0, 0., WZ.get(), ld, 0, 1, 0, 0);
+  gemm(stream_, c, c, n, 1., WZ.get(), ld, 1, WZ.get(), ld, 0, 0., dG.get(), c);
+  HIP_CHECK(hipMemcpyAsync(G, dG.get(), sizeof(double) * c * c, hipMemcpyDeviceToHost, stream_));
+  CheckInfo();
+}
+
+void DenseSolver::PsiInvDiag(int cov_type, double var, double phi, const double* d_y, double* yaux, double* diag) {
+  const int n = n_, ld = ld_;
+  Factor(cov_type, var, phi);
+  double* W = W_.get();
+  double* z = vec_.get();
+  double* ya = z + ld;
+  double* partial = z + 2 * (size_t)ld;
+  DevBuf<double> dg(n);
+  const int nb = (n + 255) / 256;
+  hipLaunchKernelGGL(trmv_lower_partial_kernel, dim3(nb, nb), dim3(256), 0, stream_, W, ld, n, d_y, partial);
+  hipLaunchKernelGGL(trmv_lower_reduce_kernel, dim3(nb), dim3(256), 0, stream_, partial, n, z);
+  hipLaunchKernelGGL(trmv_lower_t_kernel, dim3((n + 3) / 4), dim3(256), 0, stream_, W, ld, n, z, ya);
+  hipLaunchKernelGGL(colnorm2_lower_kernel, dim3((n + 3) / 4), dim3(256), 0, stream_, W, ld, n, dg.get());
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipMemcpyAsync(yaux, ya, sizeof(double) * n, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipMemcpyAsync(diag, dg.get(), sizeof(double) * n, hipMemcpyDeviceToHost, stream_));
+  CheckInfo();
 }
 
 }  // namespace gpb_amd

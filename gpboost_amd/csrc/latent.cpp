@@ -364,6 +364,27 @@ void LatentVecchia::SetY(const double* y_vo) {
   y_set_ = true;
 }
 
+void LatentVecchia::SetOffset(const double* off_vo) {
+  if (off_vo == nullptr) {
+    has_off_ = false;
+    return;
+  }
+  std::vector<double> op(n_);
+  for (int p = 0; p < n_; ++p) op[p] = off_vo[vo_[p]];
+  d_off_.alloc(n_);
+  HIP_CHECK(hipMemcpyAsync(d_off_.get(), op.data(), sizeof(double) * n_, hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  has_off_ = true;
+}
+
+void LatentVecchia::GetMode(double* mode_vo) {
+  if (!factor_ready_) Fatal("the posterior mode has not been computed (no evaluation yet)");
+  std::vector<double> mp(n_);
+  HIP_CHECK(hipMemcpyAsync(mp.data(), d_mode_.get(), sizeof(double) * n_, hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  for (int p = 0; p < n_; ++p) mode_vo[vo_[p]] = mp[p];
+}
+
 LatentVecchia::Block& LatentVecchia::GetBlock(int which, int t, int pmax) {
   std::unique_ptr<Block>& bp = which == 0 ? blk1_ : (which == 1 ? blkt_ : blkb_);
   if (!bp) bp.reset(new Block());
@@ -669,7 +690,7 @@ LatentVecchia::PcgResult LatentVecchia::Pcg(Block& b, const double* RHS, double*
 }
 
 LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, double aux, const IterativeConfig& cfg,
-                                 bool want_grad, bool want_aux_grad) {
+                                 bool want_grad, bool want_aux_grad, double* grad_f_vo) {
   if (!y_set_) Fatal("response variable y has not been set");
   if (!(trafo[0] > 0. && trafo[1] > 0.)) Fatal("covariance parameters must be > 0");
   if (lik == kLikGaussian && !(aux > 0.)) Fatal("the error variance (aux_pars) must be > 0");
@@ -705,6 +726,7 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
   if (std::getenv("GPBOOST_AMD_BENCH_PRECOND")) {   // diagnostics: preconditioner cost alone
     NewtonPrepArgs np{};
     np.n = n; np.lik = lik; np.aux = aux; np.y = d_y_.get(); np.loc = d_mode_.get(); np.mode = d_mode_.get();
+    np.offset = has_off_ ? d_off_.get() : nullptr;
     np.Dinv = d_Dinv_.get(); np.d1 = d_d1_.get(); np.W = d_W_.get(); np.W_update = 1; np.dw = d_dw_.get();
     HIP_CHECK(hipMemsetAsync(d_mode_.get(), 0, sizeof(double) * n, s_));
     launch_newton_prep(np, s_);
@@ -727,6 +749,7 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
   ScalarArgs sa{};
   sa.n = n; sa.m = m_; sa.lik = lik; sa.aux = aux;
   sa.nbr = d_nbr_.get(); sa.Bv = d_Bv_.get(); sa.Dinv = d_Dinv_.get(); sa.y = d_y_.get();
+  sa.offset = has_off_ ? d_off_.get() : nullptr;
 
   // ---- 2. mode finding (likelihoods.h:2780-3000); mode re-initialised to 0 (InitializeModeAvec)
   HIP_CHECK(hipMemsetAsync(d_mode_.get(), 0, sizeof(double) * n, s_));
@@ -760,7 +783,7 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
     std::swap(d_mode_, d_mode_new_);
     res.newton_its = it + 1;
     if (std::isnan(mll_new) || std::isinf(mll_new))
-      Fatal("NaN or Inf occurred in the mode finding algorithm for the Laplace approximation");
+      throw LatentNan("NaN or Inf occurred in the mode finding algorithm for the Laplace approximation");
     const double dc = cfg.delta_conv_mode_finding;
     const bool term = (it == 0) ? std::fabs(mll_new - mll) < dc * std::fabs(mll) : (mll_new - mll) < dc * std::fabs(mll);
     mll = mll_new;
@@ -777,6 +800,7 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
     // the block rule (each column's iterates are exactly those of a separate run).
     NewtonPrepArgs np{};
     np.n = n; np.lik = lik; np.aux = aux; np.y = d_y_.get(); np.loc = d_mode_.get(); np.mode = d_mode_.get();
+    np.offset = has_off_ ? d_off_.get() : nullptr;
     np.Dinv = d_Dinv_.get(); np.d1 = d_d1_.get(); np.W = d_W_.get(); np.W_update = 1;
     np.rhs = d_rhs_.get(); np.dw = d_dw_.get(); np.sdw = d_sdw_.get();
     launch_newton_prep(np, s_);
@@ -791,17 +815,25 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
     launch_pack_columns(n, tw, d_Zp_.get(), tw, 0, d_rhsf_.get(), tf, 1, s_);
     launch_pack_columns(n, 1, d_rhs_.get(), 1, 0, d_rhsf_.get(), tf, 0, s_);
     slq = Pcg(*bslq, d_rhsf_.get(), d_Uf_.get(), 1, true, true, cg_max, pmax_tri, cfg.cg_delta_conv, 1 + tl, nb_all);
-    if (slq.nan) Fatal("NaN or Inf occurred in the conjugate gradient algorithm (mode finding / log-determinant)");
+    if (slq.nan) throw LatentNan("NaN or Inf occurred in the conjugate gradient algorithm (mode finding / log-determinant)");
     res.cg_its = slq.its_single;
     launch_pack_columns(n, 1, d_Uf_.get(), tf, 0, d_mode_upd_.get(), 1, 0, s_);
     launch_pack_columns(n, tw, d_Uf_.get(), tf, 1, d_U_.get(), tw, 0, s_);
     line_search_and_check(0, 0.);
+    {   // first derivative at the mode (likelihoods.h:3008; used by the gradient wrt F)
+      NewtonPrepArgs nd{};
+      nd.n = n; nd.lik = lik; nd.aux = aux; nd.y = d_y_.get(); nd.loc = d_mode_.get(); nd.mode = d_mode_.get();
+      nd.offset = has_off_ ? d_off_.get() : nullptr;
+      nd.Dinv = d_Dinv_.get(); nd.d1 = d_d1_.get(); nd.W = d_W_.get(); nd.W_update = 0;
+      launch_newton_prep(nd, s_);
+    }
   } else {
     // ---- 2. mode finding (likelihoods.h:2780-3000)
     bool upd_zero = true;
     for (int it = 0; it < maxit; ++it) {
       NewtonPrepArgs np{};
       np.n = n; np.lik = lik; np.aux = aux; np.y = d_y_.get(); np.loc = d_mode_.get(); np.mode = d_mode_.get();
+    np.offset = has_off_ ? d_off_.get() : nullptr;
       np.Dinv = d_Dinv_.get(); np.d1 = d_d1_.get(); np.W = d_W_.get();
       np.W_update = 1;
       np.rhs = d_rhs_.get();
@@ -811,7 +843,7 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
       const PcgResult pr = Pcg(b1, d_rhs_.get(), d_mode_upd_.get(), 1, it == 0, upd_zero, cg_max, 0, cfg.cg_delta_conv);
       res.cg_its += pr.its_single;
       upd_zero = pr.zero_rhs;
-      if (pr.nan) Fatal("NaN or Inf occurred in the conjugate gradient algorithm during mode finding");
+      if (pr.nan) throw LatentNan("NaN or Inf occurred in the conjugate gradient algorithm during mode finding");
       // Armijo (likelihoods.h:2957-2966)
       launch_axpby(n, 1., d_mode_upd_.get(), -1., d_mode_.get(), d_dir_.get(), s_);
       ApplyA(d_dir_.get(), d_Adir_.get(), b1.G.get(), 1);
@@ -821,6 +853,7 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
     {   // derivative / information at the mode, VADU diagonal and its square root (:3000-3005, 12163-12166)
       NewtonPrepArgs np{};
       np.n = n; np.lik = lik; np.aux = aux; np.y = d_y_.get(); np.loc = d_mode_.get(); np.mode = d_mode_.get();
+    np.offset = has_off_ ? d_off_.get() : nullptr;
       np.Dinv = d_Dinv_.get(); np.d1 = d_d1_.get(); np.W = d_W_.get();
       np.W_update = info_changes ? 1 : 0;
       np.dw = d_dw_.get();
@@ -832,7 +865,7 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
     bslq = &GetBlock(1, tw, pmax_tri);
     launch_bt_apply(sp_, d_Bv_.get(), true, d_probes_.get(), tw, d_sdw_.get(), nullptr, nullptr, d_Zp_.get(), s_);
     slq = Pcg(*bslq, d_Zp_.get(), d_U_.get(), 0, true, true, 0, pmax_tri, cfg.cg_delta_conv, tl, nb_all);
-    if (slq.nan) Fatal("NaN or Inf occurred in the stochastic Lanczos quadrature (log-determinant)");
+    if (slq.nan) throw LatentNan("NaN or Inf occurred in the stochastic Lanczos quadrature (log-determinant)");
   }
   Block& bt = *bslq;
   const int L = slq.its_block;
@@ -882,6 +915,7 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
       ModeDerivArgs md{};
       md.n = n; md.m = m_; md.t = tw; md.lik = lik; md.nbr = d_nbr_.get(); md.Bv = d_Bv_.get(); md.dw = d_dw_.get();
       md.loc = d_mode_.get(); md.U = d_U_.get(); md.P = d_P_.get(); md.dmll = d_dmll_.get();
+      md.offset = has_off_ ? d_off_.get() : nullptr;
       md.t_valid = tl; md.t_all = t;
       if (coll_ == nullptr) {
         md.stage = 0;
@@ -950,6 +984,15 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
       double g = 0.5 * (2. * sc[kSqDQuadRng] - sc[kSqDDQuad] + dld);
       if (!gauss) g -= sc[kSqImpRng];
       res.grad.push_back(g);
+    }
+    if (grad_f_vo != nullptr) {   // wrt the fixed effects F (likelihoods.h:5337-5367)
+      d_gradf_.alloc(n);
+      launch_grad_f(n, d_d1_.get(), gauss ? nullptr : d_dmll_.get(), d_W_.get(), gauss ? nullptr : d_vS_.get(),
+                    d_gradf_.get(), s_);
+      std::vector<double> gp(n);
+      HIP_CHECK(hipMemcpyAsync(gp.data(), d_gradf_.get(), sizeof(double) * n, hipMemcpyDeviceToHost, s_));
+      HIP_CHECK(hipStreamSynchronize(s_));
+      for (int p = 0; p < n; ++p) grad_f_vo[vo_[p]] = gp[p];
     }
     // gaussian error variance on the log scale (:5166-5200, 10586-10597, 12520-12546)
     if (gauss && want_aux_grad) {

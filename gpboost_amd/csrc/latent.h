@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <map>
 #include <memory>
+#include <stdexcept>
 #include <vector>
 
 #include "common.h"
@@ -37,6 +38,14 @@ struct IterativeConfig {
   double delta_conv_mode_finding = 1e-8;   // likelihoods.h:12723
 };
 
+// NaN / Inf in the mode finding or a CG solve of an evaluation. The reference sets the approximate
+// marginal log-likelihood to NaN and returns (likelihoods.h:2929-2933, 2997-3000), so an L-BFGS line
+// search shrinks the step (LineSearchBacktracking.h:78); REModelAMD turns this into nll = NaN when
+// its caller tolerates it and into a fatal error otherwise.
+struct LatentNan : std::runtime_error {
+  using std::runtime_error::runtime_error;
+};
+
 struct LatentResult {
   double nll = 0.;
   std::vector<double> grad;   // [d/dlog sigma1^2, d/dlog phi, (gaussian, if requested) d/dlog aux]
@@ -53,10 +62,17 @@ class LatentVecchia {
   ~LatentVecchia();
 
   void SetY(const double* y_vo);   // host, Vecchia order
+  // Posterior mode of the last evaluation (host, Vecchia order).
+  void GetMode(double* mode_vo);
+  // Fixed effects F of the location parameter (host, Vecchia order; NULL: none). The likelihood is
+  // evaluated at mode + F (InitializeLocationPar, likelihoods.h).
+  void SetOffset(const double* off_vo);
 
   // trafo = (sigma1^2, phi). aux = gaussian error variance (ignored for bernoulli_logit).
+  // grad_f_vo (host, Vecchia order, nullable; needs want_grad): gradient wrt the fixed effects F
+  // (CalcGradNegMargLikelihoodLaplaceApproxVecchia calc_F_grad, likelihoods.h:5337-5367).
   LatentResult Eval(int cov_type, int lik, const double* trafo, double aux, const IterativeConfig& cfg,
-                    bool want_grad, bool want_aux_grad);
+                    bool want_grad, bool want_aux_grad, double* grad_f_vo = nullptr);
 
   // Operator costs on the factor of the last evaluation (benchmark roofline): out[0] = ms per
   // A = B^T D^-1 B + W application, out[1] = ms per VADU preconditioner application (both on
@@ -165,6 +181,8 @@ class LatentVecchia {
   DevBuf<double> d_gsum_, d_red_, d_mom_, d_mom2_;
   bool y_set_ = false;
   bool factor_ready_ = false;
+  DevBuf<double> d_off_, d_gradf_;   // fixed effects (storage order), gradient wrt F
+  bool has_off_ = false;
 };
 
 }  // namespace gpb_amd

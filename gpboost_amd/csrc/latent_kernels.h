@@ -269,7 +269,8 @@ struct NewtonPrepArgs {
   int n, lik;
   double aux;           // gaussian error variance
   const double* y;
-  const double* loc;    // mode (+ offset)
+  const double* loc;    // mode
+  const double* offset; // fixed effects F (nullable): the likelihood is evaluated at loc + F
   const double* mode;
   const double* Dinv;
   double* d1;           // first derivative of the log-likelihood
@@ -309,6 +310,7 @@ struct ScalarArgs {
   const double* dw;     // nullable -> log/trace terms skipped
   const double* y;
   const double* mode;
+  const double* offset; // fixed effects F (nullable): log-likelihood at mode + F
   const double* vS;     // nullable -> implicit terms skipped
 };
 void launch_latent_scalars(const ScalarArgs& a, double* partials, double* out, hipStream_t s);
@@ -343,10 +345,17 @@ struct ModeDerivArgs {
   const double* Bv;
   const double* dw;
   const double* loc;
+  const double* offset;        // nullable: third derivative at loc + F
   const double* U;
   const double* P;
   double* dmll;
 };
 void launch_mode_deriv(const ModeDerivArgs& a, hipStream_t s);
+
+// Gradient of the approximate negative marginal log-likelihood wrt the fixed effects F
+// (likelihoods.h:5360-5366, no duplicate locations): out = -d1 + dmll - W .* vS (dmll / vS
+// nullable: the likelihood's information does not depend on the mode -> out = -d1).
+void launch_grad_f(int n, const double* d1, const double* dmll, const double* W, const double* vS, double* out,
+                   hipStream_t s);
 
 }  // namespace gpb_amd

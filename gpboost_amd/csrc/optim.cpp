@@ -9,6 +9,7 @@
 #include <random>
 
 #include "cov.h"
+#include "covariates.h"
 #include "re_model.h"
 
 namespace gpb_amd {
@@ -145,16 +146,6 @@ int lbfgs_minimize(LbfgsObjective& f, std::vector<double>& x, double& fx, const 
 // REModelAMD: initial values and the optimization driver
 
 namespace {
-
-// cov_fcts.h (TransformBackCovPars): phi -> range
-double range_back(int cov_type, double phi) {
-  switch (cov_type) {
-    case kMatern05: return 1. / phi;
-    case kMatern15: return std::sqrt(3.) / phi;
-    case kMatern25: return std::sqrt(5.) / phi;
-    default: return 1. / std::sqrt(phi);
-  }
-}
 
 // utils.h:189-202 CalculateMedianPartiallySortInput
 double median_partial_sort(std::vector<double>& v) {
@@ -295,6 +286,38 @@ class GaussianProfiledObjective : public LbfgsObjective {
   bool has_grad_ = false;
 };
 
+// EvalLLforLBFGSpp for the Gaussian likelihood with covariates, optimizer_coef "wls": the
+// coefficients are profiled out by GLS at every likelihood evaluation (optim_utils.h:297-313,
+// ProfileOutCoef re_model_template.h:2427-2445), then the nugget (:303-312); x as above.
+class GaussianWlsObjective : public LbfgsObjective {
+ public:
+  GaussianWlsObjective(REModelAMD* m) : m_(m) {}
+  double Eval(const std::vector<double>& x, std::vector<double>& grad, bool eval_ll, bool calc_grad,
+              bool hint_grad) override {
+    if (eval_ll || !(has_grad_ && x == x_)) {
+      const double trafo[3] = {1., std::exp(x[0]), std::exp(x[1])};
+      EvalResult r = m_->EvalTrafoWls(trafo, calc_grad || hint_grad, /*fatal_on_nan=*/false, &beta_);
+      x_ = x;
+      nll_ = r.nll;
+      sigma2_ = r.sigma2;
+      has_grad_ = calc_grad || hint_grad;
+      if (has_grad_) grad_ = r.grad;
+    }
+    if (calc_grad) grad = grad_;
+    return nll_;
+  }
+  void SetLag1ProfiledOutVariables() override { sigma2_lag1_ = sigma2_; beta_lag1_ = beta_; }
+  void ResetProfiledOutVariablesToLag1() override { sigma2_ = sigma2_lag1_; beta_ = beta_lag1_; }
+  double sigma2() const { return sigma2_; }
+  const std::vector<double>& beta() const { return beta_; }
+
+ private:
+  REModelAMD* m_;
+  std::vector<double> x_, grad_, beta_, beta_lag1_;
+  double nll_ = 0., sigma2_ = 1., sigma2_lag1_ = 1.;
+  bool has_grad_ = false;
+};
+
 // EvalLLforLBFGSpp for the latent (Laplace) models: x = log(sigma1^2, phi[, aux]).
 class LatentObjective : public LbfgsObjective {
  public:
@@ -332,20 +355,26 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects) {
   // (re_model_template.h:846-1700) -> OptimExternal "lbfgs" (optim_utils.h:561-706)
   UseDevice();
   const int n = cfg_.n;
-  std::vector<double> yv;
-  if (y != nullptr) {
-    yv.assign(y, y + n);
-    if (fixed_effects != nullptr) {
-      if (cfg_.latent && cfg_.lik != kLikGaussian)
-        Fatal("'fixed_effects' are not supported for likelihood '%s' by gpboost_amd", cfg_.likelihood.c_str());
-      for (int i = 0; i < n; ++i) yv[i] -= fixed_effects[i];
-    }
-    for (double v : yv)
-      if (std::isnan(v) || std::isinf(v)) Fatal("NaN or Inf in response variable / label ");
-    SetY(yv.data());
-  } else if (!y_set_) {
-    Fatal("response variable y has not been set");
+  if (y == nullptr) {   // the stored response (re_model_template.h:1188-1191, GetY)
+    if (y_raw_.empty()) Fatal("response variable y has not been set");
+    y = y_raw_.data();
   }
+  for (int i = 0; i < n; ++i)
+    if (std::isnan(y[i]) || std::isinf(y[i])) Fatal("NaN or Inf in response variable / label ");
+  std::vector<double> yraw(y, y + n);   // y may alias y_raw_
+  SetResponseAndOffset(yraw.data(), fixed_effects);   // Gaussian: y - F; latent: location mode + F
+  if (fixed_effects != nullptr) {   // saved for prediction (re_model_template.h:1051-1054)
+    fixed_effects_.assign(fixed_effects, fixed_effects + n);
+    has_fixed_effects_ = true;
+  }
+  std::vector<double> yv(yraw);
+  if (fixed_effects != nullptr)
+    for (int i = 0; i < n; ++i) yv[i] -= fixed_effects[i];
+  has_covariates_ = false;   // REModel::OptimCovPar (re_model.cpp:396)
+  num_covariates_ = 0;
+  X_cov_.clear();
+  coef_.clear();
+  InitializeOptimizerNames();
   EnsureStructure();
   const bool with_aux = cfg_.latent && estimate_aux_pars && !aux_pars_.empty();
   // initial values on the transformed scale (InitializeCovParsIfNotDefined re_model.cpp:1142-1164)
@@ -365,6 +394,7 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects) {
     avg /= n;
     const double sample_var = std::max((sum_sq - n * avg * avg) / (n - 1), 1e-6);
     aux_pars_[0] = sample_var / 2.;
+    aux_pars_set_ = true;   // SetAuxPars marks them set (likelihoods.h:1809): a refit continues from here
   }
   std::vector<double> start_orig;
   if (cfg_.latent) start_orig = {trafo[0], range_back(cfg_.cov_type, trafo[1])};
@@ -396,6 +426,88 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects) {
   for (double v : x)
     if (std::isnan(v) || std::isinf(v))
       Fatal("NaN or Inf occurred in covariance parameter optimization using 'lbfgs' (the reference's nelder_mead restart is not supported by gpboost_amd)");
+  cov_pars_initialized_ = true;
+  last_nll_ = fx;
+  last_cov_pars_ = cov_pars_orig_;
+}
+
+void REModelAMD::InitializeOptimizerNames() {
+  // InitializeOptimSettings (re_model_template.h:7463-7474)
+  if (optimizer_cov_.empty()) optimizer_cov_ = "lbfgs";
+  if (optimizer_coef_.empty()) optimizer_coef_ = cfg_.latent ? "lbfgs" : "wls";
+}
+
+void REModelAMD::OptimLinRegrCoefCovPar(const double* y, const double* X, int p, const double* fixed_effects) {
+  // REModel::OptimLinRegrCoefCovPar (re_model.cpp:403-469) -> REModelTemplate::OptimLinRegrCoefCovPar
+  // with covariates (re_model_template.h:846-1700): Gaussian likelihood, optimizer_cov "lbfgs",
+  // optimizer_coef "wls" (its default, :7467-7470): OptimExternal with profile_out_coef = true
+  UseDevice();
+  const int n = cfg_.n;
+  if (X == nullptr || p <= 0) {
+    OptimCovPar(y, fixed_effects);
+    return;
+  }
+  if (cfg_.latent)
+    Fatal("linear regression covariates for likelihood '%s' are not supported by gpboost_amd (Gaussian likelihood "
+          "only)", cfg_.likelihood.c_str());
+  if (p + 1 > kCovMaxCols) Fatal("at most %d covariates are supported by gpboost_amd (got %d)", kCovMaxCols - 1, p);
+  if (y == nullptr) Fatal("response variable y must be provided");   // re_model_template.h:1078
+  for (int i = 0; i < n; ++i)
+    if (std::isnan(y[i]) || std::isinf(y[i])) Fatal("NaN or Inf in response variable / label ");
+  for (size_t i = 0; i < (size_t)n * p; ++i)
+    if (std::isnan(X[i]) || std::isinf(X[i])) Fatal("NaN or Inf in covariate data");
+  InitializeOptimizerNames();
+  if (optimizer_coef_ != "wls")
+    Fatal("optimizer_coef '%s' is not supported by gpboost_amd for the Gaussian likelihood (supported: wls)",
+          optimizer_coef_.c_str());
+  std::vector<double> yraw(y, y + n);
+  y_raw_ = yraw;
+  if (fixed_effects != nullptr) {
+    fixed_effects_.assign(fixed_effects, fixed_effects + n);
+    has_fixed_effects_ = true;
+  } else {
+    has_fixed_effects_ = false;
+    fixed_effects_.clear();
+  }
+  X_cov_.assign(X, X + (size_t)n * p);
+  num_covariates_ = p;
+  has_covariates_ = true;
+  coef_std_dev_valid_ = false;
+  EnsureStructure();
+  UploadCovariates();
+  // initial values: init_cov_pars, the previous estimate, or FindInitCovPar on y - offset
+  // (re_model.cpp:407 InitializeCovParsIfNotDefined; re_model_template.h:4388-4435)
+  double trafo[3];
+  if (cov_pars_initialized_) {
+    TransformCovPars(cov_pars_orig_.data(), trafo);
+  } else {
+    std::vector<double> yv(yraw);
+    if (fixed_effects != nullptr)
+      for (int i = 0; i < n; ++i) yv[i] -= fixed_effects[i];
+    FindInitCovPar(yv.data(), trafo);
+  }
+  const std::vector<double> start_orig = {trafo[0], trafo[1] * trafo[0], range_back(cfg_.cov_type, trafo[2])};
+  if (!cov_pars_initialized_) init_used_ = start_orig;
+  if (optim_.max_iterations <= 0) {   // parameters stay; coefficients by GLS at them
+    num_it_ = 0;
+    cov_pars_orig_ = start_orig;
+    cov_pars_initialized_ = true;
+    EvalTrafoWls(trafo, false, true, nullptr);
+    last_cov_pars_ = cov_pars_orig_;
+    return;
+  }
+  std::vector<double> x = {std::log(trafo[1]), std::log(trafo[2])};
+  double fx = 0.;
+  GaussianWlsObjective obj(this);
+  num_it_ = lbfgs_minimize(obj, x, fx, optim_);
+  for (double v : x)
+    if (std::isnan(v) || std::isinf(v))
+      Fatal("NaN or Inf occurred in covariance parameter optimization using 'lbfgs' (the reference's nelder_mead restart is not supported by gpboost_amd)");
+  const double s2 = obj.sigma2();
+  cov_pars_orig_ = {s2, std::exp(x[0]) * s2, range_back(cfg_.cov_type, std::exp(x[1]))};
+  coef_ = obj.beta();
+  for (double v : coef_)
+    if (std::isnan(v) || std::isinf(v)) Fatal("NaN or Inf occurred in the linear regression coefficients");
   cov_pars_initialized_ = true;
   last_nll_ = fx;
   last_cov_pars_ = cov_pars_orig_;

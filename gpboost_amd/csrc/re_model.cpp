@@ -41,6 +41,15 @@ double range_trafo(int cov_type, double rho) {
   }
 }
 
+double range_back(int cov_type, double phi) {
+  switch (cov_type) {
+    case kMatern05: return 1. / phi;
+    case kMatern15: return std::sqrt(3.) / phi;
+    case kMatern25: return std::sqrt(5.) / phi;
+    default: return 1. / std::sqrt(phi);
+  }
+}
+
 REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : cfg_(cfg) {
   if (cfg_.n <= 0) Fatal("num_data must be > 0");
   if (cfg_.d <= 0 || cfg_.d > 3) Fatal("dim_gp_coords = %d not supported (1..3)", cfg_.d);
@@ -142,6 +151,7 @@ void REModelAMD::EnsureStructure() {
       latent_.reset(new LatentVecchia(cfg_.n, cfg_.d, cfg_.num_neighbors, d_X_.get(), nbr_.data(), stream_));
       latent_->SetShard(rank_, world_, coll_.get());   // probe columns over the ranks (§8e Option A)
       if (y_set_) latent_->SetY(y_vo_.data());
+      latent_->SetOffset(has_offset_ ? offset_vo_.data() : nullptr);
     }
     structure_built_ = true;
   }
@@ -429,8 +439,20 @@ EvalResult REModelAMD::EvalLatentTrafo(const double* trafo, bool want_grad, bool
   UseDevice();
   EnsureStructure();
   const double aux = aux_pars_.empty() ? 1. : aux_pars_[0];
-  LatentResult r = latent_->Eval(cfg_.cov_type, cfg_.lik, trafo, aux, iter, want_grad,
-                                 estimate_aux_pars && !aux_pars_.empty());
+  const bool aux_grad = estimate_aux_pars && !aux_pars_.empty();
+  LatentResult r;
+  try {
+    // fault injection for the tests: the k-th latent evaluation of this model reports NaN
+    if (const char* e = std::getenv("GPBOOST_AMD_TEST_NAN_EVAL"))
+      if (++test_nan_count_ == std::atoi(e)) throw LatentNan("NaN or Inf occurred (injected by GPBOOST_AMD_TEST_NAN_EVAL)");
+    r = latent_->Eval(cfg_.cov_type, cfg_.lik, trafo, aux, iter, want_grad, aux_grad);
+  } catch (const LatentNan& e) {
+    HIP_CHECK(hipStreamSynchronize(stream_));   // drain what the interrupted evaluation had queued
+    if (fatal_on_nan) Fatal("%s", e.what());
+    r = LatentResult();   // the line search shrinks the step (LineSearchBacktracking.h:78)
+    r.nll = std::numeric_limits<double>::quiet_NaN();
+    r.grad.assign(want_grad ? (aux_grad ? 3 : 2) : 0, std::numeric_limits<double>::quiet_NaN());
+  }
   if (fatal_on_nan && !std::isfinite(r.nll)) Fatal("NaN or Inf occurred in the approximate negative marginal log-likelihood");
   EvalResult res;
   res.nll = r.nll;

@@ -42,6 +42,8 @@ struct ModelConfig {
 
 // cov_fcts.h:438-460: range rho -> phi on the transformed scale
 double range_trafo(int cov_type, double rho);
+// cov_fcts.h TransformBackCovPars: range transform phi -> range rho
+double range_back(int cov_type, double phi);
 
 struct EvalResult {
   double nll = 0.;
@@ -63,6 +65,18 @@ class REModelAMD {
   const ModelConfig& config() const { return cfg_; }
 
   void SetY(const double* y);
+  // Stores y as the model's response (GetResponseData) and sets y - fixed_effects (nullable) as the
+  // likelihood's response.
+  void SetResponse(const double* y, const double* fixed_effects);
+  // The response (nullable: keep) and the fixed effects F of one call: Gaussian likelihood: y - F
+  // is the response; latent models: F is the offset of the location parameter (mode + F).
+  void SetResponseAndOffset(const double* y, const double* fixed_effects);
+  // REModel::CalcGradient (re_model.cpp:667-680 -> CalcGradientF re_model_template.h:3021-3043): the
+  // gradient of the (approximate marginal) negative log-likelihood wrt F for the GPBoost algorithm,
+  // written on y. Gaussian: input y (= F - label), output Psi^-1 y / sigma^2; latent models: y is
+  // output only, F = fixed_effects (CalcGradNegMargLikelihoodLaplaceApproxVecchia calc_F_grad,
+  // likelihoods.h:5337-5367).
+  void CalcGradientF(double* y, const double* fixed_effects, bool calc_cov_factor);
   bool HasY() const { return y_set_; }
 
   // cov_pars on the original scale. profile: 0 -> include_error_var gradient, 1 -> L-BFGS unit.
@@ -102,6 +116,49 @@ class REModelAMD {
   void SetOptimSettings(const double* init_cov_pars, double lr, int max_iter, double delta_rel_conv,
                         const char* optimizer, int m_lbfgs);
   void OptimCovPar(const double* y, const double* fixed_effects);
+  // GPB_OptimLinRegrCoefCovPar (re_model.cpp:403-469 -> OptimLinRegrCoefCovPar
+  // re_model_template.h:846-1700) for the Gaussian likelihood: covariance parameters by L-BFGS with
+  // the nugget profiled out and the coefficients by generalised least squares at every objective
+  // evaluation (optimizer_coef "wls", optim_utils.h:297-313; ProfileOutCoef :2427-2445).
+  // X column-major n x num_covariates.
+  void OptimLinRegrCoefCovPar(const double* y, const double* X, int num_covariates, const double* fixed_effects);
+  // GPB_GetCoef (re_model.cpp:836-870): coefficients, then (calc_std_dev) their standard deviations
+  // sqrt(diag((X^T Psi^-1 X / sigma^2)^-1)) (CalcStdDevCoef re_model_template.h:9797-9814).
+  void GetCoef(double* out, bool calc_std_dev);
+  int num_covariates() const { return num_covariates_; }
+  bool has_covariates() const { return has_covariates_; }
+  // Gaussian residual response y - offset - X beta (original order) of the stored response.
+  std::vector<double> ResidualResponse(const double* y, const double* fixed_effects) const;
+  // Adds X_pred beta to predictions of a model with covariates (X_pred column-major n_pred x p).
+  void AddLinearPredictor(const double* X_pred, int n_pred, double* mu) const;
+  // GPB_PredictREModelTrainingDataRandomEffects (re_model.cpp PredictTrainingDataRandomEffects ->
+  // re_model_template.h PredictTrainingDataRandomEffects): Gaussian likelihood: mean y - Psi^-1 y and
+  // variance sigma^2 (1 - diag(Psi^-1)); latent models: the posterior mode (no variances).
+  void PredictTrainingDataRandomEffects(const double* cov_pars, const double* y, double* out,
+                                        const double* fixed_effects, bool calc_var);
+  // GPB_SetLikelihood (re_model.cpp:142-160, re_model_template.h:558-640)
+  void SetLikelihood(const std::string& likelihood);
+  // GPB_GetResponseData / GetCovariateData / Get- / SetOffsetData (re_model_template.h:5762-5825)
+  void GetResponseData(double* y) const;
+  void GetCovariateData(double* X) const;
+  void GetOffsetData(double* fe) const;
+  void SetOffsetData(const double* fe);
+  // GPB_SetOptimConfig's init_aux_pars (re_model.cpp:264-279 -> SetAuxPars): also marks the aux
+  // parameters as given (no FindInitialAuxPars at the next fit, re_model_template.h:1186)
+  void SetInitAuxPars(const double* aux);
+  // optimizer / preconditioner names of GPB_SetOptimConfig (NULL or "": unchanged)
+  void SetOptimizerNames(const char* optimizer_cov, const char* optimizer_coef, const char* preconditioner);
+  // GPB_GetInitAuxPars (re_model.cpp:1226-1238): -1 each when none were given
+  void GetInitAuxPars(double* out) const;
+  // GPB_GetOptimizerCovPars / GetOptimizerCoef / GetCGPreconditionerType (re_model.cpp:174-208)
+  const std::string& optimizer_cov() const { return optimizer_cov_; }
+  const std::string& optimizer_coef() const { return optimizer_coef_; }
+  std::string cg_preconditioner_type() const;
+  // CanCalculateStandardErrorsCovPars (re_model_template.h:1630-1632)
+  bool CanCalculateStandardErrorsCovPars() const { return !cfg_.latent; }
+  // GLS evaluation on the transformed scale (optimizer): beta from the Gram of [X | y], then the
+  // profiled L-BFGS unit on the residuals. beta_out (nullable) receives the coefficients.
+  EvalResult EvalTrafoWls(const double* trafo, bool want_grad, bool fatal_on_nan, std::vector<double>* beta_out);
   // Standard deviations of the covariance parameters (original scale) at cov_pars_orig: square
   // roots of the diagonal of the inverse Fisher information (CalcStdDevCovPar,
   // re_model_template.h:9775-9789; dense Gaussian models only).
@@ -161,6 +218,7 @@ class REModelAMD {
   std::vector<double> y_vo_;          // host copy (Vecchia order) for the latent solver
   std::vector<double> aux_pars_;
   double last_iter_info_[4] = {0., 0., 0., 0.};
+  int test_nan_count_ = 0;   // latent evaluations seen by the GPBOOST_AMD_TEST_NAN_EVAL fault injection
 
   std::string vecchia_pred_type_ = "order_obs_first_cond_obs_only";   // re_model_template.h:6485-6490
   int num_neighbors_pred_ = 0;                                         // 2 num_neighbors (:299)
@@ -174,6 +232,31 @@ class REModelAMD {
   double last_nll_ = 0.;
   std::vector<double> last_cov_pars_;
   double last_kernel_ms_[2] = {0., 0.};
+
+  // covariates (OptimLinRegrCoefCovPar) and stored data
+  void InitializeOptimizerNames();
+  std::vector<double> Gram(const double* trafo);   // c x c Gram of [X | y - offset] (c = p + 1)
+  void UploadCovariates();
+  void EnsureTransposedLists();                     // exact Vecchia: B^T lists for the training predictions
+  void PsiInvVecchia(const double* trafo, double* yaux, double* diag);
+  std::vector<double> X_cov_;        // column-major n x p (original order)
+  std::vector<double> coef_;
+  int num_covariates_ = 0;
+  bool has_covariates_ = false;
+  bool coef_std_dev_valid_ = false;
+  std::vector<double> coef_std_dev_;
+  std::vector<double> y_raw_;        // response as last given (original order, offset not subtracted)
+  std::vector<double> fixed_effects_;
+  bool has_fixed_effects_ = false;
+  std::vector<double> offset_vo_;     // latent models: fixed effects F of the last call (Vecchia order)
+  bool has_offset_ = false;
+  void SetLatentOffset(const double* fe);
+  DevBuf<double> d_Zcov_;            // [X | y - offset], Vecchia order row-major n x c (Vecchia models)
+  DevBuf<double> d_Bf_, d_Df_, d_gram_part_, d_gram_out_;
+  DevBuf<int> d_tptr_, d_trow_, d_tslot_;
+  std::string optimizer_cov_, optimizer_coef_;
+  std::string cg_preconditioner_type_;
+  std::vector<double> init_aux_pars_;   // given by GPB_SetOptimConfig (original scale)
 
   LbfgsSettings optim_;
   std::vector<double> init_cov_pars_, cov_pars_orig_, init_used_;   // original scale

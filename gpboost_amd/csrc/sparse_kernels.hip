@@ -1131,9 +1131,19 @@ __device__ __forceinline__ double lik_dinfo(int lik, double l) {
   return -p * (1. - p) * (2. * p - 1.);
 }
 
+__global__ void __launch_bounds__(kBT) grad_f_kernel(int n, const double* __restrict__ d1,
+                                                     const double* __restrict__ dmll, const double* __restrict__ W,
+                                                     const double* __restrict__ vS, double* __restrict__ out) {
+  for (int i = blockIdx.x * kBT + threadIdx.x; i < n; i += gridDim.x * kBT) {
+    double g = -d1[i];
+    if (dmll) g += dmll[i] - W[i] * vS[i];
+    out[i] = g;
+  }
+}
+
 __global__ void __launch_bounds__(kBT) newton_prep_kernel(NewtonPrepArgs a) {
   for (int i = blockIdx.x * kBT + threadIdx.x; i < a.n; i += gridDim.x * kBT) {
-    const double l = a.loc[i];
+    const double l = a.offset ? a.loc[i] + a.offset[i] : a.loc[i];
     const double d1 = lik_d1(a.lik, a.aux, a.y[i], l);
     a.d1[i] = d1;
     // W is only refreshed when requested (information_changes_*); otherwise the stored W is used
@@ -1172,9 +1182,10 @@ __global__ void __launch_bounds__(kBT) latent_scalars_kernel(ScalarArgs a, doubl
     }
     const double Di = a.Dinv[i];
     acc[kSqQuad] += bm * Di * bm;
-    acc[kSqLogLik] += lik_loglik(a.lik, a.aux, a.y[i], mi);
+    const double li = a.offset ? mi + a.offset[i] : mi;
+    acc[kSqLogLik] += lik_loglik(a.lik, a.aux, a.y[i], li);
     acc[kSqLogDinv] += log(Di);
-    const double r = a.y[i] - mi;
+    const double r = a.y[i] - li;
     acc[kSqRss] += r * r;
     if (a.dw) {
       const double dwi = a.dw[i];
@@ -1261,7 +1272,7 @@ __global__ void __launch_bounds__(kBT) mode_deriv_kernel(ModeDerivArgs a, int sh
     const int k = i < a.m ? i : a.m;
     const int* nb = a.nbr + (size_t)i * a.m;
     const double* bv = a.Bv + (size_t)i * a.m;
-    const double dWi = lik_dinfo(a.lik, a.loc[i]);
+    const double dWi = lik_dinfo(a.lik, a.offset ? a.loc[i] + a.offset[i] : a.loc[i]);
     // pass 1: row means of z1 = U dW P and zP = (BP)^2 dW over the t probes
     // (c_var == 0 -> c = 1, CG_utils.cpp:1036-1039).
     double s1 = 0., sP = 0.;
@@ -1634,6 +1645,12 @@ void launch_grad_cols(const GradColsArgs& a, double* partials, double* out, hipS
   HIP_CHECK(hipGetLastError());
   hipLaunchKernelGGL(reduce_blocks_kernel, dim3(kGradCols * a.t), dim3(kBT), 0, s, partials, gx, kGradCols * a.t,
                      out);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_grad_f(int n, const double* d1, const double* dmll, const double* W, const double* vS, double* out,
+                   hipStream_t s) {
+  hipLaunchKernelGGL(grad_f_kernel, dim3(grid_x(n, kBT)), dim3(kBT), 0, s, n, d1, dmll, W, vS, out);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -93,3 +93,21 @@ def bench_bernoulli_y(coords: np.ndarray) -> np.ndarray:
     n = coords.shape[0]
     p = 0.5 * (1.0 + np.sin(2 * np.pi * coords[:, 0]) * np.cos(2 * np.pi * coords[:, 1]))
     return (lcg_unif(n, 0.19341) < p).astype(np.float64)
+
+
+def bench_covariates(n: int, p: int = 2) -> np.ndarray:
+    """Linear regression covariates X (n x (p + 1), column-major-friendly): an intercept column and p
+    LCG columns (c = 0.31, 0.57, ... exact arithmetic), shifted to mean ~0."""
+    cols = [np.ones(n)]
+    for k in range(p):
+        cols.append(lcg_unif(n, 0.31 + 0.26 * k) - 0.5)
+    return np.column_stack(cols)
+
+
+def bench_gaussian_y_cov(coords: np.ndarray, X: np.ndarray, beta=None) -> np.ndarray:
+    """Response with a linear predictor: X beta + iid N(0,1) (bench_gaussian_y) + a smooth spatial term."""
+    n = coords.shape[0]
+    if beta is None:
+        beta = np.array([1.0, 2.0, -1.5, 0.5, -0.25][: X.shape[1]])
+    f = np.sin(4 * coords[:, 0]) * np.cos(3 * coords[:, 1])
+    return X @ beta + f + 0.5 * bench_gaussian_y(n)

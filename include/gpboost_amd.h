@@ -16,10 +16,13 @@
  * the call and copied; output arrays are caller-allocated. A handle is not
  * thread-safe.
  *
- * Scope of this build: one GP component (num_gp = 1) with
- * cov_fct in {exponential, matern (shape 0.5/1.5/2.5), gaussian},
- * gp_approx in {"none" (dense), "vecchia"}, likelihood "gaussian".
- * Anything else fails with -1 and a message naming the unsupported option.
+ * All 29 GPB_* functions of the reference (include/LightGBM/c_api.h:1358-1786) are exported with
+ * their signatures. Scope of this build: one GP component (num_gp = 1) with
+ * cov_fct in {exponential, matern (shape 0.5/1.5/2.5), gaussian}; gp_approx "none" (dense
+ * Cholesky) and "vecchia" with likelihood "gaussian" (exact), "vecchia" with "bernoulli_logit" and
+ * "vecchia_latent" with "gaussian" (Laplace approximation, iterative methods); linear regression
+ * covariates for the Gaussian likelihood (GLS, optimizer_coef "wls"). Anything else fails with -1
+ * and a message naming the unsupported option.
  * The compute path is HIP on gfx950; there is no CPU fallback: if no GPU is
  * visible, GPB_CreateREModel fails.
  */
@@ -90,7 +93,8 @@ GPBOOST_AMD_EXPORT int GPB_REModelFree(REModelHandle handle);
  * delta_conv_mode_finding), init_aux_pars / estimate_aux_pars, and the covariance-parameter
  * optimizer fields GPB_OptimCovPar uses: init_cov_pars (original scale), lr (L-BFGS initial
  * step factor, < 0: 1), max_iter, delta_rel_conv (< 0: 1e-6), optimizer (NULL / "" / "lbfgs";
- * others fail), m_lbfgs (<= 0: 6). Covariates (num_covariates > 0, init_coef) fail. */
+ * others fail), optimizer_coef (NULL / "" / "wls"), m_lbfgs (<= 0: 6). init_coef has no effect:
+ * the "wls" update profiles the coefficients out at every evaluation. */
 GPBOOST_AMD_EXPORT int GPB_SetOptimConfig(REModelHandle handle,
     double* init_cov_pars,
     double lr,
@@ -199,6 +203,84 @@ GPBOOST_AMD_EXPORT int GPB_GetNumAuxPars(REModelHandle handle, int* num_aux_pars
 /* replaces GPB_GetAuxPars (include/LightGBM/c_api.h:1766; c_api.cpp:3098-3107): aux_pars
  * caller-allocated (num_aux_pars), out_str receives the name of the first parameter. */
 GPBOOST_AMD_EXPORT int GPB_GetAuxPars(REModelHandle handle, double* aux_pars, char* out_str);
+
+/* replaces GPB_OptimLinRegrCoefCovPar (include/LightGBM/c_api.h:1485; c_api.cpp:2843-2852 ->
+ * re_model.cpp:403-469): covariance parameters by L-BFGS (nugget profiled out) with the linear
+ * regression coefficients profiled out by generalised least squares at every objective evaluation
+ * (the reference's default optimizer_coef "wls" for the Gaussian likelihood,
+ * re_model_template.h:7467-7470, optim_utils.h:297-313). covariate_data column-major
+ * num_data x num_covariates (num_covariates + 1 <= 32); fixed_effects: an offset (nullable).
+ * Gaussian likelihood only; results through GPB_GetCovPar / GPB_GetCoef. */
+GPBOOST_AMD_EXPORT int GPB_OptimLinRegrCoefCovPar(REModelHandle handle,
+    const double* y_data,
+    const double* covariate_data,
+    int num_covariates,
+    const double* fixed_effects);
+
+/* replaces GPB_CanCalculateStandardErrorsCovPars (include/LightGBM/c_api.h:1515; c_api.cpp:2873-2879;
+ * re_model_template.h:1630-1632): out[0] = 1 for Gaussian-likelihood models, 0 for latent ones. */
+GPBOOST_AMD_EXPORT int GPB_CanCalculateStandardErrorsCovPars(REModelHandle handle, int* out);
+
+/* replaces GPB_GetCoef (include/LightGBM/c_api.h:1548; re_model.cpp:836-870): the coefficients
+ * estimated by GPB_OptimLinRegrCoefCovPar in optim_coef[0, p); calc_std_dev also writes their
+ * standard deviations sqrt(diag((X^T Psi^-1 X / sigma^2)^-1)) to optim_coef[p, 2p)
+ * (CalcStdDevCoef, re_model_template.h:9797-9814). */
+GPBOOST_AMD_EXPORT int GPB_GetCoef(REModelHandle handle, double* optim_coef, bool calc_std_dev);
+
+/* replaces GPB_PredictREModelTrainingDataRandomEffects (include/LightGBM/c_api.h:1645;
+ * re_model.cpp PredictTrainingDataRandomEffects): cov_pars_pred on the original scale (NULL: the
+ * estimated / last evaluated ones), y_obs NULL: the stored response. Gaussian likelihood (dense and
+ * Vecchia): out[0, n) = y - Psi^-1 y (minus X beta and the offset first), with calc_var
+ * out[n, 2n) = sigma^2 (1 - diag(Psi^-1)); latent models: out[0, n) = the posterior mode
+ * (calc_var fails). */
+GPBOOST_AMD_EXPORT int GPB_PredictREModelTrainingDataRandomEffects(REModelHandle handle,
+    const double* cov_pars_pred,
+    const double* y_obs,
+    double* out_predict,
+    const double* fixed_effects,
+    bool calc_var);
+
+/* replace GPB_GetOptimizerCovPars / GPB_GetOptimizerCoef / GPB_GetCGPreconditionerType
+ * (include/LightGBM/c_api.h:1670, 1681, 1692; re_model.cpp:174-208): the optimizer names ("" until
+ * set or fitted, then "lbfgs" / "wls" for the Gaussian, "lbfgs" for latent models) and the CG
+ * preconditioner ("vadu" for latent Vecchia models, "" otherwise). out_str must hold the name;
+ * num_char receives its length + 1. */
+GPBOOST_AMD_EXPORT int GPB_GetOptimizerCovPars(REModelHandle handle, char* out_str, int* num_char);
+GPBOOST_AMD_EXPORT int GPB_GetOptimizerCoef(REModelHandle handle, char* out_str, int* num_char);
+GPBOOST_AMD_EXPORT int GPB_GetCGPreconditionerType(REModelHandle handle, char* out_str, int* num_char);
+
+/* replace GPB_GetNumCGSteps / GPB_GetNumCGStepsTridiag (include/LightGBM/c_api.h:1702, 1711): as in
+ * the reference (re_model_template.h:527-552) they are defined for models with several grouped
+ * random effects only and fail with the reference's message here. */
+GPBOOST_AMD_EXPORT int GPB_GetNumCGSteps(REModelHandle handle, int* num_cg_steps);
+GPBOOST_AMD_EXPORT int GPB_GetNumCGStepsTridiag(REModelHandle handle, int* num_cg_steps);
+
+/* replaces GPB_SetLikelihood (include/LightGBM/c_api.h:1720; re_model.cpp:142-160): switches between
+ * "gaussian" and "bernoulli_logit" before a model is estimated (Vecchia: exact <-> Laplace). */
+GPBOOST_AMD_EXPORT int GPB_SetLikelihood(REModelHandle handle, const char* likelihood);
+
+/* replace GPB_GetResponseData / GPB_GetCovariateData / GPB_GetOffsetData / GPB_SetOffsetData
+ * (include/LightGBM/c_api.h:1729, 1738, 1747, 1756; re_model_template.h:5762-5825): the stored
+ * response (original order, n), covariates (column-major n x p) and offset (n). */
+GPBOOST_AMD_EXPORT int GPB_GetResponseData(REModelHandle handle, double* response_data);
+GPBOOST_AMD_EXPORT int GPB_GetCovariateData(REModelHandle handle, double* covariate_data);
+GPBOOST_AMD_EXPORT int GPB_GetOffsetData(REModelHandle handle, double* fixed_effects);
+GPBOOST_AMD_EXPORT int GPB_SetOffsetData(REModelHandle handle, const double* fixed_effects);
+
+/* replaces GPB_GetInitAuxPars (include/LightGBM/c_api.h:1785; re_model.cpp:1226-1238): the aux
+ * parameters given by GPB_SetOptimConfig's init_aux_pars, -1 each when none were given. */
+GPBOOST_AMD_EXPORT int GPB_GetInitAuxPars(REModelHandle handle, double* aux_pars);
+
+/* EXTENSION (the reference has it as a C++ method only): REModel::CalcGradient (re_model.cpp:667-680
+ * -> CalcGradientF re_model_template.h:3021-3043), what the GPBoost boosting objective calls after
+ * GPB_OptimCovPar(handle, NULL, score) (regression_objective.hpp:164-179): the gradient of the
+ * (approximate marginal) negative log-likelihood wrt the fixed effects F at the current covariance
+ * parameters, written on y (length n, original order). Gaussian likelihood: input y = F - label,
+ * output Psi^-1 y / sigma^2; latent models (Laplace): y is output only and F = fixed_effects, output
+ * -dlog p(y|mode+F)/dF + the stochastic implicit-derivative terms (likelihoods.h:5337-5367). The
+ * factor (and the mode) are always recomputed; calc_cov_factor is accepted for the signature. */
+GPBOOST_AMD_EXPORT int GPB_CalcGradientF(REModelHandle handle, double* y, const double* fixed_effects,
+    bool calc_cov_factor);
 
 /* ---------------------------------------------------------------- EXTENSION: introspection */
 

@@ -108,6 +108,21 @@ int main(int argc, char** argv) {
   std::vector<double> coords((size_t)n * d), y(n);
   if (std::fread(coords.data(), 8, coords.size(), f) != coords.size()) return 2;
   if (std::fread(y.data(), 8, y.size(), f) != y.size()) return 2;
+  // optional linear regression covariates: int32 p, double X[n*p] (column-major)
+  int32_t p_cov = 0;
+  std::vector<double> Xcov;
+  if (std::fread(&p_cov, 4, 1, f) == 1 && p_cov > 0) {
+    Xcov.resize((size_t)n * p_cov);
+    if (std::fread(Xcov.data(), 8, Xcov.size(), f) != Xcov.size()) return 2;
+  }
+  // optional fixed effects F (offset of the location parameter): int32 1, double F[n]
+  int32_t has_fe = 0;
+  std::vector<double> fe;
+  if (std::fread(&has_fe, 4, 1, f) == 1 && has_fe == 1) {
+    fe.resize(n);
+    if (std::fread(fe.data(), 8, fe.size(), f) != fe.size()) return 2;
+  }
+  const double* fe_ptr = fe.empty() ? nullptr : fe.data();
   std::fclose(f);
 
   const std::string cov_fct = get(args, "cov_fct", "exponential");
@@ -184,13 +199,16 @@ int main(int argc, char** argv) {
       vec_t io = Eigen::Map<const vec_t>(iv.data(), (int)iv.size());
       m->TransformCovPars(io, cp);
     } else {
-      m->FindInitCovPar(y.data(), nullptr, cp.data());
+      m->FindInitCovPar(y.data(), fe_ptr, cp.data());
     }
     vec_t init_orig;
     m->TransformBackCovPars(cp, init_orig);
     int num_it = 0;
+    std::vector<double> coef(std::max(p_cov, 1), 0.);
     auto a = std::chrono::steady_clock::now();
-    m->OptimLinRegrCoefCovPar(y.data(), nullptr, 0, cp.data(), nullptr, num_it, cp.data(), nullptr, nullptr,
+    // REModel::OptimCovPar / OptimLinRegrCoefCovPar (re_model.cpp:339-469)
+    m->OptimLinRegrCoefCovPar(y.data(), p_cov > 0 ? Xcov.data() : nullptr, p_cov, cp.data(),
+                              p_cov > 0 ? coef.data() : nullptr, num_it, cp.data(), nullptr, fe_ptr,
                               true, false, false, false, false);
     auto b = std::chrono::steady_clock::now();
     vec_t fit_orig;
@@ -198,6 +216,16 @@ int main(int argc, char** argv) {
     std::printf("{\n\"n\": %d, \"d\": %d,\n", n, d);
     print_vec("init_cov_pars", init_orig.data(), (int)init_orig.size());
     print_vec("cov_pars", fit_orig.data(), (int)fit_orig.size());
+    if (p_cov > 0) {
+      print_vec("coef", coef.data(), p_cov);
+      std::vector<double> sd_coef(p_cov), sd_cov(m->num_cov_par_);
+      m->CalculateStandardErrorsCoefs(cp.data(), sd_coef.data());   // GetCoef(calc_std_dev), re_model.cpp:836-870
+      print_vec("coef_std_dev", sd_coef.data(), p_cov);
+      if (gp_approx == "none") {
+        m->CalculateStandardErrorsCovPars(cp.data(), sd_cov.data());
+        print_vec("cov_pars_std_dev", sd_cov.data(), (int)sd_cov.size());
+      }
+    }
     if (m->NumAuxPars() > 0) print_vec("aux_pars", m->GetAuxPars(), m->NumAuxPars());
     std::printf("\"nll\": %.17g,\n", m->neg_log_likelihood_);
     std::printf("\"num_it\": %d, \"num_ll_evaluations\": %d,\n", num_it, m->num_ll_evaluations_);
@@ -209,6 +237,30 @@ int main(int argc, char** argv) {
   vec_t orig = Eigen::Map<const vec_t>(cov_pars_orig.data(), (int)cov_pars_orig.size());
   vec_t trafo;
   m->TransformCovPars(orig, trafo);
+
+  if (mode == "grad_f") {
+    // REModel::CalcGradient -> CalcGradientF (re_model_template.h:3021-3043) at cov_pars: Gaussian:
+    // input y, output Psi^-1 y / sigma2; non-Gaussian: the gradient wrt F at the mode (F = fe)
+    if (!gauss)
+      for (const auto& c : m->unique_clusters_) m->likelihood_[c]->InitializeModeAvec();
+    std::vector<double> g(y);
+    m->CalcGradientF(g.data(), fe_ptr, true, trafo);
+    std::printf("{\n\"n\": %d, \"d\": %d,\n", n, d);
+    print_vec("grad_f", g.data(), n);
+    std::printf("\"ok\": true\n}\n");
+    return 0;
+  }
+
+  if (mode == "pred_train") {
+    // GPB_PredictREModelTrainingDataRandomEffects at cov_pars (re_model.cpp -> PredictTrainingDataRandomEffects)
+    std::vector<double> out((size_t)2 * n, 0.);
+    m->PredictTrainingDataRandomEffects(trafo.data(), nullptr, y.data(), out.data(), true, nullptr, gauss);
+    std::printf("{\n\"n\": %d, \"d\": %d,\n", n, d);
+    print_vec("mean", out.data(), n);
+    if (gauss) print_vec("var", out.data() + n, n);
+    std::printf("\"ok\": true\n}\n");
+    return 0;
+  }
 
   if (mode == "stddev") {
     // GPB_GetCovPar(calc_std_dev = true) at cov_pars: CalculateStandardErrorsCovPars
@@ -231,7 +283,7 @@ int main(int argc, char** argv) {
       for (const auto& c : m->unique_clusters_) m->likelihood_[c]->InitializeModeAvec();
     }
     auto a = std::chrono::steady_clock::now();
-    m->CalcCovFactorOrModeAndNegLL(cp, nullptr);
+    m->CalcCovFactorOrModeAndNegLL(cp, fe_ptr);
     nll = m->neg_log_likelihood_;
     if (gauss && mode == "lbfgs") {
       sigma2 = m->ProfileOutSigma2();
@@ -243,7 +295,7 @@ int main(int argc, char** argv) {
       m->CalcGradPars(cp, cp[0], true, false, grad, gb, true, false, nullptr, false);
     }
     else {
-      m->CalcGradPars(cp, 1., true, false, grad, gb, false, false, nullptr, false);
+      m->CalcGradPars(cp, 1., true, false, grad, gb, false, false, fe_ptr, false);
     }
     auto b = std::chrono::steady_clock::now();
     times.push_back(std::chrono::duration<double>(b - a).count());

@@ -28,12 +28,21 @@ from gpboost_amd import synthetic  # noqa: E402
 HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
 
 
-def run_ref(coords: np.ndarray, y: np.ndarray, **opts) -> dict:
+def run_ref(coords: np.ndarray, y: np.ndarray, X: np.ndarray | None = None, fe: np.ndarray | None = None,
+            **opts) -> dict:
     n, d = coords.shape
     with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
         f.write(np.array([n, d], dtype=np.int32).tobytes())
         f.write(np.asfortranarray(coords).T.astype(np.float64).tobytes())  # column-major
         f.write(y.astype(np.float64).tobytes())
+        if X is not None:   # optional covariates: int32 p, column-major n x p
+            f.write(np.array([X.shape[1]], dtype=np.int32).tobytes())
+            f.write(np.ascontiguousarray(X.T).astype(np.float64).tobytes())
+        elif fe is not None:
+            f.write(np.array([0], dtype=np.int32).tobytes())
+        if fe is not None:   # optional fixed effects: int32 1, F[n]
+            f.write(np.array([1], dtype=np.int32).tobytes())
+            f.write(np.asarray(fe, dtype=np.float64).tobytes())
         path = f.name
     try:
         args = [HARNESS, path] + [f"{k}={v}" for k, v in opts.items()]

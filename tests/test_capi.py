@@ -33,6 +33,29 @@ def test_header_declares_reference_entry_points():
         assert s in syms
 
 
+def _declared_arity():
+    txt = open(HEADER).read()
+    out = {}
+    for m in re.finditer(r"GPBOOST_AMD_EXPORT\s+[\w\s\*]+?\b((?:GPB|LGBM)_\w+)\s*\(([^;]*?)\)\s*;", txt, re.S):
+        args = [a for a in m.group(2).split(",") if a.strip() and a.strip() != "void"]
+        out[m.group(1)] = len(args)
+    return out
+
+
+def test_all_reference_entry_points_declared_and_exported(lib):
+    """The drop-in boundary covers every GPB_* function of the reference C API
+    (tests/golden/reference_c_api.json, recorded from include/LightGBM/c_api.h by
+    tests/golden/make_capi_names.py) with the same parameter count."""
+    import json
+    ref = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_c_api.json")))["functions"]
+    assert len(ref) == 29
+    arity = _declared_arity()
+    for f in ref:
+        assert f["name"] in arity, f"{f['name']} (c_api.h:{f['line']}) not declared in include/gpboost_amd.h"
+        assert arity[f["name"]] == f["nargs"], (f["name"], arity[f["name"]], f["nargs"])
+        assert hasattr(lib, f["name"]), f"{f['name']} not exported"
+
+
 def test_library_exports_every_declared_symbol(lib):
     missing = [s for s in _declared_symbols() if not hasattr(lib, s)]
     assert not missing, missing

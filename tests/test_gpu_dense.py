@@ -93,3 +93,31 @@ def test_dense_5000_gradient_finite_differences():
     lt0 = np.array([np.log(0.1), np.log(10.0), np.log(10.0)])
     fd = [(nll_at(lt0 + h * e) - nll_at(lt0 - h * e)) / (2 * h) for e in np.eye(3)]
     np.testing.assert_allclose(g, fd, rtol=1e-5, atol=1e-3)
+
+
+def _dense_big_cases():
+    import json
+    import os
+    p = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_dense_big.json")
+    return json.load(open(p)) if os.path.exists(p) else {}
+
+
+@pytest.mark.parametrize("name", sorted(_dense_big_cases()))
+def test_dense_big_matches_reference(name):
+    """Parity where the fast dense paths run (BASELINE config 2): at n = 8192 / 20000 the trailing
+    updates have >= 512 output tiles of 128, so gemm_f64_big_kernel and the two-stream lookahead
+    POTRF / TRTRI / LAUUM are what is checked against the reference (tests/golden/
+    make_golden_dense_big.py), in both evaluation modes, at the north-star 1e-6."""
+    from gpboost_amd import GPModel, synthetic
+    case = _dense_big_cases()[name]
+    n = case["n"]
+    X = synthetic.bench_coords(n)
+    Y = synthetic.bench_gaussian_y(n)
+    gm = GPModel(gp_coords=X, cov_function="exponential", gp_approx="none")
+    nll, g, _ = gm.neg_log_likelihood_and_grad(case["cov_pars"], Y)
+    assert abs(nll - case["nll"]) <= RTOL * abs(case["nll"]), (nll, case["nll"])
+    assert _close(g, case["grad"]), (g, case["grad"])
+    nll1, g1, s2 = gm.neg_log_likelihood_and_grad(case["cov_pars"], None, profile_sigma2=True)
+    assert abs(nll1 - case["lbfgs_nll"]) <= RTOL * abs(case["lbfgs_nll"]), (nll1, case["lbfgs_nll"])
+    assert _close(g1, case["lbfgs_grad"]), (g1, case["lbfgs_grad"])
+    assert abs(s2 - case["lbfgs_sigma2"]) <= RTOL * case["lbfgs_sigma2"]

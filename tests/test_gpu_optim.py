@@ -132,8 +132,11 @@ def test_fit_errors():
     gm = GPModel(gp_coords=X, cov_function="exponential")
     with pytest.raises((GPBoostError, ValueError), match="NaN or Inf"):
         gm.fit(np.where(np.arange(100) == 3, np.nan, Y))
-    with pytest.raises(GPBoostError, match="out of scope"):
-        gm.fit(Y, X=np.ones((100, 1)))
+    Xb = synthetic.bench_coords(300)
+    gl = GPModel(gp_coords=Xb, cov_function="exponential", gp_approx="vecchia", likelihood="bernoulli_logit",
+                 num_neighbors=10)
+    with pytest.raises(GPBoostError, match="not supported"):   # covariates: Gaussian likelihood only
+        gl.fit(synthetic.bench_bernoulli_y(Xb), X=np.ones((300, 1)))
 
 
 @pytest.mark.parametrize("name", ["sd_rtest_exponential", "sd_rtest_matern15", "sd_rtest_matern25", "sd_rtest_gaussian",
@@ -172,3 +175,23 @@ def test_fit_maxit_zero_keeps_initial_values(golden_fit):
     gm.fit(Y, params={"maxit": 0})
     assert gm.get_num_optim_iter() == 0
     np.testing.assert_allclose(gm.get_cov_pars(), case["init_cov_pars"], rtol=1e-12)
+
+
+def test_latent_fit_recovers_from_nan_trial(golden_fit, monkeypatch):
+    """A NaN in a line-search trial of a latent fit shrinks the step instead of failing the fit
+    (likelihoods.h:2929-2933 set the marginal likelihood to NaN, LineSearchBacktracking.h:78
+    halves the step on fx != fx). Fault injection: the 2nd latent evaluation (the first trial of
+    the first line search) reports NaN; the fit must still reach the reference optimum."""
+    case = golden_fit["latent500_bernoulli_m20"]
+    X, Y = _data(case)
+    gm = _model(case, X)
+    monkeypatch.setenv("GPBOOST_AMD_TEST_NAN_EVAL", "2")
+    gm.fit(Y, params=_params(case))
+    monkeypatch.delenv("GPBOOST_AMD_TEST_NAN_EVAL")
+    np.testing.assert_allclose(gm.get_cov_pars(), case["cov_pars"], rtol=2e-2)
+    assert abs(gm.get_current_neg_log_likelihood() - case["nll"]) <= 1e-5 * abs(case["nll"])
+    # without the tolerance of the optimizer the same NaN is an error (GPB_EvalNegLogLikelihood)
+    g2 = _model(case, X)
+    monkeypatch.setenv("GPBOOST_AMD_TEST_NAN_EVAL", "1")
+    with pytest.raises(GPBoostError, match="NaN or Inf"):
+        g2.neg_log_likelihood(case["cov_pars"], Y)

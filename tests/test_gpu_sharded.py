@@ -179,3 +179,18 @@ def test_latent_shards_need_a_probe_each():
     from gpboost_amd import GPBoostError
     with pytest.raises(GPBoostError, match="at least one probe column"):
         gm.neg_log_likelihood(case["cov_pars"], y)
+
+
+def test_host_reduce_callback_error_is_raised():
+    """An exception inside the host all-reduce callback is not swallowed by ctypes: the buffer is
+    poisoned (NaN) so the library stops, and the Python call re-raises the callback's error."""
+    from gpboost_amd import GPBoostError, GPModel, synthetic
+    X = synthetic.bench_coords(1000)
+    Y = synthetic.bench_gaussian_y(1000)
+    gm = GPModel(gp_coords=X, cov_function="exponential", gp_approx="vecchia", num_neighbors=10)
+
+    def bad(_a):
+        raise RuntimeError("transport down")
+    gm.set_distributed_host(0, 1, bad)
+    with pytest.raises(GPBoostError, match="transport down"):
+        gm.neg_log_likelihood_and_grad([0.1, 1.0, 0.1], Y)
