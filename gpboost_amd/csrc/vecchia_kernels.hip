@@ -32,6 +32,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <type_traits>
 
 #include "common.h"
 #include "cov.h"
@@ -86,6 +87,35 @@ __device__ __forceinline__ double swap_sum(double v) {
 }
 #endif
 
+// ---- lane broadcasts without LDS (Gauss-Jordan pivot column)
+template <int B, int E, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+// Value of lane L of each 16-lane DPP row, broadcast to that whole row (row_newbcast).
+template <int L>
+__device__ __forceinline__ double row_bcast(double v) {
+  return dpp_f64<0x150 + L>(v);
+}
+
+// 32-lane groups: lo = the value of group lane CP, hi = that of group lane 16 + CP, in every lane
+// of the group. One row_newbcast per dword, then the gfx950 row-swap permute of the broadcast with
+// itself: its first output holds the even DPP row's value in both rows of each pair, its second
+// the odd row's (V_PERMLANE16_SWAP exchanges rows 1/3 of VDST with rows 0/2 of VSRC).
+template <int CP>
+__device__ __forceinline__ void group_bcast_pair(double v, double& lo, double& hi) {
+  const double b = row_bcast<CP>(v);
+  const unsigned bl = __double2loint(b), bh = __double2hiint(b);
+  const auto pl = __builtin_amdgcn_permlane16_swap(bl, bl, false, false);
+  const auto ph = __builtin_amdgcn_permlane16_swap(bh, bh, false, false);
+  lo = __hiloint2double(ph[0], pl[0]);
+  hi = __hiloint2double(ph[1], pl[1]);
+}
+
 template <int K>
 __device__ __forceinline__ double group_sum(double v) {
   if constexpr (K < 16) {   // sub-row groups (the two-rows-per-lane variant): plain shuffles
@@ -127,8 +157,12 @@ __device__ unsigned long long g_rows_prof[8];
 
 // MK <= K: matrix rows (= elimination steps); lanes r >= MK of a group only take part in the
 // wave-level operations (m <= 30 with K = 32: the two identity-padding steps are not run).
-template <int K, int COV, bool PROF = false, int MK = K>
+// DPPBC (K = 16 / 32, A/B form, see rows_dpp): the Gauss-Jordan steps broadcast the pivot column
+// by DPP row broadcasts and row-swap permutes (VALU) instead of LDS slots. Same values in the same
+// FMA order: bitwise identical results.
+template <int K, int COV, bool PROF = false, int MK = K, bool DPPBC = false>
 __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(VecchiaRowsArgs a) {
+  static_assert(!DPPBC || K == 16 || K == 32, "DPP broadcasts need 16- or 32-lane groups");
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int BT = block_threads<K>();
   constexpr int G = 64 / K;                 // rows per wave
@@ -236,6 +270,56 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
 #pragma unroll
     for (int c = 0; c < MK; ++c) row[c] = (c <= r) ? Cp[packed(r, c)] : Cp[packed(c, r)];
     double aug1 = cvec, aug2 = ynb;
+    if constexpr (DPPBC) {
+      // lane c holds row c, so M[c][j] = lane c's row[j]: broadcast lane c's register
+      auto bc = [&](auto CPc, double v, double& lo, double& hi) {
+        constexpr int cp = decltype(CPc)::value;
+        if constexpr (K == 32) {
+          group_bcast_pair<cp>(v, lo, hi);
+        } else {
+          lo = row_bcast<cp>(v);
+          hi = 0.;
+        }
+      };
+      static_for<0, MK>([&](auto J) {
+        constexpr int j = decltype(J)::value;
+        constexpr int jp = j & 15;
+        double plo, phi_, a1lo, a1hi, a2lo, a2hi;
+        bc(std::integral_constant<int, jp>{}, row[j], plo, phi_);
+        bc(std::integral_constant<int, jp>{}, aug1, a1lo, a1hi);
+        bc(std::integral_constant<int, jp>{}, aug2, a2lo, a2hi);
+        const double piv = j < 16 ? plo : phi_;
+        const double a1j = j < 16 ? a1lo : a1hi;
+        const double a2j = j < 16 ? a2lo : a2hi;
+        double rinv = __builtin_amdgcn_rcp(piv);
+        rinv = fma(rinv, fma(-piv, rinv, 1.), rinv);
+        rinv = fma(rinv, fma(-piv, rinv, 1.), rinv);
+        const double q = row[j] * rinv;
+        const double f = (r == j) ? 0. : q;
+        aug1 = fma(-f, a1j, aug1);
+        aug2 = fma(-f, a2j, aug2);
+        // columns c > j in pairs (cp, cp + 16) sharing one broadcast sequence
+        static_for<0, 16>([&](auto CP) {
+          constexpr int cp = decltype(CP)::value;
+          constexpr bool need_lo = cp > j && cp < MK;
+          constexpr bool need_hi = K == 32 && cp + 16 > j && cp + 16 < MK;
+          if constexpr (need_lo || need_hi) {
+            double vlo, vhi;
+            if constexpr (cp == jp) {   // the pivot's broadcast already holds this pair
+              vlo = plo;
+              vhi = phi_;
+            } else {
+              bc(CP, row[j], vlo, vhi);
+            }
+            if constexpr (need_lo) row[cp] = fma(-f, vlo, row[cp]);
+            if constexpr (need_hi) row[cp + 16] = fma(-f, vhi, row[cp + 16]);
+          }
+        });
+#pragma unroll
+        for (int c = j + 1; c < MK; ++c) asm volatile("" : "+v"(row[c]));
+        asm volatile("" : "+v"(aug1), "+v"(aug2));
+      });
+    } else {
 #pragma unroll
     for (int j = 0; j < MK; ++j) {
       compiler_fence();
@@ -259,6 +343,7 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
 #pragma unroll
       for (int c = j + 1; c < MK; ++c) asm volatile("" : "+v"(row[c]));
       asm volatile("" : "+v"(aug1), "+v"(aug2));
+    }
     }
     double mydiag = row[0];
 #pragma unroll
@@ -614,6 +699,14 @@ bool use_v4(int K) {
   return K <= 32 && v4;
 }
 
+// Gauss-Jordan broadcasts: LDS slots (default) or DPP / row-swap permutes (GPBOOST_AMD_ROWS_DPP=1,
+// A/B; read at every launch so a test can compare both forms in one process). Measured on MI355X
+// (n = 100k, m = 30, profiles/r03/rows_dpp_ab_r03.log): DPP 0.604 ms vs LDS 0.378 ms per launch —
+// 223 instead of 249 VGPRs, but every step's broadcast chain (row_newbcast -> permlane16_swap ->
+// reciprocal -> FMAs) is a dependent VALU sequence with DPP hazard waits, while the LDS form issues
+// the step's column reads as one burst whose latencies overlap.
+bool rows_dpp() { return std::getenv("GPBOOST_AMD_ROWS_DPP") != nullptr; }
+
 template <int K>
 int rows_per_block() { return use_v4(K) ? 64 / (K / 2) : (block_threads<K>() / 64) * (64 / K); }
 
@@ -641,9 +734,20 @@ void launch_k(const VecchiaRowsArgs& a, hipStream_t s) {
   size_t lds = (size_t)rpb * group_lds_doubles<K>() * sizeof(double);
   if (lds < red) lds = red;
   static const bool prof = std::getenv("GPBOOST_AMD_ROWS_PROF") != nullptr;
+  const bool dpp = rows_dpp();
   if constexpr (K == 32) {
     if (!prof && a.m <= 30) {   // the headline configuration (m = 30): 30 elimination steps
-      hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, 30>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
+      if (dpp)
+        hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, 30, true>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
+      else
+        hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, 30>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
+      HIP_CHECK(hipGetLastError());
+      return;
+    }
+  }
+  if constexpr (K == 16 || K == 32) {
+    if (!prof && dpp) {
+      hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, K, true>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
       HIP_CHECK(hipGetLastError());
       return;
     }

@@ -244,3 +244,22 @@ def test_baseline_size_matches_reference():
     assert abs(nll - case["nll"]) <= 1e-10 * abs(case["nll"])
     assert _close(g, case["grad"], rtol=1e-8)
     assert abs(s2 - case["sigma2"]) <= 1e-10 * case["sigma2"]
+
+
+@pytest.mark.parametrize("m", [10, 16, 20, 30, 31])
+def test_rows_dpp_broadcast_bitwise_equals_lds_form(m, monkeypatch):
+    """The row kernel's Gauss-Jordan broadcasts by LDS slots (default) and by DPP row broadcasts +
+    row-swap permutes (GPBOOST_AMD_ROWS_DPP=1, A/B form) move the same values into the same FMAs:
+    the evaluations must agree bit for bit (K = 16 and 32 lane groups, 30 and 32 elimination steps)."""
+    from gpboost_amd import GPModel, synthetic
+    n = 20000
+    X = synthetic.bench_coords(n)
+    Y = synthetic.bench_gaussian_y(n)
+    gm = GPModel(gp_coords=X, cov_function="matern", cov_fct_shape=1.5, gp_approx="vecchia", num_neighbors=m,
+                 vecchia_ordering="random", seed=0)
+    monkeypatch.delenv("GPBOOST_AMD_ROWS_DPP", raising=False)
+    a = gm.neg_log_likelihood_and_grad([0.1, 1.0, 0.1], Y, profile_sigma2=True)
+    monkeypatch.setenv("GPBOOST_AMD_ROWS_DPP", "1")
+    b = gm.neg_log_likelihood_and_grad([0.1, 1.0, 0.1], None, profile_sigma2=True)
+    assert a[0] == b[0]
+    assert np.array_equal(a[1], b[1])
