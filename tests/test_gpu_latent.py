@@ -40,15 +40,6 @@ def _check(nll, g, ref_nll, ref_g, rtol=RTOL, atol_g=0.):
     np.testing.assert_allclose(g, ref_g, rtol=rtol, atol=max(rtol * np.abs(ref_g).max(), atol_g))
 
 
-def _oracle_for_case(case):
-    X, y = latent_case_data(case)
-    ct = O.cov_code(case["cov_fct"], case["shape"])
-    perm, xv, nb = O.vecchia_setup(X, case["num_neighbors"], 0, True)
-    return O.latent_iterative(xv, y[perm], nb, ct, O.transform_latent(ct, case["cov_pars"]), case["likelihood"],
-                              case["aux"] or 1.0, t=case["num_rand_vec_trace"], seed=case["seed_rand_vec_trace"],
-                              cg_delta_conv=case["cg_delta_conv"])
-
-
 @pytest.mark.parametrize("name", ["gauss_m30_exp_tight", "gauss_m30_exp_default", "gauss_m20_matern15_t20",
                                   "bern_m30_exp_tight", "bern_m30_exp_default", "bern_m10_gaussian_t30",
                                   "bern_m16_matern25", "rtest_bern_m30_exp"])
@@ -59,12 +50,15 @@ def test_latent_matches_reference(golden_latent, name):
     nll = gm.neg_log_likelihood(case["cov_pars"], y)
     assert abs(nll - case["nll"]) <= RTOL * abs(case["nll"])
     nll2, g, _ = gm.neg_log_likelihood_and_grad(case["cov_pars"], None)
-    # Conditioning-limited cases (no nugget + smooth kernel: kappa(C_i) ~ 1e8+) carry
-    # implementation noise in the gradient, measured here as the spread between two
-    # independent CPU implementations (reference vs oracle); the GPU must stay within
-    # 10x that spread, or 1e-6 relative, whichever is larger.
-    spread = np.abs(_oracle_for_case(case)["grad"] - np.asarray(case["grad"])).max()
-    _check(nll2, g, case["nll"], case["grad"], atol_g=10 * spread)
+    _check(nll2, g, case["nll"], case["grad"], atol_g=COND_LIMITED_ATOL.get(name, 0.))
+
+
+# Conditioning-limited case (Gaussian kernel, no nugget: kappa(C_i) ~ 1e8+): its gradient carries
+# implementation noise, measured ONCE as the largest gap between two independent CPU implementations
+# (the reference and the oracle restatement, max |g_oracle - g_ref| = 1.55e-4 at n = 2000); the GPU
+# must stay within 10x that fixed value. Every other case is held to 1e-6 relative (their measured
+# oracle-reference gaps are 1e-14 .. 9e-5 absolute, all below 1e-6 relative).
+COND_LIMITED_ATOL = {"bern_m10_gaussian_t30": 1.6e-3}
 
 
 def test_latent_factor_matches_oracle():
@@ -258,27 +252,48 @@ def test_baseline_size_matches_reference():
     _check(nll, g, case["nll"], case["grad"])
 
 
-def test_baseline_size_bernoulli_matches_reference():
-    """BASELINE config 5 (bernoulli_logit, Laplace + PCG / SLQ, n = 100k, m = 30, default tolerance)
-    against the reference run here (tests/golden/make_golden_100k.py). nll at the 1e-6 north-star
-    tolerance (observed 4e-8). The gradient is rounding-limited at this tolerance: six Newton steps
-    each solved by PCG to an absolute residual of 1e-2 flip their iteration counts by one under any
-    reordering of the sums — algebraically equivalent preconditioner plans of THIS implementation
-    spread the gradient by 1.5e-6 relative (scripts/gpu_latent_sens_bern.sh) — so it is checked at
-    2e-5 (observed 7.5e-6 vs the reference)."""
+def _golden100k():
     import json
     import os
-
-    from gpboost_amd import synthetic
     with open(os.path.join(os.path.dirname(__file__), "golden", "golden_100k.json")) as f:
-        case = json.load(f)["bernoulli"]
+        return json.load(f)
+
+
+def test_baseline_size_bernoulli_tight_matches_reference():
+    """BASELINE config 5 (bernoulli_logit, Laplace + PCG / SLQ, n = 100k, m = 30) with the mode-finding
+    and SLQ solves converged to cg_delta_conv = 1e-8, against the reference at the same setting
+    (tests/golden/make_golden_100k_tight.py): nll and gradient at the 1e-6 north-star tolerance."""
+    from gpboost_amd import synthetic
+    case = _golden100k()["bernoulli_tight"]
+    X = synthetic.bench_coords(case["n"])
+    y = synthetic.bench_bernoulli_y(X)
+    gm = _model(X, dict(likelihood="bernoulli_logit", cov_fct="exponential", shape=0.5, num_neighbors=30),
+                t=case["num_rand_vec_trace"], seed=1, dc=case["cg_delta_conv"])
+    nll, g, _ = gm.neg_log_likelihood_and_grad(case["cov_pars"], y)
+    _check(nll, g, case["nll"], case["grad"])
+
+
+def test_baseline_size_bernoulli_default_within_reference_sensitivity():
+    """Config 5 at the default cg_delta_conv = 1e-2. nll at 1e-6. The gradient at this tolerance is
+    rounding-limited, which the REFERENCE itself shows (tests/golden/make_golden_100k_sens.py): its
+    thread-count spread is zero, but moving the covariance parameters by 1e-14 relative (a few ulps)
+    moves its own gradient by up to ~1e-5 relative, because the six Newton solves stop on an absolute
+    residual of 1e-2 and their iteration counts flip. The bound is twice the reference's own largest
+    ulp-perturbation deviation per component, read from the fixture (no value of this implementation
+    enters it)."""
+    from gpboost_amd import synthetic
+    gold = _golden100k()
+    case, sens = gold["bernoulli"], gold["bernoulli_sensitivity"]
+    ref_g = np.asarray(case["grad"])
+    spread = np.max([np.abs(np.asarray(r["grad"]) - ref_g) for r in sens["runs"]], axis=0)
+    assert np.all(spread > 0) and np.all(spread < 1e-4 * np.abs(ref_g))   # the fixture's own statement
     X = synthetic.bench_coords(case["n"])
     y = synthetic.bench_bernoulli_y(X)
     gm = _model(X, dict(likelihood="bernoulli_logit", cov_fct="exponential", shape=0.5, num_neighbors=30),
                 t=case["num_rand_vec_trace"], seed=1, dc=case["cg_delta_conv"])
     nll, g, _ = gm.neg_log_likelihood_and_grad(case["cov_pars"], y)
     assert abs(nll - case["nll"]) <= 1e-6 * abs(case["nll"]), (nll, case["nll"])
-    np.testing.assert_allclose(g, case["grad"], rtol=2e-5)
+    assert np.all(np.abs(g - ref_g) <= 2 * spread), (g, ref_g, spread)
 
 
 def test_latent_refuses_repeated_coordinates():
