@@ -247,6 +247,83 @@ def bernoulli_leg(X, steps: int) -> dict:
             "cpu_baseline": None}
 
 
+GROUPED_N = 500_000               # BASELINE config 4 (expressible proxy)
+GROUPED_LEVELS = (5000, 500)
+GROUPED_PARS = [1.0, 1.0, 0.25]   # sigma^2, sigma_1^2, sigma_2^2
+
+
+def grouped_cpu_baseline(g, y, reps: int = 3, fit: bool = True) -> dict | None:
+    """The reference's grouped-RE path (oracle/_ref/ref_harness_grouped: REModelTemplate<sp_mat_rm_t>,
+    iterative SSOR-PCG + SLQ, default settings) on this host: `reps` L-BFGS-unit evaluations, and one
+    fit of the same data."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness_grouped")
+    if not os.path.exists(harness):
+        return None
+    import numpy as np
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", str(os.cpu_count() or 1))), 16))
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(np.array([g.shape[0], 0], dtype=np.int32).tobytes())
+        f.write(np.ascontiguousarray(y, dtype=np.float64).tobytes())
+        f.write(np.array([0, 0, g.shape[1]], dtype=np.int32).tobytes())   # no covariates, no offset, K
+        f.write(np.ascontiguousarray(g.T, dtype=np.int32).tobytes())
+        path = f.name
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads))
+    base = [harness, path, "matrix_inversion_method=iterative", "cg_delta_conv=1e-2", "num_rand_vec_trace=50"]
+    try:
+        r = json.loads(subprocess.run(base + ["mode=lbfgs", f"reps={reps}", "cov_pars=" + ",".join(map(str, GROUPED_PARS))],
+                                      capture_output=True, text=True, timeout=600, env=env, check=True).stdout)
+        t = r["median_time"]
+        out = {"value": 1.0 / t, "unit": "evals/s", "cores": threads, "kind": "reference", "nll": r["nll"],
+               "sample": f"{reps} L-BFGS-unit evals at n={g.shape[0]}, levels {GROUPED_LEVELS} "
+                         f"(median {t:.3f} s/eval; construction {r['t_construct']:.2f} s excluded)"}
+        if fit:
+            rf = json.loads(subprocess.run(base + ["mode=fit"], capture_output=True, text=True, timeout=600,
+                                           env=env, check=True).stdout)
+            out["fit"] = {"s": rf["fit_time"], "num_it": rf["num_it"], "nll": rf["nll"], "cov_pars": rf["cov_pars"]}
+        return out
+    except Exception as e:  # noqa: BLE001
+        sys.stderr.write(f"reference grouped CPU baseline failed: {e}\n")
+        return None
+    finally:
+        os.unlink(path)
+
+
+def grouped_leg(steps: int, cpu: bool) -> dict:
+    """BASELINE config 4's expressible proxy: n = 500k, two crossed grouped random effects (5000 and
+    500 levels), Gaussian likelihood, the reference's default iterative method (SSOR-PCG for
+    A^-1 Z^T y, SLQ log-determinant on 50 probes, stochastic-trace gradient), cg_delta_conv 1e-2:
+    the L-BFGS unit (nll + gradient, sigma^2 profiled) at fixed parameters, then a whole fit."""
+    import numpy as np
+
+    from gpboost_amd import GPModel, synthetic
+    g = synthetic.bench_groups(GROUPED_N, GROUPED_LEVELS)
+    y = synthetic.bench_grouped_y(g)
+    t0 = time.perf_counter()
+    gm = GPModel(group_data=g)
+    nll, gr, _ = gm.neg_log_likelihood_and_grad(GROUPED_PARS, y, profile_sigma2=True)   # SetY + first eval
+    t_construct = time.perf_counter() - t0
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        nll, gr, _ = gm.neg_log_likelihood_and_grad(GROUPED_PARS, None, profile_sigma2=True)
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    gf = GPModel(group_data=g)
+    t0 = time.perf_counter()
+    gf.fit(y)
+    tf = time.perf_counter() - t0
+    leg = {"metric": "grouped RE (2 crossed effects) neg-log-lik + grad evals/sec, n=500k",
+           "value": 1.0 / t, "unit": "evals/s", "steps": steps, "ms_per_step": t * 1e3,
+           "config": {"workload": "grouped_gaussian_iterative_ssor_lbfgs_unit", "n": GROUPED_N,
+                      "levels": list(GROUPED_LEVELS), "cov_pars": GROUPED_PARS, "num_rand_vec_trace": 50,
+                      "cg_delta_conv": 1e-2, "construction_s": round(t_construct, 3), "nll": nll,
+                      "grad": [float(v) for v in gr]},
+           "fit": {"s": tf, "num_it": gf.get_num_optim_iter(), "nll": gf.get_current_neg_log_likelihood(),
+                   "cov_pars": [float(v) for v in gf.get_cov_pars()]},
+           "cpu_baseline": grouped_cpu_baseline(g, y) if cpu else None}
+    return leg
+
+
 def fit_leg(X, Y, cpu: bool) -> dict:
     """GPB_OptimCovPar end to end on the headline data (reference default optimizer "lbfgs",
     initial values from the reference's FindInitCovPar heuristic), from model construction; the
@@ -426,7 +503,12 @@ def main():
     ap.add_argument("--latent-steps", type=int, default=3)
     ap.add_argument("--no-dense", action="store_true", help="skip the secondary dense (config 2) leg")
     ap.add_argument("--no-fit", action="store_true", help="skip the secondary GPB_OptimCovPar (fit) leg")
+    ap.add_argument("--no-grouped", action="store_true", help="skip the grouped random effects (config 4) leg")
+    ap.add_argument("--only-grouped", action="store_true", help="run only the grouped leg (prints its JSON)")
     args = ap.parse_args()
+    if args.only_grouped:
+        print(json.dumps(grouped_leg(args.steps, not args.no_cpu_baseline)))
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -539,6 +621,8 @@ def main():
         line["fit"] = fit_leg(X, Y, not args.no_cpu_baseline)
     if world == 1 and not args.no_dense:
         line["dense"] = dense_leg(3, not args.no_cpu_baseline)
+    if world == 1 and not args.no_grouped:
+        line["grouped"] = grouped_leg(5, not args.no_cpu_baseline)
     if world == 1 and not args.no_latent:
         del gm
         line["latent_iterative"] = latent_leg(X, Y, args.latent_steps, not args.no_cpu_baseline)

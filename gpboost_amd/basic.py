@@ -96,14 +96,20 @@ class GPModel:
                  free_raw_data=False, model_file=None, model_dict=None, vecchia_approx=None,
                  vecchia_pred_type=None, num_neighbors_pred=None):
         self.handle = None
-        if group_data is not None or group_rand_coef_data is not None:
-            raise GPBoostError("grouped random effects are out of scope for gpboost_amd")
+        if group_rand_coef_data is not None:
+            raise GPBoostError("grouped random coefficients are out of scope for gpboost_amd")
         if gp_rand_coef_data is not None:
             raise GPBoostError("GP random coefficients are out of scope for gpboost_amd")
-        if gp_coords is None:
-            raise ValueError("'gp_coords' must be provided (gpboost_amd evaluates GP likelihoods)")
         if model_file is not None or model_dict is not None:
             raise GPBoostError("model loading is out of scope for gpboost_amd")
+        if group_data is not None:
+            if gp_coords is not None:
+                raise GPBoostError("models with both grouped random effects and a Gaussian process are not "
+                                   "supported by gpboost_amd")
+            self._init_grouped(group_data, likelihood, matrix_inversion_method, seed, cluster_ids, weights)
+            return
+        if gp_coords is None:
+            raise ValueError("Either 'group_data' or 'gp_coords' must be provided")
         if vecchia_approx is not None and vecchia_approx:
             gp_approx = "vecchia"
         coords = np.asarray(gp_coords, dtype=np.float64)
@@ -137,6 +143,43 @@ class GPModel:
             ctypes.c_bool(weights is not None), None, ctypes.c_double(likelihood_learning_rate),
             ctypes.byref(handle)))
         self.handle = handle
+        self.num_group_re = 0
+        self._post_init()
+
+    def _init_grouped(self, group_data, likelihood, matrix_inversion_method, seed, cluster_ids, weights):
+        """Grouped random effects (reference basic.py GPModel.__init__ group_data handling): labels are
+        converted to strings and passed column-major as NUL-terminated C strings."""
+        g = np.asarray(group_data)
+        if g.ndim == 1:
+            g = g.reshape(-1, 1)
+        if g.ndim != 2 or g.shape[0] == 0:
+            raise ValueError("'group_data' must be a vector or a matrix with one row per observation")
+        self.num_data, self.num_group_re = g.shape
+        self.gp_approx = "none"
+        self.likelihood = likelihood
+        self.dim_coords = 0
+        self.num_neighbors = 0
+        self.cov_function = None
+        self.cov_fct_shape = 0.
+        labels = g.astype(np.dtype(str)).flatten(order="F")
+        buf = ctypes.create_string_buffer(b"\0".join(s.encode() for s in labels) + b"\0")
+        cluster = None
+        if cluster_ids is not None:
+            cluster = np.ascontiguousarray(np.asarray(cluster_ids), dtype=np.int32)
+        handle = ctypes.c_void_p()
+        _safe_call(lib().GPB_CreateREModel(
+            ctypes.c_int32(self.num_data), _ip(cluster) if cluster is not None else None,
+            buf, ctypes.c_int32(self.num_group_re), None, None, ctypes.c_int32(0), None,
+            ctypes.c_int32(0), None, ctypes.c_int(0), None, ctypes.c_int32(0),
+            c_str("exponential"), ctypes.c_double(0.5), c_str("none"), ctypes.c_double(1.), ctypes.c_double(1.),
+            ctypes.c_int(0), c_str("random"), ctypes.c_int(0), ctypes.c_double(1.), c_str("kmeans++"),
+            c_str(likelihood), ctypes.c_double(0.), c_str(matrix_inversion_method), ctypes.c_int(seed),
+            ctypes.c_int(-1), ctypes.c_bool(True), ctypes.c_bool(weights is not None), None, ctypes.c_double(1.),
+            ctypes.byref(handle)))
+        self.handle = handle
+        self._post_init()
+
+    def _post_init(self):
         self.has_covariates = False
         self.num_covariates = 0
         k = ctypes.c_int(0)
@@ -314,6 +357,8 @@ class GPModel:
 
     def cov_par_names(self):
         """Parameter names as the reference labels them (error term only for the Gaussian likelihood)."""
+        if getattr(self, "num_group_re", 0):
+            return ["Error_term"] + [f"Group_{k + 1}" for k in range(self.num_group_re)]
         return (["Error_term"] if self.num_cov_pars == 3 else []) + ["GP_var", "GP_range"]
 
     def summary(self, std_err=False):

@@ -9,13 +9,26 @@
 #include <cstdarg>
 #include <cstring>
 #include <exception>
+#include <mutex>
 #include <string>
+#include <unordered_set>
 
+#include "grouped_model.h"
 #include "re_model.h"
 
+using gpb_amd::GroupedModel;
 using gpb_amd::REModelAMD;
 
 namespace {
+
+// Handles of grouped-random-effects models (GroupedModel); every other handle is an REModelAMD.
+std::mutex g_grouped_mu;
+std::unordered_set<const void*> g_grouped;
+
+GroupedModel* as_grouped(REModelHandle h) {
+  std::lock_guard<std::mutex> lk(g_grouped_mu);
+  return g_grouped.count(h) ? reinterpret_cast<GroupedModel*>(h) : nullptr;
+}
 
 thread_local char g_last_error[512] = "Everything is fine";
 void (*g_log_callback)(const char*) = nullptr;
@@ -36,6 +49,8 @@ void vlog(const char* level, const char* fmt, va_list ap) {
 
 REModelAMD* model(REModelHandle h) {
   if (h == nullptr) gpb_amd::Fatal("REModelHandle is NULL");
+  if (as_grouped(h) != nullptr)
+    gpb_amd::Fatal("this function is not supported for models with grouped random effects by gpboost_amd");
   return reinterpret_cast<REModelAMD*>(h);
 }
 
@@ -120,16 +135,32 @@ int GPB_CreateREModel(int32_t num_data, const int32_t* cluster_ids_data, const c
   (void)ind_points_selection; (void)likelihood_additional_param; (void)num_parallel_threads; (void)GPU_use;
   (void)weights; (void)likelihood_learning_rate;
   if (out == nullptr) gpb_amd::Fatal("'out' is NULL");
-  if (num_re_group > 0 || re_group_data != nullptr)
-    gpb_amd::Fatal("grouped random effects are out of scope for gpboost_amd (SURVEY.md §8)");
   if (num_re_group_rand_coef > 0 || num_gp_rand_coef > 0 || gp_rand_coef_data != nullptr)
     gpb_amd::Fatal("random coefficients are out of scope for gpboost_amd (SURVEY.md §8)");
-  if (num_gp != 1 || gp_coords_data == nullptr) gpb_amd::Fatal("gpboost_amd requires exactly one GP component (num_gp = 1)");
   if (has_weights) gpb_amd::Fatal("'weights' are not supported by gpboost_amd");
   if (cluster_ids_data != nullptr) {
     for (int32_t i = 1; i < num_data; ++i)
       if (cluster_ids_data[i] != cluster_ids_data[0]) gpb_amd::Fatal("multiple clusters (cluster_ids) are out of scope for gpboost_amd");
   }
+  if (seed < 0) gpb_amd::Fatal("seed must be >= 0");
+  if (num_re_group > 0 || re_group_data != nullptr) {   // grouped random effects (GroupedModel)
+    if (num_re_group <= 0 || re_group_data == nullptr) gpb_amd::Fatal("re_group_data and num_re_group must be given together");
+    if (num_gp > 0 || gp_coords_data != nullptr)
+      gpb_amd::Fatal("models with both grouped random effects and a Gaussian process are not supported by gpboost_amd");
+    if (str_or(likelihood, "gaussian") != "gaussian")
+      gpb_amd::Fatal("grouped random effects with likelihood '%s' are not supported by gpboost_amd (supported: gaussian)",
+                     likelihood);
+    if (num_data <= 0) gpb_amd::Fatal("num_data must be > 0");
+    auto levels = gpb_amd::parse_group_levels(num_data, num_re_group, re_group_data);
+    auto* g = new GroupedModel(num_data, levels, str_or(matrix_inversion_method, "default"), seed);
+    {
+      std::lock_guard<std::mutex> lk(g_grouped_mu);
+      g_grouped.insert(g);
+    }
+    *out = g;
+    return 0;   // (inside API_BEGIN's try; API_END's trailing return is not reached)
+  }
+  if (num_gp != 1 || gp_coords_data == nullptr) gpb_amd::Fatal("gpboost_amd requires exactly one GP component (num_gp = 1)");
   gpb_amd::ModelConfig cfg;
   cfg.n = num_data;
   cfg.d = dim_gp_coords;
@@ -141,13 +172,20 @@ int GPB_CreateREModel(int32_t num_data, const int32_t* cluster_ids_data, const c
   cfg.likelihood = str_or(likelihood, "gaussian");
   cfg.matrix_inversion_method = str_or(matrix_inversion_method, "default");
   cfg.seed = seed;
-  if (seed < 0) gpb_amd::Fatal("seed must be >= 0");
   *out = new REModelAMD(cfg, gp_coords_data);
   API_END();
 }
 
 int GPB_REModelFree(REModelHandle handle) {
   API_BEGIN();
+  if (GroupedModel* g = as_grouped(handle)) {
+    {
+      std::lock_guard<std::mutex> lk(g_grouped_mu);
+      g_grouped.erase(handle);
+    }
+    delete g;
+    return 0;
+  }
   delete reinterpret_cast<REModelAMD*>(handle);
   API_END();
 }
@@ -168,6 +206,26 @@ int GPB_SetOptimConfig(REModelHandle handle, double* init_cov_pars, double lr, d
   (void)acc_rate_cov; (void)use_nesterov_acc; (void)nesterov_schedule_version; (void)trace; (void)momentum_offset;
   (void)convergence_criterion;   // L-BFGS always tests the relative change of the objective (optim_utils.h:656-657)
   (void)lr_coef; (void)acc_rate_coef; (void)piv_chol_rank;
+  if (GroupedModel* g = as_grouped(handle)) {   // Gaussian grouped model: no aux parameters, no coefficients
+    (void)num_covariates; (void)init_coef; (void)optimizer_coef; (void)init_aux_pars; (void)estimate_aux_pars;
+    (void)delta_conv_mode_finding;
+    g->SetOptimSettings(init_cov_pars, lr, max_iter, delta_rel_conv, optimizer, m_lbfgs);
+    if (g->iterative()) {
+      g->SetPreconditioner(cg_preconditioner_type);
+      g->iter.cg_max_num_it = cg_max_num_it;
+      g->iter.cg_max_num_it_tridiag = cg_max_num_it_tridiag;
+      g->iter.cg_delta_conv = cg_delta_conv;
+    }
+    if (num_rand_vec_trace <= 0) gpb_amd::Fatal("num_rand_vec_trace must be > 0");
+    g->iter.num_rand_vec_trace = num_rand_vec_trace;
+    g->iter.seed_rand_vec_trace = seed_rand_vec_trace;
+    g->iter.reuse_rand_vec_trace = reuse_rand_vec_trace;
+    if (estimate_cov_par_index != nullptr && estimate_cov_par_index[0] >= 0) {
+      for (int k = 0; k < g->num_cov_pars(); ++k)
+        if (estimate_cov_par_index[k] <= 0) gpb_amd::Fatal("estimate_cov_par_index: fixing covariance parameters is not supported by gpboost_amd");
+    }
+    return 0;
+  }
   REModelAMD* m = model(handle);
   (void)num_covariates; (void)init_coef;   // the "wls" coefficient update profiles beta out at every evaluation
   m->SetOptimSettings(init_cov_pars, lr, max_iter, delta_rel_conv, optimizer, m_lbfgs);
@@ -199,8 +257,15 @@ int GPB_SetOptimConfig(REModelHandle handle, double* init_cov_pars, double lr, d
 int GPB_EvalNegLogLikelihood(REModelHandle handle, const double* y_data, double* cov_pars,
                              const double* fixed_effects, double* negll) {
   API_BEGIN();
-  REModelAMD* m = model(handle);
   if (cov_pars == nullptr) gpb_amd::Fatal("cov_pars is NULL (initial-value heuristics are out of scope)");
+  if (GroupedModel* g = as_grouped(handle)) {
+    if (fixed_effects != nullptr && y_data == nullptr)
+      gpb_amd::Fatal("EvalNegLogLikelihood: 'y_data' cannot nullptr when 'fixed_effects' is provided");
+    g->SetResponseAndOffset(y_data, fixed_effects);
+    negll[0] = g->Eval(cov_pars, false, 0).nll;
+    return 0;
+  }
+  REModelAMD* m = model(handle);
   if (fixed_effects != nullptr && y_data == nullptr && !m->config().latent)
     gpb_amd::Fatal("EvalNegLogLikelihood: 'y_data' cannot nullptr when 'fixed_effects' is provided");
   m->SetResponseAndOffset(y_data, fixed_effects);
@@ -268,10 +333,16 @@ int GPB_EvalNegLogLikelihoodGrad(REModelHandle handle, const double* y_data, con
                                  const double* fixed_effects, int profile_sigma2, double* negll, double* grad,
                                  double* sigma2_out) {
   API_BEGIN();
-  REModelAMD* m = model(handle);
   if (cov_pars == nullptr || negll == nullptr || grad == nullptr) gpb_amd::Fatal("NULL argument");
-  m->SetResponseAndOffset(y_data, fixed_effects);
-  gpb_amd::EvalResult res = m->Eval(cov_pars, true, profile_sigma2 ? 1 : 0);
+  gpb_amd::EvalResult res;
+  if (GroupedModel* g = as_grouped(handle)) {
+    g->SetResponseAndOffset(y_data, fixed_effects);
+    res = g->Eval(cov_pars, true, profile_sigma2 ? 1 : 0);
+  } else {
+    REModelAMD* m = model(handle);
+    m->SetResponseAndOffset(y_data, fixed_effects);
+    res = m->Eval(cov_pars, true, profile_sigma2 ? 1 : 0);
+  }
   negll[0] = res.nll;
   for (size_t k = 0; k < res.grad.size(); ++k) {
     double g = res.grad[k];
@@ -287,6 +358,10 @@ int GPB_EvalNegLogLikelihoodGrad(REModelHandle handle, const double* y_data, con
 
 int GPB_GetCurrentNegLogLikelihood(REModelHandle handle, double* negll) {
   API_BEGIN();
+  if (GroupedModel* g = as_grouped(handle)) {
+    negll[0] = g->last_nll();
+    return 0;
+  }
   negll[0] = model(handle)->last_nll();
   API_END();
 }
@@ -294,6 +369,15 @@ int GPB_GetCurrentNegLogLikelihood(REModelHandle handle, double* negll) {
 int GPB_GetCovPar(REModelHandle handle, double* cov_par, bool calc_std_dev) {
   API_BEGIN();
   // re_model.cpp:767-811: cov_par[0, P) = parameters, cov_par[P, 2P) = std devs if calc_std_dev
+  if (GroupedModel* g = as_grouped(handle)) {
+    const auto& p = g->last_cov_pars();
+    if (p.empty()) gpb_amd::Fatal("Covariance parameters have not been estimated or correctly set ");
+    if (calc_std_dev)
+      gpb_amd::Fatal("standard deviations of covariance parameters are not supported for grouped random effects by "
+                     "gpboost_amd");
+    for (size_t k = 0; k < p.size(); ++k) cov_par[k] = p[k];
+    return 0;
+  }
   REModelAMD* m = model(handle);
   const auto p = m->last_cov_pars();
   if (p.empty()) gpb_amd::Fatal("Covariance parameters have not been estimated or correctly set ");
@@ -304,12 +388,20 @@ int GPB_GetCovPar(REModelHandle handle, double* cov_par, bool calc_std_dev) {
 
 int GPB_GetNumIt(REModelHandle handle, int* num_it) {
   API_BEGIN();
+  if (GroupedModel* g = as_grouped(handle)) {
+    num_it[0] = g->num_it();
+    return 0;
+  }
   num_it[0] = model(handle)->num_it();
   API_END();
 }
 
 int GPB_GetInitCovPar(REModelHandle handle, double* init_cov_pars) {
   API_BEGIN();
+  if (GroupedModel* g = as_grouped(handle)) {
+    g->GetInitCovPar(init_cov_pars);
+    return 0;
+  }
   model(handle)->GetInitCovPar(init_cov_pars);
   API_END();
 }
@@ -317,6 +409,10 @@ int GPB_GetInitCovPar(REModelHandle handle, double* init_cov_pars) {
 int GPB_OptimCovPar(REModelHandle handle, const double* y_data, const double* fixed_effects) {
   // c_api.cpp GPB_OptimCovPar -> REModel::OptimCovPar(y, fixed_effects, false, false)
   API_BEGIN();
+  if (GroupedModel* g = as_grouped(handle)) {
+    g->OptimCovPar(y_data, fixed_effects);
+    return 0;
+  }
   model(handle)->OptimCovPar(y_data, fixed_effects);
   API_END();
 }
@@ -325,6 +421,12 @@ int GPB_OptimLinRegrCoefCovPar(REModelHandle handle, const double* y_data, const
                                int num_covariates, const double* fixed_effects) {
   // c_api.cpp:2843-2852 -> REModel::OptimLinRegrCoefCovPar (re_model.cpp:403-469)
   API_BEGIN();
+  if (GroupedModel* g = as_grouped(handle)) {
+    if (covariate_data != nullptr && num_covariates > 0)
+      gpb_amd::Fatal("linear regression covariates with grouped random effects are not supported by gpboost_amd");
+    g->OptimCovPar(y_data, fixed_effects);
+    return 0;
+  }
   model(handle)->OptimLinRegrCoefCovPar(y_data, covariate_data, num_covariates, fixed_effects);
   API_END();
 }
@@ -339,6 +441,10 @@ int GPB_CalcGradientF(REModelHandle handle, double* y, const double* fixed_effec
 
 int GPB_CanCalculateStandardErrorsCovPars(REModelHandle handle, int* out) {
   API_BEGIN();
+  if (as_grouped(handle) != nullptr) {   // not built for grouped models here
+    out[0] = 0;
+    return 0;
+  }
   out[0] = (int)model(handle)->CanCalculateStandardErrorsCovPars();
   API_END();
 }
@@ -359,18 +465,30 @@ int GPB_PredictREModelTrainingDataRandomEffects(REModelHandle handle, const doub
 
 int GPB_GetOptimizerCovPars(REModelHandle handle, char* out_str, int* num_char) {
   API_BEGIN();
+  if (as_grouped(handle) != nullptr) {   // InitializeOptimSettings (re_model_template.h:7463-7474)
+    copy_name("lbfgs", out_str, num_char);
+    return 0;
+  }
   copy_name(model(handle)->optimizer_cov(), out_str, num_char);
   API_END();
 }
 
 int GPB_GetOptimizerCoef(REModelHandle handle, char* out_str, int* num_char) {
   API_BEGIN();
+  if (as_grouped(handle) != nullptr) {
+    copy_name("wls", out_str, num_char);
+    return 0;
+  }
   copy_name(model(handle)->optimizer_coef(), out_str, num_char);
   API_END();
 }
 
 int GPB_GetCGPreconditionerType(REModelHandle handle, char* out_str, int* num_char) {
   API_BEGIN();
+  if (GroupedModel* g = as_grouped(handle)) {
+    copy_name(g->cg_preconditioner_type(), out_str, num_char);
+    return 0;
+  }
   copy_name(model(handle)->cg_preconditioner_type(), out_str, num_char);
   API_END();
 }
@@ -378,31 +496,45 @@ int GPB_GetCGPreconditionerType(REModelHandle handle, char* out_str, int* num_ch
 int GPB_GetNumCGSteps(REModelHandle handle, int* num_cg_steps) {
   // re_model_template.h:527-537: defined for models of several grouped random effects only
   API_BEGIN();
-  (void)model(handle);
-  (void)num_cg_steps;
-  gpb_amd::Fatal("GetNumCGStepLast: this function is currently only implemented when having multiple grouped random "
-                 "effects and iterative methods are used ");
+  GroupedModel* g = as_grouped(handle);
+  if (g == nullptr) (void)model(handle);
+  if (g == nullptr || !g->iterative())
+    gpb_amd::Fatal("GetNumCGStepLast: this function is currently only implemented when having multiple grouped random "
+                   "effects and iterative methods are used ");
+  num_cg_steps[0] = g->num_cg_steps();
   API_END();
 }
 
 int GPB_GetNumCGStepsTridiag(REModelHandle handle, int* num_cg_steps) {
   API_BEGIN();   // re_model_template.h:542-552
-  (void)model(handle);
-  (void)num_cg_steps;
-  gpb_amd::Fatal("GetNumCGStepLast: this function is currently only implemented when having multiple grouped random "
-                 "effects and iterative methods are used ");
+  GroupedModel* g = as_grouped(handle);
+  if (g == nullptr) (void)model(handle);
+  if (g == nullptr || !g->iterative())
+    gpb_amd::Fatal("GetNumCGStepLast: this function is currently only implemented when having multiple grouped random "
+                   "effects and iterative methods are used ");
+  num_cg_steps[0] = g->num_cg_steps_tridiag();
   API_END();
 }
 
 int GPB_SetLikelihood(REModelHandle handle, const char* likelihood) {
   API_BEGIN();
   if (likelihood == nullptr) gpb_amd::Fatal("likelihood is NULL");
+  if (as_grouped(handle) != nullptr) {
+    if (std::string(likelihood) != "gaussian")
+      gpb_amd::Fatal("grouped random effects with likelihood '%s' are not supported by gpboost_amd (supported: "
+                     "gaussian)", likelihood);
+    return 0;
+  }
   model(handle)->SetLikelihood(std::string(likelihood));
   API_END();
 }
 
 int GPB_GetResponseData(REModelHandle handle, double* response_data) {
   API_BEGIN();
+  if (GroupedModel* g = as_grouped(handle)) {
+    g->GetResponseData(response_data);
+    return 0;
+  }
   model(handle)->GetResponseData(response_data);
   API_END();
 }
@@ -433,7 +565,7 @@ int GPB_GetInitAuxPars(REModelHandle handle, double* aux_pars) {
 
 int GPB_GetLikelihoodName(REModelHandle handle, char* out_str, int* num_char) {
   API_BEGIN();
-  const std::string& s = model(handle)->config().likelihood;
+  const std::string s = as_grouped(handle) != nullptr ? std::string("gaussian") : model(handle)->config().likelihood;
   std::memcpy(out_str, s.c_str(), s.size() + 1);
   num_char[0] = (int)s.size() + 1;
   API_END();
@@ -441,12 +573,17 @@ int GPB_GetLikelihoodName(REModelHandle handle, char* out_str, int* num_char) {
 
 int GPB_GetNumAuxPars(REModelHandle handle, int* num_aux_pars) {
   API_BEGIN();
-  num_aux_pars[0] = model(handle)->num_aux_pars();
+  num_aux_pars[0] = as_grouped(handle) != nullptr ? 0 : model(handle)->num_aux_pars();
   API_END();
 }
 
 int GPB_GetAuxPars(REModelHandle handle, double* aux_pars, char* out_str) {
   API_BEGIN();
+  if (as_grouped(handle) != nullptr) {
+    (void)aux_pars;
+    if (out_str != nullptr) out_str[0] = '\0';
+    return 0;
+  }
   REModelAMD* m = model(handle);
   const auto& a = m->aux_pars();
   for (size_t k = 0; k < a.size(); ++k) aux_pars[k] = a[k];
@@ -470,7 +607,8 @@ int GPB_GetLastIterationInfo(REModelHandle handle, double* info) {
 
 int GPB_GetNumCovPars(REModelHandle handle, int* num_cov_pars) {
   API_BEGIN();
-  num_cov_pars[0] = model(handle)->num_cov_pars();
+  GroupedModel* g = as_grouped(handle);
+  num_cov_pars[0] = g != nullptr ? g->num_cov_pars() : model(handle)->num_cov_pars();
   API_END();
 }
 

@@ -1,0 +1,257 @@
+// GroupedModel implementation: configuration, response handling, the combination of GroupedRE's
+// device sums into the negative log-likelihood and its gradient, and the L-BFGS fit.
+#include "grouped_model.h"
+
+#include <cmath>
+#include <cstdlib>
+#include <limits>
+#include <unordered_map>
+
+namespace gpb_amd {
+
+std::vector<std::vector<int>> parse_group_levels(int n, int K, const char* re_group_data) {
+  if (re_group_data == nullptr) Fatal("re_group_data is NULL");
+  std::vector<std::vector<int>> levels(K, std::vector<int>(n));
+  const char* p = re_group_data;
+  for (int k = 0; k < K; ++k) {
+    std::unordered_map<std::string, int> index;
+    index.reserve(1024);
+    for (int i = 0; i < n; ++i) {
+      std::string label(p);
+      p += label.size() + 1;
+      auto it = index.find(label);
+      if (it == index.end()) it = index.emplace(std::move(label), (int)index.size()).first;
+      levels[k][i] = it->second;
+    }
+  }
+  return levels;
+}
+
+GroupedModel::GroupedModel(int n, const std::vector<std::vector<int>>& levels, const std::string& mim, int seed)
+    : n_(n), mim_(mim) {
+  (void)seed;   // grouped models draw no random numbers at construction (probes use seed_rand_vec_trace)
+  if (n <= 0) Fatal("num_data must be > 0");
+  const int K = (int)levels.size();
+  if (K < 1) Fatal("num_re_group must be > 0");
+  if (mim_ == "default") mim_ = K > 1 ? "iterative" : "cholesky";
+  if (mim_ != "iterative" && mim_ != "cholesky")
+    Fatal("Matrix inversion method '%s' is not supported.", mim_.c_str());
+  if (mim_ == "iterative" && K == 1)   // CheckCompatibilitySpecialOptions (re_model_template.h:6698-6702)
+    Fatal("Cannot use matrix_inversion_method = 'iterative' if there is only a single-level grouped random effects. "
+          "Use matrix_inversion_method = 'cholesky' instead (this is very fast). Iterative methods are for multiple "
+          "grouped random effects ");
+  if (mim_ == "cholesky" && K > 1)
+    Fatal("matrix_inversion_method 'cholesky' with several grouped random effects is not supported by gpboost_amd "
+          "(supported: iterative, the reference's default there)");
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
+    Fatal("no HIP device visible: gpboost_amd has no CPU fallback");
+  if (const char* dev = std::getenv("GPBOOST_AMD_DEVICE")) {
+    device_ = std::atoi(dev);
+    if (device_ < 0 || device_ >= ndev) Fatal("GPBOOST_AMD_DEVICE=%d but %d device(s) visible", device_, ndev);
+  } else {
+    HIP_CHECK(hipGetDevice(&device_));
+  }
+  UseDevice();
+  HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  re_.reset(new GroupedRE(n, levels, stream_));
+}
+
+GroupedModel::~GroupedModel() {
+  re_.reset();
+  if (stream_) (void)hipStreamDestroy(stream_);
+}
+
+void GroupedModel::UseDevice() const { HIP_CHECK(hipSetDevice(device_)); }
+
+void GroupedModel::SetResponseAndOffset(const double* y, const double* fixed_effects) {
+  if (y == nullptr && fixed_effects == nullptr) {
+    if (!y_set_) Fatal("response variable y has not been set");
+    return;
+  }
+  if (y != nullptr) y_raw_.assign(y, y + n_);
+  if (y_raw_.empty()) Fatal("response variable y has not been set");
+  y_ = y_raw_;
+  if (fixed_effects != nullptr)
+    for (int i = 0; i < n_; ++i) y_[i] -= fixed_effects[i];
+  for (int i = 0; i < n_; ++i)
+    if (std::isnan(y_[i]) || std::isinf(y_[i])) Fatal("NaN or Inf in response variable / label ");
+  UseDevice();
+  re_->SetY(y_.data());
+  y_set_ = true;
+}
+
+void GroupedModel::GetResponseData(double* y) const {
+  if (y_raw_.empty()) Fatal("response variable y has not been set");
+  std::copy(y_raw_.begin(), y_raw_.end(), y);
+}
+
+EvalResult GroupedModel::Eval(const double* cov_pars_orig, bool want_grad, int profile) {
+  const int K = re_->K();
+  for (int k = 0; k <= K; ++k)
+    if (!(cov_pars_orig[k] > 0.)) Fatal("covariance parameters must be > 0");
+  std::vector<double> trafo(1 + K);   // TransformCovPars (re_comp.h: sigma_k^2 / sigma^2)
+  trafo[0] = cov_pars_orig[0];
+  for (int k = 0; k < K; ++k) trafo[1 + k] = cov_pars_orig[1 + k] / cov_pars_orig[0];
+  EvalResult r = EvalTrafo(trafo.data(), want_grad, profile);
+  last_cov_pars_.assign(cov_pars_orig, cov_pars_orig + 1 + K);
+  if (profile) {
+    for (int k = 0; k < K; ++k) last_cov_pars_[1 + k] = trafo[1 + k] * r.sigma2;
+    last_cov_pars_[0] = r.sigma2;
+  }
+  return r;
+}
+
+EvalResult GroupedModel::EvalTrafo(const double* trafo, bool want_grad, int profile, bool fatal_on_nan) {
+  if (!y_set_) Fatal("response variable y has not been set");
+  UseDevice();
+  const int K = re_->K();
+  GroupedParts parts;
+  re_->Eval(trafo + 1, want_grad, iterative(), num_iter_ > 0, iter, parts);
+  last_cg_its_ = parts.cg_its;
+  last_lanczos_ = parts.lanczos_steps;
+  const double q = parts.yTPsiInvy;
+  const double sigma2 = profile ? q / n_ : trafo[0];   // ProfileOutSigma2 (re_model_template.h:2407)
+  EvalResult res;
+  res.sigma2 = sigma2;
+  // CalcNegLogLikelihood (Gaussian, re_model_template.h:2880-2890)
+  res.nll = q / 2. / sigma2 + parts.logdet / 2. + n_ / 2. * (std::log(sigma2) + std::log(2. * M_PI));
+  if (!std::isfinite(res.nll)) {
+    if (fatal_on_nan) Fatal("NaN or Inf occurred in the negative log-likelihood");
+    res.nll = std::numeric_limits<double>::quiet_NaN();
+  }
+  if (want_grad) {   // CalcGradPars_Only_Grouped_REs_Woodbury_GaussLikelihood_Cluster_i (:2242-2391)
+    int off = 0;
+    res.grad.assign(profile ? K : K + 1, 0.);
+    if (!profile) {
+      res.grad[0] = -q / sigma2 / 2. + n_ / 2.;
+      off = 1;
+    }
+    for (int k = 0; k < K; ++k) res.grad[off + k] = -parts.quad[k] / sigma2 / 2. + parts.trace[k] / 2.;
+  }
+  last_nll_ = res.nll;
+  return res;
+}
+
+void GroupedModel::SetOptimSettings(const double* init_cov_pars, double lr, int max_iter, double delta_rel_conv,
+                                    const char* optimizer, int m_lbfgs) {
+  if (optimizer != nullptr && optimizer[0] != '\0' && std::string(optimizer) != "lbfgs")
+    Fatal("Optimizer option '%s' is not supported for covariance parameters by gpboost_amd (supported: lbfgs)",
+          optimizer);
+  if (init_cov_pars != nullptr) {
+    init_cov_pars_.assign(init_cov_pars, init_cov_pars + num_cov_pars());
+    for (double v : init_cov_pars_)
+      if (!(v > 0.)) Fatal("init_cov_pars must be > 0");
+    cov_pars_orig_ = init_cov_pars_;
+    cov_pars_initialized_ = true;
+  }
+  optim_.initial_step_factor = lr < 0. ? 1. : lr;
+  optim_.max_iterations = max_iter;
+  optim_.delta = delta_rel_conv < 0. ? 1e-6 : delta_rel_conv;
+  if (m_lbfgs > 0) optim_.m = m_lbfgs;
+}
+
+void GroupedModel::SetPreconditioner(const char* preconditioner) {
+  if (preconditioner == nullptr || preconditioner[0] == '\0') return;
+  const std::string p(preconditioner);
+  if (p != "ssor")   // SUPPORTED_PRECONDITIONERS_GROUPED_RE_ (re_model_template.h:5410) minus the ones not built
+    Fatal("cg_preconditioner_type '%s' is not supported for grouped random effects by gpboost_amd (supported: ssor)",
+          p.c_str());
+}
+
+void GroupedModel::FindInitCovPar(const double* y, double* trafo) const {
+  // re_model_template.h:4388-4485 (Gaussian): sigma^2 = sample variance / 2, tau_k = 1 / K
+  double mean = 0., var = 0.;
+  for (int i = 0; i < n_; ++i) mean += y[i];
+  mean /= n_;
+  for (int i = 0; i < n_; ++i) var += (y[i] - mean) * (y[i] - mean);
+  var /= (n_ - 1);
+  trafo[0] = var / 2.;
+  for (int k = 0; k < re_->K(); ++k) trafo[1 + k] = 1. / re_->K();
+}
+
+void GroupedModel::GetInitCovPar(double* out) const {
+  const std::vector<double>& v = !init_cov_pars_.empty() ? init_cov_pars_ : init_used_;
+  for (int k = 0; k < num_cov_pars(); ++k) out[k] = v.empty() ? -1. : v[k];
+}
+
+namespace {
+
+// EvalLLforLBFGSpp with the error variance profiled out (optim_utils.h:269-313): x = log tau. The
+// value and gradient come from one device evaluation, as the reference's gradient call reuses the
+// state of the preceding likelihood evaluation at the same point.
+class GroupedProfiledObjective : public LbfgsObjective {
+ public:
+  explicit GroupedProfiledObjective(GroupedModel* m) : m_(m) {}
+  double Eval(const std::vector<double>& x, std::vector<double>& grad, bool eval_ll, bool calc_grad,
+              bool) override {
+    if (eval_ll || !(has_ && x == x_)) {
+      std::vector<double> trafo(1 + x.size());
+      trafo[0] = 1.;
+      for (size_t k = 0; k < x.size(); ++k) trafo[1 + k] = std::exp(x[k]);
+      EvalResult r = m_->EvalTrafo(trafo.data(), true, 1, /*fatal_on_nan=*/false);
+      x_ = x;
+      nll_ = r.nll;
+      sigma2_ = r.sigma2;
+      grad_ = r.grad;
+      has_ = true;
+    }
+    if (calc_grad) grad = grad_;
+    return nll_;
+  }
+  void SetLag1ProfiledOutVariables() override { sigma2_lag1_ = sigma2_; }
+  void ResetProfiledOutVariablesToLag1() override { sigma2_ = sigma2_lag1_; }
+  void SetNumIter(int it) override { m_->SetNumIter(it); }
+  double sigma2() const { return sigma2_; }
+
+ private:
+  GroupedModel* m_;
+  std::vector<double> x_, grad_;
+  double nll_ = 0., sigma2_ = 1., sigma2_lag1_ = 1.;
+  bool has_ = false;
+};
+
+}  // namespace
+
+void GroupedModel::OptimCovPar(const double* y, const double* fixed_effects) {
+  UseDevice();
+  if (y == nullptr && y_raw_.empty()) Fatal("response variable y has not been set");
+  SetResponseAndOffset(y != nullptr ? y : y_raw_.data(), fixed_effects);
+  const int K = re_->K();
+  num_iter_ = 0;   // re_model_template.h:974
+  std::vector<double> trafo(1 + K);
+  if (cov_pars_initialized_) {
+    trafo[0] = cov_pars_orig_[0];
+    for (int k = 0; k < K; ++k) trafo[1 + k] = cov_pars_orig_[1 + k] / cov_pars_orig_[0];
+  } else {
+    FindInitCovPar(y_.data(), trafo.data());
+  }
+  std::vector<double> start_orig(1 + K);
+  start_orig[0] = trafo[0];
+  for (int k = 0; k < K; ++k) start_orig[1 + k] = trafo[1 + k] * trafo[0];
+  if (!cov_pars_initialized_) init_used_ = start_orig;
+  if (optim_.max_iterations <= 0) {
+    num_it_ = 0;
+    cov_pars_orig_ = start_orig;
+    cov_pars_initialized_ = true;
+    last_cov_pars_ = cov_pars_orig_;
+    return;
+  }
+  std::vector<double> x(K);
+  for (int k = 0; k < K; ++k) x[k] = std::log(trafo[1 + k]);
+  double fx = 0.;
+  GroupedProfiledObjective obj(this);
+  num_it_ = lbfgs_minimize(obj, x, fx, optim_);
+  for (double v : x)
+    if (std::isnan(v) || std::isinf(v))
+      Fatal("NaN or Inf occurred in covariance parameter optimization using 'lbfgs' (the reference's nelder_mead "
+            "restart is not supported by gpboost_amd)");
+  const double s2 = obj.sigma2();
+  cov_pars_orig_.assign(1 + K, s2);
+  for (int k = 0; k < K; ++k) cov_pars_orig_[1 + k] = std::exp(x[k]) * s2;
+  cov_pars_initialized_ = true;
+  last_nll_ = fx;
+  last_cov_pars_ = cov_pars_orig_;
+}
+
+}  // namespace gpb_amd

@@ -1,0 +1,90 @@
+// GroupedModel: the model object behind the GPB_* C ABI for Gaussian models whose random effects
+// are K grouped (crossed or nested) effects — the reference's REModelTemplate<sp_mat_rm_t, ...>
+// with num_re_group > 0 and no GP (re_model.cpp:21-111, re_model_template.h:95-465). Parameters
+// (original scale): [sigma^2 (error variance), sigma_1^2, ..., sigma_K^2]; transformed scale
+// [sigma^2, tau_1, ..., tau_K], tau_k = sigma_k^2 / sigma^2 (TransformCovPars). The likelihood runs
+// on the device in GroupedRE (grouped.h); this class keeps the configuration, the response and the
+// optimizer state.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "grouped.h"
+#include "optim.h"
+#include "re_model.h"
+
+namespace gpb_amd {
+
+class GroupedModel {
+ public:
+  // levels: K x n level indices (order of first appearance, as RECompGroup numbers its labels,
+  // re_comp.h:245-264). matrix_inversion_method: "default" -> "iterative" for K >= 2, "cholesky"
+  // for K == 1 (UseIterativeByDefault, re_model_template.h:6719-6724).
+  GroupedModel(int n, const std::vector<std::vector<int>>& levels, const std::string& matrix_inversion_method,
+               int seed);
+  ~GroupedModel();
+
+  int n() const { return n_; }
+  int K() const { return re_->K(); }
+  int num_cov_pars() const { return 1 + re_->K(); }
+  const std::string& matrix_inversion_method() const { return mim_; }
+  bool iterative() const { return mim_ == "iterative"; }
+  std::string cg_preconditioner_type() const { return iterative() ? "ssor" : ""; }
+  const std::vector<int>& levels_per_effect() const { return re_->levels_per_effect(); }
+
+  // y - fixed_effects (nullable) is the response; y (nullable: keep) is stored for GetResponseData.
+  void SetResponseAndOffset(const double* y, const double* fixed_effects);
+  bool HasY() const { return y_set_; }
+  void GetResponseData(double* y) const;
+
+  // cov_pars on the original scale. profile: 0 -> gradient wrt log of all 1 + K parameters
+  // (include_error_var), 1 -> sigma^2 profiled out, gradient wrt log tau (the L-BFGS unit).
+  EvalResult Eval(const double* cov_pars_orig, bool want_grad, int profile);
+  EvalResult EvalTrafo(const double* trafo, bool want_grad, int profile, bool fatal_on_nan = true);
+
+  void SetOptimSettings(const double* init_cov_pars, double lr, int max_iter, double delta_rel_conv,
+                        const char* optimizer, int m_lbfgs);
+  void SetPreconditioner(const char* preconditioner);
+  // OptimCovPar (re_model.cpp:339-401 -> OptimExternal "lbfgs", optim_utils.h:561-706): L-BFGS on
+  // log tau with sigma^2 profiled out (EvalLLforLBFGSpp, optim_utils.h:269-313).
+  void OptimCovPar(const double* y, const double* fixed_effects);
+  void SetNumIter(int it) { num_iter_ = it; }
+  int num_it() const { return num_it_; }
+  double last_nll() const { return last_nll_; }
+  const std::vector<double>& last_cov_pars() const { return last_cov_pars_; }
+  void GetInitCovPar(double* out) const;
+  // GPB_GetNumCGSteps / GetNumCGStepsTridiag (re_model_template.h:527-552)
+  int num_cg_steps() const { return last_cg_its_; }
+  int num_cg_steps_tridiag() const { return last_lanczos_; }
+  IterativeConfig iter;
+
+ private:
+  void UseDevice() const;
+  void FindInitCovPar(const double* y, double* trafo) const;
+
+  int n_;
+  int device_ = 0;
+  std::string mim_;
+  hipStream_t stream_ = nullptr;
+  std::unique_ptr<GroupedRE> re_;
+  std::vector<double> y_raw_, y_;
+  bool y_set_ = false;
+
+  LbfgsSettings optim_;
+  std::vector<double> init_cov_pars_, cov_pars_orig_, init_used_, last_cov_pars_;
+  bool cov_pars_initialized_ = false;
+  int num_it_ = 0;
+  int num_iter_ = 0;   // the reference's num_iter_ (warm starts of the A^-1 Z^T y solve)
+  double last_nll_ = 0.;
+  int last_cg_its_ = 0, last_lanczos_ = 0;
+};
+
+// Parses re_group_data (column-major K x n NUL-terminated labels, re_model_template.h:6246-6270)
+// into level indices numbered in order of first appearance per effect.
+std::vector<std::vector<int>> parse_group_levels(int n, int K, const char* re_group_data);
+
+}  // namespace gpb_amd

@@ -129,6 +129,7 @@ int lbfgs_minimize(LbfgsObjective& f, std::vector<double>& x, double& fx, const 
     bool converged = gnorm <= eps_grad || gnorm <= eps_grad * norm2(x);
     if ((fx_lag - fx) <= s.delta * std::max(std::fabs(fx_lag), 1.)) converged = true;
     if (s.max_iterations != 0 && k >= s.max_iterations) converged = true;
+    f.SetNumIter(k - 1);
     f.SetLag1ProfiledOutVariables();
     if (converged) return k;
     for (int i = 0; i < n; ++i) {

@@ -36,6 +36,7 @@ class LbfgsObjective {
                       bool hint_grad) = 0;
   virtual void SetLag1ProfiledOutVariables() {}     // optim_utils.h (EvalLLforLBFGSpp) / LBFGS.h:232
   virtual void ResetProfiledOutVariablesToLag1() {} // LineSearchBacktracking.h:133
+  virtual void SetNumIter(int) {}                   // LBFGS.h:231 (f.SetNumIter(k - 1))
 };
 
 // LBFGSSolver::minimize with LineSearchBacktracking (Armijo) as GPBoost runs it: returns the

@@ -111,3 +111,26 @@ def bench_gaussian_y_cov(coords: np.ndarray, X: np.ndarray, beta=None) -> np.nda
         beta = np.array([1.0, 2.0, -1.5, 0.5, -0.25][: X.shape[1]])
     f = np.sin(4 * coords[:, 0]) * np.cos(3 * coords[:, 1])
     return X @ beta + f + 0.5 * bench_gaussian_y(n)
+
+
+def _normal(n: int, c1: float, c2: float) -> np.ndarray:
+    u1 = np.maximum(lcg_unif(n, c1), 1e-300)
+    return np.sqrt(-2.0 * np.log(u1)) * np.cos(2.0 * np.pi * lcg_unif(n, c2))
+
+
+def bench_groups(n: int, levels=(5000, 500)) -> np.ndarray:
+    """Crossed grouped random effects (BASELINE config 4 proxy): an n x K integer
+    label matrix, effect k uniform over levels[k] from the LCG stream c = 0.23 + 0.17 k."""
+    return np.column_stack([np.floor(lcg_unif(n, 0.23 + 0.17 * k) * m).astype(np.int32)
+                            for k, m in enumerate(levels)])
+
+
+def bench_grouped_y(groups: np.ndarray, sd=(1.0, 0.5), noise_sd: float = 1.0) -> np.ndarray:
+    """y = sum_k b_k[g_k] + noise, b_k ~ N(0, sd_k^2) per level (LCG Box-Muller streams)."""
+    n, K = groups.shape
+    y = noise_sd * _normal(n, 0.8, 0.42)
+    for k in range(K):
+        m = int(groups[:, k].max()) + 1
+        b = sd[k % len(sd)] * _normal(m, 0.31 + 0.1 * k, 0.57 + 0.1 * k)
+        y = y + b[groups[:, k]]
+    return y

@@ -123,6 +123,20 @@ int main(int argc, char** argv) {
     if (std::fread(fe.data(), 8, fe.size(), f) != fe.size()) return 2;
   }
   const double* fe_ptr = fe.empty() ? nullptr : fe.data();
+  // optional grouped random effects: int32 K, int32 labels[n * K] (effect-major); the reference
+  // takes NUL-terminated label strings, effect-major (c_api.h:1324-1327)
+  int32_t num_re_group = 0;
+  std::string re_group_data;
+  if (std::fread(&num_re_group, 4, 1, f) == 1 && num_re_group > 0) {
+    std::vector<int32_t> lab((size_t)n * num_re_group);
+    if (std::fread(lab.data(), 4, lab.size(), f) != lab.size()) return 2;
+    for (int32_t v : lab) {
+      re_group_data += std::to_string(v);
+      re_group_data.push_back('\0');
+    }
+  } else {
+    num_re_group = 0;
+  }
   std::fclose(f);
 
   const std::string cov_fct = get(args, "cov_fct", "exponential");
@@ -142,11 +156,24 @@ int main(int argc, char** argv) {
 
   Log::ResetLogLevelRE(LogLevelRE::Warning);
   auto t0 = std::chrono::steady_clock::now();
-  std::unique_ptr<REModelTemplate<den_mat_t, chol_den_mat_t>> m(new REModelTemplate<den_mat_t, chol_den_mat_t>(
+  // GPB_HARNESS_GROUPED: the sparse instantiation the REModel facade picks for models without GPs
+  // (re_model.cpp:65-76); grouped random effects only (num_gp = 0)
+#ifdef GPB_HARNESS_GROUPED
+  typedef REModelTemplate<sp_mat_rm_t, chol_sp_mat_rm_t> Model;
+  if (num_re_group <= 0) { std::fprintf(stderr, "grouped harness needs group data\n"); return 2; }
+  std::unique_ptr<Model> m(new Model(
+      n, nullptr, re_group_data.data(), num_re_group, nullptr, nullptr, 0, nullptr,
+      0, nullptr, 0, nullptr, 0, cov_fct.c_str(), shape, gp_approx.c_str(),
+      -1., 0., num_neighbors, ordering.c_str(), 0, 1., "kmeans++",
+      likelihood.c_str(), 0., mim.c_str(), seed, threads, false, false, nullptr, 1.));
+#else
+  typedef REModelTemplate<den_mat_t, chol_den_mat_t> Model;
+  std::unique_ptr<Model> m(new Model(
       n, nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr,
       1, coords.data(), d, nullptr, 0, cov_fct.c_str(), shape, gp_approx.c_str(),
       -1., 0., num_neighbors, ordering.c_str(), 0, 1., "kmeans++",
       likelihood.c_str(), 0., mim.c_str(), seed, threads, false, false, nullptr, 1.));
+#endif
   auto t1 = std::chrono::steady_clock::now();
   double t_construct = std::chrono::duration<double>(t1 - t0).count();
 
@@ -155,7 +182,11 @@ int main(int argc, char** argv) {
     const double cg_delta_conv = std::atof(get(args, "cg_delta_conv", "1e-2").c_str());
     const int t = std::atoi(get(args, "num_rand_vec_trace", "50").c_str());
     const int cg_max = std::atoi(get(args, "cg_max_num_it", "1000").c_str());
+#ifdef GPB_HARNESS_GROUPED
+    const std::string prec = get(args, "cg_preconditioner_type", "ssor");
+#else
     const std::string prec = get(args, "cg_preconditioner_type", "vadu");
+#endif
     const int no_index[1] = {-1};   // SetOptimConfig reads estimate_cov_par_index[0] (re_model_template.h:810)
     m->SetOptimConfig(0.1, 0.5, 1000, 1e-6, true, 0, "lbfgs", 2, "relative_change_in_log_likelihood",
                       0.1, 0.5, "lbfgs", cg_max, cg_max, cg_delta_conv, t, true, prec.c_str(),
@@ -183,7 +214,12 @@ int main(int argc, char** argv) {
                       std::atoi(get(args, "cg_max_num_it", "1000").c_str()),
                       std::atoi(get(args, "cg_max_num_it", "1000").c_str()),
                       std::atof(get(args, "cg_delta_conv", "1e-2").c_str()),
-                      std::atoi(get(args, "num_rand_vec_trace", "50").c_str()), true, "vadu",
+                      std::atoi(get(args, "num_rand_vec_trace", "50").c_str()), true,
+#ifdef GPB_HARNESS_GROUPED
+                      "ssor",
+#else
+                      "vadu",
+#endif
                       std::atoi(get(args, "seed_rand_vec_trace", "1").c_str()), -1,
                       std::atoi(get(args, "estimate_aux", "1").c_str()) != 0, no_index,
                       std::atoi(get(args, "m_lbfgs", "-1").c_str()), -1.);

@@ -28,8 +28,13 @@ from gpboost_amd import synthetic  # noqa: E402
 HARNESS = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
 
 
-def run_ref(coords: np.ndarray, y: np.ndarray, X: np.ndarray | None = None, fe: np.ndarray | None = None,
-            **opts) -> dict:
+HARNESS_GROUPED = os.path.join(ROOT, "oracle", "_ref", "ref_harness_grouped")
+
+
+def run_ref(coords: np.ndarray | None, y: np.ndarray, X: np.ndarray | None = None, fe: np.ndarray | None = None,
+            groups: np.ndarray | None = None, **opts) -> dict:
+    if coords is None:   # grouped random effects only
+        coords = np.zeros((y.shape[0], 0))
     n, d = coords.shape
     with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
         f.write(np.array([n, d], dtype=np.int32).tobytes())
@@ -40,12 +45,19 @@ def run_ref(coords: np.ndarray, y: np.ndarray, X: np.ndarray | None = None, fe: 
             f.write(np.ascontiguousarray(X.T).astype(np.float64).tobytes())
         elif fe is not None:
             f.write(np.array([0], dtype=np.int32).tobytes())
+        elif groups is not None:
+            f.write(np.array([0], dtype=np.int32).tobytes())
         if fe is not None:   # optional fixed effects: int32 1, F[n]
             f.write(np.array([1], dtype=np.int32).tobytes())
             f.write(np.asarray(fe, dtype=np.float64).tobytes())
+        elif groups is not None:
+            f.write(np.array([0], dtype=np.int32).tobytes())
+        if groups is not None:   # grouped random effects: int32 K, labels effect-major
+            f.write(np.array([groups.shape[1]], dtype=np.int32).tobytes())
+            f.write(np.ascontiguousarray(groups.T).astype(np.int32).tobytes())
         path = f.name
     try:
-        args = [HARNESS, path] + [f"{k}={v}" for k, v in opts.items()]
+        args = [HARNESS_GROUPED if groups is not None else HARNESS, path] + [f"{k}={v}" for k, v in opts.items()]
         out = subprocess.run(args, check=True, capture_output=True, text=True,
                              env=dict(os.environ, OMP_NUM_THREADS="8"))
         return json.loads(out.stdout)

@@ -1,0 +1,132 @@
+"""GPU parity for grouped (crossed) random effects — BASELINE config 4's expressible proxy
+ — against the reference itself.
+
+Reference path: GPB_CreateREModel with re_group_data (re_model_template.h:246-273, RECompGroup
+re_comp.h:245-271) -> REModelTemplate<sp_mat_rm_t, chol_sp_mat_rm_t> with the Woodbury identity:
+y^T Psi^-1 y and log|Psi| from A = Sigma^-1 + Z^T Z (re_model_template.h:2778-2872, 8965-9005); K >= 2
+"iterative" (the default there): SSOR-PCG (CGRandomEffectsVec, CG_utils.cpp:1100-1234), stochastic
+Lanczos quadrature (CGTridiagRandomEffects :1236-1414, LogDetStochTridiag :988-1004) and the
+stochastic-trace gradient with the SSOR control variate (:2304-2387, CalcOptimalC :1006-1022);
+K == 1: the closed-form diagonal branch. Fixtures: tests/golden/golden_grouped.json
+(make_golden_grouped.py runs oracle/_ref/ref_harness_grouped, the reference compiled from its
+sources).
+
+Tolerances. The probe vectors are the reference's own draws (same mt19937 seeds), so the SLQ and
+trace estimates are the same estimators on the same samples: at cg_delta_conv = 1e-10 both sides
+run the same Krylov iterations and differ only by summation-order rounding (nll 1e-10 relative,
+gradient 1e-6 relative = north_star). At the default cg_delta_conv = 1e-2 the PCG stops after a
+handful of iterations whose count both sides share; the remaining difference is rounding of a
+truncated solve (same bounds unless a stopping test flips, which these fixtures do not hit). K == 1
+is a closed form (1e-10).
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from gpboost_amd import GPBoostError, GPModel, synthetic
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+EVAL_CASES = ["k1_n5000_cholesky", "k2_n20000_tight", "k2_n20000_default", "k3_n20000_tight", "k2_n20000_t20_tight"]
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with open(os.path.join(HERE, "golden", "golden_grouped.json")) as f:
+        return json.load(f)
+
+
+def _data(case):
+    g = synthetic.bench_groups(case["n"], tuple(case["levels"]))
+    return g, synthetic.bench_grouped_y(g)
+
+
+def _model(case, g):
+    o = case["opts"]
+    gm = GPModel(group_data=g, matrix_inversion_method=o.get("matrix_inversion_method", "default"))
+    params = {}
+    if "cg_delta_conv" in o:
+        params["cg_delta_conv"] = float(o["cg_delta_conv"])
+    if "num_rand_vec_trace" in o:
+        params["num_rand_vec_trace"] = int(o["num_rand_vec_trace"])
+    if "seed_rand_vec_trace" in o:
+        params["seed_rand_vec_trace"] = int(o["seed_rand_vec_trace"])
+    gm.set_optim_params(params)
+    return gm
+
+
+@pytest.mark.parametrize("name", EVAL_CASES)
+def test_grouped_nll_and_grad_match_reference(golden, name):
+    case = golden[name]
+    g, y = _data(case)
+    gm = _model(case, g)
+    cp = np.array(case["cov_pars"])
+    nll = gm.neg_log_likelihood(cp, y)
+    assert abs(nll - case["nll"]) <= 1e-10 * abs(case["nll"]), (nll, case["nll"])
+    nll2, grad, _ = gm.neg_log_likelihood_and_grad(cp, y)
+    assert abs(nll2 - case["nll"]) <= 1e-10 * abs(case["nll"])
+    np.testing.assert_allclose(grad, case["grad"], rtol=1e-6, atol=1e-6 * np.abs(case["grad"]).max())
+    # the L-BFGS unit: sigma^2 profiled out
+    nllp, gradp, s2 = gm.neg_log_likelihood_and_grad(cp, y, profile_sigma2=True)
+    assert abs(nllp - case["lbfgs_nll"]) <= 1e-10 * abs(case["lbfgs_nll"])
+    assert abs(s2 - case["lbfgs_sigma2"]) <= 1e-10 * abs(case["lbfgs_sigma2"])
+    np.testing.assert_allclose(gradp, case["lbfgs_grad"], rtol=1e-6, atol=1e-6 * np.abs(case["lbfgs_grad"]).max())
+
+
+@pytest.mark.parametrize("name", ["fit_k1_n5000", "fit_k2_n20000_tight", "fit_k2_n20000_default"])
+def test_grouped_fit_matches_reference(golden, name):
+    case = golden[name]
+    g, y = _data(case)
+    gm = _model(case, g)
+    gm.fit(y)
+    np.testing.assert_allclose(gm.get_init_cov_pars(), case["init_cov_pars"], rtol=1e-12)
+    assert gm.get_num_optim_iter() == case["num_it"]
+    np.testing.assert_allclose(gm.get_cov_pars(), case["cov_pars"], rtol=1e-6)
+    assert abs(gm.get_current_neg_log_likelihood() - case["nll"]) <= 1e-9 * abs(case["nll"])
+    assert gm.cov_par_names() == ["Error_term"] + [f"Group_{k + 1}" for k in range(len(case["levels"]))]
+
+
+def test_grouped_api_names_and_errors():
+    g = synthetic.bench_groups(3000, (60, 9))
+    y = synthetic.bench_grouped_y(g)
+    gm = GPModel(group_data=g)   # default: iterative with SSOR for K >= 2
+    p = gm.get_optim_params()
+    assert p["optimizer_cov"] == "lbfgs" and p["cg_preconditioner_type"] == "ssor"
+    assert gm.num_cov_pars == 3
+    gm.neg_log_likelihood([1.0, 0.5, 0.5], y)
+    np.testing.assert_array_equal(gm.get_response_data(), y)
+    with pytest.raises(GPBoostError, match="single-level grouped"):
+        GPModel(group_data=g[:, :1], matrix_inversion_method="iterative")
+    with pytest.raises(GPBoostError, match="not supported"):
+        gm.set_optim_params({"cg_preconditioner_type": "incomplete_cholesky"})
+    with pytest.raises(GPBoostError, match="grouped random effects"):
+        gm.vecchia_structure()
+
+
+def test_grouped_string_labels_equal_integer_labels():
+    # labels are strings in the C API (order of first appearance defines the level index)
+    g = synthetic.bench_groups(4000, (80, 11))
+    y = synthetic.bench_grouped_y(g)
+    names = np.array([f"city_{v}" for v in g[:, 0]], dtype=object)
+    gs = np.column_stack([names, g[:, 1].astype(str)])
+    a = GPModel(group_data=g).neg_log_likelihood_and_grad([1.0, 0.7, 0.3], y)
+    b = GPModel(group_data=gs).neg_log_likelihood_and_grad([1.0, 0.7, 0.3], y)
+    assert a[0] == b[0]
+    np.testing.assert_array_equal(a[1], b[1])
+
+
+def test_grouped_config4_size_matches_reference(golden):
+    # BASELINE config 4 size: n = 500000, 5000 + 500 levels (make_golden_grouped.py --big)
+    for name in ("k2_n500000_default", "k2_n500000_tight"):
+        if name not in golden:
+            pytest.skip("config-4 fixtures not generated")
+        case = golden[name]
+        g, y = _data(case)
+        gm = _model(case, g)
+        cp = np.array(case["cov_pars"])
+        nll, grad, _ = gm.neg_log_likelihood_and_grad(cp, y)
+        assert abs(nll - case["nll"]) <= 1e-10 * abs(case["nll"]), (name, nll, case["nll"])
+        np.testing.assert_allclose(grad, case["grad"], rtol=1e-6, atol=1e-6 * np.abs(case["grad"]).max())
