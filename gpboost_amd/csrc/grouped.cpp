@@ -68,6 +68,8 @@ GroupedRE::GroupedRE(int n, const std::vector<std::vector<int>>& levels, hipStre
       split[r] = e;
     }
   std::vector<double> cnt(cnt_i.begin(), cnt_i.end());
+  rowptr_h_ = rowptr;
+  split_h_ = split;
   const size_t nnz = std::max<size_t>(col.size(), 1);
   d_rowptr_.alloc(M_ + 1);
   d_split_.alloc(M_);
@@ -132,13 +134,63 @@ GroupedRE::Block& GroupedRE::GetBlock(int which, int t, int pmax) {
   return b;
 }
 
-GroupedOp GroupedRE::Op() const {
-  GroupedOp op{};
+const GroupedRE::ChunkPlan& GroupedRE::Plan(int tc) {
+  auto it = plans_.find(tc);
+  if (it != plans_.end()) return *it->second;
+  std::unique_ptr<ChunkPlan> pl(new ChunkPlan());
+  const int L = gre_chunk_len(tc);
+  for (int kind = 0; kind < 3; ++kind) {   // full, lower, upper entry ranges of every row
+    std::vector<int> e0, e1, ptr(M_ + 1, 0);
+    for (int r = 0; r < M_; ++r) {
+      const int a = kind == 2 ? split_h_[r] : rowptr_h_[r];
+      const int b = kind == 1 ? split_h_[r] : rowptr_h_[r + 1];
+      for (int e = a; e < b; e += L) {
+        e0.push_back(e);
+        e1.push_back(std::min(e + L, b));
+      }
+      ptr[r + 1] = (int)e0.size();
+    }
+    pl->n[kind] = (int)e0.size();
+    const size_t nc = std::max<size_t>(e0.size(), 1);
+    pl->e0[kind].alloc(nc);
+    pl->e1[kind].alloc(nc);
+    pl->ptr[kind].alloc(M_ + 1);
+    if (!e0.empty()) {
+      HIP_CHECK(hipMemcpyAsync(pl->e0[kind].get(), e0.data(), sizeof(int) * e0.size(), hipMemcpyHostToDevice, s_));
+      HIP_CHECK(hipMemcpyAsync(pl->e1[kind].get(), e1.data(), sizeof(int) * e1.size(), hipMemcpyHostToDevice, s_));
+    }
+    HIP_CHECK(hipMemcpyAsync(pl->ptr[kind].get(), ptr.data(), sizeof(int) * (M_ + 1), hipMemcpyHostToDevice, s_));
+    HIP_CHECK(hipStreamSynchronize(s_));   // the host vectors go out of scope
+    if (kind == 1 || kind == 2) {
+      std::vector<int>& q = kind == 1 ? pl->lower_q : pl->upper_q;
+      q.resize(K_ + 1);
+      for (int k = 0; k <= K_; ++k) q[k] = ptr[cum_[k]];
+    }
+  }
+  ChunkPlan& ref = *pl;
+  plans_[tc] = std::move(pl);
+  return ref;
+}
+
+GroupedOp GroupedRE::Op(int t) {
+  GroupedOp op;
   op.M = M_;
   op.rowptr = d_rowptr_.get();
   op.split = d_split_.get();
   op.col = d_col_.get();
   op.val = d_val_.get();
+  op.tc = gre_tc(t);
+  const ChunkPlan& pl = Plan(op.tc);
+  GreChunks* ch[3] = {&op.full, &op.lower, &op.upper};
+  for (int kind = 0; kind < 3; ++kind) {
+    ch[kind]->n = pl.n[kind];
+    ch[kind]->e0 = pl.e0[kind].get();
+    ch[kind]->e1 = pl.e1[kind].get();
+    ch[kind]->ptr = pl.ptr[kind].get();
+  }
+  const size_t need = (size_t)std::max(pl.n[0], std::max(pl.n[1], pl.n[2])) * t + 1;
+  if (d_chunk_partials_.size() < need) d_chunk_partials_.alloc(need);
+  op.P = d_chunk_partials_.get();
   return op;
 }
 
@@ -148,11 +200,13 @@ void GroupedRE::Diag(const double* tau) {
 }
 
 void GroupedRE::ApplyA(const double* X, double* Y, int t, bool with_sigma_inv) {
-  launch_gre_apply(Op(), with_sigma_inv ? d_D_.get() : d_cnt_.get(), X, Y, t, s_);
+  launch_gre_apply(Op(t), with_sigma_inv ? d_D_.get() : d_cnt_.get(), X, Y, t, s_);
 }
 
 void GroupedRE::Precond(const double* R, double* Z, double* S, int t) {
-  launch_gre_ssor(Op(), cum_, d_D_.get(), d_sqrtD_.get(), R, S, Z, t, s_);
+  const GroupedOp op = Op(t);
+  const ChunkPlan& pl = Plan(op.tc);
+  launch_gre_ssor(op, cum_, pl.lower_q, pl.upper_q, d_D_.get(), d_sqrtD_.get(), R, S, Z, t, s_);
 }
 
 // CGRandomEffectsVec (block = false; CG_utils.cpp:1100-1230) and CGTridiagRandomEffects (block =
@@ -285,7 +339,7 @@ void GroupedRE::Eval(const double* tau, bool want_grad, bool iterative, bool war
       probes_saved_ = cfg.reuse_rand_vec_trace;
     }
     d_probesP_.alloc((size_t)M_ * t);
-    launch_gre_lds_mult(Op(), d_D_.get(), d_sqrtD_.get(), d_probes_.get(), d_probesP_.get(), t, s_);
+    launch_gre_lds_mult(Op(t), d_D_.get(), d_sqrtD_.get(), d_probes_.get(), d_probesP_.get(), t, s_);
     const int pmax = std::max(1, std::min(cfg.cg_max_num_it_tridiag, M_));
     Block& bt = GetBlock(1, t, pmax);
     const int L = Pcg(bt, d_probesP_.get(), bt.U.get(), true, pmax, cfg.cg_delta_conv);
@@ -335,7 +389,7 @@ void GroupedRE::Eval(const double* tau, bool want_grad, bool iterative, bool war
   d_PI_.alloc((size_t)M_ * t);
   d_DI_.alloc((size_t)M_ * t);
   Precond(d_probesP_.get(), d_PI_.get(), bt.S.get(), t);               // PI_RV = P^-1 z
-  launch_gre_upper(Op(), d_D_.get(), d_PI_.get(), d_DI_.get(), t, s_);  // DI_L_plus_D_t_PI_RV
+  launch_gre_upper(Op(t), d_D_.get(), d_PI_.get(), d_DI_.get(), t, s_);  // DI_L_plus_D_t_PI_RV
   std::vector<double> sums((size_t)3 * t * K_);
   for (int k = 0; k < K_; ++k) {
     const size_t o = (size_t)cum_[k] * t;

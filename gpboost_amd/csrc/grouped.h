@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <map>
 #include <memory>
 #include <vector>
 
@@ -68,7 +69,14 @@ class GroupedRE {
     DevBuf<double> a_hist, b_hist;
   };
   Block& GetBlock(int which, int t, int pmax);
-  GroupedOp Op() const;
+  // Chunk plans of the off-diagonal entries for one lane split tc (grouped_kernels.h)
+  struct ChunkPlan {
+    DevBuf<int> e0[3], e1[3], ptr[3];   // full, lower, upper
+    int n[3] = {0, 0, 0};
+    std::vector<int> lower_q, upper_q;  // K + 1 chunk boundaries of each effect's rows
+  };
+  const ChunkPlan& Plan(int tc);
+  GroupedOp Op(int t);
   void Diag(const double* tau);                              // D, sqrt(D), per-effect sums of log D and 1/D
   void ApplyA(const double* X, double* Y, int t, bool with_sigma_inv);
   void Precond(const double* R, double* Z, double* S, int t); // Z = P^-1 R (S: scratch)
@@ -80,6 +88,9 @@ class GroupedRE {
   int n_, K_, M_;
   hipStream_t s_;
   std::vector<int> m_, cum_;
+  std::vector<int> rowptr_h_, split_h_;
+  std::map<int, std::unique_ptr<ChunkPlan>> plans_;
+  DevBuf<double> d_chunk_partials_;
   DevBuf<int> d_rowptr_, d_split_, d_col_, d_blk_, d_obs_ptr_, d_obs_, d_cum_;
   DevBuf<double> d_val_, d_cnt_, d_D_, d_sqrtD_, d_tau_, d_dsum_;
   DevBuf<double> d_zty_, d_y_, d_yty_, d_u_, d_ztzu_, d_partials_, d_out_;

@@ -1,9 +1,17 @@
-// Device kernels of the grouped-random-effects engine (grouped.h). Blocks of t vectors are row-major
-// M x t (one RE row = t contiguous doubles); row kernels give one wave to a row, lane = column, so a
-// neighbour row's t values are one coalesced gather. The SSOR solves mirror the reference's sparse
-// triangular solves (Eigen, row-major P_SSOR_L_D_sqrt_inv_rm, CG_utils.cpp:1143-1148) operation for
-// operation — same coefficients (L_ij sqrt(1/D_j), diagonal D_i sqrt(1/D_i)), same subtraction order,
-// no FMA contraction — so the PCG iterates round like the reference's.
+// Device kernels of the grouped-random-effects engine (grouped.h).
+//
+// Blocks of t vectors are row-major M x t (one RE row = t contiguous doubles). Every product with
+// a part of A = Sigma^-1 + Z^T Z (the matrix-vector product, the SSOR triangular solves, the probe
+// transform) is a two-phase pass over precomputed entry chunks: phase 1 gives one workgroup to a
+// chunk of one row's entries — tc lanes span the columns (a neighbour row's t values are one
+// coalesced 8t-byte gather), 256 / tc lanes split the chunk's entries — and writes the chunk's
+// partial sum (fixed-order LDS tree); phase 2 gives one thread to each (row, column), adds the
+// row's chunk partials in chunk order and applies the operation's diagonal / solve formula. Rows of
+// crossed effects have very different lengths (config 4: ~90 entries for a level of the 5000-level
+// effect, ~900 for one of the 500-level effect); chunking makes the work per workgroup uniform
+// and gives the chip tens of thousands of workgroups instead of one wave per (long) row. Results
+// are deterministic (no atomics); they differ from the reference's sequential Eigen sums only by
+// summation order.
 #include <hip/hip_runtime.h>
 
 #include "common.h"
@@ -12,20 +20,88 @@
 namespace gpb_amd {
 namespace {
 
-constexpr int kRowsPerBlock = 4;   // one wave per row, 256 threads
+constexpr int kEntriesPerLane = 8;
 
-__device__ __forceinline__ int row_of_block() { return blockIdx.x * kRowsPerBlock + (threadIdx.x >> 6); }
+// Phase 1: P[q * t + c] = sum_{e in chunk q} coef_e X[col_e, c], coef_e = val_e (SCALE = false) or
+// val_e sqrt(1/D_{col_e}) (SCALE = true: the L D^-1/2 factor of the SSOR preconditioner).
+template <int TC, bool SCALE>
+__global__ void __launch_bounds__(256) gre_chunk_kernel(const int* __restrict__ ce0, const int* __restrict__ ce1,
+                                                        int chunk0, const int* __restrict__ col,
+                                                        const double* __restrict__ val, const double* __restrict__ dis,
+                                                        const double* __restrict__ X, int t, double* __restrict__ P) {
+  constexpr int EG = 256 / TC;
+  __shared__ double red[EG][TC];
+  const int q = chunk0 + blockIdx.x;
+  const int lc = threadIdx.x % TC;
+  const int g = threadIdx.x / TC;
+  const int c = blockIdx.y * TC + lc;
+  double s = 0.;
+  if (c < t) {
+    const int e1 = ce1[q];
+    for (int e = ce0[q] + g; e < e1; e += EG) {
+      const int j = col[e];
+      const double coef = SCALE ? val[e] * dis[j] : val[e];
+      s += coef * X[(size_t)j * t + c];
+    }
+  }
+  red[g][lc] = s;
+  __syncthreads();
+#pragma unroll
+  for (int off = EG / 2; off > 0; off >>= 1) {
+    if (g < off) red[g][lc] += red[g + off][lc];
+    __syncthreads();
+  }
+  if (g == 0 && c < t) P[(size_t)q * t + c] = red[0][lc];
+}
 
-// Z^T y, one thread per RE level summing its observations in ascending order (the order of the
-// reference's col-major Zt_ * y_).
+enum GreCombine : int {
+  kCombApply = 0,   // Y = s + dg_r X_r
+  kCombFwd,         // X_r = (R_r - s) / (D_r dis_r)            (lower solve)
+  kCombBwd,         // Z_r = (X_r - dis_r s) / (D_r dis_r)      (upper solve of the transpose)
+  kCombLds,         // Y = s + D_r dis_r R_r                    (probe transform)
+  kCombUpper,       // Y = (1 / D_r) (D_r X_r + s)             (variance reduction)
+};
+
+// Phase 2 over rows [row0, row1): s = the row's chunk partials in chunk order, then the formula.
+// In: the operation's own input (X for apply/upper, R for fwd/lds, X for bwd); Out: its output.
+template <int OP>
+__global__ void __launch_bounds__(256) gre_combine_kernel(int row0, int row1, int t, const int* __restrict__ ptr,
+                                                          const double* __restrict__ P, const double* __restrict__ dg,
+                                                          const double* __restrict__ dis,
+                                                          const double* __restrict__ In, double* __restrict__ Out) {
+  const size_t idx = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t total = (size_t)(row1 - row0) * t;
+  if (idx >= total) return;
+  const int r = row0 + (int)(idx / t);
+  const int c = (int)(idx % t);
+  double s = 0.;
+  for (int q = ptr[r]; q < ptr[r + 1]; ++q) s += P[(size_t)q * t + c];
+  const size_t o = (size_t)r * t + c;
+  if (OP == kCombApply) {
+    Out[o] = s + dg[r] * In[o];
+  } else if (OP == kCombFwd) {
+    Out[o] = (In[o] - s) / (dg[r] * dis[r]);
+  } else if (OP == kCombBwd) {
+    Out[o] = (In[o] - dis[r] * s) / (dg[r] * dis[r]);
+  } else if (OP == kCombLds) {
+    Out[o] = s + (dg[r] * dis[r]) * In[o];
+  } else {
+    Out[o] = (1. / dg[r]) * (dg[r] * In[o] + s);
+  }
+}
+
+// Z^T y: one wave per RE level, lanes stride its observations, fixed-order butterfly.
 __global__ void __launch_bounds__(256) gre_zty_kernel(int M, const int* __restrict__ obs_ptr,
                                                       const int* __restrict__ obs, const double* __restrict__ y,
                                                       double* __restrict__ zty) {
-  const int r = blockIdx.x * 256 + threadIdx.x;
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   if (r >= M) return;
   double s = 0.;
-  for (int e = obs_ptr[r]; e < obs_ptr[r + 1]; ++e) s += y[obs[e]];
-  zty[r] = s;
+  for (int e = obs_ptr[r] + lane; e < obs_ptr[r + 1]; e += 64) s += y[obs[e]];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) zty[r] = s;
 }
 
 // Per effect k (one workgroup each): D_r = 1/tau_k + cnt_r, dis_r = sqrt(1/D_r) (the reference's
@@ -59,89 +135,6 @@ __global__ void __launch_bounds__(256) gre_diag_kernel(int K, const int* __restr
     out[k] = red[0][0];
     out[K + k] = red[1][0];
   }
-}
-
-// Y = A X with A = diag(dg) + offdiag(Z^T Z): per row, entries in ascending column order with the
-// diagonal at its place (Eigen row-major sparse x dense). dg = D (with Sigma^-1) or cnt (Z^T Z only).
-__global__ void __launch_bounds__(256) gre_apply_kernel(GroupedOp op, const double* __restrict__ dg,
-                                                        const double* __restrict__ X, double* __restrict__ Y, int t) {
-#pragma clang fp contract(off)
-  const int r = row_of_block();
-  if (r >= op.M) return;
-  const int c = (threadIdx.x & 63) + blockIdx.y * 64;
-  if (c >= t) return;
-  const int e0 = op.rowptr[r], es = op.split[r], e1 = op.rowptr[r + 1];
-  double s = 0.;
-  for (int e = e0; e < es; ++e) s += op.val[e] * X[(size_t)op.col[e] * t + c];
-  s += dg[r] * X[(size_t)r * t + c];
-  for (int e = es; e < e1; ++e) s += op.val[e] * X[(size_t)op.col[e] * t + c];
-  Y[(size_t)r * t + c] = s;
-}
-
-// probe_P = (L D^-1/2) R: row i sums (L_ij sqrt(1/D_j)) R_j over its lower entries, then the diagonal
-// D_i sqrt(1/D_i) R_i (CG-probe draw from N(0, P), re_model_template.h:2808-2812).
-__global__ void __launch_bounds__(256) gre_lds_mult_kernel(GroupedOp op, const double* __restrict__ D,
-                                                           const double* __restrict__ dis, const double* __restrict__ R,
-                                                           double* __restrict__ Y, int t) {
-#pragma clang fp contract(off)
-  const int r = row_of_block();
-  if (r >= op.M) return;
-  const int c = (threadIdx.x & 63) + blockIdx.y * 64;
-  if (c >= t) return;
-  double s = 0.;
-  for (int e = op.rowptr[r]; e < op.split[r]; ++e) {
-    const int j = op.col[e];
-    s += (op.val[e] * dis[j]) * R[(size_t)j * t + c];
-  }
-  s += (D[r] * dis[r]) * R[(size_t)r * t + c];
-  Y[(size_t)r * t + c] = s;
-}
-
-// Forward solve (L D^-1/2) X = R over the rows of one effect (lower effects already solved).
-__global__ void __launch_bounds__(256) gre_ssor_fwd_kernel(GroupedOp op, int row0, int row1,
-                                                           const double* __restrict__ D, const double* __restrict__ dis,
-                                                           const double* __restrict__ R, double* __restrict__ X, int t) {
-#pragma clang fp contract(off)
-  const int r = row0 + row_of_block();
-  if (r >= row1) return;
-  const int c = (threadIdx.x & 63) + blockIdx.y * 64;
-  if (c >= t) return;
-  double tmp = R[(size_t)r * t + c];
-  for (int e = op.rowptr[r]; e < op.split[r]; ++e) {
-    const int j = op.col[e];
-    tmp -= (op.val[e] * dis[j]) * X[(size_t)j * t + c];
-  }
-  X[(size_t)r * t + c] = tmp / (D[r] * dis[r]);
-}
-
-// Backward solve (L D^-1/2)^T Z = X over the rows of one effect (higher effects already solved).
-// Eigen solves the transposed (column-major upper) system by scattering each solved z_j into the
-// rows above it, j descending; gathered here in that same order.
-__global__ void __launch_bounds__(256) gre_ssor_bwd_kernel(GroupedOp op, int row0, int row1,
-                                                           const double* __restrict__ D, const double* __restrict__ dis,
-                                                           const double* __restrict__ X, double* __restrict__ Z, int t) {
-#pragma clang fp contract(off)
-  const int r = row0 + row_of_block();
-  if (r >= row1) return;
-  const int c = (threadIdx.x & 63) + blockIdx.y * 64;
-  if (c >= t) return;
-  double tmp = X[(size_t)r * t + c];
-  const double di = dis[r];
-  for (int e = op.rowptr[r + 1] - 1; e >= op.split[r]; --e) tmp -= (op.val[e] * di) * Z[(size_t)op.col[e] * t + c];
-  Z[(size_t)r * t + c] = tmp / (D[r] * di);
-}
-
-// DI = D^-1 (upper triangle of A incl. the diagonal) X (variance reduction, re_model_template.h:2327-2336)
-__global__ void __launch_bounds__(256) gre_upper_kernel(GroupedOp op, const double* __restrict__ D,
-                                                        const double* __restrict__ X, double* __restrict__ Y, int t) {
-#pragma clang fp contract(off)
-  const int r = row_of_block();
-  if (r >= op.M) return;
-  const int c = (threadIdx.x & 63) + blockIdx.y * 64;
-  if (c >= t) return;
-  double s = D[r] * X[(size_t)r * t + c];
-  for (int e = op.split[r]; e < op.rowptr[r + 1]; ++e) s += op.val[e] * X[(size_t)op.col[e] * t + c];
-  Y[(size_t)r * t + c] = (1. / D[r]) * s;
 }
 
 // One grouping variable (A diagonal, re_model_template.h:8967-8969, 2279-2296): u = zty / D and the
@@ -180,12 +173,52 @@ __global__ void __launch_bounds__(256) gre_residual_kernel(size_t count, const d
   if (i < count) R[i] = rhs[i] - V[i];
 }
 
-dim3 row_grid(int rows, int t) { return dim3((rows + kRowsPerBlock - 1) / kRowsPerBlock, (t + 63) / 64); }
+template <bool SCALE>
+void chunk_pass(const GroupedOp& op, const GreChunks& ch, int q0, int q1, const double* dis, const double* X, int t,
+                hipStream_t s) {
+  if (q1 <= q0) return;
+  const dim3 grid(q1 - q0, (t + op.tc - 1) / op.tc);
+#define GRE_CHUNK_CASE(TCV)                                                                                         \
+  case TCV:                                                                                                         \
+    hipLaunchKernelGGL((gre_chunk_kernel<TCV, SCALE>), grid, dim3(256), 0, s, ch.e0, ch.e1, q0, op.col,              \
+                       op.val, dis, X, t, op.P);                                                                    \
+    break;
+  switch (op.tc) {
+    GRE_CHUNK_CASE(1)
+    GRE_CHUNK_CASE(2)
+    GRE_CHUNK_CASE(4)
+    GRE_CHUNK_CASE(8)
+    GRE_CHUNK_CASE(16)
+    GRE_CHUNK_CASE(32)
+    GRE_CHUNK_CASE(64)
+    default: Fatal("grouped chunk pass: unsupported lane split %d", op.tc);
+  }
+#undef GRE_CHUNK_CASE
+  HIP_CHECK(hipGetLastError());
+}
+
+template <int OP>
+void combine_pass(const GreChunks& ch, const double* P, int row0, int row1, int t, const double* dg, const double* dis,
+                  const double* In, double* Out, hipStream_t s) {
+  const size_t total = (size_t)(row1 - row0) * t;
+  if (total == 0) return;
+  hipLaunchKernelGGL((gre_combine_kernel<OP>), dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, row0, row1, t,
+                     ch.ptr, P, dg, dis, In, Out);
+  HIP_CHECK(hipGetLastError());
+}
 
 }  // namespace
 
+int gre_tc(int t) {
+  int tc = 1;
+  while (tc < t && tc < 64) tc <<= 1;
+  return tc;
+}
+
+int gre_chunk_len(int tc) { return (256 / tc) * kEntriesPerLane; }
+
 void launch_gre_zty(int M, const int* obs_ptr, const int* obs, const double* y, double* zty, hipStream_t s) {
-  hipLaunchKernelGGL(gre_zty_kernel, dim3((M + 255) / 256), dim3(256), 0, s, M, obs_ptr, obs, y, zty);
+  hipLaunchKernelGGL(gre_zty_kernel, dim3((M + 3) / 4), dim3(256), 0, s, M, obs_ptr, obs, y, zty);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -196,31 +229,33 @@ void launch_gre_diag(int K, const int* cum, const double* cnt, const double* tau
 }
 
 void launch_gre_apply(const GroupedOp& op, const double* dg, const double* X, double* Y, int t, hipStream_t s) {
-  hipLaunchKernelGGL(gre_apply_kernel, row_grid(op.M, t), dim3(256), 0, s, op, dg, X, Y, t);
-  HIP_CHECK(hipGetLastError());
+  chunk_pass<false>(op, op.full, 0, op.full.n, nullptr, X, t, s);
+  combine_pass<kCombApply>(op.full, op.P, 0, op.M, t, dg, nullptr, X, Y, s);
 }
 
 void launch_gre_lds_mult(const GroupedOp& op, const double* D, const double* dis, const double* R, double* Y, int t,
                          hipStream_t s) {
-  hipLaunchKernelGGL(gre_lds_mult_kernel, row_grid(op.M, t), dim3(256), 0, s, op, D, dis, R, Y, t);
-  HIP_CHECK(hipGetLastError());
+  chunk_pass<true>(op, op.lower, 0, op.lower.n, dis, R, t, s);
+  combine_pass<kCombLds>(op.lower, op.P, 0, op.M, t, D, dis, R, Y, s);
 }
 
-void launch_gre_ssor(const GroupedOp& op, const std::vector<int>& cum, const double* D, const double* dis,
-                     const double* R, double* X, double* Z, int t, hipStream_t s) {
+void launch_gre_ssor(const GroupedOp& op, const std::vector<int>& cum, const std::vector<int>& lower_q,
+                     const std::vector<int>& upper_q, const double* D, const double* dis, const double* R, double* X,
+                     double* Z, int t, hipStream_t s) {
   const int K = (int)cum.size() - 1;
-  for (int k = 0; k < K; ++k)
-    hipLaunchKernelGGL(gre_ssor_fwd_kernel, row_grid(cum[k + 1] - cum[k], t), dim3(256), 0, s, op, cum[k], cum[k + 1],
-                       D, dis, R, X, t);
-  for (int k = K - 1; k >= 0; --k)
-    hipLaunchKernelGGL(gre_ssor_bwd_kernel, row_grid(cum[k + 1] - cum[k], t), dim3(256), 0, s, op, cum[k], cum[k + 1],
-                       D, dis, X, Z, t);
-  HIP_CHECK(hipGetLastError());
+  for (int k = 0; k < K; ++k) {   // forward: effects ascending (their lower entries are solved)
+    chunk_pass<true>(op, op.lower, lower_q[k], lower_q[k + 1], dis, X, t, s);
+    combine_pass<kCombFwd>(op.lower, op.P, cum[k], cum[k + 1], t, D, dis, R, X, s);
+  }
+  for (int k = K - 1; k >= 0; --k) {   // backward on the transpose: effects descending
+    chunk_pass<false>(op, op.upper, upper_q[k], upper_q[k + 1], nullptr, Z, t, s);
+    combine_pass<kCombBwd>(op.upper, op.P, cum[k], cum[k + 1], t, D, dis, X, Z, s);
+  }
 }
 
 void launch_gre_upper(const GroupedOp& op, const double* D, const double* X, double* Y, int t, hipStream_t s) {
-  hipLaunchKernelGGL(gre_upper_kernel, row_grid(op.M, t), dim3(256), 0, s, op, D, X, Y, t);
-  HIP_CHECK(hipGetLastError());
+  chunk_pass<false>(op, op.upper, 0, op.upper.n, nullptr, X, t, s);
+  combine_pass<kCombUpper>(op.upper, op.P, 0, op.M, t, D, nullptr, X, Y, s);
 }
 
 void launch_gre_single(int M, const double* zty, const double* cnt, const double* D, double* u, double* out,
