@@ -107,6 +107,42 @@ def cpu_baseline(X, Y, reps: int = 3) -> dict:
             "sample": f"1 eval at n={X.shape[0]} (oracle restatement, 1 thread)"}
 
 
+
+def pmc_ops() -> dict | None:
+    """The latest round's PMC summary of the operator / preconditioner kernels (scripts/pmc_ops_json.py)."""
+    for rnd in ("r03",):
+        path = os.path.join(ROOT, "profiles", rnd, "pmc_ops.json")
+        if os.path.exists(path):
+            with open(path) as f:
+                d = json.load(f)
+            d["path"] = ("rocprofv3 --pmc FETCH_SIZE (x2, gfx950 correction) + WRITE_SIZE, separate passes, "
+                         + os.path.relpath(path, ROOT))
+            return d
+    return None
+
+
+def ops_traffic(ops: dict | None, t: int, part: str) -> float | None:
+    """HBM-side bytes per application of the operator ("operator") or the VADU preconditioner
+    ("preconditioner") at t columns, from the committed PMC summary."""
+    if ops is None:
+        return None
+    return ops.get("columns", {}).get(str(t), {}).get(part + "_bytes")
+
+
+def vadu_bytes(n: int, nnz: int, r: int) -> float:
+    """one VADU application (B^-T solve and ((D^-1+W)B)^-1 solve) to r columns."""
+    return 2 * nnz * 12 + 2 * (n + 1) * 4 + n * 8 + 2 * r * n * 8
+
+
+def vadu_roofline(n: int, nnz: int, r: int, ms: float, ops: dict | None) -> dict:
+    b = vadu_bytes(n, nnz, r)
+    ach = b / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "traffic": ops_traffic(ops, r, "preconditioner"), "kernel_ms": ms, "columns": r,
+            "algorithmic_bytes_per_launch": b,
+            "note": "latency-bound dependency chain (sparse triangular solves over the Vecchia DAG), not bandwidth"}
+
+
 LATENT_T = 50                     # num_rand_vec_trace (reference default, re_model_template.h:5376)
 LATENT_PARS = [1.0, 0.1]          # sigma1^2, rho (original scale); Gaussian error variance (aux) 0.1
 
@@ -187,26 +223,23 @@ def latent_leg(X, Y, steps: int, cpu: bool) -> dict:
                            "launches": int(nlev), "us_per_launch": ms_p * 1e3 / max(nlev, 1),
                            "share_of_eval": None},
     }
-    pmc = os.path.join(ROOT, "profiles", "r01", "pmc_latent_apply.json")
-    if os.path.exists(pmc) and r == 51:   # HBM bytes per application from the committed PMC passes
-        with open(pmc) as f:
-            p = json.load(f)
-        leg["cg_matvec_roofline"]["traffic"] = p["bytes_per_application"]
-        leg["cg_matvec_roofline"]["traffic_source"] = ("rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
-                                                       + os.path.relpath(pmc, ROOT))
+    # HBM-side bytes per application from the committed PMC passes of the same operator kernels
+    # (scripts/gpu_pmc_ops.sh -> profiles/<round>/pmc_ops.json; FETCH_SIZE doubled, see there)
+    ops = pmc_ops()
+    if ops is not None:
+        leg["cg_matvec_roofline"]["traffic"] = ops_traffic(ops, r, "operator")
+        leg["cg_matvec_roofline"]["traffic_source"] = ops["path"]
     # the single-vector CG of the Newton / mode-finding solves (CGVecchiaLaplaceVec, CG_utils.cpp:21-108)
     ms_a1, ms_p1, _, _ = gm.bench_latent_operators(1, 50)
     byts1 = latent_matvec_bytes(n, int(nnz), 1)
     ach1 = byts1 / (ms_a1 * 1e-3) / 1e9
-    tr1 = None   # HBM-side bytes per application from the committed PMC passes (profiles/r02/pmc_op1_traffic.json)
-    pth = os.path.join(ROOT, "profiles", "r02", "pmc_op1_traffic.json")
-    if os.path.exists(pth):
-        with open(pth) as f:
-            tr1 = json.load(f).get("bytes_per_application")
     leg["cg_matvec_roofline_single"] = {"bound": "hbm", "achieved": ach1, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                                        "frac": ach1 / HBM_PEAK_GBS, "traffic": tr1,
-                                        "kernel": "b_apply1e (ELL) + bt_apply1s (segmented runs)", "kernel_ms": ms_a1, "columns": 1,
+                                        "frac": ach1 / HBM_PEAK_GBS,
+                                        "traffic": ops_traffic(ops, 1, "operator") if ops else None,
+                                        "kernel": "b_apply1e (ELL) + bt_apply1p (paired segmented runs)", "kernel_ms": ms_a1, "columns": 1,
                                         "algorithmic_bytes_per_launch": byts1, "preconditioner_ms": ms_p1}
+    leg["preconditioner"]["roofline"] = vadu_roofline(n, int(nnz), r, ms_p, ops)
+    leg["preconditioner"]["roofline_single"] = vadu_roofline(n, int(nnz), 1, ms_p1, ops)
     its = int(info[2])
     leg["preconditioner"]["share_of_eval"] = min(1.0, its * ms_p / (t_med * 1e3)) if its > 0 else None
     if cpu:
@@ -218,11 +251,42 @@ DENSE_N = 20_000                  # BASELINE config 2: dense Cholesky fp64 on on
 DENSE_CPU_N = 4_000               # bounded CPU sample of the same unit (the n=20000 unit is ~800 s)
 
 
-def bernoulli_leg(X, steps: int) -> dict:
+def bernoulli_cpu_baseline(X, y) -> dict | None:
+    """The reference's bernoulli_logit Laplace evaluation (Vecchia m = 30, iterative, VADU, default
+    settings) on this host: one nll + gradient evaluation (oracle/_ref/ref_harness; ~30-45 s)."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(harness):
+        return None
+    import numpy as np
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", str(os.cpu_count() or 1))), 16))
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(np.array([X.shape[0], X.shape[1]], dtype=np.int32).tobytes())
+        f.write(np.ascontiguousarray(X.T).tobytes())
+        f.write(np.ascontiguousarray(y, dtype=np.float64).tobytes())
+        path = f.name
+    try:
+        out = subprocess.run([harness, path, "cov_fct=exponential", "gp_approx=vecchia", "likelihood=bernoulli_logit",
+                              "matrix_inversion_method=iterative", f"num_neighbors={M_NEIGHBORS}", "ordering=random",
+                              "cov_pars=" + ",".join(map(str, LATENT_PARS)), "cg_delta_conv=1e-2",
+                              f"num_rand_vec_trace={LATENT_T}", "seed_rand_vec_trace=1", "reps=1", "mode=eval"],
+                             capture_output=True, text=True, timeout=600,
+                             env=dict(os.environ, OMP_NUM_THREADS=str(threads)), check=True)
+        r = json.loads(out.stdout)
+        t = r["median_time"]
+        return {"value": 1.0 / t, "unit": "evals/s", "cores": threads, "kind": "reference",
+                "sample": f"1 bernoulli_logit Laplace eval at n={X.shape[0]} (nll+grad, {t:.2f} s/eval; "
+                          f"construction {r['t_construct']:.2f} s excluded)", "nll": r["nll"], "grad": r["grad"]}
+    except Exception as e:  # noqa: BLE001
+        sys.stderr.write(f"reference bernoulli CPU baseline failed: {e}\n")
+        return None
+    finally:
+        os.unlink(path)
+
+
+def bernoulli_leg(X, steps: int, cpu: bool) -> dict:
     """BASELINE config 5: bernoulli_logit Laplace approximation with Vecchia m = 30 and iterative
-    methods (Newton mode finding by PCG, SLQ log-determinant, stochastic-trace gradient), n = 100k.
-    The reference's evaluation of the same data takes minutes on the host cores (measured in the
-    build container), beyond this script's bounded CPU sample, so none is timed here."""
+    methods (Newton mode finding by PCG, SLQ log-determinant, stochastic-trace gradient), n = 100k;
+    the reference's own evaluation of the same data on the host cores beside it (one evaluation)."""
     import numpy as np
 
     from gpboost_amd import GPModel, synthetic
@@ -238,13 +302,18 @@ def bernoulli_leg(X, steps: int) -> dict:
         ts.append(time.perf_counter() - t0)
     info = gm.last_iteration_info()
     t_med = float(np.median(ts))
-    return {"metric": "bernoulli_logit Laplace (Vecchia, iterative) neg-log-lik + grad evals/sec, n=100k m=30",
-            "value": 1.0 / t_med, "unit": "evals/s", "steps": steps, "ms_per_step": t_med * 1e3,
-            "config": {"workload": "vecchia_bernoulli_logit_laplace_iterative_vadu", "n": X.shape[0],
-                       "num_neighbors": M_NEIGHBORS, "cov_pars": LATENT_PARS, "num_rand_vec_trace": LATENT_T,
-                       "cg_delta_conv": 1e-2, "nll": nll, "grad": [float(v) for v in g],
-                       "newton_its": int(info[0]), "cg_its_mode": int(info[1]), "lanczos_steps": int(info[2])},
-            "cpu_baseline": None}
+    n = X.shape[0]
+    ms_a, ms_p, nnz, nlev = gm.bench_latent_operators(LATENT_T, 10)
+    leg = {"metric": "bernoulli_logit Laplace (Vecchia, iterative) neg-log-lik + grad evals/sec, n=100k m=30",
+           "value": 1.0 / t_med, "unit": "evals/s", "steps": steps, "ms_per_step": t_med * 1e3,
+           "config": {"workload": "vecchia_bernoulli_logit_laplace_iterative_vadu", "n": n,
+                      "num_neighbors": M_NEIGHBORS, "cov_pars": LATENT_PARS, "num_rand_vec_trace": LATENT_T,
+                      "cg_delta_conv": 1e-2, "nll": nll, "grad": [float(v) for v in g],
+                      "newton_its": int(info[0]), "cg_its_mode": int(info[1]), "lanczos_steps": int(info[2])},
+           "preconditioner": {"ms": ms_p, "launches": int(nlev),
+                              "roofline": vadu_roofline(n, int(nnz), LATENT_T, ms_p, None)},
+           "cpu_baseline": bernoulli_cpu_baseline(X, y) if cpu else None}
+    return leg
 
 
 GROUPED_N = 500_000               # BASELINE config 4 (expressible proxy)
@@ -626,7 +695,7 @@ def main():
     if world == 1 and not args.no_latent:
         del gm
         line["latent_iterative"] = latent_leg(X, Y, args.latent_steps, not args.no_cpu_baseline)
-        line["bernoulli_laplace"] = bernoulli_leg(X, args.latent_steps)
+        line["bernoulli_laplace"] = bernoulli_leg(X, args.latent_steps, not args.no_cpu_baseline)
     elif latent_sharded is not None:
         line["latent_iterative"] = latent_sharded
     print(json.dumps(line))

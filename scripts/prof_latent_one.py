@@ -1,6 +1,7 @@
 """One warm-up and one profiled latent Vecchia nll+grad evaluation at n = 100k (for rocprofv3 kernel
-traces; run with GPBOOST_AMD_NO_GRAPH=1: the profiler's tracer does not survive hipGraph replay
-on this image, so the same kernels are launched eagerly)."""
+traces and PMC passes). rocprofv3 --kernel-trace traces the default hipGraph replay path on this image
+(profiles/r03/graph_replay_trace_result_r03.txt); GPBOOST_AMD_NO_GRAPH=1 launches the same kernels
+eagerly, which the PMC scripts use so that every dispatch is attributed."""
 import os
 import sys
 import time
