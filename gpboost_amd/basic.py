@@ -303,10 +303,14 @@ class GPModel:
 
     def predict_training_data_random_effects(self, predict_var=False):
         """Predicted training-data random effects (GPB_PredictREModelTrainingDataRandomEffects,
-        reference basic.py:6316-6367): (n,) means, or (n, 2) [mean, variance] with predict_var."""
-        out = np.zeros(2 * self.num_data if predict_var else self.num_data)
+        reference basic.py:6316-6367): (n,) means, or (n, 2) [mean, variance] with predict_var; grouped
+        models: (n, K) means per effect, or (n, 2K) [means..., variances...]."""
+        k = max(1, getattr(self, "num_group_re", 0))
+        out = np.zeros((2 if predict_var else 1) * k * self.num_data)
         _safe_call(lib().GPB_PredictREModelTrainingDataRandomEffects(self.handle, None, None, _dp(out), None,
                                                                      ctypes.c_bool(bool(predict_var))))
+        if getattr(self, "num_group_re", 0):
+            return out.reshape(-1, self.num_data).T.copy()
         return out.reshape(2, -1).T.copy() if predict_var else out
 
     def _get_string(self, fn):
@@ -551,12 +555,15 @@ class GPModel:
         """Predictions at new coordinates (reference basic.py:5778-6093, GPB_PredictREModel): returns
         {"mu": mean, "cov": covariance or None, "var": variances or None}. Exact Gaussian Vecchia
         models, vecchia_pred_type "order_obs_first_cond_obs_only"."""
+        if getattr(self, "num_group_re", 0):
+            return self._predict_grouped(group_data_pred, predict_var, predict_cov_mat, predict_response, y, cov_pars,
+                                         offset, offset_pred, fixed_effects, fixed_effects_pred)
         if vecchia_pred_type is not None or num_neighbors_pred is not None:
             self.set_prediction_data(vecchia_pred_type=vecchia_pred_type, num_neighbors_pred=num_neighbors_pred)
         if any(v is not None for v in (group_data_pred, group_rand_coef_data_pred, gp_rand_coef_data_pred,
                                        cluster_ids_pred)):
             raise GPBoostError("predictions with grouped random effects, random coefficients or clusters are not "
-                               "supported by gpboost_amd")
+                               "supported by gpboost_amd for GP models")
         xpc = None
         if X_pred is not None:
             Xp = np.asarray(X_pred, dtype=np.float64)
@@ -597,6 +604,39 @@ class GPModel:
         if predict_cov_mat and predict_var:
             var = np.diag(cov).copy()
         return {"mu": mu, "cov": cov, "var": var}
+
+    def _predict_grouped(self, group_data_pred, predict_var, predict_cov_mat, predict_response, y, cov_pars, offset,
+                         offset_pred, fixed_effects, fixed_effects_pred):
+        """Predictive means of a grouped random effects model at new group labels (GPB_PredictREModel
+        with re_group_data_pred): sum over the effects of the training posterior mean of the label's
+        level, 0 for a level not seen in training."""
+        if group_data_pred is None:
+            raise ValueError("'group_data_pred' is missing")
+        g = np.asarray(group_data_pred)
+        if g.ndim == 1:
+            g = g.reshape(-1, 1)
+        if g.shape[1] != self.num_group_re:
+            raise ValueError("Incorrect number of columns in 'group_data_pred'")
+        n_pred = g.shape[0]
+        labels = g.astype(np.dtype(str)).flatten(order="F")
+        buf = ctypes.create_string_buffer(b"\0".join(s.encode() for s in labels) + b"\0")
+        yv = self._check_y(y)
+        if offset is not None:
+            fixed_effects = offset if fixed_effects is None else np.asarray(fixed_effects) + np.asarray(offset)
+        if offset_pred is not None:
+            fixed_effects_pred = offset_pred if fixed_effects_pred is None else (
+                np.asarray(fixed_effects_pred) + np.asarray(offset_pred))
+        fe = _as1d(fixed_effects, "fixed_effects") if fixed_effects is not None else None
+        fep = _as1d(fixed_effects_pred, "fixed_effects_pred") if fixed_effects_pred is not None else None
+        cp = self._check_cov_pars(cov_pars) if cov_pars is not None else None
+        out = np.zeros(n_pred)
+        _safe_call(lib().GPB_PredictREModel(
+            self.handle, _dp(yv) if yv is not None else None, ctypes.c_int32(n_pred), _dp(out),
+            ctypes.c_bool(bool(predict_cov_mat)), ctypes.c_bool(bool(predict_var)),
+            ctypes.c_bool(bool(predict_response)), None, buf, None, None, None,
+            _dp(cp) if cp is not None else None, None, ctypes.c_bool(False),
+            _dp(fe) if fe is not None else None, _dp(fep) if fep is not None else None))
+        return {"mu": out, "cov": None, "var": None}
 
     def set_distributed(self, rank: int, world_size: int, comm_id: bytes | None):
         """Join an RCCL communicator (GPB_SetDistributed): exact Vecchia shards rows, latent

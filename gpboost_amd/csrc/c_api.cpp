@@ -151,8 +151,9 @@ int GPB_CreateREModel(int32_t num_data, const int32_t* cluster_ids_data, const c
       gpb_amd::Fatal("grouped random effects with likelihood '%s' are not supported by gpboost_amd (supported: gaussian)",
                      likelihood);
     if (num_data <= 0) gpb_amd::Fatal("num_data must be > 0");
-    auto levels = gpb_amd::parse_group_levels(num_data, num_re_group, re_group_data);
-    auto* g = new GroupedModel(num_data, levels, str_or(matrix_inversion_method, "default"), seed);
+    std::vector<std::unordered_map<std::string, int>> index;
+    auto levels = gpb_amd::parse_group_levels(num_data, num_re_group, re_group_data, &index);
+    auto* g = new GroupedModel(num_data, levels, str_or(matrix_inversion_method, "default"), seed, std::move(index));
     {
       std::lock_guard<std::mutex> lk(g_grouped_mu);
       g_grouped.insert(g);
@@ -301,6 +302,15 @@ int GPB_PredictREModel(REModelHandle handle, const double* y_data, int32_t num_d
   API_BEGIN();
   if (out_predict == nullptr) gpb_amd::Fatal("out_predict is NULL");
   if (use_saved_data) gpb_amd::Fatal("use_saved_data: saved prediction data is not supported by gpboost_amd");
+  if (GroupedModel* g = as_grouped(handle)) {
+    if (cluster_ids_data_pred != nullptr || re_group_rand_coef_data_pred != nullptr || gp_coords_data_pred != nullptr ||
+        gp_rand_coef_data_pred != nullptr || covariate_data_pred != nullptr)
+      gpb_amd::Fatal("predictions with clusters, random coefficients, GP coordinates or covariates are not supported "
+                     "for grouped random effects models by gpboost_amd");
+    g->Predict(y_data, num_data_pred, re_group_data_pred, cov_pars, predict_cov_mat, predict_var, fixed_effects,
+               fixed_effects_pred, out_predict);
+    return 0;
+  }
   if (cluster_ids_data_pred != nullptr || re_group_data_pred != nullptr || re_group_rand_coef_data_pred != nullptr ||
       gp_rand_coef_data_pred != nullptr)
     gpb_amd::Fatal("predictions with clusters, grouped random effects or random coefficients are not "
@@ -459,6 +469,10 @@ int GPB_PredictREModelTrainingDataRandomEffects(REModelHandle handle, const doub
                                                 double* out_predict, const double* fixed_effects, bool calc_var) {
   API_BEGIN();
   if (out_predict == nullptr) gpb_amd::Fatal("out_predict is NULL");
+  if (GroupedModel* g = as_grouped(handle)) {
+    g->PredictTrainingDataRandomEffects(cov_pars_pred, y_obs, out_predict, fixed_effects, calc_var);
+    return 0;
+  }
   model(handle)->PredictTrainingDataRandomEffects(cov_pars_pred, y_obs, out_predict, fixed_effects, calc_var);
   API_END();
 }

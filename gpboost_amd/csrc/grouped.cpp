@@ -281,8 +281,7 @@ int GroupedRE::Pcg(Block& b, const double* RHS, double* U, bool block, int pmax,
   return its;
 }
 
-void GroupedRE::Eval(const double* tau, bool want_grad, bool iterative, bool warm, const IterativeConfig& cfg,
-                     GroupedParts& out) {
+void GroupedRE::CheckMethod(const double* tau, bool iterative) const {
   if (!y_set_) Fatal("response variable y has not been set");
   for (int k = 0; k < K_; ++k)
     if (!(tau[k] > 0.)) Fatal("covariance parameters must be > 0");
@@ -293,22 +292,63 @@ void GroupedRE::Eval(const double* tau, bool want_grad, bool iterative, bool war
   if (!iterative && K_ > 1)
     Fatal("matrix_inversion_method 'cholesky' with several grouped random effects is not supported by gpboost_amd "
           "(supported: iterative)");
-  out = GroupedParts();
-  out.quad.assign(K_, 0.);
-  out.trace.assign(K_, 0.);
-  Diag(tau);
-  // ---- u = A^-1 Z^T y (CalcYAux, re_model_template.h:8985-9003)
-  int t = 1;
-  double* single_sums = h_out_ + kOut - 2;   // pinned, read after the next synchronisation
+}
+
+// u = A^-1 Z^T y (CalcYAux, re_model_template.h:8965-9003): K == 1 closed form (single_sums: the
+// pinned slots receiving sum cnt and sum cnt^2 / D), else SSOR-PCG. Returns the PCG iterations.
+int GroupedRE::SolveU(bool iterative, bool warm, const IterativeConfig& cfg, double* single_sums) {
+  int its = 0;
   if (!iterative) {   // A diagonal: u = Z^T y / D
     launch_gre_single(M_, d_zty_.get(), d_cnt_.get(), d_D_.get(), d_u_.get(), d_out_.get() + kOut - 2, s_);
     HIP_CHECK(hipMemcpyAsync(single_sums, d_out_.get() + kOut - 2, sizeof(double) * 2, hipMemcpyDeviceToHost, s_));
   } else {
     Block& b1 = GetBlock(0, 1, std::max(cfg.cg_max_num_it, 1));
-    out.cg_its = Pcg(b1, d_zty_.get(), d_u_.get(), false, std::max(cfg.cg_max_num_it, 1), cfg.cg_delta_conv,
-                     warm && u_valid_);
+    its = Pcg(b1, d_zty_.get(), d_u_.get(), false, std::max(cfg.cg_max_num_it, 1), cfg.cg_delta_conv,
+              warm && u_valid_);
   }
   u_valid_ = true;
+  return its;
+}
+
+void GroupedRE::Blup(const double* tau, bool iterative, bool warm, const IterativeConfig& cfg, double* b,
+                     double* var) {
+  // PredictTrainingDataRandomEffects, grouped branch (re_model_template.h:4065-4167): posterior means
+  // tau_k Z_k^T Psi^-1 y = tau_k (Z^T y - Z^T Z u)_k; K == 1 variances tau (1 - tau (cnt - cnt^2 / D))
+  CheckMethod(tau, iterative);
+  Diag(tau);
+  double* single_sums = h_out_ + kOut - 2;
+  SolveU(iterative, warm, cfg, single_sums);
+  ApplyA(d_u_.get(), d_ztzu_.get(), 1, false);
+  std::vector<double> zty(M_), ztzu(M_), D, cnt;
+  HIP_CHECK(hipMemcpyAsync(zty.data(), d_zty_.get(), sizeof(double) * M_, hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipMemcpyAsync(ztzu.data(), d_ztzu_.get(), sizeof(double) * M_, hipMemcpyDeviceToHost, s_));
+  if (var != nullptr) {
+    D.resize(M_);
+    cnt.resize(M_);
+    HIP_CHECK(hipMemcpyAsync(D.data(), d_D_.get(), sizeof(double) * M_, hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipMemcpyAsync(cnt.data(), d_cnt_.get(), sizeof(double) * M_, hipMemcpyDeviceToHost, s_));
+  }
+  HIP_CHECK(hipStreamSynchronize(s_));
+  for (int k = 0; k < K_; ++k)
+    for (int r = cum_[k]; r < cum_[k + 1]; ++r) {
+      b[r] = tau[k] * (zty[r] - ztzu[r]);
+      if (var != nullptr) {
+        const double ma = cnt[r] / std::sqrt(D[r]);   // M_aux (:4088-4091)
+        var[r] = tau[k] - tau[k] * tau[k] * (cnt[r] - ma * ma);
+      }
+    }
+}
+
+void GroupedRE::Eval(const double* tau, bool want_grad, bool iterative, bool warm, const IterativeConfig& cfg,
+                     GroupedParts& out) {
+  CheckMethod(tau, iterative);
+  out = GroupedParts();
+  out.quad.assign(K_, 0.);
+  out.trace.assign(K_, 0.);
+  Diag(tau);
+  int t = 1;
+  double* single_sums = h_out_ + kOut - 2;   // pinned, read after the next synchronisation
+  out.cg_its = SolveU(iterative, warm, cfg, single_sums);
   // y^T Psi^-1 y = y^T y - (Z^T y)^T u ; the per-effect sums of log D and 1/D
   {
     const double* A[1] = {d_zty_.get()};

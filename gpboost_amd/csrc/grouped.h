@@ -60,6 +60,9 @@ class GroupedRE {
   void Eval(const double* tau, bool want_grad, bool iterative, bool warm, const IterativeConfig& cfg,
             GroupedParts& out);
   bool has_solution() const { return u_valid_; }
+  // Posterior means of the M random effects (host, effect-major): tau_k Z_k^T Psi^-1 y; var
+  // (nullable, K == 1 only): their posterior variances on the transformed scale.
+  void Blup(const double* tau, bool iterative, bool warm, const IterativeConfig& cfg, double* b, double* var);
 
  private:
   struct Block {   // work space of a t-column PCG
@@ -69,6 +72,8 @@ class GroupedRE {
     DevBuf<double> a_hist, b_hist;
   };
   Block& GetBlock(int which, int t, int pmax);
+  void CheckMethod(const double* tau, bool iterative) const;
+  int SolveU(bool iterative, bool warm, const IterativeConfig& cfg, double* single_sums);
   // Chunk plans of the off-diagonal entries for one lane split tc (grouped_kernels.h)
   struct ChunkPlan {
     DevBuf<int> e0[3], e1[3], ptr[3];   // full, lower, upper

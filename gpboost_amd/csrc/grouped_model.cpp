@@ -9,12 +9,15 @@
 
 namespace gpb_amd {
 
-std::vector<std::vector<int>> parse_group_levels(int n, int K, const char* re_group_data) {
+std::vector<std::vector<int>> parse_group_levels(int n, int K, const char* re_group_data,
+                                                 std::vector<std::unordered_map<std::string, int>>* label_index) {
   if (re_group_data == nullptr) Fatal("re_group_data is NULL");
   std::vector<std::vector<int>> levels(K, std::vector<int>(n));
+  if (label_index) label_index->assign(K, {});
   const char* p = re_group_data;
   for (int k = 0; k < K; ++k) {
-    std::unordered_map<std::string, int> index;
+    std::unordered_map<std::string, int> local;
+    std::unordered_map<std::string, int>& index = label_index ? (*label_index)[k] : local;
     index.reserve(1024);
     for (int i = 0; i < n; ++i) {
       std::string label(p);
@@ -27,8 +30,9 @@ std::vector<std::vector<int>> parse_group_levels(int n, int K, const char* re_gr
   return levels;
 }
 
-GroupedModel::GroupedModel(int n, const std::vector<std::vector<int>>& levels, const std::string& mim, int seed)
-    : n_(n), mim_(mim) {
+GroupedModel::GroupedModel(int n, const std::vector<std::vector<int>>& levels, const std::string& mim, int seed,
+                           std::vector<std::unordered_map<std::string, int>> label_index)
+    : n_(n), mim_(mim), levels_(levels), label_index_(std::move(label_index)) {
   (void)seed;   // grouped models draw no random numbers at construction (probes use seed_rand_vec_trace)
   if (n <= 0) Fatal("num_data must be > 0");
   const int K = (int)levels.size();
@@ -252,6 +256,73 @@ void GroupedModel::OptimCovPar(const double* y, const double* fixed_effects) {
   cov_pars_initialized_ = true;
   last_nll_ = fx;
   last_cov_pars_ = cov_pars_orig_;
+}
+
+std::vector<double> GroupedModel::Blup(const double* cov_pars, const double* y, const double* fixed_effects,
+                                       std::vector<double>* var) {
+  UseDevice();
+  const int K = re_->K();
+  std::vector<double> cp;
+  if (cov_pars != nullptr) cp.assign(cov_pars, cov_pars + 1 + K);
+  else if (!last_cov_pars_.empty()) cp = last_cov_pars_;
+  else Fatal("Covariance parameters have not been estimated or correctly set ");
+  for (double v : cp)
+    if (!(v > 0.)) Fatal("covariance parameters must be > 0");
+  if (y != nullptr || fixed_effects != nullptr) SetResponseAndOffset(y, fixed_effects);
+  if (!y_set_) Fatal("Response variable data is not provided and has not been set before");
+  std::vector<double> tau(K);
+  for (int k = 0; k < K; ++k) tau[k] = cp[1 + k] / cp[0];
+  std::vector<double> b(re_->M());
+  if (var) var->assign(re_->M(), 0.);
+  re_->Blup(tau.data(), iterative(), num_iter_ > 0, iter, b.data(), var ? var->data() : nullptr);
+  if (var)
+    for (double& v : *var) v *= cp[0];   // transformed -> original scale (cov_pars[0] x ..., :4095)
+  return b;
+}
+
+void GroupedModel::PredictTrainingDataRandomEffects(const double* cov_pars, const double* y, double* out,
+                                                    const double* fixed_effects, bool calc_var) {
+  const int K = re_->K();
+  if (calc_var && iterative())
+    Fatal("PredictTrainingDataRandomEffects() is currently not implemented for matrix_inversion_method_ == '%s' and "
+          "likelihood == 'Gaussian'. Call the predict() function instead.", mim_.c_str());
+  std::vector<double> var;
+  const std::vector<double> b = Blup(cov_pars, y, fixed_effects, calc_var ? &var : nullptr);
+  const std::vector<int>& cum_m = re_->levels_per_effect();
+  int off = 0;
+  for (int k = 0; k < K; ++k) {
+    for (int i = 0; i < n_; ++i) {
+      out[(size_t)k * n_ + i] = b[off + levels_[k][i]];
+      if (calc_var) out[(size_t)K * n_ + (size_t)k * n_ + i] = var[off + levels_[k][i]];
+    }
+    off += cum_m[k];
+  }
+}
+
+void GroupedModel::Predict(const double* y, int n_pred, const char* re_group_data_pred, const double* cov_pars,
+                           bool predict_cov_mat, bool predict_var, const double* fixed_effects,
+                           const double* fixed_effects_pred, double* out) {
+  if (predict_cov_mat || predict_var)
+    Fatal("predictive (co)variances for grouped random effects are not supported by gpboost_amd (predictive means "
+          "only)");
+  if (n_pred <= 0) Fatal("num_data_pred must be > 0");
+  if (re_group_data_pred == nullptr) Fatal("re_group_data_pred must be provided for grouped random effects");
+  const int K = re_->K();
+  if ((int)label_index_.size() != K) Fatal("the model has no label index (created without re_group_data)");
+  const std::vector<double> b = Blup(cov_pars, y, fixed_effects, nullptr);
+  std::vector<double> mu(n_pred, 0.);
+  const char* p = re_group_data_pred;
+  int off = 0;
+  for (int k = 0; k < K; ++k) {   // labels column-major, as re_group_data (re_model_template.h:3081-3085)
+    for (int i = 0; i < n_pred; ++i) {
+      std::string label(p);
+      p += label.size() + 1;
+      auto it = label_index_[k].find(label);
+      if (it != label_index_[k].end()) mu[i] += b[off + it->second];   // a new level contributes 0
+    }
+    off += re_->levels_per_effect()[k];
+  }
+  for (int i = 0; i < n_pred; ++i) out[i] = mu[i] + (fixed_effects_pred ? fixed_effects_pred[i] : 0.);
 }
 
 }  // namespace gpb_amd

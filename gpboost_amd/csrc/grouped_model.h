@@ -11,6 +11,7 @@
 
 #include <memory>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "grouped.h"
@@ -25,7 +26,7 @@ class GroupedModel {
   // re_comp.h:245-264). matrix_inversion_method: "default" -> "iterative" for K >= 2, "cholesky"
   // for K == 1 (UseIterativeByDefault, re_model_template.h:6719-6724).
   GroupedModel(int n, const std::vector<std::vector<int>>& levels, const std::string& matrix_inversion_method,
-               int seed);
+               int seed, std::vector<std::unordered_map<std::string, int>> label_index = {});
   ~GroupedModel();
 
   int n() const { return n_; }
@@ -60,17 +61,32 @@ class GroupedModel {
   // GPB_GetNumCGSteps / GetNumCGStepsTridiag (re_model_template.h:527-552)
   int num_cg_steps() const { return last_cg_its_; }
   int num_cg_steps_tridiag() const { return last_lanczos_; }
+  // GPB_PredictREModelTrainingDataRandomEffects (re_model.cpp -> PredictTrainingDataRandomEffects,
+  // grouped branch re_model_template.h:4065-4167): out[k n + i] = posterior mean of effect k at
+  // observation i's level; calc_var (K == 1 only, as the reference's iterative branch refuses it):
+  // out[K n + k n + i] = its posterior variance. cov_pars original scale (null: the last ones).
+  void PredictTrainingDataRandomEffects(const double* cov_pars, const double* y, double* out,
+                                        const double* fixed_effects, bool calc_var);
+  // GPB_PredictREModel with re_group_data_pred (CalcPred, re_model_template.h:10026-): the
+  // predictive means sum_k b_k(level) (0 for levels not in the training data) + fixed_effects_pred.
+  void Predict(const double* y, int n_pred, const char* re_group_data_pred, const double* cov_pars,
+               bool predict_cov_mat, bool predict_var, const double* fixed_effects, const double* fixed_effects_pred,
+               double* out);
   IterativeConfig iter;
 
  private:
   void UseDevice() const;
   void FindInitCovPar(const double* y, double* trafo) const;
+  std::vector<double> Blup(const double* cov_pars, const double* y, const double* fixed_effects,
+                           std::vector<double>* var);
 
   int n_;
   int device_ = 0;
   std::string mim_;
   hipStream_t stream_ = nullptr;
   std::unique_ptr<GroupedRE> re_;
+  std::vector<std::vector<int>> levels_;                       // K x n
+  std::vector<std::unordered_map<std::string, int>> label_index_;   // label -> level, per effect
   std::vector<double> y_raw_, y_;
   bool y_set_ = false;
 
@@ -85,6 +101,8 @@ class GroupedModel {
 
 // Parses re_group_data (column-major K x n NUL-terminated labels, re_model_template.h:6246-6270)
 // into level indices numbered in order of first appearance per effect.
-std::vector<std::vector<int>> parse_group_levels(int n, int K, const char* re_group_data);
+// label_index (nullable) receives the per-effect label -> level maps.
+std::vector<std::vector<int>> parse_group_levels(int n, int K, const char* re_group_data,
+                                                 std::vector<std::unordered_map<std::string, int>>* label_index = nullptr);
 
 }  // namespace gpb_amd

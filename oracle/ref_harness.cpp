@@ -288,12 +288,15 @@ int main(int argc, char** argv) {
   }
 
   if (mode == "pred_train") {
-    // GPB_PredictREModelTrainingDataRandomEffects at cov_pars (re_model.cpp -> PredictTrainingDataRandomEffects)
-    std::vector<double> out((size_t)2 * n, 0.);
-    m->PredictTrainingDataRandomEffects(trafo.data(), nullptr, y.data(), out.data(), true, nullptr, gauss);
+    // GPB_PredictREModelTrainingDataRandomEffects at cov_pars (re_model.cpp -> PredictTrainingDataRandomEffects):
+    // one block of n means per random-effect component (grouped: K), then the variances (calc_var)
+    const int ncomp = std::max(1, (int)num_re_group);
+    const bool calc_var = gauss && get(args, "calc_var", "1") == "1";
+    std::vector<double> out((size_t)2 * n * ncomp, 0.);
+    m->PredictTrainingDataRandomEffects(trafo.data(), nullptr, y.data(), out.data(), true, nullptr, calc_var);
     std::printf("{\n\"n\": %d, \"d\": %d,\n", n, d);
-    print_vec("mean", out.data(), n);
-    if (gauss) print_vec("var", out.data() + n, n);
+    print_vec("mean", out.data(), n * ncomp);
+    if (calc_var) print_vec("var", out.data() + (size_t)n * ncomp, n * ncomp);
     std::printf("\"ok\": true\n}\n");
     return 0;
   }

@@ -47,6 +47,29 @@ def fit_case(n, levels, **opts):
                 nll=ft["nll"], num_it=ft["num_it"], fit_time=ft["fit_time"], wall=time.time() - t0)
 
 
+def pred_case(n, levels, cov_pars, calc_var, **opts):
+    g = synthetic.bench_groups(n, levels)
+    y = synthetic.bench_grouped_y(g)
+    r = run_ref(None, y, groups=g, cov_pars=fmt_pars(cov_pars), mode="pred_train", calc_var=int(calc_var), **opts)
+    # per observation the reference writes its level's value (mean_pred_id[i] = sigma ZtYAux[level(i)],
+    # re_model_template.h:4085, 4113): stored per level (order of first appearance), checked exact
+    K = g.shape[1]
+    out = dict(n=n, levels=list(levels), cov_pars=list(cov_pars), opts=opts)
+    for key in (("mean", "var") if calc_var else ("mean",)):
+        v = np.asarray(r[key]).reshape(K, n)
+        per = []
+        for k in range(K):
+            _, first, inv = np.unique(g[:, k], return_index=True, return_inverse=True)
+            order = np.argsort(first)              # levels by first appearance
+            lev = v[k, first[order]]
+            rank = np.empty_like(order)
+            rank[order] = np.arange(order.size)
+            assert np.array_equal(lev[rank[inv]], v[k]), "per-level values differ within a level"
+            per.append(lev.tolist())
+        out[key + "_levels"] = per
+    return out
+
+
 def main():
     cases = json.load(open(OUT)) if os.path.exists(OUT) else {}
     it_tight = dict(matrix_inversion_method="iterative", cg_delta_conv="1e-10", num_rand_vec_trace="50")
@@ -63,6 +86,10 @@ def main():
         cases["fit_k2_n20000_tight"] = fit_case(20000, (500, 50), matrix_inversion_method="iterative",
                                                 cg_delta_conv="1e-10")
         cases["fit_k2_n20000_default"] = fit_case(20000, (500, 50), matrix_inversion_method="iterative")
+        cases["pred_train_k1_n5000"] = pred_case(5000, (300,), (1.0, 0.5), True, matrix_inversion_method="cholesky")
+        cases["pred_train_k2_n20000_tight"] = pred_case(20000, (500, 50), (1.0, 1.0, 0.25), False, **it_tight)
+        cases["pred_train_k3_n20000_default"] = pred_case(20000, (400, 60, 7), (1.0, 1.0, 0.25, 0.1), False,
+                                                          **it_default)
     else:
         cases["k2_n500000_default"] = case(500000, (5000, 500), (1.0, 1.0, 0.25), **it_default)
         cases["k2_n500000_tight"] = case(500000, (5000, 500), (1.0, 1.0, 0.25), **it_tight)

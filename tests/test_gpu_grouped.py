@@ -19,6 +19,7 @@ handful of iterations whose count both sides share; the remaining difference is 
 truncated solve (same bounds unless a stopping test flips, which these fixtures do not hit). K == 1
 is a closed form (1e-10).
 """
+import ctypes
 import json
 import os
 
@@ -26,6 +27,7 @@ import numpy as np
 import pytest
 
 from gpboost_amd import GPBoostError, GPModel, synthetic
+from gpboost_amd.basic import _dp, _safe_call, lib
 
 pytestmark = pytest.mark.gpu
 
@@ -130,3 +132,63 @@ def test_grouped_config4_size_matches_reference(golden):
         nll, grad, _ = gm.neg_log_likelihood_and_grad(cp, y)
         assert abs(nll - case["nll"]) <= 1e-10 * abs(case["nll"]), (name, nll, case["nll"])
         np.testing.assert_allclose(grad, case["grad"], rtol=1e-6, atol=1e-6 * np.abs(case["grad"]).max())
+
+
+def _levels_of(g):
+    """Per effect: the level index of every observation (order of first appearance)."""
+    out = []
+    for k in range(g.shape[1]):
+        _, first, inv = np.unique(g[:, k], return_index=True, return_inverse=True)
+        order = np.argsort(first)
+        rank = np.empty_like(order)
+        rank[order] = np.arange(order.size)
+        out.append(rank[inv])
+    return out
+
+
+@pytest.mark.parametrize("name", ["pred_train_k1_n5000", "pred_train_k2_n20000_tight",
+                                  "pred_train_k3_n20000_default"])
+def test_grouped_training_data_random_effects_match_reference(golden, name):
+    # PredictTrainingDataRandomEffects, grouped branch (re_model_template.h:4065-4167): the posterior
+    # mean tau_k Z_k^T Psi^-1 y of each observation's level; K == 1 also its variance (closed form)
+    case = golden[name]
+    g, y = _data(case)
+    gm = _model(case, g)
+    K = g.shape[1]
+    cp = np.array(case["cov_pars"])
+    gm.neg_log_likelihood(cp, y)   # sets y and the parameters
+    want_var = "var_levels" in case
+    out = np.zeros((2 if want_var else 1) * K * case["n"])
+    _safe_call(lib().GPB_PredictREModelTrainingDataRandomEffects(gm.handle, _dp(cp), None, _dp(out), None,
+                                                                 ctypes.c_bool(want_var)))
+    lev = _levels_of(g)
+    mean = out[:K * case["n"]].reshape(K, -1)
+    for k in range(K):
+        ref = np.asarray(case["mean_levels"][k])[lev[k]]
+        # tight: rounding of the PCG iterates (1e-9 of the largest mean); default tolerance: the same
+        # truncated PCG on both sides
+        np.testing.assert_allclose(mean[k], ref, rtol=0, atol=1e-8 * np.abs(ref).max())
+        if want_var:
+            v = out[K * case["n"]:].reshape(K, -1)[k]
+            np.testing.assert_allclose(v, np.asarray(case["var_levels"][k])[lev[k]], rtol=1e-12)
+
+
+def test_grouped_predict_new_and_seen_levels():
+    g = synthetic.bench_groups(6000, (120, 15))
+    y = synthetic.bench_grouped_y(g)
+    gm = GPModel(group_data=g)
+    cp = [1.0, 0.8, 0.3]
+    gm.neg_log_likelihood(cp, y)
+    tr = gm.predict_training_data_random_effects()          # (n, 2): per-effect posterior means
+    assert tr.shape == (6000, 2)
+    # at the training labels the predictive mean is the sum of the effects' posterior means
+    p = gm.predict(group_data_pred=g[:500], cov_pars=cp, predict_var=False)
+    np.testing.assert_allclose(p["mu"], tr[:500].sum(axis=1), rtol=0, atol=1e-12 * np.abs(tr).max())
+    # an unseen level contributes 0; an offset is added
+    gn = np.array([[10_000, g[0, 1]], [g[1, 0], 99_999], [77_777, 88_888]])
+    p = gm.predict(group_data_pred=gn, cov_pars=cp, offset_pred=np.array([1., 2., 3.]))
+    np.testing.assert_allclose(p["mu"], [tr[0, 1] + 1., tr[1, 0] + 2., 3.], rtol=0, atol=1e-12 * np.abs(tr).max())
+    with pytest.raises(GPBoostError, match="predictive"):
+        gm.predict(group_data_pred=g[:5], cov_pars=cp, predict_var=True)
+    with pytest.raises(GPBoostError, match="not implemented for matrix_inversion_method_ == 'iterative'"):
+        gm.predict_training_data_random_effects(predict_var=True)
