@@ -356,7 +356,44 @@ void LatentVecchia::BuildStructure(const int* nbr) {
   }
 }
 
+void LatentVecchia::SetObservations(const std::vector<int>& obs_row) {
+  n_obs_ = (int)obs_row.size();
+  std::vector<int> ptr(n_ + 1, 0);
+  for (int i = 0; i < n_obs_; ++i) {
+    const int v = obs_row[i];
+    if (v < 0 || v >= n_) Fatal("observation %d maps to latent row %d outside [0, %d)", i, v, n_);
+    ++ptr[lab_[v] + 1];
+  }
+  for (int p = 0; p < n_; ++p) ptr[p + 1] += ptr[p];
+  obs_order_.assign(n_obs_, 0);
+  std::vector<int> fill(ptr.begin(), ptr.end() - 1);
+  for (int i = 0; i < n_obs_; ++i) obs_order_[fill[lab_[obs_row[i]]]++] = i;   // ascending observation index per row
+  d_optr_.alloc(n_ + 1);
+  HIP_CHECK(hipMemcpyAsync(d_optr_.get(), ptr.data(), sizeof(int) * (n_ + 1), hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  d_yo_.alloc(n_obs_);
+  has_obs_ = true;
+}
+
+ObsMap LatentVecchia::Obs() const {
+  ObsMap ob;
+  if (has_obs_) {
+    ob.ptr = d_optr_.get();
+    ob.y = d_yo_.get();
+    ob.offset = has_off_ ? d_offo_.get() : nullptr;
+  }
+  return ob;
+}
+
 void LatentVecchia::SetY(const double* y_vo) {
+  if (has_obs_) {
+    std::vector<double> yo(n_obs_);
+    for (int e = 0; e < n_obs_; ++e) yo[e] = y_vo[obs_order_[e]];
+    HIP_CHECK(hipMemcpyAsync(d_yo_.get(), yo.data(), sizeof(double) * n_obs_, hipMemcpyHostToDevice, s_));
+    HIP_CHECK(hipStreamSynchronize(s_));
+    y_set_ = true;
+    return;
+  }
   std::vector<double> yp(n_);
   for (int p = 0; p < n_; ++p) yp[p] = y_vo[vo_[p]];
   HIP_CHECK(hipMemcpyAsync(d_y_.get(), yp.data(), sizeof(double) * n_, hipMemcpyHostToDevice, s_));
@@ -367,6 +404,15 @@ void LatentVecchia::SetY(const double* y_vo) {
 void LatentVecchia::SetOffset(const double* off_vo) {
   if (off_vo == nullptr) {
     has_off_ = false;
+    return;
+  }
+  if (has_obs_) {
+    std::vector<double> oo(n_obs_);
+    for (int e = 0; e < n_obs_; ++e) oo[e] = off_vo[obs_order_[e]];
+    d_offo_.alloc(n_obs_);
+    HIP_CHECK(hipMemcpyAsync(d_offo_.get(), oo.data(), sizeof(double) * n_obs_, hipMemcpyHostToDevice, s_));
+    HIP_CHECK(hipStreamSynchronize(s_));
+    has_off_ = true;
     return;
   }
   std::vector<double> op(n_);
@@ -726,7 +772,8 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
   if (std::getenv("GPBOOST_AMD_BENCH_PRECOND")) {   // diagnostics: preconditioner cost alone
     NewtonPrepArgs np{};
     np.n = n; np.lik = lik; np.aux = aux; np.y = d_y_.get(); np.loc = d_mode_.get(); np.mode = d_mode_.get();
-    np.offset = has_off_ ? d_off_.get() : nullptr;
+    np.offset = has_off_ && !has_obs_ ? d_off_.get() : nullptr;
+    np.obs = Obs();
     np.Dinv = d_Dinv_.get(); np.d1 = d_d1_.get(); np.W = d_W_.get(); np.W_update = 1; np.dw = d_dw_.get();
     HIP_CHECK(hipMemsetAsync(d_mode_.get(), 0, sizeof(double) * n, s_));
     launch_newton_prep(np, s_);
@@ -749,7 +796,8 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
   ScalarArgs sa{};
   sa.n = n; sa.m = m_; sa.lik = lik; sa.aux = aux;
   sa.nbr = d_nbr_.get(); sa.Bv = d_Bv_.get(); sa.Dinv = d_Dinv_.get(); sa.y = d_y_.get();
-  sa.offset = has_off_ ? d_off_.get() : nullptr;
+  sa.offset = has_off_ && !has_obs_ ? d_off_.get() : nullptr;
+  sa.obs = Obs();
 
   // ---- 2. mode finding (likelihoods.h:2780-3000); mode re-initialised to 0 (InitializeModeAvec)
   HIP_CHECK(hipMemsetAsync(d_mode_.get(), 0, sizeof(double) * n, s_));
@@ -800,7 +848,8 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
     // the block rule (each column's iterates are exactly those of a separate run).
     NewtonPrepArgs np{};
     np.n = n; np.lik = lik; np.aux = aux; np.y = d_y_.get(); np.loc = d_mode_.get(); np.mode = d_mode_.get();
-    np.offset = has_off_ ? d_off_.get() : nullptr;
+    np.offset = has_off_ && !has_obs_ ? d_off_.get() : nullptr;
+    np.obs = Obs();
     np.Dinv = d_Dinv_.get(); np.d1 = d_d1_.get(); np.W = d_W_.get(); np.W_update = 1;
     np.rhs = d_rhs_.get(); np.dw = d_dw_.get(); np.sdw = d_sdw_.get();
     launch_newton_prep(np, s_);
@@ -823,7 +872,8 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
     {   // first derivative at the mode (likelihoods.h:3008; used by the gradient wrt F)
       NewtonPrepArgs nd{};
       nd.n = n; nd.lik = lik; nd.aux = aux; nd.y = d_y_.get(); nd.loc = d_mode_.get(); nd.mode = d_mode_.get();
-      nd.offset = has_off_ ? d_off_.get() : nullptr;
+      nd.offset = has_off_ && !has_obs_ ? d_off_.get() : nullptr;
+      nd.obs = Obs();
       nd.Dinv = d_Dinv_.get(); nd.d1 = d_d1_.get(); nd.W = d_W_.get(); nd.W_update = 0;
       launch_newton_prep(nd, s_);
     }
@@ -833,7 +883,8 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
     for (int it = 0; it < maxit; ++it) {
       NewtonPrepArgs np{};
       np.n = n; np.lik = lik; np.aux = aux; np.y = d_y_.get(); np.loc = d_mode_.get(); np.mode = d_mode_.get();
-    np.offset = has_off_ ? d_off_.get() : nullptr;
+    np.offset = has_off_ && !has_obs_ ? d_off_.get() : nullptr;
+    np.obs = Obs();
       np.Dinv = d_Dinv_.get(); np.d1 = d_d1_.get(); np.W = d_W_.get();
       np.W_update = 1;
       np.rhs = d_rhs_.get();
@@ -853,7 +904,8 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
     {   // derivative / information at the mode, VADU diagonal and its square root (:3000-3005, 12163-12166)
       NewtonPrepArgs np{};
       np.n = n; np.lik = lik; np.aux = aux; np.y = d_y_.get(); np.loc = d_mode_.get(); np.mode = d_mode_.get();
-    np.offset = has_off_ ? d_off_.get() : nullptr;
+    np.offset = has_off_ && !has_obs_ ? d_off_.get() : nullptr;
+    np.obs = Obs();
       np.Dinv = d_Dinv_.get(); np.d1 = d_d1_.get(); np.W = d_W_.get();
       np.W_update = info_changes ? 1 : 0;
       np.dw = d_dw_.get();
@@ -915,7 +967,8 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
       ModeDerivArgs md{};
       md.n = n; md.m = m_; md.t = tw; md.lik = lik; md.nbr = d_nbr_.get(); md.Bv = d_Bv_.get(); md.dw = d_dw_.get();
       md.loc = d_mode_.get(); md.U = d_U_.get(); md.P = d_P_.get(); md.dmll = d_dmll_.get();
-      md.offset = has_off_ ? d_off_.get() : nullptr;
+      md.offset = has_off_ && !has_obs_ ? d_off_.get() : nullptr;
+      md.obs = Obs();
       md.t_valid = tl; md.t_all = t;
       if (coll_ == nullptr) {
         md.stage = 0;
@@ -939,6 +992,7 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
     ga.n = n; ga.m = m_; ga.t = tw; ga.nbr = d_nbr_.get(); ga.Bv = d_Bv_.get(); ga.dBv = d_dBv_.get();
     ga.Dinv = d_Dinv_.get(); ga.dD = d_dD_.get(); ga.W = d_W_.get();
     ga.daux = gauss ? -1. / aux : 0.;   // d information / dlog(aux) (likelihoods.h:10967-10976)
+    ga.obs_ptr = has_obs_ ? d_optr_.get() : nullptr;   // per observation: x the row's count
     ga.U = d_U_.get(); ga.P = d_P_.get();
     DevBuf<double>& cols = d_out_;
     launch_grad_cols(ga, d_partials_.get(), cols.get(), s_);
@@ -985,6 +1039,9 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
       if (!gauss) g -= sc[kSqImpRng];
       res.grad.push_back(g);
     }
+    if (grad_f_vo != nullptr && has_obs_)
+      Fatal("the gradient wrt the fixed effects of a latent model with repeated coordinates is not supported by "
+            "gpboost_amd");
     if (grad_f_vo != nullptr) {   // wrt the fixed effects F (likelihoods.h:5337-5367)
       d_gradf_.alloc(n);
       launch_grad_f(n, d_d1_.get(), gauss ? nullptr : d_dmll_.get(), d_W_.get(), gauss ? nullptr : d_vS_.get(),
@@ -1002,7 +1059,7 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
       const double trD = sc[kSqTrDw] * (-1. / aux);
       const double c = optimal_c(z1, zP, t, tr1, trP);
       const double dd = tr1 + c * trD - c * trP;
-      res.grad.push_back(sc[kSqRss] * (-0.5 / aux) + 0.5 * n + 0.5 * dd);
+      res.grad.push_back(sc[kSqRss] * (-0.5 / aux) + 0.5 * (has_obs_ ? n_obs_ : n) + 0.5 * dd);
     }
   }
   HIP_CHECK(hipEventRecord(ev1_, s_));

@@ -61,7 +61,13 @@ class LatentVecchia {
   LatentVecchia(int n, int d, int m, const double* d_X, const int* nbr, hipStream_t stream);
   ~LatentVecchia();
 
-  void SetY(const double* y_vo);   // host, Vecchia order
+  // Repeated coordinates (the reference's unique-location form, Vecchia_utils.cpp:1121-1139): the
+  // latent variables are the n unique locations and obs_row[i] is the latent Vecchia row of
+  // observation i (observations in the model's Vecchia-shuffled order). SetY / SetOffset then take
+  // one value per observation (that order); the likelihood terms of a latent variable are sums over
+  // its observations.
+  void SetObservations(const std::vector<int>& obs_row);
+  void SetY(const double* y_vo);   // host, Vecchia order (per observation after SetObservations)
   // Posterior mode of the last evaluation (host, Vecchia order).
   void GetMode(double* mode_vo);
   // Fixed effects F of the location parameter (host, Vecchia order; NULL: none). The likelihood is
@@ -183,6 +189,13 @@ class LatentVecchia {
   bool factor_ready_ = false;
   DevBuf<double> d_off_, d_gradf_;   // fixed effects (storage order), gradient wrt F
   bool has_off_ = false;
+  // observations of the latent variables (repeated coordinates): storage-row-major lists
+  bool has_obs_ = false;
+  int n_obs_ = 0;
+  std::vector<int> obs_order_;        // position e of the lists -> observation index
+  DevBuf<int> d_optr_;                // n + 1
+  DevBuf<double> d_yo_, d_offo_;      // n_obs
+  ObsMap Obs() const;
 };
 
 }  // namespace gpb_amd

@@ -265,6 +265,18 @@ void launch_axpby(size_t count, double alpha, const double* X, double beta, cons
 // ---- likelihood-specific elementwise and reductions
 enum LatentLik : int { kLikGaussian = 0, kLikBernoulliLogit = 1 };
 
+// Observations of the latent variables when coordinates repeat (the reference's unique-location
+// form: Z maps n observations to the n_u latent variables, Vecchia_utils.cpp:1121-1139,
+// re_comp.h:845-870): the observations of storage row i are [ptr[i], ptr[i+1]) of y / offset
+// (latent-variable-major). ptr == nullptr: one observation per row, y / offset indexed by row.
+// The likelihood's per-row quantities are then sums over the row's observations (Z^T d1, Z^T W Z,
+// Z^T dW), evaluated at mode_i + offset_e.
+struct ObsMap {
+  const int* ptr = nullptr;
+  const double* y = nullptr;
+  const double* offset = nullptr;
+};
+
 struct NewtonPrepArgs {
   int n, lik;
   double aux;           // gaussian error variance
@@ -279,6 +291,7 @@ struct NewtonPrepArgs {
   double* rhs;          // W*mode + d1 (nullable)
   double* dw;           // D^-1 + W (nullable)
   double* sdw;          // sqrt(dw) (nullable)
+  ObsMap obs;           // several observations per latent variable (repeated coordinates), optional
 };
 void launch_newton_prep(const NewtonPrepArgs& a, hipStream_t s);
 
@@ -312,6 +325,7 @@ struct ScalarArgs {
   const double* mode;
   const double* offset; // fixed effects F (nullable): log-likelihood at mode + F
   const double* vS;     // nullable -> implicit terms skipped
+  ObsMap obs;
 };
 void launch_latent_scalars(const ScalarArgs& a, double* partials, double* out, hipStream_t s);
 
@@ -328,6 +342,7 @@ struct GradColsArgs {
   const double* dD;
   const double* W;
   double daux;
+  const int* obs_ptr;   // nullable: dW/dlog aux of row i = daux x its number of observations
   const double* U;
   const double* P;
 };
@@ -346,6 +361,7 @@ struct ModeDerivArgs {
   const double* dw;
   const double* loc;
   const double* offset;        // nullable: third derivative at loc + F
+  ObsMap obs;
   const double* U;
   const double* P;
   double* dmll;

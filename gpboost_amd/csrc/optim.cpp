@@ -170,14 +170,16 @@ double REModelAMD::InitialRangeTrafo() const {
   // correlation 0.05 at half the median distance. The sample draws continue the model's
   // mt19937(seed) after the Vecchia ordering shuffle (re_model_template.h:154,
   // Vecchia_utils.cpp:1094-1095).
-  const int n = cfg_.n, d = cfg_.d;
+  // the GP component's coordinates: all points, or the unique locations of a latent model with
+  // repeated coordinates (RECompGP::coords_, re_comp.h:1232-1244)
+  const int d = cfg_.d, n = (int)(coords_vo_.size() / d);
   const int kMaxPoints = 1000;
   const int nf = std::min(n, kMaxPoints);
   std::vector<int> idx(nf);
   if (nf < n) {
     std::mt19937 rng(cfg_.seed);
-    if (vecchia_ && cfg_.vecchia_ordering == "random") {
-      std::vector<int> dummy(n);
+    if (vecchia_ && cfg_.vecchia_ordering == "random") {   // the ordering shuffle of the n observations
+      std::vector<int> dummy(cfg_.n);
       std::iota(dummy.begin(), dummy.end(), 0);
       std::shuffle(dummy.begin(), dummy.end(), rng);
     }

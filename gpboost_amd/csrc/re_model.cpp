@@ -95,24 +95,6 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
   for (int i = 0; i < n; ++i)
     for (int q = 0; q < d; ++q) coords_[(size_t)i * d + q] = coords_colmajor[(size_t)q * n + i];
 
-  if (cfg_.latent) {
-    // The reference runs latent GPs on the UNIQUE locations (RECompGP on unique REs with an
-    // incidence matrix, Vecchia_utils.cpp:1121-1139; only_one_GP_calculations_on_RE_scale): with
-    // repeated coordinates its latent dimension is the number of distinct points. This build keeps
-    // one latent variable per observation, so repeated coordinates would silently define a
-    // different model: refuse them.
-    std::vector<int> ord(n);
-    for (int i = 0; i < n; ++i) ord[i] = i;
-    auto row = [&](int i) { return coords_.data() + (size_t)i * d; };
-    std::sort(ord.begin(), ord.end(), [&](int a, int b) {
-      return std::lexicographical_compare(row(a), row(a) + d, row(b), row(b) + d);
-    });
-    for (int k = 1; k < n; ++k)
-      if (std::equal(row(ord[k - 1]), row(ord[k - 1]) + d, row(ord[k])))
-        Fatal("duplicate coordinates (observations %d and %d): latent Vecchia models with repeated locations "
-              "are not supported by gpboost_amd (the reference collapses them to unique locations)",
-              std::min(ord[k - 1], ord[k]), std::max(ord[k - 1], ord[k]));
-  }
   HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
   HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_sums_), 16 * sizeof(double), hipHostMallocDefault));
@@ -120,17 +102,35 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
   row_begin_ = 0;
   row_end_ = n;
   num_neighbors_pred_ = 2 * cfg_.num_neighbors;   // re_model_template.h:299
+  nu_ = n;
   if (vecchia_) {
-    if (cfg_.num_neighbors > n - 1) cfg_.num_neighbors = n - 1;  // Vecchia_utils.cpp:754-757
-    if (cfg_.num_neighbors < 1) Fatal("num_neighbors must be >= 1");
     perm_ = vecchia_order(n, cfg_.seed, cfg_.vecchia_ordering == "random");
     if (cfg_.vecchia_ordering != "random" && cfg_.vecchia_ordering != "none")
       Fatal("vecchia_ordering '%s' is not supported (supported: none, random)", cfg_.vecchia_ordering.c_str());
     coords_vo_.resize((size_t)n * d);
     for (int i = 0; i < n; ++i)
       for (int q = 0; q < d; ++q) coords_vo_[(size_t)i * d + q] = coords_[(size_t)perm_[i] * d + q];
-    d_X_.alloc((size_t)n * d);
-    HIP_CHECK(hipMemcpyAsync(d_X_.get(), coords_vo_.data(), sizeof(double) * n * d, hipMemcpyHostToDevice, stream_));
+    if (cfg_.latent) {
+      // Latent GPs live on the UNIQUE locations (RECompGP on unique coordinates with an incidence
+      // matrix, Vecchia_utils.cpp:1121-1139, re_comp.h:845-870; only_one_GP_calculations_on_RE_scale):
+      // unique points in order of first appearance in the shuffled order, the Vecchia structure
+      // over them, every observation mapped to its location's latent variable.
+      std::vector<int> uniq, idx;
+      unique_locations(coords_vo_.data(), n, d, uniq, idx);
+      if ((int)uniq.size() < n) {
+        nu_ = (int)uniq.size();
+        obs_row_ = idx;
+        std::vector<double> xu((size_t)nu_ * d);
+        for (int u = 0; u < nu_; ++u)
+          for (int q = 0; q < d; ++q) xu[(size_t)u * d + q] = coords_vo_[(size_t)uniq[u] * d + q];
+        coords_vo_.swap(xu);
+      }
+      row_end_ = nu_;
+    }
+    if (cfg_.num_neighbors > nu_ - 1) cfg_.num_neighbors = nu_ - 1;  // Vecchia_utils.cpp:754-757
+    if (cfg_.num_neighbors < 1) Fatal("num_neighbors must be >= 1");
+    d_X_.alloc((size_t)nu_ * d);
+    HIP_CHECK(hipMemcpyAsync(d_X_.get(), coords_vo_.data(), sizeof(double) * nu_ * d, hipMemcpyHostToDevice, stream_));
     // neighbour search is deferred to first use so a distributed model searches only its rows
   } else {
     coords_vo_ = coords_;
@@ -148,7 +148,8 @@ void REModelAMD::EnsureStructure() {
   if (vecchia_ && !structure_built_) {
     BuildVecchiaStructure();
     if (cfg_.latent) {
-      latent_.reset(new LatentVecchia(cfg_.n, cfg_.d, cfg_.num_neighbors, d_X_.get(), nbr_.data(), stream_));
+      latent_.reset(new LatentVecchia(nu_, cfg_.d, cfg_.num_neighbors, d_X_.get(), nbr_.data(), stream_));
+      if (has_dup()) latent_->SetObservations(obs_row_);
       latent_->SetShard(rank_, world_, coll_.get());   // probe columns over the ranks (§8e Option A)
       if (y_set_) latent_->SetY(y_vo_.data());
       latent_->SetOffset(has_offset_ ? offset_vo_.data() : nullptr);
@@ -177,7 +178,7 @@ REModelAMD::~REModelAMD() {
 }
 
 void REModelAMD::BuildVecchiaStructure() {
-  const int n = cfg_.n, m = cfg_.num_neighbors;
+  const int n = cfg_.latent ? nu_ : cfg_.n, m = cfg_.num_neighbors;   // latent: the unique locations
   // Only this rank's rows are needed on the device (each row's neighbours are earlier points).
   nbr_.assign((size_t)(row_end_ - row_begin_) * m, -1);
   nbr_row0_ = row_begin_;
@@ -205,7 +206,7 @@ void REModelAMD::ApplyPartition(int rank, int world) {
   const int n = cfg_.n;
   if (cfg_.latent) {
     row_begin_ = 0;
-    row_end_ = n;
+    row_end_ = nu_;
   } else {
     const int base = n / world, rem = n % world;
     row_begin_ = rank * base + std::min(rank, rem);
@@ -507,6 +508,7 @@ EvalResult REModelAMD::EvalTrafo(const double* trafo, bool want_grad, int profil
 
 void REModelAMD::GetVecchiaStructure(int* perm, int* nbr) const {
   if (!vecchia_) Fatal("model does not use the Vecchia approximation");
+  if (has_dup()) Fatal("GetVecchiaStructure is not available for latent models with repeated coordinates");
   if (world_ > 1) Fatal("GetVecchiaStructure is only available on single-rank models");
   const_cast<REModelAMD*>(this)->UseDevice();
   const_cast<REModelAMD*>(this)->EnsureStructure();
@@ -518,6 +520,7 @@ void REModelAMD::GetLatentVecchiaFactor(const double* cov_pars_orig, double* Din
                                         double* dBvals) {
   if (!cfg_.latent) Fatal("model does not use a latent Vecchia approximation");
   if (world_ > 1) Fatal("GetLatentVecchiaFactor is only available on single-rank models");
+  if (has_dup()) Fatal("GetLatentVecchiaFactor is not available for latent models with repeated coordinates");
   if (!(cov_pars_orig[0] > 0. && cov_pars_orig[1] > 0.)) Fatal("covariance parameters must be > 0");
   UseDevice();
   EnsureStructure();

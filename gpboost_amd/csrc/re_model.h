@@ -198,7 +198,10 @@ class REModelAMD {
   bool vecchia_ = false;
   bool structure_built_ = false;
   std::vector<double> coords_;       // row-major n x d, original order
-  std::vector<double> coords_vo_;    // Vecchia order (Vecchia) / original (dense)
+  std::vector<double> coords_vo_;    // Vecchia order (Vecchia) / original (dense); latent: the unique locations
+  int nu_ = 0;                       // latent dimension (unique locations of a latent model, else n)
+  std::vector<int> obs_row_;         // latent models with repeated coordinates: observation (Vecchia-shuffled order) -> latent row
+  bool has_dup() const { return !obs_row_.empty(); }
   std::vector<int> perm_;
   std::vector<int> nbr_;             // rows [row_begin_, row_end_) x m, or all rows when world == 1
   int nbr_row0_ = 0;

@@ -71,6 +71,9 @@ void REModelAMD::CalcGradientF(double* y, const double* fixed_effects, bool calc
     cov_pars_initialized_ = true;
   }
   if (cfg_.latent) {
+    if (has_dup())
+      Fatal("the gradient wrt the fixed effects of a latent model with repeated coordinates is not supported by "
+            "gpboost_amd");
     SetLatentOffset(fixed_effects);
     if (!y_set_) Fatal("Response variable data has not been set");
     EnsureStructure();
@@ -259,9 +262,9 @@ void REModelAMD::PredictTrainingDataRandomEffects(const double* cov_pars, const 
     if (y != nullptr) SetResponse(y, nullptr);
     if (!y_set_) Fatal("Response variable data is not provided and has not been set before");
     EvalLatent(cp.data(), false);   // the posterior mode at cov_pars
-    std::vector<double> mvo(n);
+    std::vector<double> mvo(nu_);
     latent_->GetMode(mvo.data());
-    for (int i = 0; i < n; ++i) out[perm_[i]] = mvo[i];
+    for (int i = 0; i < n; ++i) out[perm_[i]] = mvo[has_dup() ? obs_row_[i] : i];   // Z mode
     return;
   }
   const std::vector<double> r = ResidualResponse(y, fixed_effects);
@@ -338,6 +341,18 @@ void REModelAMD::SetLikelihood(const std::string& likelihood) {
     c.matrix_inversion_method = "iterative";
   } else if (!latent && cfg_.latent) {
     c.matrix_inversion_method = "cholesky";
+    if (has_dup()) {   // back to all points (the exact Gaussian Vecchia path keeps every observation)
+      const int n = cfg_.n, d = cfg_.d;
+      coords_vo_.resize((size_t)n * d);
+      for (int i = 0; i < n; ++i)
+        for (int q = 0; q < d; ++q) coords_vo_[(size_t)i * d + q] = coords_[(size_t)perm_[i] * d + q];
+      obs_row_.clear();
+      nu_ = n;
+      row_end_ = n;
+      d_X_.alloc((size_t)n * d);
+      HIP_CHECK(hipMemcpyAsync(d_X_.get(), coords_vo_.data(), sizeof(double) * n * d, hipMemcpyHostToDevice, stream_));
+      HIP_CHECK(hipStreamSynchronize(stream_));
+    }
   }
   c.lik = lik;
   c.latent = latent;

@@ -1141,13 +1141,34 @@ __global__ void __launch_bounds__(kBT) grad_f_kernel(int n, const double* __rest
   }
 }
 
+// Sums over the observations of row i (ObsMap) of the likelihood's derivative and information at
+// mode_i + offset_e; one observation per row: the row's own y / offset.
+__device__ __forceinline__ void obs_d1_info(const ObsMap& ob, int lik, double aux, int i, double mi,
+                                            const double* y, const double* offset, bool want_info, double& d1,
+                                            double& w) {
+  if (ob.ptr == nullptr) {
+    const double l = offset ? mi + offset[i] : mi;
+    d1 = lik_d1(lik, aux, y[i], l);
+    if (want_info) w = lik_info(lik, aux, l);
+    return;
+  }
+  double s1 = 0., sw = 0.;
+  for (int e = ob.ptr[i]; e < ob.ptr[i + 1]; ++e) {
+    const double l = ob.offset ? mi + ob.offset[e] : mi;
+    s1 += lik_d1(lik, aux, ob.y[e], l);
+    if (want_info) sw += lik_info(lik, aux, l);
+  }
+  d1 = s1;
+  if (want_info) w = sw;
+}
+
 __global__ void __launch_bounds__(kBT) newton_prep_kernel(NewtonPrepArgs a) {
   for (int i = blockIdx.x * kBT + threadIdx.x; i < a.n; i += gridDim.x * kBT) {
-    const double l = a.offset ? a.loc[i] + a.offset[i] : a.loc[i];
-    const double d1 = lik_d1(a.lik, a.aux, a.y[i], l);
+    double d1 = 0., winfo = 0.;
+    obs_d1_info(a.obs, a.lik, a.aux, i, a.loc[i], a.y, a.offset, a.W_update != 0, d1, winfo);
     a.d1[i] = d1;
     // W is only refreshed when requested (information_changes_*); otherwise the stored W is used
-    const double w = a.W_update ? lik_info(a.lik, a.aux, l) : a.W[i];
+    const double w = a.W_update ? winfo : a.W[i];
     if (a.W_update) a.W[i] = w;
     if (a.rhs) a.rhs[i] = fma(w, a.mode[i], d1);
     if (a.dw) {
@@ -1182,16 +1203,28 @@ __global__ void __launch_bounds__(kBT) latent_scalars_kernel(ScalarArgs a, doubl
     }
     const double Di = a.Dinv[i];
     acc[kSqQuad] += bm * Di * bm;
-    const double li = a.offset ? mi + a.offset[i] : mi;
-    acc[kSqLogLik] += lik_loglik(a.lik, a.aux, a.y[i], li);
+    double cnt = 1.;
+    if (a.obs.ptr == nullptr) {
+      const double li = a.offset ? mi + a.offset[i] : mi;
+      acc[kSqLogLik] += lik_loglik(a.lik, a.aux, a.y[i], li);
+      const double r = a.y[i] - li;
+      acc[kSqRss] += r * r;
+    } else {   // the row's observations (repeated coordinates)
+      const int e0 = a.obs.ptr[i], e1 = a.obs.ptr[i + 1];
+      cnt = (double)(e1 - e0);
+      for (int e = e0; e < e1; ++e) {
+        const double li = a.obs.offset ? mi + a.obs.offset[e] : mi;
+        acc[kSqLogLik] += lik_loglik(a.lik, a.aux, a.obs.y[e], li);
+        const double r = a.obs.y[e] - li;
+        acc[kSqRss] += r * r;
+      }
+    }
     acc[kSqLogDinv] += log(Di);
-    const double r = a.y[i] - li;
-    acc[kSqRss] += r * r;
     if (a.dw) {
       const double dwi = a.dw[i];
       acc[kSqLogDw] += log(dwi);
       acc[kSqTrVar] += Di / dwi;
-      acc[kSqTrDw] += 1. / dwi;
+      acc[kSqTrDw] += cnt / dwi;   // x dW_i/dlog aux = -cnt_i / aux on the host
       if (a.dD) acc[kSqTrRng] += Di * a.dD[i] * Di / dwi;
     }
     if (a.dBv) {
@@ -1248,12 +1281,13 @@ __global__ void __launch_bounds__(kBT) grad_cols_kernel(GradColsArgs a, int shif
         dbp = fma(dbv[r], pj, dbp);
       }
       const double Di = a.Dinv[i], dDi = a.dD[i], wi = a.W[i];
+      const double daux = a.obs_ptr ? a.daux * (double)(a.obs_ptr[i + 1] - a.obs_ptr[i]) : a.daux;
       acc[0] -= Di * bu * bp;
       acc[1] -= Di * bp * bp;
       acc[2] += Di * (dbu * bp + bu * dbp - Di * dDi * bu * bp);
       acc[3] += Di * (2. * dbp * bp - Di * dDi * bp * bp) + 2. * wi * bp * dbp;
-      acc[4] += ui * a.daux * pi;
-      acc[5] += bp * a.daux * bp;
+      acc[4] += ui * daux * pi;
+      acc[5] += bp * daux * bp;
     }
   }
   block_col_reduce<kGradCols>(acc, shift, c, t, partials);
@@ -1272,7 +1306,14 @@ __global__ void __launch_bounds__(kBT) mode_deriv_kernel(ModeDerivArgs a, int sh
     const int k = i < a.m ? i : a.m;
     const int* nb = a.nbr + (size_t)i * a.m;
     const double* bv = a.Bv + (size_t)i * a.m;
-    const double dWi = lik_dinfo(a.lik, a.offset ? a.loc[i] + a.offset[i] : a.loc[i]);
+    double dWi;
+    if (a.obs.ptr == nullptr) {
+      dWi = lik_dinfo(a.lik, a.offset ? a.loc[i] + a.offset[i] : a.loc[i]);
+    } else {   // Z^T dW: the row's observations
+      dWi = 0.;
+      for (int e = a.obs.ptr[i]; e < a.obs.ptr[i + 1]; ++e)
+        dWi += lik_dinfo(a.lik, a.obs.offset ? a.loc[i] + a.obs.offset[e] : a.loc[i]);
+    }
     // pass 1: row means of z1 = U dW P and zP = (BP)^2 dW over the t probes
     // (c_var == 0 -> c = 1, CG_utils.cpp:1036-1039).
     double s1 = 0., sP = 0.;

@@ -88,4 +88,62 @@ void vecchia_neighbors(const double* x, int n, int d, int m, int row_begin, int 
   }
 }
 
+void unique_locations(const double* x, int n, int d, std::vector<int>& uniques, std::vector<int>& idx) {
+  constexpr double kEps = 1e-10;   // EPSILON_NUMBERS (utils.h)
+  idx.assign(n, 0);
+  std::vector<double> sum(n);
+  for (int i = 0; i < n; ++i) {
+    double s = 0.;
+    for (int q = 0; q < d; ++q) s += x[(size_t)i * d + q];
+    sum[i] = s;
+  }
+  std::vector<int> ord(n);
+  for (int i = 0; i < n; ++i) ord[i] = i;
+  std::sort(ord.begin(), ord.end(), [&](int a, int b) { return sum[a] < sum[b]; });
+  auto smaller = [&](double a, double b) { return (b - a) > kEps * std::max(1.0, std::fabs(b)); };
+  auto close = [&](int a, int b) {
+    double s = 0.;
+    for (int q = 0; q < d; ++q) {
+      const double t = x[(size_t)a * d + q] - x[(size_t)b * d + q];
+      s += t * t;
+    }
+    return s < kEps * kEps;
+  };
+  std::vector<int> rep;   // representative (first appearance) of every unique found, in discovery order
+  for (int s0 = 0; s0 < n; ++s0) {
+    const int i = ord[s0];
+    int s1 = s0 + 1;
+    while (s1 < n && !smaller(sum[i], sum[ord[s1]])) ++s1;   // [s0, s1): potential duplicates of i
+    std::vector<int> local{(int)rep.size()};                  // unique indices found in this group
+    rep.push_back(i);
+    idx[i] = local[0];
+    for (int s = s0 + 1; s < s1; ++s) {
+      const int j = ord[s];
+      int hit = -1;
+      for (int u : local)
+        if (close(rep[u], j)) { hit = u; break; }
+      if (hit >= 0) {
+        if (j < rep[hit]) rep[hit] = j;   // the first appearance represents the location
+        idx[j] = hit;
+      } else {
+        local.push_back((int)rep.size());
+        idx[j] = (int)rep.size();
+        rep.push_back(j);
+      }
+    }
+    s0 = s1 - 1;
+  }
+  // renumber by first appearance
+  std::vector<int> order(rep.size());
+  for (size_t u = 0; u < rep.size(); ++u) order[u] = (int)u;
+  std::sort(order.begin(), order.end(), [&](int a, int b) { return rep[a] < rep[b]; });
+  std::vector<int> newid(rep.size());
+  uniques.resize(rep.size());
+  for (size_t k = 0; k < order.size(); ++k) {
+    newid[order[k]] = (int)k;
+    uniques[k] = rep[order[k]];
+  }
+  for (int i = 0; i < n; ++i) idx[i] = newid[idx[i]];
+}
+
 }  // namespace gpb_amd

@@ -22,4 +22,12 @@ void vecchia_neighbors(const double* x, int n, int d, int m, int row_begin, int 
 void vecchia_neighbors_gpu(const double* x, int n, int d, int m, int row_begin, int row_end, int* nbr,
                            hipStream_t s, int end_search_at = -1);
 
+// Unique locations among the rows of x (row-major n x d), the reference's
+// DetermineUniqueDuplicateCoordsFast (GP_utils.cpp:451-536): candidates grouped by their coordinate
+// sum (ascending; a group extends while the next sum is not larger by more than 1e-10 relative,
+// NumberIsSmallerThan utils.h:129-131), duplicates = squared distance < 1e-20 to a unique point of
+// the group, a unique point represented by its first appearance; uniques are returned in order of
+// first appearance (idx[i] = the unique index of row i).
+void unique_locations(const double* x, int n, int d, std::vector<int>& uniques, std::vector<int>& idx);
+
 }  // namespace gpb_amd

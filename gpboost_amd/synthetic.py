@@ -81,6 +81,19 @@ def bench_coords(n: int, d: int = 2) -> np.ndarray:
     return lcg_unif(n * d, 0.1).reshape(d, n).T.copy()
 
 
+def repeated_coords(n: int, n_unique: int, d: int = 2) -> np.ndarray:
+    """n observations at n_unique distinct locations (bench_coords(n_unique)), observation i at the
+    location floor(u_i n_unique), u from the exact LCG with c = 0.37: locations repeat at random."""
+    pts = bench_coords(n_unique, d)
+    return pts[np.floor(lcg_unif(n, 0.37) * n_unique).astype(np.int64)].copy()
+
+
+def cycled_coords(n: int, d: int = 2) -> np.ndarray:
+    """The round-1/2 benchmark coordinates: the R tests' double-arithmetic LCG (sim_rand_unif) filled
+    column-major; it cycles after ~40.6k draws, so n = 100k gives 20318 distinct locations."""
+    return sim_rand_unif(n * d, 0.1).reshape(d, n).T.copy()
+
+
 def bench_gaussian_y(n: int) -> np.ndarray:
     """iid N(0,1) by Box-Muller from LCG streams c=0.8 and c=0.42 (exact arithmetic)."""
     u1 = np.maximum(lcg_unif(n, 0.8), 1e-300)

@@ -294,12 +294,3 @@ def test_baseline_size_bernoulli_default_within_reference_sensitivity():
     nll, g, _ = gm.neg_log_likelihood_and_grad(case["cov_pars"], y)
     assert abs(nll - case["nll"]) <= 1e-6 * abs(case["nll"]), (nll, case["nll"])
     assert np.all(np.abs(g - ref_g) <= 2 * spread), (g, ref_g, spread)
-
-
-def test_latent_refuses_repeated_coordinates():
-    from gpboost_amd import GPModel, GPBoostError, synthetic
-    X = synthetic.bench_coords(500)
-    X[7] = X[3]
-    with pytest.raises(GPBoostError, match="duplicate coordinates"):
-        GPModel(gp_coords=X, likelihood="bernoulli_logit", gp_approx="vecchia", num_neighbors=10,
-                matrix_inversion_method="iterative")
