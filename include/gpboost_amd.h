@@ -21,8 +21,11 @@
  * cov_fct in {exponential, matern (shape 0.5/1.5/2.5), gaussian}; gp_approx "none" (dense
  * Cholesky) and "vecchia" with likelihood "gaussian" (exact), "vecchia" with "bernoulli_logit" and
  * "vecchia_latent" with "gaussian" (Laplace approximation, iterative methods); linear regression
- * covariates for the Gaussian likelihood (GLS, optimizer_coef "wls"). Anything else fails with -1
- * and a message naming the unsupported option.
+ * covariates for the Gaussian likelihood (GLS, optimizer_coef "wls"); OR grouped random effects
+ * (num_gp = 0, re_group_data with num_re_group >= 1 grouping variables, Gaussian likelihood; K = 1
+ * closed form, K >= 2 iterative SSOR-PCG + SLQ as the reference's default). Latent models accept
+ * repeated coordinates (the reference's unique-location form). Anything else fails with -1 and a
+ * message naming the unsupported option.
  * The compute path is HIP on gfx950; there is no CPU fallback: if no GPU is
  * visible, GPB_CreateREModel fails.
  */
