@@ -160,9 +160,26 @@ __device__ unsigned long long g_rows_prof[8];
 // DPPBC (K = 16 / 32, A/B form, see rows_dpp): the Gauss-Jordan steps broadcast the pivot column
 // by DPP row broadcasts and row-swap permutes (VALU) instead of LDS slots. Same values in the same
 // FMA order: bitwise identical results.
-template <int K, int COV, bool PROF = false, int MK = K, bool DPPBC = false>
-__global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(VecchiaRowsArgs a) {
+#ifndef GPB_ROWS_WAVES
+#define GPB_ROWS_WAVES 0
+#endif
+#ifndef GPB_ROWS_PIVRCP
+#define GPB_ROWS_PIVRCP 0
+#endif
+#if GPB_ROWS_WAVES > 0
+#define GPB_ROWS_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(GPB_ROWS_WAVES, GPB_ROWS_WAVES)))
+#else
+#define GPB_ROWS_WAVES_ATTR
+#endif
+// BORDER (MK + 2 <= K): the augmented columns ride as two extra matrix rows held by the idle lanes
+// MK and MK + 1 (the bordered symmetric matrix [[C, c, y_nbr], [c^T ...], [y_nbr^T ...]]): a step
+// broadcasts ONE column (row j of the trailing block incl. the pivot row's augmented entries
+// M[j][MK] = M[MK][j]) by one LDS store, and the lanes read it back as 16-byte pairs.
+template <int K, int COV, bool PROF = false, int MK = K, bool DPPBC = false, bool BORDER = false>
+__global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchia_rows_kernel(VecchiaRowsArgs a) {
   static_assert(!DPPBC || K == 16 || K == 32, "DPP broadcasts need 16- or 32-lane groups");
+  static_assert(!BORDER || (!DPPBC && MK + 2 <= K && (MK & 1) == 0), "bordered form: two spare lanes, even width");
+  constexpr int NC = BORDER ? MK + 2 : MK;   // register columns per lane
   extern __shared__ __attribute__((aligned(16))) double smem[];
   constexpr int BT = block_threads<K>();
   constexpr int G = 64 / K;                 // rows per wave
@@ -170,7 +187,7 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int g = lane / K;
-  const int r = lane - g * K;
+  const int r_lane = lane - g * K;
   const int group_id = wave * G + g;
   const int d = a.d;
   const double var = a.var, phi = a.phi;
@@ -200,6 +217,11 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
   const int total_groups = a.r1 - a.r0;
   for (int gbase_row = blockIdx.x * rows_per_block; gbase_row < total_groups; gbase_row += gridDim.x * rows_per_block) {
     if (prof) { t0 = __builtin_amdgcn_s_memtime(); ++tp[5]; }
+    // bordered form: the lane index is made opaque per row group, so the lane-dependent LDS
+    // addresses and pivot masks are recomputed each time instead of being hoisted out of the
+    // loop (32 address VGPRs and 60 mask SGPRs held across the whole kernel)
+    int r = r_lane;
+    if constexpr (BORDER) asm volatile("" : "+v"(r));
     const int i = a.r0 + gbase_row + group_id;
     const bool active = i < a.r1;
     const int k = active ? min(i, a.m) : 0;
@@ -217,8 +239,12 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
     const double yi = want_like ? a.Y[irow] : 0.;
     const double ynb = (want_like && rv) ? a.Y[nb] : 0.;
     compiler_fence();   // previous iteration's LDS reads are issued before these writes
+    // padding rows (r >= k) sit at distinct far-away points (1e30 (r + 1) on the first axis): their
+    // covariances with every other row are exactly 0 (exp_nonpos clamps; the distance keeps the
+    // Matern-2.5 derivative's x^3 finite for inverse ranges up to 1e72 and reaches the clamp for
+    // ranges up to 1e27), so the pair phase needs no masking selects
 #pragma unroll
-    for (int q = 0; q < kDMax; ++q) nbx[r * kDMax + q] = xr[q];
+    for (int q = 0; q < kDMax; ++q) nbx[r * kDMax + q] = rv ? xr[q] : (q == 0 ? 1e30 * (r + 1) : 0.);
 
     // observation-neighbour covariance c_r and its range derivative
     double cvec = 0., dcvec = 0.;
@@ -227,7 +253,7 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
 #pragma unroll
       for (int q = 0; q < kDMax; ++q) { const double t = xi[q] - xr[q]; s += t * t; }
       double cv, dcv;
-      cov_dcov<COV>(sqrt(s), var, phi, cv, dcv);
+      cov_dcov_sq<COV>(s, var, phi, cv, dcv);
       cvec = rv ? cv : 0.;
       dcvec = rv ? dcv : 0.;
     }
@@ -236,41 +262,108 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
     wave_lds_sync();
     mark(0);
 
-    // ---- 1. pairs (rr > cc): lanes l and l + K/2 share the rows {l mod K/2, K-1-l mod K/2}
+    // ---- 1. pairs (rr > cc): lanes l and l + K/2 share the rows {h, K-1-h}, h = l mod K/2: row h's
+    // pairs are q = 0..h-1, row K-1-h's are q = h..K-2 (column q - h); lane l takes q = 0..K/2-1,
+    // lane l + K/2 takes q = K/2..K-2. Per pair one compare selects between two precomputed bases
+    // (row, column-coordinate and packed-entry addresses), the rest is an immediate offset.
     {
-      // Branch-free (padding rows have zero coordinates and are masked by a select) and unrolled
-      // by 4 so independent sqrt/exp chains overlap (full unrolling exceeds 256 VGPRs).
       const int h = r & (K / 2 - 1);
       const int qlo = (r >= K / 2) ? K / 2 : 0;
+      const double* xA = nbx + h * kDMax;                       // row h
+      const double* xB = nbx + (K - 1 - h) * kDMax;             // row K-1-h
+      const double* cA = nbx + qlo * kDMax;                     // column q     (q < h)
+      const double* cB = nbx + (qlo - h) * kDMax;               // column q - h (q >= h)
+      double* pA = Cp + packed(h, 0) + qlo;                     // packed(h, q)
+      double* pB = Cp + packed(K - 1 - h, 0) - h + qlo;         // packed(K-1-h, q-h)
+      constexpr int dCoff = K * (K + 1) / 2;                    // dCp - Cp
 #pragma unroll kPairUnroll
       for (int qi = 0; qi < K / 2; ++qi) {
-        const int q = qlo + qi;
-        const bool lo = q < h;
-        const int rr = lo ? h : K - 1 - h;
-        const int cc = lo ? q : q - h;
+        const bool lo = qlo + qi < h;
+        const double* xrr = lo ? xA : xB;
+        const double* xcc = (lo ? cA : cB) + qi * kDMax;
+        double* pe = (lo ? pA : pB) + qi;
         double s = 0.;
 #pragma unroll
         for (int qq = 0; qq < kDMax; ++qq) {
-          const double t = nbx[rr * kDMax + qq] - nbx[cc * kDMax + qq];
+          const double t = xrr[qq] - xcc[qq];
           s += t * t;
         }
         double cv, dcv;
-        cov_dcov<COV>(sqrt(s), var, phi, cv, dcv);
-        if (q < K - 1) {
-          Cp[packed(rr, cc)] = rr < k ? cv : 0.;
-          dCp[packed(rr, cc)] = rr < k ? dcv : 0.;
+        cov_dcov_sq<COV>(s, var, phi, cv, dcv);
+        if (qi < K / 2 - 1 || qlo == 0) {   // lane l + K/2 has one pair less
+          pe[0] = cv;
+          pe[dCoff] = dcv;
         }
       }
     }
     wave_lds_sync();
+    if constexpr (BORDER) {   // border rows MK (c) and MK + 1 (y_nbr) of the packed image
+      if (r < MK) {
+        Cp[packed(MK, r)] = cvec;
+        Cp[packed(MK + 1, r)] = ynb;
+      }
+      wave_lds_sync();
+    }
     mark(1);
 
     // ---- 2. symmetric Gauss-Jordan on [C | c | y_nbr], row r in registers
-    double row[MK];
+    double row[NC];
 #pragma unroll
-    for (int c = 0; c < MK; ++c) row[c] = (c <= r) ? Cp[packed(r, c)] : Cp[packed(c, r)];
+    for (int c = 0; c < NC; ++c) row[c] = (c <= r) ? Cp[packed(r, c)] : Cp[packed(c, r)];
     double aug1 = cvec, aug2 = ynb;
-    if constexpr (DPPBC) {
+    if constexpr (BORDER) {
+      // native 16-byte vector type: HIP's double2 struct is loaded field-wise (ds_read2_b64, 4x the
+      // LDS cycles of ds_read_b128 per byte)
+      typedef double v2d __attribute__((ext_vector_type(2)));
+      const v2d* slot2 = reinterpret_cast<const v2d*>(__builtin_assume_aligned(slot_c, 16));
+      auto recip = [](double piv) {   // hardware reciprocal + two Newton steps (~1 ulp)
+        double x = __builtin_amdgcn_rcp(piv);
+        x = fma(x, fma(-piv, x, 1.), x);
+        return fma(x, fma(-piv, x, 1.), x);
+      };
+#if GPB_ROWS_PIVRCP
+      // The pivot lane publishes its pivot's reciprocal instead of the pivot: every lane computes
+      // the reciprocal of its own next diagonal entry right after updating that column (off the
+      // step's critical path), and only the pivot lane's copy is stored. Same value as the
+      // reciprocal of the broadcast pivot, so bitwise the same results.
+      double rnext = recip(row[0]);
+#endif
+#pragma unroll
+      for (int j = 0; j < MK; ++j) {
+        compiler_fence();
+#if GPB_ROWS_PIVRCP
+        slot_c[r] = (r == j) ? rnext : row[j];
+#else
+        slot_c[r] = row[j];
+#endif
+        wave_lds_sync();
+        double sv[NC];
+#pragma unroll
+        for (int p = j >> 1; p < NC / 2; ++p) {
+          const v2d v = slot2[p];
+          sv[2 * p] = v.x;
+          sv[2 * p + 1] = v.y;
+        }
+#if GPB_ROWS_PIVRCP
+        const double rinv = sv[j];
+#else
+        const double rinv = recip(sv[j]);
+#endif
+        const double q = row[j] * rinv;
+        const double f = (r == j) ? 0. : q;
+#pragma unroll
+        for (int c = j + 1; c < NC; ++c) {
+          row[c] = fma(-f, sv[c], row[c]);
+#if GPB_ROWS_PIVRCP
+          if (c == j + 1 && j + 1 < MK) rnext = recip(row[c]);
+#endif
+        }
+#pragma unroll
+        for (int c = j + 1; c < NC; ++c) asm volatile("" : "+v"(row[c]));
+      }
+      aug1 = row[NC - 2];
+      aug2 = row[NC - 1];
+    } else if constexpr (DPPBC) {
       // lane c holds row c, so M[c][j] = lane c's row[j]: broadcast lane c's register
       auto bc = [&](auto CPc, double v, double& lo, double& hi) {
         constexpr int cp = decltype(CPc)::value;
@@ -361,9 +454,11 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
     // entries with c >= k are exact zeros (padding rows of dC and of a), so the sum runs over
     // all K columns, unrolled with four partial sums
     double tq[4] = {0., 0., 0., 0.};
+    int rd = r;   // fresh addresses (not the row load's, which would stay live across the elimination)
+    if constexpr (BORDER) asm volatile("" : "+v"(rd));
 #pragma unroll
     for (int c = 0; c < MK; ++c) {
-      const double dcrc = (c < r) ? dCp[packed(r, c)] : dCp[packed(c, r)];
+      const double dcrc = (c < rd) ? dCp[packed(rd, c)] : dCp[packed(c, rd)];
       tq[c & 3] = fma(dcrc, slot_c[c], tq[c & 3]);
     }
     double t = (tq[0] + tq[1]) + (tq[2] + tq[3]);
@@ -406,7 +501,7 @@ __global__ void __launch_bounds__(block_threads<K>()) vecchia_rows_kernel(Vecchi
   // ---- block reduction of the per-group sums (fixed order -> deterministic)
   __syncthreads();
   double* red = smem;  // reuse: rows_per_block x kVecchiaSums
-  if (r == 0) {
+  if (r_lane == 0) {
 #pragma unroll
     for (int s = 0; s < kVecchiaSums; ++s) red[group_id * kVecchiaSums + s] = acc[s];
   }
@@ -706,6 +801,9 @@ bool use_v4(int K) {
 // reciprocal -> FMAs) is a dependent VALU sequence with DPP hazard waits, while the LDS form issues
 // the step's column reads as one burst whose latencies overlap.
 bool rows_dpp() { return std::getenv("GPBOOST_AMD_ROWS_DPP") != nullptr; }
+// Augmented entries: bordered rows (default where two lanes are spare) or the round-2 form with
+// separate augmented slots (GPBOOST_AMD_ROWS_SLOTS=1, A/B; read at every launch).
+bool rows_slots() { return std::getenv("GPBOOST_AMD_ROWS_SLOTS") != nullptr; }
 
 template <int K>
 int rows_per_block() { return use_v4(K) ? 64 / (K / 2) : (block_threads<K>() / 64) * (64 / K); }
@@ -739,8 +837,17 @@ void launch_k(const VecchiaRowsArgs& a, hipStream_t s) {
     if (!prof && a.m <= 30) {   // the headline configuration (m = 30): 30 elimination steps
       if (dpp)
         hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, 30, true>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
-      else
+      else if (rows_slots())
         hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, 30>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
+      else
+        hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, 30, false, true>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
+      HIP_CHECK(hipGetLastError());
+      return;
+    }
+  }
+  if constexpr (K == 16) {
+    if (!prof && !dpp && a.m <= K - 2 && !rows_slots()) {   // m <= 14: bordered, 14 steps
+      hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, K - 2, false, true>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
       HIP_CHECK(hipGetLastError());
       return;
     }

@@ -248,9 +248,12 @@ def test_baseline_size_matches_reference():
 
 @pytest.mark.parametrize("m", [10, 16, 20, 30, 31])
 def test_rows_dpp_broadcast_bitwise_equals_lds_form(m, monkeypatch):
-    """The row kernel's Gauss-Jordan broadcasts by LDS slots (default) and by DPP row broadcasts +
-    row-swap permutes (GPBOOST_AMD_ROWS_DPP=1, A/B form) move the same values into the same FMAs:
-    the evaluations must agree bit for bit (K = 16 and 32 lane groups, 30 and 32 elimination steps)."""
+    """The row kernel's Gauss-Jordan broadcasts by LDS slots (round-2 form, GPBOOST_AMD_ROWS_SLOTS=1)
+    and by DPP row broadcasts + row-swap permutes (GPBOOST_AMD_ROWS_DPP=1, A/B form) move the same
+    values into the same FMAs: the evaluations must agree bit for bit (K = 16 and 32 lane groups, 30
+    and 32 elimination steps). The default bordered form (augmented columns as two extra matrix rows)
+    reads the pivot row's augmented entries from the border rows instead, M[MK][j] for M[j][MK]:
+    equal up to rounding (1e-12 relative here)."""
     from gpboost_amd import GPModel, synthetic
     n = 20000
     X = synthetic.bench_coords(n)
@@ -258,8 +261,14 @@ def test_rows_dpp_broadcast_bitwise_equals_lds_form(m, monkeypatch):
     gm = GPModel(gp_coords=X, cov_function="matern", cov_fct_shape=1.5, gp_approx="vecchia", num_neighbors=m,
                  vecchia_ordering="random", seed=0)
     monkeypatch.delenv("GPBOOST_AMD_ROWS_DPP", raising=False)
-    a = gm.neg_log_likelihood_and_grad([0.1, 1.0, 0.1], Y, profile_sigma2=True)
+    monkeypatch.delenv("GPBOOST_AMD_ROWS_SLOTS", raising=False)
+    c = gm.neg_log_likelihood_and_grad([0.1, 1.0, 0.1], Y, profile_sigma2=True)
+    monkeypatch.setenv("GPBOOST_AMD_ROWS_SLOTS", "1")
+    a = gm.neg_log_likelihood_and_grad([0.1, 1.0, 0.1], None, profile_sigma2=True)
+    monkeypatch.delenv("GPBOOST_AMD_ROWS_SLOTS", raising=False)
     monkeypatch.setenv("GPBOOST_AMD_ROWS_DPP", "1")
     b = gm.neg_log_likelihood_and_grad([0.1, 1.0, 0.1], None, profile_sigma2=True)
     assert a[0] == b[0]
     assert np.array_equal(a[1], b[1])
+    assert abs(c[0] - a[0]) <= 1e-12 * abs(a[0])
+    np.testing.assert_allclose(c[1], a[1], rtol=1e-12)
