@@ -62,10 +62,13 @@ __device__ __forceinline__ void compiler_fence() { asm volatile("" ::: "memory")
 // Sum over a K-lane group (K = 16, 32, 64; smaller K by shuffles), result in every lane: the 16-lane DPP-row part by
 // VALU data movement (quad swaps, half-row and row mirrors), only the cross-row steps through
 // the LDS crossbar. Fixed order -> bitwise repeatable.
+// Every control used here has a source lane for every lane, so bound_ctrl (read 0 for a missing
+// source) never fires; it lets the move write all lanes without an initialised old value (the
+// update_dpp(0, ...) form costs two extra v_mov per double).
 template <int CTRL>
 __device__ __forceinline__ double dpp_f64(double v) {
-  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, false);
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
   return __hiloint2double(hi, lo);
 }
 #ifndef GPB_PERMLANE_SWAP
@@ -139,6 +142,39 @@ __device__ __forceinline__ double group_sum(double v) {
   return v;
 }
 
+// Eight sums over a 32-lane group (two DPP rows) at once. The cross-row step goes first and is
+// transposed: one row-swap permute of the pair (v[i], v[i + 4]) leaves the row-0 lanes holding
+// v[i] of both rows and the row-1 lanes v[i + 4] of both rows, so one add per pair halves the
+// values to four before the four in-row DPP steps (3 VALU per step per double instead of 5 per
+// step per sum). Result: lanes of row 0 hold the sums of v[0..3] in s[0..3], lanes of row 1 those
+// of v[4..7]. Every sum adds (row-0 part) + (row-1 part), then fixed DPP pairings: bitwise
+// repeatable.
+__device__ __forceinline__ void group_sum8_rows(const double v[8], double s[4]) {
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const auto pl = __builtin_amdgcn_permlane16_swap(__double2loint(v[q]), __double2loint(v[q + 4]), false, false);
+    const auto ph = __builtin_amdgcn_permlane16_swap(__double2hiint(v[q]), __double2hiint(v[q + 4]), false, false);
+    s[q] = __hiloint2double(ph[0], pl[0]) + __hiloint2double(ph[1], pl[1]);
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    double x = s[q];
+    x += dpp_f64<0xB1>(x);    // quad_perm [1,0,3,2]
+    x += dpp_f64<0x4E>(x);    // quad_perm [2,3,0,1]
+    x += dpp_f64<0x141>(x);   // row_half_mirror
+    x += dpp_f64<0x140>(x);   // row_mirror
+    s[q] = x;
+  }
+}
+
+// The odd DPP row's value of v in every lane of each row pair (row 1 -> rows 0 and 1).
+__device__ __forceinline__ double odd_row_value(double v) {
+  const unsigned lo = __double2loint(v), hi = __double2hiint(v);
+  const auto pl = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto ph = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  return __hiloint2double(ph[1], pl[1]);   // [0]: the even row's value, [1]: the odd row's
+}
+
 template <int K>
 constexpr int block_threads() { return K == 64 ? 64 : 128; }
 
@@ -175,7 +211,9 @@ __device__ unsigned long long g_rows_prof[8];
 // MK and MK + 1 (the bordered symmetric matrix [[C, c, y_nbr], [c^T ...], [y_nbr^T ...]]): a step
 // broadcasts ONE column (row j of the trailing block incl. the pivot row's augmented entries
 // M[j][MK] = M[MK][j]) by one LDS store, and the lanes read it back as 16-byte pairs.
-template <int K, int COV, bool PROF = false, int MK = K, bool DPPBC = false, bool BORDER = false>
+// DIM > 0: the coordinate dimension is known at compile time (DIM == a.d), else loops run to kDMax
+// over zero-padded coordinates.
+template <int K, int COV, bool PROF = false, int MK = K, bool DPPBC = false, bool BORDER = false, int DIM = 0>
 __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchia_rows_kernel(VecchiaRowsArgs a) {
   static_assert(!DPPBC || K == 16 || K == 32, "DPP broadcasts need 16- or 32-lane groups");
   static_assert(!BORDER || (!DPPBC && MK + 2 <= K && (MK & 1) == 0), "bordered form: two spare lanes, even width");
@@ -189,7 +227,10 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
   const int g = lane / K;
   const int r_lane = lane - g * K;
   const int group_id = wave * G + g;
-  const int d = a.d;
+  static_assert(DIM == 0 || (BORDER && DIM <= kDMax), "compile-time dimension: bordered form only");
+  constexpr int ND = DIM > 0 ? DIM : kDMax;   // coordinates per point in the distance loops
+  constexpr int CS = BORDER ? ND : kDMax;     // coordinate stride of the LDS copy (2: 16-byte reads)
+  const int d = DIM > 0 ? DIM : a.d;
   const double var = a.var, phi = a.phi;
   const double cdiag = var * a.diag_mult + a.diag_add;
   const double delta = cdiag - var;         // C - C_nonugget on the diagonal
@@ -197,8 +238,10 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
 
   double* Cp = smem + group_id * group_lds_doubles<K>();   // packed lower triangle of C (incl. diag)
   double* dCp = Cp + K * (K + 1) / 2;                       // packed lower triangle of dC/dlog(phi)
-  double* nbx = dCp + K * (K + 1) / 2;                      // K x kDMax
-  double* slot_c = nbx + K * kDMax;                         // column j of the current matrix
+  double* nbx = dCp + K * (K + 1) / 2;                      // K x kDMax (bordered: 2K x kDMax, two copies)
+  // bordered: the slot aliases the coordinates (read only in the pair phase, before the slot's first
+  // write; the next group's coordinate writes follow the slot reads in program order)
+  double* slot_c = BORDER ? nbx : nbx + K * kDMax;          // column j of the current matrix
   double* slot_a1 = slot_c + K;                             // augmented entries (c, y_nbr)
   double* slot_a2 = slot_a1 + K;
 
@@ -244,14 +287,20 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
     // Matern-2.5 derivative's x^3 finite for inverse ranges up to 1e72 and reaches the clamp for
     // ranges up to 1e27), so the pair phase needs no masking selects
 #pragma unroll
-    for (int q = 0; q < kDMax; ++q) nbx[r * kDMax + q] = rv ? xr[q] : (q == 0 ? 1e30 * (r + 1) : 0.);
+    for (int q = 0; q < kDMax; ++q) {
+      xr[q] = rv ? xr[q] : (q == 0 ? 1e30 * (r + 1) : 0.);
+      if (q < CS) {
+        nbx[r * CS + q] = xr[q];
+        if constexpr (BORDER) nbx[(r + K) * CS + q] = xr[q];   // second copy: partner r + delta < 2K
+      }
+    }
 
     // observation-neighbour covariance c_r and its range derivative
     double cvec = 0., dcvec = 0.;
     {
       double s = 0.;
 #pragma unroll
-      for (int q = 0; q < kDMax; ++q) { const double t = xi[q] - xr[q]; s += t * t; }
+      for (int q = 0; q < ND; ++q) { const double t = xi[q] - xr[q]; s += t * t; }
       double cv, dcv;
       cov_dcov_sq<COV>(s, var, phi, cv, dcv);
       cvec = rv ? cv : 0.;
@@ -266,7 +315,30 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
     // pairs are q = 0..h-1, row K-1-h's are q = h..K-2 (column q - h); lane l takes q = 0..K/2-1,
     // lane l + K/2 takes q = K/2..K-2. Per pair one compare selects between two precomputed bases
     // (row, column-coordinate and packed-entry addresses), the rest is an immediate offset.
-    {
+    if constexpr (BORDER) {
+      // lane r computes the pairs {r, (r + delta) mod K}, delta = 1..K/2 (circulant split: every
+      // pair once, the K/2 pairs of delta = K/2 twice with identical values). Own coordinates stay
+      // in registers, the partner's are read from the second coordinate copy at an immediate
+      // offset; the destination packed(r + delta, r) = T(r) + r + r delta + T(delta) or, past the
+      // wrap, packed(r, r + delta - K) = T(r) + r + delta - K (T(x) = x (x + 1) / 2).
+      constexpr int dCoff = K * (K + 1) / 2;   // dCp - Cp
+      const int base = r * (r + 1) / 2 + r;
+#pragma unroll
+      for (int dl = 1; dl <= K / 2; ++dl) {
+        const double* xp = nbx + (r + dl) * CS;
+        double s = 0.;
+#pragma unroll
+        for (int qq = 0; qq < ND; ++qq) {
+          const double t = xr[qq] - xp[qq];
+          s += t * t;
+        }
+        double cv, dcv;
+        cov_dcov_sq<COV>(s, var, phi, cv, dcv);
+        const int pos = (r + dl < K) ? base + r * dl + dl * (dl + 1) / 2 : base + dl - K;
+        Cp[pos] = cv;
+        Cp[pos + dCoff] = dcv;
+      }
+    } else {
       const int h = r & (K / 2 - 1);
       const int qlo = (r >= K / 2) ? K / 2 : 0;
       const double* xA = nbx + h * kDMax;                       // row h
@@ -441,8 +513,17 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
     double mydiag = row[0];
 #pragma unroll
     for (int c = 1; c < MK; ++c) mydiag = (c == r) ? row[c] : mydiag;
-    const double av_r = rv ? aug1 / mydiag : 0.;   // a = C^-1 c (lanes r >= MK hold no row)
-    const double vv_r = rv ? aug2 / mydiag : 0.;   // v = C^-1 y_nbr
+    double av_r, vv_r;
+    if constexpr (BORDER) {   // one reciprocal (rcp + two Newton steps, ~1 ulp) for both quotients
+      double dinv = __builtin_amdgcn_rcp(mydiag);
+      dinv = fma(dinv, fma(-mydiag, dinv, 1.), dinv);
+      dinv = fma(dinv, fma(-mydiag, dinv, 1.), dinv);
+      av_r = rv ? aug1 * dinv : 0.;   // a = C^-1 c (lanes r >= MK hold no row)
+      vv_r = rv ? aug2 * dinv : 0.;   // v = C^-1 y_nbr
+    } else {
+      av_r = rv ? aug1 / mydiag : 0.;
+      vv_r = rv ? aug2 / mydiag : 0.;
+    }
 
     if (active && a.B_out != nullptr && r < a.m) a.B_out[(size_t)(i - a.row_base) * a.m + r] = rv ? -av_r : 0.;
     mark(2);
@@ -466,14 +547,32 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
     mark(3);
 
     // ---- group reductions
-    const double ac = group_sum<K>(av_r * cvec);
-    const double ay = group_sum<K>(av_r * ynb);
-    const double aa = group_sum<K>(av_r * av_r);
-    const double avv = group_sum<K>(av_r * vv_r);
-    const double dca = group_sum<K>(dcvec * av_r);
-    const double dcv = group_sum<K>(dcvec * vv_r);
-    const double ta = group_sum<K>(t * av_r);
-    const double tv = group_sum<K>(t * vv_r);
+    double ac, ay, aa, avv, dD_rng, uk_rng;
+    if constexpr (K == 32) {
+      // row 0 of the group sums {ac, ay, aa, avv}, row 1 {dca, dcv, ta, tv}; row 1 forms the two
+      // range terms and hands them to row 0
+      const double v8[8] = {av_r * cvec, av_r * ynb, av_r * av_r, av_r * vv_r,
+                            dcvec * av_r, dcvec * vv_r, t * av_r, t * vv_r};
+      double s4[4];
+      group_sum8_rows(v8, s4);
+      ac = s4[0];
+      ay = s4[1];
+      aa = s4[2];
+      avv = s4[3];
+      dD_rng = odd_row_value(-(2. * s4[0] - s4[2]));   // row 1: -(2 dca - ta)
+      uk_rng = odd_row_value(-(s4[1] - s4[3]));        // row 1: -(dcv - tv)
+    } else {
+      ac = group_sum<K>(av_r * cvec);
+      ay = group_sum<K>(av_r * ynb);
+      aa = group_sum<K>(av_r * av_r);
+      avv = group_sum<K>(av_r * vv_r);
+      const double dca = group_sum<K>(dcvec * av_r);
+      const double dcv = group_sum<K>(dcvec * vv_r);
+      const double ta = group_sum<K>(t * av_r);
+      const double tv = group_sum<K>(t * vv_r);
+      dD_rng = -(2. * dca - ta);                         // dD/dlog phi
+      uk_rng = -(dcv - tv);                              // (dB_range y)_i
+    }
 
     const double D = var + a.d_nugget - ac;          // Vecchia_utils.cpp:1351, 1507, 1562
     const double Dinv = 1. / D;
@@ -483,8 +582,6 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
       const double u = By * Dinv;                        // (D^-1 B y)_i
       const double dD_var = var - delta * aa - ac;       // dD/dlog var
       const double uk_var = -delta * avv;                // (dB_var y)_i
-      const double dD_rng = -(2. * dca - ta);            // dD/dlog phi
-      const double uk_rng = -(dcv - tv);                 // (dB_range y)_i
       acc[0] += log(D);
       acc[1] += By * u;
       acc[2] += uk_var * u - 0.5 * u * u * dD_var;
@@ -839,6 +936,8 @@ void launch_k(const VecchiaRowsArgs& a, hipStream_t s) {
         hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, 30, true>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
       else if (rows_slots())
         hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, 30>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
+      else if (a.d == 2)   // planar coordinates (the BASELINE configurations)
+        hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, 30, false, true, 2>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
       else
         hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, 30, false, true>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
       HIP_CHECK(hipGetLastError());
