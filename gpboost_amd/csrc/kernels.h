@@ -27,9 +27,8 @@ struct VecchiaRowsArgs {
                          // predictions: the rows after the observed ones)
 };
 
-// Returns the number of blocks used (needed to size/finish block_sums).
-int vecchia_rows_blocks(int rows, int m);
-void launch_vecchia_rows(int cov_type, const VecchiaRowsArgs& a, hipStream_t s);
+int vecchia_rows_blocks(int rows, int m);   // upper bound of the grid (block-partial buffer size)
+int launch_vecchia_rows(int cov_type, const VecchiaRowsArgs& a, hipStream_t s);   // returns the grid size
 // Predictions from the prediction rows' factor: out[p] = -sum_r B[p, r] y[nbr[p, r]] (mean),
 // out[n_pred + p] = (1 / Dinv[p] - nugget_sub) * sigma2 (variance). B, nbr: n_pred x m.
 void launch_predict_mean_var(int n_pred, int m, const int* nbr, const double* B, const double* Dinv, const double* y,

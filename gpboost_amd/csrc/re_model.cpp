@@ -370,12 +370,12 @@ void REModelAMD::LaunchVecchiaRows(const double* trafo, int r0, int r1, double* 
   a.diag_add = 1.;
   a.d_nugget = 1.;
   a.block_sums = d_block_sums_.get();
-  const int nblocks = vecchia_rows_blocks(r1 - r0, a.m);
+  int nblocks = 0;   // the launch's grid (<= vecchia_rows_blocks, the buffer size)
   // HIP events cost ~10 us of host time per evaluation (a quarter of the host overhead): recorded
   // only once GetLastKernelTimes has been called
   const bool timing = timing_;
   if (timing) HIP_CHECK(hipEventRecord(ev_[0], stream_));
-  launch_vecchia_rows(cfg_.cov_type, a, stream_);
+  nblocks = launch_vecchia_rows(cfg_.cov_type, a, stream_);
   if (timing) HIP_CHECK(hipEventRecord(ev_[1], stream_));
   if (allreduce && coll_ != nullptr) {
     launch_sum_blocks(d_block_sums_.get(), nblocks, kVecchiaSums, d_sums_.get(), stream_);

@@ -30,6 +30,7 @@
 // Optional outputs D^-1 and B(i, nbr) = -a are written for the factor API.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <type_traits>
@@ -178,9 +179,11 @@ __device__ __forceinline__ double odd_row_value(double v) {
 template <int K>
 constexpr int block_threads() { return K == 64 ? 64 : 128; }
 
-template <int K>
+template <int K, bool BORDER = false>
 constexpr int group_lds_doubles() {
-  return K * (K + 1) + kDMax * K + 3 * K;  // packed C + packed dC + neighbour coords + 3 broadcast slots
+  // packed C + packed dC + neighbour coords + 3 broadcast slots; bordered: packed C (dC in its
+  // circulant layout over it after the row load) + two coordinate copies (the slots alias them)
+  return BORDER ? K * (K + 1) / 2 + 2 * kDMax * K : K * (K + 1) + kDMax * K + 3 * K;
 }
 
 __device__ __forceinline__ int packed(int r, int c) {  // r >= c
@@ -198,6 +201,9 @@ __device__ unsigned long long g_rows_prof[8];
 // FMA order: bitwise identical results.
 #ifndef GPB_ROWS_WAVES
 #define GPB_ROWS_WAVES 0
+#endif
+#ifndef GPB_PAIR_CHAIN
+#define GPB_PAIR_CHAIN 0
 #endif
 #ifndef GPB_ROWS_PIVRCP
 #define GPB_ROWS_PIVRCP 0
@@ -236,9 +242,11 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
   const double delta = cdiag - var;         // C - C_nonugget on the diagonal
   const bool want_like = a.Y != nullptr;
 
-  double* Cp = smem + group_id * group_lds_doubles<K>();   // packed lower triangle of C (incl. diag)
-  double* dCp = Cp + K * (K + 1) / 2;                       // packed lower triangle of dC/dlog(phi)
-  double* nbx = dCp + K * (K + 1) / 2;                      // K x kDMax (bordered: 2K x kDMax, two copies)
+  double* Cp = smem + group_id * group_lds_doubles<K, BORDER>();   // packed lower triangle of C (incl. diag)
+  // packed lower triangle of dC/dlog(phi); bordered: dC lives in registers through the row load,
+  // then in the circulant layout W[(delta - 1) K + r] over the packed C
+  double* dCp = BORDER ? Cp : Cp + K * (K + 1) / 2;
+  double* nbx = Cp + (BORDER ? 1 : 2) * (K * (K + 1) / 2);  // K x kDMax (bordered: 2K x CS, two copies)
   // bordered: the slot aliases the coordinates (read only in the pair phase, before the slot's first
   // write; the next group's coordinate writes follow the slot reads in program order)
   double* slot_c = BORDER ? nbx : nbx + K * kDMax;          // column j of the current matrix
@@ -307,10 +315,11 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
       dcvec = rv ? dcv : 0.;
     }
     Cp[packed(r, r)] = rv ? cdiag : 1.;
-    dCp[packed(r, r)] = 0.;
+    if constexpr (!BORDER) dCp[packed(r, r)] = 0.;
     wave_lds_sync();
     mark(0);
 
+    double wst[K / 2];   // bordered: dC of the lane's circulant pairs (delta = 1..K/2)
     // ---- 1. pairs (rr > cc): lanes l and l + K/2 share the rows {h, K-1-h}, h = l mod K/2: row h's
     // pairs are q = 0..h-1, row K-1-h's are q = h..K-2 (column q - h); lane l takes q = 0..K/2-1,
     // lane l + K/2 takes q = K/2..K-2. Per pair one compare selects between two precomputed bases
@@ -321,7 +330,6 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
       // in registers, the partner's are read from the second coordinate copy at an immediate
       // offset; the destination packed(r + delta, r) = T(r) + r + r delta + T(delta) or, past the
       // wrap, packed(r, r + delta - K) = T(r) + r + delta - K (T(x) = x (x + 1) / 2).
-      constexpr int dCoff = K * (K + 1) / 2;   // dCp - Cp
       const int base = r * (r + 1) / 2 + r;
 #pragma unroll
       for (int dl = 1; dl <= K / 2; ++dl) {
@@ -336,7 +344,12 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
         cov_dcov_sq<COV>(s, var, phi, cv, dcv);
         const int pos = (r + dl < K) ? base + r * dl + dl * (dl + 1) / 2 : base + dl - K;
         Cp[pos] = cv;
-        Cp[pos + dCoff] = dcv;
+        wst[dl - 1] = dcv;
+#if GPB_PAIR_CHAIN
+        // one pair in flight: the next pair's distance waits for this pair's results (bounds the
+        // registers of the unrolled phase, which also holds the dC values)
+        asm volatile("" : "+v"(xr[0]) : "v"(cv), "v"(dcv));
+#endif
       }
     } else {
       const int h = r & (K / 2 - 1);
@@ -382,6 +395,13 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
     double row[NC];
 #pragma unroll
     for (int c = 0; c < NC; ++c) row[c] = (c <= r) ? Cp[packed(r, c)] : Cp[packed(c, r)];
+    if constexpr (BORDER) {
+      // dC over the packed C in the circulant layout (lane base + immediate; the row reads above
+      // precede these writes in the wave's LDS order)
+      compiler_fence();
+#pragma unroll
+      for (int dl = 1; dl <= K / 2; ++dl) dCp[(dl - 1) * K + r] = wst[dl - 1];
+    }
     double aug1 = cvec, aug2 = ynb;
     if constexpr (BORDER) {
       // native 16-byte vector type: HIP's double2 struct is loaded field-wise (ds_read2_b64, 4x the
@@ -528,22 +548,50 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
     if (active && a.B_out != nullptr && r < a.m) a.B_out[(size_t)(i - a.row_base) * a.m + r] = rv ? -av_r : 0.;
     mark(2);
 
-    // ---- 3. t = dC a (dC from the packed image; its diagonal is 0)
-    compiler_fence();
-    slot_c[r] = av_r;
-    wave_lds_sync();
-    // entries with c >= k are exact zeros (padding rows of dC and of a), so the sum runs over
-    // all K columns, unrolled with four partial sums
-    double tq[4] = {0., 0., 0., 0.};
-    int rd = r;   // fresh addresses (not the row load's, which would stay live across the elimination)
-    if constexpr (BORDER) asm volatile("" : "+v"(rd));
+    // ---- 3. the dC forms a^T dC a and v^T dC a. Bordered: per lane over its circulant pairs
+    // {r, p = r + delta}: with S1 = sum_{delta < K/2} w a_p, S1h = w_{K/2} a_{p}, S2 = sum_{delta < K/2} w v_p,
+    // lane r adds a_r (2 S1 + S1h) to a^T dC a and v_r (S1 + S1h) + a_r S2 to v^T dC a (every ordered
+    // pair once; the delta = K/2 pairs are held by both of their lanes). [a, v] pairs sit in a
+    // doubled slot array, so p's entry is a 16-byte read at an immediate offset.
+    double tA, tV;   // this lane's shares of a^T dC a and v^T dC a
+    if constexpr (BORDER) {
+      typedef double v2d __attribute__((ext_vector_type(2)));
+      v2d* av2 = reinterpret_cast<v2d*>(__builtin_assume_aligned(nbx, 16));
+      compiler_fence();
+      const v2d mine = {av_r, vv_r};
+      av2[r] = mine;
+      av2[r + K] = mine;
+      wave_lds_sync();
+      double s1[2] = {0., 0.}, s2[2] = {0., 0.};
 #pragma unroll
-    for (int c = 0; c < MK; ++c) {
-      const double dcrc = (c < rd) ? dCp[packed(rd, c)] : dCp[packed(c, rd)];
-      tq[c & 3] = fma(dcrc, slot_c[c], tq[c & 3]);
+      for (int dl = 1; dl < K / 2; ++dl) {
+        const double w = dCp[(dl - 1) * K + r];
+        const v2d pv = av2[r + dl];
+        s1[dl & 1] = fma(w, pv.x, s1[dl & 1]);
+        s2[dl & 1] = fma(w, pv.y, s2[dl & 1]);
+      }
+      const double s1h = dCp[(K / 2 - 1) * K + r] * av2[r + K / 2].x;
+      const double S1 = s1[0] + s1[1], S2 = s2[0] + s2[1];
+      tA = av_r * (2. * S1 + s1h);
+      tV = vv_r * (S1 + s1h) + av_r * S2;
+    } else {
+      // t = dC a (dC from the packed image; its diagonal is 0)
+      compiler_fence();
+      slot_c[r] = av_r;
+      wave_lds_sync();
+      // entries with c >= k are exact zeros (padding rows of dC and of a), so the sum runs over
+      // all K columns, unrolled with four partial sums
+      double tq[4] = {0., 0., 0., 0.};
+#pragma unroll
+      for (int c = 0; c < MK; ++c) {
+        const double dcrc = (c < r) ? dCp[packed(r, c)] : dCp[packed(c, r)];
+        tq[c & 3] = fma(dcrc, slot_c[c], tq[c & 3]);
+      }
+      double t = (tq[0] + tq[1]) + (tq[2] + tq[3]);
+      t = rv ? t : 0.;
+      tA = t * av_r;
+      tV = t * vv_r;
     }
-    double t = (tq[0] + tq[1]) + (tq[2] + tq[3]);
-    t = rv ? t : 0.;
     mark(3);
 
     // ---- group reductions
@@ -552,7 +600,7 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
       // row 0 of the group sums {ac, ay, aa, avv}, row 1 {dca, dcv, ta, tv}; row 1 forms the two
       // range terms and hands them to row 0
       const double v8[8] = {av_r * cvec, av_r * ynb, av_r * av_r, av_r * vv_r,
-                            dcvec * av_r, dcvec * vv_r, t * av_r, t * vv_r};
+                            dcvec * av_r, dcvec * vv_r, tA, tV};
       double s4[4];
       group_sum8_rows(v8, s4);
       ac = s4[0];
@@ -568,8 +616,8 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
       avv = group_sum<K>(av_r * vv_r);
       const double dca = group_sum<K>(dcvec * av_r);
       const double dcv = group_sum<K>(dcvec * vv_r);
-      const double ta = group_sum<K>(t * av_r);
-      const double tv = group_sum<K>(t * vv_r);
+      const double ta = group_sum<K>(tA);
+      const double tv = group_sum<K>(tV);
       dD_rng = -(2. * dca - ta);                         // dD/dlog phi
       uk_rng = -(dcv - tv);                              // (dB_range y)_i
     }
@@ -912,8 +960,42 @@ int blocks_for(int rows) {
   return need < kMaxBlocks ? need : kMaxBlocks;
 }
 
+// Upper bound of any launch's grid (block-partial buffers are sized by it).
+constexpr int kMaxBlocksAny = 2048;
+static_assert(kMaxBlocks <= kMaxBlocksAny, "grid cap");
+
+// Bordered forms: the grid is the resident capacity (blocks per CU from the occupancy calculator
+// for this instance's registers and LDS, times the CU count), so every block strides over an
+// equal share of row groups in a single round.
+template <class KernelT>
+int resident_grid(KernelT kernel, int threads, size_t lds, int rows, int rpb) {
+  static int cap = 0;   // per kernel instance (one static per template instantiation)
+  if (cap == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kernel, threads, lds));
+    cap = std::max(1, std::min(per_cu * cus, kMaxBlocksAny));
+  }
+  const int need = (rows + rpb - 1) / rpb;
+  return need < cap ? need : cap;
+}
+
+template <int K, int COV, int MK, int DIM>
+int launch_border(const VecchiaRowsArgs& a, hipStream_t s) {
+  constexpr int rpb = (block_threads<K>() / 64) * (64 / K);
+  const size_t red = (size_t)rpb * kVecchiaSums * sizeof(double);
+  size_t lds = (size_t)rpb * group_lds_doubles<K, true>() * sizeof(double);
+  if (lds < red) lds = red;
+  auto kern = vecchia_rows_kernel<K, COV, false, MK, false, true, DIM>;
+  const int blocks = resident_grid(kern, block_threads<K>(), lds, a.r1 - a.r0, rpb);
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(block_threads<K>()), lds, s, a);
+  HIP_CHECK(hipGetLastError());
+  return blocks;
+}
+
 template <int K, int COV>
-void launch_k(const VecchiaRowsArgs& a, hipStream_t s) {
+int launch_k(const VecchiaRowsArgs& a, hipStream_t s) {
   const int rpb = rows_per_block<K>();
   const int blocks = blocks_for<K>(a.r1 - a.r0);
   const size_t red = (size_t)rpb * kVecchiaSums * sizeof(double);
@@ -923,7 +1005,7 @@ void launch_k(const VecchiaRowsArgs& a, hipStream_t s) {
       if (lds < red) lds = red;
       hipLaunchKernelGGL((vecchia_rows2_kernel<K, COV>), dim3(blocks), dim3(kV4Threads), lds, s, a);
       HIP_CHECK(hipGetLastError());
-      return;
+      return blocks;
     }
   }
   size_t lds = (size_t)rpb * group_lds_doubles<K>() * sizeof(double);
@@ -932,30 +1014,27 @@ void launch_k(const VecchiaRowsArgs& a, hipStream_t s) {
   const bool dpp = rows_dpp();
   if constexpr (K == 32) {
     if (!prof && a.m <= 30) {   // the headline configuration (m = 30): 30 elimination steps
-      if (dpp)
+      if (dpp) {
         hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, 30, true>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
-      else if (rows_slots())
+      } else if (rows_slots()) {
         hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, 30>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
-      else if (a.d == 2)   // planar coordinates (the BASELINE configurations)
-        hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, 30, false, true, 2>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
-      else
-        hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, 30, false, true>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
+      } else if (a.d == 2) {   // planar coordinates (the BASELINE configurations)
+        return launch_border<K, COV, 30, 2>(a, s);
+      } else {
+        return launch_border<K, COV, 30, 0>(a, s);
+      }
       HIP_CHECK(hipGetLastError());
-      return;
+      return blocks;
     }
   }
   if constexpr (K == 16) {
-    if (!prof && !dpp && a.m <= K - 2 && !rows_slots()) {   // m <= 14: bordered, 14 steps
-      hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, K - 2, false, true>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
-      HIP_CHECK(hipGetLastError());
-      return;
-    }
+    if (!prof && !dpp && a.m <= K - 2 && !rows_slots()) return launch_border<K, COV, K - 2, 0>(a, s);   // m <= 14
   }
   if constexpr (K == 16 || K == 32) {
     if (!prof && dpp) {
       hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, K, true>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
       HIP_CHECK(hipGetLastError());
-      return;
+      return blocks;
     }
   }
   if (prof) {
@@ -969,39 +1048,38 @@ void launch_k(const VecchiaRowsArgs& a, hipStream_t s) {
     hipLaunchKernelGGL((vecchia_rows_kernel<K, COV>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
   }
   HIP_CHECK(hipGetLastError());
+  return blocks;
 }
 
 template <int K>
-void launch_cov(int cov, const VecchiaRowsArgs& a, hipStream_t s) {
+int launch_cov(int cov, const VecchiaRowsArgs& a, hipStream_t s) {
   switch (cov) {
-    case kMatern05: launch_k<K, kMatern05>(a, s); break;
-    case kMatern15: launch_k<K, kMatern15>(a, s); break;
-    case kMatern25: launch_k<K, kMatern25>(a, s); break;
-    case kGaussian: launch_k<K, kGaussian>(a, s); break;
+    case kMatern05: return launch_k<K, kMatern05>(a, s);
+    case kMatern15: return launch_k<K, kMatern15>(a, s);
+    case kMatern25: return launch_k<K, kMatern25>(a, s);
+    case kGaussian: return launch_k<K, kGaussian>(a, s);
     default: Fatal("unsupported covariance type %d", cov);
   }
+  return 0;
 }
 
 }  // namespace
 
 int vecchia_rows_blocks(int rows, int m) {
-  switch (lanes_for_m(m)) {
-    case 16: return blocks_for<16>(rows);
-    case 32: return blocks_for<32>(rows);
-    case 64: return blocks_for<64>(rows);
-    default: Fatal("num_neighbors = %d > 64 is not supported by the GPU Vecchia kernel", m);
-  }
+  if (lanes_for_m(m) == 0) Fatal("num_neighbors = %d > 64 is not supported by the GPU Vecchia kernel", m);
+  return std::min(std::max(rows, 1), kMaxBlocksAny);   // >= any launch's grid (one row group per block at least)
 }
 
-void launch_vecchia_rows(int cov_type, const VecchiaRowsArgs& a, hipStream_t s) {
+int launch_vecchia_rows(int cov_type, const VecchiaRowsArgs& a, hipStream_t s) {
   if (a.d < 1 || a.d > kDMax) Fatal("GPU Vecchia kernel supports 1 <= dim_gp_coords <= %d, got %d", kDMax, a.d);
-  if (a.r1 <= a.r0) return;
+  if (a.r1 <= a.r0) return 0;
   switch (lanes_for_m(a.m)) {
-    case 16: launch_cov<16>(cov_type, a, s); break;
-    case 32: launch_cov<32>(cov_type, a, s); break;
-    case 64: launch_cov<64>(cov_type, a, s); break;
+    case 16: return launch_cov<16>(cov_type, a, s);
+    case 32: return launch_cov<32>(cov_type, a, s);
+    case 64: return launch_cov<64>(cov_type, a, s);
     default: Fatal("num_neighbors = %d > 64 is not supported by the GPU Vecchia kernel", a.m);
   }
+  return 0;
 }
 
 void launch_predict_mean_var(int n_pred, int m, const int* nbr, const double* B, const double* Dinv, const double* y,
