@@ -280,15 +280,14 @@ int GPB_SetPredictionData(REModelHandle handle, int32_t num_data_pred, const int
                           const double* covariate_data_pred, const char* vecchia_pred_type, int num_neighbors_pred,
                           double cg_delta_conv_pred, int nsim_var_pred, int rank_pred_approx_matrix_lanczos) {
   API_BEGIN();
-  (void)cg_delta_conv_pred;
-  (void)nsim_var_pred;
+  (void)cg_delta_conv_pred;   // the Vecchia-Laplace draws use the model's cg_delta_conv (likelihoods.h:12052)
   (void)rank_pred_approx_matrix_lanczos;
   if (num_data_pred > 0 || cluster_ids_data_pred != nullptr || re_group_data_pred != nullptr ||
       re_group_rand_coef_data_pred != nullptr || gp_coords_data_pred != nullptr || gp_rand_coef_data_pred != nullptr ||
       covariate_data_pred != nullptr)
     gpb_amd::Fatal("GPB_SetPredictionData: saving prediction data is not supported by gpboost_amd; pass the "
                    "prediction coordinates to GPB_PredictREModel");
-  model(handle)->SetPredictionData(vecchia_pred_type, num_neighbors_pred);
+  model(handle)->SetPredictionData(vecchia_pred_type, num_neighbors_pred, nsim_var_pred);
   API_END();
 }
 
@@ -325,6 +324,8 @@ int GPB_PredictREModel(REModelHandle handle, const double* y_data, int32_t num_d
     y = r.data();
   } else if (covariate_data_pred != nullptr) {
     gpb_amd::Fatal("Covariate data 'X_pred' is provided but the model has no covariates");
+  } else if (m->config().latent) {   // non-Gaussian: F is the offset of the location parameter (the mode)
+    m->SetLatentOffset(fixed_effects);
   } else if (fixed_effects != nullptr) {   // the GP part of the response (re_model_template.h:3386-3393)
     if (y_data == nullptr) gpb_amd::Fatal("'y_data' cannot be NULL when 'fixed_effects' is provided");
     r.resize(m->config().n);

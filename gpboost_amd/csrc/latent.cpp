@@ -501,6 +501,42 @@ void LatentVecchia::EnsureProbes(const IterativeConfig& cfg) {
   probes_saved_ = cfg.reuse_rand_vec_trace;
 }
 
+void LatentVecchia::PredVarSim(int nsim, int t, double delta, int cg_max, uint64_t seed, int n_pred, int mp,
+                               const int* nbr_vo, const double* d_Bpo, double* acc) {
+  if (!factor_ready_) Fatal("predictive variances need an evaluated latent model (mode and factor)");
+  if (world_ > 1) Fatal("latent predictive variances are only available on single-rank models");
+  t = std::max(1, std::min({t, nsim, 64}));
+  // neighbour indices in storage labels (Z rows)
+  std::vector<int> nb((size_t)n_pred * mp);
+  for (size_t e = 0; e < nb.size(); ++e) nb[e] = lab_[nbr_vo[e]];
+  DevBuf<int> d_nb(nb.size());
+  DevBuf<double> d_acc(n_pred), d_sdi(n_), d_sw(n_), d_e1((size_t)n_ * t), d_e2((size_t)n_ * t), d_rhs((size_t)n_ * t),
+      d_z((size_t)n_ * t);
+  HIP_CHECK(hipMemcpyAsync(d_nb.get(), nb.data(), sizeof(int) * nb.size(), hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipMemsetAsync(d_acc.get(), 0, sizeof(double) * n_pred, s_));
+  launch_sqrt_vec(n_, d_Dinv_.get(), d_sdi.get(), s_);   // D^-1/2
+  launch_sqrt_vec(n_, d_W_.get(), d_sw.get(), s_);       // W^1/2 (likelihoods.h:6661: W >= 0 checked there)
+  Block& b = GetBlock(2, t, cg_max);
+  for (int done = 0; done < nsim; done += t) {
+    const int tc = std::min(t, nsim - done);   // the last block's extra columns are zero right-hand sides
+    launch_gen_normal(n_, t, seed, 1, done, d_e1.get(), s_);
+    launch_gen_normal(n_, t, seed, 2, done, d_e2.get(), s_);
+    if (tc < t) {   // columns >= tc: zero draws (zero right-hand side -> z = 0, no contribution)
+      for (int c = tc; c < t; ++c) {
+        HIP_CHECK(hipMemset2DAsync(d_e1.get() + c, sizeof(double) * t, 0, sizeof(double), n_, s_));
+        HIP_CHECK(hipMemset2DAsync(d_e2.get() + c, sizeof(double) * t, 0, sizeof(double), n_, s_));
+      }
+    }
+    // rhs = B^T D^-1/2 e1 + W^1/2 e2 (likelihoods.h:6711), storage order
+    launch_bt_apply(sp_, d_Bv_.get(), true, d_e1.get(), t, d_sdi.get(), d_sw.get(), d_e2.get(), d_rhs.get(), s_);
+    const PcgResult pr = Pcg(b, d_rhs.get(), d_z.get(), t, true, true, cg_max, 0, delta);
+    if (pr.nan) Fatal("NaN or Inf in the conjugate gradient solves of the predictive-variance simulation");
+    launch_pred_sq_acc(n_pred, mp, t, d_nb.get(), d_Bpo, d_z.get(), d_acc.get(), s_);
+  }
+  HIP_CHECK(hipMemcpyAsync(acc, d_acc.get(), sizeof(double) * n_pred, hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+}
+
 void LatentVecchia::BenchOperators(int t, int reps, double* out) {
   if (!factor_ready_) Fatal("BenchOperators needs a previous evaluation (the factor of its parameters)");
   if (t < 1 || reps < 1) Fatal("BenchOperators: t and reps must be >= 1");

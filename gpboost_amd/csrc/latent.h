@@ -86,6 +86,15 @@ class LatentVecchia {
   // the unit diagonal, out[3] = dependent launches per preconditioner application.
   void BenchOperators(int t, int reps, double* out);
 
+  // Predictive-variance simulation of PredictLaplaceApproxVecchia (likelihoods.h:6628-6746,
+  // iterative): nsim draws z ~ N(0, (Sigma^-1 + W)^-1), each the solution of (Sigma^-1 + W) z =
+  // B^T D^-1/2 e1 + W^1/2 e2 by the VADU-preconditioned CG (own stopping rule ||r|| < delta per draw,
+  // as CGVecchiaLaplaceVec), t draws per block of independent columns; returns acc[p] = sum over the
+  // draws of (Bpo z)_p^2 (host, n_pred). Uses the factor, W and preconditioner of the last Eval.
+  // nbr_vo: host n_pred x mp neighbour indices (latent Vecchia rows), d_Bpo: device n_pred x mp.
+  void PredVarSim(int nsim, int t, double delta, int cg_max, uint64_t seed, int n_pred, int mp, const int* nbr_vo,
+                  const double* d_Bpo, double* acc);
+
   // Probe-column sharding (SURVEY.md §8e Option A): rank r of `world` runs the probe columns
   // [t r / world, t (r+1) / world) of every SLQ block — padded to ceil(t / world) columns, so
   // every rank's blocks have the same width and the replicated Newton / mode columns are

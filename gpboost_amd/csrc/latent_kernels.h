@@ -374,4 +374,16 @@ void launch_mode_deriv(const ModeDerivArgs& a, hipStream_t s);
 void launch_grad_f(int n, const double* d1, const double* dmll, const double* W, const double* vS, double* out,
                    hipStream_t s);
 
+// ---- latent predictions (latent_pred.hip)
+// out (n x t row-major) ~ N(0, 1): counter-based, a function of (seed, stream, column c0 + c, row)
+void launch_gen_normal(int n, int t, uint64_t seed, int stream, long c0, double* out, hipStream_t s);
+void launch_sqrt_vec(int n, const double* x, double* y, hipStream_t s);
+// acc[p] += sum_c (sum_r B[p, r] Z[nbr[p, r], c])^2 for the t <= 64 columns of Z (n x t row-major)
+// bernoulli_logit response means (adaptive Gauss-Hermite, likelihoods.h:7857-7889) at latent N(mean, var);
+// out_var (nullable) = p (1 - p). nodes / aw: the order-point rule, aw = w exp(x^2) (device).
+void launch_resp_logit(int n, const double* mean, const double* var, const double* nodes, const double* aw, int order,
+                       double delta, double* out_mean, double* out_var, hipStream_t s);
+void launch_pred_sq_acc(int n_pred, int mp, int t, const int* nbr, const double* B, const double* Z, double* acc,
+                        hipStream_t s);
+
 }  // namespace gpb_amd

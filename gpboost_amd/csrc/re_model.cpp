@@ -241,7 +241,8 @@ void REModelAMD::SetDistributedHost(int rank, int world, HostAllReduceFn fn, voi
   ApplyPartition(rank, world);
 }
 
-void REModelAMD::SetPredictionData(const char* vecchia_pred_type, int num_neighbors_pred) {
+void REModelAMD::SetPredictionData(const char* vecchia_pred_type, int num_neighbors_pred, int nsim_var_pred) {
+  if (nsim_var_pred > 0) nsim_var_pred_ = nsim_var_pred;
   if (vecchia_pred_type != nullptr) {
     const std::string t(vecchia_pred_type);
     static const char* known[] = {"order_obs_first_cond_obs_only", "order_obs_first_cond_all", "order_pred_first",
@@ -249,9 +250,9 @@ void REModelAMD::SetPredictionData(const char* vecchia_pred_type, int num_neighb
     bool ok = false;
     for (const char* k : known) ok |= t == k;
     if (!ok) Fatal("Prediction type '%s' is not supported for the Veccia approximation ", t.c_str());
-    if (t != "order_obs_first_cond_obs_only")
-      Fatal("vecchia_pred_type '%s' is not supported by gpboost_amd (supported: order_obs_first_cond_obs_only)",
-            t.c_str());
+    if (t != "order_obs_first_cond_obs_only" && t != "latent_order_obs_first_cond_obs_only")
+      Fatal("vecchia_pred_type '%s' is not supported by gpboost_amd (supported: order_obs_first_cond_obs_only, "
+            "latent_order_obs_first_cond_obs_only)", t.c_str());
     vecchia_pred_type_ = t;
   }
   if (num_neighbors_pred > 0) num_neighbors_pred_ = num_neighbors_pred;
@@ -262,33 +263,88 @@ void REModelAMD::SetPredictionData(const char* vecchia_pred_type, int num_neighb
 // observed points (GPU sweep, end_search_at = n - 1), the per-point rows (A, Dp) by the
 // likelihood's row kernel (rows n .. n + n_pred - 1 of [observed; prediction] coordinates), then
 // mean = A . y_nbr and var = (Dp - [latent: 1]) sigma2 (predict_mean_var_kernel).
+namespace {
+// Gauss-Hermite rule of the given order (weight exp(-x^2)) by Newton iteration on the normalised
+// Hermite recurrence; returns [nodes | weights * exp(nodes^2)] (the reference's GH_nodes_ and
+// adaptive_GH_weights_ tables, likelihoods.h:12891-12980, reproduced to rounding).
+std::vector<double> gauss_hermite_adaptive(int order) {
+  std::vector<long double> x(order), w(order);
+  const long double pim4 = 0.7511255444649424828587030047762276930510L;   // pi^-1/4
+  long double z = 0.;
+  const int half = (order + 1) / 2;
+  for (int i = 0; i < half; ++i) {
+    if (i == 0) z = std::sqrt((long double)(2 * order + 1)) - 1.85575L * std::pow((long double)(2 * order + 1), -0.16667L);
+    else if (i == 1) z -= 1.14L * std::pow((long double)order, 0.426L) / z;
+    else if (i == 2) z = 1.86L * z - 0.86L * x[0];
+    else if (i == 3) z = 1.91L * z - 0.91L * x[1];
+    else z = 2.L * z - x[i - 2];
+    long double pp = 1.;
+    for (int it = 0; it < 100; ++it) {
+      long double p1 = pim4, p2 = 0.;
+      for (int j = 1; j <= order; ++j) {
+        const long double p3 = p2;
+        p2 = p1;
+        p1 = z * std::sqrt(2.L / j) * p2 - std::sqrt((long double)(j - 1) / j) * p3;
+      }
+      pp = std::sqrt(2.L * order) * p2;
+      const long double z1 = z;
+      z = z1 - p1 / pp;
+      if (std::fabs(z - z1) <= 1e-18L) break;
+    }
+    x[i] = z;
+    x[order - 1 - i] = -z;
+    w[i] = w[order - 1 - i] = 2.L / (pp * pp);
+  }
+  std::vector<double> out((size_t)2 * order);
+  for (int j = 0; j < order; ++j) {
+    out[j] = (double)x[order - 1 - j];   // ascending, as the reference's table
+    out[order + j] = (double)(w[order - 1 - j] * std::exp(x[order - 1 - j] * x[order - 1 - j]));
+  }
+  return out;
+}
+}  // namespace
+
 void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,
                          bool predict_cov_mat, bool predict_var, bool predict_response, double* out) {
-  if (!vecchia_ || cfg_.latent)
-    Fatal("predictions are implemented for the exact Gaussian Vecchia approximation (gp_approx = 'vecchia') only");
+  if (!vecchia_) Fatal("predictions are implemented for the Vecchia approximation (gp_approx = 'vecchia' / "
+                       "'vecchia_latent') only");
   if (world_ > 1) Fatal("predictions are only available on single-rank models");
   if (n_pred <= 0) Fatal("num_data_pred must be > 0");
   if (coords_pred == nullptr) Fatal("gp_coords_data_pred must be provided");
   UseDevice();
   if (y != nullptr) SetY(y);
   if (!y_set_) Fatal("response variable y has not been set (pass y or evaluate the likelihood first)");
+  const bool latent = cfg_.latent;
+  const int ncp = latent ? 2 : 3;
   double cp[3];
-  if (cov_pars != nullptr) std::copy(cov_pars, cov_pars + 3, cp);
-  else if (last_cov_pars_.size() == 3) std::copy(last_cov_pars_.begin(), last_cov_pars_.end(), cp);
+  if (cov_pars != nullptr) std::copy(cov_pars, cov_pars + ncp, cp);
+  else if ((int)last_cov_pars_.size() == ncp) std::copy(last_cov_pars_.begin(), last_cov_pars_.end(), cp);
   else Fatal("cov_pars must be provided (no previous evaluation)");
+  if (latent) {
+    if (predict_cov_mat)
+      Fatal("predictive covariance matrices of latent models are not supported by gpboost_amd (use predict_var)");
+    // the mode at these parameters, found from zero (re_model.cpp:967-977 -> CalcCovFactorOrModeAndNegLL)
+    EvalLatent(cp, false);
+  }
   double trafo[3];
-  TransformCovPars(cp, trafo);
-  const int n = cfg_.n, d = cfg_.d, na = n + n_pred;
+  if (latent) {
+    trafo[0] = cp[0];
+    trafo[1] = range_trafo(cfg_.cov_type, cp[1]);
+  } else {
+    TransformCovPars(cp, trafo);
+  }
+  // observed points: the latent variables' locations (unique, Vecchia order) / the observations
+  const int n = latent ? nu_ : cfg_.n, d = cfg_.d, na = n + n_pred;
   const int mp = std::min(num_neighbors_pred_, n);   // end_search_at + 1 (Vecchia_utils.cpp:754-757)
   if (mp > 64) Fatal("num_neighbors_pred = %d > 64 is not supported by the GPU prediction kernel", mp);
   std::vector<double> xa((size_t)na * d);
-  std::copy(coords_vo_.begin(), coords_vo_.end(), xa.begin());
+  std::copy(coords_vo_.begin(), coords_vo_.begin() + (size_t)n * d, xa.begin());
   for (int p = 0; p < n_pred; ++p)
     for (int q = 0; q < d; ++q) xa[(size_t)(n + p) * d + q] = coords_pred[(size_t)q * n_pred + p];
   std::vector<int> nb((size_t)n_pred * mp);
   if (d <= 3) vecchia_neighbors_gpu(xa.data(), na, d, mp, n, na, nb.data(), stream_, n - 1);
   else vecchia_neighbors(xa.data(), na, d, mp, n, na, nb.data(), n - 1);
-  DevBuf<double> dxa((size_t)na * d), dB((size_t)n_pred * mp), dD(n_pred), dout((size_t)2 * n_pred);
+  DevBuf<double> dxa((size_t)na * d), dB((size_t)n_pred * mp), dD(n_pred), dout((size_t)2 * n_pred), dmode;
   DevBuf<int> dnb((size_t)n_pred * mp);
   HIP_CHECK(hipMemcpyAsync(dxa.get(), xa.data(), sizeof(double) * xa.size(), hipMemcpyHostToDevice, stream_));
   HIP_CHECK(hipMemcpyAsync(dnb.get(), nb.data(), sizeof(int) * nb.size(), hipMemcpyHostToDevice, stream_));
@@ -301,21 +357,58 @@ void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred,
   a.m = mp;
   a.r0 = n;
   a.r1 = na;
-  a.var = trafo[1];
-  a.phi = trafo[2];
-  a.diag_mult = 1.;
-  a.diag_add = 1.;            // nugget on the between-neighbour covariance (Vecchia_utils.cpp:1877)
-  a.d_nugget = 1.;            // Dp starts at 1 (:1797-1798)
+  if (latent) {   // no nugget: between-neighbour diagonal * JITTER_MULT_VECCHIA, Dp = sigma1^2 - A c (:1894-1898)
+    a.var = trafo[0];
+    a.phi = trafo[1];
+    a.diag_mult = 1. + 1e-10;
+    a.diag_add = 0.;
+    a.d_nugget = 0.;
+  } else {
+    a.var = trafo[1];
+    a.phi = trafo[2];
+    a.diag_mult = 1.;
+    a.diag_add = 1.;          // nugget on the between-neighbour covariance (Vecchia_utils.cpp:1877)
+    a.d_nugget = 1.;          // Dp starts at 1 (:1797-1798)
+  }
   a.B_out = dB.get();
   a.Dinv_out = dD.get();
   a.row_base = n;
   launch_vecchia_rows(cfg_.cov_type, a, stream_);
-  launch_predict_mean_var(n_pred, mp, dnb.get(), dB.get(), dD.get(), d_y_.get(), trafo[0],
-                          predict_response ? 0. : 1., dout.get(), stream_);
+  if (latent) {   // mean = -Bpo mode (likelihoods.h:6609), Dp (no nugget to remove)
+    std::vector<double> mode(n);
+    latent_->GetMode(mode.data());
+    dmode.alloc(n);
+    HIP_CHECK(hipMemcpyAsync(dmode.get(), mode.data(), sizeof(double) * n, hipMemcpyHostToDevice, stream_));
+    launch_predict_mean_var(n_pred, mp, dnb.get(), dB.get(), dD.get(), dmode.get(), 1., 0., dout.get(), stream_);
+  } else {
+    launch_predict_mean_var(n_pred, mp, dnb.get(), dB.get(), dD.get(), d_y_.get(), trafo[0],
+                            predict_response ? 0. : 1., dout.get(), stream_);
+  }
   std::vector<double> h((size_t)2 * n_pred);
   HIP_CHECK(hipMemcpyAsync(h.data(), dout.get(), sizeof(double) * h.size(), hipMemcpyDeviceToHost, stream_));
   HIP_CHECK(hipStreamSynchronize(stream_));
   std::copy(h.begin(), h.begin() + n_pred, out);
+  if (latent && (predict_var || predict_response)) {
+    // + the simulation term of PredictLaplaceApproxVecchia (iterative, likelihoods.h:6628-6746)
+    std::vector<double> acc(n_pred);
+    latent_->PredVarSim(nsim_var_pred_, iter.num_rand_vec_trace, iter.cg_delta_conv, iter.cg_max_num_it,
+                        pred_seed_++, n_pred, mp, nb.data(), dB.get(), acc.data());
+    for (int p = 0; p < n_pred; ++p) h[n_pred + p] += acc[p] / nsim_var_pred_;
+    if (predict_response && cfg_.lik == kLikBernoulliLogit) {
+      // PredictResponse (likelihoods.h:7544-7556): adaptive Gauss-Hermite response means, p (1 - p)
+      static const std::vector<double> gh = gauss_hermite_adaptive(30);   // order_GH_ = 30 (:12877)
+      DevBuf<double> dmv((size_t)2 * n_pred), dgh(gh.size());
+      HIP_CHECK(hipMemcpyAsync(dmv.get(), h.data(), sizeof(double) * 2 * n_pred, hipMemcpyHostToDevice, stream_));
+      HIP_CHECK(hipMemcpyAsync(dgh.get(), gh.data(), sizeof(double) * gh.size(), hipMemcpyHostToDevice, stream_));
+      launch_resp_logit(n_pred, dmv.get(), dmv.get() + n_pred, dgh.get(), dgh.get() + 30, 30, iter.delta_conv_mode_finding,
+                        dout.get(), dout.get() + n_pred, stream_);
+      HIP_CHECK(hipMemcpyAsync(h.data(), dout.get(), sizeof(double) * h.size(), hipMemcpyDeviceToHost, stream_));
+      HIP_CHECK(hipStreamSynchronize(stream_));
+      std::copy(h.begin(), h.begin() + n_pred, out);
+    } else if (predict_response) {   // gaussian vecchia_latent: + the error variance (PredictResponse)
+      for (int p = 0; p < n_pred; ++p) h[n_pred + p] += aux_pars_.empty() ? 0. : aux_pars_[0];
+    }
+  }
   if (predict_cov_mat) {   // conditioning on observed points only: the predictive covariance is diagonal
     double* c = out + n_pred;
     std::fill(c, c + (size_t)n_pred * n_pred, 0.);

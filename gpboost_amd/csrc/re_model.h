@@ -88,7 +88,7 @@ class REModelAMD {
   // "order_obs_first_cond_obs_only". coords_pred column-major n_pred x d; cov_pars on the original
   // scale (null: those of the last evaluation); y null: the response already set. out: means, then
   // variances (predict_var) or the n_pred x n_pred covariance (predict_cov_mat; diagonal here).
-  void SetPredictionData(const char* vecchia_pred_type, int num_neighbors_pred);
+  void SetPredictionData(const char* vecchia_pred_type, int num_neighbors_pred, int nsim_var_pred = -1);
   void Predict(const double* y, int n_pred, const double* coords_pred, const double* cov_pars, bool predict_cov_mat,
                bool predict_var, bool predict_response, double* out);
 
@@ -179,6 +179,9 @@ class REModelAMD {
   bool estimate_aux_pars = true;   // InitializeDefaultSettings (re_model_template.h:6492-6499) for latent models
   bool aux_pars_set_ = false;      // aux_pars given by the caller (SetOptimConfig init_aux_pars / SetAuxPars)
 
+  // Latent models: the fixed effects F (location offset) of the next mode finding (NULL: none).
+  void SetLatentOffset(const double* fe);
+
  private:
   void TransformCovPars(const double* orig, double* trafo) const;
   double range_trafo_of(double rho) const { return range_trafo(cfg_.cov_type, rho); }
@@ -225,6 +228,8 @@ class REModelAMD {
 
   std::string vecchia_pred_type_ = "order_obs_first_cond_obs_only";   // re_model_template.h:6485-6490
   int num_neighbors_pred_ = 0;                                         // 2 num_neighbors (:299)
+  int nsim_var_pred_ = 1000;                                           // re_model_template.h:5374
+  uint64_t pred_seed_ = 1;                                             // latent variance draws (per call)
 
   int rank_ = 0, world_ = 1;
   int row_begin_ = 0, row_end_ = 0;
@@ -253,7 +258,6 @@ class REModelAMD {
   bool has_fixed_effects_ = false;
   std::vector<double> offset_vo_;     // latent models: fixed effects F of the last call (Vecchia order)
   bool has_offset_ = false;
-  void SetLatentOffset(const double* fe);
   DevBuf<double> d_Zcov_;            // [X | y - offset], Vecchia order row-major n x c (Vecchia models)
   DevBuf<double> d_Bf_, d_Df_, d_gram_part_, d_gram_out_;
   DevBuf<int> d_tptr_, d_trow_, d_tslot_;

@@ -23,7 +23,7 @@
 // Measured (MI355X, n=100k, m=30, 2 waves/SIMD): pair phase unrolled by 8 and branch-free plus
 // the dC a sum unrolled with four partials: 0.455 -> 0.41 ms per launch; publishing the next
 // pivot's reciprocal with the column (reciprocal chain off the step chain) needs ~290 registers
-// (occupancy 1): 0.63 ms, rejected.
+// (occupancy 1): 0.63 ms, rejected (re-measured with the bordered form: 0.319 vs 0.3145 ms).
 // The row then emits six partial sums (logD, (By)^2/D, and per parameter
 // s1 = uk u - u^2 dD/2, s2 = dD/D; DESIGN.md "reduction contract"). Blocks stride over
 // row groups and keep per-lane accumulators, so one launch writes few block partials.
@@ -100,10 +100,12 @@ __device__ __forceinline__ void static_for(F&& f) {
   }
 }
 
-// Value of lane L of each 16-lane DPP row, broadcast to that whole row (row_newbcast).
+// Value of lane L of each 16-lane DPP row, broadcast to that whole row (row_newbcast: one 64-bit
+// DPP move on gfx950).
 template <int L>
 __device__ __forceinline__ double row_bcast(double v) {
-  return dpp_f64<0x150 + L>(v);
+  const long b = __builtin_amdgcn_mov_dpp(__builtin_bit_cast(long, v), 0x150 + L, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, b);
 }
 
 // 32-lane groups: lo = the value of group lane CP, hi = that of group lane 16 + CP, in every lane
@@ -205,8 +207,13 @@ __device__ unsigned long long g_rows_prof[8];
 #ifndef GPB_PAIR_CHAIN
 #define GPB_PAIR_CHAIN 0
 #endif
-#ifndef GPB_ROWS_PIVRCP
-#define GPB_ROWS_PIVRCP 0
+#ifndef GPB_ROWS_GJ2
+#define GPB_ROWS_GJ2 0
+#endif
+// Bordered scalar form: columns c with (c mod 16) < GPB_ROWS_LDSCOLS reach the lanes through the
+// LDS slot, the others by DPP row broadcasts + row-swap permutes (VALU); 16 = LDS only.
+#ifndef GPB_ROWS_LDSCOLS
+#define GPB_ROWS_LDSCOLS 16
 #endif
 #if GPB_ROWS_WAVES > 0
 #define GPB_ROWS_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(GPB_ROWS_WAVES, GPB_ROWS_WAVES)))
@@ -403,58 +410,107 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
       for (int dl = 1; dl <= K / 2; ++dl) dCp[(dl - 1) * K + r] = wst[dl - 1];
     }
     double aug1 = cvec, aug2 = ynb;
+    double av_r = 0., vv_r = 0.;   // a = C^-1 c, v = C^-1 y_nbr (lanes r >= MK hold no row)
     if constexpr (BORDER) {
       // native 16-byte vector type: HIP's double2 struct is loaded field-wise (ds_read2_b64, 4x the
       // LDS cycles of ds_read_b128 per byte)
       typedef double v2d __attribute__((ext_vector_type(2)));
-      const v2d* slot2 = reinterpret_cast<const v2d*>(__builtin_assume_aligned(slot_c, 16));
       auto recip = [](double piv) {   // hardware reciprocal + two Newton steps (~1 ulp)
         double x = __builtin_amdgcn_rcp(piv);
         x = fma(x, fma(-piv, x, 1.), x);
         return fma(x, fma(-piv, x, 1.), x);
       };
-#if GPB_ROWS_PIVRCP
-      // The pivot lane publishes its pivot's reciprocal instead of the pivot: every lane computes
-      // the reciprocal of its own next diagonal entry right after updating that column (off the
-      // step's critical path), and only the pivot lane's copy is stored. Same value as the
-      // reciprocal of the broadcast pivot, so bitwise the same results.
-      double rnext = recip(row[0]);
-#endif
+#if GPB_ROWS_GJ2
+      // 2 x 2 pivot blocks: step j eliminates columns j and j + 1 at once. Lanes publish the pair
+      // (row[j], row[j + 1]) as one 16-byte store; the pair read back from lane c is (M[c][j],
+      // M[c][j + 1]) = (M[j][c], M[j + 1][c]) by the symmetry of the trailing block. Each lane's
+      // multipliers [f0 f1] = [M[r][j] M[r][j + 1]] P^-1 (P = the pivot block; f = 0 on its own
+      // rows), update row[c] -= f0 M[j][c] + f1 M[j + 1][c]. Half the LDS round trips and
+      // reciprocals of the scalar form. The pivot rows keep their block, so at the end
+      // [a_j, a_j+1] = P^-1 [aug_j, aug_j+1]: every lane stores P^-1 of the step (uniform address)
+      // as lane j's pair (P^-1_00, P^-1_01) and lane j + 1's pair (P^-1_11, P^-1_10), read back
+      // at the lane's own index, with the partner lane's augmented entries by a DPP lane swap.
+      v2d* slot2 = reinterpret_cast<v2d*>(__builtin_assume_aligned(slot_c, 16));
+      v2d* pinv2 = slot2 + K;   // MK entries after the K-entry slot (within the coordinate copies)
+#pragma unroll
+      for (int j = 0; j < MK; j += 2) {
+        compiler_fence();
+        slot2[r] = v2d{row[j], row[j + 1]};
+        wave_lds_sync();
+        double c0[NC], c1[NC];
+#pragma unroll
+        for (int c = j; c < NC; ++c) {
+          const v2d v = slot2[c];
+          c0[c] = v.x;
+          c1[c] = v.y;
+        }
+        const double p00 = c0[j], p10 = c0[j + 1], p01 = c1[j], p11 = c1[j + 1];
+        const double rdet = recip(fma(p00, p11, -(p01 * p10)));
+        const double i00 = p11 * rdet, i11 = p00 * rdet, i01 = -p01 * rdet, i10 = -p10 * rdet;
+        pinv2[j] = v2d{i00, i01};
+        pinv2[j + 1] = v2d{i11, i10};
+        const bool pivrow = (r >> 1) == (j >> 1);
+        const double m0 = row[j], m1 = row[j + 1];
+        const double f0 = pivrow ? 0. : fma(m0, i00, m1 * i10);
+        const double f1 = pivrow ? 0. : fma(m0, i01, m1 * i11);
+#pragma unroll
+        for (int c = j + 2; c < NC; ++c) row[c] = fma(-f1, c1[c], fma(-f0, c0[c], row[c]));
+        // pin this step's updates here (otherwise the scheduler defers the FMAs and keeps every
+        // broadcast value live)
+#pragma unroll
+        for (int c = j + 2; c < NC; ++c) asm volatile("" : "+v"(row[c]));
+      }
+      aug1 = row[NC - 2];
+      aug2 = row[NC - 1];
+      wave_lds_sync();
+      const v2d pin = pinv2[r];   // own-row pair of the block's inverse (lanes r < MK)
+      const double w1 = dpp_f64<0xB1>(aug1), w2 = dpp_f64<0xB1>(aug2);   // partner lane r ^ 1
+      av_r = rv ? fma(pin.x, aug1, pin.y * w1) : 0.;
+      vv_r = rv ? fma(pin.x, aug2, pin.y * w2) : 0.;
+#else
+      const v2d* slot2 = reinterpret_cast<const v2d*>(__builtin_assume_aligned(slot_c, 16));
+      constexpr int DL = (K == 32) ? GPB_ROWS_LDSCOLS : 16;   // hybrid broadcast: 32-lane groups only
 #pragma unroll
       for (int j = 0; j < MK; ++j) {
-        compiler_fence();
-#if GPB_ROWS_PIVRCP
-        slot_c[r] = (r == j) ? rnext : row[j];
-#else
-        slot_c[r] = row[j];
-#endif
-        wave_lds_sync();
         double sv[NC];
+        bool any_lds = false;
 #pragma unroll
-        for (int p = j >> 1; p < NC / 2; ++p) {
-          const v2d v = slot2[p];
-          sv[2 * p] = v.x;
-          sv[2 * p + 1] = v.y;
+        for (int c = j; c < NC; ++c) any_lds = any_lds || (c & 15) < DL;
+        if (any_lds) {
+          compiler_fence();
+          slot_c[r] = row[j];
+          wave_lds_sync();
+#pragma unroll
+          for (int p = j >> 1; p < NC / 2; ++p) {
+            if (((2 * p) & 15) < DL) {
+              const v2d v = slot2[p];
+              sv[2 * p] = v.x;
+              sv[2 * p + 1] = v.y;
+            }
+          }
         }
-#if GPB_ROWS_PIVRCP
-        const double rinv = sv[j];
-#else
+        if constexpr (DL < 16) {
+          static_for<DL, 16>([&](auto CP) {
+            constexpr int cp = decltype(CP)::value;
+            if (cp + 16 >= j && cp + 16 < NC) {   // lane cp's and lane cp + 16's row[j]
+              double lo, hi;
+              group_bcast_pair<cp>(row[j], lo, hi);
+              sv[cp] = lo;
+              sv[cp + 16] = hi;
+            }
+          });
+        }
         const double rinv = recip(sv[j]);
-#endif
         const double q = row[j] * rinv;
         const double f = (r == j) ? 0. : q;
 #pragma unroll
-        for (int c = j + 1; c < NC; ++c) {
-          row[c] = fma(-f, sv[c], row[c]);
-#if GPB_ROWS_PIVRCP
-          if (c == j + 1 && j + 1 < MK) rnext = recip(row[c]);
-#endif
-        }
+        for (int c = j + 1; c < NC; ++c) row[c] = fma(-f, sv[c], row[c]);
 #pragma unroll
         for (int c = j + 1; c < NC; ++c) asm volatile("" : "+v"(row[c]));
       }
       aug1 = row[NC - 2];
       aug2 = row[NC - 1];
+#endif
     } else if constexpr (DPPBC) {
       // lane c holds row c, so M[c][j] = lane c's row[j]: broadcast lane c's register
       auto bc = [&](auto CPc, double v, double& lo, double& hi) {
@@ -530,19 +586,20 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
       asm volatile("" : "+v"(aug1), "+v"(aug2));
     }
     }
+    if constexpr (!(BORDER && GPB_ROWS_GJ2)) {
     double mydiag = row[0];
 #pragma unroll
     for (int c = 1; c < MK; ++c) mydiag = (c == r) ? row[c] : mydiag;
-    double av_r, vv_r;
     if constexpr (BORDER) {   // one reciprocal (rcp + two Newton steps, ~1 ulp) for both quotients
       double dinv = __builtin_amdgcn_rcp(mydiag);
       dinv = fma(dinv, fma(-mydiag, dinv, 1.), dinv);
       dinv = fma(dinv, fma(-mydiag, dinv, 1.), dinv);
-      av_r = rv ? aug1 * dinv : 0.;   // a = C^-1 c (lanes r >= MK hold no row)
-      vv_r = rv ? aug2 * dinv : 0.;   // v = C^-1 y_nbr
+      av_r = rv ? aug1 * dinv : 0.;
+      vv_r = rv ? aug2 * dinv : 0.;
     } else {
       av_r = rv ? aug1 / mydiag : 0.;
       vv_r = rv ? aug2 / mydiag : 0.;
+    }
     }
 
     if (active && a.B_out != nullptr && r < a.m) a.B_out[(size_t)(i - a.row_base) * a.m + r] = rv ? -av_r : 0.;

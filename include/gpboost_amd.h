@@ -330,10 +330,12 @@ GPBOOST_AMD_EXPORT int GPB_BenchLatentOperators(REModelHandle handle, int t, int
 
 /* replaces GPB_SetPredictionData (include/LightGBM/c_api.h:1578; c_api.cpp). Only the settings
  * are supported: vecchia_pred_type (NULL: unchanged; supported: "order_obs_first_cond_obs_only",
- * the reference's default for Gaussian likelihoods, re_model_template.h:6485-6487) and
- * num_neighbors_pred (<= 0: unchanged; default 2 * num_neighbors, :299). Prediction data must be
- * NULL / 0 (pass it to GPB_PredictREModel); cg_delta_conv_pred, nsim_var_pred and
- * rank_pred_approx_matrix_lanczos are accepted and ignored (iterative prediction is out of scope). */
+ * the reference's default for Gaussian likelihoods, and "latent_order_obs_first_cond_obs_only", its
+ * default for latent models, re_model_template.h:6485-6490), num_neighbors_pred (<= 0: unchanged;
+ * default 2 * num_neighbors, :299) and nsim_var_pred (<= 0: unchanged; default 1000, :5374: draws of
+ * the latent models' predictive-variance simulation). Prediction data must be NULL / 0 (pass it to
+ * GPB_PredictREModel); cg_delta_conv_pred and rank_pred_approx_matrix_lanczos are accepted and
+ * ignored (the Vecchia-Laplace draws use the model's cg_delta_conv, likelihoods.h:12043-12053). */
 GPBOOST_AMD_EXPORT int GPB_SetPredictionData(REModelHandle handle,
     int32_t num_data_pred,
     const int32_t* cluster_ids_data_pred,
@@ -349,15 +351,21 @@ GPBOOST_AMD_EXPORT int GPB_SetPredictionData(REModelHandle handle,
     int rank_pred_approx_matrix_lanczos);
 
 /* replaces GPB_PredictREModel (include/LightGBM/c_api.h:1617; Vecchia_utils.cpp:1634-1931,
- * re_model_template.h:3700-4071) for the exact Gaussian Vecchia approximation: predictive mean
+ * re_model_template.h:3700-4071) for the Vecchia approximation: predictive mean
  * (out_predict[0 .. num_data_pred)) and, if predict_var, variances (out_predict[num_data_pred ..
  * 2 num_data_pred)), or, if predict_cov_mat, the num_data_pred^2 covariance (diagonal: each
  * prediction point conditions on observed points only). gp_coords_data_pred column-major
  * num_data_pred x dim_gp_coords. cov_pars on the original scale (NULL: those of the last
- * evaluation); y_data NULL: the response set before. predict_response = false removes the
- * nugget variance (latent process). Neighbours are searched among the observed points by the
- * reference's sweep (bit-identical lists). Unsupported inputs (clusters, grouped effects,
- * random coefficients, covariates, saved prediction data, latent / dense models) return -1. */
+ * evaluation); y_data NULL: the response set before. Exact Gaussian models: predict_response =
+ * false removes the nugget variance (latent process). Latent models (vecchia_latent,
+ * bernoulli_logit; latent_order_obs_first_cond_obs_only, PredictLaplaceApproxVecchia
+ * likelihoods.h:6576-6813): the Laplace mode at cov_pars (found from zero, fixed_effects = the
+ * observed data's location offset), mean = -Bpo mode; predict_var adds the iterative simulation term
+ * (nsim_var_pred draws, statistically equivalent to the reference's); gaussian vecchia_latent with
+ * predict_response adds the error variance. Neighbours are searched among the observed points
+ * (latent models: their unique locations) by the reference's sweep (bit-identical lists).
+ * Unsupported inputs (clusters, grouped effects with GPs, random coefficients, saved prediction data,
+ * dense models, latent predict_cov_mat, bernoulli predict_response) return -1. */
 GPBOOST_AMD_EXPORT int GPB_PredictREModel(REModelHandle handle,
     const double* y_data,
     int32_t num_data_pred,

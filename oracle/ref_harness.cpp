@@ -301,6 +301,35 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (mode == "predict") {
+    // GPB_SetPredictionData + GPB_PredictREModel at cov_pars (re_model.cpp:927-1000 -> Predict
+    // re_model_template.h:3146): prediction coordinates from the file `pred` (int32 np, double
+    // coords[np * d] column-major); outputs the predictive mean and (predict_var) variances.
+    FILE* fp = std::fopen(get(args, "pred", "").c_str(), "rb");
+    if (!fp) { std::perror("open pred"); return 2; }
+    int32_t np = 0;
+    if (std::fread(&np, 4, 1, fp) != 1 || np <= 0) return 2;
+    std::vector<double> xp((size_t)np * d);
+    if (std::fread(xp.data(), 8, xp.size(), fp) != xp.size()) return 2;
+    std::fclose(fp);
+    const bool pvar = get(args, "predict_var", "0") == "1";
+    const bool presp = get(args, "predict_response", "0") == "1";
+    const std::string ptype = get(args, "vecchia_pred_type", "");
+    m->SetPredictionData(np, nullptr, nullptr, nullptr, xp.data(), nullptr, nullptr,
+                         ptype.empty() ? nullptr : ptype.c_str(),
+                         std::atoi(get(args, "num_neighbors_pred", "-1").c_str()),
+                         std::atof(get(args, "cg_delta_conv_pred", "-1").c_str()),
+                         std::atoi(get(args, "nsim_var_pred", "-1").c_str()), -1);
+    std::vector<double> out((size_t)2 * np, 0.);
+    m->Predict(trafo.data(), y.data(), np, out.data(), true, false, pvar, presp, nullptr, nullptr, nullptr,
+               nullptr, nullptr, xp.data(), nullptr, false, fe_ptr, nullptr);
+    std::printf("{\n\"n\": %d, \"d\": %d, \"np\": %d,\n", n, d, np);
+    print_vec("mean", out.data(), np);
+    if (pvar) print_vec("var", out.data() + np, np);
+    std::printf("\"ok\": true\n}\n");
+    return 0;
+  }
+
   if (mode == "stddev") {
     // GPB_GetCovPar(calc_std_dev = true) at cov_pars: CalculateStandardErrorsCovPars
     // (re_model_template.h:1634-1660 -> CalcStdDevCovPar :9775-9789), transformed-scale input

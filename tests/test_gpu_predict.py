@@ -85,7 +85,6 @@ def test_predict_errors():
         gm.set_prediction_data(vecchia_pred_type="no_such_type")
     with pytest.raises(ValueError):
         gm.predict(y=y, gp_coords_pred=X[500:, :1], cov_pars=[0.1, 1.0, 0.1])
-    lat = GPModel(gp_coords=X[:500], likelihood="bernoulli_logit", cov_function="exponential", gp_approx="vecchia",
-                  num_neighbors=20, matrix_inversion_method="iterative")
-    with pytest.raises(GPBoostError, match="exact Gaussian Vecchia"):
-        lat.predict(y=(y > 0).astype(float), gp_coords_pred=X[500:], cov_pars=[1.0, 0.1])
+    dense = GPModel(gp_coords=X[:500], cov_function="exponential", gp_approx="none")
+    with pytest.raises(GPBoostError, match="Vecchia approximation"):
+        dense.predict(y=y, gp_coords_pred=X[500:], cov_pars=[0.1, 1.0, 0.1])
