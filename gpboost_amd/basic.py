@@ -535,7 +535,8 @@ class GPModel:
                             group_rand_coef_data_pred=None, gp_coords_pred=None, gp_rand_coef_data_pred=None,
                             cluster_ids_pred=None, X_pred=None):
         """Prediction settings (reference basic.py:6095, GPB_SetPredictionData). Only
-        vecchia_pred_type / num_neighbors_pred are supported; prediction data is passed to predict()."""
+        vecchia_pred_type / num_neighbors_pred / nsim_var_pred are supported; prediction data is passed
+        to predict()."""
         if any(v is not None for v in (group_data_pred, group_rand_coef_data_pred, gp_coords_pred,
                                        gp_rand_coef_data_pred, cluster_ids_pred, X_pred)):
             raise GPBoostError("set_prediction_data: saving prediction data is not supported by gpboost_amd; "
@@ -554,7 +555,9 @@ class GPModel:
                 num_neighbors_pred=None):
         """Predictions at new coordinates (reference basic.py:5778-6093, GPB_PredictREModel): returns
         {"mu": mean, "cov": covariance or None, "var": variances or None}. Exact Gaussian Vecchia
-        models, vecchia_pred_type "order_obs_first_cond_obs_only"."""
+        models (vecchia_pred_type "order_obs_first_cond_obs_only") and latent Vecchia models
+        ("latent_order_obs_first_cond_obs_only": Laplace mode, simulated iterative variances,
+        bernoulli_logit response probabilities by adaptive Gauss-Hermite quadrature)."""
         if getattr(self, "num_group_re", 0):
             return self._predict_grouped(group_data_pred, predict_var, predict_cov_mat, predict_response, y, cov_pars,
                                          offset, offset_pred, fixed_effects, fixed_effects_pred)

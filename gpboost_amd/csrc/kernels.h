@@ -29,6 +29,8 @@ struct VecchiaRowsArgs {
 
 int vecchia_rows_blocks(int rows, int m);   // upper bound of the grid (block-partial buffer size)
 int launch_vecchia_rows(int cov_type, const VecchiaRowsArgs& a, hipStream_t s);   // returns the grid size
+// 16-lane form for m <= 30 (vecchia_rows16.hip; DPP broadcasts, four rows per wave), same contract
+int launch_vecchia_rows16(int cov_type, const VecchiaRowsArgs& a, hipStream_t s);
 // Predictions from the prediction rows' factor: out[p] = -sum_r B[p, r] y[nbr[p, r]] (mean),
 // out[n_pred + p] = (1 / Dinv[p] - nugget_sub) * sigma2 (variance). B, nbr: n_pred x m.
 void launch_predict_mean_var(int n_pred, int m, const int* nbr, const double* B, const double* Dinv, const double* y,

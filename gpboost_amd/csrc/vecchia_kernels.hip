@@ -1006,6 +1006,11 @@ bool rows_dpp() { return std::getenv("GPBOOST_AMD_ROWS_DPP") != nullptr; }
 // Augmented entries: bordered rows (default where two lanes are spare) or the round-2 form with
 // separate augmented slots (GPBOOST_AMD_ROWS_SLOTS=1, A/B; read at every launch).
 bool rows_slots() { return std::getenv("GPBOOST_AMD_ROWS_SLOTS") != nullptr; }
+// 16-lane form (vecchia_rows16.hip) for m <= 30: GPBOOST_AMD_ROWS16=1 (A/B; read at every launch)
+bool rows16() {
+  const char* e = std::getenv("GPBOOST_AMD_ROWS16");
+  return e != nullptr && e[0] == '1';
+}
 
 template <int K>
 int rows_per_block() { return use_v4(K) ? 64 / (K / 2) : (block_threads<K>() / 64) * (64 / K); }
@@ -1071,6 +1076,7 @@ int launch_k(const VecchiaRowsArgs& a, hipStream_t s) {
   const bool dpp = rows_dpp();
   if constexpr (K == 32) {
     if (!prof && a.m <= 30) {   // the headline configuration (m = 30): 30 elimination steps
+      if (rows16()) return launch_vecchia_rows16(COV, a, s);
       if (dpp) {
         hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, 30, true>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
       } else if (rows_slots()) {

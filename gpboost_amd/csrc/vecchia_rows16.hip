@@ -1,0 +1,354 @@
+// Vecchia factor + likelihood/gradient rows, 16-lane form (m <= 30), gfx950.
+//
+// Same row math as vecchia_rows_kernel's bordered form (vecchia_kernels.hip; reference:
+// CalcCovFactorGradientVecchia Vecchia_utils.cpp:1307-1632 fused with re_model_template.h:8885-9120,
+// 1768-1791), laid out so the Gauss-Jordan broadcasts never touch LDS: one row problem (the 32 x 32
+// bordered matrix [[C, c, y_nbr], [c^T ...], [y_nbr^T ...]], 30 pivots) per 16-lane DPP row, lane h
+// holding matrix rows h and h + 16. Column j of the current matrix is row j by symmetry, and row c's
+// entry sits in lane c mod 16 (register set c / 16), so one row_newbcast DPP move (a single 64-bit
+// VALU op) hands M[j][c] to the 16 lanes of the problem, where it feeds TWO FMAs (rows h, h + 16).
+// Four problems per wave, one per DPP row. The 32-lane form broadcasts every value through an LDS
+// slot (a 16-byte read per two values per lane): at 2 waves/SIMD its LDS return traffic, not the FP64
+// VALU, set the pace.
+//   1. coordinates of the 32 rows (two copies of rows 0..15, so partner r + delta < 48 is an
+//      immediate-offset read); lane h computes the circulant pairs {v, v + delta}, v in {h, h + 16},
+//      delta = 1..16 (the pair {h, h + 16} once): C to the packed lower triangle in LDS, dC/dlog(phi)
+//      in registers until the rows are loaded, then over the packed C in the circulant layout
+//      W[(delta - 1) 32 + v];
+//   2. rows h and h + 16 of the bordered matrix into registers; 30 Gauss-Jordan steps by DPP
+//      broadcasts; a_v = M[v][30] / M[v][v], w_v = M[v][31] / M[v][v] (the pivots are captured
+//      when broadcast);
+//   3. a^T dC a and w^T dC a over each lane's circulant pairs ([a, w] pairs in a doubled LDS array);
+//   4. the eight group sums by DPP within the 16-lane row, then the six row partials.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <type_traits>
+
+#include "common.h"
+#include "cov.h"
+#include "kernels.h"
+
+namespace gpb_amd {
+namespace {
+
+constexpr int kD3 = 3;   // coordinate dimension bound (VecchiaRowsArgs.d <= 3)
+
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void cfence() { asm volatile("" ::: "memory"); }
+
+template <int CTRL>
+__device__ __forceinline__ double dpp32x2(double v) {   // all controls used have a source lane for every lane
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+
+template <int L>
+__device__ __forceinline__ double bcast16(double v) {   // lane L of each 16-lane row, to the whole row
+  const long b = __builtin_amdgcn_mov_dpp(__builtin_bit_cast(long, v), 0x150 + L, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, b);
+}
+
+__device__ __forceinline__ double sum16(double v) {   // fixed-order sum over the 16-lane row
+  v += dpp32x2<0xB1>(v);    // quad_perm [1,0,3,2]
+  v += dpp32x2<0x4E>(v);    // quad_perm [2,3,0,1]
+  v += dpp32x2<0x141>(v);   // row_half_mirror
+  v += dpp32x2<0x140>(v);   // row_mirror
+  return v;
+}
+
+__device__ __forceinline__ double recip(double x) {   // hardware reciprocal + two Newton steps (~1 ulp)
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(r, fma(-x, r, 1.), r);
+  return fma(r, fma(-x, r, 1.), r);
+}
+
+template <int B, int E, class F>
+__device__ __forceinline__ void sfor(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    sfor<B + 1, E>(f);
+  }
+}
+
+__device__ __forceinline__ int tri(int x) { return x * (x + 1) / 2; }
+
+constexpr int kK = 32, kMK = 30;
+constexpr int kPacked = kK * (kK + 1) / 2;   // 528
+
+template <int CS>
+constexpr int problem_doubles() { return kPacked + 48 * CS; }   // packed C (then dC) | 48 coordinate rows
+
+template <int COV, int DIM>
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2))) vecchia_rows16_kernel(VecchiaRowsArgs a) {
+  constexpr int ND = DIM > 0 ? DIM : kD3;
+  constexpr int CS = ND;
+  constexpr int PD = problem_doubles<CS>();
+  static_assert(PD % 2 == 0, "16-byte aligned problems");
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int lane = threadIdx.x;
+  const int g = lane >> 4;
+  double* Cp = smem + g * PD;
+  double* nbx = Cp + kPacked;
+  const double var = a.var, phi = a.phi;
+  const double cdiag = var * a.diag_mult + a.diag_add;
+  const double delta = cdiag - var;
+  const bool want_like = a.Y != nullptr;
+  const int d = DIM > 0 ? DIM : a.d;
+
+  double acc[kVecchiaSums] = {0., 0., 0., 0., 0., 0.};
+  const int total = a.r1 - a.r0;
+  for (int base = blockIdx.x * 4; base < total; base += gridDim.x * 4) {
+    int h = lane & 15;
+    asm volatile("" : "+v"(h));   // lane-dependent addresses / masks recomputed per problem (not hoisted)
+    const int v1 = h + 16;
+    const int i = a.r0 + base + g;
+    const bool active = i < a.r1;
+    const int k = active ? min(i, a.m) : 0;
+    const bool rv0 = h < k, rv1 = v1 < k;
+    const int irow = active ? i : a.r0;
+
+    // ---- gather (rows h and h + 16)
+    const int nb0 = rv0 ? a.nbr[(size_t)(i - a.row_base) * a.m + h] : 0;
+    const int nb1 = rv1 ? a.nbr[(size_t)(i - a.row_base) * a.m + v1] : 0;
+    double xi[ND], x0[ND], x1[ND];
+#pragma unroll
+    for (int q = 0; q < ND; ++q) {
+      xi[q] = (q < d) ? a.X[(size_t)irow * d + q] : 0.;
+      x0[q] = (q < d && rv0) ? a.X[(size_t)nb0 * d + q] : 0.;
+      x1[q] = (q < d && rv1) ? a.X[(size_t)nb1 * d + q] : 0.;
+    }
+    const double yi = want_like ? a.Y[irow] : 0.;
+    const double y0 = (want_like && rv0) ? a.Y[nb0] : 0.;
+    const double y1 = (want_like && rv1) ? a.Y[nb1] : 0.;
+    // padding rows at distinct far-away points: covariances exactly 0 (see vecchia_rows_kernel)
+    x0[0] = rv0 ? x0[0] : 1e30 * (h + 1);
+    x1[0] = rv1 ? x1[0] : 1e30 * (v1 + 1);
+    cfence();   // the previous problem's LDS reads are issued before these writes
+#pragma unroll
+    for (int q = 0; q < ND; ++q) {
+      nbx[h * CS + q] = x0[q];
+      nbx[v1 * CS + q] = x1[q];
+      nbx[(h + 32) * CS + q] = x0[q];
+    }
+    double c0, dc0, c1, dc1;
+    {
+      double s0 = 0., s1 = 0.;
+#pragma unroll
+      for (int q = 0; q < ND; ++q) {
+        const double t0 = xi[q] - x0[q], t1 = xi[q] - x1[q];
+        s0 += t0 * t0;
+        s1 += t1 * t1;
+      }
+      cov_dcov_sq<COV>(s0, var, phi, c0, dc0);
+      cov_dcov_sq<COV>(s1, var, phi, c1, dc1);
+      c0 = rv0 ? c0 : 0.;
+      dc0 = rv0 ? dc0 : 0.;
+      c1 = rv1 ? c1 : 0.;
+      dc1 = rv1 ? dc1 : 0.;
+    }
+    Cp[tri(h) + h] = rv0 ? cdiag : 1.;
+    Cp[tri(v1) + v1] = rv1 ? cdiag : 1.;
+    lds_sync();
+
+    // ---- 1. circulant pairs: row h with h + delta (delta = 1..16), row h + 16 with h + 16 + delta
+    // (delta = 1..15; past 31 it wraps to the first coordinate copy's duplicate at +32)
+    double w0[16], w1[15];
+    {
+      const int b0 = tri(h) + h, b1 = tri(v1) + v1;
+#pragma unroll
+      for (int dl = 1; dl <= 16; ++dl) {
+        const double* xp = nbx + (h + dl) * CS;
+        double s = 0.;
+#pragma unroll
+        for (int q = 0; q < ND; ++q) {
+          const double t = x0[q] - xp[q];
+          s += t * t;
+        }
+        double cv, dcv;
+        cov_dcov_sq<COV>(s, var, phi, cv, dcv);
+        Cp[b0 + h * dl + dl * (dl + 1) / 2] = cv;   // packed(h + dl, h)
+        w0[dl - 1] = dcv;
+      }
+#pragma unroll
+      for (int dl = 1; dl <= 15; ++dl) {
+        const double* xp = nbx + (v1 + dl) * CS;
+        double s = 0.;
+#pragma unroll
+        for (int q = 0; q < ND; ++q) {
+          const double t = x1[q] - xp[q];
+          s += t * t;
+        }
+        double cv, dcv;
+        cov_dcov_sq<COV>(s, var, phi, cv, dcv);
+        const int pos = (v1 + dl < kK) ? b1 + v1 * dl + dl * (dl + 1) / 2 : b1 + dl - kK;
+        Cp[pos] = cv;
+        w1[dl - 1] = dcv;
+      }
+    }
+    lds_sync();
+    // border rows 30 (c) and 31 (y_nbr)
+    Cp[tri(kMK) + h] = c0;
+    Cp[tri(kMK + 1) + h] = y0;
+    if (v1 < kMK) {
+      Cp[tri(kMK) + v1] = c1;
+      Cp[tri(kMK + 1) + v1] = y1;
+    }
+    lds_sync();
+
+    // ---- 2. rows h and h + 16 into registers, dC over the packed C (circulant layout)
+    double r0[kK], r1[kK];
+#pragma unroll
+    for (int c = 0; c < kK; ++c) {
+      r0[c] = (c <= h) ? Cp[tri(h) + c] : Cp[tri(c) + h];
+      r1[c] = (c <= v1) ? Cp[tri(v1) + c] : Cp[tri(c) + v1];
+    }
+    cfence();
+#pragma unroll
+    for (int dl = 1; dl <= 16; ++dl) Cp[(dl - 1) * kK + h] = w0[dl - 1];
+#pragma unroll
+    for (int dl = 1; dl <= 15; ++dl) Cp[(dl - 1) * kK + v1] = w1[dl - 1];
+    Cp[15 * kK + v1] = w0[15];   // the pair {h, h + 16}: both of its rows hold it (delta = 16)
+
+    // Gauss-Jordan, 30 pivots: M[j][c] = M[c][j] from lane c mod 16 (register set c / 16)
+    double dg0 = 1., dg1 = 1.;
+    sfor<0, kMK>([&](auto J) {
+      constexpr int j = decltype(J)::value;
+      constexpr int jl = j & 15;
+      constexpr bool jhi = j >= 16;
+      const double piv = bcast16<jl>(jhi ? r1[j] : r0[j]);
+      const double rinv = recip(piv);
+      const bool own = h == jl;
+      double f0 = r0[j] * rinv, f1 = r1[j] * rinv;
+      if constexpr (jhi) {
+        f1 = own ? 0. : f1;
+        dg1 = own ? piv : dg1;
+      } else {
+        f0 = own ? 0. : f0;
+        dg0 = own ? piv : dg0;
+      }
+      sfor<j + 1, kK>([&](auto C) {
+        constexpr int c = decltype(C)::value;
+        const double mc = bcast16<c & 15>(c >= 16 ? r1[j] : r0[j]);
+        r0[c] = fma(-f0, mc, r0[c]);
+        r1[c] = fma(-f1, mc, r1[c]);
+      });
+      // pin this step's updates (otherwise the FMAs are deferred and the broadcasts stay live)
+#pragma unroll
+      for (int c = j + 1; c < kK; ++c) asm volatile("" : "+v"(r0[c]), "+v"(r1[c]));
+    });
+    const double i0 = recip(dg0), i1 = recip(dg1);
+    const double a0 = rv0 ? r0[kMK] * i0 : 0., w0v = rv0 ? r0[kMK + 1] * i0 : 0.;
+    const double a1 = rv1 ? r1[kMK] * i1 : 0., w1v = rv1 ? r1[kMK + 1] * i1 : 0.;
+    if (active && a.B_out != nullptr) {
+      double* Bo = a.B_out + (size_t)(i - a.row_base) * a.m;
+      if (h < a.m) Bo[h] = rv0 ? -a0 : 0.;
+      if (v1 < a.m) Bo[v1] = rv1 ? -a1 : 0.;
+    }
+
+    // ---- 3. a^T dC a, w^T dC a over the circulant pairs (see vecchia_rows_kernel, bordered form)
+    double tA, tV;
+    {
+      v2d* av2 = reinterpret_cast<v2d*>(__builtin_assume_aligned(nbx, 16));
+      cfence();
+      av2[h] = v2d{a0, w0v};
+      av2[v1] = v2d{a1, w1v};
+      av2[h + 32] = v2d{a0, w0v};
+      lds_sync();
+      double s10 = 0., s20 = 0., s11 = 0., s21 = 0.;
+#pragma unroll
+      for (int dl = 1; dl < 16; ++dl) {
+        const double wa = Cp[(dl - 1) * kK + h], wb = Cp[(dl - 1) * kK + v1];
+        const v2d pa = av2[h + dl], pb = av2[v1 + dl];
+        s10 = fma(wa, pa.x, s10);
+        s20 = fma(wa, pa.y, s20);
+        s11 = fma(wb, pb.x, s11);
+        s21 = fma(wb, pb.y, s21);
+      }
+      const double h0 = Cp[15 * kK + h] * av2[h + 16].x, h1 = Cp[15 * kK + v1] * av2[v1 + 16].x;
+      tA = a0 * (2. * s10 + h0) + a1 * (2. * s11 + h1);
+      tV = w0v * (s10 + h0) + a0 * s20 + w1v * (s11 + h1) + a1 * s21;
+    }
+
+    // ---- 4. group sums (16 lanes) and the row partials
+    const double ac = sum16(a0 * c0 + a1 * c1);
+    const double ay = sum16(a0 * y0 + a1 * y1);
+    const double aa = sum16(a0 * a0 + a1 * a1);
+    const double avv = sum16(a0 * w0v + a1 * w1v);
+    const double dca = sum16(dc0 * a0 + dc1 * a1);
+    const double dcv = sum16(dc0 * w0v + dc1 * w1v);
+    const double ta = sum16(tA);
+    const double tv = sum16(tV);
+    const double D = var + a.d_nugget - ac;          // Vecchia_utils.cpp:1351, 1507, 1562
+    const double Dinv = 1. / D;
+    if (active && h == 0 && a.Dinv_out != nullptr) a.Dinv_out[i - a.row_base] = Dinv;
+    if (want_like && active && h == 0) {
+      const double By = yi - ay;
+      const double u = By * Dinv;
+      const double dD_var = var - delta * aa - ac;
+      const double uk_var = -delta * avv;
+      const double dD_rng = -(2. * dca - ta);
+      const double uk_rng = -(dcv - tv);
+      acc[0] += log(D);
+      acc[1] += By * u;
+      acc[2] += uk_var * u - 0.5 * u * u * dD_var;
+      acc[3] += uk_rng * u - 0.5 * u * u * dD_rng;
+      acc[4] += Dinv * dD_var;
+      acc[5] += Dinv * dD_rng;
+    }
+  }
+  if (!want_like) return;
+  __syncthreads();
+  double* red = smem;   // 4 x kVecchiaSums
+  if ((lane & 15) == 0) {
+#pragma unroll
+    for (int s = 0; s < kVecchiaSums; ++s) red[g * kVecchiaSums + s] = acc[s];
+  }
+  __syncthreads();
+  if (lane < kVecchiaSums) {
+    const double v = ((red[lane] + red[kVecchiaSums + lane]) + red[2 * kVecchiaSums + lane]) + red[3 * kVecchiaSums + lane];
+    a.block_sums[(size_t)blockIdx.x * kVecchiaSums + lane] = v;
+  }
+}
+
+constexpr int kMaxGrid = 2048;   // vecchia_rows_blocks' bound (kernels.h)
+
+template <int COV, int DIM>
+int launch16(const VecchiaRowsArgs& a, hipStream_t s) {
+  constexpr int CS = DIM > 0 ? DIM : kD3;
+  const size_t lds = (size_t)4 * problem_doubles<CS>() * sizeof(double);
+  auto kern = vecchia_rows16_kernel<COV, DIM>;
+  static int cap = 0;
+  if (cap == 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, kern, 64, lds));
+    cap = std::max(1, std::min(per_cu * cus, kMaxGrid));
+  }
+  const int need = (a.r1 - a.r0 + 3) / 4;
+  const int blocks = std::min(need, cap);
+  hipLaunchKernelGGL(kern, dim3(blocks), dim3(64), lds, s, a);
+  HIP_CHECK(hipGetLastError());
+  return blocks;
+}
+
+}  // namespace
+
+int launch_vecchia_rows16(int cov_type, const VecchiaRowsArgs& a, hipStream_t s) {
+  if (a.m > kMK) Fatal("16-lane row kernel: num_neighbors %d > %d", a.m, kMK);
+  if (a.r1 <= a.r0) return 0;
+  const bool planar = a.d == 2;
+  switch (cov_type) {
+    case kMatern05: return planar ? launch16<kMatern05, 2>(a, s) : launch16<kMatern05, 0>(a, s);
+    case kMatern15: return planar ? launch16<kMatern15, 2>(a, s) : launch16<kMatern15, 0>(a, s);
+    case kMatern25: return planar ? launch16<kMatern25, 2>(a, s) : launch16<kMatern25, 0>(a, s);
+    case kGaussian: return planar ? launch16<kGaussian, 2>(a, s) : launch16<kGaussian, 0>(a, s);
+    default: Fatal("unsupported covariance type %d", cov_type);
+  }
+  return 0;
+}
+
+}  // namespace gpb_amd
