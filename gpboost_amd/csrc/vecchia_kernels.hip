@@ -1006,10 +1006,12 @@ bool rows_dpp() { return std::getenv("GPBOOST_AMD_ROWS_DPP") != nullptr; }
 // Augmented entries: bordered rows (default where two lanes are spare) or the round-2 form with
 // separate augmented slots (GPBOOST_AMD_ROWS_SLOTS=1, A/B; read at every launch).
 bool rows_slots() { return std::getenv("GPBOOST_AMD_ROWS_SLOTS") != nullptr; }
-// 16-lane form (vecchia_rows16.hip) for m <= 30: GPBOOST_AMD_ROWS16=1 (A/B; read at every launch)
+// 16-lane form (vecchia_rows16.hip) for m <= 30, the default: measured on MI355X at n = 100k, m = 30
+// (profiles/r03/rows_env_ab_r03i.log) 0.225 ms per launch against 0.284 ms for the bordered 32-lane
+// LDS-broadcast form, which GPBOOST_AMD_ROWS16=0 selects (A/B; read at every launch)
 bool rows16() {
   const char* e = std::getenv("GPBOOST_AMD_ROWS16");
-  return e != nullptr && e[0] == '1';
+  return e == nullptr || e[0] != '0';
 }
 
 template <int K>
