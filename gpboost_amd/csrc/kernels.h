@@ -36,7 +36,10 @@ int launch_vecchia_rows16(int cov_type, const VecchiaRowsArgs& a, hipStream_t s)
 void launch_predict_mean_var(int n_pred, int m, const int* nbr, const double* B, const double* Dinv, const double* y,
                              double sigma2, double nugget_sub, double* out, hipStream_t s);
 // Deterministic fixed-order sum of block partials -> out[kVecchiaSums].
-void launch_sum_blocks(const double* block_sums, int nblocks, int width, double* out, hipStream_t s);
+// flag (nullable; host-coherent memory): after the sums are visible system-wide, *flag = seq (the
+// host spins on it instead of synchronising the stream)
+void launch_sum_blocks(const double* block_sums, int nblocks, int width, double* out, hipStream_t s,
+                       unsigned long long* flag = nullptr, unsigned long long seq = 0);
 
 // ---------------------------------------------------------------- dense path
 struct DenseArgs {

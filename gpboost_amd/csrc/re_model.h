@@ -216,6 +216,7 @@ class REModelAMD {
   DevBuf<int> d_nbr_;
   double* h_sums_ = nullptr;  // pinned
   double* h_sums_dev_ = nullptr;  // device address of h_sums_ (the single-rank sum kernel writes it directly)
+  unsigned long long sum_seq_ = 0;  // completion flag value of the last single-rank evaluation (h_sums_[8])
   bool events_pending_ = false;   // last_kernel_ms_ of the last row launch not read from its events yet
   bool timing_ = false;           // record kernel events (set by the first GetLastKernelTimes)
 

@@ -943,7 +943,8 @@ __global__ void __launch_bounds__(kV4Threads, 1) vecchia_rows2_kernel(VecchiaRow
 }
 
 __global__ void __launch_bounds__(1024) sum_blocks_kernel(const double* __restrict__ in, int nblocks, int width,
-                                                       double* __restrict__ out) {
+                                                       double* __restrict__ out, unsigned long long* flag,
+                                                       unsigned long long seq) {
   // width <= 8: thread t sums column (t & 7) over blocks (t >> 3) + 128 u, four loads in flight
   __shared__ double red[1024];
   const int col = threadIdx.x & 7, lane_b = threadIdx.x >> 3;
@@ -964,7 +965,14 @@ __global__ void __launch_bounds__(1024) sum_blocks_kernel(const double* __restri
     if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
     __syncthreads();
   }
-  if ((int)threadIdx.x < width) out[threadIdx.x] = red[threadIdx.x];
+  if ((int)threadIdx.x < width) {
+    out[threadIdx.x] = red[threadIdx.x];
+    if (flag != nullptr) __threadfence_system();   // the sums reach the host before the flag
+  }
+  if (flag != nullptr) {
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
 }
 
 // One thread per prediction point; entries in neighbour order.
@@ -1155,9 +1163,10 @@ void launch_predict_mean_var(int n_pred, int m, const int* nbr, const double* B,
   HIP_CHECK(hipGetLastError());
 }
 
-void launch_sum_blocks(const double* block_sums, int nblocks, int width, double* out, hipStream_t s) {
+void launch_sum_blocks(const double* block_sums, int nblocks, int width, double* out, hipStream_t s,
+                       unsigned long long* flag, unsigned long long seq) {
   if (width > 8) Fatal("sum_blocks: width %d > 8", width);
-  hipLaunchKernelGGL(sum_blocks_kernel, dim3(1), dim3(1024), 0, s, block_sums, nblocks, width, out);
+  hipLaunchKernelGGL(sum_blocks_kernel, dim3(1), dim3(1024), 0, s, block_sums, nblocks, width, out, flag, seq);
   HIP_CHECK(hipGetLastError());
 }
 
