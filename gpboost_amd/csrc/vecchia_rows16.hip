@@ -98,7 +98,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   const bool want_like = a.Y != nullptr;
   const int d = DIM > 0 ? DIM : a.d;
 
-  double acc[kVecchiaSums] = {0., 0., 0., 0., 0., 0.};
+  // the row partials accumulate in LDS (4 problems x 6 doubles after the problems' areas): a register
+  // accumulator would be live across the elimination, where the registers run out
+  double* acc = smem + 4 * PD + g * kVecchiaSums;
+  if ((lane & 15) < kVecchiaSums) acc[lane & 15] = 0.;
   const int total = a.r1 - a.r0;
   for (int base = blockIdx.x * 4; base < total; base += gridDim.x * 4) {
     int h = lane & 15;
@@ -301,12 +304,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   }
   if (!want_like) return;
   __syncthreads();
-  double* red = smem;   // 4 x kVecchiaSums
-  if ((lane & 15) == 0) {
-#pragma unroll
-    for (int s = 0; s < kVecchiaSums; ++s) red[g * kVecchiaSums + s] = acc[s];
-  }
-  __syncthreads();
+  const double* red = smem + 4 * PD;   // 4 x kVecchiaSums
   if (lane < kVecchiaSums) {
     const double v = ((red[lane] + red[kVecchiaSums + lane]) + red[2 * kVecchiaSums + lane]) + red[3 * kVecchiaSums + lane];
     a.block_sums[(size_t)blockIdx.x * kVecchiaSums + lane] = v;
@@ -318,7 +316,7 @@ constexpr int kMaxGrid = 2048;   // vecchia_rows_blocks' bound (kernels.h)
 template <int COV, int DIM>
 int launch16(const VecchiaRowsArgs& a, hipStream_t s) {
   constexpr int CS = DIM > 0 ? DIM : kD3;
-  const size_t lds = (size_t)4 * problem_doubles<CS>() * sizeof(double);
+  const size_t lds = (size_t)(4 * problem_doubles<CS>() + 4 * kVecchiaSums) * sizeof(double);
   auto kern = vecchia_rows16_kernel<COV, DIM>;
   static int cap = 0;
   if (cap == 0) {
