@@ -617,6 +617,12 @@ def main():
     gm.neg_log_likelihood_and_grad(THETA, Y, profile_sigma2=True)   # SetY + neighbour search + first eval
     t_construct = time.perf_counter() - t0
 
+    # untimed clock ramp before the W counted warm-up steps: the GPU leaves its idle clocks only after
+    # some tens of ms of load (a 5-step warm-up measured the row kernel ~8 % slower than after ~100 ms,
+    # profiles/r03/rows_env_ab_r03m.log vs bench_r03n.json)
+    t_ramp = time.perf_counter()
+    while time.perf_counter() - t_ramp < 0.5:
+        gm.neg_log_likelihood_and_grad(THETA, None, profile_sigma2=True)
     for _ in range(args.warmup):
         gm.neg_log_likelihood_and_grad(THETA, None, profile_sigma2=True)
 
