@@ -33,6 +33,11 @@ namespace gpb_amd {
 namespace {
 
 constexpr int kD3 = 3;   // coordinate dimension bound (VecchiaRowsArgs.d <= 3)
+// broadcasts in flight per elimination step (1, 2 or 4): 1 / 2 / 4 measured 0.2193 / 0.2176 / 0.2162 ms
+// per launch (profiles/r03/rows_ab_r03o.log, rows_ab_r03p.log)
+#ifndef GPB_ROWS16_BCG
+#define GPB_ROWS16_BCG 4
+#endif
 
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void cfence() { asm volatile("" ::: "memory"); }
@@ -124,8 +129,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       x1[q] = (q < d && rv1) ? a.X[(size_t)nb1 * d + q] : 0.;
     }
     const double yi = want_like ? a.Y[irow] : 0.;
-    const double y0 = (want_like && rv0) ? a.Y[nb0] : 0.;
-    const double y1 = (want_like && rv1) ? a.Y[nb1] : 0.;
+    double y0s = (want_like && rv0) ? a.Y[nb0] : 0.;
+    double y1s = (want_like && rv1) ? a.Y[nb1] : 0.;
     // padding rows at distinct far-away points: covariances exactly 0 (see vecchia_rows_kernel)
     x0[0] = rv0 ? x0[0] : 1e30 * (h + 1);
     x1[0] = rv1 ? x1[0] : 1e30 * (v1 + 1);
@@ -194,13 +199,22 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     lds_sync();
     // border rows 30 (c) and 31 (y_nbr)
     Cp[tri(kMK) + h] = c0;
-    Cp[tri(kMK + 1) + h] = y0;
+    Cp[tri(kMK + 1) + h] = y0s;
     if (v1 < kMK) {
       Cp[tri(kMK) + v1] = c1;
-      Cp[tri(kMK + 1) + v1] = y1;
+      Cp[tri(kMK + 1) + v1] = y1s;
     }
     lds_sync();
 
+    // c, dc and y_nbr of both rows wait out the elimination in the (now free) coordinate area
+    // instead of 12 registers (the elimination is register-bound)
+    cfence();
+    {
+      v2d* st = reinterpret_cast<v2d*>(__builtin_assume_aligned(nbx, 16)) + 3 * h;
+      st[0] = v2d{c0, dc0};
+      st[1] = v2d{c1, dc1};
+      st[2] = v2d{y0s, y1s};
+    }
     // ---- 2. rows h and h + 16 into registers, dC over the packed C (circulant layout)
     double r0[kK], r1[kK];
 #pragma unroll
@@ -232,16 +246,55 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         f0 = own ? 0. : f0;
         dg0 = own ? piv : dg0;
       }
+#if GPB_ROWS16_BCG > 1
+      // GPB_ROWS16_BCG broadcasts in flight: a group's DPP moves issue before its FMAs (the compiler
+      // otherwise reuses one temporary, a DPP -> FMA dependency per column)
+      constexpr int BG = GPB_ROWS16_BCG;
+      constexpr int ncol = kK - 1 - j;   // columns j + 1 .. kK - 1
+      sfor<0, ncol / BG>([&](auto P) {
+        constexpr int c0g = j + 1 + BG * decltype(P)::value;
+        double m[BG];
+        sfor<0, BG>([&](auto Q) {
+          constexpr int c = c0g + decltype(Q)::value;
+          m[decltype(Q)::value] = bcast16<c & 15>(c >= 16 ? r1[j] : r0[j]);
+        });
+        if constexpr (BG == 2) asm volatile("" ::"v"(m[0]), "v"(m[1]));
+        if constexpr (BG == 4) asm volatile("" ::"v"(m[0]), "v"(m[1]), "v"(m[2]), "v"(m[3]));
+#pragma unroll
+        for (int q = 0; q < BG; ++q) {
+          r0[c0g + q] = fma(-f0, m[q], r0[c0g + q]);
+          r1[c0g + q] = fma(-f1, m[q], r1[c0g + q]);
+        }
+      });
+      sfor<j + 1 + BG * (ncol / BG), kK>([&](auto C) {   // the remainder, one at a time
+        constexpr int c = decltype(C)::value;
+        const double mc = bcast16<c & 15>(c >= 16 ? r1[j] : r0[j]);
+        r0[c] = fma(-f0, mc, r0[c]);
+        r1[c] = fma(-f1, mc, r1[c]);
+      });
+#else
       sfor<j + 1, kK>([&](auto C) {
         constexpr int c = decltype(C)::value;
         const double mc = bcast16<c & 15>(c >= 16 ? r1[j] : r0[j]);
         r0[c] = fma(-f0, mc, r0[c]);
         r1[c] = fma(-f1, mc, r1[c]);
       });
+#endif
       // pin this step's updates (otherwise the FMAs are deferred and the broadcasts stay live)
 #pragma unroll
       for (int c = j + 1; c < kK; ++c) asm volatile("" : "+v"(r0[c]), "+v"(r1[c]));
     });
+    {   // the stashed c, dc, y_nbr back (read before the [a, w] array below overwrites the area)
+      lds_sync();
+      const v2d* st = reinterpret_cast<const v2d*>(__builtin_assume_aligned(nbx, 16)) + 3 * h;
+      const v2d s0 = st[0], s1 = st[1], s2 = st[2];
+      c0 = s0.x;
+      dc0 = s0.y;
+      c1 = s1.x;
+      dc1 = s1.y;
+      y0s = s2.x;
+      y1s = s2.y;
+    }
     const double i0 = recip(dg0), i1 = recip(dg1);
     const double a0 = rv0 ? r0[kMK] * i0 : 0., w0v = rv0 ? r0[kMK + 1] * i0 : 0.;
     const double a1 = rv1 ? r1[kMK] * i1 : 0., w1v = rv1 ? r1[kMK + 1] * i1 : 0.;
@@ -277,7 +330,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 
     // ---- 4. group sums (16 lanes) and the row partials
     const double ac = sum16(a0 * c0 + a1 * c1);
-    const double ay = sum16(a0 * y0 + a1 * y1);
+    const double ay = sum16(a0 * y0s + a1 * y1s);
     const double aa = sum16(a0 * a0 + a1 * a1);
     const double avv = sum16(a0 * w0v + a1 * w1v);
     const double dca = sum16(dc0 * a0 + dc1 * a1);
