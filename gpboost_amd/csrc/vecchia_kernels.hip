@@ -204,17 +204,6 @@ __device__ unsigned long long g_rows_prof[8];
 #ifndef GPB_ROWS_WAVES
 #define GPB_ROWS_WAVES 0
 #endif
-#ifndef GPB_PAIR_CHAIN
-#define GPB_PAIR_CHAIN 0
-#endif
-#ifndef GPB_ROWS_GJ2
-#define GPB_ROWS_GJ2 0
-#endif
-// Bordered scalar form: columns c with (c mod 16) < GPB_ROWS_LDSCOLS reach the lanes through the
-// LDS slot, the others by DPP row broadcasts + row-swap permutes (VALU); 16 = LDS only.
-#ifndef GPB_ROWS_LDSCOLS
-#define GPB_ROWS_LDSCOLS 16
-#endif
 #if GPB_ROWS_WAVES > 0
 #define GPB_ROWS_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(GPB_ROWS_WAVES, GPB_ROWS_WAVES)))
 #else
@@ -352,11 +341,6 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
         const int pos = (r + dl < K) ? base + r * dl + dl * (dl + 1) / 2 : base + dl - K;
         Cp[pos] = cv;
         wst[dl - 1] = dcv;
-#if GPB_PAIR_CHAIN
-        // one pair in flight: the next pair's distance waits for this pair's results (bounds the
-        // registers of the unrolled phase, which also holds the dC values)
-        asm volatile("" : "+v"(xr[0]) : "v"(cv), "v"(dcv));
-#endif
       }
     } else {
       const int h = r & (K / 2 - 1);
@@ -420,85 +404,18 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
         x = fma(x, fma(-piv, x, 1.), x);
         return fma(x, fma(-piv, x, 1.), x);
       };
-#if GPB_ROWS_GJ2
-      // 2 x 2 pivot blocks: step j eliminates columns j and j + 1 at once. Lanes publish the pair
-      // (row[j], row[j + 1]) as one 16-byte store; the pair read back from lane c is (M[c][j],
-      // M[c][j + 1]) = (M[j][c], M[j + 1][c]) by the symmetry of the trailing block. Each lane's
-      // multipliers [f0 f1] = [M[r][j] M[r][j + 1]] P^-1 (P = the pivot block; f = 0 on its own
-      // rows), update row[c] -= f0 M[j][c] + f1 M[j + 1][c]. Half the LDS round trips and
-      // reciprocals of the scalar form. The pivot rows keep their block, so at the end
-      // [a_j, a_j+1] = P^-1 [aug_j, aug_j+1]: every lane stores P^-1 of the step (uniform address)
-      // as lane j's pair (P^-1_00, P^-1_01) and lane j + 1's pair (P^-1_11, P^-1_10), read back
-      // at the lane's own index, with the partner lane's augmented entries by a DPP lane swap.
-      v2d* slot2 = reinterpret_cast<v2d*>(__builtin_assume_aligned(slot_c, 16));
-      v2d* pinv2 = slot2 + K;   // MK entries after the K-entry slot (within the coordinate copies)
-#pragma unroll
-      for (int j = 0; j < MK; j += 2) {
-        compiler_fence();
-        slot2[r] = v2d{row[j], row[j + 1]};
-        wave_lds_sync();
-        double c0[NC], c1[NC];
-#pragma unroll
-        for (int c = j; c < NC; ++c) {
-          const v2d v = slot2[c];
-          c0[c] = v.x;
-          c1[c] = v.y;
-        }
-        const double p00 = c0[j], p10 = c0[j + 1], p01 = c1[j], p11 = c1[j + 1];
-        const double rdet = recip(fma(p00, p11, -(p01 * p10)));
-        const double i00 = p11 * rdet, i11 = p00 * rdet, i01 = -p01 * rdet, i10 = -p10 * rdet;
-        pinv2[j] = v2d{i00, i01};
-        pinv2[j + 1] = v2d{i11, i10};
-        const bool pivrow = (r >> 1) == (j >> 1);
-        const double m0 = row[j], m1 = row[j + 1];
-        const double f0 = pivrow ? 0. : fma(m0, i00, m1 * i10);
-        const double f1 = pivrow ? 0. : fma(m0, i01, m1 * i11);
-#pragma unroll
-        for (int c = j + 2; c < NC; ++c) row[c] = fma(-f1, c1[c], fma(-f0, c0[c], row[c]));
-        // pin this step's updates here (otherwise the scheduler defers the FMAs and keeps every
-        // broadcast value live)
-#pragma unroll
-        for (int c = j + 2; c < NC; ++c) asm volatile("" : "+v"(row[c]));
-      }
-      aug1 = row[NC - 2];
-      aug2 = row[NC - 1];
-      wave_lds_sync();
-      const v2d pin = pinv2[r];   // own-row pair of the block's inverse (lanes r < MK)
-      const double w1 = dpp_f64<0xB1>(aug1), w2 = dpp_f64<0xB1>(aug2);   // partner lane r ^ 1
-      av_r = rv ? fma(pin.x, aug1, pin.y * w1) : 0.;
-      vv_r = rv ? fma(pin.x, aug2, pin.y * w2) : 0.;
-#else
       const v2d* slot2 = reinterpret_cast<const v2d*>(__builtin_assume_aligned(slot_c, 16));
-      constexpr int DL = (K == 32) ? GPB_ROWS_LDSCOLS : 16;   // hybrid broadcast: 32-lane groups only
 #pragma unroll
       for (int j = 0; j < MK; ++j) {
         double sv[NC];
-        bool any_lds = false;
+        compiler_fence();
+        slot_c[r] = row[j];
+        wave_lds_sync();
 #pragma unroll
-        for (int c = j; c < NC; ++c) any_lds = any_lds || (c & 15) < DL;
-        if (any_lds) {
-          compiler_fence();
-          slot_c[r] = row[j];
-          wave_lds_sync();
-#pragma unroll
-          for (int p = j >> 1; p < NC / 2; ++p) {
-            if (((2 * p) & 15) < DL) {
-              const v2d v = slot2[p];
-              sv[2 * p] = v.x;
-              sv[2 * p + 1] = v.y;
-            }
-          }
-        }
-        if constexpr (DL < 16) {
-          static_for<DL, 16>([&](auto CP) {
-            constexpr int cp = decltype(CP)::value;
-            if (cp + 16 >= j && cp + 16 < NC) {   // lane cp's and lane cp + 16's row[j]
-              double lo, hi;
-              group_bcast_pair<cp>(row[j], lo, hi);
-              sv[cp] = lo;
-              sv[cp + 16] = hi;
-            }
-          });
+        for (int p = j >> 1; p < NC / 2; ++p) {
+          const v2d v = slot2[p];
+          sv[2 * p] = v.x;
+          sv[2 * p + 1] = v.y;
         }
         const double rinv = recip(sv[j]);
         const double q = row[j] * rinv;
@@ -510,7 +427,6 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
       }
       aug1 = row[NC - 2];
       aug2 = row[NC - 1];
-#endif
     } else if constexpr (DPPBC) {
       // lane c holds row c, so M[c][j] = lane c's row[j]: broadcast lane c's register
       auto bc = [&](auto CPc, double v, double& lo, double& hi) {
@@ -586,7 +502,7 @@ __global__ void __launch_bounds__(block_threads<K>()) GPB_ROWS_WAVES_ATTR vecchi
       asm volatile("" : "+v"(aug1), "+v"(aug2));
     }
     }
-    if constexpr (!(BORDER && GPB_ROWS_GJ2)) {
+    {
     double mydiag = row[0];
 #pragma unroll
     for (int c = 1; c < MK; ++c) mydiag = (c == r) ? row[c] : mydiag;
@@ -1086,7 +1002,7 @@ int launch_k(const VecchiaRowsArgs& a, hipStream_t s) {
   const bool dpp = rows_dpp();
   if constexpr (K == 32) {
     if (!prof && a.m <= 30) {   // the headline configuration (m = 30): 30 elimination steps
-      if (rows16()) return launch_vecchia_rows16(COV, a, s);
+      if (rows16() && !dpp && !rows_slots()) return launch_vecchia_rows16(COV, a, s);
       if (dpp) {
         hipLaunchKernelGGL((vecchia_rows_kernel<K, COV, false, 30, true>), dim3(blocks), dim3(block_threads<K>()), lds, s, a);
       } else if (rows_slots()) {

@@ -253,7 +253,8 @@ def test_rows_dpp_broadcast_bitwise_equals_lds_form(m, monkeypatch):
     values into the same FMAs: the evaluations must agree bit for bit (K = 16 and 32 lane groups, 30
     and 32 elimination steps). The default bordered form (augmented columns as two extra matrix rows)
     reads the pivot row's augmented entries from the border rows instead, M[MK][j] for M[j][MK]:
-    equal up to rounding (1e-12 relative here)."""
+    equal up to rounding (1e-12 relative here); so is the default for m <= 30, the 16-lane
+    DPP-broadcast kernel (vecchia_rows16.hip), against the 32-lane bordered form (GPBOOST_AMD_ROWS16=0)."""
     from gpboost_amd import GPModel, synthetic
     n = 20000
     X = synthetic.bench_coords(n)
@@ -268,7 +269,12 @@ def test_rows_dpp_broadcast_bitwise_equals_lds_form(m, monkeypatch):
     monkeypatch.delenv("GPBOOST_AMD_ROWS_SLOTS", raising=False)
     monkeypatch.setenv("GPBOOST_AMD_ROWS_DPP", "1")
     b = gm.neg_log_likelihood_and_grad([0.1, 1.0, 0.1], None, profile_sigma2=True)
+    monkeypatch.delenv("GPBOOST_AMD_ROWS_DPP", raising=False)
+    monkeypatch.setenv("GPBOOST_AMD_ROWS16", "0")
+    d = gm.neg_log_likelihood_and_grad([0.1, 1.0, 0.1], None, profile_sigma2=True)
     assert a[0] == b[0]
     assert np.array_equal(a[1], b[1])
     assert abs(c[0] - a[0]) <= 1e-12 * abs(a[0])
     np.testing.assert_allclose(c[1], a[1], rtol=1e-12)
+    assert abs(d[0] - a[0]) <= 1e-12 * abs(a[0])
+    np.testing.assert_allclose(d[1], a[1], rtol=1e-12)
