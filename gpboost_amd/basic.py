@@ -469,19 +469,33 @@ class GPModel:
             g = grad[: self.num_cov_pars]
         return float(negll[0]), g.copy(), float(s2[0])
 
-    def calc_gradient_f(self, y=None, fixed_effects=None):
+    def calc_gradient_f(self, y=None, fixed_effects=None, calc_cov_factor=True):
         """Gradient of the (approximate marginal) negative log-likelihood wrt the fixed effects F at the
         current covariance parameters (GPB_CalcGradientF = the reference's REModel::CalcGradient, the
         GPBoost algorithm's boosting gradient). Gaussian likelihood: y = F - label, returns
-        Psi^-1 y / sigma^2; latent models: F = fixed_effects, returns -dlog p/dF + implicit terms."""
+        Psi^-1 y / sigma^2; latent models: F = fixed_effects, returns -dlog p/dF + implicit terms.
+        calc_cov_factor=False (after optim_cov_par_boosting) keeps the last evaluation's Laplace mode."""
         if y is not None:
             out = _as1d(y, "y").copy()
         else:
             out = np.zeros(self.num_data)
         fe = _as1d(fixed_effects, "fixed_effects") if fixed_effects is not None else None
         self._call(lib().GPB_CalcGradientF(self.handle, _dp(out), _dp(fe) if fe is not None else None,
-                                           ctypes.c_bool(True)))
+                                           ctypes.c_bool(calc_cov_factor)))
         return out
+
+    def optim_cov_par_boosting(self, y=None, fixed_effects=None, reuse_learning_rates=True):
+        """The covariance update of one GPBoost boosting round (GPB_OptimCovParBoosting = the reference's
+        REModel::OptimCovPar(y, F, called_in_GPBoost_algorithm=True, reuse_learning_rates_gp_model),
+        regression_objective.hpp:164, 178). Gaussian: y = F - label, fixed_effects None; latent models:
+        y None (the label set before) and fixed_effects = the current score F."""
+        yy = _as1d(y, "y") if y is not None else None
+        fe = _as1d(fixed_effects, "fixed_effects") if fixed_effects is not None else None
+        self._call(lib().GPB_OptimCovParBoosting(self.handle, _dp(yy) if yy is not None else None,
+                                                 _dp(fe) if fe is not None else None, ctypes.c_bool(True),
+                                                 ctypes.c_bool(reuse_learning_rates)))
+        self.model_fitted = True
+        return self
 
     def last_iteration_info(self):
         """[newton iterations, CG iterations, Lanczos steps, log|Sigma W + I|] of the last latent evaluation."""

@@ -431,14 +431,14 @@ void GroupedRE::Eval(const double* tau, bool want_grad, bool iterative, bool war
   Precond(d_probesP_.get(), d_PI_.get(), bt.S.get(), t);               // PI_RV = P^-1 z
   launch_gre_upper(Op(t), d_D_.get(), d_PI_.get(), d_DI_.get(), t, s_);  // DI_L_plus_D_t_PI_RV
   std::vector<double> sums((size_t)3 * t * K_);
+  d_sums3_.alloc((size_t)3 * t * K_);   // own scratch: M x t blocks can be smaller than 3 t (M < 3)
   for (int k = 0; k < K_; ++k) {
     const size_t o = (size_t)cum_[k] * t;
     const double* A[3] = {bt.U.get() + o, d_PI_.get() + o, d_DI_.get() + o};
     const double* B[3] = {d_PI_.get() + o, d_DI_.get() + o, d_DI_.get() + o};
-    launch_coldots(m_[k], t, 3, A, B, d_partials_.get(), bt.V.get(), s_);   // V: free scratch (>= 3 t)
-    HIP_CHECK(hipMemcpyAsync(sums.data() + (size_t)3 * t * k, bt.V.get(), sizeof(double) * 3 * t,
-                             hipMemcpyDeviceToHost, s_));
+    launch_coldots(m_[k], t, 3, A, B, d_partials_.get(), d_sums3_.get() + (size_t)3 * t * k, s_);
   }
+  HIP_CHECK(hipMemcpyAsync(sums.data(), d_sums3_.get(), sizeof(double) * sums.size(), hipMemcpyDeviceToHost, s_));
   HIP_CHECK(hipStreamSynchronize(s_));
   std::vector<double> z1(t), zP(t);
   for (int k = 0; k < K_; ++k) {

@@ -90,6 +90,7 @@ class GroupedRE {
   // warm (single column only): U holds the initial guess, R = RHS - A U.
   int Pcg(Block& b, const double* RHS, double* U, bool block, int pmax, double delta, bool warm = false);
 
+  DevBuf<double> d_sums3_;   // 3 t K column sums of the trace terms
   int n_, K_, M_;
   hipStream_t s_;
   std::vector<int> m_, cum_;

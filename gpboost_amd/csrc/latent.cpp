@@ -82,6 +82,16 @@ LatentVecchia::LatentVecchia(int n, int d, int m, const double* d_X, const int* 
                   &d_rhs_, &d_dir_, &d_Adir_, &d_vS_, &d_dmll_})
     b->alloc(n);
   d_out_.alloc(kOutDoubles);
+  // InitializeModeAvec at construction (re_model_template.h:6346): a warm start before any
+  // evaluation starts from 0
+  HIP_CHECK(hipMemsetAsync(d_mode_.get(), 0, sizeof(double) * n, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+}
+
+void LatentVecchia::ResetModeToPrevious() {
+  if (!mode_prev_valid_) return;
+  launch_copy(n_, d_mode_prev_.get(), d_mode_.get(), s_);
+  HIP_CHECK(hipStreamSynchronize(s_));
 }
 
 LatentVecchia::~LatentVecchia() {
@@ -772,7 +782,7 @@ LatentVecchia::PcgResult LatentVecchia::Pcg(Block& b, const double* RHS, double*
 }
 
 LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, double aux, const IterativeConfig& cfg,
-                                 bool want_grad, bool want_aux_grad, double* grad_f_vo) {
+                                 bool want_grad, bool want_aux_grad, double* grad_f_vo, ModeStart start) {
   if (!y_set_) Fatal("response variable y has not been set");
   if (!(trafo[0] > 0. && trafo[1] > 0.)) Fatal("covariance parameters must be > 0");
   if (lik == kLikGaussian && !(aux > 0.)) Fatal("the error variance (aux_pars) must be > 0");
@@ -835,8 +845,15 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
   sa.offset = has_off_ && !has_obs_ ? d_off_.get() : nullptr;
   sa.obs = Obs();
 
-  // ---- 2. mode finding (likelihoods.h:2780-3000); mode re-initialised to 0 (InitializeModeAvec)
-  HIP_CHECK(hipMemsetAsync(d_mode_.get(), 0, sizeof(double) * n, s_));
+  // ---- 2. mode finding (likelihoods.h:2780-3000): from 0 (InitializeModeAvec) or from the previous
+  // evaluation's mode (mode_previous_value_ kept for a reset)
+  if (start == ModeStart::kZero) {
+    HIP_CHECK(hipMemsetAsync(d_mode_.get(), 0, sizeof(double) * n, s_));
+  } else if (start == ModeStart::kWarm) {
+    d_mode_prev_.alloc(n);
+    launch_copy(n, d_mode_.get(), d_mode_prev_.get(), s_);
+    mode_prev_valid_ = true;
+  }
   HIP_CHECK(hipMemsetAsync(d_mode_upd_.get(), 0, sizeof(double) * n, s_));
   double sc[kLatentScalars];
   sa.mode = d_mode_.get();
@@ -916,7 +933,8 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
   } else {
     // ---- 2. mode finding (likelihoods.h:2780-3000)
     bool upd_zero = true;
-    for (int it = 0; it < maxit; ++it) {
+    const int newton_its = start == ModeStart::kKeep ? 0 : maxit;   // kKeep: the mode as it stands
+    for (int it = 0; it < newton_its; ++it) {
       NewtonPrepArgs np{};
       np.n = n; np.lik = lik; np.aux = aux; np.y = d_y_.get(); np.loc = d_mode_.get(); np.mode = d_mode_.get();
     np.offset = has_off_ && !has_obs_ ? d_off_.get() : nullptr;

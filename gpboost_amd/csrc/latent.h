@@ -77,8 +77,21 @@ class LatentVecchia {
   // trafo = (sigma1^2, phi). aux = gaussian error variance (ignored for bernoulli_logit).
   // grad_f_vo (host, Vecchia order, nullable; needs want_grad): gradient wrt the fixed effects F
   // (CalcGradNegMargLikelihoodLaplaceApproxVecchia calc_F_grad, likelihoods.h:5337-5367).
+  // start: where the Newton iterations begin (FindModePostRandEffCalcMLLVecchia, likelihoods.h:2782-2789):
+  //   kZero  the mode re-initialised to 0 (InitializeModeAvec: GPB_EvalNegLogLikelihood, predictions);
+  //   kWarm  the mode of the previous evaluation (the L-BFGS objective: mode_initialized_ stays true,
+  //          mode_previous_value_ = mode_), kept for ResetModeToPrevious;
+  //   kKeep  no mode finding: the factor, W and log-determinant at the current mode (CalcGradientF with
+  //          calc_cov_factor = false, re_model_template.h:3021-3043, after an OptimCovPar at these
+  //          parameters). The Gaussian likelihood's single Newton step does not depend on the start.
+  enum class ModeStart { kZero, kWarm, kKeep };
   LatentResult Eval(int cov_type, int lik, const double* trafo, double aux, const IterativeConfig& cfg,
-                    bool want_grad, bool want_aux_grad, double* grad_f_vo = nullptr);
+                    bool want_grad, bool want_aux_grad, double* grad_f_vo = nullptr,
+                    ModeStart start = ModeStart::kZero);
+  // Likelihood::ResetModeToPreviousValue (likelihoods.h:528-535): the mode at the start of the last
+  // kWarm evaluation back (no-op when no such evaluation started since ClearModePrevious).
+  void ResetModeToPrevious();
+  void ClearModePrevious() { mode_prev_valid_ = false; }
 
   // Operator costs on the factor of the last evaluation (benchmark roofline): out[0] = ms per
   // A = B^T D^-1 B + W application, out[1] = ms per VADU preconditioner application (both on
@@ -178,6 +191,8 @@ class LatentVecchia {
   std::unique_ptr<VaduPrecond> pre_;
   DevBuf<double> d_y_, d_Bv_, d_dBv_, d_Dinv_, d_dD_, d_W_, d_dw_, d_sdw_, d_d1_;
   DevBuf<double> d_mode_, d_mode_upd_, d_mode_new_, d_rhs_, d_dir_, d_Adir_, d_vS_, d_dmll_;
+  DevBuf<double> d_mode_prev_;   // mode_previous_value_ (kWarm evaluations)
+  bool mode_prev_valid_ = false;
   DevBuf<double> d_probes_, d_Zp_, d_U_, d_P_;   // n x t
   DevBuf<double> d_rhsf_, d_Uf_;                 // n x (1 + t): mode column fused with the probes (gaussian)
   int probes_t_ = 0;

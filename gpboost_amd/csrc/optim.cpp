@@ -24,48 +24,6 @@ double dot(const std::vector<double>& a, const std::vector<double>& b) {
 
 double norm2(const std::vector<double>& a) { return std::sqrt(dot(a, a)); }
 
-// Limited-memory inverse-Hessian approximation: a ring of the last m (s, y) pairs and the
-// two-loop recursion (Nocedal & Wright Alg. 7.4), as BFGSMat.h:89-105 / 160-186 keeps it.
-class InverseHessian {
- public:
-  InverseHessian(int dim, int m) : m_(m), s_(m, std::vector<double>(dim)), y_(m, std::vector<double>(dim)),
-                                   ys_(m), alpha_(m) {}
-  void Add(const std::vector<double>& s, const std::vector<double>& y) {
-    const int loc = ptr_ % m_;
-    s_[loc] = s;
-    y_[loc] = y;
-    ys_[loc] = dot(s, y);
-    theta_ = dot(y, y) / ys_[loc];
-    if (count_ < m_) ++count_;
-    ptr_ = loc + 1;
-  }
-  // out = a * H * v
-  void Apply(const std::vector<double>& v, double a, std::vector<double>& out) {
-    out.resize(v.size());
-    for (size_t i = 0; i < v.size(); ++i) out[i] = a * v[i];
-    int j = ptr_ % m_;
-    for (int k = 0; k < count_; ++k) {   // newest to oldest
-      j = (j + m_ - 1) % m_;
-      alpha_[j] = dot(s_[j], out) / ys_[j];
-      for (size_t i = 0; i < out.size(); ++i) out[i] -= alpha_[j] * y_[j][i];
-    }
-    for (double& o : out) o /= theta_;
-    for (int k = 0; k < count_; ++k) {   // oldest to newest
-      const double beta = dot(y_[j], out) / ys_[j];
-      for (size_t i = 0; i < out.size(); ++i) out[i] += (alpha_[j] - beta) * s_[j][i];
-      j = (j + 1) % m_;
-    }
-  }
-
- private:
-  int m_;
-  std::vector<std::vector<double>> s_, y_;
-  std::vector<double> ys_, alpha_;
-  double theta_ = 1.;
-  int count_ = 0;
-  int ptr_ = 0;   // ptr_ % m_ is the next slot (BFGSMat reset sets m_ptr = m, i.e. slot 0)
-};
-
 // LineSearchBacktracking::LineSearch with the Armijo rule and GPBoost's changes
 // (LineSearchBacktracking.h:45-143): shrink by 1/2, or by 1/32 after a large increase;
 // after max_linesearch trials fall back to xp (step 0).
@@ -98,8 +56,52 @@ void backtracking(LbfgsObjective& f, const LbfgsSettings& s, const std::vector<d
 
 }  // namespace
 
-int lbfgs_minimize(LbfgsObjective& f, std::vector<double>& x, double& fx, const LbfgsSettings& s) {
-  // LBFGS.h:86-301 (past = 1, epsilon = epsilon_rel = 1e-20, no neighbour re-determination)
+void InverseHessian::Reset(int dim, int m) {
+  // BFGSMat::reset (BFGSMat.h:89-105): no corrections, theta = 1
+  dim_ = dim;
+  m_ = m;
+  s_.assign(m, std::vector<double>(dim));
+  y_.assign(m, std::vector<double>(dim));
+  ys_.assign(m, 0.);
+  alpha_.assign(m, 0.);
+  theta_ = 1.;
+  count_ = 0;
+  ptr_ = 0;
+}
+
+void InverseHessian::Add(const std::vector<double>& s, const std::vector<double>& y) {
+  const int loc = ptr_ % m_;
+  s_[loc] = s;
+  y_[loc] = y;
+  ys_[loc] = dot(s, y);
+  theta_ = dot(y, y) / ys_[loc];
+  if (count_ < m_) ++count_;
+  ptr_ = loc + 1;
+}
+
+void InverseHessian::Apply(const std::vector<double>& v, double a, std::vector<double>& out) {
+  out.resize(v.size());
+  for (size_t i = 0; i < v.size(); ++i) out[i] = a * v[i];
+  int j = ptr_ % m_;
+  for (int k = 0; k < count_; ++k) {   // newest to oldest
+    j = (j + m_ - 1) % m_;
+    alpha_[j] = dot(s_[j], out) / ys_[j];
+    for (size_t i = 0; i < out.size(); ++i) out[i] -= alpha_[j] * y_[j][i];
+  }
+  for (double& o : out) o /= theta_;
+  for (int k = 0; k < count_; ++k) {   // oldest to newest
+    const double beta = dot(y_[j], out) / ys_[j];
+    for (size_t i = 0; i < out.size(); ++i) out[i] += (alpha_[j] - beta) * s_[j][i];
+    j = (j + 1) % m_;
+  }
+}
+
+int lbfgs_minimize(LbfgsObjective& f, std::vector<double>& x, double& fx, const LbfgsSettings& s, InverseHessian* given,
+                   bool reuse) {
+  // LBFGS.h:86-301 (past = 1, epsilon = epsilon_rel = 1e-20, no neighbour re-determination).
+  // given: the caller's m_bfgs (REModelTemplate::GetMBFGS): with reuse it seeds the first direction
+  // -H g at step 1 (when it holds corrections of this dimension, LBFGS.h:158-171); it receives the
+  // final approximation on convergence (LBFGS.h:262, 299).
   const int n = (int)x.size();
   InverseHessian H(n, s.m);
   std::vector<double> grad(n), xp(n), gradp(n), drt(n), vs(n), vy(n);
@@ -111,8 +113,15 @@ int lbfgs_minimize(LbfgsObjective& f, std::vector<double>& x, double& fx, const 
   double gnorm = norm2(grad);
   double fx_lag = fx;
   if (gnorm <= eps_grad || gnorm <= eps_grad * norm2(x)) return 1;
-  for (int i = 0; i < n; ++i) drt[i] = -grad[i];
-  double step = s.initial_step_factor / norm2(drt);
+  double step;
+  if (reuse && given != nullptr && given->count() > 0 && given->dim() == n) {
+    H = *given;
+    step = 1.;
+    H.Apply(grad, -1., drt);
+  } else {
+    for (int i = 0; i < n; ++i) drt[i] = -grad[i];
+    step = s.initial_step_factor / norm2(drt);
+  }
   const double eps = std::numeric_limits<double>::epsilon();
   for (int k = 1;; ++k) {
     xp = x;
@@ -131,7 +140,10 @@ int lbfgs_minimize(LbfgsObjective& f, std::vector<double>& x, double& fx, const 
     if (s.max_iterations != 0 && k >= s.max_iterations) converged = true;
     f.SetNumIter(k - 1);
     f.SetLag1ProfiledOutVariables();
-    if (converged) return k;
+    if (converged) {
+      if (given != nullptr) *given = H;
+      return k;
+    }
     for (int i = 0; i < n; ++i) {
       vs[i] = x[i] - xp[i];
       vy[i] = grad[i] - gradp[i];
@@ -236,6 +248,30 @@ void REModelAMD::FindInitCovPar(const double* y, double* trafo) const {
   }
 }
 
+void REModelAMD::InitCovParsIfNotDefined(const double* y, const double* fixed_effects) {
+  // REModel::InitializeCovParsIfNotDefined (re_model.cpp:1142-1164): init_cov_pars when given (set by
+  // SetOptimSettings), else FindInitCovPar on y - F (latent models: the stored response)
+  if (cov_pars_initialized_) return;
+  const int n = cfg_.n;
+  std::vector<double> yv;
+  if (cfg_.latent) {
+    if (y != nullptr) yv.assign(y, y + n);
+    else if (!y_raw_.empty()) yv = y_raw_;
+    else Fatal("Response variable data has not been set");
+  } else {
+    if (y == nullptr) Fatal("initial covariance parameters need the response variable y");
+    yv.assign(y, y + n);
+    if (fixed_effects != nullptr)
+      for (int i = 0; i < n; ++i) yv[i] -= fixed_effects[i];
+  }
+  double trafo[3];
+  FindInitCovPar(yv.data(), trafo);
+  if (cfg_.latent) cov_pars_orig_ = {trafo[0], range_back(cfg_.cov_type, trafo[1])};
+  else cov_pars_orig_ = {trafo[0], trafo[1] * trafo[0], range_back(cfg_.cov_type, trafo[2])};
+  init_used_ = cov_pars_orig_;
+  cov_pars_initialized_ = true;
+}
+
 void REModelAMD::SetOptimSettings(const double* init_cov_pars, double lr, int max_iter, double delta_rel_conv,
                                   const char* optimizer, int m_lbfgs) {
   // re_model.cpp:264-279 and re_model_template.h:710-823
@@ -333,7 +369,16 @@ class LatentObjective : public LbfgsObjective {
         const double aux = std::exp(x[2]);
         m_->SetAuxPars(&aux);
       }
-      EvalResult r = m_->EvalLatentTrafo(trafo, calc_grad || hint_grad, /*fatal_on_nan=*/false);
+      // the L-BFGS objective continues from the previous evaluation's mode (mode_initialized_,
+      // likelihoods.h:2782-2789); a gradient-only call at the point just evaluated uses that
+      // evaluation's mode as it stands (eval_likelihood = false, optim_utils.h:314-330)
+      const bool grad_only = !eval_ll && has_x_ && x == x_;
+      EvalResult r = m_->EvalLatentTrafo(trafo, calc_grad || hint_grad, /*fatal_on_nan=*/false,
+                                         grad_only ? LatentVecchia::ModeStart::kKeep : LatentVecchia::ModeStart::kWarm);
+      has_x_ = true;
+      bool bad = !std::isfinite(r.nll);
+      for (double g : r.grad) bad = bad || !std::isfinite(g);
+      if (bad) m_->ResetLatentModeToPrevious();   // EvalLLforLBFGSpp, optim_utils.h:349-360
       x_ = x;
       nll_ = r.nll;
       has_grad_ = calc_grad || hint_grad;
@@ -348,16 +393,20 @@ class LatentObjective : public LbfgsObjective {
   bool with_aux_;
   std::vector<double> x_, grad_;
   double nll_ = 0.;
-  bool has_grad_ = false;
+  bool has_grad_ = false, has_x_ = false;
 };
 
 }  // namespace
 
-void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects) {
+void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects, bool called_in_boosting, bool reuse_lr) {
   // REModel::OptimCovPar (re_model.cpp:339-401) -> OptimLinRegrCoefCovPar without covariates
   // (re_model_template.h:846-1700) -> OptimExternal "lbfgs" (optim_utils.h:561-706)
   UseDevice();
   const int n = cfg_.n;
+  if (reuse_lr && !called_in_boosting)
+    Fatal("reuse_learning_rates_from_previous_call requires called_in_GPBoost_algorithm");   // :1026-1028
+  // reuse_m_bfgs_from_previous_call (re_model_template.h:880-881)
+  const bool reuse_m_bfgs = reuse_lr && called_in_boosting && cov_est_once_ && cov_est_last_call_;
   if (y == nullptr) {   // the stored response (re_model_template.h:1188-1191, GetY)
     if (y_raw_.empty()) Fatal("response variable y has not been set");
     y = y_raw_.data();
@@ -366,7 +415,7 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects) {
     if (std::isnan(y[i]) || std::isinf(y[i])) Fatal("NaN or Inf in response variable / label ");
   std::vector<double> yraw(y, y + n);   // y may alias y_raw_
   SetResponseAndOffset(yraw.data(), fixed_effects);   // Gaussian: y - F; latent: location mode + F
-  if (fixed_effects != nullptr) {   // saved for prediction (re_model_template.h:1051-1054)
+  if (fixed_effects != nullptr && !called_in_boosting) {   // saved for prediction (re_model_template.h:1051-1054)
     fixed_effects_.assign(fixed_effects, fixed_effects + n);
     has_fixed_effects_ = true;
   }
@@ -410,19 +459,20 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects) {
     last_cov_pars_ = cov_pars_orig_;
     return;
   }
+  if (!reuse_m_bfgs) m_bfgs_ = InverseHessian();   // a fresh solver state (LBFGS.h:42-48)
   std::vector<double> x;
   double fx = 0.;
   if (!cfg_.latent) {
     x = {std::log(trafo[1]), std::log(trafo[2])};
     GaussianProfiledObjective obj(this);
-    num_it_ = lbfgs_minimize(obj, x, fx, optim_);
+    num_it_ = lbfgs_minimize(obj, x, fx, optim_, &m_bfgs_, reuse_m_bfgs);
     const double s2 = obj.sigma2();
     cov_pars_orig_ = {s2, std::exp(x[0]) * s2, range_back(cfg_.cov_type, std::exp(x[1]))};
   } else {
     x = {std::log(trafo[0]), std::log(trafo[1])};
     if (with_aux) x.push_back(std::log(aux_pars_[0]));
     LatentObjective obj(this, with_aux);
-    num_it_ = lbfgs_minimize(obj, x, fx, optim_);
+    num_it_ = lbfgs_minimize(obj, x, fx, optim_, &m_bfgs_, reuse_m_bfgs);
     cov_pars_orig_ = {std::exp(x[0]), range_back(cfg_.cov_type, std::exp(x[1]))};
     if (with_aux) aux_pars_[0] = std::exp(x[2]);
   }
@@ -430,6 +480,8 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects) {
     if (std::isnan(v) || std::isinf(v))
       Fatal("NaN or Inf occurred in covariance parameter optimization using 'lbfgs' (the reference's nelder_mead restart is not supported by gpboost_amd)");
   cov_pars_initialized_ = true;
+  cov_est_once_ = true;          // re_model_template.h:1614-1616
+  cov_est_last_call_ = true;
   last_nll_ = fx;
   last_cov_pars_ = cov_pars_orig_;
 }
@@ -502,7 +554,8 @@ void REModelAMD::OptimLinRegrCoefCovPar(const double* y, const double* X, int p,
   std::vector<double> x = {std::log(trafo[1]), std::log(trafo[2])};
   double fx = 0.;
   GaussianWlsObjective obj(this);
-  num_it_ = lbfgs_minimize(obj, x, fx, optim_);
+  m_bfgs_ = InverseHessian();
+  num_it_ = lbfgs_minimize(obj, x, fx, optim_, &m_bfgs_, false);
   for (double v : x)
     if (std::isnan(v) || std::isinf(v))
       Fatal("NaN or Inf occurred in covariance parameter optimization using 'lbfgs' (the reference's nelder_mead restart is not supported by gpboost_amd)");
@@ -512,6 +565,8 @@ void REModelAMD::OptimLinRegrCoefCovPar(const double* y, const double* X, int p,
   for (double v : coef_)
     if (std::isnan(v) || std::isinf(v)) Fatal("NaN or Inf occurred in the linear regression coefficients");
   cov_pars_initialized_ = true;
+  cov_est_once_ = true;
+  cov_est_last_call_ = true;
   last_nll_ = fx;
   last_cov_pars_ = cov_pars_orig_;
 }

@@ -39,8 +39,31 @@ class LbfgsObjective {
   virtual void SetNumIter(int) {}                   // LBFGS.h:231 (f.SetNumIter(k - 1))
 };
 
+// Limited-memory inverse-Hessian approximation: a ring of the last m (s, y) pairs and the
+// two-loop recursion (Nocedal & Wright Alg. 7.4), as BFGSMat.h:89-105 / 160-186 keeps it.
+class InverseHessian {
+ public:
+  InverseHessian() = default;
+  InverseHessian(int dim, int m) { Reset(dim, m); }
+  void Reset(int dim, int m);
+  void Add(const std::vector<double>& s, const std::vector<double>& y);
+  void Apply(const std::vector<double>& v, double a, std::vector<double>& out);   // out = a H v
+  int count() const { return count_; }   // BFGSMat::get_m_ncorr
+  int dim() const { return dim_; }       // BFGSMat::get_dim_param
+
+ private:
+  int dim_ = 0, m_ = 1;
+  std::vector<std::vector<double>> s_, y_;
+  std::vector<double> ys_, alpha_;
+  double theta_ = 1.;
+  int count_ = 0;
+  int ptr_ = 0;   // ptr_ % m_ is the next slot (BFGSMat reset sets m_ptr = m, i.e. slot 0)
+};
+
 // LBFGSSolver::minimize with LineSearchBacktracking (Armijo) as GPBoost runs it: returns the
 // number of iterations; x is overwritten with the minimiser and fx with its objective value.
-int lbfgs_minimize(LbfgsObjective& f, std::vector<double>& x, double& fx, const LbfgsSettings& s);
+// given / reuse: the m_bfgs kept across calls (reuse_m_bfgs_from_previous_call, LBFGS.h:86-171).
+int lbfgs_minimize(LbfgsObjective& f, std::vector<double>& x, double& fx, const LbfgsSettings& s,
+                   InverseHessian* given = nullptr, bool reuse = false);
 
 }  // namespace gpb_amd

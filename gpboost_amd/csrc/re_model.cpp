@@ -309,7 +309,8 @@ std::vector<double> gauss_hermite_adaptive(int order) {
 }  // namespace
 
 void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,
-                         bool predict_cov_mat, bool predict_var, bool predict_response, double* out) {
+                         bool predict_cov_mat, bool predict_var, bool predict_response, double* out,
+                         const double* mean_add) {
   if (!vecchia_) Fatal("predictions are implemented for the Vecchia approximation (gp_approx = 'vecchia' / "
                        "'vecchia_latent') only");
   if (world_ > 1) Fatal("predictions are only available on single-rank models");
@@ -391,6 +392,8 @@ void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred,
   std::vector<double> h((size_t)2 * n_pred);
   HIP_CHECK(hipMemcpyAsync(h.data(), dout.get(), sizeof(double) * h.size(), hipMemcpyDeviceToHost, stream_));
   HIP_CHECK(hipStreamSynchronize(stream_));
+  if (mean_add != nullptr)   // external fixed effects / linear predictor on the latent mean (re_model_template.h:3929-3946)
+    for (int p = 0; p < n_pred; ++p) h[p] += mean_add[p];
   std::copy(h.begin(), h.begin() + n_pred, out);
   if (latent && (predict_var || predict_response)) {
     // + the simulation term of PredictLaplaceApproxVecchia (iterative, likelihoods.h:6628-6746)
@@ -554,10 +557,16 @@ EvalResult REModelAMD::EvalLatent(const double* cov_pars_orig, bool want_grad) {
   return res;
 }
 
-EvalResult REModelAMD::EvalLatentTrafo(const double* trafo, bool want_grad, bool fatal_on_nan) {
+void REModelAMD::ResetLatentModeToPrevious() {
+  if (latent_) latent_->ResetModeToPrevious();
+}
+
+EvalResult REModelAMD::EvalLatentTrafo(const double* trafo, bool want_grad, bool fatal_on_nan,
+                                       LatentVecchia::ModeStart start) {
   if (!y_set_) Fatal("response variable y has not been set");
   UseDevice();
   EnsureStructure();
+  latent_->ClearModePrevious();
   const double aux = aux_pars_.empty() ? 1. : aux_pars_[0];
   const bool aux_grad = estimate_aux_pars && !aux_pars_.empty();
   LatentResult r;
@@ -565,7 +574,8 @@ EvalResult REModelAMD::EvalLatentTrafo(const double* trafo, bool want_grad, bool
     // fault injection for the tests: the k-th latent evaluation of this model reports NaN
     if (const char* e = std::getenv("GPBOOST_AMD_TEST_NAN_EVAL"))
       if (++test_nan_count_ == std::atoi(e)) throw LatentNan("NaN or Inf occurred (injected by GPBOOST_AMD_TEST_NAN_EVAL)");
-    r = latent_->Eval(cfg_.cov_type, cfg_.lik, trafo, aux, iter, want_grad, aux_grad);
+    r = latent_->Eval(cfg_.cov_type, cfg_.lik, trafo, aux, iter, want_grad, aux_grad, nullptr, start);
+    latent_evaluated_ = true;
   } catch (const LatentNan& e) {
     HIP_CHECK(hipStreamSynchronize(stream_));   // drain what the interrupted evaluation had queued
     if (fatal_on_nan) Fatal("%s", e.what());

@@ -89,8 +89,10 @@ class REModelAMD {
   // scale (null: those of the last evaluation); y null: the response already set. out: means, then
   // variances (predict_var) or the n_pred x n_pred covariance (predict_cov_mat; diagonal here).
   void SetPredictionData(const char* vecchia_pred_type, int num_neighbors_pred, int nsim_var_pred = -1);
+  // mean_add (nullable, n_pred): fixed effects / linear predictor added to the predictive mean before
+  // any response transform.
   void Predict(const double* y, int n_pred, const double* coords_pred, const double* cov_pars, bool predict_cov_mat,
-               bool predict_var, bool predict_response, double* out);
+               bool predict_var, bool predict_response, double* out, const double* mean_add = nullptr);
 
   void SetDistributed(int rank, int world, const ncclUniqueId& id, bool use_comm);
   // Same partition, cross-rank sums through a host function instead of RCCL (test transport).
@@ -115,7 +117,15 @@ class REModelAMD {
   // re_model.cpp:234-401, optim.cpp). Only the reference's default optimizer "lbfgs".
   void SetOptimSettings(const double* init_cov_pars, double lr, int max_iter, double delta_rel_conv,
                         const char* optimizer, int m_lbfgs);
-  void OptimCovPar(const double* y, const double* fixed_effects);
+  // called_in_boosting / reuse_lr: the GPBoost algorithm's call (REModel::OptimCovPar(..., true,
+  // reuse_learning_rates_gp_model), regression_objective.hpp:164, 178): the offset is not saved for
+  // prediction (re_model_template.h:1051) and the L-BFGS memory of the previous call seeds the first
+  // direction when both calls estimated the covariance parameters (:880-881).
+  void OptimCovPar(const double* y, const double* fixed_effects, bool called_in_boosting = false,
+                   bool reuse_lr = false);
+  // the latent mode of the previous objective evaluation back (ResetLaplaceApproxModeToPreviousValue,
+  // optim_utils.h:350-360) after a NaN / Inf objective or gradient
+  void ResetLatentModeToPrevious();
   // GPB_OptimLinRegrCoefCovPar (re_model.cpp:403-469 -> OptimLinRegrCoefCovPar
   // re_model_template.h:846-1700) for the Gaussian likelihood: covariance parameters by L-BFGS with
   // the nugget profiled out and the coefficients by generalised least squares at every objective
@@ -172,15 +182,25 @@ class REModelAMD {
   // (sigma^2, sigma1^2 / sigma^2, phi); latent trafo = (sigma1^2, phi). fatal_on_nan = false
   // returns a NaN / Inf objective instead of failing (the line search shrinks the step).
   EvalResult EvalTrafo(const double* trafo, bool want_grad, int profile, bool fatal_on_nan = true);
-  EvalResult EvalLatentTrafo(const double* trafo, bool want_grad, bool fatal_on_nan = true);
+  EvalResult EvalLatentTrafo(const double* trafo, bool want_grad, bool fatal_on_nan = true,
+                             LatentVecchia::ModeStart start = LatentVecchia::ModeStart::kZero);
 
   // iterative-method settings (GPB_SetOptimConfig, re_model_template.h:686-823)
   IterativeConfig iter;
   bool estimate_aux_pars = true;   // InitializeDefaultSettings (re_model_template.h:6492-6499) for latent models
   bool aux_pars_set_ = false;      // aux_pars given by the caller (SetOptimConfig init_aux_pars / SetAuxPars)
 
+  // REModel::InitializeCovParsIfNotDefined: init_cov_pars or FindInitCovPar on y - F (latent: the
+  // stored response); current_cov_pars() = the parameters an evaluation with cov_pars == NULL uses.
+  void InitCovParsIfNotDefined(const double* y, const double* fixed_effects);
+  const std::vector<double>& current_cov_pars() const { return cov_pars_orig_; }
+
   // Latent models: the fixed effects F (location offset) of the next mode finding (NULL: none).
   void SetLatentOffset(const double* fe);
+  // The offset a prediction uses: the given one, else the one saved by the last fit (re_model_template.h:3306-3312).
+  const double* ResolveOffset(const double* fe) const {
+    return fe != nullptr ? fe : (has_fixed_effects_ ? fixed_effects_.data() : nullptr);
+  }
 
  private:
   void TransformCovPars(const double* orig, double* trafo) const;
@@ -270,6 +290,10 @@ class REModelAMD {
   std::vector<double> init_cov_pars_, cov_pars_orig_, init_used_;   // original scale
   bool cov_pars_initialized_ = false;
   int num_it_ = 0;
+  InverseHessian m_bfgs_;                 // REModelTemplate::m_bfgs_ (GetMBFGS), kept across OptimCovPar calls
+  bool cov_est_once_ = false;             // cov_pars_have_been_estimated_once_ (re_model_template.h:5301)
+  bool cov_est_last_call_ = false;        // cov_pars_have_been_estimated_during_last_call_ (:5303)
+  bool latent_evaluated_ = false;         // the latent state (factor, mode) holds a finished evaluation
 };
 
 }  // namespace gpb_amd

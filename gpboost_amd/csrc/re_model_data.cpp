@@ -51,24 +51,17 @@ void REModelAMD::SetResponseAndOffset(const double* y, const double* fixed_effec
 }
 
 void REModelAMD::CalcGradientF(double* y, const double* fixed_effects, bool calc_cov_factor) {
-  (void)calc_cov_factor;   // the factor (and, for latent models, the mode) is recomputed at the current parameters
+  // re_model_template.h:3021-3043. Gaussian: the factor is recomputed at the current parameters
+  // (deterministic, so equal to the existing one). Latent: calc_cov_factor re-runs the mode finding
+  // from the current mode (CalcModePostRandEffCalcMLL, no InitializeModeAvec); without it the mode
+  // of the last evaluation (e.g. OptimCovPar's last objective call) is used as it stands.
   UseDevice();
   if (world_ > 1) Fatal("CalcGradientF is only available on single-rank models");
   if (y == nullptr) Fatal("the output array 'y' is NULL");
   const int n = cfg_.n;
   if (!cov_pars_initialized_) {   // InitializeCovParsIfNotDefined (re_model.cpp:1142-1164)
     if (cfg_.latent && !y_set_) Fatal("Response variable data has not been set");
-    double trafo[3];
-    if (cfg_.latent) {
-      std::vector<double> yv(y_raw_);
-      FindInitCovPar(yv.data(), trafo);
-      cov_pars_orig_ = {trafo[0], range_back(cfg_.cov_type, trafo[1])};
-    } else {
-      std::vector<double> yv(y, y + n);
-      FindInitCovPar(yv.data(), trafo);
-      cov_pars_orig_ = {trafo[0], trafo[1] * trafo[0], range_back(cfg_.cov_type, trafo[2])};
-    }
-    cov_pars_initialized_ = true;
+    InitCovParsIfNotDefined(cfg_.latent ? nullptr : y, nullptr);
   }
   if (cfg_.latent) {
     if (has_dup())
@@ -80,7 +73,10 @@ void REModelAMD::CalcGradientF(double* y, const double* fixed_effects, bool calc
     const double trafo[2] = {cov_pars_orig_[0], range_trafo(cfg_.cov_type, cov_pars_orig_[1])};
     const double aux = aux_pars_.empty() ? 1. : aux_pars_[0];
     std::vector<double> gvo(n);
-    latent_->Eval(cfg_.cov_type, cfg_.lik, trafo, aux, iter, true, false, gvo.data());
+    const auto start = (!calc_cov_factor && latent_evaluated_) ? LatentVecchia::ModeStart::kKeep
+                                                               : LatentVecchia::ModeStart::kWarm;
+    latent_->Eval(cfg_.cov_type, cfg_.lik, trafo, aux, iter, true, false, gvo.data(), start);
+    latent_evaluated_ = true;
     for (int i = 0; i < n; ++i) y[perm_[i]] = gvo[i];
     return;
   }
@@ -261,6 +257,7 @@ void REModelAMD::PredictTrainingDataRandomEffects(const double* cov_pars, const 
             "gpboost_amd");
     if (y != nullptr) SetResponse(y, nullptr);
     if (!y_set_) Fatal("Response variable data is not provided and has not been set before");
+    SetLatentOffset(ResolveOffset(fixed_effects));   // re_model_template.h:4032-4039
     EvalLatent(cp.data(), false);   // the posterior mode at cov_pars
     std::vector<double> mvo(nu_);
     latent_->GetMode(mvo.data());

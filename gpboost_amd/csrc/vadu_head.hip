@@ -108,7 +108,7 @@ __device__ __forceinline__ void solve_row(const HeadSolve& h, const Stage<EPL>& 
   if (lane == 0 && sub == 0) xs[st.rec & 0xffff] -= acc;
 }
 
-template <int EPL>
+template <int EPL, int NS>
 __global__ void __launch_bounds__(kHeadThreads) vadu_head_kernel(HeadSolve h, int t, const double* in,
                                                                  const double* __restrict__ dw, double* X) {
   extern __shared__ double xs[];   // this column's segment values by slot; slot K = scratch
@@ -139,18 +139,23 @@ __global__ void __launch_bounds__(kHeadThreads) vadu_head_kernel(HeadSolve h, in
   if (threadIdx.x == 0) xs[h.K] = 0.;
   __syncthreads();
   const int last = h.npass - 1;
-  Stage<EPL> A, B;
-  load_stage<EPL>(h, 0, slot, lane, A);
-  for (int q = 0; q < h.npass; q += 2) {
-    load_stage<EPL>(h, min(q + 1, last), slot, lane, B);
-    solve_row<EPL>(h, A, q, slot, lane, xs);
-    // rows of one level are independent: only a level's last pass needs the barrier (a
-    // workgroup-uniform flag, so every wave takes the same barriers)
-    if (__builtin_amdgcn_readfirstlane(A.pend)) lds_barrier();
-    if (q + 1 > last) break;
-    load_stage<EPL>(h, min(q + 2, last), slot, lane, A);
-    solve_row<EPL>(h, B, min(q + 1, last), slot, lane, xs);
-    if (__builtin_amdgcn_readfirstlane(B.pend)) lds_barrier();
+  // NS stages in flight: pass q + NS's structure is loaded while pass q solves (a pass is a few
+  // hundred cycles of LDS work, a structure load an L2 / Infinity-Cache round trip of more)
+  Stage<EPL> st[NS];
+#pragma unroll
+  for (int s = 0; s < NS; ++s) load_stage<EPL>(h, min(s, last), slot, lane, st[s]);
+  for (int q = 0; q < h.npass; q += NS) {
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      if (q + s <= last) {   // workgroup-uniform
+        solve_row<EPL>(h, st[s], q + s, slot, lane, xs);
+        // rows of one level are independent: only a level's last pass needs the barrier (a
+        // workgroup-uniform flag, so every wave takes the same barriers)
+        const int pend = __builtin_amdgcn_readfirstlane(st[s].pend);
+        load_stage<EPL>(h, min(q + s + NS, last), slot, lane, st[s]);
+        if (pend) lds_barrier();
+      }
+    }
   }
   // results out after the loop: a global store inside it would make the compiler drain the
   // prefetch (its registers are reused by the next stage's loads)
@@ -218,10 +223,29 @@ __global__ void __launch_bounds__(256) vadu_partial1_kernel(PartialList p, const
 
 }  // namespace
 
+// Structure stages in flight in the segment kernel (GPBOOST_AMD_HEAD_NS = 2, 4 or 6; default 4).
+int head_stages() {
+  static const int v = [] {
+    int k = 4;
+    if (const char* e = std::getenv("GPBOOST_AMD_HEAD_NS")) {
+      k = std::atoi(e);
+      if (k != 2 && k != 4 && k != 6) Fatal("GPBOOST_AMD_HEAD_NS must be 2, 4 or 6 (got '%s')", e);
+    }
+    return k;
+  }();
+  return v;
+}
+
 void launch_vadu_head(const HeadSolve& h, const double* in, const double* dw, double* X, int t, hipStream_t s) {
   if (h.npass <= 0 || t <= 0) return;
   const size_t lds = sizeof(double) * ((size_t)h.K + 1);
-  hipLaunchKernelGGL((vadu_head_kernel<kHeadEpl>), dim3(t), dim3(kHeadThreads), lds, s, h, t, in, dw, X);
+  const int ns = head_stages();
+  if (ns == 2)
+    hipLaunchKernelGGL((vadu_head_kernel<kHeadEpl, 2>), dim3(t), dim3(kHeadThreads), lds, s, h, t, in, dw, X);
+  else if (ns == 6)
+    hipLaunchKernelGGL((vadu_head_kernel<kHeadEpl, 6>), dim3(t), dim3(kHeadThreads), lds, s, h, t, in, dw, X);
+  else
+    hipLaunchKernelGGL((vadu_head_kernel<kHeadEpl, 4>), dim3(t), dim3(kHeadThreads), lds, s, h, t, in, dw, X);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -243,8 +267,9 @@ void launch_vadu_partial(const PartialList& p, const double* in, const double* d
 void set_vadu_head_lds_limit(int K) {
   if (K > kHeadMaxRows) Fatal("LDS segment of %d rows exceeds the LDS capacity (%d)", K, kHeadMaxRows);
   const int bytes = (int)(sizeof(double) * ((size_t)kHeadMaxRows + 1));
-  HIP_CHECK(hipFuncSetAttribute((const void*)vadu_head_kernel<kHeadEpl>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                bytes));
+  for (const void* f : {(const void*)vadu_head_kernel<kHeadEpl, 2>, (const void*)vadu_head_kernel<kHeadEpl, 4>,
+                        (const void*)vadu_head_kernel<kHeadEpl, 6>})
+    HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
 }
 
 }  // namespace gpb_amd

@@ -5,6 +5,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstdlib>
+#include <string>
 
 namespace gpb_amd {
 
@@ -133,6 +134,47 @@ void build_merged(int n, long budget, int gmax, const std::vector<std::vector<in
     h.offptr.push_back((int)h.offpos.size());
   }
 }
+
+// Rows of one merged level are independent (in-group dependencies are substituted), so their
+// launch order is free: sort each merged level's positions by storage row (the Morton curve), so
+// the contiguous position range each XCD gets (xcd_block) is one compact region of the domain and
+// the rows sharing gathered source rows run under one L2. Level order within a merged level (the
+// build order) spreads every XCD's range over the whole domain.
+void sort_merged_by_row(MergeHost& h) {
+  const int P = (int)h.rows.size();
+  std::vector<int> old_of(P), newpos(P);
+  for (size_t G = 0; G + 1 < h.lptr.size(); ++G) {
+    const int a = h.lptr[G], b = h.lptr[G + 1];
+    for (int p = a; p < b; ++p) old_of[p] = p;
+    std::stable_sort(old_of.begin() + a, old_of.begin() + b, [&](int x, int y) { return h.rows[x] < h.rows[y]; });
+  }
+  for (int q = 0; q < P; ++q) newpos[old_of[q]] = q;
+  MergeHost s;
+  s.lptr = h.lptr;
+  s.map = h.map;   // op_map values index this array; unchanged
+  s.rows.resize(P);
+  s.xoff.resize(P);
+  s.eoff.assign(1, 0);
+  s.opoff.assign(1, 0);
+  for (int q = 0; q < P; ++q) {
+    const int p = old_of[q];
+    s.rows[q] = h.rows[p];
+    const int base = (int)s.eidx.size();
+    s.eidx.insert(s.eidx.end(), h.eidx.begin() + h.eoff[p], h.eidx.begin() + h.eoff[p + 1]);
+    s.xoff[q] = base + (h.xoff[p] - h.eoff[p]);
+    s.eoff.push_back((int)s.eidx.size());
+    for (int o = h.opoff[p]; o < h.opoff[p + 1]; ++o) {
+      s.op_slot.push_back(h.op_slot[o]);
+      s.op_map.push_back(h.op_map[o]);
+      s.op_a.push_back(h.op_map[o] < 0 ? h.op_a[o] : newpos[h.op_a[o]]);   // substitution: a position
+    }
+    s.opoff.push_back((int)s.op_a.size());
+  }
+  s.offptr = h.offptr;
+  s.offpos.resize(h.offpos.size());
+  for (size_t k = 0; k < h.offpos.size(); ++k) s.offpos[k] = newpos[h.offpos[k]];
+  h = std::move(s);
+}
 }  // namespace
 
 void VaduPrecond::Build(const int* nbr, const std::vector<int>& vo, const std::vector<int>& lab,
@@ -210,6 +252,14 @@ void VaduPrecond::Build(const int* nbr, const std::vector<int>& vo, const std::v
     build_merged(
         n, budget, g, groups_f, [&](int i, auto f) { for (int r = 0; r < kk(i); ++r) f(nbr[(size_t)i * m + r], i * m + r); },
         tail, ml);
+    // launch order inside a merged level (GPBOOST_AMD_TAIL_ORDER=level keeps the build's level order)
+    const char* tord = std::getenv("GPBOOST_AMD_TAIL_ORDER");
+    if (tord && std::string(tord) != "level" && std::string(tord) != "row")
+      Fatal("GPBOOST_AMD_TAIL_ORDER must be row or level (got '%s')", tord);
+    if (!tord || std::string(tord) == "row") {
+      sort_merged_by_row(mb);
+      sort_merged_by_row(ml);
+    }
     std::vector<int> mint;
     MergeHost* hs[2] = {&mb, &ml};
     size_t o[2][10];

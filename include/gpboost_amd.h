@@ -274,14 +274,27 @@ GPBOOST_AMD_EXPORT int GPB_SetOffsetData(REModelHandle handle, const double* fix
  * parameters given by GPB_SetOptimConfig's init_aux_pars, -1 each when none were given. */
 GPBOOST_AMD_EXPORT int GPB_GetInitAuxPars(REModelHandle handle, double* aux_pars);
 
+/* EXTENSION (the reference has it as a C++ method only): REModel::OptimCovPar(y, fixed_effects,
+ * called_in_GPBoost_algorithm, reuse_learning_rates_from_previous_call) (re_model.cpp:339-401), the
+ * covariance update the GPBoost boosting objective runs every boosting round
+ * (regression_objective.hpp:164, 178: Gaussian OptimCovPar(F - label, NULL, true, reuse), latent
+ * OptimCovPar(NULL, score, true, reuse); reuse = the booster's reuse_learning_rates_gp_model, default
+ * true). With called_in_GPBoost_algorithm the offset is not saved for prediction
+ * (re_model_template.h:1051); with reuse as well, the L-BFGS inverse-Hessian approximation of the
+ * previous call seeds the first direction at step 1 when both calls estimated the covariance
+ * parameters (:880-881; LBFGS.h:158-171). GPB_OptimCovPar is this call with both flags false. */
+GPBOOST_AMD_EXPORT int GPB_OptimCovParBoosting(REModelHandle handle, const double* y_data, const double* fixed_effects,
+    bool called_in_GPBoost_algorithm, bool reuse_learning_rates_from_previous_call);
+
 /* EXTENSION (the reference has it as a C++ method only): REModel::CalcGradient (re_model.cpp:667-680
  * -> CalcGradientF re_model_template.h:3021-3043), what the GPBoost boosting objective calls after
  * GPB_OptimCovPar(handle, NULL, score) (regression_objective.hpp:164-179): the gradient of the
  * (approximate marginal) negative log-likelihood wrt the fixed effects F at the current covariance
  * parameters, written on y (length n, original order). Gaussian likelihood: input y = F - label,
  * output Psi^-1 y / sigma^2; latent models (Laplace): y is output only and F = fixed_effects, output
- * -dlog p(y|mode+F)/dF + the stochastic implicit-derivative terms (likelihoods.h:5337-5367). The
- * factor (and the mode) are always recomputed; calc_cov_factor is accepted for the signature. */
+ * -dlog p(y|mode+F)/dF + the stochastic implicit-derivative terms (likelihoods.h:5337-5367).
+ * calc_cov_factor = false (the booster's call after GPB_OptimCovParBoosting) keeps the Laplace mode
+ * of the last evaluation; true re-runs the mode finding from it. */
 GPBOOST_AMD_EXPORT int GPB_CalcGradientF(REModelHandle handle, double* y, const double* fixed_effects,
     bool calc_cov_factor);
 

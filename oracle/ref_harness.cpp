@@ -270,6 +270,60 @@ int main(int argc, char** argv) {
     return 0;
   }
 
+  if (mode == "boost") {
+    // The covariance update of R consecutive GPBoost boosting rounds as the boosting objective runs
+    // it (regression_objective.hpp:153-182, objective_function.cpp:149-156): per round the score
+    // F_r = scale_r * F (F from the input file), then
+    //   Gaussian: g = F_r - y; REModel::OptimCovPar(g, NULL, true, reuse); CalcGradient(g, NULL, false)
+    //   latent:   REModel::OptimCovPar(NULL, F_r, true, reuse); CalcGradient(grad, F_r, false)
+    // REModel::OptimCovPar (re_model.cpp:339-401) = InitializeCovParsIfNotDefined(y, F) (when y is
+    // given) + OptimLinRegrCoefCovPar(y, NULL, 0, cov_pars_, NULL, num_it, cov_pars_, NULL, F, true,
+    // true, reuse, false, false); CalcGradient = CalcGradientF(y, F, false, cov_pars_) (:667-680).
+    if (fe.empty()) { std::fprintf(stderr, "boost mode needs the fixed effects F in the input\n"); return 2; }
+    const std::vector<double> scales = parse_list(get(args, "scales", "0.5,1,1.5"));
+    const bool reuse = get(args, "reuse", "1") == "1";
+    const int no_index[1] = {-1};
+    m->SetOptimConfig(-1., 0.5, 1000, -1., true, 0, "lbfgs", 2, "relative_change_in_log_likelihood", 0.1, 0.5, "",
+                      std::atoi(get(args, "cg_max_num_it", "1000").c_str()),
+                      std::atoi(get(args, "cg_max_num_it", "1000").c_str()),
+                      std::atof(get(args, "cg_delta_conv", "1e-2").c_str()),
+                      std::atoi(get(args, "num_rand_vec_trace", "50").c_str()), true, "vadu",
+                      std::atoi(get(args, "seed_rand_vec_trace", "1").c_str()), -1, true, no_index, -1, -1.);
+    vec_t cp(m->num_cov_par_);
+    bool initialized = false;
+    if (!gauss) {   // objective_function.cpp:154-156: SetY(label); InitializeCovParsIfNotDefined(NULL, NULL)
+      m->SetY(y.data());
+      m->FindInitCovPar(nullptr, nullptr, cp.data());
+      initialized = true;
+    }
+    std::printf("{\n\"n\": %d, \"d\": %d,\n\"rounds\": [\n", n, d);
+    for (size_t r = 0; r < scales.size(); ++r) {
+      std::vector<double> F(n), g(n);
+      for (int i = 0; i < n; ++i) F[i] = scales[r] * fe[i];
+      int num_it = 0;
+      if (gauss) {
+        for (int i = 0; i < n; ++i) g[i] = F[i] - y[i];
+        if (!initialized) { m->FindInitCovPar(g.data(), nullptr, cp.data()); initialized = true; }
+        m->OptimLinRegrCoefCovPar(g.data(), nullptr, 0, cp.data(), nullptr, num_it, cp.data(), nullptr, nullptr,
+                                  true, true, reuse, false, false);
+        m->CalcGradientF(g.data(), nullptr, false, cp);
+      } else {
+        m->OptimLinRegrCoefCovPar(nullptr, nullptr, 0, cp.data(), nullptr, num_it, cp.data(), nullptr, F.data(),
+                                  true, true, reuse, false, false);
+        m->CalcGradientF(g.data(), F.data(), false, cp);
+      }
+      vec_t co;
+      m->TransformBackCovPars(cp, co);
+      std::printf("{");
+      print_vec("cov_pars", co.data(), (int)co.size());
+      std::printf("\"num_it\": %d, \"nll\": %.17g,\n", num_it, m->neg_log_likelihood_);
+      print_vec("grad_f", g.data(), n, false);
+      std::printf("}%s\n", r + 1 < scales.size() ? "," : "");
+    }
+    std::printf("],\n\"ok\": true\n}\n");
+    return 0;
+  }
+
   vec_t orig = Eigen::Map<const vec_t>(cov_pars_orig.data(), (int)cov_pars_orig.size());
   vec_t trafo;
   m->TransformCovPars(orig, trafo);

@@ -10,7 +10,7 @@ TAG="${TAG:-x}"
 OUT=gpurun_out/env_ab_${TAG}.log
 : > "$OUT"
 if [ "${TESTS:-0}" = 1 ]; then
-  timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu tests/test_gpu_latent.py \
+  timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu ${TEST_FILES:-tests/test_gpu_latent.py} \
     > gpurun_out/env_ab_tests_${TAG}.log 2>&1 || { tail -30 gpurun_out/env_ab_tests_${TAG}.log; exit 1; }
   tail -1 gpurun_out/env_ab_tests_${TAG}.log >> "$OUT"
 fi
