@@ -176,6 +176,26 @@ struct HeadSolve {
 };
 void launch_vadu_head(const HeadSolve& h, const double* in, const double* dw, double* X, int t, hipStream_t s);
 void set_vadu_head_lds_limit(int K);
+// One-wave form of the same segment solve (the default): the passes are run by ONE wave per column
+// (the workgroup's other waves only load the segment into LDS and write it back), so a pass is one
+// wave's instruction stream with no workgroup barrier — LDS operations of one wave complete in
+// order, which orders every pass's writes before the next pass's reads. A pass holds up to 64 >> lg
+// rows of one level, each on a group of G = 2^lg lanes (rows with more than kSegSteps entries take
+// G > 1); lane l of a pass takes the entries j = l % G, j + G, ... of its row over L <= kSegSteps
+// steps, lanes reduce over G by DPP, and the group's first lane writes x = -acc. A row's first
+// entry is its own input with coefficient -1 (value slot -2 -> -1 in the per-factor gather), so
+// acc = sum_e c_e x_e - in and the pass needs no read-modify-write. Entries are LDS byte offsets.
+constexpr int kSegSteps = 32;
+struct SegWave {
+  int K;               // segment rows (LDS slot K = a zero, the padding entries' target)
+  int npass;
+  const int* hrow;     // K: storage row of slot v
+  const int4* meta;    // npass: {entry offset (units of 64 entries), steps L, lg, 0}
+  const int* rec;      // npass x 64: the output slot of the lane's row (first lane of the group), -1 otherwise
+  const int* eidx;     // (sum of L) x 64: LDS byte offset of the entry's value
+  const double* eval;  // same layout: coefficient (the row's own input: -1; padding: 0)
+};
+void launch_vadu_seg_wave(const SegWave& w, const double* in, const double* dw, double* X, int t, hipStream_t s);
 // Partial sums of dependencies outside a step, for each listed row r (storage rows):
 //   out[r] = (in ? in[r] / (dw ? dw[r] : 1) : out[r]) - sum_{e in [eoff[w], eoff[w+1])} eval[e] src[eidx[e]]
 struct PartialList {
@@ -203,7 +223,7 @@ struct DenseHead {
 void dense_head_factor(const DenseHead& d, double* Bd, double* G, double* GT, double* T, hipStream_t s);
 void launch_dense_head_apply(const DenseHead& d, const double* G, const double* GT, const double* dw, const double* X,
                              double* S, double* Y, int t, hipStream_t s);
-// dst[e] = idx[e] >= 0 ? src[idx[e]] : 0
+// dst[e] = idx[e] >= 0 ? src[idx[e]] : (idx[e] == -2 ? -1 : 0)
 void launch_gather(int count, const int* idx, const double* src, double* dst, hipStream_t s);
 
 // Per-column dot products: out[q*t + c] = sum_i A_q[i,c] * B_q[i,c], q < np (np <= 3).

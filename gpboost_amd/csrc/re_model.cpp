@@ -254,10 +254,20 @@ void REModelAMD::SetPredictionData(const char* vecchia_pred_type, int num_neighb
     bool ok = false;
     for (const char* k : known) ok |= t == k;
     if (!ok) Fatal("Prediction type '%s' is not supported for the Veccia approximation ", t.c_str());
-    if (t != "order_obs_first_cond_obs_only" && t != "latent_order_obs_first_cond_obs_only")
+    std::string tt = t;
+    if (cfg_.latent) {   // SetVecchiaPredType (re_model_template.h:10564-10582): latent forms for Laplace models
+      if (tt == "order_obs_first_cond_obs_only") tt = "latent_order_obs_first_cond_obs_only";
+      if (tt == "order_obs_first_cond_all") tt = "latent_order_obs_first_cond_all";
+      if (tt == "order_pred_first")
+        Fatal("Prediction type '%s' is not supported for the Veccia approximation for non-Gaussian likelihoods ", t.c_str());
+    }
+    if (tt != "order_obs_first_cond_obs_only" && tt != "order_obs_first_cond_all" &&
+        tt != "latent_order_obs_first_cond_obs_only")
       Fatal("vecchia_pred_type '%s' is not supported by gpboost_amd (supported: order_obs_first_cond_obs_only, "
-            "latent_order_obs_first_cond_obs_only)", t.c_str());
-    vecchia_pred_type_ = t;
+            "order_obs_first_cond_all, latent_order_obs_first_cond_obs_only)", t.c_str());
+    if (tt == "latent_order_obs_first_cond_obs_only" && !cfg_.latent)
+      Fatal("vecchia_pred_type '%s' for the Gaussian likelihood is not supported by gpboost_amd", t.c_str());
+    vecchia_pred_type_ = tt;
   }
   if (num_neighbors_pred > 0) num_neighbors_pred_ = num_neighbors_pred;
 }
@@ -347,8 +357,12 @@ void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred,
   for (int p = 0; p < n_pred; ++p)
     for (int q = 0; q < d; ++q) xa[(size_t)(n + p) * d + q] = coords_pred[(size_t)q * n_pred + p];
   std::vector<int> nb((size_t)n_pred * mp);
-  if (d <= 3) vecchia_neighbors_gpu(xa.data(), na, d, mp, n, na, nb.data(), stream_, n - 1);
-  else vecchia_neighbors(xa.data(), na, d, mp, n, na, nb.data(), n - 1);
+  // order_obs_first_cond_all: neighbours among the observed AND the earlier prediction points
+  // (find_nearest_neighbors_Vecchia_fast end_search_at = -1, Vecchia_utils.cpp:1729-1737)
+  const bool cond_all = !latent && vecchia_pred_type_ == "order_obs_first_cond_all";
+  const int end_at = cond_all ? -1 : n - 1;
+  if (d <= 3) vecchia_neighbors_gpu(xa.data(), na, d, mp, n, na, nb.data(), stream_, end_at);
+  else vecchia_neighbors(xa.data(), na, d, mp, n, na, nb.data(), end_at);
   DevBuf<double> dxa((size_t)na * d), dB((size_t)n_pred * mp), dD(n_pred), dout((size_t)2 * n_pred), dmode;
   DevBuf<int> dnb((size_t)n_pred * mp);
   HIP_CHECK(hipMemcpyAsync(dxa.get(), xa.data(), sizeof(double) * xa.size(), hipMemcpyHostToDevice, stream_));
@@ -385,13 +399,19 @@ void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred,
     dmode.alloc(n);
     HIP_CHECK(hipMemcpyAsync(dmode.get(), mode.data(), sizeof(double) * n, hipMemcpyHostToDevice, stream_));
     launch_predict_mean_var(n_pred, mp, dnb.get(), dB.get(), dD.get(), dmode.get(), 1., 0., dout.get(), stream_);
-  } else {
+  } else if (!cond_all) {
     launch_predict_mean_var(n_pred, mp, dnb.get(), dB.get(), dD.get(), d_y_.get(), trafo[0],
                             predict_response ? 0. : 1., dout.get(), stream_);
   }
   std::vector<double> h((size_t)2 * n_pred);
-  HIP_CHECK(hipMemcpyAsync(h.data(), dout.get(), sizeof(double) * h.size(), hipMemcpyDeviceToHost, stream_));
-  HIP_CHECK(hipStreamSynchronize(stream_));
+  std::vector<double> cov_all;   // cond_all: the dense predictive covariance (predict_cov_mat)
+  if (cond_all) {
+    PredictCondAll(n, n_pred, mp, nb, dB.get(), dD.get(), trafo[0], predict_response ? 0. : 1., predict_var,
+                   predict_cov_mat, h, cov_all);
+  } else {
+    HIP_CHECK(hipMemcpyAsync(h.data(), dout.get(), sizeof(double) * h.size(), hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
   if (mean_add != nullptr)   // external fixed effects / linear predictor on the latent mean (re_model_template.h:3929-3946)
     for (int p = 0; p < n_pred; ++p) h[p] += mean_add[p];
   std::copy(h.begin(), h.begin() + n_pred, out);
@@ -416,12 +436,92 @@ void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred,
       for (int p = 0; p < n_pred; ++p) h[n_pred + p] += aux_pars_.empty() ? 0. : aux_pars_[0];
     }
   }
-  if (predict_cov_mat) {   // conditioning on observed points only: the predictive covariance is diagonal
+  if (predict_cov_mat && cond_all) {
+    std::copy(cov_all.begin(), cov_all.end(), out + n_pred);
+  } else if (predict_cov_mat) {   // conditioning on observed points only: the predictive covariance is diagonal
     double* c = out + n_pred;
     std::fill(c, c + (size_t)n_pred * n_pred, 0.);
     for (int p = 0; p < n_pred; ++p) c[(size_t)p * n_pred + p] = h[n_pred + p];
   } else if (predict_var) {
     std::copy(h.begin() + n_pred, h.end(), out + n_pred);
+  }
+}
+
+// order_obs_first_cond_all, Gaussian likelihood (Vecchia_utils.cpp:1776-1803 the B rows split into
+// Bpo (observed neighbours) and Bp (earlier prediction points), :1977-2006 the moments): the rows
+// (A = -B, Dp) come from the row kernel like the obs-only type; then on the host
+//   mean = -Bp^-1 Bpo y                         (sp_L_solve: forward substitution in prediction order)
+//   cov  = Bp^-1 diag(Dp) Bp^-T, var its diagonal (rows of Bp^-1 by the same recursion)
+// less the nugget unless predict_response, times sigma^2 (re_model_template.h:3789-3815).
+void REModelAMD::PredictCondAll(int n, int n_pred, int mp, const std::vector<int>& nb, const double* dB,
+                                const double* dDinv, double sigma2, double nugget_sub, bool want_var, bool want_cov,
+                                std::vector<double>& h, std::vector<double>& cov) {
+  std::vector<double> B((size_t)n_pred * mp), Dinv(n_pred), y(n);
+  HIP_CHECK(hipMemcpyAsync(B.data(), dB, sizeof(double) * B.size(), hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipMemcpyAsync(Dinv.data(), dDinv, sizeof(double) * n_pred, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipMemcpyAsync(y.data(), d_y_.get(), sizeof(double) * n, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  h.assign((size_t)2 * n_pred, 0.);
+  double* mu = h.data();
+  for (int p = 0; p < n_pred; ++p) {   // -Bpo y
+    double s = 0.;
+    for (int r = 0; r < mp; ++r) {
+      const int j = nb[(size_t)p * mp + r];
+      if (j < n) s -= B[(size_t)p * mp + r] * y[j];
+    }
+    mu[p] = s;
+  }
+  for (int p = 0; p < n_pred; ++p)   // Bp mu = -Bpo y, unit lower triangular in prediction order
+    for (int r = 0; r < mp; ++r) {
+      const int j = nb[(size_t)p * mp + r];
+      if (j >= n) mu[p] -= B[(size_t)p * mp + r] * mu[j - n];
+    }
+  if (!want_var && !want_cov) return;
+  // rows of Bp^-1: R_p = e_p - sum_{j in pred nbrs(p)} B_pj R_j (sparse, column indices ascending)
+  std::vector<std::vector<std::pair<int, double>>> R(n_pred);
+  std::vector<double> acc(n_pred, 0.);
+  std::vector<int> touched;
+  std::vector<char> on(n_pred, 0);
+  for (int p = 0; p < n_pred; ++p) {
+    touched.clear();
+    acc[p] = 1.;
+    on[p] = 1;
+    touched.push_back(p);
+    for (int r = 0; r < mp; ++r) {
+      const int j = nb[(size_t)p * mp + r];
+      if (j < n) continue;
+      const double b = B[(size_t)p * mp + r];
+      for (const auto& e : R[j - n]) {
+        if (!on[e.first]) { on[e.first] = 1; acc[e.first] = 0.; touched.push_back(e.first); }
+        acc[e.first] -= b * e.second;
+      }
+    }
+    std::sort(touched.begin(), touched.end());
+    R[p].reserve(touched.size());
+    for (int k : touched) {
+      R[p].emplace_back(k, acc[k]);
+      on[k] = 0;
+    }
+  }
+  std::vector<double> Dp(n_pred);
+  for (int p = 0; p < n_pred; ++p) Dp[p] = 1. / Dinv[p];
+  for (int p = 0; p < n_pred; ++p) {
+    double v = 0.;
+    for (const auto& e : R[p]) v += e.second * e.second * Dp[e.first];
+    h[n_pred + p] = (v - nugget_sub) * sigma2;
+  }
+  if (!want_cov) return;
+  cov.assign((size_t)n_pred * n_pred, 0.);
+  std::vector<double> row(n_pred);
+  for (int p = 0; p < n_pred; ++p) {
+    std::fill(row.begin(), row.end(), 0.);
+    for (const auto& e : R[p]) row[e.first] = e.second * Dp[e.first];
+    for (int q = 0; q <= p; ++q) {
+      double c = 0.;
+      for (const auto& e : R[q]) c += row[e.first] * e.second;
+      cov[(size_t)p * n_pred + q] = cov[(size_t)q * n_pred + p] = c * sigma2;
+    }
+    cov[(size_t)p * n_pred + p] -= nugget_sub * sigma2;
   }
 }
 
@@ -482,19 +582,21 @@ void REModelAMD::LaunchVecchiaRows(const double* trafo, int r0, int r1, double* 
     launch_sum_blocks(d_block_sums_.get(), nblocks, kVecchiaSums, h_sums_dev_, stream_);
     if (timing) HIP_CHECK(hipEventRecord(ev_[2], stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
-  } else if (allreduce && coll_ != nullptr) {
-    launch_sum_blocks(d_block_sums_.get(), nblocks, kVecchiaSums, d_sums_.get(), stream_);
-    coll_->AllReduceSum(d_sums_.get(), kVecchiaSums, stream_);
-    HIP_CHECK(hipMemcpyAsync(h_sums_, d_sums_.get(), sizeof(double) * kVecchiaSums, hipMemcpyDeviceToHost, stream_));
-    if (timing) HIP_CHECK(hipEventRecord(ev_[2], stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
   } else {
-    // one rank: the fixed-order block sum writes the host-coherent buffer directly and then a
-    // sequence flag (after a system-scope release); the host spins on the flag instead of
-    // synchronising the stream: 0.2448 vs 0.2500 ms per evaluation (profiles/r03/rows_env_ab_r03k.log)
+    // the fixed-order block sum writes the host-coherent buffer directly and then a sequence flag
+    // (after a system-scope release); the host spins on the flag instead of synchronising the
+    // stream: 0.2448 vs 0.2500 ms per evaluation at one rank (profiles/r03/rows_env_ab_r03k.log).
+    // Several ranks: the block sum goes to the device, is all-reduced on the stream, and a one-block
+    // pass of the same kernel publishes the reduced sums and the flag.
     unsigned long long* flag = reinterpret_cast<unsigned long long*>(h_sums_dev_ + 8);
     const unsigned long long seq = ++sum_seq_;
-    launch_sum_blocks(d_block_sums_.get(), nblocks, kVecchiaSums, h_sums_dev_, stream_, flag, seq);
+    if (allreduce && coll_ != nullptr) {
+      launch_sum_blocks(d_block_sums_.get(), nblocks, kVecchiaSums, d_sums_.get(), stream_);
+      coll_->AllReduceSum(d_sums_.get(), kVecchiaSums, stream_);
+      launch_sum_blocks(d_sums_.get(), 1, kVecchiaSums, h_sums_dev_, stream_, flag, seq);
+    } else {
+      launch_sum_blocks(d_block_sums_.get(), nblocks, kVecchiaSums, h_sums_dev_, stream_, flag, seq);
+    }
     if (timing) HIP_CHECK(hipEventRecord(ev_[2], stream_));
     volatile unsigned long long* hf = reinterpret_cast<volatile unsigned long long*>(h_sums_ + 8);
     for (long spins = 1; *hf != seq; ++spins) {

@@ -204,6 +204,9 @@ class REModelAMD {
 
  private:
   void TransformCovPars(const double* orig, double* trafo) const;
+  void PredictCondAll(int n, int n_pred, int mp, const std::vector<int>& nb, const double* dB, const double* dDinv,
+                      double sigma2, double nugget_sub, bool want_var, bool want_cov, std::vector<double>& h,
+                      std::vector<double>& cov);
   double range_trafo_of(double rho) const { return range_trafo(cfg_.cov_type, rho); }
   void FindInitCovPar(const double* y, double* trafo) const;
   double InitialRangeTrafo() const;

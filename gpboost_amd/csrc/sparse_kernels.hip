@@ -897,7 +897,7 @@ __global__ void __launch_bounds__(kBT) gather_kernel(int count, const int* __res
                                                      const double* __restrict__ src, double* __restrict__ dst) {
   for (int e = blockIdx.x * kBT + threadIdx.x; e < count; e += gridDim.x * kBT) {
     const int k = idx[e];
-    dst[e] = k >= 0 ? src[k] : 0.;
+    dst[e] = k >= 0 ? src[k] : (k == -2 ? -1. : 0.);   // -1: zero padding; -2: the constant -1
   }
 }
 

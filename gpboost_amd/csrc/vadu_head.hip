@@ -173,6 +173,115 @@ __global__ void __launch_bounds__(kHeadThreads) vadu_head_kernel(HeadSolve h, in
   }
 }
 
+// ---- one-wave segment solve (SegWave, latent_kernels.h)
+//
+// Why one wave: the per-pass cost of vadu_head_kernel (1024 threads) was its sixteen waves each
+// running the whole pass code (gather, four DPP stages, the row write) between workgroup barriers,
+// ~0.55 us per pass. Here the pass is one wave's stream: up to kSegSteps LDS gathers and FMAs per
+// lane, a DPP reduction over the row's lane group and one LDS write, with no barrier (a wave's LDS
+// operations complete in order). The other three waves of the workgroup only stage the segment
+// into LDS and write it back.
+constexpr int kSegThreads = 256;
+
+struct SegStage {
+  int rec;
+  int id[kSegSteps];
+  double v[kSegSteps];
+};
+
+__device__ __forceinline__ void seg_load(const SegWave& w, int4 m, int lane, SegStage& st) {
+  st.rec = w.rec[(size_t)m.w * 64 + lane];   // m.w: the pass index (set by seg_meta)
+  const size_t base = (size_t)m.x * 64 + lane;
+#pragma unroll
+  for (int k0 = 0; k0 < kSegSteps; k0 += 8) {
+    if (k0 < m.y) {   // wave-uniform
+#pragma unroll
+      for (int k = k0; k < k0 + 8; ++k) {
+        st.id[k] = w.eidx[base + (size_t)k * 64];
+        st.v[k] = w.eval[base + (size_t)k * 64];
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ int4 seg_meta(const SegWave& w, int q) {
+  int4 m = w.meta[q];
+  m.w = q;
+  return m;
+}
+
+// sum over the row's lane group of 2^lg lanes (lg wave-uniform), every lane of the group gets it
+__device__ __forceinline__ double seg_group_sum(double v, int lg) {
+  if (lg >= 1) v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
+  if (lg >= 2) v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]
+  if (lg >= 3) v += dpp_f64<0x141>(v);   // row_half_mirror
+  if (lg >= 4) v += dpp_f64<0x140>(v);   // row_mirror
+  if (lg >= 5) v += __shfl_xor(v, 16, 64);
+  if (lg >= 6) v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+template <int NS>
+__global__ void __launch_bounds__(kSegThreads) vadu_seg_wave_kernel(SegWave w, int t, const double* in,
+                                                                    const double* __restrict__ dw, double* X) {
+  extern __shared__ double xs[];   // this column's segment values by slot; slot K = 0 (padding target)
+  const int c = blockIdx.x;
+  for (int v = threadIdx.x; v < w.K; v += kSegThreads) {
+    const int r = w.hrow[v];
+    const double x = in[(size_t)r * t + c];
+    xs[v] = dw ? x / dw[r] : x;
+  }
+  if (threadIdx.x == 0) xs[w.K] = 0.;
+  __syncthreads();
+  if (threadIdx.x < 64 && w.npass > 0) {
+    const int lane = threadIdx.x;
+    const char* xb = reinterpret_cast<const char*>(xs);
+    const int last = w.npass - 1;
+    SegStage st[NS];
+    int4 m[NS];
+#pragma unroll
+    for (int s = 0; s < NS; ++s) {
+      m[s] = seg_meta(w, min(s, last));
+      seg_load(w, m[s], lane, st[s]);
+    }
+    for (int q = 0; q <= last; q += NS) {
+#pragma unroll
+      for (int s = 0; s < NS; ++s) {
+        if (q + s <= last) {   // wave-uniform
+          const int L = m[s].y, lg = m[s].z;
+          double a0 = 0., a1 = 0., a2 = 0., a3 = 0.;
+#pragma unroll
+          for (int k0 = 0; k0 < kSegSteps; k0 += 8) {
+            if (k0 < L) {   // steps k0..k0+7 (padding entries beyond L hold a zero coefficient)
+              double g[8];
+#pragma unroll
+              for (int k = 0; k < 8; ++k)
+                g[k] = *reinterpret_cast<const double*>(xb + st[s].id[k0 + k]);
+              a0 = fma(st[s].v[k0 + 0], g[0], a0);
+              a1 = fma(st[s].v[k0 + 1], g[1], a1);
+              a2 = fma(st[s].v[k0 + 2], g[2], a2);
+              a3 = fma(st[s].v[k0 + 3], g[3], a3);
+              a0 = fma(st[s].v[k0 + 4], g[4], a0);
+              a1 = fma(st[s].v[k0 + 5], g[5], a1);
+              a2 = fma(st[s].v[k0 + 6], g[6], a2);
+              a3 = fma(st[s].v[k0 + 7], g[7], a3);
+            }
+          }
+          const double acc = seg_group_sum((a0 + a1) + (a2 + a3), lg);
+          const int rec = st[s].rec;
+          if (rec >= 0) xs[rec] = -acc;
+          // the next pass's gathers stay behind this write in program order (LDS is in order per wave)
+          asm volatile("" ::: "memory");
+          m[s] = seg_meta(w, min(q + s + NS, last));
+          seg_load(w, m[s], lane, st[s]);
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int v = threadIdx.x; v < w.K; v += kSegThreads) X[(size_t)w.hrow[v] * t + c] = xs[v];
+}
+
 // Partial sums of the dependencies outside a solve step, for every listed row r:
 //   out[r] = (in ? in[r] / (dw ? dw[r] : 1) : out[r]) - sum_e eval[e] src[eidx[e]]
 // (entries in list order). t >= 2: one wave per row, lane = column, the row's structure by one
@@ -262,13 +371,40 @@ void launch_vadu_partial(const PartialList& p, const double* in, const double* d
   HIP_CHECK(hipGetLastError());
 }
 
+// Structure stages in flight in the one-wave segment kernel (GPBOOST_AMD_SEG_NS = 1, 2 or 3; default 2).
+int seg_stages() {
+  static const int v = [] {
+    int k = 2;
+    if (const char* e = std::getenv("GPBOOST_AMD_SEG_NS")) {
+      k = std::atoi(e);
+      if (k < 1 || k > 3) Fatal("GPBOOST_AMD_SEG_NS must be 1, 2 or 3 (got '%s')", e);
+    }
+    return k;
+  }();
+  return v;
+}
+
+void launch_vadu_seg_wave(const SegWave& w, const double* in, const double* dw, double* X, int t, hipStream_t s) {
+  if (w.K <= 0 || t <= 0) return;
+  const size_t lds = sizeof(double) * ((size_t)w.K + 1);
+  const int ns = seg_stages();
+  if (ns == 1)
+    hipLaunchKernelGGL((vadu_seg_wave_kernel<1>), dim3(t), dim3(kSegThreads), lds, s, w, t, in, dw, X);
+  else if (ns == 3)
+    hipLaunchKernelGGL((vadu_seg_wave_kernel<3>), dim3(t), dim3(kSegThreads), lds, s, w, t, in, dw, X);
+  else
+    hipLaunchKernelGGL((vadu_seg_wave_kernel<2>), dim3(t), dim3(kSegThreads), lds, s, w, t, in, dw, X);
+  HIP_CHECK(hipGetLastError());
+}
+
 // The limit is per kernel function, not per model: always the largest head any model may use,
 // so a later model with a smaller K cannot lower it under an earlier model's launches.
 void set_vadu_head_lds_limit(int K) {
   if (K > kHeadMaxRows) Fatal("LDS segment of %d rows exceeds the LDS capacity (%d)", K, kHeadMaxRows);
   const int bytes = (int)(sizeof(double) * ((size_t)kHeadMaxRows + 1));
   for (const void* f : {(const void*)vadu_head_kernel<kHeadEpl, 2>, (const void*)vadu_head_kernel<kHeadEpl, 4>,
-                        (const void*)vadu_head_kernel<kHeadEpl, 6>})
+                        (const void*)vadu_head_kernel<kHeadEpl, 6>, (const void*)vadu_seg_wave_kernel<1>,
+                        (const void*)vadu_seg_wave_kernel<2>, (const void*)vadu_seg_wave_kernel<3>})
     HIP_CHECK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
 }
 

@@ -298,9 +298,13 @@ void launch_level(const MergedSolve& ms, const double* coef, int p0, int cnt, co
     else hipLaunchKernelGGL((merged_level1_kernel<64>), grid, dim3(256), 0, s, ms, coef, p0, cnt, in, X);
     return;
   }
-  if (ks.form == 2) {
-    hipLaunchKernelGGL((merged_levelW_kernel<16>), dim3((cnt + 3) / 4, (t + 63) / 64), dim3(256), 0, s, ms, coef, p0,
-                       cnt, in, X, t);
+  if (ks.form == 2) {   // wave per row: gathers in flight per batch = LEVELT_CH (16 or 32)
+    if (ks.ch == 32)
+      hipLaunchKernelGGL((merged_levelW_kernel<32>), dim3((cnt + 3) / 4, (t + 63) / 64), dim3(256), 0, s, ms, coef,
+                         p0, cnt, in, X, t);
+    else
+      hipLaunchKernelGGL((merged_levelW_kernel<16>), dim3((cnt + 3) / 4, (t + 63) / 64), dim3(256), 0, s, ms, coef,
+                         p0, cnt, in, X, t);
     return;
   }
   const dim3 g(cnt, (t + 63) / 64);

@@ -188,6 +188,11 @@ void VaduPrecond::Build(const int* nbr, const std::vector<int>& vo, const std::v
   K_ = K;
   DropGraphs();
   use_graph_ = std::getenv("GPBOOST_AMD_NO_GRAPH") == nullptr;   // diagnostics: eager launches (profilers)
+  if (const char* e = std::getenv("GPBOOST_AMD_SEG_FORM")) {
+    const std::string f(e);
+    if (f != "wave" && f != "block") Fatal("GPBOOST_AMD_SEG_FORM must be wave or block (got '%s')", e);
+    seg_wave_ = f == "wave";
+  }
   auto kk = [&](int p) { return std::min(vo[p], m); };             // entries of storage row p
   auto part = [&](int p) { return vo[p] < K0 ? 0 : (vo[p] < K ? 1 : 2); };
   std::vector<int> ints;    // every index array of the plan, one upload
@@ -305,7 +310,10 @@ void VaduPrecond::Build(const int* nbr, const std::vector<int>& vo, const std::v
 
   // ---- head 1 segment [K0, K): slots = Vecchia index - K0, dependencies inside the segment
   const int KS = K - K0;
-  struct SegArrays { std::vector<int> rec, eidx, slot, ooff{0}, oidx, oslot, pend; };
+  struct SegArrays {
+    std::vector<int> rec, eidx, slot, ooff{0}, oidx, oslot, pend;
+    std::vector<int> wmeta, wrec, widx, wslot;   // one-wave form (SegWave): meta as 4 ints per pass
+  };
   auto build_seg = [&](bool lower) {
     SegArrays h;
     std::vector<int> lev(KS, 0);
@@ -334,6 +342,47 @@ void VaduPrecond::Build(const int* nbr, const std::vector<int>& vo, const std::v
     for (int s = 0; s < KS; ++s) {
       const int v = lower ? s : KS - 1 - s;
       byl[lev[v]].push_back(v);
+    }
+    // one-wave form: per level, rows by lane-group class lg (2^lg lanes, each <= kSegSteps entries
+    // of the row's own input + dependencies), longest first, up to 64 >> lg rows per pass; steps
+    // padded to a multiple of 8 (padding: slot KS, coefficient 0)
+    for (const auto& rows : byl) {
+      std::vector<std::vector<int>> cls(7);
+      for (int v : rows) {
+        const int c = 1 + (int)deps[v].size();
+        int lg = 0;
+        while ((kSegSteps << lg) < c) ++lg;
+        if (lg > 6) Fatal("VADU segment row with %d entries exceeds the one-wave plan (%d)", c, kSegSteps << 6);
+        cls[lg].push_back(v);
+      }
+      for (int lg = 0; lg <= 6; ++lg) {
+        auto& cv = cls[lg];
+        std::stable_sort(cv.begin(), cv.end(), [&](int x, int y) { return deps[x].size() > deps[y].size(); });
+        const int G = 1 << lg, per = 64 >> lg;
+        for (size_t r0 = 0; r0 < cv.size(); r0 += per) {
+          const int nr = (int)std::min<size_t>(per, cv.size() - r0);
+          int L = 0;
+          for (int r = 0; r < nr; ++r) L = std::max(L, (int)(1 + deps[cv[r0 + r]].size() + G - 1) / G);
+          L = (L + 7) / 8 * 8;
+          const int off = (int)(h.widx.size() / 64);
+          const int q = (int)(h.wmeta.size() / 4);
+          h.wmeta.insert(h.wmeta.end(), {off, L, lg, 0});
+          h.wrec.resize((size_t)(q + 1) * 64, -1);
+          h.widx.resize((size_t)(off + L) * 64, KS * 8);
+          h.wslot.resize((size_t)(off + L) * 64, -1);
+          for (int r = 0; r < nr; ++r) {
+            const int v = cv[r0 + r];
+            h.wrec[(size_t)q * 64 + r * G] = v;
+            const int c = 1 + (int)deps[v].size();
+            for (int e = 0; e < c; ++e) {   // e = 0: the row's own input, coefficient -1
+              const int k = e / G, lane = r * G + e % G;
+              const size_t at = (size_t)(off + k) * 64 + lane;
+              h.widx[at] = (e == 0 ? v : deps[v][e - 1]) * 8;
+              h.wslot[at] = e == 0 ? -2 : dslot[v][e - 1];
+            }
+          }
+        }
+      }
     }
     const int E = kHeadEpl;
     auto nslots = [&](int v) {   // 1, 2 or 4 slots of kHeadG lanes (rows beyond 4 slots overflow)
@@ -382,7 +431,7 @@ void VaduPrecond::Build(const int* nbr, const std::vector<int>& vo, const std::v
   std::vector<int> hrow(KS);
   for (int v = 0; v < KS; ++v) hrow[v] = lab[K0 + v];
   const size_t o_hrow = put(hrow);
-  size_t o_s[2][5], v_s[2][2];
+  size_t o_s[2][8], v_s[2][3];
   for (int w = 0; w < 2; ++w) {
     SegArrays& h = w == 0 ? sl : sb;
     o_s[w][0] = put(h.rec);
@@ -390,10 +439,16 @@ void VaduPrecond::Build(const int* nbr, const std::vector<int>& vo, const std::v
     o_s[w][2] = put(h.oidx);
     o_s[w][3] = put(h.ooff);
     o_s[w][4] = put(h.pend);
+    while (ints.size() % 4) ints.push_back(0);   // int4 alignment of the pass metas
+    o_s[w][5] = put(h.wmeta);
+    o_s[w][6] = put(h.wrec);
+    o_s[w][7] = put(h.widx);
     v_s[w][0] = vslot.size();
     vslot.insert(vslot.end(), h.slot.begin(), h.slot.end());
     v_s[w][1] = vslot.size();
     vslot.insert(vslot.end(), h.oslot.begin(), h.oslot.end());
+    v_s[w][2] = vslot.size();
+    vslot.insert(vslot.end(), h.wslot.begin(), h.wslot.end());
   }
 
   // ---- partial sums across parts
@@ -476,6 +531,14 @@ void VaduPrecond::Build(const int* nbr, const std::vector<int>& vo, const std::v
     h.pend = I + o_s[w][4];
     h.eval = V + v_s[w][0];
     h.oval = V + v_s[w][1];
+    SegWave& sw = w == 0 ? segw_low_ : segw_bt_;
+    sw.K = KS;
+    sw.npass = (int)(a.wmeta.size() / 4);
+    sw.hrow = I + o_hrow;
+    sw.meta = reinterpret_cast<const int4*>(I + o_s[w][5]);
+    sw.rec = I + o_s[w][6];
+    sw.eidx = I + o_s[w][7];
+    sw.eval = V + v_s[w][2];
   }
   PartialList* pl[3] = {&p_th_, &p_10_, &p_01_};
   for (int w = 0; w < 3; ++w) {
@@ -524,6 +587,11 @@ void VaduPrecond::DenseApply(const double* X0, double* Z, int t, hipStream_t st,
   launch_dense_head_apply(dh_, G_.get(), GT_.get(), dw_, X0, S, Z, t, st);
 }
 
+void VaduPrecond::SegSolve(bool lower, const double* in, const double* dw, double* X, int t, hipStream_t st) {
+  if (seg_wave_) launch_vadu_seg_wave(lower ? segw_low_ : segw_bt_, in, dw, X, t, st);
+  else launch_vadu_head(lower ? seg_low_ : seg_bt_, in, dw, X, t, st);
+}
+
 void VaduPrecond::TailSolve(bool lower, const double* R, double* Xt, double* Z, int t, hipStream_t st) {
   const MergedSolve& ms = lower ? mt_low_ : mt_bt_;
   for (int L = 0; L + 1 < (int)ms.lptr.size(); ++L)
@@ -536,7 +604,7 @@ void VaduPrecond::Record(const double* R, double* Z, double* Xt, int t, hipStrea
   // the last partial sum over the head-0 rows also stores them compactly for the dense products
   double* x0 = K0_ > 0 ? S : nullptr;
   if (K_ > 0) launch_vadu_partial(p_th_, R, nullptr, Xt, Xt, t, st, seg ? nullptr : x0, K0_);
-  if (seg) launch_vadu_head(seg_bt_, Xt, nullptr, Xt, t, st);
+  if (seg) SegSolve(false, Xt, nullptr, Xt, t, st);
   if (K0_ > 0) {
     if (seg) launch_vadu_partial(p_10_, nullptr, nullptr, Xt, Xt, t, st, x0, K0_);
     DenseApply(x0, Z, t, st, S);
@@ -544,9 +612,9 @@ void VaduPrecond::Record(const double* R, double* Z, double* Xt, int t, hipStrea
   if (seg) {
     if (K0_ > 0) {
       launch_vadu_partial(p_01_, Xt, dw_, Z, Z, t, st);
-      launch_vadu_head(seg_low_, Z, nullptr, Z, t, st);
+      SegSolve(true, Z, nullptr, Z, t, st);
     } else {
-      launch_vadu_head(seg_low_, Xt, dw_, Z, t, st);
+      SegSolve(true, Xt, dw_, Z, t, st);
     }
   }
   TailSolve(true, R, Xt, Z, t, st);
@@ -603,16 +671,16 @@ void VaduPrecond::TimeParts(const double* R, double* Z, double* Xt, int t, int r
   };
   part("tail_bt", [&] { TailSolve(false, R, Xt, Z, t, s_); });
   part("part_th", [&] { launch_vadu_partial(p_th_, R, nullptr, Xt, Xt, t, s_, seg ? nullptr : S, K0_); });
-  if (seg) part("seg_bt", [&] { launch_vadu_head(seg_bt_, Xt, nullptr, Xt, t, s_); });
+  if (seg) part("seg_bt", [&] { SegSolve(false, Xt, nullptr, Xt, t, s_); });
   if (K0_ > 0 && seg) part("part_10", [&] { launch_vadu_partial(p_10_, nullptr, nullptr, Xt, Xt, t, s_, S, K0_); });
   if (K0_ > 0) part("dense", [&] { DenseApply(S, Z, t, s_, S); });
   if (K0_ > 0 && seg) part("part_01", [&] { launch_vadu_partial(p_01_, Xt, dw_, Z, Z, t, s_); });
-  if (seg) part("seg_low", [&] { launch_vadu_head(seg_low_, Z, nullptr, Z, t, s_); });
+  if (seg) part("seg_low", [&] { SegSolve(true, Z, nullptr, Z, t, s_); });
   part("tail_low", [&] { TailSolve(true, R, Xt, Z, t, s_); });
   std::fprintf(stderr,
                "[precond parts t=%d] K0=%d K=%d passes bt=%d low=%d tail merged levels bt=%d low=%d (g=%d, %ld entries) "
                "launches=%d\n",
-               t, K0_, K_, seg_bt_.npass, seg_low_.npass, tail_levels_bt(), tail_levels_lower(), merge_g_, tail_entries_,
+               t, K0_, K_, seg_wave_ ? segw_bt_.npass : seg_bt_.npass, seg_wave_ ? segw_low_.npass : seg_low_.npass, tail_levels_bt(), tail_levels_lower(), merge_g_, tail_entries_,
                launches());
   HIP_CHECK(hipEventDestroy(a));
   HIP_CHECK(hipEventDestroy(b));

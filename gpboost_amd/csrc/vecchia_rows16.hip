@@ -38,6 +38,9 @@ constexpr int kD3 = 3;   // coordinate dimension bound (VecchiaRowsArgs.d <= 3)
 #ifndef GPB_ROWS16_BCG
 #define GPB_ROWS16_BCG 4
 #endif
+#ifndef GPB_ROWS16_FMAC
+#define GPB_ROWS16_FMAC 0
+#endif
 
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void cfence() { asm volatile("" ::: "memory"); }
@@ -53,6 +56,14 @@ template <int L>
 __device__ __forceinline__ double bcast16(double v) {   // lane L of each 16-lane row, to the whole row
   const long b = __builtin_amdgcn_mov_dpp(__builtin_bit_cast(long, v), 0x150 + L, 0xF, 0xF, true);
   return __builtin_bit_cast(double, b);
+}
+
+// acc += (src of lane L of the 16-lane row) * mul, one instruction
+template <int L>
+__device__ __forceinline__ void fmac_bcast16(double& acc, double src, double mul) {
+  asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+               : "+v"(acc)
+               : "v"(src), "v"(mul), "n"(L));
 }
 
 __device__ __forceinline__ double sum16(double v) {   // fixed-order sum over the 16-lane row
@@ -246,7 +257,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         f0 = own ? 0. : f0;
         dg0 = own ? piv : dg0;
       }
-#if GPB_ROWS16_BCG > 1
+#if GPB_ROWS16_FMAC
+      // each broadcast folded into its two FMAs: v_fmac_f64_dpp row_newbcast (gfx950 takes DPP on the
+      // 64-bit fmac; the compiler never folds a 64-bit DPP move into its uses), so a column costs two
+      // VALU ops instead of three and no move -> FMA dependency
+      const double nf0 = -f0, nf1 = -f1;
+      asm volatile("s_nop 1" ::: "memory");   // VALU write -> DPP read wait states (not visible inside asm)
+      sfor<j + 1, kK>([&](auto C) {
+        constexpr int c = decltype(C)::value;
+        const double& src = c >= 16 ? r1[j] : r0[j];
+        fmac_bcast16<c & 15>(r0[c], src, nf0);
+        fmac_bcast16<c & 15>(r1[c], src, nf1);
+      });
+#elif GPB_ROWS16_BCG > 1
       // GPB_ROWS16_BCG broadcasts in flight: a group's DPP moves issue before its FMAs (the compiler
       // otherwise reuses one temporary, a DPP -> FMA dependency per column)
       constexpr int BG = GPB_ROWS16_BCG;

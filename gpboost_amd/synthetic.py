@@ -108,6 +108,13 @@ def bench_bernoulli_y(coords: np.ndarray) -> np.ndarray:
     return (lcg_unif(n, 0.19341) < p).astype(np.float64)
 
 
+def bench_spatial_gaussian_y(coords: np.ndarray) -> np.ndarray:
+    """A Gaussian response with spatial structure: sin(2 pi x1) cos(2 pi x2) + 0.5 iid N(0,1)
+    (bench_gaussian_y), for latent-Gaussian fits whose optimum is not at a zero GP variance."""
+    f = np.sin(2 * np.pi * coords[:, 0]) * np.cos(2 * np.pi * coords[:, 1])
+    return f + 0.5 * bench_gaussian_y(coords.shape[0])
+
+
 def bench_covariates(n: int, p: int = 2) -> np.ndarray:
     """Linear regression covariates X (n x (p + 1), column-major-friendly): an intercept column and p
     LCG columns (c = 0.31, 0.57, ... exact arithmetic), shifted to mean ~0."""

@@ -366,7 +366,8 @@ int main(int argc, char** argv) {
     std::vector<double> xp((size_t)np * d);
     if (std::fread(xp.data(), 8, xp.size(), fp) != xp.size()) return 2;
     std::fclose(fp);
-    const bool pvar = get(args, "predict_var", "0") == "1";
+    const bool pcov = get(args, "predict_cov", "0") == "1";
+    const bool pvar = !pcov && get(args, "predict_var", "0") == "1";
     const bool presp = get(args, "predict_response", "0") == "1";
     const std::string ptype = get(args, "vecchia_pred_type", "");
     m->SetPredictionData(np, nullptr, nullptr, nullptr, xp.data(), nullptr, nullptr,
@@ -374,12 +375,13 @@ int main(int argc, char** argv) {
                          std::atoi(get(args, "num_neighbors_pred", "-1").c_str()),
                          std::atof(get(args, "cg_delta_conv_pred", "-1").c_str()),
                          std::atoi(get(args, "nsim_var_pred", "-1").c_str()), -1);
-    std::vector<double> out((size_t)2 * np, 0.);
-    m->Predict(trafo.data(), y.data(), np, out.data(), true, false, pvar, presp, nullptr, nullptr, nullptr,
+    std::vector<double> out((size_t)np + (pcov ? (size_t)np * np : (size_t)np), 0.);
+    m->Predict(trafo.data(), y.data(), np, out.data(), true, pcov, pvar, presp, nullptr, nullptr, nullptr,
                nullptr, nullptr, xp.data(), nullptr, false, fe_ptr, nullptr);
     std::printf("{\n\"n\": %d, \"d\": %d, \"np\": %d,\n", n, d, np);
     print_vec("mean", out.data(), np);
     if (pvar) print_vec("var", out.data() + np, np);
+    if (pcov) print_vec("cov", out.data() + np, np * np);
     std::printf("\"ok\": true\n}\n");
     return 0;
   }

@@ -177,6 +177,33 @@ def test_preconditioner_plans_agree(monkeypatch, dense_rows, head_rows, merge):
         np.testing.assert_allclose(b[1], a[1], rtol=1e-7, atol=1e-7 * np.abs(a[1]).max())
 
 
+@pytest.mark.parametrize("seg_form,tail_order", [("wave", "row"), ("block", "row"), ("wave", "level")])
+def test_segment_and_tail_forms_agree(monkeypatch, seg_form, tail_order):
+    """The LDS segment solved by one wave per column (SegWave, default) or by the 1024-thread
+    barrier form, and the merged tail launched in storage (Morton) order or in level order, against
+    the plain level schedule: the same algebra in other summation orders (~1e-10 at a tight CG
+    tolerance). The segment here holds long B^T rows (2 and 4 lanes per row in the wave form)."""
+    from gpboost_amd import synthetic
+    n = 8000
+    X = synthetic.bench_coords(n)
+    for lik in ("gaussian", "bernoulli_logit"):
+        y = synthetic.bench_gaussian_y(n) if lik == "gaussian" else synthetic.bench_bernoulli_y(X)
+        case = dict(likelihood=lik, cov_fct="exponential", shape=0.5, num_neighbors=30, aux=0.1)
+        out = {}
+        for key, (k0, k, g, form, order) in {"levels": ("0", "0", "1", "wave", "row"),
+                                             "plan": ("256", "6000", "4", seg_form, tail_order)}.items():
+            monkeypatch.setenv("GPBOOST_AMD_DENSE_ROWS", k0)
+            monkeypatch.setenv("GPBOOST_AMD_HEAD_ROWS", k)
+            monkeypatch.setenv("GPBOOST_AMD_TAIL_MERGE", g)
+            monkeypatch.setenv("GPBOOST_AMD_SEG_FORM", form)
+            monkeypatch.setenv("GPBOOST_AMD_TAIL_ORDER", order)
+            gm = _model(X, case, t=12, dc=1e-9)
+            out[key] = gm.neg_log_likelihood_and_grad([1.0, 0.1], y)
+        a, b = out["levels"], out["plan"]
+        assert abs(a[0] - b[0]) <= 1e-9 * abs(a[0]), (lik, a[0], b[0])
+        np.testing.assert_allclose(b[1], a[1], rtol=1e-7, atol=1e-7 * np.abs(a[1]).max())
+
+
 def test_latent_zero_response(monkeypatch):
     """y == 0 under the Gaussian latent model: the Newton right-hand side y / aux is zero, so its
     CG column (fused with the probes) must stop at u = 0 without iterating (CG_utils.cpp:42-45)

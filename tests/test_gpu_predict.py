@@ -88,3 +88,33 @@ def test_predict_errors():
     dense = GPModel(gp_coords=X[:500], cov_function="exponential", gp_approx="none")
     with pytest.raises(GPBoostError, match="Vecchia approximation"):
         dense.predict(y=y, gp_coords_pred=X[500:], cov_pars=[0.1, 1.0, 0.1])
+
+
+@pytest.mark.parametrize("name", ["cond_all_var", "cond_all_var_resp", "cond_all_cov", "cond_all_matern_var"])
+def test_predict_cond_all_matches_reference(name):
+    """vecchia_pred_type "order_obs_first_cond_all" (prediction points condition on the observed and
+    the earlier prediction points; Vecchia_utils.cpp:1634-2006 with CondObsOnly = false) against the
+    reference itself (tests/golden/golden_pred_types.json, make_golden_pred_types.py): means,
+    variances and the full predictive covariance at 1e-9."""
+    import json
+    import os
+    from gpboost_amd import GPModel, synthetic
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_pred_types.json")) as f:
+        case = json.load(f)[name]
+    sp = case["spec"]
+    X = synthetic.bench_coords(case["n"])
+    y = synthetic.bench_spatial_gaussian_y(X)
+    xp = synthetic.lcg_unif(case["npred"] * 2, 0.713).reshape(2, case["npred"]).T.copy()
+    gm = GPModel(gp_coords=X, cov_function=sp["cov_fct"], cov_fct_shape=float(sp["shape"]), gp_approx="vecchia",
+                 num_neighbors=sp["num_neighbors"], vecchia_ordering="random", seed=0)
+    gm.set_prediction_data(vecchia_pred_type="order_obs_first_cond_all", num_neighbors_pred=case["mp"])
+    want_cov = "cov" in case
+    pred = gm.predict(y=y, gp_coords_pred=xp, cov_pars=case["cov_pars"], predict_var=not want_cov,
+                      predict_cov_mat=want_cov, predict_response=case["response"])
+    mu = np.asarray(case["mean"])
+    np.testing.assert_allclose(pred["mu"], mu, rtol=1e-9, atol=1e-9 * np.abs(mu).max())
+    if want_cov:
+        c = np.asarray(case["cov"]).reshape(case["npred"], case["npred"])
+        np.testing.assert_allclose(pred["cov"], c, rtol=1e-9, atol=1e-9 * np.abs(c).max())
+    else:
+        np.testing.assert_allclose(pred["var"], case["var"], rtol=1e-9)
