@@ -486,6 +486,87 @@ def dense_leg(steps: int, cpu: bool) -> dict:
     return leg
 
 
+FITC_N, FITC_M, FITC_CPU_N = 100_000, 500, 20_000
+
+
+def fitc_flops(n: int, m: int) -> float:
+    """Algorithmic fp64 flops of one FITC nll + gradient evaluation (fitc_kernels.hip): the GEMMs
+    V = L^-1 K_mn (triangular, m^2 n), W = K_mn K_d^T (2 m^2 n), A = L^-T V (m^2 n), G^T = W^-1 K_mn
+    (2 m^2 n), M = dK_mm A (2 m^2 n); the m^3 factorizations and O(n m) passes are not counted."""
+    return 8.0 * m * m * n
+
+
+def fitc_leg(steps: int, cpu: bool) -> dict:
+    """FITC (gp_approx='fitc', 500 kmeans++ inducing points) on the headline's
+    n=100k coordinates and spatial response, the L-BFGS unit (nll + gradient, sigma2 profiled)."""
+    import numpy as np
+
+    from gpboost_amd import GPModel, synthetic
+    X = synthetic.bench_coords(FITC_N)
+    Y = synthetic.bench_spatial_gaussian_y(X)
+    t0 = time.perf_counter()
+    gm = GPModel(gp_coords=X, cov_function="exponential", gp_approx="fitc", num_ind_points=FITC_M, seed=0)
+    t_construct = time.perf_counter() - t0
+    gm.neg_log_likelihood_and_grad(THETA, Y, profile_sigma2=True)   # warm-up
+    gm.last_kernel_ms()
+    ts, kms = [], []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        nll, g, _ = gm.neg_log_likelihood_and_grad(THETA, None, profile_sigma2=True)
+        ts.append(time.perf_counter() - t0)
+        kms.append(gm.last_kernel_ms()[1])
+    t = float(np.median(ts))
+    fl = fitc_flops(FITC_N, FITC_M)
+    kt = float(np.median(kms)) * 1e-3
+    leg = {"metric": "FITC nll + grad evals/sec, n=100k, m=500", "value": 1.0 / t, "unit": "evals/s", "steps": steps,
+           "ms_per_step": t * 1e3,
+           "config": {"workload": "fitc_gaussian_lbfgs_unit", "n": FITC_N, "num_ind_points": FITC_M,
+                      "ind_points_selection": "kmeans++", "cov_function": "exponential", "theta": THETA,
+                      "construction_s": round(t_construct, 3), "nll": nll, "grad": [float(x) for x in g]},
+           "roofline": {"bound": "mfma", "achieved": fl / kt / 1e12, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": fl / kt / 1e12 / FP64_PEAK_TFLOPS, "traffic": None, "device_ms": kt * 1e3,
+                        "kernel": "whole device evaluation (gemm_f64_big_kernel / gemm_f64_splitk_kernel GEMMs, "
+                                  "fitc column kernels)",
+                        "algorithmic_flops_per_eval": fl}}
+    del gm
+    if cpu:
+        leg["cpu_baseline"] = fitc_cpu_baseline()
+    return leg
+
+
+def fitc_cpu_baseline() -> dict | None:
+    """The reference's FITC path (oracle/_ref/ref_harness gp_approx=fitc) on this host, bounded sample
+    at n=20000 (m=500); `value_scaled_n100k` scales it by 20000/100000 (the unit is n m^2-bound)."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(harness):
+        return None
+    import numpy as np
+
+    from gpboost_amd import synthetic
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", str(os.cpu_count() or 1))), 16))
+    X = synthetic.bench_coords(FITC_CPU_N)
+    Y = synthetic.bench_spatial_gaussian_y(X)
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(np.array([X.shape[0], X.shape[1]], dtype=np.int32).tobytes())
+        f.write(np.ascontiguousarray(X.T).tobytes())
+        f.write(np.ascontiguousarray(Y).tobytes())
+        path = f.name
+    try:
+        out = subprocess.run([harness, path, "cov_fct=exponential", "gp_approx=fitc", f"num_ind_points={FITC_M}",
+                              "mode=lbfgs", "reps=1", "cov_pars=" + ",".join(map(str, THETA))], capture_output=True,
+                             text=True, timeout=600, env=dict(os.environ, OMP_NUM_THREADS=str(threads)), check=True)
+        r = json.loads(out.stdout)
+        t = r["median_time"]
+        return {"value": 1.0 / t, "unit": "evals/s", "cores": threads, "kind": "reference",
+                "sample": f"1 FITC L-BFGS-unit eval at n={FITC_CPU_N}, m={FITC_M} ({t:.2f} s; kmeans++ not timed)",
+                "value_scaled_n100k": (1.0 / t) * FITC_CPU_N / FITC_N}
+    except Exception as e:  # noqa: BLE001
+        sys.stderr.write(f"reference FITC CPU baseline failed: {e}\n")
+        return None
+    finally:
+        os.unlink(path)
+
+
 def dense_cpu_baseline() -> dict | None:
     """The reference's dense path (oracle/_ref/ref_harness) on this host, bounded sample at
     n=4000; `value_scaled_n20000` scales it by (4000/20000)^3 (the unit is n^3-bound)."""
@@ -539,6 +620,34 @@ def join_ranks(gm, rank: int, world: int, dist) -> None:
     gm.set_distributed(rank, world, obj[0])
 
 
+def row_shard_leg(gm, reps: int = 15) -> dict:
+    """Single-GPU rehearsal of the N-rank row sharding of the headline evaluation: the first and the
+    last rank's row range at N = 2, 4, 8 (the shard GPB_EvalVecchiaPartials evaluates, the same launch
+    path a rank takes) with its row-kernel HIP-event time and the host wall time of the partial
+    evaluation. The N-rank evaluation costs about max(wall over ranks) + one 6-double all-reduce."""
+    import numpy as np
+    n = N_DATA
+    out = {}
+    for nr in (2, 4, 8):
+        base, rem = divmod(n, nr)   # the library's split (re_model.cpp SetDistributed)
+        ranges = {"first": (0, base + (1 if rem else 0)), "last": (n - base, n)}
+        res = {}
+        for name, (r0, r1) in ranges.items():
+            gm.vecchia_partials(THETA, r0, r1)
+            ks, ws = [], []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                gm.vecchia_partials(THETA, r0, r1)
+                ws.append(time.perf_counter() - t0)
+                ks.append(gm.last_kernel_ms()[0])
+            res[name] = {"rows": [r0, r1], "kernel_ms": float(np.median(ks)), "wall_ms": float(np.median(ws)) * 1e3}
+        res["projected_evals_per_s"] = 1e3 / max(v["wall_ms"] for v in res.values())
+        out[f"n{nr}"] = res
+    out["note"] = ("row ranges of an N-rank run evaluated on one GPU; projection excludes the all-reduce "
+                   "of 6 doubles over RCCL")
+    return out
+
+
 def latent_leg_sharded(X, Y, steps: int, rank: int, world: int, dist) -> dict | None:
     """The latent leg at N > 1: probe columns sharded over the ranks (SURVEY.md §8e Option A,
     RCCL inside the library: one all-reduce of 1 double per PCG iteration + the per-probe terms
@@ -588,9 +697,14 @@ def main():
     ap.add_argument("--no-fit", action="store_true", help="skip the secondary GPB_OptimCovPar (fit) leg")
     ap.add_argument("--no-grouped", action="store_true", help="skip the grouped random effects (config 4) leg")
     ap.add_argument("--only-grouped", action="store_true", help="run only the grouped leg (prints its JSON)")
+    ap.add_argument("--no-fitc", action="store_true", help="skip the secondary FITC (§8 row f4) leg")
+    ap.add_argument("--only-fitc", action="store_true", help="run only the FITC leg (prints its JSON)")
     args = ap.parse_args()
     if args.only_grouped:
         print(json.dumps(grouped_leg(args.steps, not args.no_cpu_baseline)))
+        return
+    if args.only_fitc:
+        print(json.dumps(fitc_leg(args.steps, not args.no_cpu_baseline)))
         return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -706,12 +820,16 @@ def main():
                               "predictions_per_s": PRED_N / tp, "mean_of_mu": float(np.mean(pr["mu"])),
                               "note": "end to end: neighbour search among the 100k observed points (GPU), "
                                       "prediction rows (row kernel, 64-lane groups), mean/variance"}
+    if world == 1:
+        line["row_shards"] = row_shard_leg(gm)
     if world == 1 and not args.no_fit:
         line["fit"] = fit_leg(X, Y, not args.no_cpu_baseline)
     if world == 1 and not args.no_dense:
         line["dense"] = dense_leg(3, not args.no_cpu_baseline)
     if world == 1 and not args.no_grouped:
         line["grouped"] = grouped_leg(5, not args.no_cpu_baseline)
+    if world == 1 and not args.no_fitc:
+        line["fitc"] = fitc_leg(5, not args.no_cpu_baseline)
     if world == 1 and not args.no_latent:
         del gm
         line["latent_iterative"] = latent_leg(X, Y, args.latent_steps, not args.no_cpu_baseline)

@@ -497,6 +497,14 @@ class GPModel:
         self.model_fitted = True
         return self
 
+    def inducing_points(self):
+        """The inducing points of a gp_approx = "fitc" model, (m, d) (GPB_GetInducingPoints)."""
+        m = ctypes.c_int32(0)
+        self._call(lib().GPB_GetInducingPoints(self.handle, ctypes.byref(m), None))
+        out = np.zeros((m.value, self.dim_coords))
+        self._call(lib().GPB_GetInducingPoints(self.handle, ctypes.byref(m), _dp(out)))
+        return out
+
     def last_iteration_info(self):
         """[newton iterations, CG iterations, Lanczos steps, log|Sigma W + I|] of the last latent evaluation."""
         out = np.zeros(4)

@@ -131,8 +131,8 @@ int GPB_CreateREModel(int32_t num_data, const int32_t* cluster_ids_data, const c
                       REModelHandle* out) {
   API_BEGIN();
   (void)re_group_rand_coef_data; (void)ind_effect_group_rand_coef; (void)drop_intercept_group_rand_effect;
-  (void)cov_fct_taper_range; (void)cov_fct_taper_shape; (void)num_ind_points; (void)cover_tree_radius;
-  (void)ind_points_selection; (void)likelihood_additional_param; (void)num_parallel_threads; (void)GPU_use;
+  (void)cov_fct_taper_range; (void)cov_fct_taper_shape;
+  (void)likelihood_additional_param; (void)num_parallel_threads; (void)GPU_use;
   (void)weights; (void)likelihood_learning_rate;
   if (out == nullptr) gpb_amd::Fatal("'out' is NULL");
   if (num_re_group_rand_coef > 0 || num_gp_rand_coef > 0 || gp_rand_coef_data != nullptr)
@@ -173,6 +173,9 @@ int GPB_CreateREModel(int32_t num_data, const int32_t* cluster_ids_data, const c
   cfg.likelihood = str_or(likelihood, "gaussian");
   cfg.matrix_inversion_method = str_or(matrix_inversion_method, "default");
   cfg.seed = seed;
+  cfg.num_ind_points = num_ind_points;
+  cfg.cover_tree_radius = cover_tree_radius;
+  cfg.ind_points_selection = str_or(ind_points_selection, "kmeans++");
   *out = new REModelAMD(cfg, gp_coords_data);
   API_END();
 }
@@ -469,6 +472,16 @@ int GPB_OptimCovParBoosting(REModelHandle handle, const double* y_data, const do
     gpb_amd::Fatal("the GPBoost-algorithm covariance update is not supported for grouped random effects models by "
                    "gpboost_amd");
   model(handle)->OptimCovPar(y_data, fixed_effects, called_in_GPBoost_algorithm, reuse_learning_rates_from_previous_call);
+  API_END();
+}
+
+int GPB_GetInducingPoints(REModelHandle handle, int32_t* num_ind_points, double* ind_points) {
+  API_BEGIN();
+  if (as_grouped(handle) != nullptr) gpb_amd::Fatal("model does not use gp_approx = 'fitc'");
+  const std::vector<double>& Z = model(handle)->InducingPoints();
+  const int d = model(handle)->config().d;
+  if (num_ind_points != nullptr) *num_ind_points = (int32_t)(Z.size() / d);
+  if (ind_points != nullptr) std::copy(Z.begin(), Z.end(), ind_points);
   API_END();
 }
 

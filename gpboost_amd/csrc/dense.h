@@ -55,6 +55,22 @@ void gemm_f64(hipStream_t s, int M, int N, int K, double alpha, const double* A,
               int ldb, int transB, double beta, double* C, int ldc, int lower_out = 0, int a_lower = 0,
               int a_upper = 0, int b_lower = 0);
 
+// Split-K product: chunk z of K (a multiple of 16 long, as many chunks as give ~target_blocks
+// workgroups, at most max_chunks) writes op(A) op(B) over its K range to C + z * cstride (M x N, ldc). Returns the
+// number of chunks (the caller sums the partial products in chunk order). No triangle masks.
+int gemm_f64_splitk(hipStream_t s, int M, int N, int K, const double* A, int lda, int transA, const double* B, int ldb,
+                    int transB, double* C, int ldc, long cstride, int target_blocks, int max_chunks);
+
+// In-place two-level Cholesky of the lower triangle of the n x n matrix A (leading dimension ld, a
+// multiple of 64): L overwrites A's lower triangle, the inverses of its 64 x 64 diagonal blocks go to
+// W's diagonal blocks; info counts non-positive pivots (DenseSolver's factorization, also FITC's).
+void chol_lower(hipStream_t s, double* A, double* W, int n, int ld, int* info);
+// W[a:b, a:b] = L[a:b, a:b]^-1 (lower) from chol_lower's diagonal-block inverses; X: scratch of
+// >= ld x (ld / 2 + 64) doubles.
+void trtri_lower(hipStream_t s, const double* L, double* W, double* X, int a, int b, int ld);
+// out[0] = 2 sum_i log L_ii (one block, fixed order)
+void launch_logdet_chol(hipStream_t s, const double* L, int ld, int n, double* out);
+
 // host helper shared by all paths (re_model.cpp)
 void combine_partials(const double* s, int n, double sigma2_in, int profile, double* nll, double* grad,
                       double* sigma2_out);

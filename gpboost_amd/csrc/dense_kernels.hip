@@ -237,6 +237,18 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))
 
 __global__ void __launch_bounds__(256) gemm_f64_pipe_kernel(GemmArgs g) { gemm_tile_body<64>(g); }
 
+// Split-K form for long-K products with few output tiles (FITC's m x m Woodbury Gram over n
+// observations): grid.z = K chunk; chunk z writes its partial product to C + z * cstride.
+__global__ void __launch_bounds__(256) gemm_f64_splitk_kernel(GemmArgs g, int kchunk, long cstride) {
+  GemmArgs h = g;
+  const int k0 = blockIdx.z * kchunk;
+  h.K = min(g.K - k0, kchunk);
+  h.A = g.transA ? g.A + k0 : g.A + (size_t)k0 * g.lda;
+  h.B = g.transB ? g.B + (size_t)k0 * g.ldb : g.B + k0;
+  h.C = g.C + (size_t)blockIdx.z * cstride;
+  gemm_tile_body<64>(h);
+}
+
 // Lower triangle (i >= j) of Psi = Sigma + I, tile-parallel, upper tiles skipped.
 template <int COV>
 __global__ void __launch_bounds__(256) build_psi_kernel(const double* __restrict__ X, int n, int d, int ld,
@@ -635,6 +647,22 @@ void gemm_f64(hipStream_t s, int M, int N, int K, double alpha, const double* A,
   gemm(s, M, N, K, alpha, A, lda, transA, B, ldb, transB, beta, C, ldc, lower_out, a_lower, a_upper, b_lower);
 }
 
+int gemm_f64_splitk(hipStream_t s, int M, int N, int K, const double* A, int lda, int transA, const double* B, int ldb,
+                    int transB, double* C, int ldc, long cstride, int target_blocks, int max_chunks) {
+  if (M <= 0 || N <= 0 || K <= 0) return 0;
+  const long tiles = (long)((M + TN - 1) / TN) * ((N + TN - 1) / TN);
+  int chunks = (int)std::max<long>(1, std::min<long>((target_blocks + tiles - 1) / tiles, (K + 255) / 256));
+  chunks = std::max(1, std::min(chunks, max_chunks));
+  int kchunk = (K + chunks - 1) / chunks;
+  kchunk = (kchunk + TKB - 1) / TKB * TKB;
+  chunks = (K + kchunk - 1) / kchunk;
+  GemmArgs g{M, N, K, 1., 0., A, lda, transA, B, ldb, transB, C, ldc, 0, 0, 0, 0};
+  dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM, chunks);
+  hipLaunchKernelGGL(gemm_f64_splitk_kernel, grid, dim3(256), 0, s, g, kchunk, cstride);
+  HIP_CHECK(hipGetLastError());
+  return chunks;
+}
+
 DenseSolver::DenseSolver(int n, int d, const double* d_X, hipStream_t stream)
     : n_(n), d_(d), ld_(((n + 63) / 64) * 64), d_X_(d_X), stream_(stream) {
   const size_t nn = (size_t)ld_ * (size_t)ld_;
@@ -660,11 +688,8 @@ DenseSolver::~DenseSolver() {
   if (s_rest_) (void)hipStreamDestroy(s_rest_);
 }
 
-void DenseSolver::Potrf() {
+void chol_lower(hipStream_t s, double* A, double* W, int n, int ld, int* info) {
   // two-level right-looking Cholesky: 256-wide outer panels, 64-wide inner steps
-  const int n = n_, ld = ld_;
-  double* A = A_.get();
-  double* W = W_.get();
   constexpr int NBO = 256, NBI = 64;
   for (int J0 = 0; J0 < n; J0 += NBO) {
     const int jb = std::min(NBO, n - J0);
@@ -672,30 +697,51 @@ void DenseSolver::Potrf() {
       const int ib = std::min(NBI, J0 + jb - j0);
       static const bool diag_old = std::getenv("GPBOOST_AMD_DIAG_OLD") != nullptr;   // A/B: 256-thread form
       if (diag_old)
-        hipLaunchKernelGGL(potrf_diag_kernel, dim3(1), dim3(256), 0, stream_, A, ld, j0, ib, W, ld, info_.get());
+        hipLaunchKernelGGL(potrf_diag_kernel, dim3(1), dim3(256), 0, s, A, ld, j0, ib, W, ld, info);
       else
-        hipLaunchKernelGGL(potrf_diag_wave_kernel, dim3(1), dim3(64), 0, stream_, A, ld, j0, ib, W, ld, info_.get());
+        hipLaunchKernelGGL(potrf_diag_wave_kernel, dim3(1), dim3(64), 0, s, A, ld, j0, ib, W, ld, info);
       HIP_CHECK(hipGetLastError());
       const int r0 = j0 + ib;
       if (r0 < n) {
         // L21 = A21 * L11^-T  (in place: each 64-row tile reads its whole K = ib range first)
-        gemm(stream_, n - r0, ib, ib, 1., A + r0 + (size_t)j0 * ld, ld, 0, W + j0 + (size_t)j0 * ld, ld, 1, 0.,
+        gemm(s, n - r0, ib, ib, 1., A + r0 + (size_t)j0 * ld, ld, 0, W + j0 + (size_t)j0 * ld, ld, 1, 0.,
              A + r0 + (size_t)j0 * ld, ld, 0, 0, 0, 0);
       }
       if (r0 < J0 + jb) {
         // remaining panel columns: A[r0:n, r0:J0+jb] -= L[r0:n, j0:r0] L[r0:J0+jb, j0:r0]^T
-        gemm(stream_, n - r0, J0 + jb - r0, ib, -1., A + r0 + (size_t)j0 * ld, ld, 0, A + r0 + (size_t)j0 * ld, ld, 1,
+        gemm(s, n - r0, J0 + jb - r0, ib, -1., A + r0 + (size_t)j0 * ld, ld, 0, A + r0 + (size_t)j0 * ld, ld, 1,
              1., A + r0 + (size_t)r0 * ld, ld, 1, 0, 0, 0);
       }
     }
     const int t0 = J0 + jb;
     if (t0 < n) {
       // trailing SYRK: A[t0:n, t0:n] -= L[t0:n, J0:t0] L[t0:n, J0:t0]^T  (lower tiles only)
-      gemm(stream_, n - t0, n - t0, jb, -1., A + t0 + (size_t)J0 * ld, ld, 0, A + t0 + (size_t)J0 * ld, ld, 1, 1.,
+      gemm(s, n - t0, n - t0, jb, -1., A + t0 + (size_t)J0 * ld, ld, 0, A + t0 + (size_t)J0 * ld, ld, 1, 1.,
            A + t0 + (size_t)t0 * ld, ld, 1, 0, 0, 0);
     }
   }
 }
+
+void trtri_lower(hipStream_t s, const double* L, double* W, double* X, int a, int b, int ld) {
+  // W[a:b, a:b] = L[a:b, a:b]^-1 (lower); diagonal 64-blocks were inverted by chol_lower.
+  if (b - a <= 64) return;
+  const int half = ((b - a) / 2 + 63) / 64 * 64;
+  const int mid = a + half;
+  trtri_lower(s, L, W, X, a, mid, ld);
+  trtri_lower(s, L, W, X, mid, b, ld);
+  const int m2 = b - mid, m1 = mid - a;
+  // X = L21 * W11   (W11 lower)
+  gemm(s, m2, m1, m1, 1., L + mid + (size_t)a * ld, ld, 0, W + a + (size_t)a * ld, ld, 0, 0., X, ld, 0, 0, 0, 1);
+  // W21 = -W22 * X  (W22 lower)
+  gemm(s, m2, m1, m2, -1., W + mid + (size_t)mid * ld, ld, 0, X, ld, 0, 0., W + mid + (size_t)a * ld, ld, 0, 1, 0, 0);
+}
+
+void launch_logdet_chol(hipStream_t s, const double* L, int ld, int n, double* out) {
+  hipLaunchKernelGGL(logdet_kernel, dim3(1), dim3(256), 0, s, L, ld, n, out);
+  HIP_CHECK(hipGetLastError());
+}
+
+void DenseSolver::Potrf() { chol_lower(stream_, A_.get(), W_.get(), n_, ld_, info_.get()); }
 
 // The same factorization with one panel of lookahead: after panel J's inner steps, the trailing
 // update is split into the next panel's columns (on the chain stream, immediately) and the rest
@@ -757,24 +803,7 @@ void DenseSolver::PotrfLookahead() {
   HIP_CHECK(hipStreamWaitEvent(stream_, ev_rest, 0));
 }
 
-void DenseSolver::Trtri(int a, int b) {
-  // W[a:b, a:b] = L[a:b, a:b]^-1 (lower); diagonal 64-blocks were inverted by potrf_diag.
-  if (b - a <= 64) return;
-  const int half = ((b - a) / 2 + 63) / 64 * 64;
-  const int mid = a + half;
-  Trtri(a, mid);
-  Trtri(mid, b);
-  const int ld = ld_;
-  const double* L = A_.get();
-  double* W = W_.get();
-  double* X = T_.get();
-  const int m2 = b - mid, m1 = mid - a;
-  // X = L21 * W11   (W11 lower)
-  gemm(stream_, m2, m1, m1, 1., L + mid + (size_t)a * ld, ld, 0, W + a + (size_t)a * ld, ld, 0, 0., X, ld, 0, 0, 0, 1);
-  // W21 = -W22 * X  (W22 lower)
-  gemm(stream_, m2, m1, m2, -1., W + mid + (size_t)mid * ld, ld, 0, X, ld, 0, 0., W + mid + (size_t)a * ld, ld, 0, 1,
-       0, 0);
-}
+void DenseSolver::Trtri(int a, int b) { trtri_lower(stream_, A_.get(), W_.get(), T_.get(), a, b, ld_); }
 
 void DenseSolver::Eval(int cov_type, double var, double phi, const double* d_y, bool want_grad, double* sums,
                        double* kernel_ms) {

@@ -1,0 +1,753 @@
+// FITC approximation (gp_approx = "fitc", Gaussian likelihood) on gfx950: inducing-point selection
+// and the negative log-likelihood + gradient (fitc.h gives the model and the reference lines).
+//
+// One evaluation (m inducing points, n observations, every m x n matrix column-major, ld = ldm):
+//   K_mn, K_mm, K_mm,s, dK_mm            build kernels (coordinates -> covariances)
+//   L = chol(K_mm,s), L^-1                dense path POTRF / TRTRI (chol_lower / trtri_lower)
+//   V = L^-1 K_mn                         MFMA GEMM (m^2 n)
+//   d, K_d = K_mn diag(1/d), y / d        one wave per observation
+//   W = K_mn K_d^T + K_mm,s               split-K MFMA GEMM (m^2 n), fixed-order partial sum
+//   chol(W), W^-1 = Lw^-T Lw^-1           POTRF / TRTRI / GEMM (m^3)
+//   y_aux = (y - K_nm W^-1 K_mn y/d) / d  two matrix-vector passes
+// gradient (sigma1^2 and range, log scale):
+//   A = K_mm,s^-1 K_mn = L^-T V, G^T = W^-1 K_mn, M = dK_mm A    three MFMA GEMMs (3 m^2 n)
+//   a = A y_aux; one fused pass per observation (range derivative of K_mn recomputed from the
+//   coordinates) for the diagonal derivative and the Woodbury traces; m x m traces.
+// Algorithmic HBM traffic per gradient evaluation is dominated by the m x n matrices (about 12
+// passes of 8 m n bytes); the GEMMs put it at the fp64 MFMA roofline for m >= ~200.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <random>
+
+#include "cov.h"
+#include "dense.h"
+#include "fitc.h"
+#include "kernels.h"
+
+namespace gpb_amd {
+namespace {
+
+constexpr double kJitterMult = 1. + 1e-6;   // JITTER_MULT_IP_FITC_FSA (utils.h:39)
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ double block4_sum(double v, double* red) {
+  // v: wave-uniform value of each of the 4 waves; fixed order ((w0 + w1) + (w2 + w3))
+  const int w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) red[w] = v;
+  __syncthreads();
+  const double s = (red[0] + red[1]) + (red[2] + red[3]);
+  __syncthreads();
+  return s;
+}
+
+template <int COV>
+__global__ void __launch_bounds__(256) fitc_kmn_kernel(const double* __restrict__ X, const double* __restrict__ Z, int n,
+                                                       int m, int d, int ldm, double var, double phi,
+                                                       double* __restrict__ Kmn) {
+  const int j = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int i = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= n || j >= m) return;
+  double s = 0.;
+  for (int q = 0; q < d; ++q) {
+    const double t = X[(size_t)i * d + q] - Z[(size_t)j * d + q];
+    s += t * t;
+  }
+  double c, dc;
+  cov_dcov<COV>(sqrt(s), var, phi, c, dc);
+  Kmn[(size_t)j + (size_t)i * ldm] = c;
+}
+
+// K_mm (un-jittered), K_mm,s (diagonal times the jitter multiplier) and dK_mm / dlog(range), full
+template <int COV>
+__global__ void __launch_bounds__(256) fitc_kmm_kernel(const double* __restrict__ Z, int m, int d, int ldm, double var,
+                                                       double phi, double* __restrict__ Kmm, double* __restrict__ Ks,
+                                                       double* __restrict__ dK) {
+  const int j = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int k = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (j >= m || k >= m) return;
+  double c, dc;
+  if (j == k) {
+    c = var;
+    dc = 0.;
+  } else {
+    double s = 0.;
+    for (int q = 0; q < d; ++q) {
+      const double t = Z[(size_t)j * d + q] - Z[(size_t)k * d + q];
+      s += t * t;
+    }
+    cov_dcov<COV>(sqrt(s), var, phi, c, dc);
+  }
+  const size_t e = (size_t)j + (size_t)k * ldm;
+  Kmm[e] = c;
+  Ks[e] = j == k ? c * kJitterMult : c;
+  dK[e] = dc;
+}
+
+// d_i = (1 + sigma1^2 jitter) - |V[:, i]|^2 (re_model_template.h:7358-7377), K_d = K_mn diag(1/d),
+// Dy = y / d, block partial of sum log d. One wave per observation.
+__global__ void __launch_bounds__(256) fitc_diag_kernel(const double* __restrict__ V, const double* __restrict__ Kmn,
+                                                        const double* __restrict__ y, int n, int m, int ldm, double dvar,
+                                                        double* __restrict__ dvec, double* __restrict__ Kd,
+                                                        double* __restrict__ Dy, double* __restrict__ part) {
+  __shared__ double red[4];
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  double s = 0.;
+  if (i < n)
+    for (int j = lane; j < m; j += 64) {
+      const double v = V[(size_t)j + (size_t)i * ldm];
+      s += v * v;
+    }
+  s = wave_sum(s);
+  double lg = 0.;
+  if (i < n) {
+    const double di = dvar - s;
+    const double inv = 1. / di;
+    for (int j = lane; j < m; j += 64) Kd[(size_t)j + (size_t)i * ldm] = Kmn[(size_t)j + (size_t)i * ldm] * inv;
+    if (lane == 0) {
+      dvec[i] = di;
+      Dy[i] = inv * y[i];
+    }
+    lg = log(di);
+  }
+  const double t = block4_sum(lg, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = t;
+}
+
+// W = sum_z P_z + K_mm,s over the m x m entries (split-K partials in chunk order)
+__global__ void __launch_bounds__(256) fitc_wsum_kernel(const double* __restrict__ P, int chunks, long stride, int m,
+                                                        int ldm, const double* __restrict__ Ks, double* __restrict__ W) {
+  const int j = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int k = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (j >= m || k >= m) return;
+  const size_t e = (size_t)j + (size_t)k * ldm;
+  double s = P[e];
+  for (int z = 1; z < chunks; ++z) s += P[(size_t)z * stride + e];
+  W[e] = s + Ks[e];
+}
+
+// out_part[b][j] = sum_{i in chunk b} M[j, i] x_i (M m x n, ld ldm)
+__global__ void __launch_bounds__(256) fitc_gemv_part_kernel(const double* __restrict__ M, const double* __restrict__ x,
+                                                             int n, int m, int ldm, int chunk,
+                                                             double* __restrict__ part) {
+  const int i0 = blockIdx.x * chunk, i1 = min(n, i0 + chunk);
+  for (int j = threadIdx.x; j < m; j += 256) {
+    double acc = 0.;
+    for (int i = i0; i < i1; ++i) acc += M[(size_t)j + (size_t)i * ldm] * x[i];
+    part[(size_t)blockIdx.x * ldm + j] = acc;
+  }
+}
+
+__global__ void __launch_bounds__(256) fitc_gemv_reduce_kernel(const double* __restrict__ part, int nb, int m, int ldm,
+                                                               double* __restrict__ out) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= m) return;
+  double s = 0.;
+  for (int b = 0; b < nb; ++b) s += part[(size_t)b * ldm + j];
+  out[j] = s;
+}
+
+// out = S x for a full m x m S
+__global__ void __launch_bounds__(256) fitc_symv_kernel(const double* __restrict__ S, const double* __restrict__ x,
+                                                        int m, int ldm, double* __restrict__ out) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= m) return;
+  double s = 0.;
+  for (int k = 0; k < m; ++k) s += S[(size_t)j + (size_t)k * ldm] * x[k];
+  out[j] = s;
+}
+
+// y_aux_i = y_i / d_i - (K_nm w)_i / d_i (re_model_template.h:8902-8907), block partial of y^T y_aux
+__global__ void __launch_bounds__(256) fitc_yaux_kernel(const double* __restrict__ Kmn, const double* __restrict__ w,
+                                                        const double* __restrict__ y, const double* __restrict__ Dy,
+                                                        const double* __restrict__ dvec, int n, int m, int ldm,
+                                                        double* __restrict__ yaux, double* __restrict__ part) {
+  __shared__ double red[4];
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  double t = 0.;
+  if (i < n)
+    for (int j = lane; j < m; j += 64) t += Kmn[(size_t)j + (size_t)i * ldm] * w[j];
+  t = wave_sum(t);
+  double q = 0.;
+  if (i < n) {
+    const double ya = Dy[i] - t / dvec[i];
+    if (lane == 0) yaux[i] = ya;
+    q = y[i] * ya;
+  }
+  const double s = block4_sum(q, red);
+  if (threadIdx.x == 0) part[blockIdx.x] = s;
+}
+
+// Per-observation gradient terms (re_model_template.h:2046-2231, fitc branch) for the marginal
+// variance (k = v, dK_mn = K_mn, dK_mm = K_mm) and the range (k = r, dK_mn recomputed here,
+// M = dK_mm A from the GEMM); with A = K_mm,s^-1 K_mn, G^T = W^-1 K_mn, a = A y_aux:
+//   dd_k = dvar_k - 2 sum_j A_ji dK_ji + sum_j A_ji (dK_mm A)_ji      (FITC_Diag_grad)
+//   s2_k += dd_k / d_i + 2 sum_j G^T_ji dK_ji / d_i - dd_k f_i / d_i^2,  f_i = sum_j G^T_ji K_ji
+//   s1_k += -y_aux_i sum_j dK_ji a_j - 1/2 dd_k y_aux_i^2
+// For k = v, dK_mm A = K_mn - delta A with delta = sigma1^2 (jitter - 1) (K_mm = K_mm,s - delta I).
+template <int COV>
+__global__ void __launch_bounds__(256) fitc_grad_kernel(const double* __restrict__ X, const double* __restrict__ Z, int n,
+                                                        int m, int d, int ldm, double var, double phi, double delta,
+                                                        const double* __restrict__ Kmn, const double* __restrict__ A,
+                                                        const double* __restrict__ Gt, const double* __restrict__ Mr,
+                                                        const double* __restrict__ a, const double* __restrict__ dvec,
+                                                        const double* __restrict__ yaux, double* __restrict__ part) {
+  __shared__ double red[4];
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  double c1v = 0., sa2 = 0., gv = 0., f = 0., c1r = 0., c2r = 0., er = 0., gr = 0.;
+  if (i < n) {
+    double xi[3] = {0., 0., 0.};
+    for (int q = 0; q < d; ++q) xi[q] = X[(size_t)i * d + q];
+    for (int j = lane; j < m; j += 64) {
+      const size_t e = (size_t)j + (size_t)i * ldm;
+      const double k = Kmn[e], av = A[e], gt = Gt[e], mr = Mr[e], aj = a[j];
+      double s = 0.;
+      for (int q = 0; q < d; ++q) {
+        const double t = xi[q] - Z[(size_t)j * d + q];
+        s += t * t;
+      }
+      double c, dk;
+      cov_dcov<COV>(sqrt(s), var, phi, c, dk);
+      c1v += av * k;
+      sa2 += av * av;
+      gv += k * aj;
+      f += gt * k;
+      c1r += av * dk;
+      c2r += av * mr;
+      er += gt * dk;
+      gr += dk * aj;
+    }
+  }
+  c1v = wave_sum(c1v);
+  sa2 = wave_sum(sa2);
+  gv = wave_sum(gv);
+  f = wave_sum(f);
+  c1r = wave_sum(c1r);
+  c2r = wave_sum(c2r);
+  er = wave_sum(er);
+  gr = wave_sum(gr);
+  double s1v = 0., s1r = 0., s2v = 0., s2r = 0.;
+  if (i < n) {
+    const double di = dvec[i], inv = 1. / di, ya = yaux[i];
+    const double ddv = var - 2. * c1v + (c1v - delta * sa2);
+    const double ddr = -2. * c1r + c2r;
+    s2v = ddv * inv + 2. * f * inv - ddv * f * inv * inv;
+    s2r = ddr * inv + 2. * er * inv - ddr * f * inv * inv;
+    s1v = -ya * gv - 0.5 * ddv * ya * ya;
+    s1r = -ya * gr - 0.5 * ddr * ya * ya;
+  }
+  s1v = block4_sum(s1v, red);
+  s1r = block4_sum(s1r, red);
+  s2v = block4_sum(s2v, red);
+  s2r = block4_sum(s2r, red);
+  if (threadIdx.x == 0) {
+    double* p = part + (size_t)blockIdx.x * 4;
+    p[0] = s1v;
+    p[1] = s1r;
+    p[2] = s2v;
+    p[3] = s2r;
+  }
+}
+
+// m x m terms per block of 4 columns k: [sum Kinv o Kmm, sum Winv o Kmm, sum Kinv o dK, sum Winv o dK,
+// a^T Kmm a, a^T dK a]
+__global__ void __launch_bounds__(256) fitc_mm_kernel(const double* __restrict__ Kinv, const double* __restrict__ Winv,
+                                                      const double* __restrict__ Kmm, const double* __restrict__ dK,
+                                                      const double* __restrict__ a, int m, int ldm,
+                                                      double* __restrict__ part) {
+  __shared__ double red[4];
+  const int lane = threadIdx.x & 63;
+  const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+  double t[6] = {0., 0., 0., 0., 0., 0.};
+  if (k < m) {
+    const double ak = a[k];
+    for (int j = lane; j < m; j += 64) {
+      const size_t e = (size_t)j + (size_t)k * ldm;
+      const double km = Kmm[e], dk = dK[e], ki = Kinv[e], wi = Winv[e];
+      t[0] += ki * km;
+      t[1] += wi * km;
+      t[2] += ki * dk;
+      t[3] += wi * dk;
+      t[4] += a[j] * km * ak;
+      t[5] += a[j] * dk * ak;
+    }
+  }
+  for (int q = 0; q < 6; ++q) {
+    const double s = block4_sum(wave_sum(t[q]), red);
+    if (threadIdx.x == 0) part[(size_t)blockIdx.x * 6 + q] = s;
+  }
+}
+
+// out[i] = sum_j M[j, i] v[j] (v = nullptr: sum_j M[j, i]^2); one wave per column
+__global__ void __launch_bounds__(256) fitc_coldot_kernel(const double* __restrict__ M, const double* __restrict__ v,
+                                                          int np, int m, int ldm, double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= np) return;
+  double s = 0.;
+  for (int j = lane; j < m; j += 64) {
+    const double x = M[(size_t)j + (size_t)i * ldm];
+    s += v ? x * v[j] : x * x;
+  }
+  s = wave_sum(s);
+  if (lane == 0) out[i] = s;
+}
+
+// FITC prediction correction per matched pair (prediction point pi, training point oj):
+//   corr = sigma1^2 jitter - sum_j P[j, pi] K_mn[j, oj]   (P = K_mm,s^-1 K_mp; re_model_template.h:10681)
+//   Maux[:, pi] -= K_mn[:, oj] corr / d_oj                (:10800-10801)
+__global__ void __launch_bounds__(64) fitc_pred_corr_kernel(const int* __restrict__ pairs, int npairs,
+                                                            const double* __restrict__ P, const double* __restrict__ Kmn,
+                                                            const double* __restrict__ dvec, int m, int ldm, double sii,
+                                                            double* __restrict__ Maux, double* __restrict__ corr) {
+  const int q = blockIdx.x;
+  if (q >= npairs) return;
+  const int pi = pairs[2 * q], oj = pairs[2 * q + 1];
+  const int lane = threadIdx.x;
+  double s = 0.;
+  for (int j = lane; j < m; j += 64) s += P[(size_t)j + (size_t)pi * ldm] * Kmn[(size_t)j + (size_t)oj * ldm];
+  s = wave_sum(s);
+  const double c = sii - s;
+  const double f = c / dvec[oj];
+  for (int j = lane; j < m; j += 64) Maux[(size_t)j + (size_t)pi * ldm] -= Kmn[(size_t)j + (size_t)oj * ldm] * f;
+  if (lane == 0) corr[q] = c;
+}
+
+// ---- kmeans++ (GP_utils.cpp:225-295): the reference's exact arithmetic. Distances are
+// sqrt(sum_q (x_q - mu_q)^2) summed in coordinate order with separately rounded products (the
+// reference is built without FMA contraction); the first strictly smaller distance wins.
+__device__ __forceinline__ double km_dist(const double* x, const double* mu, int d) {
+#pragma clang fp contract(off)
+  double t = x[0] - mu[0];
+  double s = t * t;
+  for (int q = 1; q < d; ++q) {
+    t = x[q] - mu[q];
+    const double sq = t * t;
+    s = s + sq;
+  }
+  return sqrt(s);
+}
+
+__global__ void __launch_bounds__(256) kmeans_assign_kernel(const double* __restrict__ X, const double* __restrict__ mu,
+                                                            int n, int k, int d, int* __restrict__ cluster) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  double x[3] = {0., 0., 0.};
+  for (int q = 0; q < d; ++q) x[q] = X[(size_t)i * d + q];
+  int best = 0;
+  double bd = km_dist(x, mu, d);
+  for (int j = 1; j < k; ++j) {
+    const double dj = km_dist(x, mu + (size_t)j * d, d);
+    if (dj < bd) {
+      bd = dj;
+      best = j;
+    }
+  }
+  cluster[i] = best;
+}
+
+// new mean of cluster c: the sum of its members in increasing index order divided by their count;
+// an empty cluster keeps its mean. One wave per cluster scans the assignment 64 entries at a time.
+__global__ void __launch_bounds__(64) kmeans_means_kernel(const double* __restrict__ X, const int* __restrict__ cluster,
+                                                          int n, int k, int d, const double* __restrict__ mu_old,
+                                                          double* __restrict__ mu_new) {
+#pragma clang fp contract(off)
+  const int c = blockIdx.x;
+  const int lane = threadIdx.x;
+  double s[3] = {0., 0., 0.};
+  int count = 0;
+  for (int i0 = 0; i0 < n; i0 += 64) {
+    const int i = i0 + lane;
+    unsigned long long mask = __ballot(i < n && cluster[i] == c);
+    while (mask) {
+      const int b = __ffsll((long long)mask) - 1;
+      mask &= mask - 1;
+      const double* xr = X + (size_t)(i0 + b) * d;
+      for (int q = 0; q < d; ++q) s[q] = s[q] + xr[q];
+      ++count;
+    }
+  }
+  if (lane < d) {
+    double v = s[0];
+    for (int q = 1; q < d; ++q)
+      if (q == lane) v = s[q];
+    mu_new[(size_t)c * d + lane] = count > 0 ? v / (double)count : mu_old[(size_t)c * d + lane];
+  }
+}
+
+// flags[0] = any(mu != a), flags[1] = any(mu != b) (one block)
+__global__ void __launch_bounds__(256) kmeans_cmp_kernel(const double* __restrict__ mu, const double* __restrict__ a,
+                                                         const double* __restrict__ b, int cnt, int* __restrict__ flags) {
+  __shared__ int f[2];
+  if (threadIdx.x == 0) f[0] = f[1] = 0;
+  __syncthreads();
+  int da = 0, db = 0;
+  for (int e = threadIdx.x; e < cnt; e += 256) {
+    da |= mu[e] != a[e];
+    db |= mu[e] != b[e];
+  }
+  if (da) atomicOr(&f[0], 1);
+  if (db) atomicOr(&f[1], 1);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    flags[0] = f[0];
+    flags[1] = f[1];
+  }
+}
+
+template <typename F>
+void dispatch_cov_fitc(int cov, F&& f) {
+  switch (cov) {
+    case kMatern05: f(std::integral_constant<int, kMatern05>{}); break;
+    case kMatern15: f(std::integral_constant<int, kMatern15>{}); break;
+    case kMatern25: f(std::integral_constant<int, kMatern25>{}); break;
+    case kGaussian: f(std::integral_constant<int, kGaussian>{}); break;
+    default: Fatal("unsupported covariance type %d", cov);
+  }
+}
+
+// closest_distance (GP_utils.cpp:190-201) on the host: the reference's arithmetic
+double host_dist(const double* x, const double* mu, int d) {
+  double t = x[0] - mu[0];
+  double s = t * t;
+  for (int q = 1; q < d; ++q) {
+    t = x[q] - mu[q];
+    const double sq = t * t;
+    s = s + sq;
+  }
+  return std::sqrt(s);
+}
+
+}  // namespace
+
+std::vector<double> fitc_inducing_points(const std::vector<double>& coords, int n, int d, int m,
+                                         const std::string& method, std::mt19937& rng, hipStream_t s) {
+  if (m <= 0) Fatal("num_ind_points must be > 0");
+  if (n < m) Fatal("Cannot have more inducing points than data points for 'fitc' approximation ");
+  std::vector<double> Z((size_t)m * d);
+  if (method == "random") {
+    // SampleIntNoReplaceSort (utils.h:323-337): Floyd's sampling, then sorted
+    std::vector<int> idx;
+    for (int r = n - m; r < n; ++r) {
+      const int v = std::uniform_int_distribution<>(0, r)(rng);
+      if (std::find(idx.begin(), idx.end(), v) == idx.end()) idx.push_back(v);
+      else idx.push_back(r);
+    }
+    std::sort(idx.begin(), idx.end());
+    for (int j = 0; j < m; ++j)
+      for (int q = 0; q < d; ++q) Z[(size_t)j * d + q] = coords[(size_t)idx[j] * d + q];
+    return Z;
+  }
+  if (method != "kmeans++")
+    Fatal("Method '%s' is not supported for finding inducing points in gpboost_amd (supported: kmeans++, random)",
+          method.c_str());
+  // random_plusplus (GP_utils.cpp:203-223): D-weighted seeding on the host (the draw sequence is
+  // inherently serial: one std::discrete_distribution over all n distances per seed)
+  std::vector<double> dist(n, 1.);
+  for (int i = 0; i < m; ++i) {
+    if (i == 1)
+      for (double& v : dist) v *= -1;
+    if (i > 0) {
+      const double* mu = Z.data() + (size_t)(i - 1) * d;
+#pragma omp parallel for schedule(static)
+      for (int p = 0; p < n; ++p) {
+        const double dd = host_dist(coords.data() + (size_t)p * d, mu, d);
+        if (dist[p] > dd || dist[p] < 0) dist[p] = dd;
+      }
+    }
+    const int v = std::discrete_distribution<>(dist.data(), dist.data() + dist.size())(rng);
+    for (int q = 0; q < d; ++q) Z[(size_t)i * d + q] = coords[(size_t)v * d + q];
+  }
+  // Lloyd iterations (kmeans_plusplus, GP_utils.cpp:280-294) on the GPU: stop when the means repeat
+  // the previous or the one-before-previous iterate, or after max_it = 1000
+  // (re_model_template.h:6995)
+  const int max_it = 1000;
+  const size_t cnt = (size_t)m * d;
+  DevBuf<double> dX((size_t)n * d), b0(cnt), b1(cnt), b2(cnt);
+  DevBuf<int> cl(n), flags(2);
+  HIP_CHECK(hipMemcpyAsync(dX.get(), coords.data(), sizeof(double) * n * d, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(b0.get(), Z.data(), sizeof(double) * cnt, hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemsetAsync(b1.get(), 0, sizeof(double) * cnt, s));
+  HIP_CHECK(hipMemsetAsync(b2.get(), 0, sizeof(double) * cnt, s));
+  double* mu = b0.get();
+  double* old = b1.get();
+  double* old_old = b2.get();
+  int h_flags[2] = {1, 1};
+  int count = 0;
+  do {
+    // old_old <- old, old <- means, means <- calculate_means(old)
+    double* free_buf = old_old;
+    old_old = old;
+    old = mu;
+    mu = free_buf;
+    hipLaunchKernelGGL(kmeans_assign_kernel, dim3((n + 255) / 256), dim3(256), 0, s, dX.get(), old, n, m, d, cl.get());
+    hipLaunchKernelGGL(kmeans_means_kernel, dim3(m), dim3(64), 0, s, dX.get(), cl.get(), n, m, d, old, mu);
+    hipLaunchKernelGGL(kmeans_cmp_kernel, dim3(1), dim3(256), 0, s, mu, old, old_old, (int)cnt, flags.get());
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(h_flags, flags.get(), sizeof(int) * 2, hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    ++count;
+  } while (h_flags[0] && h_flags[1] && count != max_it);
+  HIP_CHECK(hipMemcpyAsync(Z.data(), mu, sizeof(double) * cnt, hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  return Z;
+}
+
+FitcSolver::FitcSolver(int n, int d, const double* d_X, const std::vector<double>& Z, hipStream_t stream)
+    : n_(n), d_(d), m_((int)(Z.size() / d)), ldm_(((int)(Z.size() / d) + 63) / 64 * 64), d_X_(d_X), Z_(Z),
+      stream_(stream) {
+  const int m = m_, ldm = ldm_;
+  if (m < 1) Fatal("FITC needs at least one inducing point");
+  if (d > 3) Fatal("FITC: dim_gp_coords = %d not supported (1..3)", d);
+  dZ_.alloc((size_t)m * d);
+  HIP_CHECK(hipMemcpyAsync(dZ_.get(), Z_.data(), sizeof(double) * m * d, hipMemcpyHostToDevice, stream_));
+  const size_t mn = (size_t)ldm * n, mm = (size_t)ldm * ldm;
+  for (DevBuf<double>* b : {&Kmn_, &V_, &Kd_, &A_}) b->alloc(mn);
+  for (DevBuf<double>* b : {&Kmm_, &Ks_, &Li_, &W_, &Wi_, &Kinv_, &Winv_, &dKmm_}) {
+    b->alloc(mm);
+    HIP_CHECK(hipMemsetAsync(b->get(), 0, sizeof(double) * mm, stream_));
+  }
+  T_.alloc((size_t)ldm * (ldm / 2 + 64));
+  const long tiles = (long)((m + 63) / 64) * ((m + 63) / 64);
+  max_chunks_ = (int)std::max<long>(1, std::min<long>(2048 / tiles + 1, (n + 255) / 256));
+  const int nb4 = (n + 3) / 4;
+  const int nbg = (n + 255) / 256;
+  part_.alloc(std::max<size_t>((size_t)max_chunks_ * mm, std::max<size_t>((size_t)nb4 * 4, (size_t)nbg * ldm)));
+  // vec_: d, Dy, y_aux (n each), u, w, a (ldm each), mm-partials (6 per 4 columns)
+  vec_.alloc((size_t)3 * n + 3 * ldm + (size_t)6 * ((m + 3) / 4));
+  red_.alloc(16);
+  info_.alloc(1);
+  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_red_), 16 * sizeof(double), hipHostMallocDefault));
+  for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+void FitcSolver::Factor(int cov_type, double var, double phi, const double* d_y, double* red) {
+  const int n = n_, m = m_, ldm = ldm_, d = d_;
+  double* dvec = vec_.get();
+  double* Dy = dvec + n;
+  double* yaux = Dy + n;
+  double* u = yaux + n;
+  double* w = u + ldm;
+  HIP_CHECK(hipMemsetAsync(info_.get(), 0, sizeof(int), stream_));
+  dispatch_cov_fitc(cov_type, [&](auto c) {
+    constexpr int COV = decltype(c)::value;
+    hipLaunchKernelGGL((fitc_kmn_kernel<COV>), dim3((m + 63) / 64, (n + 3) / 4), dim3(256), 0, stream_, d_X_, dZ_.get(),
+                       n, m, d, ldm, var, phi, Kmn_.get());
+    hipLaunchKernelGGL((fitc_kmm_kernel<COV>), dim3((m + 63) / 64, (m + 3) / 4), dim3(256), 0, stream_, dZ_.get(), m, d,
+                       ldm, var, phi, Kmm_.get(), Ks_.get(), dKmm_.get());
+  });
+  HIP_CHECK(hipGetLastError());
+  // L = chol(K_mm,s) in Li_ (lower), L^-1 in Wi_ -> copied to Li_'s role below
+  HIP_CHECK(hipMemcpyAsync(Li_.get(), Ks_.get(), sizeof(double) * ldm * ldm, hipMemcpyDeviceToDevice, stream_));
+  chol_lower(stream_, Li_.get(), Wi_.get(), m, ldm, info_.get());
+  launch_logdet_chol(stream_, Li_.get(), ldm, m, red + 0);
+  trtri_lower(stream_, Li_.get(), Wi_.get(), T_.get(), 0, m, ldm);
+  // Kinv = L^-T L^-1 (full) from Wi_ = L^-1; keep L^-1 in Kinv_'s place temporarily? No: V first.
+  // V = L^-1 K_mn
+  gemm_f64(stream_, m, n, m, 1., Wi_.get(), ldm, 0, Kmn_.get(), ldm, 0, 0., V_.get(), ldm, 0, 1, 0, 0);
+  gemm_f64(stream_, m, m, m, 1., Wi_.get(), ldm, 1, Wi_.get(), ldm, 0, 0., Kinv_.get(), ldm, 0, 0, 1, 1);
+  // L^-1 is still needed for A = L^-T V (gradient): keep it in Li_ (L itself is no longer needed)
+  HIP_CHECK(hipMemcpyAsync(Li_.get(), Wi_.get(), sizeof(double) * ldm * ldm, hipMemcpyDeviceToDevice, stream_));
+  const int nb4 = (n + 3) / 4;
+  hipLaunchKernelGGL(fitc_diag_kernel, dim3(nb4), dim3(256), 0, stream_, V_.get(), Kmn_.get(), d_y, n, m, ldm,
+                     1. + var * kJitterMult, dvec, Kd_.get(), Dy, part_.get());
+  HIP_CHECK(hipGetLastError());
+  launch_sum_blocks(part_.get(), nb4, 1, red + 2, stream_);
+  // W = K_mn K_d^T + K_mm,s (split K over the n observations), Lw = chol(W), Lw^-1, W^-1
+  const long mm = (long)ldm * ldm;
+  const int chunks = gemm_f64_splitk(stream_, m, m, n, Kmn_.get(), ldm, 0, Kd_.get(), ldm, 1, part_.get(), ldm, mm,
+                                     2048, max_chunks_);
+  hipLaunchKernelGGL(fitc_wsum_kernel, dim3((m + 63) / 64, (m + 3) / 4), dim3(256), 0, stream_, part_.get(), chunks, mm,
+                     m, ldm, Ks_.get(), W_.get());
+  HIP_CHECK(hipGetLastError());
+  chol_lower(stream_, W_.get(), Wi_.get(), m, ldm, info_.get());
+  launch_logdet_chol(stream_, W_.get(), ldm, m, red + 1);
+  trtri_lower(stream_, W_.get(), Wi_.get(), T_.get(), 0, m, ldm);
+  gemm_f64(stream_, m, m, m, 1., Wi_.get(), ldm, 1, Wi_.get(), ldm, 0, 0., Winv_.get(), ldm, 0, 0, 1, 1);
+  // u = K_mn (y / d), w = W^-1 u, y_aux, q
+  const int chunk = 256, nbg = (n + chunk - 1) / chunk;
+  hipLaunchKernelGGL(fitc_gemv_part_kernel, dim3(nbg), dim3(256), 0, stream_, Kmn_.get(), Dy, n, m, ldm, chunk,
+                     part_.get());
+  hipLaunchKernelGGL(fitc_gemv_reduce_kernel, dim3((m + 255) / 256), dim3(256), 0, stream_, part_.get(), nbg, m, ldm, u);
+  hipLaunchKernelGGL(fitc_symv_kernel, dim3((m + 255) / 256), dim3(256), 0, stream_, Winv_.get(), u, m, ldm, w);
+  hipLaunchKernelGGL(fitc_yaux_kernel, dim3(nb4), dim3(256), 0, stream_, Kmn_.get(), w, d_y, Dy, dvec, n, m, ldm, yaux,
+                     part_.get());
+  HIP_CHECK(hipGetLastError());
+  launch_sum_blocks(part_.get(), nb4, 1, red + 3, stream_);
+}
+
+void FitcSolver::Eval(int cov_type, double var, double phi, const double* d_y, bool want_grad, double* sums,
+                      double* kernel_ms) {
+  const int n = n_, m = m_, ldm = ldm_, d = d_;
+  double* red = red_.get();
+  HIP_CHECK(hipEventRecord(ev_[0], stream_));
+  Factor(cov_type, var, phi, d_y, red);
+  HIP_CHECK(hipEventRecord(ev_[1], stream_));
+  double* dvec = vec_.get();
+  double* yaux = dvec + 2 * (size_t)n;
+  double* a = yaux + n + 2 * ldm;
+  double* mmpart = a + ldm;
+  if (want_grad) {
+    // A = L^-T V (L^-T upper), G^T = W^-1 K_mn (into K_d), M = dK_mm A (into V)
+    gemm_f64(stream_, m, n, m, 1., Li_.get(), ldm, 1, V_.get(), ldm, 0, 0., A_.get(), ldm, 0, 0, 1, 0);
+    gemm_f64(stream_, m, n, m, 1., Winv_.get(), ldm, 0, Kmn_.get(), ldm, 0, 0., Kd_.get(), ldm);
+    gemm_f64(stream_, m, n, m, 1., dKmm_.get(), ldm, 0, A_.get(), ldm, 0, 0., V_.get(), ldm);
+    const int chunk = 256, nbg = (n + chunk - 1) / chunk;
+    hipLaunchKernelGGL(fitc_gemv_part_kernel, dim3(nbg), dim3(256), 0, stream_, A_.get(), yaux, n, m, ldm, chunk,
+                       part_.get());
+    hipLaunchKernelGGL(fitc_gemv_reduce_kernel, dim3((m + 255) / 256), dim3(256), 0, stream_, part_.get(), nbg, m, ldm, a);
+    const int nb4 = (n + 3) / 4;
+    const double delta = var * kJitterMult - var;
+    dispatch_cov_fitc(cov_type, [&](auto c) {
+      hipLaunchKernelGGL((fitc_grad_kernel<decltype(c)::value>), dim3(nb4), dim3(256), 0, stream_, d_X_, dZ_.get(), n, m,
+                         d, ldm, var, phi, delta, Kmn_.get(), A_.get(), Kd_.get(), V_.get(), a, dvec, yaux, part_.get());
+    });
+    const int mb4 = (m + 3) / 4;
+    hipLaunchKernelGGL(fitc_mm_kernel, dim3(mb4), dim3(256), 0, stream_, Kinv_.get(), Winv_.get(), Kmm_.get(),
+                       dKmm_.get(), a, m, ldm, mmpart);
+    HIP_CHECK(hipGetLastError());
+    launch_sum_blocks(part_.get(), nb4, 4, red + 4, stream_);
+    launch_sum_blocks(mmpart, mb4, 6, red + 8, stream_);
+  }
+  HIP_CHECK(hipMemcpyAsync(h_red_, red, sizeof(double) * 14, hipMemcpyDeviceToHost, stream_));
+  int info = 0;
+  HIP_CHECK(hipMemcpyAsync(&info, info_.get(), sizeof(int), hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipEventRecord(ev_[2], stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  float ms0 = 0.f, ms1 = 0.f;
+  HIP_CHECK(hipEventElapsedTime(&ms0, ev_[0], ev_[1]));
+  HIP_CHECK(hipEventElapsedTime(&ms1, ev_[0], ev_[2]));
+  kernel_ms[0] = ms0;
+  kernel_ms[1] = ms1;
+  const double nan = std::numeric_limits<double>::quiet_NaN();
+  if (info != 0) {
+    for (int k = 0; k < 6; ++k) sums[k] = nan;
+    return;
+  }
+  // log det Psi = -2 sum log L_ii + 2 sum log Lw_ii + sum log d (re_model_template.h:2700-2713)
+  sums[0] = -h_red_[0] + h_red_[1] + h_red_[2];
+  sums[1] = h_red_[3];
+  if (want_grad) {
+    const double* g = h_red_ + 4;    // per-observation sums: s1v, s1r, s2v, s2r
+    const double* t = h_red_ + 8;    // m x m: KinvKmm, WinvKmm, KinvdK, WinvdK, aKmma, adKa
+    sums[2] = g[0] + 0.5 * t[4];
+    sums[3] = g[1] + 0.5 * t[5];
+    sums[4] = g[2] - t[0] + t[1];
+    sums[5] = g[3] - t[2] + t[3];
+  } else {
+    sums[2] = sums[3] = sums[4] = sums[5] = 0.;
+  }
+}
+
+void FitcSolver::Predict(int cov_type, double var, double phi, const double* d_y, const double* Xp, int np,
+                         const std::vector<int>& match, bool want_var, bool want_cov, bool response, double* mean,
+                         double* pvar, double* pcov) {
+  const int n = n_, m = m_, ldm = ldm_, d = d_;
+  Factor(cov_type, var, phi, d_y, red_.get());
+  int info = 0;
+  HIP_CHECK(hipMemcpyAsync(&info, info_.get(), sizeof(int), hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  if (info != 0) Fatal("the FITC covariance is not positive definite (Cholesky failed)");
+  const double* dvec = vec_.get();
+  const double* yaux = dvec + 2 * (size_t)n;
+  const double* w = yaux + n + ldm;
+  DevBuf<double> dXp((size_t)np * d), Kmp((size_t)ldm * np), out((size_t)3 * np);
+  HIP_CHECK(hipMemcpyAsync(dXp.get(), Xp, sizeof(double) * np * d, hipMemcpyHostToDevice, stream_));
+  dispatch_cov_fitc(cov_type, [&](auto c) {
+    hipLaunchKernelGGL((fitc_kmn_kernel<decltype(c)::value>), dim3((m + 63) / 64, (np + 3) / 4), dim3(256), 0, stream_,
+                       dXp.get(), dZ_.get(), np, m, d, ldm, var, phi, Kmp.get());
+  });
+  const int nb4 = (np + 3) / 4;
+  // mean = K_pm W^-1 K_mn (y / d)  (:10705)
+  hipLaunchKernelGGL(fitc_coldot_kernel, dim3(nb4), dim3(256), 0, stream_, Kmp.get(), w, np, m, ldm, out.get());
+  HIP_CHECK(hipGetLastError());
+  // coincident prediction / training coordinates: the FITC diagonal correction
+  std::vector<int> pairs;
+  for (int i = 0; i < np; ++i)
+    if (match[i] >= 0) {
+      pairs.push_back(i);
+      pairs.push_back(match[i]);
+    }
+  const int npairs = (int)pairs.size() / 2;
+  const double sii = var * kJitterMult;   // sigma_ip_stable(0, 0)
+  DevBuf<double> Maux, corr;
+  std::vector<double> h_corr(npairs), h_yaux, h_d;
+  if (npairs > 0 || want_var || want_cov) {
+    Maux.alloc((size_t)ldm * np);
+    HIP_CHECK(hipMemcpyAsync(Maux.get(), Kmp.get(), sizeof(double) * ldm * np, hipMemcpyDeviceToDevice, stream_));
+  }
+  if (npairs > 0) {
+    DevBuf<double> P((size_t)ldm * np);
+    DevBuf<int> dpairs(pairs.size());
+    corr.alloc(npairs);
+    HIP_CHECK(hipMemcpyAsync(dpairs.get(), pairs.data(), sizeof(int) * pairs.size(), hipMemcpyHostToDevice, stream_));
+    gemm_f64(stream_, m, np, m, 1., Kinv_.get(), ldm, 0, Kmp.get(), ldm, 0, 0., P.get(), ldm);
+    hipLaunchKernelGGL(fitc_pred_corr_kernel, dim3(npairs), dim3(64), 0, stream_, dpairs.get(), npairs, P.get(),
+                       Kmn_.get(), dvec, m, ldm, sii, Maux.get(), corr.get());
+    HIP_CHECK(hipGetLastError());
+    h_yaux.resize(n);
+    h_d.resize(n);
+    HIP_CHECK(hipMemcpyAsync(h_corr.data(), corr.get(), sizeof(double) * npairs, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(h_yaux.data(), yaux, sizeof(double) * n, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(h_d.data(), dvec, sizeof(double) * n, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));   // P is freed at scope end
+  }
+  DevBuf<double> Vp, U;
+  if (want_var || want_cov) {
+    // resid_i = sigma_ip_stable(0, 0) - |L^-1 K_mp,i|^2 (:10742-10759); U = Lw^-1 Maux (:10803-10804)
+    Vp.alloc((size_t)ldm * np);
+    U.alloc((size_t)ldm * np);
+    gemm_f64(stream_, m, np, m, 1., Li_.get(), ldm, 0, Kmp.get(), ldm, 0, 0., Vp.get(), ldm, 0, 1, 0, 0);
+    gemm_f64(stream_, m, np, m, 1., Wi_.get(), ldm, 0, Maux.get(), ldm, 0, 0., U.get(), ldm, 0, 1, 0, 0);
+    hipLaunchKernelGGL(fitc_coldot_kernel, dim3(nb4), dim3(256), 0, stream_, Vp.get(), nullptr, np, m, ldm,
+                       out.get() + np);
+    hipLaunchKernelGGL(fitc_coldot_kernel, dim3(nb4), dim3(256), 0, stream_, U.get(), nullptr, np, m, ldm,
+                       out.get() + 2 * (size_t)np);
+    HIP_CHECK(hipGetLastError());
+  }
+  std::vector<double> h((size_t)3 * np);
+  HIP_CHECK(hipMemcpyAsync(h.data(), out.get(), sizeof(double) * h.size(), hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  std::copy(h.begin(), h.begin() + np, mean);
+  for (int q = 0; q < npairs; ++q) mean[pairs[2 * q]] += h_corr[q] * h_yaux[pairs[2 * q + 1]];   // :10706-10708
+  const double nug = response ? 1. : 0.;
+  std::vector<double> resid(np);
+  for (int i = 0; i < np; ++i) resid[i] = sii - h[np + i];
+  if (want_var) {
+    for (int i = 0; i < np; ++i) pvar[i] = nug + resid[i] + h[2 * (size_t)np + i];
+    for (int q = 0; q < npairs; ++q) {   // - corr^2 / d (:10821-10826)
+      const double c = h_corr[q];
+      pvar[pairs[2 * q]] -= c * (c / h_d[pairs[2 * q + 1]]);
+    }
+  }
+  if (want_cov) {
+    // U^T U + diag(resid) (+ I) - corr D^-1 corr^T (:10805-10814), column-major np x np
+    DevBuf<double> C((size_t)np * np);
+    gemm_f64(stream_, np, np, m, 1., U.get(), ldm, 1, U.get(), ldm, 0, 0., C.get(), np);
+    HIP_CHECK(hipMemcpyAsync(pcov, C.get(), sizeof(double) * np * np, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+    for (int i = 0; i < np; ++i) pcov[(size_t)i * np + i] += resid[i] + nug;
+    for (int q = 0; q < npairs; ++q)
+      for (int r = 0; r < npairs; ++r)
+        if (pairs[2 * q + 1] == pairs[2 * r + 1])
+          pcov[(size_t)pairs[2 * r] * np + pairs[2 * q]] -= h_corr[q] * h_corr[r] / h_d[pairs[2 * q + 1]];
+  }
+}
+
+void FitcSolver::YAux(double* out) {
+  HIP_CHECK(hipMemcpyAsync(out, vec_.get() + 2 * (size_t)n_, sizeof(double) * n_, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+}  // namespace gpb_amd

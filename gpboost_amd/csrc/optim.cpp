@@ -581,7 +581,7 @@ void REModelAMD::StdDevCovPars(const double* orig, double* sd) {
   // include_error_var = true: with Sigma^-1 = Psi^-1 / sigma^2 and dSigma_k on the original scale
   // (sigma^2: I; sigma1^2: the correlation matrix; rho: sigma1^2 dcorr/drho)
   //   FI_00 = tr(Sigma^-2) / 2, FI_0k = tr(Sigma^-2 dSigma_k) / 2, FI_kl = tr(Sigma^-1 dSigma_k Sigma^-1 dSigma_l) / 2
-  if (cfg_.latent || vecchia_)
+  if (cfg_.latent || vecchia_ || fitc_)
     Fatal("standard deviations of covariance parameters are supported by gpboost_amd only for gp_approx = 'none' "
           "with the Gaussian likelihood");
   UseDevice();

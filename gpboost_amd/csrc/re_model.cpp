@@ -68,8 +68,15 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
   } else if (cfg_.gp_approx == "none") {
     if (cfg_.lik != kLikGaussian)
       Fatal("likelihood '%s' requires gp_approx = 'vecchia' in gpboost_amd (dense Laplace is out of scope)", cfg_.likelihood.c_str());
+  } else if (cfg_.gp_approx == "fitc") {
+    if (cfg_.lik != kLikGaussian)
+      Fatal("likelihood '%s' with gp_approx = 'fitc' is not supported by gpboost_amd (supported: gaussian)", cfg_.likelihood.c_str());
+    if (cfg_.matrix_inversion_method == "iterative")   // re_model_template.h:8774-8776
+      Fatal("'iterative' methods are not implemented for gp_approx = 'fitc'. Use 'cholesky' ");
+    if (cfg_.num_ind_points <= 0) cfg_.num_ind_points = 500;   // re_model_template.h:320-326
+    if (!(cfg_.cover_tree_radius > 0.)) Fatal("cover_tree_radius must be > 0");
   } else {
-    Fatal("gp_approx '%s' is not supported by gpboost_amd (supported: none, vecchia, vecchia_latent)", cfg_.gp_approx.c_str());
+    Fatal("gp_approx '%s' is not supported by gpboost_amd (supported: none, vecchia, vecchia_latent, fitc)", cfg_.gp_approx.c_str());
   }
   std::string& mim = cfg_.matrix_inversion_method;
   if (mim == "default") mim = cfg_.latent ? "iterative" : "cholesky";
@@ -140,7 +147,24 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
     coords_vo_ = coords_;
     d_X_.alloc((size_t)n * d);
     HIP_CHECK(hipMemcpyAsync(d_X_.get(), coords_.data(), sizeof(double) * n * d, hipMemcpyHostToDevice, stream_));
-    dense_.reset(new DenseSolver(n, d, d_X_.get(), stream_));
+    if (cfg_.gp_approx == "fitc") {
+      // inducing points on the unique locations (CreateREComponentsFITC_FSA, re_model_template.h:6946-7073);
+      // with repeated coordinates the reference switches to 'full_scale_tapering' (:6963-6969), out of scope
+      std::vector<int> uniq, idx;
+      unique_locations(coords_.data(), n, d, uniq, idx);
+      if ((int)uniq.size() < n)
+        Fatal("gp_approx = 'fitc' with duplicate coordinates is not supported by gpboost_amd (the reference switches to "
+              "'full_scale_tapering')");
+      std::mt19937 rng((std::mt19937::result_type)cfg_.seed);   // rng_ = RNG_t(seed) (re_model_template.h:154)
+      const std::vector<double> Z =
+          fitc_inducing_points(coords_, n, d, cfg_.num_ind_points, cfg_.ind_points_selection, rng, stream_);
+      std::vector<int> zu, zi;
+      unique_locations(Z.data(), cfg_.num_ind_points, d, zu, zi);
+      if ((int)zu.size() < cfg_.num_ind_points) Fatal("Duplicates found in inducing points / low-dimensional knots ");
+      fitc_.reset(new FitcSolver(n, d, d_X_.get(), Z, stream_));
+    } else {
+      dense_.reset(new DenseSolver(n, d, d_X_.get(), stream_));
+    }
   }
   d_sums_.alloc(16);
   HIP_CHECK(hipStreamSynchronize(stream_));
@@ -173,6 +197,7 @@ REModelAMD::~REModelAMD() {
   (void)hipSetDevice(device_);
   if (stream_) (void)hipStreamSynchronize(stream_);
   dense_.reset();
+  fitc_.reset();
   latent_.reset();
   coll_.reset();
   if (comm_) ncclCommDestroy(comm_);
@@ -321,8 +346,12 @@ std::vector<double> gauss_hermite_adaptive(int order) {
 void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,
                          bool predict_cov_mat, bool predict_var, bool predict_response, double* out,
                          const double* mean_add) {
-  if (!vecchia_) Fatal("predictions are implemented for the Vecchia approximation (gp_approx = 'vecchia' / "
-                       "'vecchia_latent') only");
+  if (fitc_) {
+    PredictFitc(y, n_pred, coords_pred, cov_pars, predict_cov_mat, predict_var, predict_response, out, mean_add);
+    return;
+  }
+  if (!vecchia_) Fatal("predictions are implemented for the Vecchia (gp_approx = 'vecchia' / 'vecchia_latent') and "
+                       "FITC approximations only");
   if (world_ > 1) Fatal("predictions are only available on single-rank models");
   if (n_pred <= 0) Fatal("num_data_pred must be > 0");
   if (coords_pred == nullptr) Fatal("gp_coords_data_pred must be provided");
@@ -444,6 +473,69 @@ void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred,
     for (int p = 0; p < n_pred; ++p) c[(size_t)p * n_pred + p] = h[n_pred + p];
   } else if (predict_var) {
     std::copy(h.begin() + n_pred, h.end(), out + n_pred);
+  }
+}
+
+// FITC (CalcPredFITC_FSA, re_model_template.h:10600-10828 via Predict :3890-3893): means, variances or the
+// covariance matrix, times sigma^2 (:3956, :3967); prediction points that coincide with a training point
+// (TwoNumbersAreEqual on the coordinate sums, then per coordinate, utils.h:52-54 with
+// EPSILON_NUMBERS = 1e-10) get the FITC diagonal correction.
+void REModelAMD::PredictFitc(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,
+                             bool predict_cov_mat, bool predict_var, bool predict_response, double* out,
+                             const double* mean_add) {
+  if (n_pred <= 0) Fatal("num_data_pred must be > 0");
+  if (coords_pred == nullptr) Fatal("gp_coords_data_pred must be provided");
+  UseDevice();
+  if (y != nullptr) SetY(y);
+  if (!y_set_) Fatal("response variable y has not been set (pass y or evaluate the likelihood first)");
+  double cp[3];
+  if (cov_pars != nullptr) std::copy(cov_pars, cov_pars + 3, cp);
+  else if ((int)last_cov_pars_.size() == 3) std::copy(last_cov_pars_.begin(), last_cov_pars_.end(), cp);
+  else Fatal("cov_pars must be provided (no previous evaluation)");
+  double trafo[3];
+  TransformCovPars(cp, trafo);
+  const int n = cfg_.n, d = cfg_.d;
+  std::vector<double> xp((size_t)n_pred * d);
+  for (int p = 0; p < n_pred; ++p)
+    for (int q = 0; q < d; ++q) xp[(size_t)p * d + q] = coords_pred[(size_t)q * n_pred + p];
+  // coincident coordinates: candidates by sorted coordinate sums, then the reference's predicate
+  auto equal = [](double a, double b) {
+    return std::fabs(a - b) < 1e-10 * std::max({1.0, std::fabs(a), std::fabs(b)});
+  };
+  std::vector<std::pair<double, int>> sums(n);
+  for (int i = 0; i < n; ++i) {
+    double s = 0.;
+    for (int q = 0; q < d; ++q) s += coords_[(size_t)i * d + q];
+    sums[i] = {s, i};
+  }
+  std::sort(sums.begin(), sums.end());
+  std::vector<int> match(n_pred, -1);
+  for (int p = 0; p < n_pred; ++p) {
+    double sp = 0.;
+    for (int q = 0; q < d; ++q) sp += xp[(size_t)p * d + q];
+    const double tol = 1e-10 * std::max(1.0, std::fabs(sp)) * 2. + 1e-300;
+    auto it = std::lower_bound(sums.begin(), sums.end(), std::make_pair(sp - tol, -1));
+    for (; it != sums.end() && it->first <= sp + tol; ++it) {
+      if (!equal(sp, it->first)) continue;
+      bool same = true;
+      for (int q = 0; q < d; ++q) same = same && equal(xp[(size_t)p * d + q], coords_[(size_t)it->second * d + q]);
+      if (same) {
+        match[p] = it->second;   // training coordinates are unique (FITC requires it)
+        break;
+      }
+    }
+  }
+  std::vector<double> mean(n_pred), var(predict_var ? n_pred : 0);
+  std::vector<double> cov(predict_cov_mat ? (size_t)n_pred * n_pred : 0);
+  fitc_->Predict(cfg_.cov_type, trafo[1], trafo[2], d_y_.get(), xp.data(), n_pred, match, predict_var,
+                 predict_cov_mat, predict_response, mean.data(), var.data(), cov.data());
+  if (mean_add != nullptr)
+    for (int p = 0; p < n_pred; ++p) mean[p] += mean_add[p];
+  std::copy(mean.begin(), mean.end(), out);
+  if (predict_cov_mat) {
+    for (size_t e = 0; e < cov.size(); ++e) out[n_pred + e] = cov[e] * trafo[0];
+  } else if (predict_var) {
+    for (int p = 0; p < n_pred; ++p) out[n_pred + p] = var[p] * trafo[0];
   }
 }
 
@@ -645,6 +737,20 @@ void REModelAMD::EvalVecchiaPartials(const double* cov_pars_orig, int r0, int r1
   LaunchVecchiaRows(trafo, r0, r1, sums, false);
 }
 
+void REModelAMD::EvalExactGaussian(const double* trafo, bool want_grad, double* sums) {
+  if (fitc_) {
+    events_pending_ = false;
+    fitc_->Eval(cfg_.cov_type, trafo[1], trafo[2], d_y_.get(), want_grad, sums, last_kernel_ms_);
+    return;
+  }
+  EvalDense(trafo, want_grad, sums);
+}
+
+const std::vector<double>& REModelAMD::InducingPoints() const {
+  if (!fitc_) Fatal("model does not use gp_approx = 'fitc'");
+  return fitc_->inducing_points();
+}
+
 void REModelAMD::EvalDense(const double* trafo, bool want_grad, double* sums) {
   events_pending_ = false;
   dense_->Eval(cfg_.cov_type, trafo[1], trafo[2], d_y_.get(), want_grad, sums, last_kernel_ms_);
@@ -726,7 +832,7 @@ EvalResult REModelAMD::EvalTrafo(const double* trafo, bool want_grad, int profil
   EnsureStructure();
   double sums[kVecchiaSums];
   if (vecchia_) EvalVecchia(trafo, sums);
-  else EvalDense(trafo, want_grad, sums);
+  else EvalExactGaussian(trafo, want_grad, sums);
   if (fatal_on_nan && (!std::isfinite(sums[0]) || !std::isfinite(sums[1])))
     Fatal("NaN or Inf occurred in the negative log-likelihood (non-positive-definite covariance?)");
   EvalResult res;

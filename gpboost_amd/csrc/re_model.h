@@ -18,6 +18,7 @@
 #include "collective.h"
 #include "common.h"
 #include "dense.h"
+#include "fitc.h"
 #include "latent.h"
 #include "optim.h"
 
@@ -35,6 +36,10 @@ struct ModelConfig {
   std::string likelihood = "gaussian";
   std::string matrix_inversion_method = "cholesky";
   int seed = 0;
+  // FITC (gp_approx = "fitc"): num_ind_points <= 0 -> 500 (re_model_template.h:319-336)
+  int num_ind_points = 0;
+  double cover_tree_radius = 1.;
+  std::string ind_points_selection = "kmeans++";
   // derived
   bool latent = false;     // latent GP + Laplace approximation (non-Gaussian or "vecchia_latent")
   int lik = 0;             // LatentLik code when latent
@@ -109,6 +114,9 @@ class REModelAMD {
   void GetLastIterationInfo(double* out) const { for (int k = 0; k < 4; ++k) out[k] = last_iter_info_[k]; }
   void BenchLatentOperators(int t, int reps, double* out);
   void GetLastKernelTimes(double* ms);
+  // FITC inducing points (host row-major m x d; EXTENSION: GPB_GetInducingPoints)
+  const std::vector<double>& InducingPoints() const;
+  bool is_fitc() const { return fitc_ != nullptr; }
 
   double last_nll() const { return last_nll_; }
   const std::vector<double>& last_cov_pars() const { return last_cov_pars_; }
@@ -165,7 +173,7 @@ class REModelAMD {
   const std::string& optimizer_coef() const { return optimizer_coef_; }
   std::string cg_preconditioner_type() const;
   // CanCalculateStandardErrorsCovPars (re_model_template.h:1630-1632)
-  bool CanCalculateStandardErrorsCovPars() const { return !cfg_.latent; }
+  bool CanCalculateStandardErrorsCovPars() const { return !cfg_.latent && !fitc_; }
   // GLS evaluation on the transformed scale (optimizer): beta from the Gram of [X | y], then the
   // profiled L-BFGS unit on the residuals. beta_out (nullable) receives the coefficients.
   EvalResult EvalTrafoWls(const double* trafo, bool want_grad, bool fatal_on_nan, std::vector<double>* beta_out);
@@ -204,6 +212,8 @@ class REModelAMD {
 
  private:
   void TransformCovPars(const double* orig, double* trafo) const;
+  void PredictFitc(const double* y, int n_pred, const double* coords_pred, const double* cov_pars, bool predict_cov_mat,
+                   bool predict_var, bool predict_response, double* out, const double* mean_add);
   void PredictCondAll(int n, int n_pred, int mp, const std::vector<int>& nb, const double* dB, const double* dDinv,
                       double sigma2, double nugget_sub, bool want_var, bool want_cov, std::vector<double>& h,
                       std::vector<double>& cov);
@@ -214,6 +224,8 @@ class REModelAMD {
   void EvalVecchia(const double* trafo, double* sums);  // sums over this rank's rows, all-reduced
   void LaunchVecchiaRows(const double* trafo, int r0, int r1, double* sums_host, bool allreduce);
   void EvalDense(const double* trafo, bool want_grad, double* sums);
+  // "none" and "fitc" share the Gaussian Cholesky bookkeeping (dense_ or fitc_)
+  void EvalExactGaussian(const double* trafo, bool want_grad, double* sums);
 
   void EnsureStructure();
   void UseDevice() const;
@@ -244,6 +256,7 @@ class REModelAMD {
   bool timing_ = false;           // record kernel events (set by the first GetLastKernelTimes)
 
   std::unique_ptr<DenseSolver> dense_;
+  std::unique_ptr<FitcSolver> fitc_;   // gp_approx = "fitc" (Gaussian likelihood)
   std::unique_ptr<LatentVecchia> latent_;
   std::vector<double> y_vo_;          // host copy (Vecchia order) for the latent solver
   std::vector<double> aux_pars_;

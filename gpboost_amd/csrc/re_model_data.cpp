@@ -85,6 +85,15 @@ void REModelAMD::CalcGradientF(double* y, const double* fixed_effects, bool calc
   double trafo[3];
   TransformCovPars(cov_pars_orig_.data(), trafo);
   std::vector<double> yaux(n), dg(n);
+  if (fitc_) {   // Woodbury y_aux of the FITC factor (CalcYAux, re_model_template.h:8898-8908)
+    double sums[kVecchiaSums];
+    UseDevice();
+    fitc_->Eval(cfg_.cov_type, trafo[1], trafo[2], d_y_.get(), false, sums, last_kernel_ms_);
+    if (!std::isfinite(sums[0])) Fatal("the FITC covariance is not positive definite (Cholesky failed)");
+    fitc_->YAux(yaux.data());
+    for (int i = 0; i < n; ++i) y[i] = yaux[i] / trafo[0];
+    return;
+  }
   if (!vecchia_) {
     dense_->PsiInvDiag(cfg_.cov_type, trafo[1], trafo[2], d_y_.get(), yaux.data(), dg.data());
     for (int i = 0; i < n; ++i) y[i] = yaux[i] / trafo[0];
@@ -134,6 +143,7 @@ void REModelAMD::UploadCovariates() {
 
 std::vector<double> REModelAMD::Gram(const double* trafo) {
   const int n = cfg_.n, p = num_covariates_, c = p + 1;
+  if (fitc_) Fatal("linear regression covariates with gp_approx = 'fitc' are not supported by gpboost_amd");
   if (!vecchia_) {
     std::vector<double> Z((size_t)n * c), G((size_t)c * c);
     const double* fe = has_fixed_effects_ ? fixed_effects_.data() : nullptr;
@@ -269,6 +279,7 @@ void REModelAMD::PredictTrainingDataRandomEffects(const double* cov_pars, const 
   double trafo[3];
   TransformCovPars(cp.data(), trafo);
   std::vector<double> yaux(n), dg(n);
+  if (fitc_) Fatal("training-data random-effect predictions with gp_approx = 'fitc' are not supported by gpboost_amd");
   if (!vecchia_) {
     dense_->PsiInvDiag(cfg_.cov_type, trafo[1], trafo[2], d_y_.get(), yaux.data(), dg.data());
     for (int i = 0; i < n; ++i) {

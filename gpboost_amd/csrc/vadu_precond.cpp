@@ -12,6 +12,11 @@ namespace gpb_amd {
 VaduPrecond::~VaduPrecond() { DropGraphs(); }
 
 void VaduPrecond::DropGraphs() {
+  if (graphs_.empty()) return;
+  // A replay may still be in flight (Scratch grows S_ between two applications of one PCG, on
+  // possibly different streams): its exec, kernel-argument pool and scratch must outlive it, and a
+  // kernel tracer reads the dispatches' arguments after they ran. Rare (a new width, a new dw).
+  (void)hipDeviceSynchronize();
   for (GraphEntry& g : graphs_) (void)hipGraphExecDestroy(g.exec);
   graphs_.clear();
 }
@@ -623,6 +628,7 @@ void VaduPrecond::Record(const double* R, double* Z, double* Xt, int t, hipStrea
 double* VaduPrecond::Scratch(int slot, int t) {
   if (slot < 0 || slot >= kSlots) Fatal("VADU preconditioner scratch slot %d out of range", slot);
   if (K0_ > 0 && S_[slot].size() < (size_t)2 * ld0_ * t) {   // sized before any capture that uses it
+    HIP_CHECK(hipDeviceSynchronize());   // eager launches in flight may still use the old scratch
     DropGraphs();
     S_[slot].alloc((size_t)2 * ld0_ * t);
   }

@@ -90,7 +90,7 @@ class VaduPrecond {
   long tail_entries_ = 0;
   HeadSolve seg_bt_{}, seg_low_{};
   SegWave segw_bt_{}, segw_low_{};   // the one-wave form of the same segment solves (default)
-  bool seg_wave_ = true;             // GPBOOST_AMD_SEG_FORM = wave (default) | block (vadu_head_kernel)
+  bool seg_wave_ = false;            // GPBOOST_AMD_SEG_FORM = block (default, vadu_head_kernel) | wave
   void SegSolve(bool lower, const double* in, const double* dw, double* X, int t, hipStream_t st);
   PartialList p_th_{}, p_10_{}, p_01_{};
   DevBuf<int> d_int_, d_slot_;

@@ -286,6 +286,12 @@ GPBOOST_AMD_EXPORT int GPB_GetInitAuxPars(REModelHandle handle, double* aux_pars
 GPBOOST_AMD_EXPORT int GPB_OptimCovParBoosting(REModelHandle handle, const double* y_data, const double* fixed_effects,
     bool called_in_GPBoost_algorithm, bool reuse_learning_rates_from_previous_call);
 
+/* EXTENSION: the inducing points of a gp_approx = "fitc" model (the reference keeps them in
+ * REModelTemplate::gp_coords_ip_mat_, chosen by CreateREComponentsFITC_FSA re_model_template.h:6931-7073:
+ * kmeans++ GP_utils.cpp:269-295 or random utils.h:323-337). *num_ind_points receives m; ind_points
+ * (nullable) receives them row-major m x dim_gp_coords. */
+GPBOOST_AMD_EXPORT int GPB_GetInducingPoints(REModelHandle handle, int32_t* num_ind_points, double* ind_points);
+
 /* EXTENSION (the reference has it as a C++ method only): REModel::CalcGradient (re_model.cpp:667-680
  * -> CalcGradientF re_model_template.h:3021-3043), what the GPBoost boosting objective calls after
  * GPB_OptimCovPar(handle, NULL, score) (regression_objective.hpp:164-179): the gradient of the

@@ -51,6 +51,9 @@ def lib():
         L.orc_latent_vecchia_iterative.argtypes = [D, D, I, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, D,
                                                    ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                                    ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, D, D]
+        L.orc_fitc_inducing_points.argtypes = [D, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, D]
+        L.orc_fitc_nll_grad.argtypes = [D, D, ctypes.c_int, ctypes.c_int, D, ctypes.c_int, ctypes.c_int, D, ctypes.c_int,
+                                        D, D, D]
         _lib = L
     return _lib
 
@@ -227,3 +230,29 @@ def latent_iterative(coords_vo, y_vo, nbr, cov_type, trafo2, likelihood="gaussia
     ng = 3 if lk == 0 else 2
     return dict(nll=float(nll[0]), grad=grad[:ng].copy(), newton_its=int(info[0]), cg_its=int(info[1]),
                 lanczos_steps=int(info[2]), logdet=float(info[3]))
+
+
+def fitc_inducing_points(coords, m: int, method: str = "kmeans++", seed: int = 0):
+    """Inducing points of CreateREComponentsFITC_FSA (kmeans++ / random) and the Lloyd iteration count."""
+    x = np.ascontiguousarray(coords, dtype=np.float64)
+    n, d = x.shape
+    Z = np.zeros((m, d))
+    its = lib().orc_fitc_inducing_points(_d(x), n, d, m, 0 if method == "kmeans++" else 1, seed, _d(Z))
+    if its < 0:
+        raise ValueError("invalid number of inducing points")
+    return Z, its
+
+
+def fitc_nll_grad(coords, y, Z, cov_type, pars_trafo, mode):
+    """FITC Gaussian nll + gradient (transformed scale; mode 0: with the nugget, 1: profiled)."""
+    x = np.ascontiguousarray(coords, dtype=np.float64)
+    z = np.ascontiguousarray(Z, dtype=np.float64)
+    yy = np.ascontiguousarray(y, dtype=np.float64)
+    p = np.ascontiguousarray(pars_trafo, dtype=np.float64)
+    nll, s2 = np.zeros(1), np.zeros(1)
+    g = np.zeros(3 if mode == 0 else 2)
+    rc = lib().orc_fitc_nll_grad(_d(x), _d(yy), x.shape[0], x.shape[1], _d(z), z.shape[0], cov_type, _d(p), mode,
+                                 _d(nll), _d(g), _d(s2))
+    if rc != 0:
+        raise ValueError("FITC factorization failed")
+    return {"nll": float(nll[0]), "grad": g, "sigma2": float(s2[0])}

@@ -153,6 +153,10 @@ int main(int argc, char** argv) {
   const int reps = std::atoi(get(args, "reps", "1").c_str());
   const int dump_nn = std::atoi(get(args, "dump_nn", "0").c_str());
   const std::string aux = get(args, "aux_pars", "");
+  // FITC (gp_approx = "fitc"): inducing points (re_model_template.h:6931-7073)
+  const int num_ind_points = std::atoi(get(args, "num_ind_points", "0").c_str());
+  const double cover_tree_radius = std::atof(get(args, "cover_tree_radius", "1").c_str());
+  const std::string ind_points_selection = get(args, "ind_points_selection", "kmeans++");
 
   Log::ResetLogLevelRE(LogLevelRE::Warning);
   auto t0 = std::chrono::steady_clock::now();
@@ -171,7 +175,7 @@ int main(int argc, char** argv) {
   std::unique_ptr<Model> m(new Model(
       n, nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr,
       1, coords.data(), d, nullptr, 0, cov_fct.c_str(), shape, gp_approx.c_str(),
-      -1., 0., num_neighbors, ordering.c_str(), 0, 1., "kmeans++",
+      -1., 0., num_neighbors, ordering.c_str(), num_ind_points, cover_tree_radius, ind_points_selection.c_str(),
       likelihood.c_str(), 0., mim.c_str(), seed, threads, false, false, nullptr, 1.));
 #endif
   auto t1 = std::chrono::steady_clock::now();
@@ -439,6 +443,14 @@ int main(int argc, char** argv) {
   std::printf("\"t_construct\": %.9g,\n", t_construct);
   if (gauss && gp_approx == "vecchia") {
     std::printf("\"yTPsiInvy\": %.17g, \"log_det_Psi\": %.17g,\n", m->yTPsiInvy_, m->log_det_Psi_);
+  }
+  if (gauss && gp_approx == "fitc") {
+    std::printf("\"yTPsiInvy\": %.17g, \"log_det_Psi\": %.17g,\n", m->yTPsiInvy_, m->log_det_Psi_);
+    const den_mat_t& ip = m->gp_coords_ip_mat_;
+    std::vector<double> ipv((size_t)ip.rows() * ip.cols());
+    for (int i = 0; i < (int)ip.rows(); ++i)
+      for (int q = 0; q < (int)ip.cols(); ++q) ipv[(size_t)i * ip.cols() + q] = ip(i, q);
+    print_vec("ind_points", ipv.data(), (int)ipv.size());
   }
   if ((gp_approx == "vecchia" || gp_approx == "vecchia_latent") && dump_nn) {
     const auto& perm = m->data_indices_per_cluster_[m->unique_clusters_[0]];

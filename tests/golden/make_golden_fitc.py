@@ -1,0 +1,109 @@
+#!/usr/bin/env python3
+"""Reference fixtures for the FITC approximation (gp_approx = "fitc", Gaussian likelihood), from the
+reference itself (oracle/_ref/ref_harness gp_approx=fitc): the inducing points its kmeans++ / random
+selection picks (CreateREComponentsFITC_FSA, re_model_template.h:6931-7073), the negative
+log-likelihood and gradient (mode eval: nugget included; mode lbfgs: sigma^2 profiled, the optimizer's
+unit), log det Psi and y^T Psi^-1 y, and fits (GPB_OptimCovPar). Build container only:
+
+    make -C oracle ref && python3 tests/golden/make_golden_fitc.py
+"""
+from __future__ import annotations
+
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+from make_golden import ROOT, fmt_pars, run_ref  # noqa: E402
+
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+
+from gpboost_amd import synthetic  # noqa: E402
+
+OUT = os.path.join(HERE, "golden_fitc.json")
+
+
+def case(n, m, cov_pars, cov_fct="exponential", shape=0.5, sel="kmeans++", seed=0, modes=("eval", "lbfgs")):
+    X = synthetic.bench_coords(n)
+    y = synthetic.bench_spatial_gaussian_y(X)
+    spec = dict(cov_fct=cov_fct, shape=str(shape), gp_approx="fitc", num_ind_points=m, ind_points_selection=sel,
+                seed=seed)
+    out = dict(n=n, m=m, cov_pars=list(cov_pars), spec=spec)
+    for mode in modes:
+        r = run_ref(X, y, cov_pars=fmt_pars(cov_pars), mode=mode, **spec)
+        out[mode] = dict(nll=r["nll"], grad=r["grad"], sigma2=r["sigma2"], log_det_Psi=r["log_det_Psi"],
+                         yTPsiInvy=r["yTPsiInvy"])
+        out["ind_points"] = r["ind_points"]
+        out["ref_time_s"] = r["median_time"]
+    return out
+
+
+def fit_case(n, m, cov_fct="exponential", shape=0.5):
+    X = synthetic.bench_coords(n)
+    y = synthetic.bench_spatial_gaussian_y(X)
+    spec = dict(cov_fct=cov_fct, shape=str(shape), gp_approx="fitc", num_ind_points=m)
+    r = run_ref(X, y, mode="fit", **spec)
+    return dict(n=n, m=m, spec=spec, **{k: r[k] for k in r if k not in ("ok", "n", "d")})
+
+
+def pred_case(n, m, npred, cov_pars, cov_fct="exponential", shape=0.5, cov=False, response=False, train_pts=0):
+    """Predictions (CalcPredFITC_FSA): new points from the prediction LCG stream; the first
+    `train_pts` prediction points are training coordinates (the FITC diagonal correction)."""
+    import tempfile
+    X = synthetic.bench_coords(n)
+    y = synthetic.bench_spatial_gaussian_y(X)
+    Xp = synthetic.lcg_unif(npred * 2, 0.713).reshape(2, npred).T.copy()
+    if train_pts:
+        Xp[:train_pts] = X[::max(1, n // train_pts)][:train_pts]
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(np.array([npred], dtype=np.int32).tobytes())
+        f.write(np.asfortranarray(Xp).T.astype(np.float64).tobytes())
+        ppath = f.name
+    spec = dict(cov_fct=cov_fct, shape=str(shape), gp_approx="fitc", num_ind_points=m)
+    extra = {"predict_cov": "1"} if cov else {"predict_var": "1"}
+    if response:
+        extra["predict_response"] = "1"
+    try:
+        r = run_ref(X, y, cov_pars=fmt_pars(cov_pars), mode="predict", pred=ppath, **spec, **extra)
+    finally:
+        os.unlink(ppath)
+    out = dict(n=n, m=m, npred=npred, cov_pars=list(cov_pars), spec=spec, response=response, train_pts=train_pts,
+               mean=r["mean"])
+    out["cov" if cov else "var"] = r["cov" if cov else "var"]
+    return out
+
+
+def main():
+    cases = {
+        "fitc_exp_n2000_m50": case(2000, 50, (0.1, 1.0, 0.1)),
+        "fitc_matern15_n3000_m100": case(3000, 100, (0.05, 1.2, 0.15), cov_fct="matern", shape=1.5),
+        "fitc_gauss_n2500_m80_random": case(2500, 80, (0.2, 0.8, 0.2), cov_fct="gaussian", shape=0.0, sel="random",
+                                            seed=3),
+        "fitc_matern25_n4000_m300": case(4000, 300, (0.1, 1.0, 0.1), cov_fct="matern", shape=2.5, seed=7),
+        "fitc_exp_n20000_m500": case(20000, 500, (0.1, 1.0, 0.1), modes=("lbfgs",)),
+    }
+    fits = {
+        "fit_fitc_exp_n2000_m50": fit_case(2000, 50),
+        "fit_fitc_matern15_n3000_m100": fit_case(3000, 100, cov_fct="matern", shape=1.5),
+    }
+    for k, v in cases.items():
+        print(k, {mm: (v[mm]["nll"], v[mm]["grad"]) for mm in ("eval", "lbfgs") if mm in v}, v["ref_time_s"],
+              file=sys.stderr)
+    for k, v in fits.items():
+        print(k, v["cov_pars"], v["nll"], v["num_it"], file=sys.stderr)
+    cases.update(fits)
+    cases.update({
+        "pred_fitc_exp_var": pred_case(2000, 50, 300, (0.1, 1.0, 0.1)),
+        "pred_fitc_exp_var_resp": pred_case(2000, 50, 300, (0.1, 1.0, 0.1), response=True),
+        "pred_fitc_matern15_cov": pred_case(1500, 60, 100, (0.05, 1.2, 0.15), cov_fct="matern", shape=1.5, cov=True),
+        "pred_fitc_train_pts_var": pred_case(2000, 50, 200, (0.1, 1.0, 0.1), train_pts=60),
+        "pred_fitc_train_pts_cov": pred_case(2000, 50, 80, (0.1, 1.0, 0.1), cov=True, response=True, train_pts=30),
+    })
+    with open(OUT, "w") as f:
+        json.dump(cases, f)
+
+
+if __name__ == "__main__":
+    main()
