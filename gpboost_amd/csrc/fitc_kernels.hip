@@ -680,7 +680,9 @@ void FitcSolver::Predict(int cov_type, double var, double phi, const double* d_y
       pairs.push_back(match[i]);
     }
   const int npairs = (int)pairs.size() / 2;
-  const double sii = var * kJitterMult;   // sigma_ip_stable(0, 0)
+  // sigma_ip_stable(0, 0) of CalcPredFITC_FSA: GetZSigmaZt() without the jitter multiplier here
+  // (re_model_template.h:10624, 10645, 10746)
+  const double sii = var;
   DevBuf<double> Maux, corr;
   std::vector<double> h_corr(npairs), h_yaux, h_d;
   if (npairs > 0 || want_var || want_cov) {

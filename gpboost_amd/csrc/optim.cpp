@@ -184,12 +184,16 @@ double REModelAMD::InitialRangeTrafo() const {
   // Vecchia_utils.cpp:1094-1095).
   // the GP component's coordinates: all points, or the unique locations of a latent model with
   // repeated coordinates (RECompGP::coords_, re_comp.h:1232-1244)
-  const int d = cfg_.d, n = (int)(coords_vo_.size() / d);
+  // FITC: the inducing points' component (re_comps_ip_, re_model_template.h:4474-4476), the draws
+  // continuing the generator after the inducing-point selection
+  const std::vector<double>& X = fitc_ ? fitc_->inducing_points() : coords_vo_;
+  const int d = cfg_.d, n = (int)(X.size() / d);
   const int kMaxPoints = 1000;
   const int nf = std::min(n, kMaxPoints);
   std::vector<int> idx(nf);
   if (nf < n) {
     std::mt19937 rng(cfg_.seed);
+    if (fitc_) rng = fitc_rng_;
     if (vecchia_ && cfg_.vecchia_ordering == "random") {   // the ordering shuffle of the n observations
       std::vector<int> dummy(cfg_.n);
       std::iota(dummy.begin(), dummy.end(), 0);
@@ -200,7 +204,6 @@ double REModelAMD::InitialRangeTrafo() const {
   } else {
     std::iota(idx.begin(), idx.end(), 0);
   }
-  const std::vector<double>& X = coords_vo_;   // the GP component's coordinates (Vecchia order)
   std::vector<double> dist((size_t)nf * (nf - 1) / 2);
   size_t p = 0;
   for (int i = 0; i < nf - 1; ++i)

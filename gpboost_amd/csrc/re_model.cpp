@@ -162,6 +162,7 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
       unique_locations(Z.data(), cfg_.num_ind_points, d, zu, zi);
       if ((int)zu.size() < cfg_.num_ind_points) Fatal("Duplicates found in inducing points / low-dimensional knots ");
       fitc_.reset(new FitcSolver(n, d, d_X_.get(), Z, stream_));
+      fitc_rng_ = rng;
     } else {
       dense_.reset(new DenseSolver(n, d, d_X_.get(), stream_));
     }

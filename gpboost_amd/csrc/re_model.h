@@ -257,6 +257,7 @@ class REModelAMD {
 
   std::unique_ptr<DenseSolver> dense_;
   std::unique_ptr<FitcSolver> fitc_;   // gp_approx = "fitc" (Gaussian likelihood)
+  std::mt19937 fitc_rng_;              // the model's generator after the inducing-point selection
   std::unique_ptr<LatentVecchia> latent_;
   std::vector<double> y_vo_;          // host copy (Vecchia order) for the latent solver
   std::vector<double> aux_pars_;

@@ -1,4 +1,5 @@
 #!/bin/bash
+export GPBOOST_AMD_BENCH_FAST_EXIT=0   # bench.py: normal exit so the tracer writes its results
 # GPU box: does rocprofv3 --kernel-trace survive the latent path's hipGraph replay (the default
 # launch path)? One profiled latent evaluation without GPBOOST_AMD_NO_GRAPH; the exit status and
 # the log tail go to gpurun_out/graph_trace/result.txt. Run it LAST in a call (a crash ends the call).

@@ -1,4 +1,5 @@
 #!/bin/bash
+export GPBOOST_AMD_BENCH_FAST_EXIT=0   # bench.py: normal exit so the tracer writes its results
 # GPU-box: kernel trace + PMC passes (one counter group per run) of a short latent evaluation
 # (n = 100k, CG capped at 20 iterations) and of a short exact-Vecchia bench run.
 set -o pipefail

@@ -1,4 +1,5 @@
 #!/bin/bash
+export GPBOOST_AMD_BENCH_FAST_EXIT=0   # bench.py: normal exit so the tracer writes its results
 # PMC passes (one counter group per run) of a short latent evaluation with the current operator
 # kernels (gaussian vecchia_latent, n = 100k, CG capped at 20 iterations; eager launches: the
 # mode-4 graph path crashed rocprofv3 on this image)

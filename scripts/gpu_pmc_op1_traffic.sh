@@ -1,4 +1,5 @@
 #!/bin/bash
+export GPBOOST_AMD_BENCH_FAST_EXIT=0   # bench.py: normal exit so the tracer writes its results
 # GPU box: HBM-side traffic of the single-vector operator kernels (scripts/prof_op1.py):
 # FETCH_SIZE and WRITE_SIZE in separate rocprofv3 passes (they cannot share one pass on gfx950).
 set -o pipefail

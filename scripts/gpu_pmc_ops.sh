@@ -1,4 +1,5 @@
 #!/bin/bash
+export GPBOOST_AMD_BENCH_FAST_EXIT=0   # bench.py: normal exit so the tracer writes its results
 # GPU box: HBM-side traffic (rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE, separate passes) of the
 # latent operator and VADU preconditioner kernels as the bench times them (scripts/prof_op1.py ->
 # GPB_BenchLatentOperators(T, 20), eager launches), for t = 1 and t = 51 columns. The raw counter

@@ -1,4 +1,5 @@
 #!/bin/bash
+export GPBOOST_AMD_BENCH_FAST_EXIT=0   # bench.py: normal exit so the tracer writes its results
 # GPU box: two PMC passes (SQ counters) over the exact Vecchia bench (row kernel), each its own run.
 set -o pipefail
 R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"

@@ -1,4 +1,5 @@
 #!/bin/bash
+export GPBOOST_AMD_BENCH_FAST_EXIT=0   # bench.py: normal exit so the tracer writes its results
 # GPU box: HBM traffic of the exact-path row kernel — FETCH_SIZE and WRITE_SIZE in separate
 # rocprofv3 --pmc passes over the bench command — written as profiles-style JSON for bench.py.
 set -o pipefail

@@ -1,4 +1,5 @@
 #!/bin/bash
+export GPBOOST_AMD_BENCH_FAST_EXIT=0   # bench.py: normal exit so the tracer writes its results
 # GPU box: the round's profile set for the current kernels — row-kernel HBM traffic passes
 # (gpu_pmc_rows_traffic.sh), row-kernel SQ passes (gpu_pmc_rows.sh) and a rocprofv3 kernel trace of
 # the full bench with the latent preconditioner launched eagerly (GPBOOST_AMD_NO_GRAPH=1: under

@@ -37,6 +37,7 @@ done
 unset GPBOOST_AMD_VARIANT
 if [ -n "${TRACE:-}" ]; then   # the full bench (graph replay on) under the kernel tracer, last: a crash ends the call
   export TMPDIR=/tmp
+  export GPBOOST_AMD_BENCH_FAST_EXIT=0   # the tracer writes its results at normal process exit
   for kv in ${TRACE_ENV:-}; do export "$kv"; done
   timeout -k 10 500 rocprofv3 --kernel-trace --stats -d gpurun_out/trace_${TAG:-x} -o trace -- \
     python bench.py --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/r04_trace_${TAG:-x}.log 2>&1

@@ -67,6 +67,8 @@ def test_fitc_fit_matches_reference(name):
     X, y = _data(case)
     gm = _model(case, X)
     gm.fit(y)
+    # FindInitCovPar on the inducing points (re_model_template.h:4474-4476)
+    np.testing.assert_allclose(gm.get_init_cov_pars(), case["init_cov_pars"], rtol=1e-12)
     assert gm.get_num_optim_iter() == case["num_it"]
     np.testing.assert_allclose(gm.get_cov_pars(), case["cov_pars"], rtol=1e-6)
     assert abs(gm.get_current_neg_log_likelihood() - case["nll"]) <= 1e-9 * abs(case["nll"])
