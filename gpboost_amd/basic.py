@@ -84,7 +84,7 @@ def _as1d(x, name: str) -> np.ndarray:
 class GPModel:
     """Gaussian process model (reference ``gpboost.GPModel``), likelihood evaluation subset."""
 
-    _SUPPORTED_APPROX = ("none", "vecchia", "vecchia_latent")
+    _SUPPORTED_APPROX = ("none", "vecchia", "vecchia_latent", "fitc")
 
     def __init__(self, likelihood="gaussian", group_data=None, group_rand_coef_data=None,
                  ind_effect_group_rand_coef=None, drop_intercept_group_rand_effect=None, gp_coords=None,

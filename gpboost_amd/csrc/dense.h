@@ -27,6 +27,10 @@ class DenseSolver {
   void Gram(int cov_type, double var, double phi, const double* Z, int c, double* G);
   // Psi^-1 y and diag(Psi^-1) (host, n each) for the training-data random-effect predictions.
   void PsiInvDiag(int cov_type, double var, double phi, const double* d_y, double* yaux, double* diag);
+  // Predictions at np new points (host row-major Xp): mean, latent variances (nullable) and the latent
+  // covariance (column-major np x np, nullable) on the transformed scale (before sigma^2 / nugget)
+  void Predict(int cov_type, double var, double phi, const double* d_y, const double* Xp, int np, bool want_var,
+               bool want_cov, double* mean, double* pvar, double* pcov);
 
  private:
   void Potrf();
@@ -70,6 +74,24 @@ void chol_lower(hipStream_t s, double* A, double* W, int n, int ld, int* info);
 void trtri_lower(hipStream_t s, const double* L, double* W, double* X, int a, int b, int ld);
 // out[0] = 2 sum_i log L_ii (one block, fixed order)
 void launch_logdet_chol(hipStream_t s, const double* L, int ld, int n, double* out);
+
+// Dense SPD system of order n on the GPU (host column-major A): x = A^-1 b (b, x nullable),
+// diag(A^-1) (nullable), the full A^-1 column-major (nullable). Fails if A is not positive definite.
+void spd_solve_inverse(hipStream_t s, int n, const double* A, const double* b, double* x, double* diag, double* inv);
+
+// Gaussian prediction through a dense Vecchia approximation of the latent process over N points
+// (observed first: n, then np = N - n prediction points): B (host column-major N x N, unit lower),
+// D (N) -> Sigma = B^-1 diag(D) B^-T; mean = Sigma_po (Sigma_oo + I)^-1 y, cov = Sigma_pp -
+// Sigma_po (Sigma_oo + I)^-1 Sigma_op (variances its diagonal). Transformed scale (nugget 1).
+void vecchia_latent_dense_pred(hipStream_t s, int N, int n, const double* B, const double* D, const double* y,
+                               bool want_var, bool want_cov, double* mean, double* var, double* cov);
+
+// Latent-model predictive moments from nsim simulation draws (PredictLaplaceApproxVecchia,
+// likelihoods.h:6713-6749): d_V (device np x nsim column-major) = Bpo z per draw; Bp (host dense np x np
+// unit lower, nullable = identity for cond_obs_only): U = Bp^-1 V, var = rowsum(U^2) / nsim +
+// diag(Bp^-1 diag(Dp) Bp^-T), cov = U U^T / nsim + Bp^-1 diag(Dp) Bp^-T (column-major).
+void latent_pred_moments(hipStream_t s, int np, const double* Bp, const double* Dp, const double* d_V, int nsim,
+                         bool want_var, bool want_cov, double* var, double* cov);
 
 // host helper shared by all paths (re_model.cpp)
 void combine_partials(const double* s, int n, double sigma2_in, int profile, double* nll, double* grad,

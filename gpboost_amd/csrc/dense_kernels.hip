@@ -386,6 +386,25 @@ __global__ void __launch_bounds__(64) potrf_diag_wave_kernel(double* A, int lda,
     if (i < ib && r < ib) Winv[(size_t)(j0 + i) + (size_t)(j0 + r) * ldw] = (r <= i) ? x[i] : 0.;
 }
 
+// Cross-covariance C[i + p ld] = cov(|x_i - xp_p|) (n x np, column-major) and, when S is non-null,
+// the prediction points' own covariance S[p + q np] (np x np, diagonal = var)
+template <int COV>
+__global__ void __launch_bounds__(256) build_cross_kernel(const double* __restrict__ X, const double* __restrict__ Xp,
+                                                          int n, int np, int d, int ld, double var, double phi,
+                                                          double* __restrict__ C) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int p = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= n || p >= np) return;
+  double s = 0.;
+  for (int q = 0; q < d; ++q) {
+    const double t = X[(size_t)i * d + q] - Xp[(size_t)p * d + q];
+    s += t * t;
+  }
+  double c, dc;
+  if (s == 0. && X == Xp && i == p) { c = var; } else { cov_dcov<COV>(sqrt(s), var, phi, c, dc); }
+  C[(size_t)i + (size_t)p * ld] = c;
+}
+
 // 2 * sum log L_ii -> out (single block, fixed order)
 __global__ void __launch_bounds__(256) logdet_kernel(const double* A, int lda, int n, double* out) {
   __shared__ double red[256];
@@ -592,6 +611,67 @@ __global__ void __launch_bounds__(256) colnorm2_lower_kernel(const double* W, in
   if (lane == 0) diag[j] = s;
 }
 
+// Inverses of the 64 x 64 diagonal blocks of a UNIT lower-triangular matrix (one wave per block, lane
+// c = column c of the block inverse by forward substitution in LDS) into W's diagonal blocks (upper
+// part zero), the input trtri_lower expects.
+__global__ void __launch_bounds__(64) unit_lower_diag_inv_kernel(const double* A, int lda, int n, double* W, int ldw) {
+  // column r of the inverse kept in LDS (X[i][r]), the block's L broadcast from LDS
+  __shared__ double Ls[64][65];
+  __shared__ double X[64][65];
+  const int j0 = blockIdx.x * 64, ib = min(64, n - j0);
+  const int r = threadIdx.x;
+  for (int c = 0; c < 64; ++c)
+    Ls[r][c] = (r < ib && c < ib && c < r) ? A[(size_t)(j0 + r) + (size_t)(j0 + c) * lda] : 0.;
+  __syncthreads();
+  for (int i = 0; i < 64; ++i) {
+    double s = (i == r) ? 1. : 0.;
+    for (int p = r; p < i; ++p) s -= Ls[i][p] * X[p][r];
+    X[i][r] = (i >= r && i < ib) ? s : 0.;
+  }
+  for (int i = 0; i < ib; ++i)
+    if (r < ib) W[(size_t)(j0 + i) + (size_t)(j0 + r) * ldw] = (r <= i) ? X[i][r] : 0.;
+}
+
+// A[:, j] *= d[j] for j < n (rows < m)
+__global__ void __launch_bounds__(256) scale_cols_kernel(double* A, int lda, int m, int n, const double* d) {
+  const int i = blockIdx.x * 256 + threadIdx.x, j = blockIdx.y;
+  if (i < m && j < n) A[(size_t)i + (size_t)j * lda] *= d[j];
+}
+
+// A[i, i] += v for i < n
+__global__ void __launch_bounds__(256) add_diag_kernel(double* A, int lda, int n, double v) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) A[(size_t)i + (size_t)i * lda] += v;
+}
+
+// out[i] = sum_c U[i + c ld]^2 / nsim + add[i] (fixed column order)
+__global__ void __launch_bounds__(256) rowsq_kernel(const double* U, int ld, int n, int nsim, const double* add,
+                                                   double* out) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  double s = 0.;
+  for (int c = 0; c < nsim; ++c) {
+    const double u = U[(size_t)i + (size_t)c * ld];
+    s += u * u;
+  }
+  out[i] = s / nsim + add[i];
+}
+
+// out[p] = sum_i T[i + p ld]^2 for i < n (one wave per column)
+__global__ void __launch_bounds__(256) colnorm2_full_kernel(const double* T, int ld, int n, int np, double* out) {
+  const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (p >= np) return;
+  double s = 0.;
+  for (int i = lane; i < n; i += 64) {
+    const double t = T[(size_t)i + (size_t)p * ld];
+    s += t * t;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
+  if (lane == 0) out[p] = s;
+}
+
 __global__ void dot_kernel(const double* a, const double* b, int n, double* out) {
   __shared__ double red[256];
   double s = 0.;
@@ -742,6 +822,165 @@ void launch_logdet_chol(hipStream_t s, const double* L, int ld, int n, double* o
 }
 
 void DenseSolver::Potrf() { chol_lower(stream_, A_.get(), W_.get(), n_, ld_, info_.get()); }
+
+void vecchia_latent_dense_pred(hipStream_t s, int N, int n, const double* B, const double* D, const double* y,
+                               bool want_var, bool want_cov, double* mean, double* var, double* cov) {
+  // Sigma = B^-1 diag(D) B^-T over all N points (observed first), then the Gaussian conditional of
+  // the last np = N - n points given y = (latent at the observed points) + N(0, I):
+  //   mean = Sigma_po (Sigma_oo + I)^-1 y,  cov = Sigma_pp - Sigma_po (Sigma_oo + I)^-1 Sigma_op
+  const int np = N - n;
+  if (np <= 0 || n <= 0) Fatal("vecchia_latent_dense_pred: empty observed or prediction set");
+  const int ld = (N + 63) / 64 * 64, ldo = (n + 63) / 64 * 64;
+  const size_t NN = (size_t)ld * ld;
+  DevBuf<double> dB(NN), W(NN), S(NN), T((size_t)ld * (ld / 2 + 64)), dD(N), Aoo((size_t)ldo * ldo),
+      Woo((size_t)ldo * ldo), v((size_t)3 * ldo), Tm((size_t)ldo * np);
+  DevBuf<int> info(1);
+  HIP_CHECK(hipMemsetAsync(W.get(), 0, NN * sizeof(double), s));
+  HIP_CHECK(hipMemsetAsync(Woo.get(), 0, (size_t)ldo * ldo * sizeof(double), s));
+  HIP_CHECK(hipMemsetAsync(info.get(), 0, sizeof(int), s));
+  HIP_CHECK(hipMemcpy2DAsync(dB.get(), sizeof(double) * ld, B, sizeof(double) * N, sizeof(double) * N, N,
+                             hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(dD.get(), D, sizeof(double) * N, hipMemcpyHostToDevice, s));
+  // W = B^-1 (unit lower: diagonal-block inverses, then the recursive TRTRI)
+  hipLaunchKernelGGL(unit_lower_diag_inv_kernel, dim3((N + 63) / 64), dim3(64), 0, s, dB.get(), ld, N, W.get(), ld);
+  trtri_lower(s, dB.get(), W.get(), T.get(), 0, N, ld);
+  // S = (W diag(D)) W^T
+  HIP_CHECK(hipMemcpyAsync(dB.get(), W.get(), NN * sizeof(double), hipMemcpyDeviceToDevice, s));
+  hipLaunchKernelGGL(scale_cols_kernel, dim3((N + 255) / 256, N), dim3(256), 0, s, dB.get(), ld, N, N, dD.get());
+  gemm(s, N, N, N, 1., dB.get(), ld, 0, W.get(), ld, 1, 0., S.get(), ld, 0, 1, 0, 0);
+  // Aoo = Sigma_oo + I = L L^T, Woo = L^-1
+  HIP_CHECK(hipMemcpy2DAsync(Aoo.get(), sizeof(double) * ldo, S.get(), sizeof(double) * ld, sizeof(double) * n, n,
+                             hipMemcpyDeviceToDevice, s));
+  hipLaunchKernelGGL(add_diag_kernel, dim3((n + 255) / 256), dim3(256), 0, s, Aoo.get(), ldo, n, 1.);
+  chol_lower(s, Aoo.get(), Woo.get(), n, ldo, info.get());
+  trtri_lower(s, Aoo.get(), Woo.get(), T.get(), 0, n, ldo);
+  // mean = Sigma_po Woo^T Woo y
+  double* dy = v.get();
+  double* z = dy + ldo;
+  double* x = z + ldo;
+  HIP_CHECK(hipMemcpyAsync(dy, y, sizeof(double) * n, hipMemcpyHostToDevice, s));
+  gemm(s, n, 1, n, 1., Woo.get(), ldo, 0, dy, ldo, 0, 0., z, ldo, 0, 1, 0, 0);
+  hipLaunchKernelGGL(trmv_lower_t_kernel, dim3((n + 3) / 4), dim3(256), 0, s, Woo.get(), ldo, n, z, x);
+  DevBuf<double> dm(np);
+  gemm(s, np, 1, n, 1., S.get() + n, ld, 0, x, ldo, 0, 0., dm.get(), np);
+  HIP_CHECK(hipMemcpyAsync(mean, dm.get(), sizeof(double) * np, hipMemcpyDeviceToHost, s));
+  if (want_var || want_cov) {
+    // Tm = Woo Sigma_op (n x np); cov = Sigma_pp - Tm^T Tm
+    gemm(s, n, np, n, 1., Woo.get(), ldo, 0, S.get() + (size_t)n * ld, ld, 0, 0., Tm.get(), ldo, 0, 1, 0, 0);
+    DevBuf<double> C((size_t)np * np);
+    HIP_CHECK(hipMemcpy2DAsync(C.get(), sizeof(double) * np, S.get() + n + (size_t)n * ld, sizeof(double) * ld,
+                               sizeof(double) * np, np, hipMemcpyDeviceToDevice, s));
+    gemm(s, np, np, n, -1., Tm.get(), ldo, 1, Tm.get(), ldo, 0, 1., C.get(), np);
+    std::vector<double> h((size_t)np * np);
+    HIP_CHECK(hipMemcpyAsync(h.data(), C.get(), sizeof(double) * h.size(), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (want_cov) std::copy(h.begin(), h.end(), cov);
+    if (want_var)
+      for (int p = 0; p < np; ++p) var[p] = h[(size_t)p * np + p];
+  }
+  HIP_CHECK(hipGetLastError());
+  int h_info = 0;
+  HIP_CHECK(hipMemcpyAsync(&h_info, info.get(), sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  if (h_info != 0) Fatal("the observed covariance plus nugget is not positive definite (Cholesky failed)");
+}
+
+void latent_pred_moments(hipStream_t s, int np, const double* Bp, const double* Dp, const double* d_V, int nsim,
+                         bool want_var, bool want_cov, double* var, double* cov) {
+  // W = Bp^-1 (identity when Bp is null), U = W V; var = rowsum(U^2) / nsim + diag(W diag(Dp) W^T);
+  // cov = U U^T / nsim + W diag(Dp) W^T (PredictLaplaceApproxVecchia, likelihoods.h:6713-6749)
+  const int ld = (np + 63) / 64 * 64;
+  const size_t NN = (size_t)ld * ld;
+  DevBuf<double> W, dB, T, U, dD(np), det(np), out(np);
+  HIP_CHECK(hipMemcpyAsync(dD.get(), Dp, sizeof(double) * np, hipMemcpyHostToDevice, s));
+  const double* Uptr = d_V;
+  int ldu = np;
+  if (Bp != nullptr) {
+    W.alloc(NN);
+    dB.alloc(NN);
+    T.alloc((size_t)ld * (ld / 2 + 64));
+    U.alloc((size_t)ld * nsim);
+    HIP_CHECK(hipMemsetAsync(W.get(), 0, NN * sizeof(double), s));
+    HIP_CHECK(hipMemcpy2DAsync(dB.get(), sizeof(double) * ld, Bp, sizeof(double) * np, sizeof(double) * np, np,
+                               hipMemcpyHostToDevice, s));
+    hipLaunchKernelGGL(unit_lower_diag_inv_kernel, dim3((np + 63) / 64), dim3(64), 0, s, dB.get(), ld, np, W.get(), ld);
+    trtri_lower(s, dB.get(), W.get(), T.get(), 0, np, ld);
+    gemm(s, np, nsim, np, 1., W.get(), ld, 0, d_V, np, 0, 0., U.get(), ld, 0, 1, 0, 0);
+    Uptr = U.get();
+    ldu = ld;
+  }
+  DevBuf<double> WD, C;
+  if (Bp != nullptr && (want_var || want_cov)) {
+    WD.alloc(NN);   // W diag(Dp)
+    HIP_CHECK(hipMemcpyAsync(WD.get(), W.get(), NN * sizeof(double), hipMemcpyDeviceToDevice, s));
+    hipLaunchKernelGGL(scale_cols_kernel, dim3((np + 255) / 256, np), dim3(256), 0, s, WD.get(), ld, np, np, dD.get());
+  }
+  if (want_var) {
+    if (Bp != nullptr) {   // diag(W diag(Dp) W^T)_i = sum_k W_ik^2 Dp_k = rowsum(W diag(sqrt Dp))^2: by the GEMM
+      C.alloc(NN);
+      gemm(s, np, np, np, 1., WD.get(), ld, 0, W.get(), ld, 1, 0., C.get(), ld, 0, 1, 0, 0);
+      HIP_CHECK(hipMemcpy2DAsync(det.get(), sizeof(double), C.get(), sizeof(double) * (ld + 1), sizeof(double), np,
+                                 hipMemcpyDeviceToDevice, s));
+    } else {
+      HIP_CHECK(hipMemcpyAsync(det.get(), dD.get(), sizeof(double) * np, hipMemcpyDeviceToDevice, s));
+    }
+    hipLaunchKernelGGL(rowsq_kernel, dim3((np + 255) / 256), dim3(256), 0, s, Uptr, ldu, np, nsim, det.get(), out.get());
+    HIP_CHECK(hipMemcpyAsync(var, out.get(), sizeof(double) * np, hipMemcpyDeviceToHost, s));
+  }
+  if (want_cov) {
+    DevBuf<double> Cv((size_t)np * np);
+    if (Bp != nullptr) {
+      gemm(s, np, np, np, 1., WD.get(), ld, 0, W.get(), ld, 1, 0., Cv.get(), np, 0, 1, 0, 0);
+    } else {
+      HIP_CHECK(hipMemsetAsync(Cv.get(), 0, sizeof(double) * np * np, s));
+      HIP_CHECK(hipMemcpy2DAsync(Cv.get(), sizeof(double) * (np + 1), dD.get(), sizeof(double), sizeof(double), np,
+                                 hipMemcpyDeviceToDevice, s));
+    }
+    gemm(s, np, np, nsim, 1. / nsim, Uptr, ldu, 0, Uptr, ldu, 1, 1., Cv.get(), np);
+    HIP_CHECK(hipMemcpyAsync(cov, Cv.get(), sizeof(double) * np * np, hipMemcpyDeviceToHost, s));
+  }
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipStreamSynchronize(s));
+}
+
+void spd_solve_inverse(hipStream_t s, int n, const double* A, const double* b, double* x, double* diag, double* inv) {
+  // A = L L^T (POTRF), W = L^-1 (TRTRI), x = W^T (W b), diag(A^-1) = column norms^2 of W,
+  // A^-1 = W^T W (MFMA GEMM)
+  if (n <= 0) return;
+  const int ld = (n + 63) / 64 * 64;
+  const size_t nn = (size_t)ld * ld;
+  DevBuf<double> dA(nn), dW(nn), T((size_t)ld * (ld / 2 + 64)), v((size_t)3 * ld);
+  DevBuf<int> info(1);
+  HIP_CHECK(hipMemsetAsync(dW.get(), 0, nn * sizeof(double), s));
+  HIP_CHECK(hipMemsetAsync(info.get(), 0, sizeof(int), s));
+  HIP_CHECK(hipMemcpy2DAsync(dA.get(), sizeof(double) * ld, A, sizeof(double) * n, sizeof(double) * n, n,
+                             hipMemcpyHostToDevice, s));
+  chol_lower(s, dA.get(), dW.get(), n, ld, info.get());
+  trtri_lower(s, dA.get(), dW.get(), T.get(), 0, n, ld);
+  double* db = v.get();
+  double* z = db + ld;
+  double* dx = z + ld;
+  if (b != nullptr) {
+    HIP_CHECK(hipMemcpyAsync(db, b, sizeof(double) * n, hipMemcpyHostToDevice, s));
+    gemm(s, n, 1, n, 1., dW.get(), ld, 0, db, ld, 0, 0., z, ld, 0, 1, 0, 0);                          // z = W b
+    hipLaunchKernelGGL(trmv_lower_t_kernel, dim3((n + 3) / 4), dim3(256), 0, s, dW.get(), ld, n, z, dx);  // W^T z
+    HIP_CHECK(hipMemcpyAsync(x, dx, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+  }
+  if (diag != nullptr) {
+    hipLaunchKernelGGL(colnorm2_lower_kernel, dim3((n + 3) / 4), dim3(256), 0, s, dW.get(), ld, n, z);
+    HIP_CHECK(hipMemcpyAsync(diag, z, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+  }
+  if (inv != nullptr) {
+    gemm(s, n, n, n, 1., dW.get(), ld, 1, dW.get(), ld, 0, 0., dA.get(), ld, 0, 0, 1, 1);   // full W^T W
+    HIP_CHECK(hipMemcpy2DAsync(inv, sizeof(double) * n, dA.get(), sizeof(double) * ld, sizeof(double) * n, n,
+                               hipMemcpyDeviceToHost, s));
+  }
+  HIP_CHECK(hipGetLastError());
+  int h_info = 0;
+  HIP_CHECK(hipMemcpyAsync(&h_info, info.get(), sizeof(int), hipMemcpyDeviceToHost, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  if (h_info != 0) Fatal("matrix is not positive definite (Cholesky failed)");
+}
 
 // The same factorization with one panel of lookahead: after panel J's inner steps, the trailing
 // update is split into the next panel's columns (on the chain stream, immediately) and the rest
@@ -920,6 +1159,41 @@ void DenseSolver::Factor(int cov_type, double var, double phi) {
   HIP_CHECK(hipGetLastError());
   PotrfLookahead();
   Trtri(0, n);
+}
+
+void DenseSolver::Predict(int cov_type, double var, double phi, const double* d_y, const double* Xp, int np,
+                          bool want_var, bool want_cov, double* mean, double* pvar, double* pcov) {
+  // CalcPred (re_model_template.h CalcPred, gp_approx = "none", Gaussian): with Psi = L L^T, W = L^-1,
+  // T = W Sigma_op: mean = T^T (W y), cov = Sigma_pp - T^T T (variances: var - column norms of T)
+  const int n = n_, ld = ld_, d = d_;
+  Factor(cov_type, var, phi);
+  DevBuf<double> dXp((size_t)np * d), C((size_t)ld * np), T((size_t)ld * np), z(ld), m(np), v(np);
+  HIP_CHECK(hipMemcpyAsync(dXp.get(), Xp, sizeof(double) * np * d, hipMemcpyHostToDevice, stream_));
+  dispatch_cov(cov_type, [&](auto c) {
+    hipLaunchKernelGGL((build_cross_kernel<decltype(c)::value>), dim3((n + 63) / 64, (np + 3) / 4), dim3(256), 0,
+                       stream_, d_X_, dXp.get(), n, np, d, ld, var, phi, C.get());
+  });
+  HIP_CHECK(hipGetLastError());
+  gemm(stream_, n, np, n, 1., W_.get(), ld, 0, C.get(), ld, 0, 0., T.get(), ld, 0, 1, 0, 0);
+  gemm(stream_, n, 1, n, 1., W_.get(), ld, 0, d_y, ld, 0, 0., z.get(), ld, 0, 1, 0, 0);
+  gemm(stream_, np, 1, n, 1., T.get(), ld, 1, z.get(), ld, 0, 0., m.get(), np);
+  HIP_CHECK(hipMemcpyAsync(mean, m.get(), sizeof(double) * np, hipMemcpyDeviceToHost, stream_));
+  if (want_var) {
+    hipLaunchKernelGGL(colnorm2_full_kernel, dim3((np + 3) / 4), dim3(256), 0, stream_, T.get(), ld, n, np, v.get());
+    HIP_CHECK(hipMemcpyAsync(pvar, v.get(), sizeof(double) * np, hipMemcpyDeviceToHost, stream_));
+  }
+  if (want_cov) {
+    DevBuf<double> S((size_t)np * np);
+    dispatch_cov(cov_type, [&](auto c) {
+      hipLaunchKernelGGL((build_cross_kernel<decltype(c)::value>), dim3((np + 63) / 64, (np + 3) / 4), dim3(256), 0,
+                         stream_, dXp.get(), dXp.get(), np, np, d, np, var, phi, S.get());
+    });
+    gemm(stream_, np, np, n, -1., T.get(), ld, 1, T.get(), ld, 0, 1., S.get(), np);
+    HIP_CHECK(hipMemcpyAsync(pcov, S.get(), sizeof(double) * np * np, hipMemcpyDeviceToHost, stream_));
+  }
+  CheckInfo();
+  if (want_var)
+    for (int p = 0; p < np; ++p) pvar[p] = var - pvar[p];
 }
 
 void DenseSolver::CheckInfo() {

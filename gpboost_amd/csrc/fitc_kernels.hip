@@ -146,23 +146,28 @@ __global__ void __launch_bounds__(256) fitc_gemv_part_kernel(const double* __res
   }
 }
 
+// out[j] = sum_b part[b][j]: one wave per j, lane-strided partials, fixed-order wave sum
 __global__ void __launch_bounds__(256) fitc_gemv_reduce_kernel(const double* __restrict__ part, int nb, int m, int ldm,
                                                                double* __restrict__ out) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (j >= m) return;
   double s = 0.;
-  for (int b = 0; b < nb; ++b) s += part[(size_t)b * ldm + j];
-  out[j] = s;
+  for (int b = lane; b < nb; b += 64) s += part[(size_t)b * ldm + j];
+  s = wave_sum(s);
+  if (lane == 0) out[j] = s;
 }
 
-// out = S x for a full m x m S
+// out = S x for a full symmetric m x m S: one wave per j over column j (contiguous)
 __global__ void __launch_bounds__(256) fitc_symv_kernel(const double* __restrict__ S, const double* __restrict__ x,
                                                         int m, int ldm, double* __restrict__ out) {
-  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (j >= m) return;
   double s = 0.;
-  for (int k = 0; k < m; ++k) s += S[(size_t)j + (size_t)k * ldm] * x[k];
-  out[j] = s;
+  for (int k = lane; k < m; k += 64) s += S[(size_t)k + (size_t)j * ldm] * x[k];
+  s = wave_sum(s);
+  if (lane == 0) out[j] = s;
 }
 
 // y_aux_i = y_i / d_i - (K_nm w)_i / d_i (re_model_template.h:8902-8907), block partial of y^T y_aux
@@ -521,7 +526,7 @@ FitcSolver::FitcSolver(int n, int d, const double* d_X, const std::vector<double
   const long tiles = (long)((m + 63) / 64) * ((m + 63) / 64);
   max_chunks_ = (int)std::max<long>(1, std::min<long>(2048 / tiles + 1, (n + 255) / 256));
   const int nb4 = (n + 3) / 4;
-  const int nbg = (n + 255) / 256;
+  const int nbg = (n + 63) / 64;
   part_.alloc(std::max<size_t>((size_t)max_chunks_ * mm, std::max<size_t>((size_t)nb4 * 4, (size_t)nbg * ldm)));
   // vec_: d, Dy, y_aux (n each), u, w, a (ldm each), mm-partials (6 per 4 columns)
   vec_.alloc((size_t)3 * n + 3 * ldm + (size_t)6 * ((m + 3) / 4));
@@ -576,11 +581,11 @@ void FitcSolver::Factor(int cov_type, double var, double phi, const double* d_y,
   trtri_lower(stream_, W_.get(), Wi_.get(), T_.get(), 0, m, ldm);
   gemm_f64(stream_, m, m, m, 1., Wi_.get(), ldm, 1, Wi_.get(), ldm, 0, 0., Winv_.get(), ldm, 0, 0, 1, 1);
   // u = K_mn (y / d), w = W^-1 u, y_aux, q
-  const int chunk = 256, nbg = (n + chunk - 1) / chunk;
+  const int chunk = 64, nbg = (n + chunk - 1) / chunk;
   hipLaunchKernelGGL(fitc_gemv_part_kernel, dim3(nbg), dim3(256), 0, stream_, Kmn_.get(), Dy, n, m, ldm, chunk,
                      part_.get());
-  hipLaunchKernelGGL(fitc_gemv_reduce_kernel, dim3((m + 255) / 256), dim3(256), 0, stream_, part_.get(), nbg, m, ldm, u);
-  hipLaunchKernelGGL(fitc_symv_kernel, dim3((m + 255) / 256), dim3(256), 0, stream_, Winv_.get(), u, m, ldm, w);
+  hipLaunchKernelGGL(fitc_gemv_reduce_kernel, dim3((m + 3) / 4), dim3(256), 0, stream_, part_.get(), nbg, m, ldm, u);
+  hipLaunchKernelGGL(fitc_symv_kernel, dim3((m + 3) / 4), dim3(256), 0, stream_, Winv_.get(), u, m, ldm, w);
   hipLaunchKernelGGL(fitc_yaux_kernel, dim3(nb4), dim3(256), 0, stream_, Kmn_.get(), w, d_y, Dy, dvec, n, m, ldm, yaux,
                      part_.get());
   HIP_CHECK(hipGetLastError());
@@ -603,10 +608,10 @@ void FitcSolver::Eval(int cov_type, double var, double phi, const double* d_y, b
     gemm_f64(stream_, m, n, m, 1., Li_.get(), ldm, 1, V_.get(), ldm, 0, 0., A_.get(), ldm, 0, 0, 1, 0);
     gemm_f64(stream_, m, n, m, 1., Winv_.get(), ldm, 0, Kmn_.get(), ldm, 0, 0., Kd_.get(), ldm);
     gemm_f64(stream_, m, n, m, 1., dKmm_.get(), ldm, 0, A_.get(), ldm, 0, 0., V_.get(), ldm);
-    const int chunk = 256, nbg = (n + chunk - 1) / chunk;
+    const int chunk = 64, nbg = (n + chunk - 1) / chunk;
     hipLaunchKernelGGL(fitc_gemv_part_kernel, dim3(nbg), dim3(256), 0, stream_, A_.get(), yaux, n, m, ldm, chunk,
                        part_.get());
-    hipLaunchKernelGGL(fitc_gemv_reduce_kernel, dim3((m + 255) / 256), dim3(256), 0, stream_, part_.get(), nbg, m, ldm, a);
+    hipLaunchKernelGGL(fitc_gemv_reduce_kernel, dim3((m + 3) / 4), dim3(256), 0, stream_, part_.get(), nbg, m, ldm, a);
     const int nb4 = (n + 3) / 4;
     const double delta = var * kJitterMult - var;
     dispatch_cov_fitc(cov_type, [&](auto c) {

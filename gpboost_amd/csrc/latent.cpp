@@ -512,13 +512,13 @@ void LatentVecchia::EnsureProbes(const IterativeConfig& cfg) {
 }
 
 void LatentVecchia::PredVarSim(int nsim, int t, double delta, int cg_max, uint64_t seed, int n_pred, int mp,
-                               const int* nbr_vo, const double* d_Bpo, double* acc) {
+                               const int* nbr_vo, const double* d_Bpo, double* acc, double* d_V) {
   if (!factor_ready_) Fatal("predictive variances need an evaluated latent model (mode and factor)");
   if (world_ > 1) Fatal("latent predictive variances are only available on single-rank models");
   t = std::max(1, std::min({t, nsim, 64}));
   // neighbour indices in storage labels (Z rows)
   std::vector<int> nb((size_t)n_pred * mp);
-  for (size_t e = 0; e < nb.size(); ++e) nb[e] = lab_[nbr_vo[e]];
+  for (size_t e = 0; e < nb.size(); ++e) nb[e] = nbr_vo[e] >= 0 && nbr_vo[e] < n_ ? lab_[nbr_vo[e]] : 0;
   DevBuf<int> d_nb(nb.size());
   DevBuf<double> d_acc(n_pred), d_sdi(n_), d_sw(n_), d_e1((size_t)n_ * t), d_e2((size_t)n_ * t), d_rhs((size_t)n_ * t),
       d_z((size_t)n_ * t);
@@ -541,9 +541,10 @@ void LatentVecchia::PredVarSim(int nsim, int t, double delta, int cg_max, uint64
     launch_bt_apply(sp_, d_Bv_.get(), true, d_e1.get(), t, d_sdi.get(), d_sw.get(), d_e2.get(), d_rhs.get(), s_);
     const PcgResult pr = Pcg(b, d_rhs.get(), d_z.get(), t, true, true, cg_max, 0, delta);
     if (pr.nan) Fatal("NaN or Inf in the conjugate gradient solves of the predictive-variance simulation");
-    launch_pred_sq_acc(n_pred, mp, t, d_nb.get(), d_Bpo, d_z.get(), d_acc.get(), s_);
+    if (acc) launch_pred_sq_acc(n_pred, mp, t, d_nb.get(), d_Bpo, d_z.get(), d_acc.get(), s_);
+    if (d_V) launch_pred_samples(n_pred, mp, t, tc, d_nb.get(), d_Bpo, d_z.get(), d_V, n_pred, done, s_);
   }
-  HIP_CHECK(hipMemcpyAsync(acc, d_acc.get(), sizeof(double) * n_pred, hipMemcpyDeviceToHost, s_));
+  if (acc) HIP_CHECK(hipMemcpyAsync(acc, d_acc.get(), sizeof(double) * n_pred, hipMemcpyDeviceToHost, s_));
   HIP_CHECK(hipStreamSynchronize(s_));
 }
 

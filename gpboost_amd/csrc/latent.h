@@ -105,8 +105,10 @@ class LatentVecchia {
   // as CGVecchiaLaplaceVec), t draws per block of independent columns; returns acc[p] = sum over the
   // draws of (Bpo z)_p^2 (host, n_pred). Uses the factor, W and preconditioner of the last Eval.
   // nbr_vo: host n_pred x mp neighbour indices (latent Vecchia rows), d_Bpo: device n_pred x mp.
+  // d_V (nullable, device n_pred x nsim column-major): the draws Bpo z themselves (predictive
+  // covariance, cond_all); acc (nullable) as before.
   void PredVarSim(int nsim, int t, double delta, int cg_max, uint64_t seed, int n_pred, int mp, const int* nbr_vo,
-                  const double* d_Bpo, double* acc);
+                  const double* d_Bpo, double* acc, double* d_V = nullptr);
 
   // Probe-column sharding (SURVEY.md §8e Option A): rank r of `world` runs the probe columns
   // [t r / world, t (r+1) / world) of every SLQ block — padded to ceil(t / world) columns, so

@@ -405,5 +405,8 @@ void launch_resp_logit(int n, const double* mean, const double* var, const doubl
                        double delta, double* out_mean, double* out_var, hipStream_t s);
 void launch_pred_sq_acc(int n_pred, int mp, int t, const int* nbr, const double* B, const double* Z, double* acc,
                         hipStream_t s);
+// V[p + (col0 + c) ldv] = sum_r B[p, r] Z[nbr[p, r], c] for columns c < tc of the t-column block
+void launch_pred_samples(int n_pred, int mp, int t, int tc, const int* nbr, const double* B, const double* Z, double* V,
+                         int ldv, int col0, hipStream_t s);
 
 }  // namespace gpb_amd

@@ -58,6 +58,21 @@ __global__ void __launch_bounds__(256) pred_sq_acc_kernel(int n_pred, int mp, in
   if (c == 0) acc[p] += q;
 }
 
+// The draws themselves (predictive covariance / cond_all): V[p + (col0 + c) * ldv] = sum_r B[p, r]
+// Z[nbr[p, r], c] for the tc valid columns of the block; one thread per (point, column).
+__global__ void __launch_bounds__(256) pred_samples_kernel(int n_pred, int mp, int t, int tc, const int* __restrict__ nbr,
+                                                           const double* __restrict__ B, const double* __restrict__ Z,
+                                                           double* __restrict__ V, int ldv, int col0) {
+  const int p = blockIdx.x * 256 + threadIdx.x, c = blockIdx.y;
+  if (p >= n_pred || c >= tc) return;
+  double s = 0.;
+  for (int r = 0; r < mp; ++r) {
+    const double b = B[(size_t)p * mp + r];
+    if (b != 0.) s = fma(b, Z[(size_t)nbr[(size_t)p * mp + r] * t + c], s);
+  }
+  V[(size_t)p + (size_t)(col0 + c) * ldv] = s;
+}
+
 __device__ __forceinline__ double sigmoid_stable(double x) {   // DF_utils.h:37-46
   if (x >= 0.) return 1. / (1. + exp(-x));
   const double t = exp(x);
@@ -118,6 +133,14 @@ void launch_gen_normal(int n, int t, uint64_t seed, int stream, long c0, double*
 void launch_sqrt_vec(int n, const double* x, double* y, hipStream_t s) {
   if (n <= 0) return;
   hipLaunchKernelGGL(sqrt_vec_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, x, y);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_pred_samples(int n_pred, int mp, int t, int tc, const int* nbr, const double* B, const double* Z, double* V,
+                         int ldv, int col0, hipStream_t s) {
+  if (n_pred <= 0 || tc <= 0) return;
+  hipLaunchKernelGGL(pred_samples_kernel, dim3((n_pred + 255) / 256, tc), dim3(256), 0, s, n_pred, mp, t, tc, nbr, B, Z,
+                     V, ldv, col0);
   HIP_CHECK(hipGetLastError());
 }
 

@@ -287,12 +287,6 @@ void REModelAMD::SetPredictionData(const char* vecchia_pred_type, int num_neighb
       if (tt == "order_pred_first")
         Fatal("Prediction type '%s' is not supported for the Veccia approximation for non-Gaussian likelihoods ", t.c_str());
     }
-    if (tt != "order_obs_first_cond_obs_only" && tt != "order_obs_first_cond_all" &&
-        tt != "latent_order_obs_first_cond_obs_only")
-      Fatal("vecchia_pred_type '%s' is not supported by gpboost_amd (supported: order_obs_first_cond_obs_only, "
-            "order_obs_first_cond_all, latent_order_obs_first_cond_obs_only)", t.c_str());
-    if (tt == "latent_order_obs_first_cond_obs_only" && !cfg_.latent)
-      Fatal("vecchia_pred_type '%s' for the Gaussian likelihood is not supported by gpboost_amd", t.c_str());
     vecchia_pred_type_ = tt;
   }
   if (num_neighbors_pred > 0) num_neighbors_pred_ = num_neighbors_pred;
@@ -351,8 +345,10 @@ void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred,
     PredictFitc(y, n_pred, coords_pred, cov_pars, predict_cov_mat, predict_var, predict_response, out, mean_add);
     return;
   }
-  if (!vecchia_) Fatal("predictions are implemented for the Vecchia (gp_approx = 'vecchia' / 'vecchia_latent') and "
-                       "FITC approximations only");
+  if (!vecchia_) {
+    PredictDense(y, n_pred, coords_pred, cov_pars, predict_cov_mat, predict_var, predict_response, out, mean_add);
+    return;
+  }
   if (world_ > 1) Fatal("predictions are only available on single-rank models");
   if (n_pred <= 0) Fatal("num_data_pred must be > 0");
   if (coords_pred == nullptr) Fatal("gp_coords_data_pred must be provided");
@@ -366,8 +362,9 @@ void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred,
   else if ((int)last_cov_pars_.size() == ncp) std::copy(last_cov_pars_.begin(), last_cov_pars_.end(), cp);
   else Fatal("cov_pars must be provided (no previous evaluation)");
   if (latent) {
-    if (predict_cov_mat)
-      Fatal("predictive covariance matrices of latent models are not supported by gpboost_amd (use predict_var)");
+    if (predict_cov_mat && predict_response && cfg_.lik == kLikBernoulliLogit)
+      Fatal("predictive covariance matrices of the response are not supported for likelihood 'bernoulli_logit' by "
+            "gpboost_amd (use predict_response = false or predict_var)");
     // the mode at these parameters, found from zero (re_model.cpp:967-977 -> CalcCovFactorOrModeAndNegLL)
     EvalLatent(cp, false);
   }
@@ -377,6 +374,14 @@ void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred,
     trafo[1] = range_trafo(cfg_.cov_type, cp[1]);
   } else {
     TransformCovPars(cp, trafo);
+  }
+  if (!latent && vecchia_pred_type_ == "order_pred_first") {
+    PredictPredFirst(n_pred, coords_pred, trafo, predict_cov_mat, predict_var, predict_response, out, mean_add);
+    return;
+  }
+  if (!latent && vecchia_pred_type_.rfind("latent_", 0) == 0) {
+    PredictLatentGaussian(n_pred, coords_pred, trafo, predict_cov_mat, predict_var, predict_response, out, mean_add);
+    return;
   }
   // observed points: the latent variables' locations (unique, Vecchia order) / the observations
   const int n = latent ? nu_ : cfg_.n, d = cfg_.d, na = n + n_pred;
@@ -389,7 +394,8 @@ void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred,
   std::vector<int> nb((size_t)n_pred * mp);
   // order_obs_first_cond_all: neighbours among the observed AND the earlier prediction points
   // (find_nearest_neighbors_Vecchia_fast end_search_at = -1, Vecchia_utils.cpp:1729-1737)
-  const bool cond_all = !latent && vecchia_pred_type_ == "order_obs_first_cond_all";
+  const bool cond_all = vecchia_pred_type_ == "order_obs_first_cond_all" ||
+                        vecchia_pred_type_ == "latent_order_obs_first_cond_all";
   const int end_at = cond_all ? -1 : n - 1;
   if (d <= 3) vecchia_neighbors_gpu(xa.data(), na, d, mp, n, na, nb.data(), stream_, end_at);
   else vecchia_neighbors(xa.data(), na, d, mp, n, na, nb.data(), end_at);
@@ -423,6 +429,11 @@ void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred,
   a.Dinv_out = dD.get();
   a.row_base = n;
   launch_vecchia_rows(cfg_.cov_type, a, stream_);
+  if (latent && (cond_all || predict_cov_mat)) {
+    PredictLatentSim(n, n_pred, mp, nb, dB.get(), dD.get(), cond_all, predict_cov_mat, predict_var, predict_response,
+                     out, mean_add);
+    return;
+  }
   if (latent) {   // mean = -Bpo mode (likelihoods.h:6609), Dp (no nugget to remove)
     std::vector<double> mode(n);
     latent_->GetMode(mode.data());
@@ -474,6 +485,113 @@ void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred,
     for (int p = 0; p < n_pred; ++p) c[(size_t)p * n_pred + p] = h[n_pred + p];
   } else if (predict_var) {
     std::copy(h.begin() + n_pred, h.end(), out + n_pred);
+  }
+}
+
+// Latent models (Laplace, iterative) with latent_order_obs_first_cond_all or a predictive covariance
+// (PredictLaplaceApproxVecchia, likelihoods.h:6576-6749): with the prediction rows' B split into Bpo
+// (observed neighbours) and Bp (earlier prediction points; identity for cond_obs_only),
+//   mean = -Bp^-1 Bpo mode (forward substitution in prediction order, :6610-6616)
+//   var / cov = (1/nsim) sum_draws (Bp^-1 Bpo z)(.)^T + Bp^-1 diag(Dp) Bp^-T, z ~ N(0, (Sigma^-1 + W)^-1)
+// with the draws of PredVarSim kept as an n_pred x nsim matrix on the device and the moments on the
+// dense path (latent_pred_moments); then the response transform as in Predict.
+void REModelAMD::PredictLatentSim(int n, int n_pred, int mp, const std::vector<int>& nb, const double* dB,
+                                  const double* dDinv, bool cond_all, bool predict_cov_mat, bool predict_var,
+                                  bool predict_response, double* out, const double* mean_add) {
+  if (cond_all && n_pred > 20000)
+    Fatal("latent_order_obs_first_cond_all is limited to num_data_pred <= 20000 in gpboost_amd (dense Bp^-1)");
+  if (predict_cov_mat && n_pred > 40000)
+    Fatal("predictive covariance matrices are limited to num_data_pred <= 40000 in gpboost_amd");
+  std::vector<double> B((size_t)n_pred * mp), Dinv(n_pred), mode(n);
+  HIP_CHECK(hipMemcpyAsync(B.data(), dB, sizeof(double) * B.size(), hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipMemcpyAsync(Dinv.data(), dDinv, sizeof(double) * n_pred, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  latent_->GetMode(mode.data());
+  std::vector<double> mean(n_pred), D(n_pred), Bpo(B), Bp;
+  if (cond_all) Bp.assign((size_t)n_pred * n_pred, 0.);
+  for (int p = 0; p < n_pred; ++p) {
+    D[p] = 1. / Dinv[p];
+    double b = 0.;
+    for (int r = 0; r < mp; ++r) {
+      const int j = nb[(size_t)p * mp + r];
+      const double v = B[(size_t)p * mp + r];
+      if (j < n) {
+        b += v * mode[j];
+      } else {   // an earlier prediction point (cond_all)
+        Bpo[(size_t)p * mp + r] = 0.;
+        Bp[(size_t)(j - n) * n_pred + p] = v;
+        b -= v * mean[j - n];   // mean holds x = Bp^-1 (Bpo mode) for the earlier points
+      }
+    }
+    mean[p] = b;
+    if (cond_all) Bp[(size_t)p * n_pred + p] = 1.;
+  }
+  for (int p = 0; p < n_pred; ++p) mean[p] = -mean[p] + (mean_add ? mean_add[p] : 0.);
+  const bool want_var = predict_var || predict_response;
+  std::vector<double> var(n_pred), cov(predict_cov_mat ? (size_t)n_pred * n_pred : 0);
+  if (want_var || predict_cov_mat) {
+    const int nsim = nsim_var_pred_;
+    DevBuf<double> dBpo(Bpo.size()), dV((size_t)n_pred * nsim);
+    HIP_CHECK(hipMemcpyAsync(dBpo.get(), Bpo.data(), sizeof(double) * Bpo.size(), hipMemcpyHostToDevice, stream_));
+    latent_->PredVarSim(nsim, iter.num_rand_vec_trace, iter.cg_delta_conv, iter.cg_max_num_it, pred_seed_++, n_pred,
+                        mp, nb.data(), dBpo.get(), nullptr, dV.get());
+    latent_pred_moments(stream_, n_pred, cond_all ? Bp.data() : nullptr, D.data(), dV.get(), nsim, want_var,
+                        predict_cov_mat, var.data(), cov.data());
+  }
+  if (predict_response && cfg_.lik == kLikBernoulliLogit) {
+    static const std::vector<double> gh = gauss_hermite_adaptive(30);   // order_GH_ = 30 (likelihoods.h:12877)
+    DevBuf<double> dmv((size_t)2 * n_pred), dgh(gh.size()), dout((size_t)2 * n_pred);
+    HIP_CHECK(hipMemcpyAsync(dmv.get(), mean.data(), sizeof(double) * n_pred, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipMemcpyAsync(dmv.get() + n_pred, var.data(), sizeof(double) * n_pred, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipMemcpyAsync(dgh.get(), gh.data(), sizeof(double) * gh.size(), hipMemcpyHostToDevice, stream_));
+    launch_resp_logit(n_pred, dmv.get(), dmv.get() + n_pred, dgh.get(), dgh.get() + 30, 30, iter.delta_conv_mode_finding,
+                      dout.get(), dout.get() + n_pred, stream_);
+    HIP_CHECK(hipMemcpyAsync(mean.data(), dout.get(), sizeof(double) * n_pred, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(var.data(), dout.get() + n_pred, sizeof(double) * n_pred, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  } else if (predict_response) {   // gaussian vecchia_latent: + the error variance (PredictResponse)
+    const double aux = aux_pars_.empty() ? 0. : aux_pars_[0];
+    for (int p = 0; p < n_pred; ++p) var[p] += aux;
+    if (predict_cov_mat)
+      for (int p = 0; p < n_pred; ++p) cov[(size_t)p * n_pred + p] += aux;
+  }
+  std::copy(mean.begin(), mean.end(), out);
+  if (predict_cov_mat) std::copy(cov.begin(), cov.end(), out + n_pred);
+  else if (predict_var) std::copy(var.begin(), var.end(), out + n_pred);
+}
+
+// gp_approx = "none" (CalcPred, re_model_template.h:3894-3898 -> the dense conditional Gaussian):
+// mean = Sigma_po Psi^-1 y, cov = Sigma_pp - Sigma_po Psi^-1 Sigma_op (+ the nugget for the response),
+// times sigma^2 (:3956, :3967), on the dense path's factor (DenseSolver::Predict).
+void REModelAMD::PredictDense(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,
+                              bool predict_cov_mat, bool predict_var, bool predict_response, double* out,
+                              const double* mean_add) {
+  if (world_ > 1) Fatal("predictions are only available on single-rank models");
+  if (n_pred <= 0) Fatal("num_data_pred must be > 0");
+  if (coords_pred == nullptr) Fatal("gp_coords_data_pred must be provided");
+  UseDevice();
+  if (y != nullptr) SetY(y);
+  if (!y_set_) Fatal("response variable y has not been set (pass y or evaluate the likelihood first)");
+  double cp[3];
+  if (cov_pars != nullptr) std::copy(cov_pars, cov_pars + 3, cp);
+  else if ((int)last_cov_pars_.size() == 3) std::copy(last_cov_pars_.begin(), last_cov_pars_.end(), cp);
+  else Fatal("cov_pars must be provided (no previous evaluation)");
+  double trafo[3];
+  TransformCovPars(cp, trafo);
+  const int d = cfg_.d;
+  std::vector<double> xp((size_t)n_pred * d);
+  for (int p = 0; p < n_pred; ++p)
+    for (int q = 0; q < d; ++q) xp[(size_t)p * d + q] = coords_pred[(size_t)q * n_pred + p];
+  std::vector<double> mean(n_pred), var(predict_var ? n_pred : 0), cov(predict_cov_mat ? (size_t)n_pred * n_pred : 0);
+  dense_->Predict(cfg_.cov_type, trafo[1], trafo[2], d_y_.get(), xp.data(), n_pred, predict_var && !predict_cov_mat,
+                  predict_cov_mat, mean.data(), var.data(), cov.data());
+  const double nug = predict_response ? 1. : 0., s2 = trafo[0];
+  for (int p = 0; p < n_pred; ++p) out[p] = mean[p] + (mean_add ? mean_add[p] : 0.);
+  if (predict_cov_mat) {
+    for (size_t e = 0; e < cov.size(); ++e) out[n_pred + e] = cov[e] * s2;
+    for (int p = 0; p < n_pred; ++p) out[n_pred + (size_t)p * n_pred + p] += nug * s2;
+  } else if (predict_var) {
+    for (int p = 0; p < n_pred; ++p) out[n_pred + p] = (var[p] + nug) * s2;
   }
 }
 
@@ -537,6 +655,185 @@ void REModelAMD::PredictFitc(const double* y, int n_pred, const double* coords_p
     for (size_t e = 0; e < cov.size(); ++e) out[n_pred + e] = cov[e] * trafo[0];
   } else if (predict_var) {
     for (int p = 0; p < n_pred; ++p) out[n_pred + p] = var[p] * trafo[0];
+  }
+}
+
+// order_pred_first, Gaussian likelihood (CalcPredVecchiaPredictedFirstOrder, Vecchia_utils.cpp:2018-2239):
+// the prediction points first (given order), then the observations (Vecchia order); every point's
+// neighbours among ALL earlier points (GPU sweep from row 0); the rows' (B, D^-1) by the row kernel.
+// With Bp (prediction rows, prediction columns), Bop / Bo (observation rows, prediction /
+// observation columns):
+//   cond_prec = Bp^T Dp^-1 Bp + Bop^T Do^-1 Bop,  mean = -cond_prec^-1 Bop^T Do^-1 Bo y,
+//   cov = cond_prec^-1 (variances its diagonal), less the nugget unless predict_response, times
+// sigma^2 (re_model_template.h:3788-3815). cond_prec is assembled on the host (O((n + n_pred) m^2))
+// and factorized densely on the GPU (POTRF / TRTRI / GEMM). The reference factorizes it with a
+// fill-reducing (AMD) permutation and reads the variances / covariance off the inverse of the
+// permuted factor, i.e. in AMD-permuted order; here they come in prediction-point order.
+void REModelAMD::PredictPredFirst(int n_pred, const double* coords_pred, const double* trafo, bool predict_cov_mat,
+                                  bool predict_var, bool predict_response, double* out, const double* mean_add) {
+  const int n = cfg_.n, d = cfg_.d, na = n + n_pred;
+  const int mp = std::min(num_neighbors_pred_, na - 1);
+  if (mp > 64) Fatal("num_neighbors_pred = %d > 64 is not supported by the GPU prediction kernel", mp);
+  std::vector<double> xa((size_t)na * d);
+  for (int p = 0; p < n_pred; ++p)
+    for (int q = 0; q < d; ++q) xa[(size_t)p * d + q] = coords_pred[(size_t)q * n_pred + p];
+  std::copy(coords_vo_.begin(), coords_vo_.begin() + (size_t)n * d, xa.begin() + (size_t)n_pred * d);
+  std::vector<int> nb((size_t)na * mp, -1);
+  if (d <= 3) vecchia_neighbors_gpu(xa.data(), na, d, mp, 0, na, nb.data(), stream_, -1);
+  else vecchia_neighbors(xa.data(), na, d, mp, 0, na, nb.data(), -1);
+  DevBuf<double> dxa((size_t)na * d), dB((size_t)na * mp), dD(na);
+  DevBuf<int> dnb((size_t)na * mp);
+  HIP_CHECK(hipMemcpyAsync(dxa.get(), xa.data(), sizeof(double) * xa.size(), hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(dnb.get(), nb.data(), sizeof(int) * nb.size(), hipMemcpyHostToDevice, stream_));
+  VecchiaRowsArgs a{};
+  a.X = dxa.get();
+  a.Y = nullptr;
+  a.nbr = dnb.get();
+  a.n = na;
+  a.d = d;
+  a.m = mp;
+  a.r0 = 0;
+  a.r1 = na;
+  a.var = trafo[1];
+  a.phi = trafo[2];
+  a.diag_mult = 1.;
+  a.diag_add = 1.;      // nugget on the between-neighbour covariance (Vecchia_utils.cpp:2189)
+  a.d_nugget = 1.;      // Dp_inv / Do_inv start at 1 (:2124-2125)
+  a.B_out = dB.get();
+  a.Dinv_out = dD.get();
+  a.row_base = 0;
+  launch_vecchia_rows(cfg_.cov_type, a, stream_);
+  std::vector<double> B((size_t)na * mp), Dinv(na), y(n);
+  HIP_CHECK(hipMemcpyAsync(B.data(), dB.get(), sizeof(double) * B.size(), hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipMemcpyAsync(Dinv.data(), dD.get(), sizeof(double) * na, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipMemcpyAsync(y.data(), d_y_.get(), sizeof(double) * n, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  // cond_prec (column-major n_pred x n_pred) and y_aux = Bop^T Do^-1 Bo y
+  std::vector<double> P((size_t)n_pred * n_pred, 0.), yaux(n_pred, 0.);
+  std::vector<int> pc;        // prediction columns of one row (incl. the diagonal of a prediction row)
+  std::vector<double> pv;
+  for (int i = 0; i < na; ++i) {
+    const int k = std::min(i, mp);
+    pc.clear();
+    pv.clear();
+    double boy = 0.;   // (Bo y)_i for an observation row
+    if (i < n_pred) {
+      pc.push_back(i);
+      pv.push_back(1.);
+    } else {
+      boy = y[i - n_pred];
+    }
+    for (int r = 0; r < k; ++r) {
+      const int j = nb[(size_t)i * mp + r];
+      const double b = B[(size_t)i * mp + r];
+      if (j < n_pred) {
+        pc.push_back(j);
+        pv.push_back(b);
+      } else {
+        boy += b * y[j - n_pred];
+      }
+    }
+    const double w = Dinv[i];
+    for (size_t u = 0; u < pc.size(); ++u) {
+      for (size_t v = 0; v < pc.size(); ++v) P[(size_t)pc[v] * n_pred + pc[u]] += pv[u] * w * pv[v];
+      if (i >= n_pred) yaux[pc[u]] += pv[u] * w * boy;
+    }
+  }
+  std::vector<double> mean(n_pred), var(n_pred), cov(predict_cov_mat ? (size_t)n_pred * n_pred : 0);
+  spd_solve_inverse(stream_, n_pred, P.data(), yaux.data(), mean.data(), var.data(),
+                    predict_cov_mat ? cov.data() : nullptr);
+  const double nug = predict_response ? 0. : 1., s2 = trafo[0];
+  for (int p = 0; p < n_pred; ++p) out[p] = -mean[p] + (mean_add ? mean_add[p] : 0.);
+  if (predict_cov_mat) {
+    for (size_t e = 0; e < cov.size(); ++e) out[n_pred + e] = cov[e] * s2;
+    for (int p = 0; p < n_pred; ++p) out[n_pred + (size_t)p * n_pred + p] -= nug * s2;
+  } else if (predict_var) {
+    for (int p = 0; p < n_pred; ++p) out[n_pred + p] = (var[p] - nug) * s2;
+  }
+}
+
+// latent_order_obs_first_cond_obs_only / latent_order_obs_first_cond_all with the Gaussian likelihood
+// (CalcPredVecchiaLatentObservedFirstOrder, Vecchia_utils.cpp:2241-2442, dispatched at
+// re_model_template.h:3755-3786): a Vecchia approximation of the LATENT process over the observed
+// (Vecchia order) then the prediction points, num_neighbors_pred neighbours for every point among the
+// earlier observed points (cond_obs_only) or all earlier points (cond_all), no nugget (between-neighbour
+// diagonal times JITTER_MULT_VECCHIA, D = sigma1^2 - A c); then Sigma = B^-1 D B^-T and the Gaussian
+// conditional given y = latent + N(0, 1): mean = Sigma_po (Sigma_oo + I)^-1 y, cov = Sigma_pp -
+// Sigma_po (Sigma_oo + I)^-1 Sigma_op (+ I for the response), times sigma^2. The reference forms
+// B^-1 as a sparse matrix with fill; here B is dense and everything runs on the GPU's dense path, so
+// the observed plus prediction points are bounded (N <= 20000).
+void REModelAMD::PredictLatentGaussian(int n_pred, const double* coords_pred, const double* trafo,
+                                       bool predict_cov_mat, bool predict_var, bool predict_response, double* out,
+                                       const double* mean_add) {
+  const int n = cfg_.n, d = cfg_.d, N = n + n_pred;
+  if (N > 20000)
+    Fatal("vecchia_pred_type '%s' with the Gaussian likelihood is limited to num_data + num_data_pred <= 20000 in "
+          "gpboost_amd (dense latent covariance)", vecchia_pred_type_.c_str());
+  const bool cond_all = vecchia_pred_type_ == "latent_order_obs_first_cond_all";
+  const int mp = std::min(num_neighbors_pred_, N - 1);
+  if (mp > 64) Fatal("num_neighbors_pred = %d > 64 is not supported by the GPU prediction kernel", mp);
+  std::vector<double> xa((size_t)N * d);
+  std::copy(coords_vo_.begin(), coords_vo_.begin() + (size_t)n * d, xa.begin());
+  for (int p = 0; p < n_pred; ++p)
+    for (int q = 0; q < d; ++q) xa[(size_t)(n + p) * d + q] = coords_pred[(size_t)q * n_pred + p];
+  {
+    std::vector<int> uniq, idx;
+    unique_locations(xa.data(), N, d, uniq, idx);
+    if ((int)uniq.size() < N)
+      Fatal("Duplicates found among training and test coordinates. This is not supported for predictions with a "
+            "Vecchia approximation for the latent process ('latent_') in gpboost_amd ");
+  }
+  std::vector<int> nb((size_t)N * mp, -1);
+  const int end_at = cond_all ? -1 : n - 1;
+  if (d <= 3) vecchia_neighbors_gpu(xa.data(), N, d, mp, 0, N, nb.data(), stream_, end_at);
+  else vecchia_neighbors(xa.data(), N, d, mp, 0, N, nb.data(), end_at);
+  DevBuf<double> dxa((size_t)N * d), dB((size_t)N * mp), dD(N);
+  DevBuf<int> dnb((size_t)N * mp);
+  HIP_CHECK(hipMemcpyAsync(dxa.get(), xa.data(), sizeof(double) * xa.size(), hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(dnb.get(), nb.data(), sizeof(int) * nb.size(), hipMemcpyHostToDevice, stream_));
+  VecchiaRowsArgs a{};
+  a.X = dxa.get();
+  a.Y = nullptr;
+  a.nbr = dnb.get();
+  a.n = N;
+  a.d = d;
+  a.m = mp;
+  a.r0 = 0;
+  a.r1 = N;
+  a.var = trafo[1];
+  a.phi = trafo[2];
+  a.diag_mult = 1. + 1e-10;   // JITTER_MULT_VECCHIA (utils.h:36, Vecchia_utils.cpp:2382)
+  a.diag_add = 0.;
+  a.d_nugget = 0.;
+  a.B_out = dB.get();
+  a.Dinv_out = dD.get();
+  a.row_base = 0;
+  launch_vecchia_rows(cfg_.cov_type, a, stream_);
+  std::vector<double> Bv((size_t)N * mp), Dinv(N), y(n);
+  HIP_CHECK(hipMemcpyAsync(Bv.data(), dB.get(), sizeof(double) * Bv.size(), hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipMemcpyAsync(Dinv.data(), dD.get(), sizeof(double) * N, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipMemcpyAsync(y.data(), d_y_.get(), sizeof(double) * n, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  std::vector<double> Bd((size_t)N * N, 0.), D(N);
+  for (int i = 0; i < N; ++i) {
+    Bd[(size_t)i * N + i] = 1.;
+    const int k = std::min(i, mp);
+    for (int r = 0; r < k; ++r) {
+      const int j = nb[(size_t)i * mp + r];
+      if (j >= 0) Bd[(size_t)j * N + i] += Bv[(size_t)i * mp + r];
+    }
+    D[i] = 1. / Dinv[i];
+  }
+  std::vector<double> mean(n_pred), var(n_pred), cov(predict_cov_mat ? (size_t)n_pred * n_pred : 0);
+  vecchia_latent_dense_pred(stream_, N, n, Bd.data(), D.data(), y.data(), predict_var, predict_cov_mat, mean.data(),
+                            var.data(), cov.data());
+  const double nug = predict_response ? 1. : 0., s2 = trafo[0];
+  for (int p = 0; p < n_pred; ++p) out[p] = mean[p] + (mean_add ? mean_add[p] : 0.);
+  if (predict_cov_mat) {
+    for (size_t e = 0; e < cov.size(); ++e) out[n_pred + e] = cov[e] * s2;
+    for (int p = 0; p < n_pred; ++p) out[n_pred + (size_t)p * n_pred + p] += nug * s2;
+  } else if (predict_var) {
+    for (int p = 0; p < n_pred; ++p) out[n_pred + p] = (var[p] + nug) * s2;
   }
 }
 

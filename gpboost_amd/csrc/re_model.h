@@ -212,6 +212,15 @@ class REModelAMD {
 
  private:
   void TransformCovPars(const double* orig, double* trafo) const;
+  void PredictPredFirst(int n_pred, const double* coords_pred, const double* trafo, bool predict_cov_mat,
+                        bool predict_var, bool predict_response, double* out, const double* mean_add);
+  void PredictLatentGaussian(int n_pred, const double* coords_pred, const double* trafo, bool predict_cov_mat,
+                             bool predict_var, bool predict_response, double* out, const double* mean_add);
+  void PredictLatentSim(int n, int n_pred, int mp, const std::vector<int>& nb, const double* dB, const double* dDinv,
+                        bool cond_all, bool predict_cov_mat, bool predict_var, bool predict_response, double* out,
+                        const double* mean_add);
+  void PredictDense(const double* y, int n_pred, const double* coords_pred, const double* cov_pars, bool predict_cov_mat,
+                    bool predict_var, bool predict_response, double* out, const double* mean_add);
   void PredictFitc(const double* y, int n_pred, const double* coords_pred, const double* cov_pars, bool predict_cov_mat,
                    bool predict_var, bool predict_response, double* out, const double* mean_add);
   void PredictCondAll(int n, int n_pred, int mp, const std::vector<int>& nb, const double* dB, const double* dDinv,

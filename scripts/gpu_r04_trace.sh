@@ -20,9 +20,13 @@ DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 timeout -k 10 600 rocprofv3 --kernel-trace --st
   --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline > $O/bench.log 2>&1 \
   || { tail -20 $O/bench.log; exit 2; }
 find $O -name "*kernel_stats.csv" | head
+# only the summaries travel back (gpurun_out is pulled only below 64 MiB)
+find $O -name "*.csv" ! -name "*stats.csv" -delete
 if [ -n "${CRASH:-}" ]; then
   GPBOOST_AMD_DUMP_MAPS=$O/maps.txt timeout -k 10 600 rocprofv3 --kernel-trace -d $O/crash -o run \
     --output-format csv -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-dense --no-fit --no-grouped \
     --no-fitc > $O/crash.log 2>&1
   echo "crash run rc=$?"
+  find $O -name "*.csv" ! -name "*stats.csv" -delete
+  find $O -name "core*" -delete
 fi

@@ -1,0 +1,132 @@
+// Microbenchmark: one-wave 64 x 64 Cholesky + inverse of the diagonal block (dense POTRF's
+// potrf_diag_wave_kernel) and variants, on an SPD block; average device time per launch.
+//   V0: the production form (dense_kernels.hip)
+//   V1: factorization only (no inverse)
+//   V2: production factorization, inverse with 4 independent partial sums per row
+//   V3: V2 + reciprocal-multiply instead of a divide per step
+// hipcc --offload-arch=gfx950 -O3 -o diag_bench diag_bench.hip && ./diag_bench
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <vector>
+
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { std::printf("HIP error %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
+
+template <int V>
+__global__ void __launch_bounds__(64) diag_kernel(double* A, int lda, int ib, double* Winv, int ldw, int* info) {
+  __shared__ double colb[2][64];
+  __shared__ double Ls[64][65];
+  const int r = threadIdx.x;
+  double row[64];
+#pragma unroll
+  for (int c = 0; c < 64; ++c) row[c] = (r < ib && c < ib && c <= r) ? A[(size_t)r + (size_t)c * lda] : 0.;
+#pragma unroll
+  for (int j = 0; j < 64; ++j) {
+    if (j < ib) {
+      const double p = __shfl(row[j], j, 64);
+      double d;
+      if (!(p > 0.)) {
+        if (r == 0) atomicAdd(info, 1);
+        d = 1.;
+      } else {
+        d = sqrt(p);
+      }
+      double l;
+      if constexpr (V == 3) {
+        const double rd = 1. / d;
+        l = (r > j) ? row[j] * rd : (r == j ? d : 0.);
+      } else {
+        l = (r > j) ? row[j] / d : (r == j ? d : 0.);
+      }
+      if (r >= j) row[j] = l;
+      colb[j & 1][r] = l;
+      __syncthreads();
+#pragma unroll
+      for (int c = j + 1; c < 64; ++c) row[c] = fma(-l, colb[j & 1][c], row[c]);
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < 64; ++c) {
+    Ls[r][c] = row[c];
+    if (r < ib && c < ib && c <= r) A[(size_t)r + (size_t)c * lda] = row[c];
+  }
+  if constexpr (V == 1) return;
+  __syncthreads();
+  double x[64];
+  if constexpr (V == 0) {
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      double s = (i == r) ? 1. : 0.;
+#pragma unroll
+      for (int p = 0; p < i; ++p) s -= Ls[i][p] * x[p];
+      x[i] = (i >= r && i < ib) ? s / Ls[i][i] : 0.;
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 64; ++i) {
+      double s0 = (i == r) ? 1. : 0., s1 = 0., s2 = 0., s3 = 0.;
+#pragma unroll
+      for (int p = 0; p + 3 < i; p += 4) {
+        s0 -= Ls[i][p] * x[p];
+        s1 -= Ls[i][p + 1] * x[p + 1];
+        s2 -= Ls[i][p + 2] * x[p + 2];
+        s3 -= Ls[i][p + 3] * x[p + 3];
+      }
+#pragma unroll
+      for (int p = (i / 4) * 4; p < i; ++p) s0 -= Ls[i][p] * x[p];
+      const double s = (s0 + s1) + (s2 + s3);
+      x[i] = (i >= r && i < ib) ? s / Ls[i][i] : 0.;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 64; ++i)
+    if (i < ib && r < ib) Winv[(size_t)i + (size_t)r * ldw] = (r <= i) ? x[i] : 0.;
+}
+
+template <int V>
+int run(const std::vector<double>& h, double* dA, double* dW, int* dinfo, const char* name) {
+  const int reps = 200;
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  // warm-up
+  CK(hipMemcpy(dA, h.data(), sizeof(double) * 64 * 64, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(diag_kernel<V>, dim3(1), dim3(64), 0, 0, dA, 64, 64, dW, 64, dinfo);
+  CK(hipDeviceSynchronize());
+  float tot = 0.f;
+  for (int r = 0; r < reps; ++r) {
+    CK(hipMemcpy(dA, h.data(), sizeof(double) * 64 * 64, hipMemcpyHostToDevice));
+    CK(hipEventRecord(a, 0));
+    hipLaunchKernelGGL(diag_kernel<V>, dim3(1), dim3(64), 0, 0, dA, 64, 64, dW, 64, dinfo);
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, a, b));
+    tot += ms;
+  }
+  std::vector<double> W(64 * 64);
+  CK(hipMemcpy(W.data(), dW, sizeof(double) * 64 * 64, hipMemcpyDeviceToHost));
+  double chk = 0.;
+  for (double v : W) chk += v;
+  std::printf("%s: %.2f us per launch (checksum %.12g)\n", name, 1e3 * tot / reps, chk);
+  return 0;
+}
+
+int main() {
+  std::vector<double> h(64 * 64);
+  for (int i = 0; i < 64; ++i)
+    for (int j = 0; j < 64; ++j) h[i + 64 * j] = std::exp(-std::fabs(i - j) * 0.3) + (i == j ? 0.5 : 0.);
+  double *dA, *dW;
+  int* dinfo;
+  CK(hipMalloc(&dA, sizeof(double) * 64 * 64));
+  CK(hipMalloc(&dW, sizeof(double) * 64 * 64));
+  CK(hipMalloc(&dinfo, sizeof(int)));
+  CK(hipMemset(dinfo, 0, sizeof(int)));
+  CK(hipMemset(dW, 0, sizeof(double) * 64 * 64));
+  if (run<0>(h, dA, dW, dinfo, "V0 production")) return 1;
+  if (run<1>(h, dA, dW, dinfo, "V1 factor only")) return 1;
+  if (run<2>(h, dA, dW, dinfo, "V2 inverse, 4 partial sums")) return 1;
+  if (run<3>(h, dA, dW, dinfo, "V3 V2 + reciprocal multiply")) return 1;
+  return 0;
+}

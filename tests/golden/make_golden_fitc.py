@@ -87,6 +87,9 @@ def main():
     fits = {
         "fit_fitc_exp_n2000_m50": fit_case(2000, 50),
         "fit_fitc_matern15_n3000_m100": fit_case(3000, 100, cov_fct="matern", shape=1.5),
+        # more than 1000 inducing points: FindInitCovPar samples 1000 of them with the model's generator
+        # after the kmeans++ draws (re_model_template.h:4474-4476, cov_fcts.h:1275-1450)
+        "fit_fitc_exp_n4000_m1100": fit_case(4000, 1100),
     }
     for k, v in cases.items():
         print(k, {mm: (v[mm]["nll"], v[mm]["grad"]) for mm in ("eval", "lbfgs") if mm in v}, v["ref_time_s"],

@@ -34,7 +34,7 @@ def pred_coords(npred, d=2):
     return synthetic.lcg_unif(npred * d, 0.713).reshape(d, npred).T.copy()
 
 
-def case(n, npred, lik, cov_pars, nu=0, m=20, t=50, nsim=None, response=False, **opts):
+def case(n, npred, lik, cov_pars, nu=0, m=20, t=50, nsim=None, response=False, cov=False, **opts):
     X = synthetic.repeated_coords(n, nu) if nu else synthetic.bench_coords(n)
     y = synthetic.bench_bernoulli_y(X) if lik == "bernoulli_logit" else synthetic.bench_gaussian_y(n)
     Xp = pred_coords(npred)
@@ -48,6 +48,8 @@ def case(n, npred, lik, cov_pars, nu=0, m=20, t=50, nsim=None, response=False, *
     spec.update(opts)
     try:
         extra = dict(predict_var="1", nsim_var_pred=str(nsim)) if nsim else {}
+        if cov:
+            extra = dict(predict_cov="1", nsim_var_pred=str(nsim))
         if response:
             extra["predict_response"] = "1"
         r = run_ref(X, y, cov_pars=fmt_pars(cov_pars), mode="predict", pred=ppath, **spec, **extra)
@@ -55,14 +57,25 @@ def case(n, npred, lik, cov_pars, nu=0, m=20, t=50, nsim=None, response=False, *
         os.unlink(ppath)
     out = dict(n=n, nu=nu, npred=npred, lik=lik, cov_pars=list(cov_pars), spec=spec, mean=r["mean"], response=response)
     if nsim:
-        out.update(nsim=nsim, var=r["var"])
+        out.update(nsim=nsim)
+        out["cov" if cov else "var"] = r["cov" if cov else "var"]
     return out
 
 
 def main():
     cases = json.load(open(OUT)) if os.path.exists(OUT) else {}
     tight = dict(cg_delta_conv="1e-10")
-    if "--big" not in sys.argv:
+    if "--new" in sys.argv:
+        # predictive covariance (obs-only) and latent_order_obs_first_cond_all (PredictLaplaceApproxVecchia
+        # with CondObsOnly = false, likelihoods.h:6610-6749)
+        cases["bern_n2000_tight_cov"] = case(2000, 40, "bernoulli_logit", (1.0, 0.1), nsim=20000, cov=True, **tight)
+        cases["bern_n2000_tight_condall"] = case(2000, 300, "bernoulli_logit", (1.0, 0.1), nsim=20000,
+                                                 vecchia_pred_type="latent_order_obs_first_cond_all", **tight)
+        cases["gauss_n2000_tight_condall"] = case(2000, 300, "gaussian", (1.0, 0.1), aux_pars="0.1", nsim=20000,
+                                                  vecchia_pred_type="latent_order_obs_first_cond_all", **tight)
+        cases["bern_n2000_tight_condall_cov"] = case(2000, 40, "bernoulli_logit", (1.0, 0.1), nsim=20000, cov=True,
+                                                     vecchia_pred_type="latent_order_obs_first_cond_all", **tight)
+    elif "--big" not in sys.argv:
         cases["bern_n2000_tight"] = case(2000, 300, "bernoulli_logit", (1.0, 0.1), nsim=20000, **tight)
         cases["bern_n2000_default"] = case(2000, 300, "bernoulli_logit", (1.0, 0.1))
         cases["gauss_n2000_tight"] = case(2000, 300, "gaussian", (1.0, 0.1), aux_pars="0.1", nsim=20000, **tight)
@@ -73,7 +86,7 @@ def main():
     else:
         cases["bern_n100k_default"] = case(100000, 5000, "bernoulli_logit", (1.0, 0.1), m=30)
     for k, v in cases.items():
-        print(k, v["mean"][:3], v.get("var", [None])[:3], file=sys.stderr)
+        print(k, v["mean"][:3], v.get("var", v.get("cov", [None]))[:3], file=sys.stderr)
     with open(OUT, "w") as f:
         json.dump(cases, f, indent=1)
 

@@ -179,8 +179,8 @@ def test_preconditioner_plans_agree(monkeypatch, dense_rows, head_rows, merge):
 
 @pytest.mark.parametrize("seg_form,tail_order", [("wave", "row"), ("block", "row"), ("wave", "level")])
 def test_segment_and_tail_forms_agree(monkeypatch, seg_form, tail_order):
-    """The LDS segment solved by one wave per column (SegWave, default) or by the 1024-thread
-    barrier form, and the merged tail launched in storage (Morton) order or in level order, against
+    """The LDS segment solved by the 1024-thread barrier form (default) or by one wave per column
+    (SegWave), and the merged tail launched in storage (Morton) order or in level order, against
     the plain level schedule: the same algebra in other summation orders (~1e-10 at a tight CG
     tolerance). The segment here holds long B^T rows (2 and 4 lanes per row in the wave form)."""
     from gpboost_amd import synthetic
@@ -202,6 +202,41 @@ def test_segment_and_tail_forms_agree(monkeypatch, seg_form, tail_order):
         a, b = out["levels"], out["plan"]
         assert abs(a[0] - b[0]) <= 1e-9 * abs(a[0]), (lik, a[0], b[0])
         np.testing.assert_allclose(b[1], a[1], rtol=1e-7, atol=1e-7 * np.abs(a[1]).max())
+
+
+def test_graph_replay_matches_eager(monkeypatch):
+    """VaduPrecond replays one captured hipGraph per buffer set (vadu_precond.cpp Apply). Replays after
+    captures at other widths (bench_latent_operators at t = 51 and t = 1 on the model's scratch block),
+    after new parameters (refreshed factor and preconditioner values through the same captured
+    pointers) and in a second model created after the first one is freed (allocations at reused
+    addresses) must give bit for bit the results of eager launches (GPBOOST_AMD_NO_GRAPH=1)."""
+    from gpboost_amd import synthetic
+    n = 8000
+    X = synthetic.bench_coords(n)
+    y = synthetic.bench_gaussian_y(n)
+    case = dict(likelihood="gaussian", cov_fct="exponential", shape=0.5, num_neighbors=30, aux=0.1)
+
+    def sequence():
+        res = []
+        gm = _model(X, case, t=12, dc=1e-9)
+        res.append(gm.neg_log_likelihood_and_grad([1.0, 0.1], y))
+        gm.bench_latent_operators(51, 2)
+        gm.bench_latent_operators(1, 2)
+        res.append(gm.neg_log_likelihood_and_grad([0.8, 0.15], y))
+        res.append(gm.neg_log_likelihood_and_grad([1.0, 0.1], y))
+        del gm
+        gm2 = _model(X, case, t=12, dc=1e-9)
+        res.append(gm2.neg_log_likelihood_and_grad([1.0, 0.1], y))
+        return res
+
+    monkeypatch.delenv("GPBOOST_AMD_NO_GRAPH", raising=False)
+    graph = sequence()
+    monkeypatch.setenv("GPBOOST_AMD_NO_GRAPH", "1")
+    eager = sequence()
+    for g, e in zip(graph, eager):
+        assert g[0] == e[0]
+        np.testing.assert_array_equal(g[1], e[1])
+    assert graph[0][0] == graph[2][0] == graph[3][0]
 
 
 def test_latent_zero_response(monkeypatch):

@@ -108,9 +108,57 @@ def test_latent_bernoulli_response_probabilities(golden):
     np.testing.assert_allclose(pred["var"], pred["mu"] * (1 - pred["mu"]), rtol=1e-14, atol=0)
 
 
-def test_latent_cov_mat_refused(golden):
+def test_latent_response_cov_mat_refused(golden):
     case = golden["bern_n2000_default"]
     gm, X, y, Xp = _setup(case)
     with pytest.raises(GPBoostError, match="covariance matrices"):
         gm.predict(y=y, gp_coords_pred=Xp[:10], cov_pars=case["cov_pars"], predict_cov_mat=True,
-                   predict_response=False)
+                   predict_response=True)
+
+
+def _cov_bound(ref, nsim_ours, nsim_ref):
+    # standard error of a sample covariance entry: sqrt((c_ii c_jj + c_ij^2) / nsim) (Gaussian draws),
+    # with the reference's total covariance as a conservative stand-in for its simulated part
+    d = np.diag(ref)
+    return np.sqrt((np.outer(d, d) + ref ** 2) * (1. / nsim_ours + 1. / nsim_ref))
+
+
+@pytest.mark.parametrize("name", ["bern_n2000_tight_cov", "bern_n2000_tight_condall_cov"])
+def test_latent_pred_cov_statistical(golden, name):
+    """Latent predictive covariance matrices (PredictLaplaceApproxVecchia, likelihoods.h:6651-6740:
+    (1/nsim) sum (Bp^-1 Bpo z)(.)^T + Bp^-1 diag(Dp) Bp^-T), cond_obs_only and cond_all, against the
+    reference at nsim = 20000: means at 1e-6, every entry within 6 standard errors of the two sample
+    covariances, the matrix symmetric with a positive diagonal."""
+    case = golden[name]
+    gm, X, y, Xp = _setup(case)
+    if "vecchia_pred_type" in case["spec"]:
+        gm.set_prediction_data(vecchia_pred_type=case["spec"]["vecchia_pred_type"])
+    nsim = 4000
+    gm.set_prediction_data(nsim_var_pred=nsim)
+    pred = gm.predict(y=y, gp_coords_pred=Xp, cov_pars=case["cov_pars"], predict_cov_mat=True, predict_response=False)
+    ref_mu = np.asarray(case["mean"])
+    np.testing.assert_allclose(pred["mu"], ref_mu, rtol=1e-6, atol=1e-6 * np.abs(ref_mu).max())
+    npred = case["npred"]
+    ref = np.asarray(case["cov"]).reshape(npred, npred)
+    c = pred["cov"]
+    np.testing.assert_allclose(c, c.T, rtol=0, atol=1e-12 * np.abs(c).max())
+    assert np.all(np.diag(c) > 0)
+    bound = 6 * _cov_bound(ref, nsim, case["nsim"])
+    assert np.all(np.abs(c - ref) <= bound), np.max(np.abs(c - ref) / bound)
+
+
+@pytest.mark.parametrize("name", ["bern_n2000_tight_condall", "gauss_n2000_tight_condall"])
+def test_latent_pred_cond_all(golden, name):
+    """latent_order_obs_first_cond_all for latent models: mean = -Bp^-1 Bpo mode (likelihoods.h:6613-6616)
+    at 1e-6; variances statistically as in test_latent_pred_var_statistical."""
+    case = golden[name]
+    gm, X, y, Xp = _setup(case)
+    nsim = 4000
+    gm.set_prediction_data(vecchia_pred_type="latent_order_obs_first_cond_all", nsim_var_pred=nsim)
+    pred = gm.predict(y=y, gp_coords_pred=Xp, cov_pars=case["cov_pars"], predict_var=True, predict_response=False)
+    ref_mu, ref_var = np.asarray(case["mean"]), np.asarray(case["var"])
+    np.testing.assert_allclose(pred["mu"], ref_mu, rtol=1e-6, atol=1e-6 * np.abs(ref_mu).max())
+    se = np.sqrt(2. / nsim + 2. / case["nsim"])
+    rel = (pred["var"] - ref_var) / ref_var
+    assert np.all(np.abs(rel) <= 6 * se), (np.abs(rel).max(), 6 * se)
+    assert abs(rel.mean()) <= 0.01, rel.mean()
