@@ -84,6 +84,82 @@ __global__ void __launch_bounds__(64) diag_kernel(double* A, int lda, int ib, do
     if (i < ib && r < ib) Winv[(size_t)i + (size_t)r * ldw] = (r <= i) ? x[i] : 0.;
 }
 
+// V4: full 64 block without per-step branches, reciprocal multiply, column j+1 updated first (the
+//     next pivot's sqrt / reciprocal can overlap the rest of the step's FMAs); inverse with the
+//     diagonal reciprocals from the factorization and 4 partial sums
+template <int V>
+__global__ void __launch_bounds__(64) diag_kernel_la(double* A, int lda, double* Winv, int ldw, int* info) {
+  __shared__ double colb[2][64];
+  __shared__ double Ls[64][65];
+  __shared__ double rdg[64];
+  const int r = threadIdx.x;
+  double row[64];
+#pragma unroll
+  for (int c = 0; c < 64; ++c) row[c] = (c <= r) ? A[(size_t)r + (size_t)c * lda] : 0.;
+#pragma unroll
+  for (int j = 0; j < 64; ++j) {
+    const double p = __shfl(row[j], j, 64);
+    const double d = p > 0. ? sqrt(p) : 1.;
+    if (!(p > 0.) && r == 0) atomicAdd(info, 1);
+    const double rd = 1. / d;
+    const double l = (r > j) ? row[j] * rd : (r == j ? d : 0.);
+    if (r >= j) row[j] = l;
+    if (r == j) rdg[j] = rd;
+    colb[j & 1][r] = l;
+    __syncthreads();
+    if (j + 1 < 64) row[j + 1] = fma(-l, colb[j & 1][j + 1], row[j + 1]);
+#pragma unroll
+    for (int c = j + 2; c < 64; ++c) row[c] = fma(-l, colb[j & 1][c], row[c]);
+#pragma unroll
+    for (int c = j + 1; c < 64; ++c) asm volatile("" : "+v"(row[c]));   // keep the step's updates in place
+  }
+#pragma unroll
+  for (int c = 0; c < 64; ++c) {
+    Ls[r][c] = row[c];
+    if (c <= r) A[(size_t)r + (size_t)c * lda] = row[c];
+  }
+  if constexpr (V == 1) return;
+  __syncthreads();
+  // column r of L^-1 in LDS (X[i][r]), terms p < r are zero: start at p = r
+  __shared__ double X[64][65];
+  for (int i = 0; i < 64; ++i) {
+    double s0 = (i == r) ? 1. : 0., s1 = 0.;
+    int p = r;
+    for (; p + 1 < i; p += 2) {
+      s0 -= Ls[i][p] * X[p][r];
+      s1 -= Ls[i][p + 1] * X[p + 1][r];
+    }
+    if (p < i) s0 -= Ls[i][p] * X[p][r];
+    X[i][r] = (i >= r) ? (s0 + s1) * rdg[i] : 0.;
+  }
+  for (int i = 0; i < 64; ++i) Winv[(size_t)i + (size_t)r * ldw] = (r <= i) ? X[i][r] : 0.;
+}
+
+template <int V>
+int run_la(const std::vector<double>& h, double* dA, double* dW, int* dinfo, const char* name) {
+  const int reps = 200;
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  float tot = 0.f;
+  for (int r = 0; r <= reps; ++r) {
+    CK(hipMemcpy(dA, h.data(), sizeof(double) * 64 * 64, hipMemcpyHostToDevice));
+    CK(hipEventRecord(a, 0));
+    hipLaunchKernelGGL(diag_kernel_la<V>, dim3(1), dim3(64), 0, 0, dA, 64, dW, 64, dinfo);
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, a, b));
+    if (r > 0) tot += ms;
+  }
+  std::vector<double> W(64 * 64);
+  CK(hipMemcpy(W.data(), dW, sizeof(double) * 64 * 64, hipMemcpyDeviceToHost));
+  double chk = 0.;
+  for (double v : W) chk += v;
+  std::printf("%s: %.2f us per launch (checksum %.12g)\n", name, 1e3 * tot / reps, chk);
+  return 0;
+}
+
 template <int V>
 int run(const std::vector<double>& h, double* dA, double* dW, int* dinfo, const char* name) {
   const int reps = 200;
@@ -128,5 +204,26 @@ int main() {
   if (run<1>(h, dA, dW, dinfo, "V1 factor only")) return 1;
   if (run<2>(h, dA, dW, dinfo, "V2 inverse, 4 partial sums")) return 1;
   if (run<3>(h, dA, dW, dinfo, "V3 V2 + reciprocal multiply")) return 1;
+  if (run_la<1>(h, dA, dW, dinfo, "V4 lookahead factor only")) return 1;
+  if (run_la<0>(h, dA, dW, dinfo, "V5 lookahead factor + inverse")) return 1;
+  // back-to-back launches (no host copy in between: clocks stay up); the block is refactored in place
+  {
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    for (int v = 0; v < 2; ++v) {
+      CK(hipMemcpy(dA, h.data(), sizeof(double) * 64 * 64, hipMemcpyHostToDevice));
+      CK(hipEventRecord(a, 0));
+      for (int r = 0; r < 500; ++r) {
+        if (v == 0) hipLaunchKernelGGL(diag_kernel<0>, dim3(1), dim3(64), 0, 0, dA, 64, 64, dW, 64, dinfo);
+        else hipLaunchKernelGGL(diag_kernel_la<0>, dim3(1), dim3(64), 0, 0, dA, 64, dW, 64, dinfo);
+      }
+      CK(hipEventRecord(b, 0));
+      CK(hipEventSynchronize(b));
+      float ms = 0.f;
+      CK(hipEventElapsedTime(&ms, a, b));
+      std::printf("back-to-back %s: %.2f us per launch\n", v ? "V5" : "V0", 1e3 * ms / 500);
+    }
+  }
   return 0;
 }
