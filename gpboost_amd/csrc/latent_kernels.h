@@ -142,6 +142,28 @@ void launch_merged_scale(const MergedSolve& ms, const double* dw, double* coef, 
 // coef = ms.eval for the B^T solve, the launch_merged_scale output for the lower solve
 void launch_merged_level(const MergedSolve& ms, int L, const double* coef, const double* in, double* X, int t,
                          hipStream_t s);
+// Persistent form of one whole tail solve (vadu_level.hip, GPBOOST_AMD_TAIL_FORM=persist): ONE launch
+// runs every merged level, with a grid barrier between merged levels instead of a kernel boundary, so
+// the rows a level writes stay in its XCD's L2 for the later levels that gather them (a kernel
+// boundary invalidates L2). Workgroup b belongs to XCD group b % 8 (the dispatch order), and group x
+// solves the x-th eighth of every merged level's positions (Morton-sorted: one compact region of the
+// domain), so most gathers stay inside one XCD. Tail values go to a padded copy Tp (row stride 64
+// doubles = four whole cache lines: a line has one writer and is never read before it is written)
+// and to the caller's X.
+constexpr int kTailBit = 1 << 30;   // eidx_p: an X entry on a tail row (read from Tp)
+constexpr int kTailPad = 64;        // Tp row stride (doubles); t <= kTailPad
+struct TailPersist {
+  const int* lptr;    // nL + 1 merged level boundaries (device copy of MergedSolve::lptr)
+  int nL;
+  const int* eidx_p;  // MergedSolve::eidx with kTailBit on X entries whose row is a tail row
+  int W;              // workgroups per XCD group (grid 8 W; all resident at once)
+  int diag;           // timing diagnostics only (TimeParts): 1 = no barriers, 2 = no gathers
+};
+// counters: nL x 9 unsigned, zeroed by the call before the launch (stream order)
+void launch_tail_persist(const MergedSolve& ms, const TailPersist& tp, unsigned* counters, const double* coef,
+                         const double* in, const double* Xr, double* Tp, double* X, int t, hipStream_t s);
+// workgroups per XCD group the persistent tail kernel can keep resident (0: not available)
+int tail_persist_max_w();
 // LDS segment kernel (vadu_head.hip): ONE workgroup per column solves a segment of K rows with
 // the column's segment values resident in LDS (slot = position in the segment); a level costs an
 // LDS gather + a workgroup barrier instead of a launch. Dependencies outside the segment were

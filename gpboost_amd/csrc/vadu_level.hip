@@ -319,7 +319,172 @@ void launch_level(const MergedSolve& ms, const double* coef, int p0, int cnt, co
   launch_chunk(ks.nw, ks.ch, g, b, s, ms, coef, p0, in, X, t);
 }
 
+// ---- persistent tail solve (TailPersist, latent_kernels.h)
+//
+// Grid barrier between merged levels, bounded: every wave's stores are acknowledged by L2
+// (vmcnt(0)), then one thread per workgroup writes back its XCD's L2 (agent-scope release),
+// counts in at its group's counter (the last of the W workgroups of a group counts in at the level
+// counter) and polls the level counter until all 8 groups are in. No acquire on the way out: the
+// values read after the barrier are Tp rows written once in this launch and never read before
+// (their lines hold no stale copy anywhere); a foreign XCD's row misses in L2 and is fetched from
+// memory, a local one is served by L2. A poll that runs out (a workgroup never became resident)
+// poisons this workgroup's results with NaN, which the PCG reports, instead of hanging.
+template <int REL>
+__device__ __forceinline__ bool tail_grid_barrier(unsigned* ctr, int grp, int W, int* s_ok) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    if constexpr (REL == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    const unsigned old = __hip_atomic_fetch_add(ctr + grp, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (unsigned)W - 1) __hip_atomic_fetch_add(ctr + 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int ok = 1;
+    for (int spins = 0; __hip_atomic_load(ctr + 8, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 8u;) {
+      __builtin_amdgcn_s_sleep(1);
+      if (++spins > (1 << 22)) {
+        ok = 0;
+        break;
+      }
+    }
+    *s_ok = ok;
+  }
+  __syncthreads();
+  return *s_ok != 0;
+}
+
+// R rows per wave (lane = column), each row's entries in ascending order into its own accumulator
+// (the order of merged_levelW_kernel): a chunk of 64 entries of a row is one coalesced structure
+// load, each gather takes its row and coefficient by v_readlane, and the R rows' gathers of a
+// CH-entry step are issued together (R * CH in flight: the persistent grid has few waves per CU,
+// so the memory parallelism has to come from within the wave). IN entries read `in`, X entries on
+// tail rows Tp, other X entries (head rows of the lower solve, final before the launch) Xr.
+template <int R, int CH, int REL>
+__global__ void __launch_bounds__(256) tail_persist_kernel(MergedSolve ms, TailPersist tp, unsigned* ctr,
+                                                           const double* __restrict__ coef, const double* in,
+                                                           const double* Xr, double* Tp, double* X, int t) {
+  __shared__ int s_ok;
+  // lines of Tp cached by an earlier launch would be stale: drop this XCD's clean lines first
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int grp = blockIdx.x & 7;
+  const int qw = (blockIdx.x >> 3) * 4 + wave;
+  const int nwv = tp.W * 4;
+  const int cc = lane < t ? lane : t - 1;
+  bool good = true;
+  for (int L = 0; L < tp.nL; ++L) {
+    const int p0 = tp.lptr[L], cnt = tp.lptr[L + 1] - p0;
+    const int q0 = p0 + (int)(((long)cnt * grp) >> 3), q1 = p0 + (int)(((long)cnt * (grp + 1)) >> 3);
+    for (int pb = q0 + qw; pb < q1; pb += R * nwv) {
+      int i[R], e0[R], ex[R], len[R];
+      int lmax = 0;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const int p = pb + r * nwv;
+        const bool v = p < q1;
+        i[r] = v ? ms.rows[p] : -1;
+        e0[r] = v ? ms.eoff[p] : 0;
+        ex[r] = v ? ms.xoff[p] : 0;
+        len[r] = v ? ms.eoff[p + 1] - e0[r] : 0;
+        lmax = max(lmax, len[r]);
+      }
+      double s[R];
+#pragma unroll
+      for (int r = 0; r < R; ++r) s[r] = 0.;
+      for (int b = 0; b < (tp.diag == 2 ? 0 : lmax); b += 64) {
+        int my_id[R];
+        double my_w[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+          const bool ok = b + lane < len[r];
+          my_id[r] = ok ? tp.eidx_p[e0[r] + b + lane] : 0;
+          my_w[r] = ok ? coef[e0[r] + b + lane] : 0.;
+        }
+        const int nb = min(64, lmax - b);
+        for (int c0 = 0; c0 < nb; c0 += CH) {
+          double w[R][CH], g[R][CH];
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+#pragma unroll
+            for (int q = 0; q < CH; ++q) {
+              const int k = b + c0 + q;   // entry k of row r
+              const bool okq = k < len[r];
+              const int id = __builtin_amdgcn_readlane(my_id[r], okq ? c0 + q : 0);
+              w[r][q] = okq ? readlane_f64(my_w[r], c0 + q) : 0.;
+              const double* src = !okq                 ? in
+                                  : e0[r] + k < ex[r]  ? in + (size_t)id * t
+                                  : (id & kTailBit)    ? Tp + (size_t)(id & ~kTailBit) * kTailPad
+                                                       : Xr + (size_t)id * t;
+              g[r][q] = src[cc];
+            }
+          }
+#pragma unroll
+          for (int r = 0; r < R; ++r) {
+#pragma unroll
+            for (int q = 0; q < CH; ++q) s[r] = fma(w[r][q], g[r][q], s[r]);
+          }
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if (i[r] < 0) continue;
+        const double v = good ? s[r] : __builtin_nan("");
+        if (lane < t) {
+          // REL 1: written through to memory (agent-scope store), no L2 write-back at the barrier
+          if constexpr (REL == 1) __hip_atomic_store(Tp + (size_t)i[r] * kTailPad + lane, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          else Tp[(size_t)i[r] * kTailPad + lane] = v;
+          X[(size_t)i[r] * t + lane] = v;
+        }
+      }
+    }
+    if (L + 1 < tp.nL && tp.diag != 1) good = tail_grid_barrier<REL>(ctr + (size_t)L * 9, grp, tp.W, &s_ok) && good;
+  }
+}
+
 }  // namespace
+
+int tail_persist_max_w() {
+  static int w = -1;
+  if (w < 0) {
+    int dev = 0, cus = 0, per_cu = 0;
+    HIP_CHECK(hipGetDevice(&dev));
+    HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tail_persist_kernel<8, 8, 1>, 256, 0));
+    w = (cus % 8 == 0) ? (per_cu * cus) / 8 : 0;
+  }
+  return w;
+}
+
+void launch_tail_persist(const MergedSolve& ms, const TailPersist& tp, unsigned* counters, const double* coef,
+                         const double* in, const double* Xr, double* Tp, double* X, int t, hipStream_t s) {
+  if (tp.nL <= 0 || t <= 0) return;
+  if (t > kTailPad) Fatal("persistent tail solve: %d columns > %d", t, kTailPad);
+  if (tp.W < 1 || tp.W > tail_persist_max_w()) Fatal("persistent tail solve: %d workgroups per XCD not resident", tp.W);
+  HIP_CHECK(hipMemsetAsync(counters, 0, sizeof(unsigned) * 9 * (size_t)tp.nL, s));
+  // A/B: GPBOOST_AMD_TAIL_REL 0 = L2 write-back at the barrier, 1 = stores written through (default);
+  // GPBOOST_AMD_TAIL_RCH = rows per wave x gathers per row step: 4x8 (default), 2x16, 8x4, 8x8
+  static const int rel = [] {
+    const char* e = std::getenv("GPBOOST_AMD_TAIL_REL");
+    return e ? std::atoi(e) : 1;
+  }();
+  static const std::string rch = [] {
+    const char* e = std::getenv("GPBOOST_AMD_TAIL_RCH");
+    const std::string v = e ? e : "4x8";
+    if (v != "4x8" && v != "2x16" && v != "8x4" && v != "8x8") Fatal("GPBOOST_AMD_TAIL_RCH must be 4x8, 2x16, 8x4 or 8x8");
+    return v;
+  }();
+  const dim3 g(8 * tp.W), b(256);
+#define GPB_TAIL_LAUNCH(R, CH)                                                                                   \
+  do {                                                                                                          \
+    if (rel == 0) hipLaunchKernelGGL((tail_persist_kernel<R, CH, 0>), g, b, 0, s, ms, tp, counters, coef, in, Xr, Tp, X, t); \
+    else hipLaunchKernelGGL((tail_persist_kernel<R, CH, 1>), g, b, 0, s, ms, tp, counters, coef, in, Xr, Tp, X, t);      \
+  } while (0)
+  if (rch == "2x16") GPB_TAIL_LAUNCH(2, 16);
+  else if (rch == "8x4") GPB_TAIL_LAUNCH(8, 4);
+  else if (rch == "8x8") GPB_TAIL_LAUNCH(8, 8);
+  else GPB_TAIL_LAUNCH(4, 8);
+#undef GPB_TAIL_LAUNCH
+  HIP_CHECK(hipGetLastError());
+}
 
 void launch_merged_numeric(const MergedSolve& ms, const double* Bv, hipStream_t s) {
   for (size_t o = 0; o + 1 < ms.offptr.size(); ++o) {

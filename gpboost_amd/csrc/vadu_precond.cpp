@@ -22,7 +22,7 @@ void VaduPrecond::DropGraphs() {
 }
 
 int VaduPrecond::launches() const {
-  int c = tail_levels_bt() + tail_levels_lower();
+  int c = tail_persist_ ? 2 : tail_levels_bt() + tail_levels_lower();
   if (K_ > 0) ++c;                          // tail -> head partial
   if (K_ > K0_) c += 2;                     // the two segment solves
   if (K0_ > 0) c += 2 + (K_ > K0_ ? 2 : 0); // two dense products (+ the two head-1 <-> head-0 partials)
@@ -311,6 +311,47 @@ void VaduPrecond::Build(const int* nbr, const std::vector<int>& vo, const std::v
     }
     tail_entries_ = (long)nval;
     d_mcoef_.alloc(std::max<size_t>(hs[1]->eidx.size(), 1));
+
+    // persistent tail form: device level boundaries and entry rows tagged with kTailBit where an
+    // X entry's row is a tail row (read from the padded copy), per solve
+    tail_persist_ = false;
+    if (const char* e = std::getenv("GPBOOST_AMD_TAIL_FORM")) {
+      const std::string f(e);
+      if (f != "persist" && f != "launch") Fatal("GPBOOST_AMD_TAIL_FORM must be persist or launch (got '%s')", e);
+      tail_persist_ = f == "persist";
+    }
+    if (tail_persist_) {
+      int W = std::min(64, tail_persist_max_w());
+      if (const char* e = std::getenv("GPBOOST_AMD_TAIL_W")) W = std::atoi(e);
+      if (W < 1 || W > tail_persist_max_w())
+        Fatal("GPBOOST_AMD_TAIL_W: %d workgroups per XCD group, at most %d resident", W, tail_persist_max_w());
+      std::vector<int> pint;
+      size_t po[2][2];
+      for (int w = 0; w < 2; ++w) {
+        const MergeHost& h = *hs[w];
+        po[w][0] = pint.size();
+        pint.insert(pint.end(), h.lptr.begin(), h.lptr.end());
+        po[w][1] = pint.size();
+        for (size_t p = 0; p < h.rows.size(); ++p)
+          for (int q = h.eoff[p]; q < h.eoff[p + 1]; ++q) {
+            const int r = h.eidx[q];
+            pint.push_back(q >= h.xoff[p] && part(r) == 2 ? (r | kTailBit) : r);
+          }
+      }
+      d_pint_.alloc(std::max<size_t>(pint.size(), 1));
+      HIP_CHECK(hipMemcpy(d_pint_.get(), pint.data(), sizeof(int) * pint.size(), hipMemcpyHostToDevice));
+      for (int w = 0; w < 2; ++w) {
+        TailPersist& tp = w == 0 ? tp_bt_ : tp_low_;
+        tp.lptr = d_pint_.get() + po[w][0];
+        tp.nL = (int)hs[w]->lptr.size() - 1;
+        tp.eidx_p = d_pint_.get() + po[w][1];
+        tp.W = W;
+      }
+      for (int sl = 0; sl < kSlots; ++sl) {
+        Tp_[sl].release();
+        ctr_[sl].alloc((size_t)9 * std::max(1, tp_bt_.nL + tp_low_.nL));
+      }
+    }
   }
 
   // ---- head 1 segment [K0, K): slots = Vecchia index - K0, dependencies inside the segment
@@ -597,15 +638,22 @@ void VaduPrecond::SegSolve(bool lower, const double* in, const double* dw, doubl
   else launch_vadu_head(lower ? seg_low_ : seg_bt_, in, dw, X, t, st);
 }
 
-void VaduPrecond::TailSolve(bool lower, const double* R, double* Xt, double* Z, int t, hipStream_t st) {
+void VaduPrecond::TailSolve(bool lower, const double* R, double* Xt, double* Z, int t, hipStream_t st, int slot) {
   const MergedSolve& ms = lower ? mt_low_ : mt_bt_;
+  if (TailPersistOn(t)) {
+    // B^T solve: IN = R, values to Xt; lower solve: IN = Xt, head rows of Z final, values to Z
+    unsigned* ctr = ctr_[slot].get() + (lower ? (size_t)9 * tp_bt_.nL : 0);
+    if (lower) launch_tail_persist(ms, tp_low_, ctr, d_mcoef_.get(), Xt, Z, Tp_[slot].get(), Z, t, st);
+    else launch_tail_persist(ms, tp_bt_, ctr, ms.eval, R, Xt, Tp_[slot].get(), Xt, t, st);
+    return;
+  }
   for (int L = 0; L + 1 < (int)ms.lptr.size(); ++L)
     launch_merged_level(ms, L, lower ? d_mcoef_.get() : ms.eval, lower ? Xt : R, lower ? Z : Xt, t, st);
 }
 
-void VaduPrecond::Record(const double* R, double* Z, double* Xt, int t, hipStream_t st, double* S) {
+void VaduPrecond::Record(const double* R, double* Z, double* Xt, int t, hipStream_t st, double* S, int slot) {
   const bool seg = K_ > K0_;
-  TailSolve(false, R, Xt, Z, t, st);
+  TailSolve(false, R, Xt, Z, t, st, slot);
   // the last partial sum over the head-0 rows also stores them compactly for the dense products
   double* x0 = K0_ > 0 ? S : nullptr;
   if (K_ > 0) launch_vadu_partial(p_th_, R, nullptr, Xt, Xt, t, st, seg ? nullptr : x0, K0_);
@@ -622,7 +670,7 @@ void VaduPrecond::Record(const double* R, double* Z, double* Xt, int t, hipStrea
       SegSolve(true, Xt, dw_, Z, t, st);
     }
   }
-  TailSolve(true, R, Xt, Z, t, st);
+  TailSolve(true, R, Xt, Z, t, st, slot);
 }
 
 double* VaduPrecond::Scratch(int slot, int t) {
@@ -632,6 +680,11 @@ double* VaduPrecond::Scratch(int slot, int t) {
     DropGraphs();
     S_[slot].alloc((size_t)2 * ld0_ * t);
   }
+  if (TailPersistOn(t) && Tp_[slot].size() == 0) {
+    HIP_CHECK(hipDeviceSynchronize());
+    DropGraphs();
+    Tp_[slot].alloc((size_t)n_ * kTailPad);
+  }
   return S_[slot].get();
 }
 
@@ -640,7 +693,7 @@ void VaduPrecond::Apply(const double* R, double* Z, double* Xt, int t, hipStream
   if (!st) st = s_;
   double* S = Scratch(slot, t);
   if (!use_graph_) {
-    Record(R, Z, Xt, t, st, S);
+    Record(R, Z, Xt, t, st, S, slot);
     return;
   }
   for (const GraphEntry& g : graphs_) {
@@ -651,7 +704,7 @@ void VaduPrecond::Apply(const double* R, double* Z, double* Xt, int t, hipStream
   }
   hipGraph_t graph;
   HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-  Record(R, Z, Xt, t, st, S);
+  Record(R, Z, Xt, t, st, S, slot);
   HIP_CHECK(hipStreamEndCapture(st, &graph));
   GraphEntry e{{R, Z, Xt}, t, slot, nullptr};
   HIP_CHECK(hipGraphInstantiate(&e.exec, graph, nullptr, nullptr, 0));
@@ -675,14 +728,21 @@ void VaduPrecond::TimeParts(const double* R, double* Z, double* Xt, int t, int r
     HIP_CHECK(hipEventElapsedTime(&ms, a, b));
     std::fprintf(stderr, "[precond parts t=%d] %-11s %.4f ms\n", t, name, ms / reps);
   };
-  part("tail_bt", [&] { TailSolve(false, R, Xt, Z, t, s_); });
+  part("tail_bt", [&] { TailSolve(false, R, Xt, Z, t, s_, 0); });
   part("part_th", [&] { launch_vadu_partial(p_th_, R, nullptr, Xt, Xt, t, s_, seg ? nullptr : S, K0_); });
   if (seg) part("seg_bt", [&] { SegSolve(false, Xt, nullptr, Xt, t, s_); });
   if (K0_ > 0 && seg) part("part_10", [&] { launch_vadu_partial(p_10_, nullptr, nullptr, Xt, Xt, t, s_, S, K0_); });
   if (K0_ > 0) part("dense", [&] { DenseApply(S, Z, t, s_, S); });
   if (K0_ > 0 && seg) part("part_01", [&] { launch_vadu_partial(p_01_, Xt, dw_, Z, Z, t, s_); });
   if (seg) part("seg_low", [&] { SegSolve(true, Z, nullptr, Z, t, s_); });
-  part("tail_low", [&] { TailSolve(true, R, Xt, Z, t, s_); });
+  part("tail_low", [&] { TailSolve(true, R, Xt, Z, t, s_, 0); });
+  if (TailPersistOn(t)) {   // the persistent form without its barriers / without its gathers (timing only)
+    for (int d = 1; d <= 2; ++d) {
+      tp_bt_.diag = d;
+      part(d == 1 ? "tail_bt_nobar" : "tail_bt_nogath", [&] { TailSolve(false, R, Xt, Z, t, s_, 0); });
+    }
+    tp_bt_.diag = 0;
+  }
   std::fprintf(stderr,
                "[precond parts t=%d] K0=%d K=%d passes bt=%d low=%d tail merged levels bt=%d low=%d (g=%d, %ld entries) "
                "launches=%d\n",

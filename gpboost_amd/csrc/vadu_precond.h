@@ -72,8 +72,8 @@ class VaduPrecond {
   int launches() const;   // dependent launches per application
 
  private:
-  void Record(const double* R, double* Z, double* Xt, int t, hipStream_t st, double* S);
-  void TailSolve(bool lower, const double* R, double* Xt, double* Z, int t, hipStream_t st);
+  void Record(const double* R, double* Z, double* Xt, int t, hipStream_t st, double* S, int slot);
+  void TailSolve(bool lower, const double* R, double* Xt, double* Z, int t, hipStream_t st, int slot);
   void DenseApply(const double* X0, double* Z, int t, hipStream_t st, double* S);
   double* Scratch(int slot, int t);
 
@@ -87,6 +87,13 @@ class VaduPrecond {
   DevBuf<double> d_mval_;
   DevBuf<double> d_mcoef_;   // lower-solve coefficients with 1/dw folded in (SetDiag)
   int merge_g_ = 1;
+  // persistent tail solves (GPBOOST_AMD_TAIL_FORM=persist; TailPersist, latent_kernels.h)
+  bool tail_persist_ = false;
+  TailPersist tp_bt_{}, tp_low_{};
+  DevBuf<int> d_pint_;                 // both solves' level boundaries and tagged entry rows
+  DevBuf<double> Tp_[2];               // padded tail values per scratch slot (n x kTailPad)
+  DevBuf<unsigned> ctr_[2];            // barrier counters per scratch slot
+  bool TailPersistOn(int t) const { return tail_persist_ && t >= 2 && t <= kTailPad; }
   long tail_entries_ = 0;
   HeadSolve seg_bt_{}, seg_low_{};
   SegWave segw_bt_{}, segw_low_{};   // the one-wave form of the same segment solves (default)

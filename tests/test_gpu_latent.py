@@ -204,6 +204,40 @@ def test_segment_and_tail_forms_agree(monkeypatch, seg_form, tail_order):
         np.testing.assert_allclose(b[1], a[1], rtol=1e-7, atol=1e-7 * np.abs(a[1]).max())
 
 
+@pytest.mark.parametrize("dense_rows,head_rows,merge,w", [("256", "6000", "4", "64"), ("0", "0", "1", "8"),
+                                                           ("2048", "2048", "16", "3")])
+def test_persistent_tail_agrees(monkeypatch, dense_rows, head_rows, merge, w):
+    """The persistent tail solve (GPBOOST_AMD_TAIL_FORM=persist: all merged levels in one launch with
+    grid barriers, values through a padded copy) against the plain level schedule at a tight CG
+    tolerance (same algebra, other summation order: ~1e-10), and bit for bit repeatable (fixed entry
+    order per row). Covers a tail after dense + segment heads, a tail without heads at g = 1 (many
+    barriers, head rows of the lower solve read from the caller's buffer) and few workgroups per XCD
+    group (rows looped per wave)."""
+    from gpboost_amd import synthetic
+    n = 8000
+    X = synthetic.bench_coords(n)
+    for lik in ("gaussian", "bernoulli_logit"):
+        y = synthetic.bench_gaussian_y(n) if lik == "gaussian" else synthetic.bench_bernoulli_y(X)
+        case = dict(likelihood=lik, cov_fct="exponential", shape=0.5, num_neighbors=30, aux=0.1)
+        out = {}
+        for key, (k0, k, g, form) in {"levels": ("0", "0", "1", "launch"),
+                                      "persist": (dense_rows, head_rows, merge, "persist"),
+                                      "again": (dense_rows, head_rows, merge, "persist")}.items():
+            monkeypatch.setenv("GPBOOST_AMD_DENSE_ROWS", k0)
+            monkeypatch.setenv("GPBOOST_AMD_HEAD_ROWS", k)
+            monkeypatch.setenv("GPBOOST_AMD_TAIL_MERGE", g)
+            monkeypatch.setenv("GPBOOST_AMD_TAIL_FORM", form)
+            monkeypatch.setenv("GPBOOST_AMD_TAIL_W", w)
+            gm = _model(X, case, t=12, dc=1e-9)
+            out[key] = gm.neg_log_likelihood_and_grad([1.0, 0.1], y)
+        a, b = out["levels"], out["persist"]
+        assert np.isfinite(b[0]) and np.all(np.isfinite(b[1]))
+        assert abs(a[0] - b[0]) <= 1e-9 * abs(a[0]), (lik, a[0], b[0])
+        np.testing.assert_allclose(b[1], a[1], rtol=1e-7, atol=1e-7 * np.abs(a[1]).max())
+        assert out["again"][0] == b[0]
+        np.testing.assert_array_equal(out["again"][1], b[1])
+
+
 def test_graph_replay_matches_eager(monkeypatch):
     """VaduPrecond replays one captured hipGraph per buffer set (vadu_precond.cpp Apply). Replays after
     captures at other widths (bench_latent_operators at t = 51 and t = 1 on the model's scratch block),
