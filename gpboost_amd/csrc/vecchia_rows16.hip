@@ -43,6 +43,11 @@ constexpr int kD3 = 3;   // coordinate dimension bound (VecchiaRowsArgs.d <= 3)
 #ifndef GPB_ROWS16_FMAC
 #define GPB_ROWS16_FMAC 1
 #endif
+// pivots 16..29 eliminate only the B rows (h + 16); the A rows' solution is completed by one block
+// back-substitution x_A -= M_AB x_B afterwards (28 instead of 119 fused broadcasts per problem)
+#ifndef GPB_ROWS16_BACKSUB
+#define GPB_ROWS16_BACKSUB 1
+#endif
 
 __device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void cfence() { asm volatile("" ::: "memory"); }
@@ -263,12 +268,13 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       // each broadcast folded into its two FMAs: v_fmac_f64_dpp row_newbcast (gfx950 takes DPP on the
       // 64-bit fmac; the compiler never folds a 64-bit DPP move into its uses), so a column costs two
       // VALU ops instead of three and no move -> FMA dependency
-      const double nf0 = -f0, nf1 = -f1;
+      constexpr bool upd0 = !GPB_ROWS16_BACKSUB || !jhi;   // A rows take part in pivots 0..15 only
+      const double nf0 = upd0 ? -f0 : 0., nf1 = -f1;
       asm volatile("s_nop 1" ::: "memory");   // VALU write -> DPP read wait states (not visible inside asm)
       sfor<j + 1, kK>([&](auto C) {
         constexpr int c = decltype(C)::value;
         const double& src = c >= 16 ? r1[j] : r0[j];
-        fmac_bcast16<c & 15>(r0[c], src, nf0);
+        if constexpr (upd0) fmac_bcast16<c & 15>(r0[c], src, nf0);
         fmac_bcast16<c & 15>(r1[c], src, nf1);
       });
 #elif GPB_ROWS16_BCG > 1
@@ -307,8 +313,23 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
 #endif
       // pin this step's updates (otherwise the FMAs are deferred and the broadcasts stay live)
 #pragma unroll
-      for (int c = j + 1; c < kK; ++c) asm volatile("" : "+v"(r0[c]), "+v"(r1[c]));
+      for (int c = j + 1; c < kK; ++c) {
+        if (GPB_ROWS16_BACKSUB && jhi) asm volatile("" : "+v"(r1[c]));
+        else asm volatile("" : "+v"(r0[c]), "+v"(r1[c]));
+      }
     });
+#if GPB_ROWS16_FMAC && GPB_ROWS16_BACKSUB
+    {   // A rows: M[h][30..31] -= sum_{c=16..29} M[h][c] x_c, x_c = M[c][30..31] / M[c][c] (lane c - 16)
+      const double i1 = recip(dg1);
+      const double na = rv1 ? -(r1[kMK] * i1) : 0., nw = rv1 ? -(r1[kMK + 1] * i1) : 0.;
+      asm volatile("s_nop 1" ::: "memory");
+      sfor<16, kMK>([&](auto C) {
+        constexpr int c = decltype(C)::value;
+        fmac_bcast16<c & 15>(r0[kMK], na, r0[c]);
+        fmac_bcast16<c & 15>(r0[kMK + 1], nw, r0[c]);
+      });
+    }
+#endif
     {   // the stashed c, dc, y_nbr back (read before the [a, w] array below overwrites the area)
       lds_sync();
       const v2d* st = reinterpret_cast<const v2d*>(__builtin_assume_aligned(nbx, 16)) + 3 * h;
