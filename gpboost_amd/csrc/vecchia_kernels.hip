@@ -858,12 +858,51 @@ __global__ void __launch_bounds__(kV4Threads, 1) vecchia_rows2_kernel(VecchiaRow
   }
 }
 
+// A/B: GPB_SUM_FAST 1 = every partial load of a thread in flight at once and the published sums
+// written through with system-scope stores (then the flag after their acknowledgement), 0 = four
+// loads per step and a system-scope release fence (an L2 write-back) before the flag
+#ifndef GPB_SUM_FAST
+#define GPB_SUM_FAST 1
+#endif
 __global__ void __launch_bounds__(1024) sum_blocks_kernel(const double* __restrict__ in, int nblocks, int width,
                                                        double* __restrict__ out, unsigned long long* flag,
                                                        unsigned long long seq) {
-  // width <= 8: thread t sums column (t & 7) over blocks (t >> 3) + 128 u, four loads in flight
+  // width <= 8: thread t sums column (t & 7) over blocks (t >> 3) + 128 u
   __shared__ double red[1024];
   const int col = threadIdx.x & 7, lane_b = threadIdx.x >> 3;
+#if GPB_SUM_FAST
+  double acc = 0.;
+  if (col < width) {
+    constexpr int kU = 16;   // 2048 blocks (the row kernels' grid bound) in one round of loads
+    int b0 = 0;
+    for (; b0 + 128 * kU <= nblocks; b0 += 128 * kU) {
+      double v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) v[u] = in[(size_t)(b0 + lane_b + 128 * u) * width + col];
+#pragma unroll
+      for (int w = kU / 2; w >= 1; w >>= 1) {
+#pragma unroll
+        for (int u = 0; u < w; ++u) v[u] += v[u + w];
+      }
+      acc += v[0];
+    }
+    if (b0 < nblocks) {
+      double v[kU];
+#pragma unroll
+      for (int u = 0; u < kU; ++u) {
+        const int b = b0 + lane_b + 128 * u;
+        v[u] = b < nblocks ? in[(size_t)b * width + col] : 0.;
+      }
+#pragma unroll
+      for (int w = kU / 2; w >= 1; w >>= 1) {
+#pragma unroll
+        for (int u = 0; u < w; ++u) v[u] += v[u + w];
+      }
+      acc += v[0];
+    }
+  }
+  red[threadIdx.x] = acc;
+#else
   double acc0 = 0., acc1 = 0., acc2 = 0., acc3 = 0.;
   if (col < width) {
     int b = lane_b;
@@ -876,11 +915,23 @@ __global__ void __launch_bounds__(1024) sum_blocks_kernel(const double* __restri
     for (; b < nblocks; b += 128) acc0 += in[(size_t)b * width + col];
   }
   red[threadIdx.x] = (acc0 + acc1) + (acc2 + acc3);
+#endif
   __syncthreads();
   for (int off = 512; off >= 8; off >>= 1) {
     if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
     __syncthreads();
   }
+#if GPB_SUM_FAST
+  if ((int)threadIdx.x < width) {
+    if (flag != nullptr) __hip_atomic_store(out + threadIdx.x, red[threadIdx.x], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    else out[threadIdx.x] = red[threadIdx.x];
+  }
+  if (flag != nullptr) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the written-through sums are acknowledged
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+#else
   if ((int)threadIdx.x < width) {
     out[threadIdx.x] = red[threadIdx.x];
     if (flag != nullptr) __threadfence_system();   // the sums reach the host before the flag
@@ -889,6 +940,7 @@ __global__ void __launch_bounds__(1024) sum_blocks_kernel(const double* __restri
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+#endif
 }
 
 // One thread per prediction point; entries in neighbour order.
