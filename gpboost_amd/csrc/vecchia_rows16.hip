@@ -10,15 +10,17 @@
 // Four problems per wave, one per DPP row. The 32-lane form broadcasts every value through an LDS
 // slot (a 16-byte read per two values per lane): at 2 waves/SIMD its LDS return traffic, not the FP64
 // VALU, set the pace.
-//   1. coordinates of the 32 rows (two copies of rows 0..15, so partner r + delta < 48 is an
-//      immediate-offset read); lane h computes the circulant pairs {v, v + delta}, v in {h, h + 16},
-//      delta = 1..16 (the pair {h, h + 16} once): C to the packed lower triangle in LDS, dC/dlog(phi)
-//      in registers until the rows are loaded, then over the packed C in the circulant layout
-//      W[(delta - 1) 32 + v];
+//   1. a 31-point circulant over the 30 neighbours and the row's own point (slot 30 = lane 14's second
+//      slot): slot v pairs with (v + delta) mod 31, delta = 1..15, so the 465 pairs are each evaluated
+//      once (30 kernel evaluations per lane; slot 30's pairs are the border column c). Coordinates in
+//      LDS with copies of slots 0..15 at 31..46 (partner v + delta is an immediate-offset read). C to
+//      the packed lower triangle, dC/dlog(phi) in registers until the rows are loaded, then over the
+//      packed C in the circulant layout W[(delta - 1) 32 + v];
 //   2. rows h and h + 16 of the bordered matrix into registers; 30 Gauss-Jordan steps by DPP
-//      broadcasts; a_v = M[v][30] / M[v][v], w_v = M[v][31] / M[v][v] (the pivots are captured
+//      broadcasts (pivots 16..29 on the B rows only, the A rows finished by one block
+//      back-substitution); a_v = M[v][30] / M[v][v], w_v = M[v][31] / M[v][v] (the pivots are captured
 //      when broadcast);
-//   3. a^T dC a and w^T dC a over each lane's circulant pairs ([a, w] pairs in a doubled LDS array);
+//   3. a^T dC a and w^T dC a over each lane's circulant pairs ([a, w] pairs with the same wrap copies);
 //   4. the eight group sums by DPP within the 16-lane row, then the six row partials.
 #include <hip/hip_runtime.h>
 
@@ -149,43 +151,30 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     const double yi = want_like ? a.Y[irow] : 0.;
     double y0s = (want_like && rv0) ? a.Y[nb0] : 0.;
     double y1s = (want_like && rv1) ? a.Y[nb1] : 0.;
-    // padding rows at distinct far-away points: covariances exactly 0 (see vecchia_rows_kernel)
+    // padding rows at distinct far-away points: covariances exactly 0 (see vecchia_rows_kernel); slot
+    // 30 (lane 14's second slot) is the row's own point, lane 15's second slot (31) holds no point
+    const bool own1 = v1 == kMK;
+#pragma unroll
+    for (int q = 0; q < ND; ++q) x1[q] = own1 ? xi[q] : x1[q];
     x0[0] = rv0 ? x0[0] : 1e30 * (h + 1);
-    x1[0] = rv1 ? x1[0] : 1e30 * (v1 + 1);
+    x1[0] = (rv1 || own1) ? x1[0] : 1e30 * (v1 + 1);
     cfence();   // the previous problem's LDS reads are issued before these writes
 #pragma unroll
     for (int q = 0; q < ND; ++q) {
       nbx[h * CS + q] = x0[q];
-      nbx[v1 * CS + q] = x1[q];
-      nbx[(h + 32) * CS + q] = x0[q];
-    }
-    double c0, dc0, c1, dc1;
-    {
-      double s0 = 0., s1 = 0.;
-#pragma unroll
-      for (int q = 0; q < ND; ++q) {
-        const double t0 = xi[q] - x0[q], t1 = xi[q] - x1[q];
-        s0 += t0 * t0;
-        s1 += t1 * t1;
-      }
-      cov_dcov_sq<COV>(s0, var, phi, c0, dc0);
-      cov_dcov_sq<COV>(s1, var, phi, c1, dc1);
-      c0 = rv0 ? c0 : 0.;
-      dc0 = rv0 ? dc0 : 0.;
-      c1 = rv1 ? c1 : 0.;
-      dc1 = rv1 ? dc1 : 0.;
+      nbx[(h + 31) * CS + q] = x0[q];   // partners past slot 30 wrap: copies of slots 0..15 at 31..46
+      if (v1 <= kMK) nbx[v1 * CS + q] = x1[q];
     }
     Cp[tri(h) + h] = rv0 ? cdiag : 1.;
-    Cp[tri(v1) + v1] = rv1 ? cdiag : 1.;
+    Cp[tri(v1) + v1] = rv1 ? cdiag : 1.;   // slots 30, 31: 1 (border rows, not pivots)
     lds_sync();
 
-    // ---- 1. circulant pairs: row h with h + delta (delta = 1..16), row h + 16 with h + 16 + delta
-    // (delta = 1..15; past 31 it wraps to the first coordinate copy's duplicate at +32)
-    double w0[16], w1[15];
+    // ---- 1. circulant pairs: slot v with (v + delta) mod 31, delta = 1..15, for v = h and v = h + 16
+    double w0[15], w1[15];
     {
       const int b0 = tri(h) + h, b1 = tri(v1) + v1;
 #pragma unroll
-      for (int dl = 1; dl <= 16; ++dl) {
+      for (int dl = 1; dl <= 15; ++dl) {
         const double* xp = nbx + (h + dl) * CS;
         double s = 0.;
 #pragma unroll
@@ -209,43 +198,39 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         }
         double cv, dcv;
         cov_dcov_sq<COV>(s, var, phi, cv, dcv);
-        const int pos = (v1 + dl < kK) ? b1 + v1 * dl + dl * (dl + 1) / 2 : b1 + dl - kK;
+        // packed(v1 + dl, v1), or past slot 30 packed(v1, v1 + dl - 31) (slot 31: row 31, overwritten below)
+        const int pos = (v1 + dl <= kMK) ? b1 + v1 * dl + dl * (dl + 1) / 2 : b1 + dl - 31;
         Cp[pos] = cv;
         w1[dl - 1] = dcv;
       }
     }
     lds_sync();
-    // border rows 30 (c) and 31 (y_nbr)
-    Cp[tri(kMK) + h] = c0;
+    // border row 31 (y_nbr); row 30 (c) came from the slot-30 pairs
     Cp[tri(kMK + 1) + h] = y0s;
-    if (v1 < kMK) {
-      Cp[tri(kMK) + v1] = c1;
-      Cp[tri(kMK + 1) + v1] = y1s;
-    }
+    if (v1 < kMK) Cp[tri(kMK + 1) + v1] = y1s;
+    else if (v1 == kMK) Cp[tri(kMK + 1) + kMK] = 0.;
     lds_sync();
 
-    // c, dc and y_nbr of both rows wait out the elimination in the (now free) coordinate area
-    // instead of 12 registers (the elimination is register-bound)
-    cfence();
-    {
-      v2d* st = reinterpret_cast<v2d*>(__builtin_assume_aligned(nbx, 16)) + 3 * h;
-      st[0] = v2d{c0, dc0};
-      st[1] = v2d{c1, dc1};
-      st[2] = v2d{y0s, y1s};
-    }
-    // ---- 2. rows h and h + 16 into registers, dC over the packed C (circulant layout)
+    // ---- 2. rows h and h + 16 into registers; c and y_nbr (their columns 30, 31) wait out the
+    // elimination in the coordinate area; dC over the packed C (circulant layout W[(delta - 1) 32 + v])
     double r0[kK], r1[kK];
 #pragma unroll
     for (int c = 0; c < kK; ++c) {
       r0[c] = (c <= h) ? Cp[tri(h) + c] : Cp[tri(c) + h];
       r1[c] = (c <= v1) ? Cp[tri(v1) + c] : Cp[tri(c) + v1];
     }
+    double c0, c1, dc0, dc1;
     cfence();
+    {
+      v2d* st = reinterpret_cast<v2d*>(__builtin_assume_aligned(nbx, 16)) + 2 * h;
+      st[0] = v2d{r0[kMK], rv1 ? r1[kMK] : 0.};
+      st[1] = v2d{y0s, y1s};
+    }
 #pragma unroll
-    for (int dl = 1; dl <= 16; ++dl) Cp[(dl - 1) * kK + h] = w0[dl - 1];
-#pragma unroll
-    for (int dl = 1; dl <= 15; ++dl) Cp[(dl - 1) * kK + v1] = w1[dl - 1];
-    Cp[15 * kK + v1] = w0[15];   // the pair {h, h + 16}: both of its rows hold it (delta = 16)
+    for (int dl = 1; dl <= 15; ++dl) {
+      Cp[(dl - 1) * kK + h] = w0[dl - 1];
+      Cp[(dl - 1) * kK + v1] = w1[dl - 1];
+    }
 
     // Gauss-Jordan, 30 pivots: M[j][c] = M[c][j] from lane c mod 16 (register set c / 16)
     double dg0 = 1., dg1 = 1.;
@@ -330,16 +315,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       });
     }
 #endif
-    {   // the stashed c, dc, y_nbr back (read before the [a, w] array below overwrites the area)
+    {   // the stashed c, y_nbr back (read before the [a, w] array below overwrites the area); dc_v = dC(v, 30):
+        // the slot-30 pair at delta = v + 1 (v <= 14), slot v's pair at delta = 30 - v (v = 15..29)
       lds_sync();
-      const v2d* st = reinterpret_cast<const v2d*>(__builtin_assume_aligned(nbx, 16)) + 3 * h;
-      const v2d s0 = st[0], s1 = st[1], s2 = st[2];
+      const v2d* st = reinterpret_cast<const v2d*>(__builtin_assume_aligned(nbx, 16)) + 2 * h;
+      const v2d s0 = st[0], s1 = st[1];
       c0 = s0.x;
-      dc0 = s0.y;
-      c1 = s1.x;
-      dc1 = s1.y;
-      y0s = s2.x;
-      y1s = s2.y;
+      c1 = s0.y;
+      y0s = s1.x;
+      y1s = s1.y;
+      dc0 = Cp[h <= 14 ? h * kK + kMK : 14 * kK + 15];
+      dc1 = h <= 13 ? Cp[(13 - h) * kK + v1] : 0.;
     }
     const double i0 = recip(dg0), i1 = recip(dg1);
     const double a0 = rv0 ? r0[kMK] * i0 : 0., w0v = rv0 ? r0[kMK + 1] * i0 : 0.;
@@ -356,12 +342,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       v2d* av2 = reinterpret_cast<v2d*>(__builtin_assume_aligned(nbx, 16));
       cfence();
       av2[h] = v2d{a0, w0v};
-      av2[v1] = v2d{a1, w1v};
-      av2[h + 32] = v2d{a0, w0v};
+      if (v1 <= kMK) av2[v1] = v2d{a1, w1v};   // slot 30: a = w = 0
+      av2[h + 31] = v2d{a0, w0v};
       lds_sync();
       double s10 = 0., s20 = 0., s11 = 0., s21 = 0.;
 #pragma unroll
-      for (int dl = 1; dl < 16; ++dl) {
+      for (int dl = 1; dl <= 15; ++dl) {
         const double wa = Cp[(dl - 1) * kK + h], wb = Cp[(dl - 1) * kK + v1];
         const v2d pa = av2[h + dl], pb = av2[v1 + dl];
         s10 = fma(wa, pa.x, s10);
@@ -369,9 +355,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
         s11 = fma(wb, pb.x, s11);
         s21 = fma(wb, pb.y, s21);
       }
-      const double h0 = Cp[15 * kK + h] * av2[h + 16].x, h1 = Cp[15 * kK + v1] * av2[v1 + 16].x;
-      tA = a0 * (2. * s10 + h0) + a1 * (2. * s11 + h1);
-      tV = w0v * (s10 + h0) + a0 * s20 + w1v * (s11 + h1) + a1 * s21;
+      tA = 2. * (a0 * s10 + a1 * s11);
+      tV = w0v * s10 + a0 * s20 + w1v * s11 + a1 * s21;
     }
 
     // ---- 4. group sums (16 lanes) and the row partials
