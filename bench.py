@@ -698,6 +698,8 @@ def main():
     ap.add_argument("--no-grouped", action="store_true", help="skip the grouped random effects (config 4) leg")
     ap.add_argument("--only-grouped", action="store_true", help="run only the grouped leg (prints its JSON)")
     ap.add_argument("--no-fitc", action="store_true", help="skip the secondary FITC (§8 row f4) leg")
+    ap.add_argument("--no-row-shards", action="store_true",
+                    help="skip the per-rank row-range measurements (profiling the headline kernel alone)")
     ap.add_argument("--only-fitc", action="store_true", help="run only the FITC leg (prints its JSON)")
     args = ap.parse_args()
     if args.only_grouped:
@@ -820,7 +822,7 @@ def main():
                               "predictions_per_s": PRED_N / tp, "mean_of_mu": float(np.mean(pr["mu"])),
                               "note": "end to end: neighbour search among the 100k observed points (GPU), "
                                       "prediction rows (row kernel, 64-lane groups), mean/variance"}
-    if world == 1:
+    if world == 1 and not args.no_row_shards:
         line["row_shards"] = row_shard_leg(gm)
     if world == 1 and not args.no_fit:
         line["fit"] = fit_leg(X, Y, not args.no_cpu_baseline)

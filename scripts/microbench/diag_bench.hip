@@ -4,6 +4,7 @@
 //   V1: factorization only (no inverse)
 //   V2: production factorization, inverse with 4 independent partial sums per row
 //   V3: V2 + reciprocal-multiply instead of a divide per step
+//   V6, V7: see below (code size; the production kernel's fully unrolled form is ~19k instructions)
 // hipcc --offload-arch=gfx950 -O3 -o diag_bench diag_bench.hip && ./diag_bench
 #include <hip/hip_runtime.h>
 
@@ -135,6 +136,128 @@ __global__ void __launch_bounds__(64) diag_kernel_la(double* A, int lda, double*
   for (int i = 0; i < 64; ++i) Winv[(size_t)i + (size_t)r * ldw] = (r <= i) ? X[i][r] : 0.;
 }
 
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
+// V6: one wave, full 64 block always (a partial block padded with the identity), pivot by v_readlane,
+// reciprocal multiply, no per-step guards, column broadcast by one LDS write + 16-byte reads; inverse
+// with the diagonal reciprocals from the factorization (fewer instructions: the I-cache holds more of it)
+__global__ void __launch_bounds__(64) diag_v6(double* A, int lda, int ib, double* Winv, int ldw, int* info) {
+  typedef double v2d __attribute__((ext_vector_type(2)));
+  __shared__ __attribute__((aligned(16))) double colb[64];
+  __shared__ __attribute__((aligned(16))) double Ls[64][66];
+  __shared__ double rdg[64];
+  const int r = threadIdx.x;
+  const int rr = min(r, ib - 1);
+  double row[64];
+#pragma unroll
+  for (int c = 0; c < 64; ++c) {
+    const double v = A[(size_t)rr + (size_t)min(c, ib - 1) * lda];
+    row[c] = (r < ib && c < ib) ? (c <= r ? v : 0.) : (r == c ? 1. : 0.);
+  }
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < 64; ++j) {
+    const double p = readlane_f64(row[j], j);
+    bad = bad || !(p > 0.);
+    const double d = p > 0. ? sqrt(p) : 1.;
+    const double rd = 1. / d;
+    const double l = r > j ? row[j] * rd : (r == j ? d : 0.);
+    if (r >= j) row[j] = l;
+    colb[r] = l;
+    rdg[j] = rd;
+    const v2d* cb = reinterpret_cast<const v2d*>(colb);
+#pragma unroll
+    for (int c = j + 1; c < 64; ++c) {
+      const double lc = (c & 1) ? cb[c >> 1].y : cb[c >> 1].x;
+      row[c] = fma(-l, lc, row[c]);
+    }
+  }
+  if (bad && r == 0) atomicAdd(info, 1);
+#pragma unroll
+  for (int c = 0; c < 64; c += 2) *reinterpret_cast<v2d*>(&Ls[r][c]) = v2d{row[c], row[c + 1]};
+#pragma unroll
+  for (int c = 0; c < 64; ++c)
+    if (c <= r && r < ib && c < ib) A[(size_t)r + (size_t)c * lda] = row[c];
+  double x[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    double s = (i == r) ? 1. : 0.;
+    const v2d* li = reinterpret_cast<const v2d*>(&Ls[i][0]);
+#pragma unroll
+    for (int p = 0; p + 1 < i; p += 2) {
+      const v2d q = li[p >> 1];
+      s = fma(-q.x, x[p], s);
+      s = fma(-q.y, x[p + 1], s);
+    }
+    if (i & 1) s = fma(-Ls[i][i - 1], x[i - 1], s);
+    x[i] = (i >= r) ? s * rdg[i] : 0.;
+  }
+#pragma unroll
+  for (int i = 0; i < 64; ++i)
+    if (i < ib && r < ib) Winv[(size_t)i + (size_t)r * ldw] = (r <= i) ? x[i] : 0.;
+}
+
+// V7: 256 threads, the block in LDS, runtime loop over the 64 pivots (compact code); trailing update
+// thread (row r = t & 63, phase q = t >> 6) over columns j + 1 + q, +4, ...; inverse column c = t & 63
+// by forward substitution with the k-sum split over the 4 waves (LDS partials, fixed order)
+__global__ void __launch_bounds__(256) diag_v7(double* A, int lda, int ib, double* Winv, int ldw, int* info) {
+  __shared__ double Ls[64][65];
+  __shared__ double Wx[64][65];
+  __shared__ double part[4][64];
+  __shared__ double rdg[64];
+  const int t = threadIdx.x;
+  const int r = t & 63, q = t >> 6;
+  for (int e = t; e < 64 * 64; e += 256) {
+    const int i = e & 63, c = e >> 6;
+    Ls[i][c] = (i < ib && c < ib) ? (c <= i ? A[(size_t)i + (size_t)c * lda] : 0.) : (i == c ? 1. : 0.);
+  }
+  __syncthreads();
+  for (int j = 0; j < 64; ++j) {
+    const double p = Ls[j][j];
+    const double d = p > 0. ? sqrt(p) : 1.;
+    const double rd = 1. / d;
+    __syncthreads();
+    if (q == 0) {
+      if (r > j) Ls[r][j] *= rd;
+      else if (r == j) Ls[j][j] = d;
+      if (r == j) rdg[j] = rd;
+      if (r == 0 && !(p > 0.)) atomicAdd(info, 1);
+    }
+    __syncthreads();
+    if (r > j) {
+      const double lr = Ls[r][j];
+      for (int c = j + 1 + q; c <= r; c += 4) Ls[r][c] = fma(-lr, Ls[c][j], Ls[r][c]);
+    }
+    __syncthreads();
+  }
+  for (int e = t; e < 64 * 64; e += 256) {
+    const int i = e & 63, c = e >> 6;
+    if (i < ib && c < ib && c <= i) A[(size_t)i + (size_t)c * lda] = Ls[i][c];
+  }
+  // inverse: column c = r; x_i = (delta_ic - sum_{c <= k < i} L_ik x_k) * rdg_i; wave q sums k = c + q, +4, ...
+  for (int i = 0; i < 64; ++i) {
+    double s = 0.;
+    if (i > r)
+      for (int k = r + q; k < i; k += 4) s = fma(Ls[i][k], Wx[k][r], s);
+    part[q][r] = s;
+    __syncthreads();
+    if (q == 0) {
+      const double tot = (part[0][r] + part[1][r]) + (part[2][r] + part[3][r]);
+      Wx[i][r] = i < r ? 0. : (((i == r) ? 1. : 0.) - tot) * rdg[i];
+    }
+    __syncthreads();
+  }
+  for (int e = t; e < 64 * 64; e += 256) {
+    const int i = e & 63, c = e >> 6;
+    if (i < ib && c < ib) Winv[(size_t)i + (size_t)c * ldw] = (c <= i) ? Wx[i][c] : 0.;
+  }
+}
+
 template <int V>
 int run_la(const std::vector<double>& h, double* dA, double* dW, int* dinfo, const char* name) {
   const int reps = 200;
@@ -189,6 +312,48 @@ int run(const std::vector<double>& h, double* dA, double* dW, int* dinfo, const 
   return 0;
 }
 
+
+template <int KV>
+int run_new(const std::vector<double>& h, double* dA, double* dW, int* dinfo, const char* name) {
+  const int reps = 200;
+  hipEvent_t a, b;
+  CK(hipEventCreate(&a));
+  CK(hipEventCreate(&b));
+  float tot = 0.f;
+  for (int r = 0; r <= reps; ++r) {
+    CK(hipMemcpy(dA, h.data(), sizeof(double) * 64 * 64, hipMemcpyHostToDevice));
+    CK(hipEventRecord(a, 0));
+    if (KV == 6) hipLaunchKernelGGL(diag_v6, dim3(1), dim3(64), 0, 0, dA, 64, 64, dW, 64, dinfo);
+    else hipLaunchKernelGGL(diag_v7, dim3(1), dim3(256), 0, 0, dA, 64, 64, dW, 64, dinfo);
+    CK(hipEventRecord(b, 0));
+    CK(hipEventSynchronize(b));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, a, b));
+    if (r > 0) tot += ms;
+  }
+  std::vector<double> W(64 * 64), L(64 * 64);
+  CK(hipMemcpy(W.data(), dW, sizeof(double) * 64 * 64, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(L.data(), dA, sizeof(double) * 64 * 64, hipMemcpyDeviceToHost));
+  double chk = 0., chl = 0.;
+  for (double v : W) chk += v;
+  for (int i = 0; i < 64; ++i)
+    for (int c = 0; c <= i; ++c) chl += L[i + 64 * c];
+  // back-to-back (warm clocks): 500 launches refactoring the block in place
+  CK(hipMemcpy(dA, h.data(), sizeof(double) * 64 * 64, hipMemcpyHostToDevice));
+  CK(hipEventRecord(a, 0));
+  for (int r = 0; r < 500; ++r) {
+    if (KV == 6) hipLaunchKernelGGL(diag_v6, dim3(1), dim3(64), 0, 0, dA, 64, 64, dW, 64, dinfo);
+    else hipLaunchKernelGGL(diag_v7, dim3(1), dim3(256), 0, 0, dA, 64, 64, dW, 64, dinfo);
+  }
+  CK(hipEventRecord(b, 0));
+  CK(hipEventSynchronize(b));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, a, b));
+  std::printf("%s: %.2f us per launch, back-to-back %.2f us (checksums W %.12g L %.12g)\n", name, 1e3 * tot / reps,
+              1e3 * ms / 500, chk, chl);
+  return 0;
+}
+
 int main() {
   std::vector<double> h(64 * 64);
   for (int i = 0; i < 64; ++i)
@@ -206,6 +371,8 @@ int main() {
   if (run<3>(h, dA, dW, dinfo, "V3 V2 + reciprocal multiply")) return 1;
   if (run_la<1>(h, dA, dW, dinfo, "V4 lookahead factor only")) return 1;
   if (run_la<0>(h, dA, dW, dinfo, "V5 lookahead factor + inverse")) return 1;
+  if (run_new<6>(h, dA, dW, dinfo, "V6 compact registers, readlane pivot, rcp-multiply")) return 1;
+  if (run_new<7>(h, dA, dW, dinfo, "V7 LDS, 256 threads, runtime pivot loop")) return 1;
   // back-to-back launches (no host copy in between: clocks stay up); the block is refactored in place
   {
     hipEvent_t a, b;
