@@ -55,7 +55,7 @@ def pmc_traffic(scale: float) -> dict | None:
     same command (profiles/<round>/pmc_rows.json: FETCH_SIZE + WRITE_SIZE, KB per dispatch;
     PMC counters cannot be read from inside the process)."""
     path = None
-    for rnd in ("r03", "r02", "r01"):   # the latest round's passes
+    for rnd in ("r04", "r03", "r02", "r01"):   # the latest round's passes
         cand = os.path.join(ROOT, "profiles", rnd, "pmc_rows.json")
         if os.path.exists(cand):
             path = cand

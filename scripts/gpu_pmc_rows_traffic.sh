@@ -13,7 +13,7 @@ for P in FETCH_SIZE WRITE_SIZE TCC_HIT_sum; do
   EXTRA=""
   [ "$P" = TCC_HIT_sum ] && EXTRA="TCC_MISS_sum"
   ( cd /tmp && export TMPDIR=/tmp && timeout -s KILL 120 rocprofv3 --pmc $P $EXTRA --output-format csv \
-      -d "$R/gpurun_out/pmc_traffic/p$i" -o rows -- python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-latent --no-dense --no-fit --no-grouped \
+      -d "$R/gpurun_out/pmc_traffic/p$i" -o rows -- python3 "$R/bench.py" --steps 5 --warmup 2 --no-cpu-baseline --no-latent --no-dense --no-fit --no-grouped ${PMC_BENCH_ARGS:-} \
       > "$R/gpurun_out/pmc_traffic/p$i.log" 2>&1 ) || exit 1
   python scripts/pmc_by_kernel.py gpurun_out/pmc_traffic/p$i gpurun_out/pmc_traffic_${TAG}_p$i.txt > /dev/null || exit 1
 done
