@@ -19,6 +19,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <string>
 #include <vector>
 
 #include "cov.h"
@@ -384,6 +385,93 @@ __global__ void __launch_bounds__(64) potrf_diag_wave_kernel(double* A, int lda,
 #pragma unroll
   for (int i = 0; i < 64; ++i)
     if (i < ib && r < ib) Winv[(size_t)(j0 + i) + (size_t)(j0 + r) * ldw] = (r <= i) ? x[i] : 0.;
+}
+
+// The same factorization and inverse of one 64 x 64 diagonal block with four waves (the default; the
+// one-wave kernel above runs every one of its ~19k instructions on one wave, so each pivot costs the
+// whole step's issue time: 78 vs 52 us per block in scripts/microbench/diag_bench.hip, V0 vs V8).
+// Wave w holds the columns c = 4k + w (k < 16) of all 64 rows (lane r = row r) in registers; pivot j's
+// owner wave (j & 3) takes the pivot by v_readlane, scales its column (a division, as the LLT does) and
+// publishes L[:, j] (zero for rows <= j) to LDS; after ONE barrier every wave updates its columns c > j
+// (registers whose columns are all <= j skipped at compile time, the published zeros make the rest
+// branch-free). A partial block (ib < 64) is padded with the identity. Every element sees the same
+// operations in the same order as in the one-wave kernel (bit-identical factor); L^-1 by its code on
+// wave 0 (a four-wave split of that substitution changed the rounding enough to move an ill-conditioned
+// Gaussian-kernel FITC case past its 1e-9 reference bound).
+__global__ void __launch_bounds__(256) potrf_diag_quad_kernel(double* A, int lda, int j0, int ib, double* Winv,
+                                                              int ldw, int* info) {
+  __shared__ double colb[2][64];
+  __shared__ double Ls[64][65];
+  const int r = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int rr = min(r, ib - 1);
+  double col[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int c = 4 * k + w;
+    const double v = A[(size_t)(j0 + rr) + (size_t)(j0 + min(c, ib - 1)) * lda];
+    col[k] = (r < ib && c < ib) ? (c <= r ? v : 0.) : (r == c ? 1. : 0.);
+  }
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < 64; ++j) {
+    if (w == (j & 3)) {
+      const int lo = __builtin_amdgcn_readlane(__double2loint(col[j >> 2]), j);
+      const int hi = __builtin_amdgcn_readlane(__double2hiint(col[j >> 2]), j);
+      const double p = __hiloint2double(hi, lo);
+      bad = bad || !(p > 0.);   // not positive definite
+      const double d = p > 0. ? sqrt(p) : 1.;
+      const double l = r > j ? col[j >> 2] / d : (r == j ? d : col[j >> 2]);   // divisions, as the LLT
+      col[j >> 2] = l;
+      colb[j & 1][r] = r > j ? l : 0.;
+    }
+    __syncthreads();
+    const double lr = colb[j & 1][r];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (4 * k + 3 <= j) continue;   // every column of register k is <= j
+      col[k] = fma(-lr, colb[j & 1][4 * k + w], col[k]);
+    }
+  }
+  if (bad && r == 0) atomicAdd(info, 1);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int c = 4 * k + w;
+    Ls[r][c] = col[k];
+    if (c <= r && r < ib && c < ib) A[(size_t)(j0 + r) + (size_t)(j0 + c) * lda] = col[k];
+  }
+  __syncthreads();
+  // L^-1 by the one-wave kernel's forward substitution (column r on lane r; the same operations in the
+  // same order, so the factor and the inverse equal that kernel's bit for bit): wave 0 only
+  if (w != 0) return;
+  double x[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    double s = (i == r) ? 1. : 0.;
+#pragma unroll
+    for (int p = 0; p < i; ++p) s -= Ls[i][p] * x[p];
+    x[i] = (i >= r && i < ib) ? s / Ls[i][i] : 0.;
+  }
+#pragma unroll
+  for (int i = 0; i < 64; ++i)
+    if (i < ib && r < ib) Winv[(size_t)(j0 + i) + (size_t)(j0 + r) * ldw] = (r <= i) ? x[i] : 0.;
+}
+
+// one diagonal block: GPBOOST_AMD_DIAG_FORM = quad (default) | wave | old (A/B)
+void launch_potrf_diag(hipStream_t s, double* A, int ld, int j0, int ib, double* W, int* info) {
+  static const int form = [] {
+    const char* e = std::getenv("GPBOOST_AMD_DIAG_FORM");
+    if (std::getenv("GPBOOST_AMD_DIAG_OLD") != nullptr) return 2;
+    if (e == nullptr || std::string(e) == "quad") return 0;
+    if (std::string(e) == "wave") return 1;
+    if (std::string(e) == "old") return 2;
+    Fatal("GPBOOST_AMD_DIAG_FORM must be quad, wave or old (got '%s')", e);
+    return 0;
+  }();
+  if (form == 0) hipLaunchKernelGGL(potrf_diag_quad_kernel, dim3(1), dim3(256), 0, s, A, ld, j0, ib, W, ld, info);
+  else if (form == 1) hipLaunchKernelGGL(potrf_diag_wave_kernel, dim3(1), dim3(64), 0, s, A, ld, j0, ib, W, ld, info);
+  else hipLaunchKernelGGL(potrf_diag_kernel, dim3(1), dim3(256), 0, s, A, ld, j0, ib, W, ld, info);
+  HIP_CHECK(hipGetLastError());
 }
 
 // Cross-covariance C[i + p ld] = cov(|x_i - xp_p|) (n x np, column-major) and, when S is non-null,
@@ -775,12 +863,7 @@ void chol_lower(hipStream_t s, double* A, double* W, int n, int ld, int* info) {
     const int jb = std::min(NBO, n - J0);
     for (int j0 = J0; j0 < J0 + jb; j0 += NBI) {
       const int ib = std::min(NBI, J0 + jb - j0);
-      static const bool diag_old = std::getenv("GPBOOST_AMD_DIAG_OLD") != nullptr;   // A/B: 256-thread form
-      if (diag_old)
-        hipLaunchKernelGGL(potrf_diag_kernel, dim3(1), dim3(256), 0, s, A, ld, j0, ib, W, ld, info);
-      else
-        hipLaunchKernelGGL(potrf_diag_wave_kernel, dim3(1), dim3(64), 0, s, A, ld, j0, ib, W, ld, info);
-      HIP_CHECK(hipGetLastError());
+      launch_potrf_diag(s, A, ld, j0, ib, W, info);
       const int r0 = j0 + ib;
       if (r0 < n) {
         // L21 = A21 * L11^-T  (in place: each 64-row tile reads its whole K = ib range first)
@@ -1009,8 +1092,7 @@ void DenseSolver::PotrfLookahead() {
     const int jb = std::min(NBO, n - J0);
     for (int j0 = J0; j0 < J0 + jb; j0 += NBI) {
       const int ib = std::min(NBI, J0 + jb - j0);
-      hipLaunchKernelGGL(potrf_diag_wave_kernel, dim3(1), dim3(64), 0, s_chain_, A, ld, j0, ib, W, ld, info_.get());
-      HIP_CHECK(hipGetLastError());
+      launch_potrf_diag(s_chain_, A, ld, j0, ib, W, info_.get());
       const int r0 = j0 + ib;
       if (r0 < n)
         gemm(s_chain_, n - r0, ib, ib, 1., A + r0 + (size_t)j0 * ld, ld, 0, W + j0 + (size_t)j0 * ld, ld, 1, 0.,

@@ -258,6 +258,83 @@ __global__ void __launch_bounds__(256) diag_v7(double* A, int lda, int ib, doubl
   }
 }
 
+
+// V8: four waves; wave w holds the columns c = 4k + w (k < 16) of all 64 rows (lane r = row r) in
+// registers. Pivot j: its owner wave (j & 3) takes the pivot by v_readlane, scales its column and
+// publishes L[:, j] (zero for rows <= j) to LDS; after ONE barrier every wave updates its columns
+// c > j with it (registers whose columns are all <= j are skipped at compile time; the published zeros
+// make the rest branch-free). The inverse the same way by rows: wave (i & 3) owns row i of X = L^-1
+// (lane r = column r); each wave sums its rows' share of L[i][k] x_k into an LDS partial, one barrier,
+// the owner finishes x_i = (delta_ir - sum) / L_ii.
+__global__ void __launch_bounds__(256) diag_v8(double* A, int lda, int ib, double* Winv, int ldw, int* info) {
+  __shared__ double colb[2][64];
+  __shared__ double Ls[64][65];
+  __shared__ double part[2][4][64];
+  __shared__ double rdg[64];
+  const int r = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int rr = min(r, ib - 1);
+  double col[16];
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int c = 4 * k + w;
+    const double v = A[(size_t)rr + (size_t)min(c, ib - 1) * lda];
+    col[k] = (r < ib && c < ib) ? (c <= r ? v : 0.) : (r == c ? 1. : 0.);
+  }
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < 64; ++j) {
+    if (w == (j & 3)) {
+      const double p = readlane_f64(col[j >> 2], j);
+      bad = bad || !(p > 0.);
+      const double d = p > 0. ? sqrt(p) : 1.;
+      const double rd = 1. / d;
+      const double l = r > j ? col[j >> 2] * rd : (r == j ? d : col[j >> 2]);
+      col[j >> 2] = l;
+      colb[j & 1][r] = r > j ? l : 0.;
+      if (r == j) rdg[j] = rd;
+    }
+    __syncthreads();
+    const double lr = colb[j & 1][r];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (4 * k + 3 <= j) continue;   // every column of register k is <= j
+      col[k] = fma(-lr, colb[j & 1][4 * k + w], col[k]);
+    }
+  }
+  if (bad && r == 0 && w == 0) atomicAdd(info, 1);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int c = 4 * k + w;
+    Ls[r][c] = col[k];
+    if (c <= r && r < ib && c < ib) A[(size_t)r + (size_t)c * lda] = col[k];
+  }
+  __syncthreads();
+  // X = L^-1, lane r = column r; wave w owns rows i = 4m + w of X (x[m])
+  double x[16];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    double s = 0.;
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      if (4 * m >= i) continue;      // rows k = 4m + w < i only
+      const int k = 4 * m + w;
+      s = (k < i) ? fma(Ls[i][k], x[m], s) : s;
+    }
+    part[i & 1][w][r] = s;
+    __syncthreads();
+    if (w == (i & 3)) {
+      const double tot = (part[i & 1][0][r] + part[i & 1][1][r]) + (part[i & 1][2][r] + part[i & 1][3][r]);
+      x[i >> 2] = (i < r) ? 0. : (((i == r) ? 1. : 0.) - tot) * rdg[i];
+    }
+  }
+#pragma unroll
+  for (int m = 0; m < 16; ++m) {
+    const int i = 4 * m + w;
+    if (i < ib && r < ib) Winv[(size_t)i + (size_t)r * ldw] = (r <= i) ? x[m] : 0.;
+  }
+}
+
 template <int V>
 int run_la(const std::vector<double>& h, double* dA, double* dW, int* dinfo, const char* name) {
   const int reps = 200;
@@ -324,6 +401,7 @@ int run_new(const std::vector<double>& h, double* dA, double* dW, int* dinfo, co
     CK(hipMemcpy(dA, h.data(), sizeof(double) * 64 * 64, hipMemcpyHostToDevice));
     CK(hipEventRecord(a, 0));
     if (KV == 6) hipLaunchKernelGGL(diag_v6, dim3(1), dim3(64), 0, 0, dA, 64, 64, dW, 64, dinfo);
+    else if (KV == 8) hipLaunchKernelGGL(diag_v8, dim3(1), dim3(256), 0, 0, dA, 64, 64, dW, 64, dinfo);
     else hipLaunchKernelGGL(diag_v7, dim3(1), dim3(256), 0, 0, dA, 64, 64, dW, 64, dinfo);
     CK(hipEventRecord(b, 0));
     CK(hipEventSynchronize(b));
@@ -343,6 +421,7 @@ int run_new(const std::vector<double>& h, double* dA, double* dW, int* dinfo, co
   CK(hipEventRecord(a, 0));
   for (int r = 0; r < 500; ++r) {
     if (KV == 6) hipLaunchKernelGGL(diag_v6, dim3(1), dim3(64), 0, 0, dA, 64, 64, dW, 64, dinfo);
+    else if (KV == 8) hipLaunchKernelGGL(diag_v8, dim3(1), dim3(256), 0, 0, dA, 64, 64, dW, 64, dinfo);
     else hipLaunchKernelGGL(diag_v7, dim3(1), dim3(256), 0, 0, dA, 64, 64, dW, 64, dinfo);
   }
   CK(hipEventRecord(b, 0));
@@ -373,6 +452,7 @@ int main() {
   if (run_la<0>(h, dA, dW, dinfo, "V5 lookahead factor + inverse")) return 1;
   if (run_new<6>(h, dA, dW, dinfo, "V6 compact registers, readlane pivot, rcp-multiply")) return 1;
   if (run_new<7>(h, dA, dW, dinfo, "V7 LDS, 256 threads, runtime pivot loop")) return 1;
+  if (run_new<8>(h, dA, dW, dinfo, "V8 four waves, column-owner registers, one barrier per pivot")) return 1;
   // back-to-back launches (no host copy in between: clocks stay up); the block is refactored in place
   {
     hipEvent_t a, b;
