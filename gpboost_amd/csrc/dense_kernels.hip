@@ -249,6 +249,17 @@ __global__ void __launch_bounds__(256) gemm_f64_splitk_kernel(GemmArgs g, int kc
   h.C = g.C + (size_t)blockIdx.z * cstride;
   gemm_tile_body<64>(h);
 }
+// the same with 128 x 128 tiles (the big kernel's body and occupancy; same chunks -> same bits)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2)))
+gemm_f64_splitk_big_kernel(GemmArgs g, int kchunk, long cstride) {
+  GemmArgs h = g;
+  const int k0 = blockIdx.z * kchunk;
+  h.K = min(g.K - k0, kchunk);
+  h.A = g.transA ? g.A + k0 : g.A + (size_t)k0 * g.lda;
+  h.B = g.transB ? g.B + (size_t)k0 * g.ldb : g.B + k0;
+  h.C = g.C + (size_t)blockIdx.z * cstride;
+  gemm_tile_body<128>(h);
+}
 
 // Lower triangle (i >= j) of Psi = Sigma + I, tile-parallel, upper tiles skipped.
 template <int COV>
@@ -825,8 +836,18 @@ int gemm_f64_splitk(hipStream_t s, int M, int N, int K, const double* A, int lda
   kchunk = (kchunk + TKB - 1) / TKB * TKB;
   chunks = (K + kchunk - 1) / kchunk;
   GemmArgs g{M, N, K, 1., 0., A, lda, transA, B, ldb, transB, C, ldc, 0, 0, 0, 0};
-  dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM, chunks);
-  hipLaunchKernelGGL(gemm_f64_splitk_kernel, grid, dim3(256), 0, s, g, kchunk, cstride);
+  // 128-tiles once both dimensions fill them (GPBOOST_AMD_SPLITK_TILE=64 keeps the 64-tile form: A/B)
+  static const bool tile64 = [] {
+    const char* e = std::getenv("GPBOOST_AMD_SPLITK_TILE");
+    return e != nullptr && std::string(e) == "64";
+  }();
+  if (!tile64 && M >= TB && N >= TB) {
+    dim3 grid((N + TB - 1) / TB, (M + TB - 1) / TB, chunks);
+    hipLaunchKernelGGL(gemm_f64_splitk_big_kernel, grid, dim3(256), 0, s, g, kchunk, cstride);
+  } else {
+    dim3 grid((N + TN - 1) / TN, (M + TM - 1) / TM, chunks);
+    hipLaunchKernelGGL(gemm_f64_splitk_kernel, grid, dim3(256), 0, s, g, kchunk, cstride);
+  }
   HIP_CHECK(hipGetLastError());
   return chunks;
 }
