@@ -390,6 +390,101 @@ __global__ void __launch_bounds__(64) kmeans_means_kernel(const double* __restri
   }
 }
 
+// The same means from cluster member lists (default): a stable partition of the points by cluster
+// (per-block counts -> per-cluster block offsets -> cluster bases -> an in-order scatter), then one
+// thread per cluster adds its members in increasing index order exactly as above (same operations,
+// same order, same bits) instead of every cluster's wave scanning all n assignments.
+constexpr int kKmP = 256;   // points per partition block
+__global__ void __launch_bounds__(256) kmeans_count_kernel(const int* __restrict__ cluster, int n, int k,
+                                                           int* __restrict__ cnt) {
+  extern __shared__ int h[];
+  for (int c = threadIdx.x; c < k; c += 256) h[c] = 0;
+  __syncthreads();
+  const int i = blockIdx.x * kKmP + threadIdx.x;
+  if (i < n) atomicAdd(&h[cluster[i]], 1);
+  __syncthreads();
+  for (int c = threadIdx.x; c < k; c += 256) cnt[(size_t)blockIdx.x * k + c] = h[c];
+}
+// per cluster: offsets of each block's members within the cluster, and the cluster's total (loads
+// batched 8 at a time: the block counts are independent of the running sum)
+__global__ void __launch_bounds__(64) kmeans_offsets_kernel(const int* __restrict__ cnt, int nb, int k,
+                                                            int* __restrict__ off, int* __restrict__ tot) {
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= k) return;
+  int run = 0;
+  int b = 0;
+  for (; b + 8 <= nb; b += 8) {
+    int v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = cnt[(size_t)(b + u) * k + c];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      off[(size_t)(b + u) * k + c] = run;
+      run += v[u];
+    }
+  }
+  for (; b < nb; ++b) {
+    const int v = cnt[(size_t)b * k + c];
+    off[(size_t)b * k + c] = run;
+    run += v;
+  }
+  tot[c] = run;
+}
+// cluster bases: exclusive prefix of the totals (one block, serial: k is the number of inducing points)
+__global__ void kmeans_bases_kernel(const int* __restrict__ tot, int k, int* __restrict__ base) {
+  if (threadIdx.x != 0) return;
+  int run = 0;
+  for (int c = 0; c < k; ++c) {
+    base[c] = run;
+    run += tot[c];
+  }
+  base[k] = run;
+}
+// in-order scatter of a block's points: one wave per block, 64 points at a time; a point's rank among the
+// chunk's earlier points of its cluster by a lane loop over v_readlane, the chunk's last member of a
+// cluster advances that cluster's LDS cursor
+__global__ void __launch_bounds__(64) kmeans_scatter_kernel(const int* __restrict__ cluster, int n, int k,
+                                                            const int* __restrict__ off, const int* __restrict__ base,
+                                                            int* __restrict__ list) {
+  extern __shared__ int cur[];   // k cursors: base[c] + this block's offset in cluster c
+  const int b = blockIdx.x, lane = threadIdx.x;
+  for (int c = lane; c < k; c += 64) cur[c] = base[c] + off[(size_t)b * k + c];
+  __syncthreads();
+  const int i1 = min(n, (b + 1) * kKmP);
+  for (int i0 = b * kKmP; i0 < i1; i0 += 64) {
+    const int i = i0 + lane;
+    const bool ok = i < i1;
+    const int c = ok ? cluster[i] : -1;
+    int rank = 0;
+    bool last = ok;
+    for (int q = 0; q < 64; ++q) {
+      const int cq = __builtin_amdgcn_readlane(c, q);
+      rank += (q < lane && cq == c) ? 1 : 0;
+      last = last && !(q > lane && cq == c);
+    }
+    const int pos = ok ? cur[c] + rank : 0;
+    if (ok) list[pos] = i;
+    __syncthreads();   // every lane read its cursor before the last members move them
+    if (last) cur[c] = pos + 1;
+    __syncthreads();
+  }
+}
+__global__ void __launch_bounds__(64) kmeans_means_list_kernel(const double* __restrict__ X, const int* __restrict__ list,
+                                                               const int* __restrict__ base, int k, int d,
+                                                               const double* __restrict__ mu_old, double* __restrict__ mu_new) {
+#pragma clang fp contract(off)
+  const int c = blockIdx.x * 64 + threadIdx.x;
+  if (c >= k) return;
+  double s[3] = {0., 0., 0.};
+  const int e0 = base[c], e1 = base[c + 1];
+  for (int e = e0; e < e1; ++e) {
+    const double* xr = X + (size_t)list[e] * d;
+    for (int q = 0; q < d; ++q) s[q] = s[q] + xr[q];
+  }
+  const int count = e1 - e0;
+  for (int q = 0; q < d; ++q) mu_new[(size_t)c * d + q] = count > 0 ? s[q] / (double)count : mu_old[(size_t)c * d + q];
+}
+
 // flags[0] = any(mu != a), flags[1] = any(mu != b) (one block)
 __global__ void __launch_bounds__(256) kmeans_cmp_kernel(const double* __restrict__ mu, const double* __restrict__ a,
                                                          const double* __restrict__ b, int cnt, int* __restrict__ flags) {
@@ -480,6 +575,9 @@ std::vector<double> fitc_inducing_points(const std::vector<double>& coords, int 
   const size_t cnt = (size_t)m * d;
   DevBuf<double> dX((size_t)n * d), b0(cnt), b1(cnt), b2(cnt);
   DevBuf<int> cl(n), flags(2);
+  const int nbk = (n + kKmP - 1) / kKmP;
+  DevBuf<int> kcnt((size_t)nbk * m), koff((size_t)nbk * m), ktot(m), kbase(m + 1), klist(n);
+  static const bool scan_means = std::getenv("GPBOOST_AMD_KMEANS_SCAN") != nullptr;   // A/B: the scanning kernel
   HIP_CHECK(hipMemcpyAsync(dX.get(), coords.data(), sizeof(double) * n * d, hipMemcpyHostToDevice, s));
   HIP_CHECK(hipMemcpyAsync(b0.get(), Z.data(), sizeof(double) * cnt, hipMemcpyHostToDevice, s));
   HIP_CHECK(hipMemsetAsync(b1.get(), 0, sizeof(double) * cnt, s));
@@ -496,7 +594,18 @@ std::vector<double> fitc_inducing_points(const std::vector<double>& coords, int 
     old = mu;
     mu = free_buf;
     hipLaunchKernelGGL(kmeans_assign_kernel, dim3((n + 255) / 256), dim3(256), 0, s, dX.get(), old, n, m, d, cl.get());
-    hipLaunchKernelGGL(kmeans_means_kernel, dim3(m), dim3(64), 0, s, dX.get(), cl.get(), n, m, d, old, mu);
+    if (scan_means) {
+      hipLaunchKernelGGL(kmeans_means_kernel, dim3(m), dim3(64), 0, s, dX.get(), cl.get(), n, m, d, old, mu);
+    } else {
+      hipLaunchKernelGGL(kmeans_count_kernel, dim3(nbk), dim3(256), sizeof(int) * m, s, cl.get(), n, m, kcnt.get());
+      hipLaunchKernelGGL(kmeans_offsets_kernel, dim3((m + 63) / 64), dim3(64), 0, s, kcnt.get(), nbk, m, koff.get(),
+                         ktot.get());
+      hipLaunchKernelGGL(kmeans_bases_kernel, dim3(1), dim3(64), 0, s, ktot.get(), m, kbase.get());
+      hipLaunchKernelGGL(kmeans_scatter_kernel, dim3(nbk), dim3(64), sizeof(int) * m, s, cl.get(), n, m, koff.get(),
+                         kbase.get(), klist.get());
+      hipLaunchKernelGGL(kmeans_means_list_kernel, dim3((m + 63) / 64), dim3(64), 0, s, dX.get(), klist.get(), kbase.get(),
+                         m, d, old, mu);
+    }
     hipLaunchKernelGGL(kmeans_cmp_kernel, dim3(1), dim3(256), 0, s, mu, old, old_old, (int)cnt, flags.get());
     HIP_CHECK(hipGetLastError());
     HIP_CHECK(hipMemcpyAsync(h_flags, flags.get(), sizeof(int) * 2, hipMemcpyDeviceToHost, s));
