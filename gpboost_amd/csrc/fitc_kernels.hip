@@ -343,6 +343,29 @@ __device__ __forceinline__ double km_dist(const double* x, const double* mu, int
   return sqrt(s);
 }
 
+// squared distance with km_dist's operations (its sqrt argument)
+template <int D>
+__device__ __forceinline__ double km_dist2(const double* x, const double* mu, int d) {
+#pragma clang fp contract(off)
+  const int dd = D > 0 ? D : d;
+  double t = x[0] - mu[0];
+  double s = t * t;
+#pragma unroll
+  for (int q = 1; q < (D > 0 ? D : 3); ++q) {
+    if (q < dd) {
+      t = x[q] - mu[q];
+      const double sq = t * t;
+      s = s + sq;
+    }
+  }
+  return s;
+}
+
+// The reference compares the distances sqrt(s): a squared distance above the best one's cannot win
+// (sqrt is monotone), and one below it wins only if its sqrt is strictly smaller — so the sqrt is
+// taken only for those candidates, with the reference's comparison on the sqrt values (ties after
+// rounding keep the earlier center, as the reference's strict < does).
+template <int D>
 __global__ void __launch_bounds__(256) kmeans_assign_kernel(const double* __restrict__ X, const double* __restrict__ mu,
                                                             int n, int k, int d, int* __restrict__ cluster) {
   const int i = blockIdx.x * 256 + threadIdx.x;
@@ -350,12 +373,18 @@ __global__ void __launch_bounds__(256) kmeans_assign_kernel(const double* __rest
   double x[3] = {0., 0., 0.};
   for (int q = 0; q < d; ++q) x[q] = X[(size_t)i * d + q];
   int best = 0;
-  double bd = km_dist(x, mu, d);
+  double bs = km_dist2<D>(x, mu, d);
+  double bd = sqrt(bs);
+#pragma unroll 4
   for (int j = 1; j < k; ++j) {
-    const double dj = km_dist(x, mu + (size_t)j * d, d);
-    if (dj < bd) {
-      bd = dj;
-      best = j;
+    const double sj = km_dist2<D>(x, mu + (size_t)j * d, d);
+    if (sj < bs) {
+      const double dj = sqrt(sj);
+      if (dj < bd) {
+        bd = dj;
+        bs = sj;
+        best = j;
+      }
     }
   }
   cluster[i] = best;
@@ -434,7 +463,18 @@ __global__ void __launch_bounds__(64) kmeans_offsets_kernel(const int* __restric
 __global__ void kmeans_bases_kernel(const int* __restrict__ tot, int k, int* __restrict__ base) {
   if (threadIdx.x != 0) return;
   int run = 0;
-  for (int c = 0; c < k; ++c) {
+  int c = 0;
+  for (; c + 8 <= k; c += 8) {
+    int v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) v[u] = tot[c + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      base[c + u] = run;
+      run += v[u];
+    }
+  }
+  for (; c < k; ++c) {
     base[c] = run;
     run += tot[c];
   }
@@ -477,7 +517,23 @@ __global__ void __launch_bounds__(64) kmeans_means_list_kernel(const double* __r
   if (c >= k) return;
   double s[3] = {0., 0., 0.};
   const int e0 = base[c], e1 = base[c + 1];
-  for (int e = e0; e < e1; ++e) {
+  int e = e0;
+  for (; e + 8 <= e1; e += 8) {   // eight members' loads in flight, added in order (d <= 3: registers)
+    double v[8][3];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const double* xr = X + (size_t)list[e + u] * d;
+#pragma unroll
+      for (int q = 0; q < 3; ++q) v[u][q] = q < d ? xr[q] : 0.;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+#pragma unroll
+      for (int q = 0; q < 3; ++q)
+        if (q < d) s[q] = s[q] + v[u][q];
+    }
+  }
+  for (; e < e1; ++e) {
     const double* xr = X + (size_t)list[e] * d;
     for (int q = 0; q < d; ++q) s[q] = s[q] + xr[q];
   }
@@ -593,7 +649,10 @@ std::vector<double> fitc_inducing_points(const std::vector<double>& coords, int 
     old_old = old;
     old = mu;
     mu = free_buf;
-    hipLaunchKernelGGL(kmeans_assign_kernel, dim3((n + 255) / 256), dim3(256), 0, s, dX.get(), old, n, m, d, cl.get());
+    if (d == 2)
+      hipLaunchKernelGGL(kmeans_assign_kernel<2>, dim3((n + 255) / 256), dim3(256), 0, s, dX.get(), old, n, m, d, cl.get());
+    else
+      hipLaunchKernelGGL(kmeans_assign_kernel<0>, dim3((n + 255) / 256), dim3(256), 0, s, dX.get(), old, n, m, d, cl.get());
     if (scan_means) {
       hipLaunchKernelGGL(kmeans_means_kernel, dim3(m), dim3(64), 0, s, dX.get(), cl.get(), n, m, d, old, mu);
     } else {
