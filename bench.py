@@ -685,6 +685,44 @@ def latent_leg_sharded(X, Y, steps: int, rank: int, world: int, dist) -> dict | 
     }
 
 
+def spawn_ranks(world: int, argv: list[str]) -> int:
+    """`bench.py --gpus N` without an external launcher: start N fresh rank processes (this process
+    never touches the GPU), with RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT set as
+    torch.distributed.run would; relay rank 0's JSON line; non-zero exit if any rank fails."""
+    import signal
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    out0 = tempfile.TemporaryFile()
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(world), LOCAL_WORLD_SIZE=str(world),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=out0 if r == 0 else subprocess.DEVNULL, start_new_session=True))
+    codes: list = [None] * world
+    while any(c is None for c in codes):
+        for r, p in enumerate(procs):
+            if codes[r] is None:
+                codes[r] = p.poll()
+        if any(c not in (None, 0) for c in codes):   # a failed rank leaves its peers blocked in a collective
+            for r, p in enumerate(procs):
+                if codes[r] is None:
+                    os.killpg(p.pid, signal.SIGKILL)
+                    codes[r] = p.wait()
+            break
+        time.sleep(0.05)
+    out0.seek(0)
+    sys.stdout.write(out0.read().decode())
+    sys.stdout.flush()
+    bad = [(r, c) for r, c in enumerate(codes) if c]
+    if bad:
+        sys.stderr.write(f"bench.py: rank(s) failed (rank, exit code): {bad}\n")
+        return 1
+    return 0
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -702,6 +740,12 @@ def main():
                     help="skip the per-rank row-range measurements (profiling the headline kernel alone)")
     ap.add_argument("--only-fitc", action="store_true", help="run only the FITC leg (prints its JSON)")
     args = ap.parse_args()
+    launched = os.environ.get("WORLD_SIZE")
+    if launched is not None and int(launched) != args.gpus:
+        sys.stderr.write(f"bench.py: --gpus {args.gpus} disagrees with the launcher's WORLD_SIZE={launched}\n")
+        sys.exit(2)
+    if launched is None and args.gpus > 1:
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     if args.only_grouped:
         print(json.dumps(grouped_leg(args.steps, not args.no_cpu_baseline)))
         return

@@ -753,7 +753,7 @@ __global__ void __launch_bounds__(256) rowsq_kernel(const double* U, int ld, int
     const double u = U[(size_t)i + (size_t)c * ld];
     s += u * u;
   }
-  out[i] = s / nsim + add[i];
+  out[i] = (nsim > 0 ? s / nsim : 0.) + add[i];
 }
 
 // out[p] = sum_i T[i + p ld]^2 for i < n (one wave per column)
@@ -992,7 +992,8 @@ void vecchia_latent_dense_pred(hipStream_t s, int N, int n, const double* B, con
 void latent_pred_moments(hipStream_t s, int np, const double* Bp, const double* Dp, const double* d_V, int nsim,
                          bool want_var, bool want_cov, double* var, double* cov) {
   // W = Bp^-1 (identity when Bp is null), U = W V; var = rowsum(U^2) / nsim + diag(W diag(Dp) W^T);
-  // cov = U U^T / nsim + W diag(Dp) W^T (PredictLaplaceApproxVecchia, likelihoods.h:6713-6749)
+  // cov = U U^T / nsim + W diag(Dp) W^T (PredictLaplaceApproxVecchia, likelihoods.h:6713-6749).
+  // nsim = 0 (d_V unused): the Gaussian likelihood's W diag(Dp) W^T alone (Vecchia_utils.cpp:1977-2006)
   const int ld = (np + 63) / 64 * 64;
   const size_t NN = (size_t)ld * ld;
   DevBuf<double> W, dB, T, U, dD(np), det(np), out(np);
@@ -1003,13 +1004,13 @@ void latent_pred_moments(hipStream_t s, int np, const double* Bp, const double* 
     W.alloc(NN);
     dB.alloc(NN);
     T.alloc((size_t)ld * (ld / 2 + 64));
-    U.alloc((size_t)ld * nsim);
+    if (nsim > 0) U.alloc((size_t)ld * nsim);
     HIP_CHECK(hipMemsetAsync(W.get(), 0, NN * sizeof(double), s));
     HIP_CHECK(hipMemcpy2DAsync(dB.get(), sizeof(double) * ld, Bp, sizeof(double) * np, sizeof(double) * np, np,
                                hipMemcpyHostToDevice, s));
     hipLaunchKernelGGL(unit_lower_diag_inv_kernel, dim3((np + 63) / 64), dim3(64), 0, s, dB.get(), ld, np, W.get(), ld);
     trtri_lower(s, dB.get(), W.get(), T.get(), 0, np, ld);
-    gemm(s, np, nsim, np, 1., W.get(), ld, 0, d_V, np, 0, 0., U.get(), ld, 0, 1, 0, 0);
+    if (nsim > 0) gemm(s, np, nsim, np, 1., W.get(), ld, 0, d_V, np, 0, 0., U.get(), ld, 0, 1, 0, 0);
     Uptr = U.get();
     ldu = ld;
   }
@@ -1040,7 +1041,7 @@ void latent_pred_moments(hipStream_t s, int np, const double* Bp, const double* 
       HIP_CHECK(hipMemcpy2DAsync(Cv.get(), sizeof(double) * (np + 1), dD.get(), sizeof(double), sizeof(double), np,
                                  hipMemcpyDeviceToDevice, s));
     }
-    gemm(s, np, np, nsim, 1. / nsim, Uptr, ldu, 0, Uptr, ldu, 1, 1., Cv.get(), np);
+    if (nsim > 0) gemm(s, np, np, nsim, 1. / nsim, Uptr, ldu, 0, Uptr, ldu, 1, 1., Cv.get(), np);
     HIP_CHECK(hipMemcpyAsync(cov, Cv.get(), sizeof(double) * np * np, hipMemcpyDeviceToHost, s));
   }
   HIP_CHECK(hipGetLastError());

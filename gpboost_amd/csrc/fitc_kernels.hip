@@ -913,10 +913,21 @@ void FitcSolver::Predict(int cov_type, double var, double phi, const double* d_y
     HIP_CHECK(hipMemcpyAsync(pcov, C.get(), sizeof(double) * np * np, hipMemcpyDeviceToHost, stream_));
     HIP_CHECK(hipStreamSynchronize(stream_));
     for (int i = 0; i < np; ++i) pcov[(size_t)i * np + i] += resid[i] + nug;
-    for (int q = 0; q < npairs; ++q)
-      for (int r = 0; r < npairs; ++r)
-        if (pairs[2 * q + 1] == pairs[2 * r + 1])
+    // pairs grouped by training index (stable: pair order kept within a group), so the correction
+    // costs the number of entries it writes instead of npairs^2 comparisons
+    std::vector<int> order(npairs);
+    for (int q = 0; q < npairs; ++q) order[q] = q;
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return pairs[2 * a + 1] < pairs[2 * b + 1]; });
+    for (int g0 = 0; g0 < npairs;) {
+      int g1 = g0 + 1;
+      while (g1 < npairs && pairs[2 * order[g1] + 1] == pairs[2 * order[g0] + 1]) ++g1;
+      for (int a = g0; a < g1; ++a)
+        for (int b = g0; b < g1; ++b) {
+          const int q = order[a], r = order[b];
           pcov[(size_t)pairs[2 * r] * np + pairs[2 * q]] -= h_corr[q] * h_corr[r] / h_d[pairs[2 * q + 1]];
+        }
+      g0 = g1;
+    }
   }
 }
 

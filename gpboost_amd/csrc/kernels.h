@@ -25,6 +25,9 @@ struct VecchiaRowsArgs {
   double* B_out;         // optional [n x m], B(i, nbr) = -A_i, 0-padded
   int row_base;          // nbr, B_out and Dinv_out hold rows from row_base on (0: all rows;
                          // predictions: the rows after the observed ones)
+  int sched;             // 16-lane kernel, grid grid G < problem sets: 0 = wave w takes sets w, w + G, ...;
+                         // 1 = the last, partial round's sets spread evenly over the waves;
+                         // 2 = as 0 with G = ceil(sets / rounds) (every wave the same count)
 };
 
 int vecchia_rows_blocks(int rows, int m);   // upper bound of the grid (block-partial buffer size)

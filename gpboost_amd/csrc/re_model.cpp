@@ -901,18 +901,20 @@ void REModelAMD::PredictCondAll(int n, int n_pred, int mp, const std::vector<int
     h[n_pred + p] = (v - nugget_sub) * sigma2;
   }
   if (!want_cov) return;
-  cov.assign((size_t)n_pred * n_pred, 0.);
-  std::vector<double> row(n_pred);
+  // cov = Bp^-1 diag(Dp) Bp^-T on the dense path (unit-lower inverse + MFMA GEMM; the host product of
+  // the filled-in rows was O(n_pred^3)); Bp column-major with its unit diagonal, as PredictLatentSim
+  std::vector<double> Bp((size_t)n_pred * n_pred, 0.);
   for (int p = 0; p < n_pred; ++p) {
-    std::fill(row.begin(), row.end(), 0.);
-    for (const auto& e : R[p]) row[e.first] = e.second * Dp[e.first];
-    for (int q = 0; q <= p; ++q) {
-      double c = 0.;
-      for (const auto& e : R[q]) c += row[e.first] * e.second;
-      cov[(size_t)p * n_pred + q] = cov[(size_t)q * n_pred + p] = c * sigma2;
+    Bp[(size_t)p * n_pred + p] = 1.;
+    for (int r = 0; r < mp; ++r) {
+      const int j = nb[(size_t)p * mp + r];
+      if (j >= n) Bp[(size_t)(j - n) * n_pred + p] = B[(size_t)p * mp + r];
     }
-    cov[(size_t)p * n_pred + p] -= nugget_sub * sigma2;
   }
+  cov.assign((size_t)n_pred * n_pred, 0.);
+  latent_pred_moments(stream_, n_pred, Bp.data(), Dp.data(), nullptr, 0, false, true, nullptr, cov.data());
+  for (double& c : cov) c *= sigma2;
+  for (int p = 0; p < n_pred; ++p) cov[(size_t)p * n_pred + p] -= nugget_sub * sigma2;
 }
 
 void REModelAMD::TransformCovPars(const double* orig, double* trafo) const {
@@ -960,6 +962,11 @@ void REModelAMD::LaunchVecchiaRows(const double* trafo, int r0, int r1, double* 
   a.diag_add = 1.;
   a.d_nugget = 1.;
   a.block_sums = d_block_sums_.get();
+  static const int sched = [] {   // A/B of the partial-round schedule (kernels.h VecchiaRowsArgs::sched)
+    const char* e = std::getenv("GPBOOST_AMD_ROWS16_SCHED");
+    return e ? std::atoi(e) : 0;
+  }();
+  a.sched = sched;
   int nblocks = 0;   // the launch's grid (<= vecchia_rows_blocks, the buffer size)
   // HIP events cost ~10 us of host time per evaluation (a quarter of the host overhead): recorded
   // only once GetLastKernelTimes has been called

@@ -448,7 +448,22 @@ int tail_persist_max_w() {
     int dev = 0, cus = 0, per_cu = 0;
     HIP_CHECK(hipGetDevice(&dev));
     HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, tail_persist_kernel<8, 8, 1>, 256, 0));
+    // the grid barriers need every workgroup resident: take the lowest occupancy over all the
+    // instantiations GPBOOST_AMD_TAIL_RCH / _REL can select
+    per_cu = 1 << 30;
+    auto occ = [&](const void* k) {
+      int v = 0;
+      HIP_CHECK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&v, k, 256, 0));
+      per_cu = std::min(per_cu, v);
+    };
+    occ((const void*)tail_persist_kernel<4, 8, 0>);
+    occ((const void*)tail_persist_kernel<4, 8, 1>);
+    occ((const void*)tail_persist_kernel<2, 16, 0>);
+    occ((const void*)tail_persist_kernel<2, 16, 1>);
+    occ((const void*)tail_persist_kernel<8, 4, 0>);
+    occ((const void*)tail_persist_kernel<8, 4, 1>);
+    occ((const void*)tail_persist_kernel<8, 8, 0>);
+    occ((const void*)tail_persist_kernel<8, 8, 1>);
     w = (cus % 8 == 0) ? (per_cu * cus) / 8 : 0;
   }
   return w;

@@ -927,6 +927,13 @@ __global__ void __launch_bounds__(1024) sum_blocks_kernel(const double* __restri
     else out[threadIdx.x] = red[threadIdx.x];
   }
   if (flag != nullptr) {
+    // Ordering of the sums before the flag: on gfx9 (this library targets gfx950 only) vmcnt also
+    // counts stores, so waiting on it means the system-scope stores are acknowledged before the
+    // barrier and the relaxed flag store. gfx10+ counts stores in vscnt instead: there this would
+    // race, hence the guard.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__GFX9__)
+#error "GPB_SUM_FAST relies on gfx9 vmcnt counting stores; use a release store for the flag elsewhere"
+#endif
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the written-through sums are acknowledged
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(flag, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);

@@ -67,12 +67,21 @@ __device__ __forceinline__ double bcast16(double v) {   // lane L of each 16-lan
   return __builtin_bit_cast(double, b);
 }
 
-// acc += (src of lane L of the 16-lane row) * mul, one instruction
-template <int L>
+// acc += (src of lane L of the 16-lane row) * mul, one instruction. NOP: the VALU-write -> DPP-read
+// wait states (2) emitted inside the same asm statement, so no compiler-scheduled VALU op can land
+// between them and the DPP read (the hazard recognizer does not see into inline asm). The first
+// broadcast of every sequence whose source was just written carries them; tests/test_isa_hazards.py
+// disassembles the built kernels and checks every DPP source against the preceding VALU writes.
+template <int L, bool NOP = false>
 __device__ __forceinline__ void fmac_bcast16(double& acc, double src, double mul) {
-  asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-               : "+v"(acc)
-               : "v"(src), "v"(mul), "n"(L));
+  if constexpr (NOP)
+    asm volatile("s_nop 1\n\tv_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc)
+                 : "v"(src), "v"(mul), "n"(L));
+  else
+    asm volatile("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+                 : "+v"(acc)
+                 : "v"(src), "v"(mul), "n"(L));
 }
 
 __device__ __forceinline__ double sum16(double v) {   // fixed-order sum over the 16-lane row
@@ -128,7 +137,20 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
   double* acc = smem + 4 * PD + g * kVecchiaSums;
   if ((lane & 15) < kVecchiaSums) acc[lane & 15] = 0.;
   const int total = a.r1 - a.r0;
-  for (int base = blockIdx.x * 4; base < total; base += gridDim.x * 4) {
+  // problem sets (4 rows) over the G waves: full rounds w + it G; the last round's E sets either on
+  // waves 0..E-1 (sched 0/2) or spread evenly over the grid (sched 1), so its waves do not crowd the
+  // first SIMDs the dispatcher fills
+  const int nsets = (total + 3) / 4, G = gridDim.x, w = blockIdx.x;
+  const int R = (nsets + G - 1) / G, E = nsets - (R - 1) * G;
+  int last_set = (R - 1) * G + w;
+  if (a.sched == 1) {
+    const long lo = (long)w * E / G, hi = (long)(w + 1) * E / G;
+    last_set = hi > lo ? (R - 1) * G + (int)lo : nsets;
+  }
+  for (int it = 0; it < R; ++it) {
+    const int set = it + 1 < R ? it * G + w : last_set;
+    if (set >= nsets) break;
+    const int base = set * 4;
     int h = lane & 15;
     asm volatile("" : "+v"(h));   // lane-dependent addresses / masks recomputed per problem (not hoisted)
     const int v1 = h + 16;
@@ -255,12 +277,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
       // VALU ops instead of three and no move -> FMA dependency
       constexpr bool upd0 = !GPB_ROWS16_BACKSUB || !jhi;   // A rows take part in pivots 0..15 only
       const double nf0 = upd0 ? -f0 : 0., nf1 = -f1;
-      asm volatile("s_nop 1" ::: "memory");   // VALU write -> DPP read wait states (not visible inside asm)
       sfor<j + 1, kK>([&](auto C) {
         constexpr int c = decltype(C)::value;
+        constexpr bool first = c == j + 1;   // wait states before the step's first DPP read
         const double& src = c >= 16 ? r1[j] : r0[j];
-        if constexpr (upd0) fmac_bcast16<c & 15>(r0[c], src, nf0);
-        fmac_bcast16<c & 15>(r1[c], src, nf1);
+        if constexpr (upd0) fmac_bcast16<c & 15, first>(r0[c], src, nf0);
+        fmac_bcast16<c & 15, first && !upd0>(r1[c], src, nf1);
       });
 #elif GPB_ROWS16_BCG > 1
       // GPB_ROWS16_BCG broadcasts in flight: a group's DPP moves issue before its FMAs (the compiler
@@ -307,11 +329,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 2)))
     {   // A rows: M[h][30..31] -= sum_{c=16..29} M[h][c] x_c, x_c = M[c][30..31] / M[c][c] (lane c - 16)
       const double i1 = recip(dg1);
       const double na = rv1 ? -(r1[kMK] * i1) : 0., nw = rv1 ? -(r1[kMK + 1] * i1) : 0.;
-      asm volatile("s_nop 1" ::: "memory");
       sfor<16, kMK>([&](auto C) {
         constexpr int c = decltype(C)::value;
-        fmac_bcast16<c & 15>(r0[kMK], na, r0[c]);
-        fmac_bcast16<c & 15>(r0[kMK + 1], nw, r0[c]);
+        fmac_bcast16<c & 15, c == 16>(r0[kMK], na, r0[c]);
+        fmac_bcast16<c & 15, c == 16>(r0[kMK + 1], nw, r0[c]);
       });
     }
 #endif
@@ -411,7 +432,11 @@ int launch16(const VecchiaRowsArgs& a, hipStream_t s) {
     cap = std::max(1, std::min(per_cu * cus, kMaxGrid));
   }
   const int need = (a.r1 - a.r0 + 3) / 4;
-  const int blocks = std::min(need, cap);
+  int blocks = std::min(need, cap);
+  if (a.sched == 2) {   // the same number of sets per wave
+    const int rounds = (need + blocks - 1) / blocks;
+    blocks = (need + rounds - 1) / rounds;
+  }
   hipLaunchKernelGGL(kern, dim3(blocks), dim3(64), lds, s, a);
   HIP_CHECK(hipGetLastError());
   return blocks;
