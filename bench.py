@@ -33,6 +33,7 @@ PRED_N = 100_000                 # prediction points of the secondary prediction
 M_NEIGHBORS = 30
 THETA = [0.1, 1.0, 0.1]          # sigma2, sigma1^2, rho (original scale), exponential kernel
 FP64_PEAK_TFLOPS = 78.6          # MI355X FP64 vector = FP64 matrix peak (spec)
+RAMP_EVALS_MULTI = 2500          # untimed clock-ramp evaluations at N > 1 (~0.5 s of the 1-GPU rate)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -780,8 +781,13 @@ def main():
     # untimed clock ramp before the W counted warm-up steps: the GPU leaves its idle clocks only after
     # some tens of ms of load (a 5-step warm-up measured the row kernel ~8 % slower than after ~100 ms,
     # profiles/r03/rows_env_ab_r03m.log vs bench_r03n.json)
+    # Several ranks: a fixed count (every evaluation is a collective, so all ranks must run the same
+    # number; a per-rank clock would leave one rank waiting in an all-reduce the others never join)
+    if world > 1:
+        for _ in range(RAMP_EVALS_MULTI):
+            gm.neg_log_likelihood_and_grad(THETA, None, profile_sigma2=True)
     t_ramp = time.perf_counter()
-    while time.perf_counter() - t_ramp < 0.5:
+    while world == 1 and time.perf_counter() - t_ramp < 0.5:
         gm.neg_log_likelihood_and_grad(THETA, None, profile_sigma2=True)
     for _ in range(args.warmup):
         gm.neg_log_likelihood_and_grad(THETA, None, profile_sigma2=True)

@@ -37,6 +37,17 @@ namespace gpb_amd {
 std::vector<double> fitc_inducing_points(const std::vector<double>& coords, int n, int d, int m,
                                          const std::string& method, std::mt19937& rng, hipStream_t s);
 
+// Building blocks shared with the Laplace approximation (fitc_kernels.hip): out = S x (S symmetric
+// m x m, ld ldm); W = sum of `chunks` split-K partials + K_mm,s; the six m x m terms of the gradient
+// [sum Kinv o Kmm, sum Winv o Kmm, sum Kinv o dK, sum Winv o dK, a^T Kmm a, a^T dK a] (part: 6 (m + 3) / 4
+// doubles of scratch); K_mn (m x n, ld ldm) of the coordinates X (row-major n x d) and inducing points Z.
+void fitc_symv(hipStream_t s, const double* S, const double* x, int m, int ldm, double* out);
+void fitc_wsum(hipStream_t s, const double* P, int chunks, long stride, int m, int ldm, const double* Ks, double* W);
+void fitc_mm_terms(hipStream_t s, const double* Kinv, const double* Winv, const double* Kmm, const double* dK,
+                   const double* a, int m, int ldm, double* part, double* out6);
+void fitc_kmn(hipStream_t s, int cov_type, const double* X, const double* Z, int n, int m, int d, int ldm, double var,
+              double phi, double* Kmn);
+
 class FitcSolver {
  public:
   // d_X: device row-major n x d coordinates; Z: host row-major m x d inducing points.
@@ -60,6 +71,10 @@ class FitcSolver {
                double* pvar, double* pcov);
 
  private:
+  friend class FitcLaplace;   // the Laplace approximation (fitc_laplace.h) works on these buffers
+  // K_mn, K_mm, K_mm,s, dK_mm, L = chol(K_mm,s) (red[0] = 2 sum log L_ii), L^-1 (Li_), V = L^-1 K_mn,
+  // K_mm,s^-1 (Kinv_): the part of the factorization that does not depend on the likelihood
+  void Prior(int cov_type, double var, double phi, double* red);
   void Factor(int cov_type, double var, double phi, const double* d_y, double* red);
 
   int n_, d_, m_, ldm_;

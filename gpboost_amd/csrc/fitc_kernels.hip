@@ -705,13 +705,8 @@ FitcSolver::FitcSolver(int n, int d, const double* d_X, const std::vector<double
   HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
-void FitcSolver::Factor(int cov_type, double var, double phi, const double* d_y, double* red) {
+void FitcSolver::Prior(int cov_type, double var, double phi, double* red) {
   const int n = n_, m = m_, ldm = ldm_, d = d_;
-  double* dvec = vec_.get();
-  double* Dy = dvec + n;
-  double* yaux = Dy + n;
-  double* u = yaux + n;
-  double* w = u + ldm;
   HIP_CHECK(hipMemsetAsync(info_.get(), 0, sizeof(int), stream_));
   dispatch_cov_fitc(cov_type, [&](auto c) {
     constexpr int COV = decltype(c)::value;
@@ -732,6 +727,16 @@ void FitcSolver::Factor(int cov_type, double var, double phi, const double* d_y,
   gemm_f64(stream_, m, m, m, 1., Wi_.get(), ldm, 1, Wi_.get(), ldm, 0, 0., Kinv_.get(), ldm, 0, 0, 1, 1);
   // L^-1 is still needed for A = L^-T V (gradient): keep it in Li_ (L itself is no longer needed)
   HIP_CHECK(hipMemcpyAsync(Li_.get(), Wi_.get(), sizeof(double) * ldm * ldm, hipMemcpyDeviceToDevice, stream_));
+}
+
+void FitcSolver::Factor(int cov_type, double var, double phi, const double* d_y, double* red) {
+  const int n = n_, m = m_, ldm = ldm_;
+  double* dvec = vec_.get();
+  double* Dy = dvec + n;
+  double* yaux = Dy + n;
+  double* u = yaux + n;
+  double* w = u + ldm;
+  Prior(cov_type, var, phi, red);
   const int nb4 = (n + 3) / 4;
   hipLaunchKernelGGL(fitc_diag_kernel, dim3(nb4), dim3(256), 0, stream_, V_.get(), Kmn_.get(), d_y, n, m, ldm,
                      1. + var * kJitterMult, dvec, Kd_.get(), Dy, part_.get());
@@ -929,6 +934,35 @@ void FitcSolver::Predict(int cov_type, double var, double phi, const double* d_y
       g0 = g1;
     }
   }
+}
+
+// ---- building blocks shared with the Laplace approximation (fitc_laplace.hip)
+void fitc_symv(hipStream_t s, const double* S, const double* x, int m, int ldm, double* out) {
+  hipLaunchKernelGGL(fitc_symv_kernel, dim3((m + 3) / 4), dim3(256), 0, s, S, x, m, ldm, out);
+  HIP_CHECK(hipGetLastError());
+}
+
+void fitc_wsum(hipStream_t s, const double* P, int chunks, long stride, int m, int ldm, const double* Ks, double* W) {
+  hipLaunchKernelGGL(fitc_wsum_kernel, dim3((m + 63) / 64, (m + 3) / 4), dim3(256), 0, s, P, chunks, stride, m, ldm,
+                     Ks, W);
+  HIP_CHECK(hipGetLastError());
+}
+
+void fitc_mm_terms(hipStream_t s, const double* Kinv, const double* Winv, const double* Kmm, const double* dK,
+                   const double* a, int m, int ldm, double* part, double* out6) {
+  const int mb4 = (m + 3) / 4;
+  hipLaunchKernelGGL(fitc_mm_kernel, dim3(mb4), dim3(256), 0, s, Kinv, Winv, Kmm, dK, a, m, ldm, part);
+  HIP_CHECK(hipGetLastError());
+  launch_sum_blocks(part, mb4, 6, out6, s);
+}
+
+void fitc_kmn(hipStream_t s, int cov_type, const double* X, const double* Z, int n, int m, int d, int ldm, double var,
+              double phi, double* Kmn) {
+  dispatch_cov_fitc(cov_type, [&](auto c) {
+    hipLaunchKernelGGL((fitc_kmn_kernel<decltype(c)::value>), dim3((m + 63) / 64, (n + 3) / 4), dim3(256), 0, s, X, Z,
+                       n, m, d, ldm, var, phi, Kmn);
+  });
+  HIP_CHECK(hipGetLastError());
 }
 
 void FitcSolver::YAux(double* out) {

@@ -54,7 +54,30 @@ struct LatentResult {
   double ms_total = 0.;       // device time of the whole evaluation (HIP events)
 };
 
-class LatentVecchia {
+// What REModelAMD needs from a latent (Laplace) solver, whatever the approximation: LatentVecchia
+// (gp_approx = "vecchia", iterative) and FitcLaplace (gp_approx = "fitc", Cholesky; fitc_laplace.h).
+// Host vectors are in the model's internal order (Vecchia order / the original order for FITC).
+class LatentSolverBase {
+ public:
+  // start: where the Newton iterations begin (FindModePostRandEffCalcMLL*, likelihoods.h):
+  //   kZero  the mode re-initialised to 0 (InitializeModeAvec: GPB_EvalNegLogLikelihood, predictions);
+  //   kWarm  from the previous evaluation (the L-BFGS objective: mode_initialized_ stays true), kept for
+  //          ResetModeToPrevious;
+  //   kKeep  no mode finding: the factor, W and log-determinant at the current mode (CalcGradientF with
+  //          calc_cov_factor = false, re_model_template.h:3021-3043).
+  enum class ModeStart { kZero, kWarm, kKeep };
+  virtual ~LatentSolverBase() = default;
+  virtual void SetY(const double* y) = 0;
+  virtual void SetOffset(const double* off) = 0;   // NULL: none
+  virtual void GetMode(double* mode) = 0;
+  virtual LatentResult Eval(int cov_type, int lik, const double* trafo, double aux, const IterativeConfig& cfg,
+                            bool want_grad, bool want_aux_grad, double* grad_f = nullptr,
+                            ModeStart start = ModeStart::kZero) = 0;
+  virtual void ResetModeToPrevious() = 0;
+  virtual void ClearModePrevious() = 0;
+};
+
+class LatentVecchia : public LatentSolverBase {
  public:
   // d_X: coordinates (Vecchia order, row-major n x d) on the device, owned by the caller.
   // nbr: host n x m neighbour table (row i holds min(i, m) entries).
@@ -67,31 +90,26 @@ class LatentVecchia {
   // one value per observation (that order); the likelihood terms of a latent variable are sums over
   // its observations.
   void SetObservations(const std::vector<int>& obs_row);
-  void SetY(const double* y_vo);   // host, Vecchia order (per observation after SetObservations)
+  void SetY(const double* y_vo) override;   // host, Vecchia order (per observation after SetObservations)
   // Posterior mode of the last evaluation (host, Vecchia order).
-  void GetMode(double* mode_vo);
+  void GetMode(double* mode_vo) override;
   // Fixed effects F of the location parameter (host, Vecchia order; NULL: none). The likelihood is
   // evaluated at mode + F (InitializeLocationPar, likelihoods.h).
-  void SetOffset(const double* off_vo);
+  void SetOffset(const double* off_vo) override;
 
   // trafo = (sigma1^2, phi). aux = gaussian error variance (ignored for bernoulli_logit).
   // grad_f_vo (host, Vecchia order, nullable; needs want_grad): gradient wrt the fixed effects F
   // (CalcGradNegMargLikelihoodLaplaceApproxVecchia calc_F_grad, likelihoods.h:5337-5367).
-  // start: where the Newton iterations begin (FindModePostRandEffCalcMLLVecchia, likelihoods.h:2782-2789):
-  //   kZero  the mode re-initialised to 0 (InitializeModeAvec: GPB_EvalNegLogLikelihood, predictions);
-  //   kWarm  the mode of the previous evaluation (the L-BFGS objective: mode_initialized_ stays true,
-  //          mode_previous_value_ = mode_), kept for ResetModeToPrevious;
-  //   kKeep  no mode finding: the factor, W and log-determinant at the current mode (CalcGradientF with
-  //          calc_cov_factor = false, re_model_template.h:3021-3043, after an OptimCovPar at these
-  //          parameters). The Gaussian likelihood's single Newton step does not depend on the start.
-  enum class ModeStart { kZero, kWarm, kKeep };
+  // start (LatentSolverBase::ModeStart; FindModePostRandEffCalcMLLVecchia, likelihoods.h:2782-2789): kWarm
+  // continues from the previous mode (mode_previous_value_ = mode_). The Gaussian likelihood's single
+  // Newton step does not depend on the start.
   LatentResult Eval(int cov_type, int lik, const double* trafo, double aux, const IterativeConfig& cfg,
                     bool want_grad, bool want_aux_grad, double* grad_f_vo = nullptr,
-                    ModeStart start = ModeStart::kZero);
+                    ModeStart start = ModeStart::kZero) override;
   // Likelihood::ResetModeToPreviousValue (likelihoods.h:528-535): the mode at the start of the last
   // kWarm evaluation back (no-op when no such evaluation started since ClearModePrevious).
-  void ResetModeToPrevious();
-  void ClearModePrevious() { mode_prev_valid_ = false; }
+  void ResetModeToPrevious() override;
+  void ClearModePrevious() override { mode_prev_valid_ = false; }
 
   // Operator costs on the factor of the last evaluation (benchmark roofline): out[0] = ms per
   // A = B^T D^-1 B + W application, out[1] = ms per VADU preconditioner application (both on

@@ -2,6 +2,7 @@
 #include "re_model.h"
 
 #include <algorithm>
+#include <numeric>
 #include <atomic>
 #include <cmath>
 #include <cstdlib>
@@ -69,8 +70,7 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
     if (cfg_.lik != kLikGaussian)
       Fatal("likelihood '%s' requires gp_approx = 'vecchia' in gpboost_amd (dense Laplace is out of scope)", cfg_.likelihood.c_str());
   } else if (cfg_.gp_approx == "fitc") {
-    if (cfg_.lik != kLikGaussian)
-      Fatal("likelihood '%s' with gp_approx = 'fitc' is not supported by gpboost_amd (supported: gaussian)", cfg_.likelihood.c_str());
+    cfg_.latent = cfg_.lik != kLikGaussian;   // Laplace approximation (FitcLaplace)
     if (cfg_.matrix_inversion_method == "iterative")   // re_model_template.h:8774-8776
       Fatal("'iterative' methods are not implemented for gp_approx = 'fitc'. Use 'cholesky' ");
     if (cfg_.num_ind_points <= 0) cfg_.num_ind_points = 500;   // re_model_template.h:320-326
@@ -79,10 +79,10 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
     Fatal("gp_approx '%s' is not supported by gpboost_amd (supported: none, vecchia, vecchia_latent, fitc)", cfg_.gp_approx.c_str());
   }
   std::string& mim = cfg_.matrix_inversion_method;
-  if (mim == "default") mim = cfg_.latent ? "iterative" : "cholesky";
-  if (cfg_.latent && mim != "iterative")
+  if (mim == "default") mim = cfg_.latent && vecchia_ ? "iterative" : "cholesky";
+  if (cfg_.latent && vecchia_ && mim != "iterative")
     Fatal("matrix_inversion_method '%s' is not supported for latent Vecchia models in gpboost_amd (supported: iterative)", mim.c_str());
-  if (!cfg_.latent && mim != "cholesky")
+  if (!(cfg_.latent && vecchia_) && mim != "cholesky")
     Fatal("matrix_inversion_method '%s' is not supported for likelihood 'gaussian' in gpboost_amd (supported: cholesky)", mim.c_str());
   if (cfg_.latent && cfg_.lik == kLikGaussian) aux_pars_ = {1.};   // likelihoods.h:241 (error_variance)
   int ndev = 0;
@@ -163,6 +163,11 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
       if ((int)zu.size() < cfg_.num_ind_points) Fatal("Duplicates found in inducing points / low-dimensional knots ");
       fitc_.reset(new FitcSolver(n, d, d_X_.get(), Z, stream_));
       fitc_rng_ = rng;
+      if (cfg_.latent) {   // FindModePostRandEffCalcMLLFITC / CalcGradNegMargLikelihoodLaplaceApproxFITC
+        fitc_lap_.reset(new FitcLaplace(fitc_.get(), stream_));
+        perm_.resize(n);   // no reordering: the model order is the data order
+        std::iota(perm_.begin(), perm_.end(), 0);
+      }
     } else {
       dense_.reset(new DenseSolver(n, d, d_X_.get(), stream_));
     }
@@ -198,6 +203,7 @@ REModelAMD::~REModelAMD() {
   (void)hipSetDevice(device_);
   if (stream_) (void)hipStreamSynchronize(stream_);
   dense_.reset();
+  fitc_lap_.reset();
   fitc_.reset();
   latent_.reset();
   coll_.reset();
@@ -595,29 +601,11 @@ void REModelAMD::PredictDense(const double* y, int n_pred, const double* coords_
   }
 }
 
-// FITC (CalcPredFITC_FSA, re_model_template.h:10600-10828 via Predict :3890-3893): means, variances or the
-// covariance matrix, times sigma^2 (:3956, :3967); prediction points that coincide with a training point
-// (TwoNumbersAreEqual on the coordinate sums, then per coordinate, utils.h:52-54 with
-// EPSILON_NUMBERS = 1e-10) get the FITC diagonal correction.
-void REModelAMD::PredictFitc(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,
-                             bool predict_cov_mat, bool predict_var, bool predict_response, double* out,
-                             const double* mean_add) {
-  if (n_pred <= 0) Fatal("num_data_pred must be > 0");
-  if (coords_pred == nullptr) Fatal("gp_coords_data_pred must be provided");
-  UseDevice();
-  if (y != nullptr) SetY(y);
-  if (!y_set_) Fatal("response variable y has not been set (pass y or evaluate the likelihood first)");
-  double cp[3];
-  if (cov_pars != nullptr) std::copy(cov_pars, cov_pars + 3, cp);
-  else if ((int)last_cov_pars_.size() == 3) std::copy(last_cov_pars_.begin(), last_cov_pars_.end(), cp);
-  else Fatal("cov_pars must be provided (no previous evaluation)");
-  double trafo[3];
-  TransformCovPars(cp, trafo);
+// FITC: the training point whose coordinates equal prediction point p's, or -1 (CalcPredFITC_FSA,
+// re_model_template.h:10643-10691: TwoNumbersAreEqual on the coordinate sums, then per coordinate,
+// utils.h:52-54 with EPSILON_NUMBERS = 1e-10); candidates by sorted coordinate sums.
+std::vector<int> REModelAMD::FitcMatch(const std::vector<double>& xp, int n_pred) const {
   const int n = cfg_.n, d = cfg_.d;
-  std::vector<double> xp((size_t)n_pred * d);
-  for (int p = 0; p < n_pred; ++p)
-    for (int q = 0; q < d; ++q) xp[(size_t)p * d + q] = coords_pred[(size_t)q * n_pred + p];
-  // coincident coordinates: candidates by sorted coordinate sums, then the reference's predicate
   auto equal = [](double a, double b) {
     return std::fabs(a - b) < 1e-10 * std::max({1.0, std::fabs(a), std::fabs(b)});
   };
@@ -644,6 +632,36 @@ void REModelAMD::PredictFitc(const double* y, int n_pred, const double* coords_p
       }
     }
   }
+  return match;
+}
+
+// FITC (CalcPredFITC_FSA, re_model_template.h:10600-10828 via Predict :3890-3893): means, variances or the
+// covariance matrix, times sigma^2 (:3956, :3967); prediction points that coincide with a training point
+// (TwoNumbersAreEqual on the coordinate sums, then per coordinate, utils.h:52-54 with
+// EPSILON_NUMBERS = 1e-10) get the FITC diagonal correction.
+void REModelAMD::PredictFitc(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,
+                             bool predict_cov_mat, bool predict_var, bool predict_response, double* out,
+                             const double* mean_add) {
+  if (n_pred <= 0) Fatal("num_data_pred must be > 0");
+  if (coords_pred == nullptr) Fatal("gp_coords_data_pred must be provided");
+  if (cfg_.latent) {
+    PredictFitcLaplace(y, n_pred, coords_pred, cov_pars, predict_cov_mat, predict_var, predict_response, out, mean_add);
+    return;
+  }
+  UseDevice();
+  if (y != nullptr) SetY(y);
+  if (!y_set_) Fatal("response variable y has not been set (pass y or evaluate the likelihood first)");
+  double cp[3];
+  if (cov_pars != nullptr) std::copy(cov_pars, cov_pars + 3, cp);
+  else if ((int)last_cov_pars_.size() == 3) std::copy(last_cov_pars_.begin(), last_cov_pars_.end(), cp);
+  else Fatal("cov_pars must be provided (no previous evaluation)");
+  double trafo[3];
+  TransformCovPars(cp, trafo);
+  const int d = cfg_.d;
+  std::vector<double> xp((size_t)n_pred * d);
+  for (int p = 0; p < n_pred; ++p)
+    for (int q = 0; q < d; ++q) xp[(size_t)p * d + q] = coords_pred[(size_t)q * n_pred + p];
+  const std::vector<int> match = FitcMatch(xp, n_pred);
   std::vector<double> mean(n_pred), var(predict_var ? n_pred : 0);
   std::vector<double> cov(predict_cov_mat ? (size_t)n_pred * n_pred : 0);
   fitc_->Predict(cfg_.cov_type, trafo[1], trafo[2], d_y_.get(), xp.data(), n_pred, match, predict_var,
@@ -656,6 +674,53 @@ void REModelAMD::PredictFitc(const double* y, int n_pred, const double* coords_p
   } else if (predict_var) {
     for (int p = 0; p < n_pred; ++p) out[n_pred + p] = var[p] * trafo[0];
   }
+}
+
+// FITC with a Laplace likelihood (CalcPredFITC_FSA, re_model_template.h:10600-10760, then
+// PredictLaplaceApproxFITC, likelihoods.h:7157-7232): the mode at the parameters (found from zero, as
+// the Vecchia latent path), then latent means / variances / covariance (FitcLaplace::Predict), the
+// fixed effects of the prediction points added to the mean, and for predict_response the bernoulli_logit
+// response probabilities by the adaptive Gauss-Hermite rule (PredictResponse, likelihoods.h:7544-7556).
+void REModelAMD::PredictFitcLaplace(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,
+                                    bool predict_cov_mat, bool predict_var, bool predict_response, double* out,
+                                    const double* mean_add) {
+  UseDevice();
+  if (y != nullptr) SetY(y);
+  if (!y_set_) Fatal("response variable y has not been set (pass y or evaluate the likelihood first)");
+  double cp[2];
+  if (cov_pars != nullptr) std::copy(cov_pars, cov_pars + 2, cp);
+  else if ((int)last_cov_pars_.size() == 2) std::copy(last_cov_pars_.begin(), last_cov_pars_.end(), cp);
+  else Fatal("cov_pars must be provided (no previous evaluation)");
+  if (predict_cov_mat && predict_response)
+    Fatal("predictive covariance matrices of the response are not supported for likelihood '%s' by gpboost_amd "
+          "(use predict_response = false or predict_var)", cfg_.likelihood.c_str());
+  EvalLatent(cp, false);   // the mode at these parameters (SetYCalcCovCalcYAuxForPred, re_model_template.h:3306-3312)
+  const int d = cfg_.d;
+  std::vector<double> xp((size_t)n_pred * d);
+  for (int p = 0; p < n_pred; ++p)
+    for (int q = 0; q < d; ++q) xp[(size_t)p * d + q] = coords_pred[(size_t)q * n_pred + p];
+  const std::vector<int> match = FitcMatch(xp, n_pred);
+  const bool want_var = predict_var || predict_response;
+  std::vector<double> mean(n_pred), var(want_var ? n_pred : 0), cov(predict_cov_mat ? (size_t)n_pred * n_pred : 0);
+  fitc_lap_->Predict(cfg_.cov_type, cp[0], range_trafo(cfg_.cov_type, cp[1]), xp.data(), n_pred, match, want_var,
+                     predict_cov_mat, mean.data(), var.data(), cov.data());
+  if (mean_add != nullptr)
+    for (int p = 0; p < n_pred; ++p) mean[p] += mean_add[p];
+  if (predict_response && cfg_.lik == kLikBernoulliLogit) {
+    static const std::vector<double> gh = gauss_hermite_adaptive(30);   // order_GH_ = 30 (likelihoods.h:12877)
+    DevBuf<double> dmv((size_t)2 * n_pred), dgh(gh.size()), dout((size_t)2 * n_pred);
+    HIP_CHECK(hipMemcpyAsync(dmv.get(), mean.data(), sizeof(double) * n_pred, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipMemcpyAsync(dmv.get() + n_pred, var.data(), sizeof(double) * n_pred, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipMemcpyAsync(dgh.get(), gh.data(), sizeof(double) * gh.size(), hipMemcpyHostToDevice, stream_));
+    launch_resp_logit(n_pred, dmv.get(), dmv.get() + n_pred, dgh.get(), dgh.get() + 30, 30, iter.delta_conv_mode_finding,
+                      dout.get(), dout.get() + n_pred, stream_);
+    HIP_CHECK(hipMemcpyAsync(mean.data(), dout.get(), sizeof(double) * n_pred, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(var.data(), dout.get() + n_pred, sizeof(double) * n_pred, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
+  std::copy(mean.begin(), mean.end(), out);
+  if (predict_cov_mat) std::copy(cov.begin(), cov.end(), out + n_pred);
+  else if (predict_var) std::copy(var.begin(), var.end(), out + n_pred);
 }
 
 // order_pred_first, Gaussian likelihood (CalcPredVecchiaPredictedFirstOrder, Vecchia_utils.cpp:2018-2239):
@@ -938,7 +1003,7 @@ void REModelAMD::SetY(const double* y) {
         if (yv[i] != 0. && yv[i] != 1.) Fatal("Response variable (label) data needs to be 0 or 1 for likelihood = 'bernoulli_logit' ");
     }
     y_vo_ = yv;
-    if (latent_) latent_->SetY(y_vo_.data());
+    if (lat()) lat()->SetY(y_vo_.data());
   }
   d_y_.alloc(n);
   HIP_CHECK(hipMemcpyAsync(d_y_.get(), yv.data(), sizeof(double) * n, hipMemcpyHostToDevice, stream_));
@@ -1071,7 +1136,7 @@ EvalResult REModelAMD::EvalLatent(const double* cov_pars_orig, bool want_grad) {
 }
 
 void REModelAMD::ResetLatentModeToPrevious() {
-  if (latent_) latent_->ResetModeToPrevious();
+  if (lat()) lat()->ResetModeToPrevious();
 }
 
 EvalResult REModelAMD::EvalLatentTrafo(const double* trafo, bool want_grad, bool fatal_on_nan,
@@ -1079,7 +1144,7 @@ EvalResult REModelAMD::EvalLatentTrafo(const double* trafo, bool want_grad, bool
   if (!y_set_) Fatal("response variable y has not been set");
   UseDevice();
   EnsureStructure();
-  latent_->ClearModePrevious();
+  lat()->ClearModePrevious();
   const double aux = aux_pars_.empty() ? 1. : aux_pars_[0];
   const bool aux_grad = estimate_aux_pars && !aux_pars_.empty();
   LatentResult r;
@@ -1087,7 +1152,7 @@ EvalResult REModelAMD::EvalLatentTrafo(const double* trafo, bool want_grad, bool
     // fault injection for the tests: the k-th latent evaluation of this model reports NaN
     if (const char* e = std::getenv("GPBOOST_AMD_TEST_NAN_EVAL"))
       if (++test_nan_count_ == std::atoi(e)) throw LatentNan("NaN or Inf occurred (injected by GPBOOST_AMD_TEST_NAN_EVAL)");
-    r = latent_->Eval(cfg_.cov_type, cfg_.lik, trafo, aux, iter, want_grad, aux_grad, nullptr, start);
+    r = lat()->Eval(cfg_.cov_type, cfg_.lik, trafo, aux, iter, want_grad, aux_grad, nullptr, start);
     latent_evaluated_ = true;
   } catch (const LatentNan& e) {
     HIP_CHECK(hipStreamSynchronize(stream_));   // drain what the interrupted evaluation had queued

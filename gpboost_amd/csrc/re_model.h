@@ -19,6 +19,7 @@
 #include "common.h"
 #include "dense.h"
 #include "fitc.h"
+#include "fitc_laplace.h"
 #include "latent.h"
 #include "optim.h"
 
@@ -223,6 +224,10 @@ class REModelAMD {
                     bool predict_var, bool predict_response, double* out, const double* mean_add);
   void PredictFitc(const double* y, int n_pred, const double* coords_pred, const double* cov_pars, bool predict_cov_mat,
                    bool predict_var, bool predict_response, double* out, const double* mean_add);
+  std::vector<int> FitcMatch(const std::vector<double>& xp_rowmajor, int n_pred) const;
+  void PredictFitcLaplace(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,
+                          bool predict_cov_mat, bool predict_var, bool predict_response, double* out,
+                          const double* mean_add);
   void PredictCondAll(int n, int n_pred, int mp, const std::vector<int>& nb, const double* dB, const double* dDinv,
                       double sigma2, double nugget_sub, bool want_var, bool want_cov, std::vector<double>& h,
                       std::vector<double>& cov);
@@ -265,9 +270,14 @@ class REModelAMD {
   bool timing_ = false;           // record kernel events (set by the first GetLastKernelTimes)
 
   std::unique_ptr<DenseSolver> dense_;
-  std::unique_ptr<FitcSolver> fitc_;   // gp_approx = "fitc" (Gaussian likelihood)
+  std::unique_ptr<FitcSolver> fitc_;   // gp_approx = "fitc"
+  std::unique_ptr<FitcLaplace> fitc_lap_;   // gp_approx = "fitc", non-Gaussian likelihood (Laplace)
   std::mt19937 fitc_rng_;              // the model's generator after the inducing-point selection
   std::unique_ptr<LatentVecchia> latent_;
+  // the latent solver of a Laplace model: the Vecchia (iterative) or the FITC (Cholesky) one
+  LatentSolverBase* lat() const {
+    return latent_ ? static_cast<LatentSolverBase*>(latent_.get()) : static_cast<LatentSolverBase*>(fitc_lap_.get());
+  }
   std::vector<double> y_vo_;          // host copy (Vecchia order) for the latent solver
   std::vector<double> aux_pars_;
   double last_iter_info_[4] = {0., 0., 0., 0.};

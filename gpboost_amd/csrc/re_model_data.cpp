@@ -4,6 +4,7 @@
 #include <cmath>
 #include <cstring>
 #include <limits>
+#include <numeric>
 
 #include "cov.h"
 #include "covariates.h"
@@ -34,7 +35,7 @@ void REModelAMD::SetLatentOffset(const double* fe) {
     for (int i = 0; i < n; ++i) offset_vo_[i] = fe[perm_[i]];
     has_offset_ = true;
   }
-  if (latent_) latent_->SetOffset(has_offset_ ? offset_vo_.data() : nullptr);
+  if (lat()) lat()->SetOffset(has_offset_ ? offset_vo_.data() : nullptr);
 }
 
 void REModelAMD::SetResponseAndOffset(const double* y, const double* fixed_effects) {
@@ -75,7 +76,7 @@ void REModelAMD::CalcGradientF(double* y, const double* fixed_effects, bool calc
     std::vector<double> gvo(n);
     const auto start = (!calc_cov_factor && latent_evaluated_) ? LatentVecchia::ModeStart::kKeep
                                                                : LatentVecchia::ModeStart::kWarm;
-    latent_->Eval(cfg_.cov_type, cfg_.lik, trafo, aux, iter, true, false, gvo.data(), start);
+    lat()->Eval(cfg_.cov_type, cfg_.lik, trafo, aux, iter, true, false, gvo.data(), start);
     latent_evaluated_ = true;
     for (int i = 0; i < n; ++i) y[perm_[i]] = gvo[i];
     return;
@@ -270,7 +271,7 @@ void REModelAMD::PredictTrainingDataRandomEffects(const double* cov_pars, const 
     SetLatentOffset(ResolveOffset(fixed_effects));   // re_model_template.h:4032-4039
     EvalLatent(cp.data(), false);   // the posterior mode at cov_pars
     std::vector<double> mvo(nu_);
-    latent_->GetMode(mvo.data());
+    lat()->GetMode(mvo.data());
     for (int i = 0; i < n; ++i) out[perm_[i]] = mvo[has_dup() ? obs_row_[i] : i];   // Z mode
     return;
   }
@@ -333,10 +334,19 @@ void REModelAMD::SetLikelihood(const std::string& likelihood) {
   if (likelihood == "gaussian") lik = kLikGaussian;
   else if (likelihood == "bernoulli_logit") lik = kLikBernoulliLogit;
   else Fatal("likelihood '%s' is not supported by gpboost_amd (supported: gaussian, bernoulli_logit)", likelihood.c_str());
-  const bool latent = c.gp_approx == "vecchia_latent" || (vecchia_ && lik != kLikGaussian);
-  if (!vecchia_ && lik != kLikGaussian)
-    Fatal("likelihood '%s' requires gp_approx = 'vecchia' in gpboost_amd (dense Laplace is out of scope)", likelihood.c_str());
-  if (latent && !cfg_.latent) {   // exact -> latent: distinct coordinates, iterative solver (re_model_template.h:568-571)
+  const bool latent = c.gp_approx == "vecchia_latent" || ((vecchia_ || fitc_) && lik != kLikGaussian);
+  if (!vecchia_ && !fitc_ && lik != kLikGaussian)
+    Fatal("likelihood '%s' requires gp_approx = 'vecchia' or 'fitc' in gpboost_amd (dense Laplace is out of scope)",
+          likelihood.c_str());
+  if (fitc_) {   // FITC: the Laplace solver on the same inducing points (Cholesky either way)
+    if (latent && !fitc_lap_) {
+      fitc_lap_.reset(new FitcLaplace(fitc_.get(), stream_));
+      perm_.resize(cfg_.n);
+      std::iota(perm_.begin(), perm_.end(), 0);
+    } else if (!latent) {
+      fitc_lap_.reset();
+    }
+  } else if (latent && !cfg_.latent) {   // exact -> latent: distinct coordinates, iterative solver (re_model_template.h:568-571)
     std::vector<int> ord(cfg_.n);
     for (int i = 0; i < cfg_.n; ++i) ord[i] = i;
     const int d = cfg_.d;

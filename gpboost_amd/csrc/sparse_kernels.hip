@@ -19,6 +19,7 @@
 
 #include "common.h"
 #include "latent_kernels.h"
+#include "lik_device.h"
 #include "wave_ops.h"
 
 namespace gpb_amd {
@@ -1097,39 +1098,7 @@ __global__ void pack_columns_kernel(size_t rows, int ncols, const double* __rest
   }
 }
 
-// ------------------------------------------------------------------ likelihoods
-// likelihoods.h: gaussian :8795, 9263, 9937; bernoulli_logit :8724, 9226, 9896, 10187;
-// sigmoid_stable / softplus DF_utils.h:37-60
-__device__ __forceinline__ double sigmoid_stable(double x) {
-  if (x >= 0.) {
-    const double e = exp(-x);
-    return 1. / (1. + e);
-  }
-  const double e = exp(x);
-  return e / (1. + e);
-}
-__device__ __forceinline__ double softplus(double x) { return log1p(exp(-fabs(x))) + fmax(x, 0.); }
-
-__device__ __forceinline__ double lik_loglik(int lik, double aux, double y, double l) {
-  if (lik == kLikGaussian) {
-    const double r = y - l;
-    return -r * r / 2. / aux - 0.91893853320467274178 - 0.5 * log(aux);   // M_LOGSQRT2PI
-  }
-  return y * l - softplus(l);
-}
-__device__ __forceinline__ double lik_d1(int lik, double aux, double y, double l) {
-  return lik == kLikGaussian ? (y - l) / aux : y - sigmoid_stable(l);
-}
-__device__ __forceinline__ double lik_info(int lik, double aux, double l) {
-  if (lik == kLikGaussian) return 1. / aux;
-  const double p = sigmoid_stable(l);
-  return p * (1. - p);
-}
-__device__ __forceinline__ double lik_dinfo(int lik, double l) {
-  if (lik == kLikGaussian) return 0.;
-  const double p = sigmoid_stable(l);
-  return -p * (1. - p) * (2. * p - 1.);
-}
+// ------------------------------------------------------------------ likelihoods: lik_device.h
 
 __global__ void __launch_bounds__(kBT) grad_f_kernel(int n, const double* __restrict__ d1,
                                                      const double* __restrict__ dmll, const double* __restrict__ W,

@@ -444,8 +444,8 @@ int main(int argc, char** argv) {
   if (gauss && gp_approx == "vecchia") {
     std::printf("\"yTPsiInvy\": %.17g, \"log_det_Psi\": %.17g,\n", m->yTPsiInvy_, m->log_det_Psi_);
   }
-  if (gauss && gp_approx == "fitc") {
-    std::printf("\"yTPsiInvy\": %.17g, \"log_det_Psi\": %.17g,\n", m->yTPsiInvy_, m->log_det_Psi_);
+  if (gp_approx == "fitc") {
+    if (gauss) std::printf("\"yTPsiInvy\": %.17g, \"log_det_Psi\": %.17g,\n", m->yTPsiInvy_, m->log_det_Psi_);
     const den_mat_t& ip = m->gp_coords_ip_mat_;
     std::vector<double> ipv((size_t)ip.rows() * ip.cols());
     for (int i = 0; i < (int)ip.rows(); ++i)

@@ -99,8 +99,6 @@ def test_fitc_refusals():
     X = synthetic.bench_coords(500)
     with pytest.raises(GPBoostError, match="iterative"):
         GPModel(gp_coords=X, gp_approx="fitc", num_ind_points=20, matrix_inversion_method="iterative")
-    with pytest.raises(GPBoostError, match="fitc"):
-        GPModel(gp_coords=X, gp_approx="fitc", num_ind_points=20, likelihood="bernoulli_logit")
     with pytest.raises(GPBoostError, match="more inducing points"):
         GPModel(gp_coords=X, gp_approx="fitc", num_ind_points=600)
     Xd = np.vstack([X, X[:10]])

@@ -1,0 +1,86 @@
+"""Pins the FITC-Laplace CPU restatement (oracle/fitc_laplace_oracle.py) to the reference's own outputs
+(tests/golden/golden_fitc_laplace.json, make_golden_fitc_laplace.py): the approximate negative marginal
+log-likelihood, its gradient, the gradient wrt the fixed effects and the latent predictions, given the
+reference's inducing points. CPU only.
+
+Tolerances: nll 1e-10, gradients 1e-7 (the same Cholesky-solve formulation as the reference; rounding only),
+predictions 1e-9.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from gpboost_amd import synthetic
+from oracle import oracle as O
+from oracle.fitc_laplace_oracle import FitcLaplaceOracle
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+with open(os.path.join(HERE, "golden", "golden_fitc_laplace.json")) as _f:
+    GOLDEN = json.load(_f)
+
+
+def _setup(case, fe=None, ind_points=None):
+    sp = case["spec"]
+    X = synthetic.bench_coords(case["n"])
+    y = synthetic.bench_bernoulli_y(X)
+    Z = np.array(ind_points if ind_points is not None else case["ind_points"]).reshape(case["m"], -1)
+    ct = O.cov_code(sp["cov_fct"], float(sp["shape"]))
+    tr = O.transform_latent(ct, case["cov_pars"])
+    return X, y, FitcLaplaceOracle(X, y, Z, ct, tr[0], tr[1], fixed_effects=fe)
+
+
+@pytest.mark.parametrize("name", [k for k in GOLDEN if k.startswith("fl_") and GOLDEN[k]["n"] <= 4000])
+def test_oracle_fitc_laplace_matches_reference(name):
+    case = GOLDEN[name]
+    _, _, orc = _setup(case)
+    nll = orc.find_mode()
+    assert abs(nll - case["nll"]) <= 1e-10 * abs(case["nll"])
+    np.testing.assert_allclose(orc.gradient()["grad"], case["grad"], rtol=1e-7)
+
+
+def _ind_points_of(case):
+    """Inducing points of a fixture that did not store them: the eval fixture of the same selection."""
+    for v in GOLDEN.values():
+        if "ind_points" in v and v["n"] == case["n"] and v["m"] == case["m"] and v["spec"]["seed"] == case["spec"]["seed"]:
+            return v["ind_points"]
+    from oracle.oracle import fitc_inducing_points
+    X = synthetic.bench_coords(case["n"])
+    return fitc_inducing_points(X, case["m"], case["spec"]["ind_points_selection"], case["spec"]["seed"])[0]
+
+
+def test_oracle_fitc_laplace_gradient_f():
+    case = GOLDEN["gradf_fl_exp_n2000_m80"]
+    X = synthetic.bench_coords(case["n"])
+    fe = 0.3 * np.sin(3.0 * X[:, 0]) - 0.2
+    _, _, orc = _setup(case, fe=fe, ind_points=_ind_points_of(case))
+    nll = orc.find_mode()
+    assert abs(nll - case["nll"]) <= 1e-10 * abs(case["nll"])
+    out = orc.gradient(want_f=True)
+    np.testing.assert_allclose(out["grad"], case["grad"], rtol=1e-7)
+    ref = np.asarray(case["grad_f"])
+    assert np.max(np.abs(out["grad_f"] - ref)) <= 1e-9 * np.max(np.abs(ref))
+
+
+@pytest.mark.parametrize("name", [k for k in GOLDEN if k.startswith("pred_") and not GOLDEN[k]["response"]])
+def test_oracle_fitc_laplace_predict(name):
+    case = GOLDEN[name]
+    X, _, orc = _setup(case, ind_points=_ind_points_of(case))
+    orc.find_mode()
+    npred = case["npred"]
+    xp = synthetic.lcg_unif(npred * 2, 0.713).reshape(2, npred).T.copy()
+    match = None
+    if case["train_pts"]:
+        k = case["train_pts"]
+        idx = np.arange(0, case["n"], max(1, case["n"] // k))[:k]
+        xp[:k] = X[idx]
+        match = -np.ones(npred, dtype=int)
+        match[:k] = idx
+    want_cov = "cov" in case
+    out = orc.predict(xp, match=match, want_var=not want_cov, want_cov=want_cov)
+    np.testing.assert_allclose(out["mean"], case["mean"], rtol=1e-9, atol=1e-12)
+    if want_cov:
+        np.testing.assert_allclose(out["cov"], np.asarray(case["cov"]).reshape(npred, npred), rtol=1e-9, atol=1e-12)
+    else:
+        np.testing.assert_allclose(out["var"], case["var"], rtol=1e-9, atol=1e-12)
