@@ -556,19 +556,50 @@ class GPModel:
                             nsim_var_pred=None, rank_pred_approx_matrix_lanczos=None, group_data_pred=None,
                             group_rand_coef_data_pred=None, gp_coords_pred=None, gp_rand_coef_data_pred=None,
                             cluster_ids_pred=None, X_pred=None):
-        """Prediction settings (reference basic.py:6095, GPB_SetPredictionData). Only
-        vecchia_pred_type / num_neighbors_pred / nsim_var_pred are supported; prediction data is passed
-        to predict()."""
-        if any(v is not None for v in (group_data_pred, group_rand_coef_data_pred, gp_coords_pred,
-                                       gp_rand_coef_data_pred, cluster_ids_pred, X_pred)):
-            raise GPBoostError("set_prediction_data: saving prediction data is not supported by gpboost_amd; "
-                               "pass gp_coords_pred to predict()")
+        """Prediction settings and data (reference basic.py:6095-6190, GPB_SetPredictionData): the data is
+        saved in the model for predict(use_saved_data=True) (gp_coords_pred / X_pred for GP models,
+        group_data_pred for grouped random effects)."""
+        if any(v is not None for v in (group_rand_coef_data_pred, gp_rand_coef_data_pred, cluster_ids_pred)):
+            raise GPBoostError("set_prediction_data: random coefficients and clusters are not supported by gpboost_amd")
+        num_data_pred = 0
+        gbuf = xcol = xpc = None
+        if group_data_pred is not None:
+            g = np.asarray(group_data_pred)
+            if g.ndim == 1:
+                g = g.reshape(-1, 1)
+            if g.shape[1] != getattr(self, "num_group_re", 0):
+                raise ValueError("Number of grouped random effects in group_data_pred is not correct")
+            num_data_pred = g.shape[0]
+            labels = g.astype(np.dtype(str)).flatten(order="F")
+            gbuf = ctypes.create_string_buffer(b"\0".join(s.encode() for s in labels) + b"\0")
+        if gp_coords_pred is not None:
+            xp = np.asarray(gp_coords_pred, dtype=np.float64)
+            if xp.ndim == 1:
+                xp = xp.reshape(-1, 1)
+            if xp.shape[1] != self.dim_coords:
+                raise ValueError("Incorrect dimension / number of coordinates (=features) in gp_coords_pred")
+            if num_data_pred and xp.shape[0] != num_data_pred:
+                raise ValueError("Incorrect number of data points in gp_coords_pred")
+            num_data_pred = xp.shape[0]
+            xcol = np.ascontiguousarray(xp.T.reshape(-1))
+        if X_pred is not None:
+            Xp = np.asarray(X_pred, dtype=np.float64)
+            if Xp.ndim == 1:
+                Xp = Xp.reshape(-1, 1)
+            if num_data_pred and Xp.shape[0] != num_data_pred:
+                raise ValueError("Incorrect number of data points in X_pred")
+            num_data_pred = Xp.shape[0]
+            xpc = np.ascontiguousarray(Xp.T).reshape(-1)
         _safe_call(lib().GPB_SetPredictionData(
-            self.handle, ctypes.c_int32(0), None, None, None, None, None, None, c_str(vecchia_pred_type),
+            self.handle, ctypes.c_int32(num_data_pred), None, gbuf, None, _dp(xcol) if xcol is not None else None,
+            None, _dp(xpc) if xpc is not None else None, c_str(vecchia_pred_type),
             ctypes.c_int(int(num_neighbors_pred) if num_neighbors_pred is not None else -1),
             ctypes.c_double(float(cg_delta_conv_pred) if cg_delta_conv_pred is not None else -1.),
             ctypes.c_int(int(nsim_var_pred) if nsim_var_pred is not None else -1),
             ctypes.c_int(int(rank_pred_approx_matrix_lanczos) if rank_pred_approx_matrix_lanczos is not None else -1)))
+        if num_data_pred > 0:
+            self.prediction_data_is_set = True
+            self.num_data_pred = num_data_pred
 
     def predict(self, predict_response=True, predict_var=False, predict_cov_mat=False, y=None, cov_pars=None,
                 group_data_pred=None, group_rand_coef_data_pred=None, gp_coords_pred=None,
@@ -580,6 +611,11 @@ class GPModel:
         models (vecchia_pred_type "order_obs_first_cond_obs_only") and latent Vecchia models
         ("latent_order_obs_first_cond_obs_only": Laplace mode, simulated iterative variances,
         bernoulli_logit response probabilities by adaptive Gauss-Hermite quadrature)."""
+        if use_saved_data:   # reference basic.py:6035-6038: the data saved by set_prediction_data
+            if not getattr(self, "prediction_data_is_set", False):
+                raise ValueError("No data has been set for making predictions. Call set_prediction_data first")
+            return self._predict_saved(predict_var, predict_cov_mat, predict_response, y, cov_pars, offset,
+                                       offset_pred, fixed_effects, fixed_effects_pred)
         if getattr(self, "num_group_re", 0):
             return self._predict_grouped(group_data_pred, predict_var, predict_cov_mat, predict_response, y, cov_pars,
                                          offset, offset_pred, fixed_effects, fixed_effects_pred)
@@ -628,6 +664,33 @@ class GPModel:
         var = out[n_pred:].copy() if (predict_var and not predict_cov_mat) else None
         if predict_cov_mat and predict_var:
             var = np.diag(cov).copy()
+        return {"mu": mu, "cov": cov, "var": var}
+
+    def _predict_saved(self, predict_var, predict_cov_mat, predict_response, y, cov_pars, offset, offset_pred,
+                       fixed_effects, fixed_effects_pred):
+        """GPB_PredictREModel(use_saved_data = true): every data argument NULL, num_data_pred that of the
+        saved data (re_model_template.h:3168-3206)."""
+        n_pred = self.num_data_pred
+        yv = self._check_y(y)
+        if offset is not None:
+            fixed_effects = offset if fixed_effects is None else np.asarray(fixed_effects) + np.asarray(offset)
+        if offset_pred is not None:
+            fixed_effects_pred = offset_pred if fixed_effects_pred is None else (
+                np.asarray(fixed_effects_pred) + np.asarray(offset_pred))
+        fe = _as1d(fixed_effects, "fixed_effects") if fixed_effects is not None else None
+        fep = _as1d(fixed_effects_pred, "fixed_effects_pred") if fixed_effects_pred is not None else None
+        cp = self._check_cov_pars(cov_pars) if cov_pars is not None else None
+        size = n_pred + (n_pred * n_pred if predict_cov_mat else (n_pred if predict_var else 0))
+        out = np.zeros(size)
+        _safe_call(lib().GPB_PredictREModel(
+            self.handle, _dp(yv) if yv is not None else None, ctypes.c_int32(n_pred), _dp(out),
+            ctypes.c_bool(bool(predict_cov_mat)), ctypes.c_bool(bool(predict_var)),
+            ctypes.c_bool(bool(predict_response)), None, None, None, None, None,
+            _dp(cp) if cp is not None else None, None, ctypes.c_bool(True),
+            _dp(fe) if fe is not None else None, _dp(fep) if fep is not None else None))
+        mu = out[:n_pred].copy()
+        cov = out[n_pred:].reshape(n_pred, n_pred).T.copy() if predict_cov_mat else None
+        var = out[n_pred:].copy() if (predict_var and not predict_cov_mat) else None
         return {"mu": mu, "cov": cov, "var": var}
 
     def _predict_grouped(self, group_data_pred, predict_var, predict_cov_mat, predict_response, y, cov_pars, offset,

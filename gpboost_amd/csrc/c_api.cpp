@@ -11,7 +11,9 @@
 #include <exception>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <unordered_set>
+#include <vector>
 
 #include "grouped_model.h"
 #include "re_model.h"
@@ -29,6 +31,18 @@ GroupedModel* as_grouped(REModelHandle h) {
   std::lock_guard<std::mutex> lk(g_grouped_mu);
   return g_grouped.count(h) ? reinterpret_cast<GroupedModel*>(h) : nullptr;
 }
+
+// Prediction data saved by GPB_SetPredictionData for GPB_PredictREModel(use_saved_data = true)
+// (REModelTemplate::SetPredictionData / Predict, re_model_template.h:3061-3119, 3168-3206): copies, per
+// handle; a later call replaces the kinds of data it gives.
+struct SavedPred {
+  int num_data_pred = 0;
+  std::vector<double> gp_coords;     // column-major num_data_pred x dim
+  std::vector<double> covariates;    // column-major num_data_pred x p
+  std::vector<char> re_group;        // num_data_pred x K NUL-terminated level strings, effect-major
+};
+std::mutex g_saved_mu;
+std::unordered_map<const void*, SavedPred> g_saved;
 
 thread_local char g_last_error[512] = "Everything is fine";
 void (*g_log_callback)(const char*) = nullptr;
@@ -182,6 +196,10 @@ int GPB_CreateREModel(int32_t num_data, const int32_t* cluster_ids_data, const c
 
 int GPB_REModelFree(REModelHandle handle) {
   API_BEGIN();
+  {
+    std::lock_guard<std::mutex> lk(g_saved_mu);
+    g_saved.erase(handle);
+  }
   if (GroupedModel* g = as_grouped(handle)) {
     {
       std::lock_guard<std::mutex> lk(g_grouped_mu);
@@ -298,12 +316,42 @@ int GPB_SetPredictionData(REModelHandle handle, int32_t num_data_pred, const int
   API_BEGIN();
   (void)cg_delta_conv_pred;   // the Vecchia-Laplace draws use the model's cg_delta_conv (likelihoods.h:12052)
   (void)rank_pred_approx_matrix_lanczos;
-  if (num_data_pred > 0 || cluster_ids_data_pred != nullptr || re_group_data_pred != nullptr ||
-      re_group_rand_coef_data_pred != nullptr || gp_coords_data_pred != nullptr || gp_rand_coef_data_pred != nullptr ||
-      covariate_data_pred != nullptr)
-    gpb_amd::Fatal("GPB_SetPredictionData: saving prediction data is not supported by gpboost_amd; pass the "
-                   "prediction coordinates to GPB_PredictREModel");
-  model(handle)->SetPredictionData(vecchia_pred_type, num_neighbors_pred, nsim_var_pred);
+  if (handle == nullptr) gpb_amd::Fatal("REModelHandle is NULL");
+  if (cluster_ids_data_pred != nullptr || re_group_rand_coef_data_pred != nullptr || gp_rand_coef_data_pred != nullptr)
+    gpb_amd::Fatal("GPB_SetPredictionData: clusters and random coefficients are not supported by gpboost_amd");
+  GroupedModel* g = as_grouped(handle);
+  const bool has_data = re_group_data_pred != nullptr || gp_coords_data_pred != nullptr || covariate_data_pred != nullptr;
+  if (has_data) {
+    if (num_data_pred <= 0) gpb_amd::Fatal("num_data_pred must be > 0 when prediction data is given");   // CHECK :3075
+    if (g != nullptr && (gp_coords_data_pred != nullptr || covariate_data_pred != nullptr))
+      gpb_amd::Fatal("GP coordinates or covariates for a grouped random effects model are not supported by gpboost_amd");
+    if (g == nullptr && re_group_data_pred != nullptr)
+      gpb_amd::Fatal("grouped random effects data for a GP model are not supported by gpboost_amd");
+    SavedPred sp;
+    {
+      std::lock_guard<std::mutex> lk(g_saved_mu);
+      auto it = g_saved.find(handle);
+      if (it != g_saved.end()) sp = it->second;
+    }
+    sp.num_data_pred = num_data_pred;
+    if (gp_coords_data_pred != nullptr) {
+      const size_t cnt = (size_t)num_data_pred * model(handle)->config().d;
+      sp.gp_coords.assign(gp_coords_data_pred, gp_coords_data_pred + cnt);
+    }
+    if (covariate_data_pred != nullptr) {
+      const int p = model(handle)->num_covariates();
+      if (p <= 0) gpb_amd::Fatal("Covariate data 'X_pred' is provided but the model has no covariates");
+      sp.covariates.assign(covariate_data_pred, covariate_data_pred + (size_t)num_data_pred * p);
+    }
+    if (re_group_data_pred != nullptr) {   // num_data_pred x K NUL-terminated strings
+      const char* e = re_group_data_pred;
+      for (long k = 0; k < (long)num_data_pred * g->K(); ++k) e += std::strlen(e) + 1;
+      sp.re_group.assign(re_group_data_pred, e);
+    }
+    std::lock_guard<std::mutex> lk(g_saved_mu);
+    g_saved[handle] = std::move(sp);
+  }
+  if (g == nullptr) model(handle)->SetPredictionData(vecchia_pred_type, num_neighbors_pred, nsim_var_pred);
   API_END();
 }
 
@@ -316,7 +364,25 @@ int GPB_PredictREModel(REModelHandle handle, const double* y_data, int32_t num_d
                        const double* fixed_effects_pred) {
   API_BEGIN();
   if (out_predict == nullptr) gpb_amd::Fatal("out_predict is NULL");
-  if (use_saved_data) gpb_amd::Fatal("use_saved_data: saved prediction data is not supported by gpboost_amd");
+  SavedPred saved;
+  if (use_saved_data) {   // re_model_template.h:3168-3206: the saved data replaces the arguments
+    {
+      std::lock_guard<std::mutex> lk(g_saved_mu);
+      auto it = g_saved.find(handle);
+      if (it == g_saved.end() || it->second.num_data_pred <= 0)
+        gpb_amd::Fatal("No data has been set for making predictions. Call set_prediction_data first");
+      saved = it->second;
+    }
+    if (num_data_pred > 0 && num_data_pred != saved.num_data_pred)
+      gpb_amd::Fatal("num_data_pred (%d) differs from the saved prediction data (%d)", num_data_pred, saved.num_data_pred);
+    num_data_pred = saved.num_data_pred;
+    cluster_ids_data_pred = nullptr;
+    re_group_rand_coef_data_pred = nullptr;
+    gp_rand_coef_data_pred = nullptr;
+    re_group_data_pred = saved.re_group.empty() ? nullptr : saved.re_group.data();
+    gp_coords_data_pred = saved.gp_coords.empty() ? nullptr : saved.gp_coords.data();
+    covariate_data_pred = saved.covariates.empty() ? nullptr : saved.covariates.data();
+  }
   if (GroupedModel* g = as_grouped(handle)) {
     if (cluster_ids_data_pred != nullptr || re_group_rand_coef_data_pred != nullptr || gp_coords_data_pred != nullptr ||
         gp_rand_coef_data_pred != nullptr || covariate_data_pred != nullptr)

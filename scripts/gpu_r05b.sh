@@ -7,7 +7,7 @@ R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
 cd "$R"
 O=gpurun_out
 mkdir -p $O
-timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_fitc_laplace.py tests/test_gpu_fitc.py > $O/r05b_tests.log 2>&1 \
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_gpu_fitc_laplace.py tests/test_gpu_fitc.py tests/test_gpu_predict.py tests/test_gpu_grouped.py -k "fitc or saved" > $O/r05b_tests.log 2>&1 \
   || { tail -40 $O/r05b_tests.log; exit 1; }
 tail -3 $O/r05b_tests.log
 echo "n2 bench start"

@@ -56,6 +56,32 @@ def test_all_reference_entry_points_declared_and_exported(lib):
         assert hasattr(lib, f["name"]), f"{f['name']} not exported"
 
 
+def _declared_types():
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("make_capi_names",
+                                                  os.path.join(ROOT, "tests", "golden", "make_capi_names.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)   # defines param_type only (reads no reference file)
+    txt = open(HEADER).read()
+    out = {}
+    for m in re.finditer(r"GPBOOST_AMD_EXPORT\s+([\w\s\*]+?)\b((?:GPB|LGBM)_\w+)\s*\(([^;]*?)\)\s*;", txt, re.S):
+        args = [a for a in m.group(3).split(",") if a.strip() and a.strip() != "void"]
+        out[m.group(2)] = (m.group(1).strip(), [mod.param_type(a) for a in args])
+    return out
+
+
+def test_reference_entry_points_have_the_same_parameter_types():
+    """Type-level ABI check: every GPB_* entry point returns int and takes the reference's parameter
+    types in the reference's order (handles normalised to void*, as both headers typedef them)."""
+    import json
+    ref = json.load(open(os.path.join(ROOT, "tests", "golden", "reference_c_api.json")))["functions"]
+    decl = _declared_types()
+    for f in ref:
+        ret, types = decl[f["name"]]
+        assert ret == "int", (f["name"], ret)
+        assert types == f["types"], (f["name"], f"c_api.h:{f['line']}", types, f["types"])
+
+
 def test_library_exports_every_declared_symbol(lib):
     missing = [s for s in _declared_symbols() if not hasattr(lib, s)]
     assert not missing, missing

@@ -192,3 +192,18 @@ def test_grouped_predict_new_and_seen_levels():
         gm.predict(group_data_pred=g[:5], cov_pars=cp, predict_var=True)
     with pytest.raises(GPBoostError, match="not implemented for matrix_inversion_method_ == 'iterative'"):
         gm.predict_training_data_random_effects(predict_var=True)
+
+
+def test_grouped_predict_saved_data():
+    """set_prediction_data(group_data_pred=...) -> predict(use_saved_data=True) (reference basic.py
+    6095-6190, re_model_template.h:3081-3085, 3168-3206): the same means as passing the labels."""
+    g = synthetic.bench_groups(6000, (120, 15))
+    y = synthetic.bench_grouped_y(g)
+    gm = GPModel(group_data=g)
+    cp = [1.0, 0.8, 0.3]
+    gm.neg_log_likelihood(cp, y)
+    gn = np.vstack([g[:40], [[10_000, g[0, 1]], [77_777, 88_888]]])
+    direct = gm.predict(group_data_pred=gn, cov_pars=cp)
+    gm.set_prediction_data(group_data_pred=gn)
+    saved = gm.predict(cov_pars=cp, use_saved_data=True)
+    np.testing.assert_array_equal(saved["mu"], direct["mu"])

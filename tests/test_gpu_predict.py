@@ -274,3 +274,58 @@ def test_predict_dense_matches_reference(name):
         np.testing.assert_allclose(pred["cov"], c, rtol=1e-9, atol=1e-9 * np.abs(c).max())
     else:
         np.testing.assert_allclose(pred["var"], case["var"], rtol=1e-9)
+
+
+def test_predict_saved_data_sequence():
+    """The reference GPModel's set_prediction_data(gp_coords_pred=...) -> predict(use_saved_data=True)
+    sequence (python-package/gpboost/basic.py:6095-6190, 5940-6038; GPB_SetPredictionData /
+    GPB_PredictREModel(use_saved_data), re_model_template.h:3061-3119, 3168-3206): the saved coordinates
+    give the same numbers as passing them directly, bit for bit; without saved data the call fails."""
+    from gpboost_amd import GPBoostError, synthetic
+    n, n_pred = 2000, 300
+    X = synthetic.bench_coords(n + n_pred)
+    Xo, Xp = X[:n], X[n:]
+    y = synthetic.bench_gaussian_y(n)
+    cp = [0.2, 1.3, 0.15]
+    gm = _model(Xo, 30)
+    with pytest.raises(ValueError, match="set_prediction_data"):
+        gm.predict(y=y, cov_pars=cp, use_saved_data=True)
+    direct = gm.predict(y=y, gp_coords_pred=Xp, cov_pars=cp, predict_var=True)
+    gm.set_prediction_data(gp_coords_pred=Xp, num_neighbors_pred=60)
+    saved = gm.predict(y=y, cov_pars=cp, predict_var=True, use_saved_data=True)
+    np.testing.assert_array_equal(saved["mu"], direct["mu"])
+    np.testing.assert_array_equal(saved["var"], direct["var"])
+    # a later call without data keeps the saved coordinates (only the settings change)
+    gm.set_prediction_data(vecchia_pred_type="order_obs_first_cond_all")
+    ca = gm.predict(y=y, cov_pars=cp, predict_var=True, use_saved_data=True)
+    ca_direct = gm.predict(y=y, gp_coords_pred=Xp, cov_pars=cp, predict_var=True)
+    np.testing.assert_array_equal(ca["mu"], ca_direct["mu"])
+    assert np.max(np.abs(ca["var"] - saved["var"])) > 0.   # cond_all conditions on earlier prediction points
+    # the C ABI directly: a num_data_pred that disagrees with the saved data is an error
+    import ctypes
+    from gpboost_amd.basic import lib
+    out = np.zeros(2 * n_pred)
+    rc = lib().GPB_PredictREModel(gm.handle, None, ctypes.c_int32(n_pred + 1),
+                                  out.ctypes.data_as(ctypes.POINTER(ctypes.c_double)), ctypes.c_bool(False),
+                                  ctypes.c_bool(True), ctypes.c_bool(True), None, None, None, None, None,
+                                  (ctypes.c_double * 3)(*cp), None, ctypes.c_bool(True), None, None)
+    assert rc == -1 and b"saved" in lib().LGBM_GetLastError()
+    with pytest.raises(GPBoostError, match="random coefficients"):
+        gm.set_prediction_data(gp_rand_coef_data_pred=np.ones((n_pred, 1)))
+
+
+def test_predict_saved_data_covariates():
+    """Saved X_pred next to the coordinates: the linear predictor joins the mean as with direct data."""
+    from gpboost_amd import GPModel, synthetic
+    n, n_pred = 1500, 200
+    X = synthetic.bench_coords(n + n_pred)
+    Xo, Xp = X[:n], X[n:]
+    Z = np.column_stack([np.ones(n + n_pred), np.sin(4 * X[:, 0])])
+    y = synthetic.bench_gaussian_y(n) + Z[:n] @ np.array([0.5, -1.0])
+    gm = GPModel(gp_coords=Xo, cov_function="exponential", gp_approx="vecchia", num_neighbors=20, seed=0)
+    gm.fit(y, X=Z[:n])
+    direct = gm.predict(gp_coords_pred=Xp, X_pred=Z[n:], predict_var=True)
+    gm.set_prediction_data(gp_coords_pred=Xp, X_pred=Z[n:])
+    saved = gm.predict(predict_var=True, use_saved_data=True)
+    np.testing.assert_array_equal(saved["mu"], direct["mu"])
+    np.testing.assert_array_equal(saved["var"], direct["var"])
