@@ -568,6 +568,73 @@ def fitc_cpu_baseline() -> dict | None:
         os.unlink(path)
 
 
+def fitc_laplace_leg(steps: int, cpu: bool) -> dict:
+    """SURVEY §8 row f4, the Laplace rows: FITC with likelihood bernoulli_logit (FindModePostRandEffCalcMLLFITC
+    + CalcGradNegMargLikelihoodLaplaceApproxFITC) on the headline's n=100k coordinates, 500 kmeans++
+    inducing points: one approximate-marginal-likelihood + gradient evaluation from the zero mode per step
+    (the Newton iterations included); the reference on the box's cores at n=20000 beside it."""
+    import numpy as np
+
+    from gpboost_amd import GPModel, synthetic
+    X = synthetic.bench_coords(FITC_N)
+    y = synthetic.bench_bernoulli_y(X)
+    gm = GPModel(gp_coords=X, cov_function="exponential", gp_approx="fitc", num_ind_points=FITC_M,
+                 likelihood="bernoulli_logit", seed=0)
+    gm.neg_log_likelihood_and_grad(LATENT_PARS, y)   # warm-up
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        nll, g, _ = gm.neg_log_likelihood_and_grad(LATENT_PARS, None)
+        ts.append(time.perf_counter() - t0)
+    info = gm.last_iteration_info()
+    t = float(np.median(ts))
+    leg = {"metric": "FITC bernoulli_logit Laplace nll + grad evals/sec, n=100k, m=500", "value": 1.0 / t,
+           "unit": "evals/s", "steps": steps, "ms_per_step": t * 1e3,
+           "config": {"workload": "fitc_bernoulli_logit_laplace_cholesky", "n": FITC_N, "num_ind_points": FITC_M,
+                      "cov_function": "exponential", "cov_pars": LATENT_PARS, "nll": nll,
+                      "grad": [float(v) for v in g], "newton_its": int(info[0])},
+           "note": "per Newton step one split-K MFMA Gram K_mn diag(w) K_nm (2 m^2 n flops) + m x m POTRF/TRTRI + "
+                   "five matrix-vector passes over K_mn; gradient: three m^2 n GEMMs + three fused passes"}
+    del gm
+    if cpu:
+        leg["cpu_baseline"] = fitc_laplace_cpu_baseline()
+    return leg
+
+
+def fitc_laplace_cpu_baseline() -> dict | None:
+    """The reference's FITC bernoulli_logit evaluation (oracle/_ref/ref_harness) at n=20000, m=500 on this host;
+    `value_scaled_n100k` scales it by 20000/100000 (the unit is n m^2-bound)."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(harness):
+        return None
+    import numpy as np
+
+    from gpboost_amd import synthetic
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", str(os.cpu_count() or 1))), 16))
+    X = synthetic.bench_coords(FITC_CPU_N)
+    y = synthetic.bench_bernoulli_y(X)
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(np.array([X.shape[0], X.shape[1]], dtype=np.int32).tobytes())
+        f.write(np.ascontiguousarray(X.T).tobytes())
+        f.write(np.ascontiguousarray(y, dtype=np.float64).tobytes())
+        path = f.name
+    try:
+        out = subprocess.run([harness, path, "cov_fct=exponential", "gp_approx=fitc", f"num_ind_points={FITC_M}",
+                              "likelihood=bernoulli_logit", "mode=eval", "reps=1",
+                              "cov_pars=" + ",".join(map(str, LATENT_PARS))], capture_output=True, text=True,
+                             timeout=600, env=dict(os.environ, OMP_NUM_THREADS=str(threads)), check=True)
+        r = json.loads(out.stdout)
+        t = r["median_time"]
+        return {"value": 1.0 / t, "unit": "evals/s", "cores": threads, "kind": "reference", "nll": r["nll"],
+                "sample": f"1 FITC bernoulli_logit eval at n={FITC_CPU_N}, m={FITC_M} ({t:.2f} s; kmeans++ not timed)",
+                "value_scaled_n100k": (1.0 / t) * FITC_CPU_N / FITC_N}
+    except Exception as e:  # noqa: BLE001
+        sys.stderr.write(f"reference FITC-Laplace CPU baseline failed: {e}\n")
+        return None
+    finally:
+        os.unlink(path)
+
+
 def dense_cpu_baseline() -> dict | None:
     """The reference's dense path (oracle/_ref/ref_harness) on this host, bounded sample at
     n=4000; `value_scaled_n20000` scales it by (4000/20000)^3 (the unit is n^3-bound)."""
@@ -715,7 +782,9 @@ def spawn_ranks(world: int, argv: list[str]) -> int:
             break
         time.sleep(0.05)
     out0.seek(0)
-    sys.stdout.write(out0.read().decode())
+    for ln in out0.read().decode().splitlines():   # rank 0's JSON line only
+        if ln.startswith("{"):
+            sys.stdout.write(ln + "\n")
     sys.stdout.flush()
     bad = [(r, c) for r, c in enumerate(codes) if c]
     if bad:
@@ -739,7 +808,7 @@ def main():
     ap.add_argument("--no-fitc", action="store_true", help="skip the secondary FITC (§8 row f4) leg")
     ap.add_argument("--no-row-shards", action="store_true",
                     help="skip the per-rank row-range measurements (profiling the headline kernel alone)")
-    ap.add_argument("--only-fitc", action="store_true", help="run only the FITC leg (prints its JSON)")
+    ap.add_argument("--only-fitc", action="store_true", help="run only the FITC legs (prints their JSON)")
     args = ap.parse_args()
     launched = os.environ.get("WORLD_SIZE")
     if launched is not None and int(launched) != args.gpus:
@@ -751,7 +820,8 @@ def main():
         print(json.dumps(grouped_leg(args.steps, not args.no_cpu_baseline)))
         return
     if args.only_fitc:
-        print(json.dumps(fitc_leg(args.steps, not args.no_cpu_baseline)))
+        print(json.dumps({"fitc": fitc_leg(args.steps, not args.no_cpu_baseline),
+                          "fitc_laplace": fitc_laplace_leg(3, not args.no_cpu_baseline)}))
         return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -760,7 +830,13 @@ def main():
     os.environ["GPBOOST_AMD_DEVICE"] = "0" if host_transport() else str(local_rank)
 
     dist = None
+    json_out = sys.stdout
     if world > 1:
+        # the one-JSON-line contract: gloo / RCCL write status lines to fd 1 from C++; send fd 1 to stderr
+        # and keep the real stdout for the JSON line only
+        json_out = os.fdopen(os.dup(1), "w")
+        sys.stdout.flush()
+        os.dup2(2, 1)
         import torch.distributed as dist  # bootstrap + timing only (gloo); data path is RCCL in the library
         dist.init_process_group("gloo")
 
@@ -882,6 +958,7 @@ def main():
         line["grouped"] = grouped_leg(5, not args.no_cpu_baseline)
     if world == 1 and not args.no_fitc:
         line["fitc"] = fitc_leg(5, not args.no_cpu_baseline)
+        line["fitc_laplace"] = fitc_laplace_leg(3, not args.no_cpu_baseline)
     if world == 1 and not args.no_latent:
         del gm
         if os.environ.get("GPBOOST_AMD_DUMP_MAPS"):   # symbolising a crash under a tracer: the loaded libraries
@@ -891,7 +968,8 @@ def main():
         line["bernoulli_laplace"] = bernoulli_leg(X, args.latent_steps, not args.no_cpu_baseline)
     elif latent_sharded is not None:
         line["latent_iterative"] = latent_sharded
-    print(json.dumps(line))
+    print(json.dumps(line), file=json_out)
+    json_out.flush()
     if dist is not None:
         dist.destroy_process_group()
 
