@@ -56,7 +56,7 @@ def pmc_traffic(scale: float) -> dict | None:
     same command (profiles/<round>/pmc_rows.json: FETCH_SIZE + WRITE_SIZE, KB per dispatch;
     PMC counters cannot be read from inside the process)."""
     path = None
-    for rnd in ("r04", "r03", "r02", "r01"):   # the latest round's passes
+    for rnd in ("r05", "r04", "r03", "r02", "r01"):   # the latest round's passes
         cand = os.path.join(ROOT, "profiles", rnd, "pmc_rows.json")
         if os.path.exists(cand):
             path = cand
@@ -111,7 +111,7 @@ def cpu_baseline(X, Y, reps: int = 3) -> dict:
 
 def pmc_ops() -> dict | None:
     """The latest round's PMC summary of the operator / preconditioner kernels (scripts/pmc_ops_json.py)."""
-    for rnd in ("r03",):
+    for rnd in ("r05", "r04", "r03"):
         path = os.path.join(ROOT, "profiles", rnd, "pmc_ops.json")
         if os.path.exists(path):
             with open(path) as f:
