@@ -42,6 +42,11 @@ std::vector<double> fitc_inducing_points(const std::vector<double>& coords, int 
 // [sum Kinv o Kmm, sum Winv o Kmm, sum Kinv o dK, sum Winv o dK, a^T Kmm a, a^T dK a] (part: 6 (m + 3) / 4
 // doubles of scratch); K_mn (m x n, ld ldm) of the coordinates X (row-major n x d) and inducing points Z.
 void fitc_symv(hipStream_t s, const double* S, const double* x, int m, int ldm, double* out);
+// out = S^-1 x = Li^T (Li x) from the inverse Li of S's Cholesky factor (lower triangle read only; tmp: m
+// doubles). Two triangular products instead of one product with the explicit S^-1: the Cholesky-solve
+// accuracy (error ~ cond(L) eps rather than cond(S) eps), which the Laplace Newton iteration needs when
+// K_mm,s or the Woodbury matrix is ill-conditioned.
+void fitc_chol_solve(hipStream_t s, const double* Li, const double* x, int m, int ldm, double* tmp, double* out);
 void fitc_wsum(hipStream_t s, const double* P, int chunks, long stride, int m, int ldm, const double* Ks, double* W);
 void fitc_mm_terms(hipStream_t s, const double* Kinv, const double* Winv, const double* Kmm, const double* dK,
                    const double* a, int m, int ldm, double* part, double* out6);

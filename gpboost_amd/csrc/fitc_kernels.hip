@@ -170,6 +170,33 @@ __global__ void __launch_bounds__(256) fitc_symv_kernel(const double* __restrict
   if (lane == 0) out[j] = s;
 }
 
+// out = L x for the lower triangle of L (k <= j; entries above the diagonal are not read): 64 rows per
+// block (coalesced along a column), 4 interleaved k-slices per row summed in a fixed order
+__global__ void __launch_bounds__(256) fitc_trmv_lower_kernel(const double* __restrict__ L, const double* __restrict__ x,
+                                                              int m, int ldm, double* __restrict__ out) {
+  __shared__ double red[4][64];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
+  double s = 0.;
+  if (j < m)
+    for (int k = q; k <= j; k += 4) s += L[(size_t)j + (size_t)k * ldm] * x[k];
+  red[q][lane] = s;
+  __syncthreads();
+  if (q == 0 && j < m) out[j] = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+}
+
+// out = L^T t for the lower triangle of L: out_k = sum_{j >= k} L[j, k] t_j, one wave per k (contiguous column)
+__global__ void __launch_bounds__(256) fitc_trmv_lower_t_kernel(const double* __restrict__ L, const double* __restrict__ t,
+                                                                int m, int ldm, double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int k = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (k >= m) return;
+  double s = 0.;
+  for (int j = k + lane; j < m; j += 64) s += L[(size_t)j + (size_t)k * ldm] * t[j];
+  s = wave_sum(s);
+  if (lane == 0) out[k] = s;
+}
+
 // y_aux_i = y_i / d_i - (K_nm w)_i / d_i (re_model_template.h:8902-8907), block partial of y^T y_aux
 __global__ void __launch_bounds__(256) fitc_yaux_kernel(const double* __restrict__ Kmn, const double* __restrict__ w,
                                                         const double* __restrict__ y, const double* __restrict__ Dy,
@@ -939,6 +966,12 @@ void FitcSolver::Predict(int cov_type, double var, double phi, const double* d_y
 // ---- building blocks shared with the Laplace approximation (fitc_laplace.hip)
 void fitc_symv(hipStream_t s, const double* S, const double* x, int m, int ldm, double* out) {
   hipLaunchKernelGGL(fitc_symv_kernel, dim3((m + 3) / 4), dim3(256), 0, s, S, x, m, ldm, out);
+  HIP_CHECK(hipGetLastError());
+}
+
+void fitc_chol_solve(hipStream_t s, const double* Li, const double* x, int m, int ldm, double* tmp, double* out) {
+  hipLaunchKernelGGL(fitc_trmv_lower_kernel, dim3((m + 63) / 64), dim3(256), 0, s, Li, x, m, ldm, tmp);
+  hipLaunchKernelGGL(fitc_trmv_lower_t_kernel, dim3((m + 3) / 4), dim3(256), 0, s, Li, tmp, m, ldm, out);
   HIP_CHECK(hipGetLastError());
 }
 

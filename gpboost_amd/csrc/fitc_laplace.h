@@ -59,9 +59,9 @@ class FitcLaplace : public LatentSolverBase {
   void Gemv(const double* M, int nv, const double* const* x, double* const* out);
   // Sigma x = K_nm K_mm,s^-1 K_mn x + d o x (into out)
   void SigmaApply(const double* x, double* out);
-  // Woodbury matrix K_mm,s + K_mn diag(s) K_nm: Cholesky into W_, logdet, inverse into Winv_; false if
-  // not positive definite
-  void Woodbury(const double* s, double* logdet_dev);
+  // Woodbury matrix K_mm,s + K_mn diag(s) K_nm: Cholesky into W_, logdet, the factor's inverse into Wi_
+  // and (full_inverse) M^-1 into Winv_; a non-positive pivot is counted in F_->info_
+  void Woodbury(const double* s, double* logdet_dev, bool full_inverse);
 
   FitcSolver* F_;
   hipStream_t s_;

@@ -4,8 +4,12 @@
 //   M = K_mm,s + K diag(W DW) K^T                        split-K MFMA Gram (2 m^2 n) + POTRF / TRTRI
 //   Sigma rhs, K^T M^-1 K (W DW Sigma rhs), Sigma a      five matrix-vector passes over K
 //   Armijo line search on -1/2 a^T mode + sum log p(y | mode + F)
-// and for the gradient A = K_mm,s^-1 K, G = M^-1 K, dK_mm A (three MFMA GEMMs) and three fused passes
+// and for the gradient A = K_mm,s^-1 K, G = M^-1 K, dK_mm A (four MFMA GEMMs) and three fused passes
 // per observation (the range derivative of K recomputed from the coordinates).
+// Solves with K_mm,s and M apply the inverse Cholesky factor twice (L^-T (L^-1 x), fitc_chol_solve) rather
+// than an explicit inverse: Poisson / probit information makes M ill-conditioned enough (cond ~1e6..1e12)
+// that S^-1 x formed with the explicit S^-1 moves the Newton fixed point by ~cond(S) eps (measured 1e-7
+// relative in the nll against the reference's Cholesky solves; 1e-11 with the factor form).
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -93,7 +97,7 @@ __global__ void __launch_bounds__(kT) fl_prep_kernel(int n, int lik, const doubl
   d1[i] = g;
   double wi;
   if (w_update) {
-    wi = lik_info(lik, 1., l);
+    wi = lik_info(lik, 1., y[i], l);
     w[i] = wi;
   } else {
     wi = w[i];
@@ -250,7 +254,7 @@ __global__ void __launch_bounds__(kT) fl_final_kernel(int n, int lik, const doub
     const double mi = mode[i];
     const double l = off ? mi + off[i] : mi;
     d1[i] = lik_d1(lik, 1., y[i], l);
-    const double wi = lik_info(lik, 1., l);
+    const double wi = lik_info(lik, 1., y[i], l);
     w[i] = wi;
     const double di = dvec[i];
     DW[i] = 1. / (wi * di + 1.);
@@ -320,7 +324,8 @@ __global__ void __launch_bounds__(kT) fl_grad_p1_kernel(
     const double* __restrict__ u2v, const double* __restrict__ u3v, const double* __restrict__ u2r,
     const double* __restrict__ u3r, const double* __restrict__ avec, const double* __restrict__ g,
     const double* __restrict__ w, const double* __restrict__ DW, const double* __restrict__ dpwi,
-    const double* __restrict__ mode, const double* __restrict__ off, double* __restrict__ sgv,
+    const double* __restrict__ mode, const double* __restrict__ off, const double* __restrict__ y,
+    double* __restrict__ sgv,
     double* __restrict__ sgr, double* __restrict__ dmll, double* __restrict__ part) {
   __shared__ double red[4];
   const int lane = threadIdx.x & 63;
@@ -375,7 +380,7 @@ __global__ void __launch_bounds__(kT) fl_grad_p1_kernel(
       const double wi_inv = 1. / wi;
       const double sw = f * dw * dw + wi_inv - dw * wi_inv;   // diag of (Sigma^-1 + W)^-1 (:5447-5449)
       const double mi = mode[i];
-      dmll[i] = 0.5 * sw * lik_dinfo(lik, off ? mi + off[i] : mi);
+      dmll[i] = 0.5 * sw * lik_dinfo(lik, y[i], off ? mi + off[i] : mi);
     }
   }
   ev = block4(ev, red);
@@ -545,7 +550,7 @@ void FitcLaplace::SigmaApply(const double* x, double* out) {
   double* t1 = mv_.get();
   double* t2 = t1 + ldm_;
   Gemv(F_->Kmn_.get(), 1, &x, &t1);
-  fitc_symv(s_, F_->Kinv_.get(), t1, m_, ldm_, t2);
+  fitc_chol_solve(s_, F_->Li_.get(), t1, m_, ldm_, t1 + 4 * (size_t)ldm_, t2);
   hipLaunchKernelGGL(fl_coldot_kernel, dim3((n_ + 3) / 4), dim3(kT), 0, s_, F_->Kmn_.get(), t2, nullptr, n_, m_, ldm_,
                      c_.get(), nullptr);
   const double* dvec = F_->vec_.get();
@@ -553,7 +558,7 @@ void FitcLaplace::SigmaApply(const double* x, double* out) {
   HIP_CHECK(hipGetLastError());
 }
 
-void FitcLaplace::Woodbury(const double* s, double* logdet_dev) {
+void FitcLaplace::Woodbury(const double* s, double* logdet_dev, bool full_inverse) {
   FitcSolver& F = *F_;
   const int n = n_, m = m_, ldm = ldm_;
   hipLaunchKernelGGL(fl_colscale_kernel, dim3((m + 63) / 64, (n + 3) / 4), dim3(kT), 0, s_, F.Kmn_.get(), s, n, m, ldm,
@@ -566,7 +571,9 @@ void FitcLaplace::Woodbury(const double* s, double* logdet_dev) {
   chol_lower(s_, F.W_.get(), F.Wi_.get(), m, ldm, F.info_.get());
   launch_logdet_chol(s_, F.W_.get(), ldm, m, logdet_dev);
   trtri_lower(s_, F.W_.get(), F.Wi_.get(), F.T_.get(), 0, m, ldm);
-  gemm_f64(s_, m, m, m, 1., F.Wi_.get(), ldm, 1, F.Wi_.get(), ldm, 0, 0., F.Winv_.get(), ldm, 0, 0, 1, 1);
+  // M^-1 itself only for the gradient's trace terms (fitc_mm_terms)
+  if (full_inverse)
+    gemm_f64(s_, m, m, m, 1., F.Wi_.get(), ldm, 1, F.Wi_.get(), ldm, 0, 0., F.Winv_.get(), ldm, 0, 0, 1, 1);
 }
 
 LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, double /*aux*/, const IterativeConfig& cfg,
@@ -600,7 +607,7 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
     launch_sum_blocks(part_.get(), nbr, 2, red + 4, s_);
     HIP_CHECK(hipMemcpyAsync(h_red_ + 4, red + 4, 2 * sizeof(double), hipMemcpyDeviceToHost, s_));
     HIP_CHECK(hipStreamSynchronize(s_));
-    return -0.5 * h_red_[4] + h_red_[5];
+    return -0.5 * h_red_[4] + (h_red_[5] + loglik_const_);
   };
   LatentResult res;
   if (info_failed()) throw LatentNan("the inducing-point covariance is not positive definite (Cholesky failed)");
@@ -629,13 +636,13 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
       hipLaunchKernelGGL(fl_prep_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, lik, y_.get(), off, mode_.get(), dvec, 1,
                          d1_.get(), w_.get(), wdw_.get(), dw_.get(), rhs_.get());
       HIP_CHECK(hipGetLastError());
-      Woodbury(wdw_.get(), logdet_M);
+      Woodbury(wdw_.get(), logdet_M, false);
       // Sigma rhs, vaux = K (W DW Sigma rhs), vaux2 = M^-1 vaux, K^T vaux2 (likelihoods.h:3152-3157)
       SigmaApply(rhs_.get(), sig_.get());
       hipLaunchKernelGGL(fl_mul_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, wdw_.get(), sig_.get(), z_.get());
       const double* zp = z_.get();
       Gemv(F.Kmn_.get(), 1, &zp, &vaux);
-      fitc_symv(s_, F.Winv_.get(), vaux, m, ldm, vaux2);
+      fitc_chol_solve(s_, F.Wi_.get(), vaux, m, ldm, mv_.get() + 4 * (size_t)ldm, vaux2);
       hipLaunchKernelGGL(fl_coldot_kernel, dim3((n + 3) / 4), dim3(kT), 0, s_, F.Kmn_.get(), vaux2, nullptr, n, m, ldm,
                          c_.get(), nullptr);
       hipLaunchKernelGGL(fl_aupd_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, rhs_.get(), w_.get(), dw_.get(),
@@ -685,7 +692,7 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
                      w_.get(), dw_.get(), wdw_.get(), part_.get());
   HIP_CHECK(hipGetLastError());
   launch_sum_blocks(part_.get(), nbr, 3, red + 8, s_);
-  Woodbury(wdw_.get(), logdet_M);
+  Woodbury(wdw_.get(), logdet_M, want_grad || grad_f != nullptr);
   HIP_CHECK(hipMemcpyAsync(h_red_, red, 12 * sizeof(double), hipMemcpyDeviceToHost, s_));
   HIP_CHECK(hipStreamSynchronize(s_));
   if (h_red_[10] > 0.)
@@ -712,7 +719,9 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
     double* xr = mv + 15 * (size_t)ldm;
     // A = K_mm,s^-1 K = L^-T V (A_), G = M^-1 K (Kd_), M_r = dK_mm A (V_)
     gemm_f64(s_, m, n, m, 1., F.Li_.get(), ldm, 1, F.V_.get(), ldm, 0, 0., F.A_.get(), ldm, 0, 0, 1, 0);
-    gemm_f64(s_, m, n, m, 1., F.Winv_.get(), ldm, 0, F.Kmn_.get(), ldm, 0, 0., F.Kd_.get(), ldm);
+    // G = Lm^-T (Lm^-1 K) through V_ (free until M_r below): the Cholesky-solve accuracy (fitc_chol_solve)
+    gemm_f64(s_, m, n, m, 1., F.Wi_.get(), ldm, 0, F.Kmn_.get(), ldm, 0, 0., F.V_.get(), ldm, 0, 1, 0, 0);
+    gemm_f64(s_, m, n, m, 1., F.Wi_.get(), ldm, 1, F.V_.get(), ldm, 0, 0., F.Kd_.get(), ldm, 0, 0, 1, 0);
     gemm_f64(s_, m, n, m, 1., F.dKmm_.get(), ldm, 0, F.A_.get(), ldm, 0, 0., F.V_.get(), ldm);
     const int nbg = (n + kChunk - 1) / kChunk;
     dispatch_cov(cov_type, [&](auto c) {
@@ -731,7 +740,7 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
     dispatch_cov(cov_type, [&](auto c) {
       hipLaunchKernelGGL((fl_grad_p1_kernel<decltype(c)::value>), dim3(nb4), dim3(kT), 0, s_, F.d_X_, F.dZ_.get(), n, m, d,
                          ldm, lik, var, phi, delta_j, F.Kmn_.get(), F.A_.get(), F.Kd_.get(), F.V_.get(), b, u1, u2v, u3v,
-                         u2r, u3r, a_.get(), d1_.get(), w_.get(), dw_.get(), wdw_.get(), mode_.get(), off, sgv_.get(),
+                         u2r, u3r, a_.get(), d1_.get(), w_.get(), dw_.get(), wdw_.get(), mode_.get(), off, y_.get(), sgv_.get(),
                          sgr_.get(), dmll_.get(), part1);
     });
     HIP_CHECK(hipGetLastError());
@@ -742,8 +751,8 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
     const double* zx[2] = {z_.get(), rhs_.get()};
     double* zo[2] = {rv, rr};
     Gemv(F.Kmn_.get(), 2, zx, zo);
-    fitc_symv(s_, F.Winv_.get(), rv, m, ldm, xv);
-    fitc_symv(s_, F.Winv_.get(), rr, m, ldm, xr);
+    fitc_chol_solve(s_, F.Wi_.get(), rv, m, ldm, mv + 4 * (size_t)ldm, xv);
+    fitc_chol_solve(s_, F.Wi_.get(), rr, m, ldm, mv + 4 * (size_t)ldm, xr);
     hipLaunchKernelGGL(fl_grad_p3_kernel, dim3(nb4), dim3(kT), 0, s_, F.Kmn_.get(), n, m, ldm, xv, xr, sgv_.get(),
                        sgr_.get(), w_.get(), wdw_.get(), dmll_.get(), part1);
     HIP_CHECK(hipGetLastError());
@@ -754,7 +763,7 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
       hipLaunchKernelGGL(fl_mul_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, dw_.get(), dmll_.get(), z_.get());
       const double* zp = z_.get();
       Gemv(F.Kmn_.get(), 1, &zp, &q);
-      fitc_symv(s_, F.Winv_.get(), q, m, ldm, q2);
+      fitc_chol_solve(s_, F.Wi_.get(), q, m, ldm, mv + 4 * (size_t)ldm, q2);
       hipLaunchKernelGGL(fl_coldot_kernel, dim3(nb4), dim3(kT), 0, s_, F.Kmn_.get(), q2, nullptr, n, m, ldm, c_.get(),
                          nullptr);
       hipLaunchKernelGGL(fl_gradf_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, d1_.get(), dmll_.get(), w_.get(),
@@ -790,7 +799,7 @@ void FitcLaplace::Predict(int cov_type, double var, double phi, const double* Xp
   double* t2 = t1 + ldm;
   const double* g = d1_.get();
   Gemv(F.Kmn_.get(), 1, &g, &t1);
-  fitc_symv(s_, F.Kinv_.get(), t1, m, ldm, t2);
+  fitc_chol_solve(s_, F.Li_.get(), t1, m, ldm, t1 + 4 * (size_t)ldm, t2);
   const int nb4 = (np + 3) / 4;
   hipLaunchKernelGGL(fl_coldot_kernel, dim3(nb4), dim3(kT), 0, s_, Kmp.get(), t2, nullptr, np, m, ldm, out.get(), nullptr);
   HIP_CHECK(hipGetLastError());

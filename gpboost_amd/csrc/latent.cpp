@@ -669,6 +669,7 @@ void LatentVecchia::Scalars(const ScalarArgs& a, double* out) {
   HIP_CHECK(hipMemcpyAsync(h_out_, d_out_.get(), sizeof(double) * kLatentScalars, hipMemcpyDeviceToHost, s_));
   HIP_CHECK(hipStreamSynchronize(s_));
   std::copy(h_out_, h_out_ + kLatentScalars, out);
+  out[kSqLogLik] += loglik_const_;   // log_normalizing_constant_ (likelihoods.h:8638)
 }
 
 // Spin until the device's stopping check `seq` has landed in the host-coherent words (it is
@@ -1023,6 +1024,7 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
       md.n = n; md.m = m_; md.t = tw; md.lik = lik; md.nbr = d_nbr_.get(); md.Bv = d_Bv_.get(); md.dw = d_dw_.get();
       md.loc = d_mode_.get(); md.U = d_U_.get(); md.P = d_P_.get(); md.dmll = d_dmll_.get();
       md.offset = has_off_ && !has_obs_ ? d_off_.get() : nullptr;
+      md.y = has_obs_ ? nullptr : d_y_.get();
       md.obs = Obs();
       md.t_valid = tl; md.t_all = t;
       if (coll_ == nullptr) {

@@ -75,6 +75,12 @@ class LatentSolverBase {
                             ModeStart start = ModeStart::kZero) = 0;
   virtual void ResetModeToPrevious() = 0;
   virtual void ClearModePrevious() = 0;
+  // the log-likelihood's normalizing constant (e.g. -sum log y! for poisson, CalculateLogNormalizingConstant
+  // likelihoods.h:8290-8310), part of the mode-finding objective and of the marginal likelihood
+  void SetLogLikConst(double c) { loglik_const_ = c; }
+
+ protected:
+  double loglik_const_ = 0.;
 };
 
 class LatentVecchia : public LatentSolverBase {

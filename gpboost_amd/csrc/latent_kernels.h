@@ -305,7 +305,7 @@ void launch_axpby(size_t count, double alpha, const double* X, double beta, cons
                   hipStream_t s);
 
 // ---- likelihood-specific elementwise and reductions
-enum LatentLik : int { kLikGaussian = 0, kLikBernoulliLogit = 1 };
+enum LatentLik : int { kLikGaussian = 0, kLikBernoulliLogit = 1, kLikBernoulliProbit = 2, kLikPoisson = 3 };
 
 // Observations of the latent variables when coordinates repeat (the reference's unique-location
 // form: Z maps n observations to the n_u latent variables, Vecchia_utils.cpp:1121-1139,
@@ -403,6 +403,7 @@ struct ModeDerivArgs {
   const double* dw;
   const double* loc;
   const double* offset;        // nullable: third derivative at loc + F
+  const double* y;             // response (the probit information depends on it)
   ObsMap obs;
   const double* U;
   const double* P;

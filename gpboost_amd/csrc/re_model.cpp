@@ -16,6 +16,17 @@
 
 namespace gpb_amd {
 
+// likelihood names of the Laplace paths (likelihoods.h:12656 SUPPORTED_LIKELIHOODS_, the subset built here)
+int parse_likelihood(const std::string& name) {
+  if (name == "gaussian") return kLikGaussian;
+  if (name == "bernoulli_logit") return kLikBernoulliLogit;
+  if (name == "bernoulli_probit") return kLikBernoulliProbit;
+  if (name == "poisson") return kLikPoisson;
+  Fatal("likelihood '%s' is not supported by gpboost_amd (supported: gaussian, bernoulli_logit, bernoulli_probit, poisson)",
+        name.c_str());
+  return -1;
+}
+
 namespace {
 
 int parse_cov(const std::string& name, double shape) {
@@ -57,9 +68,7 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
   if (cfg_.d <= 0 || cfg_.d > 3) Fatal("dim_gp_coords = %d not supported (1..3)", cfg_.d);
   cfg_.cov_type = parse_cov(cfg_.cov_fct, cfg_.shape);
   // likelihood and approximation (re_model_template.h:207-211, 563; likelihoods.h:240-257)
-  if (cfg_.likelihood == "gaussian") cfg_.lik = kLikGaussian;
-  else if (cfg_.likelihood == "bernoulli_logit") cfg_.lik = kLikBernoulliLogit;
-  else Fatal("likelihood '%s' is not supported by gpboost_amd (supported: gaussian, bernoulli_logit)", cfg_.likelihood.c_str());
+  cfg_.lik = parse_likelihood(cfg_.likelihood);
   if (cfg_.gp_approx == "vecchia_latent") {
     vecchia_ = true;
     cfg_.latent = true;
@@ -185,6 +194,7 @@ void REModelAMD::EnsureStructure() {
       latent_.reset(new LatentVecchia(nu_, cfg_.d, cfg_.num_neighbors, d_X_.get(), nbr_.data(), stream_));
       if (has_dup()) latent_->SetObservations(obs_row_);
       latent_->SetShard(rank_, world_, coll_.get());   // probe columns over the ranks (§8e Option A)
+      latent_->SetLogLikConst(loglik_const_);
       if (y_set_) latent_->SetY(y_vo_.data());
       latent_->SetOffset(has_offset_ ? offset_vo_.data() : nullptr);
     }
@@ -368,9 +378,9 @@ void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred,
   else if ((int)last_cov_pars_.size() == ncp) std::copy(last_cov_pars_.begin(), last_cov_pars_.end(), cp);
   else Fatal("cov_pars must be provided (no previous evaluation)");
   if (latent) {
-    if (predict_cov_mat && predict_response && cfg_.lik == kLikBernoulliLogit)
-      Fatal("predictive covariance matrices of the response are not supported for likelihood 'bernoulli_logit' by "
-            "gpboost_amd (use predict_response = false or predict_var)");
+    if (predict_cov_mat && predict_response && cfg_.lik != kLikGaussian)
+      Fatal("predictive covariance matrices of the response are not supported for likelihood '%s' by "
+            "gpboost_amd (use predict_response = false or predict_var)", cfg_.likelihood.c_str());
     // the mode at these parameters, found from zero (re_model.cpp:967-977 -> CalcCovFactorOrModeAndNegLL)
     EvalLatent(cp, false);
   }
@@ -468,19 +478,9 @@ void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred,
     latent_->PredVarSim(nsim_var_pred_, iter.num_rand_vec_trace, iter.cg_delta_conv, iter.cg_max_num_it,
                         pred_seed_++, n_pred, mp, nb.data(), dB.get(), acc.data());
     for (int p = 0; p < n_pred; ++p) h[n_pred + p] += acc[p] / nsim_var_pred_;
-    if (predict_response && cfg_.lik == kLikBernoulliLogit) {
-      // PredictResponse (likelihoods.h:7544-7556): adaptive Gauss-Hermite response means, p (1 - p)
-      static const std::vector<double> gh = gauss_hermite_adaptive(30);   // order_GH_ = 30 (:12877)
-      DevBuf<double> dmv((size_t)2 * n_pred), dgh(gh.size());
-      HIP_CHECK(hipMemcpyAsync(dmv.get(), h.data(), sizeof(double) * 2 * n_pred, hipMemcpyHostToDevice, stream_));
-      HIP_CHECK(hipMemcpyAsync(dgh.get(), gh.data(), sizeof(double) * gh.size(), hipMemcpyHostToDevice, stream_));
-      launch_resp_logit(n_pred, dmv.get(), dmv.get() + n_pred, dgh.get(), dgh.get() + 30, 30, iter.delta_conv_mode_finding,
-                        dout.get(), dout.get() + n_pred, stream_);
-      HIP_CHECK(hipMemcpyAsync(h.data(), dout.get(), sizeof(double) * h.size(), hipMemcpyDeviceToHost, stream_));
-      HIP_CHECK(hipStreamSynchronize(stream_));
+    if (predict_response) {
+      ResponseTransform(n_pred, h.data(), h.data() + n_pred, nullptr);
       std::copy(h.begin(), h.begin() + n_pred, out);
-    } else if (predict_response) {   // gaussian vecchia_latent: + the error variance (PredictResponse)
-      for (int p = 0; p < n_pred; ++p) h[n_pred + p] += aux_pars_.empty() ? 0. : aux_pars_[0];
     }
   }
   if (predict_cov_mat && cond_all) {
@@ -544,23 +544,7 @@ void REModelAMD::PredictLatentSim(int n, int n_pred, int mp, const std::vector<i
     latent_pred_moments(stream_, n_pred, cond_all ? Bp.data() : nullptr, D.data(), dV.get(), nsim, want_var,
                         predict_cov_mat, var.data(), cov.data());
   }
-  if (predict_response && cfg_.lik == kLikBernoulliLogit) {
-    static const std::vector<double> gh = gauss_hermite_adaptive(30);   // order_GH_ = 30 (likelihoods.h:12877)
-    DevBuf<double> dmv((size_t)2 * n_pred), dgh(gh.size()), dout((size_t)2 * n_pred);
-    HIP_CHECK(hipMemcpyAsync(dmv.get(), mean.data(), sizeof(double) * n_pred, hipMemcpyHostToDevice, stream_));
-    HIP_CHECK(hipMemcpyAsync(dmv.get() + n_pred, var.data(), sizeof(double) * n_pred, hipMemcpyHostToDevice, stream_));
-    HIP_CHECK(hipMemcpyAsync(dgh.get(), gh.data(), sizeof(double) * gh.size(), hipMemcpyHostToDevice, stream_));
-    launch_resp_logit(n_pred, dmv.get(), dmv.get() + n_pred, dgh.get(), dgh.get() + 30, 30, iter.delta_conv_mode_finding,
-                      dout.get(), dout.get() + n_pred, stream_);
-    HIP_CHECK(hipMemcpyAsync(mean.data(), dout.get(), sizeof(double) * n_pred, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipMemcpyAsync(var.data(), dout.get() + n_pred, sizeof(double) * n_pred, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
-  } else if (predict_response) {   // gaussian vecchia_latent: + the error variance (PredictResponse)
-    const double aux = aux_pars_.empty() ? 0. : aux_pars_[0];
-    for (int p = 0; p < n_pred; ++p) var[p] += aux;
-    if (predict_cov_mat)
-      for (int p = 0; p < n_pred; ++p) cov[(size_t)p * n_pred + p] += aux;
-  }
+  if (predict_response) ResponseTransform(n_pred, mean.data(), var.data(), predict_cov_mat ? cov.data() : nullptr);
   std::copy(mean.begin(), mean.end(), out);
   if (predict_cov_mat) std::copy(cov.begin(), cov.end(), out + n_pred);
   else if (predict_var) std::copy(var.begin(), var.end(), out + n_pred);
@@ -676,6 +660,40 @@ void REModelAMD::PredictFitc(const double* y, int n_pred, const double* coords_p
   }
 }
 
+// PredictResponse (likelihoods.h:7526-7580) on the latent predictive mean / variance (n_pred each, in place):
+// bernoulli_logit by the adaptive Gauss-Hermite rule on the GPU, bernoulli_probit / poisson in closed form,
+// gaussian (vecchia_latent) + the error variance (also on the covariance diagonal, cov nullable).
+void REModelAMD::ResponseTransform(int n_pred, double* mean, double* var, double* cov) {
+  if (cfg_.lik == kLikBernoulliLogit) {
+    static const std::vector<double> gh = gauss_hermite_adaptive(30);   // order_GH_ = 30 (likelihoods.h:12877)
+    DevBuf<double> dmv((size_t)2 * n_pred), dgh(gh.size()), dout((size_t)2 * n_pred);
+    HIP_CHECK(hipMemcpyAsync(dmv.get(), mean, sizeof(double) * n_pred, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipMemcpyAsync(dmv.get() + n_pred, var, sizeof(double) * n_pred, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipMemcpyAsync(dgh.get(), gh.data(), sizeof(double) * gh.size(), hipMemcpyHostToDevice, stream_));
+    launch_resp_logit(n_pred, dmv.get(), dmv.get() + n_pred, dgh.get(), dgh.get() + 30, 30, iter.delta_conv_mode_finding,
+                      dout.get(), dout.get() + n_pred, stream_);
+    HIP_CHECK(hipMemcpyAsync(mean, dout.get(), sizeof(double) * n_pred, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipMemcpyAsync(var, dout.get() + n_pred, sizeof(double) * n_pred, hipMemcpyDeviceToHost, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  } else if (cfg_.lik == kLikBernoulliProbit) {   // :7531-7543
+    for (int p = 0; p < n_pred; ++p) {
+      mean[p] = 0.5 * std::erfc(-(mean[p] / std::sqrt(1. + var[p])) * M_SQRT1_2);
+      var[p] = mean[p] * (1. - mean[p]);
+    }
+  } else if (cfg_.lik == kLikPoisson) {   // :7557-7569
+    for (int p = 0; p < n_pred; ++p) {
+      const double pm = std::exp(mean[p] + 0.5 * var[p]);
+      var[p] = pm * ((std::exp(var[p]) - 1.) * pm + 1.);
+      mean[p] = pm;
+    }
+  } else {   // gaussian vecchia_latent: + the error variance
+    const double aux = aux_pars_.empty() ? 0. : aux_pars_[0];
+    for (int p = 0; p < n_pred; ++p) var[p] += aux;
+    if (cov != nullptr)
+      for (int p = 0; p < n_pred; ++p) cov[(size_t)p * n_pred + p] += aux;
+  }
+}
+
 // FITC with a Laplace likelihood (CalcPredFITC_FSA, re_model_template.h:10600-10760, then
 // PredictLaplaceApproxFITC, likelihoods.h:7157-7232): the mode at the parameters (found from zero, as
 // the Vecchia latent path), then latent means / variances / covariance (FitcLaplace::Predict), the
@@ -706,18 +724,7 @@ void REModelAMD::PredictFitcLaplace(const double* y, int n_pred, const double* c
                      predict_cov_mat, mean.data(), var.data(), cov.data());
   if (mean_add != nullptr)
     for (int p = 0; p < n_pred; ++p) mean[p] += mean_add[p];
-  if (predict_response && cfg_.lik == kLikBernoulliLogit) {
-    static const std::vector<double> gh = gauss_hermite_adaptive(30);   // order_GH_ = 30 (likelihoods.h:12877)
-    DevBuf<double> dmv((size_t)2 * n_pred), dgh(gh.size()), dout((size_t)2 * n_pred);
-    HIP_CHECK(hipMemcpyAsync(dmv.get(), mean.data(), sizeof(double) * n_pred, hipMemcpyHostToDevice, stream_));
-    HIP_CHECK(hipMemcpyAsync(dmv.get() + n_pred, var.data(), sizeof(double) * n_pred, hipMemcpyHostToDevice, stream_));
-    HIP_CHECK(hipMemcpyAsync(dgh.get(), gh.data(), sizeof(double) * gh.size(), hipMemcpyHostToDevice, stream_));
-    launch_resp_logit(n_pred, dmv.get(), dmv.get() + n_pred, dgh.get(), dgh.get() + 30, 30, iter.delta_conv_mode_finding,
-                      dout.get(), dout.get() + n_pred, stream_);
-    HIP_CHECK(hipMemcpyAsync(mean.data(), dout.get(), sizeof(double) * n_pred, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipMemcpyAsync(var.data(), dout.get() + n_pred, sizeof(double) * n_pred, hipMemcpyDeviceToHost, stream_));
-    HIP_CHECK(hipStreamSynchronize(stream_));
-  }
+  if (predict_response) ResponseTransform(n_pred, mean.data(), var.data(), nullptr);
   std::copy(mean.begin(), mean.end(), out);
   if (predict_cov_mat) std::copy(cov.begin(), cov.end(), out + n_pred);
   else if (predict_var) std::copy(var.begin(), var.end(), out + n_pred);
@@ -998,12 +1005,26 @@ void REModelAMD::SetY(const double* y) {
   if (vecchia_) for (int i = 0; i < n; ++i) yv[i] = y[perm_[i]];
   else std::copy(y, y + n, yv.begin());
   if (cfg_.latent) {
-    if (cfg_.lik == kLikBernoulliLogit) {   // likelihoods.h CheckY: binary labels
+    double lognorm = 0.;   // CheckY (likelihoods.h:637-737), CalculateLogNormalizingConstant (:8290-8310)
+    if (cfg_.lik == kLikBernoulliLogit || cfg_.lik == kLikBernoulliProbit) {
       for (int i = 0; i < n; ++i)
-        if (yv[i] != 0. && yv[i] != 1.) Fatal("Response variable (label) data needs to be 0 or 1 for likelihood = 'bernoulli_logit' ");
+        if (yv[i] != 0. && yv[i] != 1.)
+          Fatal("The response variable ('y') needs to be 0 or 1 for likelihood = '%s' ", cfg_.likelihood.c_str());
+    } else if (cfg_.lik == kLikPoisson) {
+      for (int i = 0; i < n; ++i) {
+        if (yv[i] < 0.) Fatal(" Must have y >= 0 for the response variable ('y') for likelihood = 'poisson', found %g ", yv[i]);
+        double ip;
+        if (std::modf(yv[i], &ip) != 0.)
+          Fatal("Found non-integer response variable ('y'). Response variable can only be integer valued for likelihood = 'poisson' ");
+        for (int k = 2; k <= (int)yv[i]; ++k) lognorm -= std::log((double)k);   // LogNormalizingConstantPoissonOneSample
+      }
     }
+    loglik_const_ = lognorm;
     y_vo_ = yv;
-    if (lat()) lat()->SetY(y_vo_.data());
+    if (lat()) {
+      lat()->SetLogLikConst(loglik_const_);
+      lat()->SetY(y_vo_.data());
+    }
   }
   d_y_.alloc(n);
   HIP_CHECK(hipMemcpyAsync(d_y_.get(), yv.data(), sizeof(double) * n, hipMemcpyHostToDevice, stream_));

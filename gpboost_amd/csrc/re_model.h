@@ -46,6 +46,7 @@ struct ModelConfig {
   int lik = 0;             // LatentLik code when latent
 };
 
+int parse_likelihood(const std::string& name);   // LatentLik code
 // cov_fcts.h:438-460: range rho -> phi on the transformed scale
 double range_trafo(int cov_type, double rho);
 // cov_fcts.h TransformBackCovPars: range transform phi -> range rho
@@ -225,6 +226,7 @@ class REModelAMD {
   void PredictFitc(const double* y, int n_pred, const double* coords_pred, const double* cov_pars, bool predict_cov_mat,
                    bool predict_var, bool predict_response, double* out, const double* mean_add);
   std::vector<int> FitcMatch(const std::vector<double>& xp_rowmajor, int n_pred) const;
+  void ResponseTransform(int n_pred, double* mean, double* var, double* cov);
   void PredictFitcLaplace(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,
                           bool predict_cov_mat, bool predict_var, bool predict_response, double* out,
                           const double* mean_add);
@@ -280,6 +282,7 @@ class REModelAMD {
   }
   std::vector<double> y_vo_;          // host copy (Vecchia order) for the latent solver
   std::vector<double> aux_pars_;
+  double loglik_const_ = 0.;          // the latent likelihood's normalizing constant at the current y
   double last_iter_info_[4] = {0., 0., 0., 0.};
   int test_nan_count_ = 0;   // latent evaluations seen by the GPBOOST_AMD_TEST_NAN_EVAL fault injection
 

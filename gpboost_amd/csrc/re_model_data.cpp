@@ -330,10 +330,7 @@ void REModelAMD::SetLikelihood(const std::string& likelihood) {
     Fatal("Cannot change likelihood after a model has been estimated ");
   ModelConfig c = cfg_;
   c.likelihood = likelihood;
-  int lik = -1;
-  if (likelihood == "gaussian") lik = kLikGaussian;
-  else if (likelihood == "bernoulli_logit") lik = kLikBernoulliLogit;
-  else Fatal("likelihood '%s' is not supported by gpboost_amd (supported: gaussian, bernoulli_logit)", likelihood.c_str());
+  const int lik = parse_likelihood(likelihood);
   const bool latent = c.gp_approx == "vecchia_latent" || ((vecchia_ || fitc_) && lik != kLikGaussian);
   if (!vecchia_ && !fitc_ && lik != kLikGaussian)
     Fatal("likelihood '%s' requires gp_approx = 'vecchia' or 'fitc' in gpboost_amd (dense Laplace is out of scope)",

@@ -1118,14 +1118,14 @@ __device__ __forceinline__ void obs_d1_info(const ObsMap& ob, int lik, double au
   if (ob.ptr == nullptr) {
     const double l = offset ? mi + offset[i] : mi;
     d1 = lik_d1(lik, aux, y[i], l);
-    if (want_info) w = lik_info(lik, aux, l);
+    if (want_info) w = lik_info(lik, aux, y[i], l);
     return;
   }
   double s1 = 0., sw = 0.;
   for (int e = ob.ptr[i]; e < ob.ptr[i + 1]; ++e) {
     const double l = ob.offset ? mi + ob.offset[e] : mi;
     s1 += lik_d1(lik, aux, ob.y[e], l);
-    if (want_info) sw += lik_info(lik, aux, l);
+    if (want_info) sw += lik_info(lik, aux, ob.y[e], l);
   }
   d1 = s1;
   if (want_info) w = sw;
@@ -1277,11 +1277,11 @@ __global__ void __launch_bounds__(kBT) mode_deriv_kernel(ModeDerivArgs a, int sh
     const double* bv = a.Bv + (size_t)i * a.m;
     double dWi;
     if (a.obs.ptr == nullptr) {
-      dWi = lik_dinfo(a.lik, a.offset ? a.loc[i] + a.offset[i] : a.loc[i]);
+      dWi = lik_dinfo(a.lik, a.y ? a.y[i] : 0., a.offset ? a.loc[i] + a.offset[i] : a.loc[i]);
     } else {   // Z^T dW: the row's observations
       dWi = 0.;
       for (int e = a.obs.ptr[i]; e < a.obs.ptr[i + 1]; ++e)
-        dWi += lik_dinfo(a.lik, a.obs.offset ? a.loc[i] + a.obs.offset[e] : a.loc[i]);
+        dWi += lik_dinfo(a.lik, a.obs.y[e], a.obs.offset ? a.loc[i] + a.obs.offset[e] : a.loc[i]);
     }
     // pass 1: row means of z1 = U dW P and zP = (BP)^2 dW over the t probes
     // (c_var == 0 -> c = 1, CG_utils.cpp:1036-1039).

@@ -63,6 +63,31 @@ def rtest_bernoulli_probit_y(n: int = 100) -> tuple[np.ndarray, np.ndarray]:
     return coords, y
 
 
+def _rtest_field(n: int = 100) -> tuple[np.ndarray, np.ndarray]:
+    from scipy.stats import norm
+
+    coords = rtest_coords(n)
+    diff = coords[:, None, :] - coords[None, :, :]
+    dist = np.sqrt((diff ** 2).sum(-1))
+    chol = np.linalg.cholesky(np.exp(-dist / 0.1) + np.eye(n) * 1e-20)
+    return coords, chol @ norm.ppf(sim_rand_unif(n, 0.8))
+
+
+def rtest_poisson_y(n: int = 100) -> tuple[np.ndarray, np.ndarray]:
+    """R non-Gaussian test data, spatial Poisson case (test_GPModel_non_Gaussian_data.R:2386-2387):
+    y = qpois(sim_rand_unif(n, 0.435), exp(L b_1))."""
+    from scipy.stats import poisson
+
+    coords, eps = _rtest_field(n)
+    return coords, poisson.ppf(sim_rand_unif(n, 0.435), np.exp(eps)).astype(np.float64)
+
+
+def rtest_probit_X(n: int = 100) -> np.ndarray:
+    """X <- cbind(rep(1,n), sin((1:n-n/2)^2*2*pi/n)) (test_GPModel_non_Gaussian_data.R:60)."""
+    i = np.arange(1, n + 1, dtype=np.float64)
+    return np.column_stack([np.ones(n), np.sin((i - n / 2) ** 2 * 2 * np.pi / n)])
+
+
 def lcg_unif(n: int, init_c: float = 0.1) -> np.ndarray:
     """The same LCG in exact integer arithmetic, u_{k+1} = (22695477 u_k + 1) mod 2^32.
     The R tests' double-arithmetic version (sim_rand_unif) rounds 22695477 u_k once it exceeds 2^53
@@ -106,6 +131,24 @@ def bench_bernoulli_y(coords: np.ndarray) -> np.ndarray:
     n = coords.shape[0]
     p = 0.5 * (1.0 + np.sin(2 * np.pi * coords[:, 0]) * np.cos(2 * np.pi * coords[:, 1]))
     return (lcg_unif(n, 0.19341) < p).astype(np.float64)
+
+
+def bench_poisson_y(coords: np.ndarray) -> np.ndarray:
+    """Counts with log-rate 0.5 + sin(2 pi x1) cos(2 pi x2), drawn by inversion of the Poisson CDF
+    at u from LCG c=0.27183 (exact arithmetic)."""
+    n = coords.shape[0]
+    lam = np.exp(0.5 + np.sin(2 * np.pi * coords[:, 0]) * np.cos(2 * np.pi * coords[:, 1]))
+    u = lcg_unif(n, 0.27183)
+    k = np.zeros(n)
+    p = np.exp(-lam)
+    cdf = p.copy()
+    active = u > cdf
+    while active.any():
+        k[active] += 1.0
+        p[active] *= lam[active] / k[active]
+        cdf[active] += p[active]
+        active &= u > cdf
+    return k
 
 
 def bench_spatial_gaussian_y(coords: np.ndarray) -> np.ndarray:

@@ -1,7 +1,8 @@
 """ORACLE TEST INFRASTRUCTURE — NOT PART OF THE PRODUCT.
 
 CPU restatement (numpy) of the reference's FITC approximation with a Laplace likelihood
-(gp_approx = "fitc", likelihood = "bernoulli_logit", matrix_inversion_method = "cholesky"), the checker
+(gp_approx = "fitc", likelihood = "bernoulli_logit" | "bernoulli_probit" | "poisson",
+matrix_inversion_method = "cholesky"), the checker
 of gpboost_amd's FitcLaplace (csrc/fitc_laplace.hip). Importable only from tests/. Follows, step for
 step and with the reference's own factorizations (Cholesky solves, not explicit inverses):
   CalcSigmaComps                          re_model_template.h:7341-7378 (fitc_resid_diag, no nugget)
@@ -10,6 +11,8 @@ step and with the reference's own factorizations (Cholesky solves, not explicit 
   CalcGradNegMargLikelihoodLaplaceApproxFITC  likelihoods.h:5397-5593 (cov_grad, fixed_effect_grad)
   CalcPredFITC_FSA + PredictLaplaceApproxFITC re_model_template.h:10600-10760, likelihoods.h:7157-7232
   bernoulli_logit log-likelihood / derivatives likelihoods.h:8724, 9226, 9896, 10187 (DF_utils.h:37-60)
+  bernoulli_probit :8708, 9208, 9871, 10171 (here through scipy's log_ndtr);  poisson :8730, 9230, 9904,
+  10200 with the normalizing constant -sum log y! (CalculateAuxQuantLogNormalizingConstant)
   covariance functions and log-range derivatives cov_fcts.h:1681-1786, 2116-2143 (transformed scale)
 The inducing points are an input (the reference's own, from the fixtures; their selection is pinned by
 test_oracle_fitc.py / test_gpu_fitc.py).
@@ -18,6 +21,7 @@ from __future__ import annotations
 
 import numpy as np
 from scipy.linalg import cho_factor, cho_solve, solve_triangular
+from scipy.special import gammaln, log_ndtr
 
 JITTER = 1.0 + 1e-6   # JITTER_MULT_IP_FITC_FSA (utils.h:39)
 
@@ -54,13 +58,32 @@ def _sigmoid(x):
     return out
 
 
-def _loglik(y, l):
-    return float(np.sum(y * l - (np.log1p(np.exp(-np.abs(l))) + np.maximum(l, 0.))))
+def _lik(lik, y, l):
+    """(sum of log-likelihoods, first derivative, information, d information / d l) per sample."""
+    if lik == "bernoulli_logit":
+        p = _sigmoid(l)
+        ll = float(np.sum(y * l - (np.log1p(np.exp(-np.abs(l))) + np.maximum(l, 0.))))
+        return ll, y - p, p * (1. - p), -p * (1. - p) * (2. * p - 1.)
+    if lik == "poisson":
+        e = np.exp(l)
+        return float(np.sum(y * l - e)), y - e, e, e
+    if lik != "bernoulli_probit":
+        raise ValueError(lik)
+    s = 2. * y - 1.                       # log Phi(s l); d/dl = s r, r = phi(s l) / Phi(s l)
+    x = s * l
+    lc = log_ndtr(x)
+    r = np.exp(-0.5 * x * x - 0.5 * np.log(2. * np.pi) - lc)
+    d1 = s * r
+    w = r * (x + r)                       # -d2/dl2 log Phi(s l)
+    dinfo = -s * r * (x * x - 1. + r * (3. * x + 2. * r))
+    return float(lc.sum()), d1, w, dinfo
 
 
 class FitcLaplaceOracle:
-    def __init__(self, X, y, Z, cov_type, var, phi, fixed_effects=None):
+    def __init__(self, X, y, Z, cov_type, var, phi, fixed_effects=None, likelihood="bernoulli_logit"):
         self.X, self.y, self.Z = np.asarray(X, float), np.asarray(y, float), np.asarray(Z, float)
+        self.lik = likelihood
+        self.const = -float(gammaln(self.y + 1.).sum()) if likelihood == "poisson" else 0.
         self.ct, self.var, self.phi = cov_type, var, phi
         self.F = np.zeros(len(y)) if fixed_effects is None else np.asarray(fixed_effects, float)
         K, dK = cov_dcov(_dist(self.X, self.Z), var, phi, cov_type)          # n x m (cross_cov)
@@ -77,20 +100,20 @@ class FitcLaplaceOracle:
         self.d = var * JITTER - (V * V).sum(0)                                 # fitc_resid_diag (no nugget)
         self.logdet_Ks_half = float(np.log(np.diag(self.cKs[0])).sum())
 
+    def _ll(self, mode):
+        return _lik(self.lik, self.y, mode + self.F)[0] + self.const
+
     def sigma(self, x):   # K (K_mm,s^-1 (K^T x)) + d o x (likelihoods.h:3153-3154)
         return self.K @ cho_solve(self.cKs, self.K.T @ x) + self.d * x
 
-    def find_mode(self, delta=1e-8, mode=None, a=None):
+    def find_mode(self, delta=1e-8, mode=None, a=None, maxit=1000):
         n = len(self.y)
         K, d, y = self.K, self.d, self.y
         mode = np.zeros(n) if mode is None else mode.copy()
         a = np.zeros(n) if a is None else a.copy()
-        obj = -0.5 * a.dot(mode) + _loglik(y, mode + self.F)
-        for it in range(1000):
-            l = mode + self.F
-            p = _sigmoid(l)
-            g = y - p
-            w = p * (1. - p)
+        obj = -0.5 * a.dot(mode) + self._ll(mode)
+        for it in range(maxit):
+            _, g, w, _ = _lik(self.lik, y, mode + self.F)
             ws = np.sqrt(w)
             DW = 1. / (w * d + 1.)
             wdw = ws * ws * DW
@@ -111,7 +134,7 @@ class FitcLaplaceOracle:
                 else:
                     a_new = (1 - lr) * a + lr * a_upd
                     m_new = (1 - lr) * mode + lr * m_upd
-                obj_new = -0.5 * a_new.dot(m_new) + _loglik(y, m_new + self.F)
+                obj_new = -0.5 * a_new.dot(m_new) + self._ll(m_new)
                 if obj_new < obj + 1e-4 * lr * gdd or not np.isfinite(obj_new):
                     lr *= 0.5
                 else:
@@ -125,10 +148,7 @@ class FitcLaplaceOracle:
                 break
         self.mode, self.a, self.obj, self.newton_its = mode, a, obj, it + 1
         # after the mode finding (:3200-3232)
-        l = mode + self.F
-        p = _sigmoid(l)
-        self.g = y - p
-        self.w = p * (1. - p)
+        _, self.g, self.w, self.dinfo = _lik(self.lik, y, mode + self.F)
         self.dpwi = 1. / (d + 1. / self.w)
         self.cM = cho_factor(self.Ks + K.T @ (self.dpwi[:, None] * K), lower=True)
         mll = obj - np.log(np.diag(self.cM[0])).sum() + self.logdet_Ks_half + 0.5 * np.log(self.dpwi).sum() \
@@ -140,9 +160,7 @@ class FitcLaplaceOracle:
         """[d/dlog sigma1^2, d/dlog phi] of the negative approximate marginal log-likelihood (and the
         gradient wrt F) at the mode (likelihoods.h:5397-5593)."""
         K, d, w, g, a = self.K, self.d, self.w, self.g, self.a
-        l = self.mode + self.F
-        p = _sigmoid(l)
-        dinfo = -p * (1. - p) * (2. * p - 1.)
+        dinfo = self.dinfo
         WI = 1. / w
         DW = 1. / (w * d + 1.)
         Linv_KT_DW = solve_triangular(self.cM[0], K.T * DW[None, :], lower=True)

@@ -45,6 +45,17 @@ def golden_latent():
         return json.load(f)
 
 
+def lik_case_data(case):
+    """Inputs of a golden_latent_lik.json case (bernoulli_probit / poisson; make_golden_latent_lik.py)."""
+    from gpboost_amd import synthetic
+    if case["data"] == "rtest_probit":
+        return synthetic.rtest_bernoulli_probit_y(case["n"])
+    if case["data"] == "rtest_poisson":
+        return synthetic.rtest_poisson_y(case["n"])
+    X = synthetic.bench_coords(case["n"])
+    return X, (synthetic.bench_poisson_y(X) if case["data"] == "bench_pois" else synthetic.bench_bernoulli_y(X))
+
+
 def latent_case_data(case):
     """Inputs of a golden_latent.json case (regenerated from the portable LCG generators)."""
     from gpboost_amd import synthetic

@@ -15,6 +15,7 @@ import pytest
 from gpboost_amd import synthetic
 from oracle import oracle as O
 from oracle.fitc_laplace_oracle import FitcLaplaceOracle
+from conftest import lik_case_data
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 with open(os.path.join(HERE, "golden", "golden_fitc_laplace.json")) as _f:
@@ -84,3 +85,50 @@ def test_oracle_fitc_laplace_predict(name):
         np.testing.assert_allclose(out["cov"], np.asarray(case["cov"]).reshape(npred, npred), rtol=1e-9, atol=1e-12)
     else:
         np.testing.assert_allclose(out["var"], case["var"], rtol=1e-9, atol=1e-12)
+
+
+# ---- bernoulli_probit and poisson (tests/golden/golden_latent_lik.json, make_golden_latent_lik.py) ----
+with open(os.path.join(HERE, "golden", "golden_latent_lik.json")) as _f:
+    GOLDEN_LIK = json.load(_f)
+
+
+def _lik_setup(case, fe=None, ind_points=None):
+    X, y = lik_case_data(case)
+    sp = case["spec"]
+    Z = np.array(ind_points if ind_points is not None else case["ind_points"]).reshape(case["m"], -1)
+    ct = O.cov_code(sp["cov_fct"], float(sp["shape"]))
+    tr = O.transform_latent(ct, case["cov_pars"])
+    return X, FitcLaplaceOracle(X, y, Z, ct, tr[0], tr[1], fixed_effects=fe, likelihood=case["likelihood"])
+
+
+@pytest.mark.parametrize("name", [k for k in GOLDEN_LIK if GOLDEN_LIK[k]["kind"] == "fitc"])
+def test_oracle_fitc_laplace_likelihoods_match_reference(name):
+    case = GOLDEN_LIK[name]
+    _, orc = _lik_setup(case)
+    nll = orc.find_mode()
+    assert abs(nll - case["nll"]) <= 1e-10 * abs(case["nll"]), (nll, case["nll"])
+    np.testing.assert_allclose(orc.gradient()["grad"], case["grad"], rtol=1e-7)
+
+
+@pytest.mark.parametrize("name", [k for k in GOLDEN_LIK if GOLDEN_LIK[k]["kind"] == "fitc_gradf"])
+def test_oracle_fitc_laplace_likelihoods_gradient_f(name):
+    case = GOLDEN_LIK[name]
+    X = synthetic.bench_coords(case["n"])
+    fe = 0.3 * np.sin(3.0 * X[:, 0]) - 0.2
+    _, orc = _lik_setup(case, fe=fe)
+    nll = orc.find_mode()
+    assert abs(nll - case["nll"]) <= 1e-10 * abs(case["nll"])
+    out = orc.gradient(want_f=True)
+    np.testing.assert_allclose(out["grad"], case["grad"], rtol=1e-7)
+    ref = np.asarray(case["grad_f"])
+    assert np.max(np.abs(out["grad_f"] - ref)) <= 1e-9 * np.max(np.abs(ref))
+
+
+def test_rtest_generators_match_r_goldens():
+    """The R tests' data regenerated here give the R tests' hard-coded nll values through the reference's
+    dense path (test_GPModel_non_Gaussian_data.R:1196 probit, :2410 poisson; TOLERANCE_STRICT = 1e-6)."""
+    for k in ("rtest_dense_probit", "rtest_dense_pois"):
+        c = GOLDEN_LIK[k]
+        assert abs(c["nll"] - c["r_expected_nll"]) <= 1e-6, (k, c["nll"], c["r_expected_nll"])
+    _, y = synthetic.rtest_poisson_y(100)
+    assert np.all(y >= 0) and np.all(y == np.round(y)) and y.sum() > 0
