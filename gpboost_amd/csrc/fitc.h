@@ -42,11 +42,18 @@ std::vector<double> fitc_inducing_points(const std::vector<double>& coords, int 
 // [sum Kinv o Kmm, sum Winv o Kmm, sum Kinv o dK, sum Winv o dK, a^T Kmm a, a^T dK a] (part: 6 (m + 3) / 4
 // doubles of scratch); K_mn (m x n, ld ldm) of the coordinates X (row-major n x d) and inducing points Z.
 void fitc_symv(hipStream_t s, const double* S, const double* x, int m, int ldm, double* out);
-// out = S^-1 x = Li^T (Li x) from the inverse Li of S's Cholesky factor (lower triangle read only; tmp: m
-// doubles). Two triangular products instead of one product with the explicit S^-1: the Cholesky-solve
-// accuracy (error ~ cond(L) eps rather than cond(S) eps), which the Laplace Newton iteration needs when
-// K_mm,s or the Woodbury matrix is ill-conditioned.
-void fitc_chol_solve(hipStream_t s, const double* Li, const double* x, int m, int ldm, double* tmp, double* out);
+// out = S^-1 x = Li^T (Li x) from the inverse Li of S's Cholesky factor (lower triangle read only) and its
+// transpose LiT (fitc_lower_t; tmp: m doubles). Two triangular products instead of one product with the
+// explicit S^-1: the Cholesky-solve accuracy (error ~ cond(L) eps rather than cond(S) eps), which the
+// Laplace Newton iteration needs when K_mm,s or the Woodbury matrix is ill-conditioned.
+void fitc_chol_solve(hipStream_t s, const double* Li, const double* LiT, const double* x, int m, int ldm, double* tmp,
+                     double* out);
+// LT = transpose of the lower triangle of L (zeros above the diagonal)
+void fitc_lower_t(hipStream_t s, const double* L, int m, int ldm, double* LT);
+// out = S^-1 K_mn (m x n, ld ldm) with the explicit Sinv (one full MFMA GEMM), or Li^T (Li K_mn) through tmp
+// (two triangle-masked GEMMs) when GPBOOST_AMD_FITC_G=tri (A/B: same gradients, slower; fitc_kernels.hip)
+void fitc_solve_kmn(hipStream_t s, const double* Li, const double* Sinv, const double* Kmn, int m, int n, int ldm,
+                    double* tmp, double* out);
 void fitc_wsum(hipStream_t s, const double* P, int chunks, long stride, int m, int ldm, const double* Ks, double* W);
 void fitc_mm_terms(hipStream_t s, const double* Kinv, const double* Winv, const double* Kmm, const double* dK,
                    const double* a, int m, int ldm, double* part, double* out6);
@@ -90,6 +97,7 @@ class FitcSolver {
   DevBuf<double> dZ_;
   DevBuf<double> Kmn_, V_, Kd_, A_;        // m x n (ldm)
   DevBuf<double> Kmm_, Ks_, Li_, W_, Wi_, Kinv_, Winv_, dKmm_, T_;   // m x m (ldm)
+  DevBuf<double> LiT_, WiT_;                                         // transposed inverse factors
   DevBuf<double> part_, vec_, red_;
   DevBuf<int> info_;
   double* h_red_ = nullptr;

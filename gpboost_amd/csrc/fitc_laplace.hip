@@ -4,7 +4,7 @@
 //   M = K_mm,s + K diag(W DW) K^T                        split-K MFMA Gram (2 m^2 n) + POTRF / TRTRI
 //   Sigma rhs, K^T M^-1 K (W DW Sigma rhs), Sigma a      five matrix-vector passes over K
 //   Armijo line search on -1/2 a^T mode + sum log p(y | mode + F)
-// and for the gradient A = K_mm,s^-1 K, G = M^-1 K, dK_mm A (four MFMA GEMMs) and three fused passes
+// and for the gradient A = K_mm,s^-1 K, G = M^-1 K, dK_mm A (three MFMA GEMMs) and three fused passes
 // per observation (the range derivative of K recomputed from the coordinates).
 // Solves with K_mm,s and M apply the inverse Cholesky factor twice (L^-T (L^-1 x), fitc_chol_solve) rather
 // than an explicit inverse: Poisson / probit information makes M ill-conditioned enough (cond ~1e6..1e12)
@@ -550,7 +550,7 @@ void FitcLaplace::SigmaApply(const double* x, double* out) {
   double* t1 = mv_.get();
   double* t2 = t1 + ldm_;
   Gemv(F_->Kmn_.get(), 1, &x, &t1);
-  fitc_chol_solve(s_, F_->Li_.get(), t1, m_, ldm_, t1 + 4 * (size_t)ldm_, t2);
+  fitc_chol_solve(s_, F_->Li_.get(), F_->LiT_.get(), t1, m_, ldm_, t1 + 4 * (size_t)ldm_, t2);
   hipLaunchKernelGGL(fl_coldot_kernel, dim3((n_ + 3) / 4), dim3(kT), 0, s_, F_->Kmn_.get(), t2, nullptr, n_, m_, ldm_,
                      c_.get(), nullptr);
   const double* dvec = F_->vec_.get();
@@ -571,6 +571,7 @@ void FitcLaplace::Woodbury(const double* s, double* logdet_dev, bool full_invers
   chol_lower(s_, F.W_.get(), F.Wi_.get(), m, ldm, F.info_.get());
   launch_logdet_chol(s_, F.W_.get(), ldm, m, logdet_dev);
   trtri_lower(s_, F.W_.get(), F.Wi_.get(), F.T_.get(), 0, m, ldm);
+  fitc_lower_t(s_, F.Wi_.get(), m, ldm, F.WiT_.get());
   // M^-1 itself only for the gradient's trace terms (fitc_mm_terms)
   if (full_inverse)
     gemm_f64(s_, m, m, m, 1., F.Wi_.get(), ldm, 1, F.Wi_.get(), ldm, 0, 0., F.Winv_.get(), ldm, 0, 0, 1, 1);
@@ -642,7 +643,7 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
       hipLaunchKernelGGL(fl_mul_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, wdw_.get(), sig_.get(), z_.get());
       const double* zp = z_.get();
       Gemv(F.Kmn_.get(), 1, &zp, &vaux);
-      fitc_chol_solve(s_, F.Wi_.get(), vaux, m, ldm, mv_.get() + 4 * (size_t)ldm, vaux2);
+      fitc_chol_solve(s_, F.Wi_.get(), F.WiT_.get(), vaux, m, ldm, mv_.get() + 4 * (size_t)ldm, vaux2);
       hipLaunchKernelGGL(fl_coldot_kernel, dim3((n + 3) / 4), dim3(kT), 0, s_, F.Kmn_.get(), vaux2, nullptr, n, m, ldm,
                          c_.get(), nullptr);
       hipLaunchKernelGGL(fl_aupd_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, rhs_.get(), w_.get(), dw_.get(),
@@ -719,9 +720,8 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
     double* xr = mv + 15 * (size_t)ldm;
     // A = K_mm,s^-1 K = L^-T V (A_), G = M^-1 K (Kd_), M_r = dK_mm A (V_)
     gemm_f64(s_, m, n, m, 1., F.Li_.get(), ldm, 1, F.V_.get(), ldm, 0, 0., F.A_.get(), ldm, 0, 0, 1, 0);
-    // G = Lm^-T (Lm^-1 K) through V_ (free until M_r below): the Cholesky-solve accuracy (fitc_chol_solve)
-    gemm_f64(s_, m, n, m, 1., F.Wi_.get(), ldm, 0, F.Kmn_.get(), ldm, 0, 0., F.V_.get(), ldm, 0, 1, 0, 0);
-    gemm_f64(s_, m, n, m, 1., F.Wi_.get(), ldm, 1, F.V_.get(), ldm, 0, 0., F.Kd_.get(), ldm, 0, 0, 1, 0);
+    // G = M^-1 K (fitc_solve_kmn; V_ is scratch until M_r below)
+    fitc_solve_kmn(s_, F.Wi_.get(), F.Winv_.get(), F.Kmn_.get(), m, n, ldm, F.V_.get(), F.Kd_.get());
     gemm_f64(s_, m, n, m, 1., F.dKmm_.get(), ldm, 0, F.A_.get(), ldm, 0, 0., F.V_.get(), ldm);
     const int nbg = (n + kChunk - 1) / kChunk;
     dispatch_cov(cov_type, [&](auto c) {
@@ -751,8 +751,8 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
     const double* zx[2] = {z_.get(), rhs_.get()};
     double* zo[2] = {rv, rr};
     Gemv(F.Kmn_.get(), 2, zx, zo);
-    fitc_chol_solve(s_, F.Wi_.get(), rv, m, ldm, mv + 4 * (size_t)ldm, xv);
-    fitc_chol_solve(s_, F.Wi_.get(), rr, m, ldm, mv + 4 * (size_t)ldm, xr);
+    fitc_chol_solve(s_, F.Wi_.get(), F.WiT_.get(), rv, m, ldm, mv + 4 * (size_t)ldm, xv);
+    fitc_chol_solve(s_, F.Wi_.get(), F.WiT_.get(), rr, m, ldm, mv + 4 * (size_t)ldm, xr);
     hipLaunchKernelGGL(fl_grad_p3_kernel, dim3(nb4), dim3(kT), 0, s_, F.Kmn_.get(), n, m, ldm, xv, xr, sgv_.get(),
                        sgr_.get(), w_.get(), wdw_.get(), dmll_.get(), part1);
     HIP_CHECK(hipGetLastError());
@@ -763,7 +763,7 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
       hipLaunchKernelGGL(fl_mul_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, dw_.get(), dmll_.get(), z_.get());
       const double* zp = z_.get();
       Gemv(F.Kmn_.get(), 1, &zp, &q);
-      fitc_chol_solve(s_, F.Wi_.get(), q, m, ldm, mv + 4 * (size_t)ldm, q2);
+      fitc_chol_solve(s_, F.Wi_.get(), F.WiT_.get(), q, m, ldm, mv + 4 * (size_t)ldm, q2);
       hipLaunchKernelGGL(fl_coldot_kernel, dim3(nb4), dim3(kT), 0, s_, F.Kmn_.get(), q2, nullptr, n, m, ldm, c_.get(),
                          nullptr);
       hipLaunchKernelGGL(fl_gradf_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, d1_.get(), dmll_.get(), w_.get(),
@@ -799,7 +799,7 @@ void FitcLaplace::Predict(int cov_type, double var, double phi, const double* Xp
   double* t2 = t1 + ldm;
   const double* g = d1_.get();
   Gemv(F.Kmn_.get(), 1, &g, &t1);
-  fitc_chol_solve(s_, F.Li_.get(), t1, m, ldm, t1 + 4 * (size_t)ldm, t2);
+  fitc_chol_solve(s_, F.Li_.get(), F.LiT_.get(), t1, m, ldm, t1 + 4 * (size_t)ldm, t2);
   const int nb4 = (np + 3) / 4;
   hipLaunchKernelGGL(fl_coldot_kernel, dim3(nb4), dim3(kT), 0, s_, Kmp.get(), t2, nullptr, np, m, ldm, out.get(), nullptr);
   HIP_CHECK(hipGetLastError());
