@@ -48,10 +48,13 @@ void fwd(const std::vector<double>& L, int k, double* b) {
 
 extern "C" {
 
-// method 0 = kmeans++, 1 = random. coords row-major n x d; Z row-major m x d.
-int orc_fitc_inducing_points(const double* x, int n, int d, int m, int method, int seed, double* Z) {
+}  // extern "C"
+
+namespace {
+
+// the selection with the caller's generator (CreateREComponentsFITC_FSA continues the model's rng_)
+int inducing_points(const double* x, int n, int d, int m, int method, std::mt19937& gen, double* Z) {
   if (m > n || m < 1) return -1;
-  std::mt19937 gen((std::mt19937::result_type)seed);
   if (method == 1) {
     std::vector<int> idx;
     for (int r = n - m; r < n; ++r) {
@@ -111,6 +114,32 @@ int orc_fitc_inducing_points(const double* x, int n, int d, int m, int method, i
   } while (mu != old && mu != old_old && it != max_it);
   std::copy(mu.begin(), mu.end(), Z);
   return it;
+}
+
+}  // namespace
+
+extern "C" {
+
+// method 0 = kmeans++, 1 = random. coords row-major n x d; Z row-major m x d.
+int orc_fitc_inducing_points(const double* x, int n, int d, int m, int method, int seed, double* Z) {
+  std::mt19937 gen((std::mt19937::result_type)seed);
+  return inducing_points(x, n, d, m, method, gen, Z);
+}
+
+// full_scale_vecchia (re_model_template.h:348-357): the model's rng_ = mt19937(seed) first shuffles the
+// data order (random ordering), then CreateREComponentsFITC_FSA selects the inducing points on the
+// coordinates in that order with the same generator. perm (n) receives the order.
+int orc_vif_inducing_points(const double* x, int n, int d, int m, int method, int seed, int shuffle, double* Z,
+                            int* perm) {
+  std::mt19937 gen((std::mt19937::result_type)seed);
+  std::vector<int> idx(n);
+  for (int i = 0; i < n; ++i) idx[i] = i;
+  if (shuffle) std::shuffle(idx.begin(), idx.end(), gen);
+  std::vector<double> xv((size_t)n * d);
+  for (int i = 0; i < n; ++i)
+    for (int q = 0; q < d; ++q) xv[(size_t)i * d + q] = x[(size_t)idx[i] * d + q];
+  std::copy(idx.begin(), idx.end(), perm);
+  return inducing_points(xv.data(), n, d, m, method, gen, Z);
 }
 
 // FITC nll + gradient on the transformed scale pars = (sigma2, sigma1^2 / sigma2, phi); mode 0:

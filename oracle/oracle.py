@@ -52,6 +52,8 @@ def lib():
                                                    ctypes.c_int, ctypes.c_double, ctypes.c_int, ctypes.c_int,
                                                    ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_int, D, D, D]
         L.orc_fitc_inducing_points.argtypes = [D, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, D]
+        L.orc_vif_inducing_points.argtypes = [D, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int, D, I]
         L.orc_fitc_nll_grad.argtypes = [D, D, ctypes.c_int, ctypes.c_int, D, ctypes.c_int, ctypes.c_int, D, ctypes.c_int,
                                         D, D, D]
         _lib = L
@@ -241,6 +243,20 @@ def fitc_inducing_points(coords, m: int, method: str = "kmeans++", seed: int = 0
     if its < 0:
         raise ValueError("invalid number of inducing points")
     return Z, its
+
+
+def vif_inducing_points(coords, m: int, method: str = "kmeans++", seed: int = 0, shuffle: bool = True):
+    """full_scale_vecchia: the ordering shuffle, then the inducing points on the coordinates in that order
+    with the same generator (re_model_template.h:348-357). Returns (perm, Z, Lloyd iterations)."""
+    x = np.ascontiguousarray(coords, dtype=np.float64)
+    n, d = x.shape
+    Z = np.zeros((m, d))
+    perm = np.zeros(n, dtype=np.int32)
+    its = lib().orc_vif_inducing_points(_d(x), n, d, m, 0 if method == "kmeans++" else 1, seed, int(shuffle), _d(Z),
+                                        _i(perm))
+    if its < 0:
+        raise ValueError("invalid number of inducing points")
+    return perm, Z, its
 
 
 def fitc_nll_grad(coords, y, Z, cov_type, pars_trafo, mode):

@@ -444,7 +444,8 @@ int main(int argc, char** argv) {
   if (gauss && gp_approx == "vecchia") {
     std::printf("\"yTPsiInvy\": %.17g, \"log_det_Psi\": %.17g,\n", m->yTPsiInvy_, m->log_det_Psi_);
   }
-  if (gp_approx == "fitc") {
+  const bool vif = gp_approx == "full_scale_vecchia" || gp_approx == "vif";
+  if (gp_approx == "fitc" || vif) {
     if (gauss) std::printf("\"yTPsiInvy\": %.17g, \"log_det_Psi\": %.17g,\n", m->yTPsiInvy_, m->log_det_Psi_);
     const den_mat_t& ip = m->gp_coords_ip_mat_;
     std::vector<double> ipv((size_t)ip.rows() * ip.cols());
@@ -452,7 +453,7 @@ int main(int argc, char** argv) {
       for (int q = 0; q < (int)ip.cols(); ++q) ipv[(size_t)i * ip.cols() + q] = ip(i, q);
     print_vec("ind_points", ipv.data(), (int)ipv.size());
   }
-  if ((gp_approx == "vecchia" || gp_approx == "vecchia_latent") && dump_nn) {
+  if ((gp_approx == "vecchia" || gp_approx == "vecchia_latent" || vif) && dump_nn) {
     const auto& perm = m->data_indices_per_cluster_[m->unique_clusters_[0]];
     std::printf("\"perm\": [");
     for (size_t i = 0; i < perm.size(); ++i) std::printf("%s%d", i ? "," : "", perm[i]);

@@ -1,0 +1,109 @@
+"""ORACLE TEST INFRASTRUCTURE — NOT PART OF THE PRODUCT.
+
+CPU restatement (numpy, dense algebra) of the reference's full-scale Vecchia approximation ("VIF",
+gp_approx = "full_scale_vecchia" / "vif") for the Gaussian likelihood, the checker of gpboost_amd's
+VifSolver (csrc/vif.h). Importable only from tests/. Transformed scale: pars = (sigma^2, sigma1^2 / sigma^2,
+phi), nugget 1 inside Psi. Follows the reference:
+  ordering + inducing points      re_model_template.h:348-357 (shuffle, then CreateREComponentsFITC_FSA with the
+                                  same generator; oracle.vif_inducing_points)
+  Sigma components                re_model_template.h:7341-7378 (K_mm,s = K_mm diag * (1 + 1e-6), chol_ip_cross_cov)
+  residual Vecchia factor          Vecchia_utils.cpp:1388-1617 (CalcCovFactorGradientVecchia, full_scale_vecchia
+                                  branches: residual covariances among the neighbours, B, D and their derivatives)
+  Psi = K K_mm,s^-1 K^T + B^-1 D B^-T   (CalcCovFactorFITC_FSA :8770-8880, log det :2698-2714)
+The nll and gradient are formed densely from Psi and dPsi_k (with the reference's derivative conventions:
+the un-jittered dK_mm, B_grad, D_grad of the row factor), an algebra independent of the reference's
+Woodbury formulas (re_model_template.h:1985-2232); pinned to the reference by tests/test_oracle_vif.py.
+"""
+from __future__ import annotations
+
+import numpy as np
+from scipy.linalg import cho_factor, cho_solve, solve_triangular
+
+from oracle.fitc_laplace_oracle import JITTER, cov_dcov, _dist
+
+
+def vif_factor(xv, nb, Z, cov_type, var, phi):
+    """Residual Vecchia factor on the transformed scale: B (n x n unit lower), D (n) and per parameter
+    (log var, log phi) dB, dD; plus the low-rank pieces K (n x m), K_mm, dK_mm, K_mm,s."""
+    xv = np.asarray(xv, float)
+    n = xv.shape[0]
+    K, dKr = cov_dcov(_dist(xv, Z), var, phi, cov_type)
+    Kmm, dKmmr = cov_dcov(_dist(Z, Z), var, phi, cov_type)
+    np.fill_diagonal(Kmm, var)
+    np.fill_diagonal(dKmmr, 0.)
+    Ks = Kmm.copy()
+    Ks[np.diag_indices_from(Ks)] *= JITTER
+    cKs = cho_factor(Ks, lower=True)
+    A = cho_solve(cKs, K.T)                                # sigma_ip_inv_cross_cov_T (m x n)
+    V = solve_triangular(cKs[0], K.T, lower=True)          # chol_ip_cross_cov = L^-1 K^T
+    dK = [K, dKr]                                          # d cross_cov / dlog var, dlog phi
+    dKmm = [Kmm, dKmmr]                                    # un-jittered (GetZSigmaZtGrad)
+    dKA = [dKmm[p] @ A for p in range(2)]                  # sigma_ip_grad_sigma_ip_inv_cross_cov_T
+    B = np.eye(n)
+    D = np.zeros(n)
+    dB = [np.zeros((n, n)), np.zeros((n, n))]
+    dD = [np.zeros(n), np.zeros(n)]
+    for i in range(n):
+        k = min(i, nb.shape[1])
+        N = nb[i, :k]
+        D[i] = 1. + var - V[:, i] @ V[:, i]
+        for p in range(2):   # D_grad init (var on the transformed scale), minus the low-rank part's derivative
+            dD[p][i] = (var if p == 0 else 0.) - A[:, i] @ (2. * dK[p][i] - dKA[p][:, i])
+        if k == 0:
+            continue
+        xs = xv[N]
+        cnn, dcnn = cov_dcov(_dist(xs, xs), var, phi, cov_type)
+        np.fill_diagonal(cnn, var)
+        np.fill_diagonal(dcnn, 0.)
+        cni, dcni = cov_dcov(_dist(xs, xv[i:i + 1])[:, 0], var, phi, cov_type)
+        C = cnn + np.eye(k) - V[:, N].T @ V[:, N]
+        c = cni - V[:, N].T @ V[:, i]
+        cC = cho_factor(C, lower=True)
+        a = cho_solve(cC, c)
+        B[i, N] = -a
+        D[i] -= a @ c
+        for p in range(2):
+            base_nn = cnn if p == 0 else dcnn
+            base_ni = cni if p == 0 else dcni
+            # Vecchia_utils.cpp:1445-1462: d(residual) = d(base) - [dK_a A_b + A_a (dK_b - dK_mm A_b)]
+            dC = base_nn - (dK[p][N] @ A[:, N] + A[:, N].T @ (dK[p][N].T - dKA[p][:, N]))
+            dC = 0.5 * (dC + dC.T)
+            dc = base_ni - (dK[p][N] @ A[:, i] + A[:, N].T @ (dK[p][i] - dKA[p][:, i]))
+            da = cho_solve(cC, dc - dC @ a)
+            dB[p][i, N] = -da
+            dD[p][i] -= da @ c + a @ dc
+    return dict(K=K, Kmm=Kmm, Ks=Ks, cKs=cKs, dK=dK, dKmm=dKmm, B=B, D=D, dB=dB, dD=dD)
+
+
+def vif_nll_grad(xv, y_vo, nb, Z, cov_type, pars, mode=0):
+    """nll and gradient (mode 0: [nugget, var, range] at sigma^2 = pars[0]; mode 1: sigma^2 profiled, [var,
+    range]) on the transformed scale, plus the pieces (log det Psi, y^T Psi^-1 y)."""
+    sigma2, var, phi = pars
+    f = vif_factor(xv, nb, Z, cov_type, var, phi)
+    n = len(y_vo)
+    K, cKs = f["K"], f["cKs"]
+    Bi = np.linalg.inv(f["B"])
+    R = Bi @ np.diag(f["D"]) @ Bi.T
+    KA = K @ cho_solve(cKs, K.T)
+    Psi = KA + R
+    cP = cho_factor(Psi, lower=True)
+    logdet = 2. * np.log(np.diag(cP[0])).sum()
+    yaux = cho_solve(cP, y_vo)
+    q = float(y_vo @ yaux)
+    Pinv = cho_solve(cP, np.eye(n))
+    s1, s2 = [], []
+    for p in range(2):
+        G = f["dK"][p] @ cho_solve(cKs, K.T)
+        H = K @ cho_solve(cKs, f["dKmm"][p] @ cho_solve(cKs, K.T))
+        dR = -Bi @ f["dB"][p] @ R - R @ f["dB"][p].T @ Bi.T + Bi @ np.diag(f["dD"][p]) @ Bi.T
+        dPsi = G + G.T - H + dR
+        s1.append(-0.5 * yaux @ dPsi @ yaux)
+        s2.append(float(np.sum(Pinv * dPsi)))
+    if mode == 1:
+        sigma2 = q / n
+    nll = q / 2. / sigma2 + logdet / 2. + n / 2. * (np.log(sigma2) + np.log(2 * np.pi))
+    grad = [s1[p] / sigma2 + 0.5 * s2[p] for p in range(2)]
+    if mode == 0:
+        grad = [-q / sigma2 / 2. + n / 2.] + grad
+    return dict(nll=float(nll), grad=np.array(grad), sigma2=float(sigma2), logdet=float(logdet), q=q,
+                D=f["D"], B=f["B"])
