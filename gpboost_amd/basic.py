@@ -120,8 +120,11 @@ class GPModel:
         self.gp_approx = gp_approx
         self.cov_function = cov_function
         self.cov_fct_shape = float(cov_fct_shape)
-        if num_neighbors is None:
-            num_neighbors = 20  # reference default (basic.py: num_neighbors None -> 20)
+        vif = gp_approx in ("full_scale_vecchia", "vif", "VIF")
+        if num_neighbors is None:   # the reference's defaults (re_model_template.h:288-297, 320-330)
+            num_neighbors = 30 if vif else 20
+        if num_ind_points is None:
+            num_ind_points = 200 if vif else 500
         self.num_neighbors = int(num_neighbors)
         self.likelihood = likelihood
         coords_cm = np.ascontiguousarray(coords.T).reshape(-1)  # column-major, as the reference passes it
@@ -136,7 +139,7 @@ class GPModel:
             ctypes.c_int32(1), _dp(coords_cm), ctypes.c_int(self.dim_coords), None, ctypes.c_int32(0),
             c_str(cov_function), ctypes.c_double(self.cov_fct_shape), c_str(gp_approx),
             ctypes.c_double(cov_fct_taper_range), ctypes.c_double(cov_fct_taper_shape),
-            ctypes.c_int(self.num_neighbors), c_str(vecchia_ordering), ctypes.c_int(num_ind_points or 500),
+            ctypes.c_int(self.num_neighbors), c_str(vecchia_ordering), ctypes.c_int(num_ind_points),
             ctypes.c_double(cover_tree_radius), c_str(ind_points_selection), c_str(likelihood),
             ctypes.c_double(likelihood_additional_param or 0.), c_str(matrix_inversion_method),
             ctypes.c_int(seed), ctypes.c_int(num_parallel_threads or -1), ctypes.c_bool(GPU_use),

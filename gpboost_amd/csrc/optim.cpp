@@ -185,7 +185,8 @@ double REModelAMD::InitialRangeTrafo() const {
   // the GP component's coordinates: all points, or the unique locations of a latent model with
   // repeated coordinates (RECompGP::coords_, re_comp.h:1232-1244)
   // FITC: the inducing points' component (re_comps_ip_, re_model_template.h:4474-4476), the draws
-  // continuing the generator after the inducing-point selection
+  // continuing the generator after the inducing-point selection; full_scale_vecchia: the Vecchia component
+  // (all points in the model order, :4452-4456) with the generator after the shuffle and the selection
   const std::vector<double>& X = fitc_ ? fitc_->inducing_points() : coords_vo_;
   const int d = cfg_.d, n = (int)(X.size() / d);
   const int kMaxPoints = 1000;
@@ -193,7 +194,7 @@ double REModelAMD::InitialRangeTrafo() const {
   std::vector<int> idx(nf);
   if (nf < n) {
     std::mt19937 rng(cfg_.seed);
-    if (fitc_) rng = fitc_rng_;
+    if (fitc_ || vif_) rng = fitc_rng_;   // full_scale_vecchia: after the shuffle and the inducing points
     if (vecchia_ && cfg_.vecchia_ordering == "random") {   // the ordering shuffle of the n observations
       std::vector<int> dummy(cfg_.n);
       std::iota(dummy.begin(), dummy.end(), 0);

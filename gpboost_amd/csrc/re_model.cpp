@@ -84,8 +84,20 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
       Fatal("'iterative' methods are not implemented for gp_approx = 'fitc'. Use 'cholesky' ");
     if (cfg_.num_ind_points <= 0) cfg_.num_ind_points = 500;   // re_model_template.h:320-326
     if (!(cfg_.cover_tree_radius > 0.)) Fatal("cover_tree_radius must be > 0");
+  } else if (cfg_.gp_approx == "full_scale_vecchia" || cfg_.gp_approx == "vif" || cfg_.gp_approx == "VIF") {
+    cfg_.gp_approx = "full_scale_vecchia";   // re_model_template.h:204-206
+    if (cfg_.lik != kLikGaussian)
+      Fatal("gp_approx = 'full_scale_vecchia' with likelihood '%s' (Laplace approximation) is not supported by "
+            "gpboost_amd (supported: gaussian)", cfg_.likelihood.c_str());
+    if (cfg_.matrix_inversion_method == "iterative")   // re_model_template.h:8780-8782
+      Fatal("The iterative methods are not implemented for the Full-Scale-Vecchia approximation with Gaussian "
+            "likelihood. Please use Cholesky.");
+    if (cfg_.num_ind_points <= 0) cfg_.num_ind_points = 200;   // re_model_template.h:320-330
+    if (cfg_.num_neighbors <= 0) cfg_.num_neighbors = 30;      // :288-297
+    if (!(cfg_.cover_tree_radius > 0.)) Fatal("cover_tree_radius must be > 0");
   } else {
-    Fatal("gp_approx '%s' is not supported by gpboost_amd (supported: none, vecchia, vecchia_latent, fitc)", cfg_.gp_approx.c_str());
+    Fatal("gp_approx '%s' is not supported by gpboost_amd (supported: none, vecchia, vecchia_latent, fitc, "
+          "full_scale_vecchia)", cfg_.gp_approx.c_str());
   }
   std::string& mim = cfg_.matrix_inversion_method;
   if (mim == "default") mim = cfg_.latent && vecchia_ ? "iterative" : "cholesky";
@@ -152,6 +164,38 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
     d_X_.alloc((size_t)nu_ * d);
     HIP_CHECK(hipMemcpyAsync(d_X_.get(), coords_vo_.data(), sizeof(double) * nu_ * d, hipMemcpyHostToDevice, stream_));
     // neighbour search is deferred to first use so a distributed model searches only its rows
+  } else if (cfg_.gp_approx == "full_scale_vecchia") {
+    // re_model_template.h:348-357: rng_ = mt19937(seed) shuffles the order first (random ordering), then
+    // CreateREComponentsFITC_FSA selects the inducing points on the coordinates in that order with the same
+    // generator; the Vecchia neighbours (Euclidean, vecchia_neighbor_selection = "nearest") follow
+    if (cfg_.vecchia_ordering != "random" && cfg_.vecchia_ordering != "none")
+      Fatal("vecchia_ordering '%s' is not supported (supported: none, random)", cfg_.vecchia_ordering.c_str());
+    std::mt19937 rng((std::mt19937::result_type)cfg_.seed);
+    perm_.resize(n);
+    std::iota(perm_.begin(), perm_.end(), 0);
+    if (cfg_.vecchia_ordering == "random") std::shuffle(perm_.begin(), perm_.end(), rng);
+    coords_vo_.resize((size_t)n * d);
+    for (int i = 0; i < n; ++i)
+      for (int q = 0; q < d; ++q) coords_vo_[(size_t)i * d + q] = coords_[(size_t)perm_[i] * d + q];
+    std::vector<int> uniq, idx;
+    unique_locations(coords_vo_.data(), n, d, uniq, idx);
+    if ((int)uniq.size() < n)
+      Fatal("gp_approx = 'full_scale_vecchia' with duplicate coordinates is not supported by gpboost_amd");
+    const std::vector<double> Z =
+        fitc_inducing_points(coords_vo_, n, d, cfg_.num_ind_points, cfg_.ind_points_selection, rng, stream_);
+    std::vector<int> zu, zi;
+    unique_locations(Z.data(), cfg_.num_ind_points, d, zu, zi);
+    if ((int)zu.size() < cfg_.num_ind_points) Fatal("Duplicates found in inducing points / low-dimensional knots ");
+    fitc_rng_ = rng;
+    if (cfg_.num_neighbors > n - 1) cfg_.num_neighbors = n - 1;   // Vecchia_utils.cpp:754-757
+    if (cfg_.num_neighbors < 1) Fatal("num_neighbors must be >= 1");
+    const int m = cfg_.num_neighbors;
+    std::vector<int> nbr((size_t)n * m, -1);
+    if (m > 64 || d > 3) vecchia_neighbors(coords_vo_.data(), n, d, m, 0, n, nbr.data());
+    else vecchia_neighbors_gpu(coords_vo_.data(), n, d, m, 0, n, nbr.data(), stream_);
+    d_X_.alloc((size_t)n * d);
+    HIP_CHECK(hipMemcpyAsync(d_X_.get(), coords_vo_.data(), sizeof(double) * n * d, hipMemcpyHostToDevice, stream_));
+    vif_.reset(new VifSolver(n, d, d_X_.get(), Z, nbr, m, stream_));
   } else {
     coords_vo_ = coords_;
     d_X_.alloc((size_t)n * d);
@@ -213,6 +257,7 @@ REModelAMD::~REModelAMD() {
   (void)hipSetDevice(device_);
   if (stream_) (void)hipStreamSynchronize(stream_);
   dense_.reset();
+  vif_.reset();
   fitc_lap_.reset();
   fitc_.reset();
   latent_.reset();
@@ -357,6 +402,7 @@ std::vector<double> gauss_hermite_adaptive(int order) {
 void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,
                          bool predict_cov_mat, bool predict_var, bool predict_response, double* out,
                          const double* mean_add) {
+  if (vif_) Fatal("predictions with gp_approx = 'full_scale_vecchia' are not supported by gpboost_amd");
   if (fitc_) {
     PredictFitc(y, n_pred, coords_pred, cov_pars, predict_cov_mat, predict_var, predict_response, out, mean_add);
     return;
@@ -1002,7 +1048,7 @@ void REModelAMD::SetY(const double* y) {
   UseDevice();
   const int n = cfg_.n;
   std::vector<double> yv(n);
-  if (vecchia_) for (int i = 0; i < n; ++i) yv[i] = y[perm_[i]];
+  if (vecchia_ || vif_) for (int i = 0; i < n; ++i) yv[i] = y[perm_[i]];
   else std::copy(y, y + n, yv.begin());
   if (cfg_.latent) {
     double lognorm = 0.;   // CheckY (likelihoods.h:637-737), CalculateLogNormalizingConstant (:8290-8310)
@@ -1129,6 +1175,11 @@ void REModelAMD::EvalVecchiaPartials(const double* cov_pars_orig, int r0, int r1
 }
 
 void REModelAMD::EvalExactGaussian(const double* trafo, bool want_grad, double* sums) {
+  if (vif_) {
+    events_pending_ = false;
+    vif_->Eval(cfg_.cov_type, trafo[1], trafo[2], d_y_.get(), want_grad, sums, last_kernel_ms_);
+    return;
+  }
   if (fitc_) {
     events_pending_ = false;
     fitc_->Eval(cfg_.cov_type, trafo[1], trafo[2], d_y_.get(), want_grad, sums, last_kernel_ms_);
@@ -1138,7 +1189,8 @@ void REModelAMD::EvalExactGaussian(const double* trafo, bool want_grad, double* 
 }
 
 const std::vector<double>& REModelAMD::InducingPoints() const {
-  if (!fitc_) Fatal("model does not use gp_approx = 'fitc'");
+  if (vif_) return vif_->inducing_points();
+  if (!fitc_) Fatal("model does not use gp_approx = 'fitc' or 'full_scale_vecchia'");
   return fitc_->inducing_points();
 }
 

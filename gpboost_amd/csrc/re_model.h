@@ -20,6 +20,7 @@
 #include "dense.h"
 #include "fitc.h"
 #include "fitc_laplace.h"
+#include "vif.h"
 #include "latent.h"
 #include "optim.h"
 
@@ -119,6 +120,7 @@ class REModelAMD {
   // FITC inducing points (host row-major m x d; EXTENSION: GPB_GetInducingPoints)
   const std::vector<double>& InducingPoints() const;
   bool is_fitc() const { return fitc_ != nullptr; }
+  bool is_vif() const { return vif_ != nullptr; }
 
   double last_nll() const { return last_nll_; }
   const std::vector<double>& last_cov_pars() const { return last_cov_pars_; }
@@ -175,7 +177,7 @@ class REModelAMD {
   const std::string& optimizer_coef() const { return optimizer_coef_; }
   std::string cg_preconditioner_type() const;
   // CanCalculateStandardErrorsCovPars (re_model_template.h:1630-1632)
-  bool CanCalculateStandardErrorsCovPars() const { return !cfg_.latent && !fitc_; }
+  bool CanCalculateStandardErrorsCovPars() const { return !cfg_.latent && !fitc_ && !vif_; }
   // GLS evaluation on the transformed scale (optimizer): beta from the Gram of [X | y], then the
   // profiled L-BFGS unit on the residuals. beta_out (nullable) receives the coefficients.
   EvalResult EvalTrafoWls(const double* trafo, bool want_grad, bool fatal_on_nan, std::vector<double>* beta_out);
@@ -274,6 +276,7 @@ class REModelAMD {
   std::unique_ptr<DenseSolver> dense_;
   std::unique_ptr<FitcSolver> fitc_;   // gp_approx = "fitc"
   std::unique_ptr<FitcLaplace> fitc_lap_;   // gp_approx = "fitc", non-Gaussian likelihood (Laplace)
+  std::unique_ptr<VifSolver> vif_;          // gp_approx = "full_scale_vecchia" (Gaussian likelihood)
   std::mt19937 fitc_rng_;              // the model's generator after the inducing-point selection
   std::unique_ptr<LatentVecchia> latent_;
   // the latent solver of a Laplace model: the Vecchia (iterative) or the FITC (Cholesky) one

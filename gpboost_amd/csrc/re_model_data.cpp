@@ -86,6 +86,7 @@ void REModelAMD::CalcGradientF(double* y, const double* fixed_effects, bool calc
   double trafo[3];
   TransformCovPars(cov_pars_orig_.data(), trafo);
   std::vector<double> yaux(n), dg(n);
+  if (vif_) Fatal("the gradient wrt the fixed effects with gp_approx = 'full_scale_vecchia' is not supported by gpboost_amd");
   if (fitc_) {   // Woodbury y_aux of the FITC factor (CalcYAux, re_model_template.h:8898-8908)
     double sums[kVecchiaSums];
     UseDevice();
@@ -144,7 +145,8 @@ void REModelAMD::UploadCovariates() {
 
 std::vector<double> REModelAMD::Gram(const double* trafo) {
   const int n = cfg_.n, p = num_covariates_, c = p + 1;
-  if (fitc_) Fatal("linear regression covariates with gp_approx = 'fitc' are not supported by gpboost_amd");
+  if (fitc_ || vif_)
+    Fatal("linear regression covariates with gp_approx = '%s' are not supported by gpboost_amd", cfg_.gp_approx.c_str());
   if (!vecchia_) {
     std::vector<double> Z((size_t)n * c), G((size_t)c * c);
     const double* fe = has_fixed_effects_ ? fixed_effects_.data() : nullptr;
@@ -280,7 +282,9 @@ void REModelAMD::PredictTrainingDataRandomEffects(const double* cov_pars, const 
   double trafo[3];
   TransformCovPars(cp.data(), trafo);
   std::vector<double> yaux(n), dg(n);
-  if (fitc_) Fatal("training-data random-effect predictions with gp_approx = 'fitc' are not supported by gpboost_amd");
+  if (fitc_ || vif_)
+    Fatal("training-data random-effect predictions with gp_approx = '%s' are not supported by gpboost_amd",
+          cfg_.gp_approx.c_str());
   if (!vecchia_) {
     dense_->PsiInvDiag(cfg_.cov_type, trafo[1], trafo[2], d_y_.get(), yaux.data(), dg.data());
     for (int i = 0; i < n; ++i) {

@@ -1,0 +1,80 @@
+// Full-scale Vecchia approximation ("VIF", gp_approx = "full_scale_vecchia" / "vif") for the Gaussian
+// likelihood: the reference's predictive-process-plus-Vecchia-residual covariance
+//   Psi = K_nm K_mm,s^-1 K_mn + B^-1 D B^-T
+// on the transformed scale (nugget 1 in the residual part), where B (unit lower, the Vecchia neighbours
+// of each point in the model order) and D come from the RESIDUAL covariances
+//   C_res(a, b) = k(a, b) + [a == b] - V_a . V_b,   V = L^-1 K_mn,  L = chol(K_mm,s)
+// among each point and its neighbours, and K_mm,s = K_mm with its diagonal times (1 + 1e-6).
+//
+// Reference path replaced:
+//   ordering + inducing points  re_model_template.h:348-357 (shuffle with rng_, then CreateREComponentsFITC_FSA
+//                               on the shuffled coordinates with the same generator)
+//   neighbours                  Vecchia_utils.cpp:732-1058 (Euclidean kNN among earlier points; the GPU search)
+//   Sigma components            re_model_template.h:7341-7378 (CalcSigmaComps)
+//   residual factor + gradient  Vecchia_utils.cpp:1388-1617 (CalcCovFactorGradientVecchia, full_scale_vecchia)
+//   Woodbury factor             re_model_template.h:8770-8880 (CalcCovFactorFITC_FSA, cholesky)
+//   y_aux, log det              re_model_template.h:8898-8935, 2698-2714
+//   gradient                    re_model_template.h:1985-2232 (CalcGradPars_FITC_FSA_GaussLikelihood_Cluster_i)
+// The reference runs these with Eigen sparse products, cuBLAS / cuSPARSE offloads (cuda_kernel.cu:613-941).
+// This build: one workgroup per row for the residual factor (the neighbour set's columns of V and of the
+// derivative factors staged through LDS in m-chunks, the Gram blocks and the small Cholesky solves in
+// LDS), sparse B / B^T products over contiguous m-vectors (one wave per point), and every m x n / m x m
+// product on the fp64 MFMA GEMM (split-K for the m x m Woodbury Gram).
+//
+// HBM layout: every m x n matrix column-major with leading dimension ldm = round_up(m, 64) (point i's m
+// entries contiguous), the B / D factor and its derivatives as n x nn value rows beside the neighbour lists.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <memory>
+#include <vector>
+
+#include "common.h"
+#include "fitc.h"
+
+namespace gpb_amd {
+
+class VifSolver {
+ public:
+  // d_X: device row-major n x d coordinates in the model order; Z: host row-major m x d inducing points;
+  // nbr: host n x nn neighbour lists (row i holds its min(i, nn) neighbours, the rest -1).
+  VifSolver(int n, int d, const double* d_X, const std::vector<double>& Z, const std::vector<int>& nbr, int nn,
+            hipStream_t stream);
+  ~VifSolver();
+  const std::vector<double>& inducing_points() const { return F_->inducing_points(); }
+  // sums = [logdet, q, s1_var, s1_range, s2_var, s2_range] (combine_partials): s1_k = -1/2 y_aux^T dPsi_k
+  // y_aux, s2_k = tr(Psi^-1 dPsi_k) with the reference's dPsi_k (un-jittered dK_mm, B_grad, D_grad). A
+  // non-positive-definite factor gives NaN sums. kernel_ms[0] = factor part, [1] = whole evaluation.
+  void Eval(int cov_type, double var, double phi, const double* d_y, bool want_grad, double* sums, double* kernel_ms);
+  // D (n) and B's values (n x nn, 0 past a row's neighbours) of the last Eval (host)
+  void GetFactor(double* D, double* Bv) const;
+
+ private:
+  void Rows(int cov_type, double var, double phi, bool grad);
+  // out = B in (self = 1) or dB in (self = 0) over m-vector columns; div: then times D^-1
+  void BRow(const double* in, const double* coef, double self, bool div, double* out);
+  // out = B^T in (self = 1) or dB^T in (self = 0) over m-vector columns
+  void BCol(const double* in, const double* coef, double self, double* out);
+  void BVec(const double* x, const double* coef, double self, double* out);
+  void BtVec(const double* x, const double* coef, double self, double* out);
+  void Gemv(const double* M, const double* x, double* out);   // out (m) = M x, M m x n
+  void ColDot(const double* M, const double* w, const double* M2, double* out);   // out_i = M_i . (w | M2_i)
+
+  std::unique_ptr<FitcSolver> F_;
+  int n_, d_, m_, ldm_, nn_;
+  hipStream_t s_;
+  const double* d_X_;
+  DevBuf<int> nbr_, tptr_, trow_, tslot_;
+  DevBuf<double> dK_, P0_, P1_, BK_;                 // m x n (ldm)
+  DevBuf<double> Bv_, dBv0_, dBv1_;                   // n x nn
+  DevBuf<double> D_, dD0_, dD1_;                      // n
+  DevBuf<double> vec_;                                // n-vectors (scratch)
+  DevBuf<double> mvec_;                               // m-vectors (scratch)
+  DevBuf<double> part_, red_;
+  double* h_red_ = nullptr;
+  size_t lds_bytes_ = 0;
+  hipEvent_t ev_[3] = {nullptr, nullptr, nullptr};
+};
+
+}  // namespace gpb_amd

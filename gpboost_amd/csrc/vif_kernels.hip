@@ -1,0 +1,740 @@
+// Full-scale Vecchia approximation (vif.h gives the model and the reference lines). Per evaluation
+// (n points, m inducing points, nn neighbours, ld ldm):
+//   low-rank part   K_mn, K_mm, L = chol(K_mm,s), V = L^-1 K_mn                  FitcSolver::Prior (MFMA GEMM)
+//   derivatives     A = K_mm,s^-1 K_mn, P_k = L^-1 (dK_mn,k - 1/2 dK_mm,k A)       four MFMA GEMMs
+//   residual rows   per point: the Gram blocks V_S^T V_S, V_S^T P_k,S of its neighbour set S through LDS,
+//                   the residual covariances, one Cholesky + 3 solves             vif_rows_kernel (one WG / row)
+//   Woodbury        BK = B K_mn^T (sparse over m-vectors), M = K_mm,s + BK^T D^-1 BK  split-K MFMA Gram
+//   y_aux, traces   B / B^T vector products, m-vector solves with the inverse Cholesky factor, column dots
+// The gradient's m x m traces come from tr(M^-1 X^T Y) = sum_i (M^-1 X_i) . Y_i with M^-1 X formed by
+// one MFMA GEMM per matrix (re_model_template.h:2041-2079 forms the m x m products instead).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <limits>
+#include <type_traits>
+
+#include "cov.h"
+#include "dense.h"
+#include "fitc.h"
+#include "kernels.h"
+#include "vif.h"
+
+namespace gpb_amd {
+namespace {
+
+constexpr int kT = 256;
+constexpr int kCh = 32;      // m-rows per LDS staging chunk in the row kernel
+constexpr int kEpt = 16;     // Gram entries per thread per pass
+constexpr int kMaxNn = 48;   // neighbours per row (LDS budget of the row kernel)
+constexpr int kNv = 16;      // n-vector scratch slots
+constexpr int kMv = 12;      // m-vector scratch slots
+
+template <class F>
+void dispatch_cov_vif(int cov, F&& f) {
+  switch (cov) {
+    case kMatern05: f(std::integral_constant<int, kMatern05>{}); break;
+    case kMatern15: f(std::integral_constant<int, kMatern15>{}); break;
+    case kMatern25: f(std::integral_constant<int, kMatern25>{}); break;
+    case kGaussian: f(std::integral_constant<int, kGaussian>{}); break;
+    default: Fatal("unsupported covariance type %d", cov);
+  }
+}
+
+__device__ __forceinline__ double wsum(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ __forceinline__ double dist_pts(const double* X, int d, int a, int b) {
+  double s = 0.;
+  for (int q = 0; q < d; ++q) {
+    const double t = X[(size_t)a * d + q] - X[(size_t)b * d + q];
+    s += t * t;
+  }
+  return sqrt(s);
+}
+
+// dK_mn / dlog(phi) (m x n, ld ldm)
+template <int COV>
+__global__ void __launch_bounds__(kT) vif_dkmn_kernel(const double* __restrict__ X, const double* __restrict__ Z, int n,
+                                                     int m, int d, int ldm, double var, double phi,
+                                                     double* __restrict__ dK) {
+  const int j = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int i = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= n || j >= m) return;
+  double s = 0.;
+  for (int q = 0; q < d; ++q) {
+    const double t = X[(size_t)i * d + q] - Z[(size_t)j * d + q];
+    s += t * t;
+  }
+  double c, dc;
+  cov_dcov<COV>(sqrt(s), var, phi, c, dc);
+  dK[(size_t)j + (size_t)i * ldm] = dc;
+}
+
+struct VifRowsArgs {
+  const double* X;
+  const int* nbr;
+  int n, d, nn, mi, ldm;
+  const double* V;
+  const double* P0;
+  const double* P1;
+  double var, phi;
+  int r1;   // doubles of the staging / residual-matrix region
+  double* Bv;
+  double* D;
+  double* dBv0;
+  double* dBv1;
+  double* dD0;
+  double* dD1;
+};
+
+// Residual Vecchia row i (Vecchia_utils.cpp:1405-1617, full_scale_vecchia branches), transformed scale:
+//   C = k(N, N) + I - V_N^T V_N,  c = k(N, i) - V_N^T V_i,  d0 = 1 + var - |V_i|^2
+//   A = C^-1 c,  B(i, N) = -A,  D_i = d0 - A . c
+// and per parameter k (log var, log phi), with P_k = L^-1 (dK_k - 1/2 dK_mm,k A) so that
+// dK_a . A_b + A_a . (dK_b - dK_mm A_b) = V_a . P_b + P_a . V_b:
+//   dC = dk(N, N) - (G + G^T),  dc = dk(N, i) - (V_N . P_i + P_N . V_i),  dd0 = [k = var] var - 2 V_i . P_i
+//   dA = C^-1 (dc - dC A),  dB(i, N) = -dA,  dD_i = dd0 - (dA . c + A . dc)
+// One 256-thread workgroup per row: the Gram blocks of the neighbour set S = N + {i} accumulate over
+// m-chunks staged in LDS; the k x k Cholesky and the solves run in LDS with a barrier per step.
+template <int COV, bool GRAD>
+__global__ void __launch_bounds__(kT) vif_rows_kernel(VifRowsArgs a) {
+  extern __shared__ double lds[];
+  __shared__ int idx[kMaxNn + 1];
+  __shared__ double vecs[7][kMaxNn];   // c, dc0, dc1, A / x, r0 / dA0, r1 / dA1, spare
+  __shared__ double scal[4];
+  constexpr int G = GRAD ? 3 : 1;
+  const int i = blockIdx.x, tid = threadIdx.x;
+  const int nn = a.nn, k = min(i, nn), S = k + 1;
+  if (tid < k) idx[tid] = a.nbr[(size_t)i * nn + tid];
+  if (tid == k) idx[k] = i;
+  double* st = lds;            // staging [g][a][q] (kCh), later C, dC0, dC1 (k x k each)
+  double* gram = lds + a.r1;   // [g][a][b] = V_a . M^g_b, S x S each
+  __syncthreads();
+  const int E = G * S * S;
+  for (int e0 = 0; e0 < E; e0 += kT * kEpt) {
+    double acc[kEpt];
+#pragma unroll
+    for (int j = 0; j < kEpt; ++j) acc[j] = 0.;
+    for (int q0 = 0; q0 < a.mi; q0 += kCh) {
+      const int tot = G * S * kCh;
+      for (int t = tid; t < tot; t += kT) {
+        const int g = t / (S * kCh);
+        const int r = t - g * S * kCh;
+        const int p = r / kCh;
+        const int q = q0 + (r - p * kCh);
+        const double* M = g == 0 ? a.V : (g == 1 ? a.P0 : a.P1);
+        st[t] = q < a.mi ? M[(size_t)idx[p] * a.ldm + q] : 0.;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int j = 0; j < kEpt; ++j) {
+        const int e = e0 + j * kT + tid;
+        if (e < E) {
+          const int g = e / (S * S);
+          const int r = e - g * S * S;
+          const int p = r / S, b = r - p * S;
+          const double* L = st + p * kCh;
+          const double* R = st + (size_t)g * S * kCh + b * kCh;
+          double s = 0.;
+#pragma unroll 8
+          for (int q = 0; q < kCh; ++q) s = fma(L[q], R[q], s);
+          acc[j] += s;
+        }
+      }
+      __syncthreads();
+    }
+#pragma unroll
+    for (int j = 0; j < kEpt; ++j) {
+      const int e = e0 + j * kT + tid;
+      if (e < E) gram[e] = acc[j];
+    }
+  }
+  __syncthreads();
+  const int SS = S * S;
+  double* C = st;
+  double* dC0 = st + k * k;
+  double* dC1 = st + 2 * k * k;
+  for (int e = tid; e < k * k; e += kT) {
+    const int p = e / k, b = e - p * k;
+    double c = a.var, dc = 0.;
+    if (p != b) cov_dcov<COV>(dist_pts(a.X, a.d, idx[p], idx[b]), a.var, a.phi, c, dc);
+    C[e] = c + (p == b ? 1. : 0.) - gram[p * S + b];
+    if (GRAD) {
+      dC0[e] = c - (gram[SS + p * S + b] + gram[SS + b * S + p]);
+      dC1[e] = dc - (gram[2 * SS + p * S + b] + gram[2 * SS + b * S + p]);
+    }
+  }
+  for (int p = tid; p < k; p += kT) {
+    double c, dc;
+    cov_dcov<COV>(dist_pts(a.X, a.d, idx[p], i), a.var, a.phi, c, dc);
+    vecs[0][p] = c - gram[p * S + k];
+    vecs[3][p] = vecs[0][p];
+    if (GRAD) {
+      vecs[1][p] = c - (gram[SS + p * S + k] + gram[SS + k * S + p]);
+      vecs[2][p] = dc - (gram[2 * SS + p * S + k] + gram[2 * SS + k * S + p]);
+    }
+  }
+  if (tid == 0) {
+    scal[0] = 1. + a.var - gram[k * S + k];
+    if (GRAD) {
+      scal[1] = a.var - 2. * gram[SS + k * S + k];
+      scal[2] = -2. * gram[2 * SS + k * S + k];
+    }
+  }
+  __syncthreads();
+  // Cholesky C = L L^T in place (lower, row-major k x k)
+  for (int j = 0; j < k; ++j) {
+    if (tid == 0) C[j * k + j] = sqrt(C[j * k + j]);
+    __syncthreads();
+    if (tid > j && tid < k) C[tid * k + j] /= C[j * k + j];
+    __syncthreads();
+    if (tid > j && tid < k) {
+      const double l = C[tid * k + j];
+      for (int s2 = j + 1; s2 <= tid; ++s2) C[tid * k + s2] -= l * C[s2 * k + j];
+    }
+    __syncthreads();
+  }
+  // solve L L^T x = b for nrhs right-hand sides in vecs[3 + r] (thread = (rhs, row))
+  auto solve = [&](int nrhs) {
+    const int r = tid >> 6, row = tid & 63;
+    for (int j = 0; j < k; ++j) {
+      if (r < nrhs && row == j) vecs[3 + r][j] /= C[j * k + j];
+      __syncthreads();
+      if (r < nrhs && row > j && row < k) vecs[3 + r][row] -= C[row * k + j] * vecs[3 + r][j];
+      __syncthreads();
+    }
+    for (int j = k - 1; j >= 0; --j) {
+      if (r < nrhs && row == j) vecs[3 + r][j] /= C[j * k + j];
+      __syncthreads();
+      if (r < nrhs && row < j) vecs[3 + r][row] -= C[j * k + row] * vecs[3 + r][j];
+      __syncthreads();
+    }
+  };
+  solve(1);   // vecs[3] = A
+  if (GRAD) {
+    // r_k = dc_k - dC_k A into vecs[4 + k], then dA_k = C^-1 r_k in place (the solve uses slots 4, 5 as
+    // right-hand sides 1, 2; slot 3 (A) is passed through untouched by restricting to rhs 1..2)
+    for (int e = tid; e < 2 * k; e += kT) {
+      const int kk = e / k, p = e - kk * k;
+      const double* dC = kk == 0 ? dC0 : dC1;
+      double s = vecs[1 + kk][p];
+      for (int b = 0; b < k; ++b) s -= dC[p * k + b] * vecs[3][b];
+      vecs[4 + kk][p] = s;
+    }
+    __syncthreads();
+    {
+      const int r = tid >> 6, row = tid & 63;
+      const bool act = r >= 1 && r <= 2;
+      for (int j = 0; j < k; ++j) {
+        if (act && row == j) vecs[3 + r][j] /= C[j * k + j];
+        __syncthreads();
+        if (act && row > j && row < k) vecs[3 + r][row] -= C[row * k + j] * vecs[3 + r][j];
+        __syncthreads();
+      }
+      for (int j = k - 1; j >= 0; --j) {
+        if (act && row == j) vecs[3 + r][j] /= C[j * k + j];
+        __syncthreads();
+        if (act && row < j) vecs[3 + r][row] -= C[j * k + row] * vecs[3 + r][j];
+        __syncthreads();
+      }
+    }
+  }
+  if (tid < 64) {
+    // D_i = d0 - A . c; dD_k = dd0_k - (dA_k . c + A . dc_k) (wave sums in a fixed order)
+    const int p = tid;
+    double s0 = 0., s1 = 0., s2 = 0.;
+    if (p < k) {
+      s0 = vecs[3][p] * vecs[0][p];
+      if (GRAD) {
+        s1 = vecs[4][p] * vecs[0][p] + vecs[3][p] * vecs[1][p];
+        s2 = vecs[5][p] * vecs[0][p] + vecs[3][p] * vecs[2][p];
+      }
+    }
+    s0 = wsum(s0);
+    if (GRAD) {
+      s1 = wsum(s1);
+      s2 = wsum(s2);
+    }
+    const size_t row = (size_t)i * nn;
+    if (p < nn) {
+      a.Bv[row + p] = p < k ? -vecs[3][p] : 0.;
+      if (GRAD) {
+        a.dBv0[row + p] = p < k ? -vecs[4][p] : 0.;
+        a.dBv1[row + p] = p < k ? -vecs[5][p] : 0.;
+      }
+    }
+    if (p == 0) {
+      a.D[i] = scal[0] - s0;
+      if (GRAD) {
+        a.dD0[i] = scal[1] - s1;
+        a.dD1[i] = scal[2] - s2;
+      }
+    }
+  }
+}
+
+// out[:, i] = (self in[:, i] + sum_r coef[i nn + r] in[:, nbr[i nn + r]]) (/ D_i): one wave per column
+__global__ void __launch_bounds__(kT) vif_brow_kernel(const double* __restrict__ in, const int* __restrict__ nbr,
+                                                     const double* __restrict__ coef, const double* __restrict__ D,
+                                                     int n, int nn, int m, int ldm, double self, int div,
+                                                     double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const int k = min(i, nn);
+  const double sc = div ? 1. / D[i] : 1.;
+  for (int q = lane; q < m; q += 64) {
+    double s = self != 0. ? self * in[(size_t)i * ldm + q] : 0.;
+    for (int r = 0; r < k; ++r) s = fma(coef[(size_t)i * nn + r], in[(size_t)nbr[(size_t)i * nn + r] * ldm + q], s);
+    out[(size_t)i * ldm + q] = s * sc;
+  }
+}
+
+// out[:, j] = self in[:, j] + sum over rows i with j among their neighbours of coef(i, j) in[:, i]
+__global__ void __launch_bounds__(kT) vif_bcol_kernel(const double* __restrict__ in, const int* __restrict__ tptr,
+                                                     const int* __restrict__ trow, const int* __restrict__ tslot,
+                                                     const double* __restrict__ coef, int n, int m, int ldm, double self,
+                                                     double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= n) return;
+  const int t0 = tptr[j], t1 = tptr[j + 1];
+  for (int q = lane; q < m; q += 64) {
+    double s = self != 0. ? self * in[(size_t)j * ldm + q] : 0.;
+    for (int t = t0; t < t1; ++t) s = fma(coef[tslot[t]], in[(size_t)trow[t] * ldm + q], s);
+    out[(size_t)j * ldm + q] = s;
+  }
+}
+
+__global__ void __launch_bounds__(kT) vif_bvec_kernel(const double* __restrict__ x, const int* __restrict__ nbr,
+                                                     const double* __restrict__ coef, const double* __restrict__ D,
+                                                     int n, int nn, double self, double* __restrict__ out) {
+  const int i = blockIdx.x * kT + threadIdx.x;
+  if (i >= n) return;
+  const int k = min(i, nn);
+  double s = self != 0. ? self * x[i] : 0.;
+  for (int r = 0; r < k; ++r) s = fma(coef[(size_t)i * nn + r], x[nbr[(size_t)i * nn + r]], s);
+  out[i] = D ? s / D[i] : s;
+}
+
+__global__ void __launch_bounds__(kT) vif_btvec_kernel(const double* __restrict__ x, const int* __restrict__ tptr,
+                                                      const int* __restrict__ trow, const int* __restrict__ tslot,
+                                                      const double* __restrict__ coef, int n, double self,
+                                                      double* __restrict__ out) {
+  const int j = blockIdx.x * kT + threadIdx.x;
+  if (j >= n) return;
+  double s = self != 0. ? self * x[j] : 0.;
+  for (int t = tptr[j]; t < tptr[j + 1]; ++t) s = fma(coef[tslot[t]], x[trow[t]], s);
+  out[j] = s;
+}
+
+// part[b ldm + j] = sum_{i in chunk b} M[j, i] x_i
+__global__ void __launch_bounds__(kT) vif_gemv_part_kernel(const double* __restrict__ M, const double* __restrict__ x,
+                                                          int n, int m, int ldm, double* __restrict__ part) {
+  const int i0 = blockIdx.x * 64, i1 = min(n, i0 + 64);
+  for (int j = threadIdx.x; j < m; j += kT) {
+    double acc = 0.;
+    for (int i = i0; i < i1; ++i) acc = fma(M[(size_t)i * ldm + j], x[i], acc);
+    part[(size_t)blockIdx.x * ldm + j] = acc;
+  }
+}
+
+__global__ void __launch_bounds__(kT) vif_gemv_reduce_kernel(const double* __restrict__ part, int nb, int m, int ldm,
+                                                            double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (j >= m) return;
+  double s = 0.;
+  for (int b = lane; b < nb; b += 64) s += part[(size_t)b * ldm + j];
+  s = wsum(s);
+  if (lane == 0) out[j] = s;
+}
+
+// out_i = M[:, i] . w (w != nullptr) or M[:, i] . M2[:, i]
+__global__ void __launch_bounds__(kT) vif_coldot_kernel(const double* __restrict__ M, const double* __restrict__ w,
+                                                       const double* __restrict__ M2, int n, int m, int ldm,
+                                                       double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  double s = 0.;
+  for (int q = lane; q < m; q += 64) s = fma(M[(size_t)i * ldm + q], w ? w[q] : M2[(size_t)i * ldm + q], s);
+  s = wsum(s);
+  if (lane == 0) out[i] = s;
+}
+
+// z_i = (-dD_i u_i + e_i) / D_i
+__global__ void __launch_bounds__(kT) vif_zvec_kernel(int n, const double* __restrict__ dD, const double* __restrict__ u,
+                                                     const double* __restrict__ e, const double* __restrict__ D,
+                                                     double* __restrict__ z) {
+  const int i = blockIdx.x * kT + threadIdx.x;
+  if (i >= n) return;
+  z[i] = (e[i] - dD[i] * u[i]) / D[i];
+}
+
+__global__ void __launch_bounds__(kT) vif_add_kernel(int n, const double* __restrict__ a, const double* __restrict__ b,
+                                                    double* __restrict__ out) {
+  const int i = blockIdx.x * kT + threadIdx.x;
+  if (i < n) out[i] = a[i] + b[i];
+}
+
+__global__ void __launch_bounds__(kT) vif_sub_kernel(int n, const double* __restrict__ a, const double* __restrict__ b,
+                                                    double* __restrict__ out) {
+  const int i = blockIdx.x * kT + threadIdx.x;
+  if (i < n) out[i] = a[i] - b[i];
+}
+
+// Per-block partial sums of up to 8 elementwise terms; op 0: a (b) (c) (nullable factors), 1: log a,
+// 2: a (b) / c, 3: a b^2 / c^2, 4: a b / c^2
+struct VifTerms {
+  const double* a[8];
+  const double* b[8];
+  const double* c[8];
+  int op[8];
+};
+
+__global__ void __launch_bounds__(kT) vif_sum_kernel(int n, int nt, VifTerms T, double* __restrict__ part) {
+  __shared__ double red[kT / 64][8];
+  double acc[8];
+#pragma unroll
+  for (int t = 0; t < 8; ++t) acc[t] = 0.;
+  for (int i = blockIdx.x * kT + threadIdx.x; i < n; i += gridDim.x * kT) {
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      if (t >= nt) break;
+      const double av = T.a[t][i];
+      const double bv = T.b[t] ? T.b[t][i] : 1.;
+      const double cv = T.c[t] ? T.c[t][i] : 1.;
+      double v;
+      switch (T.op[t]) {
+        case 1: v = log(av); break;
+        case 2: v = av * bv / cv; break;
+        case 3: v = av * bv * bv / (cv * cv); break;
+        case 4: v = av * bv / (cv * cv); break;
+        default: v = av * bv * cv;
+      }
+      acc[t] += v;
+    }
+  }
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    if (t >= nt) break;
+    const double s = wsum(acc[t]);
+    if (lane == 0) red[w][t] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < nt) {
+    const int t = threadIdx.x;
+    part[(size_t)blockIdx.x * nt + t] = (red[0][t] + red[1][t]) + (red[2][t] + red[3][t]);
+  }
+}
+
+size_t rows_lds_bytes(int nn, bool grad) {
+  const int G = grad ? 3 : 1, S = nn + 1;
+  const int r1 = std::max(G * S * kCh, G * nn * nn);
+  return sizeof(double) * ((size_t)r1 + (size_t)G * S * S);
+}
+
+}  // namespace
+
+VifSolver::VifSolver(int n, int d, const double* d_X, const std::vector<double>& Z, const std::vector<int>& nbr, int nn,
+                     hipStream_t stream)
+    : n_(n), d_(d), nn_(nn), s_(stream), d_X_(d_X) {
+  if (nn < 1) Fatal("full_scale_vecchia needs num_neighbors >= 1");
+  if (nn > kMaxNn) Fatal("num_neighbors = %d > %d is not supported for gp_approx = 'full_scale_vecchia' by gpboost_amd", nn, kMaxNn);
+  if ((long)nbr.size() != (long)n * nn) Fatal("VifSolver: neighbour lists of the wrong size");
+  F_.reset(new FitcSolver(n, d, d_X, Z, stream));
+  m_ = F_->m_;
+  ldm_ = F_->ldm_;
+  const size_t mn = (size_t)ldm_ * n;
+  for (DevBuf<double>* b : {&dK_, &P0_, &P1_, &BK_}) b->alloc(mn);
+  for (DevBuf<double>* b : {&Bv_, &dBv0_, &dBv1_}) b->alloc((size_t)n * nn);
+  for (DevBuf<double>* b : {&D_, &dD0_, &dD1_}) b->alloc(n);
+  vec_.alloc((size_t)kNv * n);
+  mvec_.alloc((size_t)kMv * ldm_);
+  HIP_CHECK(hipMemsetAsync(mvec_.get(), 0, sizeof(double) * kMv * ldm_, stream));
+  const int nbg = (n + 63) / 64, nbs = 512;
+  part_.alloc(std::max<size_t>((size_t)nbg * ldm_, (size_t)nbs * 8));
+  red_.alloc(64);
+  HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_red_), 64 * sizeof(double), hipHostMallocDefault));
+  nbr_.alloc((size_t)n * nn);
+  HIP_CHECK(hipMemcpyAsync(nbr_.get(), nbr.data(), sizeof(int) * nbr.size(), hipMemcpyHostToDevice, stream));
+  // B^T lists: for every column j the rows i (ascending) that hold j among their neighbours, with the slot
+  std::vector<int> tptr(n + 1, 0);
+  for (int i = 0; i < n; ++i)
+    for (int r = 0; r < std::min(i, nn); ++r) ++tptr[nbr[(size_t)i * nn + r] + 1];
+  for (int j = 0; j < n; ++j) tptr[j + 1] += tptr[j];
+  const int nnz = tptr[n];
+  std::vector<int> trow(std::max(nnz, 1)), tslot(std::max(nnz, 1)), fill(tptr.begin(), tptr.end() - 1);
+  for (int i = 0; i < n; ++i)
+    for (int r = 0; r < std::min(i, nn); ++r) {
+      const int j = nbr[(size_t)i * nn + r];
+      trow[fill[j]] = i;
+      tslot[fill[j]] = i * nn + r;
+      ++fill[j];
+    }
+  tptr_.alloc(n + 1);
+  trow_.alloc(trow.size());
+  tslot_.alloc(tslot.size());
+  HIP_CHECK(hipMemcpyAsync(tptr_.get(), tptr.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice, stream));
+  HIP_CHECK(hipMemcpyAsync(trow_.get(), trow.data(), sizeof(int) * trow.size(), hipMemcpyHostToDevice, stream));
+  HIP_CHECK(hipMemcpyAsync(tslot_.get(), tslot.data(), sizeof(int) * tslot.size(), hipMemcpyHostToDevice, stream));
+  lds_bytes_ = rows_lds_bytes(nn, true);
+  for (int cov : {kMatern05, kMatern15, kMatern25, kGaussian})
+    dispatch_cov_vif(cov, [&](auto c) {
+      constexpr int COV = decltype(c)::value;
+      HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&vif_rows_kernel<COV, true>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)rows_lds_bytes(nn, true)));
+      HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&vif_rows_kernel<COV, false>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)rows_lds_bytes(nn, false)));
+    });
+  for (auto& e : ev_) HIP_CHECK(hipEventCreate(&e));
+  HIP_CHECK(hipStreamSynchronize(stream));
+}
+
+VifSolver::~VifSolver() {
+  if (h_red_) (void)hipHostFree(h_red_);
+  for (auto& e : ev_) if (e) (void)hipEventDestroy(e);
+}
+
+void VifSolver::Rows(int cov_type, double var, double phi, bool grad) {
+  VifRowsArgs a{};
+  a.X = d_X_;
+  a.nbr = nbr_.get();
+  a.n = n_; a.d = d_; a.nn = nn_; a.mi = m_; a.ldm = ldm_;
+  a.V = F_->V_.get(); a.P0 = P0_.get(); a.P1 = P1_.get();
+  a.var = var; a.phi = phi;
+  const int G = grad ? 3 : 1, S = nn_ + 1;
+  a.r1 = std::max(G * S * kCh, G * nn_ * nn_);
+  a.Bv = Bv_.get(); a.D = D_.get(); a.dBv0 = dBv0_.get(); a.dBv1 = dBv1_.get(); a.dD0 = dD0_.get(); a.dD1 = dD1_.get();
+  const size_t lds = rows_lds_bytes(nn_, grad);
+  dispatch_cov_vif(cov_type, [&](auto c) {
+    constexpr int COV = decltype(c)::value;
+    if (grad) hipLaunchKernelGGL((vif_rows_kernel<COV, true>), dim3(n_), dim3(kT), lds, s_, a);
+    else hipLaunchKernelGGL((vif_rows_kernel<COV, false>), dim3(n_), dim3(kT), lds, s_, a);
+  });
+  HIP_CHECK(hipGetLastError());
+}
+
+void VifSolver::BRow(const double* in, const double* coef, double self, bool div, double* out) {
+  hipLaunchKernelGGL(vif_brow_kernel, dim3((n_ + 3) / 4), dim3(kT), 0, s_, in, nbr_.get(), coef, D_.get(), n_, nn_, m_,
+                     ldm_, self, div ? 1 : 0, out);
+  HIP_CHECK(hipGetLastError());
+}
+
+void VifSolver::BCol(const double* in, const double* coef, double self, double* out) {
+  hipLaunchKernelGGL(vif_bcol_kernel, dim3((n_ + 3) / 4), dim3(kT), 0, s_, in, tptr_.get(), trow_.get(), tslot_.get(),
+                     coef, n_, m_, ldm_, self, out);
+  HIP_CHECK(hipGetLastError());
+}
+
+void VifSolver::BVec(const double* x, const double* coef, double self, double* out) {
+  hipLaunchKernelGGL(vif_bvec_kernel, dim3((n_ + kT - 1) / kT), dim3(kT), 0, s_, x, nbr_.get(), coef,
+                     static_cast<const double*>(nullptr), n_, nn_, self, out);
+  HIP_CHECK(hipGetLastError());
+}
+
+void VifSolver::BtVec(const double* x, const double* coef, double self, double* out) {
+  hipLaunchKernelGGL(vif_btvec_kernel, dim3((n_ + kT - 1) / kT), dim3(kT), 0, s_, x, tptr_.get(), trow_.get(),
+                     tslot_.get(), coef, n_, self, out);
+  HIP_CHECK(hipGetLastError());
+}
+
+void VifSolver::Gemv(const double* M, const double* x, double* out) {
+  const int nb = (n_ + 63) / 64;
+  hipLaunchKernelGGL(vif_gemv_part_kernel, dim3(nb), dim3(kT), 0, s_, M, x, n_, m_, ldm_, part_.get());
+  hipLaunchKernelGGL(vif_gemv_reduce_kernel, dim3((m_ + 3) / 4), dim3(kT), 0, s_, part_.get(), nb, m_, ldm_, out);
+  HIP_CHECK(hipGetLastError());
+}
+
+void VifSolver::ColDot(const double* M, const double* w, const double* M2, double* out) {
+  hipLaunchKernelGGL(vif_coldot_kernel, dim3((n_ + 3) / 4), dim3(kT), 0, s_, M, w, M2, n_, m_, ldm_, out);
+  HIP_CHECK(hipGetLastError());
+}
+
+void VifSolver::Eval(int cov_type, double var, double phi, const double* d_y, bool want_grad, double* sums,
+                     double* kernel_ms) {
+  FitcSolver& F = *F_;
+  const int n = n_, m = m_, ldm = ldm_;
+  const size_t mn = (size_t)ldm * n;
+  double* red = red_.get();
+  HIP_CHECK(hipEventRecord(ev_[0], s_));
+  // low-rank part (CalcSigmaComps): K_mn, K_mm, K_mm,s, dK_mm, L, L^-1, V = L^-1 K_mn, K_mm,s^-1; red[0] =
+  // log det K_mm,s
+  F.Prior(cov_type, var, phi, red);
+  if (want_grad) {
+    dispatch_cov_vif(cov_type, [&](auto c) {
+      constexpr int COV = decltype(c)::value;
+      hipLaunchKernelGGL((vif_dkmn_kernel<COV>), dim3((m + 63) / 64, (n + 3) / 4), dim3(kT), 0, s_, d_X_, F.dZ_.get(),
+                         n, m, d_, ldm, var, phi, dK_.get());
+    });
+    HIP_CHECK(hipGetLastError());
+    // A = L^-T V; P_0 = L^-1 (K_mn - 1/2 K_mm A), P_1 = L^-1 (dK_mn - 1/2 dK_mm A) (Kd_ as the staging)
+    gemm_f64(s_, m, n, m, 1., F.Li_.get(), ldm, 1, F.V_.get(), ldm, 0, 0., F.A_.get(), ldm, 0, 0, 1, 0);
+    HIP_CHECK(hipMemcpyAsync(F.Kd_.get(), F.Kmn_.get(), sizeof(double) * mn, hipMemcpyDeviceToDevice, s_));
+    gemm_f64(s_, m, n, m, -0.5, F.Kmm_.get(), ldm, 0, F.A_.get(), ldm, 0, 1., F.Kd_.get(), ldm);
+    gemm_f64(s_, m, n, m, 1., F.Li_.get(), ldm, 0, F.Kd_.get(), ldm, 0, 0., P0_.get(), ldm, 0, 1, 0, 0);
+    HIP_CHECK(hipMemcpyAsync(F.Kd_.get(), dK_.get(), sizeof(double) * mn, hipMemcpyDeviceToDevice, s_));
+    gemm_f64(s_, m, n, m, -0.5, F.dKmm_.get(), ldm, 0, F.A_.get(), ldm, 0, 1., F.Kd_.get(), ldm);
+    gemm_f64(s_, m, n, m, 1., F.Li_.get(), ldm, 0, F.Kd_.get(), ldm, 0, 0., P1_.get(), ldm, 0, 1, 0, 0);
+  }
+  // residual Vecchia factor (CalcCovFactorGradientVecchia)
+  Rows(cov_type, var, phi, want_grad);
+  // Woodbury matrix M = K_mm,s + BK^T D^-1 BK (CalcCovFactorFITC_FSA): BK_ = B K, Kd_ = D^-1 B K
+  BRow(F.Kmn_.get(), Bv_.get(), 1., false, BK_.get());
+  BRow(F.Kmn_.get(), Bv_.get(), 1., true, F.Kd_.get());
+  const long mm = (long)ldm * ldm;
+  const int chunks = gemm_f64_splitk(s_, m, m, n, BK_.get(), ldm, 0, F.Kd_.get(), ldm, 1, F.part_.get(), ldm, mm, 2048,
+                                     F.max_chunks_);
+  fitc_wsum(s_, F.part_.get(), chunks, mm, m, ldm, F.Ks_.get(), F.W_.get());
+  chol_lower(s_, F.W_.get(), F.Wi_.get(), m, ldm, F.info_.get());
+  launch_logdet_chol(s_, F.W_.get(), ldm, m, red + 1);
+  trtri_lower(s_, F.W_.get(), F.Wi_.get(), F.T_.get(), 0, m, ldm);
+  fitc_lower_t(s_, F.Wi_.get(), m, ldm, F.WiT_.get());
+  HIP_CHECK(hipEventRecord(ev_[1], s_));
+  // y_aux = R^-1 y - R^-1 K M^-1 K^T R^-1 y with R^-1 = B^T D^-1 B (CalcYAux :8910-8925)
+  double* v = vec_.get();
+  double* u = v;                      // D^-1 B y (vecchia_y)
+  double* ry = v + (size_t)n;         // R^-1 y
+  double* kw = v + 2 * (size_t)n;     // K s
+  double* t1 = v + 3 * (size_t)n;
+  double* rk = v + 4 * (size_t)n;     // R^-1 K s
+  double* yaux = v + 5 * (size_t)n;
+  double* mv = mvec_.get();
+  double* mt = mv;                    // K^T R^-1 y
+  double* ms = mv + ldm;              // w = M^-1 K^T R^-1 y
+  double* mtmp = mv + 2 * (size_t)ldm;
+  hipLaunchKernelGGL(vif_bvec_kernel, dim3((n + kT - 1) / kT), dim3(kT), 0, s_, d_y, nbr_.get(), Bv_.get(), D_.get(), n,
+                     nn_, 1., u);
+  BtVec(u, Bv_.get(), 1., ry);
+  Gemv(F.Kmn_.get(), ry, mt);
+  fitc_chol_solve(s_, F.Wi_.get(), F.WiT_.get(), mt, m, ldm, mtmp, ms);
+  ColDot(F.Kmn_.get(), ms, nullptr, kw);
+  hipLaunchKernelGGL(vif_bvec_kernel, dim3((n + kT - 1) / kT), dim3(kT), 0, s_, kw, nbr_.get(), Bv_.get(), D_.get(), n,
+                     nn_, 1., t1);
+  BtVec(t1, Bv_.get(), 1., rk);
+  hipLaunchKernelGGL(vif_sub_kernel, dim3((n + kT - 1) / kT), dim3(kT), 0, s_, n, ry, rk, yaux);
+  HIP_CHECK(hipGetLastError());
+  const int nbs = std::min(512, (n + kT - 1) / kT);
+  {
+    VifTerms T{};
+    T.a[0] = D_.get(); T.op[0] = 1;                      // sum log D
+    T.a[1] = d_y; T.b[1] = yaux; T.op[1] = 0;            // y^T y_aux
+    hipLaunchKernelGGL(vif_sum_kernel, dim3(nbs), dim3(kT), 0, s_, n, 2, T, part_.get());
+    launch_sum_blocks(part_.get(), nbs, 2, red + 2, s_);
+  }
+  double* mv_a = mv + 3 * (size_t)ldm;    // a = K_mm,s^-1 K^T y_aux
+  double* mv_g[2] = {mv + 4 * (size_t)ldm, mv + 5 * (size_t)ldm};   // dK_k^T y_aux
+  double* mv_k[2] = {mv + 6 * (size_t)ldm, mv + 7 * (size_t)ldm};   // K^T vgy_k
+  if (want_grad) {
+    // the gradient (CalcGradPars_FITC_FSA_GaussLikelihood_Cluster_i, re_model_template.h:1985-2232): M^-1 for
+    // the m x m traces, then per parameter the quadratic and trace sums
+    gemm_f64(s_, m, m, m, 1., F.Wi_.get(), ldm, 1, F.Wi_.get(), ldm, 0, 0., F.Winv_.get(), ldm, 0, 0, 1, 1);
+    double* mt2 = mv + 8 * (size_t)ldm;
+    Gemv(F.Kmn_.get(), yaux, mt2);
+    fitc_chol_solve(s_, F.Li_.get(), F.LiT_.get(), mt2, m, ldm, mtmp, mv_a);
+    HIP_CHECK(hipMemcpyAsync(mv_g[0], mt2, sizeof(double) * m, hipMemcpyDeviceToDevice, s_));
+    Gemv(dK_.get(), yaux, mv_g[1]);
+    for (int p = 0; p < 2; ++p)
+      fitc_mm_terms(s_, F.Kinv_.get(), F.Winv_.get(), F.Kmm_.get(), p == 0 ? F.Kmm_.get() : F.dKmm_.get(), mv_a, m, ldm,
+                    F.part_.get(), red + 8 + 6 * p);
+    // X = B^T D^-1 B K (A_), Xw = M^-1 X (V_), Bw = M^-1 BK (P0_)
+    BCol(F.Kd_.get(), Bv_.get(), 1., F.A_.get());
+    gemm_f64(s_, m, n, m, 1., F.Winv_.get(), ldm, 0, F.A_.get(), ldm, 0, 0., F.V_.get(), ldm);
+    gemm_f64(s_, m, n, m, 1., F.Winv_.get(), ldm, 0, BK_.get(), ldm, 0, 0., P0_.get(), ldm);
+    double* bkw = v + 6 * (size_t)n;   // (B K w)_i
+    double* cg = v + 7 * (size_t)n;    // BK_i . Bw_i
+    ColDot(BK_.get(), ms, nullptr, bkw);
+    ColDot(BK_.get(), nullptr, P0_.get(), cg);
+    for (int p = 0; p < 2; ++p) {
+      const double* dBv = p == 0 ? dBv0_.get() : dBv1_.get();
+      const double* dD = p == 0 ? dD0_.get() : dD1_.get();
+      double* dby = v + 8 * (size_t)n;
+      double* zp = v + 9 * (size_t)n;
+      double* btz = v + 10 * (size_t)n;
+      double* vgy = v + 11 * (size_t)n;
+      double* dbkw = v + 12 * (size_t)n;
+      double* cxw = v + 13 * (size_t)n;
+      double* cf = v + 14 * (size_t)n;
+      // vecchia_grad_y = dB^T u - B^T D^-1 (dD o u) + B^T D^-1 dB y (:2084-2085)
+      BVec(d_y, dBv, 0., dby);
+      hipLaunchKernelGGL(vif_zvec_kernel, dim3((n + kT - 1) / kT), dim3(kT), 0, s_, n, dD, u, dby, D_.get(), zp);
+      BtVec(zp, Bv_.get(), 1., btz);
+      BtVec(u, dBv, 0., vgy);
+      hipLaunchKernelGGL(vif_add_kernel, dim3((n + kT - 1) / kT), dim3(kT), 0, s_, n, vgy, btz, vgy);
+      HIP_CHECK(hipGetLastError());
+      Gemv(F.Kmn_.get(), vgy, mv_k[p]);
+      BVec(kw, dBv, 0., dbkw);                                             // dB K w
+      ColDot(F.V_.get(), nullptr, p == 0 ? F.Kmn_.get() : dK_.get(), cxw);  // (M^-1 X_i) . dK_k,i
+      BRow(F.Kmn_.get(), dBv, 0., false, P1_.get());                      // dB K
+      ColDot(P1_.get(), nullptr, P0_.get(), cf);                           // (dB K)_i . (M^-1 BK)_i
+      VifTerms T{};
+      T.a[0] = d_y; T.b[0] = vgy; T.op[0] = 0;                      // y . vgy
+      T.a[1] = dbkw; T.b[1] = bkw; T.c[1] = D_.get(); T.op[1] = 2;  // w^T F w
+      T.a[2] = dD; T.b[2] = bkw; T.c[2] = D_.get(); T.op[2] = 3;    // sum dD (D^-1 BK w)^2
+      T.a[3] = dD; T.c[3] = D_.get(); T.op[3] = 2;                  // sum dD / D
+      T.a[4] = cxw; T.op[4] = 0;                                     // tr(M^-1 E)
+      T.a[5] = cf; T.c[5] = D_.get(); T.op[5] = 2;                  // tr(M^-1 F)
+      T.a[6] = dD; T.b[6] = cg; T.c[6] = D_.get(); T.op[6] = 4;     // tr(M^-1 G)
+      hipLaunchKernelGGL(vif_sum_kernel, dim3(nbs), dim3(kT), 0, s_, n, 7, T, part_.get());
+      launch_sum_blocks(part_.get(), nbs, 7, red + 20 + 8 * p, s_);
+    }
+  }
+  HIP_CHECK(hipMemcpyAsync(h_red_, red, sizeof(double) * 36, hipMemcpyDeviceToHost, s_));
+  std::vector<double> hm(want_grad ? (size_t)6 * m : 0);
+  if (want_grad) {
+    const double* srcs[6] = {mv_a, mv_g[0], mv_g[1], mv_k[0], mv_k[1], ms};
+    for (int k = 0; k < 6; ++k)
+      HIP_CHECK(hipMemcpyAsync(hm.data() + (size_t)k * m, srcs[k], sizeof(double) * m, hipMemcpyDeviceToHost, s_));
+  }
+  int info = 0;
+  HIP_CHECK(hipMemcpyAsync(&info, F.info_.get(), sizeof(int), hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipEventRecord(ev_[2], s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  float ms0 = 0.f, ms1 = 0.f;
+  HIP_CHECK(hipEventElapsedTime(&ms0, ev_[0], ev_[1]));
+  HIP_CHECK(hipEventElapsedTime(&ms1, ev_[0], ev_[2]));
+  kernel_ms[0] = ms0;
+  kernel_ms[1] = ms1;
+  const double nan = std::numeric_limits<double>::quiet_NaN();
+  if (info != 0) {
+    for (int k = 0; k < 6; ++k) sums[k] = nan;
+    return;
+  }
+  // log det Psi = log det M - log det K_mm,s + sum log D (re_model_template.h:2700-2710)
+  sums[0] = h_red_[1] - h_red_[0] + h_red_[2];
+  sums[1] = h_red_[3];
+  if (!want_grad) {
+    for (int k = 2; k < 6; ++k) sums[k] = nan;
+    return;
+  }
+  auto dot = [&](int x, int y) {
+    double s = 0.;
+    for (int j = 0; j < m; ++j) s += hm[(size_t)x * m + j] * hm[(size_t)y * m + j];
+    return s;
+  };
+  for (int p = 0; p < 2; ++p) {
+    const double* mmt = h_red_ + 8 + 6 * p;   // [tr Kinv Kmm, tr Winv Kmm, tr Kinv dK_mm, tr Winv dK_mm, ., a dK_mm a]
+    const double* g = h_red_ + 20 + 8 * p;
+    // / error_var part (:2040-2041, 2086-2089)
+    const double quad = 0.5 * mmt[5] - dot(1 + p, 0) + 0.5 * g[0] - dot(3 + p, 5) + g[1] - 0.5 * g[2];
+    // trace part (:2037-2038, 2085, 2215-2218): -1/2 tr(K_mm,s^-1 dK_mm) + 1/2 sum dD / D + 1/2 tr(M^-1 dM)
+    const double tr = -0.5 * mmt[2] + 0.5 * g[3] + 0.5 * (2. * g[4] + 2. * g[5] - g[6] + mmt[3]);
+    sums[2 + p] = quad;
+    sums[4 + p] = 2. * tr;
+  }
+}
+
+void VifSolver::GetFactor(double* D, double* Bv) const {
+  HIP_CHECK(hipMemcpyAsync(D, D_.get(), sizeof(double) * n_, hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipMemcpyAsync(Bv, Bv_.get(), sizeof(double) * n_ * nn_, hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+}
+
+}  // namespace gpb_amd
