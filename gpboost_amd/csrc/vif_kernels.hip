@@ -26,7 +26,6 @@ namespace {
 
 constexpr int kT = 256;
 constexpr int kCh = 32;      // m-rows per LDS staging chunk in the row kernel
-constexpr int kEpt = 16;     // Gram entries per thread per pass
 constexpr int kMaxNn = 48;   // neighbours per row (LDS budget of the row kernel)
 constexpr int kNv = 16;      // n-vector scratch slots
 constexpr int kMv = 12;      // m-vector scratch slots
@@ -112,46 +111,78 @@ __global__ void __launch_bounds__(kT) vif_rows_kernel(VifRowsArgs a) {
   const int nn = a.nn, k = min(i, nn), S = k + 1;
   if (tid < k) idx[tid] = a.nbr[(size_t)i * nn + tid];
   if (tid == k) idx[k] = i;
-  double* st = lds;            // staging [g][a][q] (kCh), later C, dC0, dC1 (k x k each)
+  double* st = lds;            // staging [g][q][a] (kCh x Sp each), later C, dC0, dC1 (k x k each)
   double* gram = lds + a.r1;   // [g][a][b] = V_a . M^g_b, S x S each
+  // Gram blocks in 4 x 4 register tiles (8 LDS reads per 16 FMAs); the staging rows are padded to
+  // Sp = round_up(S, 4) + 2 doubles so that the tiles of one wave fall on distinct banks
+  const int Sp = ((S + 3) & ~3) + 2, T4 = (S + 3) >> 2, NT = G * T4 * T4;
+  for (int t = tid; t < G * kCh * (Sp - S); t += kT) {
+    const int w = Sp - S;
+    const int gq = t / w;
+    st[gq * Sp + S + (t - gq * w)] = 0.;
+  }
   __syncthreads();
-  const int E = G * S * S;
-  for (int e0 = 0; e0 < E; e0 += kT * kEpt) {
-    double acc[kEpt];
+  double acc[2][16];
 #pragma unroll
-    for (int j = 0; j < kEpt; ++j) acc[j] = 0.;
-    for (int q0 = 0; q0 < a.mi; q0 += kCh) {
-      const int tot = G * S * kCh;
-      for (int t = tid; t < tot; t += kT) {
-        const int g = t / (S * kCh);
-        const int r = t - g * S * kCh;
-        const int p = r / kCh;
-        const int q = q0 + (r - p * kCh);
-        const double* M = g == 0 ? a.V : (g == 1 ? a.P0 : a.P1);
-        st[t] = q < a.mi ? M[(size_t)idx[p] * a.ldm + q] : 0.;
-      }
-      __syncthreads();
+  for (int s2 = 0; s2 < 2; ++s2)
 #pragma unroll
-      for (int j = 0; j < kEpt; ++j) {
-        const int e = e0 + j * kT + tid;
-        if (e < E) {
-          const int g = e / (S * S);
-          const int r = e - g * S * S;
-          const int p = r / S, b = r - p * S;
-          const double* L = st + p * kCh;
-          const double* R = st + (size_t)g * S * kCh + b * kCh;
-          double s = 0.;
-#pragma unroll 8
-          for (int q = 0; q < kCh; ++q) s = fma(L[q], R[q], s);
-          acc[j] += s;
+    for (int j = 0; j < 16; ++j) acc[s2][j] = 0.;
+  for (int q0 = 0; q0 < a.mi; q0 += kCh) {
+    const int tot = G * S * kCh;
+    for (int t = tid; t < tot; t += kT) {
+      const int g = t / (S * kCh);
+      const int r = t - g * S * kCh;
+      const int p = r / kCh;
+      const int q = r - p * kCh;
+      const double* M = g == 0 ? a.V : (g == 1 ? a.P0 : a.P1);
+      st[(g * kCh + q) * Sp + p] = q0 + q < a.mi ? M[(size_t)idx[p] * a.ldm + q0 + q] : 0.;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const int tile = tid + s2 * kT;
+      if (tile < NT) {
+        const int g = tile / (T4 * T4);
+        const int r = tile - g * T4 * T4;
+        const int pa = r / T4, pb = r - pa * T4;
+        const double* L = st + 4 * pa;
+        const double* R = st + (size_t)g * kCh * Sp + 4 * pb;
+        for (int q = 0; q < kCh; ++q) {
+          const double l0 = L[q * Sp], l1 = L[q * Sp + 1], l2 = L[q * Sp + 2], l3 = L[q * Sp + 3];
+          const double r0 = R[q * Sp], r1 = R[q * Sp + 1], r2 = R[q * Sp + 2], r3 = R[q * Sp + 3];
+          acc[s2][0] = fma(l0, r0, acc[s2][0]);
+          acc[s2][1] = fma(l0, r1, acc[s2][1]);
+          acc[s2][2] = fma(l0, r2, acc[s2][2]);
+          acc[s2][3] = fma(l0, r3, acc[s2][3]);
+          acc[s2][4] = fma(l1, r0, acc[s2][4]);
+          acc[s2][5] = fma(l1, r1, acc[s2][5]);
+          acc[s2][6] = fma(l1, r2, acc[s2][6]);
+          acc[s2][7] = fma(l1, r3, acc[s2][7]);
+          acc[s2][8] = fma(l2, r0, acc[s2][8]);
+          acc[s2][9] = fma(l2, r1, acc[s2][9]);
+          acc[s2][10] = fma(l2, r2, acc[s2][10]);
+          acc[s2][11] = fma(l2, r3, acc[s2][11]);
+          acc[s2][12] = fma(l3, r0, acc[s2][12]);
+          acc[s2][13] = fma(l3, r1, acc[s2][13]);
+          acc[s2][14] = fma(l3, r2, acc[s2][14]);
+          acc[s2][15] = fma(l3, r3, acc[s2][15]);
         }
       }
-      __syncthreads();
     }
+    __syncthreads();
+  }
 #pragma unroll
-    for (int j = 0; j < kEpt; ++j) {
-      const int e = e0 + j * kT + tid;
-      if (e < E) gram[e] = acc[j];
+  for (int s2 = 0; s2 < 2; ++s2) {
+    const int tile = tid + s2 * kT;
+    if (tile < NT) {
+      const int g = tile / (T4 * T4);
+      const int r = tile - g * T4 * T4;
+      const int pa = r / T4, pb = r - pa * T4;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        const int p = 4 * pa + (j >> 2), b = 4 * pb + (j & 3);
+        if (p < S && b < S) gram[g * S * S + p * S + b] = acc[s2][j];
+      }
     }
   }
   __syncthreads();
@@ -435,10 +466,15 @@ __global__ void __launch_bounds__(kT) vif_sum_kernel(int n, int nt, VifTerms T, 
   }
 }
 
+// staging / residual-matrix region (doubles) for neighbour sets of up to nn + 1 points
+int rows_r1(int nn, bool grad) {
+  const int G = grad ? 3 : 1, S = nn + 1, Sp = ((S + 3) & ~3) + 2;
+  return std::max(G * kCh * Sp, G * nn * nn);
+}
+
 size_t rows_lds_bytes(int nn, bool grad) {
   const int G = grad ? 3 : 1, S = nn + 1;
-  const int r1 = std::max(G * S * kCh, G * nn * nn);
-  return sizeof(double) * ((size_t)r1 + (size_t)G * S * S);
+  return sizeof(double) * ((size_t)rows_r1(nn, grad) + (size_t)G * S * S);
 }
 
 }  // namespace
@@ -510,8 +546,7 @@ void VifSolver::Rows(int cov_type, double var, double phi, bool grad) {
   a.n = n_; a.d = d_; a.nn = nn_; a.mi = m_; a.ldm = ldm_;
   a.V = F_->V_.get(); a.P0 = P0_.get(); a.P1 = P1_.get();
   a.var = var; a.phi = phi;
-  const int G = grad ? 3 : 1, S = nn_ + 1;
-  a.r1 = std::max(G * S * kCh, G * nn_ * nn_);
+  a.r1 = rows_r1(nn_, grad);
   a.Bv = Bv_.get(); a.D = D_.get(); a.dBv0 = dBv0_.get(); a.dBv1 = dBv1_.get(); a.dD0 = dD0_.get(); a.dD1 = dD1_.get();
   const size_t lds = rows_lds_bytes(nn_, grad);
   dispatch_cov_vif(cov_type, [&](auto c) {
