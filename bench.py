@@ -635,6 +635,92 @@ def fitc_laplace_cpu_baseline() -> dict | None:
         os.unlink(path)
 
 
+VIF_N, VIF_M, VIF_NN, VIF_CPU_N = 100_000, 200, 30, 20_000   # the reference's VIF defaults (200 / 30)
+
+
+def vif_flops(n: int, m: int, nn: int) -> float:
+    """Algorithmic flops of one VIF nll + gradient: the residual rows' Gram blocks V_S^T [V P_0 P_1]_S
+    (3 (nn + 1)^2 m FMAs per point) and the m^2 n GEMMs (V, A, K_mm A, dK_mm A, two L^-1 products, the
+    Woodbury Gram, M^-1 X, M^-1 BK: 14 m^2 n); the small Cholesky solves and sparse passes are not counted."""
+    return 2.0 * 3 * (nn + 1) ** 2 * m * n + 14.0 * m * m * n
+
+
+def vif_leg(steps: int, cpu: bool) -> dict:
+    """full-scale Vecchia ("VIF", gp_approx='full_scale_vecchia') with the reference's
+    defaults (200 kmeans++ inducing points, 30 neighbours) on the headline's n=100k coordinates and spatial
+    response, the L-BFGS unit (nll + gradient, sigma2 profiled)."""
+    import numpy as np
+
+    from gpboost_amd import GPModel, synthetic
+    X = synthetic.bench_coords(VIF_N)
+    Y = synthetic.bench_spatial_gaussian_y(X)
+    t0 = time.perf_counter()
+    gm = GPModel(gp_coords=X, cov_function="exponential", gp_approx="full_scale_vecchia", num_ind_points=VIF_M,
+                 num_neighbors=VIF_NN, seed=0)
+    t_construct = time.perf_counter() - t0
+    gm.neg_log_likelihood_and_grad(THETA, Y, profile_sigma2=True)   # warm-up
+    gm.last_kernel_ms()
+    ts, kms = [], []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        nll, g, _ = gm.neg_log_likelihood_and_grad(THETA, None, profile_sigma2=True)
+        ts.append(time.perf_counter() - t0)
+        kms.append(gm.last_kernel_ms()[1])
+    t = float(np.median(ts))
+    fl = vif_flops(VIF_N, VIF_M, VIF_NN)
+    kt = float(np.median(kms)) * 1e-3
+    leg = {"metric": "VIF (full-scale Vecchia) nll + grad evals/sec, n=100k, m=200, nn=30", "value": 1.0 / t,
+           "unit": "evals/s", "steps": steps, "ms_per_step": t * 1e3,
+           "config": {"workload": "vif_gaussian_lbfgs_unit", "n": VIF_N, "num_ind_points": VIF_M,
+                      "num_neighbors": VIF_NN, "ind_points_selection": "kmeans++", "cov_function": "exponential",
+                      "theta": THETA, "construction_s": round(t_construct, 3), "nll": nll,
+                      "grad": [float(x) for x in g]},
+           "roofline": {"bound": "fp64", "achieved": fl / kt / 1e12, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": fl / kt / 1e12 / FP64_PEAK_TFLOPS, "traffic": None, "device_ms": kt * 1e3,
+                        "kernel": "whole device evaluation (vif_rows_kernel residual factor, MFMA GEMMs, sparse "
+                                  "B / B^T passes)",
+                        "algorithmic_flops_per_eval": fl}}
+    del gm
+    if cpu:
+        leg["cpu_baseline"] = vif_cpu_baseline()
+    return leg
+
+
+def vif_cpu_baseline() -> dict | None:
+    """The reference's VIF path (oracle/_ref/ref_harness gp_approx=full_scale_vecchia) on this host at
+    n=20000 (m=200, nn=30); `value_scaled_n100k` scales it by 20000/100000 (the unit is linear in n)."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(harness):
+        return None
+    import numpy as np
+
+    from gpboost_amd import synthetic
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", str(os.cpu_count() or 1))), 16))
+    X = synthetic.bench_coords(VIF_CPU_N)
+    Y = synthetic.bench_spatial_gaussian_y(X)
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(np.array([X.shape[0], X.shape[1]], dtype=np.int32).tobytes())
+        f.write(np.ascontiguousarray(X.T).tobytes())
+        f.write(np.ascontiguousarray(Y).tobytes())
+        path = f.name
+    try:
+        out = subprocess.run([harness, path, "cov_fct=exponential", "gp_approx=full_scale_vecchia",
+                              f"num_ind_points={VIF_M}", f"num_neighbors={VIF_NN}", "mode=lbfgs", "reps=1",
+                              "cov_pars=" + ",".join(map(str, THETA))], capture_output=True, text=True, timeout=600,
+                             env=dict(os.environ, OMP_NUM_THREADS=str(threads)), check=True)
+        r = json.loads(out.stdout)
+        t = r["median_time"]
+        return {"value": 1.0 / t, "unit": "evals/s", "cores": threads, "kind": "reference",
+                "sample": f"1 VIF L-BFGS-unit eval at n={VIF_CPU_N}, m={VIF_M}, nn={VIF_NN} ({t:.2f} s; "
+                          f"construction not timed)",
+                "value_scaled_n100k": (1.0 / t) * VIF_CPU_N / VIF_N}
+    except Exception as e:  # noqa: BLE001
+        sys.stderr.write(f"reference VIF CPU baseline failed: {e}\n")
+        return None
+    finally:
+        os.unlink(path)
+
+
 def dense_cpu_baseline() -> dict | None:
     """The reference's dense path (oracle/_ref/ref_harness) on this host, bounded sample at
     n=4000; `value_scaled_n20000` scales it by (4000/20000)^3 (the unit is n^3-bound)."""
@@ -821,7 +907,8 @@ def main():
         return
     if args.only_fitc:
         print(json.dumps({"fitc": fitc_leg(args.steps, not args.no_cpu_baseline),
-                          "fitc_laplace": fitc_laplace_leg(3, not args.no_cpu_baseline)}))
+                          "fitc_laplace": fitc_laplace_leg(3, not args.no_cpu_baseline),
+                          "vif": vif_leg(args.steps, not args.no_cpu_baseline)}))
         return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -959,6 +1046,7 @@ def main():
     if world == 1 and not args.no_fitc:
         line["fitc"] = fitc_leg(5, not args.no_cpu_baseline)
         line["fitc_laplace"] = fitc_laplace_leg(3, not args.no_cpu_baseline)
+        line["vif"] = vif_leg(5, not args.no_cpu_baseline)
     if world == 1 and not args.no_latent:
         del gm
         if os.environ.get("GPBOOST_AMD_DUMP_MAPS"):   # symbolising a crash under a tracer: the loaded libraries

@@ -16,10 +16,12 @@
 //   y_aux, log det              re_model_template.h:8898-8935, 2698-2714
 //   gradient                    re_model_template.h:1985-2232 (CalcGradPars_FITC_FSA_GaussLikelihood_Cluster_i)
 // The reference runs these with Eigen sparse products, cuBLAS / cuSPARSE offloads (cuda_kernel.cu:613-941).
-// This build: one workgroup per row for the residual factor (the neighbour set's columns of V and of the
-// derivative factors staged through LDS in m-chunks, the Gram blocks and the small Cholesky solves in
-// LDS), sparse B / B^T products over contiguous m-vectors (one wave per point), and every m x n / m x m
-// product on the fp64 MFMA GEMM (split-K for the m x m Woodbury Gram).
+// This build: one wave per row for the residual factor with the neighbour set's Gram blocks V_S^T [V P_0
+// P_1]_S on the fp64 MFMA (operands loaded straight from the m x n matrices; sets of up to 32 points, the
+// reference's default 30 neighbours; larger sets: a 256-thread LDS-staged register-tile form), the small
+// Cholesky and solves in LDS / registers of that wave; sparse B / B^T products over contiguous m-vectors
+// (one wave per point; B^T vectors from the factor values gathered into column order); every m x n /
+// m x m product on the fp64 MFMA GEMM (split-K for the m x m Woodbury Gram).
 //
 // HBM layout: every m x n matrix column-major with leading dimension ldm = round_up(m, 64) (point i's m
 // entries contiguous), the B / D factor and its derivatives as n x nn value rows beside the neighbour lists.
@@ -52,12 +54,14 @@ class VifSolver {
 
  private:
   void Rows(int cov_type, double var, double phi, bool grad);
-  // out = B in (self = 1) or dB in (self = 0) over m-vector columns; div: then times D^-1
-  void BRow(const double* in, const double* coef, double self, bool div, double* out);
+  // out = B in (self = 1) or dB in (self = 0) over m-vector columns; div: then times D^-1; out_div
+  // (nullable): the same columns times D^-1 as a second output
+  void BRow(const double* in, const double* coef, double self, bool div, double* out, double* out_div = nullptr);
   // out = B^T in (self = 1) or dB^T in (self = 0) over m-vector columns
   void BCol(const double* in, const double* coef, double self, double* out);
   void BVec(const double* x, const double* coef, double self, double* out);
-  void BtVec(const double* x, const double* coef, double self, double* out);
+  // out = B^T x (self = 1) or dB^T x (self = 0), coefT: the factor's values in column order (BvT_ ...)
+  void BtVec(const double* x, const double* coefT, double self, double* out);
   void Gemv(const double* M, const double* x, double* out);   // out (m) = M x, M m x n
   void ColDot(const double* M, const double* w, const double* M2, double* out);   // out_i = M_i . (w | M2_i)
 
@@ -68,6 +72,8 @@ class VifSolver {
   DevBuf<int> nbr_, tptr_, trow_, tslot_;
   DevBuf<double> dK_, P0_, P1_, BK_;                 // m x n (ldm)
   DevBuf<double> Bv_, dBv0_, dBv1_;                   // n x nn
+  DevBuf<double> BvT_, dBvT0_, dBvT1_;                // the same values in column (B^T) order
+  int nnz_ = 0;
   DevBuf<double> D_, dD0_, dD1_;                      // n
   DevBuf<double> vec_;                                // n-vectors (scratch)
   DevBuf<double> mvec_;                               // m-vectors (scratch)

@@ -13,6 +13,8 @@
 #include <algorithm>
 #include <cmath>
 #include <limits>
+#include <cstdlib>
+#include <string>
 #include <type_traits>
 
 #include "cov.h"
@@ -47,6 +49,14 @@ __device__ __forceinline__ double wsum(double v) {
   return v;
 }
 
+// LDS ordering among the lanes of one wave (its LDS operations execute in order; the fences keep the
+// compiler from moving them across)
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
 __device__ __forceinline__ double dist_pts(const double* X, int d, int a, int b) {
   double s = 0.;
   for (int q = 0; q < d; ++q) {
@@ -54,6 +64,26 @@ __device__ __forceinline__ double dist_pts(const double* X, int d, int a, int b)
     s += t * t;
   }
   return sqrt(s);
+}
+
+// In-place Cholesky of the k x k matrix C (row stride ld, lower) by one wave, row-oriented (left-looking):
+// step j forms L_jj from row j's dot product, then every lane t > j forms L_tj = (C_tj - L_t . L_j) / L_jj
+// from its own row; the dot products read rows written in earlier steps only, so their LDS loads pipeline.
+__device__ __forceinline__ void wave_chol(double* C, int ld, int k, int lane) {
+  for (int j = 0; j < k; ++j) {
+    if (lane == j) {
+      double sacc = C[j * ld + j];
+      for (int q = 0; q < j; ++q) sacc -= C[j * ld + q] * C[j * ld + q];
+      C[j * ld + j] = sqrt(sacc);
+    }
+    wave_sync();
+    if (lane > j && lane < k) {
+      double sacc = C[lane * ld + j];
+      for (int q = 0; q < j; ++q) sacc -= C[lane * ld + q] * C[j * ld + q];
+      C[lane * ld + j] = sacc / C[j * ld + j];
+    }
+    wave_sync();
+  }
 }
 
 // dK_mn / dlog(phi) (m x n, ld ldm)
@@ -99,12 +129,13 @@ struct VifRowsArgs {
 //   dC = dk(N, N) - (G + G^T),  dc = dk(N, i) - (V_N . P_i + P_N . V_i),  dd0 = [k = var] var - 2 V_i . P_i
 //   dA = C^-1 (dc - dC A),  dB(i, N) = -dA,  dD_i = dd0 - (dA . c + A . dc)
 // One 256-thread workgroup per row: the Gram blocks of the neighbour set S = N + {i} accumulate over
-// m-chunks staged in LDS; the k x k Cholesky and the solves run in LDS with a barrier per step.
+// m-chunks staged in LDS; then one wave factors the k x k matrix and solves (right-hand sides in
+// registers, pivots broadcast by lane shuffles).
 template <int COV, bool GRAD>
 __global__ void __launch_bounds__(kT) vif_rows_kernel(VifRowsArgs a) {
   extern __shared__ double lds[];
   __shared__ int idx[kMaxNn + 1];
-  __shared__ double vecs[7][kMaxNn];   // c, dc0, dc1, A / x, r0 / dA0, r1 / dA1, spare
+  __shared__ double vecs[4][kMaxNn];   // c, dc0, dc1, A
   __shared__ double scal[4];
   constexpr int G = GRAD ? 3 : 1;
   const int i = blockIdx.x, tid = threadIdx.x;
@@ -204,7 +235,6 @@ __global__ void __launch_bounds__(kT) vif_rows_kernel(VifRowsArgs a) {
     double c, dc;
     cov_dcov<COV>(dist_pts(a.X, a.d, idx[p], i), a.var, a.phi, c, dc);
     vecs[0][p] = c - gram[p * S + k];
-    vecs[3][p] = vecs[0][p];
     if (GRAD) {
       vecs[1][p] = c - (gram[SS + p * S + k] + gram[SS + k * S + p]);
       vecs[2][p] = dc - (gram[2 * SS + p * S + k] + gram[2 * SS + k * S + p]);
@@ -218,72 +248,60 @@ __global__ void __launch_bounds__(kT) vif_rows_kernel(VifRowsArgs a) {
     }
   }
   __syncthreads();
-  // Cholesky C = L L^T in place (lower, row-major k x k)
-  for (int j = 0; j < k; ++j) {
-    if (tid == 0) C[j * k + j] = sqrt(C[j * k + j]);
-    __syncthreads();
-    if (tid > j && tid < k) C[tid * k + j] /= C[j * k + j];
-    __syncthreads();
-    if (tid > j && tid < k) {
-      const double l = C[tid * k + j];
-      for (int s2 = j + 1; s2 <= tid; ++s2) C[tid * k + s2] -= l * C[s2 * k + j];
-    }
-    __syncthreads();
-  }
-  // solve L L^T x = b for nrhs right-hand sides in vecs[3 + r] (thread = (rhs, row))
-  auto solve = [&](int nrhs) {
-    const int r = tid >> 6, row = tid & 63;
+  // From here one wave: the Cholesky factor in LDS (lane = row), the right-hand sides in registers with
+  // the pivot entries broadcast by lane shuffles; wave-scope ordering instead of workgroup barriers.
+  if (tid >= 64) return;
+  const int lane = tid;
+  wave_chol(C, k, k, lane);
+  // L L^T x = b for the lane-distributed right-hand sides x[0 .. NR)
+  auto solve = [&](double* x, int nr) {
     for (int j = 0; j < k; ++j) {
-      if (r < nrhs && row == j) vecs[3 + r][j] /= C[j * k + j];
-      __syncthreads();
-      if (r < nrhs && row > j && row < k) vecs[3 + r][row] -= C[row * k + j] * vecs[3 + r][j];
-      __syncthreads();
+      const double ljj = C[j * k + j];
+      const double lij = lane < k ? C[lane * k + j] : 0.;
+      for (int r = 0; r < nr; ++r) {
+        const double xj = __shfl(x[r], j, 64) / ljj;
+        if (lane == j) x[r] = xj;
+        else if (lane > j) x[r] -= lij * xj;
+      }
     }
     for (int j = k - 1; j >= 0; --j) {
-      if (r < nrhs && row == j) vecs[3 + r][j] /= C[j * k + j];
-      __syncthreads();
-      if (r < nrhs && row < j) vecs[3 + r][row] -= C[j * k + row] * vecs[3 + r][j];
-      __syncthreads();
+      const double ljj = C[j * k + j];
+      const double lji = lane < j ? C[j * k + lane] : 0.;
+      for (int r = 0; r < nr; ++r) {
+        const double xj = __shfl(x[r], j, 64) / ljj;
+        if (lane == j) x[r] = xj;
+        else if (lane < j) x[r] -= lji * xj;
+      }
     }
   };
-  solve(1);   // vecs[3] = A
+  double xa[1] = {lane < k ? vecs[0][lane] : 0.};
+  solve(xa, 1);   // A
+  double xd[2] = {0., 0.};
   if (GRAD) {
-    // r_k = dc_k - dC_k A into vecs[4 + k], then dA_k = C^-1 r_k in place (the solve uses slots 4, 5 as
-    // right-hand sides 1, 2; slot 3 (A) is passed through untouched by restricting to rhs 1..2)
-    for (int e = tid; e < 2 * k; e += kT) {
-      const int kk = e / k, p = e - kk * k;
-      const double* dC = kk == 0 ? dC0 : dC1;
-      double s = vecs[1 + kk][p];
-      for (int b = 0; b < k; ++b) s -= dC[p * k + b] * vecs[3][b];
-      vecs[4 + kk][p] = s;
-    }
-    __syncthreads();
-    {
-      const int r = tid >> 6, row = tid & 63;
-      const bool act = r >= 1 && r <= 2;
-      for (int j = 0; j < k; ++j) {
-        if (act && row == j) vecs[3 + r][j] /= C[j * k + j];
-        __syncthreads();
-        if (act && row > j && row < k) vecs[3 + r][row] -= C[row * k + j] * vecs[3 + r][j];
-        __syncthreads();
+    // r_k = dc_k - dC_k A, then dA_k = C^-1 r_k
+    if (lane < k) vecs[3][lane] = xa[0];
+    wave_sync();
+    if (lane < k) {
+      double r0 = vecs[1][lane], r1 = vecs[2][lane];
+      for (int b = 0; b < k; ++b) {
+        const double ab = vecs[3][b];
+        r0 -= dC0[lane * k + b] * ab;
+        r1 -= dC1[lane * k + b] * ab;
       }
-      for (int j = k - 1; j >= 0; --j) {
-        if (act && row == j) vecs[3 + r][j] /= C[j * k + j];
-        __syncthreads();
-        if (act && row < j) vecs[3 + r][row] -= C[j * k + row] * vecs[3 + r][j];
-        __syncthreads();
-      }
+      xd[0] = r0;
+      xd[1] = r1;
     }
+    solve(xd, 2);
   }
-  if (tid < 64) {
+  {
     // D_i = d0 - A . c; dD_k = dd0_k - (dA_k . c + A . dc_k) (wave sums in a fixed order)
-    const int p = tid;
+    const int p = lane;
     double s0 = 0., s1 = 0., s2 = 0.;
     if (p < k) {
-      s0 = vecs[3][p] * vecs[0][p];
+      s0 = xa[0] * vecs[0][p];
       if (GRAD) {
-        s1 = vecs[4][p] * vecs[0][p] + vecs[3][p] * vecs[1][p];
-        s2 = vecs[5][p] * vecs[0][p] + vecs[3][p] * vecs[2][p];
+        s1 = xd[0] * vecs[0][p] + xa[0] * vecs[1][p];
+        s2 = xd[1] * vecs[0][p] + xa[0] * vecs[2][p];
       }
     }
     s0 = wsum(s0);
@@ -293,10 +311,10 @@ __global__ void __launch_bounds__(kT) vif_rows_kernel(VifRowsArgs a) {
     }
     const size_t row = (size_t)i * nn;
     if (p < nn) {
-      a.Bv[row + p] = p < k ? -vecs[3][p] : 0.;
+      a.Bv[row + p] = p < k ? -xa[0] : 0.;
       if (GRAD) {
-        a.dBv0[row + p] = p < k ? -vecs[4][p] : 0.;
-        a.dBv1[row + p] = p < k ? -vecs[5][p] : 0.;
+        a.dBv0[row + p] = p < k ? -xd[0] : 0.;
+        a.dBv1[row + p] = p < k ? -xd[1] : 0.;
       }
     }
     if (p == 0) {
@@ -309,20 +327,182 @@ __global__ void __launch_bounds__(kT) vif_rows_kernel(VifRowsArgs a) {
   }
 }
 
-// out[:, i] = (self in[:, i] + sum_r coef[i nn + r] in[:, nbr[i nn + r]]) (/ D_i): one wave per column
+typedef double vif_double4 __attribute__((ext_vector_type(4)));
+
+// The same row factor for neighbour sets of at most 32 points (nn <= 31, the reference's default 30) with
+// the Gram blocks on the fp64 MFMA: one wave per row, V_S^T [V P_0 P_1]_S as 16x16x4 tiles whose A / B
+// operands are loaded straight from the m x n matrices (lane l: point S[l & 15] (+ 16), q = q0 + l / 4 ..
+// i.e. the 4 consecutive entries of 16 contiguous columns per load), 12 MFMAs per 4 entries of m. The
+// accumulators go to LDS once; the residual matrix C overwrites the V^T V block in place and dC_k is
+// never stored (r_k = dc_k - dC_k A is formed from the P blocks and the recomputed base covariances).
+template <int COV, bool GRAD>
+__global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
+  constexpr int LD = 33;   // gram row stride
+  __shared__ double gram[GRAD ? 3 : 1][32 * LD];
+  __shared__ int idx[32];
+  __shared__ double vecs[4][32];   // c, dc0, dc1, A
+  const int i = blockIdx.x, lane = threadIdx.x;
+  const int nn = a.nn, k = min(i, nn), S = k + 1;
+  if (lane < 32) idx[lane] = lane < k ? a.nbr[(size_t)i * nn + lane] : i;
+  wave_sync();
+  const int m0 = lane & 15, kq = lane >> 4;
+  const size_t c0 = (size_t)idx[m0] * a.ldm, c1 = (size_t)idx[16 + m0] * a.ldm;
+  vif_double4 acc[GRAD ? 3 : 1][2][2];
+#pragma unroll
+  for (int g = 0; g < (GRAD ? 3 : 1); ++g)
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y) acc[g][x][y] = vif_double4{0., 0., 0., 0.};
+  const double* V = a.V;
+  const double* P0 = a.P0;
+  const double* P1 = a.P1;
+#pragma unroll 4
+  for (int q0 = 0; q0 < a.mi; q0 += 4) {
+    const int q = q0 + kq;
+    const bool ok = q < a.mi;
+    const double v0 = ok ? V[c0 + q] : 0., v1 = ok ? V[c1 + q] : 0.;
+    acc[0][0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, v0, acc[0][0][0], 0, 0, 0);
+    acc[0][0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, v1, acc[0][0][1], 0, 0, 0);
+    acc[0][1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1, v0, acc[0][1][0], 0, 0, 0);
+    acc[0][1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1, v1, acc[0][1][1], 0, 0, 0);
+    if (GRAD) {
+      const double p00 = ok ? P0[c0 + q] : 0., p01 = ok ? P0[c1 + q] : 0.;
+      const double p10 = ok ? P1[c0 + q] : 0., p11 = ok ? P1[c1 + q] : 0.;
+      acc[GRAD ? 1 : 0][0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, p00, acc[GRAD ? 1 : 0][0][0], 0, 0, 0);
+      acc[GRAD ? 1 : 0][0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, p01, acc[GRAD ? 1 : 0][0][1], 0, 0, 0);
+      acc[GRAD ? 1 : 0][1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1, p00, acc[GRAD ? 1 : 0][1][0], 0, 0, 0);
+      acc[GRAD ? 1 : 0][1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1, p01, acc[GRAD ? 1 : 0][1][1], 0, 0, 0);
+      acc[GRAD ? 2 : 0][0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, p10, acc[GRAD ? 2 : 0][0][0], 0, 0, 0);
+      acc[GRAD ? 2 : 0][0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, p11, acc[GRAD ? 2 : 0][0][1], 0, 0, 0);
+      acc[GRAD ? 2 : 0][1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1, p10, acc[GRAD ? 2 : 0][1][0], 0, 0, 0);
+      acc[GRAD ? 2 : 0][1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1, p11, acc[GRAD ? 2 : 0][1][1], 0, 0, 0);
+    }
+  }
+  // C/D layout: row = (lane >> 4) + 4 r, col = lane & 15 within each 16 x 16 tile
+#pragma unroll
+  for (int g = 0; g < (GRAD ? 3 : 1); ++g)
+#pragma unroll
+    for (int x = 0; x < 2; ++x)
+#pragma unroll
+      for (int y = 0; y < 2; ++y)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) gram[g][(16 * x + kq + 4 * r) * LD + 16 * y + m0] = acc[g][x][y][r];
+  wave_sync();
+  const double var = a.var, phi = a.phi;
+  // c, dc_k (column k of the blocks) and the diagonal terms, before C overwrites the V^T V block
+  double d0 = 0., dd0 = 0., dd1 = 0.;
+  if (lane < k) {
+    double c, dc;
+    cov_dcov<COV>(dist_pts(a.X, a.d, idx[lane], i), var, phi, c, dc);
+    vecs[0][lane] = c - gram[0][lane * LD + k];
+    if (GRAD) {
+      vecs[1][lane] = c - (gram[1][lane * LD + k] + gram[1][k * LD + lane]);
+      vecs[2][lane] = dc - (gram[2][lane * LD + k] + gram[2][k * LD + lane]);
+    }
+  }
+  d0 = 1. + var - gram[0][k * LD + k];
+  if (GRAD) {
+    dd0 = var - 2. * gram[1][k * LD + k];
+    dd1 = -2. * gram[2][k * LD + k];
+  }
+  wave_sync();
+  double* C = gram[0];   // C(p, b) = C[p LD + b], in place of V^T V
+  for (int e = lane; e < k * k; e += 64) {
+    const int p = e / k, b = e - p * k;
+    double c = var, dc = 0.;
+    if (p != b) cov_dcov<COV>(dist_pts(a.X, a.d, idx[p], idx[b]), var, phi, c, dc);
+    C[p * LD + b] = c + (p == b ? 1. : 0.) - C[p * LD + b];
+  }
+  wave_sync();
+  wave_chol(C, LD, k, lane);
+  auto solve = [&](double* x, int nr) {
+    for (int j = 0; j < k; ++j) {
+      const double ljj = C[j * LD + j];
+      const double lij = lane < k ? C[lane * LD + j] : 0.;
+      for (int r = 0; r < nr; ++r) {
+        const double xj = __shfl(x[r], j, 64) / ljj;
+        if (lane == j) x[r] = xj;
+        else if (lane > j) x[r] -= lij * xj;
+      }
+    }
+    for (int j = k - 1; j >= 0; --j) {
+      const double ljj = C[j * LD + j];
+      const double lji = lane < j ? C[j * LD + lane] : 0.;
+      for (int r = 0; r < nr; ++r) {
+        const double xj = __shfl(x[r], j, 64) / ljj;
+        if (lane == j) x[r] = xj;
+        else if (lane < j) x[r] -= lji * xj;
+      }
+    }
+  };
+  double xa[1] = {lane < k ? vecs[0][lane] : 0.};
+  solve(xa, 1);
+  double xd[2] = {0., 0.};
+  if (GRAD) {
+    if (lane < k) vecs[3][lane] = xa[0];
+    wave_sync();
+    if (lane < k) {
+      // r_k = dc_k - dC_k A with dC_0 = k(N, N) - (G_0 + G_0^T), dC_1 = dk(N, N) - (G_1 + G_1^T)
+      double r0 = vecs[1][lane], r1 = vecs[2][lane];
+      for (int b = 0; b < k; ++b) {
+        double c = var, dc = 0.;
+        if (b != lane) cov_dcov<COV>(dist_pts(a.X, a.d, idx[lane], idx[b]), var, phi, c, dc);
+        const double ab = vecs[3][b];
+        r0 -= (c - (gram[1][lane * LD + b] + gram[1][b * LD + lane])) * ab;
+        r1 -= (dc - (gram[2][lane * LD + b] + gram[2][b * LD + lane])) * ab;
+      }
+      xd[0] = r0;
+      xd[1] = r1;
+    }
+    solve(xd, 2);
+  }
+  double s0 = 0., s1 = 0., s2 = 0.;
+  if (lane < k) {
+    s0 = xa[0] * vecs[0][lane];
+    if (GRAD) {
+      s1 = xd[0] * vecs[0][lane] + xa[0] * vecs[1][lane];
+      s2 = xd[1] * vecs[0][lane] + xa[0] * vecs[2][lane];
+    }
+  }
+  s0 = wsum(s0);
+  if (GRAD) {
+    s1 = wsum(s1);
+    s2 = wsum(s2);
+  }
+  const size_t row = (size_t)i * nn;
+  if (lane < nn) {
+    a.Bv[row + lane] = lane < k ? -xa[0] : 0.;
+    if (GRAD) {
+      a.dBv0[row + lane] = lane < k ? -xd[0] : 0.;
+      a.dBv1[row + lane] = lane < k ? -xd[1] : 0.;
+    }
+  }
+  if (lane == 0) {
+    a.D[i] = d0 - s0;
+    if (GRAD) {
+      a.dD0[i] = dd0 - s1;
+      a.dD1[i] = dd1 - s2;
+    }
+  }
+}
+
+// out[:, i] = (self in[:, i] + sum_r coef[i nn + r] in[:, nbr[i nn + r]]) (/ D_i); out2 (nullable) gets
+// the same column divided by D_i: one wave per column
 __global__ void __launch_bounds__(kT) vif_brow_kernel(const double* __restrict__ in, const int* __restrict__ nbr,
                                                      const double* __restrict__ coef, const double* __restrict__ D,
                                                      int n, int nn, int m, int ldm, double self, int div,
-                                                     double* __restrict__ out) {
+                                                     double* __restrict__ out, double* __restrict__ out2) {
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (i >= n) return;
   const int k = min(i, nn);
-  const double sc = div ? 1. / D[i] : 1.;
+  const double inv = (div || out2) ? 1. / D[i] : 1.;
   for (int q = lane; q < m; q += 64) {
     double s = self != 0. ? self * in[(size_t)i * ldm + q] : 0.;
     for (int r = 0; r < k; ++r) s = fma(coef[(size_t)i * nn + r], in[(size_t)nbr[(size_t)i * nn + r] * ldm + q], s);
-    out[(size_t)i * ldm + q] = s * sc;
+    out[(size_t)i * ldm + q] = div ? s * inv : s;
+    if (out2) out2[(size_t)i * ldm + q] = s * inv;
   }
 }
 
@@ -353,15 +533,26 @@ __global__ void __launch_bounds__(kT) vif_bvec_kernel(const double* __restrict__
   out[i] = D ? s / D[i] : s;
 }
 
+// out_j = self x_j + sum over column j's entries of coefT[t] x[trow[t]] (coefT: the values in column order):
+// 16 lanes per column stride its entry list (contiguous trow / coefT reads), fixed-order shuffle sum
 __global__ void __launch_bounds__(kT) vif_btvec_kernel(const double* __restrict__ x, const int* __restrict__ tptr,
-                                                      const int* __restrict__ trow, const int* __restrict__ tslot,
-                                                      const double* __restrict__ coef, int n, double self,
-                                                      double* __restrict__ out) {
-  const int j = blockIdx.x * kT + threadIdx.x;
+                                                      const int* __restrict__ trow, const double* __restrict__ coefT,
+                                                      int n, double self, double* __restrict__ out) {
+  const int sub = threadIdx.x & 15;
+  const int j = blockIdx.x * (kT / 16) + (threadIdx.x >> 4);
   if (j >= n) return;
-  double s = self != 0. ? self * x[j] : 0.;
-  for (int t = tptr[j]; t < tptr[j + 1]; ++t) s = fma(coef[tslot[t]], x[trow[t]], s);
-  out[j] = s;
+  double s = 0.;
+  for (int t = tptr[j] + sub; t < tptr[j + 1]; t += 16) s = fma(coefT[t], x[trow[t]], s);
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 16);
+  if (sub == 0) out[j] = self != 0. ? fma(self, x[j], s) : s;
+}
+
+// coefT[t] = coef[tslot[t]] (the row-major factor values in column order)
+__global__ void __launch_bounds__(kT) vif_gather_kernel(int nnz, const int* __restrict__ tslot,
+                                                       const double* __restrict__ coef, double* __restrict__ coefT) {
+  const int t = blockIdx.x * kT + threadIdx.x;
+  if (t < nnz) coefT[t] = coef[tslot[t]];
 }
 
 // part[b ldm + j] = sum_{i in chunk b} M[j, i] x_i
@@ -515,6 +706,8 @@ VifSolver::VifSolver(int n, int d, const double* d_X, const std::vector<double>&
       tslot[fill[j]] = i * nn + r;
       ++fill[j];
     }
+  nnz_ = nnz;
+  for (DevBuf<double>* b : {&BvT_, &dBvT0_, &dBvT1_}) b->alloc(std::max(nnz, 1));
   tptr_.alloc(n + 1);
   trow_.alloc(trow.size());
   tslot_.alloc(tslot.size());
@@ -549,17 +742,26 @@ void VifSolver::Rows(int cov_type, double var, double phi, bool grad) {
   a.r1 = rows_r1(nn_, grad);
   a.Bv = Bv_.get(); a.D = D_.get(); a.dBv0 = dBv0_.get(); a.dBv1 = dBv1_.get(); a.dD0 = dD0_.get(); a.dD1 = dD1_.get();
   const size_t lds = rows_lds_bytes(nn_, grad);
+  const char* form = std::getenv("GPBOOST_AMD_VIF_ROWS");   // "lds": the LDS-staged VALU form (A/B)
+  const bool lds_form = form != nullptr && std::string(form) == "lds";
+  const bool mfma = nn_ <= 31 && !lds_form;   // neighbour sets of <= 32 points: the MFMA Gram form
   dispatch_cov_vif(cov_type, [&](auto c) {
     constexpr int COV = decltype(c)::value;
-    if (grad) hipLaunchKernelGGL((vif_rows_kernel<COV, true>), dim3(n_), dim3(kT), lds, s_, a);
-    else hipLaunchKernelGGL((vif_rows_kernel<COV, false>), dim3(n_), dim3(kT), lds, s_, a);
+    if (mfma) {
+      if (grad) hipLaunchKernelGGL((vif_rows_mfma_kernel<COV, true>), dim3(n_), dim3(64), 0, s_, a);
+      else hipLaunchKernelGGL((vif_rows_mfma_kernel<COV, false>), dim3(n_), dim3(64), 0, s_, a);
+    } else if (grad) {
+      hipLaunchKernelGGL((vif_rows_kernel<COV, true>), dim3(n_), dim3(kT), lds, s_, a);
+    } else {
+      hipLaunchKernelGGL((vif_rows_kernel<COV, false>), dim3(n_), dim3(kT), lds, s_, a);
+    }
   });
   HIP_CHECK(hipGetLastError());
 }
 
-void VifSolver::BRow(const double* in, const double* coef, double self, bool div, double* out) {
+void VifSolver::BRow(const double* in, const double* coef, double self, bool div, double* out, double* out_div) {
   hipLaunchKernelGGL(vif_brow_kernel, dim3((n_ + 3) / 4), dim3(kT), 0, s_, in, nbr_.get(), coef, D_.get(), n_, nn_, m_,
-                     ldm_, self, div ? 1 : 0, out);
+                     ldm_, self, div ? 1 : 0, out, out_div);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -575,9 +777,9 @@ void VifSolver::BVec(const double* x, const double* coef, double self, double* o
   HIP_CHECK(hipGetLastError());
 }
 
-void VifSolver::BtVec(const double* x, const double* coef, double self, double* out) {
-  hipLaunchKernelGGL(vif_btvec_kernel, dim3((n_ + kT - 1) / kT), dim3(kT), 0, s_, x, tptr_.get(), trow_.get(),
-                     tslot_.get(), coef, n_, self, out);
+void VifSolver::BtVec(const double* x, const double* coefT, double self, double* out) {
+  hipLaunchKernelGGL(vif_btvec_kernel, dim3((n_ + kT / 16 - 1) / (kT / 16)), dim3(kT), 0, s_, x, tptr_.get(),
+                     trow_.get(), coefT, n_, self, out);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -619,11 +821,19 @@ void VifSolver::Eval(int cov_type, double var, double phi, const double* d_y, bo
     gemm_f64(s_, m, n, m, -0.5, F.dKmm_.get(), ldm, 0, F.A_.get(), ldm, 0, 1., F.Kd_.get(), ldm);
     gemm_f64(s_, m, n, m, 1., F.Li_.get(), ldm, 0, F.Kd_.get(), ldm, 0, 0., P1_.get(), ldm, 0, 1, 0, 0);
   }
-  // residual Vecchia factor (CalcCovFactorGradientVecchia)
+  // residual Vecchia factor (CalcCovFactorGradientVecchia), its values also in column order for B^T
   Rows(cov_type, var, phi, want_grad);
+  if (nnz_ > 0) {
+    const int nbt = (nnz_ + kT - 1) / kT;
+    hipLaunchKernelGGL(vif_gather_kernel, dim3(nbt), dim3(kT), 0, s_, nnz_, tslot_.get(), Bv_.get(), BvT_.get());
+    if (want_grad) {
+      hipLaunchKernelGGL(vif_gather_kernel, dim3(nbt), dim3(kT), 0, s_, nnz_, tslot_.get(), dBv0_.get(), dBvT0_.get());
+      hipLaunchKernelGGL(vif_gather_kernel, dim3(nbt), dim3(kT), 0, s_, nnz_, tslot_.get(), dBv1_.get(), dBvT1_.get());
+    }
+    HIP_CHECK(hipGetLastError());
+  }
   // Woodbury matrix M = K_mm,s + BK^T D^-1 BK (CalcCovFactorFITC_FSA): BK_ = B K, Kd_ = D^-1 B K
-  BRow(F.Kmn_.get(), Bv_.get(), 1., false, BK_.get());
-  BRow(F.Kmn_.get(), Bv_.get(), 1., true, F.Kd_.get());
+  BRow(F.Kmn_.get(), Bv_.get(), 1., false, BK_.get(), F.Kd_.get());
   const long mm = (long)ldm * ldm;
   const int chunks = gemm_f64_splitk(s_, m, m, n, BK_.get(), ldm, 0, F.Kd_.get(), ldm, 1, F.part_.get(), ldm, mm, 2048,
                                      F.max_chunks_);
@@ -647,13 +857,13 @@ void VifSolver::Eval(int cov_type, double var, double phi, const double* d_y, bo
   double* mtmp = mv + 2 * (size_t)ldm;
   hipLaunchKernelGGL(vif_bvec_kernel, dim3((n + kT - 1) / kT), dim3(kT), 0, s_, d_y, nbr_.get(), Bv_.get(), D_.get(), n,
                      nn_, 1., u);
-  BtVec(u, Bv_.get(), 1., ry);
+  BtVec(u, BvT_.get(), 1., ry);
   Gemv(F.Kmn_.get(), ry, mt);
   fitc_chol_solve(s_, F.Wi_.get(), F.WiT_.get(), mt, m, ldm, mtmp, ms);
   ColDot(F.Kmn_.get(), ms, nullptr, kw);
   hipLaunchKernelGGL(vif_bvec_kernel, dim3((n + kT - 1) / kT), dim3(kT), 0, s_, kw, nbr_.get(), Bv_.get(), D_.get(), n,
                      nn_, 1., t1);
-  BtVec(t1, Bv_.get(), 1., rk);
+  BtVec(t1, BvT_.get(), 1., rk);
   hipLaunchKernelGGL(vif_sub_kernel, dim3((n + kT - 1) / kT), dim3(kT), 0, s_, n, ry, rk, yaux);
   HIP_CHECK(hipGetLastError());
   const int nbs = std::min(512, (n + kT - 1) / kT);
@@ -700,8 +910,8 @@ void VifSolver::Eval(int cov_type, double var, double phi, const double* d_y, bo
       // vecchia_grad_y = dB^T u - B^T D^-1 (dD o u) + B^T D^-1 dB y (:2084-2085)
       BVec(d_y, dBv, 0., dby);
       hipLaunchKernelGGL(vif_zvec_kernel, dim3((n + kT - 1) / kT), dim3(kT), 0, s_, n, dD, u, dby, D_.get(), zp);
-      BtVec(zp, Bv_.get(), 1., btz);
-      BtVec(u, dBv, 0., vgy);
+      BtVec(zp, BvT_.get(), 1., btz);
+      BtVec(u, p == 0 ? dBvT0_.get() : dBvT1_.get(), 0., vgy);
       hipLaunchKernelGGL(vif_add_kernel, dim3((n + kT - 1) / kT), dim3(kT), 0, s_, n, vgy, btz, vgy);
       HIP_CHECK(hipGetLastError());
       Gemv(F.Kmn_.get(), vgy, mv_k[p]);

@@ -138,3 +138,35 @@ def test_vif_refusals():
     y = synthetic.bench_spatial_gaussian_y(X)
     with pytest.raises(GPBoostError, match="full_scale_vecchia"):
         gm.predict(y=y, gp_coords_pred=X[:5], cov_pars=[0.3, 1.0, 0.1])
+
+
+@pytest.mark.parametrize("name", ["vif_matern15_n2000_m100_nn20", "vif_matern25_n3000_m200_nn30"])
+def test_vif_row_forms_agree(monkeypatch, name):
+    """The residual rows by the MFMA Gram form (neighbour sets <= 32, default) and by the LDS-staged VALU
+    form (GPBOOST_AMD_VIF_ROWS=lds; used for nn > 31): the same factor up to summation order."""
+    case = GOLDEN[name]
+    X, y = _data(case["n"])
+    out = {}
+    for form in ("lds", "mfma"):
+        monkeypatch.setenv("GPBOOST_AMD_VIF_ROWS", form)
+        out[form] = _model(case, X).neg_log_likelihood_and_grad(case["cov_pars"], y)
+    assert abs(out["lds"][0] - out["mfma"][0]) <= 1e-11 * abs(out["lds"][0])
+    np.testing.assert_allclose(out["mfma"][1], out["lds"][1], rtol=1e-9)
+
+
+def test_vif_many_neighbours_vs_oracle():
+    """nn = 40 > 31: the LDS-staged row form (neighbour sets beyond one 32-point MFMA tile pair)."""
+    from oracle import oracle as O
+    from oracle.vif_oracle import vif_nll_grad
+    n, m, nn = 1500, 60, 40
+    X, y = _data(n)
+    gm = GPModel(gp_coords=X, cov_function="matern", cov_fct_shape=1.5, gp_approx="full_scale_vecchia",
+                 num_ind_points=m, num_neighbors=nn, seed=4)
+    cp = [0.2, 1.0, 0.15]
+    nll, g, _ = gm.neg_log_likelihood_and_grad(cp, y)
+    perm, Z, _ = O.vif_inducing_points(X, m, "kmeans++", 4, True)
+    xv = X[perm]
+    nb = O.find_neighbors(xv, nn)
+    o = vif_nll_grad(xv, y[perm], nb, Z, 1, O.transform(1, cp), mode=0)
+    assert abs(nll - o["nll"]) <= 1e-9 * abs(o["nll"]), (nll, o["nll"])
+    np.testing.assert_allclose(g, o["grad"], rtol=1e-7, atol=1e-9 * abs(o["nll"]))
