@@ -341,6 +341,7 @@ __global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
   __shared__ double gram[GRAD ? 3 : 1][32 * LD];
   __shared__ int idx[32];
   __shared__ double vecs[4][32];   // c, dc0, dc1, A
+  __shared__ double rdg[32];       // 1 / L_jj
   const int i = blockIdx.x, lane = threadIdx.x;
   const int nn = a.nn, k = min(i, nn), S = k + 1;
   if (lane < 32) idx[lane] = lane < k ? a.nbr[(size_t)i * nn + lane] : i;
@@ -357,7 +358,7 @@ __global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
   const double* V = a.V;
   const double* P0 = a.P0;
   const double* P1 = a.P1;
-#pragma unroll 4
+#pragma unroll 8
   for (int q0 = 0; q0 < a.mi; q0 += 4) {
     const int q = q0 + kq;
     const bool ok = q < a.mi;
@@ -407,30 +408,52 @@ __global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
     dd1 = -2. * gram[2][k * LD + k];
   }
   wave_sync();
-  double* C = gram[0];   // C(p, b) = C[p LD + b], in place of V^T V
-  for (int e = lane; e < k * k; e += 64) {
-    const int p = e / k, b = e - p * k;
-    double c = var, dc = 0.;
-    if (p != b) cov_dcov<COV>(dist_pts(a.X, a.d, idx[p], idx[b]), var, phi, c, dc);
-    C[p * LD + b] = c + (p == b ? 1. : 0.) - C[p * LD + b];
+  double* C = gram[0];   // C(p, b) = C[p LD + b], in place of V^T V; dC_k in place of the P blocks
+  double dv0[16], dv1[16];
+#pragma unroll
+  for (int t = 0; t < 16; ++t) {
+    const int e = lane + 64 * t;
+    if (e < k * k) {
+      const int p = e / k, b = e - p * k;
+      double c = var, dc = 0.;
+      if (p != b) cov_dcov<COV>(dist_pts(a.X, a.d, idx[p], idx[b]), var, phi, c, dc);
+      C[p * LD + b] = c + (p == b ? 1. : 0.) - C[p * LD + b];
+      if (GRAD) {
+        dv0[t] = c - (gram[GRAD ? 1 : 0][p * LD + b] + gram[GRAD ? 1 : 0][b * LD + p]);
+        dv1[t] = dc - (gram[GRAD ? 2 : 0][p * LD + b] + gram[GRAD ? 2 : 0][b * LD + p]);
+      }
+    }
   }
   wave_sync();
+  if (GRAD) {
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const int e = lane + 64 * t;
+      if (e < k * k) {
+        const int p = e / k, b = e - p * k;
+        gram[GRAD ? 1 : 0][p * LD + b] = dv0[t];
+        gram[GRAD ? 2 : 0][p * LD + b] = dv1[t];
+      }
+    }
+  }
   wave_chol(C, LD, k, lane);
+  if (lane < k) rdg[lane] = 1. / C[lane * LD + lane];
+  wave_sync();
   auto solve = [&](double* x, int nr) {
     for (int j = 0; j < k; ++j) {
-      const double ljj = C[j * LD + j];
+      const double rjj = rdg[j];
       const double lij = lane < k ? C[lane * LD + j] : 0.;
       for (int r = 0; r < nr; ++r) {
-        const double xj = __shfl(x[r], j, 64) / ljj;
+        const double xj = __shfl(x[r], j, 64) * rjj;
         if (lane == j) x[r] = xj;
         else if (lane > j) x[r] -= lij * xj;
       }
     }
     for (int j = k - 1; j >= 0; --j) {
-      const double ljj = C[j * LD + j];
+      const double rjj = rdg[j];
       const double lji = lane < j ? C[j * LD + lane] : 0.;
       for (int r = 0; r < nr; ++r) {
-        const double xj = __shfl(x[r], j, 64) / ljj;
+        const double xj = __shfl(x[r], j, 64) * rjj;
         if (lane == j) x[r] = xj;
         else if (lane < j) x[r] -= lji * xj;
       }
@@ -446,11 +469,9 @@ __global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
       // r_k = dc_k - dC_k A with dC_0 = k(N, N) - (G_0 + G_0^T), dC_1 = dk(N, N) - (G_1 + G_1^T)
       double r0 = vecs[1][lane], r1 = vecs[2][lane];
       for (int b = 0; b < k; ++b) {
-        double c = var, dc = 0.;
-        if (b != lane) cov_dcov<COV>(dist_pts(a.X, a.d, idx[lane], idx[b]), var, phi, c, dc);
         const double ab = vecs[3][b];
-        r0 -= (c - (gram[1][lane * LD + b] + gram[1][b * LD + lane])) * ab;
-        r1 -= (dc - (gram[2][lane * LD + b] + gram[2][b * LD + lane])) * ab;
+        r0 -= gram[GRAD ? 1 : 0][lane * LD + b] * ab;
+        r1 -= gram[GRAD ? 2 : 0][lane * LD + b] * ab;
       }
       xd[0] = r0;
       xd[1] = r1;
