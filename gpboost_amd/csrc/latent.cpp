@@ -2,6 +2,7 @@
 #include "latent.h"
 
 #include <algorithm>
+#include <random>
 #include <cmath>
 #include <cstdlib>
 #include <cstdio>
@@ -512,7 +513,8 @@ void LatentVecchia::EnsureProbes(const IterativeConfig& cfg) {
 }
 
 void LatentVecchia::PredVarSim(int nsim, int t, double delta, int cg_max, uint64_t seed, int n_pred, int mp,
-                               const int* nbr_vo, const double* d_Bpo, double* acc, double* d_V) {
+                               const int* nbr_vo, const double* d_Bpo, double* acc, double* d_V,
+                               std::mt19937* ref_gen) {
   if (!factor_ready_) Fatal("predictive variances need an evaluated latent model (mode and factor)");
   if (world_ > 1) Fatal("latent predictive variances are only available on single-rank models");
   t = std::max(1, std::min({t, nsim, 64}));
@@ -527,11 +529,37 @@ void LatentVecchia::PredVarSim(int nsim, int t, double delta, int cg_max, uint64
   launch_sqrt_vec(n_, d_Dinv_.get(), d_sdi.get(), s_);   // D^-1/2
   launch_sqrt_vec(n_, d_W_.get(), d_sw.get(), s_);       // W^1/2 (likelihoods.h:6661: W >= 0 checked there)
   Block& b = GetBlock(2, t, cg_max);
+  // ref_gen: the reference's own stream (PredictLaplaceApproxVecchia on one thread, likelihoods.h:6668-6700):
+  // rng = mt19937(unif{0 .. 2147483646}(cg_generator_)), per draw a fresh normal_distribution giving
+  // z1_j, z2_j interleaved over the latent variables in the model order (host, libstdc++ as the reference)
+  std::mt19937 rng;
+  std::vector<double> h1, h2;
+  if (ref_gen) {
+    std::uniform_int_distribution<> unif(0, 2147483646);
+    rng.seed((std::mt19937::result_type)unif(*ref_gen));
+    h1.assign((size_t)n_ * t, 0.);
+    h2.assign((size_t)n_ * t, 0.);
+  }
   for (int done = 0; done < nsim; done += t) {
     const int tc = std::min(t, nsim - done);   // the last block's extra columns are zero right-hand sides
-    launch_gen_normal(n_, t, seed, 1, done, d_e1.get(), s_);
-    launch_gen_normal(n_, t, seed, 2, done, d_e2.get(), s_);
-    if (tc < t) {   // columns >= tc: zero draws (zero right-hand side -> z = 0, no contribution)
+    if (ref_gen) {
+      std::fill(h1.begin(), h1.end(), 0.);
+      std::fill(h2.begin(), h2.end(), 0.);
+      for (int c = 0; c < tc; ++c) {
+        std::normal_distribution<double> nd(0., 1.);
+        for (int j = 0; j < n_; ++j) {
+          const size_t e = (size_t)lab_[j] * t + c;
+          h1[e] = nd(rng);
+          h2[e] = nd(rng);
+        }
+      }
+      HIP_CHECK(hipMemcpyAsync(d_e1.get(), h1.data(), sizeof(double) * h1.size(), hipMemcpyHostToDevice, s_));
+      HIP_CHECK(hipMemcpyAsync(d_e2.get(), h2.data(), sizeof(double) * h2.size(), hipMemcpyHostToDevice, s_));
+    } else {
+      launch_gen_normal(n_, t, seed, 1, done, d_e1.get(), s_);
+      launch_gen_normal(n_, t, seed, 2, done, d_e2.get(), s_);
+    }
+    if (tc < t && !ref_gen) {   // columns >= tc: zero draws (zero right-hand side -> z = 0, no contribution)
       for (int c = tc; c < t; ++c) {
         HIP_CHECK(hipMemset2DAsync(d_e1.get() + c, sizeof(double) * t, 0, sizeof(double), n_, s_));
         HIP_CHECK(hipMemset2DAsync(d_e2.get() + c, sizeof(double) * t, 0, sizeof(double), n_, s_));
@@ -543,6 +571,7 @@ void LatentVecchia::PredVarSim(int nsim, int t, double delta, int cg_max, uint64
     if (pr.nan) Fatal("NaN or Inf in the conjugate gradient solves of the predictive-variance simulation");
     if (acc) launch_pred_sq_acc(n_pred, mp, t, d_nb.get(), d_Bpo, d_z.get(), d_acc.get(), s_);
     if (d_V) launch_pred_samples(n_pred, mp, t, tc, d_nb.get(), d_Bpo, d_z.get(), d_V, n_pred, done, s_);
+    if (ref_gen) HIP_CHECK(hipStreamSynchronize(s_));   // h1 / h2 are refilled for the next block
   }
   if (acc) HIP_CHECK(hipMemcpyAsync(acc, d_acc.get(), sizeof(double) * n_pred, hipMemcpyDeviceToHost, s_));
   HIP_CHECK(hipStreamSynchronize(s_));

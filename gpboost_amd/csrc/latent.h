@@ -19,6 +19,7 @@
 #include <map>
 #include <memory>
 #include <stdexcept>
+#include <random>
 #include <vector>
 
 #include "common.h"
@@ -130,9 +131,10 @@ class LatentVecchia : public LatentSolverBase {
   // draws of (Bpo z)_p^2 (host, n_pred). Uses the factor, W and preconditioner of the last Eval.
   // nbr_vo: host n_pred x mp neighbour indices (latent Vecchia rows), d_Bpo: device n_pred x mp.
   // d_V (nullable, device n_pred x nsim column-major): the draws Bpo z themselves (predictive
-  // covariance, cond_all); acc (nullable) as before.
+  // covariance, cond_all); acc (nullable) as before. ref_gen (nullable): draw the reference's one-thread
+  // stream from this generator on the host instead of the counter-based GPU draws.
   void PredVarSim(int nsim, int t, double delta, int cg_max, uint64_t seed, int n_pred, int mp, const int* nbr_vo,
-                  const double* d_Bpo, double* acc, double* d_V = nullptr);
+                  const double* d_Bpo, double* acc, double* d_V = nullptr, std::mt19937* ref_gen = nullptr);
 
   // Probe-column sharding (SURVEY.md §8e Option A): rank r of `world` runs the probe columns
   // [t r / world, t (r+1) / world) of every SLQ block — padded to ceil(t / world) columns, so

@@ -231,6 +231,14 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
 
 void REModelAMD::UseDevice() const { HIP_CHECK(hipSetDevice(device_)); }
 
+// GPBOOST_AMD_PRED_DRAWS=reference: the predictive-variance simulation of Laplace models draws the
+// reference's own one-thread stream (the likelihood's default-seeded cg_generator_, likelihoods.h:6668-6700)
+// on the host, so results equal the reference run with one thread; default: counter-based GPU draws.
+std::mt19937* REModelAMD::RefDraws() {
+  const char* e = std::getenv("GPBOOST_AMD_PRED_DRAWS");
+  return e != nullptr && std::string(e) == "reference" ? &pred_ref_gen_ : nullptr;
+}
+
 void REModelAMD::EnsureStructure() {
   if (vecchia_ && !structure_built_) {
     BuildVecchiaStructure();
@@ -522,7 +530,7 @@ void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred,
     // + the simulation term of PredictLaplaceApproxVecchia (iterative, likelihoods.h:6628-6746)
     std::vector<double> acc(n_pred);
     latent_->PredVarSim(nsim_var_pred_, iter.num_rand_vec_trace, iter.cg_delta_conv, iter.cg_max_num_it,
-                        pred_seed_++, n_pred, mp, nb.data(), dB.get(), acc.data());
+                        pred_seed_++, n_pred, mp, nb.data(), dB.get(), acc.data(), nullptr, RefDraws());
     for (int p = 0; p < n_pred; ++p) h[n_pred + p] += acc[p] / nsim_var_pred_;
     if (predict_response) {
       ResponseTransform(n_pred, h.data(), h.data() + n_pred, nullptr);
@@ -586,7 +594,7 @@ void REModelAMD::PredictLatentSim(int n, int n_pred, int mp, const std::vector<i
     DevBuf<double> dBpo(Bpo.size()), dV((size_t)n_pred * nsim);
     HIP_CHECK(hipMemcpyAsync(dBpo.get(), Bpo.data(), sizeof(double) * Bpo.size(), hipMemcpyHostToDevice, stream_));
     latent_->PredVarSim(nsim, iter.num_rand_vec_trace, iter.cg_delta_conv, iter.cg_max_num_it, pred_seed_++, n_pred,
-                        mp, nb.data(), dBpo.get(), nullptr, dV.get());
+                        mp, nb.data(), dBpo.get(), nullptr, dV.get(), RefDraws());
     latent_pred_moments(stream_, n_pred, cond_all ? Bp.data() : nullptr, D.data(), dV.get(), nsim, want_var,
                         predict_cov_mat, var.data(), cov.data());
   }

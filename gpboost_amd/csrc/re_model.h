@@ -278,6 +278,8 @@ class REModelAMD {
   std::unique_ptr<FitcLaplace> fitc_lap_;   // gp_approx = "fitc", non-Gaussian likelihood (Laplace)
   std::unique_ptr<VifSolver> vif_;          // gp_approx = "full_scale_vecchia" (Gaussian likelihood)
   std::mt19937 fitc_rng_;              // the model's generator after the inducing-point selection
+  std::mt19937 pred_ref_gen_;          // the likelihood's cg_generator_ (default seed) for reference draws
+  std::mt19937* RefDraws();
   std::unique_ptr<LatentVecchia> latent_;
   // the latent solver of a Laplace model: the Vecchia (iterative) or the FITC (Cholesky) one
   LatentSolverBase* lat() const {
