@@ -122,12 +122,15 @@ def test_predict_pred_first_matches_reference(name):
     reference itself (tests/golden/golden_pred_types.json): means at 1e-9. The reference reads the
     variances / covariance off the inverse of its AMD-permuted sparse Cholesky factor
     (Vecchia_utils.cpp:2220-2237, chol_sp_mat_t = SimplicialLLT<..., AMDOrdering>, type_defs.h:38),
-    so they come out in that permuted order; this build returns them in prediction-point order. The
-    parity check is therefore on the permutation-invariant content: the sorted variances and the
-    sorted entries of the covariance matrix (and its sorted diagonal), at 1e-9."""
+    so they come out in that permuted order; this build returns them in prediction-point order. They
+    are checked ELEMENTWISE at 1e-9 against the dense restatement oracle/pred_first_oracle.py, which
+    test_oracle_pred_first.py pins to the reference (its covariance equals the reference's under one
+    permutation of the prediction points, elementwise), plus the permutation-invariant content against
+    the reference directly."""
     import json
     import os
     from gpboost_amd import GPModel, synthetic
+    from oracle.pred_first_oracle import pred_first
     with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "golden_pred_types.json")) as f:
         case = json.load(f)[name]
     sp = case["spec"]
@@ -143,12 +146,16 @@ def test_predict_pred_first_matches_reference(name):
                       predict_cov_mat=want_cov, predict_response=case["response"])
     mu = np.asarray(case["mean"])
     np.testing.assert_allclose(pred["mu"], mu, rtol=1e-9, atol=1e-9 * np.abs(mu).max())
+    ct = O.cov_code(sp["cov_fct"], float(sp["shape"]))
+    _, ocov = pred_first(X, y, xp, ct, O.transform(ct, case["cov_pars"]), int(sp["num_neighbors"]), case["mp"],
+                         case["response"])
     if want_cov:
         c = np.asarray(case["cov"]).reshape(npred, npred)
-        np.testing.assert_allclose(np.sort(np.diag(pred["cov"])), np.sort(np.diag(c)), rtol=1e-9)
+        np.testing.assert_allclose(pred["cov"], ocov, rtol=1e-9, atol=1e-9 * np.abs(ocov).max())
         np.testing.assert_allclose(np.sort(pred["cov"].ravel()), np.sort(c.ravel()), rtol=1e-9,
                                    atol=1e-9 * np.abs(c).max())
     else:
+        np.testing.assert_allclose(pred["var"], np.diag(ocov), rtol=1e-9)
         np.testing.assert_allclose(np.sort(pred["var"]), np.sort(case["var"]), rtol=1e-9)
 
 
