@@ -371,7 +371,7 @@ class GPModel:
     def summary(self, std_err=False):
         """Print a summary of the fitted parameters (reference basic.py:5709-5770, GP models):
         log-likelihood, AIC and BIC after a fit, covariance parameters (with standard deviations
-        when std_err, dense Gaussian models only) and auxiliary parameters."""
+        when std_err, Gaussian models with gp_approx "none" / "vecchia") and auxiliary parameters."""
         import pandas as pd
         cp = self.get_cov_pars(std_err=std_err)
         rows = cp if std_err else cp.reshape(1, -1)

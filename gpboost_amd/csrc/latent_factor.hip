@@ -137,7 +137,7 @@ __global__ void __launch_bounds__(block_threads<K>()) latent_factor_kernel(Laten
   const int group_id = wave * G + g;
   const int d = a.d;
   const double var = a.var, phi = a.phi;
-  const double cdiag = var * a.jitter;
+  const double cdiag = var * a.jitter + a.nugget;
   const bool want_grad = a.dBv != nullptr;
 
   double* Cp = smem + group_id * group_lds_doubles<K>();
@@ -210,8 +210,16 @@ __global__ void __launch_bounds__(block_threads<K>()) latent_factor_kernel(Laten
     const double av_r = back_solve<K>(Cp, invd, r, slot_a, y1);
     const double ac = group_sum<K>(av_r * cvec);
     if (active && r < a.m) a.Bv[(size_t)i * a.m + r] = rv ? -av_r : 0.;
-    if (active && r == 0) a.Dinv[i] = 1. / (var - ac);             // Vecchia_utils.cpp:1507, 1562, 1615
+    if (active && r == 0) a.Dinv[i] = 1. / (var + a.nugget - ac);   // Vecchia_utils.cpp:1507, 1562, 1615
 
+    if (a.dBv_var != nullptr) {
+      // dc = c, dC = C - nugget I: dA^T = C^-1 (c - (C - I) a) = C^-1 a, dD = var - (dA.c + a.c) = var - a.a - a.c
+      const double aa = group_sum<K>(av_r * av_r);
+      const double yv = fwd_solve<K>(row, invd, r, slot_a, av_r);
+      const double wv = back_solve<K>(Cp, invd, r, slot_a, yv);
+      if (active && r < a.m) a.dBv_var[(size_t)i * a.m + r] = rv ? -wv : 0.;
+      if (active && r == 0) a.dD_var[i] = var - ac - aa;
+    }
     if (want_grad) {
       // t = dC a (dC diagonal is 0), then w = C^-1 (dc - t) = dA^T (:1573-1574)
       compiler_fence();

@@ -29,6 +29,13 @@ struct LatentFactorArgs {
   double* dBv;       // nullable (no gradient)
   double* Dinv;
   double* dD;        // nullable
+  // Gaussian form (transformed scale, VecchiaFisher): nugget 1 on the between-neighbour diagonal and in
+  // D (Vecchia_utils.cpp:1351-1353, 1540); 0 = the latent form above
+  double nugget;
+  // nullable: dB / dlog(var) and dD / dlog(var) (the nugget form's variance derivative,
+  // Vecchia_utils.cpp:1512, 1573-1580: dA = C^-1 a, dD = var - a.c - a.a)
+  double* dBv_var;
+  double* dD_var;
 };
 void launch_latent_factor(int cov_type, const LatentFactorArgs& a, hipStream_t s);
 

@@ -585,19 +585,31 @@ void REModelAMD::StdDevCovPars(const double* orig, double* sd) {
   // include_error_var = true: with Sigma^-1 = Psi^-1 / sigma^2 and dSigma_k on the original scale
   // (sigma^2: I; sigma1^2: the correlation matrix; rho: sigma1^2 dcorr/drho)
   //   FI_00 = tr(Sigma^-2) / 2, FI_0k = tr(Sigma^-2 dSigma_k) / 2, FI_kl = tr(Sigma^-1 dSigma_k Sigma^-1 dSigma_l) / 2
-  if (cfg_.latent || vecchia_ || fitc_)
+  if (cfg_.latent || fitc_ || vif_)
     Fatal("standard deviations of covariance parameters are supported by gpboost_amd only for gp_approx = 'none' "
-          "with the Gaussian likelihood");
+          "and 'vecchia' with the Gaussian likelihood");
   UseDevice();
   EnsureStructure();
   double trafo[3];
   TransformCovPars(orig, trafo);
-  const double s2 = orig[0], rho = orig[2];
-  const double dlogphi_drho = (cfg_.cov_type == kGaussian ? -2. : -1.) / rho;
-  double t[6];
-  dense_->Fisher(cfg_.cov_type, trafo[1], trafo[2], orig[1] * dlogphi_drho, t);
-  const double c = 0.5 / (s2 * s2);
-  const double F[3][3] = {{c * t[0], c * t[1], c * t[2]}, {c * t[1], c * t[3], c * t[4]}, {c * t[2], c * t[4], c * t[5]}};
+  double F[3][3];
+  if (vecchia_) {
+    // CalcFisherInformation_Vecchia, stochastic-trace form (re_model_template.h:9246-9298); probes from
+    // (seed_rand_vec_trace, cg_generator_counter_ = 0: a Cholesky-based Gaussian model never draws)
+    if (world_ > 1) Fatal("standard deviations of covariance parameters are only available on single-rank models");
+    if (!vfisher_)
+      vfisher_.reset(new VecchiaFisher(cfg_.n, cfg_.d, cfg_.num_neighbors, d_X_.get(), d_nbr_.get(), nbr_, stream_));
+    vfisher_->Fisher(cfg_.cov_type, orig, trafo, iter.num_rand_vec_trace, iter.seed_rand_vec_trace, 0, &F[0][0]);
+  } else {
+    const double s2 = orig[0], rho = orig[2];
+    const double dlogphi_drho = (cfg_.cov_type == kGaussian ? -2. : -1.) / rho;
+    double t[6];
+    dense_->Fisher(cfg_.cov_type, trafo[1], trafo[2], orig[1] * dlogphi_drho, t);
+    const double c = 0.5 / (s2 * s2);
+    const double Fd[3][3] = {{c * t[0], c * t[1], c * t[2]}, {c * t[1], c * t[3], c * t[4]},
+                             {c * t[2], c * t[4], c * t[5]}};
+    std::copy(&Fd[0][0], &Fd[0][0] + 9, &F[0][0]);
+  }
   // inverse of the symmetric 3 x 3 matrix by cofactors (FI.inverse(), :9788)
   const double c00 = F[1][1] * F[2][2] - F[1][2] * F[2][1];
   const double c11 = F[0][0] * F[2][2] - F[0][2] * F[2][0];

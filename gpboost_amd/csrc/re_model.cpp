@@ -265,6 +265,7 @@ REModelAMD::~REModelAMD() {
   (void)hipSetDevice(device_);
   if (stream_) (void)hipStreamSynchronize(stream_);
   dense_.reset();
+  vfisher_.reset();
   vif_.reset();
   fitc_lap_.reset();
   fitc_.reset();

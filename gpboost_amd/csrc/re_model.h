@@ -21,6 +21,7 @@
 #include "fitc.h"
 #include "fitc_laplace.h"
 #include "vif.h"
+#include "vecchia_fisher.h"
 #include "latent.h"
 #include "optim.h"
 
@@ -183,7 +184,7 @@ class REModelAMD {
   EvalResult EvalTrafoWls(const double* trafo, bool want_grad, bool fatal_on_nan, std::vector<double>* beta_out);
   // Standard deviations of the covariance parameters (original scale) at cov_pars_orig: square
   // roots of the diagonal of the inverse Fisher information (CalcStdDevCovPar,
-  // re_model_template.h:9775-9789; dense Gaussian models only).
+  // re_model_template.h:9775-9789; dense and Vecchia Gaussian models).
   void StdDevCovPars(const double* cov_pars_orig, double* sd);
   int num_it() const { return num_it_; }
   // GPB_GetInitCovPar (re_model.cpp:813-834): initial values on the original scale, or -1 each
@@ -277,6 +278,7 @@ class REModelAMD {
   std::unique_ptr<FitcSolver> fitc_;   // gp_approx = "fitc"
   std::unique_ptr<FitcLaplace> fitc_lap_;   // gp_approx = "fitc", non-Gaussian likelihood (Laplace)
   std::unique_ptr<VifSolver> vif_;          // gp_approx = "full_scale_vecchia" (Gaussian likelihood)
+  std::unique_ptr<VecchiaFisher> vfisher_;  // gp_approx = "vecchia", Gaussian: standard deviations (lazy)
   std::mt19937 fitc_rng_;              // the model's generator after the inducing-point selection
   std::mt19937 pred_ref_gen_;          // the likelihood's cg_generator_ (default seed) for reference draws
   std::mt19937* RefDraws();
