@@ -23,6 +23,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <cstdint>
 #include <random>
 #include <string>
 #include <vector>
@@ -81,6 +82,10 @@ class FitcSolver {
   void Predict(int cov_type, double var, double phi, const double* d_y, const double* Xp, int np,
                const std::vector<int>& match, bool want_var, bool want_cov, bool response, double* mean,
                double* pvar, double* pcov);
+  // Fisher information of the covariance parameters (3 x 3 row-major, [sigma^2, sigma1^2, rho]) at the
+  // original-scale orig (trafo: the same transformed), Hutchinson estimates over t probes from (seed,
+  // run_id): CalcFisherInformation_FITC_FSA (re_model_template.h:9363-9548; fitc_fisher.hip).
+  void Fisher(int cov_type, const double* orig, const double* trafo, int t, int seed, uint64_t run_id, double* FI);
 
  private:
   friend class FitcLaplace;   // the Laplace approximation (fitc_laplace.h) works on these buffers

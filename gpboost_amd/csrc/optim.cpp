@@ -585,9 +585,9 @@ void REModelAMD::StdDevCovPars(const double* orig, double* sd) {
   // include_error_var = true: with Sigma^-1 = Psi^-1 / sigma^2 and dSigma_k on the original scale
   // (sigma^2: I; sigma1^2: the correlation matrix; rho: sigma1^2 dcorr/drho)
   //   FI_00 = tr(Sigma^-2) / 2, FI_0k = tr(Sigma^-2 dSigma_k) / 2, FI_kl = tr(Sigma^-1 dSigma_k Sigma^-1 dSigma_l) / 2
-  if (cfg_.latent || fitc_ || vif_)
-    Fatal("standard deviations of covariance parameters are supported by gpboost_amd only for gp_approx = 'none' "
-          "and 'vecchia' with the Gaussian likelihood");
+  if (cfg_.latent || vif_)
+    Fatal("standard deviations of covariance parameters are supported by gpboost_amd only for gp_approx = 'none', "
+          "'vecchia' and 'fitc' with the Gaussian likelihood");
   UseDevice();
   EnsureStructure();
   double trafo[3];
@@ -600,6 +600,9 @@ void REModelAMD::StdDevCovPars(const double* orig, double* sd) {
     if (!vfisher_)
       vfisher_.reset(new VecchiaFisher(cfg_.n, cfg_.d, cfg_.num_neighbors, d_X_.get(), d_nbr_.get(), nbr_, stream_));
     vfisher_->Fisher(cfg_.cov_type, orig, trafo, iter.num_rand_vec_trace, iter.seed_rand_vec_trace, 0, &F[0][0]);
+  } else if (fitc_) {
+    // CalcFisherInformation_FITC_FSA (re_model_template.h:9363-9548), the same probes
+    fitc_->Fisher(cfg_.cov_type, orig, trafo, iter.num_rand_vec_trace, iter.seed_rand_vec_trace, 0, &F[0][0]);
   } else {
     const double s2 = orig[0], rho = orig[2];
     const double dlogphi_drho = (cfg_.cov_type == kGaussian ? -2. : -1.) / rho;

@@ -178,13 +178,13 @@ class REModelAMD {
   const std::string& optimizer_coef() const { return optimizer_coef_; }
   std::string cg_preconditioner_type() const;
   // CanCalculateStandardErrorsCovPars (re_model_template.h:1630-1632)
-  bool CanCalculateStandardErrorsCovPars() const { return !cfg_.latent && !fitc_ && !vif_; }
+  bool CanCalculateStandardErrorsCovPars() const { return !cfg_.latent && !vif_; }
   // GLS evaluation on the transformed scale (optimizer): beta from the Gram of [X | y], then the
   // profiled L-BFGS unit on the residuals. beta_out (nullable) receives the coefficients.
   EvalResult EvalTrafoWls(const double* trafo, bool want_grad, bool fatal_on_nan, std::vector<double>* beta_out);
   // Standard deviations of the covariance parameters (original scale) at cov_pars_orig: square
   // roots of the diagonal of the inverse Fisher information (CalcStdDevCovPar,
-  // re_model_template.h:9775-9789; dense and Vecchia Gaussian models).
+  // re_model_template.h:9775-9789; dense, Vecchia and FITC Gaussian models).
   void StdDevCovPars(const double* cov_pars_orig, double* sd);
   int num_it() const { return num_it_; }
   // GPB_GetInitCovPar (re_model.cpp:813-834): initial values on the original scale, or -1 each

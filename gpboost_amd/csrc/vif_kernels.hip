@@ -343,7 +343,7 @@ __global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
   __shared__ double vecs[4][32];   // c, dc0, dc1, A
   __shared__ double rdg[32];       // 1 / L_jj
   const int i = blockIdx.x, lane = threadIdx.x;
-  const int nn = a.nn, k = min(i, nn), S = k + 1;
+  const int nn = a.nn, k = min(i, nn);
   if (lane < 32) idx[lane] = lane < k ? a.nbr[(size_t)i * nn + lane] : i;
   wave_sync();
   const int m0 = lane & 15, kq = lane >> 4;

@@ -162,8 +162,9 @@ def test_std_dev_after_fit_and_errors(golden_fit):
     out = gm.get_cov_pars(std_err=True)
     np.testing.assert_allclose(out[0], case["cov_pars"], rtol=1e-6)
     assert np.all(np.isfinite(out[1])) and np.all(out[1] > 0)
-    # FITC: CalcFisherInformation_FITC_FSA is not part of this build (refused, not approximated)
-    gv = GPModel(gp_coords=X, cov_function="exponential", gp_approx="fitc", num_ind_points=20)
+    # full_scale_vecchia: the reference refuses too (re_model_template.h:1666-1668)
+    gv = GPModel(gp_coords=X, cov_function="exponential", gp_approx="full_scale_vecchia", num_ind_points=20,
+                 num_neighbors=10)
     gv.neg_log_likelihood([0.1, 1.0, 0.1], Y)
     with pytest.raises(GPBoostError, match="standard deviations"):
         gv.get_cov_pars(std_err=True)
