@@ -8,6 +8,8 @@
 #include <cstring>
 #include <numeric>
 
+#include "dense.h"
+#include "fitc.h"
 #include "grouped_kernels.h"
 #include "latent_kernels.h"
 #include "slq_host.h"
@@ -17,6 +19,7 @@ namespace gpb_amd {
 namespace {
 constexpr double kZeroRhsAbs = 1e-100;   // THRESHOLD_ZERO_RHS_CG (utils.h), on sum |rhs|
 constexpr int kOut = 4096;   // pinned host / device scalar slots (>= 1024 residual norms, 2 + 2K sums)
+constexpr int kDenseMaxM = 60000;   // K >= 2 cholesky: dense M x M factor (3.5 M^2 doubles, ~100 GB at the limit)
 }  // namespace
 
 GroupedRE::GroupedRE(int n, const std::vector<std::vector<int>>& levels, hipStream_t s)
@@ -289,16 +292,51 @@ void GroupedRE::CheckMethod(const double* tau, bool iterative) const {
     Fatal("Cannot use matrix_inversion_method = 'iterative' if there is only a single-level grouped random effects. "
           "Use matrix_inversion_method = 'cholesky' instead (this is very fast). Iterative methods are for multiple "
           "grouped random effects ");
-  if (!iterative && K_ > 1)
-    Fatal("matrix_inversion_method 'cholesky' with several grouped random effects is not supported by gpboost_amd "
-          "(supported: iterative)");
+  if (!iterative && K_ > 1 && M_ > kDenseMaxM)
+    Fatal("matrix_inversion_method 'cholesky' with several grouped random effects: %d random effects exceed the "
+          "dense factor's limit of %d in gpboost_amd (use 'iterative')", M_, kDenseMaxM);
+}
+
+void GroupedRE::DenseFactor() {
+  // A = Sigma^-1 + Z^T Z dense (diag(A) = D from Diag), in-place Cholesky, log|A|, the inverse factor
+  const int M = M_;
+  if (ldM_ == 0) {
+    ldM_ = (M + 63) / 64 * 64;
+    const size_t mm = (size_t)ldM_ * ldM_;
+    dA_.alloc(mm);
+    dW_.alloc(mm);
+    dLiT_.alloc(mm);
+    dX_.alloc((size_t)ldM_ * (ldM_ / 2 + 64));
+    d_invdiag_.alloc(M);
+    d_tmpM_.alloc(ldM_);
+    d_info_.alloc(1);
+    HIP_CHECK(hipMemsetAsync(dW_.get(), 0, sizeof(double) * mm, s_));
+  }
+  const int ld = ldM_;
+  HIP_CHECK(hipMemsetAsync(dA_.get(), 0, sizeof(double) * (size_t)ld * ld, s_));
+  HIP_CHECK(hipMemsetAsync(d_info_.get(), 0, sizeof(int), s_));
+  launch_gre_dense_build(M, ld, d_rowptr_.get(), d_col_.get(), d_val_.get(), d_D_.get(), dA_.get(), s_);
+  chol_lower(s_, dA_.get(), dW_.get(), M, ld, d_info_.get());
+  launch_logdet_chol(s_, dA_.get(), ld, M, d_out_.get() + kOut - 3);
+  trtri_lower(s_, dA_.get(), dW_.get(), dX_.get(), 0, M, ld);
+  fitc_lower_t(s_, dW_.get(), M, ld, dLiT_.get());
+  launch_gre_inv_diag(M, ld, dW_.get(), d_invdiag_.get(), s_);
+  fitc_chol_solve(s_, dW_.get(), dLiT_.get(), d_zty_.get(), M, ld, d_tmpM_.get(), d_u_.get());
+  int info = 0;
+  HIP_CHECK(hipMemcpyAsync(&info, d_info_.get(), sizeof(int), hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipMemcpyAsync(h_out_ + kOut - 3, d_out_.get() + kOut - 3, sizeof(double), hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  if (info != 0) Fatal("the matrix Sigma^-1 + Z^T Z is not positive definite");
+  dense_logdet_ = h_out_[kOut - 3];
 }
 
 // u = A^-1 Z^T y (CalcYAux, re_model_template.h:8965-9003): K == 1 closed form (single_sums: the
 // pinned slots receiving sum cnt and sum cnt^2 / D), else SSOR-PCG. Returns the PCG iterations.
 int GroupedRE::SolveU(bool iterative, bool warm, const IterativeConfig& cfg, double* single_sums) {
   int its = 0;
-  if (!iterative) {   // A diagonal: u = Z^T y / D
+  if (!iterative && K_ > 1) {
+    DenseFactor();
+  } else if (!iterative) {   // A diagonal: u = Z^T y / D
     launch_gre_single(M_, d_zty_.get(), d_cnt_.get(), d_D_.get(), d_u_.get(), d_out_.get() + kOut - 2, s_);
     HIP_CHECK(hipMemcpyAsync(single_sums, d_out_.get() + kOut - 2, sizeof(double) * 2, hipMemcpyDeviceToHost, s_));
   } else {
@@ -322,7 +360,11 @@ void GroupedRE::Blup(const double* tau, bool iterative, bool warm, const Iterati
   std::vector<double> zty(M_), ztzu(M_), D, cnt;
   HIP_CHECK(hipMemcpyAsync(zty.data(), d_zty_.get(), sizeof(double) * M_, hipMemcpyDeviceToHost, s_));
   HIP_CHECK(hipMemcpyAsync(ztzu.data(), d_ztzu_.get(), sizeof(double) * M_, hipMemcpyDeviceToHost, s_));
-  if (var != nullptr) {
+  std::vector<double> invdiag;
+  if (var != nullptr && K_ > 1) {   // cholesky (iterative is refused by the caller): diag(A^-1)
+    invdiag.resize(M_);
+    HIP_CHECK(hipMemcpyAsync(invdiag.data(), d_invdiag_.get(), sizeof(double) * M_, hipMemcpyDeviceToHost, s_));
+  } else if (var != nullptr) {
     D.resize(M_);
     cnt.resize(M_);
     HIP_CHECK(hipMemcpyAsync(D.data(), d_D_.get(), sizeof(double) * M_, hipMemcpyDeviceToHost, s_));
@@ -332,7 +374,9 @@ void GroupedRE::Blup(const double* tau, bool iterative, bool warm, const Iterati
   for (int k = 0; k < K_; ++k)
     for (int r = cum_[k]; r < cum_[k + 1]; ++r) {
       b[r] = tau[k] * (zty[r] - ztzu[r]);
-      if (var != nullptr) {
+      if (var != nullptr && K_ > 1) {
+        var[r] = invdiag[r];   // tau + tau^2 (M_aux^T M_aux - Z_j^T Z_j)_rr = (A^-1)_rr (:4122-4139)
+      } else if (var != nullptr) {
         const double ma = cnt[r] / std::sqrt(D[r]);   // M_aux (:4088-4091)
         var[r] = tau[k] - tau[k] * tau[k] * (cnt[r] - ma * ma);
       }
@@ -362,7 +406,9 @@ void GroupedRE::Eval(const double* tau, bool want_grad, bool iterative, bool war
   out.yTPsiInvy = h_out_[1] - h_out_[0];
   std::vector<double> sum_logD(h_out_ + 2, h_out_ + 2 + K_), sum_Dinv(h_out_ + 2 + K_, h_out_ + 2 + 2 * K_);
   double logdet = 0.;
-  if (!iterative) {
+  if (!iterative && K_ > 1) {
+    logdet = dense_logdet_;   // 2 sum log L_ii (re_model_template.h:2780)
+  } else if (!iterative) {
     for (int k = 0; k < K_; ++k) logdet += sum_logD[k];   // 2 sum log sqrt(D) (re_model_template.h:2780)
   } else {
     // ---- SLQ: probes r ~ N(0, I) (GenRandVecNormalParallel), P-distributed L D^-1/2 r, block PCG
@@ -421,6 +467,17 @@ void GroupedRE::Eval(const double* tau, bool want_grad, bool iterative, bool war
   HIP_CHECK(hipStreamSynchronize(s_));
   for (int k = 0; k < K_; ++k)
     out.quad[k] = (h_out_[3 * k] - 2. * h_out_[3 * k + 1] + h_out_[3 * k + 2]) * tau[k];
+  if (!iterative && K_ > 1) {   // tr(Psi^-1 dPsi_k) = m_k - tr(A^-1_kk) / tau_k (:2279-2296)
+    std::vector<double> invdiag(M_);
+    HIP_CHECK(hipMemcpyAsync(invdiag.data(), d_invdiag_.get(), sizeof(double) * M_, hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipStreamSynchronize(s_));
+    for (int k = 0; k < K_; ++k) {
+      double tr = 0.;
+      for (int r = cum_[k]; r < cum_[k + 1]; ++r) tr += invdiag[r];
+      out.trace[k] = m_[k] - tr / tau[k];
+    }
+    return;
+  }
   if (!iterative) {   // tr(Psi^-1 dPsi_k) = tau_k (sum cnt - sum cnt^2 / D) (:2279-2296)
     out.trace[0] = (single_sums[0] - single_sums[1]) * tau[0];
     return;

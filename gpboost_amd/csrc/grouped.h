@@ -13,6 +13,12 @@
 // N(0, P) (CGTridiagRandomEffects :1232-1400, LogDetStochTridiag :988-1004) plus log|P| = sum log D,
 // and the gradient by stochastic traces with the SSOR variance reduction (CalcOptimalC :1006).
 // K == 1: A is diagonal and everything is closed-form (the reference's Cholesky branch).
+// K >= 2 "cholesky" (:8571-8598, the reference's sparse SimplicialLLT): A assembled DENSE in HBM
+// (M x M column-major; the integer counts of Z^T Z are exact in any order) and factored on the
+// dense path's MFMA POTRF / TRTRI (chol_lower / trtri_lower): log|A| = 2 sum log L_ii, u = A^-1 Z^T y
+// by the two triangular products of the inverse factor, and the traces from diag(A^-1):
+// tr(Psi^-1 dPsi_k) = m_k - tr(A^-1_kk) / tau_k (the reference's tau_k (||Z_k||^2 - ||L^-1 Z^T Z_k||^2),
+// :2279-2296, without its cancellation). Posterior variances of the levels: diag(A^-1).
 //
 // Data layout in HBM: Z^T Z as its diagonal `cnt` (M) and its off-diagonal part in CSR over RE rows
 // (columns ascending: the entries of lower effects first, `split` marks the first entry of a
@@ -83,6 +89,13 @@ class GroupedRE {
   const ChunkPlan& Plan(int tc);
   GroupedOp Op(int t);
   void Diag(const double* tau);                              // D, sqrt(D), per-effect sums of log D and 1/D
+  // K >= 2 cholesky: A dense, its Cholesky factor, log|A| (dense_logdet_), the inverse factor Li (dW_)
+  // and its transpose (dLiT_), diag(A^-1) (d_invdiag_); u = A^-1 Z^T y
+  void DenseFactor();
+  int ldM_ = 0;
+  double dense_logdet_ = 0.;
+  DevBuf<double> dA_, dW_, dLiT_, dX_, d_invdiag_, d_tmpM_;
+  DevBuf<int> d_info_;
   void ApplyA(const double* X, double* Y, int t, bool with_sigma_inv);
   void Precond(const double* R, double* Z, double* S, int t); // Z = P^-1 R (S: scratch)
   // Reference PCG forms: single column (stop on ||r|| < delta) or block (stop on the mean column

@@ -55,5 +55,11 @@ void launch_gre_single(int M, const double* zty, const double* cnt, const double
                        hipStream_t s);
 // R = rhs - V (elementwise)
 void launch_gre_residual(size_t count, const double* rhs, const double* V, double* R, hipStream_t s);
+// Dense Cholesky form (K >= 2, matrix_inversion_method = "cholesky"): A = diag(D) + the off-diagonal
+// Z^T Z counts into the column-major M x M matrix (ld; zero-filled beforehand), and diag(A^-1)_i =
+// sum_{r >= i} Li[r, i]^2 from the lower inverse Cholesky factor Li.
+void launch_gre_dense_build(int M, int ld, const int* rowptr, const int* col, const double* val, const double* D,
+                            double* A, hipStream_t s);
+void launch_gre_inv_diag(int M, int ld, const double* Li, double* out, hipStream_t s);
 
 }  // namespace gpb_amd

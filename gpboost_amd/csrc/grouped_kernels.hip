@@ -264,6 +264,42 @@ void launch_gre_single(int M, const double* zty, const double* cnt, const double
   HIP_CHECK(hipGetLastError());
 }
 
+namespace {
+__global__ void __launch_bounds__(256) gre_dense_build_kernel(int M, int ld, const int* __restrict__ rowptr,
+                                                              const int* __restrict__ col, const double* __restrict__ val,
+                                                              const double* __restrict__ D, double* __restrict__ A) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r >= M) return;
+  A[(size_t)r * ld + r] = D[r];
+  for (int e = rowptr[r]; e < rowptr[r + 1]; ++e) A[(size_t)col[e] * ld + r] = val[e];
+}
+
+// one wave per column: sum of squares of the column's lower part (fixed lane order, then a shuffle tree)
+__global__ void __launch_bounds__(256) gre_inv_diag_kernel(int M, int ld, const double* __restrict__ Li,
+                                                           double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= M) return;
+  const double* c = Li + (size_t)i * ld;
+  double s = 0.;
+  for (int r = i + lane; r < M; r += 64) s = fma(c[r], c[r], s);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (lane == 0) out[i] = s;
+}
+}  // namespace
+
+void launch_gre_dense_build(int M, int ld, const int* rowptr, const int* col, const double* val, const double* D,
+                            double* A, hipStream_t s) {
+  hipLaunchKernelGGL(gre_dense_build_kernel, dim3((M + 255) / 256), dim3(256), 0, s, M, ld, rowptr, col, val, D, A);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_gre_inv_diag(int M, int ld, const double* Li, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(gre_inv_diag_kernel, dim3((M + 3) / 4), dim3(256), 0, s, M, ld, Li, out);
+  HIP_CHECK(hipGetLastError());
+}
+
 void launch_gre_residual(size_t count, const double* rhs, const double* V, double* R, hipStream_t s) {
   if (count == 0) return;
   hipLaunchKernelGGL(gre_residual_kernel, dim3((unsigned)((count + 255) / 256)), dim3(256), 0, s, count, rhs, V, R);

@@ -44,9 +44,6 @@ GroupedModel::GroupedModel(int n, const std::vector<std::vector<int>>& levels, c
     Fatal("Cannot use matrix_inversion_method = 'iterative' if there is only a single-level grouped random effects. "
           "Use matrix_inversion_method = 'cholesky' instead (this is very fast). Iterative methods are for multiple "
           "grouped random effects ");
-  if (mim_ == "cholesky" && K > 1)
-    Fatal("matrix_inversion_method 'cholesky' with several grouped random effects is not supported by gpboost_amd "
-          "(supported: iterative, the reference's default there)");
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
     Fatal("no HIP device visible: gpboost_amd has no CPU fallback");

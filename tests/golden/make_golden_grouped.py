@@ -90,6 +90,16 @@ def main():
         cases["pred_train_k2_n20000_tight"] = pred_case(20000, (500, 50), (1.0, 1.0, 0.25), False, **it_tight)
         cases["pred_train_k3_n20000_default"] = pred_case(20000, (400, 60, 7), (1.0, 1.0, 0.25, 0.1), False,
                                                           **it_default)
+        # K >= 2 with matrix_inversion_method = "cholesky" (the reference's sparse Cholesky of
+        # Sigma^-1 + Z^T Z, re_model_template.h:8571-8598)
+        chol = dict(matrix_inversion_method="cholesky")
+        cases["k2_n20000_cholesky"] = case(20000, (500, 50), (1.0, 1.0, 0.25), **chol)
+        cases["k3_n20000_cholesky"] = case(20000, (400, 60, 7), (1.0, 1.0, 0.25, 0.1), **chol)
+        cases["k2_n3000_cholesky_small"] = case(3000, (900, 3), (0.5, 2.0, 0.05), **chol)
+        cases["fit_k2_n20000_cholesky"] = fit_case(20000, (500, 50), **chol)
+        cases["fit_k3_n20000_cholesky"] = fit_case(20000, (400, 60, 7), **chol)
+        cases["pred_train_k2_n20000_cholesky"] = pred_case(20000, (500, 50), (1.0, 1.0, 0.25), True, **chol)
+        cases["pred_train_k3_n20000_cholesky"] = pred_case(20000, (400, 60, 7), (1.0, 1.0, 0.25, 0.1), True, **chol)
     else:
         cases["k2_n500000_default"] = case(500000, (5000, 500), (1.0, 1.0, 0.25), **it_default)
         cases["k2_n500000_tight"] = case(500000, (5000, 500), (1.0, 1.0, 0.25), **it_tight)

@@ -7,7 +7,8 @@ y^T Psi^-1 y and log|Psi| from A = Sigma^-1 + Z^T Z (re_model_template.h:2778-28
 "iterative" (the default there): SSOR-PCG (CGRandomEffectsVec, CG_utils.cpp:1100-1234), stochastic
 Lanczos quadrature (CGTridiagRandomEffects :1236-1414, LogDetStochTridiag :988-1004) and the
 stochastic-trace gradient with the SSOR control variate (:2304-2387, CalcOptimalC :1006-1022);
-K == 1: the closed-form diagonal branch. Fixtures: tests/golden/golden_grouped.json
+K == 1: the closed-form diagonal branch; K >= 2 "cholesky": the dense M x M factor on the MFMA POTRF (1e-10 nll,
+1e-8 gradient: the reference's sparse factor and trace subtraction vs the dense inverse diagonal). Fixtures: tests/golden/golden_grouped.json
 (make_golden_grouped.py runs oracle/_ref/ref_harness_grouped, the reference compiled from its
 sources).
 
@@ -32,7 +33,8 @@ from gpboost_amd.basic import _dp, _safe_call, lib
 pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-EVAL_CASES = ["k1_n5000_cholesky", "k2_n20000_tight", "k2_n20000_default", "k3_n20000_tight", "k2_n20000_t20_tight"]
+EVAL_CASES = ["k1_n5000_cholesky", "k2_n20000_tight", "k2_n20000_default", "k3_n20000_tight", "k2_n20000_t20_tight",
+              "k2_n20000_cholesky", "k3_n20000_cholesky", "k2_n3000_cholesky_small"]
 
 
 @pytest.fixture(scope="module")
@@ -78,7 +80,8 @@ def test_grouped_nll_and_grad_match_reference(golden, name):
     np.testing.assert_allclose(gradp, case["lbfgs_grad"], rtol=1e-6, atol=1e-6 * np.abs(case["lbfgs_grad"]).max())
 
 
-@pytest.mark.parametrize("name", ["fit_k1_n5000", "fit_k2_n20000_tight", "fit_k2_n20000_default"])
+@pytest.mark.parametrize("name", ["fit_k1_n5000", "fit_k2_n20000_tight", "fit_k2_n20000_default",
+                                  "fit_k2_n20000_cholesky", "fit_k3_n20000_cholesky"])
 def test_grouped_fit_matches_reference(golden, name):
     case = golden[name]
     g, y = _data(case)
@@ -147,7 +150,8 @@ def _levels_of(g):
 
 
 @pytest.mark.parametrize("name", ["pred_train_k1_n5000", "pred_train_k2_n20000_tight",
-                                  "pred_train_k3_n20000_default"])
+                                  "pred_train_k3_n20000_default", "pred_train_k2_n20000_cholesky",
+                                  "pred_train_k3_n20000_cholesky"])
 def test_grouped_training_data_random_effects_match_reference(golden, name):
     # PredictTrainingDataRandomEffects, grouped branch (re_model_template.h:4065-4167): the posterior
     # mean tau_k Z_k^T Psi^-1 y of each observation's level; K == 1 also its variance (closed form)
@@ -170,7 +174,8 @@ def test_grouped_training_data_random_effects_match_reference(golden, name):
         np.testing.assert_allclose(mean[k], ref, rtol=0, atol=1e-8 * np.abs(ref).max())
         if want_var:
             v = out[K * case["n"]:].reshape(K, -1)[k]
-            np.testing.assert_allclose(v, np.asarray(case["var_levels"][k])[lev[k]], rtol=1e-12)
+            # K == 1 closed form 1e-12; K >= 2 cholesky: diag(A^-1) from the dense inverse factor
+            np.testing.assert_allclose(v, np.asarray(case["var_levels"][k])[lev[k]], rtol=1e-12 if K == 1 else 1e-9)
 
 
 def test_grouped_predict_new_and_seen_levels():
