@@ -698,9 +698,10 @@ class GPModel:
 
     def _predict_grouped(self, group_data_pred, predict_var, predict_cov_mat, predict_response, y, cov_pars, offset,
                          offset_pred, fixed_effects, fixed_effects_pred):
-        """Predictive means of a grouped random effects model at new group labels (GPB_PredictREModel
-        with re_group_data_pred): sum over the effects of the training posterior mean of the label's
-        level, 0 for a level not seen in training."""
+        """Predictions of a grouped random effects model at new group labels (GPB_PredictREModel
+        with re_group_data_pred): means = sum over the effects of the training posterior mean of the
+        label's level (0 for a level not seen in training); with predict_var / predict_cov_mat
+        (matrix_inversion_method = "cholesky") the predictive variances / covariance matrix."""
         if group_data_pred is None:
             raise ValueError("'group_data_pred' is missing")
         g = np.asarray(group_data_pred)
@@ -720,14 +721,18 @@ class GPModel:
         fe = _as1d(fixed_effects, "fixed_effects") if fixed_effects is not None else None
         fep = _as1d(fixed_effects_pred, "fixed_effects_pred") if fixed_effects_pred is not None else None
         cp = self._check_cov_pars(cov_pars) if cov_pars is not None else None
-        out = np.zeros(n_pred)
+        size = n_pred + (n_pred * n_pred if predict_cov_mat else (n_pred if predict_var else 0))
+        out = np.zeros(size)
         _safe_call(lib().GPB_PredictREModel(
             self.handle, _dp(yv) if yv is not None else None, ctypes.c_int32(n_pred), _dp(out),
             ctypes.c_bool(bool(predict_cov_mat)), ctypes.c_bool(bool(predict_var)),
             ctypes.c_bool(bool(predict_response)), None, buf, None, None, None,
             _dp(cp) if cp is not None else None, None, ctypes.c_bool(False),
             _dp(fe) if fe is not None else None, _dp(fep) if fep is not None else None))
-        return {"mu": out, "cov": None, "var": None}
+        mu = out[:n_pred].copy()
+        cov = out[n_pred:].reshape(n_pred, n_pred).T.copy() if predict_cov_mat else None
+        var = out[n_pred:].copy() if (predict_var and not predict_cov_mat) else None
+        return {"mu": mu, "cov": cov, "var": var}
 
     def set_distributed(self, rank: int, world_size: int, comm_id: bytes | None):
         """Join an RCCL communicator (GPB_SetDistributed): exact Vecchia shards rows, latent

@@ -388,8 +388,8 @@ int GPB_PredictREModel(REModelHandle handle, const double* y_data, int32_t num_d
         gp_rand_coef_data_pred != nullptr || covariate_data_pred != nullptr)
       gpb_amd::Fatal("predictions with clusters, random coefficients, GP coordinates or covariates are not supported "
                      "for grouped random effects models by gpboost_amd");
-    g->Predict(y_data, num_data_pred, re_group_data_pred, cov_pars, predict_cov_mat, predict_var, fixed_effects,
-               fixed_effects_pred, out_predict);
+    g->Predict(y_data, num_data_pred, re_group_data_pred, cov_pars, predict_cov_mat, predict_var, predict_response,
+               fixed_effects, fixed_effects_pred, out_predict);
     return 0;
   }
   if (cluster_ids_data_pred != nullptr || re_group_data_pred != nullptr || re_group_rand_coef_data_pred != nullptr ||

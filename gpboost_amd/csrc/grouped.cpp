@@ -383,6 +383,39 @@ void GroupedRE::Blup(const double* tau, bool iterative, bool warm, const Iterati
     }
 }
 
+void GroupedRE::PredCov(int np, const std::vector<int>& idx, bool want_cov, double* out) {
+  if (np <= 0) return;
+  if (K_ == 1) {   // A^-1 = diag(1/D)
+    std::vector<double> D(M_);
+    HIP_CHECK(hipMemcpyAsync(D.data(), d_D_.get(), sizeof(double) * M_, hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipStreamSynchronize(s_));
+    if (want_cov) {
+      for (int q = 0; q < np; ++q)
+        for (int p = 0; p < np; ++p)
+          out[(size_t)q * np + p] = (idx[p] >= 0 && idx[p] == idx[q]) ? 1. / D[idx[p]] : 0.;
+    } else {
+      for (int p = 0; p < np; ++p) out[p] = idx[p] >= 0 ? 1. / D[idx[p]] : 0.;
+    }
+    return;
+  }
+  if (ldM_ == 0) Fatal("predictive variances need the Cholesky factor (matrix_inversion_method = 'cholesky')");
+  const int ld = ldM_;
+  DevBuf<int> d_idx(idx.size());
+  HIP_CHECK(hipMemcpyAsync(d_idx.get(), idx.data(), sizeof(int) * idx.size(), hipMemcpyHostToDevice, s_));
+  if (want_cov) {
+    DevBuf<double> E((size_t)ld * np), C((size_t)np * np);
+    HIP_CHECK(hipMemsetAsync(E.get(), 0, sizeof(double) * (size_t)ld * np, s_));
+    launch_gre_pred_cols(M_, ld, K_, np, d_idx.get(), dW_.get(), E.get(), nullptr, s_);
+    gemm_f64(s_, np, np, M_, 1., E.get(), ld, 1, E.get(), ld, 0, 0., C.get(), np);
+    HIP_CHECK(hipMemcpyAsync(out, C.get(), sizeof(double) * (size_t)np * np, hipMemcpyDeviceToHost, s_));
+  } else {
+    DevBuf<double> v(np);
+    launch_gre_pred_cols(M_, ld, K_, np, d_idx.get(), dW_.get(), nullptr, v.get(), s_);
+    HIP_CHECK(hipMemcpyAsync(out, v.get(), sizeof(double) * np, hipMemcpyDeviceToHost, s_));
+  }
+  HIP_CHECK(hipStreamSynchronize(s_));
+}
+
 void GroupedRE::Eval(const double* tau, bool want_grad, bool iterative, bool warm, const IterativeConfig& cfg,
                      GroupedParts& out) {
   CheckMethod(tau, iterative);

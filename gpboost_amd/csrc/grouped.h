@@ -69,6 +69,14 @@ class GroupedRE {
   // Posterior means of the M random effects (host, effect-major): tau_k Z_k^T Psi^-1 y; var
   // (nullable, K == 1 only): their posterior variances on the transformed scale.
   void Blup(const double* tau, bool iterative, bool warm, const IterativeConfig& cfg, double* b, double* var);
+  // After Blup (cholesky): the e_p^T A^-1 e_q part of the predictive (co)variances on the transformed scale,
+  // e_p the indicator vector of prediction point p's seen levels (idx: np x K global level indices, -1 for
+  // a level not in the training data). want_cov: out = np x np column-major, else out = np variances.
+  // Derivation: Cov = U - Ztilde Sigma Z^T Z Sigma Ztilde^T + Ztilde Sigma Z^T Z A^-1 Z^T Z Sigma Ztilde^T
+  // (re_model_template.h:10350-10358, 10510-10522) with Z^T Z = A - Sigma^-1 collapses to
+  // U - sum_k tau_k [same seen level] + e_p^T A^-1 e_q. K >= 2: E = Li [e_p] on the device (one wave per
+  // point), variances ||E_p||^2, covariances E^T E on the MFMA GEMM; K == 1: A^-1 = diag(1/D).
+  void PredCov(int np, const std::vector<int>& idx, bool want_cov, double* out);
 
  private:
   struct Block {   // work space of a t-column PCG

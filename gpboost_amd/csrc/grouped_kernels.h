@@ -61,5 +61,9 @@ void launch_gre_residual(size_t count, const double* rhs, const double* V, doubl
 void launch_gre_dense_build(int M, int ld, const int* rowptr, const int* col, const double* val, const double* D,
                             double* A, hipStream_t s);
 void launch_gre_inv_diag(int M, int ld, const double* Li, double* out, hipStream_t s);
+// E[:, p] = sum_k Li[:, idx[p K + k]] (lower part only; idx < 0 skipped) into E (M x np, ld), or (E null)
+// var[p] = ||that column||^2
+void launch_gre_pred_cols(int M, int ld, int K, int np, const int* idx, const double* Li, double* E, double* var,
+                          hipStream_t s);
 
 }  // namespace gpb_amd

@@ -287,7 +287,34 @@ __global__ void __launch_bounds__(256) gre_inv_diag_kernel(int M, int ld, const 
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   if (lane == 0) out[i] = s;
 }
+__global__ void __launch_bounds__(256) gre_pred_cols_kernel(int M, int ld, int K, int np, const int* __restrict__ idx,
+                                                            const double* __restrict__ Li, double* __restrict__ E,
+                                                            double* __restrict__ var) {
+  const int lane = threadIdx.x & 63;
+  const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= np) return;
+  const int* ip = idx + (size_t)p * K;
+  double s = 0.;
+  for (int r = lane; r < M; r += 64) {
+    double v = 0.;
+    for (int k = 0; k < K; ++k) {
+      const int a = ip[k];
+      if (a >= 0 && r >= a) v += Li[(size_t)a * ld + r];
+    }
+    if (E) E[(size_t)p * ld + r] = v;
+    s = fma(v, v, s);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+  if (var && lane == 0) var[p] = s;
+}
 }  // namespace
+
+void launch_gre_pred_cols(int M, int ld, int K, int np, const int* idx, const double* Li, double* E, double* var,
+                          hipStream_t s) {
+  hipLaunchKernelGGL(gre_pred_cols_kernel, dim3((np + 3) / 4), dim3(256), 0, s, M, ld, K, np, idx, Li, E, var);
+  HIP_CHECK(hipGetLastError());
+}
 
 void launch_gre_dense_build(int M, int ld, const int* rowptr, const int* col, const double* val, const double* D,
                             double* A, hipStream_t s) {

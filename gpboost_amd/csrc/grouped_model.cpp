@@ -297,29 +297,66 @@ void GroupedModel::PredictTrainingDataRandomEffects(const double* cov_pars, cons
 }
 
 void GroupedModel::Predict(const double* y, int n_pred, const char* re_group_data_pred, const double* cov_pars,
-                           bool predict_cov_mat, bool predict_var, const double* fixed_effects,
+                           bool predict_cov_mat, bool predict_var, bool predict_response, const double* fixed_effects,
                            const double* fixed_effects_pred, double* out) {
-  if (predict_cov_mat || predict_var)
-    Fatal("predictive (co)variances for grouped random effects are not supported by gpboost_amd (predictive means "
-          "only)");
+  if ((predict_cov_mat || predict_var) && iterative())
+    Fatal("predictive (co)variances for grouped random effects with matrix_inversion_method = 'iterative' (the "
+          "reference's simulation-based estimate) are not supported by gpboost_amd (use 'cholesky')");
   if (n_pred <= 0) Fatal("num_data_pred must be > 0");
   if (re_group_data_pred == nullptr) Fatal("re_group_data_pred must be provided for grouped random effects");
   const int K = re_->K();
   if ((int)label_index_.size() != K) Fatal("the model has no label index (created without re_group_data)");
+  const bool want_unc = predict_cov_mat || predict_var;
+  if (predict_cov_mat && n_pred > 40000)
+    Fatal("predictive covariance matrices are limited to 40000 prediction points by gpboost_amd");
   const std::vector<double> b = Blup(cov_pars, y, fixed_effects, nullptr);
+  // labels column-major, as re_group_data (re_model_template.h:3081-3085): seen levels to their global
+  // index, new labels to -1 (their label string kept for the same-new-label covariance terms)
+  std::vector<int> idx((size_t)n_pred * K, -1);
+  std::vector<std::vector<std::string>> labels(want_unc ? K : 0);
   std::vector<double> mu(n_pred, 0.);
   const char* p = re_group_data_pred;
   int off = 0;
-  for (int k = 0; k < K; ++k) {   // labels column-major, as re_group_data (re_model_template.h:3081-3085)
+  for (int k = 0; k < K; ++k) {
+    if (want_unc) labels[k].resize(n_pred);
     for (int i = 0; i < n_pred; ++i) {
       std::string label(p);
       p += label.size() + 1;
       auto it = label_index_[k].find(label);
-      if (it != label_index_[k].end()) mu[i] += b[off + it->second];   // a new level contributes 0
+      if (it != label_index_[k].end()) {
+        mu[i] += b[off + it->second];   // a new level contributes 0
+        idx[(size_t)i * K + k] = off + it->second;
+      }
+      if (want_unc) labels[k][i] = std::move(label);
     }
     off += re_->levels_per_effect()[k];
   }
   for (int i = 0; i < n_pred; ++i) out[i] = mu[i] + (fixed_effects_pred ? fixed_effects_pred[i] : 0.);
+  if (!want_unc) return;
+  std::vector<double> cp;
+  if (cov_pars != nullptr) cp.assign(cov_pars, cov_pars + 1 + K);
+  else cp = last_cov_pars_;
+  std::vector<double> tau(K);
+  for (int k = 0; k < K; ++k) tau[k] = cp[1 + k] / cp[0];
+  const double nug = predict_response ? 1. : 0., s2 = cp[0];
+  double* o = out + n_pred;
+  re_->PredCov(n_pred, idx, predict_cov_mat, o);
+  if (predict_cov_mat) {
+    for (int q = 0; q < n_pred; ++q)
+      for (int i = 0; i < n_pred; ++i) {
+        double v = o[(size_t)q * n_pred + i] + (i == q ? nug : 0.);
+        for (int k = 0; k < K; ++k)
+          if (idx[(size_t)i * K + k] < 0 && idx[(size_t)q * K + k] < 0 && labels[k][i] == labels[k][q]) v += tau[k];
+        o[(size_t)q * n_pred + i] = v * s2;
+      }
+  } else {
+    for (int i = 0; i < n_pred; ++i) {
+      double v = o[i] + nug;
+      for (int k = 0; k < K; ++k)
+        if (idx[(size_t)i * K + k] < 0) v += tau[k];
+      o[i] = v * s2;
+    }
+  }
 }
 
 }  // namespace gpb_amd

@@ -63,15 +63,17 @@ class GroupedModel {
   int num_cg_steps_tridiag() const { return last_lanczos_; }
   // GPB_PredictREModelTrainingDataRandomEffects (re_model.cpp -> PredictTrainingDataRandomEffects,
   // grouped branch re_model_template.h:4065-4167): out[k n + i] = posterior mean of effect k at
-  // observation i's level; calc_var (K == 1 only, as the reference's iterative branch refuses it):
+  // observation i's level; calc_var (cholesky only, as the reference's iterative branch refuses it):
   // out[K n + k n + i] = its posterior variance. cov_pars original scale (null: the last ones).
   void PredictTrainingDataRandomEffects(const double* cov_pars, const double* y, double* out,
                                         const double* fixed_effects, bool calc_var);
-  // GPB_PredictREModel with re_group_data_pred (CalcPred, re_model_template.h:10026-): the
-  // predictive means sum_k b_k(level) (0 for levels not in the training data) + fixed_effects_pred.
+  // GPB_PredictREModel with re_group_data_pred (re_model_template.h:3146 -> CalcPred :10026-10535, Woodbury branch): means; with
+  // predict_var / predict_cov_mat (cholesky only; iterative: the reference's simulation, refused) the
+  // predictive (co)variances nugget [predict_response] + sum_k tau_k [new level, same label] + e_p^T A^-1 e_q,
+  // e_p the indicator of p's seen levels (derivation in grouped.h), times sigma^2.
   void Predict(const double* y, int n_pred, const char* re_group_data_pred, const double* cov_pars,
-               bool predict_cov_mat, bool predict_var, const double* fixed_effects, const double* fixed_effects_pred,
-               double* out);
+               bool predict_cov_mat, bool predict_var, bool predict_response, const double* fixed_effects,
+               const double* fixed_effects_pred, double* out);
   IterativeConfig iter;
 
  private:

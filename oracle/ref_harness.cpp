@@ -363,25 +363,40 @@ int main(int argc, char** argv) {
     // GPB_SetPredictionData + GPB_PredictREModel at cov_pars (re_model.cpp:927-1000 -> Predict
     // re_model_template.h:3146): prediction coordinates from the file `pred` (int32 np, double
     // coords[np * d] column-major); outputs the predictive mean and (predict_var) variances.
+    // Grouped models (num_re_group > 0): the file holds int32 np, then int32 labels[np * K]
+    // (effect-major), passed as the NUL-separated label strings of re_group_data_pred.
     FILE* fp = std::fopen(get(args, "pred", "").c_str(), "rb");
     if (!fp) { std::perror("open pred"); return 2; }
     int32_t np = 0;
     if (std::fread(&np, 4, 1, fp) != 1 || np <= 0) return 2;
-    std::vector<double> xp((size_t)np * d);
-    if (std::fread(xp.data(), 8, xp.size(), fp) != xp.size()) return 2;
+    std::vector<double> xp;
+    std::string re_group_pred;
+    if (num_re_group > 0) {
+      std::vector<int32_t> lab((size_t)np * num_re_group);
+      if (std::fread(lab.data(), 4, lab.size(), fp) != lab.size()) return 2;
+      for (int32_t v : lab) {
+        re_group_pred += std::to_string(v);
+        re_group_pred.push_back('\0');
+      }
+    } else {
+      xp.resize((size_t)np * d);
+      if (std::fread(xp.data(), 8, xp.size(), fp) != xp.size()) return 2;
+    }
     std::fclose(fp);
     const bool pcov = get(args, "predict_cov", "0") == "1";
     const bool pvar = !pcov && get(args, "predict_var", "0") == "1";
     const bool presp = get(args, "predict_response", "0") == "1";
     const std::string ptype = get(args, "vecchia_pred_type", "");
-    m->SetPredictionData(np, nullptr, nullptr, nullptr, xp.data(), nullptr, nullptr,
-                         ptype.empty() ? nullptr : ptype.c_str(),
-                         std::atoi(get(args, "num_neighbors_pred", "-1").c_str()),
-                         std::atof(get(args, "cg_delta_conv_pred", "-1").c_str()),
-                         std::atoi(get(args, "nsim_var_pred", "-1").c_str()), -1);
+    if (num_re_group == 0)
+      m->SetPredictionData(np, nullptr, nullptr, nullptr, xp.data(), nullptr, nullptr,
+                           ptype.empty() ? nullptr : ptype.c_str(),
+                           std::atoi(get(args, "num_neighbors_pred", "-1").c_str()),
+                           std::atof(get(args, "cg_delta_conv_pred", "-1").c_str()),
+                           std::atoi(get(args, "nsim_var_pred", "-1").c_str()), -1);
     std::vector<double> out((size_t)np + (pcov ? (size_t)np * np : (size_t)np), 0.);
     m->Predict(trafo.data(), y.data(), np, out.data(), true, pcov, pvar, presp, nullptr, nullptr, nullptr,
-               nullptr, nullptr, xp.data(), nullptr, false, fe_ptr, nullptr);
+               num_re_group > 0 ? re_group_pred.data() : nullptr, nullptr, num_re_group > 0 ? nullptr : xp.data(),
+               nullptr, false, fe_ptr, nullptr);
     std::printf("{\n\"n\": %d, \"d\": %d, \"np\": %d,\n", n, d, np);
     print_vec("mean", out.data(), np);
     if (pvar) print_vec("var", out.data() + np, np);

@@ -193,7 +193,7 @@ def test_grouped_predict_new_and_seen_levels():
     gn = np.array([[10_000, g[0, 1]], [g[1, 0], 99_999], [77_777, 88_888]])
     p = gm.predict(group_data_pred=gn, cov_pars=cp, offset_pred=np.array([1., 2., 3.]))
     np.testing.assert_allclose(p["mu"], [tr[0, 1] + 1., tr[1, 0] + 2., 3.], rtol=0, atol=1e-12 * np.abs(tr).max())
-    with pytest.raises(GPBoostError, match="predictive"):
+    with pytest.raises(GPBoostError, match="predictive"):   # iterative: the reference's simulation, refused
         gm.predict(group_data_pred=g[:5], cov_pars=cp, predict_var=True)
     with pytest.raises(GPBoostError, match="not implemented for matrix_inversion_method_ == 'iterative'"):
         gm.predict_training_data_random_effects(predict_var=True)
@@ -212,3 +212,29 @@ def test_grouped_predict_saved_data():
     gm.set_prediction_data(group_data_pred=gn)
     saved = gm.predict(cov_pars=cp, use_saved_data=True)
     np.testing.assert_array_equal(saved["mu"], direct["mu"])
+
+
+GOLDEN_PRED = os.path.join(HERE, "golden", "golden_grouped_pred.json")
+
+
+@pytest.mark.parametrize("name", ["gp_k1_var_resp", "gp_k1_cov", "gp_k2_var_resp", "gp_k2_var", "gp_k2_cov_resp",
+                                  "gp_k3_var", "gp_k3_cov"])
+def test_grouped_predictive_variances_match_reference(name):
+    """Predictive variances / covariance matrices at new labels (seen levels, repeated new labels, mixes),
+    matrix_inversion_method = "cholesky" (CalcPred, re_model_template.h:10350-10358, 10510-10522): the
+    reference's sparse triangular solves vs e_p^T A^-1 e_q from the dense inverse factor: 1e-9."""
+    with open(GOLDEN_PRED) as f:
+        case = json.load(f)[name]
+    g = synthetic.bench_groups(case["n"], tuple(case["levels"]))
+    y = synthetic.bench_grouped_y(g)
+    gm = GPModel(group_data=g, matrix_inversion_method="cholesky")
+    cp = np.array(case["cov_pars"])
+    want_cov = "cov" in case
+    p = gm.predict(y=y, group_data_pred=np.array(case["labels"]), cov_pars=cp, predict_var=not want_cov,
+                   predict_cov_mat=want_cov, predict_response=case["response"])
+    np.testing.assert_allclose(p["mu"], case["mean"], rtol=0, atol=1e-10 * np.abs(case["mean"]).max())
+    if want_cov:
+        ref = np.asarray(case["cov"]).reshape(case["npred"], case["npred"])
+        np.testing.assert_allclose(p["cov"], ref, rtol=1e-9, atol=1e-12 * np.abs(ref).max())
+    else:
+        np.testing.assert_allclose(p["var"], case["var"], rtol=1e-9)
