@@ -471,10 +471,8 @@ int GPB_GetCovPar(REModelHandle handle, double* cov_par, bool calc_std_dev) {
   if (GroupedModel* g = as_grouped(handle)) {
     const auto& p = g->last_cov_pars();
     if (p.empty()) gpb_amd::Fatal("Covariance parameters have not been estimated or correctly set ");
-    if (calc_std_dev)
-      gpb_amd::Fatal("standard deviations of covariance parameters are not supported for grouped random effects by "
-                     "gpboost_amd");
     for (size_t k = 0; k < p.size(); ++k) cov_par[k] = p[k];
+    if (calc_std_dev) g->StdDevCovPars(p.data(), cov_par + p.size());
     return 0;
   }
   REModelAMD* m = model(handle);
@@ -561,8 +559,8 @@ int GPB_CalcGradientF(REModelHandle handle, double* y, const double* fixed_effec
 
 int GPB_CanCalculateStandardErrorsCovPars(REModelHandle handle, int* out) {
   API_BEGIN();
-  if (as_grouped(handle) != nullptr) {   // not built for grouped models here
-    out[0] = 0;
+  if (GroupedModel* g = as_grouped(handle)) {   // cholesky: exact Fisher information; iterative: refused
+    out[0] = (int)g->CanCalculateStandardErrorsCovPars();
     return 0;
   }
   out[0] = (int)model(handle)->CanCalculateStandardErrorsCovPars();

@@ -416,6 +416,57 @@ void GroupedRE::PredCov(int np, const std::vector<int>& idx, bool want_cov, doub
   HIP_CHECK(hipStreamSynchronize(s_));
 }
 
+void GroupedRE::Fisher(const double* tau, double sigma2, double* FI) {
+  CheckMethod(tau, false);
+  const int K = K_, M = M_;
+  Diag(tau);
+  std::vector<double> F((size_t)K * K, 0.), tr(K, 0.);
+  if (K == 1) {   // A^-1 = diag(1/D): B_rr = 1 / (tau D_r)
+    std::vector<double> D(M);
+    HIP_CHECK(hipMemcpyAsync(D.data(), d_D_.get(), sizeof(double) * M, hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipStreamSynchronize(s_));
+    for (int r = 0; r < M; ++r) {
+      const double b = 1. / (tau[0] * D[r]);
+      F[0] += b * b;
+      tr[0] += b;
+    }
+  } else {
+    DenseFactor();
+    const int ld = ldM_;
+    // A^-1 = L^-T L^-1 = LiT LiT^T (the clean transposed factor; L itself is not needed any more)
+    gemm_f64(s_, M, M, M, 1., dLiT_.get(), ld, 0, dLiT_.get(), ld, 1, 0., dA_.get(), ld);
+    std::vector<double> sc(M);
+    for (int k = 0; k < K; ++k)
+      for (int r = cum_[k]; r < cum_[k + 1]; ++r) sc[r] = 1. / std::sqrt(tau[k]);
+    DevBuf<double> dsc(M), dpart((size_t)M * K), ddiag(M);
+    HIP_CHECK(hipMemcpyAsync(dsc.get(), sc.data(), sizeof(double) * M, hipMemcpyHostToDevice, s_));
+    launch_gre_fisher_cols(M, ld, K, d_cum_.get(), dsc.get(), dA_.get(), dpart.get(), ddiag.get(), s_);
+    std::vector<double> part((size_t)M * K), diag(M);
+    HIP_CHECK(hipMemcpyAsync(part.data(), dpart.get(), sizeof(double) * part.size(), hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipMemcpyAsync(diag.data(), ddiag.get(), sizeof(double) * M, hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipStreamSynchronize(s_));
+    for (int k = 0; k < K; ++k)
+      for (int c = cum_[k]; c < cum_[k + 1]; ++c) {
+        tr[k] += diag[c];
+        for (int j = 0; j < K; ++j) F[(size_t)j * K + k] += part[(size_t)c * K + j];
+      }
+  }
+  const int P = 1 + K;
+  const double c4 = 0.5 / (sigma2 * sigma2);
+  double f00 = (double)n_ - M;
+  for (double v : F) f00 += v;
+  FI[0] = f00 * c4;
+  for (int j = 0; j < K; ++j) {
+    double rs = 0.;
+    for (int k = 0; k < K; ++k) rs += F[(size_t)j * K + k];
+    FI[j + 1] = FI[(size_t)(j + 1) * P] = (tr[j] - rs) / tau[j] * c4;
+    for (int k = j; k < K; ++k) {
+      const double v = (F[(size_t)j * K + k] + (j == k ? m_[j] - 2. * tr[j] : 0.)) / (tau[j] * tau[k]) * c4;
+      FI[(size_t)(j + 1) * P + k + 1] = FI[(size_t)(k + 1) * P + j + 1] = v;
+    }
+  }
+}
+
 void GroupedRE::Eval(const double* tau, bool want_grad, bool iterative, bool warm, const IterativeConfig& cfg,
                      GroupedParts& out) {
   CheckMethod(tau, iterative);

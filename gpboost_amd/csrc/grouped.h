@@ -77,6 +77,14 @@ class GroupedRE {
   // U - sum_k tau_k [same seen level] + e_p^T A^-1 e_q. K >= 2: E = Li [e_p] on the device (one wave per
   // point), variances ||E_p||^2, covariances E^T E on the MFMA GEMM; K == 1: A^-1 = diag(1/D).
   void PredCov(int np, const std::vector<int>& idx, bool want_cov, double* out);
+  // Fisher information of the original-scale parameters [sigma^2, sigma_1^2 .. sigma_K^2] (cholesky;
+  // CalcFisherInformation_Only_Grouped_REs_Woodbury re_model_template.h:9559-9651 with transf_scale =
+  // false): with B = S^1/2 A^-1 S^1/2 (S = Sigma^-1 on the transformed scale), F_jk = ||B_jk||_F^2 and
+  // t_j = tr(B_jj), Z_j^T Psi^-1 Z_k = S^1/2 (delta_jk I - B_jk) S^1/2 and Psi^-1 Z = Z A^-1 S give
+  //   2 sigma^4 FI_00 = n - M + sum_jk F_jk,  2 sigma^4 FI_0j = (t_j - sum_k F_jk) / tau_j,
+  //   2 sigma^4 FI_jk = (F_jk + delta_jk (m_j - 2 t_j)) / (tau_j tau_k).
+  // Factors A at tau first. FI: (1 + K)^2 row-major.
+  void Fisher(const double* tau, double sigma2, double* FI);
 
  private:
   struct Block {   // work space of a t-column PCG

@@ -65,5 +65,9 @@ void launch_gre_inv_diag(int M, int ld, const double* Li, double* out, hipStream
 // var[p] = ||that column||^2
 void launch_gre_pred_cols(int M, int ld, int K, int np, const int* idx, const double* Li, double* E, double* var,
                           hipStream_t s);
+// Fisher information pieces (cholesky): B = S^1/2 A^-1 S^1/2 (sc[r] = 1 / sqrt(tau_k(r))) from the dense
+// A^-1 (Ainv, ld); part[c K + k] = sum_{r in effect k} B[r, c]^2, diag[c] = B[c, c]. One wave per column.
+void launch_gre_fisher_cols(int M, int ld, int K, const int* cum, const double* sc, const double* Ainv, double* part,
+                            double* diag, hipStream_t s);
 
 }  // namespace gpb_amd

@@ -308,7 +308,34 @@ __global__ void __launch_bounds__(256) gre_pred_cols_kernel(int M, int ld, int K
   for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
   if (var && lane == 0) var[p] = s;
 }
+__global__ void __launch_bounds__(256) gre_fisher_cols_kernel(int M, int ld, int K, const int* __restrict__ cum,
+                                                              const double* __restrict__ sc,
+                                                              const double* __restrict__ Ainv, double* __restrict__ part,
+                                                              double* __restrict__ diag) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (c >= M) return;
+  const double* col = Ainv + (size_t)c * ld;
+  const double scc = sc[c];
+  for (int k = 0; k < K; ++k) {
+    double s = 0.;
+    for (int r = cum[k] + lane; r < cum[k + 1]; r += 64) {
+      const double b = col[r] * sc[r] * scc;
+      s = fma(b, b, s);
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0) part[(size_t)c * K + k] = s;
+  }
+  if (lane == 0) diag[c] = col[c] * scc * scc;
+}
 }  // namespace
+
+void launch_gre_fisher_cols(int M, int ld, int K, const int* cum, const double* sc, const double* Ainv, double* part,
+                            double* diag, hipStream_t s) {
+  hipLaunchKernelGGL(gre_fisher_cols_kernel, dim3((M + 3) / 4), dim3(256), 0, s, M, ld, K, cum, sc, Ainv, part, diag);
+  HIP_CHECK(hipGetLastError());
+}
 
 void launch_gre_pred_cols(int M, int ld, int K, int np, const int* idx, const double* Li, double* E, double* var,
                           hipStream_t s) {

@@ -359,4 +359,45 @@ void GroupedModel::Predict(const double* y, int n_pred, const char* re_group_dat
   }
 }
 
+void GroupedModel::StdDevCovPars(const double* cov_pars, double* sd) {
+  if (iterative())
+    Fatal("standard deviations of covariance parameters for grouped random effects with matrix_inversion_method = "
+          "'iterative' (the reference's stochastic estimate) are not supported by gpboost_amd (use 'cholesky')");
+  UseDevice();
+  const int K = re_->K(), P = 1 + K;
+  for (int k = 0; k < P; ++k)
+    if (!(cov_pars[k] > 0.)) Fatal("covariance parameters must be > 0");
+  std::vector<double> tau(K), FI((size_t)P * P);
+  for (int k = 0; k < K; ++k) tau[k] = cov_pars[1 + k] / cov_pars[0];
+  re_->Fisher(tau.data(), cov_pars[0], FI.data());
+  // FI.inverse() (re_model_template.h:9788): Gauss-Jordan with partial pivoting on the small P x P matrix
+  std::vector<double> inv((size_t)P * P, 0.);
+  for (int i = 0; i < P; ++i) inv[(size_t)i * P + i] = 1.;
+  for (int c = 0; c < P; ++c) {
+    int piv = c;
+    for (int r = c + 1; r < P; ++r)
+      if (std::fabs(FI[(size_t)r * P + c]) > std::fabs(FI[(size_t)piv * P + c])) piv = r;
+    if (!(FI[(size_t)piv * P + c] != 0.) || !std::isfinite(FI[(size_t)piv * P + c]))
+      Fatal("the Fisher information is singular");
+    for (int j = 0; j < P; ++j) {
+      std::swap(FI[(size_t)c * P + j], FI[(size_t)piv * P + j]);
+      std::swap(inv[(size_t)c * P + j], inv[(size_t)piv * P + j]);
+    }
+    const double d = FI[(size_t)c * P + c];
+    for (int j = 0; j < P; ++j) {
+      FI[(size_t)c * P + j] /= d;
+      inv[(size_t)c * P + j] /= d;
+    }
+    for (int r = 0; r < P; ++r) {
+      if (r == c) continue;
+      const double f = FI[(size_t)r * P + c];
+      for (int j = 0; j < P; ++j) {
+        FI[(size_t)r * P + j] -= f * FI[(size_t)c * P + j];
+        inv[(size_t)r * P + j] -= f * inv[(size_t)c * P + j];
+      }
+    }
+  }
+  for (int k = 0; k < P; ++k) sd[k] = std::sqrt(inv[(size_t)k * P + k]);
+}
+
 }  // namespace gpb_amd

@@ -74,6 +74,11 @@ class GroupedModel {
   void Predict(const double* y, int n_pred, const char* re_group_data_pred, const double* cov_pars,
                bool predict_cov_mat, bool predict_var, bool predict_response, const double* fixed_effects,
                const double* fixed_effects_pred, double* out);
+  // GPB_GetCovPar(calc_std_dev) (CalcStdDevCovPar re_model_template.h:9775-9789 ->
+  // CalcFisherInformation_Only_Grouped_REs_Woodbury :9559-9651): sqrt(diag(FI^-1)) at the original-scale
+  // cov_pars; cholesky only (the iterative branch is a stochastic estimate: refused)
+  void StdDevCovPars(const double* cov_pars, double* sd);
+  bool CanCalculateStandardErrorsCovPars() const { return !iterative(); }
   IterativeConfig iter;
 
  private:

@@ -238,3 +238,25 @@ def test_grouped_predictive_variances_match_reference(name):
         np.testing.assert_allclose(p["cov"], ref, rtol=1e-9, atol=1e-12 * np.abs(ref).max())
     else:
         np.testing.assert_allclose(p["var"], case["var"], rtol=1e-9)
+
+
+@pytest.mark.parametrize("name", ["sdg_k1_n5000", "sdg_k2_n20000", "sdg_k3_n20000", "sdg_k2_n3000_small"])
+def test_grouped_std_dev_matches_reference(name):
+    """get_cov_pars(std_err=True), cholesky: CalcFisherInformation_Only_Grouped_REs_Woodbury
+    (re_model_template.h:9559-9651) restated through B = S^1/2 A^-1 S^1/2 on the GPU (csrc/grouped.h):
+    1e-8 against the reference (its sparse solves vs the dense inverse)."""
+    with open(os.path.join(HERE, "golden", "golden_grouped_sd.json")) as f:
+        case = json.load(f)[name]
+    g = synthetic.bench_groups(case["n"], tuple(case["levels"]))
+    y = synthetic.bench_grouped_y(g)
+    gm = GPModel(group_data=g, matrix_inversion_method="cholesky")
+    assert gm.can_calculate_standard_errors_cov_pars()
+    gm.neg_log_likelihood(case["cov_pars"], y)
+    out = gm.get_cov_pars(std_err=True)
+    np.testing.assert_allclose(out[1], case["std_dev"], rtol=1e-8)
+    gi = GPModel(group_data=g) if g.shape[1] > 1 else None   # iterative: the stochastic estimate is refused
+    if gi is not None:
+        assert not gi.can_calculate_standard_errors_cov_pars()
+        gi.neg_log_likelihood(case["cov_pars"], y)
+        with pytest.raises(GPBoostError, match="standard deviations"):
+            gi.get_cov_pars(std_err=True)
