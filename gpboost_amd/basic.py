@@ -102,11 +102,9 @@ class GPModel:
             raise GPBoostError("GP random coefficients are out of scope for gpboost_amd")
         if model_file is not None or model_dict is not None:
             raise GPBoostError("model loading is out of scope for gpboost_amd")
-        if group_data is not None:
-            if gp_coords is not None:
-                raise GPBoostError("models with both grouped random effects and a Gaussian process are not "
-                                   "supported by gpboost_amd")
-            self._init_grouped(group_data, likelihood, matrix_inversion_method, seed, cluster_ids, weights)
+        if group_data is not None:   # grouped random effects, optionally beside one dense GP (gp_approx "none")
+            self._init_grouped(group_data, likelihood, matrix_inversion_method, seed, cluster_ids, weights,
+                               gp_coords, cov_function, cov_fct_shape, gp_approx)
             return
         if gp_coords is None:
             raise ValueError("Either 'group_data' or 'gp_coords' must be provided")
@@ -149,9 +147,11 @@ class GPModel:
         self.num_group_re = 0
         self._post_init()
 
-    def _init_grouped(self, group_data, likelihood, matrix_inversion_method, seed, cluster_ids, weights):
+    def _init_grouped(self, group_data, likelihood, matrix_inversion_method, seed, cluster_ids, weights,
+                      gp_coords=None, cov_function="matern", cov_fct_shape=1.5, gp_approx="none"):
         """Grouped random effects (reference basic.py GPModel.__init__ group_data handling): labels are
-        converted to strings and passed column-major as NUL-terminated C strings."""
+        converted to strings and passed column-major as NUL-terminated C strings. With gp_coords: the
+        combined model with one GP component (gp_approx "none")."""
         g = np.asarray(group_data)
         if g.ndim == 1:
             g = g.reshape(-1, 1)
@@ -164,6 +164,19 @@ class GPModel:
         self.num_neighbors = 0
         self.cov_function = None
         self.cov_fct_shape = 0.
+        self.has_gp = gp_coords is not None
+        coords_cm = None
+        if self.has_gp:
+            coords = np.asarray(gp_coords, dtype=np.float64)
+            if coords.ndim == 1:
+                coords = coords.reshape(-1, 1)
+            if coords.shape[0] != self.num_data:
+                raise ValueError("Incorrect number of data points in 'gp_coords'")
+            self.dim_coords = coords.shape[1]
+            self.cov_function = cov_function
+            self.cov_fct_shape = float(cov_fct_shape)
+            self.gp_approx = gp_approx
+            coords_cm = np.ascontiguousarray(coords.T).reshape(-1)
         labels = g.astype(np.dtype(str)).flatten(order="F")
         buf = ctypes.create_string_buffer(b"\0".join(s.encode() for s in labels) + b"\0")
         cluster = None
@@ -173,8 +186,11 @@ class GPModel:
         _safe_call(lib().GPB_CreateREModel(
             ctypes.c_int32(self.num_data), _ip(cluster) if cluster is not None else None,
             buf, ctypes.c_int32(self.num_group_re), None, None, ctypes.c_int32(0), None,
-            ctypes.c_int32(0), None, ctypes.c_int(0), None, ctypes.c_int32(0),
-            c_str("exponential"), ctypes.c_double(0.5), c_str("none"), ctypes.c_double(1.), ctypes.c_double(1.),
+            ctypes.c_int32(1 if self.has_gp else 0), _dp(coords_cm) if self.has_gp else None,
+            ctypes.c_int(self.dim_coords), None, ctypes.c_int32(0),
+            c_str(cov_function if self.has_gp else "exponential"),
+            ctypes.c_double(self.cov_fct_shape if self.has_gp else 0.5), c_str(self.gp_approx),
+            ctypes.c_double(1.), ctypes.c_double(1.),
             ctypes.c_int(0), c_str("random"), ctypes.c_int(0), ctypes.c_double(1.), c_str("kmeans++"),
             c_str(likelihood), ctypes.c_double(0.), c_str(matrix_inversion_method), ctypes.c_int(seed),
             ctypes.c_int(-1), ctypes.c_bool(True), ctypes.c_bool(weights is not None), None, ctypes.c_double(1.),
@@ -365,7 +381,8 @@ class GPModel:
     def cov_par_names(self):
         """Parameter names as the reference labels them (error term only for the Gaussian likelihood)."""
         if getattr(self, "num_group_re", 0):
-            return ["Error_term"] + [f"Group_{k + 1}" for k in range(self.num_group_re)]
+            return (["Error_term"] + [f"Group_{k + 1}" for k in range(self.num_group_re)] +
+                    (["GP_var", "GP_range"] if getattr(self, "has_gp", False) else []))
         return (["Error_term"] if self.num_cov_pars == 3 else []) + ["GP_var", "GP_range"]
 
     def summary(self, std_err=False):
@@ -621,7 +638,7 @@ class GPModel:
                                        offset_pred, fixed_effects, fixed_effects_pred)
         if getattr(self, "num_group_re", 0):
             return self._predict_grouped(group_data_pred, predict_var, predict_cov_mat, predict_response, y, cov_pars,
-                                         offset, offset_pred, fixed_effects, fixed_effects_pred)
+                                         offset, offset_pred, fixed_effects, fixed_effects_pred, gp_coords_pred)
         if vecchia_pred_type is not None or num_neighbors_pred is not None:
             self.set_prediction_data(vecchia_pred_type=vecchia_pred_type, num_neighbors_pred=num_neighbors_pred)
         if any(v is not None for v in (group_data_pred, group_rand_coef_data_pred, gp_rand_coef_data_pred,
@@ -697,7 +714,7 @@ class GPModel:
         return {"mu": mu, "cov": cov, "var": var}
 
     def _predict_grouped(self, group_data_pred, predict_var, predict_cov_mat, predict_response, y, cov_pars, offset,
-                         offset_pred, fixed_effects, fixed_effects_pred):
+                         offset_pred, fixed_effects, fixed_effects_pred, gp_coords_pred=None):
         """Predictions of a grouped random effects model at new group labels (GPB_PredictREModel
         with re_group_data_pred): means = sum over the effects of the training posterior mean of the
         label's level (0 for a level not seen in training); with predict_var / predict_cov_mat
@@ -721,12 +738,20 @@ class GPModel:
         fe = _as1d(fixed_effects, "fixed_effects") if fixed_effects is not None else None
         fep = _as1d(fixed_effects_pred, "fixed_effects_pred") if fixed_effects_pred is not None else None
         cp = self._check_cov_pars(cov_pars) if cov_pars is not None else None
+        xcol = None
+        if gp_coords_pred is not None:
+            xp = np.asarray(gp_coords_pred, dtype=np.float64)
+            if xp.ndim == 1:
+                xp = xp.reshape(-1, 1)
+            if xp.shape[0] != n_pred:
+                raise ValueError("'gp_coords_pred' and 'group_data_pred' have different numbers of rows")
+            xcol = np.ascontiguousarray(xp.T).reshape(-1)
         size = n_pred + (n_pred * n_pred if predict_cov_mat else (n_pred if predict_var else 0))
         out = np.zeros(size)
         _safe_call(lib().GPB_PredictREModel(
             self.handle, _dp(yv) if yv is not None else None, ctypes.c_int32(n_pred), _dp(out),
             ctypes.c_bool(bool(predict_cov_mat)), ctypes.c_bool(bool(predict_var)),
-            ctypes.c_bool(bool(predict_response)), None, buf, None, None, None,
+            ctypes.c_bool(bool(predict_response)), None, buf, None, _dp(xcol) if xcol is not None else None, None,
             _dp(cp) if cp is not None else None, None, ctypes.c_bool(False),
             _dp(fe) if fe is not None else None, _dp(fep) if fep is not None else None))
         mu = out[:n_pred].copy()

@@ -31,6 +31,15 @@ class DenseSolver {
   // covariance (column-major np x np, nullable) on the transformed scale (before sigma^2 / nugget)
   void Predict(int cov_type, double var, double phi, const double* d_y, const double* Xp, int np, bool want_var,
                bool want_cov, double* mean, double* pvar, double* pcov);
+  // Combined GP + grouped random effects (gp_approx = "none"; re_model_template.h:8430-8441 CalcZSigmaZt sums the
+  // components): Psi gains sum_k tau_k [lev_k(i) == lev_k(j)] (d_lev: device K x n level indices, K <= 8)
+  // in every build; K = 0 switches it off. Predictions then take the prediction points' levels (SetGroupedPred:
+  // device K x np, -1 - id for a label not in the training data, equal ids for equal new labels).
+  void SetGrouped(int K, const int* d_lev, const double* tau);
+  void SetGroupedPred(int np, const int* d_plev);
+  // After Eval(want_grad = true): tr(Psi^-1 dPsi / dlog tau_k) = tau_k sum_{lev_k(i) == lev_k(j)} (Psi^-1)_ij
+  // (K values) and y_aux = Psi^-1 y (host, n) for the quadratic terms.
+  void GroupedTraces(double* s2, double* yaux);
 
  private:
   void Potrf();
@@ -43,6 +52,12 @@ class DenseSolver {
   const double* d_X_;
   hipStream_t stream_;
   DevBuf<double> A_, W_, T_, vec_, red_;
+  void AddGrouped();   // Psi += the grouped term (lower triangle), after a build
+  int gK_ = 0, gnp_ = 0;
+  const int* g_lev_ = nullptr;
+  const int* g_plev_ = nullptr;
+  double g_tau_[8] = {0., 0., 0., 0., 0., 0., 0., 0.};
+  DevBuf<double> g_part_;
   DevBuf<int> info_;
   double* h_red_ = nullptr;
   hipEvent_t ev_[3] = {nullptr, nullptr, nullptr};

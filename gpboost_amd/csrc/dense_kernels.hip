@@ -504,6 +504,75 @@ __global__ void __launch_bounds__(256) build_cross_kernel(const double* __restri
   C[(size_t)i + (size_t)p * ld] = c;
 }
 
+// Combined GP + grouped random effects: the grouped components' covariances sum_k tau_k [lev_k(a) == lev_k(b)]
+struct GroupedTau {
+  double t[8];
+};
+
+// A (lower triangle incl. the diagonal) += sum_k tau_k [lev_k(i) == lev_k(j)]
+__global__ void __launch_bounds__(256) add_grouped_kernel(int n, int ld, int K, const int* __restrict__ lev,
+                                                          GroupedTau tau, double* __restrict__ A) {
+  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+  if (j0 > i0 + 63) return;
+  const int ti = threadIdx.x & 63;
+  for (int jj = threadIdx.x >> 6; jj < 64; jj += 4) {
+    const int i = i0 + ti, j = j0 + jj;
+    if (i >= n || j >= n || j > i) continue;
+    double v = 0.;
+    for (int k = 0; k < K; ++k)
+      if (lev[(size_t)k * n + i] == lev[(size_t)k * n + j]) v += tau.t[k];
+    A[(size_t)i + (size_t)j * ld] += v;
+  }
+}
+
+// C (n x np, ld) += sum_k tau_k [lev_k(i) == plev_k(p)] (cross-covariances to the prediction points), or with
+// lev = plev (np x np, square) the prediction points' own grouped covariances
+__global__ void __launch_bounds__(256) add_grouped_cross_kernel(int n, int np, int ld, int K, const int* __restrict__ lev,
+                                                                const int* __restrict__ plev, GroupedTau tau,
+                                                                double* __restrict__ C) {
+  const int i = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int p = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (i >= n || p >= np) return;
+  double v = 0.;
+  for (int k = 0; k < K; ++k)
+    if (lev[(size_t)k * n + i] == plev[(size_t)k * np + p]) v += tau.t[k];
+  C[(size_t)i + (size_t)p * ld] += v;
+}
+
+// per 64 x 64 tile of the lower triangle of P = Psi^-1: part[tile * K + k] = sum over the tile's entries with
+// lev_k(i) == lev_k(j) of w P_ij (w = 1 on the diagonal, 2 below: the full symmetric sum); upper tiles write 0
+__global__ void __launch_bounds__(256) grouped_trace_kernel(int n, int ld, int K, const int* __restrict__ lev,
+                                                            const double* __restrict__ P, double* __restrict__ part) {
+  __shared__ double red[4][8];
+  const int i0 = blockIdx.y * 64, j0 = blockIdx.x * 64;
+  const int tile = blockIdx.y * gridDim.x + blockIdx.x;
+  double acc[8] = {0., 0., 0., 0., 0., 0., 0., 0.};
+  if (j0 <= i0 + 63) {
+    const int ti = threadIdx.x & 63;
+    for (int jj = threadIdx.x >> 6; jj < 64; jj += 4) {
+      const int i = i0 + ti, j = j0 + jj;
+      if (i >= n || j >= n || j > i) continue;
+      const double v = P[(size_t)i + (size_t)j * ld] * (i == j ? 1. : 2.);
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (k < K && lev[(size_t)k * n + i] == lev[(size_t)k * n + j]) acc[k] += v;
+    }
+  }
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    double s = acc[k];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (lane == 0) red[w][k] = s;
+  }
+  __syncthreads();
+  if (threadIdx.x < K) {
+    const int k = threadIdx.x;
+    part[(size_t)tile * K + k] = (red[0][k] + red[1][k]) + (red[2][k] + red[3][k]);
+  }
+}
+
 // 2 * sum log L_ii -> out (single block, fixed order)
 __global__ void __launch_bounds__(256) logdet_kernel(const double* A, int lda, int n, double* out) {
   __shared__ double red[256];
@@ -1165,6 +1234,7 @@ void DenseSolver::Eval(int cov_type, double var, double phi, const double* d_y, 
                        phi, A);
   });
   HIP_CHECK(hipGetLastError());
+  AddGrouped();
   static const bool no_lookahead = std::getenv("GPBOOST_AMD_DENSE_NO_LOOKAHEAD") != nullptr;   // A/B
   if (!no_lookahead)
     PotrfLookahead();
@@ -1228,6 +1298,7 @@ void DenseSolver::Fisher(int cov_type, double var, double phi, double dscale, do
                        phi, A);
   });
   HIP_CHECK(hipGetLastError());
+  AddGrouped();
   PotrfLookahead();
   Trtri(0, n);
   gemm(stream_, n, n, n, 1., W, ld, 1, W, ld, 0, 0., A, ld, 1, 0, 1, 1);   // P = W^T W (lower)
@@ -1252,6 +1323,43 @@ void DenseSolver::Fisher(int cov_type, double var, double phi, double dscale, do
   for (int q = 0; q < 6; ++q) sums6[q] = h_red_[q];
 }
 
+void DenseSolver::SetGrouped(int K, const int* d_lev, const double* tau) {
+  if (K < 0 || K > 8) Fatal("the dense GP + grouped random effects path supports at most 8 grouped effects, got %d", K);
+  gK_ = K;
+  g_lev_ = d_lev;
+  for (int k = 0; k < 8; ++k) g_tau_[k] = k < K ? tau[k] : 0.;
+}
+
+void DenseSolver::SetGroupedPred(int np, const int* d_plev) {
+  gnp_ = np;
+  g_plev_ = d_plev;
+}
+
+void DenseSolver::AddGrouped() {
+  if (gK_ == 0) return;
+  GroupedTau t;
+  for (int k = 0; k < 8; ++k) t.t[k] = g_tau_[k];
+  const int nt = (n_ + 63) / 64;
+  hipLaunchKernelGGL(add_grouped_kernel, dim3(nt, nt), dim3(256), 0, stream_, n_, ld_, gK_, g_lev_, t, A_.get());
+  HIP_CHECK(hipGetLastError());
+}
+
+void DenseSolver::GroupedTraces(double* s2, double* yaux) {
+  if (gK_ == 0) Fatal("GroupedTraces without grouped effects");
+  const int n = n_, ld = ld_, nt = (n + 63) / 64, K = gK_;
+  const int tiles = nt * nt;
+  g_part_.alloc((size_t)tiles * K + K);
+  double* out = g_part_.get() + (size_t)tiles * K;
+  hipLaunchKernelGGL(grouped_trace_kernel, dim3(nt, nt), dim3(256), 0, stream_, n, ld, K, g_lev_, A_.get(),
+                     g_part_.get());
+  HIP_CHECK(hipGetLastError());
+  launch_sum_blocks(g_part_.get(), tiles, K, out, stream_);
+  HIP_CHECK(hipMemcpyAsync(s2, out, sizeof(double) * K, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipMemcpyAsync(yaux, vec_.get() + ld, sizeof(double) * n, hipMemcpyDeviceToHost, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  for (int k = 0; k < K; ++k) s2[k] *= g_tau_[k];
+}
+
 void DenseSolver::Factor(int cov_type, double var, double phi) {
   const int n = n_, ld = ld_, d = d_;
   HIP_CHECK(hipMemsetAsync(info_.get(), 0, sizeof(int), stream_));
@@ -1261,6 +1369,7 @@ void DenseSolver::Factor(int cov_type, double var, double phi) {
                        phi, A_.get());
   });
   HIP_CHECK(hipGetLastError());
+  AddGrouped();
   PotrfLookahead();
   Trtri(0, n);
 }
@@ -1278,6 +1387,14 @@ void DenseSolver::Predict(int cov_type, double var, double phi, const double* d_
                        stream_, d_X_, dXp.get(), n, np, d, ld, var, phi, C.get());
   });
   HIP_CHECK(hipGetLastError());
+  GroupedTau gt;
+  for (int k = 0; k < 8; ++k) gt.t[k] = g_tau_[k];
+  if (gK_ > 0) {
+    if (gnp_ != np || g_plev_ == nullptr) Fatal("prediction group levels missing for the combined model");
+    hipLaunchKernelGGL(add_grouped_cross_kernel, dim3((n + 63) / 64, (np + 3) / 4), dim3(256), 0, stream_, n, np, ld, gK_,
+                       g_lev_, g_plev_, gt, C.get());
+    HIP_CHECK(hipGetLastError());
+  }
   gemm(stream_, n, np, n, 1., W_.get(), ld, 0, C.get(), ld, 0, 0., T.get(), ld, 0, 1, 0, 0);
   gemm(stream_, n, 1, n, 1., W_.get(), ld, 0, d_y, ld, 0, 0., z.get(), ld, 0, 1, 0, 0);
   gemm(stream_, np, 1, n, 1., T.get(), ld, 1, z.get(), ld, 0, 0., m.get(), np);
@@ -1292,12 +1409,17 @@ void DenseSolver::Predict(int cov_type, double var, double phi, const double* d_
       hipLaunchKernelGGL((build_cross_kernel<decltype(c)::value>), dim3((np + 63) / 64, (np + 3) / 4), dim3(256), 0,
                          stream_, dXp.get(), dXp.get(), np, np, d, np, var, phi, S.get());
     });
+    if (gK_ > 0)
+      hipLaunchKernelGGL(add_grouped_cross_kernel, dim3((np + 63) / 64, (np + 3) / 4), dim3(256), 0, stream_, np, np, np,
+                         gK_, g_plev_, g_plev_, gt, S.get());
     gemm(stream_, np, np, n, -1., T.get(), ld, 1, T.get(), ld, 0, 1., S.get(), np);
     HIP_CHECK(hipMemcpyAsync(pcov, S.get(), sizeof(double) * np * np, hipMemcpyDeviceToHost, stream_));
   }
   CheckInfo();
+  double gvar = 0.;   // every grouped effect adds its variance to the prior variance of a prediction point
+  for (int k = 0; k < gK_; ++k) gvar += g_tau_[k];
   if (want_var)
-    for (int p = 0; p < np; ++p) pvar[p] = var - pvar[p];
+    for (int p = 0; p < np; ++p) pvar[p] = var + gvar - pvar[p];
 }
 
 void DenseSolver::CheckInfo() {

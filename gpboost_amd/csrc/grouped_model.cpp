@@ -65,6 +65,53 @@ GroupedModel::~GroupedModel() {
 
 void GroupedModel::UseDevice() const { HIP_CHECK(hipSetDevice(device_)); }
 
+void GroupedModel::AttachGP(int d, const double* coords_colmajor, int cov_type, int seed) {
+  if (d < 1 || d > 3) Fatal("dim_gp_coords = %d is not supported by gpboost_amd's dense path (1..3)", d);
+  if (coords_colmajor == nullptr) Fatal("gp_coords_data is NULL");
+  if (re_->K() > 8) Fatal("GP + grouped random effects: at most 8 grouped effects are supported by gpboost_amd");
+  if (iterative())
+    Fatal("matrix_inversion_method = 'iterative' is not supported for GP + grouped random effects models by "
+          "gpboost_amd (use 'cholesky')");
+  UseDevice();
+  gp_d_ = d;
+  cov_type_ = cov_type;
+  seed_ = seed;
+  coords_.resize((size_t)n_ * d);
+  for (int i = 0; i < n_; ++i)
+    for (int q = 0; q < d; ++q) coords_[(size_t)i * d + q] = coords_colmajor[(size_t)q * n_ + i];
+  const int K = re_->K();
+  std::vector<int> lev((size_t)K * n_);
+  for (int k = 0; k < K; ++k)
+    for (int i = 0; i < n_; ++i) lev[(size_t)k * n_ + i] = levels_[k][i];
+  d_X_.alloc(coords_.size());
+  d_lev_.alloc(lev.size());
+  d_y_.alloc(n_);
+  HIP_CHECK(hipMemcpyAsync(d_X_.get(), coords_.data(), sizeof(double) * coords_.size(), hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipMemcpyAsync(d_lev_.get(), lev.data(), sizeof(int) * lev.size(), hipMemcpyHostToDevice, stream_));
+  HIP_CHECK(hipStreamSynchronize(stream_));
+  dense_.reset(new DenseSolver(n_, d, d_X_.get(), stream_));
+}
+
+void GroupedModel::ToTrafo(const double* orig, double* trafo) const {
+  const int K = re_->K();
+  trafo[0] = orig[0];
+  for (int k = 0; k < K; ++k) trafo[1 + k] = orig[1 + k] / orig[0];
+  if (has_gp()) {
+    trafo[1 + K] = orig[1 + K] / orig[0];
+    trafo[2 + K] = range_trafo(cov_type_, orig[2 + K]);
+  }
+}
+
+void GroupedModel::ToOrig(const double* trafo, double sigma2, double* orig) const {
+  const int K = re_->K();
+  orig[0] = sigma2;
+  for (int k = 0; k < K; ++k) orig[1 + k] = trafo[1 + k] * sigma2;
+  if (has_gp()) {
+    orig[1 + K] = trafo[1 + K] * sigma2;
+    orig[2 + K] = range_back(cov_type_, trafo[2 + K]);
+  }
+}
+
 void GroupedModel::SetResponseAndOffset(const double* y, const double* fixed_effects) {
   if (y == nullptr && fixed_effects == nullptr) {
     if (!y_set_) Fatal("response variable y has not been set");
@@ -79,6 +126,10 @@ void GroupedModel::SetResponseAndOffset(const double* y, const double* fixed_eff
     if (std::isnan(y_[i]) || std::isinf(y_[i])) Fatal("NaN or Inf in response variable / label ");
   UseDevice();
   re_->SetY(y_.data());
+  if (has_gp()) {
+    HIP_CHECK(hipMemcpyAsync(d_y_.get(), y_.data(), sizeof(double) * n_, hipMemcpyHostToDevice, stream_));
+    HIP_CHECK(hipStreamSynchronize(stream_));
+  }
   y_set_ = true;
 }
 
@@ -88,24 +139,21 @@ void GroupedModel::GetResponseData(double* y) const {
 }
 
 EvalResult GroupedModel::Eval(const double* cov_pars_orig, bool want_grad, int profile) {
-  const int K = re_->K();
-  for (int k = 0; k <= K; ++k)
+  const int P = num_cov_pars();
+  for (int k = 0; k < P; ++k)
     if (!(cov_pars_orig[k] > 0.)) Fatal("covariance parameters must be > 0");
-  std::vector<double> trafo(1 + K);   // TransformCovPars (re_comp.h: sigma_k^2 / sigma^2)
-  trafo[0] = cov_pars_orig[0];
-  for (int k = 0; k < K; ++k) trafo[1 + k] = cov_pars_orig[1 + k] / cov_pars_orig[0];
+  std::vector<double> trafo(P);   // TransformCovPars (re_comp.h: sigma_k^2 / sigma^2; the GP range transform)
+  ToTrafo(cov_pars_orig, trafo.data());
   EvalResult r = EvalTrafo(trafo.data(), want_grad, profile);
-  last_cov_pars_.assign(cov_pars_orig, cov_pars_orig + 1 + K);
-  if (profile) {
-    for (int k = 0; k < K; ++k) last_cov_pars_[1 + k] = trafo[1 + k] * r.sigma2;
-    last_cov_pars_[0] = r.sigma2;
-  }
+  last_cov_pars_.assign(cov_pars_orig, cov_pars_orig + P);
+  if (profile) ToOrig(trafo.data(), r.sigma2, last_cov_pars_.data());
   return r;
 }
 
 EvalResult GroupedModel::EvalTrafo(const double* trafo, bool want_grad, int profile, bool fatal_on_nan) {
   if (!y_set_) Fatal("response variable y has not been set");
   UseDevice();
+  if (has_gp()) return EvalDense(trafo, want_grad, profile, fatal_on_nan);
   const int K = re_->K();
   GroupedParts parts;
   re_->Eval(trafo + 1, want_grad, iterative(), num_iter_ > 0, iter, parts);
@@ -129,6 +177,46 @@ EvalResult GroupedModel::EvalTrafo(const double* trafo, bool want_grad, int prof
       off = 1;
     }
     for (int k = 0; k < K; ++k) res.grad[off + k] = -parts.quad[k] / sigma2 / 2. + parts.trace[k] / 2.;
+  }
+  last_nll_ = res.nll;
+  return res;
+}
+
+EvalResult GroupedModel::EvalDense(const double* trafo, bool want_grad, int profile, bool fatal_on_nan) {
+  // Psi = sum_k tau_k Z_k Z_k^T + v K(phi) + I on the dense path; gradient wrt the log of the transformed
+  // parameters [nugget], tau_1 .. tau_K, v, phi (CalcGradPars dense, re_model_template.h:1798-1818, with the
+  // grouped components' dPsi / dlog tau_k = tau_k Z_k Z_k^T)
+  const int K = re_->K();
+  for (int k = 1; k < K + 3; ++k)
+    if (!(trafo[k] > 0.)) Fatal("covariance parameters must be > 0");
+  dense_->SetGrouped(K, d_lev_.get(), trafo + 1);
+  double sums[6], kms[2];
+  dense_->Eval(cov_type_, trafo[1 + K], trafo[2 + K], d_y_.get(), want_grad, sums, kms);
+  const double q = sums[1];
+  const double sigma2 = profile ? q / n_ : trafo[0];
+  EvalResult res;
+  res.sigma2 = sigma2;
+  res.nll = q / 2. / sigma2 + sums[0] / 2. + n_ / 2. * (std::log(sigma2) + std::log(2. * M_PI));
+  if (!std::isfinite(res.nll)) {
+    if (fatal_on_nan) Fatal("NaN or Inf occurred in the negative log-likelihood");
+    res.nll = std::numeric_limits<double>::quiet_NaN();
+  }
+  if (want_grad) {
+    std::vector<double> s2(K), yaux(n_);
+    dense_->GroupedTraces(s2.data(), yaux.data());
+    const int off = profile ? 0 : 1;
+    res.grad.assign(off + K + 2, 0.);
+    if (!profile) res.grad[0] = -q / sigma2 / 2. + n_ / 2.;
+    for (int k = 0; k < K; ++k) {   // y_aux^T dPsi_k y_aux = tau_k sum over levels of (sum of y_aux)^2
+      std::vector<double> lsum(re_->levels_per_effect()[k], 0.);
+      for (int i = 0; i < n_; ++i) lsum[levels_[k][i]] += yaux[i];
+      double quad = 0.;
+      for (double v : lsum) quad += v * v;
+      quad *= trafo[1 + k];
+      res.grad[off + k] = -quad / sigma2 / 2. + s2[k] / 2.;
+    }
+    res.grad[off + K] = sums[2] / sigma2 + sums[4] / 2.;
+    res.grad[off + K + 1] = sums[3] / sigma2 + sums[5] / 2.;
   }
   last_nll_ = res.nll;
   return res;
@@ -161,14 +249,22 @@ void GroupedModel::SetPreconditioner(const char* preconditioner) {
 }
 
 void GroupedModel::FindInitCovPar(const double* y, double* trafo) const {
-  // re_model_template.h:4388-4485 (Gaussian): sigma^2 = sample variance / 2, tau_k = 1 / K
+  // re_model_template.h:4388-4485 (Gaussian): sigma^2 = sample variance / 2, every component's marginal
+  // variance 1 / num_comps on the transformed scale; the GP range from the median distance (cov_fcts.h
+  // FindInitCovPar, draws from the model's mt19937(seed) when n > 1000)
   double mean = 0., var = 0.;
   for (int i = 0; i < n_; ++i) mean += y[i];
   mean /= n_;
   for (int i = 0; i < n_; ++i) var += (y[i] - mean) * (y[i] - mean);
   var /= (n_ - 1);
+  const int K = re_->K(), comps = K + (has_gp() ? 1 : 0);
   trafo[0] = var / 2.;
-  for (int k = 0; k < re_->K(); ++k) trafo[1 + k] = 1. / re_->K();
+  for (int k = 0; k < K; ++k) trafo[1 + k] = 1. / comps;
+  if (has_gp()) {
+    trafo[1 + K] = 1. / comps;
+    std::mt19937 rng((std::mt19937::result_type)seed_);
+    trafo[2 + K] = init_range_trafo(coords_, gp_d_, cov_type_, rng);
+  }
 }
 
 void GroupedModel::GetInitCovPar(double* out) const {
@@ -218,18 +314,13 @@ void GroupedModel::OptimCovPar(const double* y, const double* fixed_effects) {
   UseDevice();
   if (y == nullptr && y_raw_.empty()) Fatal("response variable y has not been set");
   SetResponseAndOffset(y != nullptr ? y : y_raw_.data(), fixed_effects);
-  const int K = re_->K();
+  const int P = num_cov_pars();
   num_iter_ = 0;   // re_model_template.h:974
-  std::vector<double> trafo(1 + K);
-  if (cov_pars_initialized_) {
-    trafo[0] = cov_pars_orig_[0];
-    for (int k = 0; k < K; ++k) trafo[1 + k] = cov_pars_orig_[1 + k] / cov_pars_orig_[0];
-  } else {
-    FindInitCovPar(y_.data(), trafo.data());
-  }
-  std::vector<double> start_orig(1 + K);
-  start_orig[0] = trafo[0];
-  for (int k = 0; k < K; ++k) start_orig[1 + k] = trafo[1 + k] * trafo[0];
+  std::vector<double> trafo(P);
+  if (cov_pars_initialized_) ToTrafo(cov_pars_orig_.data(), trafo.data());
+  else FindInitCovPar(y_.data(), trafo.data());
+  std::vector<double> start_orig(P);
+  ToOrig(trafo.data(), trafo[0], start_orig.data());
   if (!cov_pars_initialized_) init_used_ = start_orig;
   if (optim_.max_iterations <= 0) {
     num_it_ = 0;
@@ -238,8 +329,8 @@ void GroupedModel::OptimCovPar(const double* y, const double* fixed_effects) {
     last_cov_pars_ = cov_pars_orig_;
     return;
   }
-  std::vector<double> x(K);
-  for (int k = 0; k < K; ++k) x[k] = std::log(trafo[1 + k]);
+  std::vector<double> x(P - 1);   // log of the transformed parameters, sigma^2 profiled out
+  for (int k = 0; k < P - 1; ++k) x[k] = std::log(trafo[1 + k]);
   double fx = 0.;
   GroupedProfiledObjective obj(this);
   num_it_ = lbfgs_minimize(obj, x, fx, optim_);
@@ -247,9 +338,9 @@ void GroupedModel::OptimCovPar(const double* y, const double* fixed_effects) {
     if (std::isnan(v) || std::isinf(v))
       Fatal("NaN or Inf occurred in covariance parameter optimization using 'lbfgs' (the reference's nelder_mead "
             "restart is not supported by gpboost_amd)");
-  const double s2 = obj.sigma2();
-  cov_pars_orig_.assign(1 + K, s2);
-  for (int k = 0; k < K; ++k) cov_pars_orig_[1 + k] = std::exp(x[k]) * s2;
+  for (int k = 0; k < P - 1; ++k) trafo[1 + k] = std::exp(x[k]);
+  cov_pars_orig_.assign(P, 0.);
+  ToOrig(trafo.data(), obj.sigma2(), cov_pars_orig_.data());
   cov_pars_initialized_ = true;
   last_nll_ = fx;
   last_cov_pars_ = cov_pars_orig_;
@@ -280,6 +371,9 @@ std::vector<double> GroupedModel::Blup(const double* cov_pars, const double* y, 
 void GroupedModel::PredictTrainingDataRandomEffects(const double* cov_pars, const double* y, double* out,
                                                     const double* fixed_effects, bool calc_var) {
   const int K = re_->K();
+  if (has_gp())
+    Fatal("PredictTrainingDataRandomEffects() for GP + grouped random effects models is not supported by "
+          "gpboost_amd (call predict())");
   if (calc_var && iterative())
     Fatal("PredictTrainingDataRandomEffects() is currently not implemented for matrix_inversion_method_ == '%s' and "
           "likelihood == 'Gaussian'. Call the predict() function instead.", mim_.c_str());
@@ -296,9 +390,15 @@ void GroupedModel::PredictTrainingDataRandomEffects(const double* cov_pars, cons
   }
 }
 
-void GroupedModel::Predict(const double* y, int n_pred, const char* re_group_data_pred, const double* cov_pars,
-                           bool predict_cov_mat, bool predict_var, bool predict_response, const double* fixed_effects,
-                           const double* fixed_effects_pred, double* out) {
+void GroupedModel::Predict(const double* y, int n_pred, const char* re_group_data_pred, const double* gp_coords_pred,
+                           const double* cov_pars, bool predict_cov_mat, bool predict_var, bool predict_response,
+                           const double* fixed_effects, const double* fixed_effects_pred, double* out) {
+  if (has_gp()) {
+    PredictCombined(y, n_pred, re_group_data_pred, gp_coords_pred, cov_pars, predict_cov_mat, predict_var,
+                    predict_response, fixed_effects, fixed_effects_pred, out);
+    return;
+  }
+  if (gp_coords_pred != nullptr) Fatal("gp_coords_pred given for a model without a Gaussian process");
   if ((predict_cov_mat || predict_var) && iterative())
     Fatal("predictive (co)variances for grouped random effects with matrix_inversion_method = 'iterative' (the "
           "reference's simulation-based estimate) are not supported by gpboost_amd (use 'cholesky')");
@@ -359,7 +459,83 @@ void GroupedModel::Predict(const double* y, int n_pred, const char* re_group_dat
   }
 }
 
+
+std::vector<int> GroupedModel::PredLevels(int n_pred, const char* re_group_data_pred,
+                                          std::vector<std::vector<std::string>>* labels) const {
+  const int K = re_->K();
+  std::vector<int> lev((size_t)K * n_pred, -1);
+  if (labels) labels->assign(K, std::vector<std::string>(n_pred));
+  const char* p = re_group_data_pred;
+  for (int k = 0; k < K; ++k) {
+    std::unordered_map<std::string, int> fresh;
+    for (int i = 0; i < n_pred; ++i) {
+      std::string label(p);
+      p += label.size() + 1;
+      auto it = label_index_[k].find(label);
+      if (it != label_index_[k].end()) {
+        lev[(size_t)k * n_pred + i] = it->second;
+      } else {
+        auto f = fresh.emplace(label, (int)fresh.size()).first;
+        lev[(size_t)k * n_pred + i] = -1 - f->second;
+      }
+      if (labels) (*labels)[k][i] = std::move(label);
+    }
+  }
+  return lev;
+}
+
+void GroupedModel::PredictCombined(const double* y, int n_pred, const char* re_group_data_pred,
+                                   const double* gp_coords_pred, const double* cov_pars, bool predict_cov_mat,
+                                   bool predict_var, bool predict_response, const double* fixed_effects,
+                                   const double* fixed_effects_pred, double* out) {
+  // CalcPred, !use_woodbury_identity_ branch (re_model_template.h:10165-10244, 10265-10266, 10361-10365,
+  // 10526-10534): cross-covariance = grouped indicators + GP cross-covariance, mean = cross_cov Psi^-1 y,
+  // cov = Sigma_pp - cross_cov Psi^-1 cross_cov^T, times sigma^2, plus the nugget for responses
+  if (n_pred <= 0) Fatal("num_data_pred must be > 0");
+  if (re_group_data_pred == nullptr || gp_coords_pred == nullptr)
+    Fatal("predictions of GP + grouped random effects models need both group_data_pred and gp_coords_pred");
+  if (predict_cov_mat && n_pred > 40000)
+    Fatal("predictive covariance matrices are limited to 40000 prediction points by gpboost_amd");
+  UseDevice();
+  const int K = re_->K(), P = num_cov_pars();
+  std::vector<double> cp;
+  if (cov_pars != nullptr) cp.assign(cov_pars, cov_pars + P);
+  else if (!last_cov_pars_.empty()) cp = last_cov_pars_;
+  else Fatal("Covariance parameters have not been estimated or correctly set ");
+  for (double v : cp)
+    if (!(v > 0.)) Fatal("covariance parameters must be > 0");
+  if (y != nullptr || fixed_effects != nullptr) SetResponseAndOffset(y, fixed_effects);
+  if (!y_set_) Fatal("Response variable data is not provided and has not been set before");
+  std::vector<double> trafo(P);
+  ToTrafo(cp.data(), trafo.data());
+  const std::vector<int> plev = PredLevels(n_pred, re_group_data_pred, nullptr);
+  DevBuf<int> d_plev(plev.size());
+  HIP_CHECK(hipMemcpyAsync(d_plev.get(), plev.data(), sizeof(int) * plev.size(), hipMemcpyHostToDevice, stream_));
+  std::vector<double> xp((size_t)n_pred * gp_d_);
+  for (int i = 0; i < n_pred; ++i)
+    for (int q = 0; q < gp_d_; ++q) xp[(size_t)i * gp_d_ + q] = gp_coords_pred[(size_t)q * n_pred + i];
+  dense_->SetGrouped(K, d_lev_.get(), trafo.data() + 1);
+  dense_->SetGroupedPred(n_pred, d_plev.get());
+  std::vector<double> mean(n_pred), var(predict_var && !predict_cov_mat ? n_pred : 0),
+      cov(predict_cov_mat ? (size_t)n_pred * n_pred : 0);
+  dense_->Predict(cov_type_, trafo[1 + K], trafo[2 + K], d_y_.get(), xp.data(), n_pred,
+                  predict_var && !predict_cov_mat, predict_cov_mat, mean.data(), var.data(), cov.data());
+  dense_->SetGroupedPred(0, nullptr);
+  const double nug = predict_response ? 1. : 0., s2 = cp[0];
+  for (int i = 0; i < n_pred; ++i) out[i] = mean[i] + (fixed_effects_pred ? fixed_effects_pred[i] : 0.);
+  if (predict_cov_mat) {
+    for (int q = 0; q < n_pred; ++q)
+      for (int i = 0; i < n_pred; ++i)
+        out[n_pred + (size_t)q * n_pred + i] = (cov[(size_t)q * n_pred + i] + (i == q ? nug : 0.)) * s2;
+  } else if (predict_var) {
+    for (int i = 0; i < n_pred; ++i) out[n_pred + i] = (var[i] + nug) * s2;
+  }
+}
+
 void GroupedModel::StdDevCovPars(const double* cov_pars, double* sd) {
+  if (has_gp())
+    Fatal("standard deviations of covariance parameters for GP + grouped random effects models are not "
+          "supported by gpboost_amd");
   if (iterative())
     Fatal("standard deviations of covariance parameters for grouped random effects with matrix_inversion_method = "
           "'iterative' (the reference's stochastic estimate) are not supported by gpboost_amd (use 'cholesky')");

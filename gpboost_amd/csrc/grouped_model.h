@@ -28,10 +28,17 @@ class GroupedModel {
   GroupedModel(int n, const std::vector<std::vector<int>>& levels, const std::string& matrix_inversion_method,
                int seed, std::vector<std::unordered_map<std::string, int>> label_index = {});
   ~GroupedModel();
+  // Combined model (re_model_template.h:236-239 allows grouped random effects beside a GP for
+  // gp_approx = "none"): one dense GP component on coords (host column-major n x d, as GPB_CreateREModel passes
+  // them) with covariance cov_type. Parameters [sigma^2, sigma_1^2 .. sigma_K^2, sigma_gp^2, rho] (the
+  // reference's component order: grouped effects first); the likelihood on DenseSolver with the grouped term.
+  void AttachGP(int d, const double* coords_colmajor, int cov_type, int seed);
+  bool has_gp() const { return dense_ != nullptr; }
+  int gp_dim() const { return gp_d_; }
 
   int n() const { return n_; }
   int K() const { return re_->K(); }
-  int num_cov_pars() const { return 1 + re_->K(); }
+  int num_cov_pars() const { return 1 + re_->K() + (has_gp() ? 2 : 0); }
   const std::string& matrix_inversion_method() const { return mim_; }
   bool iterative() const { return mim_ == "iterative"; }
   std::string cg_preconditioner_type() const { return iterative() ? "ssor" : ""; }
@@ -71,19 +78,31 @@ class GroupedModel {
   // predict_var / predict_cov_mat (cholesky only; iterative: the reference's simulation, refused) the
   // predictive (co)variances nugget [predict_response] + sum_k tau_k [new level, same label] + e_p^T A^-1 e_q,
   // e_p the indicator of p's seen levels (derivation in grouped.h), times sigma^2.
-  void Predict(const double* y, int n_pred, const char* re_group_data_pred, const double* cov_pars,
-               bool predict_cov_mat, bool predict_var, bool predict_response, const double* fixed_effects,
-               const double* fixed_effects_pred, double* out);
+  // Combined models: gp_coords_pred (column-major n_pred x d) required; mean = Sigma_po Psi^-1 y, (co)variances
+  // from the dense factor with the grouped cross-covariances (DenseSolver::Predict).
+  void Predict(const double* y, int n_pred, const char* re_group_data_pred, const double* gp_coords_pred,
+               const double* cov_pars, bool predict_cov_mat, bool predict_var, bool predict_response,
+               const double* fixed_effects, const double* fixed_effects_pred, double* out);
   // GPB_GetCovPar(calc_std_dev) (CalcStdDevCovPar re_model_template.h:9775-9789 ->
   // CalcFisherInformation_Only_Grouped_REs_Woodbury :9559-9651): sqrt(diag(FI^-1)) at the original-scale
   // cov_pars; cholesky only (the iterative branch is a stochastic estimate: refused)
   void StdDevCovPars(const double* cov_pars, double* sd);
-  bool CanCalculateStandardErrorsCovPars() const { return !iterative(); }
+  bool CanCalculateStandardErrorsCovPars() const { return !iterative() && !has_gp(); }
   IterativeConfig iter;
 
  private:
   void UseDevice() const;
   void FindInitCovPar(const double* y, double* trafo) const;
+  // transformed <-> original scale: tau_k = sigma_k^2 / sigma^2, v = sigma_gp^2 / sigma^2, phi = range_trafo(rho)
+  void ToTrafo(const double* orig, double* trafo) const;
+  void ToOrig(const double* trafo, double sigma2, double* orig) const;
+  EvalResult EvalDense(const double* trafo, bool want_grad, int profile, bool fatal_on_nan);
+  // the prediction points' level indices (K x n_pred, effect-major; -1 - id for labels not seen in training,
+  // equal ids for equal new labels) and the per-effect label strings (nullable)
+  void PredictCombined(const double* y, int n_pred, const char* re_group_data_pred, const double* gp_coords_pred,
+                       const double* cov_pars, bool predict_cov_mat, bool predict_var, bool predict_response,
+                       const double* fixed_effects, const double* fixed_effects_pred, double* out);
+  std::vector<int> PredLevels(int n_pred, const char* re_group_data_pred, std::vector<std::vector<std::string>>* labels) const;
   std::vector<double> Blup(const double* cov_pars, const double* y, const double* fixed_effects,
                            std::vector<double>* var);
 
@@ -104,6 +123,12 @@ class GroupedModel {
   int num_iter_ = 0;   // the reference's num_iter_ (warm starts of the A^-1 Z^T y solve)
   double last_nll_ = 0.;
   int last_cg_its_ = 0, last_lanczos_ = 0;
+  // combined GP + grouped (AttachGP)
+  std::unique_ptr<DenseSolver> dense_;
+  int gp_d_ = 0, cov_type_ = 0, seed_ = 0;
+  std::vector<double> coords_;   // row-major n x d
+  DevBuf<double> d_X_, d_y_;
+  DevBuf<int> d_lev_;            // K x n
 };
 
 // Parses re_group_data (column-major K x n NUL-terminated labels, re_model_template.h:6246-6270)

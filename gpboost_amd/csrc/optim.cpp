@@ -188,18 +188,24 @@ double REModelAMD::InitialRangeTrafo() const {
   // continuing the generator after the inducing-point selection; full_scale_vecchia: the Vecchia component
   // (all points in the model order, :4452-4456) with the generator after the shuffle and the selection
   const std::vector<double>& X = fitc_ ? fitc_->inducing_points() : coords_vo_;
-  const int d = cfg_.d, n = (int)(X.size() / d);
-  const int kMaxPoints = 1000;
-  const int nf = std::min(n, kMaxPoints);
-  std::vector<int> idx(nf);
-  if (nf < n) {
-    std::mt19937 rng(cfg_.seed);
+  std::mt19937 rng(cfg_.seed);
+  if ((int)(X.size() / cfg_.d) > 1000) {
     if (fitc_ || vif_) rng = fitc_rng_;   // full_scale_vecchia: after the shuffle and the inducing points
     if (vecchia_ && cfg_.vecchia_ordering == "random") {   // the ordering shuffle of the n observations
       std::vector<int> dummy(cfg_.n);
       std::iota(dummy.begin(), dummy.end(), 0);
       std::shuffle(dummy.begin(), dummy.end(), rng);
     }
+  }
+  return init_range_trafo(X, cfg_.d, cfg_.cov_type, rng);
+}
+
+double init_range_trafo(const std::vector<double>& X, int d, int cov_type, std::mt19937& rng) {
+  const int n = (int)(X.size() / d);
+  const int kMaxPoints = 1000;
+  const int nf = std::min(n, kMaxPoints);
+  std::vector<int> idx(nf);
+  if (nf < n) {
     std::uniform_int_distribution<> dis(0, n - 1);
     for (int i = 0; i < nf; ++i) idx[i] = dis(rng);
   } else {
@@ -222,7 +228,7 @@ double REModelAMD::InitialRangeTrafo() const {
   if (med < kEpsilonNumbers)
     Fatal("Cannot find an initial value for the range parameter since both the median and the average distances among coordinates are zero %s",
           nf < n ? "on a random sub-sample of size 1000 " : "");
-  switch (cfg_.cov_type) {
+  switch (cov_type) {
     case kMatern05: return 2. * 3. / med;
     case kMatern15: return 2. * 4.7 / med;
     case kMatern25: return 2. * 5.9 / med;

@@ -27,8 +27,6 @@ int parse_likelihood(const std::string& name) {
   return -1;
 }
 
-namespace {
-
 int parse_cov(const std::string& name, double shape) {
   // cov_fcts.h:2753-2770 ParseCovFunctionAlias; :170-183 shape handling
   auto eq = [](double a, double b) { return std::fabs(a - b) < 1e-10; };
@@ -42,8 +40,6 @@ int parse_cov(const std::string& name, double shape) {
   if (name == "gaussian" || name == "Gaussian") return kGaussian;
   Fatal("cov_fct '%s' is not supported by gpboost_amd (supported: exponential, matern, gaussian)", name.c_str());
 }
-
-}  // namespace
 
 double range_trafo(int cov_type, double rho) {
   switch (cov_type) {

@@ -12,6 +12,7 @@
 #include <rccl/rccl.h>
 
 #include <memory>
+#include <random>
 #include <string>
 #include <vector>
 
@@ -50,6 +51,12 @@ struct ModelConfig {
 
 int parse_likelihood(const std::string& name);   // LatentLik code
 // cov_fcts.h:438-460: range rho -> phi on the transformed scale
+// cov_fcts.h:2753-2770 ParseCovFunctionAlias (+ shape) -> kMatern05 / kMatern15 / kMatern25 / kGaussian
+int parse_cov(const std::string& name, double shape);
+// FindInitCovPar's initial transformed range (cov_fcts.h:1275-1450): median distance among the points X
+// (host row-major n x d), at most 1000 of them drawn uniformly with rng (which continues the caller's
+// generator) when n > 1000
+double init_range_trafo(const std::vector<double>& X, int d, int cov_type, std::mt19937& rng);
 double range_trafo(int cov_type, double rho);
 // cov_fcts.h TransformBackCovPars: range transform phi -> range rho
 double range_back(int cov_type, double phi);

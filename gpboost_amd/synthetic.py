@@ -73,6 +73,19 @@ def _rtest_field(n: int = 100) -> tuple[np.ndarray, np.ndarray]:
     return coords, chol @ norm.ppf(sim_rand_unif(n, 0.8))
 
 
+def rtest_combined_y(n: int = 100) -> tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """The R tests' combined GP + grouped random effects data (test_GPModel_combined_GP_random_effects.R:23-79):
+    coords, group = rep(1:10, each = n/10), y = L b_1 + Z1 b_gr_1 + xi."""
+    from scipy.stats import norm
+
+    coords, field = _rtest_field(n)
+    m = 10
+    group = np.repeat(np.arange(1, m + 1), n // m)
+    b_gr_1 = norm.ppf(sim_rand_unif(m, 0.56))
+    xi = norm.ppf(sim_rand_unif(n, 0.1)) / 5.0
+    return coords, group, field + b_gr_1[group - 1] + xi
+
+
 def rtest_poisson_y(n: int = 100) -> tuple[np.ndarray, np.ndarray]:
     """R non-Gaussian test data, spatial Poisson case (test_GPModel_non_Gaussian_data.R:2386-2387):
     y = qpois(sim_rand_unif(n, 0.435), exp(L b_1))."""

@@ -172,8 +172,9 @@ int main(int argc, char** argv) {
       likelihood.c_str(), 0., mim.c_str(), seed, threads, false, false, nullptr, 1.));
 #else
   typedef REModelTemplate<den_mat_t, chol_den_mat_t> Model;
+  // grouped random effects beside the GP (combined model, gp_approx = "none"): the same label input
   std::unique_ptr<Model> m(new Model(
-      n, nullptr, nullptr, 0, nullptr, nullptr, 0, nullptr,
+      n, nullptr, num_re_group > 0 ? re_group_data.data() : nullptr, num_re_group, nullptr, nullptr, 0, nullptr,
       1, coords.data(), d, nullptr, 0, cov_fct.c_str(), shape, gp_approx.c_str(),
       -1., 0., num_neighbors, ordering.c_str(), num_ind_points, cover_tree_radius, ind_points_selection.c_str(),
       likelihood.c_str(), 0., mim.c_str(), seed, threads, false, false, nullptr, 1.));
@@ -369,8 +370,10 @@ int main(int argc, char** argv) {
     if (!fp) { std::perror("open pred"); return 2; }
     int32_t np = 0;
     if (std::fread(&np, 4, 1, fp) != 1 || np <= 0) return 2;
-    std::vector<double> xp;
+    // (combined GP + grouped models: double coords[np * d] first, then the labels)
+    std::vector<double> xp((size_t)np * d);
     std::string re_group_pred;
+    if (d > 0 && std::fread(xp.data(), 8, xp.size(), fp) != xp.size()) return 2;
     if (num_re_group > 0) {
       std::vector<int32_t> lab((size_t)np * num_re_group);
       if (std::fread(lab.data(), 4, lab.size(), fp) != lab.size()) return 2;
@@ -378,16 +381,13 @@ int main(int argc, char** argv) {
         re_group_pred += std::to_string(v);
         re_group_pred.push_back('\0');
       }
-    } else {
-      xp.resize((size_t)np * d);
-      if (std::fread(xp.data(), 8, xp.size(), fp) != xp.size()) return 2;
     }
     std::fclose(fp);
     const bool pcov = get(args, "predict_cov", "0") == "1";
     const bool pvar = !pcov && get(args, "predict_var", "0") == "1";
     const bool presp = get(args, "predict_response", "0") == "1";
     const std::string ptype = get(args, "vecchia_pred_type", "");
-    if (num_re_group == 0)
+    if (d > 0)
       m->SetPredictionData(np, nullptr, nullptr, nullptr, xp.data(), nullptr, nullptr,
                            ptype.empty() ? nullptr : ptype.c_str(),
                            std::atoi(get(args, "num_neighbors_pred", "-1").c_str()),
@@ -395,7 +395,7 @@ int main(int argc, char** argv) {
                            std::atoi(get(args, "nsim_var_pred", "-1").c_str()), -1);
     std::vector<double> out((size_t)np + (pcov ? (size_t)np * np : (size_t)np), 0.);
     m->Predict(trafo.data(), y.data(), np, out.data(), true, pcov, pvar, presp, nullptr, nullptr, nullptr,
-               num_re_group > 0 ? re_group_pred.data() : nullptr, nullptr, num_re_group > 0 ? nullptr : xp.data(),
+               num_re_group > 0 ? re_group_pred.data() : nullptr, nullptr, d > 0 ? xp.data() : nullptr,
                nullptr, false, fe_ptr, nullptr);
     std::printf("{\n\"n\": %d, \"d\": %d, \"np\": %d,\n", n, d, np);
     print_vec("mean", out.data(), np);

@@ -57,7 +57,7 @@ def run_ref(coords: np.ndarray | None, y: np.ndarray, X: np.ndarray | None = Non
             f.write(np.ascontiguousarray(groups.T).astype(np.int32).tobytes())
         path = f.name
     try:
-        args = [HARNESS_GROUPED if groups is not None else HARNESS, path] + [f"{k}={v}" for k, v in opts.items()]
+        args = [HARNESS_GROUPED if (groups is not None and d == 0) else HARNESS, path] + [f"{k}={v}" for k, v in opts.items()]
         out = subprocess.run(args, check=True, capture_output=True, text=True,
                              env=dict(os.environ, OMP_NUM_THREADS="8"))
         return json.loads(out.stdout)
