@@ -214,7 +214,9 @@ class GPModel:
                        # covariance-parameter optimizer (reference basic.py:4510-4533 defaults)
                        "optimizer_cov": None, "init_cov_pars": None, "maxit": 1000, "delta_rel_conv": -1.,
                        "lr_cov": -1., "m_lbfgs": -1, "trace": False,
-                       "convergence_criterion": "relative_change_in_log_likelihood"}
+                       "convergence_criterion": "relative_change_in_log_likelihood",
+                       "acc_rate_cov": 0.5, "use_nesterov_acc": True, "nesterov_schedule_version": 0,
+                       "momentum_offset": 2}
 
     def __del__(self):
         try:
@@ -249,9 +251,11 @@ class GPModel:
 
     def set_optim_params(self, params=None):
         """Store likelihood-path and optimizer settings through GPB_SetOptimConfig (reference
-        basic.py:5380-5540). Covariance-parameter optimizer: "lbfgs" (the reference default) only;
-        keys of the other optimizers (gradient descent, Nesterov, coefficients) are accepted and have
-        no effect."""
+        basic.py:5380-5540). Covariance-parameter optimizers: "lbfgs" (the reference default),
+        "gradient_descent" (Nesterov: use_nesterov_acc, acc_rate_cov, momentum_offset,
+        nesterov_schedule_version) and "fisher_scoring" (Gaussian likelihood, no covariates);
+        convergence_criterion as the reference's. Keys of the coefficient optimizers are accepted and
+        have no effect."""
         if params:
             for key, val in params.items():
                 if key == "init_aux_pars" and val is not None:
@@ -268,8 +272,9 @@ class GPModel:
         init = p["init_cov_pars"]
         no_index = np.array([-1], dtype=np.int32)
         _safe_call(lib().GPB_SetOptimConfig(
-            self.handle, _dp(init) if init is not None else None, float(p["lr_cov"]), 0.5, int(p["maxit"]),
-            float(p["delta_rel_conv"]), True, 0, bool(p["trace"]), c_str(p["optimizer_cov"]), 2,
+            self.handle, _dp(init) if init is not None else None, float(p["lr_cov"]), float(p["acc_rate_cov"]),
+            int(p["maxit"]), float(p["delta_rel_conv"]), bool(p["use_nesterov_acc"]),
+            int(p["nesterov_schedule_version"]), bool(p["trace"]), c_str(p["optimizer_cov"]), int(p["momentum_offset"]),
             c_str(p["convergence_criterion"]), 0, None, 0.1, 0.5, None,
             int(p["cg_max_num_it"]), int(p["cg_max_num_it_tridiag"]), float(p["cg_delta_conv"]),
             int(p["num_rand_vec_trace"]), bool(p["reuse_rand_vec_trace"]),

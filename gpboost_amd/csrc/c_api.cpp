@@ -234,13 +234,17 @@ int GPB_SetOptimConfig(REModelHandle handle, double* init_cov_pars, double lr, d
   // of the covariance-parameter optimizer (GPB_OptimCovPar; "lbfgs" only). Settings of the
   // gradient-descent / Nesterov / coefficient optimizers have no effect here (no covariates).
   API_BEGIN();
-  (void)acc_rate_cov; (void)use_nesterov_acc; (void)nesterov_schedule_version; (void)trace; (void)momentum_offset;
-  (void)convergence_criterion;   // L-BFGS always tests the relative change of the objective (optim_utils.h:656-657)
+  // acc_rate_cov / use_nesterov_acc / nesterov_schedule_version / momentum_offset / convergence_criterion drive the
+  // internal optimizers ("gradient_descent", "fisher_scoring"); L-BFGS always tests the relative change of the
+  // objective (optim_utils.h:656-657)
+  (void)trace;
   (void)lr_coef; (void)acc_rate_coef; (void)piv_chol_rank;
   if (GroupedModel* g = as_grouped(handle)) {   // Gaussian grouped model: no aux parameters, no coefficients
     (void)num_covariates; (void)init_coef; (void)optimizer_coef; (void)init_aux_pars; (void)estimate_aux_pars;
     (void)delta_conv_mode_finding;
     g->SetOptimSettings(init_cov_pars, lr, max_iter, delta_rel_conv, optimizer, m_lbfgs);
+    g->SetInternalOptimSettings(acc_rate_cov, use_nesterov_acc, nesterov_schedule_version, momentum_offset,
+                                convergence_criterion);
     if (g->iterative()) {
       g->SetPreconditioner(cg_preconditioner_type);
       g->iter.cg_max_num_it = cg_max_num_it;
@@ -267,6 +271,8 @@ int GPB_SetOptimConfig(REModelHandle handle, double* init_cov_pars, double lr, d
       gpb_amd::Fatal("cg_preconditioner_type '%s' is not supported by gpboost_amd (supported: vadu)", p.c_str());
   }
   m->SetOptimSettings(init_cov_pars, lr, max_iter, delta_rel_conv, optimizer, m_lbfgs);
+  m->SetInternalOptimSettings(acc_rate_cov, use_nesterov_acc, nesterov_schedule_version, momentum_offset,
+                              convergence_criterion);
   // validated above; the preconditioner name is recorded for iterative models only (canonical "vadu")
   m->SetOptimizerNames(optimizer, optimizer_coef, iterative ? cg_preconditioner_type : nullptr);
   if (iterative) {   // :775-801
@@ -596,8 +602,8 @@ int GPB_PredictREModelTrainingDataRandomEffects(REModelHandle handle, const doub
 
 int GPB_GetOptimizerCovPars(REModelHandle handle, char* out_str, int* num_char) {
   API_BEGIN();
-  if (as_grouped(handle) != nullptr) {   // InitializeOptimSettings (re_model_template.h:7463-7474)
-    copy_name("lbfgs", out_str, num_char);
+  if (GroupedModel* g = as_grouped(handle)) {   // InitializeOptimSettings (re_model_template.h:7463-7474)
+    copy_name(g->optimizer_cov(), out_str, num_char);
     return 0;
   }
   copy_name(model(handle)->optimizer_cov(), out_str, num_char);

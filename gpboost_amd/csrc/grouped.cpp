@@ -417,10 +417,31 @@ void GroupedRE::PredCov(int np, const std::vector<int>& idx, bool want_cov, doub
 }
 
 void GroupedRE::Fisher(const double* tau, double sigma2, double* FI) {
+  const int K = K_, M = M_;
+  std::vector<double> F, tr;
+  FisherParts(tau, F, tr);
+  const int P = 1 + K;
+  const double c4 = 0.5 / (sigma2 * sigma2);
+  double f00 = (double)n_ - M;
+  for (double v : F) f00 += v;
+  FI[0] = f00 * c4;
+  for (int j = 0; j < K; ++j) {
+    double rs = 0.;
+    for (int k = 0; k < K; ++k) rs += F[(size_t)j * K + k];
+    FI[j + 1] = FI[(size_t)(j + 1) * P] = (tr[j] - rs) / tau[j] * c4;
+    for (int k = j; k < K; ++k) {
+      const double v = (F[(size_t)j * K + k] + (j == k ? m_[j] - 2. * tr[j] : 0.)) / (tau[j] * tau[k]) * c4;
+      FI[(size_t)(j + 1) * P + k + 1] = FI[(size_t)(k + 1) * P + j + 1] = v;
+    }
+  }
+}
+
+void GroupedRE::FisherParts(const double* tau, std::vector<double>& F, std::vector<double>& tr) {
   CheckMethod(tau, false);
   const int K = K_, M = M_;
   Diag(tau);
-  std::vector<double> F((size_t)K * K, 0.), tr(K, 0.);
+  F.assign((size_t)K * K, 0.);
+  tr.assign(K, 0.);
   if (K == 1) {   // A^-1 = diag(1/D): B_rr = 1 / (tau D_r)
     std::vector<double> D(M);
     HIP_CHECK(hipMemcpyAsync(D.data(), d_D_.get(), sizeof(double) * M, hipMemcpyDeviceToHost, s_));
@@ -450,20 +471,6 @@ void GroupedRE::Fisher(const double* tau, double sigma2, double* FI) {
         tr[k] += diag[c];
         for (int j = 0; j < K; ++j) F[(size_t)j * K + k] += part[(size_t)c * K + j];
       }
-  }
-  const int P = 1 + K;
-  const double c4 = 0.5 / (sigma2 * sigma2);
-  double f00 = (double)n_ - M;
-  for (double v : F) f00 += v;
-  FI[0] = f00 * c4;
-  for (int j = 0; j < K; ++j) {
-    double rs = 0.;
-    for (int k = 0; k < K; ++k) rs += F[(size_t)j * K + k];
-    FI[j + 1] = FI[(size_t)(j + 1) * P] = (tr[j] - rs) / tau[j] * c4;
-    for (int k = j; k < K; ++k) {
-      const double v = (F[(size_t)j * K + k] + (j == k ? m_[j] - 2. * tr[j] : 0.)) / (tau[j] * tau[k]) * c4;
-      FI[(size_t)(j + 1) * P + k + 1] = FI[(size_t)(k + 1) * P + j + 1] = v;
-    }
   }
 }
 

@@ -85,6 +85,8 @@ class GroupedRE {
   //   2 sigma^4 FI_jk = (F_jk + delta_jk (m_j - 2 t_j)) / (tau_j tau_k).
   // Factors A at tau first. FI: (1 + K)^2 row-major.
   void Fisher(const double* tau, double sigma2, double* FI);
+  // the pieces of both forms: F (K x K, F_jk = ||B_jk||_F^2) and t_j = tr(B_jj)
+  void FisherParts(const double* tau, std::vector<double>& F, std::vector<double>& tr);
 
  private:
   struct Block {   // work space of a t-column PCG

@@ -224,9 +224,17 @@ EvalResult GroupedModel::EvalDense(const double* trafo, bool want_grad, int prof
 
 void GroupedModel::SetOptimSettings(const double* init_cov_pars, double lr, int max_iter, double delta_rel_conv,
                                     const char* optimizer, int m_lbfgs) {
-  if (optimizer != nullptr && optimizer[0] != '\0' && std::string(optimizer) != "lbfgs")
-    Fatal("Optimizer option '%s' is not supported for covariance parameters by gpboost_amd (supported: lbfgs)",
-          optimizer);
+  if (optimizer != nullptr && optimizer[0] != '\0') {
+    const std::string o(optimizer);
+    if (o != "lbfgs" && !is_internal_optimizer(o))
+      Fatal("Optimizer option '%s' is not supported for covariance parameters by gpboost_amd (supported: lbfgs, "
+            "gradient_descent, fisher_scoring)", optimizer);
+    isettings_.optimizer = o == "lbfgs" ? "" : o;
+    optimizer_name_ = o;
+  }
+  isettings_.lr = lr;
+  isettings_.max_iter = max_iter;
+  isettings_.delta = delta_rel_conv < 0. ? 1e-6 : delta_rel_conv;
   if (init_cov_pars != nullptr) {
     init_cov_pars_.assign(init_cov_pars, init_cov_pars + num_cov_pars());
     for (double v : init_cov_pars_)
@@ -308,7 +316,41 @@ class GroupedProfiledObjective : public LbfgsObjective {
   bool has_ = false;
 };
 
+class GroupedInternalAdapter : public InternalObjective {
+ public:
+  explicit GroupedInternalAdapter(GroupedModel* m) : m_(m) {}
+  double Nll(const std::vector<double>& t) override { return m_->EvalTrafo(t.data(), false, 0, false).nll; }
+  std::vector<double> Grad(const std::vector<double>& t, bool profile, double* sigma2) override {
+    EvalResult r = m_->EvalTrafo(t.data(), true, profile ? 1 : 0, false);
+    if (sigma2) *sigma2 = r.sigma2;
+    return r.grad;
+  }
+  std::vector<double> FisherTrafo(const std::vector<double>& t) override { return m_->FisherTrafo(t.data()); }
+
+ private:
+  GroupedModel* m_;
+};
+
 }  // namespace
+
+std::vector<double> GroupedModel::FisherTrafo(const double* trafo) {
+  // CalcFisherInformation_Only_Grouped_REs_Woodbury with transf_scale = true (re_model_template.h:9579-9586,
+  // 9638-9647): FI_00 = n / 2, FI_0j = tau_j tr(Z_j^T Psi^-1 Z_j) / 2 = (m_j - t_j) / 2,
+  // FI_jk = tau_j tau_k ||Z_j^T Psi^-1 Z_k||^2 / 2 = (F_jk + delta_jk (m_j - 2 t_j)) / 2 (grouped.h)
+  UseDevice();
+  const int K = re_->K(), P = 1 + K;
+  std::vector<double> F, tr;
+  re_->FisherParts(trafo + 1, F, tr);
+  std::vector<double> FI((size_t)P * P, 0.);
+  FI[0] = n_ / 2.;
+  for (int j = 0; j < K; ++j) {
+    const double mj = re_->levels_per_effect()[j];
+    FI[j + 1] = FI[(size_t)(j + 1) * P] = (mj - tr[j]) / 2.;
+    for (int k = 0; k < K; ++k)
+      FI[(size_t)(j + 1) * P + k + 1] = (F[(size_t)j * K + k] + (j == k ? mj - 2. * tr[j] : 0.)) / 2.;
+  }
+  return FI;
+}
 
 void GroupedModel::OptimCovPar(const double* y, const double* fixed_effects) {
   UseDevice();
@@ -326,6 +368,20 @@ void GroupedModel::OptimCovPar(const double* y, const double* fixed_effects) {
     num_it_ = 0;
     cov_pars_orig_ = start_orig;
     cov_pars_initialized_ = true;
+    last_cov_pars_ = cov_pars_orig_;
+    return;
+  }
+  if (!isettings_.optimizer.empty()) {   // "gradient_descent" / "fisher_scoring" (re_model_template.h:1287-1549)
+    if (isettings_.optimizer == "fisher_scoring" && (has_gp() || iterative()))
+      Fatal("optimizer_cov = 'fisher_scoring' is supported by gpboost_amd for grouped random effects with "
+            "matrix_inversion_method = 'cholesky' only (use 'lbfgs')");
+    GroupedInternalAdapter obj(this);
+    double fx = 0.;
+    num_it_ = internal_optimize(obj, trafo, isettings_, &fx);
+    cov_pars_orig_.assign(P, 0.);
+    ToOrig(trafo.data(), trafo[0], cov_pars_orig_.data());
+    cov_pars_initialized_ = true;
+    last_nll_ = fx;
     last_cov_pars_ = cov_pars_orig_;
     return;
   }

@@ -57,6 +57,18 @@ class GroupedModel {
   void SetOptimSettings(const double* init_cov_pars, double lr, int max_iter, double delta_rel_conv,
                         const char* optimizer, int m_lbfgs);
   void SetPreconditioner(const char* preconditioner);
+  void SetInternalOptimSettings(double acc_rate, bool nesterov, int schedule, int momentum_offset,
+                                const char* convergence_criterion) {
+    isettings_.acc_rate = acc_rate;
+    isettings_.nesterov = nesterov;
+    isettings_.schedule = schedule;
+    isettings_.momentum_offset = momentum_offset;
+    if (convergence_criterion != nullptr && convergence_criterion[0] != '\0')
+      isettings_.crit_params = check_convergence_criterion(convergence_criterion);
+  }
+  // Fisher information of the log transformed parameters (Fisher scoring; cholesky, no GP), row-major
+  std::vector<double> FisherTrafo(const double* trafo);
+  const std::string& optimizer_cov() const { return optimizer_name_; }
   // OptimCovPar (re_model.cpp:339-401 -> OptimExternal "lbfgs", optim_utils.h:561-706): L-BFGS on
   // log tau with sigma^2 profiled out (EvalLLforLBFGSpp, optim_utils.h:269-313).
   void OptimCovPar(const double* y, const double* fixed_effects);
@@ -117,6 +129,8 @@ class GroupedModel {
   bool y_set_ = false;
 
   LbfgsSettings optim_;
+  InternalSettings isettings_;
+  std::string optimizer_name_ = "lbfgs";
   std::vector<double> init_cov_pars_, cov_pars_orig_, init_used_, last_cov_pars_;
   bool cov_pars_initialized_ = false;
   int num_it_ = 0;

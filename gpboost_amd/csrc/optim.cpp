@@ -155,6 +155,140 @@ int lbfgs_minimize(LbfgsObjective& f, std::vector<double>& x, double& fx, const 
   }
 }
 
+bool is_internal_optimizer(const std::string& name) { return name == "gradient_descent" || name == "fisher_scoring"; }
+
+int internal_optimize(InternalObjective& f, std::vector<double>& pars, const InternalSettings& s, double* nll_out) {
+  const bool gd = s.optimizer == "gradient_descent";
+  if (!gd && s.optimizer != "fisher_scoring") Fatal("internal optimizer '%s' is not supported", s.optimizer.c_str());
+  const bool profile = gd;                  // profile_out_error_variance_ (re_model_template.h:946-948)
+  const bool nest = gd && s.nesterov;       // Nesterov acceleration for gradient descent only (:960-965)
+  if (nest && s.schedule != 0 && s.schedule != 1)
+    Fatal("NesterovSchedule: version = %d is not supported ", s.schedule);
+  if (nest && s.schedule == 1) Fatal("Armijo condition backtracking is not implemented when nesterov_schedule_version = 1 ");
+  const double kMaxLogUpdate = std::log(100.);   // MAX_GRADIENT_UPDATE_LOG_SCALE_ (:5287-5289)
+  const double kCArmijo = 1e-4, kCArmijoMom = 1e-4;   // C_ARMIJO_DEFAULT_, C_ARMIJO_MOM_DEFAULT_ (:5317-5319)
+  const int kMaxShrink = 30;                     // MAX_NUMBER_LR_SHRINKAGE_STEPS_DEFAULT_ (:5255)
+  const int P = (int)pars.size();
+  double lr_cov = s.lr < 0. ? (gd ? 0.1 : 1.) : s.lr;   // SetInitialValueLRCov (:7505-7521)
+  auto schedule = [&](int it, double acc) { return it < s.momentum_offset ? 0. : acc; };   // NesterovSchedule v0
+  double nll = f.Nll(pars);   // initial objective (:1233-1262)
+  if (!std::isfinite(nll))
+    Fatal("%s occurred in initial negative log-likelihood. Possible solutions: try other initial values ('init_cov_pars')",
+          std::isnan(nll) ? "NaN" : "Inf");
+  std::vector<double> after_grad = pars, after_grad_lag1 = pars;
+  int num_it = s.max_iter;
+  for (int it = 0; it < s.max_iter; ++it) {
+    const double nll_lag1 = nll;
+    const std::vector<double> pars_lag1 = pars;
+    std::vector<double> grad, step;
+    if (gd) {
+      double s2 = 0.;
+      grad = f.Grad(pars, true, &s2);   // ProfileOutSigma2 then CalcGradPars without the nugget (:1363-1372)
+      pars[0] = s2;
+      step = grad;
+      double mx = 0.;   // AvoidTooLargeLearningRatesCovAuxPars (:7539-7560, MaximalLearningRateCovAuxPars :4937-4945)
+      for (double v : step) mx = std::max(mx, std::fabs(v));
+      const double max_lr = kMaxLogUpdate / mx;
+      if (lr_cov > max_lr) lr_cov = max_lr;
+    } else {
+      grad = f.Grad(pars, false, nullptr);   // with the nugget (:1378-1384)
+      std::vector<double> F = f.FisherTrafo(pars);
+      // approx_Hessian.llt().solve(grad)
+      std::vector<double> L(F.size(), 0.);
+      for (int j = 0; j < P; ++j) {
+        double d = F[(size_t)j * P + j];
+        for (int k = 0; k < j; ++k) d -= L[(size_t)j * P + k] * L[(size_t)j * P + k];
+        if (!(d > 0.)) Fatal("the Fisher information is not positive definite in Fisher scoring");
+        L[(size_t)j * P + j] = std::sqrt(d);
+        for (int i = j + 1; i < P; ++i) {
+          double v = F[(size_t)i * P + j];
+          for (int k = 0; k < j; ++k) v -= L[(size_t)i * P + k] * L[(size_t)j * P + k];
+          L[(size_t)i * P + j] = v / L[(size_t)j * P + j];
+        }
+      }
+      step = grad;
+      for (int i = 0; i < P; ++i) {
+        for (int k = 0; k < i; ++k) step[i] -= L[(size_t)i * P + k] * step[k];
+        step[i] /= L[(size_t)i * P + i];
+      }
+      for (int i = P - 1; i >= 0; --i) {
+        for (int k = i + 1; k < P; ++k) step[i] -= L[(size_t)k * P + i] * step[k];
+        step[i] /= L[(size_t)i * P + i];
+      }
+    }
+    // CalcDirDerivArmijoAndLearningRateConstChangeCovAuxPars (armijo_condition_ = true)
+    const int ng = (int)step.size();
+    double dir_deriv = 0.;
+    for (int i = 0; i < ng; ++i) dir_deriv -= grad[i] * step[i];
+    double mom_dir_deriv = 0.;
+    if (nest) {
+      for (int i = 0; i < ng; ++i) {
+        const int p = profile ? i + 1 : i;
+        mom_dir_deriv += grad[i] * (std::log(pars[p]) - std::log(after_grad[p]));
+      }
+    }
+    // UpdateCovAuxPars: step on the log scale, momentum, Armijo backtracking
+    double lr = lr_cov, acc = s.acc_rate;
+    bool found = false, halving = false;
+    std::vector<double> np(P);
+    for (int ih = 0; ih < kMaxShrink; ++ih) {
+      std::vector<double> upd(ng);
+      for (int i = 0; i < ng; ++i) {
+        upd[i] = lr * step[i];
+        if (!gd) upd[i] = std::min(std::max(upd[i], -kMaxLogUpdate), kMaxLogUpdate);
+      }
+      if (profile) {
+        np[0] = pars[0];
+        for (int i = 0; i < ng; ++i) np[i + 1] = std::exp(std::log(pars[i + 1]) - upd[i]);
+      } else {
+        for (int i = 0; i < P; ++i) np[i] = std::exp(std::log(pars[i]) - upd[i]);
+      }
+      if (nest) {   // ApplyMomentumStep(exclude_first_log_scale = profile)
+        after_grad = np;
+        const double mu = schedule(it, acc);
+        for (int i = profile ? 1 : 0; i < P; ++i)
+          np[i] = std::exp((mu + 1.) * std::log(after_grad[i]) - mu * std::log(after_grad_lag1[i]));
+        if (profile) np[0] = after_grad[0];
+      }
+      nll = f.Nll(np);
+      const double mu = nest ? schedule(it, acc) : 0.;
+      if (nll <= nll_lag1 + kCArmijo * lr * dir_deriv + kCArmijoMom * mu * mom_dir_deriv) {
+        found = true;
+        break;
+      }
+      halving = true;
+      lr *= 0.5;    // LR_SHRINKAGE_FACTOR_
+      acc *= 0.5;
+    }
+    (void)found;
+    if (halving && gd) lr_cov = lr;   // permanently decreased for gradient descent (:7978-7979)
+    if (nest) after_grad_lag1 = after_grad;
+    pars = np;
+    bool bad = !std::isfinite(nll);
+    for (double v : pars) bad = bad || !std::isfinite(v);
+    if (bad)
+      Fatal("NaN or Inf occurred in covariance parameter optimization using '%s' (the reference's nelder_mead restart "
+            "is not supported by gpboost_amd)", s.optimizer.c_str());
+    bool conv;
+    if (s.crit_params) {
+      double dn = 0., ln = 0.;
+      for (int i = 0; i < P; ++i) {
+        dn += (pars[i] - pars_lag1[i]) * (pars[i] - pars_lag1[i]);
+        ln += pars_lag1[i] * pars_lag1[i];
+      }
+      conv = std::sqrt(dn) <= s.delta * std::sqrt(ln);
+    } else {
+      conv = (nll_lag1 - nll) <= s.delta * std::max(std::fabs(nll_lag1), 1.);
+    }
+    if (conv) {
+      num_it = it + 1;
+      break;
+    }
+  }
+  *nll_out = nll;
+  return num_it;
+}
+
 // ---------------------------------------------------------------------------------------------
 // REModelAMD: initial values and the optimization driver
 
@@ -287,9 +421,14 @@ void REModelAMD::SetOptimSettings(const double* init_cov_pars, double lr, int ma
   // re_model.cpp:264-279 and re_model_template.h:710-823
   if (optimizer != nullptr && optimizer[0] != '\0') {
     const std::string o(optimizer);
-    if (o != "lbfgs")
-      Fatal("Optimizer option '%s' is not supported for covariance parameters by gpboost_amd (supported: lbfgs)", o.c_str());
+    if (o != "lbfgs" && !is_internal_optimizer(o))
+      Fatal("Optimizer option '%s' is not supported for covariance parameters by gpboost_amd (supported: lbfgs, "
+            "gradient_descent, fisher_scoring)", o.c_str());
+    isettings_.optimizer = o == "lbfgs" ? "" : o;
   }
+  isettings_.lr = lr;
+  isettings_.max_iter = max_iter;
+  isettings_.delta = delta_rel_conv < 0. ? 1e-6 : delta_rel_conv;
   if (init_cov_pars != nullptr) {
     init_cov_pars_.assign(init_cov_pars, init_cov_pars + num_cov_pars());
     for (double v : init_cov_pars_)
@@ -406,7 +545,38 @@ class LatentObjective : public LbfgsObjective {
   bool has_grad_ = false, has_x_ = false;
 };
 
+// The reference's internal optimizers on the exact Gaussian likelihood (internal_optimize).
+class InternalAdapter : public InternalObjective {
+ public:
+  explicit InternalAdapter(REModelAMD* m) : m_(m) {}
+  double Nll(const std::vector<double>& t) override { return m_->EvalTrafo(t.data(), false, 0, false).nll; }
+  std::vector<double> Grad(const std::vector<double>& t, bool profile, double* sigma2) override {
+    EvalResult r = m_->EvalTrafo(t.data(), true, profile ? 1 : 0, false);
+    if (sigma2) *sigma2 = r.sigma2;
+    return r.grad;
+  }
+  std::vector<double> FisherTrafo(const std::vector<double>& t) override { return m_->FisherTrafo(t.data()); }
+
+ private:
+  REModelAMD* m_;
+};
+
 }  // namespace
+
+std::vector<double> REModelAMD::FisherTrafo(const double* trafo) {
+  // CalcFisherInformation(transf_scale = true, include_error_var = true), dense branch (re_model_template.h:
+  // 9203-9209, 9219-9227): FI_00 = n / 2, FI_0k = tr(Psi^-1 dPsi_k) / 2, FI_kl = tr(Psi^-1 dPsi_k Psi^-1 dPsi_l) / 2
+  // with dPsi / dlog v = v corr, dPsi / dlog phi = v dcorr / dlog phi
+  if (!dense_) Fatal("the transformed-scale Fisher information is available for gp_approx = 'none' only");
+  const double v = trafo[1], phi = trafo[2];
+  double sums[6], kms[2], t[6];
+  dense_->Eval(cfg_.cov_type, v, phi, d_y_.get(), true, sums, kms);   // tr(dPsi_k Psi^-1) = sums[4], sums[5]
+  dense_->Fisher(cfg_.cov_type, v, phi, v, t);
+  const double n = cfg_.n;
+  return {n / 2., sums[4] / 2., sums[5] / 2.,
+          sums[4] / 2., 0.5 * v * v * t[3], 0.5 * v * t[4],
+          sums[5] / 2., 0.5 * v * t[4], 0.5 * t[5]};
+}
 
 void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects, bool called_in_boosting, bool reuse_lr) {
   // REModel::OptimCovPar (re_model.cpp:339-401) -> OptimLinRegrCoefCovPar without covariates
@@ -472,7 +642,17 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects, bool 
   if (!reuse_m_bfgs) m_bfgs_ = InverseHessian();   // a fresh solver state (LBFGS.h:42-48)
   std::vector<double> x;
   double fx = 0.;
-  if (!cfg_.latent) {
+  if (!isettings_.optimizer.empty()) {   // "gradient_descent" / "fisher_scoring" (re_model_template.h:1287-1549)
+    if (cfg_.latent)
+      Fatal("optimizer_cov = '%s' is supported by gpboost_amd for the Gaussian likelihood only (use 'lbfgs')",
+            isettings_.optimizer.c_str());
+    if (isettings_.optimizer == "fisher_scoring" && !dense_)
+      Fatal("optimizer_cov = 'fisher_scoring' is supported by gpboost_amd for gp_approx = 'none' only (use 'lbfgs')");
+    std::vector<double> tv(trafo, trafo + 3);
+    InternalAdapter obj(this);
+    num_it_ = internal_optimize(obj, tv, isettings_, &fx);
+    cov_pars_orig_ = {tv[0], tv[1] * tv[0], range_back(cfg_.cov_type, tv[2])};
+  } else if (!cfg_.latent) {
     x = {std::log(trafo[1]), std::log(trafo[2])};
     GaussianProfiledObjective obj(this);
     num_it_ = lbfgs_minimize(obj, x, fx, optim_, &m_bfgs_, reuse_m_bfgs);
@@ -503,6 +683,9 @@ void REModelAMD::InitializeOptimizerNames() {
 }
 
 void REModelAMD::OptimLinRegrCoefCovPar(const double* y, const double* X, int p, const double* fixed_effects) {
+  if (!isettings_.optimizer.empty())
+    Fatal("optimizer_cov = '%s' with linear regression covariates is not supported by gpboost_amd (use 'lbfgs')",
+          isettings_.optimizer.c_str());
   // REModel::OptimLinRegrCoefCovPar (re_model.cpp:403-469) -> REModelTemplate::OptimLinRegrCoefCovPar
   // with covariates (re_model_template.h:846-1700): Gaussian likelihood, optimizer_cov "lbfgs",
   // optimizer_coef "wls" (its default, :7467-7470): OptimExternal with profile_out_coef = true

@@ -10,6 +10,7 @@
 // gradient comes from the device evaluation of REModelAMD.
 #pragma once
 
+#include <string>
 #include <vector>
 
 namespace gpb_amd {
@@ -65,5 +66,42 @@ class InverseHessian {
 // given / reuse: the m_bfgs kept across calls (reuse_m_bfgs_from_previous_call, LBFGS.h:86-171).
 int lbfgs_minimize(LbfgsObjective& f, std::vector<double>& x, double& fx, const LbfgsSettings& s,
                    InverseHessian* given = nullptr, bool reuse = false);
+
+// ---- the reference's internal optimizers for covariance parameters (Gaussian likelihood, no covariates):
+// "gradient_descent" (with Nesterov acceleration by default) and "fisher_scoring" (OptimLinRegrCoefCovPar's
+// loop re_model_template.h:1290-1549 with AvoidTooLargeLearningRatesCovAuxPars :7539-7560,
+// CalcDirDerivArmijoAndLearningRateConstChangeCovAuxPars :7587-7634, UpdateCovAuxPars :7850-8000,
+// ApplyMomentumStep :4600-4623, NesterovSchedule :5643-5662, CheckOptimizerHasConverged :1708-1729; settings
+// SetOptimConfig :710-755, SetInitialValueLRCov :7505-7521, constants :5255-5345).
+struct InternalSettings {
+  std::string optimizer;           // "gradient_descent" | "fisher_scoring"
+  double lr = -1.;                 // lr_cov (< 0: 0.1 for gradient descent, 1 for Fisher scoring)
+  double acc_rate = 0.5;           // acc_rate_cov
+  bool nesterov = true;            // use_nesterov_acc (gradient descent only)
+  int schedule = 0;                // nesterov_schedule_version
+  int momentum_offset = 2;
+  int max_iter = 1000;
+  double delta = 1e-6;             // delta_rel_conv
+  bool crit_params = false;        // convergence_criterion = "relative_change_in_parameters"
+};
+
+// The objective on the transformed scale (trafo[0] = sigma^2, then the log-scale parameters' values).
+class InternalObjective {
+ public:
+  virtual ~InternalObjective() = default;
+  // negative log-likelihood at trafo (sigma^2 = trafo[0] as given); NaN allowed (non-fatal)
+  virtual double Nll(const std::vector<double>& trafo) = 0;
+  // gradient wrt the log of the transformed parameters: profile -> sigma^2 = q / n (returned) and no nugget
+  // entry (include_error_var = false), else the nugget first
+  virtual std::vector<double> Grad(const std::vector<double>& trafo, bool profile, double* sigma2) = 0;
+  // Fisher information of the log transformed parameters incl. the nugget (CalcFisherInformation with
+  // transf_scale = true, include_error_var = true), row-major
+  virtual std::vector<double> FisherTrafo(const std::vector<double>& trafo) = 0;
+};
+
+// Runs the optimizer from trafo (overwritten with the estimate; trafo[0] the final sigma^2); returns the
+// number of iterations (the reference's num_it) and the final objective value in *nll.
+int internal_optimize(InternalObjective& f, std::vector<double>& trafo, const InternalSettings& s, double* nll);
+bool is_internal_optimizer(const std::string& name);
 
 }  // namespace gpb_amd

@@ -41,6 +41,13 @@ int parse_cov(const std::string& name, double shape) {
   Fatal("cov_fct '%s' is not supported by gpboost_amd (supported: exponential, matern, gaussian)", name.c_str());
 }
 
+bool check_convergence_criterion(const std::string& name) {
+  if (name == "relative_change_in_parameters") return true;
+  if (name == "relative_change_in_log_likelihood") return false;
+  Fatal("Convergence criterion '%s' is not supported.", name.c_str());
+  return false;
+}
+
 double range_trafo(int cov_type, double rho) {
   switch (cov_type) {
     case kMatern05: return 1. / rho;

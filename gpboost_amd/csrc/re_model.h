@@ -58,6 +58,9 @@ int parse_cov(const std::string& name, double shape);
 // generator) when n > 1000
 double init_range_trafo(const std::vector<double>& X, int d, int cov_type, std::mt19937& rng);
 double range_trafo(int cov_type, double rho);
+// SUPPORTED_CONV_CRIT_ (re_model_template.h:756-760): true for "relative_change_in_parameters", false for
+// "relative_change_in_log_likelihood"; anything else fails
+bool check_convergence_criterion(const std::string& name);
 // cov_fcts.h TransformBackCovPars: range transform phi -> range rho
 double range_back(int cov_type, double phi);
 
@@ -193,6 +196,19 @@ class REModelAMD {
   // roots of the diagonal of the inverse Fisher information (CalcStdDevCovPar,
   // re_model_template.h:9775-9789; dense, Vecchia and FITC Gaussian models).
   void StdDevCovPars(const double* cov_pars_orig, double* sd);
+  // Fisher information of the log transformed parameters (Fisher scoring; dense models), 3 x 3 row-major
+  std::vector<double> FisherTrafo(const double* trafo);
+  // acc_rate_cov, use_nesterov_acc, nesterov_schedule_version, momentum_offset, convergence_criterion of
+  // GPB_SetOptimConfig (re_model_template.h:710-761) for the internal optimizers
+  void SetInternalOptimSettings(double acc_rate, bool nesterov, int schedule, int momentum_offset,
+                                const char* convergence_criterion) {
+    isettings_.acc_rate = acc_rate;
+    isettings_.nesterov = nesterov;
+    isettings_.schedule = schedule;
+    isettings_.momentum_offset = momentum_offset;
+    if (convergence_criterion != nullptr && convergence_criterion[0] != '\0')
+      isettings_.crit_params = check_convergence_criterion(convergence_criterion);
+  }
   int num_it() const { return num_it_; }
   // GPB_GetInitCovPar (re_model.cpp:813-834): initial values on the original scale, or -1 each
   // when none were given or determined yet
@@ -336,6 +352,7 @@ class REModelAMD {
   DevBuf<double> d_Bf_, d_Df_, d_gram_part_, d_gram_out_;
   DevBuf<int> d_tptr_, d_trow_, d_tslot_;
   std::string optimizer_cov_, optimizer_coef_;
+  InternalSettings isettings_;   // "gradient_descent" / "fisher_scoring" (optimizer empty: lbfgs)
   std::string cg_preconditioner_type_;
   std::vector<double> init_aux_pars_;   // given by GPB_SetOptimConfig (original scale)
 

@@ -212,10 +212,16 @@ int main(int argc, char** argv) {
     // Python package's default optimizer settings (basic.py:4510-4533: lr_cov = -1,
     // delta_rel_conv = -1, maxit = 1000, m_lbfgs = -1 -> C++ defaults; optimizer "lbfgs").
     const int no_index[1] = {-1};
-    m->SetOptimConfig(std::atof(get(args, "lr_cov", "-1").c_str()), 0.5,
+    // optimizer / use_nesterov_acc / acc_rate_cov / momentum_offset / convergence_criterion: the internal
+    // optimizers' settings (GPB_SetOptimConfig's arguments), defaults as the Python package's
+    const std::string optimizer = get(args, "optimizer", "lbfgs");
+    const std::string crit = get(args, "convergence_criterion", "relative_change_in_log_likelihood");
+    m->SetOptimConfig(std::atof(get(args, "lr_cov", "-1").c_str()),
+                      std::atof(get(args, "acc_rate_cov", "0.5").c_str()),
                       std::atoi(get(args, "maxit", "1000").c_str()),
-                      std::atof(get(args, "delta_rel_conv", "-1").c_str()), true, 0, "lbfgs", 2,
-                      "relative_change_in_log_likelihood", 0.1, 0.5, "",
+                      std::atof(get(args, "delta_rel_conv", "-1").c_str()),
+                      std::atoi(get(args, "use_nesterov_acc", "1").c_str()) != 0, 0, optimizer.c_str(),
+                      std::atoi(get(args, "momentum_offset", "2").c_str()), crit.c_str(), 0.1, 0.5, "",
                       std::atoi(get(args, "cg_max_num_it", "1000").c_str()),
                       std::atoi(get(args, "cg_max_num_it", "1000").c_str()),
                       std::atof(get(args, "cg_delta_conv", "1e-2").c_str()),

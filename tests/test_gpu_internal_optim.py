@@ -1,0 +1,136 @@
+"""GPU parity for the reference's internal covariance-parameter optimizers: "gradient_descent" (with and
+without Nesterov acceleration) and "fisher_scoring" (Gaussian likelihood, no covariates).
+
+Reference: REModelTemplate::OptimLinRegrCoefCovPar (re_model_template.h:1290-1549) with
+AvoidTooLargeLearningRatesCovAuxPars (:7539-7560), the Armijo backtracking of UpdateCovAuxPars
+(:7850-8000), ApplyMomentumStep (:4600-4623) and CheckOptimizerHasConverged (:1708-1729); Fisher
+information CalcFisherInformation (dense :9450-9557, grouped :9559-9651) on the transformed scale.
+Fixtures: tests/golden/golden_internal_optim.json (make_golden_internal_optim.py, the reference itself)
+and the values hard-coded in R-package/tests/testthat/test_GPModel_gaussian_process.R:117-170.
+
+The device objective, gradient and Fisher information match the reference's to ~1e-12 relative and
+the optimizers follow its trajectory step for step, so iteration counts must be identical and the
+estimates agree to 1e-6 relative.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from gpboost_amd import GPModel, GPBoostError, synthetic
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with open(os.path.join(HERE, "golden", "golden_internal_optim.json")) as f:
+        return json.load(f)
+
+
+def _params(sp):
+    p = {"optimizer_cov": sp["optimizer"]}
+    if "lr_cov" in sp:
+        p["lr_cov"] = float(sp["lr_cov"])
+    if "delta_rel_conv" in sp:
+        p["delta_rel_conv"] = float(sp["delta_rel_conv"])
+    if "use_nesterov_acc" in sp:
+        p["use_nesterov_acc"] = sp["use_nesterov_acc"] != "0"
+    if "convergence_criterion" in sp:
+        p["convergence_criterion"] = sp["convergence_criterion"]
+    if "init_cov_pars" in sp:
+        p["init_cov_pars"] = np.array([float(v) for v in sp["init_cov_pars"].split(",")])
+    return p
+
+
+def _model_and_y(case):
+    sp = case["spec"]
+    if case["data"] == "grouped":
+        g = synthetic.bench_groups(case["n"], tuple(case["levels"]))
+        return GPModel(group_data=g, matrix_inversion_method=sp["matrix_inversion_method"]), \
+            synthetic.bench_grouped_y(g)
+    if case["data"] == "rtest_combined":
+        X, g, y = synthetic.rtest_combined_y(100)
+        return GPModel(gp_coords=X, group_data=g, cov_function=sp["cov_fct"]), y
+    if case["data"] == "rtest_gaussian":
+        X, y = synthetic.rtest_gaussian_y(100)
+    else:
+        X = synthetic.bench_coords(case["n"])
+        y = synthetic.bench_gaussian_y(case["n"])
+    kw = dict(gp_coords=X, cov_function=sp["cov_fct"], cov_fct_shape=float(sp.get("shape", 0.5)),
+              gp_approx=sp["gp_approx"], seed=0)
+    if sp["gp_approx"] != "none":
+        kw.update(num_neighbors=sp["num_neighbors"], vecchia_ordering=sp["ordering"])
+    return GPModel(**kw), y
+
+
+NAMES = ["rtest_gd_nesterov", "rtest_gd_no_acc", "rtest_gd_lr1", "rtest_gd_crit_pars", "rtest_fisher",
+         "rtest_gd_default", "rtest_fisher_default", "synth2000_dense_gd", "synth2000_dense_fisher_matern15",
+         "synth2000_vecchia_gd", "grouped_k1_gd", "grouped_k1_fisher", "grouped_k2_gd", "grouped_k2_fisher",
+         "grouped_k2_gd_no_acc_crit_pars", "combined_rtest_gd"]
+
+
+@pytest.mark.parametrize("name", NAMES)
+def test_internal_optimizer_matches_reference(golden, name):
+    case = golden[name]
+    gm, y = _model_and_y(case)
+    gm.fit(y, params=_params(case["spec"]))
+    assert gm.get_num_optim_iter() == case["num_it"], (gm.get_num_optim_iter(), case["num_it"])
+    np.testing.assert_allclose(gm.get_init_cov_pars(), case["init_cov_pars"], rtol=1e-12)
+    np.testing.assert_allclose(gm.get_cov_pars(), case["cov_pars"], rtol=1e-6)
+    assert abs(gm.get_current_neg_log_likelihood() - case["nll"]) <= 1e-9 * abs(case["nll"])
+
+
+# test_GPModel_gaussian_process.R:117-170: estimates with standard errors (column-major as R's
+# as.vector of the 2 x 3 matrix), iteration counts, TOLERANCE_STRICT = 1e-5 (5e-6 for no acc)
+R_CASES = {
+    "rtest_gd_nesterov": ([0.03784221, 0.07943467, 1.07390943, 0.25351519, 0.11451432, 0.03840236], 59, 1e-5),
+    "rtest_gd_no_acc": ([0.04040441, 0.08036674, 1.06926607, 0.25360131, 0.11502362, 0.03877014], 97, 5e-6),
+    "rtest_gd_lr1": ([0.03738147, 0.07929704, 1.07520000, 0.25359186, 0.11441031, 0.03833048], 49, 1e-5),
+    "rtest_gd_crit_pars": ([0.03276547, 0.07715343, 1.07617676, 0.25177603, 0.11352557, 0.03770062], 382, 1e-5),
+    "rtest_fisher": ([0.03294841, 0.07722844, 1.07591929, 0.25179816, 0.11355958, 0.03772550], 8, 1e-5),
+}
+
+
+@pytest.mark.parametrize("name", list(R_CASES))
+def test_internal_optimizer_r_test_values(golden, name):
+    vals, num_it, tol = R_CASES[name]
+    gm, y = _model_and_y(golden[name])
+    gm.fit(y, params=_params(golden[name]["spec"]))
+    out = gm.get_cov_pars(std_err=True)
+    assert out.shape == (2, 3)
+    assert np.sum(np.abs(out.T.reshape(-1) - vals)) < tol
+    assert gm.get_num_optim_iter() == num_it
+    if name == "rtest_gd_nesterov":
+        assert abs(gm.get_current_neg_log_likelihood() - 122.7771373) < 1e-5
+    if name == "rtest_fisher":
+        assert abs(gm.get_current_neg_log_likelihood() - 122.7771373) < 1e-2
+
+
+def test_internal_optimizer_defaults_and_refusals():
+    X, y = synthetic.rtest_gaussian_y(100)
+    # default delta_rel_conv for gradient descent is 1e-6 (SetInitialValueDeltaRelConv :7524-7533)
+    a = GPModel(gp_coords=X, cov_function="exponential")
+    a.fit(y, params={"optimizer_cov": "gradient_descent"})
+    b = GPModel(gp_coords=X, cov_function="exponential")
+    b.fit(y, params={"optimizer_cov": "gradient_descent", "delta_rel_conv": 1e-6})
+    c = GPModel(gp_coords=X, cov_function="exponential")
+    c.fit(y, params={"optimizer_cov": "gradient_descent", "delta_rel_conv": 1e-8})
+    np.testing.assert_array_equal(a.get_cov_pars(), b.get_cov_pars())
+    assert not np.array_equal(a.get_cov_pars(), c.get_cov_pars())
+    assert a.get_optim_params()["optimizer_cov"] == "gradient_descent"
+    with pytest.raises(GPBoostError, match="not supported"):
+        GPModel(gp_coords=X, cov_function="exponential").fit(y, params={"optimizer_cov": "adam"})
+    with pytest.raises(GPBoostError, match="not supported"):
+        GPModel(gp_coords=X, cov_function="exponential").fit(
+            y, params={"optimizer_cov": "gradient_descent", "convergence_criterion": "abc"})
+    with pytest.raises(GPBoostError, match="covariates"):
+        GPModel(gp_coords=X, cov_function="exponential").fit(
+            y, X=np.ones((100, 1)), params={"optimizer_cov": "gradient_descent"})
+    Xb = synthetic.bench_coords(300)
+    gv = GPModel(gp_coords=Xb, cov_function="exponential", gp_approx="vecchia", num_neighbors=10)
+    with pytest.raises(GPBoostError, match="fisher_scoring"):
+        gv.fit(synthetic.bench_gaussian_y(300), params={"optimizer_cov": "fisher_scoring"})
