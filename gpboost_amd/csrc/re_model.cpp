@@ -79,8 +79,10 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
     vecchia_ = true;
     cfg_.latent = cfg_.lik != kLikGaussian;
   } else if (cfg_.gp_approx == "none") {
-    if (cfg_.lik != kLikGaussian)
-      Fatal("likelihood '%s' requires gp_approx = 'vecchia' in gpboost_amd (dense Laplace is out of scope)", cfg_.likelihood.c_str());
+    cfg_.latent = cfg_.lik != kLikGaussian;   // Laplace approximation (DenseLaplace)
+    if (cfg_.latent && cfg_.matrix_inversion_method == "iterative")   // CanUseIterative, re_model_template.h:6712-6717
+      Fatal("matrix_inversion_method = 'iterative' is not supported for gp_approx = 'none' with likelihood '%s'. Use 'cholesky' ",
+            cfg_.likelihood.c_str());
   } else if (cfg_.gp_approx == "fitc") {
     cfg_.latent = cfg_.lik != kLikGaussian;   // Laplace approximation (FitcLaplace)
     if (cfg_.matrix_inversion_method == "iterative")   // re_model_template.h:8774-8776
@@ -224,6 +226,17 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
         perm_.resize(n);   // no reordering: the model order is the data order
         std::iota(perm_.begin(), perm_.end(), 0);
       }
+    } else if (cfg_.latent) {
+      // FindModePostRandEffCalcMLLStable / CalcGradNegMargLikelihoodLaplaceApproxStable on the distinct locations;
+      // repeated coordinates (the reference's incidence-matrix form) are not supported here
+      std::vector<int> uniq, idx;
+      unique_locations(coords_.data(), n, d, uniq, idx);
+      if ((int)uniq.size() < n)
+        Fatal("gp_approx = 'none' with likelihood '%s' and duplicate coordinates is not supported by gpboost_amd",
+              cfg_.likelihood.c_str());
+      dense_lap_.reset(new DenseLaplace(n, d, d_X_.get(), stream_));
+      perm_.resize(n);   // no reordering: the model order is the data order
+      std::iota(perm_.begin(), perm_.end(), 0);
     } else {
       dense_.reset(new DenseSolver(n, d, d_X_.get(), stream_));
     }
@@ -268,6 +281,7 @@ REModelAMD::~REModelAMD() {
   (void)hipSetDevice(device_);
   if (stream_) (void)hipStreamSynchronize(stream_);
   dense_.reset();
+  dense_lap_.reset();
   vfisher_.reset();
   vif_.reset();
   fitc_lap_.reset();
@@ -417,6 +431,10 @@ void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred,
   if (vif_) Fatal("predictions with gp_approx = 'full_scale_vecchia' are not supported by gpboost_amd");
   if (fitc_) {
     PredictFitc(y, n_pred, coords_pred, cov_pars, predict_cov_mat, predict_var, predict_response, out, mean_add);
+    return;
+  }
+  if (dense_lap_) {
+    PredictDenseLaplace(y, n_pred, coords_pred, cov_pars, predict_cov_mat, predict_var, predict_response, out, mean_add);
     return;
   }
   if (!vecchia_) {
@@ -780,6 +798,42 @@ void REModelAMD::PredictFitcLaplace(const double* y, int n_pred, const double* c
   std::vector<double> mean(n_pred), var(want_var ? n_pred : 0), cov(predict_cov_mat ? (size_t)n_pred * n_pred : 0);
   fitc_lap_->Predict(cfg_.cov_type, cp[0], range_trafo(cfg_.cov_type, cp[1]), xp.data(), n_pred, match, want_var,
                      predict_cov_mat, mean.data(), var.data(), cov.data());
+  if (mean_add != nullptr)
+    for (int p = 0; p < n_pred; ++p) mean[p] += mean_add[p];
+  if (predict_response) ResponseTransform(n_pred, mean.data(), var.data(), nullptr);
+  std::copy(mean.begin(), mean.end(), out);
+  if (predict_cov_mat) std::copy(cov.begin(), cov.end(), out + n_pred);
+  else if (predict_var) std::copy(var.begin(), var.end(), out + n_pred);
+}
+
+// gp_approx = "none" with a Laplace likelihood (CalcPred, re_model_template.h:10026- -> PredictLaplaceApproxStable,
+// likelihoods.h:5610-5676): the mode at the parameters (found from zero), latent means Sigma_po d1 and
+// (co)variances from the factor of I + W^1/2 Sigma W^1/2, the prediction points' fixed effects added to the mean,
+// the response transform for predict_response.
+void REModelAMD::PredictDenseLaplace(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,
+                                     bool predict_cov_mat, bool predict_var, bool predict_response, double* out,
+                                     const double* mean_add) {
+  if (n_pred <= 0) Fatal("num_data_pred must be > 0");
+  if (coords_pred == nullptr) Fatal("gp_coords_data_pred must be provided");
+  UseDevice();
+  if (y != nullptr) SetY(y);
+  if (!y_set_) Fatal("response variable y has not been set (pass y or evaluate the likelihood first)");
+  double cp[2];
+  if (cov_pars != nullptr) std::copy(cov_pars, cov_pars + 2, cp);
+  else if ((int)last_cov_pars_.size() == 2) std::copy(last_cov_pars_.begin(), last_cov_pars_.end(), cp);
+  else Fatal("cov_pars must be provided (no previous evaluation)");
+  if (predict_cov_mat && predict_response)
+    Fatal("predictive covariance matrices of the response are not supported for likelihood '%s' by gpboost_amd "
+          "(use predict_response = false or predict_var)", cfg_.likelihood.c_str());
+  EvalLatent(cp, false);   // the mode at these parameters (SetYCalcCovCalcYAuxForPred, re_model_template.h:3306-3312)
+  const int d = cfg_.d;
+  std::vector<double> xp((size_t)n_pred * d);
+  for (int p = 0; p < n_pred; ++p)
+    for (int q = 0; q < d; ++q) xp[(size_t)p * d + q] = coords_pred[(size_t)q * n_pred + p];
+  const bool want_var = predict_var || predict_response;
+  std::vector<double> mean(n_pred), var(want_var ? n_pred : 0), cov(predict_cov_mat ? (size_t)n_pred * n_pred : 0);
+  dense_lap_->Predict(cfg_.cov_type, cp[0], range_trafo(cfg_.cov_type, cp[1]), xp.data(), n_pred, want_var,
+                      predict_cov_mat, mean.data(), var.data(), cov.data());
   if (mean_add != nullptr)
     for (int p = 0; p < n_pred; ++p) mean[p] += mean_add[p];
   if (predict_response) ResponseTransform(n_pred, mean.data(), var.data(), nullptr);

@@ -20,6 +20,7 @@
 #include "common.h"
 #include "dense.h"
 #include "fitc.h"
+#include "dense_laplace.h"
 #include "fitc_laplace.h"
 #include "vif.h"
 #include "vecchia_fisher.h"
@@ -249,6 +250,9 @@ class REModelAMD {
                         const double* mean_add);
   void PredictDense(const double* y, int n_pred, const double* coords_pred, const double* cov_pars, bool predict_cov_mat,
                     bool predict_var, bool predict_response, double* out, const double* mean_add);
+  void PredictDenseLaplace(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,
+                           bool predict_cov_mat, bool predict_var, bool predict_response, double* out,
+                           const double* mean_add);
   void PredictFitc(const double* y, int n_pred, const double* coords_pred, const double* cov_pars, bool predict_cov_mat,
                    bool predict_var, bool predict_response, double* out, const double* mean_add);
   std::vector<int> FitcMatch(const std::vector<double>& xp_rowmajor, int n_pred) const;
@@ -300,6 +304,7 @@ class REModelAMD {
   std::unique_ptr<DenseSolver> dense_;
   std::unique_ptr<FitcSolver> fitc_;   // gp_approx = "fitc"
   std::unique_ptr<FitcLaplace> fitc_lap_;   // gp_approx = "fitc", non-Gaussian likelihood (Laplace)
+  std::unique_ptr<DenseLaplace> dense_lap_; // gp_approx = "none", non-Gaussian likelihood (Laplace)
   std::unique_ptr<VifSolver> vif_;          // gp_approx = "full_scale_vecchia" (Gaussian likelihood)
   std::unique_ptr<VecchiaFisher> vfisher_;  // gp_approx = "vecchia", Gaussian: standard deviations (lazy)
   std::mt19937 fitc_rng_;              // the model's generator after the inducing-point selection
@@ -308,7 +313,9 @@ class REModelAMD {
   std::unique_ptr<LatentVecchia> latent_;
   // the latent solver of a Laplace model: the Vecchia (iterative) or the FITC (Cholesky) one
   LatentSolverBase* lat() const {
-    return latent_ ? static_cast<LatentSolverBase*>(latent_.get()) : static_cast<LatentSolverBase*>(fitc_lap_.get());
+    if (latent_) return latent_.get();
+    if (dense_lap_) return dense_lap_.get();
+    return fitc_lap_.get();
   }
   std::vector<double> y_vo_;          // host copy (Vecchia order) for the latent solver
   std::vector<double> aux_pars_;

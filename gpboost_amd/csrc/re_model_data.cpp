@@ -10,6 +10,7 @@
 #include "covariates.h"
 #include "kernels.h"
 #include "re_model.h"
+#include "vecchia_host.h"
 
 namespace gpb_amd {
 
@@ -335,11 +336,28 @@ void REModelAMD::SetLikelihood(const std::string& likelihood) {
   ModelConfig c = cfg_;
   c.likelihood = likelihood;
   const int lik = parse_likelihood(likelihood);
-  const bool latent = c.gp_approx == "vecchia_latent" || ((vecchia_ || fitc_) && lik != kLikGaussian);
-  if (!vecchia_ && !fitc_ && lik != kLikGaussian)
-    Fatal("likelihood '%s' requires gp_approx = 'vecchia' or 'fitc' in gpboost_amd (dense Laplace is out of scope)",
-          likelihood.c_str());
-  if (fitc_) {   // FITC: the Laplace solver on the same inducing points (Cholesky either way)
+  const bool dense = c.gp_approx == "none";
+  const bool latent = c.gp_approx == "vecchia_latent" || ((vecchia_ || fitc_ || dense) && lik != kLikGaussian);
+  if (vif_ && lik != kLikGaussian)
+    Fatal("gp_approx = 'full_scale_vecchia' with likelihood '%s' (Laplace approximation) is not supported by "
+          "gpboost_amd (supported: gaussian)", likelihood.c_str());
+  if (dense) {   // gp_approx = "none": DenseLaplace (Cholesky) for the Laplace likelihoods, DenseSolver for gaussian
+    if (latent && !dense_lap_) {
+      std::vector<int> uniq, idx;
+      unique_locations(coords_.data(), cfg_.n, cfg_.d, uniq, idx);
+      if ((int)uniq.size() < cfg_.n)
+        Fatal("gp_approx = 'none' with likelihood '%s' and duplicate coordinates is not supported by gpboost_amd",
+              likelihood.c_str());
+      dense_.reset();
+      dense_lap_.reset(new DenseLaplace(cfg_.n, cfg_.d, d_X_.get(), stream_));
+      perm_.resize(cfg_.n);
+      std::iota(perm_.begin(), perm_.end(), 0);
+    } else if (!latent) {
+      dense_lap_.reset();
+      if (!dense_) dense_.reset(new DenseSolver(cfg_.n, cfg_.d, d_X_.get(), stream_));
+    }
+    c.matrix_inversion_method = "cholesky";
+  } else if (fitc_) {   // FITC: the Laplace solver on the same inducing points (Cholesky either way)
     if (latent && !fitc_lap_) {
       fitc_lap_.reset(new FitcLaplace(fitc_.get(), stream_));
       perm_.resize(cfg_.n);

@@ -1,0 +1,114 @@
+"""GPU parity for the Laplace approximation without a GP approximation (gp_approx = "none", the reference's
+default for non-Gaussian likelihoods), through the C ABI: DenseLaplace (csrc/dense_laplace.h) against
+FindModePostRandEffCalcMLLStable, CalcGradNegMargLikelihoodLaplaceApproxStable and
+PredictLaplaceApproxStable (likelihoods.h:1843-1960, 3261-3413, 5610-5676).
+
+Fixtures: tests/golden/golden_dense_laplace.json (the reference itself, make_golden_dense_laplace.py) for
+bernoulli_logit / bernoulli_probit / poisson and four covariance functions, plus the R tests' hard-coded
+values on their own data (test_GPModel_non_Gaussian_data.R:1196 probit 67.18342059, :2410 poisson
+195.03708036, tolerance 1e-5 there). Both sides are exact dense algebra, so the nll must agree to 1e-9
+relative, gradients to 1e-7, fits with the reference's iteration count to 1e-6, predictions to 1e-8.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from conftest import lik_case_data
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+with open(os.path.join(HERE, "golden", "golden_dense_laplace.json")) as _f:
+    GOLDEN = json.load(_f)
+
+
+def _of(kind):
+    return [k for k in GOLDEN if GOLDEN[k]["kind"] == kind]
+
+
+def _model(X, case):
+    from gpboost_amd import GPModel
+    sp = case["spec"]
+    return GPModel(gp_coords=X, cov_function=sp["cov_fct"], cov_fct_shape=float(sp["shape"]), likelihood=sp["likelihood"])
+
+
+@pytest.mark.parametrize("name", _of("eval"))
+def test_dense_laplace_nll_grad_match_reference(name):
+    case = GOLDEN[name]
+    X, y = lik_case_data(case)
+    gm = _model(X, case)
+    nll = gm.neg_log_likelihood(case["cov_pars"], y)
+    assert abs(nll - case["nll"]) <= 1e-9 * abs(case["nll"]), (nll, case["nll"])
+    nll2, g, _ = gm.neg_log_likelihood_and_grad(case["cov_pars"], y)
+    assert abs(nll2 - case["nll"]) <= 1e-9 * abs(case["nll"])
+    ref = np.asarray(case["grad"])
+    np.testing.assert_allclose(g, ref, rtol=1e-7, atol=1e-9 * abs(case["nll"]))
+    if "r_expected_nll" in case:   # the R test's own value (TOLERANCE_STRICT = 1e-5)
+        assert abs(nll - case["r_expected_nll"]) < 1e-5
+
+
+@pytest.mark.parametrize("name", _of("fit"))
+def test_dense_laplace_fit_matches_reference(name):
+    case = GOLDEN[name]
+    X, y = lik_case_data(case)
+    gm = _model(X, case)
+    gm.fit(y)
+    np.testing.assert_allclose(gm.get_init_cov_pars(), case["init_cov_pars"], rtol=1e-12)
+    assert gm.get_num_optim_iter() == case["num_it"]
+    np.testing.assert_allclose(gm.get_cov_pars(), case["cov_pars"], rtol=1e-6)
+    assert abs(gm.get_current_neg_log_likelihood() - case["nll"]) <= 1e-9 * abs(case["nll"])
+
+
+@pytest.mark.parametrize("name", _of("gradf"))
+def test_dense_laplace_gradient_wrt_fixed_effects(name):
+    case = GOLDEN[name]
+    X, y = lik_case_data(case)
+    fe = 0.3 * np.sin(3.0 * X[:, 0]) - 0.2
+    gm = _model(X, case)
+    nll, g, _ = gm.neg_log_likelihood_and_grad(case["cov_pars"], y, fixed_effects=fe)
+    assert abs(nll - case["nll"]) <= 1e-9 * abs(case["nll"])
+    np.testing.assert_allclose(g, case["grad"], rtol=1e-7)
+    gm.set_optim_params({"init_cov_pars": np.array(case["cov_pars"])})
+    gf = gm.calc_gradient_f(fixed_effects=fe)
+    ref = np.asarray(case["grad_f"])
+    assert np.max(np.abs(gf - ref)) <= 1e-8 * max(1.0, np.max(np.abs(ref))), np.max(np.abs(gf - ref))
+
+
+@pytest.mark.parametrize("name", _of("pred"))
+def test_dense_laplace_predict_matches_reference(name):
+    from gpboost_amd import synthetic
+    case = GOLDEN[name]
+    X, y = lik_case_data(case)
+    npred = case["npred"]
+    xp = synthetic.lcg_unif(npred * 2, 0.713).reshape(2, npred).T.copy()
+    xp[: min(5, npred)] = X[: min(5, npred)]
+    gm = _model(X, case)
+    want_cov = "cov" in case
+    pred = gm.predict(y=y, gp_coords_pred=xp, cov_pars=case["cov_pars"], predict_var=not want_cov,
+                      predict_cov_mat=want_cov, predict_response=case["response"])
+    mu = np.asarray(case["mean"])
+    np.testing.assert_allclose(pred["mu"], mu, rtol=1e-8, atol=1e-8 * np.abs(mu).max())
+    if want_cov:
+        c = np.asarray(case["cov"]).reshape(npred, npred)
+        np.testing.assert_allclose(pred["cov"], c, rtol=1e-8, atol=1e-8 * np.abs(c).max())
+    else:
+        np.testing.assert_allclose(pred["var"], case["var"], rtol=1e-8, atol=1e-11)
+
+
+def test_dense_laplace_refusals_and_switch():
+    from gpboost_amd import GPModel, GPBoostError, synthetic
+    X, y = synthetic.rtest_bernoulli_probit_y(100)
+    with pytest.raises(GPBoostError, match="iterative"):
+        GPModel(gp_coords=X, likelihood="bernoulli_probit", cov_function="exponential", matrix_inversion_method="iterative")
+    with pytest.raises(GPBoostError, match="duplicate"):
+        GPModel(gp_coords=np.vstack([X[:50], X[:50]]), likelihood="bernoulli_probit")
+    # likelihood switch gaussian -> probit on a dense model (GPB_SetLikelihood, the R package's set_likelihood;
+    # re_model.cpp:142-147) reaches the same value
+    from gpboost_amd.basic import _safe_call, c_str, lib
+    gm = GPModel(gp_coords=X, likelihood="gaussian", cov_function="exponential")
+    _safe_call(lib().GPB_SetLikelihood(gm.handle, c_str("bernoulli_probit")))
+    gm.num_cov_pars = 2
+    nll = gm.neg_log_likelihood([1.0, 0.2], y)
+    assert abs(nll - GOLDEN["ev_rtest_probit"]["nll"]) <= 1e-9 * abs(nll)
