@@ -35,7 +35,9 @@ class DenseLaplace : public LatentSolverBase {
   void SetOffset(const double* off) override;
   void GetMode(double* mode) override;
   // trafo = (sigma1^2, phi); grad = [d/dlog sigma1^2, d/dlog phi] of the negative approximate marginal
-  // log-likelihood; grad_f (nullable, host n): the gradient wrt the fixed effects F (booster).
+  // log-likelihood (+ d/dlog shape for likelihood 'gamma' with want_aux_grad: CalcGradNegLogLikAuxPars +
+  // 1/2 sum dW/dlog shape o diag((Sigma^-1 + W)^-1) + the implicit term, likelihoods.h:3379-3411, 10508-10524,
+  // 10856-10869); aux: the gamma shape; grad_f (nullable, host n): the gradient wrt the fixed effects F (booster).
   LatentResult Eval(int cov_type, int lik, const double* trafo, double aux, const IterativeConfig& cfg,
                     bool want_grad, bool want_aux_grad, double* grad_f = nullptr,
                     ModeStart start = ModeStart::kZero) override;
@@ -60,11 +62,13 @@ class DenseLaplace : public LatentSolverBase {
   hipStream_t s_;
   bool y_set_ = false, has_off_ = false, prev_valid_ = false, evaluated_ = false;
   double cached_obj_ = 0.;
+  double aux_ = 1.;   // the likelihood's auxiliary parameter (gamma: shape)
+  double sum_log_y_ = 0.;
   int cov_type_ = 0;
   double var_ = 0., phi_ = 0.;
   DevBuf<double> Sig_, B_, Li_, X_, R_, C_;   // n x n (ld); X_: trtri scratch
   DevBuf<double> y_, off_, mode_, a_, mode_prev_, a_prev_, mode_upd_, a_upd_, d1_, w_, ws_, rhs_, t1_, t2_, t3_, t4_;
-  DevBuf<double> dmll_, uv_, ur_, rec_, cols_, red_;
+  DevBuf<double> dmll_, dg_, uv_, ur_, rec_, cols_, red_;
   DevBuf<int> info_;
   double* h_red_ = nullptr;
   hipEvent_t ev_[2] = {nullptr, nullptr};

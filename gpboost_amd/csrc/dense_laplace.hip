@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(kT) dl_build_b_kernel(const double* __restrict
 }
 
 // Newton step quantities (likelihoods.h:1881-1895): d1, W, W^1/2, rhs = W mode + d1
-__global__ void __launch_bounds__(kT) dl_prep_kernel(int n, int lik, const double* __restrict__ y,
+__global__ void __launch_bounds__(kT) dl_prep_kernel(int n, int lik, double aux, const double* __restrict__ y,
                                                     const double* __restrict__ off, const double* __restrict__ mode,
                                                     double* __restrict__ d1, double* __restrict__ w,
                                                     double* __restrict__ ws, double* __restrict__ rhs) {
@@ -102,8 +102,8 @@ __global__ void __launch_bounds__(kT) dl_prep_kernel(int n, int lik, const doubl
   if (i >= n) return;
   const double mi = mode[i];
   const double l = off ? mi + off[i] : mi;
-  const double g = lik_d1(lik, 1., y[i], l);
-  const double wi = lik_info(lik, 1., y[i], l);
+  const double g = lik_d1(lik, aux, y[i], l);
+  const double wi = lik_info(lik, aux, y[i], l);
   d1[i] = g;
   w[i] = wi;
   ws[i] = sqrt(wi);
@@ -139,7 +139,7 @@ __global__ void __launch_bounds__(kT) dl_gdd_kernel(int n, const double* __restr
 }
 
 // one line-search trial (likelihoods.h:1910-1928) at learning rate lam; partials of [a^T mode, sum log p]
-__global__ void __launch_bounds__(kT) dl_trial_kernel(int n, int lik, double lam, const double* __restrict__ mode,
+__global__ void __launch_bounds__(kT) dl_trial_kernel(int n, int lik, double aux, double lam, const double* __restrict__ mode,
                                                      const double* __restrict__ a, const double* __restrict__ mupd,
                                                      const double* __restrict__ aupd, const double* __restrict__ y,
                                                      const double* __restrict__ off, double* __restrict__ mnew,
@@ -158,7 +158,7 @@ __global__ void __launch_bounds__(kT) dl_trial_kernel(int n, int lik, double lam
     mnew[i] = mi;
     anew[i] = ai;
     sq += ai * mi;
-    sl += lik_loglik(lik, 1., y[i], off ? mi + off[i] : mi);
+    sl += lik_loglik(lik, aux, y[i], off ? mi + off[i] : mi);
   }
   const double s0 = block_sum(sq, red);
   const double s1 = block_sum(sl, red);
@@ -184,8 +184,9 @@ __global__ void __launch_bounds__(kT) dl_colscale_lower_kernel(double* __restric
 // diag((Sigma^-1 + W)^-1) = diag(Sigma) - colsums(C o C), C = Q Sigma (likelihoods.h:3305-3311); then
 // d_mll_d_mode = 1/2 diag o dW/dmode (:3315); one wave per column
 __global__ void __launch_bounds__(kT) dl_dmll_kernel(const double* __restrict__ C, const double* __restrict__ S, int n, int ld,
-                                                    int lik, const double* __restrict__ y, const double* __restrict__ off,
-                                                    const double* __restrict__ mode, double* __restrict__ dmll) {
+                                                    int lik, double aux, const double* __restrict__ y,
+                                                    const double* __restrict__ off, const double* __restrict__ mode,
+                                                    double* __restrict__ dmll, double* __restrict__ dgo) {
   const int lane = threadIdx.x & 63;
   const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (j >= n) return;
@@ -198,7 +199,8 @@ __global__ void __launch_bounds__(kT) dl_dmll_kernel(const double* __restrict__ 
   if (lane == 0) {
     const double dg = S[(size_t)j + (size_t)j * ld] - s;
     const double l = off ? mode[j] + off[j] : mode[j];
-    dmll[j] = 0.5 * dg * lik_dinfo(lik, y[j], l);
+    dmll[j] = 0.5 * dg * lik_dinfo(lik, aux, y[j], l);
+    if (dgo) dgo[j] = dg;
   }
 }
 
@@ -261,6 +263,20 @@ __global__ void __launch_bounds__(kT) dl_grad_rec_kernel(int n, int ld, const do
   r[5] = dmll[i] * (cols[3 * (size_t)ld + i] - yr[i]);
 }
 
+// gamma shape gradient records [l + y e^-l, W diag, d1 v] (likelihoods.h:3379-3411, 10514-10524, 10862-10868)
+__global__ void __launch_bounds__(kT) dl_aux_rec_kernel(int n, const double* __restrict__ y, const double* __restrict__ off,
+                                                       const double* __restrict__ mode, const double* __restrict__ w,
+                                                       const double* __restrict__ dg, const double* __restrict__ d1,
+                                                       const double* __restrict__ t, const double* __restrict__ v,
+                                                       double* __restrict__ rec) {
+  const int i = blockIdx.x * kT + threadIdx.x;
+  if (i >= n) return;
+  const double l = off ? mode[i] + off[i] : mode[i];
+  rec[3 * (size_t)i] = l + y[i] * exp(-l);
+  rec[3 * (size_t)i + 1] = w[i] * dg[i];
+  rec[3 * (size_t)i + 2] = d1[i] * (t[i] - v[i]);
+}
+
 // fixed_effect_grad = -d1 + dmll - W o (Sigma dmll - C^T C dmll) (likelihoods.h:3354-3376)
 __global__ void __launch_bounds__(kT) dl_gradf_kernel(int n, const double* __restrict__ d1, const double* __restrict__ dmll,
                                                      const double* __restrict__ w, const double* __restrict__ t,
@@ -310,7 +326,7 @@ DenseLaplace::DenseLaplace(int n, int d, const double* d_X, hipStream_t stream)
   }
   X_.alloc((size_t)ld_ * (ld_ / 2 + 64));
   for (DevBuf<double>* b : {&y_, &off_, &mode_, &a_, &mode_prev_, &a_prev_, &mode_upd_, &a_upd_, &d1_, &w_, &ws_, &rhs_,
-                            &t1_, &t2_, &t3_, &t4_, &dmll_, &uv_, &ur_}) {
+                            &t1_, &t2_, &t3_, &t4_, &dmll_, &dg_, &uv_, &ur_}) {
     b->alloc(ld_);
     HIP_CHECK(hipMemsetAsync(b->get(), 0, sizeof(double) * ld_, s_));
   }
@@ -330,6 +346,8 @@ DenseLaplace::~DenseLaplace() {
 }
 
 void DenseLaplace::SetY(const double* y) {
+  sum_log_y_ = 0.;   // aux_log_normalizing_constant_ of likelihood 'gamma' (likelihoods.h:8181-8191)
+  for (int i = 0; i < n_; ++i) sum_log_y_ += y[i] > 0. ? std::log(y[i]) : 0.;
   HIP_CHECK(hipMemcpyAsync(y_.get(), y, sizeof(double) * n_, hipMemcpyHostToDevice, s_));
   HIP_CHECK(hipStreamSynchronize(s_));
   y_set_ = true;
@@ -386,9 +404,11 @@ bool DenseLaplace::InfoFailed() {
   return info != 0;
 }
 
-LatentResult DenseLaplace::Eval(int cov_type, int lik, const double* trafo, double /*aux*/, const IterativeConfig& cfg,
-                                bool want_grad, bool /*want_aux_grad*/, double* grad_f, ModeStart start) {
+LatentResult DenseLaplace::Eval(int cov_type, int lik, const double* trafo, double aux, const IterativeConfig& cfg,
+                                bool want_grad, bool want_aux_grad, double* grad_f, ModeStart start) {
   if (!y_set_) Fatal("response variable y has not been set");
+  aux_ = lik == kLikGamma ? aux : 1.;
+  want_aux_grad = want_aux_grad && want_grad && lik == kLikGamma;
   if (lik == kLikGaussian) Fatal("DenseLaplace: the Gaussian likelihood uses the exact dense path");
   const int n = n_, ld = ld_;
   const double var = trafo[0], phi = trafo[1];
@@ -401,7 +421,7 @@ LatentResult DenseLaplace::Eval(int cov_type, int lik, const double* trafo, doub
   BuildSigma(cov_type, var, phi);
   const int nbr = nb_red(n);
   auto objective = [&](double lam, const double* mu, const double* au, double* mnew, double* anew) {
-    hipLaunchKernelGGL(dl_trial_kernel, dim3(nbr), dim3(kT), 0, s_, n, lik, lam, mode_.get(), a_.get(), mu, au, y_.get(),
+    hipLaunchKernelGGL(dl_trial_kernel, dim3(nbr), dim3(kT), 0, s_, n, lik, aux_, lam, mode_.get(), a_.get(), mu, au, y_.get(),
                        off, mnew, anew, rec_.get());
     HIP_CHECK(hipGetLastError());
     launch_sum_blocks(rec_.get(), nbr, 2, red + 4, s_);
@@ -430,7 +450,7 @@ LatentResult DenseLaplace::Eval(int cov_type, int lik, const double* trafo, doub
     bool terminate = false, has_nan = false;
     for (it = 0; it < maxit; ++it) {
       // the information changes in every step for the supported likelihoods (information_changes_during_mode_finding_)
-      hipLaunchKernelGGL(dl_prep_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, lik, y_.get(), off, mode_.get(),
+      hipLaunchKernelGGL(dl_prep_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, lik, aux_, y_.get(), off, mode_.get(),
                          d1_.get(), w_.get(), ws_.get(), rhs_.get());
       HIP_CHECK(hipGetLastError());
       FactorB(logdet_B, true);
@@ -482,8 +502,8 @@ LatentResult DenseLaplace::Eval(int cov_type, int lik, const double* trafo, doub
   }
   evaluated_ = true;
   // at the mode (:1941-1953): d1, W, B = I + W^1/2 Sigma W^1/2 = L L^T; mll = obj - sum log L_ii
-  const bool need_inv = want_grad || grad_f != nullptr;
-  hipLaunchKernelGGL(dl_prep_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, lik, y_.get(), off, mode_.get(), d1_.get(),
+  const bool need_inv = want_grad || want_aux_grad || grad_f != nullptr;
+  hipLaunchKernelGGL(dl_prep_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, lik, aux_, y_.get(), off, mode_.get(), d1_.get(),
                      w_.get(), ws_.get(), nullptr);
   HIP_CHECK(hipGetLastError());
   FactorB(logdet_B, need_inv);
@@ -501,8 +521,8 @@ LatentResult DenseLaplace::Eval(int cov_type, int lik, const double* trafo, doub
     // C = Q Sigma (Q lower), R = Q^T Q
     gemm_f64(s_, n, n, n, 1., Q, ld, 0, Sig_.get(), ld, 0, 0., C_.get(), ld, 0, 1, 0, 0);
     gemm_f64(s_, n, n, n, 1., Q, ld, 1, Q, ld, 0, 0., R_.get(), ld, 0, 0, 1, 1);
-    hipLaunchKernelGGL(dl_dmll_kernel, dim3((n + 3) / 4), dim3(kT), 0, s_, C_.get(), Sig_.get(), n, ld, lik, y_.get(), off,
-                       mode_.get(), dmll_.get());
+    hipLaunchKernelGGL(dl_dmll_kernel, dim3((n + 3) / 4), dim3(kT), 0, s_, C_.get(), Sig_.get(), n, ld, lik, aux_, y_.get(),
+                       off, mode_.get(), dmll_.get(), dg_.get());
     HIP_CHECK(hipGetLastError());
     if (want_grad) {
       double* recs = rec_.get();   // n records of 6
@@ -527,10 +547,27 @@ LatentResult DenseLaplace::Eval(int cov_type, int lik, const double* trafo, doub
       // cov_grad = -1/2 a^T dSigma a + 1/2 tr((W^-1 + Sigma)^-1 dSigma) + d_mll_d_mode^T d_mode (:3338-3346)
       res.grad = {-0.5 * g[0] + 0.5 * g[2] + g[4], -0.5 * g[1] + 0.5 * g[3] + g[5]};
     }
-    if (grad_f != nullptr) {
+    if (grad_f != nullptr || want_aux_grad) {   // SigmaI_plus_W_inv_d_mll_d_mode = Sigma dmll - C^T C dmll (:3354-3358)
       Gemv(Sig_.get(), false, false, dmll_.get(), t1_.get());
       Gemv(C_.get(), false, false, dmll_.get(), t2_.get());
       Gemv(C_.get(), false, true, t2_.get(), t3_.get());
+    }
+    if (want_aux_grad) {
+      // gamma shape on the log scale: a [sum (l + y e^-l) - n (log a + 1 - digamma(a)) - sum log y]
+      // + 1/2 sum W_i diag_i + sum d1_i (Sigma dmll - C^T C dmll)_i  (dW/dlog a = W, d2 ll / dl dlog a = d1)
+      hipLaunchKernelGGL(dl_aux_rec_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, y_.get(), off, mode_.get(), w_.get(),
+                         dg_.get(), d1_.get(), t1_.get(), t3_.get(), rec_.get());
+      HIP_CHECK(hipGetLastError());
+      launch_sum_blocks(rec_.get(), n, 3, red + 16, s_);
+      HIP_CHECK(hipMemcpyAsync(h_red_ + 16, red + 16, 3 * sizeof(double), hipMemcpyDeviceToHost, s_));
+      HIP_CHECK(hipStreamSynchronize(s_));
+      const double a = aux_;
+      double neg = h_red_[16] - n * (std::log(a) + 1. - digamma_asa103(a)) - sum_log_y_;
+      neg *= a;
+      if (res.grad.empty()) res.grad = {0., 0.};
+      res.grad.push_back(neg + 0.5 * h_red_[17] + h_red_[18]);
+    }
+    if (grad_f != nullptr) {
       hipLaunchKernelGGL(dl_gradf_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, d1_.get(), dmll_.get(), w_.get(),
                          t1_.get(), t3_.get(), t4_.get());
       HIP_CHECK(hipGetLastError());

@@ -83,7 +83,7 @@ __global__ void __launch_bounds__(kT) fl_diag_kernel(const double* __restrict__ 
 
 // Newton step quantities (likelihoods.h:3130-3150): d1, W (when w_update), DW = (W d + 1)^-1,
 // wdw = sqrt(W)^2 DW, rhs = W mode + d1
-__global__ void __launch_bounds__(kT) fl_prep_kernel(int n, int lik, const double* __restrict__ y,
+__global__ void __launch_bounds__(kT) fl_prep_kernel(int n, int lik, double aux, const double* __restrict__ y,
                                                     const double* __restrict__ off, const double* __restrict__ mode,
                                                     const double* __restrict__ dvec, int w_update,
                                                     double* __restrict__ d1, double* __restrict__ w,
@@ -93,11 +93,11 @@ __global__ void __launch_bounds__(kT) fl_prep_kernel(int n, int lik, const doubl
   if (i >= n) return;
   const double mi = mode[i];
   const double l = off ? mi + off[i] : mi;
-  const double g = lik_d1(lik, 1., y[i], l);
+  const double g = lik_d1(lik, aux, y[i], l);
   d1[i] = g;
   double wi;
   if (w_update) {
-    wi = lik_info(lik, 1., y[i], l);
+    wi = lik_info(lik, aux, y[i], l);
     w[i] = wi;
   } else {
     wi = w[i];
@@ -212,7 +212,7 @@ __global__ void __launch_bounds__(kT) fl_gdd_kernel(int n, const double* __restr
 
 // one line-search trial (likelihoods.h:3171-3190): the new state mixed at learning rate lam (lam = 1:
 // the update itself), partials of [a^T mode, sum log p(y | mode + F)]
-__global__ void __launch_bounds__(kT) fl_trial_kernel(int n, int lik, double lam, const double* __restrict__ mode,
+__global__ void __launch_bounds__(kT) fl_trial_kernel(int n, int lik, double aux, double lam, const double* __restrict__ mode,
                                                      const double* __restrict__ a, const double* __restrict__ mupd,
                                                      const double* __restrict__ aupd, const double* __restrict__ y,
                                                      const double* __restrict__ off, double* __restrict__ mnew,
@@ -231,7 +231,7 @@ __global__ void __launch_bounds__(kT) fl_trial_kernel(int n, int lik, double lam
     mnew[i] = mi;
     anew[i] = ai;
     sq += ai * mi;
-    sl += lik_loglik(lik, 1., y[i], off ? mi + off[i] : mi);
+    sl += lik_loglik(lik, aux, y[i], off ? mi + off[i] : mi);
   }
   const double s0 = block_sum(sq, red);
   const double s1 = block_sum(sl, red);
@@ -243,7 +243,7 @@ __global__ void __launch_bounds__(kT) fl_trial_kernel(int n, int lik, double lam
 
 // after the mode finding (likelihoods.h:3200-3232): d1, W at the mode, DW = (W d + 1)^-1,
 // dpwi = (d + W^-1)^-1; partials of [sum log dpwi, sum log W, #(W == 0)]
-__global__ void __launch_bounds__(kT) fl_final_kernel(int n, int lik, const double* __restrict__ y,
+__global__ void __launch_bounds__(kT) fl_final_kernel(int n, int lik, double aux, const double* __restrict__ y,
                                                      const double* __restrict__ off, const double* __restrict__ mode,
                                                      const double* __restrict__ dvec, double* __restrict__ d1,
                                                      double* __restrict__ w, double* __restrict__ DW,
@@ -253,8 +253,8 @@ __global__ void __launch_bounds__(kT) fl_final_kernel(int n, int lik, const doub
   for (int i = blockIdx.x * kT + threadIdx.x; i < n; i += gridDim.x * kT) {
     const double mi = mode[i];
     const double l = off ? mi + off[i] : mi;
-    d1[i] = lik_d1(lik, 1., y[i], l);
-    const double wi = lik_info(lik, 1., y[i], l);
+    d1[i] = lik_d1(lik, aux, y[i], l);
+    const double wi = lik_info(lik, aux, y[i], l);
     w[i] = wi;
     const double di = dvec[i];
     DW[i] = 1. / (wi * di + 1.);
@@ -318,7 +318,7 @@ __global__ void __launch_bounds__(kT) fl_grad_p0_kernel(const double* __restrict
 // For k = var, dK = K and dK_mm A = K - delta A (K_mm = K_mm,s - delta I).
 template <int COV>
 __global__ void __launch_bounds__(kT) fl_grad_p1_kernel(
-    const double* __restrict__ X, const double* __restrict__ Z, int n, int m, int d, int ldm, int lik, double var,
+    const double* __restrict__ X, const double* __restrict__ Z, int n, int m, int d, int ldm, int lik, double aux, double var,
     double phi, double delta, const double* __restrict__ K, const double* __restrict__ A, const double* __restrict__ G,
     const double* __restrict__ Mr, const double* __restrict__ b, const double* __restrict__ u1,
     const double* __restrict__ u2v, const double* __restrict__ u3v, const double* __restrict__ u2r,
@@ -380,7 +380,7 @@ __global__ void __launch_bounds__(kT) fl_grad_p1_kernel(
       const double wi_inv = 1. / wi;
       const double sw = f * dw * dw + wi_inv - dw * wi_inv;   // diag of (Sigma^-1 + W)^-1 (:5447-5449)
       const double mi = mode[i];
-      dmll[i] = 0.5 * sw * lik_dinfo(lik, y[i], off ? mi + off[i] : mi);
+      dmll[i] = 0.5 * sw * lik_dinfo(lik, aux, y[i], off ? mi + off[i] : mi);
     }
   }
   ev = block4(ev, red);
@@ -577,9 +577,13 @@ void FitcLaplace::Woodbury(const double* s, double* logdet_dev, bool full_invers
     gemm_f64(s_, m, m, m, 1., F.Wi_.get(), ldm, 1, F.Wi_.get(), ldm, 0, 0., F.Winv_.get(), ldm, 0, 0, 1, 1);
 }
 
-LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, double /*aux*/, const IterativeConfig& cfg,
-                               bool want_grad, bool /*want_aux_grad*/, double* grad_f, ModeStart start) {
+LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, double aux, const IterativeConfig& cfg,
+                               bool want_grad, bool want_aux_grad, double* grad_f, ModeStart start) {
   if (!y_set_) Fatal("response variable y has not been set");
+  if (want_aux_grad && want_grad && lik == kLikGamma)
+    Fatal("estimating the shape of likelihood 'gamma' with gp_approx = 'fitc' is not supported by gpboost_amd (set "
+          "estimate_aux_pars = false, or use gp_approx = 'none')");
+  aux_ = lik == kLikGamma ? aux : 1.;
   if (lik == kLikGaussian) Fatal("FitcLaplace: the Gaussian likelihood uses the exact FITC path");
   FitcSolver& F = *F_;
   const int n = n_, m = m_, ldm = ldm_, d = F.d_;
@@ -602,7 +606,7 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
   const int nbr = nb_red(n);
   // objective -1/2 a^T mode + log p(y | mode + F) of the state (mode_, a_)
   auto objective = [&](double lam, const double* mu, const double* au, double* mnew, double* anew) {
-    hipLaunchKernelGGL(fl_trial_kernel, dim3(nbr), dim3(kT), 0, s_, n, lik, lam, mode_.get(), a_.get(), mu, au, y_.get(),
+    hipLaunchKernelGGL(fl_trial_kernel, dim3(nbr), dim3(kT), 0, s_, n, lik, aux_, lam, mode_.get(), a_.get(), mu, au, y_.get(),
                        off, mnew, anew, part_.get());
     HIP_CHECK(hipGetLastError());
     launch_sum_blocks(part_.get(), nbr, 2, red + 4, s_);
@@ -634,7 +638,7 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
     double* vaux2 = mv_.get() + 3 * (size_t)ldm;
     for (it = 0; it < maxit; ++it) {
       // information changes in every step for the supported likelihoods (information_changes_during_mode_finding_)
-      hipLaunchKernelGGL(fl_prep_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, lik, y_.get(), off, mode_.get(), dvec, 1,
+      hipLaunchKernelGGL(fl_prep_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, lik, aux_, y_.get(), off, mode_.get(), dvec, 1,
                          d1_.get(), w_.get(), wdw_.get(), dw_.get(), rhs_.get());
       HIP_CHECK(hipGetLastError());
       Woodbury(wdw_.get(), logdet_M, false);
@@ -689,7 +693,7 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
   }
   evaluated_ = true;
   // after the mode finding (:3200-3232): d1, W at the mode; M = K_mm,s + K diag((d + W^-1)^-1) K^T
-  hipLaunchKernelGGL(fl_final_kernel, dim3(nbr), dim3(kT), 0, s_, n, lik, y_.get(), off, mode_.get(), dvec, d1_.get(),
+  hipLaunchKernelGGL(fl_final_kernel, dim3(nbr), dim3(kT), 0, s_, n, lik, aux_, y_.get(), off, mode_.get(), dvec, d1_.get(),
                      w_.get(), dw_.get(), wdw_.get(), part_.get());
   HIP_CHECK(hipGetLastError());
   launch_sum_blocks(part_.get(), nbr, 3, red + 8, s_);
@@ -739,7 +743,7 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
     double* part1 = F.part_.get();   // pass-1 partials (the split-K Gram scratch is free now)
     dispatch_cov(cov_type, [&](auto c) {
       hipLaunchKernelGGL((fl_grad_p1_kernel<decltype(c)::value>), dim3(nb4), dim3(kT), 0, s_, F.d_X_, F.dZ_.get(), n, m, d,
-                         ldm, lik, var, phi, delta_j, F.Kmn_.get(), F.A_.get(), F.Kd_.get(), F.V_.get(), b, u1, u2v, u3v,
+                         ldm, lik, aux_, var, phi, delta_j, F.Kmn_.get(), F.A_.get(), F.Kd_.get(), F.V_.get(), b, u1, u2v, u3v,
                          u2r, u3r, a_.get(), d1_.get(), w_.get(), dw_.get(), wdw_.get(), mode_.get(), off, y_.get(), sgv_.get(),
                          sgr_.get(), dmll_.get(), part1);
     });

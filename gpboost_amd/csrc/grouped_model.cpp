@@ -226,15 +226,15 @@ void GroupedModel::SetOptimSettings(const double* init_cov_pars, double lr, int 
                                     const char* optimizer, int m_lbfgs) {
   if (optimizer != nullptr && optimizer[0] != '\0') {
     const std::string o(optimizer);
-    if (o != "lbfgs" && !is_internal_optimizer(o))
+    if (o != "lbfgs" && o != "nelder_mead" && !is_internal_optimizer(o))
       Fatal("Optimizer option '%s' is not supported for covariance parameters by gpboost_amd (supported: lbfgs, "
-            "gradient_descent, fisher_scoring)", optimizer);
+            "gradient_descent, fisher_scoring, nelder_mead)", optimizer);
     isettings_.optimizer = o == "lbfgs" ? "" : o;
     optimizer_name_ = o;
   }
   isettings_.lr = lr;
   isettings_.max_iter = max_iter;
-  isettings_.delta = delta_rel_conv < 0. ? 1e-6 : delta_rel_conv;
+  isettings_.delta = delta_rel_conv < 0. ? (isettings_.optimizer == "nelder_mead" ? 1e-8 : 1e-6) : delta_rel_conv;
   if (init_cov_pars != nullptr) {
     init_cov_pars_.assign(init_cov_pars, init_cov_pars + num_cov_pars());
     for (double v : init_cov_pars_)
@@ -368,6 +368,32 @@ void GroupedModel::OptimCovPar(const double* y, const double* fixed_effects) {
     num_it_ = 0;
     cov_pars_orig_ = start_orig;
     cov_pars_initialized_ = true;
+    last_cov_pars_ = cov_pars_orig_;
+    return;
+  }
+  if (isettings_.optimizer == "nelder_mead") {   // OptimExternal "nelder_mead" with the nugget profiled out
+    if (iterative())
+      Fatal("optimizer_cov = 'nelder_mead' is supported by gpboost_amd for grouped random effects with "
+            "matrix_inversion_method = 'cholesky' only (use 'lbfgs')");
+    const double tol_obj = isettings_.crit_params ? 1e-20 : isettings_.delta;
+    const double tol_sol = isettings_.crit_params ? isettings_.delta : 1e-20;
+    std::vector<double> x(P - 1);
+    for (int k = 0; k < P - 1; ++k) x[k] = std::log(trafo[1 + k]);
+    double s2 = 1., fx = 0.;
+    auto fn = [&](const std::vector<double>& v) {
+      std::vector<double> t(P, 1.);
+      for (int k = 0; k < P - 1; ++k) t[1 + k] = std::exp(v[k]);
+      EvalResult r = EvalTrafo(t.data(), false, 1, /*fatal_on_nan=*/false);
+      s2 = r.sigma2;
+      return r.nll;
+    };
+    num_it_ = nelder_mead(fn, x, isettings_.max_iter, tol_obj, tol_sol, &fx);
+    fn(x);   // the profiled sigma^2 at the solution (optim_utils.h:683-686)
+    for (int k = 0; k < P - 1; ++k) trafo[1 + k] = std::exp(x[k]);
+    cov_pars_orig_.assign(P, 0.);
+    ToOrig(trafo.data(), s2, cov_pars_orig_.data());
+    cov_pars_initialized_ = true;
+    last_nll_ = fx;
     last_cov_pars_ = cov_pars_orig_;
     return;
   }

@@ -817,6 +817,9 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
   if (!y_set_) Fatal("response variable y has not been set");
   if (!(trafo[0] > 0. && trafo[1] > 0.)) Fatal("covariance parameters must be > 0");
   if (lik == kLikGaussian && !(aux > 0.)) Fatal("the error variance (aux_pars) must be > 0");
+  if (lik == kLikGamma && want_grad && want_aux_grad)
+    Fatal("estimating the shape of likelihood 'gamma' with gp_approx = 'vecchia' is not supported by gpboost_amd (set "
+          "estimate_aux_pars = false, or use gp_approx = 'none')");
   const int n = n_;
   const bool gauss = lik == kLikGaussian;
   const int t = cfg.num_rand_vec_trace;
@@ -1050,7 +1053,7 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
     Precond(d_Zp_.get(), d_P_.get(), bt.Xt.get(), tw);   // PI_Z = P^-1 Z (:12321-12327)
     if (!gauss) {   // grad_information_wrt_mode_non_zero_: implicit derivative through the mode
       ModeDerivArgs md{};
-      md.n = n; md.m = m_; md.t = tw; md.lik = lik; md.nbr = d_nbr_.get(); md.Bv = d_Bv_.get(); md.dw = d_dw_.get();
+      md.n = n; md.m = m_; md.t = tw; md.lik = lik; md.aux = aux; md.nbr = d_nbr_.get(); md.Bv = d_Bv_.get(); md.dw = d_dw_.get();
       md.loc = d_mode_.get(); md.U = d_U_.get(); md.P = d_P_.get(); md.dmll = d_dmll_.get();
       md.offset = has_off_ && !has_obs_ ? d_off_.get() : nullptr;
       md.y = has_obs_ ? nullptr : d_y_.get();

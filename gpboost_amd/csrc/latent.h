@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <map>
 #include <memory>
+#include <cmath>
 #include <stdexcept>
 #include <random>
 #include <vector>
@@ -43,6 +44,21 @@ struct IterativeConfig {
 // marginal log-likelihood to NaN and returns (likelihoods.h:2929-2933, 2997-3000), so an L-BFGS line
 // search shrinks the step (LineSearchBacktracking.h:78); REModelAMD turns this into nll = NaN when
 // its caller tolerates it and into a fatal error otherwise.
+// digamma by the asymptotic expansion after recurrence to x >= 8.5 (Bernardo 1976, Algorithm AS 103; the form the
+// reference's GPBoost::digamma uses, DF_utils.cpp:82-123)
+inline double digamma_asa103(double x) {
+  if (x <= 0.000001) return -0.57721566490153286060 - 1.0 / x + 1.6449340668482264365 * x;
+  double value = 0., x2 = x;
+  while (x2 < 8.5) {
+    value = value - 1.0 / x2;
+    x2 = x2 + 1.0;
+  }
+  double r = 1.0 / x2;
+  value = value + std::log(x2) - 0.5 * r;
+  r = r * r;
+  return value - r * (1.0 / 12.0 - r * (1.0 / 120.0 - r * (1.0 / 252.0 - r * (1.0 / 240.0 - r * (1.0 / 132.0)))));
+}
+
 struct LatentNan : std::runtime_error {
   using std::runtime_error::runtime_error;
 };

@@ -312,7 +312,7 @@ void launch_axpby(size_t count, double alpha, const double* X, double beta, cons
                   hipStream_t s);
 
 // ---- likelihood-specific elementwise and reductions
-enum LatentLik : int { kLikGaussian = 0, kLikBernoulliLogit = 1, kLikBernoulliProbit = 2, kLikPoisson = 3 };
+enum LatentLik : int { kLikGaussian = 0, kLikBernoulliLogit = 1, kLikBernoulliProbit = 2, kLikPoisson = 3, kLikGamma = 4 };
 
 // Observations of the latent variables when coordinates repeat (the reference's unique-location
 // form: Z maps n observations to the n_u latent variables, Vecchia_utils.cpp:1121-1139,
@@ -402,6 +402,7 @@ void launch_grad_cols(const GradColsArgs& a, double* partials, double* out, hipS
 // dmll[i] = 0.5 * ( tr1_i + c_i * dW_i / dw_i - c_i * trP_i ).
 struct ModeDerivArgs {
   int n, m, t, lik;
+  double aux;                  // the likelihood's auxiliary parameter (gamma: shape)
   int t_valid, t_all, stage;   // see mode_deriv_kernel; single rank: t_valid = t_all = t, stage 0
   double* mom;                 // stages 1-3: n x 2 row sums (all-reduced between stages)
   double* mom2;

@@ -3,6 +3,7 @@
 //   gaussian        likelihoods.h :8795, 9263, 9937 (aux = error variance)
 //   bernoulli_logit likelihoods.h :8724, 9226, 9896, 10187; sigmoid_stable / softplus DF_utils.h:37-60
 //   bernoulli_probit :8708, 9208, 9871, 10171;  poisson :8730, 9230, 9904, 10200
+//   gamma           :8740, 9234, 9908, 10228 (aux = shape; log link, the normalizing constant on the host)
 // Shared by the Vecchia (sparse_kernels.hip) and FITC (fitc_laplace.hip) Laplace paths.
 #pragma once
 
@@ -47,12 +48,14 @@ __device__ __forceinline__ double lik_loglik(int lik, double aux, double y, doub
   }
   if (lik == kLikBernoulliProbit) return y == 0. ? normal_log_cdf(-l) : normal_log_cdf(l);   // :8708-8715
   if (lik == kLikPoisson) return y * l - exp(l);                                              // :8730-8737
+  if (lik == kLikGamma) return -aux * (l + y * exp(-l));                                      // :8740-8748
   return y * l - softplus(l);
 }
 __device__ __forceinline__ double lik_d1(int lik, double aux, double y, double l) {
   if (lik == kLikGaussian) return (y - l) / aux;
   if (lik == kLikBernoulliProbit) return y == 0. ? -mills_one_minus_phi(l) : mills_phi(l);    // :9208-9215
   if (lik == kLikPoisson) return y - exp(l);                                                  // :9230-9232
+  if (lik == kLikGamma) return aux * (y * exp(-l) - 1.);                                      // :9234-9236
   return y - sigmoid_stable(l);
 }
 // information (negative second derivative), likelihoods.h:9871-9906
@@ -67,12 +70,14 @@ __device__ __forceinline__ double lik_info(int lik, double aux, double y, double
     return r * (l + r);
   }
   if (lik == kLikPoisson) return exp(l);
+  if (lik == kLikGamma) return aux * y * exp(-l);   // :9908-9910
   const double p = sigmoid_stable(l);
   return p * (1. - p);
 }
 // derivative of the information wrt the location parameter, likelihoods.h:10165-10195
-__device__ __forceinline__ double lik_dinfo(int lik, double y, double l) {
+__device__ __forceinline__ double lik_dinfo(int lik, double aux, double y, double l) {
   if (lik == kLikGaussian) return 0.;
+  if (lik == kLikGamma) return -aux * y * exp(-l);   // :10228-10233
   if (lik == kLikBernoulliProbit) {
     const double x2 = l * l;
     if (y == 0.) {

@@ -289,6 +289,106 @@ int internal_optimize(InternalObjective& f, std::vector<double>& pars, const Int
   return num_it;
 }
 
+int nelder_mead(const std::function<double(const std::vector<double>&)>& f, std::vector<double>& x0, int iter_max,
+                double tol_obj, double tol_sol, double* fval) {
+  const int nv = (int)x0.size();
+  const double alpha = 1., beta = 0.75 - 1. / (2. * nv), gamma = 1. + 2. / nv, delta = 1. - 1. / nv;   // adaptive_pars
+  std::vector<std::vector<double>> P(nv + 1, x0);
+  std::vector<double> F(nv + 1);
+  F[0] = f(x0);
+  for (int i = 1; i <= nv; ++i) {
+    const double xi = x0[i - 1];
+    P[i][i - 1] = xi + (xi != 0. ? 0.05 * xi : 0.00025);
+    F[i] = f(P[i]);
+  }
+  auto max_abs = [](double v, double acc) { return std::max(acc, std::fabs(v)); };
+  std::vector<std::vector<double>> Pold = P;
+  std::vector<double> Fold = F;
+  int iter = 0;
+  bool converged = false;
+  while (!converged) {
+    ++iter;
+    bool next = false;
+    // step 1: sort the vertices by value (get_sort_index: std::sort of the indices)
+    std::vector<int> idx(nv + 1);
+    std::iota(idx.begin(), idx.end(), 0);
+    std::sort(idx.begin(), idx.end(), [&](int a, int b) { return F[a] < F[b]; });
+    {
+      std::vector<std::vector<double>> P2(nv + 1);
+      std::vector<double> F2(nv + 1);
+      for (int i = 0; i <= nv; ++i) { P2[i] = P[idx[i]]; F2[i] = F[idx[i]]; }
+      P.swap(P2);
+      F.swap(F2);
+    }
+    // step 2: centroid of the best nv vertices, reflection
+    std::vector<double> c(nv, 0.);
+    for (int j = 0; j < nv; ++j) {
+      double sacc = 0.;
+      for (int i = 0; i < nv; ++i) sacc += P[i][j];
+      c[j] = sacc / (double)nv;
+    }
+    auto along = [&](double t, const std::vector<double>& dir_end) {   // c + t (dir_end - c)
+      std::vector<double> out(nv);
+      for (int j = 0; j < nv; ++j) out[j] = c[j] + t * (dir_end[j] - c[j]);
+      return out;
+    };
+    std::vector<double> xr(nv);
+    for (int j = 0; j < nv; ++j) xr[j] = c[j] + alpha * (c[j] - P[nv][j]);
+    const double fr = f(xr);
+    if (fr >= F[0] && fr < F[nv - 1]) {
+      P[nv] = xr;
+      F[nv] = fr;
+      next = true;
+    }
+    // step 3: expansion
+    if (!next && fr < F[0]) {
+      std::vector<double> xe = along(gamma, xr);
+      const double fe = f(xe);
+      if (fe < fr) { P[nv] = xe; F[nv] = fe; }
+      else { P[nv] = xr; F[nv] = fr; }
+      next = true;
+    }
+    // steps 4, 5: contractions
+    if (!next && fr >= F[nv - 1]) {
+      if (fr < F[nv]) {
+        std::vector<double> xoc = along(beta, xr);
+        const double foc = f(xoc);
+        if (foc <= fr) { P[nv] = xoc; F[nv] = foc; next = true; }
+      } else {
+        std::vector<double> xic = along(beta, P[nv]);
+        const double fic = f(xic);
+        if (fic < F[nv]) { P[nv] = xic; F[nv] = fic; next = true; }
+      }
+    }
+    // step 6: shrink toward the best vertex
+    if (!next) {
+      for (int i = 1; i <= nv; ++i)
+        for (int j = 0; j < nv; ++j) P[i][j] = P[0][j] + delta * (P[i][j] - P[0][j]);
+      for (int i = 1; i <= nv; ++i) F[i] = f(P[i]);
+    }
+    // convergence (nm.hpp:303-311): changes against the previous iteration's (unsorted) arrays
+    double dF = 0., mF = 0.;
+    for (int i = 0; i <= nv; ++i) { dF = max_abs(F[i] - Fold[i], dF); mF = max_abs(Fold[i], mF); }
+    const double rel_obj = dF / (1.0e-08 + mF);
+    Fold = F;
+    double rel_sol = 2. * std::fabs(tol_sol);
+    if (tol_sol >= 0.) {
+      double dP = 0., mP = 0.;
+      for (int i = 0; i <= nv; ++i)
+        for (int j = 0; j < nv; ++j) { dP = max_abs(P[i][j] - Pold[i][j], dP); mP = max_abs(Pold[i][j], mP); }
+      rel_sol = dP / (1.0e-08 + mP);
+      Pold = P;
+    }
+    converged = !(rel_obj > tol_obj && rel_sol > tol_sol && iter < iter_max);
+  }
+  int best = 0;   // index_min
+  for (int i = 1; i <= nv; ++i)
+    if (F[i] < F[best]) best = i;
+  x0 = P[best];
+  *fval = f(x0);
+  return iter;
+}
+
 // ---------------------------------------------------------------------------------------------
 // REModelAMD: initial values and the optimization driver
 
@@ -421,14 +521,15 @@ void REModelAMD::SetOptimSettings(const double* init_cov_pars, double lr, int ma
   // re_model.cpp:264-279 and re_model_template.h:710-823
   if (optimizer != nullptr && optimizer[0] != '\0') {
     const std::string o(optimizer);
-    if (o != "lbfgs" && !is_internal_optimizer(o))
+    if (o != "lbfgs" && o != "nelder_mead" && !is_internal_optimizer(o))
       Fatal("Optimizer option '%s' is not supported for covariance parameters by gpboost_amd (supported: lbfgs, "
-            "gradient_descent, fisher_scoring)", o.c_str());
+            "gradient_descent, fisher_scoring, nelder_mead)", o.c_str());
     isettings_.optimizer = o == "lbfgs" ? "" : o;
   }
   isettings_.lr = lr;
   isettings_.max_iter = max_iter;
-  isettings_.delta = delta_rel_conv < 0. ? 1e-6 : delta_rel_conv;
+  // SetInitialValueDeltaRelConv (re_model_template.h:7524-7533): 1e-8 for nelder_mead, else 1e-6
+  isettings_.delta = delta_rel_conv < 0. ? (isettings_.optimizer == "nelder_mead" ? 1e-8 : 1e-6) : delta_rel_conv;
   if (init_cov_pars != nullptr) {
     init_cov_pars_.assign(init_cov_pars, init_cov_pars + num_cov_pars());
     for (double v : init_cov_pars_)
@@ -619,13 +720,28 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects, bool 
     FindInitCovPar(yv.data(), trafo);
   }
   if (with_aux && !aux_pars_set_) {
-    // likelihoods.h:1087-1116, 1223-1225 (FindInitialAuxPars, gaussian): sample variance / 2
     if (yv.empty()) Fatal("initial auxiliary parameters need the response variable y");
-    double avg = 0., sum_sq = 0.;
-    for (int i = 0; i < n; ++i) { avg += yv[i]; sum_sq += yv[i] * yv[i]; }
-    avg /= n;
-    const double sample_var = std::max((sum_sq - n * avg * avg) / (n - 1), 1e-6);
-    aux_pars_[0] = sample_var / 2.;
+    if (cfg_.lik == kLikGamma) {
+      // likelihoods.h:1116-1145 (FindInitialAuxPars, gamma): approximate MLE of the shape ignoring the random
+      // effects, s = log(mean y e^-F) - mean(log y - F), k = (3 - s + sqrt((s - 3)^2 + 24 s)) / (12 s)
+      double log_avg = 0., avg_log = 0.;
+      for (int i = 0; i < n; ++i) {
+        const double f = fixed_effects != nullptr ? fixed_effects[i] : 0.;
+        log_avg += fixed_effects != nullptr ? yraw[i] / std::exp(f) : yraw[i];
+        avg_log += fixed_effects != nullptr ? std::log(yraw[i]) - f : std::log(yraw[i]);
+      }
+      log_avg = std::log(log_avg / n);
+      avg_log /= n;
+      const double sv = log_avg - avg_log;
+      aux_pars_[0] = (3. - sv + std::sqrt((sv - 3.) * (sv - 3.) + 24. * sv)) / (12. * sv);
+    } else {
+      // likelihoods.h:1087-1116, 1223-1225 (FindInitialAuxPars, gaussian): sample variance / 2
+      double avg = 0., sum_sq = 0.;
+      for (int i = 0; i < n; ++i) { avg += yv[i]; sum_sq += yv[i] * yv[i]; }
+      avg /= n;
+      const double sample_var = std::max((sum_sq - n * avg * avg) / (n - 1), 1e-6);
+      aux_pars_[0] = sample_var / 2.;
+    }
     aux_pars_set_ = true;   // SetAuxPars marks them set (likelihoods.h:1809): a refit continues from here
   }
   std::vector<double> start_orig;
@@ -642,7 +758,39 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects, bool 
   if (!reuse_m_bfgs) m_bfgs_ = InverseHessian();   // a fresh solver state (LBFGS.h:42-48)
   std::vector<double> x;
   double fx = 0.;
-  if (!isettings_.optimizer.empty()) {   // "gradient_descent" / "fisher_scoring" (re_model_template.h:1287-1549)
+  if (isettings_.optimizer == "nelder_mead") {   // OptimExternal "nelder_mead" (optim_utils.h:642-643, 680-700)
+    const double tol_obj = isettings_.crit_params ? 1e-20 : isettings_.delta;
+    const double tol_sol = isettings_.crit_params ? isettings_.delta : 1e-20;
+    double s2 = 1.;
+    if (!cfg_.latent) {   // EvalLLforOptimLib with the nugget profiled out: x = log(sigma1^2 / sigma^2, phi)
+      x = {std::log(trafo[1]), std::log(trafo[2])};
+      auto fn = [&](const std::vector<double>& v) {
+        const double t[3] = {1., std::exp(v[0]), std::exp(v[1])};
+        EvalResult r = EvalTrafo(t, false, 1, /*fatal_on_nan=*/false);
+        s2 = r.sigma2;
+        return r.nll;
+      };
+      num_it_ = nelder_mead(fn, x, isettings_.max_iter, tol_obj, tol_sol, &fx);
+      fn(x);   // OptimExternal re-evaluates at the solution for the profiled sigma^2 (:683-686)
+      cov_pars_orig_ = {s2, std::exp(x[0]) * s2, range_back(cfg_.cov_type, std::exp(x[1]))};
+    } else {   // x = log(sigma1^2, phi[, aux]); the Laplace mode continues from the previous evaluation
+      x = {std::log(trafo[0]), std::log(trafo[1])};
+      if (with_aux) x.push_back(std::log(aux_pars_[0]));
+      auto fn = [&](const std::vector<double>& v) {
+        const double t[2] = {std::exp(v[0]), std::exp(v[1])};
+        if (with_aux) {
+          const double aux = std::exp(v[2]);
+          SetAuxPars(&aux);
+        }
+        EvalResult r = EvalLatentTrafo(t, false, /*fatal_on_nan=*/false, LatentVecchia::ModeStart::kWarm);
+        if (!std::isfinite(r.nll)) ResetLatentModeToPrevious();   // EvalLLforOptimLib, optim_utils.h:196-199
+        return r.nll;
+      };
+      num_it_ = nelder_mead(fn, x, isettings_.max_iter, tol_obj, tol_sol, &fx);
+      cov_pars_orig_ = {std::exp(x[0]), range_back(cfg_.cov_type, std::exp(x[1]))};
+      if (with_aux) aux_pars_[0] = std::exp(x[2]);
+    }
+  } else if (!isettings_.optimizer.empty()) {   // "gradient_descent" / "fisher_scoring" (re_model_template.h:1287-1549)
     if (cfg_.latent)
       Fatal("optimizer_cov = '%s' is supported by gpboost_amd for the Gaussian likelihood only (use 'lbfgs')",
             isettings_.optimizer.c_str());

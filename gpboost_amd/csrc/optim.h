@@ -10,6 +10,7 @@
 // gradient comes from the device evaluation of REModelAMD.
 #pragma once
 
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -103,5 +104,15 @@ class InternalObjective {
 // number of iterations (the reference's num_it) and the final objective value in *nll.
 int internal_optimize(InternalObjective& f, std::vector<double>& trafo, const InternalSettings& s, double* nll);
 bool is_internal_optimizer(const std::string& name);
+
+// "nelder_mead": OptimLib's Nelder-Mead as OptimExternal runs it (optim_utils.h:626-643, 680-700;
+// external_libs/OptimLib/unconstrained/nm.hpp nm_impl with adaptive parameters, algo_settings_t defaults):
+// the initial simplex x0 + 0.05 x0_i e_i (0.00025 e_i for a zero entry), reflection / expansion / outside and
+// inside contraction / shrink, convergence when the largest change of the vertex values relative to
+// 1e-8 + max |old value| is <= tol_obj, or the same for the vertices <= tol_sol, or iter_max iterations.
+// x is overwritten with the best vertex; returns the reference's opt_iter and the objective at x in *fval
+// (error_reporting's final evaluation).
+int nelder_mead(const std::function<double(const std::vector<double>&)>& f, std::vector<double>& x, int iter_max,
+                double tol_obj, double tol_sol, double* fval);
 
 }  // namespace gpb_amd

@@ -22,8 +22,9 @@ int parse_likelihood(const std::string& name) {
   if (name == "bernoulli_logit") return kLikBernoulliLogit;
   if (name == "bernoulli_probit") return kLikBernoulliProbit;
   if (name == "poisson") return kLikPoisson;
-  Fatal("likelihood '%s' is not supported by gpboost_amd (supported: gaussian, bernoulli_logit, bernoulli_probit, poisson)",
-        name.c_str());
+  if (name == "gamma") return kLikGamma;
+  Fatal("likelihood '%s' is not supported by gpboost_amd (supported: gaussian, bernoulli_logit, bernoulli_probit, poisson, "
+        "gamma)", name.c_str());
   return -1;
 }
 
@@ -110,7 +111,8 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
     Fatal("matrix_inversion_method '%s' is not supported for latent Vecchia models in gpboost_amd (supported: iterative)", mim.c_str());
   if (!(cfg_.latent && vecchia_) && mim != "cholesky")
     Fatal("matrix_inversion_method '%s' is not supported for likelihood 'gaussian' in gpboost_amd (supported: cholesky)", mim.c_str());
-  if (cfg_.latent && cfg_.lik == kLikGaussian) aux_pars_ = {1.};   // likelihoods.h:241 (error_variance)
+  if (cfg_.latent && (cfg_.lik == kLikGaussian || cfg_.lik == kLikGamma))
+    aux_pars_ = {1.};   // likelihoods.h:241 (error_variance), :181-186 (gamma shape)
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0)
     Fatal("no HIP device visible: gpboost_amd has no CPU fallback");
@@ -539,6 +541,10 @@ void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred,
   std::vector<double> h((size_t)2 * n_pred);
   std::vector<double> cov_all;   // cond_all: the dense predictive covariance (predict_cov_mat)
   if (cond_all) {
+    // the covariance of cond_all is assembled on the host from the rows of Bp^-1 (they fill in): bounded like the
+    // latent forms (PredictLatentSim) rather than running O(n_pred^3) host work unannounced
+    if (predict_cov_mat && n_pred > 20000)
+      Fatal("order_obs_first_cond_all with predict_cov_mat is limited to num_data_pred <= 20000 in gpboost_amd");
     PredictCondAll(n, n_pred, mp, nb, dB.get(), dD.get(), trafo[0], predict_response ? 0. : 1., predict_var,
                    predict_cov_mat, h, cov_all);
   } else {
@@ -755,6 +761,13 @@ void REModelAMD::ResponseTransform(int n_pred, double* mean, double* var, double
     for (int p = 0; p < n_pred; ++p) {
       mean[p] = 0.5 * std::erfc(-(mean[p] / std::sqrt(1. + var[p])) * M_SQRT1_2);
       var[p] = mean[p] * (1. - mean[p]);
+    }
+  } else if (cfg_.lik == kLikGamma) {   // :7571-7584
+    const double a = aux_pars_.empty() ? 1. : aux_pars_[0];
+    for (int p = 0; p < n_pred; ++p) {
+      const double pm = std::exp(mean[p] + 0.5 * var[p]);
+      var[p] = (std::exp(var[p]) - 1.) * pm * pm + std::exp(2 * mean[p] + 2 * var[p]) / a;
+      mean[p] = pm;
     }
   } else if (cfg_.lik == kLikPoisson) {   // :7557-7569
     for (int p = 0; p < n_pred; ++p) {
@@ -1122,6 +1135,13 @@ void REModelAMD::SetY(const double* y) {
       for (int i = 0; i < n; ++i)
         if (yv[i] != 0. && yv[i] != 1.)
           Fatal("The response variable ('y') needs to be 0 or 1 for likelihood = '%s' ", cfg_.likelihood.c_str());
+    } else if (cfg_.lik == kLikGamma) {   // :668-673; sum log y for the normalizing constant (:8181-8191)
+      sum_log_y_ = 0.;
+      for (int i = 0; i < n; ++i) {
+        if (yv[i] <= 0.)
+          Fatal(" Must have y > 0 for the response variable ('y') for likelihood = '%s', found %g ", cfg_.likelihood.c_str(), yv[i]);
+        sum_log_y_ += std::log(yv[i]);
+      }
     } else if (cfg_.lik == kLikPoisson) {
       for (int i = 0; i < n; ++i) {
         if (yv[i] < 0.) Fatal(" Must have y >= 0 for the response variable ('y') for likelihood = 'poisson', found %g ", yv[i]);
@@ -1286,6 +1306,12 @@ EvalResult REModelAMD::EvalLatentTrafo(const double* trafo, bool want_grad, bool
   lat()->ClearModePrevious();
   const double aux = aux_pars_.empty() ? 1. : aux_pars_[0];
   const bool aux_grad = estimate_aux_pars && !aux_pars_.empty();
+  if (cfg_.lik == kLikGamma) {   // LogNormalizingConstantGamma (likelihoods.h:8431-8440): 0 at shape 1 (TwoNumbersAreEqual)
+    const double c = std::fabs(aux - 1.) < 1e-10 * std::max({1., std::fabs(aux), 1.})
+                         ? 0.
+                         : (aux - 1.) * sum_log_y_ + cfg_.n * (aux * std::log(aux) - std::lgamma(aux));
+    lat()->SetLogLikConst(c);
+  }
   LatentResult r;
   try {
     // fault injection for the tests: the k-th latent evaluation of this model reports NaN

@@ -79,7 +79,10 @@ class REModelAMD {
   int num_cov_pars() const { return cfg_.latent ? 2 : 3; }
   int num_aux_pars() const { return (int)aux_pars_.size(); }
   const std::vector<double>& aux_pars() const { return aux_pars_; }
-  std::string aux_par_name() const { return cfg_.latent && cfg_.lik == kLikGaussian ? "error_variance" : ""; }
+  std::string aux_par_name() const {
+    if (!cfg_.latent) return "";
+    return cfg_.lik == kLikGaussian ? "error_variance" : (cfg_.lik == kLikGamma ? "shape" : "");
+  }
   void SetAuxPars(const double* aux);
   int device() const { return device_; }
   const ModelConfig& config() const { return cfg_; }
@@ -305,6 +308,7 @@ class REModelAMD {
   std::unique_ptr<FitcSolver> fitc_;   // gp_approx = "fitc"
   std::unique_ptr<FitcLaplace> fitc_lap_;   // gp_approx = "fitc", non-Gaussian likelihood (Laplace)
   std::unique_ptr<DenseLaplace> dense_lap_; // gp_approx = "none", non-Gaussian likelihood (Laplace)
+  double sum_log_y_ = 0.;                   // likelihood 'gamma': sum log y (its normalizing constant)
   std::unique_ptr<VifSolver> vif_;          // gp_approx = "full_scale_vecchia" (Gaussian likelihood)
   std::unique_ptr<VecchiaFisher> vfisher_;  // gp_approx = "vecchia", Gaussian: standard deviations (lazy)
   std::mt19937 fitc_rng_;              // the model's generator after the inducing-point selection

@@ -395,7 +395,7 @@ void REModelAMD::SetLikelihood(const std::string& likelihood) {
   c.latent = latent;
   cfg_ = c;
   aux_pars_.clear();
-  if (cfg_.latent && cfg_.lik == kLikGaussian) aux_pars_ = {1.};
+  if (cfg_.latent && (cfg_.lik == kLikGaussian || cfg_.lik == kLikGamma)) aux_pars_ = {1.};
   latent_.reset();
   structure_built_ = false;
   y_set_ = false;

@@ -1277,11 +1277,11 @@ __global__ void __launch_bounds__(kBT) mode_deriv_kernel(ModeDerivArgs a, int sh
     const double* bv = a.Bv + (size_t)i * a.m;
     double dWi;
     if (a.obs.ptr == nullptr) {
-      dWi = lik_dinfo(a.lik, a.y ? a.y[i] : 0., a.offset ? a.loc[i] + a.offset[i] : a.loc[i]);
+      dWi = lik_dinfo(a.lik, a.aux, a.y ? a.y[i] : 0., a.offset ? a.loc[i] + a.offset[i] : a.loc[i]);
     } else {   // Z^T dW: the row's observations
       dWi = 0.;
       for (int e = a.obs.ptr[i]; e < a.obs.ptr[i + 1]; ++e)
-        dWi += lik_dinfo(a.lik, a.obs.y[e], a.obs.offset ? a.loc[i] + a.obs.offset[e] : a.loc[i]);
+        dWi += lik_dinfo(a.lik, a.aux, a.obs.y[e], a.obs.offset ? a.loc[i] + a.obs.offset[e] : a.loc[i]);
     }
     // pass 1: row means of z1 = U dW P and zP = (BP)^2 dW over the t probes
     // (c_var == 0 -> c = 1, CG_utils.cpp:1036-1039).

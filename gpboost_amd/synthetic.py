@@ -95,6 +95,25 @@ def rtest_poisson_y(n: int = 100) -> tuple[np.ndarray, np.ndarray]:
     return coords, poisson.ppf(sim_rand_unif(n, 0.435), np.exp(eps)).astype(np.float64)
 
 
+def rtest_gamma_y(n: int = 100, shape: float = 1.0) -> tuple[np.ndarray, np.ndarray]:
+    """R non-Gaussian test data, spatial gamma case (test_GPModel_non_Gaussian_data.R:2603-2604):
+    y = qgamma(sim_rand_unif(n, 0.435), scale = mu / shape, shape = shape), mu = exp(L b_1)."""
+    from scipy.stats import gamma
+
+    coords, eps = _rtest_field(n)
+    mu = np.exp(eps)
+    return coords, gamma.ppf(sim_rand_unif(n, 0.435), a=shape, scale=mu / shape)
+
+
+def bench_gamma_y(coords: np.ndarray, shape: float = 2.0) -> np.ndarray:
+    """Gamma responses with log-mean 0.3 + sin(2 pi x1) cos(2 pi x2) and the given shape, drawn by inversion of
+    the gamma CDF at u from LCG c=0.31415 (exact arithmetic)."""
+    from scipy.stats import gamma
+
+    mu = np.exp(0.3 + np.sin(2 * np.pi * coords[:, 0]) * np.cos(2 * np.pi * coords[:, 1]))
+    return gamma.ppf(lcg_unif(coords.shape[0], 0.31415), a=shape, scale=mu / shape)
+
+
 def rtest_probit_X(n: int = 100) -> np.ndarray:
     """X <- cbind(rep(1,n), sin((1:n-n/2)^2*2*pi/n)) (test_GPModel_non_Gaussian_data.R:60)."""
     i = np.arange(1, n + 1, dtype=np.float64)

@@ -52,7 +52,11 @@ def lik_case_data(case):
         return synthetic.rtest_bernoulli_probit_y(case["n"])
     if case["data"] == "rtest_poisson":
         return synthetic.rtest_poisson_y(case["n"])
+    if case["data"] == "rtest_gamma":
+        return synthetic.rtest_gamma_y(case["n"])
     X = synthetic.bench_coords(case["n"])
+    if case["data"] == "bench_gamma":
+        return X, synthetic.bench_gamma_y(X)
     return X, (synthetic.bench_poisson_y(X) if case["data"] == "bench_pois" else synthetic.bench_bernoulli_y(X))
 
 

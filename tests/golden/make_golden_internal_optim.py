@@ -96,6 +96,41 @@ def main():
     cases["combined_rtest_gd"] = dict(data="rtest_combined", spec=opts, **_keep(r))
     print("combined_rtest_gd", r["cov_pars"], r["nll"], r["num_it"], file=sys.stderr)
 
+    # nelder_mead (OptimExternal -> OptimLib nm, optim_utils.h:642-643): default delta_rel_conv 1e-8
+    NM = dict(optimizer="nelder_mead")
+    for name, opts in {
+        "nm_rtest_dense": dict(cov_fct="exponential", gp_approx="none", init_cov_pars=init, **NM),
+        "nm_rtest_dense_default": dict(cov_fct="exponential", gp_approx="none", **NM),
+        "nm_rtest_dense_crit_pars": dict(cov_fct="exponential", gp_approx="none", init_cov_pars=init,
+                                         convergence_criterion="relative_change_in_parameters", delta_rel_conv="1e-6", **NM),
+    }.items():
+        r = run_ref(X, y, mode="fit", **opts)
+        cases[name] = dict(data="rtest_gaussian", spec=opts, **_keep(r))
+        print(name, r["cov_pars"], r["nll"], r["num_it"], file=sys.stderr)
+    r = run_ref(sc, sy, mode="fit", cov_fct="matern", shape=1.5, gp_approx="vecchia", num_neighbors=20, ordering="random",
+                **NM)
+    cases["nm_synth2000_vecchia_matern15"] = dict(data="bench", n=n, spec=dict(cov_fct="matern", shape=1.5, gp_approx="vecchia",
+                                                  num_neighbors=20, ordering="random", **NM), **_keep(r))
+    g = synthetic.bench_groups(3000, (80, 15))
+    r = run_ref(None, synthetic.bench_grouped_y(g), groups=g, mode="fit", matrix_inversion_method="cholesky", **NM)
+    cases["nm_grouped_k2"] = dict(data="grouped", n=3000, levels=[80, 15],
+                                  spec=dict(matrix_inversion_method="cholesky", **NM), **_keep(r))
+    r = run_ref(Xc, yc, groups=gc.reshape(-1, 1), mode="fit", cov_fct="exponential", gp_approx="none", **NM)
+    cases["nm_combined_rtest"] = dict(data="rtest_combined", spec=dict(cov_fct="exponential", gp_approx="none", **NM),
+                                      **_keep(r))
+    # Laplace models: dense (probit, R-test data) and FITC (poisson)
+    from make_golden_latent_lik import data as lik_data
+    Xp_, yp_ = lik_data("rtest_probit", 100)
+    opts = dict(cov_fct="exponential", gp_approx="none", likelihood="bernoulli_probit", **NM)
+    r = run_ref(Xp_, yp_, mode="fit", **opts)
+    cases["nm_dense_probit_rtest"] = dict(data="lik", lik_data="rtest_probit", n=100, spec=opts, **_keep(r))
+    Xq_, yq_ = lik_data("bench_pois", 1000)
+    opts = dict(cov_fct="exponential", gp_approx="fitc", num_ind_points=50, likelihood="poisson", **NM)
+    r = run_ref(Xq_, yq_, mode="fit", **opts)
+    cases["nm_fitc_pois"] = dict(data="lik", lik_data="bench_pois", n=1000, spec=opts, **_keep(r))
+    for k in ("nm_synth2000_vecchia_matern15", "nm_grouped_k2", "nm_combined_rtest", "nm_dense_probit_rtest", "nm_fitc_pois"):
+        print(k, cases[k]["cov_pars"], cases[k]["nll"], cases[k]["num_it"], file=sys.stderr)
+
     with open(OUT, "w") as f:
         json.dump(cases, f, indent=1)
 

@@ -43,7 +43,11 @@ def data(kind, n):
         return synthetic.rtest_bernoulli_probit_y(n)
     if kind == "rtest_poisson":
         return synthetic.rtest_poisson_y(n)
+    if kind == "rtest_gamma":
+        return synthetic.rtest_gamma_y(n)
     X = synthetic.bench_coords(n)
+    if kind == "bench_gamma":
+        return X, synthetic.bench_gamma_y(X)
     return X, (synthetic.bench_poisson_y(X) if kind == "bench_pois" else synthetic.bench_bernoulli_y(X))
 
 

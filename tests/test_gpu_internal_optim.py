@@ -52,6 +52,13 @@ def _model_and_y(case):
         g = synthetic.bench_groups(case["n"], tuple(case["levels"]))
         return GPModel(group_data=g, matrix_inversion_method=sp["matrix_inversion_method"]), \
             synthetic.bench_grouped_y(g)
+    if case["data"] == "lik":   # Laplace models (make_golden_latent_lik.py's generators)
+        from conftest import lik_case_data
+        X, y = lik_case_data(dict(data=case["lik_data"], n=case["n"]))
+        kw = dict(gp_coords=X, cov_function=sp["cov_fct"], gp_approx=sp["gp_approx"], likelihood=sp["likelihood"], seed=0)
+        if sp["gp_approx"] == "fitc":
+            kw["num_ind_points"] = int(sp["num_ind_points"])
+        return GPModel(**kw), y
     if case["data"] == "rtest_combined":
         X, g, y = synthetic.rtest_combined_y(100)
         return GPModel(gp_coords=X, group_data=g, cov_function=sp["cov_fct"]), y
@@ -70,7 +77,10 @@ def _model_and_y(case):
 NAMES = ["rtest_gd_nesterov", "rtest_gd_no_acc", "rtest_gd_lr1", "rtest_gd_crit_pars", "rtest_fisher",
          "rtest_gd_default", "rtest_fisher_default", "synth2000_dense_gd", "synth2000_dense_fisher_matern15",
          "synth2000_vecchia_gd", "grouped_k1_gd", "grouped_k1_fisher", "grouped_k2_gd", "grouped_k2_fisher",
-         "grouped_k2_gd_no_acc_crit_pars", "combined_rtest_gd"]
+         "grouped_k2_gd_no_acc_crit_pars", "combined_rtest_gd",
+         # nelder_mead (OptimExternal -> OptimLib nm.hpp)
+         "nm_rtest_dense", "nm_rtest_dense_default", "nm_rtest_dense_crit_pars", "nm_synth2000_vecchia_matern15",
+         "nm_grouped_k2", "nm_combined_rtest", "nm_dense_probit_rtest", "nm_fitc_pois"]
 
 
 @pytest.mark.parametrize("name", NAMES)
@@ -124,6 +134,16 @@ def test_internal_optimizer_defaults_and_refusals():
     assert a.get_optim_params()["optimizer_cov"] == "gradient_descent"
     with pytest.raises(GPBoostError, match="not supported"):
         GPModel(gp_coords=X, cov_function="exponential").fit(y, params={"optimizer_cov": "adam"})
+    # default delta_rel_conv for nelder_mead is 1e-8 (test_GPModel_gaussian_process.R:187-196)
+    a = GPModel(gp_coords=X, cov_function="exponential")
+    a.fit(y, params={"optimizer_cov": "nelder_mead"})
+    b = GPModel(gp_coords=X, cov_function="exponential")
+    b.fit(y, params={"optimizer_cov": "nelder_mead", "delta_rel_conv": 1e-8})
+    np.testing.assert_array_equal(a.get_cov_pars(), b.get_cov_pars())
+    # test_GPModel_gaussian_process.R:179-186: within 0.02 of the gradient-descent estimate, nll within 0.01
+    gd = np.array([0.03784221, 0.07943467, 1.07390943, 0.25351519, 0.11451432, 0.03840236])
+    assert np.sum(np.abs(a.get_cov_pars() - gd[[0, 2, 4]])) < 0.02
+    assert abs(a.get_current_neg_log_likelihood() - 122.7771373) < 0.01
     with pytest.raises(GPBoostError, match="not supported"):
         GPModel(gp_coords=X, cov_function="exponential").fit(
             y, params={"optimizer_cov": "gradient_descent", "convergence_criterion": "abc"})

@@ -128,7 +128,7 @@ def test_fit_errors():
     X, Y = synthetic.rtest_gaussian_y(100)
     gm = GPModel(gp_coords=X, cov_function="exponential")
     with pytest.raises(GPBoostError, match="not supported"):
-        gm.fit(Y, params={"optimizer_cov": "nelder_mead"})
+        gm.fit(Y, params={"optimizer_cov": "adam"})
     gm = GPModel(gp_coords=X, cov_function="exponential")
     with pytest.raises((GPBoostError, ValueError), match="NaN or Inf"):
         gm.fit(np.where(np.arange(100) == 3, np.nan, Y))
