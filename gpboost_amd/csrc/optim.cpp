@@ -487,7 +487,8 @@ void REModelAMD::FindInitCovPar(const double* y, double* trafo) const {
     trafo[1] = 1.;         // marginal variance / nugget
     trafo[2] = InitialRangeTrafo();
   } else {
-    trafo[0] = cfg_.lik == kLikGaussian ? var / 2. : 1.;
+    // init_marg_var: var / 2 for the gaussian latent likelihood, 0.1 with nelder_mead, else 1 (re_model_template.h:4444-4451)
+    trafo[0] = cfg_.lik == kLikGaussian ? var / 2. : (isettings_.optimizer == "nelder_mead" ? 0.1 : 1.);
     trafo[1] = InitialRangeTrafo();
   }
 }
