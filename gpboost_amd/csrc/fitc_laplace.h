@@ -35,7 +35,7 @@ class FitcLaplace : public LatentSolverBase {
   void SetY(const double* y) override;
   void SetOffset(const double* off) override;
   void GetMode(double* mode) override;
-  // trafo = (sigma1^2, phi); aux: the shape of likelihood 'gamma' (fixed here: want_aux_grad is refused).
+  // trafo = (sigma1^2, phi); aux: the shape of likelihood 'gamma' (want_aux_grad: its gradient appended to grad).
   // grad = [d/dlog sigma1^2, d/dlog phi] of the negative approximate marginal log-likelihood;
   // grad_f (nullable, host n): the gradient wrt the fixed effects F (booster).
   LatentResult Eval(int cov_type, int lik, const double* trafo, double aux, const IterativeConfig& cfg,
@@ -70,7 +70,8 @@ class FitcLaplace : public LatentSolverBase {
   double cached_obj_ = 0.;     // -1/2 a^T mode + log p(y | mode + F) at the current mode
   double aux_ = 1.;            // the likelihood's auxiliary parameter (gamma: shape)
   DevBuf<double> y_, off_, mode_, a_, mode_prev_, a_prev_, mode_upd_, a_upd_, d1_, w_, wdw_, dw_, rhs_, sig_, c_, z_;
-  DevBuf<double> sgv_, sgr_, dmll_;
+  DevBuf<double> sgv_, sgr_, dmll_, sdiag_, auxrec_;
+  double sum_log_y_ = 0.;
   DevBuf<double> mv_;          // m-vectors: 18 x ldm (fitc_laplace.hip kMv)
   DevBuf<double> part_, red_;  // partials and reduced scalars
   double* h_red_ = nullptr;    // pinned

@@ -326,7 +326,7 @@ __global__ void __launch_bounds__(kT) fl_grad_p1_kernel(
     const double* __restrict__ w, const double* __restrict__ DW, const double* __restrict__ dpwi,
     const double* __restrict__ mode, const double* __restrict__ off, const double* __restrict__ y,
     double* __restrict__ sgv,
-    double* __restrict__ sgr, double* __restrict__ dmll, double* __restrict__ part) {
+    double* __restrict__ sgr, double* __restrict__ dmll, double* __restrict__ sdiag, double* __restrict__ part) {
   __shared__ double red[4];
   const int lane = threadIdx.x & 63;
   const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -381,6 +381,7 @@ __global__ void __launch_bounds__(kT) fl_grad_p1_kernel(
       const double sw = f * dw * dw + wi_inv - dw * wi_inv;   // diag of (Sigma^-1 + W)^-1 (:5447-5449)
       const double mi = mode[i];
       dmll[i] = 0.5 * sw * lik_dinfo(lik, aux, y[i], off ? mi + off[i] : mi);
+      sdiag[i] = sw;
     }
   }
   ev = block4(ev, red);
@@ -437,6 +438,24 @@ __global__ void __launch_bounds__(kT) fl_gradf_kernel(int n, const double* __res
   out[i] = -d1[i] + (dm - s * w[i]);
 }
 
+// gamma shape gradient records [l + y e^-l, W o diag((Sigma^-1 + W)^-1), d1 o (Sigma^-1 + W)^-1 dmll] with the
+// implicit vector as in fl_gradf_kernel (likelihoods.h:5536-5540, 5560-5590)
+__global__ void __launch_bounds__(kT) fl_aux_rec_kernel(int n, const double* __restrict__ y, const double* __restrict__ off,
+                                                       const double* __restrict__ mode, const double* __restrict__ w,
+                                                       const double* __restrict__ sdiag, const double* __restrict__ d1,
+                                                       const double* __restrict__ dmll, const double* __restrict__ DW,
+                                                       const double* __restrict__ kq, double* __restrict__ rec) {
+  const int i = blockIdx.x * kT + threadIdx.x;
+  if (i >= n) return;
+  const double l = off ? mode[i] + off[i] : mode[i];
+  const double wi_inv = 1. / w[i], dm = dmll[i], dw = DW[i];
+  const double wdm = wi_inv * dm;
+  const double sv = wdm - (1. / dw) * wdm + dw * kq[i];
+  rec[3 * (size_t)i] = l + y[i] * exp(-l);
+  rec[3 * (size_t)i + 1] = w[i] * sdiag[i];
+  rec[3 * (size_t)i + 2] = d1[i] * sv;
+}
+
 __global__ void __launch_bounds__(kT) fl_mul_kernel(int n, const double* __restrict__ a, const double* __restrict__ b,
                                                    double* __restrict__ out) {
   const int i = blockIdx.x * kT + threadIdx.x;
@@ -484,8 +503,9 @@ FitcLaplace::FitcLaplace(FitcSolver* fitc, hipStream_t stream)
     : F_(fitc), s_(stream), n_(fitc->n_), m_(fitc->m_), ldm_(fitc->ldm_) {
   const int n = n_, ldm = ldm_;
   for (DevBuf<double>* b : {&y_, &off_, &mode_, &a_, &mode_prev_, &a_prev_, &mode_upd_, &a_upd_, &d1_, &w_, &wdw_, &dw_,
-                            &rhs_, &sig_, &c_, &z_, &sgv_, &sgr_, &dmll_})
+                            &rhs_, &sig_, &c_, &z_, &sgv_, &sgr_, &dmll_, &sdiag_})
     b->alloc(n);
+  auxrec_.alloc((size_t)3 * n);
   mv_.alloc((size_t)kMv * ldm);
   HIP_CHECK(hipMemsetAsync(mv_.get(), 0, sizeof(double) * kMv * ldm, s_));
   const size_t nbg = (size_t)(n + kChunk - 1) / kChunk;
@@ -502,6 +522,8 @@ FitcLaplace::~FitcLaplace() {
 }
 
 void FitcLaplace::SetY(const double* y) {
+  sum_log_y_ = 0.;   // aux_log_normalizing_constant_ of likelihood 'gamma' (likelihoods.h:8181-8191)
+  for (int i = 0; i < n_; ++i) sum_log_y_ += y[i] > 0. ? std::log(y[i]) : 0.;
   HIP_CHECK(hipMemcpyAsync(y_.get(), y, sizeof(double) * n_, hipMemcpyHostToDevice, s_));
   HIP_CHECK(hipStreamSynchronize(s_));
   y_set_ = true;
@@ -580,10 +602,8 @@ void FitcLaplace::Woodbury(const double* s, double* logdet_dev, bool full_invers
 LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, double aux, const IterativeConfig& cfg,
                                bool want_grad, bool want_aux_grad, double* grad_f, ModeStart start) {
   if (!y_set_) Fatal("response variable y has not been set");
-  if (want_aux_grad && want_grad && lik == kLikGamma)
-    Fatal("estimating the shape of likelihood 'gamma' with gp_approx = 'fitc' is not supported by gpboost_amd (set "
-          "estimate_aux_pars = false, or use gp_approx = 'none')");
   aux_ = lik == kLikGamma ? aux : 1.;
+  const bool want_aux = want_aux_grad && want_grad && lik == kLikGamma;
   if (lik == kLikGaussian) Fatal("FitcLaplace: the Gaussian likelihood uses the exact FITC path");
   FitcSolver& F = *F_;
   const int n = n_, m = m_, ldm = ldm_, d = F.d_;
@@ -745,7 +765,7 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
       hipLaunchKernelGGL((fl_grad_p1_kernel<decltype(c)::value>), dim3(nb4), dim3(kT), 0, s_, F.d_X_, F.dZ_.get(), n, m, d,
                          ldm, lik, aux_, var, phi, delta_j, F.Kmn_.get(), F.A_.get(), F.Kd_.get(), F.V_.get(), b, u1, u2v, u3v,
                          u2r, u3r, a_.get(), d1_.get(), w_.get(), dw_.get(), wdw_.get(), mode_.get(), off, y_.get(), sgv_.get(),
-                         sgr_.get(), dmll_.get(), part1);
+                         sgr_.get(), dmll_.get(), sdiag_.get(), part1);
     });
     HIP_CHECK(hipGetLastError());
     launch_sum_blocks(part1, nb4, 2, red + 18, s_);
@@ -761,7 +781,7 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
                        sgr_.get(), w_.get(), wdw_.get(), dmll_.get(), part1);
     HIP_CHECK(hipGetLastError());
     launch_sum_blocks(part1, nb4, 2, red + 20, s_);
-    if (grad_f != nullptr) {
+    if (grad_f != nullptr || want_aux) {   // kq = K^T M^-1 K (DW o dmll) for (Sigma^-1 + W)^-1 dmll
       double* q = mv + 16 * (size_t)ldm;
       double* q2 = mv + 17 * (size_t)ldm;
       hipLaunchKernelGGL(fl_mul_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, dw_.get(), dmll_.get(), z_.get());
@@ -770,6 +790,14 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
       fitc_chol_solve(s_, F.Wi_.get(), F.WiT_.get(), q, m, ldm, mv + 4 * (size_t)ldm, q2);
       hipLaunchKernelGGL(fl_coldot_kernel, dim3(nb4), dim3(kT), 0, s_, F.Kmn_.get(), q2, nullptr, n, m, ldm, c_.get(),
                          nullptr);
+    }
+    if (want_aux) {
+      hipLaunchKernelGGL(fl_aux_rec_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, y_.get(), off, mode_.get(), w_.get(),
+                         sdiag_.get(), d1_.get(), dmll_.get(), dw_.get(), c_.get(), auxrec_.get());
+      HIP_CHECK(hipGetLastError());
+      launch_sum_blocks(auxrec_.get(), n, 3, red + 24, s_);
+    }
+    if (grad_f != nullptr) {
       hipLaunchKernelGGL(fl_gradf_kernel, dim3(nb_thread(n)), dim3(kT), 0, s_, n, d1_.get(), dmll_.get(), w_.get(),
                          dw_.get(), c_.get(), z_.get());
       HIP_CHECK(hipGetLastError());
@@ -781,6 +809,13 @@ LatentResult FitcLaplace::Eval(int cov_type, int lik, const double* trafo, doubl
     const double* ex = h_red_ + 18;  // explicit per-observation sums (var, range)
     const double* im = h_red_ + 20;  // implicit sums
     res.grad = {ex[0] + 0.5 * t[4] + 0.5 * t[1] - 0.5 * t[0] + im[0], ex[1] + 0.5 * t[5] + 0.5 * t[3] - 0.5 * t[2] + im[1]};
+    if (want_aux) {   // gamma shape on the log scale (likelihoods.h:10514-10524 + the two trace terms)
+      HIP_CHECK(hipMemcpyAsync(h_red_ + 24, red + 24, 3 * sizeof(double), hipMemcpyDeviceToHost, s_));
+      HIP_CHECK(hipStreamSynchronize(s_));
+      const double a = aux_;
+      const double neg = a * (h_red_[24] - n * (std::log(a) + 1. - digamma_asa103(a)) - sum_log_y_);
+      res.grad.push_back(neg + 0.5 * h_red_[25] + h_red_[26]);
+    }
   }
   HIP_CHECK(hipEventRecord(e1, s_));
   HIP_CHECK(hipEventSynchronize(e1));

@@ -9,6 +9,7 @@
 #include <map>
 #include <cstring>
 
+#include "kernels.h"
 #include "slq_host.h"
 
 namespace gpb_amd {
@@ -407,6 +408,8 @@ void LatentVecchia::SetY(const double* y_vo) {
   }
   std::vector<double> yp(n_);
   for (int p = 0; p < n_; ++p) yp[p] = y_vo[vo_[p]];
+  sum_log_y_ = 0.;   // likelihood 'gamma': aux_log_normalizing_constant_ (likelihoods.h:8181-8191)
+  for (int p = 0; p < n_; ++p) sum_log_y_ += yp[p] > 0. ? std::log(yp[p]) : 0.;
   HIP_CHECK(hipMemcpyAsync(d_y_.get(), yp.data(), sizeof(double) * n_, hipMemcpyHostToDevice, s_));
   HIP_CHECK(hipStreamSynchronize(s_));
   y_set_ = true;
@@ -817,9 +820,9 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
   if (!y_set_) Fatal("response variable y has not been set");
   if (!(trafo[0] > 0. && trafo[1] > 0.)) Fatal("covariance parameters must be > 0");
   if (lik == kLikGaussian && !(aux > 0.)) Fatal("the error variance (aux_pars) must be > 0");
-  if (lik == kLikGamma && want_grad && want_aux_grad)
-    Fatal("estimating the shape of likelihood 'gamma' with gp_approx = 'vecchia' is not supported by gpboost_amd (set "
-          "estimate_aux_pars = false, or use gp_approx = 'none')");
+  if (lik == kLikGamma && want_grad && want_aux_grad && has_obs_)
+    Fatal("estimating the shape of likelihood 'gamma' with gp_approx = 'vecchia' and repeated coordinates is not "
+          "supported by gpboost_amd (set estimate_aux_pars = false)");
   const int n = n_;
   const bool gauss = lik == kLikGaussian;
   const int t = cfg.num_rand_vec_trace;
@@ -1139,6 +1142,18 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
       HIP_CHECK(hipMemcpyAsync(gp.data(), d_gradf_.get(), sizeof(double) * n, hipMemcpyDeviceToHost, s_));
       HIP_CHECK(hipStreamSynchronize(s_));
       for (int p = 0; p < n; ++p) grad_f_vo[vo_[p]] = gp[p];
+    }
+    // gamma shape on the log scale (:5139-5202, 10508-10524, 10856-10869)
+    if (lik == kLikGamma && want_aux_grad) {
+      DevBuf<double> rec((size_t)3 * n), red(3);
+      launch_gamma_aux_rec(n, aux, d_y_.get(), has_off_ ? d_off_.get() : nullptr, d_mode_.get(), d_W_.get(),
+                           d_dmll_.get(), d_d1_.get(), d_vS_.get(), rec.get(), s_);
+      launch_sum_blocks(rec.get(), n, 3, red.get(), s_);
+      double h[3];
+      HIP_CHECK(hipMemcpyAsync(h, red.get(), sizeof(h), hipMemcpyDeviceToHost, s_));
+      HIP_CHECK(hipStreamSynchronize(s_));
+      const double neg = aux * (h[0] - n * (std::log(aux) + 1. - digamma_asa103(aux)) - sum_log_y_);
+      res.grad.push_back(neg + 0.5 * h[1] + h[2]);
     }
     // gaussian error variance on the log scale (:5166-5200, 10586-10597, 12520-12546)
     if (gauss && want_aux_grad) {

@@ -234,6 +234,7 @@ class LatentVecchia : public LatentSolverBase {
   int dense_rows_ = 0, head_rows_ = 0;   // VADU plan split (VaduPrecond)
   std::unique_ptr<VaduPrecond> pre_;
   DevBuf<double> d_y_, d_Bv_, d_dBv_, d_Dinv_, d_dD_, d_W_, d_dw_, d_sdw_, d_d1_;
+  double sum_log_y_ = 0.;   // likelihood 'gamma
   DevBuf<double> d_mode_, d_mode_upd_, d_mode_new_, d_rhs_, d_dir_, d_Adir_, d_vS_, d_dmll_;
   DevBuf<double> d_mode_prev_;   // mode_previous_value_ (kWarm evaluations)
   bool mode_prev_valid_ = false;

@@ -424,6 +424,10 @@ void launch_mode_deriv(const ModeDerivArgs& a, hipStream_t s);
 // nullable: the likelihood's information does not depend on the mode -> out = -d1).
 void launch_grad_f(int n, const double* d1, const double* dmll, const double* W, const double* vS, double* out,
                    hipStream_t s);
+// likelihood 'gamma': per-observation records [l + y e^-l, W diag((Sigma^-1 + W)^-1), d1 (Sigma^-1 + W)^-1 dmll] of
+// the shape gradient (n x 3; no duplicate locations)
+void launch_gamma_aux_rec(int n, double aux, const double* y, const double* off, const double* loc, const double* W,
+                          const double* dmll, const double* d1, const double* vS, double* rec, hipStream_t s);
 
 // ---- latent predictions (latent_pred.hip)
 // out (n x t row-major) ~ N(0, 1): counter-based, a function of (seed, stream, column c0 + c, row)

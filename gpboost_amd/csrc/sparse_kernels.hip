@@ -1658,6 +1658,28 @@ void launch_grad_cols(const GradColsArgs& a, double* partials, double* out, hipS
   HIP_CHECK(hipGetLastError());
 }
 
+// gamma shape gradient records (likelihoods.h:5139-5202 with SigmaI_plus_W_inv_diag = d_log_det / dinfo,
+// :5126-5127, d_log_det = 2 d_mll_d_mode): [l + y e^-l, W (2 dmll / dinfo), d1 vS]
+__global__ void gamma_aux_rec_kernel(int n, double aux, const double* __restrict__ y, const double* __restrict__ off,
+                                     const double* __restrict__ loc, const double* __restrict__ W,
+                                     const double* __restrict__ dmll, const double* __restrict__ d1,
+                                     const double* __restrict__ vS, double* __restrict__ rec) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double l = off ? loc[i] + off[i] : loc[i];
+  const double e = y[i] * exp(-l);
+  rec[3 * (size_t)i] = l + e;
+  rec[3 * (size_t)i + 1] = W[i] * ((2. * dmll[i]) / (-aux * e));
+  rec[3 * (size_t)i + 2] = d1[i] * vS[i];
+}
+
+void launch_gamma_aux_rec(int n, double aux, const double* y, const double* off, const double* loc, const double* W,
+                          const double* dmll, const double* d1, const double* vS, double* rec, hipStream_t s) {
+  hipLaunchKernelGGL(gamma_aux_rec_kernel, dim3(grid_x(n, kBT)), dim3(kBT), 0, s, n, aux, y, off, loc, W, dmll, d1, vS,
+                     rec);
+  HIP_CHECK(hipGetLastError());
+}
+
 void launch_grad_f(int n, const double* d1, const double* dmll, const double* W, const double* vS, double* out,
                    hipStream_t s) {
   hipLaunchKernelGGL(grad_f_kernel, dim3(grid_x(n, kBT)), dim3(kBT), 0, s, n, d1, dmll, W, vS, out);

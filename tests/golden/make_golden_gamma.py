@@ -50,7 +50,9 @@ def eval_case(kind, n, cp, aux, estimate_aux, **sp):
 def fit_case(kind, n, estimate_aux, init=None, aux=None, **sp):
     X, y = data(kind, n)
     spec = dict(likelihood="gamma", cov_fct=sp.get("cov_fct", "exponential"), shape=str(sp.get("shape", 0.5)),
-                gp_approx="none")
+                gp_approx=sp.get("gp_approx", "none"))
+    if "num_ind_points" in sp:
+        spec["num_ind_points"] = sp["num_ind_points"]
     extra = dict(estimate_aux=str(int(estimate_aux)))
     if init is not None:
         extra["init_cov_pars"] = fmt_pars(init)
@@ -96,8 +98,14 @@ def main():
                                                     shape=1.5),
         "ev_bench_dense_exp_shape07": eval_case("bench_gamma", 600, (1.1, 0.1), 0.7, True),
         "ev_bench_fitc": eval_case("bench_gamma", 1500, (0.7, 0.15), 2.0, False, gp_approx="fitc", num_ind_points=60),
+        "ev_bench_fitc_shape_grad": eval_case("bench_gamma", 1500, (0.7, 0.15), 2.0, True, gp_approx="fitc",
+                                              num_ind_points=60),
+        "fit_bench_fitc_shape": fit_case("bench_gamma", 1000, True, gp_approx="fitc", num_ind_points=50),
         "ev_bench_vecchia_tight": eval_case("bench_gamma", 2000, (0.7, 0.15), 2.0, False, gp_approx="vecchia",
                                             mim="iterative", num_neighbors=20, ordering="random", cg_delta_conv=1e-10),
+        "ev_bench_vecchia_tight_shape_grad": eval_case("bench_gamma", 2000, (0.7, 0.15), 2.0, True, gp_approx="vecchia",
+                                                       mim="iterative", num_neighbors=20, ordering="random",
+                                                       cg_delta_conv=1e-10),
         # test_GPModel_non_Gaussian_data.R:2605-2614: lbfgs, shape fixed at 1, init (1, mean(dist) / 3)
         "fit_rtest_fixed_shape": fit_case("rtest_gamma", 100, False, init=(1.0, mean_dist / 3), aux=1.0),
         "fit_bench_shape": fit_case("bench_gamma", 500, True),
