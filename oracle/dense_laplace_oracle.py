@@ -21,11 +21,36 @@ from scipy.special import gammaln
 from oracle.fitc_laplace_oracle import _dist, _lik, cov_dcov
 
 
+def _lik_any(lik, y, l, aux):
+    """_lik plus likelihood 'gamma' with shape aux (likelihoods.h:8740, 9234, 9908, 10228)."""
+    if lik != "gamma":
+        return _lik(lik, y, l)
+    e = y * np.exp(-l)
+    return float(np.sum(-aux * (l + e))), aux * (e - 1.), aux * e, -aux * e
+
+
+def _digamma(x):
+    """AS 103 (the reference's GPBoost::digamma, DF_utils.cpp:82-123)."""
+    if x <= 1e-6:
+        return -0.57721566490153286060 - 1. / x + 1.6449340668482264365 * x
+    v, x2 = 0., x
+    while x2 < 8.5:
+        v -= 1. / x2
+        x2 += 1.
+    r = 1. / x2
+    v += np.log(x2) - 0.5 * r
+    r *= r
+    return v - r * (1. / 12 - r * (1. / 120 - r * (1. / 252 - r * (1. / 240 - r * (1. / 132)))))
+
+
 class DenseLaplaceOracle:
-    def __init__(self, X, y, cov_type, var, phi, likelihood, fixed_effects=None, delta=1e-8):
+    def __init__(self, X, y, cov_type, var, phi, likelihood, fixed_effects=None, delta=1e-8, aux=1.):
         self.X, self.y = np.asarray(X, float), np.asarray(y, float)
-        self.lik, self.ct, self.var, self.phi, self.delta = likelihood, cov_type, var, phi, delta
+        self.lik, self.ct, self.var, self.phi, self.delta, self.aux = likelihood, cov_type, var, phi, delta, aux
         self.const = -float(gammaln(self.y + 1.).sum()) if likelihood == "poisson" else 0.
+        if likelihood == "gamma" and abs(aux - 1.) >= 1e-10 * max(1., aux):   # :8431-8449
+            n = len(self.y)
+            self.const = (aux - 1.) * float(np.log(self.y).sum()) + n * (aux * np.log(aux) - gammaln(aux))
         self.F = np.zeros(len(self.y)) if fixed_effects is None else np.asarray(fixed_effects, float)
         D = _dist(self.X, self.X)
         self.S, self.dS = cov_dcov(D, var, phi, cov_type)
@@ -34,14 +59,14 @@ class DenseLaplaceOracle:
         self._mode()
 
     def _obj(self, mode, a):
-        return -0.5 * float(a @ mode) + _lik(self.lik, self.y, mode + self.F)[0] + self.const
+        return -0.5 * float(a @ mode) + _lik_any(self.lik, self.y, mode + self.F, self.aux)[0] + self.const
 
     def _mode(self):
         n = len(self.y)
         mode, a = np.zeros(n), np.zeros(n)
         obj = self._obj(mode, a)
         for it in range(1000):
-            _, d1, w, _ = _lik(self.lik, self.y, mode + self.F)
+            _, d1, w, _ = _lik_any(self.lik, self.y, mode + self.F, self.aux)
             ws = np.sqrt(w)
             B = np.eye(n) + ws[:, None] * self.S * ws[None, :]
             L = np.linalg.cholesky(B)
@@ -67,7 +92,7 @@ class DenseLaplaceOracle:
             if conv:
                 break
         self.mode, self.a, self.obj = mode, a, obj
-        _, self.d1, self.w, self.dw = _lik(self.lik, self.y, mode + self.F)
+        _, self.d1, self.w, self.dw = _lik_any(self.lik, self.y, mode + self.F, self.aux)
         self.ws = np.sqrt(self.w)
         B = np.eye(n) + self.ws[:, None] * self.S * self.ws[None, :]
         self.L = np.linalg.cholesky(B)
@@ -83,7 +108,13 @@ class DenseLaplaceOracle:
         for dS in (self.S, self.dS):
             u = dS @ self.d1
             g.append(-0.5 * float(self.a @ dS @ self.a) + 0.5 * float(np.sum(R * dS)) + float(dmll @ (u - self.S @ (R @ u))))
-        gf = -self.d1 + dmll - self.w * (self.S @ dmll - C.T @ (C @ dmll))
+        v = self.S @ dmll - C.T @ (C @ dmll)
+        gf = -self.d1 + dmll - self.w * v
+        if self.lik == "gamma":   # shape on the log scale (:3379-3411, 10508-10524, 10856-10869)
+            a, l, n = self.aux, self.mode + self.F, len(self.y)
+            neg = a * (float(np.sum(l + self.y * np.exp(-l))) - n * (np.log(a) + 1. - _digamma(a))
+                       - float(np.log(self.y).sum()))
+            g.append(neg + 0.5 * float(self.w @ diag) + float(self.d1 @ v))
         return np.array(g), gf
 
     def predict(self, Xp, want_cov=False):

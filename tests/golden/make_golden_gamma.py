@@ -47,7 +47,7 @@ def eval_case(kind, n, cp, aux, estimate_aux, **sp):
                 extra=extra, nll=r["nll"], grad=r["grad"])
 
 
-def fit_case(kind, n, estimate_aux, init=None, aux=None, **sp):
+def fit_case(kind, n, estimate_aux, init=None, aux=None, optimizer=None, **sp):
     X, y = data(kind, n)
     spec = dict(likelihood="gamma", cov_fct=sp.get("cov_fct", "exponential"), shape=str(sp.get("shape", 0.5)),
                 gp_approx=sp.get("gp_approx", "none"))
@@ -58,6 +58,8 @@ def fit_case(kind, n, estimate_aux, init=None, aux=None, **sp):
         extra["init_cov_pars"] = fmt_pars(init)
     if aux is not None:
         extra["aux_pars"] = repr(float(aux))
+    if optimizer is not None:
+        extra["optimizer"] = optimizer
     r = run_ref(X, y, mode="fit", **spec, **extra)
     out = dict(kind="fit", data=kind, n=n, estimate_aux=estimate_aux, spec=spec, extra=extra,
                **{k: r[k] for k in ("init_cov_pars", "cov_pars", "nll", "num_it")})
@@ -109,12 +111,18 @@ def main():
         # test_GPModel_non_Gaussian_data.R:2605-2614: lbfgs, shape fixed at 1, init (1, mean(dist) / 3)
         "fit_rtest_fixed_shape": fit_case("rtest_gamma", 100, False, init=(1.0, mean_dist / 3), aux=1.0),
         "fit_bench_shape": fit_case("bench_gamma", 500, True),
+        # :2626-2635: nelder_mead with the shape estimated, init (1, mean(dist) / 3), shape 1
+        "fit_rtest_nm_shape": fit_case("rtest_gamma", 100, True, init=(1.0, mean_dist / 3), aux=1.0,
+                                       optimizer="nelder_mead"),
         "pred_rtest_cov": pred_case("rtest_gamma", 100, 3, (1.0, 0.3), 1.0, cov=True),
         "pred_bench_resp": pred_case("bench_gamma", 600, 100, (0.7, 0.15), 2.0, response=True),
     }
     cases["ev_rtest_dense"]["r_expected_nll"] = 154.4561783                                  # :2624-2625
     cases["fit_rtest_fixed_shape"]["r_expected_cov_pars"] = [1.0649277352, 0.2738906496]     # :2613
     cases["fit_rtest_fixed_shape"]["r_expected_num_it"] = 5                                  # :2614
+    cases["fit_rtest_nm_shape"]["r_expected_cov_pars"] = [1.0445949478, 0.2971884204]        # :2631-2635
+    cases["fit_rtest_nm_shape"]["r_expected_aux_pars"] = [0.9400943304]
+    cases["fit_rtest_nm_shape"]["r_expected_num_it"] = 115
     for k, v in cases.items():
         print(k, v.get("nll"), v.get("grad", v.get("cov_pars")), v.get("num_it"), v.get("aux_pars"), file=sys.stderr)
     with open(OUT, "w") as f:

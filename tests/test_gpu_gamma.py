@@ -73,6 +73,8 @@ def test_gamma_fit_matches_reference(name):
     X, y = lik_case_data(case)
     gm = _model(X, case)
     params = {}
+    if "optimizer" in case["extra"]:
+        params["optimizer_cov"] = case["extra"]["optimizer"]
     if "init_cov_pars" in case["extra"]:
         params["init_cov_pars"] = np.array([float(v) for v in case["extra"]["init_cov_pars"].split(",")])
     gm.fit(y, params=params)
@@ -84,6 +86,8 @@ def test_gamma_fit_matches_reference(name):
     if "r_expected_cov_pars" in case:
         assert np.sum(np.abs(gm.get_cov_pars() - case["r_expected_cov_pars"])) < 1e-5
         assert gm.get_num_optim_iter() == case["r_expected_num_it"]
+    if "r_expected_aux_pars" in case:
+        assert np.sum(np.abs(gm.get_aux_pars()[0] - case["r_expected_aux_pars"])) < 1e-5
 
 
 @pytest.mark.parametrize("name", [k for k in GOLDEN if GOLDEN[k]["kind"] == "pred"])

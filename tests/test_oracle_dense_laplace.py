@@ -15,6 +15,8 @@ from oracle.dense_laplace_oracle import DenseLaplaceOracle
 HERE = os.path.dirname(os.path.abspath(__file__))
 with open(os.path.join(HERE, "golden", "golden_dense_laplace.json")) as _f:
     GOLDEN = json.load(_f)
+with open(os.path.join(HERE, "golden", "golden_gamma.json")) as _f:
+    GAMMA = json.load(_f)
 
 CT = {("exponential", "0.5"): 0, ("matern", "1.5"): 1, ("matern", "2.5"): 2, ("gaussian", "0.0"): 3}
 
@@ -62,3 +64,21 @@ def test_oracle_dense_laplace_predict(name):
     np.testing.assert_allclose(mean, case["mean"], rtol=1e-8, atol=1e-10)
     ref = np.asarray(case["cov"]).reshape(npred, npred) if want_cov else np.asarray(case["var"])
     np.testing.assert_allclose(v, ref, rtol=1e-8, atol=1e-10)
+
+
+@pytest.mark.parametrize("name", [k for k in GAMMA if GAMMA[k]["kind"] == "eval" and GAMMA[k]["spec"]["gp_approx"] == "none"])
+def test_oracle_dense_laplace_gamma(name):
+    """likelihood 'gamma' incl. the shape gradient (golden_gamma.json, make_golden_gamma.py); the R test's nll."""
+    case = GAMMA[name]
+    X, y = lik_case_data(case)
+    sp = case["spec"]
+    ct = CT[(sp["cov_fct"], sp["shape"])]
+    var, rho = case["cov_pars"]
+    phi = {0: 1. / rho, 1: np.sqrt(3.) / rho, 2: np.sqrt(5.) / rho, 3: 1. / rho ** 2}[ct]
+    o = DenseLaplaceOracle(X, y, ct, var, phi, "gamma", aux=case["aux"])
+    assert abs(o.nll - case["nll"]) <= 1e-10 * abs(case["nll"])
+    g, _ = o.grad()
+    ref = np.asarray(case["grad"])
+    np.testing.assert_allclose(g[: len(ref)], ref, rtol=1e-8)
+    if "r_expected_nll" in case:
+        assert abs(o.nll - case["r_expected_nll"]) < 1e-5
