@@ -216,7 +216,7 @@ class GPModel:
                        "lr_cov": -1., "m_lbfgs": -1, "trace": False,
                        "convergence_criterion": "relative_change_in_log_likelihood",
                        "acc_rate_cov": 0.5, "use_nesterov_acc": True, "nesterov_schedule_version": 0,
-                       "momentum_offset": 2}
+                       "momentum_offset": 2, "estimate_cov_par_index": None}
 
     def __del__(self):
         try:
@@ -271,6 +271,10 @@ class GPModel:
         aux = p["init_aux_pars"]
         init = p["init_cov_pars"]
         no_index = np.array([-1], dtype=np.int32)
+        if p["estimate_cov_par_index"] is not None:   # reference basic.py: int32 array of num_cov_pars entries
+            no_index = np.asarray(p["estimate_cov_par_index"], dtype=np.int32).reshape(-1)
+            if no_index.shape[0] != self.num_cov_pars:
+                raise ValueError("params['estimate_cov_par_index'] does not contain the correct number of parameters")
         _safe_call(lib().GPB_SetOptimConfig(
             self.handle, _dp(init) if init is not None else None, float(p["lr_cov"]), float(p["acc_rate_cov"]),
             int(p["maxit"]), float(p["delta_rel_conv"]), bool(p["use_nesterov_acc"]),

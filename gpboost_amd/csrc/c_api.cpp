@@ -287,10 +287,8 @@ int GPB_SetOptimConfig(REModelHandle handle, double* init_cov_pars, double lr, d
   if (delta_conv_mode_finding > 0.) m->iter.delta_conv_mode_finding = delta_conv_mode_finding;   // :820-822
   if (init_aux_pars != nullptr) m->SetInitAuxPars(init_aux_pars);
   m->estimate_aux_pars = estimate_aux_pars;   // :803
-  if (estimate_cov_par_index != nullptr && estimate_cov_par_index[0] >= 0) {
-    for (int k = 0; k < m->num_cov_pars(); ++k)
-      if (estimate_cov_par_index[k] <= 0) gpb_amd::Fatal("estimate_cov_par_index: fixing covariance parameters is not supported by gpboost_amd");
-  }
+  if (estimate_cov_par_index != nullptr && estimate_cov_par_index[0] >= 0)   // SetOptimConfig :806-816
+    m->SetEstimateCovParIndex(std::vector<int>(estimate_cov_par_index, estimate_cov_par_index + m->num_cov_pars()));
   API_END();
 }
 

@@ -547,23 +547,43 @@ void REModelAMD::SetOptimSettings(const double* init_cov_pars, double lr, int ma
 namespace {
 
 // EvalLLforLBFGSpp for the Gaussian likelihood with the nugget profiled out
-// (optim_utils.h:269-313, 333-348): x = log(sigma1^2 / sigma^2, phi).
+// (optim_utils.h:269-313, 333-348): x = log(sigma1^2 / sigma^2, phi). With estimate_cov_par_index (idx, original
+// order [nugget, sigma1^2, range]): fixed parameters get a zero gradient (CalcGradPars skips them,
+// re_model_template.h:1773-1816); a fixed nugget is not profiled (ProfileOutSigma2 :2407-2412), a fixed marginal
+// variance stays constant on the original scale through the last profiled sigma^2 (MaybeKeepVarianceConstant
+// :7104-7121: tau = sigma1^2_init / sigma^2).
 class GaussianProfiledObjective : public LbfgsObjective {
  public:
-  GaussianProfiledObjective(REModelAMD* m) : m_(m) {}
+  GaussianProfiledObjective(REModelAMD* m, std::vector<int> idx = {}, double sigma2_init = 1., double var_init = 1.)
+      : m_(m), idx_(std::move(idx)), sigma2_(sigma2_init), sigma2_lag1_(sigma2_init), var_orig_(var_init) {}
   double Eval(const std::vector<double>& x, std::vector<double>& grad, bool eval_ll, bool calc_grad,
               bool hint_grad) override {
     if (eval_ll || !(has_grad_ && x == x_)) {
-      const double trafo[3] = {1., std::exp(x[0]), std::exp(x[1])};
-      EvalResult r = m_->EvalTrafo(trafo, calc_grad || hint_grad, 1);
+      const bool fix_nug = !idx_.empty() && idx_[0] <= 0;
+      const bool fix_var = !idx_.empty() && idx_[1] <= 0;
+      double trafo[3] = {fix_nug ? sigma2_ : 1., std::exp(x[0]), std::exp(x[1])};
+      if (fix_var && !fix_nug) trafo[1] = var_orig_ / sigma2_;
+      EvalResult r = m_->EvalTrafo(trafo, calc_grad || hint_grad, fix_nug ? 0 : 1);
       x_ = x;
       nll_ = r.nll;
-      sigma2_ = r.sigma2;
+      if (!fix_nug) sigma2_ = r.sigma2;
       has_grad_ = calc_grad || hint_grad;
-      if (has_grad_) grad_ = r.grad;
+      if (has_grad_) {
+        grad_ = r.grad;
+        if (fix_nug) grad_.erase(grad_.begin());   // include_error_var = false
+        if (!idx_.empty())
+          for (int k = 0; k < 2; ++k)
+            if (idx_[k + 1] <= 0) grad_[k] = 0.;
+      }
     }
     if (calc_grad) grad = grad_;
     return nll_;
+  }
+  // sigma1^2 / sigma^2 actually used at x (the fixed-variance form rescales it)
+  double tau_at(const std::vector<double>& x) const {
+    const bool fix_nug = !idx_.empty() && idx_[0] <= 0;
+    if (!idx_.empty() && idx_[1] <= 0 && !fix_nug) return var_orig_ / sigma2_;
+    return std::exp(x[0]);
   }
   void SetLag1ProfiledOutVariables() override { sigma2_lag1_ = sigma2_; }
   void ResetProfiledOutVariablesToLag1() override { sigma2_ = sigma2_lag1_; }
@@ -571,8 +591,9 @@ class GaussianProfiledObjective : public LbfgsObjective {
 
  private:
   REModelAMD* m_;
+  std::vector<int> idx_;
   std::vector<double> x_, grad_;
-  double nll_ = 0., sigma2_ = 1., sigma2_lag1_ = 1.;
+  double nll_ = 0., sigma2_ = 1., sigma2_lag1_ = 1., var_orig_ = 1.;
   bool has_grad_ = false;
 };
 
@@ -759,6 +780,9 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects, bool 
   if (!reuse_m_bfgs) m_bfgs_ = InverseHessian();   // a fresh solver state (LBFGS.h:42-48)
   std::vector<double> x;
   double fx = 0.;
+  if (!est_idx_.empty() && (cfg_.latent || !isettings_.optimizer.empty()))
+    Fatal("estimate_cov_par_index (fixing covariance parameters) is supported by gpboost_amd for the Gaussian likelihood "
+          "with optimizer_cov = 'lbfgs' only");
   if (isettings_.optimizer == "nelder_mead") {   // OptimExternal "nelder_mead" (optim_utils.h:642-643, 680-700)
     const double tol_obj = isettings_.crit_params ? 1e-20 : isettings_.delta;
     const double tol_sol = isettings_.crit_params ? isettings_.delta : 1e-20;
@@ -803,10 +827,10 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects, bool 
     cov_pars_orig_ = {tv[0], tv[1] * tv[0], range_back(cfg_.cov_type, tv[2])};
   } else if (!cfg_.latent) {
     x = {std::log(trafo[1]), std::log(trafo[2])};
-    GaussianProfiledObjective obj(this);
+    GaussianProfiledObjective obj(this, est_idx_, trafo[0], trafo[1] * trafo[0]);
     num_it_ = lbfgs_minimize(obj, x, fx, optim_, &m_bfgs_, reuse_m_bfgs);
     const double s2 = obj.sigma2();
-    cov_pars_orig_ = {s2, std::exp(x[0]) * s2, range_back(cfg_.cov_type, std::exp(x[1]))};
+    cov_pars_orig_ = {s2, obj.tau_at(x) * s2, range_back(cfg_.cov_type, std::exp(x[1]))};
   } else {
     x = {std::log(trafo[0]), std::log(trafo[1])};
     if (with_aux) x.push_back(std::log(aux_pars_[0]));
@@ -832,6 +856,9 @@ void REModelAMD::InitializeOptimizerNames() {
 }
 
 void REModelAMD::OptimLinRegrCoefCovPar(const double* y, const double* X, int p, const double* fixed_effects) {
+  if (!est_idx_.empty() && X != nullptr && p > 0)
+    Fatal("estimate_cov_par_index (fixing covariance parameters) with linear regression covariates is not supported by "
+          "gpboost_amd");
   if (!isettings_.optimizer.empty())
     Fatal("optimizer_cov = '%s' with linear regression covariates is not supported by gpboost_amd (use 'lbfgs')",
           isettings_.optimizer.c_str());

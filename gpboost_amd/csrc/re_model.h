@@ -204,6 +204,14 @@ class REModelAMD {
   std::vector<double> FisherTrafo(const double* trafo);
   // acc_rate_cov, use_nesterov_acc, nesterov_schedule_version, momentum_offset, convergence_criterion of
   // GPB_SetOptimConfig (re_model_template.h:710-761) for the internal optimizers
+  // estimate_cov_par_index (re_model_template.h:806-816): a parameter with index <= 0 keeps its initial value.
+  // Supported for the Gaussian likelihood with "lbfgs" (zero gradient entries, MaybeKeepVarianceConstant
+  // :7104-7121, ProfileOutSigma2 :2407-2412 keeping a fixed nugget).
+  void SetEstimateCovParIndex(const std::vector<int>& idx) {
+    bool all = true;
+    for (int v : idx) all = all && v > 0;
+    est_idx_ = all ? std::vector<int>() : idx;
+  }
   void SetInternalOptimSettings(double acc_rate, bool nesterov, int schedule, int momentum_offset,
                                 const char* convergence_criterion) {
     isettings_.acc_rate = acc_rate;
@@ -309,6 +317,7 @@ class REModelAMD {
   std::unique_ptr<FitcLaplace> fitc_lap_;   // gp_approx = "fitc", non-Gaussian likelihood (Laplace)
   std::unique_ptr<DenseLaplace> dense_lap_; // gp_approx = "none", non-Gaussian likelihood (Laplace)
   double sum_log_y_ = 0.;                   // likelihood 'gamma': sum log y (its normalizing constant)
+  std::vector<int> est_idx_;                // estimate_cov_par_index (empty: all estimated)
   std::unique_ptr<VifSolver> vif_;          // gp_approx = "full_scale_vecchia" (Gaussian likelihood)
   std::unique_ptr<VecchiaFisher> vfisher_;  // gp_approx = "vecchia", Gaussian: standard deviations (lazy)
   std::mt19937 fitc_rng_;              // the model's generator after the inducing-point selection

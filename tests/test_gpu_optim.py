@@ -229,3 +229,32 @@ def test_fit_matches_reference_latent_tight(golden_fit_latent, name):
     if "aux_pars" in case:
         np.testing.assert_allclose(gm.get_aux_pars()[0], case["aux_pars"][0], rtol=1e-6)
     assert abs(gm.get_current_neg_log_likelihood() - case["nll"]) <= 1e-6 * abs(case["nll"])
+
+
+def test_fit_fixed_covariance_parameters_r_golden():
+    """estimate_cov_par_index (test_GPModel_gaussian_process.R:232-250): lbfgs with the range, then the marginal
+    variance and the range held at their initial values (init var(y)/2, var(y)/2, mean(dist)/3); estimates with
+    standard errors (column-major) and nll at the R test's TOLERANCE_STRICT 1e-5."""
+    X, Y = synthetic.rtest_gaussian_y(100)
+    D = np.sqrt(((X[:, None, :] - X[None, :, :]) ** 2).sum(-1))
+    init = np.array([np.var(Y, ddof=1) / 2, np.var(Y, ddof=1) / 2, D[np.triu_indices(100, 1)].mean() / 3])
+    for idx, nll_ref, vals in [
+        ([1, 1, 0], 123.4853915, [0.10273152252, 0.08925506562, 1.23337072589, 0.37123039633, 0.17864807736, 0.07351705425]),
+        ([1, 0, 0], 127.7832271, [0.4583440607, 0.1476785505, 0.5170731356, 0.2240355344, 0.1786480774, 0.1126220657]),
+        ([0, 1, 0], 127.9879294, [0.5170731356, 0.1687492120, 0.6088800134, 0.2602195062, 0.1786480774, 0.1112692786]),
+        ([0, 0, 0], 128.132446, None),
+    ]:
+        gm = GPModel(gp_coords=X, cov_function="exponential")
+        # params_loc = DEFAULT_OPTIM_PARAMS (lr_cov 0.1, delta_rel_conv 1e-6) with optimizer_cov "lbfgs"
+        gm.fit(Y, params={"optimizer_cov": "lbfgs", "lr_cov": 0.1, "delta_rel_conv": 1e-6, "init_cov_pars": init,
+                          "estimate_cov_par_index": idx})
+        out = gm.get_cov_pars(std_err=True)
+        if vals is not None:
+            assert np.sum(np.abs(out.T.reshape(-1) - vals)) < 1e-5, (idx, out)
+        assert abs(gm.get_current_neg_log_likelihood() - nll_ref) < 1e-5
+        for k in range(3):
+            if idx[k] == 0:
+                assert abs(out[0, k] - init[k]) < 1e-5
+    gm = GPModel(gp_coords=X, cov_function="exponential")
+    with pytest.raises(GPBoostError, match="estimate_cov_par_index"):
+        gm.fit(Y, params={"optimizer_cov": "nelder_mead", "init_cov_pars": init, "estimate_cov_par_index": [1, 1, 0]})
