@@ -632,7 +632,9 @@ class GaussianWlsObjective : public LbfgsObjective {
 // EvalLLforLBFGSpp for the latent (Laplace) models: x = log(sigma1^2, phi[, aux]).
 class LatentObjective : public LbfgsObjective {
  public:
-  LatentObjective(REModelAMD* m, bool with_aux) : m_(m), with_aux_(with_aux) {}
+  // idx: estimate_cov_par_index (empty: all estimated); fixed parameters get a zero gradient (:1773-1816)
+  LatentObjective(REModelAMD* m, bool with_aux, std::vector<int> idx = {})
+      : m_(m), with_aux_(with_aux), idx_(std::move(idx)) {}
   double Eval(const std::vector<double>& x, std::vector<double>& grad, bool eval_ll, bool calc_grad,
               bool hint_grad) override {
     if (eval_ll || !(has_grad_ && x == x_)) {
@@ -654,7 +656,11 @@ class LatentObjective : public LbfgsObjective {
       x_ = x;
       nll_ = r.nll;
       has_grad_ = calc_grad || hint_grad;
-      if (has_grad_) grad_ = r.grad;
+      if (has_grad_) {
+        grad_ = r.grad;
+        for (size_t k = 0; k < idx_.size() && k < grad_.size(); ++k)
+          if (idx_[k] <= 0) grad_[k] = 0.;
+      }
     }
     if (calc_grad) grad = grad_;
     return nll_;
@@ -663,6 +669,7 @@ class LatentObjective : public LbfgsObjective {
  private:
   REModelAMD* m_;
   bool with_aux_;
+  std::vector<int> idx_;
   std::vector<double> x_, grad_;
   double nll_ = 0.;
   bool has_grad_ = false, has_x_ = false;
@@ -780,9 +787,9 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects, bool 
   if (!reuse_m_bfgs) m_bfgs_ = InverseHessian();   // a fresh solver state (LBFGS.h:42-48)
   std::vector<double> x;
   double fx = 0.;
-  if (!est_idx_.empty() && (cfg_.latent || !isettings_.optimizer.empty()))
-    Fatal("estimate_cov_par_index (fixing covariance parameters) is supported by gpboost_amd for the Gaussian likelihood "
-          "with optimizer_cov = 'lbfgs' only");
+  if (!est_idx_.empty() && !isettings_.optimizer.empty())
+    Fatal("estimate_cov_par_index (fixing covariance parameters) is supported by gpboost_amd with optimizer_cov = "
+          "'lbfgs' only");
   if (isettings_.optimizer == "nelder_mead") {   // OptimExternal "nelder_mead" (optim_utils.h:642-643, 680-700)
     const double tol_obj = isettings_.crit_params ? 1e-20 : isettings_.delta;
     const double tol_sol = isettings_.crit_params ? isettings_.delta : 1e-20;
@@ -834,7 +841,7 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects, bool 
   } else {
     x = {std::log(trafo[0]), std::log(trafo[1])};
     if (with_aux) x.push_back(std::log(aux_pars_[0]));
-    LatentObjective obj(this, with_aux);
+    LatentObjective obj(this, with_aux, est_idx_);
     num_it_ = lbfgs_minimize(obj, x, fx, optim_, &m_bfgs_, reuse_m_bfgs);
     cov_pars_orig_ = {std::exp(x[0]), range_back(cfg_.cov_type, std::exp(x[1]))};
     if (with_aux) aux_pars_[0] = std::exp(x[2]);

@@ -123,3 +123,26 @@ def test_gamma_checks_and_refusals():
                  matrix_inversion_method="iterative")
     with pytest.raises(GPBoostError, match="estimate_aux_pars"):
         gv.fit(y)
+
+
+def test_gamma_fixed_covariance_parameters_r_test():
+    """estimate_cov_par_index with likelihood 'gamma' (test_GPModel_non_Gaussian_data.R:2646-2676): lbfgs with both
+    covariance parameters fixed at (1, mean(dist) / 3) estimates the shape alone (0.9902641, TOLERANCE_STRICT);
+    with one of them fixed the fixed one keeps its initial value (dense and FITC)."""
+    from gpboost_amd import GPModel, synthetic
+    X, y = synthetic.rtest_gamma_y(100)
+    D = np.sqrt(((X[:, None, :] - X[None, :, :]) ** 2).sum(-1))
+    init = np.array([1.0, D[np.triu_indices(100, 1)].mean() / 3])
+    gm = GPModel(gp_coords=X, cov_function="exponential", likelihood="gamma")
+    gm.fit(y, params={"optimizer_cov": "lbfgs", "init_cov_pars": init, "init_aux_pars": [1.0],
+                      "estimate_aux_pars": True, "estimate_cov_par_index": [0, 0]})
+    assert np.sum(np.abs(gm.get_cov_pars() - [1.0, 0.1786481])) < 1e-5
+    assert abs(gm.get_aux_pars()[0][0] - 0.9902641) < 1e-5
+    for approx in ("none", "fitc"):
+        for idx in ([1, 0], [0, 1]):
+            kw = dict(num_ind_points=50) if approx == "fitc" else {}
+            gm = GPModel(gp_coords=X, cov_function="exponential", likelihood="gamma", gp_approx=approx, **kw)
+            gm.fit(y, params={"optimizer_cov": "lbfgs", "init_cov_pars": init, "init_aux_pars": [2.0],
+                              "estimate_aux_pars": True, "estimate_cov_par_index": idx})
+            k = idx.index(0)
+            assert abs(gm.get_cov_pars()[k] - init[k]) < 1e-5
