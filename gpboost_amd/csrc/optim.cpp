@@ -787,7 +787,7 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects, bool 
   if (!reuse_m_bfgs) m_bfgs_ = InverseHessian();   // a fresh solver state (LBFGS.h:42-48)
   std::vector<double> x;
   double fx = 0.;
-  if (!est_idx_.empty() && !isettings_.optimizer.empty())
+  if (!est_idx_.empty() && !isettings_.optimizer.empty() && !(cfg_.latent && isettings_.optimizer == "gradient_descent"))
     Fatal("estimate_cov_par_index (fixing covariance parameters) is supported by gpboost_amd with optimizer_cov = "
           "'lbfgs' only");
   if (isettings_.optimizer == "nelder_mead") {   // OptimExternal "nelder_mead" (optim_utils.h:642-643, 680-700)
@@ -822,6 +822,92 @@ void REModelAMD::OptimCovPar(const double* y, const double* fixed_effects, bool 
       cov_pars_orig_ = {std::exp(x[0]), range_back(cfg_.cov_type, std::exp(x[1]))};
       if (with_aux) aux_pars_[0] = std::exp(x[2]);
     }
+  } else if (isettings_.optimizer == "gradient_descent" && cfg_.latent) {
+    // Laplace models: OptimLinRegrCoefCovPar's loop without profiling (re_model_template.h:1290-1549), the
+    // covariance parameters and the auxiliary parameters on the log scale with their own learning rates
+    // (lr_cov_, lr_aux_pars_; AvoidTooLargeLearningRatesCovAuxPars :7539-7560), separate Armijo conditions for
+    // both blocks (UpdateCovAuxPars :7850-7990), Nesterov momentum over all of them (ApplyMomentumStep), the
+    // Laplace mode continued across evaluations and reset to its previous value after a rejected trial.
+    const int nc = 2, na = with_aux ? 1 : 0, P = nc + na;
+    std::vector<double> pars = {trafo[0], trafo[1]};
+    if (with_aux) pars.push_back(aux_pars_[0]);
+    const double kMaxLog = std::log(100.);
+    double lr_cov = isettings_.lr < 0. ? 0.1 : isettings_.lr, lr_aux = lr_cov;   // SetInitialValueLRCov :7505-7521
+    const bool nest = isettings_.nesterov;
+    if (nest && isettings_.schedule != 0) Fatal("NesterovSchedule: version = %d is not supported ", isettings_.schedule);
+    auto sched = [&](int it, double acc) { return it < isettings_.momentum_offset ? 0. : acc; };
+    auto eval_nll = [&](const std::vector<double>& v) {
+      const double t[2] = {v[0], v[1]};
+      if (with_aux) SetAuxPars(&v[2]);
+      EvalResult r = EvalLatentTrafo(t, false, /*fatal_on_nan=*/false, LatentVecchia::ModeStart::kWarm);
+      return r.nll;
+    };
+    double nll = eval_nll(pars);
+    if (!std::isfinite(nll)) Fatal("NaN or Inf occurred in initial approximate negative marginal log-likelihood");
+    std::vector<double> after = pars, after_lag1 = pars;
+    num_it_ = isettings_.max_iter;
+    for (int it = 0; it < isettings_.max_iter; ++it) {
+      const double nll_lag1 = nll;
+      const std::vector<double> pars_lag1 = pars;
+      const double t[2] = {pars[0], pars[1]};
+      EvalResult gr = EvalLatentTrafo(t, true, false, LatentVecchia::ModeStart::kKeep);   // CalcGradPars at the mode
+      std::vector<double> g = gr.grad;
+      if ((int)g.size() < P) Fatal("internal error: latent gradient has %d entries", (int)g.size());
+      g.resize(P);
+      for (size_t k = 0; k < est_idx_.size() && k < (size_t)nc; ++k)
+        if (est_idx_[k] <= 0) g[k] = 0.;
+      double mc = 0., ma = 0.;
+      for (int k = 0; k < nc; ++k) mc = std::max(mc, std::fabs(g[k]));
+      for (int k = nc; k < P; ++k) ma = std::max(ma, std::fabs(g[k]));
+      if (mc > 0. && lr_cov > kMaxLog / mc) lr_cov = kMaxLog / mc;
+      if (na && ma > 0. && lr_aux > kMaxLog / ma) lr_aux = kMaxLog / ma;
+      double dd_c = 0., dd_a = 0., md_c = 0., md_a = 0.;
+      for (int k = 0; k < nc; ++k) dd_c -= g[k] * g[k];
+      for (int k = nc; k < P; ++k) dd_a -= g[k] * g[k];
+      if (nest) {
+        for (int k = 0; k < nc; ++k) md_c += g[k] * (std::log(pars[k]) - std::log(after[k]));
+        for (int k = nc; k < P; ++k) md_a += g[k] * (std::log(pars[k]) - std::log(after[k]));
+      }
+      double lc = lr_cov, la = lr_aux, acc = isettings_.acc_rate;
+      bool halving = false;
+      std::vector<double> np(P);
+      for (int ih = 0; ih < 30; ++ih) {
+        for (int k = 0; k < P; ++k) np[k] = std::exp(std::log(pars[k]) - (k < nc ? lc : la) * g[k]);
+        const double mu = nest ? sched(it, acc) : 0.;
+        if (nest) {
+          after = np;
+          for (int k = 0; k < P; ++k) np[k] = std::exp((mu + 1.) * std::log(after[k]) - mu * std::log(after_lag1[k]));
+        }
+        nll = eval_nll(np);
+        bool ok = nll <= nll_lag1 + 1e-4 * lc * dd_c + 1e-4 * mu * md_c;
+        if (na) ok = ok && nll <= nll_lag1 + 1e-4 * la * dd_a + 1e-4 * mu * md_a;
+        if (ok) break;
+        halving = true;
+        lc *= 0.5;
+        la *= 0.5;
+        acc *= 0.5;
+        ResetLatentModeToPrevious();
+      }
+      if (halving) { lr_cov = lc; lr_aux = la; }
+      if (nest) after_lag1 = after;
+      pars = np;
+      bool bad = !std::isfinite(nll);
+      for (double v : pars) bad = bad || !std::isfinite(v);
+      if (bad) Fatal("NaN or Inf occurred in covariance parameter optimization using 'gradient_descent'");
+      bool conv;
+      if (isettings_.crit_params) {
+        double dn = 0., ln = 0.;
+        for (int k = 0; k < P; ++k) { dn += (pars[k] - pars_lag1[k]) * (pars[k] - pars_lag1[k]); ln += pars_lag1[k] * pars_lag1[k]; }
+        conv = std::sqrt(dn) <= isettings_.delta * std::sqrt(ln);
+      } else {
+        conv = (nll_lag1 - nll) <= isettings_.delta * std::max(std::fabs(nll_lag1), 1.);
+      }
+      if (conv) { num_it_ = it + 1; break; }
+    }
+    fx = nll;
+    x = {std::log(pars[0]), std::log(pars[1])};
+    cov_pars_orig_ = {pars[0], range_back(cfg_.cov_type, pars[1])};
+    if (with_aux) aux_pars_[0] = pars[2];
   } else if (!isettings_.optimizer.empty()) {   // "gradient_descent" / "fisher_scoring" (re_model_template.h:1287-1549)
     if (cfg_.latent)
       Fatal("optimizer_cov = '%s' is supported by gpboost_amd for the Gaussian likelihood only (use 'lbfgs')",

@@ -146,3 +146,18 @@ def test_gamma_fixed_covariance_parameters_r_test():
                               "estimate_aux_pars": True, "estimate_cov_par_index": idx})
             k = idx.index(0)
             assert abs(gm.get_cov_pars()[k] - init[k]) < 1e-5
+
+
+def test_gamma_gradient_descent_r_test():
+    """gradient_descent (Nesterov) for a Laplace model with the shape estimated (test_GPModel_non_Gaussian_data.R:
+    2636-2645): (1.0323441289, 0.2898716638), shape 0.9413081183, 26 iterations (TOLERANCE_STRICT 1e-5)."""
+    from gpboost_amd import GPModel, synthetic
+    X, y = synthetic.rtest_gamma_y(100)
+    D = np.sqrt(((X[:, None, :] - X[None, :, :]) ** 2).sum(-1))
+    init = np.array([1.0, D[np.triu_indices(100, 1)].mean() / 3])
+    gm = GPModel(gp_coords=X, cov_function="exponential", likelihood="gamma")
+    gm.fit(y, params={"optimizer_cov": "gradient_descent", "init_cov_pars": init, "init_aux_pars": [1.0],
+                      "estimate_aux_pars": True})
+    assert np.sum(np.abs(gm.get_cov_pars() - [1.0323441289, 0.2898716638])) < 1e-5, gm.get_cov_pars()
+    assert abs(gm.get_aux_pars()[0][0] - 0.9413081183) < 1e-5, gm.get_aux_pars()
+    assert gm.get_num_optim_iter() == 26
