@@ -47,8 +47,9 @@ def rtest_gaussian_y(n: int = 100) -> tuple[np.ndarray, np.ndarray]:
     return coords, eps + xi
 
 
-def rtest_bernoulli_probit_y(n: int = 100) -> tuple[np.ndarray, np.ndarray]:
-    """R non-Gaussian test data (test_GPModel_non_Gaussian_data.R:17-81 pattern)."""
+def rtest_bernoulli_probit_y(n: int = 100, init_c: float = 0.19341) -> tuple[np.ndarray, np.ndarray]:
+    """R non-Gaussian test data (test_GPModel_non_Gaussian_data.R:17-81 pattern); init_c = 0.2341 gives the data of
+    the "Binary classification with Gaussian process model" test (:89-90)."""
     from scipy.stats import norm
 
     coords = rtest_coords(n)
@@ -59,7 +60,7 @@ def rtest_bernoulli_probit_y(n: int = 100) -> tuple[np.ndarray, np.ndarray]:
     b1 = norm.ppf(sim_rand_unif(n, 0.8))
     eps = chol @ b1
     probs = norm.cdf(eps)
-    y = (sim_rand_unif(n, 0.19341) < probs).astype(np.float64)
+    y = (sim_rand_unif(n, init_c) < probs).astype(np.float64)
     return coords, y
 
 

@@ -112,3 +112,38 @@ def test_dense_laplace_refusals_and_switch():
     gm.num_cov_pars = 2
     nll = gm.neg_log_likelihood([1.0, 0.2], y)
     assert abs(nll - GOLDEN["ev_rtest_probit"]["nll"]) <= 1e-9 * abs(nll)
+
+
+def test_dense_laplace_probit_r_test_optimizers():
+    """test_GPModel_non_Gaussian_data.R:105-165 on its own data (probit GP, gp_approx = "none", cholesky): gradient
+    descent without acceleration (parameter criterion) 40 iterations, with Nesterov (lr 0.01) 26, Nelder-Mead 6, each
+    at TOLERANCE_STRICT 1e-5; predictions of the lr-0.01 gradient-descent fit (means and covariance, 1e-5)."""
+    from gpboost_amd import GPModel, synthetic
+    X, y = synthetic.rtest_bernoulli_probit_y(100, init_c=0.2341)
+    D = np.sqrt(((X[:, None, :] - X[None, :, :]) ** 2).sum(-1))
+    init = np.array([1.0, D[np.triu_indices(100, 1)].mean() / 3])
+
+    def fit(params):
+        gm = GPModel(gp_coords=X, cov_function="exponential", likelihood="bernoulli_probit",
+                     matrix_inversion_method="cholesky")
+        gm.fit(y, params=dict(params, init_cov_pars=init))
+        return gm
+
+    gm = fit(dict(optimizer_cov="gradient_descent", lr_cov=0.1, use_nesterov_acc=False,
+                  convergence_criterion="relative_change_in_parameters"))
+    assert np.sum(np.abs(gm.get_cov_pars() - [0.9419234, 0.1866877])) < 1e-5
+    assert abs(gm.get_current_neg_log_likelihood() - 63.61263619) < 1e-5
+    assert gm.get_num_optim_iter() == 40
+    gm = fit(dict(optimizer_cov="gradient_descent", lr_cov=0.01, use_nesterov_acc=True, acc_rate_cov=0.5))
+    assert np.sum(np.abs(gm.get_cov_pars() - [0.9646422, 0.1844797])) < 1e-5
+    assert gm.get_num_optim_iter() == 26
+    gm = fit(dict(optimizer_cov="nelder_mead", delta_rel_conv=1e-6))
+    assert np.sum(np.abs(gm.get_cov_pars() - [0.9998047, 0.1855072])) < 1e-5
+    assert gm.get_num_optim_iter() == 6
+    gm = fit(dict(optimizer_cov="gradient_descent", lr_cov=0.01, use_nesterov_acc=False))
+    xp = np.array([[0.1, 0.9], [0.11, 0.91], [0.7, 0.55]])
+    pred = gm.predict(y=y, gp_coords_pred=xp, predict_cov_mat=True, predict_response=False)
+    assert np.sum(np.abs(pred["mu"] - [-0.6595663, -0.6638940, 0.4997690])) < 1e-5
+    cov = [0.6482224576, 0.5765285950, -0.0001030520, 0.5765285950, 0.6478191338, -0.0001163496, -0.0001030520,
+           -0.0001163496, 0.4435551436]
+    assert np.sum(np.abs(np.asarray(pred["cov"]).T.reshape(-1) - cov)) < 1e-5
