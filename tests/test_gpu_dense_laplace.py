@@ -147,3 +147,27 @@ def test_dense_laplace_probit_r_test_optimizers():
     cov = [0.6482224576, 0.5765285950, -0.0001030520, 0.5765285950, 0.6478191338, -0.0001163496, -0.0001030520,
            -0.0001163496, 0.4435551436]
     assert np.sum(np.abs(np.asarray(pred["cov"]).T.reshape(-1) - cov)) < 1e-5
+
+
+def test_dense_laplace_poisson_r_test():
+    """test_GPModel_non_Gaussian_data.R:2385-2410 on its own data (Poisson GP, gp_approx = "none"): gradient descent
+    with Nesterov (DEFAULT_OPTIM_PARAMS, lr 0.1) from (1, mean(dist) / 3): (1.1853922, 0.1500197) in 6 iterations
+    (1e-5); latent predictive means (1e-3) and covariance (1e-5); response means / variances (1e-3)."""
+    from gpboost_amd import GPModel, synthetic
+    X, y = synthetic.rtest_poisson_y(100)
+    D = np.sqrt(((X[:, None, :] - X[None, :, :]) ** 2).sum(-1))
+    init = np.array([1.0, D[np.triu_indices(100, 1)].mean() / 3])
+    gm = GPModel(gp_coords=X, cov_function="exponential", likelihood="poisson")
+    gm.fit(y, params=dict(optimizer_cov="gradient_descent", use_nesterov_acc=True, lr_cov=0.1, maxit=1000,
+                          acc_rate_cov=0.5, init_cov_pars=init))
+    assert np.sum(np.abs(gm.get_cov_pars() - [1.1853922, 0.1500197])) < 1e-5, gm.get_cov_pars()
+    assert gm.get_num_optim_iter() == 6
+    xp = np.array([[0.1, 0.9], [0.11, 0.91], [0.7, 0.55]])
+    pred = gm.predict(y=y, gp_coords_pred=xp, predict_cov_mat=True, predict_response=False)
+    assert np.sum(np.abs(pred["mu"] - [0.4329068, 0.4042531, 0.6833738])) < 1e-3
+    cov = [6.550626e-01, 5.553938e-01, -8.406290e-06, 5.553938e-01, 6.631295e-01, -7.658261e-06, -8.406290e-06,
+           -7.658261e-06, 4.170417e-01]
+    assert np.sum(np.abs(np.asarray(pred["cov"]).T.reshape(-1) - cov)) < 1e-5
+    pred = gm.predict(y=y, gp_coords_pred=xp, predict_var=True, predict_response=True)
+    assert np.sum(np.abs(pred["mu"] - [2.139213, 2.087188, 2.439748])) < 1e-3
+    assert np.sum(np.abs(pred["var"] - [6.373433, 6.185895, 5.519896])) < 1e-3
