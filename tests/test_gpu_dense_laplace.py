@@ -171,3 +171,31 @@ def test_dense_laplace_poisson_r_test():
     pred = gm.predict(y=y, gp_coords_pred=xp, predict_var=True, predict_response=True)
     assert np.sum(np.abs(pred["mu"] - [2.139213, 2.087188, 2.439748])) < 1e-3
     assert np.sum(np.abs(pred["var"] - [6.373433, 6.185895, 5.519896])) < 1e-3
+
+
+def test_dense_laplace_logit_r_test():
+    """test_GPModel_non_Gaussian_data.R:2298-2328 on its own data (bernoulli_logit GP, gp_approx = "none"): Nesterov
+    gradient descent (lr 0.01) from (1, mean(dist) / 3): (1.4300136, 0.1891952) in 85 iterations (1e-5); predictive
+    means (1e-5) and covariance (1e-3); response probabilities and variances (adaptive Gauss-Hermite, 1e-5); nll at
+    (0.9, 0.2) 66.299571 (1e-5)."""
+    from gpboost_amd import GPModel, synthetic
+    X, eps = synthetic._rtest_field(100)
+    y = (synthetic.sim_rand_unif(100, 0.2341) < 1. / (1. + np.exp(-eps))).astype(np.float64)
+    D = np.sqrt(((X[:, None, :] - X[None, :, :]) ** 2).sum(-1))
+    init = np.array([1.0, D[np.triu_indices(100, 1)].mean() / 3])
+    gm = GPModel(gp_coords=X, cov_function="exponential", likelihood="bernoulli_logit")
+    gm.fit(y, params=dict(optimizer_cov="gradient_descent", use_nesterov_acc=True, lr_cov=0.01, maxit=1000,
+                          acc_rate_cov=0.5, init_cov_pars=init))
+    assert np.sum(np.abs(gm.get_cov_pars() - [1.4300136, 0.1891952])) < 1e-5, gm.get_cov_pars()
+    assert gm.get_num_optim_iter() == 85
+    xp = np.array([[0.1, 0.9], [0.11, 0.91], [0.7, 0.55]])
+    pred = gm.predict(y=y, gp_coords_pred=xp, predict_cov_mat=True, predict_response=False)
+    assert np.sum(np.abs(pred["mu"] - [-0.7792960, -0.7876208, 0.5476390])) < 1e-5
+    cov = [1.024266883e+00, 9.215203622e-01, 5.561463409e-05, 9.215203622e-01, 1.022897212e+00, 2.028646043e-05,
+           5.561463409e-05, 2.028646043e-05, 7.395745025e-01]
+    assert np.sum(np.abs(np.asarray(pred["cov"]).T.reshape(-1) - cov)) < 1e-3
+    pred = gm.predict(y=y, gp_coords_pred=xp, predict_var=True, predict_response=True)
+    mu = np.array([0.3442815, 0.3426873, 0.6159933])
+    assert np.sum(np.abs(pred["mu"] - mu)) < 1e-5
+    assert np.sum(np.abs(pred["var"] - mu * (1 - mu))) < 1e-5
+    assert abs(gm.neg_log_likelihood([0.9, 0.2], y) - 66.299571) < 1e-5
