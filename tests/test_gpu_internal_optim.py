@@ -166,3 +166,26 @@ def test_internal_optimizer_defaults_and_refusals():
     gv = GPModel(gp_coords=Xb, cov_function="exponential", gp_approx="vecchia", num_neighbors=10)
     with pytest.raises(GPBoostError, match="fisher_scoring"):
         gv.fit(synthetic.bench_gaussian_y(300), params={"optimizer_cov": "fisher_scoring"})
+
+
+def test_fisher_scoring_fit_then_predict_r_test():
+    """test_GPModel_gaussian_process.R:266-290: Fisher scoring from FindInitCovPar (delta 1e-6, parameter criterion),
+    then predictive means / covariance / variances at three points (TOLERANCE_STRICT 1e-5) and the training-data
+    random effects equal to predictions at the training coordinates."""
+    X, y = synthetic.rtest_gaussian_y(100)
+    gm = GPModel(gp_coords=X, cov_function="exponential")
+    gm.fit(y, params={"optimizer_cov": "fisher_scoring", "delta_rel_conv": 1e-6, "use_nesterov_acc": False,
+                      "convergence_criterion": "relative_change_in_parameters"})
+    xp = np.array([[0.1, 0.9], [0.2, 0.4], [0.7, 0.55]])
+    pred = gm.predict(y=y, gp_coords_pred=xp, predict_cov_mat=True)
+    mu = [0.06960478, 1.61299381, 0.44053480]
+    cov = [6.218737e-01, 2.024102e-05, 2.278875e-07, 2.024102e-05, 3.535390e-01, 8.479210e-07, 2.278875e-07,
+           8.479210e-07, 4.202154e-01]
+    assert np.sum(np.abs(pred["mu"] - mu)) < 1e-5
+    assert np.sum(np.abs(np.asarray(pred["cov"]).T.reshape(-1) - cov)) < 1e-5
+    pv = gm.predict(y=y, gp_coords_pred=xp, predict_var=True)
+    assert np.sum(np.abs(pv["var"] - np.asarray(cov)[[0, 4, 8]])) < 1e-5
+    re = gm.predict_training_data_random_effects(predict_var=True)
+    pt = gm.predict(gp_coords_pred=X, predict_var=True, predict_response=False)
+    assert np.sum(np.abs(np.asarray(re)[:, 0] - pt["mu"])) < 1e-5
+    assert np.sum(np.abs(np.asarray(re)[:, 1] - pt["var"])) < 1e-5
