@@ -189,3 +189,34 @@ def test_fisher_scoring_fit_then_predict_r_test():
     pt = gm.predict(gp_coords_pred=X, predict_var=True, predict_response=False)
     assert np.sum(np.abs(np.asarray(re)[:, 0] - pt["mu"])) < 1e-5
     assert np.sum(np.abs(np.asarray(re)[:, 1] - pt["var"])) < 1e-5
+
+
+def test_gradient_descent_other_covariance_functions_r_test():
+    """test_GPModel_gaussian_process.R:344-389: Nesterov gradient descent (lr 0.1, delta 1e-6) for Matern 1.5 / 2.5
+    and the Gaussian kernel from the R test's initial values: estimates with standard errors (1e-5), iteration
+    counts 16 / 13 / 11, nll; and the default initial values with maxit = 0 (:401-421)."""
+    X, y = synthetic.rtest_gaussian_y(100)
+    D = np.sqrt(((X[:, None, :] - X[None, :, :]) ** 2).sum(-1))
+    dv = D[np.triu_indices(100, 1)]
+    v2 = np.var(y, ddof=1) / 2
+    cases = [
+        ("matern", 1.5, dv.mean() / 4.7 * np.sqrt(3), [0.22926543, 0.08486055, 0.87886348, 0.24059253, 0.10726402, 0.02672378], 16, 123.6388965),
+        ("matern", 2.5, dv.mean() / 5.9 * np.sqrt(5), [0.27251105, 0.08316755, 0.83205621, 0.23561744, 0.10536460, 0.02375078], 13, 123.9752771),
+        ("gaussian", 2.5, np.sqrt((dv.mean() / 2) ** 2 / 3), [0.33824439, 0.07955527, 0.75776861, 0.22661022, 0.14361521, 0.02589934], 11, None),
+    ]
+    for cov_fct, shape, rho0, vals, nit, nll in cases:
+        gm = GPModel(gp_coords=X, cov_function=cov_fct, cov_fct_shape=shape)
+        gm.fit(y, params={"optimizer_cov": "gradient_descent", "lr_cov": 0.1, "use_nesterov_acc": True,
+                          "acc_rate_cov": 0.5, "delta_rel_conv": 1e-6, "init_cov_pars": np.array([v2, v2, rho0])})
+        out = gm.get_cov_pars(std_err=True)
+        assert np.sum(np.abs(out.T.reshape(-1) - vals)) < 1e-5, (cov_fct, shape, out)
+        assert gm.get_num_optim_iter() == nit
+        if nll is not None:
+            assert abs(gm.get_current_neg_log_likelihood() - nll) < 1e-5
+    med = np.median(dv)
+    for cov_fct, shape, rho in [("matern", 0.5, med / 3 / 2), ("matern", 1.5, med / 4.7 * np.sqrt(3) / 2),
+                                ("matern", 2.5, med / 5.9 * np.sqrt(5) / 2)]:
+        gm = GPModel(gp_coords=X, cov_function=cov_fct, cov_fct_shape=shape)
+        gm.fit(y, params={"optimizer_cov": "gradient_descent", "maxit": 0})
+        cp = gm.get_cov_pars()
+        assert abs(cp[0] - v2) < 1e-5 and abs(cp[1] - v2) < 1e-5 and abs(cp[2] - rho) < 1e-5, (cov_fct, shape, cp)
