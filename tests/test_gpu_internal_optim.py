@@ -220,3 +220,4 @@ def test_gradient_descent_other_covariance_functions_r_test():
         gm.fit(y, params={"optimizer_cov": "gradient_descent", "maxit": 0})
         cp = gm.get_cov_pars()
         assert abs(cp[0] - v2) < 1e-5 and abs(cp[1] - v2) < 1e-5 and abs(cp[2] - rho) < 1e-5, (cov_fct, shape, cp)
+
