@@ -96,6 +96,21 @@ def rtest_poisson_y(n: int = 100) -> tuple[np.ndarray, np.ndarray]:
     return coords, poisson.ppf(sim_rand_unif(n, 0.435), np.exp(eps)).astype(np.float64)
 
 
+def rtest_multiple_y(n: int = 100) -> tuple[np.ndarray, np.ndarray]:
+    """The R tests' GP data with multiple observations per location (test_GPModel_gaussian_process.R:63-70, 645):
+    25 locations from sim_rand_unif(n*d/4, 0.1) repeated 4 times, Sigma = exp(-D / 0.1) + 1e-10 I,
+    y = chol(Sigma) qnorm(sim_rand_unif(n, 0.8)) + qnorm(sim_rand_unif(n, 0.1)) / 5."""
+    from scipy.stats import norm
+
+    m = n // 4
+    c = sim_rand_unif(m * 2, 0.1).reshape(2, m).T
+    coords = np.vstack([c, c, c, c])
+    dist = np.sqrt(((coords[:, None, :] - coords[None, :, :]) ** 2).sum(-1))
+    chol = np.linalg.cholesky(np.exp(-dist / 0.1) + np.eye(n) * 1e-10)
+    eps = chol @ norm.ppf(sim_rand_unif(n, 0.8))
+    return coords, eps + norm.ppf(sim_rand_unif(n, 0.1)) / 5.
+
+
 def rtest_gamma_y(n: int = 100, shape: float = 1.0) -> tuple[np.ndarray, np.ndarray]:
     """R non-Gaussian test data, spatial gamma case (test_GPModel_non_Gaussian_data.R:2603-2604):
     y = qgamma(sim_rand_unif(n, 0.435), scale = mu / shape, shape = shape), mu = exp(L b_1)."""

@@ -221,3 +221,39 @@ def test_gradient_descent_other_covariance_functions_r_test():
         cp = gm.get_cov_pars()
         assert abs(cp[0] - v2) < 1e-5 and abs(cp[1] - v2) < 1e-5 and abs(cp[2] - rho) < 1e-5, (cov_fct, shape, cp)
 
+
+
+def test_multiple_observations_per_location_r_test():
+    """test_GPModel_gaussian_process.R:643-696 (25 locations x 4 observations, dense): Nesterov gradient descent
+    (6 iterations), Fisher scoring (15 iterations), estimates with standard errors and nll at 1e-5, training-data random
+    effects = predictions at the training coordinates, predictions at given parameters."""
+    X, y = synthetic.rtest_multiple_y(100)
+    U = X[:25]
+    D = np.sqrt(((U[:, None, :] - U[None, :, :]) ** 2).sum(-1))
+    init = np.array([np.var(y, ddof=1) / 2, np.var(y, ddof=1) / 2, D[np.triu_indices(25, 1)].mean() / 3])
+    gm = GPModel(gp_coords=X, cov_function="exponential")
+    gm.fit(y, params={"optimizer_cov": "gradient_descent", "lr_cov": 0.1, "use_nesterov_acc": True, "acc_rate_cov": 0.5,
+                      "delta_rel_conv": 1e-6, "init_cov_pars": init})
+    out = gm.get_cov_pars(std_err=True)
+    ref = [0.037168482, 0.006069406, 1.168105814, 0.445122816, 0.196226850, 0.105105379]
+    assert np.sum(np.abs(out.T.reshape(-1) - ref)) < 1e-5, out
+    assert gm.get_num_optim_iter() == 6
+    assert abs(gm.get_current_neg_log_likelihood() - 33.43686607) < 1e-5
+    gm = GPModel(gp_coords=X, cov_function="exponential")
+    gm.fit(y, params={"optimizer_cov": "fisher_scoring", "use_nesterov_acc": False, "delta_rel_conv": 1e-6,
+                      "convergence_criterion": "relative_change_in_parameters", "init_cov_pars": init})
+    out = gm.get_cov_pars(std_err=True)
+    ref = [0.037136462, 0.006064181, 1.153630335, 0.435788570, 0.192080613, 0.102631006]
+    assert np.sum(np.abs(out.T.reshape(-1) - ref)) < 1e-5, out
+    assert gm.get_num_optim_iter() == 15
+    re = gm.predict_training_data_random_effects(predict_var=True)
+    pt = gm.predict(gp_coords_pred=X, predict_var=True, predict_response=False)
+    assert np.sum(np.abs(np.asarray(re)[:, 0] - pt["mu"])) < 1e-5
+    assert np.sum(np.abs(np.asarray(re)[:, 1] - pt["var"])) < 1e-5
+    gp = GPModel(gp_coords=X, cov_function="exponential")
+    xp = np.array([[0.1, 0.9], [0.2, 0.4], [0.7, 0.55]])
+    pred = gp.predict(y=y, gp_coords_pred=xp, cov_pars=[0.1, 1, 0.15], predict_cov_mat=True)
+    assert np.sum(np.abs(pred["mu"] - [-0.1460550, 1.0042814, 0.7840301])) < 1e-5
+    cov = [0.6739502109, 0.0008824337, -0.0003815281, 0.0008824337, 0.6060039551, -0.0004157361, -0.0003815281,
+           -0.0004157361, 0.7851787946]
+    assert np.sum(np.abs(np.asarray(pred["cov"]).T.reshape(-1) - cov)) < 1e-5
