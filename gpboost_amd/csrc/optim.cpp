@@ -157,7 +157,8 @@ int lbfgs_minimize(LbfgsObjective& f, std::vector<double>& x, double& fx, const 
 
 bool is_internal_optimizer(const std::string& name) { return name == "gradient_descent" || name == "fisher_scoring"; }
 
-int internal_optimize(InternalObjective& f, std::vector<double>& pars, const InternalSettings& s, double* nll_out) {
+int internal_optimize(InternalObjective& f, std::vector<double>& pars, const InternalSettings& s, double* nll_out,
+                      InternalCoefHook* coef) {
   const bool gd = s.optimizer == "gradient_descent";
   if (!gd && s.optimizer != "fisher_scoring") Fatal("internal optimizer '%s' is not supported", s.optimizer.c_str());
   const bool profile = gd;                  // profile_out_error_variance_ (re_model_template.h:946-948)
@@ -180,6 +181,8 @@ int internal_optimize(InternalObjective& f, std::vector<double>& pars, const Int
   for (int it = 0; it < s.max_iter; ++it) {
     const double nll_lag1 = nll;
     const std::vector<double> pars_lag1 = pars;
+    // neg_log_likelihood_after_lin_coef_update_ (:1327-1330, 1356)
+    const double base = coef != nullptr ? coef->Update(pars) : nll_lag1;
     std::vector<double> grad, step;
     if (gd) {
       double s2 = 0.;
@@ -252,7 +255,7 @@ int internal_optimize(InternalObjective& f, std::vector<double>& pars, const Int
       }
       nll = f.Nll(np);
       const double mu = nest ? schedule(it, acc) : 0.;
-      if (nll <= nll_lag1 + kCArmijo * lr * dir_deriv + kCArmijoMom * mu * mom_dir_deriv) {
+      if (nll <= base + kCArmijo * lr * dir_deriv + kCArmijoMom * mu * mom_dir_deriv) {
         found = true;
         break;
       }
@@ -276,7 +279,9 @@ int internal_optimize(InternalObjective& f, std::vector<double>& pars, const Int
         dn += (pars[i] - pars_lag1[i]) * (pars[i] - pars_lag1[i]);
         ln += pars_lag1[i] * pars_lag1[i];
       }
-      conv = std::sqrt(dn) <= s.delta * std::sqrt(ln);
+      // with covariates: both the coefficients and the covariance parameters (strict <, :1712-1716)
+      conv = coef != nullptr ? coef->CoefConverged(s.delta) && std::sqrt(dn) < s.delta * std::sqrt(ln)
+                             : std::sqrt(dn) <= s.delta * std::sqrt(ln);
     } else {
       conv = (nll_lag1 - nll) <= s.delta * std::max(std::fabs(nll_lag1), 1.);
     }
@@ -691,6 +696,52 @@ class InternalAdapter : public InternalObjective {
   REModelAMD* m_;
 };
 
+// optimizer_coef "wls" inside the internal optimizers: GLS at the current parameters, the residual response
+// y - F - X beta for the covariance step
+class WlsCoefHook : public InternalCoefHook {
+ public:
+  WlsCoefHook(REModelAMD* m, const std::vector<double>& y, const std::vector<double>& F, const std::vector<double>& X,
+              int p, std::vector<double> beta0)
+      : m_(m), y_(y), F_(F), X_(X), p_(p), beta_(std::move(beta0)) {
+    SetResidual();
+  }
+  double Update(const std::vector<double>& trafo) override {
+    beta_lag1_ = beta_;
+    std::vector<double> b;
+    m_->EvalTrafoWls(trafo.data(), false, /*fatal_on_nan=*/false, &b);   // ProfileOutCoef (:2427-2445)
+    beta_ = b;
+    SetResidual();
+    return m_->EvalTrafo(trafo.data(), false, 0, false).nll;   // EvalNegLogLikelihoodOnlyUpdateFixedEffects
+  }
+  bool CoefConverged(double delta) const override {
+    double dn = 0., ln = 0.;
+    for (int k = 0; k < p_; ++k) {
+      dn += (beta_[k] - beta_lag1_[k]) * (beta_[k] - beta_lag1_[k]);
+      ln += beta_lag1_[k] * beta_lag1_[k];
+    }
+    return std::sqrt(dn) <= delta * std::sqrt(ln);
+  }
+  const std::vector<double>& beta() const { return beta_; }
+
+ private:
+  void SetResidual() {
+    const int n = (int)y_.size();
+    std::vector<double> off(n);
+    for (int i = 0; i < n; ++i) {
+      double v = F_.empty() ? 0. : F_[i];
+      for (int k = 0; k < p_; ++k) v += X_[(size_t)k * n + i] * beta_[k];
+      off[i] = v;
+    }
+    m_->SetResponseAndOffset(y_.data(), off.data());
+  }
+  REModelAMD* m_;
+  const std::vector<double>& y_;
+  const std::vector<double>& F_;
+  const std::vector<double>& X_;
+  int p_;
+  std::vector<double> beta_, beta_lag1_;
+};
+
 }  // namespace
 
 std::vector<double> REModelAMD::FisherTrafo(const double* trafo) {
@@ -952,9 +1003,9 @@ void REModelAMD::OptimLinRegrCoefCovPar(const double* y, const double* X, int p,
   if (!est_idx_.empty() && X != nullptr && p > 0)
     Fatal("estimate_cov_par_index (fixing covariance parameters) with linear regression covariates is not supported by "
           "gpboost_amd");
-  if (!isettings_.optimizer.empty())
-    Fatal("optimizer_cov = '%s' with linear regression covariates is not supported by gpboost_amd (use 'lbfgs')",
-          isettings_.optimizer.c_str());
+  if (!isettings_.optimizer.empty() && !is_internal_optimizer(isettings_.optimizer) && X != nullptr && p > 0)
+    Fatal("optimizer_cov = '%s' with linear regression covariates is not supported by gpboost_amd (use 'lbfgs', "
+          "'gradient_descent' or 'fisher_scoring')", isettings_.optimizer.c_str());
   // REModel::OptimLinRegrCoefCovPar (re_model.cpp:403-469) -> REModelTemplate::OptimLinRegrCoefCovPar
   // with covariates (re_model_template.h:846-1700): Gaussian likelihood, optimizer_cov "lbfgs",
   // optimizer_coef "wls" (its default, :7467-7470): OptimExternal with profile_out_coef = true
@@ -1010,6 +1061,57 @@ void REModelAMD::OptimLinRegrCoefCovPar(const double* y, const double* X, int p,
     cov_pars_orig_ = start_orig;
     cov_pars_initialized_ = true;
     EvalTrafoWls(trafo, false, true, nullptr);
+    last_cov_pars_ = cov_pars_orig_;
+    return;
+  }
+  if (is_internal_optimizer(isettings_.optimizer)) {   // gradient descent / Fisher scoring with "wls" coefficients
+    if (isettings_.optimizer == "fisher_scoring" && !dense_)
+      Fatal("optimizer_cov = 'fisher_scoring' is supported by gpboost_amd for gp_approx = 'none' only (use 'lbfgs')");
+    // initial coefficients: OLS of y - F on X (re_model_template.h:1110-1140), then GLS in every iteration
+    std::vector<double> yF(yraw);
+    if (fixed_effects != nullptr)
+      for (int i = 0; i < n; ++i) yF[i] -= fixed_effects[i];
+    std::vector<double> XtX((size_t)p * p, 0.), Xty(p, 0.);
+    for (int a = 0; a < p; ++a) {
+      for (int i = 0; i < n; ++i) Xty[a] += X[(size_t)a * n + i] * yF[i];
+      for (int b = 0; b < p; ++b)
+        for (int i = 0; i < n; ++i) XtX[(size_t)a * p + b] += X[(size_t)a * n + i] * X[(size_t)b * n + i];
+    }
+    std::vector<double> b0 = Xty;   // solve by Gaussian elimination (p small)
+    {
+      std::vector<double> A = XtX;
+      for (int c = 0; c < p; ++c) {
+        int piv = c;
+        for (int r = c + 1; r < p; ++r)
+          if (std::fabs(A[(size_t)r * p + c]) > std::fabs(A[(size_t)piv * p + c])) piv = r;
+        for (int k = 0; k < p; ++k) std::swap(A[(size_t)c * p + k], A[(size_t)piv * p + k]);
+        std::swap(b0[c], b0[piv]);
+        for (int r = c + 1; r < p; ++r) {
+          const double f = A[(size_t)r * p + c] / A[(size_t)c * p + c];
+          for (int k = c; k < p; ++k) A[(size_t)r * p + k] -= f * A[(size_t)c * p + k];
+          b0[r] -= f * b0[c];
+        }
+      }
+      for (int c = p - 1; c >= 0; --c) {
+        for (int k = c + 1; k < p; ++k) b0[c] -= A[(size_t)c * p + k] * b0[k];
+        b0[c] /= A[(size_t)c * p + c];
+      }
+    }
+    std::vector<double> Fv = fixed_effects != nullptr ? std::vector<double>(fixed_effects, fixed_effects + n)
+                                                       : std::vector<double>();
+    WlsCoefHook hook(this, yraw, Fv, X_cov_, p, b0);
+    std::vector<double> tv(trafo, trafo + 3);
+    InternalAdapter obj(this);
+    double fx = 0.;
+    num_it_ = internal_optimize(obj, tv, isettings_, &fx, &hook);
+    cov_pars_orig_ = {tv[0], tv[1] * tv[0], range_back(cfg_.cov_type, tv[2])};
+    coef_ = hook.beta();
+    for (double v : coef_)
+      if (std::isnan(v) || std::isinf(v)) Fatal("NaN or Inf occurred in the linear regression coefficients");
+    cov_pars_initialized_ = true;
+    cov_est_once_ = true;
+    cov_est_last_call_ = true;
+    last_nll_ = fx;
     last_cov_pars_ = cov_pars_orig_;
     return;
   }

@@ -100,9 +100,20 @@ class InternalObjective {
   virtual std::vector<double> FisherTrafo(const std::vector<double>& trafo) = 0;
 };
 
+// Linear regression coefficients updated by GLS at the start of every iteration (optimizer_coef "wls",
+// re_model_template.h:1327-1330): Update returns the objective after the update (the Armijo baseline,
+// EvalNegLogLikelihoodOnlyUpdateFixedEffects); CoefConverged tests |beta - beta_lag1| <= delta |beta_lag1| (:1712-1716).
+class InternalCoefHook {
+ public:
+  virtual ~InternalCoefHook() = default;
+  virtual double Update(const std::vector<double>& trafo) = 0;
+  virtual bool CoefConverged(double delta) const = 0;
+};
+
 // Runs the optimizer from trafo (overwritten with the estimate; trafo[0] the final sigma^2); returns the
 // number of iterations (the reference's num_it) and the final objective value in *nll.
-int internal_optimize(InternalObjective& f, std::vector<double>& trafo, const InternalSettings& s, double* nll);
+int internal_optimize(InternalObjective& f, std::vector<double>& trafo, const InternalSettings& s, double* nll,
+                      InternalCoefHook* coef = nullptr);
 bool is_internal_optimizer(const std::string& name);
 
 // "nelder_mead": OptimLib's Nelder-Mead as OptimExternal runs it (optim_utils.h:626-643, 680-700;

@@ -161,7 +161,7 @@ def test_internal_optimizer_defaults_and_refusals():
             y, params={"optimizer_cov": "gradient_descent", "convergence_criterion": "abc"})
     with pytest.raises(GPBoostError, match="covariates"):
         GPModel(gp_coords=X, cov_function="exponential").fit(
-            y, X=np.ones((100, 1)), params={"optimizer_cov": "gradient_descent"})
+            y, X=np.ones((100, 1)), params={"optimizer_cov": "nelder_mead"})
     Xb = synthetic.bench_coords(300)
     gv = GPModel(gp_coords=Xb, cov_function="exponential", gp_approx="vecchia", num_neighbors=10)
     with pytest.raises(GPBoostError, match="fisher_scoring"):
@@ -256,4 +256,33 @@ def test_multiple_observations_per_location_r_test():
     assert np.sum(np.abs(pred["mu"] - [-0.1460550, 1.0042814, 0.7840301])) < 1e-5
     cov = [0.6739502109, 0.0008824337, -0.0003815281, 0.0008824337, 0.6060039551, -0.0004157361, -0.0003815281,
            -0.0004157361, 0.7851787946]
+    assert np.sum(np.abs(np.asarray(pred["cov"]).T.reshape(-1) - cov)) < 1e-5
+
+
+def test_fisher_scoring_wls_linear_regression_r_test():
+    """test_GPModel_gaussian_process.R:430-457: y = eps + X beta + xi, X = (1, sin((i - n/2)^2 2 pi / n)), beta = (2, 2);
+    Fisher scoring with optimizer_coef 'wls' (GLS coefficients at the start of every iteration,
+    re_model_template.h:1327-1330; both coefficients and covariance parameters converged, :1712-1716), then predictions
+    with X_pred (TOLERANCE_STRICT 1e-5 on sums of absolute differences)."""
+    coords, y0 = synthetic.rtest_gaussian_y(100)
+    Xc = synthetic.rtest_probit_X(100)
+    y = y0 + Xc @ np.array([2., 2.])
+    D = np.sqrt(((coords[:, None, :] - coords[None, :, :]) ** 2).sum(-1))
+    init = [np.var(y, ddof=1) / 2, np.var(y, ddof=1) / 2, D[np.triu_indices(100, 1)].mean() / 3]
+    gm = GPModel(gp_coords=coords, cov_function="exponential")
+    gm.fit(y, X=Xc, params={"optimizer_cov": "fisher_scoring", "optimizer_coef": "wls", "delta_rel_conv": 1e-6,
+                            "use_nesterov_acc": False, "convergence_criterion": "relative_change_in_parameters",
+                            "init_cov_pars": init})
+    cov_pars = [0.008461342, 0.069973492, 1.001562822, 0.214358560, 0.094656409, 0.029400407]
+    coef = [2.30780026, 0.21365770, 1.89951426, 0.09484768]
+    assert np.sum(np.abs(np.asarray(gm.get_cov_pars(std_err=True)).T.reshape(-1) - cov_pars)) < 1e-5
+    assert np.sum(np.abs(np.asarray(gm.get_coef(std_err=True)).T.reshape(-1) - coef)) < 1e-5
+    assert abs(gm.get_current_neg_log_likelihood() - 121.482402) < 1e-5
+    xp = np.array([[0.1, 0.9], [0.2, 0.4], [0.7, 0.55]])
+    Xp = np.column_stack([np.ones(3), [-0.5, 0.2, 0.4]])
+    pred = gm.predict(gp_coords_pred=xp, X_pred=Xp, predict_cov_mat=True)
+    mu = [1.196952, 4.063324, 3.156427]
+    cov = [6.305383e-01, 1.358861e-05, 8.317903e-08, 1.358861e-05, 3.469270e-01, 2.686334e-07, 8.317903e-08,
+           2.686334e-07, 4.255400e-01]
+    assert np.sum(np.abs(pred["mu"] - mu)) < 1e-5
     assert np.sum(np.abs(np.asarray(pred["cov"]).T.reshape(-1) - cov)) < 1e-5
