@@ -286,3 +286,31 @@ def test_fisher_scoring_wls_linear_regression_r_test():
            2.686334e-07, 4.255400e-01]
     assert np.sum(np.abs(pred["mu"] - mu)) < 1e-5
     assert np.sum(np.abs(np.asarray(pred["cov"]).T.reshape(-1) - cov)) < 1e-5
+
+
+@pytest.fixture(scope="module")
+def golden_cov():
+    with open(os.path.join(os.path.dirname(__file__), "golden", "golden_internal_optim_cov.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("name", ["linreg_rtest_gd", "linreg_rtest_gd_crit_pars", "linreg_rtest_fisher",
+                                  "linreg_synth2000_vecchia_gd"])
+def test_internal_optimizer_with_covariates_matches_reference(golden_cov, name):
+    """Gradient descent / Fisher scoring with optimizer_coef 'wls' against the reference's fits
+    (tests/golden/make_golden_internal_optim_cov.py): identical iteration counts, parameters and coefficients."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    from make_golden_internal_optim_cov import data
+    case = golden_cov[name]
+    sp = case["spec"]
+    coords, Xc, y = data(case["data"])
+    kw = dict(gp_coords=coords, cov_function=sp["cov_fct"], gp_approx=sp["gp_approx"])
+    if sp["gp_approx"] == "vecchia":
+        kw.update(num_neighbors=sp["num_neighbors"], vecchia_ordering=sp["ordering"])
+    gm = GPModel(**kw)
+    gm.fit(y, X=Xc, params=_params(sp))
+    assert gm.get_num_optim_iter() == case["num_it"]
+    np.testing.assert_allclose(gm.get_cov_pars(), case["cov_pars"], rtol=1e-5, atol=1e-8)
+    np.testing.assert_allclose(gm.get_coef(), case["coef"], rtol=1e-6)
+    assert abs(gm.get_current_neg_log_likelihood() - case["nll"]) <= 1e-8 * abs(case["nll"])
