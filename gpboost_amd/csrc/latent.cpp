@@ -380,6 +380,8 @@ void LatentVecchia::SetObservations(const std::vector<int>& obs_row) {
   obs_order_.assign(n_obs_, 0);
   std::vector<int> fill(ptr.begin(), ptr.end() - 1);
   for (int i = 0; i < n_obs_; ++i) obs_order_[fill[lab_[obs_row[i]]]++] = i;   // ascending observation index per row
+  obs_cnt_.resize(n_);
+  for (int p = 0; p < n_; ++p) obs_cnt_[p] = ptr[p + 1] - ptr[p];
   d_optr_.alloc(n_ + 1);
   HIP_CHECK(hipMemcpyAsync(d_optr_.get(), ptr.data(), sizeof(int) * (n_ + 1), hipMemcpyHostToDevice, s_));
   HIP_CHECK(hipStreamSynchronize(s_));
@@ -817,6 +819,7 @@ LatentVecchia::PcgResult LatentVecchia::Pcg(Block& b, const double* RHS, double*
 
 LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, double aux, const IterativeConfig& cfg,
                                  bool want_grad, bool want_aux_grad, double* grad_f_vo, ModeStart start) {
+  if (use_chol_) return EvalChol(cov_type, lik, trafo, aux, cfg, want_grad, want_aux_grad, grad_f_vo, start);
   if (!y_set_) Fatal("response variable y has not been set");
   if (!(trafo[0] > 0. && trafo[1] > 0.)) Fatal("covariance parameters must be > 0");
   if (lik == kLikGaussian && !(aux > 0.)) Fatal("the error variance (aux_pars) must be > 0");

@@ -27,6 +27,7 @@
 #include "collective.h"
 #include "latent_kernels.h"
 #include "vadu_precond.h"
+#include "sparse_chol.h"
 
 namespace gpb_amd {
 
@@ -161,6 +162,17 @@ class LatentVecchia : public LatentSolverBase {
   // world 1.
   void SetShard(int rank, int world, Collective* coll);
 
+  // matrix_inversion_method = "cholesky" (latent_chol.cpp): Eval runs the reference's exact Laplace-Vecchia
+  // branch on the GPU sparse Cholesky of Sigma^-1 + W (sparse_chol.h) instead of PCG / SLQ. The plan is
+  // built at the first evaluation; CholPlanInfo builds it on demand (statistics).
+  void SetCholesky(bool on);
+  bool cholesky() const { return use_chol_; }
+  const CholPlan* CholPlanInfo();
+  // Cholesky predictive-variance terms (likelihoods.h:6751-6811) on the factor of the last evaluation:
+  // d_V (device n_pred x n column-major) = sqrt(n) (L^-1 P Bpo^T)^T, for latent_pred_moments with nsim = n.
+  // nbr_vo: host n_pred x mp neighbour indices (latent Vecchia rows; >= n: none), d_Bpo device n_pred x mp.
+  void PredVarChol(int n_pred, int mp, const int* nbr_vo, const double* d_Bpo, double* d_V);
+
  private:
   // Device work space of a t-column PCG (t = 1 for the Newton solves, t probes for SLQ).
   struct Block {
@@ -178,6 +190,13 @@ class LatentVecchia : public LatentSolverBase {
     double* b() const { return small.get() + 5 * t; }
   };
 
+  LatentResult EvalChol(int cov_type, int lik, const double* trafo, double aux, const IterativeConfig& cfg,
+                        bool want_grad, bool want_aux_grad, double* grad_f_vo, ModeStart start);
+  void EnsureChol();
+  bool use_chol_ = false;
+  std::unique_ptr<SparseChol> chol_;
+  DevBuf<double> d_diagS_;
+  std::vector<int> obs_cnt_;   // observations per storage row (repeated coordinates)
   void Relabel(const int* nbr, std::vector<int>& nbr_p);   // storage order for locality
   void BuildStructure(const int* nbr);
   Block& GetBlock(int which, int t, int pmax);

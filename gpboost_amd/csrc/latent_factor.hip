@@ -17,6 +17,8 @@
 // reuses it. The kernel runs once per likelihood evaluation.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "common.h"
 #include "cov.h"
 #include "latent_kernels.h"
@@ -242,6 +244,131 @@ __global__ void __launch_bounds__(block_threads<K>()) latent_factor_kernel(Laten
   }
 }
 
+// Rows with more than 64 neighbours (e.g. num_neighbors = n - 1, the R tests' exact Vecchia): one 256-thread
+// workgroup per row, the packed between-neighbour covariance in LDS, right-looking Cholesky with the workgroup
+// (two barriers per column), the triangular solves on one thread. dC is recomputed from the coordinates when
+// the gradient needs t = dC a. Correct for any k <= kWideMax; far slower per row than the lane-group kernel.
+constexpr int kWideMax = 180;
+template <int COV>
+__global__ void __launch_bounds__(256) latent_factor_wide_kernel(LatentFactorArgs a) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int K = a.m;
+  double* Cp = smem;                        // K (K + 1) / 2
+  double* nbx = Cp + K * (K + 1) / 2;       // K x kDMax
+  double* cv = nbx + K * kDMax;             // c
+  double* dcv = cv + K;                     // dc / dlog(phi)
+  double* av = dcv + K;                     // a = C^-1 c
+  double* wv = av + K;                      // work
+  const int tid = threadIdx.x, d = a.d;
+  const double var = a.var, phi = a.phi;
+  const double cdiag = var * a.jitter + a.nugget;
+  for (int i = blockIdx.x; i < a.n; i += gridDim.x) {
+    const int k = min(i, a.m);
+    __syncthreads();
+    for (int r = tid; r < k; r += 256) {
+      const int nb = a.nbr[(size_t)i * a.m + r];
+      double s = 0.;
+      for (int q = 0; q < kDMax; ++q) {
+        const double x = q < d ? a.X[(size_t)nb * d + q] : 0.;
+        nbx[r * kDMax + q] = x;
+        const double t = (q < d ? a.X[(size_t)i * d + q] : 0.) - x;
+        s += t * t;
+      }
+      double c, dc;
+      cov_dcov<COV>(sqrt(s), var, phi, c, dc);
+      cv[r] = c;
+      dcv[r] = dc;
+    }
+    __syncthreads();
+    for (int e = tid; e < k * (k + 1) / 2; e += 256) {
+      int r = (int)((sqrt(8. * e + 1.) - 1.) / 2.);
+      while (r * (r + 1) / 2 > e) --r;
+      while ((r + 1) * (r + 2) / 2 <= e) ++r;
+      const int c = e - r * (r + 1) / 2;
+      double v = cdiag;
+      if (c != r) {
+        double s = 0.;
+        for (int q = 0; q < kDMax; ++q) { const double t = nbx[r * kDMax + q] - nbx[c * kDMax + q]; s += t * t; }
+        double dv;
+        cov_dcov<COV>(sqrt(s), var, phi, v, dv);
+      }
+      Cp[e] = v;
+    }
+    __syncthreads();
+    for (int j = 0; j < k; ++j) {   // right-looking LLT of the packed lower triangle
+      if (tid == 0) Cp[packed(j, j)] = sqrt(Cp[packed(j, j)]);
+      __syncthreads();
+      const double ljj = Cp[packed(j, j)];
+      for (int r = j + 1 + tid; r < k; r += 256) Cp[packed(r, j)] /= ljj;
+      __syncthreads();
+      const int w = k - j - 1;
+      for (int e = tid; e < w * (w + 1) / 2; e += 256) {
+        int rr = (int)((sqrt(8. * e + 1.) - 1.) / 2.);
+        while (rr * (rr + 1) / 2 > e) --rr;
+        while ((rr + 1) * (rr + 2) / 2 <= e) ++rr;
+        const int r = j + 1 + rr, c = j + 1 + (e - rr * (rr + 1) / 2);
+        Cp[packed(r, c)] -= Cp[packed(r, j)] * Cp[packed(c, j)];
+      }
+      __syncthreads();
+    }
+    auto solve = [&](const double* rhs, double* x) {   // x = C^-1 rhs (thread 0)
+      for (int r = 0; r < k; ++r) {
+        double s = rhs[r];
+        for (int c = 0; c < r; ++c) s -= Cp[packed(r, c)] * x[c];
+        x[r] = s / Cp[packed(r, r)];
+      }
+      for (int r = k - 1; r >= 0; --r) {
+        double s = x[r];
+        for (int c = r + 1; c < k; ++c) s -= Cp[packed(c, r)] * x[c];
+        x[r] = s / Cp[packed(r, r)];
+      }
+    };
+    if (tid == 0) {
+      solve(cv, av);
+      double ac = 0.;
+      for (int r = 0; r < k; ++r) ac += av[r] * cv[r];
+      a.Dinv[i] = 1. / (var + a.nugget - ac);
+      if (a.dBv != nullptr) {
+        // t = dC a (zero diagonal), w = C^-1 (dc - t) = dA^T, dD = -(2 dc.a - t.a) (Vecchia_utils.cpp:1573-1583)
+        double dca = 0., ta = 0.;
+        for (int r = 0; r < k; ++r) {
+          double t = 0.;
+          for (int c = 0; c < k; ++c) {
+            if (c == r) continue;
+            double s = 0.;
+            for (int q = 0; q < kDMax; ++q) { const double u = nbx[r * kDMax + q] - nbx[c * kDMax + q]; s += u * u; }
+            double cvv, dvv;
+            cov_dcov<COV>(sqrt(s), var, phi, cvv, dvv);
+            t += dvv * av[c];
+          }
+          dca += dcv[r] * av[r];
+          ta += t * av[r];
+          wv[r] = dcv[r] - t;
+        }
+        a.dD[i] = -(2. * dca - ta);
+      }
+    }
+    __syncthreads();
+    for (int r = tid; r < a.m; r += 256) a.Bv[(size_t)i * a.m + r] = r < k ? -av[r] : 0.;
+    if (a.dBv != nullptr) {
+      __syncthreads();
+      if (tid == 0) {
+        double* x = av;   // a no longer needed
+        solve(wv, x);
+      }
+      __syncthreads();
+      for (int r = tid; r < a.m; r += 256) a.dBv[(size_t)i * a.m + r] = r < k ? -av[r] : 0.;
+    }
+  }
+}
+
+template <int COV>
+void launch_wide(const LatentFactorArgs& a, hipStream_t s) {
+  const size_t lds = sizeof(double) * ((size_t)a.m * (a.m + 1) / 2 + (size_t)a.m * kDMax + 4 * (size_t)a.m);
+  hipLaunchKernelGGL((latent_factor_wide_kernel<COV>), dim3(std::min(a.n, kMaxBlocks)), dim3(256), lds, s, a);
+  HIP_CHECK(hipGetLastError());
+}
+
 int lanes_for_m(int m) {
   if (m <= 16) return 16;
   if (m <= 32) return 32;
@@ -279,7 +406,16 @@ void launch_latent_factor(int cov_type, const LatentFactorArgs& a, hipStream_t s
     case 16: launch_cov<16>(cov_type, a, s); break;
     case 32: launch_cov<32>(cov_type, a, s); break;
     case 64: launch_cov<64>(cov_type, a, s); break;
-    default: Fatal("num_neighbors = %d > 64 is not supported by the GPU Vecchia kernel", a.m);
+    default:
+      if (a.m > kWideMax) Fatal("num_neighbors = %d > %d is not supported by the GPU latent Vecchia kernel", a.m, kWideMax);
+      if (a.dBv_var != nullptr) Fatal("num_neighbors = %d > 64 is not supported for the Vecchia Fisher information", a.m);
+      switch (cov_type) {
+        case kMatern05: launch_wide<kMatern05>(a, s); break;
+        case kMatern15: launch_wide<kMatern15>(a, s); break;
+        case kMatern25: launch_wide<kMatern25>(a, s); break;
+        case kGaussian: launch_wide<kGaussian>(a, s); break;
+        default: Fatal("unsupported covariance type %d", cov_type);
+      }
   }
 }
 

@@ -107,8 +107,9 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
   }
   std::string& mim = cfg_.matrix_inversion_method;
   if (mim == "default") mim = cfg_.latent && vecchia_ ? "iterative" : "cholesky";
-  if (cfg_.latent && vecchia_ && mim != "iterative")
-    Fatal("matrix_inversion_method '%s' is not supported for latent Vecchia models in gpboost_amd (supported: iterative)", mim.c_str());
+  if (cfg_.latent && vecchia_ && mim != "iterative" && mim != "cholesky")
+    Fatal("matrix_inversion_method '%s' is not supported for latent Vecchia models in gpboost_amd (supported: iterative, "
+          "cholesky)", mim.c_str());
   if (!(cfg_.latent && vecchia_) && mim != "cholesky")
     Fatal("matrix_inversion_method '%s' is not supported for likelihood 'gaussian' in gpboost_amd (supported: cholesky)", mim.c_str());
   if (cfg_.latent && (cfg_.lik == kLikGaussian || cfg_.lik == kLikGamma))
@@ -262,6 +263,7 @@ void REModelAMD::EnsureStructure() {
     BuildVecchiaStructure();
     if (cfg_.latent) {
       latent_.reset(new LatentVecchia(nu_, cfg_.d, cfg_.num_neighbors, d_X_.get(), nbr_.data(), stream_));
+      latent_->SetCholesky(cfg_.matrix_inversion_method == "cholesky");   // likelihoods.h:2935-2955 vs :2925-2934
       if (has_dup()) latent_->SetObservations(obs_row_);
       latent_->SetShard(rank_, world_, coll_.get());   // probe columns over the ranks (§8e Option A)
       latent_->SetLogLikConst(loglik_const_);
@@ -310,8 +312,10 @@ void REModelAMD::BuildVecchiaStructure() {
   d_nbr_.alloc((size_t)n * m);
   HIP_CHECK(hipMemcpyAsync(d_nbr_.get() + (size_t)row_begin_ * m, nbr_.data(), sizeof(int) * nbr_.size(),
                            hipMemcpyHostToDevice, stream_));
-  const int nblocks = vecchia_rows_blocks(row_end_ - row_begin_, m);
-  d_block_sums_.alloc((size_t)std::max(nblocks, 1) * kVecchiaSums);
+  if (!cfg_.latent) {   // the exact path's row kernel (m <= 64) and its block sums; latent models run their own
+    const int nblocks = vecchia_rows_blocks(row_end_ - row_begin_, m);
+    d_block_sums_.alloc((size_t)std::max(nblocks, 1) * kVecchiaSums);
+  }
 }
 
 // Exact Vecchia: rows (Vecchia order) split into `world` contiguous blocks, one all-reduce of the
@@ -523,7 +527,7 @@ void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred,
   a.Dinv_out = dD.get();
   a.row_base = n;
   launch_vecchia_rows(cfg_.cov_type, a, stream_);
-  if (latent && (cond_all || predict_cov_mat)) {
+  if (latent && (cond_all || predict_cov_mat || latent_->cholesky())) {
     PredictLatentSim(n, n_pred, mp, nb, dB.get(), dD.get(), cond_all, predict_cov_mat, predict_var, predict_response,
                      out, mean_add);
     return;
@@ -618,11 +622,20 @@ void REModelAMD::PredictLatentSim(int n, int n_pred, int mp, const std::vector<i
   const bool want_var = predict_var || predict_response;
   std::vector<double> var(n_pred), cov(predict_cov_mat ? (size_t)n_pred * n_pred : 0);
   if (want_var || predict_cov_mat) {
-    const int nsim = nsim_var_pred_;
+    // iterative: nsim simulation draws; cholesky: the exact term through L^-1 Bpo^T (likelihoods.h:6751-6811),
+    // as n "draws" whose second moment is Bpo (Sigma^-1 + W)^-1 Bpo^T
+    const bool chol = latent_->cholesky();
+    const int nsim = chol ? n : nsim_var_pred_;
+    if (chol && (double)n_pred * n > 4e9)
+      Fatal("latent Vecchia predictions with matrix_inversion_method = 'cholesky' are limited to num_data_pred * "
+            "num_data <= 4e9 in gpboost_amd (predict in batches)");
     DevBuf<double> dBpo(Bpo.size()), dV((size_t)n_pred * nsim);
     HIP_CHECK(hipMemcpyAsync(dBpo.get(), Bpo.data(), sizeof(double) * Bpo.size(), hipMemcpyHostToDevice, stream_));
-    latent_->PredVarSim(nsim, iter.num_rand_vec_trace, iter.cg_delta_conv, iter.cg_max_num_it, pred_seed_++, n_pred,
-                        mp, nb.data(), dBpo.get(), nullptr, dV.get(), RefDraws());
+    if (chol)
+      latent_->PredVarChol(n_pred, mp, nb.data(), dBpo.get(), dV.get());
+    else
+      latent_->PredVarSim(nsim, iter.num_rand_vec_trace, iter.cg_delta_conv, iter.cg_max_num_it, pred_seed_++, n_pred,
+                          mp, nb.data(), dBpo.get(), nullptr, dV.get(), RefDraws());
     latent_pred_moments(stream_, n_pred, cond_all ? Bp.data() : nullptr, D.data(), dV.get(), nsim, want_var,
                         predict_cov_mat, var.data(), cov.data());
   }
@@ -1179,6 +1192,8 @@ void REModelAMD::LaunchVecchiaRows(const double* trafo, int r0, int r1, double* 
   a.diag_mult = 1.;   // Gaussian likelihood: nugget 1 on the transformed scale (Vecchia_utils.cpp:1540)
   a.diag_add = 1.;
   a.d_nugget = 1.;
+  if (d_block_sums_.size() == 0)   // built as a latent model and switched to the Gaussian likelihood
+    d_block_sums_.alloc((size_t)std::max(vecchia_rows_blocks(row_end_ - row_begin_, a.m), 1) * kVecchiaSums);
   a.block_sums = d_block_sums_.get();
   static const int sched = [] {   // A/B of the partial-round schedule (kernels.h VecchiaRowsArgs::sched)
     const char* e = std::getenv("GPBOOST_AMD_ROWS16_SCHED");

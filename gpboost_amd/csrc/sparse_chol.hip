@@ -1,0 +1,757 @@
+// Numeric phases of the sparse Cholesky of Sigma^-1 + W (sparse_chol.h) on gfx950.
+//
+// Every launch executes one CholOp of a host-built schedule (sparse_chol_sym.cpp): the tasks of one
+// level of the supernodal tree, so independent fronts of a level share one grid. Kernels:
+//   chol_assemble   one workgroup per 64 front columns: zero, A's entries (+ W on the diagonal), then the
+//                   children's update blocks by extend-add, children in a fixed order (no atomics: each
+//                   workgroup owns its target columns)
+//   chol_diag       one workgroup (4 waves) per 64 x 64 diagonal block: the Cholesky pivots and the
+//                   block inverse W = L^-1 in one register-resident sweep (row r of L and column r of
+//                   W on lane r, columns / rows split over the waves, the pivot column broadcast
+//                   through LDS, one barrier per step)
+//   chol_gemm       one 64 x 64 output tile per 256-thread workgroup, v_mfma_f64_16x16x4 on 4 waves
+//                   (2 x 2 MFMA tiles each), K staged through double-buffered LDS: TRSM (times W^T),
+//                   the panel updates, the update block U -= L21 L21^T (K = ns), the solves' block
+//                   steps and the selected inverse's products
+//   chol_gather_s / chol_mirror / chol_asmv / chol_gather_x / chol_scatter_x: the selected inverse's
+//                   parent-to-child gathers, symmetric completion, and the solves' front vectors.
+// Reductions (log-determinant, traces) are two-pass with a fixed order: results are bitwise repeatable.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <map>
+#include <utility>
+#include <vector>
+
+#include "sparse_chol.h"
+
+namespace gpb_amd {
+namespace {
+
+typedef double double4_t __attribute__((ext_vector_type(4)));
+
+struct Bufs {
+  double* p[4];   // kCbF, kCbS, kCbW, kCbY
+};
+
+struct DevPlan {
+  int n;
+  const int* sfirst;
+  const int64_t* rptr;
+  const int* rows;
+  const int64_t* foff;
+  const int* rel;
+  const int* cptr;
+  const int* child;
+  const int* sparent;
+  const int* perm;
+};
+
+__device__ __forceinline__ int lower_bound_dev(const int* a, int n, int v) {
+  int lo = 0, hi = n;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (a[mid] < v) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// ---- A's entries: clique sums of D^-1 B B^T and of its range derivative
+__global__ void __launch_bounds__(256) chol_entry_values_kernel(int64_t ne, const int64_t* __restrict__ cptr,
+                                                                const uint64_t* __restrict__ ctr, int m,
+                                                                const double* __restrict__ Bv,
+                                                                const double* __restrict__ Dinv,
+                                                                const double* __restrict__ dBv,
+                                                                const double* __restrict__ dD, double* __restrict__ aval,
+                                                                double* __restrict__ daval) {
+  for (int64_t e = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; e < ne; e += (int64_t)gridDim.x * blockDim.x) {
+    double v = 0., dv = 0.;
+    for (int64_t c = cptr[e]; c < cptr[e + 1]; ++c) {
+      const uint64_t w = ctr[c];
+      const int r = (int)(w >> 16), a = (int)((w >> 8) & 255), b = (int)(w & 255);
+      const double* br = Bv + (size_t)r * m;
+      const double ba = a == 0 ? 1. : br[a - 1];
+      const double bb = b == 0 ? 1. : br[b - 1];
+      const double di = Dinv[r];
+      v += di * ba * bb;
+      if (daval != nullptr) {
+        const double* dr = dBv + (size_t)r * m;
+        const double da = a == 0 ? 0. : dr[a - 1];
+        const double db = b == 0 ? 0. : dr[b - 1];
+        dv += di * (da * bb + ba * db) - di * di * dD[r] * ba * bb;
+      }
+    }
+    aval[e] = v;
+    if (daval != nullptr) daval[e] = dv;
+  }
+}
+
+// ---- front assembly (factorization): columns [c0, c1) of supernode s
+__global__ void __launch_bounds__(256) chol_assemble_kernel(const CholColTask* __restrict__ tasks, int64_t t0,
+                                                            DevPlan P, double* __restrict__ F,
+                                                            const int64_t* __restrict__ ecol,
+                                                            const int64_t* __restrict__ eoff,
+                                                            const double* __restrict__ aval,
+                                                            const double* __restrict__ W) {
+  const CholColTask tk = tasks[t0 + blockIdx.x];
+  const int s = tk.s;
+  const int sf = P.sfirst[s], ns = P.sfirst[s + 1] - sf;
+  const int nr = (int)(P.rptr[s + 1] - P.rptr[s]);
+  const int fs = ns + nr;
+  double* Fs = F + P.foff[s];
+  const int tid = threadIdx.x;
+  for (int j = tk.c0; j < tk.c1; ++j)
+    for (int r = j + tid; r < fs; r += 256) Fs[r + (size_t)j * fs] = 0.;
+  __syncthreads();
+  const int jend = min(tk.c1, ns);
+  for (int j = tk.c0; j < jend; ++j) {
+    const int g = sf + j;
+    const int64_t e0 = ecol[g], e1 = ecol[g + 1];
+    for (int64_t e = e0 + tid; e < e1; e += 256) {
+      double v = aval[e];
+      if (e == e0 && W != nullptr) v += W[P.perm[g]];   // the diagonal leads its column
+      F[eoff[e]] = v;
+    }
+  }
+  for (int q = P.cptr[s]; q < P.cptr[s + 1]; ++q) {
+    __syncthreads();
+    const int ch = P.child[q];
+    const int nsc = P.sfirst[ch + 1] - P.sfirst[ch];
+    const int nrc = (int)(P.rptr[ch + 1] - P.rptr[ch]);
+    const int fc = nsc + nrc;
+    const int* rel = P.rel + P.rptr[ch];
+    const double* U = F + P.foff[ch] + nsc + (size_t)nsc * fc;
+    const int b0 = lower_bound_dev(rel, nrc, tk.c0), b1 = lower_bound_dev(rel, nrc, tk.c1);
+    for (int b = b0; b < b1; ++b) {
+      const int tb = rel[b];
+      double* dst = Fs + (size_t)tb * fs;
+      const double* src = U + (size_t)b * fc;
+      for (int a = b + tid; a < nrc; a += 256) dst[rel[a]] += src[a];
+    }
+  }
+}
+
+// ---- one 64 x 64 diagonal block: L and W = L^-1 by four waves. Lane r of wave w holds row r of the block
+// at the columns x = 4k + w (L) and column r of W at the rows x = 4k + w. Step j: the wave owning column
+// j takes the pivot from lane j, scales its column (divisions, as the LLT) and its W row j, publishes
+// l_x = L[x][j] and W[j][r] to LDS; after one barrier every wave applies them to its columns of the
+// trailing matrix (A[r][x] -= l_r l_x) and its rows of W (W[x][r] -= l_x W[j][r]). The padding of a
+// partial block (ib < 64) is the identity.
+__global__ void __launch_bounds__(256) chol_diag_kernel(const CholDiagTask* __restrict__ tasks, int64_t t0,
+                                                        double* __restrict__ F, double* __restrict__ Wd,
+                                                        int* __restrict__ info) {
+  const CholDiagTask tk = tasks[t0 + blockIdx.x];
+  double* A = F + tk.c;
+  const int ld = tk.ld, ib = tk.ib;
+  const int r = threadIdx.x & 63;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  __shared__ double lsh[2][64];
+  __shared__ double wsh[2][64];
+  double row[16], wc[16];
+  const int rr = min(r, ib - 1);
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int x = 4 * k + w;
+    const double v = A[rr + (size_t)min(x, ib - 1) * ld];
+    row[k] = (r < ib && x < ib) ? (x <= r ? v : 0.) : (r == x ? 1. : 0.);
+    wc[k] = (x == r) ? 1. : 0.;
+  }
+  bool bad = false;
+#pragma unroll
+  for (int j = 0; j < 64; ++j) {
+    const int kj = j >> 2;
+    if (w == (j & 3)) {
+      const int lo = __builtin_amdgcn_readlane(__double2loint(row[kj]), j);
+      const int hi = __builtin_amdgcn_readlane(__double2hiint(row[kj]), j);
+      const double p = __hiloint2double(hi, lo);
+      bad = bad || !(p > 0.);
+      const double d = p > 0. ? sqrt(p) : 1.;
+      const double l = r > j ? row[kj] / d : (r == j ? d : 0.);
+      row[kj] = l;
+      wc[kj] = wc[kj] / d;   // W[j][r] final
+      lsh[j & 1][r] = r > j ? l : 0.;
+      wsh[j & 1][r] = wc[kj];
+    }
+    __syncthreads();
+    const double lr = lsh[j & 1][r], wjr = wsh[j & 1][r];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (4 * k + 3 <= j) continue;   // every column / row of register k is <= j
+      const double lx = lsh[j & 1][4 * k + w];   // 0 for x <= j
+      row[k] = fma(-lr, lx, row[k]);
+      wc[k] = fma(-lx, wjr, wc[k]);
+    }
+  }
+  if (bad && r == 0) atomicAdd(info, 1);
+  double* W = Wd + tk.w;
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const int x = 4 * k + w;
+    if (r < ib && x < ib) {
+      if (x <= r) A[r + (size_t)x * ld] = row[k];
+      W[x + (size_t)r * 64] = wc[k];   // W[x][r] (zero above the diagonal)
+    }
+  }
+}
+
+// ---- batched GEMM tile: C = alpha op(A) op(B) + beta C, one task per workgroup
+constexpr int GT = 64, GK = 16;
+__global__ void __launch_bounds__(256) chol_gemm_kernel(const CholGemmTask* __restrict__ tasks, int64_t t0, Bufs bufs) {
+  const CholGemmTask g = tasks[t0 + blockIdx.x];
+  const double* A = bufs.p[(g.flags >> 4) & 3] + g.a;
+  const double* B = bufs.p[(g.flags >> 6) & 3] + g.b;
+  double* C = bufs.p[(g.flags >> 8) & 3] + g.c;
+  const bool ta = g.flags & kCgTA, tb = g.flags & kCgTB;
+  __shared__ double As[2][GK][GT + 1];
+  __shared__ double Bs[2][GK][GT + 1];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  double4_t acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = (double4_t){0., 0., 0., 0.};
+  constexpr int EPT = GK * GT / 256;
+  double ra[EPT], rb[EPT];
+  auto load = [&](int kk) {
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      const int idx = tid + e * 256;
+      int i, k;
+      if (ta) { k = idx & (GK - 1); i = idx / GK; } else { i = idx & (GT - 1); k = idx / GT; }
+      const int gk = kk + k;
+      double v = 0.;
+      if (i < g.M && gk < g.K) v = ta ? A[(size_t)gk + (size_t)i * g.lda] : A[(size_t)i + (size_t)gk * g.lda];
+      ra[e] = v;
+      int j, kb;
+      if (tb) { j = idx & (GT - 1); kb = idx / GT; } else { kb = idx & (GK - 1); j = idx / GK; }
+      const int gkb = kk + kb;
+      double w = 0.;
+      if (j < g.N && gkb < g.K) w = tb ? B[(size_t)j + (size_t)gkb * g.ldb] : B[(size_t)gkb + (size_t)j * g.ldb];
+      rb[e] = w;
+    }
+  };
+  auto store = [&](int buf) {
+#pragma unroll
+    for (int e = 0; e < EPT; ++e) {
+      const int idx = tid + e * 256;
+      int i, k;
+      if (ta) { k = idx & (GK - 1); i = idx / GK; } else { i = idx & (GT - 1); k = idx / GT; }
+      As[buf][k][i] = ra[e];
+      int j, kb;
+      if (tb) { j = idx & (GT - 1); kb = idx / GT; } else { kb = idx & (GK - 1); j = idx / GK; }
+      Bs[buf][kb][j] = rb[e];
+    }
+  };
+  if (g.K > 0) {
+    load(0);
+    store(0);
+  }
+  __syncthreads();
+  int buf = 0;
+  for (int kk = 0; kk < g.K; kk += GK) {
+    const bool more = kk + GK < g.K;
+    if (more) load(kk + GK);
+#pragma unroll
+    for (int k4 = 0; k4 < GK; k4 += 4) {
+      const int kl = k4 + (lane >> 4);
+      const double a0 = As[buf][kl][wm + (lane & 15)], a1 = As[buf][kl][wm + 16 + (lane & 15)];
+      const double b0 = Bs[buf][kl][wn + (lane & 15)], b1 = Bs[buf][kl][wn + 16 + (lane & 15)];
+      acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+    buf ^= 1;
+  }
+  const bool lower = g.flags & kCgLower;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int i = wm + a * 16 + (lane >> 4) + 4 * rg;
+        const int j = wn + b * 16 + (lane & 15);
+        if (i < g.M && j < g.N && !(lower && i - j + g.doff < 0)) {
+          double* c = C + (size_t)i + (size_t)j * g.ldc;
+          const double prev = g.beta == 0. ? 0. : g.beta * (*c);
+          *c = prev + g.alpha * acc[a][b][rg];
+        }
+      }
+}
+
+// ---- selected inverse: S_RR of supernode s from its parent's front (both triangles), R columns [c0, c1)
+__global__ void __launch_bounds__(256) chol_gather_s_kernel(const CholColTask* __restrict__ tasks, int64_t t0,
+                                                            DevPlan P, double* __restrict__ S) {
+  const CholColTask tk = tasks[t0 + blockIdx.x];
+  const int s = tk.s, p = P.sparent[s];
+  const int ns = P.sfirst[s + 1] - P.sfirst[s];
+  const int nr = (int)(P.rptr[s + 1] - P.rptr[s]);
+  const int fs = ns + nr;
+  const int fp = (P.sfirst[p + 1] - P.sfirst[p]) + (int)(P.rptr[p + 1] - P.rptr[p]);
+  const int* rel = P.rel + P.rptr[s];
+  double* Ss = S + P.foff[s];
+  const double* Sp = S + P.foff[p];
+  for (int b = tk.c0; b < tk.c1; ++b) {
+    const double* src = Sp + (size_t)rel[b] * fp;
+    double* dst = Ss + ns + (size_t)(ns + b) * fs;
+    for (int a = threadIdx.x; a < nr; a += 256) dst[a] = src[rel[a]];
+  }
+}
+
+// S[j, r] = S[r, j] for front columns j in [c0, c1) and rows r > j (LDS-transposed 64 x 64 tiles)
+__global__ void __launch_bounds__(256) chol_mirror_kernel(const CholColTask* __restrict__ tasks, int64_t t0,
+                                                          DevPlan P, double* __restrict__ S) {
+  const CholColTask tk = tasks[t0 + blockIdx.x];
+  const int s = tk.s;
+  const int ns = P.sfirst[s + 1] - P.sfirst[s];
+  const int fs = ns + (int)(P.rptr[s + 1] - P.rptr[s]);
+  double* Ss = S + P.foff[s];
+  __shared__ double T[64][65];
+  const int nc = tk.c1 - tk.c0;
+  const int tid = threadIdx.x;
+  for (int R0 = tk.c0; R0 < fs; R0 += 64) {
+    __syncthreads();
+    for (int e = tid; e < 64 * 64; e += 256) {
+      const int rr = e & 63, cc = e >> 6;
+      if (cc < nc && R0 + rr < fs) T[rr][cc] = Ss[(R0 + rr) + (size_t)(tk.c0 + cc) * fs];
+    }
+    __syncthreads();
+    for (int e = tid; e < 64 * 64; e += 256) {
+      const int cc = e & 63, rr = e >> 6;
+      const int row = R0 + rr, col = tk.c0 + cc;
+      if (cc < nc && row < fs && row > col) Ss[col + (size_t)row * fs] = T[rr][cc];
+    }
+  }
+}
+
+// ---- solves: front vectors V_s (fs x t, ld fs)
+struct SolveArgs {
+  double* V;
+  const int64_t* vofs;
+  const double* b;   // input, matrix labels, n x t (ld n)
+  double* X;         // global X, matrix labels, n x t (ld n)
+  int t;
+};
+
+__global__ void __launch_bounds__(256) chol_asmv_kernel(const CholColTask* __restrict__ tasks, int64_t t0, DevPlan P,
+                                                        SolveArgs a) {
+  const CholColTask tk = tasks[t0 + blockIdx.x];
+  const int s = tk.s;
+  const int sf = P.sfirst[s], ns = P.sfirst[s + 1] - sf;
+  const int fs = ns + (int)(P.rptr[s + 1] - P.rptr[s]);
+  double* V = a.V + a.vofs[s];
+  for (int k = 0; k < a.t; ++k)
+    for (int r = threadIdx.x; r < fs; r += 256)
+      V[r + (size_t)k * fs] = r < ns ? a.b[P.perm[sf + r] + (size_t)k * P.n] : 0.;
+  for (int q = P.cptr[s]; q < P.cptr[s + 1]; ++q) {
+    __syncthreads();
+    const int ch = P.child[q];
+    const int nsc = P.sfirst[ch + 1] - P.sfirst[ch];
+    const int nrc = (int)(P.rptr[ch + 1] - P.rptr[ch]);
+    const int fc = nsc + nrc;
+    const int* rel = P.rel + P.rptr[ch];
+    const double* Vc = a.V + a.vofs[ch];
+    for (int k = 0; k < a.t; ++k)
+      for (int i = threadIdx.x; i < nrc; i += 256) V[rel[i] + (size_t)k * fs] += Vc[nsc + i + (size_t)k * fc];
+  }
+}
+
+__global__ void __launch_bounds__(256) chol_gather_x_kernel(const CholColTask* __restrict__ tasks, int64_t t0,
+                                                            DevPlan P, SolveArgs a) {
+  const CholColTask tk = tasks[t0 + blockIdx.x];
+  const int s = tk.s;
+  const int ns = P.sfirst[s + 1] - P.sfirst[s];
+  const int nr = (int)(P.rptr[s + 1] - P.rptr[s]);
+  const int fs = ns + nr;
+  const int* R = P.rows + P.rptr[s];
+  double* V = a.V + a.vofs[s];
+  for (int k = 0; k < a.t; ++k)
+    for (int i = tk.c0 + threadIdx.x; i < tk.c1; i += 256) V[ns + i + (size_t)k * fs] = a.X[P.perm[R[i]] + (size_t)k * P.n];
+}
+
+__global__ void __launch_bounds__(256) chol_scatter_x_kernel(const CholColTask* __restrict__ tasks, int64_t t0,
+                                                             DevPlan P, SolveArgs a) {
+  const CholColTask tk = tasks[t0 + blockIdx.x];
+  const int s = tk.s;
+  const int sf = P.sfirst[s], ns = P.sfirst[s + 1] - sf;
+  const int fs = ns + (int)(P.rptr[s + 1] - P.rptr[s]);
+  const double* V = a.V + a.vofs[s];
+  for (int k = 0; k < a.t; ++k)
+    for (int i = tk.c0 + threadIdx.x; i < tk.c1; i += 256) a.X[P.perm[sf + i] + (size_t)k * P.n] = V[i + (size_t)k * fs];
+}
+
+// ---- reductions (two passes, fixed order)
+constexpr int kRedBlocks = 1024;
+// part[blk * 4 + q]: q = 0: sum 2 log L_gg; 1: sum_e aval S; 2: sum_diag aval S; 3: sum_e daval S;
+// (diagonal part of daval in part2[blk])
+__global__ void __launch_bounds__(256) chol_logdet_kernel(int n, const int64_t* __restrict__ dpos,
+                                                          const double* __restrict__ F, double* __restrict__ part) {
+  __shared__ double red[256];
+  double s = 0.;
+  for (int g = blockIdx.x * 256 + threadIdx.x; g < n; g += gridDim.x * 256) s += 2. * log(F[dpos[g]]);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(256) chol_trace_kernel(int n, const int64_t* __restrict__ ecol,
+                                                         const int64_t* __restrict__ eoff,
+                                                         const double* __restrict__ aval,
+                                                         const double* __restrict__ daval,
+                                                         const double* __restrict__ S, double* __restrict__ part) {
+  // per column g: off-diagonal entries count twice (symmetric), the diagonal (first entry) once
+  __shared__ double red[2][256];
+  double s0 = 0., s1 = 0.;
+  for (int g = blockIdx.x * 256 + threadIdx.x; g < n; g += gridDim.x * 256) {
+    const int64_t e0 = ecol[g], e1 = ecol[g + 1];
+    for (int64_t e = e0; e < e1; ++e) {
+      const double w = e == e0 ? 1. : 2.;
+      const double sv = S[eoff[e]];
+      s0 += w * aval[e] * sv;
+      if (daval != nullptr) s1 += w * daval[e] * sv;
+    }
+  }
+  red[0][threadIdx.x] = s0;
+  red[1][threadIdx.x] = s1;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + off];
+      red[1][threadIdx.x] += red[1][threadIdx.x + off];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = red[0][0];
+    part[2 * blockIdx.x + 1] = red[1][0];
+  }
+}
+
+__global__ void __launch_bounds__(256) chol_sum_parts_kernel(const double* __restrict__ part, int nblk, int stride,
+                                                             int q, double* __restrict__ out) {
+  __shared__ double red[256];
+  double s = 0.;
+  for (int b = threadIdx.x; b < nblk; b += 256) s += part[(size_t)b * stride + q];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if ((int)threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) out[q] = red[0];
+}
+
+__global__ void __launch_bounds__(256) chol_diag_s_kernel(int n, const int64_t* __restrict__ dpos,
+                                                          const int* __restrict__ perm, const double* __restrict__ S,
+                                                          double* __restrict__ diag) {
+  const int g = blockIdx.x * 256 + threadIdx.x;
+  if (g < n) diag[perm[g]] = S[dpos[g]];
+}
+
+template <typename T>
+void upload(DevBuf<T>& d, const std::vector<T>& h) {
+  d.alloc(std::max<size_t>(h.size(), 1));
+  if (!h.empty()) HIP_CHECK(hipMemcpy(d.get(), h.data(), sizeof(T) * h.size(), hipMemcpyHostToDevice));
+}
+
+int grid_for(int64_t n, int per) { return (int)std::max<int64_t>(1, std::min<int64_t>((n + per - 1) / per, 65536)); }
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------------------
+struct SparseCholDev {
+  DevBuf<CholGemmTask> gemm;
+  DevBuf<CholDiagTask> diag;
+  DevBuf<CholColTask> col;
+  std::vector<CholOp> ops;
+  int64_t y_doubles = 0;
+  void Upload(const CholSchedule& S) {
+    upload(gemm, S.gemm);
+    upload(diag, S.diag);
+    upload(col, S.col);
+    ops = S.ops;
+    y_doubles = S.y_doubles;
+  }
+};
+
+struct SparseChol::Impl {
+  SparseCholDev factor, selinv;
+  std::map<std::pair<int, int>, std::unique_ptr<SparseCholDev>> solve;   // (t, forward_only)
+  std::map<std::pair<int, int>, std::vector<int64_t>> vofs_h;
+  std::map<std::pair<int, int>, std::unique_ptr<DevBuf<int64_t>>> vofs_d;
+  DevPlan dp{};
+  DevBuf<double> V;   // solve scratch
+};
+
+SparseChol::SparseChol(int n, int m, const int* nbr, int d, const double* X, hipStream_t s)
+    : s_(s), n_(n), m_(m), impl_(new Impl) {
+  int leaf = 64;
+  if (const char* e = std::getenv("GPBOOST_AMD_CHOL_LEAF")) leaf = std::max(1, std::atoi(e));
+  chol_analyze(n, m, nbr, d, X, leaf, plan_);
+  CholEntries E;
+  chol_entry_lists(plan_, m, nbr, E);
+  nent_ = E.ecol[n];
+  const CholPlan& P = plan_;
+  upload(d_perm_, P.perm);
+  upload(d_sfirst_, P.sfirst);
+  upload(d_rptr_, P.rptr);
+  upload(d_rows_, P.rows);
+  upload(d_foff_, P.foff);
+  upload(d_rel_, P.rel);
+  upload(d_cptr_, P.cptr);
+  upload(d_child_, P.child);
+  upload(d_sparent_, P.sparent);
+  upload(d_ecol_, E.ecol);
+  upload(d_eoff_, E.eoff);
+  upload(d_ecptr_, E.cptr);
+  upload(d_ctr_, E.ctr);
+  upload(d_dpos_, E.dpos);
+  impl_->factor.Upload(P.factor);
+  impl_->selinv.Upload(P.selinv);
+  DevPlan& dp = impl_->dp;
+  dp.n = n;
+  dp.sfirst = d_sfirst_.get();
+  dp.rptr = d_rptr_.get();
+  dp.rows = d_rows_.get();
+  dp.foff = d_foff_.get();
+  dp.rel = d_rel_.get();
+  dp.cptr = d_cptr_.get();
+  dp.child = d_child_.get();
+  dp.sparent = d_sparent_.get();
+  dp.perm = d_perm_.get();
+  d_F_.alloc(std::max<int64_t>(P.front_doubles, 1));
+  d_Wd_.alloc(std::max<int64_t>(P.woff[P.nsup], 1));
+  d_aval_.alloc(std::max<int64_t>(nent_, 1));
+  d_daval_.alloc(std::max<int64_t>(nent_, 1));
+  d_info_.alloc(1);
+  d_red_.alloc((size_t)2 * kRedBlocks + 8);
+  HIP_CHECK(hipMemset(d_Wd_.get(), 0, sizeof(double) * d_Wd_.size()));
+  HIP_CHECK(hipEventCreate(&ev0_));
+  HIP_CHECK(hipEventCreate(&ev1_));
+}
+
+SparseChol::~SparseChol() {
+  if (ev0_) (void)hipEventDestroy(ev0_);
+  if (ev1_) (void)hipEventDestroy(ev1_);
+}
+
+void SparseChol::SetB(const double* Bv, const double* Dinv, const double* dBv, const double* dD) {
+  has_dA_ = dBv != nullptr;
+  hipLaunchKernelGGL(chol_entry_values_kernel, dim3(grid_for(nent_, 256)), dim3(256), 0, s_, nent_, d_ecptr_.get(),
+                     d_ctr_.get(), m_, Bv, Dinv, dBv, dD, d_aval_.get(), has_dA_ ? d_daval_.get() : nullptr);
+  HIP_CHECK(hipGetLastError());
+}
+
+void SparseChol::Run(const SparseCholDev& sch, double* ybuf, const void* solve_args) {
+  Bufs b{{d_F_.get(), d_S_.get(), d_Wd_.get(), ybuf}};
+  const DevPlan& dp = impl_->dp;
+  for (const CholOp& op : sch.ops) {
+    const dim3 grid(op.ntask);
+    switch (op.type) {
+      case kOpAssemble:
+        hipLaunchKernelGGL(chol_assemble_kernel, grid, dim3(256), 0, s_, sch.col.get(), op.task0, dp, d_F_.get(),
+                           d_ecol_.get(), d_eoff_.get(), d_aval_.get(), cur_W_);
+        break;
+      case kOpDiag:
+        hipLaunchKernelGGL(chol_diag_kernel, grid, dim3(256), 0, s_, sch.diag.get(), op.task0, d_F_.get(), d_Wd_.get(),
+                           d_info_.get());
+        break;
+      case kOpGemm:
+        hipLaunchKernelGGL(chol_gemm_kernel, grid, dim3(256), 0, s_, sch.gemm.get(), op.task0, b);
+        break;
+      case kOpGatherS:
+        hipLaunchKernelGGL(chol_gather_s_kernel, grid, dim3(256), 0, s_, sch.col.get(), op.task0, dp, d_S_.get());
+        break;
+      case kOpMirror:
+        hipLaunchKernelGGL(chol_mirror_kernel, grid, dim3(256), 0, s_, sch.col.get(), op.task0, dp, d_S_.get());
+        break;
+      case kOpAsmV:
+        hipLaunchKernelGGL(chol_asmv_kernel, grid, dim3(256), 0, s_, sch.col.get(), op.task0, dp,
+                           *static_cast<const SolveArgs*>(solve_args));
+        break;
+      case kOpGatherX:
+        hipLaunchKernelGGL(chol_gather_x_kernel, grid, dim3(256), 0, s_, sch.col.get(), op.task0, dp,
+                           *static_cast<const SolveArgs*>(solve_args));
+        break;
+      case kOpScatterX:
+        hipLaunchKernelGGL(chol_scatter_x_kernel, grid, dim3(256), 0, s_, sch.col.get(), op.task0, dp,
+                           *static_cast<const SolveArgs*>(solve_args));
+        break;
+      default:
+        Fatal("sparse Cholesky: unknown op %d", op.type);
+    }
+    HIP_CHECK(hipGetLastError());
+  }
+}
+
+void SparseChol::Factor(const double* W) {
+  HIP_CHECK(hipMemsetAsync(d_info_.get(), 0, sizeof(int), s_));
+  HIP_CHECK(hipEventRecord(ev0_, s_));
+  cur_W_ = W;
+  Run(impl_->factor, nullptr, nullptr);
+  HIP_CHECK(hipEventRecord(ev1_, s_));
+  factored_ = true;
+  timed_ = true;
+}
+
+float SparseChol::last_factor_ms() {
+  if (!timed_) return 0.f;
+  HIP_CHECK(hipEventSynchronize(ev1_));
+  float ms = 0.f;
+  HIP_CHECK(hipEventElapsedTime(&ms, ev0_, ev1_));
+  return ms;
+}
+
+int SparseChol::Info() {
+  int h = 0;
+  HIP_CHECK(hipMemcpyAsync(&h, d_info_.get(), sizeof(int), hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  return h;
+}
+
+double SparseChol::LogDet() {
+  const int nb = std::min(kRedBlocks, grid_for(n_, 256));
+  hipLaunchKernelGGL(chol_logdet_kernel, dim3(nb), dim3(256), 0, s_, n_, d_dpos_.get(), d_F_.get(), d_red_.get());
+  hipLaunchKernelGGL(chol_sum_parts_kernel, dim3(1), dim3(256), 0, s_, d_red_.get(), nb, 1, 0,
+                     d_red_.get() + 2 * kRedBlocks);
+  HIP_CHECK(hipGetLastError());
+  double h = 0.;
+  HIP_CHECK(hipMemcpyAsync(&h, d_red_.get() + 2 * kRedBlocks, sizeof(double), hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  return h;
+}
+
+void SparseChol::SolveCols(const double* b, double* x, int t, bool forward_only) {
+  if (!factored_) Fatal("sparse Cholesky: solve before a factorization");
+  if (t <= 0) return;
+  const std::pair<int, int> key(t, forward_only ? 1 : 0);
+  Impl& I = *impl_;
+  auto it = I.solve.find(key);
+  if (it == I.solve.end()) {
+    CholSchedule S;
+    std::vector<int64_t> vofs;
+    chol_solve_schedule(plan_, t, forward_only, S, vofs);
+    std::unique_ptr<SparseCholDev> dev(new SparseCholDev);
+    dev->Upload(S);
+    std::unique_ptr<DevBuf<int64_t>> dv(new DevBuf<int64_t>);
+    upload(*dv, vofs);
+    I.vofs_d[key] = std::move(dv);
+    it = I.solve.emplace(key, std::move(dev)).first;
+  }
+  const SparseCholDev& sch = *it->second;
+  if ((int64_t)I.V.size() < sch.y_doubles) I.V.alloc(sch.y_doubles);
+  SolveArgs a{I.V.get(), I.vofs_d[key]->get(), b, x, t};
+  Run(sch, I.V.get(), &a);
+}
+
+void SparseChol::Solve(const double* b, double* x) { SolveCols(b, x, 1, false); }
+
+void SparseChol::ForwardCols(const double* B, double* X, int nrhs) { SolveCols(B, X, nrhs, true); }
+
+void SparseChol::SelectedInverse(double* tr_bdb, double* tr_da, double* diagS) {
+  if (!factored_) Fatal("sparse Cholesky: selected inverse before a factorization");
+  if (d_S_.size() < (size_t)std::max<int64_t>(plan_.front_doubles, 1)) d_S_.alloc(std::max<int64_t>(plan_.front_doubles, 1));
+  if ((int64_t)d_Y_.size() < impl_->selinv.y_doubles) d_Y_.alloc(std::max<int64_t>(impl_->selinv.y_doubles, 1));
+  Run(impl_->selinv, d_Y_.get(), nullptr);
+  const int nb = std::min(kRedBlocks, grid_for(n_, 256));
+  hipLaunchKernelGGL(chol_trace_kernel, dim3(nb), dim3(256), 0, s_, n_, d_ecol_.get(), d_eoff_.get(), d_aval_.get(),
+                     has_dA_ ? d_daval_.get() : nullptr, d_S_.get(), d_red_.get());
+  for (int q = 0; q < 2; ++q)
+    hipLaunchKernelGGL(chol_sum_parts_kernel, dim3(1), dim3(256), 0, s_, d_red_.get(), nb, 2, q,
+                       d_red_.get() + 2 * kRedBlocks);
+  if (diagS != nullptr)
+    hipLaunchKernelGGL(chol_diag_s_kernel, dim3(grid_for(n_, 256)), dim3(256), 0, s_, n_, d_dpos_.get(),
+                       d_perm_.get(), d_S_.get(), diagS);
+  HIP_CHECK(hipGetLastError());
+  double h[2] = {0., 0.};
+  HIP_CHECK(hipMemcpyAsync(h, d_red_.get() + 2 * kRedBlocks, sizeof(h), hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  if (tr_bdb) *tr_bdb = h[0];
+  if (tr_da) *tr_da = h[1];
+}
+
+}  // namespace gpb_amd
+
+// ---- helpers of the Cholesky Laplace path
+#include "lik_device.h"
+
+namespace gpb_amd {
+namespace {
+
+__global__ void __launch_bounds__(256) chol_dmll_kernel(int n, int lik, double aux, const double* __restrict__ y,
+                                                        const double* __restrict__ loc,
+                                                        const double* __restrict__ offset, ObsMap obs,
+                                                        const double* __restrict__ diagS, double* __restrict__ dmll) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  double dW;
+  if (obs.ptr == nullptr) {
+    dW = lik_dinfo(lik, aux, y ? y[i] : 0., offset ? loc[i] + offset[i] : loc[i]);
+  } else {
+    dW = 0.;
+    for (int e = obs.ptr[i]; e < obs.ptr[i + 1]; ++e)
+      dW += lik_dinfo(lik, aux, obs.y[e], obs.offset ? loc[i] + obs.offset[e] : loc[i]);
+  }
+  dmll[i] = 0.5 * diagS[i] * dW;
+}
+
+__global__ void __launch_bounds__(256) chol_pred_cols_kernel(int n, int mp, const int* __restrict__ nb,
+                                                             const double* __restrict__ Bpo, double* __restrict__ cols) {
+  const int p = blockIdx.x;   // the columns were zeroed before
+  for (int r = threadIdx.x; r < mp; r += 256) {
+    const int j = nb[(size_t)p * mp + r];
+    if (j >= 0) cols[j + (size_t)p * n] = Bpo[(size_t)p * mp + r];
+  }
+}
+
+__global__ void __launch_bounds__(256) chol_transpose_scale_kernel(int n, int np, const double* __restrict__ M,
+                                                                   double scale, double* __restrict__ V, int ldv) {
+  __shared__ double T[64][65];
+  const int k0 = blockIdx.x * 64, p0 = blockIdx.y * 64;
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+    const int kk = e & 63, pp = e >> 6;
+    if (k0 + kk < n && p0 + pp < np) T[kk][pp] = M[(k0 + kk) + (size_t)(p0 + pp) * n];
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+    const int pp = e & 63, kk = e >> 6;
+    if (k0 + kk < n && p0 + pp < np) V[(p0 + pp) + (size_t)(k0 + kk) * ldv] = scale * T[kk][pp];
+  }
+}
+
+}  // namespace
+
+void launch_chol_dmll(int n, int lik, double aux, const double* y, const double* loc, const double* offset,
+                      const ObsMap& obs, const double* diagS, double* dmll, hipStream_t s) {
+  hipLaunchKernelGGL(chol_dmll_kernel, dim3((n + 255) / 256), dim3(256), 0, s, n, lik, aux, y, loc, offset, obs, diagS,
+                     dmll);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_chol_pred_cols(int n, int np, int mp, const int* nb, const double* Bpo, double* cols, hipStream_t s) {
+  if (np <= 0) return;
+  HIP_CHECK(hipMemsetAsync(cols, 0, sizeof(double) * (size_t)n * np, s));
+  hipLaunchKernelGGL(chol_pred_cols_kernel, dim3(np), dim3(256), 0, s, n, mp, nb, Bpo, cols);
+  HIP_CHECK(hipGetLastError());
+}
+
+void launch_chol_transpose_scale(int n, int np, const double* M, double scale, double* V, int ldv, hipStream_t s) {
+  if (n <= 0 || np <= 0) return;
+  hipLaunchKernelGGL(chol_transpose_scale_kernel, dim3((n + 63) / 64, (np + 63) / 64), dim3(256), 0, s, n, np, M, scale,
+                     V, ldv);
+  HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace gpb_amd
