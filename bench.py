@@ -331,6 +331,101 @@ def bernoulli_leg(X, steps: int, cpu: bool) -> dict:
     return leg
 
 
+CHOL_SAMPLE_N = 10_000            # bounded size of the reference's Cholesky Laplace-Vecchia baseline
+
+
+def bernoulli_chol_cpu_baseline(n: int) -> dict | None:
+    """The reference's bernoulli_logit Laplace evaluation with matrix_inversion_method = "cholesky" (Eigen
+    SimplicialLLT per Newton step, L^-1 for the gradient; likelihoods.h:2935-2955, 5207-5336) on this host, at a
+    bounded n (the reference's cost grows ~n^2: 6.6 / 23.5 / 97 s at n = 5k / 10k / 20k on 8 cores of the build
+    container, so n = 100k is out of reach): one nll + gradient evaluation (oracle/_ref/ref_harness)."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(harness):
+        return None
+    import numpy as np
+
+    from gpboost_amd import synthetic
+    X = synthetic.bench_coords(n)
+    y = synthetic.bench_bernoulli_y(X)
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", str(os.cpu_count() or 1))), 16))
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(np.array([X.shape[0], X.shape[1]], dtype=np.int32).tobytes())
+        f.write(np.ascontiguousarray(X.T).tobytes())
+        f.write(np.ascontiguousarray(y, dtype=np.float64).tobytes())
+        path = f.name
+    try:
+        out = subprocess.run([harness, path, "cov_fct=exponential", "gp_approx=vecchia", "likelihood=bernoulli_logit",
+                              "matrix_inversion_method=cholesky", f"num_neighbors={M_NEIGHBORS}", "ordering=random",
+                              "cov_pars=" + ",".join(map(str, LATENT_PARS)), "reps=1", "mode=eval"],
+                             capture_output=True, text=True, timeout=600,
+                             env=dict(os.environ, OMP_NUM_THREADS=str(threads)), check=True)
+        r = json.loads(out.stdout)
+        t = r["median_time"]
+        return {"value": 1.0 / t, "unit": "evals/s", "cores": threads, "kind": "reference",
+                "sample": f"1 bernoulli_logit Laplace eval (cholesky) at n={n} (nll+grad, {t:.2f} s/eval; "
+                          f"construction {r['t_construct']:.2f} s excluded)", "n": n, "nll": r["nll"],
+                "grad": r["grad"]}
+    except Exception as e:  # noqa: BLE001
+        sys.stderr.write(f"reference cholesky CPU baseline failed: {e}\n")
+        return None
+    finally:
+        os.unlink(path)
+
+
+def bernoulli_chol_leg(X, steps: int, cpu: bool) -> dict:
+    """BASELINE config 5 with the reference's exact Laplace-Vecchia branch (matrix_inversion_method =
+    "cholesky"): Newton mode finding on the sparse Cholesky of Sigma^-1 + W (one factorization per Newton step),
+    the exact log-determinant and the selected-inverse gradient, n = 100k, m = 30; the same evaluation at the
+    reference's bounded sample size beside the reference's own time there."""
+    import numpy as np
+
+    from gpboost_amd import GPModel, synthetic
+
+    def model(Xs):
+        return GPModel(gp_coords=Xs, likelihood="bernoulli_logit", cov_function="exponential", gp_approx="vecchia",
+                       num_neighbors=M_NEIGHBORS, vecchia_ordering="random", seed=0, matrix_inversion_method="cholesky")
+
+    y = synthetic.bench_bernoulli_y(X)
+    gm = model(X)
+    t0 = time.perf_counter()
+    nll, g, _ = gm.neg_log_likelihood_and_grad(LATENT_PARS, y)          # construction + first eval (warm-up)
+    t_first = time.perf_counter() - t0
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        nll, g, _ = gm.neg_log_likelihood_and_grad(LATENT_PARS, None)
+        ts.append(time.perf_counter() - t0)
+    info = gm.last_iteration_info()
+    plan = gm.cholesky_plan_info()
+    t_med = float(np.median(ts))
+    fl, fms = plan["factor_flops"], plan["last_factor_ms"]
+    leg = {"metric": "bernoulli_logit Laplace (Vecchia, cholesky) neg-log-lik + grad evals/sec, n=100k m=30",
+           "value": 1.0 / t_med, "unit": "evals/s", "steps": steps, "ms_per_step": t_med * 1e3,
+           "config": {"workload": "vecchia_bernoulli_logit_laplace_cholesky", "n": X.shape[0],
+                      "num_neighbors": M_NEIGHBORS, "cov_pars": LATENT_PARS, "nll": nll,
+                      "grad": [float(v) for v in g], "newton_its": int(info[0]), "factorizations": int(info[1])},
+           "plan": plan, "construction_and_first_eval_s": t_first,
+           "factor_roofline": {"bound": "mfma", "achieved": fl / (fms * 1e-3) / 1e12, "peak": FP64_PEAK_TFLOPS,
+                               "unit": "TFLOP/s", "frac": fl / (fms * 1e-3) / 1e12 / FP64_PEAK_TFLOPS,
+                               "flops_per_factorization": fl, "ms_per_factorization": fms,
+                               "note": "plan flops (POTRF + TRSM + SYRK per front) / HIP-event time of one "
+                                       "numeric factorization (all levels, assembly included)"}}
+    if cpu:
+        base = bernoulli_chol_cpu_baseline(CHOL_SAMPLE_N)
+        if base is not None:   # the GPU at the reference's sample size, for a same-size ratio
+            Xs = synthetic.bench_coords(CHOL_SAMPLE_N)
+            gs = model(Xs)
+            ys = synthetic.bench_bernoulli_y(Xs)
+            a = gs.neg_log_likelihood_and_grad(LATENT_PARS, ys)
+            t0 = time.perf_counter()
+            for _ in range(3):
+                a = gs.neg_log_likelihood_and_grad(LATENT_PARS, None)
+            base["gpu_at_sample_ms"] = (time.perf_counter() - t0) / 3 * 1e3
+            base["gpu_nll_at_sample"] = a[0]
+        leg["cpu_baseline"] = base
+    return leg
+
+
 GROUPED_N = 500_000               # BASELINE config 4 (expressible proxy, SURVEY.md §0.4)
 GROUPED_LEVELS = (5000, 500)
 GROUPED_PARS = [1.0, 1.0, 0.25]   # sigma^2, sigma_1^2, sigma_2^2
@@ -1063,6 +1158,7 @@ def main():
                 dst.write(src.read())
         line["latent_iterative"] = latent_leg(X, Y, args.latent_steps, not args.no_cpu_baseline)
         line["bernoulli_laplace"] = bernoulli_leg(X, args.latent_steps, not args.no_cpu_baseline)
+        line["bernoulli_laplace_cholesky"] = bernoulli_chol_leg(X, args.latent_steps, not args.no_cpu_baseline)
     elif latent_sharded is not None:
         line["latent_iterative"] = latent_sharded
     print(json.dumps(line), file=json_out)

@@ -540,6 +540,15 @@ class GPModel:
         _safe_call(lib().GPB_GetLastIterationInfo(self.handle, _dp(out)))
         return out
 
+    def cholesky_plan_info(self):
+        """Statistics of the sparse Cholesky plan of a latent Vecchia model with matrix_inversion_method =
+        "cholesky" (include/gpboost_amd.h GPB_GetCholeskyPlanInfo)."""
+        out = np.zeros(9)
+        _safe_call(lib().GPB_GetCholeskyPlanInfo(self.handle, _dp(out)))
+        keys = ["supernodes", "levels", "nnz_L", "front_doubles", "factor_flops", "max_front", "max_supernode",
+                "analyze_ms", "last_factor_ms"]
+        return {k: float(v) for k, v in zip(keys, out)}
+
     def latent_vecchia_factor(self, cov_pars):
         cp = self._check_cov_pars(cov_pars)
         m = min(self.num_neighbors, self.num_data - 1)
@@ -754,6 +763,8 @@ class GPModel:
                 xp = xp.reshape(-1, 1)
             if xp.shape[0] != n_pred:
                 raise ValueError("'gp_coords_pred' and 'group_data_pred' have different numbers of rows")
+            if xp.shape[1] != self.dim_coords:
+                raise ValueError("'gp_coords_pred' must have %d columns (the dimension of 'gp_coords')" % self.dim_coords)
             xcol = np.ascontiguousarray(xp.T).reshape(-1)
         size = n_pred + (n_pred * n_pred if predict_cov_mat else (n_pred if predict_var else 0))
         out = np.zeros(size)

@@ -346,6 +346,11 @@ int GPB_SetPredictionData(REModelHandle handle, int32_t num_data_pred, const int
       auto it = g_saved.find(handle);
       if (it != g_saved.end()) sp = it->second;
     }
+    if (sp.num_data_pred != num_data_pred) {   // kinds saved for another size would be read past their end
+      if (gp_coords_data_pred == nullptr) sp.gp_coords.clear();
+      if (covariate_data_pred == nullptr) sp.covariates.clear();
+      if (re_group_data_pred == nullptr) sp.re_group.clear();
+    }
     sp.num_data_pred = num_data_pred;
     if (gp_coords_data_pred != nullptr) {
       const size_t cnt = (size_t)num_data_pred * (g != nullptr ? g->gp_dim() : model(handle)->config().d);
@@ -737,6 +742,13 @@ int GPB_GetLatentVecchiaFactor(REModelHandle handle, const double* cov_pars, dou
 int GPB_GetLastIterationInfo(REModelHandle handle, double* info) {
   API_BEGIN();
   model(handle)->GetLastIterationInfo(info);
+  API_END();
+}
+
+int GPB_GetCholeskyPlanInfo(REModelHandle handle, double* info) {
+  API_BEGIN();
+  if (info == nullptr) gpb_amd::Fatal("NULL argument");
+  model(handle)->CholeskyPlanInfo(info);
   API_END();
 }
 

@@ -493,14 +493,16 @@ void GroupedModel::Predict(const double* y, int n_pred, const char* re_group_dat
     Fatal("predictive covariance matrices are limited to 40000 prediction points by gpboost_amd");
   const std::vector<double> b = Blup(cov_pars, y, fixed_effects, nullptr);
   // labels column-major, as re_group_data (re_model_template.h:3081-3085): seen levels to their global
-  // index, new labels to -1 (their label string kept for the same-new-label covariance terms)
+  // index, new labels to -1; fresh[k][i] numbers the distinct new labels (the same-new-label covariance terms
+  // compare these ids, not the strings)
   std::vector<int> idx((size_t)n_pred * K, -1);
-  std::vector<std::vector<std::string>> labels(want_unc ? K : 0);
+  std::vector<std::vector<int>> fresh(want_unc ? K : 0);
   std::vector<double> mu(n_pred, 0.);
   const char* p = re_group_data_pred;
   int off = 0;
   for (int k = 0; k < K; ++k) {
-    if (want_unc) labels[k].resize(n_pred);
+    std::unordered_map<std::string, int> fresh_ids;
+    if (want_unc) fresh[k].assign(n_pred, -1);
     for (int i = 0; i < n_pred; ++i) {
       std::string label(p);
       p += label.size() + 1;
@@ -508,8 +510,9 @@ void GroupedModel::Predict(const double* y, int n_pred, const char* re_group_dat
       if (it != label_index_[k].end()) {
         mu[i] += b[off + it->second];   // a new level contributes 0
         idx[(size_t)i * K + k] = off + it->second;
+      } else if (want_unc) {
+        fresh[k][i] = fresh_ids.emplace(std::move(label), (int)fresh_ids.size()).first->second;
       }
-      if (want_unc) labels[k][i] = std::move(label);
     }
     off += re_->levels_per_effect()[k];
   }
@@ -528,7 +531,7 @@ void GroupedModel::Predict(const double* y, int n_pred, const char* re_group_dat
       for (int i = 0; i < n_pred; ++i) {
         double v = o[(size_t)q * n_pred + i] + (i == q ? nug : 0.);
         for (int k = 0; k < K; ++k)
-          if (idx[(size_t)i * K + k] < 0 && idx[(size_t)q * K + k] < 0 && labels[k][i] == labels[k][q]) v += tau[k];
+          if (fresh[k][i] >= 0 && fresh[k][i] == fresh[k][q]) v += tau[k];
         o[(size_t)q * n_pred + i] = v * s2;
       }
   } else {

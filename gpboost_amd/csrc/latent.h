@@ -168,6 +168,7 @@ class LatentVecchia : public LatentSolverBase {
   void SetCholesky(bool on);
   bool cholesky() const { return use_chol_; }
   const CholPlan* CholPlanInfo();
+  float CholLastFactorMs() { return chol_ ? chol_->last_factor_ms() : 0.f; }
   // Cholesky predictive-variance terms (likelihoods.h:6751-6811) on the factor of the last evaluation:
   // d_V (device n_pred x n column-major) = sqrt(n) (L^-1 P Bpo^T)^T, for latent_pred_moments with nsim = n.
   // nbr_vo: host n_pred x mp neighbour indices (latent Vecchia rows; >= n: none), d_Bpo device n_pred x mp.

@@ -708,7 +708,9 @@ class WlsCoefHook : public InternalCoefHook {
   double Update(const std::vector<double>& trafo) override {
     beta_lag1_ = beta_;
     std::vector<double> b;
-    m_->EvalTrafoWls(trafo.data(), false, /*fatal_on_nan=*/false, &b);   // ProfileOutCoef (:2427-2445)
+    const double nll = m_->EvalTrafoWls(trafo.data(), false, /*fatal_on_nan=*/false, &b).nll;   // ProfileOutCoef (:2427-2445)
+    if (std::isnan(nll) || (int)b.size() != p_)   // a non-finite Gram matrix leaves no coefficients: stop cleanly
+      Fatal("NaN or Inf occurred in the generalized least squares coefficients of the covariance parameter step");
     beta_ = b;
     SetResidual();
     return m_->EvalTrafo(trafo.data(), false, 0, false).nll;   // EvalNegLogLikelihoodOnlyUpdateFixedEffects

@@ -1465,4 +1465,21 @@ void combine_partials(const double* s, int n, double sigma2_in, int profile, dou
   if (sigma2_out) *sigma2_out = sigma2;
 }
 
+void REModelAMD::CholeskyPlanInfo(double* out) {
+  if (!(cfg_.latent && vecchia_) || cfg_.matrix_inversion_method != "cholesky")
+    Fatal("GPB_GetCholeskyPlanInfo needs a latent Vecchia model with matrix_inversion_method = 'cholesky'");
+  UseDevice();
+  EnsureStructure();
+  const CholPlan* p = latent_->CholPlanInfo();
+  out[0] = p->nsup;
+  out[1] = (double)p->lvl_ptr.size() - 1;
+  out[2] = (double)p->nnz_l;
+  out[3] = (double)p->front_doubles;
+  out[4] = p->flops;
+  out[5] = p->max_fs;
+  out[6] = p->max_ns;
+  out[7] = p->ms_analyze;
+  out[8] = latent_->CholLastFactorMs();
+}
+
 }  // namespace gpb_amd

@@ -130,6 +130,7 @@ class REModelAMD {
   void GetLatentVecchiaFactor(const double* cov_pars_orig, double* Dinv, double* Bvals, double* dD, double* dBvals);
   // [newton iterations, mode-finding CG iterations, Lanczos steps, log|Sigma W + I|] of the last latent eval
   void GetLastIterationInfo(double* out) const { for (int k = 0; k < 4; ++k) out[k] = last_iter_info_[k]; }
+  void CholeskyPlanInfo(double* out);   // GPB_GetCholeskyPlanInfo (latent Vecchia, cholesky)
   void BenchLatentOperators(int t, int reps, double* out);
   void GetLastKernelTimes(double* ms);
   // FITC inducing points (host row-major m x d; EXTENSION: GPB_GetInducingPoints)

@@ -38,10 +38,11 @@ namespace gpb_amd {
 // ---- work items of the numeric phases (host-built once per plan, executed by sparse_chol.hip)
 // Buffers a task can address (bits of CholGemmTask::flags): the fronts F (factor + update blocks), the
 // selected inverse S (same layout), the diagonal-block inverses Wd (64 x 64 per block), a scratch Y.
-enum CholBuf { kCbF = 0, kCbS = 1, kCbW = 2, kCbY = 3 };
+// P holds split-K partial products (reduced by CholReduceTask).
+enum CholBuf { kCbF = 0, kCbS = 1, kCbW = 2, kCbY = 3, kCbP = 4 };
 // One output tile (M, N <= 64): C = alpha op(A) op(B) + beta C, column-major, element offsets into the
 // flagged buffers. flags: bit 0 transA, bit 1 transB, bit 2 lower-only output (write when
-// i - j + doff >= 0, tile-local i, j), bits 4-5 / 6-7 / 8-9 the buffers of A / B / C.
+// i - j + doff >= 0, tile-local i, j), bits 4-6 / 7-9 / 10-12 the buffers of A / B / C.
 struct CholGemmTask {
   int64_t a, b, c;
   int lda, ldb, ldc;
@@ -50,7 +51,13 @@ struct CholGemmTask {
   double alpha, beta;
 };
 constexpr int kCgTA = 1, kCgTB = 2, kCgLower = 4;
-inline int cg_bufs(int a, int b, int c) { return (a << 4) | (b << 6) | (c << 8); }
+inline int cg_bufs(int a, int b, int c) { return (a << 4) | (b << 7) | (c << 10); }
+// C (M x N <= 64 x 64, ld ldc, buffer bufc) = beta C + alpha sum_{q < nslices} P[p + q pstride] (slices M x N, ld M)
+struct CholReduceTask {
+  int64_t c, p, pstride;
+  int ldc, M, N, nslices, bufc, pad;
+  double alpha, beta;
+};
 // Diagonal block (j0, j0) of a front: ib x ib Cholesky in place + its inverse to Wd[w] (ld 64).
 struct CholDiagTask {
   int64_t c, w;
@@ -61,14 +68,18 @@ struct CholColTask {
   int s, c0, c1, pad;
 };
 enum CholOpType {
-  kOpAssemble = 0,   // CholColTask: zero, A's entries (+ W), children's update blocks (extend-add)
+  kOpAsmTile = 0,        // CholColTask {s, row tile, column tile}: front tile = sum of the children's update blocks
+  kOpAsmEntries,     // CholColTask {s, j0, j1}: A's entries of front columns [j0, j1) (+ W on the diagonal) added
+  kOpReduce,         // CholReduceTask
   kOpDiag,           // CholDiagTask
   kOpGemm,           // CholGemmTask
   kOpGatherS,        // CholColTask over the R x R block: S_RR of s from its parent's front (both triangles)
-  kOpMirror,         // CholColTask: S[j, i] = S[i, j] for front columns [c0, c1) and rows below
+  kOpMirror,         // CholColTask: S[j, i] = S[i, j] for front columns [c0, c1), rows [pad, pad + 64) below
   kOpAsmV,           // CholColTask (c0 = 0, c1 = fs): V_s = [P b at the columns; 0] + children's parts
   kOpGatherX,        // CholColTask: V_s[ns:fs] = X[R_s]
   kOpScatterX,       // CholColTask: X[cols(s)] = V_s[0:ns]
+  kOpFSolve1,        // t = 1, a level of small supernodes: one workgroup per supernode runs its whole forward
+  kOpBSolve1,        //   / backward panel sweep; ntask = the level's supernodes, task0 = its first lvl_sup index
 };
 struct CholOp {
   int type, ntask;
@@ -79,7 +90,9 @@ struct CholSchedule {
   std::vector<CholGemmTask> gemm;
   std::vector<CholDiagTask> diag;
   std::vector<CholColTask> col;
+  std::vector<CholReduceTask> red;
   int64_t y_doubles = 0;   // scratch the schedule needs
+  int64_t p_doubles = 0;   // split-K partials
 };
 
 // Host symbolic analysis.
@@ -103,6 +116,9 @@ struct CholPlan {
   // extend-add maps: rel[rptr[s] + a] = position of R_s[a] in the parent's front; children CSR
   std::vector<int> rel;
   std::vector<int> cptr, child;
+  // cinv[cinv_off[c] + p] = index in R_c of the parent's front position p (-1: none), for the tile assembly
+  std::vector<int64_t> cinv_off;
+  std::vector<int> cinv;
   std::vector<int64_t> woff;      // nsup + 1: offset of s's diagonal-block inverses (64 x 64 per block)
   // schedules
   CholSchedule factor, selinv;
@@ -176,13 +192,16 @@ class SparseChol {
   hipStream_t s_;
   int n_ = 0, m_ = 0;
   std::unique_ptr<Impl> impl_;
-  DevBuf<int> d_perm_, d_sfirst_, d_rows_, d_rel_, d_cptr_, d_child_, d_sparent_;
+  DevBuf<int> d_perm_, d_sfirst_, d_rows_, d_rel_, d_cptr_, d_child_, d_sparent_, d_cinv_;
+  DevBuf<int64_t> d_cinv_off_, d_woff_, d_vofs1_;
+  DevBuf<int> d_lvl_sup_;
+  int64_t vofs1_total_ = 0;
   DevBuf<int64_t> d_rptr_, d_foff_;
   DevBuf<int64_t> d_ecol_, d_eoff_, d_ecptr_, d_dpos_;
   DevBuf<uint64_t> d_ctr_;
   int64_t nent_ = 0;
   DevBuf<double> d_aval_, d_daval_;     // values of A's entries (B^T D^-1 B) and of dA
-  DevBuf<double> d_F_, d_S_, d_Wd_, d_Y_;
+  DevBuf<double> d_F_, d_S_, d_Wd_, d_Y_, d_P_;
   DevBuf<int> d_info_;
   DevBuf<double> d_red_;
   const double* cur_W_ = nullptr;

@@ -2,9 +2,9 @@
 //
 // Every launch executes one CholOp of a host-built schedule (sparse_chol_sym.cpp): the tasks of one
 // level of the supernodal tree, so independent fronts of a level share one grid. Kernels:
-//   chol_assemble   one workgroup per 64 front columns: zero, A's entries (+ W on the diagonal), then the
-//                   children's update blocks by extend-add, children in a fixed order (no atomics: each
-//                   workgroup owns its target columns)
+//   chol_asm_tile   one workgroup per lower 64 x 64 front tile: the children's update blocks gathered through
+//                   their position maps (extend-add as a gather, children in a fixed order, no atomics)
+//   chol_asm_entries A's entries (+ W on the diagonal) added to the panel columns
 //   chol_diag       one workgroup (4 waves) per 64 x 64 diagonal block: the Cholesky pivots and the
 //                   block inverse W = L^-1 in one register-resident sweep (row r of L and column r of
 //                   W on lane r, columns / rows split over the waves, the pivot column broadcast
@@ -33,7 +33,7 @@ namespace {
 typedef double double4_t __attribute__((ext_vector_type(4)));
 
 struct Bufs {
-  double* p[4];   // kCbF, kCbS, kCbW, kCbY
+  double* p[5];   // kCbF, kCbS, kCbW, kCbY, kCbP
 };
 
 struct DevPlan {
@@ -47,6 +47,8 @@ struct DevPlan {
   const int* child;
   const int* sparent;
   const int* perm;
+  const int64_t* cinv_off;
+  const int* cinv;
 };
 
 __device__ __forceinline__ int lower_bound_dev(const int* a, int n, int v) {
@@ -89,48 +91,78 @@ __global__ void __launch_bounds__(256) chol_entry_values_kernel(int64_t ne, cons
   }
 }
 
-// ---- front assembly (factorization): columns [c0, c1) of supernode s
-__global__ void __launch_bounds__(256) chol_assemble_kernel(const CholColTask* __restrict__ tasks, int64_t t0,
-                                                            DevPlan P, double* __restrict__ F,
-                                                            const int64_t* __restrict__ ecol,
-                                                            const int64_t* __restrict__ eoff,
-                                                            const double* __restrict__ aval,
-                                                            const double* __restrict__ W) {
+// ---- front assembly (factorization), two launches per level:
+// (1) one workgroup per lower 64 x 64 tile of a front: F[i][j] = sum over the children of U_child[inv(i)][inv(j)]
+//     (the extend-add as a gather through the children's position maps, children in a fixed order; zero where
+//     no child contributes), so every tile of every front of the level is written in parallel;
+// (2) A's entries of the panel columns (and W on the diagonal) added, one target per entry.
+__global__ void __launch_bounds__(256) chol_asm_tile_kernel(const CholColTask* __restrict__ tasks, int64_t t0,
+                                                            DevPlan P, double* __restrict__ F, int* info_reset) {
   const CholColTask tk = tasks[t0 + blockIdx.x];
-  const int s = tk.s;
-  const int sf = P.sfirst[s], ns = P.sfirst[s + 1] - sf;
-  const int nr = (int)(P.rptr[s + 1] - P.rptr[s]);
-  const int fs = ns + nr;
-  double* Fs = F + P.foff[s];
+  if (info_reset != nullptr && blockIdx.x == 0 && threadIdx.x == 0) *info_reset = 0;   // first op of a factorization
+  const int s = tk.s, rt = tk.c0, ct = tk.c1;
+  const int ns = P.sfirst[s + 1] - P.sfirst[s];
+  const int fs = ns + (int)(P.rptr[s + 1] - P.rptr[s]);
+  __shared__ int ri[64], ci[64];
   const int tid = threadIdx.x;
-  for (int j = tk.c0; j < tk.c1; ++j)
-    for (int r = j + tid; r < fs; r += 256) Fs[r + (size_t)j * fs] = 0.;
-  __syncthreads();
-  const int jend = min(tk.c1, ns);
-  for (int j = tk.c0; j < jend; ++j) {
-    const int g = sf + j;
-    const int64_t e0 = ecol[g], e1 = ecol[g + 1];
-    for (int64_t e = e0 + tid; e < e1; e += 256) {
-      double v = aval[e];
-      if (e == e0 && W != nullptr) v += W[P.perm[g]];   // the diagonal leads its column
-      F[eoff[e]] = v;
+  const int ii = tid & 63;
+  double acc[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.;
+  for (int qc = P.cptr[s]; qc < P.cptr[s + 1]; ++qc) {
+    const int ch = P.child[qc];
+    const int* inv = P.cinv + P.cinv_off[ch];
+    __syncthreads();
+    if (tid < 64) ri[tid] = rt + tid < fs ? inv[rt + tid] : -1;
+    else if (tid < 128) ci[tid - 64] = ct + tid - 64 < fs ? inv[ct + tid - 64] : -1;
+    __syncthreads();
+    const int nsc = P.sfirst[ch + 1] - P.sfirst[ch];
+    const int fc = nsc + (int)(P.rptr[ch + 1] - P.rptr[ch]);
+    const double* U = F + P.foff[ch] + nsc + (size_t)nsc * fc;
+    const int ia = ri[ii];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int ib = ci[(tid >> 6) + 4 * q];
+      if (ia >= 0 && ib >= 0 && ia >= ib) acc[q] += U[ia + (size_t)ib * fc];
     }
   }
-  for (int q = P.cptr[s]; q < P.cptr[s + 1]; ++q) {
+  const int i = rt + ii;
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int j = ct + (tid >> 6) + 4 * q;
+    if (i < fs && j < fs && i >= j) F[P.foff[s] + i + (size_t)j * fs] = acc[q];
+  }
+}
+
+__global__ void __launch_bounds__(256) chol_asm_entries_kernel(const CholColTask* __restrict__ tasks, int64_t t0,
+                                                               DevPlan P, double* __restrict__ F,
+                                                               const int64_t* __restrict__ ecol,
+                                                               const int64_t* __restrict__ eoff,
+                                                               const double* __restrict__ aval,
+                                                               const double* __restrict__ W) {
+  const CholColTask tk = tasks[t0 + blockIdx.x];
+  const int sf = P.sfirst[tk.s];
+  const int64_t e0 = ecol[sf + tk.c0], e1 = ecol[sf + tk.c1];
+  for (int64_t e = e0 + threadIdx.x; e < e1; e += 256) F[eoff[e]] += aval[e];
+  if (W != nullptr) {   // the diagonal leads each column's entries
     __syncthreads();
-    const int ch = P.child[q];
-    const int nsc = P.sfirst[ch + 1] - P.sfirst[ch];
-    const int nrc = (int)(P.rptr[ch + 1] - P.rptr[ch]);
-    const int fc = nsc + nrc;
-    const int* rel = P.rel + P.rptr[ch];
-    const double* U = F + P.foff[ch] + nsc + (size_t)nsc * fc;
-    const int b0 = lower_bound_dev(rel, nrc, tk.c0), b1 = lower_bound_dev(rel, nrc, tk.c1);
-    for (int b = b0; b < b1; ++b) {
-      const int tb = rel[b];
-      double* dst = Fs + (size_t)tb * fs;
-      const double* src = U + (size_t)b * fc;
-      for (int a = b + tid; a < nrc; a += 256) dst[rel[a]] += src[a];
-    }
+    for (int j = tk.c0 + threadIdx.x; j < tk.c1; j += 256) F[eoff[ecol[sf + j]]] += W[P.perm[sf + j]];
+  }
+}
+
+// ---- split-K reduction: C = beta C + alpha sum of the P slices (64 x 64, ld 64)
+__global__ void __launch_bounds__(256) chol_reduce_kernel(const CholReduceTask* __restrict__ tasks, int64_t t0,
+                                                          Bufs bufs) {
+  const CholReduceTask r = tasks[t0 + blockIdx.x];
+  double* C = bufs.p[r.bufc] + r.c;
+  const double* Pb = bufs.p[kCbP] + r.p;
+  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+    const int i = e & 63, j = e >> 6;
+    if (i >= r.M || j >= r.N) continue;
+    double s = 0.;
+    for (int q = 0; q < r.nslices; ++q) s += Pb[(size_t)q * r.pstride + i + j * 64];
+    double* c = C + i + (size_t)j * r.ldc;
+    *c = (r.beta == 0. ? 0. : r.beta * (*c)) + r.alpha * s;
   }
 }
 
@@ -201,9 +233,9 @@ __global__ void __launch_bounds__(256) chol_diag_kernel(const CholDiagTask* __re
 constexpr int GT = 64, GK = 16;
 __global__ void __launch_bounds__(256) chol_gemm_kernel(const CholGemmTask* __restrict__ tasks, int64_t t0, Bufs bufs) {
   const CholGemmTask g = tasks[t0 + blockIdx.x];
-  const double* A = bufs.p[(g.flags >> 4) & 3] + g.a;
-  const double* B = bufs.p[(g.flags >> 6) & 3] + g.b;
-  double* C = bufs.p[(g.flags >> 8) & 3] + g.c;
+  const double* A = bufs.p[(g.flags >> 4) & 7] + g.a;
+  const double* B = bufs.p[(g.flags >> 7) & 7] + g.b;
+  double* C = bufs.p[(g.flags >> 10) & 7] + g.c;
   const bool ta = g.flags & kCgTA, tb = g.flags & kCgTB;
   __shared__ double As[2][GK][GT + 1];
   __shared__ double Bs[2][GK][GT + 1];
@@ -306,29 +338,26 @@ __global__ void __launch_bounds__(256) chol_gather_s_kernel(const CholColTask* _
   }
 }
 
-// S[j, r] = S[r, j] for front columns j in [c0, c1) and rows r > j (LDS-transposed 64 x 64 tiles)
+// S[j, r] = S[r, j] for front columns j in [c0, c1) and rows r > j of the 64-row tile at pad (LDS-transposed)
 __global__ void __launch_bounds__(256) chol_mirror_kernel(const CholColTask* __restrict__ tasks, int64_t t0,
                                                           DevPlan P, double* __restrict__ S) {
   const CholColTask tk = tasks[t0 + blockIdx.x];
-  const int s = tk.s;
+  const int s = tk.s, R0 = tk.pad;
   const int ns = P.sfirst[s + 1] - P.sfirst[s];
   const int fs = ns + (int)(P.rptr[s + 1] - P.rptr[s]);
   double* Ss = S + P.foff[s];
   __shared__ double T[64][65];
   const int nc = tk.c1 - tk.c0;
   const int tid = threadIdx.x;
-  for (int R0 = tk.c0; R0 < fs; R0 += 64) {
-    __syncthreads();
-    for (int e = tid; e < 64 * 64; e += 256) {
-      const int rr = e & 63, cc = e >> 6;
-      if (cc < nc && R0 + rr < fs) T[rr][cc] = Ss[(R0 + rr) + (size_t)(tk.c0 + cc) * fs];
-    }
-    __syncthreads();
-    for (int e = tid; e < 64 * 64; e += 256) {
-      const int cc = e & 63, rr = e >> 6;
-      const int row = R0 + rr, col = tk.c0 + cc;
-      if (cc < nc && row < fs && row > col) Ss[col + (size_t)row * fs] = T[rr][cc];
-    }
+  for (int e = tid; e < 64 * 64; e += 256) {
+    const int rr = e & 63, cc = e >> 6;
+    if (cc < nc && R0 + rr < fs) T[rr][cc] = Ss[(R0 + rr) + (size_t)(tk.c0 + cc) * fs];
+  }
+  __syncthreads();
+  for (int e = tid; e < 64 * 64; e += 256) {
+    const int cc = e & 63, rr = e >> 6;
+    const int row = R0 + rr, col = tk.c0 + cc;
+    if (cc < nc && row < fs && row > col) Ss[col + (size_t)row * fs] = T[rr][cc];
   }
 }
 
@@ -386,6 +415,111 @@ __global__ void __launch_bounds__(256) chol_scatter_x_kernel(const CholColTask* 
   const double* V = a.V + a.vofs[s];
   for (int k = 0; k < a.t; ++k)
     for (int i = tk.c0 + threadIdx.x; i < tk.c1; i += 256) a.X[P.perm[sf + i] + (size_t)k * P.n] = V[i + (size_t)k * fs];
+}
+
+// ---- single right-hand side: one workgroup per supernode of a level runs its whole panel (the forward
+// sweep assembles its front vector from b and the children, then per 64-column block x_b = W_b v_b and
+// v[below] -= L[below, b] x_b; the backward sweep gathers x at its rows R_s, then per block from the last
+// v_b -= L[below, b]^T v[below] (one wave per 16 columns, wave-reduced) and x_b = W_b^T v_b), so a solve is
+// two launches per tree level instead of one per block step.
+struct Solve1Args {
+  const int* lvl_sup;
+  int l0;
+  const double* F;
+  const double* Wd;
+  const int64_t* woff;
+  double* V;
+  const int64_t* vofs;
+  const double* b;
+  double* x;
+};
+
+__global__ void __launch_bounds__(256) chol_fsolve1_kernel(DevPlan P, Solve1Args a) {
+  const int s = a.lvl_sup[a.l0 + blockIdx.x];
+  const int sf = P.sfirst[s], ns = P.sfirst[s + 1] - sf;
+  const int fs = ns + (int)(P.rptr[s + 1] - P.rptr[s]);
+  double* V = a.V + a.vofs[s];
+  const double* L = a.F + P.foff[s];
+  const int tid = threadIdx.x;
+  for (int r = tid; r < fs; r += 256) V[r] = r < ns ? a.b[P.perm[sf + r]] : 0.;
+  for (int q = P.cptr[s]; q < P.cptr[s + 1]; ++q) {
+    __syncthreads();
+    const int ch = P.child[q];
+    const int nsc = P.sfirst[ch + 1] - P.sfirst[ch];
+    const int nrc = (int)(P.rptr[ch + 1] - P.rptr[ch]);
+    const int* rel = P.rel + P.rptr[ch];
+    const double* Vc = a.V + a.vofs[ch] + nsc;
+    for (int i = tid; i < nrc; i += 256) V[rel[i]] += Vc[i];
+  }
+  __shared__ double vb[64], xb[64];
+  const int nblk = (ns + 63) / 64;
+  for (int k = 0; k < nblk; ++k) {
+    const int j0 = 64 * k, ib = min(64, ns - j0);
+    __syncthreads();
+    if (tid < 64) vb[tid] = tid < ib ? V[j0 + tid] : 0.;
+    __syncthreads();
+    if (tid < ib) {
+      const double* W = a.Wd + a.woff[s] + (int64_t)k * 4096;
+      double x = 0.;
+      for (int j = 0; j <= tid; ++j) x = fma(W[tid + j * 64], vb[j], x);
+      xb[tid] = x;
+      V[j0 + tid] = x;
+    }
+    __syncthreads();
+    for (int r = j0 + ib + tid; r < fs; r += 256) {
+      double acc = V[r];
+      const double* Lr = L + r + (size_t)j0 * fs;
+      for (int j = 0; j < ib; ++j) acc = fma(-Lr[(size_t)j * fs], xb[j], acc);
+      V[r] = acc;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256) chol_bsolve1_kernel(DevPlan P, Solve1Args a) {
+  const int s = a.lvl_sup[a.l0 + blockIdx.x];
+  const int sf = P.sfirst[s], ns = P.sfirst[s + 1] - sf;
+  const int nr = (int)(P.rptr[s + 1] - P.rptr[s]);
+  const int fs = ns + nr;
+  double* V = a.V + a.vofs[s];
+  const double* L = a.F + P.foff[s];
+  const int* R = P.rows + P.rptr[s];
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = tid; i < nr; i += 256) V[ns + i] = a.x[P.perm[R[i]]];
+  __shared__ double vb[64], dsum[64];
+  const int nblk = (ns + 63) / 64;
+  for (int k = nblk - 1; k >= 0; --k) {
+    const int j0 = 64 * k, ib = min(64, ns - j0), r0 = j0 + ib;
+    __syncthreads();
+    double acc[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = 0.;
+    for (int r = r0 + lane; r < fs; r += 64) {
+      const double vr = V[r];
+      const double* Lr = L + r + (size_t)j0 * fs;
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int j = w + 4 * q;
+        if (j < ib) acc[q] = fma(Lr[(size_t)j * fs], vr, acc[q]);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      double v = acc[q];
+      for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+      if (lane == 0) dsum[w + 4 * q] = v;
+    }
+    __syncthreads();
+    if (tid < 64) vb[tid] = tid < ib ? V[j0 + tid] - dsum[tid] : 0.;
+    __syncthreads();
+    if (tid < ib) {
+      const double* W = a.Wd + a.woff[s] + (int64_t)k * 4096;
+      double x = 0.;
+      for (int j = tid; j < ib; ++j) x = fma(W[j + tid * 64], vb[j], x);
+      V[j0 + tid] = x;
+    }
+  }
+  __syncthreads();
+  for (int i = tid; i < ns; i += 256) a.x[P.perm[sf + i]] = V[i];
 }
 
 // ---- reductions (two passes, fixed order)
@@ -475,14 +609,17 @@ struct SparseCholDev {
   DevBuf<CholGemmTask> gemm;
   DevBuf<CholDiagTask> diag;
   DevBuf<CholColTask> col;
+  DevBuf<CholReduceTask> red;
   std::vector<CholOp> ops;
-  int64_t y_doubles = 0;
+  int64_t y_doubles = 0, p_doubles = 0;
   void Upload(const CholSchedule& S) {
     upload(gemm, S.gemm);
     upload(diag, S.diag);
     upload(col, S.col);
+    upload(red, S.red);
     ops = S.ops;
     y_doubles = S.y_doubles;
+    p_doubles = S.p_doubles;
   }
 };
 
@@ -513,11 +650,21 @@ SparseChol::SparseChol(int n, int m, const int* nbr, int d, const double* X, hip
   upload(d_cptr_, P.cptr);
   upload(d_child_, P.child);
   upload(d_sparent_, P.sparent);
+  upload(d_cinv_off_, P.cinv_off);
+  upload(d_cinv_, P.cinv);
   upload(d_ecol_, E.ecol);
   upload(d_eoff_, E.eoff);
   upload(d_ecptr_, E.cptr);
   upload(d_ctr_, E.ctr);
   upload(d_dpos_, E.dpos);
+  upload(d_lvl_sup_, P.lvl_sup);
+  upload(d_woff_, P.woff);
+  {
+    std::vector<int64_t> v1(P.nsup + 1, 0);
+    for (int s = 0; s < P.nsup; ++s) v1[s + 1] = v1[s] + P.fs(s);
+    vofs1_total_ = v1[P.nsup];
+    upload(d_vofs1_, v1);
+  }
   impl_->factor.Upload(P.factor);
   impl_->selinv.Upload(P.selinv);
   DevPlan& dp = impl_->dp;
@@ -531,6 +678,8 @@ SparseChol::SparseChol(int n, int m, const int* nbr, int d, const double* X, hip
   dp.child = d_child_.get();
   dp.sparent = d_sparent_.get();
   dp.perm = d_perm_.get();
+  dp.cinv_off = d_cinv_off_.get();
+  dp.cinv = d_cinv_.get();
   d_F_.alloc(std::max<int64_t>(P.front_doubles, 1));
   d_Wd_.alloc(std::max<int64_t>(P.woff[P.nsup], 1));
   d_aval_.alloc(std::max<int64_t>(nent_, 1));
@@ -555,13 +704,18 @@ void SparseChol::SetB(const double* Bv, const double* Dinv, const double* dBv, c
 }
 
 void SparseChol::Run(const SparseCholDev& sch, double* ybuf, const void* solve_args) {
-  Bufs b{{d_F_.get(), d_S_.get(), d_Wd_.get(), ybuf}};
+  if ((int64_t)d_P_.size() < sch.p_doubles) d_P_.alloc(sch.p_doubles);
+  Bufs b{{d_F_.get(), d_S_.get(), d_Wd_.get(), ybuf, d_P_.get()}};
   const DevPlan& dp = impl_->dp;
   for (const CholOp& op : sch.ops) {
     const dim3 grid(op.ntask);
     switch (op.type) {
-      case kOpAssemble:
-        hipLaunchKernelGGL(chol_assemble_kernel, grid, dim3(256), 0, s_, sch.col.get(), op.task0, dp, d_F_.get(),
+      case kOpAsmTile:
+        hipLaunchKernelGGL(chol_asm_tile_kernel, grid, dim3(256), 0, s_, sch.col.get(), op.task0, dp, d_F_.get(),
+                           (&op == &sch.ops.front() && &sch == &impl_->factor) ? d_info_.get() : nullptr);
+        break;
+      case kOpAsmEntries:
+        hipLaunchKernelGGL(chol_asm_entries_kernel, grid, dim3(256), 0, s_, sch.col.get(), op.task0, dp, d_F_.get(),
                            d_ecol_.get(), d_eoff_.get(), d_aval_.get(), cur_W_);
         break;
       case kOpDiag:
@@ -570,6 +724,9 @@ void SparseChol::Run(const SparseCholDev& sch, double* ybuf, const void* solve_a
         break;
       case kOpGemm:
         hipLaunchKernelGGL(chol_gemm_kernel, grid, dim3(256), 0, s_, sch.gemm.get(), op.task0, b);
+        break;
+      case kOpReduce:
+        hipLaunchKernelGGL(chol_reduce_kernel, grid, dim3(256), 0, s_, sch.red.get(), op.task0, b);
         break;
       case kOpGatherS:
         hipLaunchKernelGGL(chol_gather_s_kernel, grid, dim3(256), 0, s_, sch.col.get(), op.task0, dp, d_S_.get());
@@ -589,6 +746,16 @@ void SparseChol::Run(const SparseCholDev& sch, double* ybuf, const void* solve_a
         hipLaunchKernelGGL(chol_scatter_x_kernel, grid, dim3(256), 0, s_, sch.col.get(), op.task0, dp,
                            *static_cast<const SolveArgs*>(solve_args));
         break;
+      case kOpFSolve1:
+      case kOpBSolve1: {
+        const SolveArgs& sa = *static_cast<const SolveArgs*>(solve_args);
+        Solve1Args a1{d_lvl_sup_.get(), (int)op.task0, d_F_.get(), d_Wd_.get(), d_woff_.get(), sa.V, sa.vofs, sa.b, sa.X};
+        if (op.type == kOpFSolve1)
+          hipLaunchKernelGGL(chol_fsolve1_kernel, grid, dim3(256), 0, s_, dp, a1);
+        else
+          hipLaunchKernelGGL(chol_bsolve1_kernel, grid, dim3(256), 0, s_, dp, a1);
+        break;
+      }
       default:
         Fatal("sparse Cholesky: unknown op %d", op.type);
     }
@@ -597,7 +764,7 @@ void SparseChol::Run(const SparseCholDev& sch, double* ybuf, const void* solve_a
 }
 
 void SparseChol::Factor(const double* W) {
-  HIP_CHECK(hipMemsetAsync(d_info_.get(), 0, sizeof(int), s_));
+  // (the info counter is reset by the first assembly launch)
   HIP_CHECK(hipEventRecord(ev0_, s_));
   cur_W_ = W;
   Run(impl_->factor, nullptr, nullptr);

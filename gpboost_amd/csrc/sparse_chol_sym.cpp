@@ -380,6 +380,10 @@ void chol_analyze(int n, int m, const int* nbr, int d, const double* X, int leaf
 // assembles), the selected inverse root-first (a child reads its parent's finished S block).
 namespace {
 
+constexpr int kSplitK = 512;        // K chunk of the selected inverse's long products
+constexpr int kSplitKSolve = 256;   // K chunk of the backward solve's transposed products
+constexpr int64_t kSmallPanel = 64 * 1024;   // fs x ns of the largest panel a single-workgroup level sweep takes
+
 CholGemmTask gemm_task(int bufa, int64_t a, int lda, int bufb, int64_t b, int ldb, int bufc, int64_t c, int ldc, int M,
                        int N, int K, int flags, int doff, double alpha, double beta) {
   CholGemmTask t;
@@ -397,13 +401,16 @@ struct OpBuilder {
   explicit OpBuilder(CholSchedule& s) : S(s) {}
   int type = -1;
   int64_t t0 = 0;
+  int64_t count(int ty) const {
+    return ty == kOpDiag ? (int64_t)S.diag.size() : ty == kOpGemm ? (int64_t)S.gemm.size()
+                          : ty == kOpReduce ? (int64_t)S.red.size() : (int64_t)S.col.size();
+  }
   void begin(int ty) {
     type = ty;
-    t0 = ty == kOpDiag ? (int64_t)S.diag.size() : ty == kOpGemm ? (int64_t)S.gemm.size() : (int64_t)S.col.size();
+    t0 = count(ty);
   }
   void end() {
-    const int64_t t1 = type == kOpDiag ? (int64_t)S.diag.size() : type == kOpGemm ? (int64_t)S.gemm.size()
-                                                                                   : (int64_t)S.col.size();
+    const int64_t t1 = count(type);
     if (t1 > t0) S.ops.push_back(CholOp{type, (int)(t1 - t0), t0});
   }
 };
@@ -419,10 +426,17 @@ void build_factor_schedule(const CholPlan& P, CholSchedule& S) {
   OpBuilder ob(S);
   const int nlev = (int)P.lvl_ptr.size() - 1;
   for (int l = 0; l < nlev; ++l) {
-    ob.begin(kOpAssemble);
+    ob.begin(kOpAsmTile);   // every lower 64 x 64 tile of the level's fronts: the children's update blocks
     for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) {
       const int s = P.lvl_sup[q], fs = P.fs(s);
-      for (int c0 = 0; c0 < fs; c0 += 64) S.col.push_back(CholColTask{s, c0, std::min(c0 + 64, fs), 0});
+      for (int ct = 0; ct < fs; ct += 64)
+        for (int rt = ct; rt < fs; rt += 64) S.col.push_back(CholColTask{s, rt, ct, 0});
+    }
+    ob.end();
+    ob.begin(kOpAsmEntries);   // + A's entries (and W) of the panel columns
+    for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) {
+      const int s = P.lvl_sup[q], ns = P.ns(s);
+      for (int j0 = 0; j0 < ns; j0 += 16) S.col.push_back(CholColTask{s, j0, std::min(j0 + 16, ns), 0});
     }
     ob.end();
     const int mb = level_maxblk(P, l);
@@ -513,34 +527,72 @@ void build_selinv_schedule(const CholPlan& P, CholSchedule& S) {
                                    0, 1., 0.));
       }
       ob.end();
-      ob.begin(kOpGemm);   // S[R_b, b] = -S[R_b, R_b] Y
-      for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) {
-        const int s = P.lvl_sup[q];
-        if (P.nblk(s) <= k) continue;
-        const int fs = P.fs(s), j0 = 64 * k, ib = std::min(64, P.ns(s) - j0), r0 = j0 + ib, fr = fs - r0;
-        const int64_t base = P.foff[s];
-        for (int rt = 0; rt < fr; rt += 64)
-          S.gemm.push_back(gemm_task(kCbS, base + r0 + rt + (int64_t)r0 * fs, fs, kCbY, yoff[s], fr, kCbS,
-                                     base + r0 + rt + (int64_t)j0 * fs, fs, std::min(64, fr - rt), ib, fr, 0, 0, -1., 0.));
+      // S[R_b, b] = -S[R_b, R_b] Y: split K into kSplitK chunks (partials in P, then one reduce per row tile)
+      {
+        std::vector<CholReduceTask> reds;
+        int64_t pb = 0;
+        ob.begin(kOpGemm);
+        for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) {
+          const int s = P.lvl_sup[q];
+          if (P.nblk(s) <= k) continue;
+          const int fs = P.fs(s), j0 = 64 * k, ib = std::min(64, P.ns(s) - j0), r0 = j0 + ib, fr = fs - r0;
+          const int64_t base = P.foff[s];
+          const int nch = (fr + kSplitK - 1) / kSplitK;
+          for (int rt = 0; rt < fr; rt += 64) {
+            const int M = std::min(64, fr - rt);
+            for (int kc = 0; kc < nch; ++kc) {
+              const int k0 = kc * kSplitK, K = std::min(kSplitK, fr - k0);
+              S.gemm.push_back(gemm_task(kCbS, base + r0 + rt + (int64_t)(r0 + k0) * fs, fs, kCbY, yoff[s] + k0, fr,
+                                         kCbP, pb + (int64_t)kc * 4096, 64, M, ib, K, 0, 0, 1., 0.));
+            }
+            CholReduceTask rd{};
+            rd.c = base + r0 + rt + (int64_t)j0 * fs; rd.ldc = fs; rd.M = M; rd.N = ib; rd.bufc = kCbS;
+            rd.p = pb; rd.pstride = 4096; rd.nslices = nch; rd.alpha = -1.; rd.beta = 0.;
+            reds.push_back(rd);
+            pb += (int64_t)nch * 4096;
+          }
+        }
+        ob.end();
+        S.p_doubles = std::max(S.p_doubles, pb);
+        ob.begin(kOpReduce);
+        S.red.insert(S.red.end(), reds.begin(), reds.end());
+        ob.end();
       }
-      ob.end();
-      ob.begin(kOpGemm);   // S_bb -= Y^T S[R_b, b]
-      for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) {
-        const int s = P.lvl_sup[q];
-        if (P.nblk(s) <= k) continue;
-        const int fs = P.fs(s), j0 = 64 * k, ib = std::min(64, P.ns(s) - j0), r0 = j0 + ib, fr = fs - r0;
-        if (fr == 0) continue;
-        const int64_t base = P.foff[s];
-        S.gemm.push_back(gemm_task(kCbY, yoff[s], fr, kCbS, base + r0 + (int64_t)j0 * fs, fs, kCbS,
-                                   base + j0 + (int64_t)j0 * fs, fs, ib, ib, fr, kCgTA, 0, -1., 1.));
+      // S_bb -= Y^T S[R_b, b] (split K)
+      {
+        std::vector<CholReduceTask> reds;
+        int64_t pb = 0;
+        ob.begin(kOpGemm);
+        for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) {
+          const int s = P.lvl_sup[q];
+          if (P.nblk(s) <= k) continue;
+          const int fs = P.fs(s), j0 = 64 * k, ib = std::min(64, P.ns(s) - j0), r0 = j0 + ib, fr = fs - r0;
+          if (fr == 0) continue;
+          const int64_t base = P.foff[s];
+          const int nch = (fr + kSplitK - 1) / kSplitK;
+          for (int kc = 0; kc < nch; ++kc) {
+            const int k0 = kc * kSplitK, K = std::min(kSplitK, fr - k0);
+            S.gemm.push_back(gemm_task(kCbY, yoff[s] + k0, fr, kCbS, base + r0 + k0 + (int64_t)j0 * fs, fs, kCbP,
+                                       pb + (int64_t)kc * 4096, 64, ib, ib, K, kCgTA, 0, 1., 0.));
+          }
+          CholReduceTask rd{};
+          rd.c = base + j0 + (int64_t)j0 * fs; rd.ldc = fs; rd.M = ib; rd.N = ib; rd.bufc = kCbS;
+          rd.p = pb; rd.pstride = 4096; rd.nslices = nch; rd.alpha = -1.; rd.beta = 1.;
+          reds.push_back(rd);
+          pb += (int64_t)nch * 4096;
+        }
+        ob.end();
+        S.p_doubles = std::max(S.p_doubles, pb);
+        ob.begin(kOpReduce);
+        S.red.insert(S.red.end(), reds.begin(), reds.end());
+        ob.end();
       }
-      ob.end();
-      ob.begin(kOpMirror);   // S[b, b..fs) = S[b..fs, b]^T
+      ob.begin(kOpMirror);   // S[b, b..fs) = S[b..fs, b]^T, one task per 64-row tile
       for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) {
         const int s = P.lvl_sup[q];
         if (P.nblk(s) <= k) continue;
         const int j0 = 64 * k, ib = std::min(64, P.ns(s) - j0);
-        S.col.push_back(CholColTask{s, j0, j0 + ib, 0});
+        for (int R0 = j0; R0 < P.fs(s); R0 += 64) S.col.push_back(CholColTask{s, j0, j0 + ib, R0});
       }
       ob.end();
     }
@@ -556,7 +608,20 @@ void chol_solve_schedule(const CholPlan& P, int t, bool forward_only, CholSchedu
   for (int s = 0; s < P.nsup; ++s) vofs[s + 1] = vofs[s] + (int64_t)P.fs(s) * t;
   S.y_doubles = vofs[P.nsup];
   const int nlev = (int)P.lvl_ptr.size() - 1;
+  // t = 1: levels whose panels are all small run one workgroup per supernode (two launches per level); the
+  // levels of large separators keep the tiled form (its parallelism over row tiles)
+  std::vector<char> small(nlev, 0);
+  if (t == 1)
+    for (int l = 0; l < nlev; ++l) {
+      int64_t mx = 0;
+      for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) mx = std::max<int64_t>(mx, (int64_t)P.fs(P.lvl_sup[q]) * P.ns(P.lvl_sup[q]));
+      small[l] = mx <= kSmallPanel;
+    }
   for (int l = 0; l < nlev; ++l) {
+    if (small[l] && !forward_only) {
+      S.ops.push_back(CholOp{kOpFSolve1, P.lvl_ptr[l + 1] - P.lvl_ptr[l], (int64_t)P.lvl_ptr[l]});
+      continue;
+    }
     ob.begin(kOpAsmV);
     for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) {
       const int s = P.lvl_sup[q];
@@ -601,6 +666,10 @@ void chol_solve_schedule(const CholPlan& P, int t, bool forward_only, CholSchedu
   }
   if (forward_only) return;
   for (int l = nlev - 1; l >= 0; --l) {
+    if (small[l]) {
+      S.ops.push_back(CholOp{kOpBSolve1, P.lvl_ptr[l + 1] - P.lvl_ptr[l], (int64_t)P.lvl_ptr[l]});
+      continue;
+    }
     ob.begin(kOpGatherX);
     for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) {
       const int s = P.lvl_sup[q];
@@ -609,18 +678,37 @@ void chol_solve_schedule(const CholPlan& P, int t, bool forward_only, CholSchedu
     ob.end();
     const int mb = level_maxblk(P, l);
     for (int k = mb - 1; k >= 0; --k) {
-      ob.begin(kOpGemm);   // v_b -= L[r0:fs, b]^T v[r0:fs]
-      for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) {
-        const int s = P.lvl_sup[q];
-        if (P.nblk(s) <= k) continue;
-        const int fs = P.fs(s), j0 = 64 * k, ib = std::min(64, P.ns(s) - j0), r0 = j0 + ib;
-        if (r0 == fs) continue;
-        for (int ct = 0; ct < t; ct += 64)
-          S.gemm.push_back(gemm_task(kCbF, P.foff[s] + r0 + (int64_t)j0 * fs, fs, kCbY,
-                                     vofs[s] + r0 + (int64_t)ct * fs, fs, kCbY, vofs[s] + j0 + (int64_t)ct * fs, fs, ib,
-                                     std::min(64, t - ct), fs - r0, kCgTA, 0, -1., 1.));
+      {   // v_b -= L[r0:fs, b]^T v[r0:fs] (split K: partials in P, then one reduce per column chunk)
+        std::vector<CholReduceTask> reds;
+        int64_t pb = 0;
+        ob.begin(kOpGemm);
+        for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) {
+          const int s = P.lvl_sup[q];
+          if (P.nblk(s) <= k) continue;
+          const int fs = P.fs(s), j0 = 64 * k, ib = std::min(64, P.ns(s) - j0), r0 = j0 + ib, fr = fs - r0;
+          if (fr == 0) continue;
+          const int nch = (fr + kSplitKSolve - 1) / kSplitKSolve;
+          for (int ct = 0; ct < t; ct += 64) {
+            const int N = std::min(64, t - ct);
+            for (int kc = 0; kc < nch; ++kc) {
+              const int k0 = kc * kSplitKSolve, K = std::min(kSplitKSolve, fr - k0);
+              S.gemm.push_back(gemm_task(kCbF, P.foff[s] + r0 + k0 + (int64_t)j0 * fs, fs, kCbY,
+                                         vofs[s] + r0 + k0 + (int64_t)ct * fs, fs, kCbP, pb + (int64_t)kc * 4096, 64,
+                                         ib, N, K, kCgTA, 0, 1., 0.));
+            }
+            CholReduceTask rd{};
+            rd.c = vofs[s] + j0 + (int64_t)ct * fs; rd.ldc = fs; rd.M = ib; rd.N = N; rd.bufc = kCbY;
+            rd.p = pb; rd.pstride = 4096; rd.nslices = nch; rd.alpha = -1.; rd.beta = 1.;
+            reds.push_back(rd);
+            pb += (int64_t)nch * 4096;
+          }
+        }
+        ob.end();
+        S.p_doubles = std::max(S.p_doubles, pb);
+        ob.begin(kOpReduce);
+        S.red.insert(S.red.end(), reds.begin(), reds.end());
+        ob.end();
       }
-      ob.end();
       ob.begin(kOpGemm);   // x_b = W_b^T v_b (in place)
       for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) {
         const int s = P.lvl_sup[q];
@@ -674,6 +762,13 @@ void chol_finish_plan(CholPlan& P) {
     std::vector<int> pos(P.cptr.begin(), P.cptr.end() - 1);
     for (int s = 0; s < P.nsup; ++s)
       if (P.sparent[s] >= 0) P.child[pos[P.sparent[s]]++] = s;
+  }
+  P.cinv_off.assign(P.nsup + 1, 0);
+  for (int s = 0; s < P.nsup; ++s) P.cinv_off[s + 1] = P.cinv_off[s] + (P.sparent[s] >= 0 ? P.fs(P.sparent[s]) : 0);
+  P.cinv.assign(std::max<int64_t>(P.cinv_off[P.nsup], 1), -1);
+  for (int s = 0; s < P.nsup; ++s) {
+    if (P.sparent[s] < 0) continue;
+    for (int a = 0; a < P.nr(s); ++a) P.cinv[P.cinv_off[s] + P.rel[P.rptr[s] + a]] = a;
   }
   P.woff.assign(P.nsup + 1, 0);
   for (int s = 0; s < P.nsup; ++s) P.woff[s + 1] = P.woff[s] + (int64_t)P.nblk(s) * 4096;

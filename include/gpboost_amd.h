@@ -330,6 +330,14 @@ GPBOOST_AMD_EXPORT int GPB_GetLatentVecchiaFactor(REModelHandle handle, const do
  * block CG, info[3] the estimate of log|Sigma W + I|. */
 GPBOOST_AMD_EXPORT int GPB_GetLastIterationInfo(REModelHandle handle, double* info);
 
+/* Latent Vecchia models with matrix_inversion_method = "cholesky" (the sparse Cholesky of Sigma^-1 + W;
+ * replaces the reference's SimplicialLLT analyzePattern / factorize, likelihoods.h:2946-2950): statistics of
+ * the symbolic plan (built on first use): info[0] supernodes, info[1] levels of the supernodal tree,
+ * info[2] entries of L (incl. amalgamation zeros), info[3] doubles of the dense fronts, info[4]
+ * factorization flops, info[5] largest front, info[6] widest supernode, info[7] host analysis time (ms),
+ * info[8] device time of the last factorization (ms). No reference counterpart (measurement only). */
+GPBOOST_AMD_EXPORT int GPB_GetCholeskyPlanInfo(REModelHandle handle, double* info);
+
 /* Timing of the last evaluation's dominant kernel (ms, HIP events on the model's stream),
  * for the benchmark's live roofline. kernel_ms[0] = factor/Cholesky kernel,
  * kernel_ms[1] = whole device-side evaluation. Exact Vecchia models record the events only for

@@ -21,11 +21,11 @@ using namespace gpb_amd;
 
 struct Exec {
   const CholPlan& P;
-  std::vector<double>& F; std::vector<double>& S; std::vector<double>& Wd; std::vector<double>& Y;
+  std::vector<double>& F; std::vector<double>& S; std::vector<double>& Wd; std::vector<double>& Y; std::vector<double>& Pp;
   const std::vector<double>* A;   // dense n x n (matrix labels)
   int n;
   const double* b = nullptr; double* X = nullptr; int t = 1; const std::vector<int64_t>* vofs = nullptr;
-  double* buf(int id) { return id == kCbF ? F.data() : id == kCbS ? S.data() : id == kCbW ? Wd.data() : Y.data(); }
+  double* buf(int id) { return id == kCbF ? F.data() : id == kCbS ? S.data() : id == kCbW ? Wd.data() : id == kCbY ? Y.data() : Pp.data(); }
   void run(const CholSchedule& sch) {
     for (const CholOp& op : sch.ops)
       for (int q = 0; q < op.ntask; ++q) {
@@ -33,14 +33,17 @@ struct Exec {
         switch (op.type) {
           case kOpGemm: gemm(sch.gemm[ti]); break;
           case kOpDiag: diag(sch.diag[ti]); break;
+          case kOpReduce: reduce(sch.red[ti]); break;
+          case kOpFSolve1: fsolve1(P.lvl_sup[op.task0 + q]); break;
+          case kOpBSolve1: bsolve1(P.lvl_sup[op.task0 + q]); break;
           default: col(op.type, sch.col[ti]);
         }
       }
   }
   void gemm(const CholGemmTask& g) {
-    const double* Ab = buf((g.flags >> 4) & 3) + g.a;
-    const double* Bb = buf((g.flags >> 6) & 3) + g.b;
-    double* Cb = buf((g.flags >> 8) & 3) + g.c;
+    const double* Ab = buf((g.flags >> 4) & 7) + g.a;
+    const double* Bb = buf((g.flags >> 7) & 7) + g.b;
+    double* Cb = buf((g.flags >> 10) & 7) + g.c;
     const bool ta = g.flags & kCgTA, tb = g.flags & kCgTB, lo = g.flags & kCgLower;
     std::vector<double> out((size_t)g.M * g.N);
     for (int j = 0; j < g.N; ++j)
@@ -58,6 +61,49 @@ struct Exec {
         if (lo && i - j + g.doff < 0) continue;
         double& c = Cb[i + (size_t)j * g.ldc];
         c = (g.beta == 0. ? 0. : g.beta * c) + g.alpha * out[i + (size_t)j * g.M];
+      }
+  }
+  void fsolve1(int s) {
+    const int sf = P.sfirst[s], ns = P.ns(s), fs = P.fs(s);
+    double* V = Y.data() + (*vofs)[s];
+    const double* L = F.data() + P.foff[s];
+    for (int r = 0; r < fs; ++r) V[r] = r < ns ? b[P.perm[sf + r]] : 0.;
+    for (int q = P.cptr[s]; q < P.cptr[s + 1]; ++q) {
+      const int ch = P.child[q];
+      for (int i = 0; i < P.nr(ch); ++i) V[P.rel[P.rptr[ch] + i]] += Y[(*vofs)[ch] + P.ns(ch) + i];
+    }
+    for (int k = 0; k < P.nblk(s); ++k) {
+      const int j0 = 64 * k, ib = std::min(64, ns - j0);
+      const double* W = Wd.data() + P.woff[s] + (int64_t)k * 4096;
+      double x[64];
+      for (int i = 0; i < ib; ++i) { double v = 0.; for (int j = 0; j <= i; ++j) v += W[i + j * 64] * V[j0 + j]; x[i] = v; }
+      for (int i = 0; i < ib; ++i) V[j0 + i] = x[i];
+      for (int r = j0 + ib; r < fs; ++r) for (int j = 0; j < ib; ++j) V[r] -= L[r + (size_t)(j0 + j) * fs] * x[j];
+    }
+  }
+  void bsolve1(int s) {
+    const int sf = P.sfirst[s], ns = P.ns(s), nr = P.nr(s), fs = P.fs(s);
+    double* V = Y.data() + (*vofs)[s];
+    const double* L = F.data() + P.foff[s];
+    for (int i = 0; i < nr; ++i) V[ns + i] = X[P.perm[P.rows[P.rptr[s] + i]]];
+    for (int k = P.nblk(s) - 1; k >= 0; --k) {
+      const int j0 = 64 * k, ib = std::min(64, ns - j0), r0 = j0 + ib;
+      const double* W = Wd.data() + P.woff[s] + (int64_t)k * 4096;
+      double vb[64];
+      for (int j = 0; j < ib; ++j) { double d = 0.; for (int r = r0; r < fs; ++r) d += L[r + (size_t)(j0 + j) * fs] * V[r]; vb[j] = V[j0 + j] - d; }
+      for (int i = 0; i < ib; ++i) { double v = 0.; for (int j = i; j < ib; ++j) v += W[j + i * 64] * vb[j]; V[j0 + i] = v; }
+    }
+    for (int i = 0; i < ns; ++i) X[P.perm[sf + i]] = V[i];
+  }
+  void reduce(const CholReduceTask& r) {
+    double* C = buf(r.bufc) + r.c;
+    const double* Pb = Pp.data() + r.p;
+    for (int j = 0; j < r.N; ++j)
+      for (int i = 0; i < r.M; ++i) {
+        double s = 0.;
+        for (int q = 0; q < r.nslices; ++q) s += Pb[q * r.pstride + i + j * 64];
+        double& c = C[i + (size_t)j * r.ldc];
+        c = (r.beta == 0. ? 0. : r.beta * c) + r.alpha * s;
       }
   }
   void diag(const CholDiagTask& d) {
@@ -89,23 +135,22 @@ struct Exec {
     const int s = c.s, fs = P.fs(s), ns = P.ns(s), nr = P.nr(s);
     double* Fs = F.data() + P.foff[s];
     double* Ss = S.data() + P.foff[s];
-    if (type == kOpAssemble) {
+    if (type == kOpAsmTile) {
+      const int rt = c.c0, ct = c.c1;
+      for (int j = ct; j < std::min(ct + 64, fs); ++j)
+        for (int i = std::max(rt, j); i < std::min(rt + 64, fs); ++i) {
+          double v = 0.;
+          for (int q = P.cptr[s]; q < P.cptr[s + 1]; ++q) {
+            const int ch = P.child[q], fc = P.fs(ch), nsc = P.ns(ch);
+            const int ia = P.cinv[P.cinv_off[ch] + i], ib = P.cinv[P.cinv_off[ch] + j];
+            if (ia >= 0 && ib >= 0) v += F[P.foff[ch] + (nsc + ia) + (size_t)(nsc + ib) * fc];
+          }
+          Fs[i + (size_t)j * fs] = v;
+        }
+    } else if (type == kOpAsmEntries) {
       for (int j = c.c0; j < c.c1; ++j) {
-        for (int r = j; r < fs; ++r) Fs[r + (size_t)j * fs] = 0.;
-        if (j < ns) {
-          const int gj = P.perm[P.sfirst[s] + j];
-          for (int r = j; r < fs; ++r) Fs[r + (size_t)j * fs] = (*A)[(size_t)P.perm[rowpos(s, r)] * n + gj];
-        }
-      }
-      for (int q = P.cptr[s]; q < P.cptr[s + 1]; ++q) {
-        const int ch = P.child[q], fc = P.fs(ch), nsc = P.ns(ch), nrc = P.nr(ch);
-        const int* rel = P.rel.data() + P.rptr[ch];
-        const double* Fc = F.data() + P.foff[ch];
-        for (int bb = 0; bb < nrc; ++bb) {
-          const int tb = rel[bb];
-          if (tb < c.c0 || tb >= c.c1) continue;
-          for (int a = bb; a < nrc; ++a) Fs[rel[a] + (size_t)tb * fs] += Fc[(nsc + a) + (size_t)(nsc + bb) * fc];
-        }
+        const int gj = P.perm[P.sfirst[s] + j];
+        for (int r = j; r < fs; ++r) Fs[r + (size_t)j * fs] += (*A)[(size_t)P.perm[rowpos(s, r)] * n + gj];
       }
     } else if (type == kOpGatherS) {
       const int p = P.sparent[s], fp = P.fs(p);
@@ -115,7 +160,7 @@ struct Exec {
         for (int a = 0; a < nr; ++a) Ss[(ns + a) + (size_t)(ns + bb) * fs] = Sp[rel[a] + (size_t)rel[bb] * fp];
     } else if (type == kOpMirror) {
       for (int j = c.c0; j < c.c1; ++j)
-        for (int r = j + 1; r < fs; ++r) Ss[j + (size_t)r * fs] = Ss[r + (size_t)j * fs];
+        for (int r = std::max(j + 1, c.pad); r < std::min(fs, c.pad + 64); ++r) Ss[j + (size_t)r * fs] = Ss[r + (size_t)j * fs];
     } else if (type == kOpAsmV) {
       double* V = Y.data() + (*vofs)[s];
       for (int k = 0; k < t; ++k) {
@@ -189,8 +234,9 @@ int main(int argc, char** argv) {
   }
   double ld_dense = 0.;
   for (int j = 0; j < n; ++j) ld_dense += 2. * std::log(L[(size_t)j * n + j]);
-  std::vector<double> F(P.front_doubles, 0.), S(P.front_doubles, 0.), Wd(P.woff[P.nsup], 0.), Yb(std::max<int64_t>(P.selinv.y_doubles, 1), 0.);
-  Exec ex{P, F, S, Wd, Yb, &A, n};
+  std::vector<double> F(P.front_doubles, 7.), S(P.front_doubles, 0.), Wd(P.woff[P.nsup], 0.), Yb(std::max<int64_t>(P.selinv.y_doubles, 1), 0.);
+  std::vector<double> Pp(std::max<int64_t>(std::max(P.selinv.p_doubles, P.factor.p_doubles), 1), 0.);
+  Exec ex{P, F, S, Wd, Yb, Pp, &A, n};
   ex.run(P.factor);
   double ld = 0.;
   for (int s = 0; s < P.nsup; ++s)
@@ -204,7 +250,8 @@ int main(int argc, char** argv) {
   CholSchedule ss;
   chol_solve_schedule(P, t, false, ss, vofs);
   std::vector<double> V(ss.y_doubles, 0.);
-  Exec ev{P, F, S, Wd, V, &A, n, bvec.data(), xs.data(), t, &vofs};
+  std::vector<double> Pv(std::max<int64_t>(ss.p_doubles, 1), 0.);
+  Exec ev{P, F, S, Wd, V, Pv, &A, n, bvec.data(), xs.data(), t, &vofs};
   ev.run(ss);
   double res = 0., nb = 0.;
   for (int k = 0; k < t; ++k)
@@ -215,6 +262,19 @@ int main(int argc, char** argv) {
       nb = std::max(nb, std::fabs(bvec[i + (size_t)k * n]));
     }
   printf("solve residual max %.2e (|b| %.2e)\n", res, nb);
+  {   // t = 1 (hybrid schedule: per-supernode level sweeps + tiled levels)
+    std::vector<int64_t> vo1;
+    CholSchedule s1;
+    chol_solve_schedule(P, 1, false, s1, vo1);
+    std::vector<double> V1(s1.y_doubles, 0.), P1(std::max<int64_t>(s1.p_doubles, 1), 0.), x1(n, 0.);
+    int nf = 0;
+    for (auto& o : s1.ops) nf += o.type == kOpFSolve1;
+    Exec e1{P, F, S, Wd, V1, P1, &A, n, bvec.data(), x1.data(), 1, &vo1};
+    e1.run(s1);
+    double r1 = 0.;
+    for (int i = 0; i < n; ++i) { double s2 = 0.; for (int j = 0; j < n; ++j) s2 += A[(size_t)i * n + j] * x1[j]; r1 = std::max(r1, std::fabs(s2 - bvec[i])); }
+    printf("t=1 solve residual max %.2e (%d single-workgroup levels, %zu launches)\n", r1, nf, s1.ops.size());
+  }
   // selected inverse vs dense inverse (columns of A^-1 by dense solves)
   ex.run(P.selinv);
   std::vector<double> Ainv((size_t)n * n);

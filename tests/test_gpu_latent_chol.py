@@ -184,4 +184,5 @@ def test_latent_chol_100k_fd_gradient_and_determinism(lik):
         fp = gm.neg_log_likelihood(cp * np.exp(e), None)
         fm = gm.neg_log_likelihood(cp * np.exp(-e), None)
         fd = (fp - fm) / (2 * h)
-        assert abs(fd - a[1][k]) <= 2e-6 * max(abs(a[1][k]), 1e-3 * abs(a[0])), (k, fd, a[1][k])
+        ga = a[1][k] if k == 0 else -a[1][k]   # the gradient is wrt log(phi), phi = 1 / range (exponential)
+        assert abs(fd - ga) <= 2e-6 * max(abs(ga), 1e-3 * abs(a[0])), (k, fd, ga)
