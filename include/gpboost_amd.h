@@ -377,22 +377,25 @@ GPBOOST_AMD_EXPORT int GPB_SetPredictionData(REModelHandle handle,
     int nsim_var_pred,
     int rank_pred_approx_matrix_lanczos);
 
-/* replaces GPB_PredictREModel (include/LightGBM/c_api.h:1617; Vecchia_utils.cpp:1634-1931,
- * re_model_template.h:3700-4071) for the Vecchia approximation: predictive mean
+/* replaces GPB_PredictREModel (include/LightGBM/c_api.h:1617; Vecchia_utils.cpp:1634-2442,
+ * re_model_template.h:3700-4071; dense CalcPred, FITC CalcPredFITC_FSA, grouped CalcPred): predictive mean
  * (out_predict[0 .. num_data_pred)) and, if predict_var, variances (out_predict[num_data_pred ..
- * 2 num_data_pred)), or, if predict_cov_mat, the num_data_pred^2 covariance (diagonal: each
- * prediction point conditions on observed points only). gp_coords_data_pred column-major
- * num_data_pred x dim_gp_coords. cov_pars on the original scale (NULL: those of the last
- * evaluation); y_data NULL: the response set before. Exact Gaussian models: predict_response =
- * false removes the nugget variance (latent process). Latent models (vecchia_latent,
- * bernoulli_logit; latent_order_obs_first_cond_obs_only, PredictLaplaceApproxVecchia
- * likelihoods.h:6576-6813): the Laplace mode at cov_pars (found from zero, fixed_effects = the
- * observed data's location offset), mean = -Bpo mode; predict_var adds the iterative simulation term
- * (nsim_var_pred draws, statistically equivalent to the reference's); gaussian vecchia_latent with
- * predict_response adds the error variance. Neighbours are searched among the observed points
- * (latent models: their unique locations) by the reference's sweep (bit-identical lists).
- * Unsupported inputs (clusters, grouped effects with GPs, random coefficients, saved prediction data,
- * dense models, latent predict_cov_mat, bernoulli predict_response) return -1. */
+ * 2 num_data_pred)), or, if predict_cov_mat, the num_data_pred^2 covariance (column-major).
+ * gp_coords_data_pred column-major num_data_pred x dim_gp_coords. cov_pars on the original scale (NULL: those
+ * of the last evaluation); y_data NULL: the response set before; use_saved_data: the data of
+ * GPB_SetPredictionData. Exact Gaussian models: predict_response = false removes the nugget variance (latent
+ * process). Every vecchia_pred_type is supported: order_obs_first_cond_obs_only / _cond_all, order_pred_first,
+ * latent_order_obs_first_cond_obs_only / _cond_all (Gaussian and Laplace models). Latent Vecchia models
+ * (PredictLaplaceApproxVecchia likelihoods.h:6576-6813): the Laplace mode at cov_pars, mean = -Bpo mode
+ * (cond_all: Bp^-1 on top); with matrix_inversion_method = "iterative" predict_var / predict_cov_mat add the
+ * reference's simulation term (nsim_var_pred draws; statistically equivalent, or the reference's own one-thread
+ * stream with GPBOOST_AMD_PRED_DRAWS=reference), with "cholesky" the exact term ||L^-1 Bpo^T e_p||^2 on the
+ * sparse Cholesky factor of Sigma^-1 + W (:6751-6811); predict_response gives the response mean / variance.
+ * Deviation from the reference, by design: with vecchia_pred_type = "order_pred_first" the variances and the
+ * covariance matrix are returned in prediction-point order (row p = the p-th prediction point); the
+ * reference returns them in the order of its sparse factor's AMD permutation (an artefact of its
+ * SimplicialLLT; the means are in prediction-point order on both sides). Unsupported inputs (clusters,
+ * random coefficients, full_scale_vecchia, num_neighbors_pred > 64) return -1 with a message. */
 GPBOOST_AMD_EXPORT int GPB_PredictREModel(REModelHandle handle,
     const double* y_data,
     int32_t num_data_pred,
