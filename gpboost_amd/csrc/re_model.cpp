@@ -434,7 +434,10 @@ std::vector<double> gauss_hermite_adaptive(int order) {
 void REModelAMD::Predict(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,
                          bool predict_cov_mat, bool predict_var, bool predict_response, double* out,
                          const double* mean_add) {
-  if (vif_) Fatal("predictions with gp_approx = 'full_scale_vecchia' are not supported by gpboost_amd");
+  if (vif_) {
+    PredictVif(y, n_pred, coords_pred, cov_pars, predict_cov_mat, predict_var, predict_response, out, mean_add);
+    return;
+  }
   if (fitc_) {
     PredictFitc(y, n_pred, coords_pred, cov_pars, predict_cov_mat, predict_var, predict_response, out, mean_add);
     return;
@@ -718,6 +721,62 @@ std::vector<int> REModelAMD::FitcMatch(const std::vector<double>& xp, int n_pred
 // covariance matrix, times sigma^2 (:3956, :3967); prediction points that coincide with a training point
 // (TwoNumbersAreEqual on the coordinate sums, then per coordinate, utils.h:52-54 with
 // EPSILON_NUMBERS = 1e-10) get the FITC diagonal correction.
+// gp_approx = "full_scale_vecchia", Gaussian likelihood (re_model_template.h:3708-3752 ->
+// CalcPredVecchiaObservedFirstOrder with the full-scale branches, Vecchia_utils.cpp:1634-1980): the prediction
+// points follow the observed ones in the model order; neighbours among the observed points (cond_obs_only) or
+// the observed and earlier prediction points (cond_all) by the reference's sweep; VifSolver::Predict on the
+// transformed scale, then times sigma^2 with the nugget removed for the latent process (:3776-3792).
+void REModelAMD::PredictVif(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,
+                            bool predict_cov_mat, bool predict_var, bool predict_response, double* out,
+                            const double* mean_add) {
+  if (world_ > 1) Fatal("predictions are only available on single-rank models");
+  if (n_pred <= 0) Fatal("num_data_pred must be > 0");
+  if (coords_pred == nullptr) Fatal("gp_coords_data_pred must be provided");
+  const bool cond_all = vecchia_pred_type_ == "order_obs_first_cond_all";
+  if (!cond_all && vecchia_pred_type_ != "order_obs_first_cond_obs_only") {
+    if (vecchia_pred_type_ == "order_pred_first")   // re_model_template.h:3748-3750
+      Fatal("The full-scale Vecchia approximation is currently not implemented when prediction locations appear "
+            "first in the ordering. Please use vecchia_pred_type = order_obs_first_cond_all or vecchia_pred_type = "
+            "order_obs_first_cond_obs_only");
+    Fatal("The full-scale Vecchia approximation for latent process(es) is currently not implemented");   // :3761-3763
+  }
+  UseDevice();
+  if (y != nullptr) SetY(y);
+  if (!y_set_) Fatal("response variable y has not been set (pass y or evaluate the likelihood first)");
+  double cp[3];
+  if (cov_pars != nullptr) std::copy(cov_pars, cov_pars + 3, cp);
+  else if ((int)last_cov_pars_.size() == 3) std::copy(last_cov_pars_.begin(), last_cov_pars_.end(), cp);
+  else Fatal("cov_pars must be provided (no previous evaluation)");
+  double trafo[3];
+  TransformCovPars(cp, trafo);
+  const int n = cfg_.n, d = cfg_.d, na = n + n_pred;
+  const int mp = std::min(num_neighbors_pred_, cond_all ? na - 1 : n);
+  std::vector<double> xa((size_t)na * d);
+  std::copy(coords_vo_.begin(), coords_vo_.begin() + (size_t)n * d, xa.begin());
+  for (int p = 0; p < n_pred; ++p)
+    for (int q = 0; q < d; ++q) xa[(size_t)(n + p) * d + q] = coords_pred[(size_t)q * n_pred + p];
+  std::vector<int> nb((size_t)n_pred * mp);
+  const int end_at = cond_all ? -1 : n - 1;
+  if (d <= 3 && mp <= 64) vecchia_neighbors_gpu(xa.data(), na, d, mp, n, na, nb.data(), stream_, end_at);
+  else vecchia_neighbors(xa.data(), na, d, mp, n, na, nb.data(), end_at);
+  if (cond_all)   // the first prediction points have fewer candidates: their unused slots are -1 (no neighbour)
+    for (int p = 0; p < n_pred; ++p)
+      for (int r = std::min(n + p, mp); r < mp; ++r) nb[(size_t)p * mp + r] = -1;
+  std::vector<double> mean(n_pred), var(predict_var ? n_pred : 0), cov(predict_cov_mat ? (size_t)n_pred * n_pred : 0);
+  vif_->Predict(cfg_.cov_type, trafo[1], trafo[2], d_y_.get(), xa.data() + (size_t)n * d, n_pred, nb.data(), mp,
+                cond_all, mean.data(), predict_var ? var.data() : nullptr, predict_cov_mat ? cov.data() : nullptr);
+  if (mean_add != nullptr)
+    for (int p = 0; p < n_pred; ++p) mean[p] += mean_add[p];
+  std::copy(mean.begin(), mean.end(), out);
+  const double nug = predict_response ? 0. : 1.;
+  if (predict_cov_mat) {
+    for (int p = 0; p < n_pred; ++p) cov[(size_t)p * n_pred + p] -= nug;
+    for (size_t e = 0; e < cov.size(); ++e) out[n_pred + e] = cov[e] * trafo[0];
+  } else if (predict_var) {
+    for (int p = 0; p < n_pred; ++p) out[n_pred + p] = (var[p] - nug) * trafo[0];
+  }
+}
+
 void REModelAMD::PredictFitc(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,
                              bool predict_cov_mat, bool predict_var, bool predict_response, double* out,
                              const double* mean_add) {

@@ -51,6 +51,13 @@ class VifSolver {
   void Eval(int cov_type, double var, double phi, const double* d_y, bool want_grad, double* sums, double* kernel_ms);
   // D (n) and B's values (n x nn, 0 past a row's neighbours) of the last Eval (host)
   void GetFactor(double* D, double* Bv) const;
+  // Predictions for the Gaussian likelihood (CalcPredVecchiaObservedFirstOrder, full_scale_vecchia branches,
+  // Vecchia_utils.cpp:1686-1707, 1826-1840, 1872-1873, 1901-1980) at (var, phi) on the transformed scale,
+  // nugget 1 included: Xp host row-major np x d prediction points (after the n observed points); nbr host
+  // np x mp neighbour indices (< n: observed points; >= n: earlier prediction points, cond_all). mean (np);
+  // pvar (np, nullable); pcov (np x np column-major, nullable). Runs Eval(want_grad = false) first.
+  void Predict(int cov_type, double var, double phi, const double* d_y, const double* Xp, int np, const int* nbr,
+               int mp, bool cond_all, double* mean, double* pvar, double* pcov);
 
  private:
   void Rows(int cov_type, double var, double phi, bool grad);

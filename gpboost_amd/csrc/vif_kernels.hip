@@ -20,6 +20,7 @@
 #include "cov.h"
 #include "dense.h"
 #include "fitc.h"
+#include "latent_kernels.h"
 #include "kernels.h"
 #include "vif.h"
 
@@ -28,7 +29,8 @@ namespace {
 
 constexpr int kT = 256;
 constexpr int kCh = 32;      // m-rows per LDS staging chunk in the row kernel
-constexpr int kMaxNn = 48;   // neighbours per row (LDS budget of the row kernel)
+constexpr int kMaxNn = 64;        // neighbours per row without derivatives (prediction rows; LDS of the row kernel)
+constexpr int kMaxNnGrad = 48;    // with the two derivative blocks (the likelihood's rows)
 constexpr int kNv = 16;      // n-vector scratch slots
 constexpr int kMv = 12;      // m-vector scratch slots
 
@@ -113,6 +115,7 @@ struct VifRowsArgs {
   const double* P1;
   double var, phi;
   int r1;   // doubles of the staging / residual-matrix region
+  int i0;   // first row (prediction rows follow the n observed points); nbr / Bv / D are indexed by i - i0
   double* Bv;
   double* D;
   double* dBv0;
@@ -138,9 +141,9 @@ __global__ void __launch_bounds__(kT) vif_rows_kernel(VifRowsArgs a) {
   __shared__ double vecs[4][kMaxNn];   // c, dc0, dc1, A
   __shared__ double scal[4];
   constexpr int G = GRAD ? 3 : 1;
-  const int i = blockIdx.x, tid = threadIdx.x;
+  const int i = a.i0 + blockIdx.x, tid = threadIdx.x, ir = blockIdx.x;
   const int nn = a.nn, k = min(i, nn), S = k + 1;
-  if (tid < k) idx[tid] = a.nbr[(size_t)i * nn + tid];
+  if (tid < k) idx[tid] = a.nbr[(size_t)ir * nn + tid];
   if (tid == k) idx[k] = i;
   double* st = lds;            // staging [g][q][a] (kCh x Sp each), later C, dC0, dC1 (k x k each)
   double* gram = lds + a.r1;   // [g][a][b] = V_a . M^g_b, S x S each
@@ -309,7 +312,7 @@ __global__ void __launch_bounds__(kT) vif_rows_kernel(VifRowsArgs a) {
       s1 = wsum(s1);
       s2 = wsum(s2);
     }
-    const size_t row = (size_t)i * nn;
+    const size_t row = (size_t)ir * nn;
     if (p < nn) {
       a.Bv[row + p] = p < k ? -xa[0] : 0.;
       if (GRAD) {
@@ -318,10 +321,10 @@ __global__ void __launch_bounds__(kT) vif_rows_kernel(VifRowsArgs a) {
       }
     }
     if (p == 0) {
-      a.D[i] = scal[0] - s0;
+      a.D[ir] = scal[0] - s0;
       if (GRAD) {
-        a.dD0[i] = scal[1] - s1;
-        a.dD1[i] = scal[2] - s2;
+        a.dD0[ir] = scal[1] - s1;
+        a.dD1[ir] = scal[2] - s2;
       }
     }
   }
@@ -342,9 +345,9 @@ __global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
   __shared__ int idx[32];
   __shared__ double vecs[4][32];   // c, dc0, dc1, A
   __shared__ double rdg[32];       // 1 / L_jj
-  const int i = blockIdx.x, lane = threadIdx.x;
+  const int i = a.i0 + blockIdx.x, lane = threadIdx.x, ir = blockIdx.x;
   const int nn = a.nn, k = min(i, nn);
-  if (lane < 32) idx[lane] = lane < k ? a.nbr[(size_t)i * nn + lane] : i;
+  if (lane < 32) idx[lane] = lane < k ? a.nbr[(size_t)ir * nn + lane] : i;
   wave_sync();
   const int m0 = lane & 15, kq = lane >> 4;
   const size_t c0 = (size_t)idx[m0] * a.ldm, c1 = (size_t)idx[16 + m0] * a.ldm;
@@ -491,7 +494,7 @@ __global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
     s1 = wsum(s1);
     s2 = wsum(s2);
   }
-  const size_t row = (size_t)i * nn;
+  const size_t row = (size_t)ir * nn;
   if (lane < nn) {
     a.Bv[row + lane] = lane < k ? -xa[0] : 0.;
     if (GRAD) {
@@ -500,10 +503,10 @@ __global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
     }
   }
   if (lane == 0) {
-    a.D[i] = d0 - s0;
+    a.D[ir] = d0 - s0;
     if (GRAD) {
-      a.dD0[i] = dd0 - s1;
-      a.dD1[i] = dd1 - s2;
+      a.dD0[ir] = dd0 - s1;
+      a.dD1[ir] = dd1 - s2;
     }
   }
 }
@@ -689,13 +692,65 @@ size_t rows_lds_bytes(int nn, bool grad) {
   return sizeof(double) * ((size_t)rows_r1(nn, grad) + (size_t)G * S * S);
 }
 
+// Prediction rows (full_scale_vecchia): mo_p = sum over observed neighbours of B(p, j) r_j (the Bpo r of the
+// mean) and column p of Q^T = (Bpo K_nm)^T, one wave per prediction point (Vecchia_utils.cpp:1904, 1917-1921)
+__global__ void __launch_bounds__(64) vif_pred_bpo_kernel(int np, int n, int mp, const int* __restrict__ nbr,
+                                                          const double* __restrict__ Bv, const double* __restrict__ r,
+                                                          const double* __restrict__ Kmn, int m, int ldm,
+                                                          double* __restrict__ mo, double* __restrict__ Qt) {
+  const int p = blockIdx.x, lane = threadIdx.x;
+  const int* nb = nbr + (size_t)p * mp;
+  const double* bv = Bv + (size_t)p * mp;
+  double s = 0.;
+  for (int j = lane; j < mp; j += 64)
+    if (nb[j] >= 0 && nb[j] < n) s = fma(bv[j], r[nb[j]], s);
+  s = wsum(s);
+  if (lane == 0) mo[p] = s;
+  for (int q = lane; q < m; q += 64) {
+    double t = 0.;
+    for (int j = 0; j < mp; ++j)
+      if (nb[j] >= 0 && nb[j] < n) t = fma(bv[j], Kmn[(size_t)nb[j] * ldm + q], t);
+    Qt[(size_t)p * ldm + q] = t;
+  }
+}
+
+// var_p = (KP - PPV + 2 Q)_p . Sig_p + (PPV - 2 Q)_p . S2_p + Q_p . S3_p (Vecchia_utils.cpp:1966-1973), columns
+// of m x np matrices (ld ldm)
+__global__ void __launch_bounds__(kT) vif_pred_var_kernel(int np, int m, int ldm, const double* __restrict__ KP,
+                                                          const double* __restrict__ PPV, const double* __restrict__ Q,
+                                                          const double* __restrict__ Sig, const double* __restrict__ S2,
+                                                          const double* __restrict__ S3, double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= np) return;
+  const size_t o = (size_t)p * ldm;
+  double s = 0.;
+  for (int q = lane; q < m; q += 64) {
+    const double kp = KP[o + q], pv = PPV[o + q], qq = Q[o + q];
+    s += (kp - pv + 2. * qq) * Sig[o + q] + (pv - 2. * qq) * S2[o + q] + qq * S3[o + q];
+  }
+  s = wsum(s);
+  if (lane == 0) out[p] = s;
+}
+
+__global__ void __launch_bounds__(kT) vif_sum_parts_kernel(const double* __restrict__ part, int chunks, long stride,
+                                                           int m, int ldm, double* __restrict__ out) {
+  const int q = blockIdx.x * kT + threadIdx.x;
+  if (q >= m * m) return;
+  const int i = q % m, j = q / m;
+  double s = 0.;
+  for (int c = 0; c < chunks; ++c) s += part[(size_t)c * stride + i + (size_t)j * ldm];
+  out[i + (size_t)j * ldm] = s;
+}
+
 }  // namespace
 
 VifSolver::VifSolver(int n, int d, const double* d_X, const std::vector<double>& Z, const std::vector<int>& nbr, int nn,
                      hipStream_t stream)
     : n_(n), d_(d), nn_(nn), s_(stream), d_X_(d_X) {
   if (nn < 1) Fatal("full_scale_vecchia needs num_neighbors >= 1");
-  if (nn > kMaxNn) Fatal("num_neighbors = %d > %d is not supported for gp_approx = 'full_scale_vecchia' by gpboost_amd", nn, kMaxNn);
+  if (nn > kMaxNnGrad)
+    Fatal("num_neighbors = %d > %d is not supported for gp_approx = 'full_scale_vecchia' by gpboost_amd", nn, kMaxNnGrad);
   if ((long)nbr.size() != (long)n * nn) Fatal("VifSolver: neighbour lists of the wrong size");
   F_.reset(new FitcSolver(n, d, d_X, Z, stream));
   m_ = F_->m_;
@@ -1001,6 +1056,161 @@ void VifSolver::GetFactor(double* D, double* Bv) const {
   HIP_CHECK(hipMemcpyAsync(D, D_.get(), sizeof(double) * n_, hipMemcpyDeviceToHost, s_));
   HIP_CHECK(hipMemcpyAsync(Bv, Bv_.get(), sizeof(double) * n_ * nn_, hipMemcpyDeviceToHost, s_));
   HIP_CHECK(hipStreamSynchronize(s_));
+}
+
+void VifSolver::Predict(int cov_type, double var, double phi, const double* d_y, const double* Xp, int np,
+                        const int* nbr, int mp, bool cond_all, double* mean, double* pvar, double* pcov) {
+  if (np <= 0) return;
+  if (mp < 1 || mp > kMaxNn) Fatal("num_neighbors_pred = %d is not supported for gp_approx = 'full_scale_vecchia' (1..%d)",
+                                   mp, kMaxNn);
+  if (cond_all && pcov != nullptr && np > 20000)
+    Fatal("order_obs_first_cond_all with predict_cov_mat is limited to num_data_pred <= 20000 in gpboost_amd");
+  FitcSolver& F = *F_;
+  const int n = n_, m = m_, ldm = ldm_, d = d_;
+  double sums[6], kms[2];
+  Eval(cov_type, var, phi, d_y, false, sums, kms);   // factor, Woodbury M, w = M^-1 K^T R^-1 y, kw = K w
+  if (std::isnan(sums[0])) Fatal("full_scale_vecchia prediction: the Woodbury matrix is not positive definite");
+  const double* w = mvec_.get() + ldm;
+  const double* kw = vec_.get() + 2 * (size_t)n;
+  // coordinates and V of the observed points followed by the prediction points
+  const int na = n + np;
+  DevBuf<double> Xa((size_t)na * d), KP((size_t)ldm * np), Va((size_t)ldm * na), Bvp((size_t)np * mp), Dp(np),
+      r(n), mo(np), Qt((size_t)ldm * np), kpw(np);
+  DevBuf<int> dnb((size_t)np * mp);
+  HIP_CHECK(hipMemcpyAsync(Xa.get(), d_X_, sizeof(double) * (size_t)n * d, hipMemcpyDeviceToDevice, s_));
+  HIP_CHECK(hipMemcpyAsync(Xa.get() + (size_t)n * d, Xp, sizeof(double) * (size_t)np * d, hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipMemcpyAsync(dnb.get(), nbr, sizeof(int) * (size_t)np * mp, hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipMemsetAsync(KP.get(), 0, sizeof(double) * KP.size(), s_));
+  fitc_kmn(s_, cov_type, Xa.get() + (size_t)n * d, F.dZ_.get(), np, m, d, ldm, var, phi, KP.get());   // K_mp
+  HIP_CHECK(hipMemcpyAsync(Va.get(), F.V_.get(), sizeof(double) * (size_t)ldm * n, hipMemcpyDeviceToDevice, s_));
+  HIP_CHECK(hipMemsetAsync(Va.get() + (size_t)ldm * n, 0, sizeof(double) * (size_t)ldm * np, s_));
+  // V_p = L^-1 K_mp (chol_ip_cross_cov_pred, :1698-1699)
+  gemm_f64(s_, m, np, m, 1., F.Li_.get(), ldm, 0, KP.get(), ldm, 0, 0., Va.get() + (size_t)ldm * n, ldm, 0, 1, 0, 0);
+  // residual Vecchia rows of the prediction points (:1807-1896), no derivatives
+  {
+    VifRowsArgs a{};
+    a.X = Xa.get();
+    a.nbr = dnb.get();
+    a.n = na; a.d = d; a.nn = mp; a.mi = m; a.ldm = ldm;
+    a.V = Va.get(); a.P0 = nullptr; a.P1 = nullptr;
+    a.var = var; a.phi = phi;
+    a.r1 = rows_r1(mp, false);
+    a.i0 = n;
+    a.Bv = Bvp.get(); a.D = Dp.get();
+    const size_t lds = rows_lds_bytes(mp, false);
+    dispatch_cov_vif(cov_type, [&](auto c) {
+      constexpr int COV = decltype(c)::value;
+      if (mp <= 31) {
+        hipLaunchKernelGGL((vif_rows_mfma_kernel<COV, false>), dim3(np), dim3(64), 0, s_, a);
+      } else {
+        HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&vif_rows_kernel<COV, false>),
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        hipLaunchKernelGGL((vif_rows_kernel<COV, false>), dim3(np), dim3(kT), lds, s_, a);
+      }
+    });
+    HIP_CHECK(hipGetLastError());
+  }
+  // mean = -Bpo (y - K w) [Bp^-1] + K_pm w (:1903-1908)
+  hipLaunchKernelGGL(vif_sub_kernel, dim3((n + kT - 1) / kT), dim3(kT), 0, s_, n, d_y, kw, r.get());
+  hipLaunchKernelGGL(vif_pred_bpo_kernel, dim3(np), dim3(64), 0, s_, np, n, mp, dnb.get(), Bvp.get(), r.get(),
+                     F.Kmn_.get(), m, ldm, mo.get(), Qt.get());
+  hipLaunchKernelGGL(vif_coldot_kernel, dim3((np + 3) / 4), dim3(kT), 0, s_, KP.get(), w,
+                     static_cast<const double*>(nullptr), np, m, ldm, kpw.get());
+  HIP_CHECK(hipGetLastError());
+  std::vector<double> hmo(np), hkpw(np), hD(np), hB((size_t)np * mp);
+  HIP_CHECK(hipMemcpyAsync(hmo.data(), mo.get(), sizeof(double) * np, hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipMemcpyAsync(hkpw.data(), kpw.get(), sizeof(double) * np, hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipMemcpyAsync(hD.data(), Dp.get(), sizeof(double) * np, hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipMemcpyAsync(hB.data(), Bvp.get(), sizeof(double) * hB.size(), hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  // Bp x = b (unit lower; its off-diagonal entries are the rows' values at earlier prediction points)
+  auto bp_solve = [&](double* x, size_t stride, int width) {
+    for (int p = 0; p < np; ++p)
+      for (int j = 0; j < mp; ++j) {
+        const int q = nbr[(size_t)p * mp + j];
+        if (q < n) continue;
+        const double b = hB[(size_t)p * mp + j];
+        for (int c = 0; c < width; ++c) x[(size_t)p * stride + c] -= b * x[(size_t)(q - n) * stride + c];
+      }
+  };
+  std::vector<double> mu(np);
+  for (int p = 0; p < np; ++p) mu[p] = -hmo[p];
+  if (cond_all) bp_solve(mu.data(), 1, 1);
+  for (int p = 0; p < np; ++p) mean[p] = mu[p] + hkpw[p];
+  if (pvar == nullptr && pcov == nullptr) return;
+  // Bp^-1 (dense, cond_all) for the Bp^-1 Dp Bp^-T part and Bp^-1 (Bpo K) (:1935-1948)
+  std::vector<double> Binv;
+  if (cond_all) {
+    Binv.assign((size_t)np * np, 0.);   // row-major: row p = e_p^T Bp^-1
+    for (int p = 0; p < np; ++p) Binv[(size_t)p * np + p] = 1.;
+    bp_solve(Binv.data(), np, np);
+    std::vector<double> hQ((size_t)ldm * np);
+    HIP_CHECK(hipMemcpyAsync(hQ.data(), Qt.get(), sizeof(double) * hQ.size(), hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipStreamSynchronize(s_));
+    bp_solve(hQ.data(), ldm, m);   // rows of Q = columns of Q^T (ld ldm)
+    HIP_CHECK(hipMemcpyAsync(Qt.get(), hQ.data(), sizeof(double) * hQ.size(), hipMemcpyHostToDevice, s_));
+  }
+  // G = V (B^T D^-1 B K_nm) (m x m; :1910-1915), PPV^T = G^T V_p; Sig = K_mm,s^-1 K_mp; M^-1 PPV^T, M^-1 Q^T
+  BRow(F.Kmn_.get(), Bv_.get(), 1., false, BK_.get(), F.Kd_.get());
+  BCol(F.Kd_.get(), Bv_.get(), 1., F.A_.get());
+  const long mm = (long)ldm * ldm;
+  const int chunks = gemm_f64_splitk(s_, m, m, n, F.V_.get(), ldm, 0, F.A_.get(), ldm, 1, F.part_.get(), ldm, mm, 2048,
+                                     F.max_chunks_);
+  DevBuf<double> G(mm), PPV((size_t)ldm * np), Sig((size_t)ldm * np), S2((size_t)ldm * np), S3((size_t)ldm * np);
+  hipLaunchKernelGGL(vif_sum_parts_kernel, dim3((m * m + kT - 1) / kT), dim3(kT), 0, s_, F.part_.get(), chunks, mm, m,
+                     ldm, G.get());
+  HIP_CHECK(hipGetLastError());
+  for (auto* b : {&PPV, &Sig, &S2, &S3}) HIP_CHECK(hipMemsetAsync(b->get(), 0, sizeof(double) * b->size(), s_));
+  gemm_f64(s_, m, np, m, 1., G.get(), ldm, 1, Va.get() + (size_t)ldm * n, ldm, 0, 0., PPV.get(), ldm);
+  gemm_f64(s_, m, np, m, 1., F.Kinv_.get(), ldm, 0, KP.get(), ldm, 0, 0., Sig.get(), ldm);
+  gemm_f64(s_, m, m, m, 1., F.Wi_.get(), ldm, 1, F.Wi_.get(), ldm, 0, 0., F.Winv_.get(), ldm, 0, 0, 1, 1);   // M^-1
+  gemm_f64(s_, m, np, m, 1., F.Winv_.get(), ldm, 0, PPV.get(), ldm, 0, 0., S2.get(), ldm);
+  gemm_f64(s_, m, np, m, 1., F.Winv_.get(), ldm, 0, Qt.get(), ldm, 0, 0., S3.get(), ldm);
+  if (pvar != nullptr) {
+    DevBuf<double> dv(np);
+    hipLaunchKernelGGL(vif_pred_var_kernel, dim3((np + 3) / 4), dim3(kT), 0, s_, np, m, ldm, KP.get(), PPV.get(),
+                       Qt.get(), Sig.get(), S2.get(), S3.get(), dv.get());
+    HIP_CHECK(hipGetLastError());
+    HIP_CHECK(hipMemcpyAsync(pvar, dv.get(), sizeof(double) * np, hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipStreamSynchronize(s_));
+    for (int p = 0; p < np; ++p) {
+      double dpart = hD[p];
+      if (cond_all) {
+        dpart = 0.;
+        for (int q = 0; q <= p; ++q) dpart += Binv[(size_t)p * np + q] * Binv[(size_t)p * np + q] * hD[q];
+      }
+      pvar[p] += dpart;
+    }
+  }
+  if (pcov != nullptr) {
+    // cov = [Bp^-1] Dp [Bp^-T] + (KP - PPV + Q)^T Sig + (PPV - Q)^T S2 + Q^T S3 + Sig^T Q - S2^T Q (:1956-1964)
+    DevBuf<double> C((size_t)np * np), T1((size_t)ldm * np);
+    HIP_CHECK(hipMemcpyAsync(T1.get(), KP.get(), sizeof(double) * T1.size(), hipMemcpyDeviceToDevice, s_));
+    launch_axpby(T1.size(), -1., PPV.get(), 1., T1.get(), T1.get(), s_);
+    launch_axpby(T1.size(), 1., Qt.get(), 1., T1.get(), T1.get(), s_);
+    gemm_f64(s_, np, np, m, 1., T1.get(), ldm, 1, Sig.get(), ldm, 0, 0., C.get(), np);
+    HIP_CHECK(hipMemcpyAsync(T1.get(), PPV.get(), sizeof(double) * T1.size(), hipMemcpyDeviceToDevice, s_));
+    launch_axpby(T1.size(), -1., Qt.get(), 1., T1.get(), T1.get(), s_);
+    gemm_f64(s_, np, np, m, 1., T1.get(), ldm, 1, S2.get(), ldm, 0, 1., C.get(), np);
+    gemm_f64(s_, np, np, m, 1., Qt.get(), ldm, 1, S3.get(), ldm, 0, 1., C.get(), np);
+    gemm_f64(s_, np, np, m, 1., Sig.get(), ldm, 1, Qt.get(), ldm, 0, 1., C.get(), np);
+    gemm_f64(s_, np, np, m, -1., S2.get(), ldm, 1, Qt.get(), ldm, 0, 1., C.get(), np);
+    if (cond_all) {   // + Bp^-1 Dp Bp^-T: the row-major Bp^-1 read column-major is X = Bp^-T, C += (D X)^T X
+      std::vector<double> XD(Binv);
+      for (int p = 0; p < np; ++p)
+        for (int k = 0; k < np; ++k) XD[(size_t)p * np + k] *= hD[k];
+      DevBuf<double> dX((size_t)np * np), dXD((size_t)np * np);
+      HIP_CHECK(hipMemcpyAsync(dX.get(), Binv.data(), sizeof(double) * Binv.size(), hipMemcpyHostToDevice, s_));
+      HIP_CHECK(hipMemcpyAsync(dXD.get(), XD.data(), sizeof(double) * XD.size(), hipMemcpyHostToDevice, s_));
+      gemm_f64(s_, np, np, np, 1., dXD.get(), np, 1, dX.get(), np, 0, 1., C.get(), np);
+      HIP_CHECK(hipMemcpyAsync(pcov, C.get(), sizeof(double) * C.size(), hipMemcpyDeviceToHost, s_));
+      HIP_CHECK(hipStreamSynchronize(s_));
+    } else {
+      HIP_CHECK(hipMemcpyAsync(pcov, C.get(), sizeof(double) * C.size(), hipMemcpyDeviceToHost, s_));
+      HIP_CHECK(hipStreamSynchronize(s_));
+      for (int p = 0; p < np; ++p) pcov[(size_t)p * np + p] += hD[p];
+    }
+  }
 }
 
 }  // namespace gpb_amd

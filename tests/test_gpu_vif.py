@@ -136,7 +136,8 @@ def test_vif_refusals():
         GPModel(gp_coords=X, gp_approx="vif", num_ind_points=20, num_neighbors=60)
     gm = GPModel(gp_coords=X, gp_approx="vif", num_ind_points=20, num_neighbors=10)
     y = synthetic.bench_spatial_gaussian_y(X)
-    with pytest.raises(GPBoostError, match="full_scale_vecchia"):
+    gm.set_prediction_data(vecchia_pred_type="latent_order_obs_first_cond_obs_only")   # re_model_template.h:3761-3763
+    with pytest.raises(GPBoostError, match="latent process"):
         gm.predict(y=y, gp_coords_pred=X[:5], cov_pars=[0.3, 1.0, 0.1])
 
 
