@@ -22,9 +22,11 @@ from scipy.linalg import cho_factor, cho_solve, solve_triangular
 from oracle.fitc_laplace_oracle import JITTER, cov_dcov, _dist
 
 
-def vif_factor(xv, nb, Z, cov_type, var, phi):
+def vif_factor(xv, nb, Z, cov_type, var, phi, nugget=1.):
     """Residual Vecchia factor on the transformed scale: B (n x n unit lower), D (n) and per parameter
-    (log var, log phi) dB, dD; plus the low-rank pieces K (n x m), K_mm, dK_mm, K_mm,s."""
+    (log var, log phi) dB, dD; plus the low-rank pieces K (n x m), K_mm, dK_mm, K_mm,s. nugget = 0: the latent
+    form of the non-Gaussian likelihoods (Vecchia_utils.cpp:1355-1356, 1546-1548: D without the nugget, the
+    neighbours' residual matrix with its diagonal times JITTER_MULT_VECCHIA = 1 + 1e-10)."""
     xv = np.asarray(xv, float)
     n = xv.shape[0]
     K, dKr = cov_dcov(_dist(xv, Z), var, phi, cov_type)
@@ -46,7 +48,7 @@ def vif_factor(xv, nb, Z, cov_type, var, phi):
     for i in range(n):
         k = min(i, nb.shape[1])
         N = nb[i, :k]
-        D[i] = 1. + var - V[:, i] @ V[:, i]
+        D[i] = (nugget - V[:, i] @ V[:, i]) + var
         for p in range(2):   # D_grad init (var on the transformed scale), minus the low-rank part's derivative
             dD[p][i] = (var if p == 0 else 0.) - A[:, i] @ (2. * dK[p][i] - dKA[p][:, i])
         if k == 0:
@@ -56,7 +58,11 @@ def vif_factor(xv, nb, Z, cov_type, var, phi):
         np.fill_diagonal(cnn, var)
         np.fill_diagonal(dcnn, 0.)
         cni, dcni = cov_dcov(_dist(xs, xv[i:i + 1])[:, 0], var, phi, cov_type)
-        C = cnn + np.eye(k) - V[:, N].T @ V[:, N]
+        C = cnn - V[:, N].T @ V[:, N]
+        if nugget == 0.:
+            C[np.diag_indices_from(C)] *= 1. + 1e-10
+        else:
+            C += nugget * np.eye(k)
         c = cni - V[:, N].T @ V[:, i]
         cC = cho_factor(C, lower=True)
         a = cho_solve(cC, c)
