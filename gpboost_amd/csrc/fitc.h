@@ -90,6 +90,7 @@ class FitcSolver {
  private:
   friend class FitcLaplace;   // the Laplace approximation (fitc_laplace.h) works on these buffers
   friend class VifSolver;     // the full-scale Vecchia approximation (vif.h) reuses the low-rank part
+  friend class VifLaplace;    // and its Laplace approximation (vif_laplace.h)
   // K_mn, K_mm, K_mm,s, dK_mm, L = chol(K_mm,s) (red[0] = 2 sum log L_ii), L^-1 (Li_), V = L^-1 K_mn,
   // K_mm,s^-1 (Kinv_): the part of the factorization that does not depend on the likelihood
   void Prior(int cov_type, double var, double phi, double* red);

@@ -92,12 +92,18 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
     if (!(cfg_.cover_tree_radius > 0.)) Fatal("cover_tree_radius must be > 0");
   } else if (cfg_.gp_approx == "full_scale_vecchia" || cfg_.gp_approx == "vif" || cfg_.gp_approx == "VIF") {
     cfg_.gp_approx = "full_scale_vecchia";   // re_model_template.h:204-206
-    if (cfg_.lik != kLikGaussian)
-      Fatal("gp_approx = 'full_scale_vecchia' with likelihood '%s' (Laplace approximation) is not supported by "
-            "gpboost_amd (supported: gaussian)", cfg_.likelihood.c_str());
-    if (cfg_.matrix_inversion_method == "iterative")   // re_model_template.h:8780-8782
+    cfg_.latent = cfg_.lik != kLikGaussian;   // Laplace approximation (VifLaplace, the reference's FSVA)
+    if (!cfg_.latent && cfg_.matrix_inversion_method == "iterative")   // re_model_template.h:8780-8782
       Fatal("The iterative methods are not implemented for the Full-Scale-Vecchia approximation with Gaussian "
             "likelihood. Please use Cholesky.");
+    // non-Gaussian: the reference's default is "iterative" (PCG + SLQ with the FITC preconditioner,
+    // re_model_template.h:6719-6723); this build runs the exact Cholesky branch for "default" and "cholesky"
+    if (cfg_.latent && cfg_.matrix_inversion_method == "iterative")
+      Fatal("matrix_inversion_method = 'iterative' for gp_approx = 'full_scale_vecchia' with likelihood '%s' is not "
+            "supported by gpboost_amd (supported: cholesky)", cfg_.likelihood.c_str());
+    if (cfg_.latent && cfg_.ind_points_selection == "random")   // the reference's FSVA component construction
+      Fatal("Method 'random' is not supported for finding inducing points in the full-scale-vecchia approximation "
+            "for non-Gaussian data");
     if (cfg_.num_ind_points <= 0) cfg_.num_ind_points = 200;   // re_model_template.h:320-330
     if (cfg_.num_neighbors <= 0) cfg_.num_neighbors = 30;      // :288-297
     if (!(cfg_.cover_tree_radius > 0.)) Fatal("cover_tree_radius must be > 0");
@@ -204,6 +210,8 @@ REModelAMD::REModelAMD(const ModelConfig& cfg, const double* coords_colmajor) : 
     d_X_.alloc((size_t)n * d);
     HIP_CHECK(hipMemcpyAsync(d_X_.get(), coords_vo_.data(), sizeof(double) * n * d, hipMemcpyHostToDevice, stream_));
     vif_.reset(new VifSolver(n, d, d_X_.get(), Z, nbr, m, stream_));
+    vif_nbr_ = nbr;
+    if (cfg_.latent) vif_lap_.reset(new VifLaplace(vif_.get(), nbr, coords_vo_, stream_));
   } else {
     coords_vo_ = coords_;
     d_X_.alloc((size_t)n * d);
@@ -287,6 +295,7 @@ REModelAMD::~REModelAMD() {
   dense_.reset();
   dense_lap_.reset();
   vfisher_.reset();
+  vif_lap_.reset();
   vif_.reset();
   fitc_lap_.reset();
   fitc_.reset();

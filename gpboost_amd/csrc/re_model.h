@@ -23,6 +23,7 @@
 #include "dense_laplace.h"
 #include "fitc_laplace.h"
 #include "vif.h"
+#include "vif_laplace.h"
 #include "vecchia_fisher.h"
 #include "latent.h"
 #include "optim.h"
@@ -321,7 +322,9 @@ class REModelAMD {
   std::unique_ptr<DenseLaplace> dense_lap_; // gp_approx = "none", non-Gaussian likelihood (Laplace)
   double sum_log_y_ = 0.;                   // likelihood 'gamma': sum log y (its normalizing constant)
   std::vector<int> est_idx_;                // estimate_cov_par_index (empty: all estimated)
-  std::unique_ptr<VifSolver> vif_;          // gp_approx = "full_scale_vecchia" (Gaussian likelihood)
+  std::unique_ptr<VifSolver> vif_;          // gp_approx = "full_scale_vecchia"
+  std::unique_ptr<VifLaplace> vif_lap_;     // gp_approx = "full_scale_vecchia", non-Gaussian likelihood (Laplace)
+  std::vector<int> vif_nbr_;                // the full-scale Vecchia neighbour lists (host, model order)
   std::unique_ptr<VecchiaFisher> vfisher_;  // gp_approx = "vecchia", Gaussian: standard deviations (lazy)
   std::mt19937 fitc_rng_;              // the model's generator after the inducing-point selection
   std::mt19937 pred_ref_gen_;          // the likelihood's cg_generator_ (default seed) for reference draws
@@ -331,6 +334,7 @@ class REModelAMD {
   LatentSolverBase* lat() const {
     if (latent_) return latent_.get();
     if (dense_lap_) return dense_lap_.get();
+    if (vif_lap_) return vif_lap_.get();
     return fitc_lap_.get();
   }
   std::vector<double> y_vo_;          // host copy (Vecchia order) for the latent solver

@@ -37,6 +37,7 @@ void REModelAMD::SetLatentOffset(const double* fe) {
     has_offset_ = true;
   }
   if (lat()) lat()->SetOffset(has_offset_ ? offset_vo_.data() : nullptr);
+  if (vif_lap_) vif_lap_->SetGradOffset(fe);   // data order: the reference's covariance gradient (vif_laplace.h)
 }
 
 void REModelAMD::SetResponseAndOffset(const double* y, const double* fixed_effects) {
@@ -337,11 +338,18 @@ void REModelAMD::SetLikelihood(const std::string& likelihood) {
   c.likelihood = likelihood;
   const int lik = parse_likelihood(likelihood);
   const bool dense = c.gp_approx == "none";
-  const bool latent = c.gp_approx == "vecchia_latent" || ((vecchia_ || fitc_ || dense) && lik != kLikGaussian);
-  if (vif_ && lik != kLikGaussian)
-    Fatal("gp_approx = 'full_scale_vecchia' with likelihood '%s' (Laplace approximation) is not supported by "
-          "gpboost_amd (supported: gaussian)", likelihood.c_str());
-  if (dense) {   // gp_approx = "none": DenseLaplace (Cholesky) for the Laplace likelihoods, DenseSolver for gaussian
+  const bool latent = c.gp_approx == "vecchia_latent" || ((vecchia_ || fitc_ || vif_ || dense) && lik != kLikGaussian);
+  if (vif_) {   // full-scale Vecchia: the Laplace solver on the same inducing points and neighbours (Cholesky)
+    if (latent && !vif_lap_) {
+      if (c.ind_points_selection == "random")
+        Fatal("Method 'random' is not supported for finding inducing points in the full-scale-vecchia approximation "
+              "for non-Gaussian data");
+      vif_lap_.reset(new VifLaplace(vif_.get(), vif_nbr_, coords_vo_, stream_));
+    } else if (!latent) {
+      vif_lap_.reset();
+    }
+    c.matrix_inversion_method = "cholesky";
+  } else if (dense) {   // gp_approx = "none": DenseLaplace (Cholesky) for the Laplace likelihoods, DenseSolver for gaussian
     if (latent && !dense_lap_) {
       std::vector<int> uniq, idx;
       unique_locations(coords_.data(), cfg_.n, cfg_.d, uniq, idx);

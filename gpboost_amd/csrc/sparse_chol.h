@@ -174,6 +174,8 @@ class SparseChol {
   // elimination positions mapped back to the labels): the reference's TriangularSolveGivenCholesky(L, Maux)
   // for predictive variances (likelihoods.h:6765); column norms are label-invariant.
   void ForwardCols(const double* B, double* X, int nrhs);
+  // X = A^-1 B for nrhs columns (device column-major n x nrhs, ld n, matrix labels; X may alias B)
+  void SolveMulti(const double* B, double* X, int nrhs);
   // 2 sum log L_ii (synchronises)
   double LogDet();
   // non-positive pivots of the last factorization (synchronises)

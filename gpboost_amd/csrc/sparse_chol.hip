@@ -827,6 +827,8 @@ void SparseChol::Solve(const double* b, double* x) { SolveCols(b, x, 1, false); 
 
 void SparseChol::ForwardCols(const double* B, double* X, int nrhs) { SolveCols(B, X, nrhs, true); }
 
+void SparseChol::SolveMulti(const double* B, double* X, int nrhs) { SolveCols(B, X, nrhs, false); }
+
 void SparseChol::SelectedInverse(double* tr_bdb, double* tr_da, double* diagS) {
   if (!factored_) Fatal("sparse Cholesky: selected inverse before a factorization");
   if (d_S_.size() < (size_t)std::max<int64_t>(plan_.front_doubles, 1)) d_S_.alloc(std::max<int64_t>(plan_.front_doubles, 1));

@@ -60,6 +60,12 @@ class VifSolver {
                int mp, bool cond_all, double* mean, double* pvar, double* pcov);
 
  private:
+  friend class VifLaplace;   // the Laplace approximation for non-Gaussian likelihoods (vif_laplace.h)
+  // the likelihood-independent part of an evaluation: the low-rank part (K_mn, K_mm,s, L, V), with grad the
+  // derivative blocks (dK, A, P_0, P_1), the residual factor (+ column-order values) and the Woodbury
+  // matrix M = K_mm,s + BK^T D^-1 BK factored in place (F_->W_ = L_M, Wi_ = L_M^-1, WiT_); red[0] = log det
+  // K_mm,s, red[1] = log det M; M_copy (nullable, ldm x ldm): M before its factorization
+  void Prepare(int cov_type, double var, double phi, bool grad, double* red, double* M_copy = nullptr);
   void Rows(int cov_type, double var, double phi, bool grad);
   // out = B in (self = 1) or dB in (self = 0) over m-vector columns; div: then times D^-1; out_div
   // (nullable): the same columns times D^-1 as a second output
@@ -74,6 +80,7 @@ class VifSolver {
 
   std::unique_ptr<FitcSolver> F_;
   int n_, d_, m_, ldm_, nn_;
+  bool latent_ = false;   // residual rows of the latent form (no nugget; JITTER_MULT_VECCHIA on the neighbour diagonal)
   hipStream_t s_;
   const double* d_X_;
   DevBuf<int> nbr_, tptr_, trow_, tslot_;

@@ -116,6 +116,8 @@ struct VifRowsArgs {
   double var, phi;
   int r1;   // doubles of the staging / residual-matrix region
   int i0;   // first row (prediction rows follow the n observed points); nbr / Bv / D are indexed by i - i0
+  double nugget;   // 1 (Gaussian likelihood, transformed scale) or 0 (latent form of the non-Gaussian likelihoods)
+  double cjit;     // multiplier of the neighbour matrix's diagonal: 1, or JITTER_MULT_VECCHIA without a nugget
   double* Bv;
   double* D;
   double* dBv0;
@@ -228,7 +230,7 @@ __global__ void __launch_bounds__(kT) vif_rows_kernel(VifRowsArgs a) {
     const int p = e / k, b = e - p * k;
     double c = a.var, dc = 0.;
     if (p != b) cov_dcov<COV>(dist_pts(a.X, a.d, idx[p], idx[b]), a.var, a.phi, c, dc);
-    C[e] = c + (p == b ? 1. : 0.) - gram[p * S + b];
+    C[e] = p == b ? (a.nugget + c - gram[p * S + b]) * a.cjit : c - gram[p * S + b];
     if (GRAD) {
       dC0[e] = c - (gram[SS + p * S + b] + gram[SS + b * S + p]);
       dC1[e] = dc - (gram[2 * SS + p * S + b] + gram[2 * SS + b * S + p]);
@@ -244,7 +246,7 @@ __global__ void __launch_bounds__(kT) vif_rows_kernel(VifRowsArgs a) {
     }
   }
   if (tid == 0) {
-    scal[0] = 1. + a.var - gram[k * S + k];
+    scal[0] = a.nugget + a.var - gram[k * S + k];
     if (GRAD) {
       scal[1] = a.var - 2. * gram[SS + k * S + k];
       scal[2] = -2. * gram[2 * SS + k * S + k];
@@ -405,7 +407,7 @@ __global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
       vecs[2][lane] = dc - (gram[2][lane * LD + k] + gram[2][k * LD + lane]);
     }
   }
-  d0 = 1. + var - gram[0][k * LD + k];
+  d0 = a.nugget + var - gram[0][k * LD + k];
   if (GRAD) {
     dd0 = var - 2. * gram[1][k * LD + k];
     dd1 = -2. * gram[2][k * LD + k];
@@ -420,7 +422,7 @@ __global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
       const int p = e / k, b = e - p * k;
       double c = var, dc = 0.;
       if (p != b) cov_dcov<COV>(dist_pts(a.X, a.d, idx[p], idx[b]), var, phi, c, dc);
-      C[p * LD + b] = c + (p == b ? 1. : 0.) - C[p * LD + b];
+      C[p * LD + b] = p == b ? (a.nugget + c - C[p * LD + b]) * a.cjit : c - C[p * LD + b];
       if (GRAD) {
         dv0[t] = c - (gram[GRAD ? 1 : 0][p * LD + b] + gram[GRAD ? 1 : 0][b * LD + p]);
         dv1[t] = dc - (gram[GRAD ? 2 : 0][p * LD + b] + gram[GRAD ? 2 : 0][b * LD + p]);
@@ -815,6 +817,8 @@ void VifSolver::Rows(int cov_type, double var, double phi, bool grad) {
   a.n = n_; a.d = d_; a.nn = nn_; a.mi = m_; a.ldm = ldm_;
   a.V = F_->V_.get(); a.P0 = P0_.get(); a.P1 = P1_.get();
   a.var = var; a.phi = phi;
+  a.nugget = latent_ ? 0. : 1.;
+  a.cjit = latent_ ? 1. + 1e-10 : 1.;   // JITTER_MULT_VECCHIA (utils.h:36; Vecchia_utils.cpp:1546-1548)
   a.r1 = rows_r1(nn_, grad);
   a.Bv = Bv_.get(); a.D = D_.get(); a.dBv0 = dBv0_.get(); a.dBv1 = dBv1_.get(); a.dD0 = dD0_.get(); a.dD1 = dD1_.get();
   const size_t lds = rows_lds_bytes(nn_, grad);
@@ -871,13 +875,10 @@ void VifSolver::ColDot(const double* M, const double* w, const double* M2, doubl
   HIP_CHECK(hipGetLastError());
 }
 
-void VifSolver::Eval(int cov_type, double var, double phi, const double* d_y, bool want_grad, double* sums,
-                     double* kernel_ms) {
+void VifSolver::Prepare(int cov_type, double var, double phi, bool want_grad, double* red, double* M_copy) {
   FitcSolver& F = *F_;
   const int n = n_, m = m_, ldm = ldm_;
   const size_t mn = (size_t)ldm * n;
-  double* red = red_.get();
-  HIP_CHECK(hipEventRecord(ev_[0], s_));
   // low-rank part (CalcSigmaComps): K_mn, K_mm, K_mm,s, dK_mm, L, L^-1, V = L^-1 K_mn, K_mm,s^-1; red[0] =
   // log det K_mm,s
   F.Prior(cov_type, var, phi, red);
@@ -914,10 +915,22 @@ void VifSolver::Eval(int cov_type, double var, double phi, const double* d_y, bo
   const int chunks = gemm_f64_splitk(s_, m, m, n, BK_.get(), ldm, 0, F.Kd_.get(), ldm, 1, F.part_.get(), ldm, mm, 2048,
                                      F.max_chunks_);
   fitc_wsum(s_, F.part_.get(), chunks, mm, m, ldm, F.Ks_.get(), F.W_.get());
+  if (M_copy != nullptr)
+    HIP_CHECK(hipMemcpyAsync(M_copy, F.W_.get(), sizeof(double) * mm, hipMemcpyDeviceToDevice, s_));
   chol_lower(s_, F.W_.get(), F.Wi_.get(), m, ldm, F.info_.get());
   launch_logdet_chol(s_, F.W_.get(), ldm, m, red + 1);
   trtri_lower(s_, F.W_.get(), F.Wi_.get(), F.T_.get(), 0, m, ldm);
   fitc_lower_t(s_, F.Wi_.get(), m, ldm, F.WiT_.get());
+}
+
+void VifSolver::Eval(int cov_type, double var, double phi, const double* d_y, bool want_grad, double* sums,
+                     double* kernel_ms) {
+  if (latent_) Fatal("VifSolver::Eval is the Gaussian likelihood's evaluation (the model is latent)");
+  FitcSolver& F = *F_;
+  const int n = n_, m = m_, ldm = ldm_;
+  double* red = red_.get();
+  HIP_CHECK(hipEventRecord(ev_[0], s_));
+  Prepare(cov_type, var, phi, want_grad, red);
   HIP_CHECK(hipEventRecord(ev_[1], s_));
   // y_aux = R^-1 y - R^-1 K M^-1 K^T R^-1 y with R^-1 = B^T D^-1 B (CalcYAux :8910-8925)
   double* v = vec_.get();
@@ -1094,6 +1107,8 @@ void VifSolver::Predict(int cov_type, double var, double phi, const double* d_y,
     a.n = na; a.d = d; a.nn = mp; a.mi = m; a.ldm = ldm;
     a.V = Va.get(); a.P0 = nullptr; a.P1 = nullptr;
     a.var = var; a.phi = phi;
+    a.nugget = latent_ ? 0. : 1.;
+    a.cjit = latent_ ? 1. + 1e-10 : 1.;
     a.r1 = rows_r1(mp, false);
     a.i0 = n;
     a.Bv = Bvp.get(); a.D = Dp.get();

@@ -130,8 +130,9 @@ def test_vif_refusals():
     X = synthetic.bench_coords(300)
     with pytest.raises(GPBoostError, match="iterative"):
         GPModel(gp_coords=X, gp_approx="full_scale_vecchia", num_ind_points=20, matrix_inversion_method="iterative")
-    with pytest.raises(GPBoostError, match="not supported"):
-        GPModel(gp_coords=X, gp_approx="vif", num_ind_points=20, likelihood="bernoulli_logit")
+    with pytest.raises(GPBoostError, match="random"):   # non-Gaussian VIF: kmeans++ / cover tree only (reference)
+        GPModel(gp_coords=X, gp_approx="vif", num_ind_points=20, likelihood="bernoulli_logit",
+                ind_points_selection="random")
     with pytest.raises(GPBoostError, match="num_neighbors"):
         GPModel(gp_coords=X, gp_approx="vif", num_ind_points=20, num_neighbors=60)
     gm = GPModel(gp_coords=X, gp_approx="vif", num_ind_points=20, num_neighbors=10)
