@@ -741,6 +741,10 @@ void REModelAMD::PredictVif(const double* y, int n_pred, const double* coords_pr
   if (world_ > 1) Fatal("predictions are only available on single-rank models");
   if (n_pred <= 0) Fatal("num_data_pred must be > 0");
   if (coords_pred == nullptr) Fatal("gp_coords_data_pred must be provided");
+  if (cfg_.latent) {
+    PredictVifLaplace(y, n_pred, coords_pred, cov_pars, predict_cov_mat, predict_var, predict_response, out, mean_add);
+    return;
+  }
   const bool cond_all = vecchia_pred_type_ == "order_obs_first_cond_all";
   if (!cond_all && vecchia_pred_type_ != "order_obs_first_cond_obs_only") {
     if (vecchia_pred_type_ == "order_pred_first")   // re_model_template.h:3748-3750
@@ -784,6 +788,53 @@ void REModelAMD::PredictVif(const double* y, int n_pred, const double* coords_pr
   } else if (predict_var) {
     for (int p = 0; p < n_pred; ++p) out[n_pred + p] = (var[p] - nug) * trafo[0];
   }
+}
+
+// gp_approx = "full_scale_vecchia" with a Laplace likelihood (re_model_template.h:3811-3846 ->
+// CalcPredVecchiaObservedFirstOrder for Bpo / Bp / Dp of the latent residual and PredictLaplaceApproxFSVA,
+// likelihoods.h:6060-6551): the mode at the parameters (found from zero), latent means, variances or covariance
+// matrices by VifLaplace::Predict, the prediction points' fixed effects added, the response transform.
+void REModelAMD::PredictVifLaplace(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,
+                                   bool predict_cov_mat, bool predict_var, bool predict_response, double* out,
+                                   const double* mean_add) {
+  const std::string& t = vecchia_pred_type_;
+  const bool cond_all = t == "latent_order_obs_first_cond_all" || t == "order_obs_first_cond_all";
+  if (!cond_all && t != "latent_order_obs_first_cond_obs_only" && t != "order_obs_first_cond_obs_only")
+    Fatal("Prediction type '%s' is not supported for the Veccia approximation.", t.c_str());   // :3848-3850
+  UseDevice();
+  if (y != nullptr) SetY(y);
+  if (!y_set_) Fatal("response variable y has not been set (pass y or evaluate the likelihood first)");
+  double cp[2];
+  if (cov_pars != nullptr) std::copy(cov_pars, cov_pars + 2, cp);
+  else if ((int)last_cov_pars_.size() == 2) std::copy(last_cov_pars_.begin(), last_cov_pars_.end(), cp);
+  else Fatal("cov_pars must be provided (no previous evaluation)");
+  if (predict_cov_mat && predict_response)
+    Fatal("predictive covariance matrices of the response are not supported for likelihood '%s' by gpboost_amd "
+          "(use predict_response = false or predict_var)", cfg_.likelihood.c_str());
+  EvalLatent(cp, false);   // the mode at these parameters (found from zero)
+  const int n = cfg_.n, d = cfg_.d, na = n + n_pred;
+  const int mp = std::min(num_neighbors_pred_, cond_all ? na - 1 : n);
+  std::vector<double> xa((size_t)na * d);
+  std::copy(coords_vo_.begin(), coords_vo_.begin() + (size_t)n * d, xa.begin());
+  for (int p = 0; p < n_pred; ++p)
+    for (int q = 0; q < d; ++q) xa[(size_t)(n + p) * d + q] = coords_pred[(size_t)q * n_pred + p];
+  std::vector<int> nb((size_t)n_pred * mp);
+  const int end_at = cond_all ? -1 : n - 1;
+  if (d <= 3 && mp <= 64) vecchia_neighbors_gpu(xa.data(), na, d, mp, n, na, nb.data(), stream_, end_at);
+  else vecchia_neighbors(xa.data(), na, d, mp, n, na, nb.data(), end_at);
+  if (cond_all)
+    for (int p = 0; p < n_pred; ++p)
+      for (int r = std::min(n + p, mp); r < mp; ++r) nb[(size_t)p * mp + r] = -1;
+  const bool want_var = predict_var || predict_response;
+  std::vector<double> mean(n_pred), var(want_var ? n_pred : 0), cov(predict_cov_mat ? (size_t)n_pred * n_pred : 0);
+  vif_lap_->Predict(cfg_.cov_type, cp[0], range_trafo(cfg_.cov_type, cp[1]), xa.data() + (size_t)n * d, n_pred, nb.data(),
+                    mp, cond_all, mean.data(), want_var ? var.data() : nullptr, predict_cov_mat ? cov.data() : nullptr);
+  if (mean_add != nullptr)
+    for (int p = 0; p < n_pred; ++p) mean[p] += mean_add[p];
+  if (predict_response) ResponseTransform(n_pred, mean.data(), var.data(), nullptr);
+  std::copy(mean.begin(), mean.end(), out);
+  if (predict_cov_mat) std::copy(cov.begin(), cov.end(), out + n_pred);
+  else if (predict_var) std::copy(var.begin(), var.end(), out + n_pred);
 }
 
 void REModelAMD::PredictFitc(const double* y, int n_pred, const double* coords_pred, const double* cov_pars,

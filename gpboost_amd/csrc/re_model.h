@@ -268,6 +268,8 @@ class REModelAMD {
                            const double* mean_add);
   void PredictVif(const double* y, int n_pred, const double* coords_pred, const double* cov_pars, bool predict_cov_mat,
                   bool predict_var, bool predict_response, double* out, const double* mean_add);
+  void PredictVifLaplace(const double* y, int n_pred, const double* coords_pred, const double* cov_pars, bool predict_cov_mat,
+                  bool predict_var, bool predict_response, double* out, const double* mean_add);
   void PredictFitc(const double* y, int n_pred, const double* coords_pred, const double* cov_pars, bool predict_cov_mat,
                    bool predict_var, bool predict_response, double* out, const double* mean_add);
   std::vector<int> FitcMatch(const std::vector<double>& xp_rowmajor, int n_pred) const;

@@ -67,6 +67,15 @@ class VifSolver {
   // K_mm,s, red[1] = log det M; M_copy (nullable, ldm x ldm): M before its factorization
   void Prepare(int cov_type, double var, double phi, bool grad, double* red, double* M_copy = nullptr);
   void Rows(int cov_type, double var, double phi, bool grad);
+  // the prediction points' residual rows (Xp host np x d after the n observed points, nbr host np x mp):
+  // KP = K_mp (m x np), Va = [V | L^-1 K_mp], Bvp (np x mp), Dp (np), dnb the neighbour lists on the device
+  void PredRows(int cov_type, double var, double phi, const double* Xp, int np, const int* nbr, int mp,
+                DevBuf<double>& KP, DevBuf<double>& Va, DevBuf<double>& Bvp, DevBuf<double>& Dp, DevBuf<int>& dnb);
+  // mo_p = sum over observed neighbours of B(p, j) r_j, Qt[:, p] = sum of B(p, j) M[:, j] (M m x n; Qt m x np)
+  void PredBpo(int np, int mp, const int* dnb, const double* Bvp, const double* r, const double* M, double* mo,
+               double* Qt);
+  // out_i = M[:, i] . w (w != nullptr) or M[:, i] . M2[:, i] for `cols` columns
+  void ColDotN(const double* M, const double* w, const double* M2, int cols, double* out);
   // out = B in (self = 1) or dB in (self = 0) over m-vector columns; div: then times D^-1; out_div
   // (nullable): the same columns times D^-1 as a second output
   void BRow(const double* in, const double* coef, double self, bool div, double* out, double* out_div = nullptr);

@@ -870,6 +870,17 @@ void VifSolver::Gemv(const double* M, const double* x, double* out) {
   HIP_CHECK(hipGetLastError());
 }
 
+void VifSolver::PredBpo(int np, int mp, const int* dnb, const double* Bvp, const double* r, const double* M, double* mo,
+                        double* Qt) {
+  hipLaunchKernelGGL(vif_pred_bpo_kernel, dim3(np), dim3(64), 0, s_, np, n_, mp, dnb, Bvp, r, M, m_, ldm_, mo, Qt);
+  HIP_CHECK(hipGetLastError());
+}
+
+void VifSolver::ColDotN(const double* M, const double* w, const double* M2, int cols, double* out) {
+  hipLaunchKernelGGL(vif_coldot_kernel, dim3((cols + 3) / 4), dim3(kT), 0, s_, M, w, M2, cols, m_, ldm_, out);
+  HIP_CHECK(hipGetLastError());
+}
+
 void VifSolver::ColDot(const double* M, const double* w, const double* M2, double* out) {
   hipLaunchKernelGGL(vif_coldot_kernel, dim3((n_ + 3) / 4), dim3(kT), 0, s_, M, w, M2, n_, m_, ldm_, out);
   HIP_CHECK(hipGetLastError());
@@ -1071,6 +1082,56 @@ void VifSolver::GetFactor(double* D, double* Bv) const {
   HIP_CHECK(hipStreamSynchronize(s_));
 }
 
+// The prediction points' residual Vecchia rows (Vecchia_utils.cpp:1807-1896, no derivatives): KP = K_mp (m x np),
+// Va = [V | V_p] with V_p = L^-1 K_mp (chol_ip_cross_cov_pred, :1698-1699), Bvp (np x mp), Dp (np) from the row
+// kernel at the row offset n (the latent form without a nugget when latent_), dnb the neighbour lists on the device.
+void VifSolver::PredRows(int cov_type, double var, double phi, const double* Xp, int np, const int* nbr, int mp,
+                         DevBuf<double>& KP, DevBuf<double>& Va, DevBuf<double>& Bvp, DevBuf<double>& Dp,
+                         DevBuf<int>& dnb) {
+  if (mp < 1 || mp > kMaxNn) Fatal("num_neighbors_pred = %d is not supported for gp_approx = 'full_scale_vecchia' (1..%d)",
+                                   mp, kMaxNn);
+  FitcSolver& F = *F_;
+  const int n = n_, m = m_, ldm = ldm_, d = d_;
+  const int na = n + np;
+  DevBuf<double> Xa((size_t)na * d);
+  KP.alloc((size_t)ldm * np);
+  Va.alloc((size_t)ldm * na);
+  Bvp.alloc((size_t)np * mp);
+  Dp.alloc(np);
+  dnb.alloc((size_t)np * mp);
+  HIP_CHECK(hipMemcpyAsync(Xa.get(), d_X_, sizeof(double) * (size_t)n * d, hipMemcpyDeviceToDevice, s_));
+  HIP_CHECK(hipMemcpyAsync(Xa.get() + (size_t)n * d, Xp, sizeof(double) * (size_t)np * d, hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipMemcpyAsync(dnb.get(), nbr, sizeof(int) * (size_t)np * mp, hipMemcpyHostToDevice, s_));
+  HIP_CHECK(hipMemsetAsync(KP.get(), 0, sizeof(double) * KP.size(), s_));
+  fitc_kmn(s_, cov_type, Xa.get() + (size_t)n * d, F.dZ_.get(), np, m, d, ldm, var, phi, KP.get());   // K_mp
+  HIP_CHECK(hipMemcpyAsync(Va.get(), F.V_.get(), sizeof(double) * (size_t)ldm * n, hipMemcpyDeviceToDevice, s_));
+  HIP_CHECK(hipMemsetAsync(Va.get() + (size_t)ldm * n, 0, sizeof(double) * (size_t)ldm * np, s_));
+  gemm_f64(s_, m, np, m, 1., F.Li_.get(), ldm, 0, KP.get(), ldm, 0, 0., Va.get() + (size_t)ldm * n, ldm, 0, 1, 0, 0);
+  VifRowsArgs a{};
+  a.X = Xa.get();
+  a.nbr = dnb.get();
+  a.n = na; a.d = d; a.nn = mp; a.mi = m; a.ldm = ldm;
+  a.V = Va.get(); a.P0 = nullptr; a.P1 = nullptr;
+  a.var = var; a.phi = phi;
+  a.nugget = latent_ ? 0. : 1.;
+  a.cjit = latent_ ? 1. + 1e-10 : 1.;
+  a.r1 = rows_r1(mp, false);
+  a.i0 = n;
+  a.Bv = Bvp.get(); a.D = Dp.get();
+  const size_t lds = rows_lds_bytes(mp, false);
+  dispatch_cov_vif(cov_type, [&](auto c) {
+    constexpr int COV = decltype(c)::value;
+    if (mp <= 31) {
+      hipLaunchKernelGGL((vif_rows_mfma_kernel<COV, false>), dim3(np), dim3(64), 0, s_, a);
+    } else {
+      HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&vif_rows_kernel<COV, false>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+      hipLaunchKernelGGL((vif_rows_kernel<COV, false>), dim3(np), dim3(kT), lds, s_, a);
+    }
+  });
+  HIP_CHECK(hipGetLastError());
+}
+
 void VifSolver::Predict(int cov_type, double var, double phi, const double* d_y, const double* Xp, int np,
                         const int* nbr, int mp, bool cond_all, double* mean, double* pvar, double* pcov) {
   if (np <= 0) return;
@@ -1079,52 +1140,15 @@ void VifSolver::Predict(int cov_type, double var, double phi, const double* d_y,
   if (cond_all && pcov != nullptr && np > 20000)
     Fatal("order_obs_first_cond_all with predict_cov_mat is limited to num_data_pred <= 20000 in gpboost_amd");
   FitcSolver& F = *F_;
-  const int n = n_, m = m_, ldm = ldm_, d = d_;
+  const int n = n_, m = m_, ldm = ldm_;
   double sums[6], kms[2];
   Eval(cov_type, var, phi, d_y, false, sums, kms);   // factor, Woodbury M, w = M^-1 K^T R^-1 y, kw = K w
   if (std::isnan(sums[0])) Fatal("full_scale_vecchia prediction: the Woodbury matrix is not positive definite");
   const double* w = mvec_.get() + ldm;
   const double* kw = vec_.get() + 2 * (size_t)n;
-  // coordinates and V of the observed points followed by the prediction points
-  const int na = n + np;
-  DevBuf<double> Xa((size_t)na * d), KP((size_t)ldm * np), Va((size_t)ldm * na), Bvp((size_t)np * mp), Dp(np),
-      r(n), mo(np), Qt((size_t)ldm * np), kpw(np);
-  DevBuf<int> dnb((size_t)np * mp);
-  HIP_CHECK(hipMemcpyAsync(Xa.get(), d_X_, sizeof(double) * (size_t)n * d, hipMemcpyDeviceToDevice, s_));
-  HIP_CHECK(hipMemcpyAsync(Xa.get() + (size_t)n * d, Xp, sizeof(double) * (size_t)np * d, hipMemcpyHostToDevice, s_));
-  HIP_CHECK(hipMemcpyAsync(dnb.get(), nbr, sizeof(int) * (size_t)np * mp, hipMemcpyHostToDevice, s_));
-  HIP_CHECK(hipMemsetAsync(KP.get(), 0, sizeof(double) * KP.size(), s_));
-  fitc_kmn(s_, cov_type, Xa.get() + (size_t)n * d, F.dZ_.get(), np, m, d, ldm, var, phi, KP.get());   // K_mp
-  HIP_CHECK(hipMemcpyAsync(Va.get(), F.V_.get(), sizeof(double) * (size_t)ldm * n, hipMemcpyDeviceToDevice, s_));
-  HIP_CHECK(hipMemsetAsync(Va.get() + (size_t)ldm * n, 0, sizeof(double) * (size_t)ldm * np, s_));
-  // V_p = L^-1 K_mp (chol_ip_cross_cov_pred, :1698-1699)
-  gemm_f64(s_, m, np, m, 1., F.Li_.get(), ldm, 0, KP.get(), ldm, 0, 0., Va.get() + (size_t)ldm * n, ldm, 0, 1, 0, 0);
-  // residual Vecchia rows of the prediction points (:1807-1896), no derivatives
-  {
-    VifRowsArgs a{};
-    a.X = Xa.get();
-    a.nbr = dnb.get();
-    a.n = na; a.d = d; a.nn = mp; a.mi = m; a.ldm = ldm;
-    a.V = Va.get(); a.P0 = nullptr; a.P1 = nullptr;
-    a.var = var; a.phi = phi;
-    a.nugget = latent_ ? 0. : 1.;
-    a.cjit = latent_ ? 1. + 1e-10 : 1.;
-    a.r1 = rows_r1(mp, false);
-    a.i0 = n;
-    a.Bv = Bvp.get(); a.D = Dp.get();
-    const size_t lds = rows_lds_bytes(mp, false);
-    dispatch_cov_vif(cov_type, [&](auto c) {
-      constexpr int COV = decltype(c)::value;
-      if (mp <= 31) {
-        hipLaunchKernelGGL((vif_rows_mfma_kernel<COV, false>), dim3(np), dim3(64), 0, s_, a);
-      } else {
-        HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(&vif_rows_kernel<COV, false>),
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        hipLaunchKernelGGL((vif_rows_kernel<COV, false>), dim3(np), dim3(kT), lds, s_, a);
-      }
-    });
-    HIP_CHECK(hipGetLastError());
-  }
+  DevBuf<double> KP, Va, Bvp, Dp, r(n), mo(np), Qt((size_t)ldm * np), kpw(np);
+  DevBuf<int> dnb;
+  PredRows(cov_type, var, phi, Xp, np, nbr, mp, KP, Va, Bvp, Dp, dnb);
   // mean = -Bpo (y - K w) [Bp^-1] + K_pm w (:1903-1908)
   hipLaunchKernelGGL(vif_sub_kernel, dim3((n + kT - 1) / kT), dim3(kT), 0, s_, n, d_y, kw, r.get());
   hipLaunchKernelGGL(vif_pred_bpo_kernel, dim3(np), dim3(64), 0, s_, np, n, mp, dnb.get(), Bvp.get(), r.get(),

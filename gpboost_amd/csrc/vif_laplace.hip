@@ -236,6 +236,57 @@ __global__ void __launch_bounds__(kT) vl_gamma_kernel(int n, const double* __res
   }
 }
 
+// point-major m x n: out_i = K_i * s_i
+__global__ void __launch_bounds__(kT) vl_colscale_kernel(int n, int m, int ldm, const double* __restrict__ K,
+                                                         const double* __restrict__ sc, double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  const double f = sc[i];
+  for (int q = lane; q < m; q += 64) out[(size_t)i * ldm + q] = K[(size_t)i * ldm + q] * f;
+}
+
+// out = add (nullable) + sum of the split-K chunks
+__global__ void __launch_bounds__(kT) vl_psum_kernel(const double* __restrict__ P, int chunks, long stride, int m, int ldm,
+                                                     const double* __restrict__ add, double* __restrict__ out) {
+  const int j = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int k = blockIdx.y * 4 + (threadIdx.x >> 6);
+  if (j >= m || k >= m) return;
+  const size_t e = (size_t)j + (size_t)k * ldm;
+  double s = P[e];
+  for (int z = 1; z < chunks; ++z) s += P[(size_t)z * stride + e];
+  out[e] = add ? add[e] + s : s;
+}
+
+// out[p] = sum_k M(k, p)^2 over the n rows of column p (column-major n x np), one block per column
+__global__ void __launch_bounds__(kT) vl_colsq_kernel(int n, const double* __restrict__ M, double* __restrict__ out) {
+  __shared__ double red[4];
+  const double* c = M + (size_t)blockIdx.x * n;
+  double acc = 0.;
+  for (int k = threadIdx.x; k < n; k += kT) acc += c[k] * c[k];
+  const double s = block_sum(acc, red);
+  if (threadIdx.x == 0) out[blockIdx.x] = s;
+}
+
+// the low-rank terms of the predictive variance (likelihoods.h:6539-6543), columns p of m x np sets:
+// |Vp|^2 - Sig . X1 + X2 . X1 + 2 Sig . X3 - 2 X2 . X3 + X4 . X3
+__global__ void __launch_bounds__(kT) vl_pvar_kernel(int np, int m, int ldm, const double* __restrict__ Vp,
+                                                     const double* __restrict__ Sig, const double* __restrict__ X1,
+                                                     const double* __restrict__ X2, const double* __restrict__ X3,
+                                                     const double* __restrict__ X4, double* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int p = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (p >= np) return;
+  const size_t o = (size_t)p * ldm;
+  double s = 0.;
+  for (int q = lane; q < m; q += 64) {
+    const double v = Vp[o + q], sg = Sig[o + q], x1 = X1[o + q], x2 = X2[o + q], x3 = X3[o + q], x4 = X4[o + q];
+    s += v * v - sg * x1 + x2 * x1 + 2. * sg * x3 - 2. * x2 * x3 + x4 * x3;
+  }
+  s = wsum64(s);
+  if (lane == 0) out[p] = s;
+}
+
 }  // namespace
 
 VifLaplace::VifLaplace(VifSolver* vif, const std::vector<int>& nbr, const std::vector<double>& X, hipStream_t stream)
@@ -763,6 +814,192 @@ LatentResult VifLaplace::Eval(int cov_type, int lik, const double* trafo, double
     std::fprintf(stderr, "[vif laplace] %.2f ms: %d Newton steps (last factorization %.2f ms)\n", ms, res.newton_its,
                  chol_->last_factor_ms());
   return res;
+}
+
+
+// PredictLaplaceApproxFSVA, Cholesky branch (likelihoods.h:6060-6130, 6478-6548), at the mode of the last Eval:
+//   s = mode - K M^-1 C^T mode (sigma_inv_mode), mean = -Bpo s [Bp^-1] + K_pm K_mm,s^-1 C^T s
+//   SRW = A^-1 (W K), Mw2 = K_mm,s + C^T SRW, Sig = K_mm,s^-1 K_mp, X1 = M_aux_1^T = (C^T SRW)^T Sig,
+//   X2 = Mw2^-1 X1, X3 = M_aux_3^T = SRW^T Bpo^T [Bp^-T], X4 = Mw2^-1 X3, Maux = L_A^-1 P Bpo^T [Bp^-T]
+//   var = Dp [diag Bp^-1 Dp Bp^-T] + |Maux_p|^2 + |Vp_p|^2 - Sig.X1 + X2.X1 + 2 Sig.X3 - 2 X2.X3 + X4.X3
+//   cov = [Dp | Bp^-1 Dp Bp^-T] + Maux^T Maux + Vp^T Vp - X1^T Sig + X1^T X2 + X3^T Sig + Sig^T X3 - X3^T X2
+//         - X2^T X3 + X3^T X4
+void VifLaplace::Predict(int cov_type, double var, double phi, const double* Xp, int np, const int* nbr, int mp,
+                         bool cond_all, double* mean, double* pvar, double* pcov) {
+  if (np <= 0) return;
+  if (!evaluated_) Fatal("VifLaplace::Predict: no mode (evaluate the model at the parameters first)");
+  if (cond_all && (pcov != nullptr || pvar != nullptr) && np > 20000)
+    Fatal("latent_order_obs_first_cond_all with predictive (co)variances is limited to num_data_pred <= 20000 in "
+          "gpboost_amd");
+  FitcSolver& F = *V_->F_;
+  const int n = n_, m = m_, ldm = ldm_;
+  const long mm = (long)ldm * ldm;
+  DevBuf<double> KP, Va, Bvp, Dp;
+  DevBuf<int> dnb;
+  V_->PredRows(cov_type, var, phi, Xp, np, nbr, mp, KP, Va, Bvp, Dp, dnb);
+  double* sv = vec_.get();
+  double* ku = vec_.get() + (size_t)n;
+  double* mt = mv_.get();
+  double* mu = mv_.get() + ldm;
+  double* mtmp = mv_.get() + 2 * (size_t)ldm;
+  double* u2 = mv_.get() + 3 * (size_t)ldm;
+  // sigma_inv_mode (:6107)
+  V_->Gemv(C_.get(), mode_.get(), mt);
+  fitc_chol_solve(s_, F.Wi_.get(), F.WiT_.get(), mt, m, ldm, mtmp, mu);
+  V_->ColDot(F.Kmn_.get(), mu, nullptr, ku);
+  launch_axpby(n, 1., mode_.get(), -1., ku, sv, s_);
+  // mean (:6108-6115)
+  DevBuf<double> mo(np), kpw(np), Qscr((size_t)ldm * np);
+  V_->PredBpo(np, mp, dnb.get(), Bvp.get(), sv, F.Kmn_.get(), mo.get(), Qscr.get());
+  V_->Gemv(C_.get(), sv, mt);
+  fitc_symv(s_, F.Kinv_.get(), mt, m, ldm, u2);
+  V_->ColDotN(KP.get(), u2, nullptr, np, kpw.get());
+  std::vector<double> hmo(np), hkpw(np), hD(np), hB((size_t)np * mp);
+  HIP_CHECK(hipMemcpyAsync(hmo.data(), mo.get(), sizeof(double) * np, hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipMemcpyAsync(hkpw.data(), kpw.get(), sizeof(double) * np, hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipMemcpyAsync(hD.data(), Dp.get(), sizeof(double) * np, hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipMemcpyAsync(hB.data(), Bvp.get(), sizeof(double) * hB.size(), hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  // Bp x = b (unit lower; its off-diagonal entries are the rows' values at earlier prediction points)
+  auto bp_solve = [&](double* x, size_t stride, int width) {
+    for (int p = 0; p < np; ++p)
+      for (int j = 0; j < mp; ++j) {
+        const int q = nbr[(size_t)p * mp + j];
+        if (q < n) continue;
+        const double b = hB[(size_t)p * mp + j];
+        for (int c = 0; c < width; ++c) x[(size_t)p * stride + c] -= b * x[(size_t)(q - n) * stride + c];
+      }
+  };
+  std::vector<double> mu_h(np);
+  for (int p = 0; p < np; ++p) mu_h[p] = -hmo[p];
+  if (cond_all) bp_solve(mu_h.data(), 1, 1);
+  for (int p = 0; p < np; ++p) mean[p] = mu_h[p] + hkpw[p];
+  if (pvar == nullptr && pcov == nullptr) return;
+  std::vector<double> Binv;
+  if (cond_all) {
+    Binv.assign((size_t)np * np, 0.);   // row-major: row p = e_p^T Bp^-1
+    for (int p = 0; p < np; ++p) Binv[(size_t)p * np + p] = 1.;
+    bp_solve(Binv.data(), np, np);
+  }
+  const size_t mnp = (size_t)ldm * np, mn = (size_t)ldm * n;
+  const double* Vp = Va.get() + (size_t)ldm * n;
+  DevBuf<double> Sig(mnp), X1(mnp), X2(mnp), X3(mnp), X4(mnp), CS(mm), mo2(np);
+  for (DevBuf<double>* b : {&Sig, &X1, &X2, &X3, &X4}) HIP_CHECK(hipMemsetAsync(b->get(), 0, sizeof(double) * mnp, s_));
+  gemm_f64(s_, m, np, m, 1., F.Kinv_.get(), ldm, 0, KP.get(), ldm, 0, 0., Sig.get(), ldm);
+  // SRW = A^-1 (W o K) (sigma_resid_plus_W_inv_cross_cov, :6480), point-major in T2_
+  for (DevBuf<double>* b : {&T1_, &T2_})
+    if (b->size() < mn) {
+      b->alloc(mn);
+      HIP_CHECK(hipMemsetAsync(b->get(), 0, sizeof(double) * mn, s_));
+    }
+  hipLaunchKernelGGL(vl_colscale_kernel, dim3((n + 3) / 4), dim3(kT), 0, s_, n, m, ldm, F.Kmn_.get(), w_.get(), T1_.get());
+  HIP_CHECK(hipGetLastError());
+  ToNM(T1_.get(), CL_.get());
+  chol_->SolveMulti(CL_.get(), CL_.get(), m);
+  double* SRW = T2_.get();
+  ToMN(CL_.get(), SRW);
+  // CS = C^T SRW; Mw2 = K_mm,s + CS (sigma_woodbury_2, :6481-6483): factor and inverse in M2_ / M2i_ / M2inv_
+  const int chunks = gemm_f64_splitk(s_, m, m, n, C_.get(), ldm, 0, SRW, ldm, 1, F.part_.get(), ldm, mm, 2048,
+                                     F.max_chunks_);
+  hipLaunchKernelGGL(vl_psum_kernel, dim3((m + 63) / 64, (m + 3) / 4), dim3(kT), 0, s_, F.part_.get(), chunks, mm, m, ldm,
+                     static_cast<const double*>(nullptr), CS.get());
+  hipLaunchKernelGGL(vl_psum_kernel, dim3((m + 63) / 64, (m + 3) / 4), dim3(kT), 0, s_, F.part_.get(), chunks, mm, m, ldm,
+                     F.Ks_.get(), M2_.get());
+  HIP_CHECK(hipGetLastError());
+  HIP_CHECK(hipMemsetAsync(info_.get(), 0, sizeof(int), s_));
+  chol_lower(s_, M2_.get(), M2i_.get(), m, ldm, info_.get());
+  trtri_lower(s_, M2_.get(), M2i_.get(), F.T_.get(), 0, m, ldm);
+  gemm_f64(s_, m, m, m, 1., M2i_.get(), ldm, 1, M2i_.get(), ldm, 0, 0., M2inv_.get(), ldm, 0, 0, 1, 1);
+  // X1 = CS^T Sig, X2 = Mw2^-1 X1, X3 = SRW^T Bpo^T [Bp^-T] (columns of M_aux_3^T), X4 = Mw2^-1 X3
+  gemm_f64(s_, m, np, m, 1., CS.get(), ldm, 1, Sig.get(), ldm, 0, 0., X1.get(), ldm);
+  gemm_f64(s_, m, np, m, 1., M2inv_.get(), ldm, 0, X1.get(), ldm, 0, 0., X2.get(), ldm);
+  V_->PredBpo(np, mp, dnb.get(), Bvp.get(), sv, SRW, mo2.get(), X3.get());
+  if (cond_all) {
+    std::vector<double> hQ(mnp);
+    HIP_CHECK(hipMemcpyAsync(hQ.data(), X3.get(), sizeof(double) * mnp, hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipStreamSynchronize(s_));
+    bp_solve(hQ.data(), ldm, m);
+    HIP_CHECK(hipMemcpyAsync(X3.get(), hQ.data(), sizeof(double) * mnp, hipMemcpyHostToDevice, s_));
+  }
+  gemm_f64(s_, m, np, m, 1., M2inv_.get(), ldm, 0, X3.get(), ldm, 0, 0., X4.get(), ldm);
+  int info = 0;
+  HIP_CHECK(hipMemcpyAsync(&info, info_.get(), sizeof(int), hipMemcpyDeviceToHost, s_));
+  HIP_CHECK(hipStreamSynchronize(s_));
+  if (info != 0) Fatal("full_scale_vecchia prediction: the Woodbury matrix K_mm + C^T (Sigma_resid^-1 + W)^-1 W K is not "
+                       "positive definite");
+  // Maux = L_A^-1 P Bpo^T [Bp^-T] (n x np columns; :6492-6505): Bpo^T over the observed neighbours
+  std::vector<int> nb_obs((size_t)np * mp);
+  for (size_t e = 0; e < nb_obs.size(); ++e) nb_obs[e] = nbr[e] >= 0 && nbr[e] < n ? nbr[e] : -1;
+  DevBuf<int> dnbo(nb_obs.size());
+  HIP_CHECK(hipMemcpyAsync(dnbo.get(), nb_obs.data(), sizeof(int) * nb_obs.size(), hipMemcpyHostToDevice, s_));
+  DevBuf<double> dvar(np);
+  const bool all_at_once = cond_all || pcov != nullptr;
+  const int chunk = all_at_once ? np : std::max(1, std::min(np, 256));
+  DevBuf<double> cols((size_t)n * chunk), Maux((size_t)n * chunk);
+  DevBuf<double> dcov;
+  if (pcov != nullptr) {
+    dcov.alloc((size_t)np * np);
+    HIP_CHECK(hipMemsetAsync(dcov.get(), 0, sizeof(double) * dcov.size(), s_));
+  }
+  DevBuf<double> dX;
+  if (cond_all) {   // the row-major Bp^-1 read column-major is X = Bp^-T
+    dX.alloc((size_t)np * np);
+    HIP_CHECK(hipMemcpyAsync(dX.get(), Binv.data(), sizeof(double) * Binv.size(), hipMemcpyHostToDevice, s_));
+  }
+  for (int p0 = 0; p0 < np; p0 += chunk) {
+    const int c = std::min(chunk, np - p0);
+    launch_chol_pred_cols(n, c, mp, dnbo.get() + (size_t)p0 * mp, Bvp.get() + (size_t)p0 * mp, cols.get(), s_);
+    if (cond_all) {
+      gemm_f64(s_, n, np, np, 1., cols.get(), n, 0, dX.get(), np, 0, 0., Maux.get(), n);
+      HIP_CHECK(hipMemcpyAsync(cols.get(), Maux.get(), sizeof(double) * (size_t)n * np, hipMemcpyDeviceToDevice, s_));
+    }
+    chol_->ForwardCols(cols.get(), Maux.get(), c);
+    hipLaunchKernelGGL(vl_colsq_kernel, dim3(c), dim3(kT), 0, s_, n, Maux.get(), dvar.get() + p0);
+    HIP_CHECK(hipGetLastError());
+    if (pcov != nullptr) gemm_f64(s_, np, np, n, 1., Maux.get(), n, 1, Maux.get(), n, 0, 0., dcov.get(), np);
+  }
+  if (pvar != nullptr) {
+    DevBuf<double> dv2(np);
+    hipLaunchKernelGGL(vl_pvar_kernel, dim3((np + 3) / 4), dim3(kT), 0, s_, np, m, ldm, Vp, Sig.get(), X1.get(), X2.get(),
+                       X3.get(), X4.get(), dv2.get());
+    HIP_CHECK(hipGetLastError());
+    launch_axpby(np, 1., dv2.get(), 1., dvar.get(), dvar.get(), s_);
+    HIP_CHECK(hipMemcpyAsync(pvar, dvar.get(), sizeof(double) * np, hipMemcpyDeviceToHost, s_));
+    HIP_CHECK(hipStreamSynchronize(s_));
+    for (int p = 0; p < np; ++p) {
+      double dpart = hD[p];
+      if (cond_all) {
+        dpart = 0.;
+        for (int q = 0; q <= p; ++q) dpart += Binv[(size_t)p * np + q] * Binv[(size_t)p * np + q] * hD[q];
+      }
+      pvar[p] += dpart;
+    }
+  }
+  if (pcov != nullptr) {
+    double* C = dcov.get();
+    gemm_f64(s_, np, np, m, 1., Vp, ldm, 1, Vp, ldm, 0, 1., C, np);
+    gemm_f64(s_, np, np, m, -1., X1.get(), ldm, 1, Sig.get(), ldm, 0, 1., C, np);
+    gemm_f64(s_, np, np, m, 1., X1.get(), ldm, 1, X2.get(), ldm, 0, 1., C, np);
+    gemm_f64(s_, np, np, m, 1., X3.get(), ldm, 1, Sig.get(), ldm, 0, 1., C, np);
+    gemm_f64(s_, np, np, m, 1., Sig.get(), ldm, 1, X3.get(), ldm, 0, 1., C, np);
+    gemm_f64(s_, np, np, m, -1., X3.get(), ldm, 1, X2.get(), ldm, 0, 1., C, np);
+    gemm_f64(s_, np, np, m, -1., X2.get(), ldm, 1, X3.get(), ldm, 0, 1., C, np);
+    gemm_f64(s_, np, np, m, 1., X3.get(), ldm, 1, X4.get(), ldm, 0, 1., C, np);
+    if (cond_all) {   // + Bp^-1 Dp Bp^-T = (D X)^T X with X = Bp^-T
+      std::vector<double> XD(Binv);
+      for (int p = 0; p < np; ++p)
+        for (int k = 0; k < np; ++k) XD[(size_t)p * np + k] *= hD[k];
+      DevBuf<double> dXD((size_t)np * np);
+      HIP_CHECK(hipMemcpyAsync(dXD.get(), XD.data(), sizeof(double) * XD.size(), hipMemcpyHostToDevice, s_));
+      gemm_f64(s_, np, np, np, 1., dXD.get(), np, 1, dX.get(), np, 0, 1., C, np);
+      HIP_CHECK(hipMemcpyAsync(pcov, C, sizeof(double) * (size_t)np * np, hipMemcpyDeviceToHost, s_));
+      HIP_CHECK(hipStreamSynchronize(s_));
+    } else {
+      HIP_CHECK(hipMemcpyAsync(pcov, C, sizeof(double) * (size_t)np * np, hipMemcpyDeviceToHost, s_));
+      HIP_CHECK(hipStreamSynchronize(s_));
+      for (int p = 0; p < np; ++p) pcov[(size_t)p * np + p] += hD[p];
+    }
+  }
 }
 
 }  // namespace gpb_amd

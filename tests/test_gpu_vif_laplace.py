@@ -5,7 +5,7 @@ likelihoods.h:2316-2742, CalcGradNegMargLikelihoodLaplaceApproxFSVA :3886-4925) 
 
 Fixtures: tests/golden/golden_vif_laplace.json (the reference itself, make_golden_vif_laplace.py): nll + gradient for
 bernoulli_logit / bernoulli_probit / poisson / gamma (with the shape gradient) over four covariance functions, m = 20-200
-inducing points, 8-30 neighbours, n = 1000-20000; L-BFGS fits; the gradient wrt F (with fixed effects the reference's
+inducing points, 8-30 neighbours, n = 1000-20000; L-BFGS fits; latent / response predictions; the gradient wrt F (with fixed effects the reference's
 covariance gradient evaluates its location-dependent terms at mode + F in data order, re_model_template.h:1859,
 reproduced by VifLaplace::SetGradOffset). Both sides are exact algebra: nll
 within 1e-9 relative (2e-9 for the smooth-kernel cases, whose residual factor the reference forms by cancellation,
@@ -154,3 +154,26 @@ def test_vif_laplace_default_method_is_cholesky_and_deterministic():
     assert ra[0] == rb[0] == rc[0]
     np.testing.assert_array_equal(ra[1], rb[1])
     np.testing.assert_array_equal(rb[1], rc[1])
+
+
+@pytest.mark.parametrize("name", _of("pred"))
+def test_vif_laplace_predict_matches_reference(name):
+    """PredictLaplaceApproxFSVA, Cholesky branch (likelihoods.h:6060-6130, 6478-6548): latent means, variances,
+    covariance matrices (cond_obs_only / cond_all) and response probabilities at 1e-8."""
+    from gpboost_amd import synthetic
+    case = GOLDEN[name]
+    X, y = _data(case["data"], case["n"])
+    npred = case["npred"]
+    xp = synthetic.lcg_unif(npred * 2, 0.713).reshape(2, npred).T.copy()
+    gm = _model(X, case["spec"])
+    gm.set_prediction_data(vecchia_pred_type=case["vecchia_pred_type"])
+    want_cov = "cov" in case
+    pred = gm.predict(y=y, gp_coords_pred=xp, cov_pars=case["cov_pars"], predict_var=not want_cov,
+                      predict_cov_mat=want_cov, predict_response=case["response"])
+    mu = np.asarray(case["mean"])
+    np.testing.assert_allclose(pred["mu"], mu, rtol=1e-8, atol=1e-8 * np.abs(mu).max())
+    if want_cov:
+        c = np.asarray(case["cov"]).reshape(npred, npred)
+        np.testing.assert_allclose(pred["cov"], c, rtol=1e-8, atol=1e-8 * np.abs(c).max())
+    else:
+        np.testing.assert_allclose(pred["var"], case["var"], rtol=1e-8, atol=1e-11)
