@@ -781,6 +781,98 @@ def vif_leg(steps: int, cpu: bool) -> dict:
     return leg
 
 
+VIFL_CPU_N = 6_000                # bounded size of the reference's VIF Laplace baseline (~n^2 cost: 240 s at 20k)
+
+
+def vif_laplace_cpu_baseline(n: int) -> dict | None:
+    """The reference's VIF Laplace evaluation (FSVA, matrix_inversion_method = "cholesky", bernoulli_logit;
+    likelihoods.h:2316-2742, 3886-4925) on this host at a bounded n: one nll + gradient evaluation
+    (oracle/_ref/ref_harness)."""
+    harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
+    if not os.path.exists(harness):
+        return None
+    import numpy as np
+
+    from gpboost_amd import synthetic
+    X = synthetic.bench_coords(n)
+    y = synthetic.bench_bernoulli_y(X)
+    threads = max(1, min(int(os.environ.get("OMP_NUM_THREADS", str(os.cpu_count() or 1))), 16))
+    with tempfile.NamedTemporaryFile(suffix=".bin", delete=False) as f:
+        f.write(np.array([X.shape[0], X.shape[1]], dtype=np.int32).tobytes())
+        f.write(np.ascontiguousarray(X.T).tobytes())
+        f.write(np.ascontiguousarray(y, dtype=np.float64).tobytes())
+        path = f.name
+    try:
+        out = subprocess.run([harness, path, "cov_fct=exponential", "gp_approx=full_scale_vecchia",
+                              "likelihood=bernoulli_logit", "matrix_inversion_method=cholesky",
+                              f"num_ind_points={VIF_M}", f"num_neighbors={VIF_NN}", "ordering=random",
+                              "cov_pars=" + ",".join(map(str, LATENT_PARS)), "reps=1", "mode=eval"],
+                             capture_output=True, text=True, timeout=600,
+                             env=dict(os.environ, OMP_NUM_THREADS=str(threads)), check=True)
+        r = json.loads(out.stdout)
+        t = r["median_time"]
+        return {"value": 1.0 / t, "unit": "evals/s", "cores": threads, "kind": "reference",
+                "sample": f"1 bernoulli_logit VIF Laplace eval (cholesky) at n={n}, m={VIF_M}, nn={VIF_NN} (nll+grad, "
+                          f"{t:.2f} s/eval; construction excluded)", "n": n, "nll": r["nll"], "grad": r["grad"]}
+    except Exception as e:  # noqa: BLE001
+        sys.stderr.write(f"reference VIF Laplace CPU baseline failed: {e}\n")
+        return None
+    finally:
+        os.unlink(path)
+
+
+def vif_laplace_leg(steps: int, cpu: bool) -> dict:
+    """SURVEY §8 row f4, non-Gaussian: full-scale Vecchia with the Laplace approximation (the reference's FSVA,
+    matrix_inversion_method = "cholesky"): bernoulli_logit on the headline's n = 100k coordinates with the
+    reference's VIF defaults (200 kmeans++ inducing points, 30 neighbours): Newton mode finding on the GPU sparse
+    Cholesky of B^T D^-1 B + W with the m x m Woodbury correction, exact log-determinant, selected-inverse gradient."""
+    import numpy as np
+
+    from gpboost_amd import GPModel, synthetic
+
+    def model(Xs):
+        return GPModel(gp_coords=Xs, likelihood="bernoulli_logit", cov_function="exponential",
+                       gp_approx="full_scale_vecchia", num_ind_points=VIF_M, num_neighbors=VIF_NN, seed=0,
+                       matrix_inversion_method="cholesky")
+
+    X = synthetic.bench_coords(VIF_N)
+    y = synthetic.bench_bernoulli_y(X)
+    t0 = time.perf_counter()
+    gm = model(X)
+    nll, g, _ = gm.neg_log_likelihood_and_grad(LATENT_PARS, y)   # construction + first eval (warm-up)
+    t_first = time.perf_counter() - t0
+    ts = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        nll, g, _ = gm.neg_log_likelihood_and_grad(LATENT_PARS, None)
+        ts.append(time.perf_counter() - t0)
+    info = gm.last_iteration_info()
+    plan = gm.cholesky_plan_info()
+    t_med = float(np.median(ts))
+    leg = {"metric": "bernoulli_logit VIF Laplace (full-scale Vecchia, cholesky) neg-log-lik + grad evals/sec, "
+                     "n=100k m=200 nn=30",
+           "value": 1.0 / t_med, "unit": "evals/s", "steps": steps, "ms_per_step": t_med * 1e3,
+           "config": {"workload": "vif_bernoulli_logit_laplace_cholesky", "n": VIF_N, "num_ind_points": VIF_M,
+                      "num_neighbors": VIF_NN, "cov_pars": LATENT_PARS, "nll": nll, "grad": [float(v) for v in g],
+                      "newton_its": int(info[0])},
+           "plan": plan, "construction_and_first_eval_s": t_first}
+    del gm
+    if cpu:
+        base = vif_laplace_cpu_baseline(VIFL_CPU_N)
+        if base is not None:   # the GPU at the reference's sample size
+            Xs = synthetic.bench_coords(VIFL_CPU_N)
+            gs = model(Xs)
+            ys = synthetic.bench_bernoulli_y(Xs)
+            a = gs.neg_log_likelihood_and_grad(LATENT_PARS, ys)
+            t0 = time.perf_counter()
+            for _ in range(3):
+                a = gs.neg_log_likelihood_and_grad(LATENT_PARS, None)
+            base["gpu_at_sample_ms"] = (time.perf_counter() - t0) / 3 * 1e3
+            base["gpu_nll_at_sample"] = a[0]
+        leg["cpu_baseline"] = base
+    return leg
+
+
 def vif_cpu_baseline() -> dict | None:
     """The reference's VIF path (oracle/_ref/ref_harness gp_approx=full_scale_vecchia) on this host at
     n=20000 (m=200, nn=30); `value_scaled_n100k` scales it by 20000/100000 (the unit is linear in n)."""
@@ -1151,6 +1243,7 @@ def main():
         line["fitc"] = fitc_leg(5, not args.no_cpu_baseline)
         line["fitc_laplace"] = fitc_laplace_leg(3, not args.no_cpu_baseline)
         line["vif"] = vif_leg(5, not args.no_cpu_baseline)
+        line["vif_laplace"] = vif_laplace_leg(3, not args.no_cpu_baseline)
     if world == 1 and not args.no_latent:
         del gm
         if os.environ.get("GPBOOST_AMD_DUMP_MAPS"):   # symbolising a crash under a tracer: the loaded libraries

@@ -1585,11 +1585,12 @@ void combine_partials(const double* s, int n, double sigma2_in, int profile, dou
 }
 
 void REModelAMD::CholeskyPlanInfo(double* out) {
-  if (!(cfg_.latent && vecchia_) || cfg_.matrix_inversion_method != "cholesky")
-    Fatal("GPB_GetCholeskyPlanInfo needs a latent Vecchia model with matrix_inversion_method = 'cholesky'");
+  if (!vif_lap_ && (!(cfg_.latent && vecchia_) || cfg_.matrix_inversion_method != "cholesky"))
+    Fatal("GPB_GetCholeskyPlanInfo needs a latent Vecchia or full-scale Vecchia model with matrix_inversion_method = "
+          "'cholesky'");
   UseDevice();
   EnsureStructure();
-  const CholPlan* p = latent_->CholPlanInfo();
+  const CholPlan* p = vif_lap_ ? &vif_lap_->plan() : latent_->CholPlanInfo();
   out[0] = p->nsup;
   out[1] = (double)p->lvl_ptr.size() - 1;
   out[2] = (double)p->nnz_l;
@@ -1598,7 +1599,7 @@ void REModelAMD::CholeskyPlanInfo(double* out) {
   out[5] = p->max_fs;
   out[6] = p->max_ns;
   out[7] = p->ms_analyze;
-  out[8] = latent_->CholLastFactorMs();
+  out[8] = vif_lap_ ? vif_lap_->last_factor_ms() : latent_->CholLastFactorMs();
 }
 
 }  // namespace gpb_amd

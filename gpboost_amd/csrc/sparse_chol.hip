@@ -370,6 +370,8 @@ struct SolveArgs {
   int t;
 };
 
+constexpr int kSolveColGroup = 4;   // right-hand sides per block of the solve's assembly / gather / scatter passes
+
 __global__ void __launch_bounds__(256) chol_asmv_kernel(const CholColTask* __restrict__ tasks, int64_t t0, DevPlan P,
                                                         SolveArgs a) {
   const CholColTask tk = tasks[t0 + blockIdx.x];
@@ -377,7 +379,9 @@ __global__ void __launch_bounds__(256) chol_asmv_kernel(const CholColTask* __res
   const int sf = P.sfirst[s], ns = P.sfirst[s + 1] - sf;
   const int fs = ns + (int)(P.rptr[s + 1] - P.rptr[s]);
   double* V = a.V + a.vofs[s];
-  for (int k = 0; k < a.t; ++k)
+  // columns [k0, k1) of this block (blockIdx.y: column group of kSolveColGroup right-hand sides)
+  const int k0 = blockIdx.y * kSolveColGroup, k1 = min(a.t, k0 + kSolveColGroup);
+  for (int k = k0; k < k1; ++k)
     for (int r = threadIdx.x; r < fs; r += 256)
       V[r + (size_t)k * fs] = r < ns ? a.b[P.perm[sf + r] + (size_t)k * P.n] : 0.;
   for (int q = P.cptr[s]; q < P.cptr[s + 1]; ++q) {
@@ -388,7 +392,7 @@ __global__ void __launch_bounds__(256) chol_asmv_kernel(const CholColTask* __res
     const int fc = nsc + nrc;
     const int* rel = P.rel + P.rptr[ch];
     const double* Vc = a.V + a.vofs[ch];
-    for (int k = 0; k < a.t; ++k)
+    for (int k = k0; k < k1; ++k)
       for (int i = threadIdx.x; i < nrc; i += 256) V[rel[i] + (size_t)k * fs] += Vc[nsc + i + (size_t)k * fc];
   }
 }
@@ -402,7 +406,8 @@ __global__ void __launch_bounds__(256) chol_gather_x_kernel(const CholColTask* _
   const int fs = ns + nr;
   const int* R = P.rows + P.rptr[s];
   double* V = a.V + a.vofs[s];
-  for (int k = 0; k < a.t; ++k)
+  const int k0 = blockIdx.y * kSolveColGroup, k1 = min(a.t, k0 + kSolveColGroup);
+  for (int k = k0; k < k1; ++k)
     for (int i = tk.c0 + threadIdx.x; i < tk.c1; i += 256) V[ns + i + (size_t)k * fs] = a.X[P.perm[R[i]] + (size_t)k * P.n];
 }
 
@@ -413,7 +418,8 @@ __global__ void __launch_bounds__(256) chol_scatter_x_kernel(const CholColTask* 
   const int sf = P.sfirst[s], ns = P.sfirst[s + 1] - sf;
   const int fs = ns + (int)(P.rptr[s + 1] - P.rptr[s]);
   const double* V = a.V + a.vofs[s];
-  for (int k = 0; k < a.t; ++k)
+  const int k0 = blockIdx.y * kSolveColGroup, k1 = min(a.t, k0 + kSolveColGroup);
+  for (int k = k0; k < k1; ++k)
     for (int i = tk.c0 + threadIdx.x; i < tk.c1; i += 256) a.X[P.perm[sf + i] + (size_t)k * P.n] = V[i + (size_t)k * fs];
 }
 
@@ -735,17 +741,18 @@ void SparseChol::Run(const SparseCholDev& sch, double* ybuf, const void* solve_a
         hipLaunchKernelGGL(chol_mirror_kernel, grid, dim3(256), 0, s_, sch.col.get(), op.task0, dp, d_S_.get());
         break;
       case kOpAsmV:
-        hipLaunchKernelGGL(chol_asmv_kernel, grid, dim3(256), 0, s_, sch.col.get(), op.task0, dp,
-                           *static_cast<const SolveArgs*>(solve_args));
-        break;
       case kOpGatherX:
-        hipLaunchKernelGGL(chol_gather_x_kernel, grid, dim3(256), 0, s_, sch.col.get(), op.task0, dp,
-                           *static_cast<const SolveArgs*>(solve_args));
+      case kOpScatterX: {   // one block per (supernode, group of kSolveColGroup right-hand sides)
+        const SolveArgs& sa = *static_cast<const SolveArgs*>(solve_args);
+        const dim3 g2(op.ntask, (sa.t + kSolveColGroup - 1) / kSolveColGroup);
+        if (op.type == kOpAsmV)
+          hipLaunchKernelGGL(chol_asmv_kernel, g2, dim3(256), 0, s_, sch.col.get(), op.task0, dp, sa);
+        else if (op.type == kOpGatherX)
+          hipLaunchKernelGGL(chol_gather_x_kernel, g2, dim3(256), 0, s_, sch.col.get(), op.task0, dp, sa);
+        else
+          hipLaunchKernelGGL(chol_scatter_x_kernel, g2, dim3(256), 0, s_, sch.col.get(), op.task0, dp, sa);
         break;
-      case kOpScatterX:
-        hipLaunchKernelGGL(chol_scatter_x_kernel, grid, dim3(256), 0, s_, sch.col.get(), op.task0, dp,
-                           *static_cast<const SolveArgs*>(solve_args));
-        break;
+      }
       case kOpFSolve1:
       case kOpBSolve1: {
         const SolveArgs& sa = *static_cast<const SolveArgs*>(solve_args);
