@@ -915,6 +915,7 @@ LatentResult LatentVecchia::Eval(int cov_type, int lik, const double* trafo, dou
     for (int ih = 0; ih < max_shrink; ++ih) {
       if (ih == 0) launch_copy(n, d_mode_upd_.get(), d_mode_new_.get(), s_);
       else launch_axpby(n, 1. - lr, d_mode_.get(), lr, d_mode_upd_.get(), d_mode_new_.get(), s_);
+      if (lik == kLikPoisson || lik == kLikGamma) launch_cap_mode_change(n, d_mode_.get(), d_mode_new_.get(), s_);
       sa.mode = d_mode_new_.get();
       Scalars(sa, sc);
       mll_new = sc[kSqLogLik] - 0.5 * sc[kSqQuad];

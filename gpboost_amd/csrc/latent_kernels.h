@@ -310,6 +310,9 @@ void launch_copy(size_t count, const double* X, double* Y, hipStream_t s);
 // Z = alpha X + beta Y (elementwise, count entries; Z may alias X or Y)
 void launch_axpby(size_t count, double alpha, const double* X, double beta, const double* Y, double* Z,
                   hipStream_t s);
+// the Newton trial mode's change capped at log(100) per entry (CapChangeModeUpdateNewton, likelihoods.h:11800-11810;
+// cap_change_mode_newton_ for poisson / gamma, :481-490)
+void launch_cap_mode_change(size_t count, const double* mode, double* mnew, hipStream_t s);
 
 // ---- likelihood-specific elementwise and reductions
 enum LatentLik : int { kLikGaussian = 0, kLikBernoulliLogit = 1, kLikBernoulliProbit = 2, kLikPoisson = 3, kLikGamma = 4 };

@@ -1614,6 +1614,23 @@ void launch_copy(size_t count, const double* X, double* Y, hipStream_t s) {
   HIP_CHECK(hipGetLastError());
 }
 
+// CapChangeModeUpdateNewton (likelihoods.h:11800-11810): |mnew - mode| capped at MAX_CHANGE_MODE_NEWTON_ = log(100)
+__global__ void cap_mode_kernel(size_t total, const double* __restrict__ mode, double* __restrict__ mnew) {
+  constexpr double kMaxChange = 4.605170185988091;
+  for (size_t o = (size_t)blockIdx.x * kBT + threadIdx.x; o < total; o += (size_t)gridDim.x * kBT) {
+    const double c = fabs(mnew[o] - mode[o]);
+    if (c > kMaxChange) mnew[o] = mode[o] + (mnew[o] - mode[o]) / c * kMaxChange;
+  }
+}
+
+void launch_cap_mode_change(size_t count, const double* mode, double* mnew, hipStream_t s) {
+  int g = (int)((count + kBT - 1) / kBT);
+  if (g > kMaxGridX) g = kMaxGridX;
+  if (g < 1) g = 1;
+  hipLaunchKernelGGL(cap_mode_kernel, dim3(g), dim3(kBT), 0, s, count, mode, mnew);
+  HIP_CHECK(hipGetLastError());
+}
+
 void launch_axpby(size_t count, double alpha, const double* X, double beta, const double* Y, double* Z,
                   hipStream_t s) {
   int g = (int)((count + kBT - 1) / kBT);

@@ -5,7 +5,8 @@ matrix_inversion_method = "cholesky", the checker of gpboost_amd's sparse-Choles
 csrc/sparse_chol.{h,hip}). Importable only from tests/. Follows
   FindModePostRandEffCalcMLLVecchia, Cholesky branch   likelihoods.h:2780-3070
       (mode from 0; per Newton step SigmaI_plus_W = B^T D^-1 B + diag(W), mode_update = (SigmaI + W)^-1 (W mode + d1),
-      Armijo with grad_dot_direction = dir^T (SigmaI + W) dir, c = 1e-4, up to 20 halvings (:2957-2995),
+      Armijo with grad_dot_direction = dir^T (SigmaI + W) dir, c = 1e-4, up to 20 halvings (:2957-2995), the
+      trial mode's change capped at log(100) for poisson / gamma (CapChangeModeUpdateNewton :11800-11810),
       CheckConvergenceModeFinding :11820-11870; approx_marginal_ll = log p(y | mode + F) - 1/2 (Bm)^T D^-1 (Bm)
       - sum log L_ii + 1/2 sum log D^-1_ii (:3067-3070))
   CalcGradNegMargLikelihoodLaplaceApproxVecchia, Cholesky branch   likelihoods.h:5207-5336
@@ -77,6 +78,10 @@ class LatentCholOracle:
             lam = 1.
             for ih in range(1 if gauss else 20):
                 new = upd if ih == 0 else (1 - lam) * mode + lam * upd
+                if self.lik in ("poisson", "gamma"):   # CapChangeModeUpdateNewton (:11800-11810, log(100))
+                    c = np.abs(new - mode)
+                    big = c > np.log(100.)
+                    new = np.where(big, mode + (new - mode) / np.where(big, c, 1.) * np.log(100.), new)
                 obj_new = self._obj(new)
                 if obj_new < obj + 1e-4 * lam * gdd or not np.isfinite(obj_new):
                     lam *= 0.5
