@@ -56,7 +56,7 @@ def pmc_traffic(scale: float) -> dict | None:
     same command (profiles/<round>/pmc_rows.json: FETCH_SIZE + WRITE_SIZE, KB per dispatch;
     PMC counters cannot be read from inside the process)."""
     path = None
-    for rnd in ("r05", "r04", "r03", "r02", "r01"):   # the latest round's passes
+    for rnd in ("r06", "r05", "r04", "r03", "r02", "r01"):   # the latest round's passes
         cand = os.path.join(ROOT, "profiles", rnd, "pmc_rows.json")
         if os.path.exists(cand):
             path = cand
@@ -111,7 +111,7 @@ def cpu_baseline(X, Y, reps: int = 3) -> dict:
 
 def pmc_ops() -> dict | None:
     """The latest round's PMC summary of the operator / preconditioner kernels (scripts/pmc_ops_json.py)."""
-    for rnd in ("r05", "r04", "r03"):
+    for rnd in ("r06", "r05", "r04", "r03"):
         path = os.path.join(ROOT, "profiles", rnd, "pmc_ops.json")
         if os.path.exists(path):
             with open(path) as f:
@@ -970,31 +970,54 @@ def join_ranks(gm, rank: int, world: int, dist) -> None:
     gm.set_distributed(rank, world, obj[0])
 
 
-def row_shard_leg(gm, reps: int = 15) -> dict:
+def row_shard_leg(X, Y, reps: int = 200) -> dict:
     """Single-GPU rehearsal of the N-rank row sharding of the headline evaluation: the first and the
     last rank's row range at N = 2, 4, 8 (the shard GPB_EvalVecchiaPartials evaluates, the same launch
-    path a rank takes) with its row-kernel HIP-event time and the host wall time of the partial
-    evaluation. The N-rank evaluation costs about max(wall over ranks) + one 6-double all-reduce."""
+    path a rank takes) with the host wall time of the partial evaluation (a fresh model: no kernel HIP
+    events are recorded in these evaluations, as in the timed headline loop) and, in a second pass, the
+    row-kernel HIP-event time. The N-rank evaluation costs about max(wall over ranks) + one 6-double
+    all-reduce."""
     import numpy as np
+
+    from gpboost_amd import GPModel
+    gm = GPModel(gp_coords=X, cov_function="exponential", gp_approx="vecchia", num_neighbors=M_NEIGHBORS,
+                 vecchia_ordering="random", seed=0)
+    gm.neg_log_likelihood_and_grad(THETA, Y, profile_sigma2=True)
+    t_end = time.perf_counter() + 0.3
+    while time.perf_counter() < t_end:   # clock ramp
+        gm.vecchia_partials(THETA, 0, N_DATA)
     n = N_DATA
     out = {}
+    shards = {}
     for nr in (2, 4, 8):
         base, rem = divmod(n, nr)   # the library's split (re_model.cpp SetDistributed)
-        ranges = {"first": (0, base + (1 if rem else 0)), "last": (n - base, n)}
+        shards[nr] = {"first": (0, base + (1 if rem else 0)), "last": (n - base, n)}
+    for nr, ranges in shards.items():
         res = {}
         for name, (r0, r1) in ranges.items():
-            gm.vecchia_partials(THETA, r0, r1)
-            ks, ws = [], []
+            for _ in range(20):
+                gm.vecchia_partials(THETA, r0, r1)
+            ws = []
             for _ in range(reps):
                 t0 = time.perf_counter()
                 gm.vecchia_partials(THETA, r0, r1)
                 ws.append(time.perf_counter() - t0)
-                ks.append(gm.last_kernel_ms()[0])
-            res[name] = {"rows": [r0, r1], "kernel_ms": float(np.median(ks)), "wall_ms": float(np.median(ws)) * 1e3}
-        res["projected_evals_per_s"] = 1e3 / max(v["wall_ms"] for v in res.values())
+            res[name] = {"rows": [r0, r1], "wall_ms": float(np.median(ws)) * 1e3}
         out[f"n{nr}"] = res
-    out["note"] = ("row ranges of an N-rank run evaluated on one GPU; projection excludes the all-reduce "
-                   "of 6 doubles over RCCL")
+    gm.last_kernel_ms()   # from here on the evaluations record their kernel events
+    for nr, ranges in shards.items():
+        res = out[f"n{nr}"]
+        for name, (r0, r1) in ranges.items():
+            ks = []
+            for _ in range(20):
+                gm.vecchia_partials(THETA, r0, r1)
+                ks.append(gm.last_kernel_ms()[0])
+            res[name]["kernel_ms"] = float(np.median(ks))
+        res["projected_evals_per_s"] = 1e3 / max(v["wall_ms"] for v in res.values() if isinstance(v, dict))
+    out["note"] = ("row ranges of an N-rank run evaluated on one GPU (wall: host time of the partial evaluation "
+                   "without kernel events; kernel: row-kernel HIP-event time, separate pass); projection excludes "
+                   "the all-reduce of 6 doubles over RCCL")
+    del gm
     return out
 
 
@@ -1232,7 +1255,7 @@ def main():
                               "note": "end to end: neighbour search among the 100k observed points (GPU), "
                                       "prediction rows (row kernel, 64-lane groups), mean/variance"}
     if world == 1 and not args.no_row_shards:
-        line["row_shards"] = row_shard_leg(gm)
+        line["row_shards"] = row_shard_leg(X, Y)
     if world == 1 and not args.no_fit:
         line["fit"] = fit_leg(X, Y, not args.no_cpu_baseline)
     if world == 1 and not args.no_dense:

@@ -43,9 +43,12 @@ def _compile(src: str) -> str:
     path = os.path.join(CSRC, src)
     deps = [path] + [os.path.join(CSRC, h) for h in os.listdir(CSRC) if h.endswith(".h")]
     deps.append(os.path.join(ROOT, "include", "gpboost_amd.h"))
+    deps.append(os.path.abspath(__file__))
     if os.path.exists(obj) and os.path.getmtime(obj) >= max(os.path.getmtime(p) for p in deps):
         return obj
-    lang = ["-x", "hip"] if src.endswith(".hip") else []
+    # MFMA accumulators in VGPRs (gfx950's unified register file): without this the compiler keeps loop-carried
+    # accumulators in VGPRs and copies them to and from AGPRs around every MFMA loop iteration
+    lang = ["-x", "hip", "-mllvm", "-amdgpu-mfma-vgpr-form"] if src.endswith(".hip") else []
     cmd = [os.path.join(ROCM, "bin", "hipcc")] + CXXFLAGS + DEFS + lang + ["-c", path, "-o", obj]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:

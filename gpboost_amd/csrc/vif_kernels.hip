@@ -333,111 +333,183 @@ __global__ void __launch_bounds__(kT) vif_rows_kernel(VifRowsArgs a) {
 }
 
 typedef double vif_double4 __attribute__((ext_vector_type(4)));
+typedef double vif_double2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
+// (row, column) of entry e of a lower triangle stored row by row (e < 528)
+__device__ __forceinline__ void tri_rc(int e, int& p, int& b) {
+  p = (int)((sqrtf(8.f * (float)e + 1.f) - 1.f) * 0.5f);
+  if ((p + 1) * (p + 2) / 2 <= e) ++p;
+  if (p * (p + 1) / 2 > e) --p;
+  b = e - p * (p + 1) / 2;
+}
 
 // The same row factor for neighbour sets of at most 32 points (nn <= 31, the reference's default 30) with
-// the Gram blocks on the fp64 MFMA: one wave per row, V_S^T [V P_0 P_1]_S as 16x16x4 tiles whose A / B
-// operands are loaded straight from the m x n matrices (lane l: point S[l & 15] (+ 16), q = q0 + l / 4 ..
-// i.e. the 4 consecutive entries of 16 contiguous columns per load), 12 MFMAs per 4 entries of m. The
-// accumulators go to LDS once; the residual matrix C overwrites the V^T V block in place and dC_k is
-// never stored (r_k = dc_k - dC_k A is formed from the P blocks and the recomputed base covariances).
+// the Gram blocks on the fp64 MFMA: one wave per row, V_S^T [V P_0 P_1]_S as 16x16x4 tiles. The m-range is
+// walked in chunks of 8: lane (kq, m0) loads entries 2 kq, 2 kq + 1 of the chunk of columns S[m0] and
+// S[16 + m0] as one 16-byte load per matrix (the k-slot kq of MFMA step e takes entry 2 kq + e; any
+// assignment of the m entries to k-slots gives the same Gram), the next chunk's loads are issued before the
+// current chunk's MFMAs, no branches in the loop (the tail chunk reads the zero-masked padding of the ld-m
+// column). V^T V is symmetric: its (1, 0) block is stored from the transposed (0, 1) accumulator (11 MFMAs
+// per k-step with the derivative blocks). LDS: the V^T V block becomes the residual matrix C in place (lower
+// triangle); one scratch matrix takes G_1 = V^T P_0, then G_2 = V^T P_1 for the transposed sums, and finally
+// dC_0 (lower triangle) and dC_1 (upper triangle, diagonal in column 32): two 32 x 33 matrices per wave.
 template <int COV, bool GRAD>
 __global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
-  constexpr int LD = 33;   // gram row stride
-  __shared__ double gram[GRAD ? 3 : 1][32 * LD];
+  constexpr int LD = 33;   // row stride of the 32 x 32 blocks
+  constexpr int G = GRAD ? 3 : 1;
+  __shared__ double C[32 * LD];
+  __shared__ double X[GRAD ? 32 * LD : 1];
   __shared__ int idx[32];
   __shared__ double vecs[4][32];   // c, dc0, dc1, A
   __shared__ double rdg[32];       // 1 / L_jj
-  const int i = a.i0 + blockIdx.x, lane = threadIdx.x, ir = blockIdx.x;
+  const int ir = blockIdx.x, lane = threadIdx.x;
+  const int i = a.i0 + ir;
   const int nn = a.nn, k = min(i, nn);
   if (lane < 32) idx[lane] = lane < k ? a.nbr[(size_t)ir * nn + lane] : i;
   wave_sync();
   const int m0 = lane & 15, kq = lane >> 4;
-  const size_t c0 = (size_t)idx[m0] * a.ldm, c1 = (size_t)idx[16 + m0] * a.ldm;
-  vif_double4 acc[GRAD ? 3 : 1][2][2];
+  const size_t o0 = (size_t)idx[m0] * a.ldm + 2 * kq, o1 = (size_t)idx[16 + m0] * a.ldm + 2 * kq;
+  vif_double4 acc[G][2][2];
 #pragma unroll
-  for (int g = 0; g < (GRAD ? 3 : 1); ++g)
+  for (int g = 0; g < G; ++g)
 #pragma unroll
     for (int x = 0; x < 2; ++x)
 #pragma unroll
       for (int y = 0; y < 2; ++y) acc[g][x][y] = vif_double4{0., 0., 0., 0.};
-  const double* V = a.V;
-  const double* P0 = a.P0;
-  const double* P1 = a.P1;
-#pragma unroll 8
-  for (int q0 = 0; q0 < a.mi; q0 += 4) {
-    const int q = q0 + kq;
-    const bool ok = q < a.mi;
-    const double v0 = ok ? V[c0 + q] : 0., v1 = ok ? V[c1 + q] : 0.;
-    acc[0][0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, v0, acc[0][0][0], 0, 0, 0);
-    acc[0][0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, v1, acc[0][0][1], 0, 0, 0);
-    acc[0][1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1, v0, acc[0][1][0], 0, 0, 0);
-    acc[0][1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1, v1, acc[0][1][1], 0, 0, 0);
-    if (GRAD) {
-      const double p00 = ok ? P0[c0 + q] : 0., p01 = ok ? P0[c1 + q] : 0.;
-      const double p10 = ok ? P1[c0 + q] : 0., p11 = ok ? P1[c1 + q] : 0.;
-      acc[GRAD ? 1 : 0][0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, p00, acc[GRAD ? 1 : 0][0][0], 0, 0, 0);
-      acc[GRAD ? 1 : 0][0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, p01, acc[GRAD ? 1 : 0][0][1], 0, 0, 0);
-      acc[GRAD ? 1 : 0][1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1, p00, acc[GRAD ? 1 : 0][1][0], 0, 0, 0);
-      acc[GRAD ? 1 : 0][1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1, p01, acc[GRAD ? 1 : 0][1][1], 0, 0, 0);
-      acc[GRAD ? 2 : 0][0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, p10, acc[GRAD ? 2 : 0][0][0], 0, 0, 0);
-      acc[GRAD ? 2 : 0][0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, p11, acc[GRAD ? 2 : 0][0][1], 0, 0, 0);
-      acc[GRAD ? 2 : 0][1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1, p10, acc[GRAD ? 2 : 0][1][0], 0, 0, 0);
-      acc[GRAD ? 2 : 0][1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1, p11, acc[GRAD ? 2 : 0][1][1], 0, 0, 0);
+  typedef vif_double2 Buf[G][2];
+  auto load = [&](Buf& buf, int ch) {
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      const double* M = g == 0 ? a.V : (g == 1 ? a.P0 : a.P1);
+      buf[g][0] = *reinterpret_cast<const vif_double2*>(M + o0 + 8 * ch);
+      buf[g][1] = *reinterpret_cast<const vif_double2*>(M + o1 + 8 * ch);
     }
+  };
+  auto step = [&](Buf& buf) {
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const double v0 = buf[0][0][e], v1 = buf[0][1][e];
+      acc[0][0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, v0, acc[0][0][0], 0, 0, 0);
+      acc[0][0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, v1, acc[0][0][1], 0, 0, 0);
+      acc[0][1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1, v1, acc[0][1][1], 0, 0, 0);
+#pragma unroll
+      for (int g = 1; g < G; ++g) {
+        const double p0 = buf[g][0][e], p1 = buf[g][1][e];
+        acc[g][0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, p0, acc[g][0][0], 0, 0, 0);
+        acc[g][0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v0, p1, acc[g][0][1], 0, 0, 0);
+        acc[g][1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1, p0, acc[g][1][0], 0, 0, 0);
+        acc[g][1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(v1, p1, acc[g][1][1], 0, 0, 0);
+      }
+    }
+  };
+  auto mask = [&](Buf& buf, int ch) {   // entries beyond m: the column's padding (ld m is a multiple of 64), zeroed
+    const int q = 8 * ch + 2 * kq;
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int x = 0; x < 2; ++x)
+#pragma unroll
+        for (int e = 0; e < 2; ++e)
+          if (q + e >= a.mi) buf[g][x][e] = 0.;
+  };
+  // ping-pong over two register buffers (no copies): chunk ch + 1 is in flight while chunk ch is multiplied
+  const int nch = (a.mi + 7) >> 3, nfull = a.mi >> 3;
+  Buf cur, nxt;
+  load(cur, 0);
+  int ch = 0;
+  for (; ch + 1 < nfull; ch += 2) {
+    load(nxt, ch + 1);
+    step(cur);
+    load(cur, min(ch + 2, nch - 1));
+    step(nxt);
+  }
+  if (ch < nfull) {   // odd number of full chunks: cur holds the last one
+    if (ch + 1 < nch) load(nxt, ch + 1);
+    step(cur);
+    if (ch + 1 < nch) {
+      mask(nxt, ch + 1);
+      step(nxt);
+    }
+  } else if (ch < nch) {   // cur holds the tail chunk
+    mask(cur, ch);
+    step(cur);
   }
   // C/D layout: row = (lane >> 4) + 4 r, col = lane & 15 within each 16 x 16 tile
+  auto store = [&](double* W, const vif_double4 (&t)[2][2], bool sym) {
 #pragma unroll
-  for (int g = 0; g < (GRAD ? 3 : 1); ++g)
-#pragma unroll
-    for (int x = 0; x < 2; ++x)
-#pragma unroll
-      for (int y = 0; y < 2; ++y)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) gram[g][(16 * x + kq + 4 * r) * LD + 16 * y + m0] = acc[g][x][y][r];
+    for (int r = 0; r < 4; ++r) {
+      W[(kq + 4 * r) * LD + m0] = t[0][0][r];
+      W[(kq + 4 * r) * LD + 16 + m0] = t[0][1][r];
+      W[(16 + kq + 4 * r) * LD + 16 + m0] = t[1][1][r];
+      if (sym) W[(16 + m0) * LD + kq + 4 * r] = t[0][1][r];
+      else W[(16 + kq + 4 * r) * LD + m0] = t[1][0][r];
+    }
+  };
+  store(C, acc[0], true);
+  if (GRAD) store(X, acc[GRAD ? 1 : 0], false);
   wave_sync();
   const double var = a.var, phi = a.phi;
   // c, dc_k (column k of the blocks) and the diagonal terms, before C overwrites the V^T V block
-  double d0 = 0., dd0 = 0., dd1 = 0.;
+  double cs = 0., dcs = 0., d0 = 0., dd0 = 0., dd1 = 0.;
   if (lane < k) {
-    double c, dc;
-    cov_dcov<COV>(dist_pts(a.X, a.d, idx[lane], i), var, phi, c, dc);
-    vecs[0][lane] = c - gram[0][lane * LD + k];
-    if (GRAD) {
-      vecs[1][lane] = c - (gram[1][lane * LD + k] + gram[1][k * LD + lane]);
-      vecs[2][lane] = dc - (gram[2][lane * LD + k] + gram[2][k * LD + lane]);
-    }
+    cov_dcov<COV>(dist_pts(a.X, a.d, idx[lane], i), var, phi, cs, dcs);
+    vecs[0][lane] = cs - C[lane * LD + k];
+    if (GRAD) vecs[1][lane] = cs - (X[lane * LD + k] + X[k * LD + lane]);
   }
-  d0 = a.nugget + var - gram[0][k * LD + k];
-  if (GRAD) {
-    dd0 = var - 2. * gram[1][k * LD + k];
-    dd1 = -2. * gram[2][k * LD + k];
-  }
-  wave_sync();
-  double* C = gram[0];   // C(p, b) = C[p LD + b], in place of V^T V; dC_k in place of the P blocks
-  double dv0[16], dv1[16];
+  d0 = a.nugget + var - C[k * LD + k];
+  if (GRAD) dd0 = var - 2. * X[k * LD + k];
+  // the lower triangle of C in place; dC_0 and the base derivative covariances in registers
+  const int nl = k * (k + 1) / 2;
+  double dv0[8], dcv[8];
 #pragma unroll
-  for (int t = 0; t < 16; ++t) {
+  for (int t = 0; t < 8; ++t) {
     const int e = lane + 64 * t;
-    if (e < k * k) {
-      const int p = e / k, b = e - p * k;
+    dv0[t] = 0.;
+    dcv[t] = 0.;
+    if (e < nl) {
+      int p, b;
+      tri_rc(e, p, b);
       double c = var, dc = 0.;
       if (p != b) cov_dcov<COV>(dist_pts(a.X, a.d, idx[p], idx[b]), var, phi, c, dc);
       C[p * LD + b] = p == b ? (a.nugget + c - C[p * LD + b]) * a.cjit : c - C[p * LD + b];
       if (GRAD) {
-        dv0[t] = c - (gram[GRAD ? 1 : 0][p * LD + b] + gram[GRAD ? 1 : 0][b * LD + p]);
-        dv1[t] = dc - (gram[GRAD ? 2 : 0][p * LD + b] + gram[GRAD ? 2 : 0][b * LD + p]);
+        dv0[t] = c - (X[p * LD + b] + X[b * LD + p]);
+        dcv[t] = dc;
       }
     }
   }
   wave_sync();
   if (GRAD) {
+    store(X, acc[GRAD ? 2 : 0], false);
+    wave_sync();
+    if (lane < k) vecs[2][lane] = dcs - (X[lane * LD + k] + X[k * LD + lane]);
+    dd1 = -2. * X[k * LD + k];
+    double dv1[8];
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
+    for (int t = 0; t < 8; ++t) {
       const int e = lane + 64 * t;
-      if (e < k * k) {
-        const int p = e / k, b = e - p * k;
-        gram[GRAD ? 1 : 0][p * LD + b] = dv0[t];
-        gram[GRAD ? 2 : 0][p * LD + b] = dv1[t];
+      dv1[t] = 0.;
+      if (e < nl) {
+        int p, b;
+        tri_rc(e, p, b);
+        dv1[t] = dcv[t] - (X[p * LD + b] + X[b * LD + p]);
+      }
+    }
+    wave_sync();
+#pragma unroll
+    for (int t = 0; t < 8; ++t) {
+      const int e = lane + 64 * t;
+      if (e < nl) {
+        int p, b;
+        tri_rc(e, p, b);
+        X[p * LD + b] = dv0[t];
+        X[p == b ? p * LD + 32 : b * LD + p] = dv1[t];
       }
     }
   }
@@ -449,7 +521,7 @@ __global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
       const double rjj = rdg[j];
       const double lij = lane < k ? C[lane * LD + j] : 0.;
       for (int r = 0; r < nr; ++r) {
-        const double xj = __shfl(x[r], j, 64) * rjj;
+        const double xj = readlane_d(x[r], j) * rjj;
         if (lane == j) x[r] = xj;
         else if (lane > j) x[r] -= lij * xj;
       }
@@ -458,7 +530,7 @@ __global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
       const double rjj = rdg[j];
       const double lji = lane < j ? C[j * LD + lane] : 0.;
       for (int r = 0; r < nr; ++r) {
-        const double xj = __shfl(x[r], j, 64) * rjj;
+        const double xj = readlane_d(x[r], j) * rjj;
         if (lane == j) x[r] = xj;
         else if (lane < j) x[r] -= lji * xj;
       }
@@ -471,12 +543,15 @@ __global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
     if (lane < k) vecs[3][lane] = xa[0];
     wave_sync();
     if (lane < k) {
-      // r_k = dc_k - dC_k A with dC_0 = k(N, N) - (G_0 + G_0^T), dC_1 = dk(N, N) - (G_1 + G_1^T)
+      // r_k = dc_k - dC_k A (dC_0 from the lower triangle of X, dC_1 from the upper one, both symmetric)
       double r0 = vecs[1][lane], r1 = vecs[2][lane];
       for (int b = 0; b < k; ++b) {
         const double ab = vecs[3][b];
-        r0 -= gram[GRAD ? 1 : 0][lane * LD + b] * ab;
-        r1 -= gram[GRAD ? 2 : 0][lane * LD + b] * ab;
+        const double u = X[lane * LD + b], w = X[b * LD + lane];
+        const double e0 = b <= lane ? u : w;
+        const double e1 = b < lane ? w : (b > lane ? u : X[lane * LD + 32]);
+        r0 -= e0 * ab;
+        r1 -= e1 * ab;
       }
       xd[0] = r0;
       xd[1] = r1;
