@@ -80,7 +80,7 @@ class VifSolver {
   // (nullable): the same columns times D^-1 as a second output
   void BRow(const double* in, const double* coef, double self, bool div, double* out, double* out_div = nullptr);
   // out = B^T in (self = 1) or dB^T in (self = 0) over m-vector columns
-  void BCol(const double* in, const double* coef, double self, double* out);
+  void BCol(const double* in, const double* coefT, double self, double* out);   // coefT: values in column order
   void BVec(const double* x, const double* coef, double self, double* out);
   // out = B^T x (self = 1) or dB^T x (self = 0), coefT: the factor's values in column order (BvT_ ...)
   void BtVec(const double* x, const double* coefT, double self, double* out);
@@ -93,6 +93,7 @@ class VifSolver {
   hipStream_t s_;
   const double* d_X_;
   DevBuf<int> nbr_, tptr_, trow_, tslot_;
+  DevBuf<int> ord_;   // the points in spatial (Morton) order: processing order of the row / B-product kernels
   DevBuf<double> dK_, P0_, P1_, BK_;                 // m x n (ldm)
   DevBuf<double> Bv_, dBv0_, dBv1_;                   // n x nn
   DevBuf<double> BvT_, dBvT0_, dBvT1_;                // the same values in column (B^T) order

@@ -68,6 +68,16 @@ __device__ __forceinline__ double dist_pts(const double* X, int d, int a, int b)
   return sqrt(s);
 }
 
+// Work item of block b in a grid of 8 * chunk blocks: without an order the block index itself; with one, the
+// blocks dealt to one XCD (b, b + 8, ...: the hardware's round-robin) take one contiguous run of the spatial
+// (Morton) order, so the neighbour columns the rows gather stay in that XCD's L2. -1: padding block.
+__device__ __forceinline__ int vif_row_slot(const int* ord, int chunk, int nitems) {
+  const int b = blockIdx.x;
+  if (!ord) return b;
+  const int pos = (b & 7) * chunk + (b >> 3);
+  return pos < nitems ? ord[pos] : -1;
+}
+
 // In-place Cholesky of the k x k matrix C (row stride ld, lower) by one wave, row-oriented (left-looking):
 // step j forms L_jj from row j's dot product, then every lane t > j forms L_tj = (C_tj - L_t . L_j) / L_jj
 // from its own row; the dot products read rows written in earlier steps only, so their LDS loads pipeline.
@@ -118,6 +128,8 @@ struct VifRowsArgs {
   int i0;   // first row (prediction rows follow the n observed points); nbr / Bv / D are indexed by i - i0
   double nugget;   // 1 (Gaussian likelihood, transformed scale) or 0 (latent form of the non-Gaussian likelihoods)
   double cjit;     // multiplier of the neighbour matrix's diagonal: 1, or JITTER_MULT_VECCHIA without a nugget
+  const int* ord;   // nullable: rows in spatial order, processed XCD-chunked (vif_row_slot)
+  int chunk;        // ceil(rows / 8) with ord
   double* Bv;
   double* D;
   double* dBv0;
@@ -143,7 +155,9 @@ __global__ void __launch_bounds__(kT) vif_rows_kernel(VifRowsArgs a) {
   __shared__ double vecs[4][kMaxNn];   // c, dc0, dc1, A
   __shared__ double scal[4];
   constexpr int G = GRAD ? 3 : 1;
-  const int i = a.i0 + blockIdx.x, tid = threadIdx.x, ir = blockIdx.x;
+  const int ir = vif_row_slot(a.ord, a.chunk, a.n - a.i0), tid = threadIdx.x;
+  if (ir < 0) return;
+  const int i = a.i0 + ir;
   const int nn = a.nn, k = min(i, nn), S = k + 1;
   if (tid < k) idx[tid] = a.nbr[(size_t)ir * nn + tid];
   if (tid == k) idx[k] = i;
@@ -368,7 +382,8 @@ __global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
   __shared__ int idx[32];
   __shared__ double vecs[4][32];   // c, dc0, dc1, A
   __shared__ double rdg[32];       // 1 / L_jj
-  const int ir = blockIdx.x, lane = threadIdx.x;
+  const int ir = vif_row_slot(a.ord, a.chunk, a.n - a.i0), lane = threadIdx.x;
+  if (ir < 0) return;
   const int i = a.i0 + ir;
   const int nn = a.nn, k = min(i, nn);
   if (lane < 32) idx[lane] = lane < k ? a.nbr[(size_t)ir * nn + lane] : i;
@@ -589,37 +604,90 @@ __global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
 }
 
 // out[:, i] = (self in[:, i] + sum_r coef[i nn + r] in[:, nbr[i nn + r]]) (/ D_i); out2 (nullable) gets
-// the same column divided by D_i: one wave per column
-__global__ void __launch_bounds__(kT) vif_brow_kernel(const double* __restrict__ in, const int* __restrict__ nbr,
-                                                     const double* __restrict__ coef, const double* __restrict__ D,
-                                                     int n, int nn, int m, int ldm, double self, int div,
-                                                     double* __restrict__ out, double* __restrict__ out2) {
-  const int lane = threadIdx.x & 63;
-  const int i = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (i >= n) return;
-  const int k = min(i, nn);
-  const double inv = (div || out2) ? 1. / D[i] : 1.;
-  for (int q = lane; q < m; q += 64) {
-    double s = self != 0. ? self * in[(size_t)i * ldm + q] : 0.;
-    for (int r = 0; r < k; ++r) s = fma(coef[(size_t)i * nn + r], in[(size_t)nbr[(size_t)i * nn + r] * ldm + q], s);
-    out[(size_t)i * ldm + q] = div ? s * inv : s;
-    if (out2) out2[(size_t)i * ldm + q] = s * inv;
+// the same column divided by D_i: one wave per column (i wave-uniform: the neighbour list and the coefficients are
+// scalar loads), lane l holds entries 4 l .. 4 l + 3 of a 256-entry slice (two 16-byte loads per neighbour; ld m
+// is a multiple of 64, so the slice stays inside the column; entries >= m are not stored)
+__device__ __forceinline__ void vif_store4(double* dst, int q, int m, vif_double2 a, vif_double2 b) {
+  if (q + 3 < m) {
+    reinterpret_cast<vif_double2*>(dst + q)[0] = a;
+    reinterpret_cast<vif_double2*>(dst + q)[1] = b;
+  } else {
+    if (q < m) dst[q] = a[0];
+    if (q + 1 < m) dst[q + 1] = a[1];
+    if (q + 2 < m) dst[q + 2] = b[0];
   }
 }
 
-// out[:, j] = self in[:, j] + sum over rows i with j among their neighbours of coef(i, j) in[:, i]
-__global__ void __launch_bounds__(kT) vif_bcol_kernel(const double* __restrict__ in, const int* __restrict__ tptr,
-                                                     const int* __restrict__ trow, const int* __restrict__ tslot,
-                                                     const double* __restrict__ coef, int n, int m, int ldm, double self,
-                                                     double* __restrict__ out) {
+__global__ void __launch_bounds__(kT) vif_brow_kernel(const double* __restrict__ in, const int* __restrict__ nbr,
+                                                     const double* __restrict__ coef, const double* __restrict__ D,
+                                                     int n, int nn, int m, int ldm, double self, int div,
+                                                     double* __restrict__ out, double* __restrict__ out2,
+                                                     const int* __restrict__ ord, int chunk) {
   const int lane = threadIdx.x & 63;
-  const int j = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int b = ord ? (blockIdx.x & 7) * chunk + (blockIdx.x >> 3) : blockIdx.x;
+  int i = b * 4 + (threadIdx.x >> 6);
+  if (i >= n) return;
+  if (ord) i = ord[i];
+  i = __builtin_amdgcn_readfirstlane(i);
+  const int k = min(i, nn);
+  const int* nb = nbr + (size_t)i * nn;
+  const double* cf = coef + (size_t)i * nn;
+  const double inv = (div || out2) ? 1. / D[i] : 1.;
+  for (int q = 4 * lane; q < m; q += 256) {
+    vif_double2 s0 = {0., 0.}, s1 = {0., 0.};
+    if (self != 0.) {
+      const vif_double2* src = reinterpret_cast<const vif_double2*>(in + (size_t)i * ldm + q);
+      s0 = self * src[0];
+      s1 = self * src[1];
+    }
+#pragma unroll 8
+    for (int r = 0; r < k; ++r) {
+      const double c = cf[r];
+      const vif_double2* src = reinterpret_cast<const vif_double2*>(in + (size_t)nb[r] * ldm + q);
+      const vif_double2 x0 = src[0], x1 = src[1];
+      s0[0] = fma(c, x0[0], s0[0]);
+      s0[1] = fma(c, x0[1], s0[1]);
+      s1[0] = fma(c, x1[0], s1[0]);
+      s1[1] = fma(c, x1[1], s1[1]);
+    }
+    const vif_double2 d0 = s0 * inv, d1 = s1 * inv;
+    if (div) vif_store4(out + (size_t)i * ldm, q, m, d0, d1);
+    else vif_store4(out + (size_t)i * ldm, q, m, s0, s1);
+    if (out2) vif_store4(out2 + (size_t)i * ldm, q, m, d0, d1);
+  }
+}
+
+// out[:, j] = self in[:, j] + sum over rows i with j among their neighbours of coef(i, j) in[:, i] (coefT: the
+// factor's values in column order), the same wave / lane layout
+__global__ void __launch_bounds__(kT) vif_bcol_kernel(const double* __restrict__ in, const int* __restrict__ tptr,
+                                                     const int* __restrict__ trow, const double* __restrict__ coefT,
+                                                     int n, int m, int ldm, double self, double* __restrict__ out,
+                                                     const int* __restrict__ ord, int chunk) {
+  const int lane = threadIdx.x & 63;
+  const int b = ord ? (blockIdx.x & 7) * chunk + (blockIdx.x >> 3) : blockIdx.x;
+  int j = b * 4 + (threadIdx.x >> 6);
   if (j >= n) return;
+  if (ord) j = ord[j];
+  j = __builtin_amdgcn_readfirstlane(j);
   const int t0 = tptr[j], t1 = tptr[j + 1];
-  for (int q = lane; q < m; q += 64) {
-    double s = self != 0. ? self * in[(size_t)j * ldm + q] : 0.;
-    for (int t = t0; t < t1; ++t) s = fma(coef[tslot[t]], in[(size_t)trow[t] * ldm + q], s);
-    out[(size_t)j * ldm + q] = s;
+  for (int q = 4 * lane; q < m; q += 256) {
+    vif_double2 s0 = {0., 0.}, s1 = {0., 0.};
+    if (self != 0.) {
+      const vif_double2* src = reinterpret_cast<const vif_double2*>(in + (size_t)j * ldm + q);
+      s0 = self * src[0];
+      s1 = self * src[1];
+    }
+#pragma unroll 8
+    for (int t = t0; t < t1; ++t) {
+      const double c = coefT[t];
+      const vif_double2* src = reinterpret_cast<const vif_double2*>(in + (size_t)trow[t] * ldm + q);
+      const vif_double2 x0 = src[0], x1 = src[1];
+      s0[0] = fma(c, x0[0], s0[0]);
+      s0[1] = fma(c, x0[1], s0[1]);
+      s1[0] = fma(c, x1[0], s1[0]);
+      s1[1] = fma(c, x1[1], s1[1]);
+    }
+    vif_store4(out + (size_t)j * ldm, q, m, s0, s1);
   }
 }
 
@@ -867,6 +935,41 @@ VifSolver::VifSolver(int n, int d, const double* d_X, const std::vector<double>&
   HIP_CHECK(hipMemcpyAsync(tptr_.get(), tptr.data(), sizeof(int) * (n + 1), hipMemcpyHostToDevice, stream));
   HIP_CHECK(hipMemcpyAsync(trow_.get(), trow.data(), sizeof(int) * trow.size(), hipMemcpyHostToDevice, stream));
   HIP_CHECK(hipMemcpyAsync(tslot_.get(), tslot.data(), sizeof(int) * tslot.size(), hipMemcpyHostToDevice, stream));
+  // processing order of the row and B-product kernels: the points along a Morton curve of their (first two)
+  // coordinates, so that rows worked on together share neighbour columns in L2 (the results do not depend on
+  // it: every row / column is computed by one wave); GPBOOST_AMD_VIF_ORDER=0 keeps the index order
+  const char* ordenv = std::getenv("GPBOOST_AMD_VIF_ORDER");
+  if (!(ordenv && std::string(ordenv) == "0") && n > 1) {
+    std::vector<double> hx((size_t)n * d);
+    HIP_CHECK(hipMemcpyAsync(hx.data(), d_X, sizeof(double) * hx.size(), hipMemcpyDeviceToHost, stream));
+    HIP_CHECK(hipStreamSynchronize(stream));
+    const int dd = std::min(d, 2);
+    double lo[2] = {0., 0.}, hi[2] = {0., 0.};
+    for (int q = 0; q < dd; ++q) {
+      lo[q] = hi[q] = hx[q];
+      for (int i = 0; i < n; ++i) {
+        lo[q] = std::min(lo[q], hx[(size_t)i * d + q]);
+        hi[q] = std::max(hi[q], hx[(size_t)i * d + q]);
+      }
+    }
+    std::vector<std::pair<uint64_t, int>> key(n);
+    for (int i = 0; i < n; ++i) {
+      uint64_t code = 0;
+      uint32_t c[2] = {0, 0};
+      for (int q = 0; q < dd; ++q) {
+        const double w = hi[q] > lo[q] ? (hx[(size_t)i * d + q] - lo[q]) / (hi[q] - lo[q]) : 0.;
+        c[q] = (uint32_t)std::min(65535., std::max(0., w * 65536.));
+      }
+      for (int bit = 15; bit >= 0; --bit)
+        for (int q = 0; q < dd; ++q) code = (code << 1) | ((c[q] >> bit) & 1u);
+      key[i] = {code, i};
+    }
+    std::sort(key.begin(), key.end());
+    std::vector<int> ord(n);
+    for (int i = 0; i < n; ++i) ord[i] = key[i].second;
+    ord_.alloc(n);
+    HIP_CHECK(hipMemcpyAsync(ord_.get(), ord.data(), sizeof(int) * n, hipMemcpyHostToDevice, stream));
+  }
   lds_bytes_ = rows_lds_bytes(nn, true);
   for (int cov : {kMatern05, kMatern15, kMatern25, kGaussian})
     dispatch_cov_vif(cov, [&](auto c) {
@@ -896,6 +999,9 @@ void VifSolver::Rows(int cov_type, double var, double phi, bool grad) {
   a.cjit = latent_ ? 1. + 1e-10 : 1.;   // JITTER_MULT_VECCHIA (utils.h:36; Vecchia_utils.cpp:1546-1548)
   a.r1 = rows_r1(nn_, grad);
   a.Bv = Bv_.get(); a.D = D_.get(); a.dBv0 = dBv0_.get(); a.dBv1 = dBv1_.get(); a.dD0 = dD0_.get(); a.dD1 = dD1_.get();
+  a.ord = ord_.size() ? ord_.get() : nullptr;
+  a.chunk = (n_ + 7) / 8;
+  const int grid = a.ord ? 8 * a.chunk : n_;
   const size_t lds = rows_lds_bytes(nn_, grad);
   const char* form = std::getenv("GPBOOST_AMD_VIF_ROWS");   // "lds": the LDS-staged VALU form (A/B)
   const bool lds_form = form != nullptr && std::string(form) == "lds";
@@ -903,26 +1009,30 @@ void VifSolver::Rows(int cov_type, double var, double phi, bool grad) {
   dispatch_cov_vif(cov_type, [&](auto c) {
     constexpr int COV = decltype(c)::value;
     if (mfma) {
-      if (grad) hipLaunchKernelGGL((vif_rows_mfma_kernel<COV, true>), dim3(n_), dim3(64), 0, s_, a);
-      else hipLaunchKernelGGL((vif_rows_mfma_kernel<COV, false>), dim3(n_), dim3(64), 0, s_, a);
+      if (grad) hipLaunchKernelGGL((vif_rows_mfma_kernel<COV, true>), dim3(grid), dim3(64), 0, s_, a);
+      else hipLaunchKernelGGL((vif_rows_mfma_kernel<COV, false>), dim3(grid), dim3(64), 0, s_, a);
     } else if (grad) {
-      hipLaunchKernelGGL((vif_rows_kernel<COV, true>), dim3(n_), dim3(kT), lds, s_, a);
+      hipLaunchKernelGGL((vif_rows_kernel<COV, true>), dim3(grid), dim3(kT), lds, s_, a);
     } else {
-      hipLaunchKernelGGL((vif_rows_kernel<COV, false>), dim3(n_), dim3(kT), lds, s_, a);
+      hipLaunchKernelGGL((vif_rows_kernel<COV, false>), dim3(grid), dim3(kT), lds, s_, a);
     }
   });
   HIP_CHECK(hipGetLastError());
 }
 
 void VifSolver::BRow(const double* in, const double* coef, double self, bool div, double* out, double* out_div) {
-  hipLaunchKernelGGL(vif_brow_kernel, dim3((n_ + 3) / 4), dim3(kT), 0, s_, in, nbr_.get(), coef, D_.get(), n_, nn_, m_,
-                     ldm_, self, div ? 1 : 0, out, out_div);
+  const int* ord = ord_.size() ? ord_.get() : nullptr;
+  const int nb = (n_ + 3) / 4, chunk = (nb + 7) / 8;
+  hipLaunchKernelGGL(vif_brow_kernel, dim3(ord ? 8 * chunk : nb), dim3(kT), 0, s_, in, nbr_.get(), coef, D_.get(), n_,
+                     nn_, m_, ldm_, self, div ? 1 : 0, out, out_div, ord, chunk);
   HIP_CHECK(hipGetLastError());
 }
 
-void VifSolver::BCol(const double* in, const double* coef, double self, double* out) {
-  hipLaunchKernelGGL(vif_bcol_kernel, dim3((n_ + 3) / 4), dim3(kT), 0, s_, in, tptr_.get(), trow_.get(), tslot_.get(),
-                     coef, n_, m_, ldm_, self, out);
+void VifSolver::BCol(const double* in, const double* coefT, double self, double* out) {
+  const int* ord = ord_.size() ? ord_.get() : nullptr;
+  const int nb = (n_ + 3) / 4, chunk = (nb + 7) / 8;
+  hipLaunchKernelGGL(vif_bcol_kernel, dim3(ord ? 8 * chunk : nb), dim3(kT), 0, s_, in, tptr_.get(), trow_.get(),
+                     coefT, n_, m_, ldm_, self, out, ord, chunk);
   HIP_CHECK(hipGetLastError());
 }
 
@@ -1065,7 +1175,7 @@ void VifSolver::Eval(int cov_type, double var, double phi, const double* d_y, bo
       fitc_mm_terms(s_, F.Kinv_.get(), F.Winv_.get(), F.Kmm_.get(), p == 0 ? F.Kmm_.get() : F.dKmm_.get(), mv_a, m, ldm,
                     F.part_.get(), red + 8 + 6 * p);
     // X = B^T D^-1 B K (A_), Xw = M^-1 X (V_), Bw = M^-1 BK (P0_)
-    BCol(F.Kd_.get(), Bv_.get(), 1., F.A_.get());
+    BCol(F.Kd_.get(), BvT_.get(), 1., F.A_.get());
     gemm_f64(s_, m, n, m, 1., F.Winv_.get(), ldm, 0, F.A_.get(), ldm, 0, 0., F.V_.get(), ldm);
     gemm_f64(s_, m, n, m, 1., F.Winv_.get(), ldm, 0, BK_.get(), ldm, 0, 0., P0_.get(), ldm);
     double* bkw = v + 6 * (size_t)n;   // (B K w)_i
@@ -1266,7 +1376,7 @@ void VifSolver::Predict(int cov_type, double var, double phi, const double* d_y,
   }
   // G = V (B^T D^-1 B K_nm) (m x m; :1910-1915), PPV^T = G^T V_p; Sig = K_mm,s^-1 K_mp; M^-1 PPV^T, M^-1 Q^T
   BRow(F.Kmn_.get(), Bv_.get(), 1., false, BK_.get(), F.Kd_.get());
-  BCol(F.Kd_.get(), Bv_.get(), 1., F.A_.get());
+  BCol(F.Kd_.get(), BvT_.get(), 1., F.A_.get());
   const long mm = (long)ldm * ldm;
   const int chunks = gemm_f64_splitk(s_, m, m, n, F.V_.get(), ldm, 0, F.A_.get(), ldm, 1, F.part_.get(), ldm, mm, 2048,
                                      F.max_chunks_);

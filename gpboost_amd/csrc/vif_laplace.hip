@@ -392,7 +392,7 @@ void VifLaplace::SpVec(const double* x, double* out, double* t, double* t2) {
 
 void VifLaplace::RMat(const double* X, double* out, double* t) {
   V_->BRow(X, V_->Bv_.get(), 1., true, t);
-  V_->BCol(t, V_->Bv_.get(), 1., out);
+  V_->BCol(t, V_->BvT_.get(), 1., out);
 }
 
 void VifLaplace::SpMat(const double* X, double* out, double* t, double* t2) {
@@ -401,8 +401,8 @@ void VifLaplace::SpMat(const double* X, double* out, double* t, double* t2) {
   hipLaunchKernelGGL(vl_zmat_kernel, dim3((n_ + 3) / 4), dim3(kT), 0, s_, n_, m_, ldm_, t2, t, V_->dD1_.get(),
                      V_->D_.get());
   HIP_CHECK(hipGetLastError());
-  V_->BCol(t2, V_->Bv_.get(), 1., out);
-  V_->BCol(t, V_->dBv1_.get(), 0., t2);
+  V_->BCol(t2, V_->BvT_.get(), 1., out);
+  V_->BCol(t, V_->dBvT1_.get(), 0., t2);
   launch_axpby((size_t)ldm_ * n_, 1., out, 1., t2, out, s_);
 }
 
@@ -493,7 +493,7 @@ LatentResult VifLaplace::Eval(int cov_type, int lik, const double* trafo, double
   V_->Prepare(cov_type, var, phi, grad_any, red + 48, M_.get());   // red[48] log det K_mm,s, red[49] log det M
   hipLaunchKernelGGL(vl_recip_kernel, dim3((n + kT - 1) / kT), dim3(kT), 0, s_, n, V_->D_.get(), dinv_.get());
   HIP_CHECK(hipGetLastError());
-  V_->BCol(F.Kd_.get(), V_->Bv_.get(), 1., C_.get());
+  V_->BCol(F.Kd_.get(), V_->BvT_.get(), 1., C_.get());
   ToNM(C_.get(), Cnm_.get());
   chol_->SetB(V_->Bv_.get(), dinv_.get(), grad_any ? V_->dBv1_.get() : nullptr, grad_any ? V_->dD1_.get() : nullptr);
   auto info_failed = [&](const int* info) {

@@ -5,7 +5,7 @@ import time
 
 import numpy as np
 
-sys.path.insert(0, ".")
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 os.environ.setdefault("GPBOOST_AMD_TIMING", "1")
 from gpboost_amd import GPModel, synthetic  # noqa: E402
 
