@@ -249,22 +249,27 @@ __global__ void __launch_bounds__(256) chol_gemm_kernel(const CholGemmTask* __re
     for (int b = 0; b < 2; ++b) acc[a][b] = (double4_t){0., 0., 0., 0.};
   constexpr int EPT = GK * GT / 256;
   double ra[EPT], rb[EPT];
+  // branch-free tile loads: out-of-range elements read a clamped (valid, finite) address and are multiplied by 0
+  // when stored to LDS (a product, not a select, so the loads stay unconditional; the product after the MFMAs of the
+  // current tile, so the loads of the next tile are in flight meanwhile)
+  unsigned okA = 0, okB = 0;
   auto load = [&](int kk) {
+    okA = okB = 0;
 #pragma unroll
     for (int e = 0; e < EPT; ++e) {
       const int idx = tid + e * 256;
       int i, k;
       if (ta) { k = idx & (GK - 1); i = idx / GK; } else { i = idx & (GT - 1); k = idx / GT; }
       const int gk = kk + k;
-      double v = 0.;
-      if (i < g.M && gk < g.K) v = ta ? A[(size_t)gk + (size_t)i * g.lda] : A[(size_t)i + (size_t)gk * g.lda];
-      ra[e] = v;
+      const int ic = min(i, g.M - 1), kc = min(gk, g.K - 1);
+      ra[e] = ta ? A[(size_t)kc + (size_t)ic * g.lda] : A[(size_t)ic + (size_t)kc * g.lda];
+      okA |= (i < g.M && gk < g.K) ? 1u << e : 0u;
       int j, kb;
       if (tb) { j = idx & (GT - 1); kb = idx / GT; } else { kb = idx & (GK - 1); j = idx / GK; }
       const int gkb = kk + kb;
-      double w = 0.;
-      if (j < g.N && gkb < g.K) w = tb ? B[(size_t)j + (size_t)gkb * g.ldb] : B[(size_t)gkb + (size_t)j * g.ldb];
-      rb[e] = w;
+      const int jc = min(j, g.N - 1), kbc = min(gkb, g.K - 1);
+      rb[e] = tb ? B[(size_t)jc + (size_t)kbc * g.ldb] : B[(size_t)kbc + (size_t)jc * g.ldb];
+      okB |= (j < g.N && gkb < g.K) ? 1u << e : 0u;
     }
   };
   auto store = [&](int buf) {
@@ -273,10 +278,10 @@ __global__ void __launch_bounds__(256) chol_gemm_kernel(const CholGemmTask* __re
       const int idx = tid + e * 256;
       int i, k;
       if (ta) { k = idx & (GK - 1); i = idx / GK; } else { i = idx & (GT - 1); k = idx / GT; }
-      As[buf][k][i] = ra[e];
+      As[buf][k][i] = ra[e] * ((okA >> e) & 1u ? 1. : 0.);
       int j, kb;
       if (tb) { j = idx & (GT - 1); kb = idx / GT; } else { kb = idx & (GK - 1); j = idx / GK; }
-      Bs[buf][kb][j] = rb[e];
+      Bs[buf][kb][j] = rb[e] * ((okB >> e) & 1u ? 1. : 0.);
     }
   };
   if (g.K > 0) {

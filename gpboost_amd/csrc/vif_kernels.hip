@@ -374,13 +374,13 @@ __device__ __forceinline__ void tri_rc(int e, int& p, int& b) {
 // triangle); one scratch matrix takes G_1 = V^T P_0, then G_2 = V^T P_1 for the transposed sums, and finally
 // dC_0 (lower triangle) and dC_1 (upper triangle, diagonal in column 32): two 32 x 33 matrices per wave.
 template <int COV, bool GRAD>
-__global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) vif_rows_mfma_kernel(VifRowsArgs a) {
   constexpr int LD = 33;   // row stride of the 32 x 32 blocks
   constexpr int G = GRAD ? 3 : 1;
   __shared__ double C[32 * LD];
   __shared__ double X[GRAD ? 32 * LD : 1];
   __shared__ int idx[32];
-  __shared__ double vecs[4][32];   // c, dc0, dc1, A
+  __shared__ double vecs[3][32];   // c, dc0, dc1
   __shared__ double rdg[32];       // 1 / L_jj
   const int ir = vif_row_slot(a.ord, a.chunk, a.n - a.i0), lane = threadIdx.x;
   if (ir < 0) return;
@@ -528,26 +528,48 @@ __global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
       }
     }
   }
-  wave_chol(C, LD, k, lane);
-  if (lane < k) rdg[lane] = 1. / C[lane * LD + lane];
   wave_sync();
+  // Cholesky of C in registers, right-looking: lane p < 32 holds row p (lower part; the rows / columns >= k padded
+  // with the identity, so all 32 steps run unconditionally), the column entries L(c, j) broadcast by readlane
+  const int pl = min(lane, 31);
+  double rw[32];
+#pragma unroll
+  for (int c = 0; c < 32; ++c) {
+    const double v = C[pl * LD + c];
+    rw[c] = (lane < k && c < k) ? (c <= lane ? v : 0.) : (c == lane ? 1. : 0.);
+  }
+  double dj = 1.;
+#pragma unroll
+  for (int j = 0; j < 32; ++j) {
+    const double djj = sqrt(readlane_d(rw[j], j));
+    rw[j] = lane > j ? rw[j] / djj : (lane == j ? djj : 0.);
+    dj = lane == j ? djj : dj;
+#pragma unroll
+    for (int c = j + 1; c < 32; ++c) rw[c] = fma(-rw[j], readlane_d(rw[j], c), rw[c]);
+  }
+  // the factor's rows back to LDS (the backward sweep reads its columns), 1 / L_jj
+#pragma unroll
+  for (int c = 0; c < 32; ++c)
+    if (lane < 32) C[lane * LD + c] = rw[c];
+  if (lane < 32) rdg[lane] = 1. / dj;
+  wave_sync();
+  // L L^T x = b for lane-distributed right-hand sides (lane p holds entry p; zero beyond k)
   auto solve = [&](double* x, int nr) {
-    for (int j = 0; j < k; ++j) {
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
       const double rjj = rdg[j];
-      const double lij = lane < k ? C[lane * LD + j] : 0.;
       for (int r = 0; r < nr; ++r) {
         const double xj = readlane_d(x[r], j) * rjj;
-        if (lane == j) x[r] = xj;
-        else if (lane > j) x[r] -= lij * xj;
+        x[r] = lane == j ? xj : (lane > j ? fma(-rw[j], xj, x[r]) : x[r]);
       }
     }
-    for (int j = k - 1; j >= 0; --j) {
+#pragma unroll
+    for (int j = 31; j >= 0; --j) {
       const double rjj = rdg[j];
-      const double lji = lane < j ? C[j * LD + lane] : 0.;
+      const double lji = C[j * LD + pl];   // L(j, lane), used for lane < j
       for (int r = 0; r < nr; ++r) {
         const double xj = readlane_d(x[r], j) * rjj;
-        if (lane == j) x[r] = xj;
-        else if (lane < j) x[r] -= lji * xj;
+        x[r] = lane == j ? xj : (lane < j ? fma(-lji, xj, x[r]) : x[r]);
       }
     }
   };
@@ -555,22 +577,21 @@ __global__ void __launch_bounds__(64) vif_rows_mfma_kernel(VifRowsArgs a) {
   solve(xa, 1);
   double xd[2] = {0., 0.};
   if (GRAD) {
-    if (lane < k) vecs[3][lane] = xa[0];
-    wave_sync();
-    if (lane < k) {
-      // r_k = dc_k - dC_k A (dC_0 from the lower triangle of X, dC_1 from the upper one, both symmetric)
-      double r0 = vecs[1][lane], r1 = vecs[2][lane];
-      for (int b = 0; b < k; ++b) {
-        const double ab = vecs[3][b];
-        const double u = X[lane * LD + b], w = X[b * LD + lane];
+    // r_k = dc_k - dC_k A (dC_0 from the lower triangle of X, dC_1 from the upper one, both symmetric; A_b by readlane)
+    double r0 = lane < k ? vecs[1][lane] : 0., r1 = lane < k ? vecs[2][lane] : 0.;
+#pragma unroll
+    for (int b = 0; b < 32; ++b) {
+      if (b < k) {
+        const double ab = readlane_d(xa[0], b);
+        const double u = X[pl * LD + b], w = X[b * LD + pl];
         const double e0 = b <= lane ? u : w;
-        const double e1 = b < lane ? w : (b > lane ? u : X[lane * LD + 32]);
-        r0 -= e0 * ab;
-        r1 -= e1 * ab;
+        const double e1 = b < lane ? w : (b > lane ? u : X[pl * LD + 32]);
+        r0 = fma(-e0, ab, r0);
+        r1 = fma(-e1, ab, r1);
       }
-      xd[0] = r0;
-      xd[1] = r1;
     }
+    xd[0] = lane < k ? r0 : 0.;
+    xd[1] = lane < k ? r1 : 0.;
     solve(xd, 2);
   }
   double s0 = 0., s1 = 0., s2 = 0.;
