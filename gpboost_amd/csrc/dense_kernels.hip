@@ -452,20 +452,36 @@ __global__ void __launch_bounds__(256) potrf_diag_quad_kernel(double* A, int lda
     if (c <= r && r < ib && c < ib) A[(size_t)(j0 + r) + (size_t)(j0 + c) * lda] = col[k];
   }
   __syncthreads();
-  // L^-1 by the one-wave kernel's forward substitution (column r on lane r; the same operations in the
-  // same order, so the factor and the inverse equal that kernel's bit for bit): wave 0 only
-  if (w != 0) return;
-  double x[64];
+  // L^-1 (column r on lane r) by the right-looking form of the one-wave kernel's forward substitution, on the
+  // four waves: wave w keeps the partial sums acc_i of its rows i = 4k + w; step p: the owner of row p forms
+  // x_p = acc_p / L_pp (its final entry) and publishes it, one barrier, every wave updates acc_i -= L_ip x_p for
+  // its rows i > p. Each acc_i sees the same fmas in the same order (p ascending from delta_ir) as the one-wave
+  // kernel's dot products, so the inverse is bit-identical, at one division + one fma of latency per step instead
+  // of a dependent LDS-load + fma chain of length i per row on one wave.
+  double acc[16];
 #pragma unroll
-  for (int i = 0; i < 64; ++i) {
-    double s = (i == r) ? 1. : 0.;
+  for (int k = 0; k < 16; ++k) acc[k] = (4 * k + w == r) ? 1. : 0.;
 #pragma unroll
-    for (int p = 0; p < i; ++p) s -= Ls[i][p] * x[p];
-    x[i] = (i >= r && i < ib) ? s / Ls[i][i] : 0.;
+  for (int p = 0; p < 64; ++p) {
+    if (w == (p & 3)) {
+      const double xp = (p >= r && p < ib) ? acc[p >> 2] / Ls[p][p] : 0.;
+      acc[p >> 2] = xp;
+      colb[p & 1][r] = xp;
+    }
+    __syncthreads();
+    const double xp = colb[p & 1][r];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (4 * k + 3 <= p) continue;   // every row of register k is <= p
+      const int i = 4 * k + w;
+      if (i > p) acc[k] = fma(-Ls[i][p], xp, acc[k]);
+    }
   }
 #pragma unroll
-  for (int i = 0; i < 64; ++i)
-    if (i < ib && r < ib) Winv[(size_t)(j0 + i) + (size_t)(j0 + r) * ldw] = (r <= i) ? x[i] : 0.;
+  for (int k = 0; k < 16; ++k) {
+    const int i = 4 * k + w;
+    if (i < ib && r < ib) Winv[(size_t)(j0 + i) + (size_t)(j0 + r) * ldw] = (r <= i) ? acc[k] : 0.;
+  }
 }
 
 // one diagonal block: GPBOOST_AMD_DIAG_FORM = quad (default) | wave | old (A/B)

@@ -80,6 +80,7 @@ enum CholOpType {
   kOpScatterX,       // CholColTask: X[cols(s)] = V_s[0:ns]
   kOpFSolve1,        // t = 1, a level of small supernodes: one workgroup per supernode runs its whole forward
   kOpBSolve1,        //   / backward panel sweep; ntask = the level's supernodes, task0 = its first lvl_sup index
+  kOpLoadV,          // CholColTask: V_s[0:ns] = X[cols(s)] (a backward-only sweep's input)
 };
 struct CholOp {
   int type, ntask;
@@ -135,8 +136,10 @@ void chol_analyze(int n, int m, const int* nbr, int d, const double* X, int leaf
 // Schedule of a forward + backward solve with t right-hand sides (front vectors fs x t per supernode
 // in the scratch, ld fs; the global X is n x t, ld n, in elimination positions). vofs: per supernode
 // scratch offsets (nsup + 1). forward_only: stop after the forward sweep (L^-1 b left in the fronts,
-// scattered to X).
-void chol_solve_schedule(const CholPlan& P, int t, bool forward_only, CholSchedule& S, std::vector<int64_t>& vofs);
+// scattered to X). backward_only: the backward sweep alone, its input (the layout a forward-only sweep
+// leaves in X) loaded into the fronts first.
+void chol_solve_schedule(const CholPlan& P, int t, bool forward_only, CholSchedule& S, std::vector<int64_t>& vofs,
+                         bool backward_only = false);
 
 // A's lower entries in the front layout and their clique contributions (host, once per plan):
 //   column g (elimination position) holds entries [ecol[g], ecol[g+1]) (rows ascending, the diagonal
@@ -176,6 +179,9 @@ class SparseChol {
   void ForwardCols(const double* B, double* X, int nrhs);
   // X = A^-1 B for nrhs columns (device column-major n x nrhs, ld n, matrix labels; X may alias B)
   void SolveMulti(const double* B, double* X, int nrhs);
+  // X = P^T L^-T B for nrhs columns, B in the layout ForwardCols returns (so BackwardCols(ForwardCols(b)) = A^-1 b;
+  // X may alias B)
+  void BackwardCols(const double* B, double* X, int nrhs);
   // 2 sum log L_ii (synchronises)
   double LogDet();
   // non-positive pivots of the last factorization (synchronises)
@@ -188,7 +194,7 @@ class SparseChol {
 
  private:
   void Run(const SparseCholDev& sch, double* ybuf, const void* solve_args);
-  void SolveCols(const double* b, double* x, int t, bool forward_only);
+  void SolveCols(const double* b, double* x, int t, int mode);   // mode 0: full, 1: forward only, 2: backward only
   struct Impl;
   CholPlan plan_;
   hipStream_t s_;

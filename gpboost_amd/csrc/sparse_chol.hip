@@ -21,6 +21,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <string>
 #include <map>
 #include <utility>
 #include <vector>
@@ -233,6 +234,7 @@ __global__ void __launch_bounds__(256) chol_diag_kernel(const CholDiagTask* __re
 constexpr int GT = 64, GK = 16;
 __global__ void __launch_bounds__(256) chol_gemm_kernel(const CholGemmTask* __restrict__ tasks, int64_t t0, Bufs bufs) {
   const CholGemmTask g = tasks[t0 + blockIdx.x];
+  if (g.M <= 0 || g.N <= 0) return;   // empty tile (the clamped loads below need M, N >= 1)
   const double* A = bufs.p[(g.flags >> 4) & 7] + g.a;
   const double* B = bufs.p[(g.flags >> 7) & 7] + g.b;
   double* C = bufs.p[(g.flags >> 10) & 7] + g.c;
@@ -306,6 +308,89 @@ __global__ void __launch_bounds__(256) chol_gemm_kernel(const CholGemmTask* __re
     if (more) store(buf ^ 1);
     __syncthreads();
     buf ^= 1;
+  }
+  const bool lower = g.flags & kCgLower;
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int i = wm + a * 16 + (lane >> 4) + 4 * rg;
+        const int j = wn + b * 16 + (lane & 15);
+        if (i < g.M && j < g.N && !(lower && i - j + g.doff < 0)) {
+          double* c = C + (size_t)i + (size_t)j * g.ldc;
+          const double prev = g.beta == 0. ? 0. : g.beta * (*c);
+          *c = prev + g.alpha * acc[a][b][rg];
+        }
+      }
+}
+
+// ---- the same tile product for tasks with K <= 64 in launches of few tiles (the solves' per-block steps, the
+// small fronts): all of op(A) (64 x K) and op(B) (K x 64) are loaded at once (16 + 16 loads in flight per thread),
+// one barrier, then the K / 4 MFMA steps; a lone tile costs one memory round trip instead of one per K step of 16.
+// Same k order through the MFMA as chol_gemm_kernel, so the same bits.
+constexpr int kSmallGemmTiles = 2048;
+__global__ void __launch_bounds__(256) chol_gemm_k64_kernel(const CholGemmTask* __restrict__ tasks, int64_t t0, Bufs bufs) {
+  const CholGemmTask g = tasks[t0 + blockIdx.x];
+  if (g.M <= 0 || g.N <= 0) return;   // empty tile (the clamped loads below need M, N >= 1)
+  const double* A = bufs.p[(g.flags >> 4) & 7] + g.a;
+  const double* B = bufs.p[(g.flags >> 7) & 7] + g.b;
+  double* C = bufs.p[(g.flags >> 10) & 7] + g.c;
+  const bool ta = g.flags & kCgTA, tb = g.flags & kCgTB;
+  __shared__ double As[64][GT + 1];
+  __shared__ double Bs[64][GT + 1];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = (wave >> 1) * 32, wn = (wave & 1) * 32;
+  constexpr int EPT = 64 * GT / 256;
+  double ra[EPT], rb[EPT];
+  unsigned okA = 0, okB = 0;
+  // K = 0 (an empty product): every element is masked; the clamped loads then read element 0 of the operands,
+  // which is avoided by pointing them at C's (valid) tile origin instead
+  const int Kc = max(g.K, 1);
+  const double* Ar = g.K > 0 ? A : C;
+  const double* Br = g.K > 0 ? B : C;
+  const int lda = g.K > 0 ? g.lda : 0, ldb = g.K > 0 ? g.ldb : 0;
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const int idx = tid + e * 256;
+    int i, k;
+    if (ta) { k = idx & 63; i = idx >> 6; } else { i = idx & (GT - 1); k = idx / GT; }
+    const int ic = g.K > 0 ? min(i, g.M - 1) : 0, kc = min(k, Kc - 1);
+    ra[e] = ta ? Ar[(size_t)kc + (size_t)ic * lda] : Ar[(size_t)ic + (size_t)kc * lda];
+    okA |= (i < g.M && k < g.K) ? 1u << e : 0u;
+    int j, kb;
+    if (tb) { j = idx & (GT - 1); kb = idx / GT; } else { kb = idx & 63; j = idx >> 6; }
+    const int jc = g.K > 0 ? min(j, g.N - 1) : 0, kbc = min(kb, Kc - 1);
+    rb[e] = tb ? Br[(size_t)jc + (size_t)kbc * ldb] : Br[(size_t)kbc + (size_t)jc * ldb];
+    okB |= (j < g.N && kb < g.K) ? 1u << e : 0u;
+  }
+#pragma unroll
+  for (int e = 0; e < EPT; ++e) {
+    const int idx = tid + e * 256;
+    int i, k;
+    if (ta) { k = idx & 63; i = idx >> 6; } else { i = idx & (GT - 1); k = idx / GT; }
+    As[k][i] = ra[e] * ((okA >> e) & 1u ? 1. : 0.);
+    int j, kb;
+    if (tb) { j = idx & (GT - 1); kb = idx / GT; } else { kb = idx & 63; j = idx >> 6; }
+    Bs[kb][j] = rb[e] * ((okB >> e) & 1u ? 1. : 0.);
+  }
+  __syncthreads();
+  double4_t acc[2][2];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b) acc[a][b] = (double4_t){0., 0., 0., 0.};
+  const int kmax = (g.K + 3) & ~3;
+  for (int k4 = 0; k4 < kmax; k4 += 4) {
+    const int kl = k4 + (lane >> 4);
+    const double a0 = As[kl][wm + (lane & 15)], a1 = As[kl][wm + 16 + (lane & 15)];
+    const double b0 = Bs[kl][wn + (lane & 15)], b1 = Bs[kl][wn + 16 + (lane & 15)];
+    acc[0][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b0, acc[0][0], 0, 0, 0);
+    acc[0][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, b1, acc[0][1], 0, 0, 0);
+    acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
+    acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
   }
   const bool lower = g.flags & kCgLower;
 #pragma unroll
@@ -426,6 +511,18 @@ __global__ void __launch_bounds__(256) chol_scatter_x_kernel(const CholColTask* 
   const int k0 = blockIdx.y * kSolveColGroup, k1 = min(a.t, k0 + kSolveColGroup);
   for (int k = k0; k < k1; ++k)
     for (int i = tk.c0 + threadIdx.x; i < tk.c1; i += 256) a.X[P.perm[sf + i] + (size_t)k * P.n] = V[i + (size_t)k * fs];
+}
+
+__global__ void __launch_bounds__(256) chol_load_v_kernel(const CholColTask* __restrict__ tasks, int64_t t0, DevPlan P,
+                                                          SolveArgs a) {
+  const CholColTask tk = tasks[t0 + blockIdx.x];
+  const int s = tk.s;
+  const int sf = P.sfirst[s], ns = P.sfirst[s + 1] - sf;
+  const int fs = ns + (int)(P.rptr[s + 1] - P.rptr[s]);
+  double* V = a.V + a.vofs[s];
+  const int k0 = blockIdx.y * kSolveColGroup, k1 = min(a.t, k0 + kSolveColGroup);
+  for (int k = k0; k < k1; ++k)
+    for (int i = tk.c0 + threadIdx.x; i < tk.c1; i += 256) V[i + (size_t)k * fs] = a.b[P.perm[sf + i] + (size_t)k * P.n];
 }
 
 // ---- single right-hand side: one workgroup per supernode of a level runs its whole panel (the forward
@@ -622,8 +719,19 @@ struct SparseCholDev {
   DevBuf<CholColTask> col;
   DevBuf<CholReduceTask> red;
   std::vector<CholOp> ops;
+  std::vector<char> k64;   // per op: a GEMM launch of few tiles, all with K <= 64 (chol_gemm_k64_kernel)
   int64_t y_doubles = 0, p_doubles = 0;
   void Upload(const CholSchedule& S) {
+    k64.assign(S.ops.size(), 0);
+    const char* e = std::getenv("GPBOOST_AMD_CHOL_K64");   // "0": always the K-pipelined form (A/B)
+    if (!(e && std::string(e) == "0"))
+      for (size_t o = 0; o < S.ops.size(); ++o) {
+        const CholOp& op = S.ops[o];
+        if (op.type != kOpGemm || op.ntask > kSmallGemmTiles) continue;
+        int kmax = 0;
+        for (int64_t t = op.task0; t < op.task0 + op.ntask; ++t) kmax = std::max(kmax, S.gemm[t].K);
+        k64[o] = kmax <= 64;
+      }
     upload(gemm, S.gemm);
     upload(diag, S.diag);
     upload(col, S.col);
@@ -718,7 +826,8 @@ void SparseChol::Run(const SparseCholDev& sch, double* ybuf, const void* solve_a
   if ((int64_t)d_P_.size() < sch.p_doubles) d_P_.alloc(sch.p_doubles);
   Bufs b{{d_F_.get(), d_S_.get(), d_Wd_.get(), ybuf, d_P_.get()}};
   const DevPlan& dp = impl_->dp;
-  for (const CholOp& op : sch.ops) {
+  for (size_t oi = 0; oi < sch.ops.size(); ++oi) {
+    const CholOp& op = sch.ops[oi];
     const dim3 grid(op.ntask);
     switch (op.type) {
       case kOpAsmTile:
@@ -734,7 +843,10 @@ void SparseChol::Run(const SparseCholDev& sch, double* ybuf, const void* solve_a
                            d_info_.get());
         break;
       case kOpGemm:
-        hipLaunchKernelGGL(chol_gemm_kernel, grid, dim3(256), 0, s_, sch.gemm.get(), op.task0, b);
+        if (sch.k64[oi])
+          hipLaunchKernelGGL(chol_gemm_k64_kernel, grid, dim3(256), 0, s_, sch.gemm.get(), op.task0, b);
+        else
+          hipLaunchKernelGGL(chol_gemm_kernel, grid, dim3(256), 0, s_, sch.gemm.get(), op.task0, b);
         break;
       case kOpReduce:
         hipLaunchKernelGGL(chol_reduce_kernel, grid, dim3(256), 0, s_, sch.red.get(), op.task0, b);
@@ -747,10 +859,13 @@ void SparseChol::Run(const SparseCholDev& sch, double* ybuf, const void* solve_a
         break;
       case kOpAsmV:
       case kOpGatherX:
+      case kOpLoadV:
       case kOpScatterX: {   // one block per (supernode, group of kSolveColGroup right-hand sides)
         const SolveArgs& sa = *static_cast<const SolveArgs*>(solve_args);
         const dim3 g2(op.ntask, (sa.t + kSolveColGroup - 1) / kSolveColGroup);
-        if (op.type == kOpAsmV)
+        if (op.type == kOpLoadV)
+          hipLaunchKernelGGL(chol_load_v_kernel, g2, dim3(256), 0, s_, sch.col.get(), op.task0, dp, sa);
+        else if (op.type == kOpAsmV)
           hipLaunchKernelGGL(chol_asmv_kernel, g2, dim3(256), 0, s_, sch.col.get(), op.task0, dp, sa);
         else if (op.type == kOpGatherX)
           hipLaunchKernelGGL(chol_gather_x_kernel, g2, dim3(256), 0, s_, sch.col.get(), op.task0, dp, sa);
@@ -812,16 +927,16 @@ double SparseChol::LogDet() {
   return h;
 }
 
-void SparseChol::SolveCols(const double* b, double* x, int t, bool forward_only) {
+void SparseChol::SolveCols(const double* b, double* x, int t, int mode) {
   if (!factored_) Fatal("sparse Cholesky: solve before a factorization");
   if (t <= 0) return;
-  const std::pair<int, int> key(t, forward_only ? 1 : 0);
+  const std::pair<int, int> key(t, mode);
   Impl& I = *impl_;
   auto it = I.solve.find(key);
   if (it == I.solve.end()) {
     CholSchedule S;
     std::vector<int64_t> vofs;
-    chol_solve_schedule(plan_, t, forward_only, S, vofs);
+    chol_solve_schedule(plan_, t, mode == 1, S, vofs, mode == 2);
     std::unique_ptr<SparseCholDev> dev(new SparseCholDev);
     dev->Upload(S);
     std::unique_ptr<DevBuf<int64_t>> dv(new DevBuf<int64_t>);
@@ -835,11 +950,13 @@ void SparseChol::SolveCols(const double* b, double* x, int t, bool forward_only)
   Run(sch, I.V.get(), &a);
 }
 
-void SparseChol::Solve(const double* b, double* x) { SolveCols(b, x, 1, false); }
+void SparseChol::Solve(const double* b, double* x) { SolveCols(b, x, 1, 0); }
 
-void SparseChol::ForwardCols(const double* B, double* X, int nrhs) { SolveCols(B, X, nrhs, true); }
+void SparseChol::ForwardCols(const double* B, double* X, int nrhs) { SolveCols(B, X, nrhs, 1); }
 
-void SparseChol::SolveMulti(const double* B, double* X, int nrhs) { SolveCols(B, X, nrhs, false); }
+void SparseChol::SolveMulti(const double* B, double* X, int nrhs) { SolveCols(B, X, nrhs, 0); }
+
+void SparseChol::BackwardCols(const double* B, double* X, int nrhs) { SolveCols(B, X, nrhs, 2); }
 
 void SparseChol::SelectedInverse(double* tr_bdb, double* tr_da, double* diagS) {
   if (!factored_) Fatal("sparse Cholesky: selected inverse before a factorization");

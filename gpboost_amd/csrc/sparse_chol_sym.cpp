@@ -601,7 +601,8 @@ void build_selinv_schedule(const CholPlan& P, CholSchedule& S) {
 
 }  // namespace
 
-void chol_solve_schedule(const CholPlan& P, int t, bool forward_only, CholSchedule& S, std::vector<int64_t>& vofs) {
+void chol_solve_schedule(const CholPlan& P, int t, bool forward_only, CholSchedule& S, std::vector<int64_t>& vofs,
+                         bool backward_only) {
   S = CholSchedule();
   OpBuilder ob(S);
   vofs.assign(P.nsup + 1, 0);
@@ -617,9 +618,17 @@ void chol_solve_schedule(const CholPlan& P, int t, bool forward_only, CholSchedu
       for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) mx = std::max<int64_t>(mx, (int64_t)P.fs(P.lvl_sup[q]) * P.ns(P.lvl_sup[q]));
       small[l] = mx <= kSmallPanel;
     }
-  for (int l = 0; l < nlev; ++l) {
-    if (small[l] && !forward_only) {
+  for (int l = 0; l < nlev && !backward_only; ++l) {
+    if (small[l]) {
       S.ops.push_back(CholOp{kOpFSolve1, P.lvl_ptr[l + 1] - P.lvl_ptr[l], (int64_t)P.lvl_ptr[l]});
+      if (forward_only) {   // the level's L^-1 b to X
+        ob.begin(kOpScatterX);
+        for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) {
+          const int s = P.lvl_sup[q];
+          S.col.push_back(CholColTask{s, 0, P.ns(s), 0});
+        }
+        ob.end();
+      }
       continue;
     }
     ob.begin(kOpAsmV);
@@ -665,6 +674,11 @@ void chol_solve_schedule(const CholPlan& P, int t, bool forward_only, CholSchedu
     }
   }
   if (forward_only) return;
+  if (backward_only) {   // the input (L^-1 b, forward-sweep layout) into every front's first ns entries
+    ob.begin(kOpLoadV);
+    for (int s = 0; s < P.nsup; ++s) S.col.push_back(CholColTask{s, 0, P.ns(s), 0});
+    ob.end();
+  }
   for (int l = nlev - 1; l >= 0; --l) {
     if (small[l]) {
       S.ops.push_back(CholOp{kOpBSolve1, P.lvl_ptr[l + 1] - P.lvl_ptr[l], (int64_t)P.lvl_ptr[l]});

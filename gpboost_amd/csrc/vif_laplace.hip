@@ -14,6 +14,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <limits>
+#include <string>
+#include <utility>
+#include <vector>
 
 #include "dense.h"
 #include "fitc.h"
@@ -451,6 +454,9 @@ void VifLaplace::Woodbury2(double* logdet_dev) {
   fitc_lower_t(s_, M2i_.get(), m, ldm, M2iT_.get());
 }
 
+// out = (A - C M^-1 C^T)^-1 r = A^-1 r + A^-1 C M2^-1 C^T A^-1 r (likelihoods.h:2586-2601: two full solves; the
+// algebraically equal one-forward-one-backward form y = L^-1 P r, out = P^T L^-T (y + CL M2^-1 CL^T y) halves the
+// sweeps but moved the smooth-kernel fixtures' nll by ~3e-9 relative, past the parity bound). x: A^-1 r.
 void VifLaplace::SolveSW(const double* r, double* out, double* x) {
   const int m = m_, ldm = ldm_;
   double* t = mv_.get() + 3 * (size_t)ldm;
@@ -487,6 +493,16 @@ LatentResult VifLaplace::Eval(int cov_type, int lik, const double* trafo, double
   const bool cap = lik == kLikPoisson || lik == kLikGamma;   // cap_change_mode_newton_ (likelihoods.h:481-490)
   double* red = red_.get();
   HIP_CHECK(hipEventRecord(ev_[0], s_));
+  // phase timing (GPBOOST_AMD_TIMING): events after each phase, summed per label at the end
+  static const bool timing = std::getenv("GPBOOST_AMD_TIMING") != nullptr;
+  std::vector<std::pair<const char*, hipEvent_t>> marks;
+  auto mark = [&](const char* label) {
+    if (!timing) return;
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    HIP_CHECK(hipEventRecord(e, s_));
+    marks.emplace_back(label, e);
+  };
   // prior: K, K_mm,s, V, residual factor (+ derivatives), M = K_mm,s + (BK)^T D^-1 (BK) (red[0] log det K_mm,s,
   // red[1] log det M), C = B^T D^-1 B K (the reference's Bt_D_inv_B_cross_cov, re_model_template.h:8839-8855)
   HIP_CHECK(hipMemsetAsync(F.info_.get(), 0, sizeof(int), s_));
@@ -496,6 +512,7 @@ LatentResult VifLaplace::Eval(int cov_type, int lik, const double* trafo, double
   V_->BCol(F.Kd_.get(), V_->BvT_.get(), 1., C_.get());
   ToNM(C_.get(), Cnm_.get());
   chol_->SetB(V_->Bv_.get(), dinv_.get(), grad_any ? V_->dBv1_.get() : nullptr, grad_any ? V_->dD1_.get() : nullptr);
+  mark("prepare");
   auto info_failed = [&](const int* info) {
     int h = 0;
     HIP_CHECK(hipMemcpyAsync(&h, info, sizeof(int), hipMemcpyDeviceToHost, s_));
@@ -535,13 +552,17 @@ LatentResult VifLaplace::Eval(int cov_type, int lik, const double* trafo, double
       hipLaunchKernelGGL(vl_prep_kernel, dim3(nb), dim3(kT), 0, s_, n, lik, aux_, y_.get(), off, mode_.get(), d1_.get(),
                          w_.get(), static_cast<double*>(nullptr), rhs_.get(), static_cast<double*>(nullptr));
       HIP_CHECK(hipGetLastError());
+      mark("newton other");
       factor();
+      mark("factor");
       Woodbury2(logdet_M2);
+      mark("woodbury (L^-1 P C, m columns)");
       if (info_failed(info_.get())) {
         has_nan = true;
         break;
       }
       SolveSW(rhs_.get(), upd_.get(), x);
+      mark("newton solves");
       // Armijo slope (:2603-2611): dir^T (Sigma^-1 + W) dir with Sigma^-1 by the Woodbury form
       launch_axpby(n, 1., upd_.get(), -1., mode_.get(), dir, s_);
       {
@@ -594,8 +615,11 @@ LatentResult VifLaplace::Eval(int cov_type, int lik, const double* trafo, double
                      w_.get(), dw_.get(), static_cast<double*>(nullptr), part_.get());
   HIP_CHECK(hipGetLastError());
   launch_sum_blocks(part_.get(), nb, 1, red + 6, s_);
+  mark("newton other");
   factor();
+  mark("factor");
   Woodbury2(logdet_M2);
+  mark("woodbury (L^-1 P C, m columns)");
   if (info_failed(info_.get())) throw LatentNan("the full-scale Vecchia Woodbury matrix M2 is not positive definite");
   const double ldA = chol_->LogDet();
   HIP_CHECK(hipMemcpyAsync(h_red_, red, 50 * sizeof(double), hipMemcpyDeviceToHost, s_));
@@ -636,9 +660,12 @@ LatentResult VifLaplace::Eval(int cov_type, int lik, const double* trafo, double
       }
     // selected inverse of A: tr(S R), tr(S S'_1), diag(A^-1) (CalcLtLGivenSparsityPattern, :4737-4739)
     double tr_R = 0., tr_Sp1 = 0.;
+    mark("gradient other");
     chol_->SelectedInverse(&tr_R, &tr_Sp1, diagS_.get());
+    mark("selected inverse");
     // A^-1 C (m columns), M2^-1 (full), Y = M2^-1 (A^-1 C), G = M2^-1 K, CM = M2^-1 C (point-major)
     chol_->SolveMulti(Cnm_.get(), CL_.get(), m);
+    mark("A^-1 C (m columns)");
     ToMN(CL_.get(), AiC_.get());
     gemm_f64(s_, m, m, m, 1., M2i_.get(), ldm, 1, M2i_.get(), ldm, 0, 0., M2inv_.get(), ldm, 0, 0, 1, 1);
     double* CM = CL_.get();   // n x m free again: M2^-1 C (point-major)
@@ -805,14 +832,28 @@ LatentResult VifLaplace::Eval(int cov_type, int lik, const double* trafo, double
       res.grad.push_back(neg + 0.5 * h_red_[41] + h_red_[42]);
     }
   }
+  mark("gradient other");
   HIP_CHECK(hipEventRecord(ev_[1], s_));
   HIP_CHECK(hipEventSynchronize(ev_[1]));
   float ms = 0.f;
   HIP_CHECK(hipEventElapsedTime(&ms, ev_[0], ev_[1]));
   res.ms_total = ms;
-  if (std::getenv("GPBOOST_AMD_TIMING") != nullptr)
+  if (timing) {
     std::fprintf(stderr, "[vif laplace] %.2f ms: %d Newton steps (last factorization %.2f ms)\n", ms, res.newton_its,
                  chol_->last_factor_ms());
+    std::vector<std::pair<std::string, double>> sums;
+    hipEvent_t prev = ev_[0];
+    for (auto& mk : marks) {
+      float d = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&d, prev, mk.second));
+      auto it = std::find_if(sums.begin(), sums.end(), [&](const auto& q) { return q.first == mk.first; });
+      if (it == sums.end()) sums.emplace_back(mk.first, d);
+      else it->second += d;
+      prev = mk.second;
+    }
+    for (auto& q : sums) std::fprintf(stderr, "    %-34s %8.2f ms\n", q.first.c_str(), q.second);
+    for (auto& mk : marks) HIP_CHECK(hipEventDestroy(mk.second));
+  }
   return res;
 }
 
