@@ -216,20 +216,36 @@ __device__ __forceinline__ void gemm_tile_body(const GemmArgs& g) {
     __syncthreads();
     buf ^= 1;
   }
+  // epilogue: the beta C reads of a row group of tiles are issued together (clamped addresses, unconditional), then
+  // the masked stores -- one memory round trip per group instead of one per element
 #pragma unroll
-  for (int a = 0; a < WT; ++a)
+  for (int a = 0; a < WT; ++a) {
+    double prev[WT][4];
+    if (g.beta != 0.) {
+#pragma unroll
+      for (int b = 0; b < WT; ++b)
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) {
+          const int i = min(m0 + wm + a * 16 + (lane >> 4) + 4 * rg, g.M - 1);
+          const int j = min(n0 + wn + b * 16 + (lane & 15), g.N - 1);
+          prev[b][rg] = g.C[(size_t)i + (size_t)j * g.ldc];
+        }
+    } else {
+#pragma unroll
+      for (int b = 0; b < WT; ++b)
+#pragma unroll
+        for (int rg = 0; rg < 4; ++rg) prev[b][rg] = 0.;
+    }
 #pragma unroll
     for (int b = 0; b < WT; ++b)
 #pragma unroll
       for (int rg = 0; rg < 4; ++rg) {
         const int i = m0 + wm + a * 16 + (lane >> 4) + 4 * rg;
         const int j = n0 + wn + b * 16 + (lane & 15);
-        if (i < g.M && j < g.N && !(g.lower_out && j > i)) {
-          double* c = g.C + (size_t)i + (size_t)j * g.ldc;
-          const double prev = (g.beta == 0.) ? 0. : g.beta * (*c);
-          *c = prev + g.alpha * acc[a][b][rg];
-        }
+        const double v = (g.beta == 0. ? 0. : g.beta * prev[b][rg]) + g.alpha * acc[a][b][rg];
+        if (i < g.M && j < g.N && !(g.lower_out && j > i)) g.C[(size_t)i + (size_t)j * g.ldc] = v;
       }
+  }
 }
 
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2, 2))) gemm_f64_big_kernel(GemmArgs g) {

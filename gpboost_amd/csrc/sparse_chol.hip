@@ -121,10 +121,14 @@ __global__ void __launch_bounds__(256) chol_asm_tile_kernel(const CholColTask* _
     const int fc = nsc + (int)(P.rptr[ch + 1] - P.rptr[ch]);
     const double* U = F + P.foff[ch] + nsc + (size_t)nsc * fc;
     const int ia = ri[ii];
+    // unconditional loads (all 16 in flight): a missing or upper entry reads the child's lower element at the
+    // swapped / clamped indices (finite) and adds it times 0; fma(v, 1, acc) is the rounding of acc + v
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
       const int ib = ci[(tid >> 6) + 4 * q];
-      if (ia >= 0 && ib >= 0 && ia >= ib) acc[q] += U[ia + (size_t)ib * fc];
+      const double m = (ia >= 0 && ib >= 0 && ia >= ib) ? 1. : 0.;
+      const int hi = max(max(ia, ib), 0), lo = max(min(ia, ib), 0);
+      acc[q] = fma(U[hi + (size_t)lo * fc], m, acc[q]);
     }
   }
   const int i = rt + ii;
@@ -232,6 +236,34 @@ __global__ void __launch_bounds__(256) chol_diag_kernel(const CholDiagTask* __re
 
 // ---- batched GEMM tile: C = alpha op(A) op(B) + beta C, one task per workgroup
 constexpr int GT = 64, GK = 16;
+// the tile's epilogue: the beta C reads issued together (clamped addresses, unconditional), then the masked stores
+// (one memory round trip per tile instead of one per element)
+__device__ __forceinline__ void chol_gemm_epilogue(const CholGemmTask& g, double* C, const double4_t (&acc)[2][2], int wm,
+                                                   int wn, int lane) {
+  const bool lower = g.flags & kCgLower;
+  double prev[2][2][4];
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int i = min(wm + a * 16 + (lane >> 4) + 4 * rg, g.M - 1);
+        const int j = min(wn + b * 16 + (lane & 15), g.N - 1);
+        prev[a][b][rg] = g.beta == 0. ? 0. : C[(size_t)i + (size_t)j * g.ldc];
+      }
+#pragma unroll
+  for (int a = 0; a < 2; ++a)
+#pragma unroll
+    for (int b = 0; b < 2; ++b)
+#pragma unroll
+      for (int rg = 0; rg < 4; ++rg) {
+        const int i = wm + a * 16 + (lane >> 4) + 4 * rg;
+        const int j = wn + b * 16 + (lane & 15);
+        const double v = (g.beta == 0. ? 0. : g.beta * prev[a][b][rg]) + g.alpha * acc[a][b][rg];
+        if (i < g.M && j < g.N && !(lower && i - j + g.doff < 0)) C[(size_t)i + (size_t)j * g.ldc] = v;
+      }
+}
 __global__ void __launch_bounds__(256) chol_gemm_kernel(const CholGemmTask* __restrict__ tasks, int64_t t0, Bufs bufs) {
   const CholGemmTask g = tasks[t0 + blockIdx.x];
   if (g.M <= 0 || g.N <= 0) return;   // empty tile (the clamped loads below need M, N >= 1)
@@ -309,21 +341,7 @@ __global__ void __launch_bounds__(256) chol_gemm_kernel(const CholGemmTask* __re
     __syncthreads();
     buf ^= 1;
   }
-  const bool lower = g.flags & kCgLower;
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        const int i = wm + a * 16 + (lane >> 4) + 4 * rg;
-        const int j = wn + b * 16 + (lane & 15);
-        if (i < g.M && j < g.N && !(lower && i - j + g.doff < 0)) {
-          double* c = C + (size_t)i + (size_t)j * g.ldc;
-          const double prev = g.beta == 0. ? 0. : g.beta * (*c);
-          *c = prev + g.alpha * acc[a][b][rg];
-        }
-      }
+  chol_gemm_epilogue(g, C, acc, wm, wn, lane);
 }
 
 // ---- the same tile product for tasks with K <= 64 in launches of few tiles (the solves' per-block steps, the
@@ -392,21 +410,7 @@ __global__ void __launch_bounds__(256) chol_gemm_k64_kernel(const CholGemmTask* 
     acc[1][0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b0, acc[1][0], 0, 0, 0);
     acc[1][1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, b1, acc[1][1], 0, 0, 0);
   }
-  const bool lower = g.flags & kCgLower;
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int b = 0; b < 2; ++b)
-#pragma unroll
-      for (int rg = 0; rg < 4; ++rg) {
-        const int i = wm + a * 16 + (lane >> 4) + 4 * rg;
-        const int j = wn + b * 16 + (lane & 15);
-        if (i < g.M && j < g.N && !(lower && i - j + g.doff < 0)) {
-          double* c = C + (size_t)i + (size_t)j * g.ldc;
-          const double prev = g.beta == 0. ? 0. : g.beta * (*c);
-          *c = prev + g.alpha * acc[a][b][rg];
-        }
-      }
+  chol_gemm_epilogue(g, C, acc, wm, wn, lane);
 }
 
 // ---- selected inverse: S_RR of supernode s from its parent's front (both triangles), R columns [c0, c1)
@@ -605,9 +609,10 @@ __global__ void __launch_bounds__(256) chol_bsolve1_kernel(DevPlan P, Solve1Args
       const double vr = V[r];
       const double* Lr = L + r + (size_t)j0 * fs;
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {
+      for (int q = 0; q < 16; ++q) {   // unconditional loads; columns >= ib read column ib - 1 times 0
         const int j = w + 4 * q;
-        if (j < ib) acc[q] = fma(Lr[(size_t)j * fs], vr, acc[q]);
+        const double l = Lr[(size_t)min(j, ib - 1) * fs] * (j < ib ? 1. : 0.);
+        acc[q] = fma(l, vr, acc[q]);
       }
     }
 #pragma unroll
