@@ -81,6 +81,10 @@ enum CholOpType {
   kOpFSolve1,        // t = 1, a level of small supernodes: one workgroup per supernode runs its whole forward
   kOpBSolve1,        //   / backward panel sweep; ntask = the level's supernodes, task0 = its first lvl_sup index
   kOpLoadV,          // CholColTask: V_s[0:ns] = X[cols(s)] (a backward-only sweep's input)
+  kOpFwdVec,         // t = 1, CholColTask {s, block k, row tile rt}: x_b = W_b v_b (to the side buffer XS when rt is
+                     //   the first row tile) and v[rt:rt+64] -= L[rt:rt+64, b] x_b, one wave per task (one launch per
+                     //   block step instead of two)
+  kOpCopyXS,         // CholColTask: V_s[c0:c1] = XS_s[c0:c1] (the forward results of a fused level)
 };
 struct CholOp {
   int type, ntask;

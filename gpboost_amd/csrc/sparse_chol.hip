@@ -462,6 +462,10 @@ struct SolveArgs {
   const double* b;   // input, matrix labels, n x t (ld n)
   double* X;         // global X, matrix labels, n x t (ld n)
   int t;
+  double* XS;        // t = 1 fused forward steps: the block results (V's layout)
+  const double* F;   // the factor's fronts
+  const double* Wd;  // diagonal-block inverses
+  const int64_t* woff;
 };
 
 constexpr int kSolveColGroup = 4;   // right-hand sides per block of the solve's assembly / gather / scatter passes
@@ -529,6 +533,48 @@ __global__ void __launch_bounds__(256) chol_load_v_kernel(const CholColTask* __r
     for (int i = tk.c0 + threadIdx.x; i < tk.c1; i += 256) V[i + (size_t)k * fs] = a.b[P.perm[sf + i] + (size_t)k * P.n];
 }
 
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), l);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), l);
+  return __hiloint2double(hi, lo);
+}
+
+// ---- t = 1, one block step of a large level's forward sweep in one launch: every wave (task {s, k, rt}) forms
+// x_b = W_b v_b itself (lane i: sum over j of W[i][j] v_j, j ascending: fsolve1's order; W_b is zero above the
+// diagonal and beyond ib), the first row tile's wave stores it to XS (V[j0:j0+ib] is still being read by the other
+// waves), then rows rt + lane: v_r -= sum_j L[r][j0 + j] x_j (j ascending, as fsolve1)
+__global__ void __launch_bounds__(64) chol_fwd_vec_kernel(const CholColTask* __restrict__ tasks, int64_t t0, DevPlan P,
+                                                          SolveArgs a) {
+  const CholColTask tk = tasks[t0 + blockIdx.x];
+  const int s = tk.s, k = tk.c0, rt = tk.c1;
+  const int sf = P.sfirst[s], ns = P.sfirst[s + 1] - sf;
+  const int fs = ns + (int)(P.rptr[s + 1] - P.rptr[s]);
+  const int j0 = 64 * k, ib = min(64, ns - j0), r0 = j0 + ib;
+  double* V = a.V + a.vofs[s];
+  const int lane = threadIdx.x;
+  const double vl = lane < ib ? V[j0 + min(lane, ib - 1)] : 0.;
+  const double* W = a.Wd + a.woff[s] + (int64_t)k * 4096;
+  double x = 0.;
+#pragma unroll
+  for (int j = 0; j < 64; ++j) x = fma(W[lane + 64 * j], readlane_f64(vl, j), x);
+  if (rt == r0 && lane < ib) a.XS[a.vofs[s] + j0 + lane] = x;
+  const int r = rt + lane;
+  if (rt >= fs) return;
+  const int rc = min(r, fs - 1);
+  const double* Lr = a.F + P.foff[s] + rc + (size_t)j0 * fs;
+  double acc = V[rc];
+#pragma unroll
+  for (int j = 0; j < 64; ++j)   // x_j = 0 for j >= ib (those columns read column ib - 1: finite, times 0)
+    acc = fma(-Lr[(size_t)min(j, ib - 1) * fs], readlane_f64(x, j), acc);
+  if (r < fs) V[r] = acc;
+}
+
+__global__ void __launch_bounds__(256) chol_copy_xs_kernel(const CholColTask* __restrict__ tasks, int64_t t0, SolveArgs a) {
+  const CholColTask tk = tasks[t0 + blockIdx.x];
+  const int64_t o = a.vofs[tk.s];
+  for (int i = tk.c0 + threadIdx.x; i < tk.c1; i += 256) a.V[o + i] = a.XS[o + i];
+}
+
 // ---- single right-hand side: one workgroup per supernode of a level runs its whole panel (the forward
 // sweep assembles its front vector from b and the children, then per 64-column block x_b = W_b v_b and
 // v[below] -= L[below, b] x_b; the backward sweep gathers x at its rows R_s, then per block from the last
@@ -576,12 +622,16 @@ __global__ void __launch_bounds__(256) chol_fsolve1_kernel(DevPlan P, Solve1Args
       for (int j = 0; j <= tid; ++j) x = fma(W[tid + j * 64], vb[j], x);
       xb[tid] = x;
       V[j0 + tid] = x;
+    } else if (tid < 64) {
+      xb[tid] = 0.;
     }
     __syncthreads();
+    // all 64 column loads of a row in flight (columns >= ib read column ib - 1, times x_j = 0)
     for (int r = j0 + ib + tid; r < fs; r += 256) {
       double acc = V[r];
       const double* Lr = L + r + (size_t)j0 * fs;
-      for (int j = 0; j < ib; ++j) acc = fma(-Lr[(size_t)j * fs], xb[j], acc);
+#pragma unroll
+      for (int j = 0; j < 64; ++j) acc = fma(-Lr[(size_t)min(j, ib - 1) * fs], xb[j], acc);
       V[r] = acc;
     }
   }
@@ -605,15 +655,25 @@ __global__ void __launch_bounds__(256) chol_bsolve1_kernel(DevPlan P, Solve1Args
     double acc[16];
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[q] = 0.;
-    for (int r = r0 + lane; r < fs; r += 64) {
-      const double vr = V[r];
-      const double* Lr = L + r + (size_t)j0 * fs;
+    // four rows per lane per iteration (64 loads in flight; rows past fs read row fs - 1 times v = 0, columns
+    // >= ib column ib - 1 times 0); each acc[q] still sums its rows in ascending order
+    for (int rb = r0; rb < fs; rb += 256) {
+      double vr[4];
+      const double* Lr[4];
 #pragma unroll
-      for (int q = 0; q < 16; ++q) {   // unconditional loads; columns >= ib read column ib - 1 times 0
-        const int j = w + 4 * q;
-        const double l = Lr[(size_t)min(j, ib - 1) * fs] * (j < ib ? 1. : 0.);
-        acc[q] = fma(l, vr, acc[q]);
+      for (int u = 0; u < 4; ++u) {
+        const int r = rb + 64 * u + lane;
+        vr[u] = r < fs ? V[min(r, fs - 1)] : 0.;
+        Lr[u] = L + min(r, fs - 1) + (size_t)j0 * fs;
       }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int j = w + 4 * q;
+          const double l = Lr[u][(size_t)min(j, ib - 1) * fs] * (j < ib ? 1. : 0.);
+          acc[q] = fma(l, vr[u], acc[q]);
+        }
     }
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -754,6 +814,7 @@ struct SparseChol::Impl {
   std::map<std::pair<int, int>, std::unique_ptr<DevBuf<int64_t>>> vofs_d;
   DevPlan dp{};
   DevBuf<double> V;   // solve scratch
+  DevBuf<double> XS;  // t = 1 fused forward steps' block results
 };
 
 SparseChol::SparseChol(int n, int m, const int* nbr, int d, const double* X, hipStream_t s)
@@ -878,6 +939,15 @@ void SparseChol::Run(const SparseCholDev& sch, double* ybuf, const void* solve_a
           hipLaunchKernelGGL(chol_scatter_x_kernel, g2, dim3(256), 0, s_, sch.col.get(), op.task0, dp, sa);
         break;
       }
+      case kOpFwdVec:
+      case kOpCopyXS: {
+        const SolveArgs& sa = *static_cast<const SolveArgs*>(solve_args);
+        if (op.type == kOpFwdVec)
+          hipLaunchKernelGGL(chol_fwd_vec_kernel, grid, dim3(64), 0, s_, sch.col.get(), op.task0, dp, sa);
+        else
+          hipLaunchKernelGGL(chol_copy_xs_kernel, grid, dim3(256), 0, s_, sch.col.get(), op.task0, sa);
+        break;
+      }
       case kOpFSolve1:
       case kOpBSolve1: {
         const SolveArgs& sa = *static_cast<const SolveArgs*>(solve_args);
@@ -951,7 +1021,9 @@ void SparseChol::SolveCols(const double* b, double* x, int t, int mode) {
   }
   const SparseCholDev& sch = *it->second;
   if ((int64_t)I.V.size() < sch.y_doubles) I.V.alloc(sch.y_doubles);
-  SolveArgs a{I.V.get(), I.vofs_d[key]->get(), b, x, t};
+  if (t == 1 && (int64_t)I.XS.size() < sch.y_doubles) I.XS.alloc(sch.y_doubles);
+  SolveArgs a{I.V.get(), I.vofs_d[key]->get(), b, x, t, t == 1 ? I.XS.get() : nullptr, d_F_.get(), d_Wd_.get(),
+              d_woff_.get()};
   Run(sch, I.V.get(), &a);
 }
 

@@ -6,6 +6,7 @@
 // balanced supernodal tree (many independent fronts per level at the bottom, few large dense fronts at
 // the top that run on the MFMA GEMM).
 #include <algorithm>
+#include <cstdlib>
 #include <chrono>
 #include <cmath>
 #include <cstring>
@@ -610,13 +611,22 @@ void chol_solve_schedule(const CholPlan& P, int t, bool forward_only, CholSchedu
   S.y_doubles = vofs[P.nsup];
   const int nlev = (int)P.lvl_ptr.size() - 1;
   // t = 1: levels whose panels are all small run one workgroup per supernode (two launches per level); the
-  // levels of large separators keep the tiled form (its parallelism over row tiles)
+  // levels of large separators keep the tiled form (its parallelism over row tiles).
+  // GPBOOST_AMD_CHOL_SMALL_PANEL: the fs x ns bound (A/B)
+  static const int64_t small_panel = [] {
+    const char* e = std::getenv("GPBOOST_AMD_CHOL_SMALL_PANEL");
+    return e ? std::max<int64_t>(0, std::atoll(e)) : kSmallPanel;
+  }();
   std::vector<char> small(nlev, 0);
+  static const bool fuse_vec = [] {   // GPBOOST_AMD_CHOL_FWDVEC=0: the two-launch tiled form for t = 1 (A/B)
+    const char* e = std::getenv("GPBOOST_AMD_CHOL_FWDVEC");
+    return !(e && e[0] == '0');
+  }();
   if (t == 1)
     for (int l = 0; l < nlev; ++l) {
       int64_t mx = 0;
       for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) mx = std::max<int64_t>(mx, (int64_t)P.fs(P.lvl_sup[q]) * P.ns(P.lvl_sup[q]));
-      small[l] = mx <= kSmallPanel;
+      small[l] = mx <= small_panel;
     }
   for (int l = 0; l < nlev && !backward_only; ++l) {
     if (small[l]) {
@@ -638,7 +648,26 @@ void chol_solve_schedule(const CholPlan& P, int t, bool forward_only, CholSchedu
     }
     ob.end();
     const int mb = level_maxblk(P, l);
-    for (int k = 0; k < mb; ++k) {
+    if (t == 1 && fuse_vec) {   // one launch per block step (kOpFwdVec), the level's x moved back from XS after
+      for (int k = 0; k < mb; ++k) {
+        ob.begin(kOpFwdVec);
+        for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) {
+          const int s = P.lvl_sup[q];
+          if (P.nblk(s) <= k) continue;
+          const int fs = P.fs(s), r0 = std::min(64 * (k + 1), P.ns(s));
+          if (r0 >= fs) S.col.push_back(CholColTask{s, k, r0, 0});
+          for (int rt = r0; rt < fs; rt += 64) S.col.push_back(CholColTask{s, k, rt, 0});
+        }
+        ob.end();
+      }
+      ob.begin(kOpCopyXS);
+      for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) {
+        const int s = P.lvl_sup[q];
+        S.col.push_back(CholColTask{s, 0, P.ns(s), 0});
+      }
+      ob.end();
+    }
+    for (int k = 0; k < mb && !(t == 1 && fuse_vec); ++k) {
       ob.begin(kOpGemm);   // x_b = W_b v_b (in place)
       for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) {
         const int s = P.lvl_sup[q];
