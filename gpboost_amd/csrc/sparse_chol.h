@@ -85,6 +85,8 @@ enum CholOpType {
                      //   the first row tile) and v[rt:rt+64] -= L[rt:rt+64, b] x_b, one wave per task (one launch per
                      //   block step instead of two)
   kOpCopyXS,         // CholColTask: V_s[c0:c1] = XS_s[c0:c1] (the forward results of a fused level)
+  kOpBwdVecPart,     // t = 1, CholColTask {s, block k, row chunk kc, slot}: P[slot] = L[chunk, b]^T v[chunk] (256 rows)
+  kOpBwdVecFin,      // t = 1, CholColTask {s, block k, nch, slot0}: x_b = W_b^T (v_b - sum_kc P[slot0 + kc]) in place
 };
 struct CholOp {
   int type, ntask;

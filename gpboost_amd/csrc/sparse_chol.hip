@@ -569,6 +569,62 @@ __global__ void __launch_bounds__(64) chol_fwd_vec_kernel(const CholColTask* __r
   if (r < fs) V[r] = acc;
 }
 
+// ---- t = 1 backward block step of a large level: partial sums of L[chunk, b]^T v[chunk] over 256-row chunks (lane =
+// row, wave w = columns w + 4 q, four rows per lane in flight; wave-reduced), then per supernode the reduce in chunk
+// order and x_b = W_b^T v_b (lane i: sum over j of W[j][i] v_j, j ascending: bsolve1's order)
+__global__ void __launch_bounds__(256) chol_bwd_vec_part_kernel(const CholColTask* __restrict__ tasks, int64_t t0,
+                                                                DevPlan P, SolveArgs a, double* __restrict__ part) {
+  const CholColTask tk = tasks[t0 + blockIdx.x];
+  const int s = tk.s, k = tk.c0, kc = tk.c1, slot = tk.pad;
+  const int sf = P.sfirst[s], ns = P.sfirst[s + 1] - sf;
+  const int fs = ns + (int)(P.rptr[s + 1] - P.rptr[s]);
+  const int j0 = 64 * k, ib = min(64, ns - j0), r0 = j0 + ib;
+  const int rs = r0 + 256 * kc, re = min(rs + 256, fs);
+  const double* V = a.V + a.vofs[s];
+  const double* L = a.F + P.foff[s] + (size_t)j0 * fs;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double acc[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) acc[q] = 0.;
+  double vr[4];
+  int rc[4];
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int r = rs + 64 * u + lane;
+    rc[u] = min(r, re - 1);
+    vr[u] = r < re ? V[rc[u]] : 0.;
+  }
+#pragma unroll
+  for (int u = 0; u < 4; ++u)
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = fma(L[rc[u] + (size_t)min(w + 4 * q, ib - 1) * fs], vr[u], acc[q]);
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    double v = acc[q];
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    if (lane == 0) part[(size_t)slot * 64 + w + 4 * q] = v;
+  }
+}
+
+__global__ void __launch_bounds__(64) chol_bwd_vec_fin_kernel(const CholColTask* __restrict__ tasks, int64_t t0,
+                                                              DevPlan P, SolveArgs a, const double* __restrict__ part) {
+  const CholColTask tk = tasks[t0 + blockIdx.x];
+  const int s = tk.s, k = tk.c0, nch = tk.c1, slot0 = tk.pad;
+  const int ns = P.sfirst[s + 1] - P.sfirst[s];
+  const int j0 = 64 * k, ib = min(64, ns - j0);
+  double* V = a.V + a.vofs[s];
+  const int lane = threadIdx.x;
+  double v = lane < ib ? V[j0 + min(lane, ib - 1)] : 0.;
+  double d = 0.;
+  for (int c = 0; c < nch; ++c) d += part[(size_t)(slot0 + c) * 64 + lane];
+  v = lane < ib ? v - d : 0.;
+  const double* W = a.Wd + a.woff[s] + (int64_t)k * 4096;
+  double x = 0.;
+#pragma unroll
+  for (int j = 0; j < 64; ++j) x = fma(W[j + 64 * lane], readlane_f64(v, j), x);
+  if (lane < ib) V[j0 + lane] = x;
+}
+
 __global__ void __launch_bounds__(256) chol_copy_xs_kernel(const CholColTask* __restrict__ tasks, int64_t t0, SolveArgs a) {
   const CholColTask tk = tasks[t0 + blockIdx.x];
   const int64_t o = a.vofs[tk.s];
@@ -946,6 +1002,15 @@ void SparseChol::Run(const SparseCholDev& sch, double* ybuf, const void* solve_a
           hipLaunchKernelGGL(chol_fwd_vec_kernel, grid, dim3(64), 0, s_, sch.col.get(), op.task0, dp, sa);
         else
           hipLaunchKernelGGL(chol_copy_xs_kernel, grid, dim3(256), 0, s_, sch.col.get(), op.task0, sa);
+        break;
+      }
+      case kOpBwdVecPart:
+      case kOpBwdVecFin: {
+        const SolveArgs& sa = *static_cast<const SolveArgs*>(solve_args);
+        if (op.type == kOpBwdVecPart)
+          hipLaunchKernelGGL(chol_bwd_vec_part_kernel, grid, dim3(256), 0, s_, sch.col.get(), op.task0, dp, sa, d_P_.get());
+        else
+          hipLaunchKernelGGL(chol_bwd_vec_fin_kernel, grid, dim3(64), 0, s_, sch.col.get(), op.task0, dp, sa, d_P_.get());
         break;
       }
       case kOpFSolve1:

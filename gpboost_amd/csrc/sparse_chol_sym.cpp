@@ -720,7 +720,28 @@ void chol_solve_schedule(const CholPlan& P, int t, bool forward_only, CholSchedu
     }
     ob.end();
     const int mb = level_maxblk(P, l);
-    for (int k = mb - 1; k >= 0; --k) {
+    if (t == 1 && fuse_vec) {   // two launches per block step: row-chunk partials, then reduce + W_b^T per supernode
+      for (int k = mb - 1; k >= 0; --k) {
+        std::vector<CholColTask> fins;
+        int slot = 0;
+        ob.begin(kOpBwdVecPart);
+        for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) {
+          const int s = P.lvl_sup[q];
+          if (P.nblk(s) <= k) continue;
+          const int fr = P.fs(s) - std::min(64 * (k + 1), P.ns(s));
+          const int nch = fr > 0 ? (fr + 255) / 256 : 0;
+          for (int kc = 0; kc < nch; ++kc) S.col.push_back(CholColTask{s, k, kc, slot + kc});
+          fins.push_back(CholColTask{s, k, nch, slot});
+          slot += nch;
+        }
+        ob.end();
+        S.p_doubles = std::max(S.p_doubles, (int64_t)slot * 64);
+        ob.begin(kOpBwdVecFin);
+        S.col.insert(S.col.end(), fins.begin(), fins.end());
+        ob.end();
+      }
+    }
+    for (int k = mb - 1; k >= 0 && !(t == 1 && fuse_vec); --k) {
       {   // v_b -= L[r0:fs, b]^T v[r0:fs] (split K: partials in P, then one reduce per column chunk)
         std::vector<CholReduceTask> reds;
         int64_t pb = 0;
