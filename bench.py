@@ -109,6 +109,28 @@ def cpu_baseline(X, Y, reps: int = 3) -> dict:
 
 
 
+def pmc_eval_traffic(tag: str, evals: int) -> dict | None:
+    """HBM-side bytes per evaluation of a whole path from the latest round's per-kernel PMC passes
+    (profiles/<round>/pmc/<tag>_p1.txt FETCH_SIZE, _p2.txt WRITE_SIZE; KiB per dispatch x dispatches, over the
+    `evals` evaluations of scripts/time_<tag>.py; raw counter bytes: the gfx950 x2 for 16-B-per-lane streaming reads
+    is not applied, the GEMM tiles load 8 B per lane)."""
+    import re
+    for rnd in ("r06",):
+        f1 = os.path.join(ROOT, "profiles", rnd, "pmc", f"{tag}_p1.txt")
+        f2 = os.path.join(ROOT, "profiles", rnd, "pmc", f"{tag}_p2.txt")
+        if not (os.path.exists(f1) and os.path.exists(f2)):
+            continue
+        tot = 0.
+        for f, key in ((f1, "FETCH_SIZE"), (f2, "WRITE_SIZE")):
+            for line in open(f):
+                m = re.search(key + r"=([0-9.e+-]+)", line)
+                if m and not line.split()[1].startswith("__amd"):
+                    tot += int(line.split()[0]) * float(m.group(1)) * 1024.
+        return {"bytes": tot / evals, "source": f"rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes), "
+                                                f"profiles/{rnd}/pmc/{tag}_p1.txt, _p2.txt, {evals} evaluations"}
+    return None
+
+
 def pmc_ops() -> dict | None:
     """The latest round's PMC summary of the operator / preconditioner kernels (scripts/pmc_ops_json.py)."""
     for rnd in ("r06", "r05", "r04", "r03"):
@@ -567,12 +589,15 @@ def dense_leg(steps: int, cpu: bool) -> dict:
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
     fl = dense_flops(DENSE_N)
+    traffic = pmc_eval_traffic("dense", 4)
     leg = {"metric": "dense nll + grad evals/sec, n=20000", "value": 1.0 / t, "unit": "evals/s", "steps": steps,
            "ms_per_step": t * 1e3,
            "config": {"workload": "dense_gaussian_lbfgs_unit", "n": DENSE_N, "cov_function": "exponential",
                       "theta": THETA, "nll": nll, "grad": [float(x) for x in g]},
            "roofline": {"bound": "mfma", "achieved": fl / t / 1e12, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                        "frac": fl / t / 1e12 / FP64_PEAK_TFLOPS, "traffic": None,
+                        "frac": fl / t / 1e12 / FP64_PEAK_TFLOPS,
+                        "traffic": traffic["bytes"] if traffic else None,
+                        "traffic_source": traffic["source"] if traffic else None,
                         "kernel": "whole evaluation (POTRF + TRTRI + LAUUM through gemm_f64_big_kernel / "
                                   "gemm_f64_kernel, v_mfma_f64_16x16x4f64)",
                         "algorithmic_flops_per_eval": fl}}
