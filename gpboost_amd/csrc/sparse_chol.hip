@@ -425,10 +425,29 @@ __global__ void __launch_bounds__(256) chol_gather_s_kernel(const CholColTask* _
   const int* rel = P.rel + P.rptr[s];
   double* Ss = S + P.foff[s];
   const double* Sp = S + P.foff[p];
+  // the position map in LDS (one pass), then per column one gather per element with four elements in flight per
+  // thread (the round-5 loop re-read the map from global memory before every gather: two dependent round trips)
+  constexpr int kRelLds = 6144;
+  __shared__ int rel_s[kRelLds];
+  const bool in_lds = nr <= kRelLds;
+  if (in_lds)
+    for (int a = threadIdx.x; a < nr; a += 256) rel_s[a] = rel[a];
+  __syncthreads();
+  const int* rm = in_lds ? rel_s : rel;
   for (int b = tk.c0; b < tk.c1; ++b) {
     const double* src = Sp + (size_t)rel[b] * fp;
     double* dst = Ss + ns + (size_t)(ns + b) * fs;
-    for (int a = threadIdx.x; a < nr; a += 256) dst[a] = src[rel[a]];
+    for (int a0 = threadIdx.x; a0 < nr; a0 += 1024) {
+      double v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int a = a0 + 256 * u;
+        v[u] = a < nr ? src[rm[a]] : 0.;
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (a0 + 256 * u < nr) dst[a0 + 256 * u] = v[u];
+    }
   }
 }
 

@@ -510,7 +510,9 @@ void build_selinv_schedule(const CholPlan& P, CholSchedule& S) {
     ob.begin(kOpGatherS);
     for (int q = P.lvl_ptr[l]; q < P.lvl_ptr[l + 1]; ++q) {
       const int s = P.lvl_sup[q], nr = P.nr(s);
-      for (int c0 = 0; c0 < nr; c0 += 64) S.col.push_back(CholColTask{s, c0, std::min(c0 + 64, nr), 0});
+      // 8 columns per task: the top levels' few supernodes still fill the chip (64 per task left their gathers
+      // on a handful of workgroups, 0.6 ms per launch)
+      for (int c0 = 0; c0 < nr; c0 += 8) S.col.push_back(CholColTask{s, c0, std::min(c0 + 8, nr), 0});
     }
     ob.end();
     const int mb = level_maxblk(P, l);

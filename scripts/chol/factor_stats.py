@@ -3,6 +3,7 @@ launch-size bucket (tiles per launch), totals over the trace's factorizations.
 python scripts/chol/factor_stats.py <kernel_trace.csv>"""
 import collections
 import csv
+import re
 import sys
 
 rows = list(csv.DictReader(open(sys.argv[1])))
@@ -22,11 +23,12 @@ for r in rows:
         phase = "selinv"
     elif "chol_" not in n:
         phase = "other"
-    if phase != "factor":
+    if phase not in ("factor", "selinv"):
         continue
     d = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6
-    short = n.split("(anonymous namespace)::")[-1].split("(")[0]
-    if "gemm" in short:
+    m = re.search(r"::(\w+)(?:<[^>]*>)?\(", n)
+    short = phase + " " + (m.group(1) if m else n[:40])
+    if "gemm" in short or "reduce" in short:
         g = int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))
         b = 1
         while b < g:
@@ -36,6 +38,6 @@ for r in rows:
     by[short][1] += d
 print(f"factorizations: {nfac}")
 tot = sum(v[1] for v in by.values())
-print(f"factor kernels total {tot:.1f} ms, {tot / max(nfac, 1):.2f} ms per factorization")
-for k, (c, t) in sorted(by.items(), key=lambda x: -x[1][1])[:20]:
+print(f"factor + selinv kernels total {tot:.1f} ms")
+for k, (c, t) in sorted(by.items(), key=lambda x: -x[1][1])[:30]:
     print(f"  {k:40s} {c:6d} launches {t:8.2f} ms {t / c * 1e3:8.1f} us avg")
