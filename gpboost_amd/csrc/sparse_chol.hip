@@ -161,13 +161,24 @@ __global__ void __launch_bounds__(256) chol_reduce_kernel(const CholReduceTask* 
   const CholReduceTask r = tasks[t0 + blockIdx.x];
   double* C = bufs.p[r.bufc] + r.c;
   const double* Pb = bufs.p[kCbP] + r.p;
-  for (int e = threadIdx.x; e < 64 * 64; e += 256) {
-    const int i = e & 63, j = e >> 6;
-    if (i >= r.M || j >= r.N) continue;
-    double s = 0.;
-    for (int q = 0; q < r.nslices; ++q) s += Pb[(size_t)q * r.pstride + i + j * 64];
-    double* c = C + i + (size_t)j * r.ldc;
-    *c = (r.beta == 0. ? 0. : r.beta * (*c)) + r.alpha * s;
+  // the 16 elements' C reads issued together, then 16 partial loads in flight per slice (slice order kept per element)
+  double cv[16], sv[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int e = threadIdx.x + 256 * u, i = e & 63, j = e >> 6;
+    sv[u] = 0.;
+    cv[u] = r.beta == 0. ? 0. : C[min(i, r.M - 1) + (size_t)min(j, r.N - 1) * r.ldc];
+  }
+  for (int q = 0; q < r.nslices; ++q) {
+    const double* Pq = Pb + (size_t)q * r.pstride + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < 16; ++u) sv[u] += Pq[256 * u];
+  }
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int e = threadIdx.x + 256 * u, i = e & 63, j = e >> 6;
+    if (i < r.M && j < r.N)
+      C[i + (size_t)j * r.ldc] = (r.beta == 0. ? 0. : r.beta * cv[u]) + r.alpha * sv[u];
   }
 }
 
@@ -235,7 +246,7 @@ __global__ void __launch_bounds__(256) chol_diag_kernel(const CholDiagTask* __re
 }
 
 // ---- batched GEMM tile: C = alpha op(A) op(B) + beta C, one task per workgroup
-constexpr int GT = 64, GK = 16;
+constexpr int GT = 64, GK = 16;   // GK = 32 measured slower (2 waves per SIMD instead of 4)
 // the tile's epilogue: the beta C reads issued together (clamped addresses, unconditional), then the masked stores
 // (one memory round trip per tile instead of one per element)
 __device__ __forceinline__ void chol_gemm_epilogue(const CholGemmTask& g, double* C, const double4_t (&acc)[2][2], int wm,

@@ -1,0 +1,17 @@
+#!/bin/bash
+# Round 6: sparse diagonal blocks with split-K update blocks (A/B with GPBOOST_AMD_CHOL_SPLIT_UPDATE=0): Cholesky-path parity, VIF-Laplace / Cholesky probes
+set -o pipefail
+R="${GRAFT_REPO_ROOT:-$(cd "$(dirname "$0")/.." && pwd)}"
+cd "$R"
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_latent_chol.py \
+  tests/test_gpu_vif_laplace.py tests/test_gpu_mode_cap.py tests/test_gpu_latent_pred.py -p no:cacheprovider > gpurun_out/sk_tests.log 2>&1 || { tail -30 gpurun_out/sk_tests.log; exit 1; }
+tail -2 gpurun_out/sk_tests.log
+timeout -k 10 300 python3 scripts/vifl_time.py 100000 > gpurun_out/sk_vifl.log 2>&1 || { tail -5 gpurun_out/sk_vifl.log; exit 1; }
+GPBOOST_AMD_TIMING=1 timeout -k 10 300 python3 scripts/chol/time_chol.py 100000 3 > gpurun_out/sk_chol.log 2>&1 || { tail -5 gpurun_out/sk_chol.log; exit 1; }
+echo "vifl $(grep '    factor' gpurun_out/sk_vifl.log | tail -1) ; $(grep 'n=100000' gpurun_out/sk_vifl.log | cut -c1-120)"
+echo "chol $(grep 'eval 2' gpurun_out/sk_chol.log) $(grep 'latent cholesky' gpurun_out/sk_chol.log | tail -1)"
+GPBOOST_AMD_CHOL_SPLIT_UPDATE=0 timeout -k 10 300 python3 scripts/vifl_time.py 100000 > gpurun_out/sk_vifl0.log 2>&1 || { tail -5 gpurun_out/sk_vifl0.log; exit 1; }
+GPBOOST_AMD_CHOL_SPLIT_UPDATE=0 GPBOOST_AMD_TIMING=1 timeout -k 10 300 python3 scripts/chol/time_chol.py 100000 3 > gpurun_out/sk_chol0.log 2>&1 || { tail -5 gpurun_out/sk_chol0.log; exit 1; }
+echo "unsplit vifl $(grep '    factor' gpurun_out/sk_vifl0.log | tail -1) ; $(grep 'n=100000' gpurun_out/sk_vifl0.log | cut -c1-120)"
+echo "unsplit chol $(grep 'eval 2' gpurun_out/sk_chol0.log) $(grep 'latent cholesky' gpurun_out/sk_chol0.log | tail -1)"
