@@ -216,10 +216,16 @@ __global__ void __launch_bounds__(256) chol_diag_kernel(const CholDiagTask* __re
       const int hi = __builtin_amdgcn_readlane(__double2hiint(row[kj]), j);
       const double p = __hiloint2double(hi, lo);
       bad = bad || !(p > 0.);
-      const double d = p > 0. ? sqrt(p) : 1.;
-      const double l = r > j ? row[kj] / d : (r == j ? d : 0.);
+      // y = 1 / sqrt(p) by the hardware estimate and two Newton steps, d = p y; the column and W row scaled by y
+      // (multiplies instead of a square root and two IEEE divisions on the pivot chain)
+      const double ps = p > 0. ? p : 1., h = 0.5 * ps;
+      double y = __builtin_amdgcn_rsq(ps);
+      y = y * fma(-h * y, y, 1.5);
+      y = y * fma(-h * y, y, 1.5);
+      const double d = ps * y;
+      const double l = r > j ? row[kj] * y : (r == j ? d : 0.);
       row[kj] = l;
-      wc[kj] = wc[kj] / d;   // W[j][r] final
+      wc[kj] = wc[kj] * y;   // W[j][r] final
       lsh[j & 1][r] = r > j ? l : 0.;
       wsh[j & 1][r] = wc[kj];
     }
