@@ -538,12 +538,17 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) vi
     const double v = C[pl * LD + c];
     rw[c] = (lane < k && c < k) ? (c <= lane ? v : 0.) : (c == lane ? 1. : 0.);
   }
-  double dj = 1.;
+  // pivot j: y = 1 / sqrt(p) by the hardware estimate and two Newton steps, L_jj = p y, the column scaled by y
+  // (multiplies instead of a square root and a division on the pivot chain; y is also the solves' 1 / L_jj)
+  double yd = 1.;
 #pragma unroll
   for (int j = 0; j < 32; ++j) {
-    const double djj = sqrt(readlane_d(rw[j], j));
-    rw[j] = lane > j ? rw[j] / djj : (lane == j ? djj : 0.);
-    dj = lane == j ? djj : dj;
+    const double p = readlane_d(rw[j], j), h = 0.5 * p;
+    double y = __builtin_amdgcn_rsq(p);
+    y = y * fma(-h * y, y, 1.5);
+    y = y * fma(-h * y, y, 1.5);
+    rw[j] = lane > j ? rw[j] * y : (lane == j ? p * y : 0.);
+    yd = lane == j ? y : yd;
 #pragma unroll
     for (int c = j + 1; c < 32; ++c) rw[c] = fma(-rw[j], readlane_d(rw[j], c), rw[c]);
   }
@@ -551,7 +556,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) vi
 #pragma unroll
   for (int c = 0; c < 32; ++c)
     if (lane < 32) C[lane * LD + c] = rw[c];
-  if (lane < 32) rdg[lane] = 1. / dj;
+  if (lane < 32) rdg[lane] = yd;
   wave_sync();
   // L L^T x = b for lane-distributed right-hand sides (lane p holds entry p; zero beyond k)
   auto solve = [&](double* x, int nr) {
