@@ -418,11 +418,12 @@ __global__ void __launch_bounds__(64) potrf_diag_wave_kernel(double* A, int lda,
 // one-wave kernel above runs every one of its ~19k instructions on one wave, so each pivot costs the
 // whole step's issue time: 78 vs 52 us per block in scripts/microbench/diag_bench.hip, V0 vs V8).
 // Wave w holds the columns c = 4k + w (k < 16) of all 64 rows (lane r = row r) in registers; pivot j's
-// owner wave (j & 3) takes the pivot by v_readlane, scales its column (a division, as the LLT does) and
+// owner wave (j & 3) takes the pivot by v_readlane, scales its column (by 1 / sqrt(p) from the rsqrt estimate) and
 // publishes L[:, j] (zero for rows <= j) to LDS; after ONE barrier every wave updates its columns c > j
 // (registers whose columns are all <= j skipped at compile time, the published zeros make the rest
 // branch-free). A partial block (ib < 64) is padded with the identity. Every element sees the same
-// operations in the same order as in the one-wave kernel (bit-identical factor); L^-1 by its code on
+// operations in the same order as in the one-wave kernel except the pivot scaling (multiplies by the Newton-refined
+// 1 / sqrt(p) instead of the one-wave form's sqrt + division: within an ulp per entry); L^-1 by its code on
 // wave 0 (a four-wave split of that substitution changed the rounding enough to move an ill-conditioned
 // Gaussian-kernel FITC case past its 1e-9 reference bound).
 __global__ void __launch_bounds__(256) potrf_diag_quad_kernel(double* A, int lda, int j0, int ib, double* Winv,
@@ -447,8 +448,13 @@ __global__ void __launch_bounds__(256) potrf_diag_quad_kernel(double* A, int lda
       const int hi = __builtin_amdgcn_readlane(__double2hiint(col[j >> 2]), j);
       const double p = __hiloint2double(hi, lo);
       bad = bad || !(p > 0.);   // not positive definite
-      const double d = p > 0. ? sqrt(p) : 1.;
-      const double l = r > j ? col[j >> 2] / d : (r == j ? d : col[j >> 2]);   // divisions, as the LLT
+      // y = 1 / sqrt(p) by the hardware estimate and two Newton steps, L_jj = p y, the column scaled by y
+      // (multiplies instead of a square root and a division on the pivot chain)
+      const double ps = p > 0. ? p : 1., h = 0.5 * ps;
+      double y = __builtin_amdgcn_rsq(ps);
+      y = y * fma(-h * y, y, 1.5);
+      y = y * fma(-h * y, y, 1.5);
+      const double l = r > j ? col[j >> 2] * y : (r == j ? ps * y : col[j >> 2]);
       col[j >> 2] = l;
       colb[j & 1][r] = r > j ? l : 0.;
     }
